@@ -1,0 +1,157 @@
+/*
+ * vslam_abi.h — C ABI of libvslam_hip.so, the MI355X (gfx950) implementation of the
+ * per-frame compute hot path of salah-dev-stu/visual-slam-pipeline.
+ *
+ * Drop-in boundary.  Each entry point replaces one reference interface (file:line under the
+ * reference tree); the C++ facade in visual-slam-pipeline_amd/host/ keeps the reference class
+ * surfaces (FeatureExtractor / Frame / Optimizer / match_features / estimate_motion_3d3d) on
+ * top of these calls, and INTEGRATION.md shows the binding a maintainer adds to Slam.cpp.
+ *
+ * Conventions
+ *   - No C++ types, exceptions or OpenCV types cross this ABI: plain pointers, sizes, ints.
+ *   - Every call returns int status: VS_OK (0) or a negative VS_ERR_* code; vs_last_error()
+ *     returns a thread-local human-readable message for the last failure.
+ *   - "host" entry points take caller-owned HOST buffers and are synchronous (the reference
+ *     semantics).  "_dev" entry points take DEVICE pointers (hipMalloc'd, e.g. torch tensors)
+ *     and a hipStream_t passed as void* (NULL = the context's own stream); they only enqueue.
+ *   - A vs_ctx owns device scratch, the SuperPoint weights and a stream.  One context per
+ *     host thread x GPU; contexts are not thread-safe (neither is the reference's
+ *     FeatureExtractor, FeatureExtractor.cpp:52,79).
+ *   - Layouts match the reference's OpenCV types bit for bit: vs_keypoint == cv::KeyPoint,
+ *     vs_match == cv::DMatch, descriptors are row-major N x 256 fp32 (CV_32F), depth maps are
+ *     row-major H x W fp32 metres with 0 = invalid (Frame.cpp:47-54), poses are row-major
+ *     3x3 / 3x1 fp64 (CV_64F), K = {fx, fy, cx, cy} (Config.h:14-17).
+ */
+#ifndef VSLAM_ABI_H
+#define VSLAM_ABI_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define VS_ABI_VERSION 1
+
+enum {
+    VS_OK = 0,
+    VS_ERR_ARG = -1,      /* bad argument (null pointer, bad size)                    */
+    VS_ERR_HIP = -2,      /* HIP runtime failure (message in vs_last_error)           */
+    VS_ERR_NOMEM = -3,    /* device or host allocation failed                         */
+    VS_ERR_IO = -4,       /* weight file missing or malformed                         */
+    VS_ERR_CAPACITY = -5, /* an internal bound was exceeded (message says which)      */
+    VS_ERR_NOTCONV = -6   /* an iterative device stage did not converge (NMS rounds)  */
+};
+
+/* == cv::KeyPoint (28 B) == one SPCF keypoint record (FeatureExtractor.cpp:294-304). */
+typedef struct {
+    float x, y, size, angle, response;
+    int32_t octave, class_id;
+} vs_keypoint;
+
+/* == cv::DMatch (16 B). */
+typedef struct {
+    int32_t query_idx, train_idx, img_idx;
+    float distance;
+} vs_match;
+
+typedef struct vs_ctx vs_ctx;
+
+/* ---- library / context --------------------------------------------------------------- */
+int         vs_abi_version(void);
+const char* vs_last_error(void);
+
+/* Replaces FeatureExtractor::init (FeatureExtractor.h:18, FeatureExtractor.cpp:22-44).
+ * superpoint_weights: path of a VSPW weight file (see vs_superpoint_save_weights), or NULL
+ * for the seeded synthetic He-normal weights (seed VS_SYNTH_WEIGHT_SEED).  Unlike the
+ * reference, a failure is reported (VS_ERR_IO) instead of silently switching to ORB. */
+#define VS_SYNTH_WEIGHT_SEED 20261015ull
+int  vs_create(int device, const char* superpoint_weights, vs_ctx** out);
+void vs_destroy(vs_ctx* ctx);
+void* vs_stream(vs_ctx* ctx); /* the context's hipStream_t */
+
+/* SuperPoint parameter blob, canonical order (PyTorch/ONNX layout per layer:
+ * weight [Cout][Cin][kh][kw] then bias [Cout]; layers conv1a conv1b conv2a conv2b conv3a conv3b
+ * conv4a conv4b convPa convPb convDa convDb).  Used by tests to build the fp32 torch reference. */
+size_t vs_superpoint_num_params(void);
+int    vs_superpoint_get_weights(vs_ctx* ctx, float* out, size_t count);
+int    vs_superpoint_save_weights(vs_ctx* ctx, const char* path);
+
+/* ---- A1-A6: FeatureExtractor::extract (FeatureExtractor.cpp:49-81, 87-207, 219-259) ---- */
+/* One frame, host buffers.  img: H x W BGR (channels=3, cv::Mat 8UC3) or gray (channels=1),
+ * row stride in bytes.  kps: cap records; desc: cap*256 floats; *n = keypoints written
+ * (descending score order, reference NMS semantics).  cap must be >= 1; at most
+ * min(cap, 400) keypoints are kept (SP_MAX_KEYPOINTS, Config.h:42). */
+int vs_extract(vs_ctx* ctx, const uint8_t* img, int h, int w, int channels, size_t stride,
+               vs_keypoint* kps, float* desc, int cap, int* n);
+
+/* B frames, host buffers: imgs[b] points at frame b; kps is B*cap, desc B*cap*256, n is B. */
+int vs_extract_batch(vs_ctx* ctx, int B, const uint8_t* const* imgs, int h, int w, int channels,
+                     size_t stride, vs_keypoint* kps, float* desc, int cap, int* n);
+
+/* B frames, device buffers (offline batch mode): d_imgs is B contiguous H x W x 3 BGR u8
+ * frames; outputs d_kps [B][cap], d_desc [B][cap][256], d_n [B]. */
+int vs_extract_batch_dev(vs_ctx* ctx, int B, const uint8_t* d_imgs, int h, int w,
+                         vs_keypoint* d_kps, float* d_desc, int* d_n, int cap, void* stream);
+
+/* Stage isolation.  Network only: gray fp32 image (already /255 normalised, H x W) ->
+ * semi [65][H/8][W/8] and desc [256][H/8][W/8], the ORT output layout
+ * (FeatureExtractor.cpp:120-124,167-168).  H and W must be multiples of 8. */
+int vs_superpoint_forward(vs_ctx* ctx, const float* gray01, int h, int w, float* semi,
+                          float* desc_grid);
+/* Post-network only (A4-A6): ORT-layout semi/desc -> keypoints + sampled descriptors, for a
+ * padded image of Hp = 8*Hc rows, Wp = 8*Wc cols and original size h x w (border erase
+ * FeatureExtractor.cpp:155-160). */
+int vs_postprocess(vs_ctx* ctx, const float* semi, const float* desc_grid, int hc, int wc,
+                   int h, int w, vs_keypoint* kps, float* desc, int cap, int* n);
+
+/* ---- A7: Slam::match_features (Slam.cpp:1140-1172) -------------------------------------- */
+/* desc1 = query (reference keyframe), desc2 = train (current frame), rows of 256 fp32.
+ * Exact L2 2-NN (replaces FLANN's approximate search), raw = best neighbour of
+ * every query row when n2 >= 2, good = rows with d0 < ratio * d1, both in query order.
+ * raw/good need n1 records each. */
+int vs_match_ratio(vs_ctx* ctx, const float* desc1, int n1, const float* desc2, int n2,
+                   float ratio, vs_match* raw, int* n_raw, vs_match* good, int* n_good);
+
+/* P frame pairs on device: d_pairs[2p] = query frame, d_pairs[2p+1] = train frame, indexing
+ * the F frames of d_desc [F][cap][256] and d_n [F].  Outputs d_raw/d_good [P][cap],
+ * d_nraw/d_ngood [P]. */
+int vs_match_pairs_dev(vs_ctx* ctx, int P, const int* d_pairs, int F, const float* d_desc,
+                       const int* d_n, int cap, float ratio, vs_match* d_raw, int* d_nraw,
+                       vs_match* d_good, int* d_ngood, void* stream);
+
+/* ---- A9: Slam::estimate_motion_3d3d (Slam.cpp:214-375) ---------------------------------- */
+/* pts1/pts2: n (x,y) float pairs (matched keypoint positions), depth1/depth2: h x w fp32
+ * metres.  seed = 42 + frame_count_ (Slam.cpp:276), iters = RANSAC_3D3D_ITERATIONS (200),
+ * thr = RANSAC_3D3D_INLIER_THRESH (0.05).  R,t map ref-camera points to current-camera points.
+ * *ok = the reference's boolean result; diag (may be NULL) receives
+ * {N back-projected, best inliers, best iteration, refit inliers}. */
+int vs_ransac_3d3d(vs_ctx* ctx, const float* pts1, const float* pts2, int n,
+                   const float* depth1, const float* depth2, int h, int w, const double K[4],
+                   uint32_t seed, int iters, double thr, double R[9], double t[3], int* ok,
+                   int diag[4]);
+
+/* P pairs on device, fed straight from vs_match_pairs_dev's good lists: pair p uses
+ * d_good[p][0..d_ngood[p]) with keypoints d_kps[F][cap] and depth maps d_depth [F][h][w] of
+ * its two frames.  Outputs d_R [P][9], d_t [P][3], d_ok [P], d_diag [P][4].
+ * seeds[p] (device) = 42 + frame_count for that pair. */
+int vs_ransac_3d3d_pairs_dev(vs_ctx* ctx, int P, const int* d_pairs, const vs_keypoint* d_kps,
+                             int cap, const vs_match* d_good, const int* d_ngood,
+                             const float* d_depth, int h, int w, const double K[4],
+                             const uint32_t* d_seeds, int iters, double thr, double* d_R,
+                             double* d_t, int* d_ok, int* d_diag, void* stream);
+
+/* ---- profiling ----------------------------------------------------------------------- */
+/* When enabled, every stage of the _dev pipelines brackets its launches with hipEvents on the
+ * stream it runs on; vs_profile_read returns per-stage accumulated milliseconds and launch
+ * counts since the last reset.  Stage names are static strings. */
+int vs_profile_enable(vs_ctx* ctx, int on);
+int vs_profile_reset(vs_ctx* ctx);
+int vs_profile_read(vs_ctx* ctx, int max_stages, const char** names, double* ms, int* launches,
+                    int* n_stages);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* VSLAM_ABI_H */

@@ -1,0 +1,190 @@
+"""ctypes binding of oracle/liboracle.so — TEST INFRASTRUCTURE ONLY.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg import this module, and only
+as the checker or the timed CPU baseline.  See oracle/oracle.h for what the oracle restates and how
+it is pinned ("parity unpinned" against the reference binary, which cannot be built here).
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "liboracle.so")
+
+KEYPOINT_DTYPE = np.dtype([("x", "<f4"), ("y", "<f4"), ("size", "<f4"), ("angle", "<f4"),
+                           ("response", "<f4"), ("octave", "<i4"), ("class_id", "<i4")])
+MATCH_DTYPE = np.dtype([("query_idx", "<i4"), ("train_idx", "<i4"), ("img_idx", "<i4"),
+                        ("distance", "<f4")])
+
+_P = ctypes.c_void_p
+_I = ctypes.c_int
+_SIG = {
+    "orc_bgr_to_gray": (None, [_P, _I, _I, ctypes.c_size_t, _P]),
+    "orc_gray_to_f32": (None, [_P, _I, _I, _P]),
+    "orc_superpoint_num_params": (ctypes.c_size_t, []),
+    "orc_superpoint_forward": (_I, [_P, _P, _I, _I, _P, _P, _I]),
+    "orc_decode_heatmap": (None, [_P, _I, _I, _P]),
+    "orc_nms": (_I, [_P, _I, _I, _I, _I, ctypes.c_float, _I, _I, _I, _P, _P, _P]),
+    "orc_sample_descriptors": (None, [_P, _I, _I, _P, _I, _P]),
+    "orc_postprocess": (_I, [_P, _P, _I, _I, _I, _I, _I, _I, _P, _P]),
+    "orc_extract": (_I, [_P, _P, _I, _I, ctypes.c_size_t, _I, _I, _P, _P]),
+    "orc_match_ratio": (None, [_P, _I, _P, _I, ctypes.c_float, _P, _P, _P, _P]),
+    "orc_match_ratio_f64": (None, [_P, _I, _P, _I, ctypes.c_float, _P, _P, _P, _P]),
+    "orc_ransac_3d3d": (_I, [_P, _P, _I, _P, _P, _I, _I, _P, ctypes.c_uint32, _I, ctypes.c_double, _P, _P, _P]),
+    "orc_mt19937": (None, [ctypes.c_uint32, _I, _P]),
+    "orc_expf_array": (None, [_P, _I, _P]),
+    "orc_expf_exhaustive_check": (ctypes.c_long, [ctypes.c_float, ctypes.c_float]),
+    "orc_expf_restated_check": (ctypes.c_long, [ctypes.c_float, ctypes.c_float, ctypes.c_int]),
+}
+
+_lib = None
+
+
+def build():
+    subprocess.run(["make", "-C", _HERE, "-s", "-j8"], check=True)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        L = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in _SIG.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+def _p(a):
+    return a.ctypes.data_as(ctypes.c_void_p) if a is not None else None
+
+
+def bgr_to_gray(bgr):
+    bgr = np.ascontiguousarray(bgr, np.uint8)
+    h, w = bgr.shape[:2]
+    g = np.zeros((h, w), np.uint8)
+    lib().orc_bgr_to_gray(_p(bgr), h, w, bgr.strides[0], _p(g))
+    return g
+
+
+def gray_to_f32(g):
+    g = np.ascontiguousarray(g, np.uint8)
+    out = np.zeros(g.shape, np.float32)
+    lib().orc_gray_to_f32(_p(g), g.shape[0], g.shape[1], _p(out))
+    return out
+
+
+def superpoint_forward(weights, img01, nthreads=0):
+    img = np.ascontiguousarray(img01, np.float32)
+    h, w = img.shape
+    semi = np.zeros((65, h // 8, w // 8), np.float32)
+    desc = np.zeros((256, h // 8, w // 8), np.float32)
+    rc = lib().orc_superpoint_forward(_p(np.ascontiguousarray(weights, np.float32)), _p(img), h, w, _p(semi),
+                                      _p(desc), nthreads)
+    assert rc == 0
+    return semi, desc
+
+
+def decode_heatmap(semi):
+    semi = np.ascontiguousarray(semi, np.float32)
+    hc, wc = semi.shape[1:]
+    heat = np.zeros((hc * 8, wc * 8), np.float32)
+    lib().orc_decode_heatmap(_p(semi), hc, wc, _p(heat))
+    return heat
+
+
+def nms(heat, h=None, w=None, thr=0.005, radius=4, max_kp=400, order_mode=1):
+    heat = np.ascontiguousarray(heat, np.float32)
+    hp, wp = heat.shape
+    h = hp if h is None else h
+    w = wp if w is None else w
+    out = np.zeros(max(max_kp, 1), KEYPOINT_DTYPE)
+    nc, nt = ctypes.c_int(0), ctypes.c_int(0)
+    n = lib().orc_nms(_p(heat), hp, wp, h, w, thr, radius, max_kp, order_mode, _p(out), ctypes.byref(nc),
+                      ctypes.byref(nt))
+    return out[:n].copy(), nc.value, nt.value
+
+
+def sample_descriptors(desc_grid, kps):
+    dg = np.ascontiguousarray(desc_grid, np.float32)
+    kps = np.ascontiguousarray(kps, KEYPOINT_DTYPE)
+    out = np.zeros((len(kps), 256), np.float32)
+    lib().orc_sample_descriptors(_p(dg), dg.shape[1], dg.shape[2], _p(kps), len(kps), _p(out))
+    return out
+
+
+def postprocess(semi, desc_grid, h=None, w=None, max_kp=400, order_mode=1):
+    semi = np.ascontiguousarray(semi, np.float32)
+    dg = np.ascontiguousarray(desc_grid, np.float32)
+    hc, wc = semi.shape[1:]
+    h = hc * 8 if h is None else h
+    w = wc * 8 if w is None else w
+    kps = np.zeros(max(max_kp, 1), KEYPOINT_DTYPE)
+    desc = np.zeros((max(max_kp, 1), 256), np.float32)
+    n = lib().orc_postprocess(_p(semi), _p(dg), hc, wc, h, w, max_kp, order_mode, _p(kps), _p(desc))
+    return kps[:n].copy(), desc[:n].copy()
+
+
+def extract(weights, bgr, max_kp=400, nthreads=0):
+    bgr = np.ascontiguousarray(bgr, np.uint8)
+    h, w = bgr.shape[:2]
+    kps = np.zeros(max_kp, KEYPOINT_DTYPE)
+    desc = np.zeros((max_kp, 256), np.float32)
+    n = lib().orc_extract(_p(np.ascontiguousarray(weights, np.float32)), _p(bgr), h, w, bgr.strides[0], max_kp,
+                          nthreads, _p(kps), _p(desc))
+    assert n >= 0
+    return kps[:n].copy(), desc[:n].copy()
+
+
+def match_ratio(d1, d2, ratio=0.75, f64=False):
+    d1 = np.ascontiguousarray(d1, np.float32).reshape(-1, 256)
+    d2 = np.ascontiguousarray(d2, np.float32).reshape(-1, 256)
+    n1, n2 = d1.shape[0], d2.shape[0]
+    raw = np.zeros(max(n1, 1), MATCH_DTYPE)
+    good = np.zeros(max(n1, 1), MATCH_DTYPE)
+    nr, ng = ctypes.c_int(0), ctypes.c_int(0)
+    fn = lib().orc_match_ratio_f64 if f64 else lib().orc_match_ratio
+    fn(_p(d1), n1, _p(d2), n2, ratio, _p(raw), ctypes.byref(nr), _p(good), ctypes.byref(ng))
+    return raw[:nr.value].copy(), good[:ng.value].copy()
+
+
+def ransac_3d3d(pts1, pts2, depth1, depth2, K=(525.0, 525.0, 319.5, 239.5), seed=42, iters=200, thr=0.05):
+    p1 = np.ascontiguousarray(pts1, np.float32).reshape(-1, 2)
+    p2 = np.ascontiguousarray(pts2, np.float32).reshape(-1, 2)
+    d1 = np.ascontiguousarray(depth1, np.float32)
+    d2 = np.ascontiguousarray(depth2, np.float32)
+    Ka = np.asarray(K, np.float64)
+    R = np.zeros(9)
+    t = np.zeros(3)
+    diag = np.zeros(4, np.int32)
+    ok = lib().orc_ransac_3d3d(_p(p1), _p(p2), p1.shape[0], _p(d1), _p(d2), d1.shape[0], d1.shape[1], _p(Ka), seed,
+                               iters, thr, _p(R), _p(t), _p(diag))
+    return bool(ok), R.reshape(3, 3), t, diag
+
+
+def mt19937(seed, count):
+    out = np.zeros(count, np.uint32)
+    lib().orc_mt19937(seed, count, _p(out))
+    return out
+
+
+def expf(x):
+    x = np.ascontiguousarray(x, np.float32)
+    out = np.zeros_like(x)
+    lib().orc_expf_array(_p(x), x.size, _p(out))
+    return out
+
+
+def expf_exhaustive_check(lo, hi):
+    """Number of floats x in [lo, hi] where glibc expf(x) != (float)exp((double)x)."""
+    return lib().orc_expf_exhaustive_check(lo, hi)
+
+
+def expf_restated_check(lo, hi, use_fma=1):
+    """Number of floats x in [lo, hi] (hi <= 0) where the product's glibc_expf.h differs from libm."""
+    return lib().orc_expf_restated_check(lo, hi, use_fma)

@@ -1,0 +1,161 @@
+"""Independent numpy / pure-Python restatements used to pin the C oracle (test infrastructure).
+
+Each function follows the reference source it cites; none of them calls the oracle except for
+glibc's expf values, which the reference itself takes from libm (std::exp(float)).
+"""
+import numpy as np
+
+
+def decode_heatmap(semi, expf):
+    """FeatureExtractor.cpp:126-151 with float32 arithmetic in the reference's order."""
+    semi = np.asarray(semi, np.float32)
+    C, hc, wc = semi.shape
+    cells = semi.reshape(C, -1)
+    mx = cells.max(axis=0)
+    e = expf((cells - mx[None, :]).astype(np.float32))
+    s = np.zeros(cells.shape[1], np.float32)
+    for c in range(C):  # sequential float sum over c
+        s = (s + e[c]).astype(np.float32)
+    prob = (e / s[None, :]).astype(np.float32)
+    heat = np.zeros((hc * 8, wc * 8), np.float32)
+    p = prob[:64].reshape(8, 8, hc, wc)  # c -> (c // 8, c % 8)
+    heat[:, :] = p.transpose(2, 0, 3, 1).reshape(hc * 8, wc * 8)
+    return heat
+
+
+def greedy_nms(heat, thr=0.005, radius=4, max_kp=400, stable=True):
+    """FeatureExtractor.cpp:219-259 (stable=True: ties broken by raster order)."""
+    H, W = heat.shape
+    ys, xs = np.nonzero(heat > np.float32(thr))  # raster order
+    scores = heat[ys, xs]
+    order = np.argsort(-scores, kind="stable")
+    sup = np.zeros((H, W), bool)
+    out = []
+    for i in order:
+        if len(out) >= max_kp:
+            break
+        y, x = ys[i], xs[i]
+        if sup[y, x]:
+            continue
+        out.append((int(x), int(y), float(scores[i])))
+        sup[max(0, y - radius):y + radius + 1, max(0, x - radius):x + radius + 1] = True
+    return out
+
+
+def mis_rounds_nms(heat, thr=0.005, radius=4, max_kp=400):
+    """The GPU's algorithm (sp_post.hip), in global Jacobi rounds over the dense heatmap:
+    undecided -> kept when no undecided higher-priority pixel is in the window and no kept one,
+    undecided -> out when a kept pixel is in the window; then the top max_kp kept by priority.
+    Returns (keypoints, rounds)."""
+    H, W = heat.shape
+    UND, KEPT, OUT = 0, 1, 2
+    st = np.where(heat > np.float32(thr), UND, OUT).astype(np.int8)
+    r = radius
+    pad = lambda a, v: np.pad(a, r, constant_values=v)
+    rounds = 0
+    while (st == UND).any():
+        rounds += 1
+        sp = pad(st, OUT)
+        hp = pad(heat, -1.0)
+        kept_nb = np.zeros((H, W), bool)
+        blocked = np.zeros((H, W), bool)
+        for dy in range(-r, r + 1):
+            for dx in range(-r, r + 1):
+                if dx == 0 and dy == 0:
+                    continue
+                sq = sp[r + dy:r + dy + H, r + dx:r + dx + W]
+                hq = hp[r + dy:r + dy + H, r + dx:r + dx + W]
+                kept_nb |= sq == KEPT
+                earlier = dy < 0 or (dy == 0 and dx < 0)
+                higher = (hq > heat) | ((hq == heat) & earlier)
+                blocked |= (sq == UND) & higher
+        und = st == UND
+        new = st.copy()
+        new[und & kept_nb] = OUT
+        new[und & ~kept_nb & ~blocked] = KEPT
+        st = new
+    ys, xs = np.nonzero(st == KEPT)
+    sc = heat[ys, xs]
+    idx = ys * W + xs
+    order = np.lexsort((idx, -sc))[:max_kp]
+    return [(int(xs[i]), int(ys[i]), float(sc[i])) for i in order], rounds
+
+
+def sample_descriptors(desc_grid, kps_xy):
+    """FeatureExtractor.cpp:167-206 in float32, expression order kept, sequential norm."""
+    dg = np.asarray(desc_grid, np.float32)
+    _, hc, wc = dg.shape
+    f32 = np.float32
+    out = np.zeros((len(kps_xy), 256), np.float32)
+    for i, (x, y) in enumerate(kps_xy):
+        sx = f32(x) / f32(8.0)
+        sy = f32(y) / f32(8.0)
+        x0 = max(0, min(int(np.floor(sx)), wc - 1))
+        y0 = max(0, min(int(np.floor(sy)), hc - 1))
+        x1 = min(x0 + 1, wc - 1)
+        y1 = min(y0 + 1, hc - 1)
+        wx = f32(sx - f32(x0))
+        wy = f32(sy - f32(y0))
+        v00, v01, v10, v11 = dg[:, y0, x0], dg[:, y0, x1], dg[:, y1, x0], dg[:, y1, x1]
+        one = f32(1.0)
+        a = ((one - wx) * v00).astype(f32) + (wx * v01).astype(f32)
+        b = ((one - wx) * v10).astype(f32) + (wx * v11).astype(f32)
+        val = ((one - wy) * a.astype(f32)).astype(f32) + (wy * b.astype(f32)).astype(f32)
+        val = val.astype(f32)
+        nrm = f32(0.0)
+        for c in range(256):
+            nrm = f32(nrm + f32(val[c] * val[c]))
+        nrm = f32(np.sqrt(nrm))
+        if nrm > f32(1e-8):
+            val = (val / nrm).astype(f32)
+        out[i] = val
+    return out
+
+
+def rodrigues(rv):
+    th = np.linalg.norm(rv)
+    if th < 1e-15:
+        return np.eye(3)
+    k = rv / th
+    Kx = np.array([[0, -k[2], k[1]], [k[2], 0, -k[0]], [-k[1], k[0], 0]])
+    return np.eye(3) + np.sin(th) * Kx + (1 - np.cos(th)) * Kx @ Kx
+
+
+def rigid_scene(n, outlier_frac, seed, K=(525.0, 525.0, 319.5, 239.5), h=480, w=640, noise=0.0,
+                rot=0.04, trans=(0.03, -0.01, 0.05)):
+    """Known-answer 3D-3D problem: two depth maps + matched pixels related by (R, t) (ref -> cur).
+    Returns pts1, pts2 (float32 Nx2), depth1, depth2, R, t, inlier mask."""
+    rng = np.random.default_rng(seed)
+    fx, fy, cx, cy = K
+    R = rodrigues(rng.normal(size=3) * rot)
+    t = np.asarray(trans, np.float64)
+    depth1 = np.zeros((h, w), np.float32)
+    depth2 = np.zeros((h, w), np.float32)
+    pts1, pts2, inl = [], [], []
+    used1, used2 = set(), set()
+    while len(pts1) < n:
+        u1 = int(rng.integers(20, w - 20))
+        v1 = int(rng.integers(20, h - 20))
+        z1 = float(np.float32(rng.uniform(0.8, 4.0)))
+        P1 = np.array([(u1 - cx) * z1 / fx, (v1 - cy) * z1 / fy, z1])
+        is_in = rng.random() >= outlier_frac
+        if is_in:
+            P2 = R @ P1 + t + rng.normal(size=3) * noise
+        else:
+            P2 = P1 + rng.normal(size=3) * 0.5
+        if P2[2] < 0.5:
+            continue
+        # sub-pixel projection (float32), depth stored at the round()-ed pixel the reference reads
+        u2f = np.float32(fx * P2[0] / P2[2] + cx)
+        v2f = np.float32(fy * P2[1] / P2[2] + cy)
+        u2, v2 = int(np.round(u2f)), int(np.round(v2f))
+        if not (0 <= u2 < w and 0 <= v2 < h) or (u1, v1) in used1 or (u2, v2) in used2:
+            continue
+        used1.add((u1, v1))
+        used2.add((u2, v2))
+        depth1[v1, u1] = np.float32(z1)
+        depth2[v2, u2] = np.float32(P2[2])
+        pts1.append((u1, v1))
+        pts2.append((u2f, v2f))
+        inl.append(is_in)
+    return (np.array(pts1, np.float32), np.array(pts2, np.float32), depth1, depth2, R, t, np.array(inl))

@@ -1,0 +1,42 @@
+"""C-ABI boundary checks that need no GPU: the library loads and exports every declared symbol."""
+import ctypes
+import os
+
+import pytest
+
+import vslam_abi
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "vslam_abi.h")
+
+
+def test_header_declares_expected_entry_points():
+    names = vslam_abi.exported_symbols_from_header(HEADER)
+    for must in ["vs_create", "vs_destroy", "vs_extract", "vs_extract_batch", "vs_extract_batch_dev",
+                 "vs_superpoint_forward", "vs_postprocess", "vs_match_ratio", "vs_match_pairs_dev",
+                 "vs_ransac_3d3d", "vs_ransac_3d3d_pairs_dev"]:
+        assert must in names
+
+
+@pytest.mark.skipif(not os.path.exists(vslam_abi.LIB_PATH), reason="libvslam_hip.so not built")
+def test_library_exports_every_declared_symbol():
+    lib = ctypes.CDLL(vslam_abi.LIB_PATH)
+    missing = [n for n in vslam_abi.exported_symbols_from_header(HEADER) if not hasattr(lib, n)]
+    assert missing == []
+    # every binding in the ctypes table corresponds to a declared symbol
+    declared = set(vslam_abi.exported_symbols_from_header(HEADER))
+    assert set(vslam_abi._SIG) <= declared
+
+
+@pytest.mark.skipif(not os.path.exists(vslam_abi.LIB_PATH), reason="libvslam_hip.so not built")
+def test_library_reports_abi_version_without_gpu():
+    lib = vslam_abi.load_library()
+    assert lib.vs_abi_version() == 1
+    assert lib.vs_superpoint_num_params() == 1300865
+
+
+def test_record_layouts_match_opencv():
+    # cv::KeyPoint: Point2f pt, float size, angle, response, int octave, class_id
+    assert vslam_abi.KEYPOINT_DTYPE.itemsize == 28
+    # cv::DMatch: int queryIdx, trainIdx, imgIdx, float distance
+    assert vslam_abi.MATCH_DTYPE.itemsize == 16

@@ -1,0 +1,222 @@
+"""GPU parity tests: libvslam_hip.so (HIP, gfx950) against the CPU oracle on identical inputs.
+
+Bars (DESIGN.md "Parity"): keypoint pixel indices, scores, sampled descriptors and match pair
+lists bit-exact; 3D-3D RANSAC decisions (ok, N, best inliers, best iteration, refit inliers)
+exact and R, t within 1e-12; network outputs within the fp32 tolerance stated in each test.
+"""
+import numpy as np
+import pytest
+
+import restate
+
+pytestmark = pytest.mark.gpu
+
+
+def _kp_equal(a, b):
+    return len(a) == len(b) and np.array_equal(a.view(np.uint8), b.view(np.uint8))
+
+
+def _bits_equal(a, b):
+    return a.shape == b.shape and np.array_equal(np.ascontiguousarray(a).view(np.uint32),
+                                                 np.ascontiguousarray(b).view(np.uint32))
+
+
+# ---------------------------------------------------------------------------------- network
+def test_network_matches_torch_fp64(vsctx, seq4):
+    from test_oracle import _torch_superpoint
+    import oracle_py
+    w = vsctx.weights()
+    gray = oracle_py.gray_to_f32(oracle_py.bgr_to_gray(seq4[0]["bgr"]))
+    semi, desc = vsctx.superpoint_forward(gray)
+    ts, td = _torch_superpoint(w, gray)
+    # fp32 accumulation over K <= 4608 products vs an fp64 reference
+    tol_semi = 2e-4 * max(1.0, float(np.max(np.abs(ts))))
+    assert np.max(np.abs(semi - ts)) <= tol_semi
+    assert np.max(np.abs(desc - td)) <= 2e-5
+
+
+def test_network_matches_oracle_cpu_network(vsctx, oracle, seq4):
+    w = vsctx.weights()
+    gray = oracle.gray_to_f32(oracle.bgr_to_gray(seq4[1]["bgr"]))
+    semi, desc = vsctx.superpoint_forward(gray)
+    os_, od = oracle.superpoint_forward(w, gray)
+    assert np.max(np.abs(semi - os_)) <= 2e-4 * max(1.0, float(np.max(np.abs(os_))))
+    assert np.max(np.abs(desc - od)) <= 2e-5
+
+
+# ------------------------------------------------------------------- post-processing (A4-A6)
+@pytest.mark.parametrize("seed", [0, 1, 2, 3])
+def test_postprocess_bit_exact_random(vsctx, oracle, seed):
+    rng = np.random.default_rng(seed)
+    hc, wc = 60, 80
+    semi = (rng.standard_normal((65, hc, wc)) * (2.0 + seed)).astype(np.float32)
+    if seed == 3:  # quantised logits -> many exactly tied scores
+        semi = np.round(semi * 4) / 4
+    dg = rng.standard_normal((256, hc, wc)).astype(np.float32)
+    dg /= np.linalg.norm(dg, axis=0, keepdims=True)
+    kg, dgpu = vsctx.postprocess(semi, dg)
+    ko, do = oracle.postprocess(semi, dg, order_mode=1)
+    assert _kp_equal(kg, ko)
+    assert _bits_equal(dgpu, do)
+
+
+def test_postprocess_bit_exact_network_outputs(vsctx, oracle, seq4):
+    for f in seq4:
+        gray = oracle.gray_to_f32(oracle.bgr_to_gray(f["bgr"]))
+        semi, dg = vsctx.superpoint_forward(gray)
+        kg, dgpu = vsctx.postprocess(semi, dg)
+        ko, do = oracle.postprocess(semi, dg, order_mode=1)
+        assert _kp_equal(kg, ko) and _bits_equal(dgpu, do)
+        assert len(kg) == 400
+
+
+def test_postprocess_edges(vsctx, oracle):
+    hc, wc = 12, 16
+    dg = np.ones((256, hc, wc), np.float32) / 16.0
+    semi = np.zeros((65, hc, wc), np.float32)
+    semi[64] = 50.0  # everything in the dustbin: no candidates
+    kg, d = vsctx.postprocess(semi, dg)
+    assert len(kg) == 0
+    # padded frame: border erase (h, w not multiples of 8), and a tiny cap
+    rng = np.random.default_rng(11)
+    semi = (rng.standard_normal((65, hc, wc)) * 3).astype(np.float32)
+    for h, w, cap in [(93, 121, 400), (96, 128, 7), (90, 128, 1)]:
+        kg, dgpu = vsctx.postprocess(semi, dg, h=h, w=w, cap=cap)
+        ko, do = oracle.postprocess(semi, dg, h=h, w=w, max_kp=min(cap, 400), order_mode=1)
+        assert _kp_equal(kg, ko) and _bits_equal(dgpu, do)
+
+
+def test_extract_end_to_end_equals_network_plus_oracle_post(vsctx, oracle, seq4):
+    f = seq4[2]
+    kps, desc = vsctx.extract(f["bgr"])
+    gray = oracle.gray_to_f32(oracle.bgr_to_gray(f["bgr"]))
+    semi, dg = vsctx.superpoint_forward(gray)
+    ko, do = oracle.postprocess(semi, dg, order_mode=1)
+    assert _kp_equal(kps, ko) and _bits_equal(desc, do)
+
+
+def test_extract_gray_input_and_batch_consistency(vsctx, oracle, seq4):
+    imgs = [f["bgr"] for f in seq4]
+    batch = vsctx.extract_batch(imgs)
+    for img, (kb, db) in zip(imgs, batch):
+        ks, ds = vsctx.extract(img)
+        assert _kp_equal(kb, ks) and _bits_equal(db, ds)
+    g = oracle.bgr_to_gray(imgs[0])
+    kg, dg = vsctx.extract(g)  # channels == 1 path
+    assert _kp_equal(kg, batch[0][0]) and _bits_equal(dg, batch[0][1])
+
+
+# ----------------------------------------------------------------------------- matching (A7)
+def _match_equal(a, b):
+    return len(a) == len(b) and np.array_equal(a.view(np.uint8), b.view(np.uint8))
+
+
+@pytest.mark.parametrize("n1,n2", [(400, 400), (37, 513), (1, 2), (128, 129), (300, 1000), (513, 64)])
+def test_match_bit_exact_random(vsctx, oracle, n1, n2):
+    import synth
+    d1 = synth.random_descriptors(n1, n1 * 7 + 1)
+    d2 = synth.random_descriptors(n2, n2 * 11 + 2)
+    k = min(n1, n2) // 2
+    d2[:k] = d1[:k] + 0.1 * synth.random_descriptors(k, 5)[:k]  # planted neighbours
+    raw_g, good_g = vsctx.match_ratio(d1, d2)
+    raw_o, good_o = oracle.match_ratio(d1, d2)
+    assert _match_equal(raw_g, raw_o) and _match_equal(good_g, good_o)
+
+
+def test_match_edges_and_ties(vsctx, oracle):
+    import synth
+    d = synth.random_descriptors(50, 3)
+    for d1, d2 in [(d, d[:1]), (d[:0], d), (d, d[:0]), (d, np.concatenate([d, d])), (d[:1], d[:2])]:
+        rg, gg = vsctx.match_ratio(d1, d2)
+        ro, go = oracle.match_ratio(d1, d2)
+        assert _match_equal(rg, ro) and _match_equal(gg, go)
+
+
+def test_match_bit_exact_real_descriptors(vsctx, oracle, seq4):
+    feats = vsctx.extract_batch([f["bgr"] for f in seq4])
+    for i in range(3):
+        rg, gg = vsctx.match_ratio(feats[i][1], feats[i + 1][1])
+        ro, go = oracle.match_ratio(feats[i][1], feats[i + 1][1])
+        assert _match_equal(rg, ro) and _match_equal(gg, go)
+        assert len(gg) > 50  # consecutive synthetic frames do match
+
+
+# ------------------------------------------------------------------------ 3D-3D RANSAC (A9)
+def _ransac_equal(g, o):
+    okg, Rg, tg, dg = g
+    oko, Ro, to, do = o
+    assert okg == oko
+    assert np.array_equal(dg, do)
+    if do[3] > 0:
+        assert np.max(np.abs(Rg - Ro)) <= 1e-12 and np.max(np.abs(tg - to)) <= 1e-12
+
+
+@pytest.mark.parametrize("seed,outliers,noise,n", [(0, 0.4, 0.0, 200), (1, 0.4, 0.002, 300), (2, 0.6, 0.001, 400),
+                                                   (3, 0.0, 0.0, 10), (4, 0.9, 0.0, 120)])
+def test_ransac_3d3d_matches_oracle(vsctx, oracle, seed, outliers, noise, n):
+    p1, p2, d1, d2, R, t, inl = restate.rigid_scene(n, outliers, seed, noise=noise)
+    g = vsctx.ransac_3d3d(p1, p2, d1, d2, seed=42 + seed)
+    o = oracle.ransac_3d3d(p1, p2, d1, d2, seed=42 + seed)
+    _ransac_equal(g, o)
+
+
+def test_ransac_3d3d_on_pipeline_matches(vsctx, oracle, seq4):
+    feats = vsctx.extract_batch([f["bgr"] for f in seq4])
+    for i in range(3):
+        (k1, d1), (k2, d2) = feats[i], feats[i + 1]
+        _, good = vsctx.match_ratio(d1, d2)
+        p1 = np.stack([k1["x"][good["query_idx"]], k1["y"][good["query_idx"]]], 1)
+        p2 = np.stack([k2["x"][good["train_idx"]], k2["y"][good["train_idx"]]], 1)
+        g = vsctx.ransac_3d3d(p1, p2, seq4[i]["depth"], seq4[i + 1]["depth"], seed=42 + i)
+        o = oracle.ransac_3d3d(p1, p2, seq4[i]["depth"], seq4[i + 1]["depth"], seed=42 + i)
+        _ransac_equal(g, o)
+
+
+def test_ransac_3d3d_small_n_and_many_draws(vsctx, oracle):
+    # N == 10 forces many rejection draws; iters = 1024 consumes > 1248 MT outputs (lane-0 twist path)
+    p1, p2, d1, d2, R, t, inl = restate.rigid_scene(10, 0.3, 21)
+    for iters in (200, 1024):
+        g = vsctx.ransac_3d3d(p1, p2, d1, d2, seed=7, iters=iters)
+        o = oracle.ransac_3d3d(p1, p2, d1, d2, seed=7, iters=iters)
+        _ransac_equal(g, o)
+
+
+# ------------------------------------------------------------ device-batched entry points
+def test_device_pipeline_matches_host_entry_points(vsctx, seq4):
+    import torch
+    from vslam_pipeline import DevicePipeline
+    pipe = DevicePipeline(vsctx, B=len(seq4), h=480, w=640)
+    frames = torch.from_numpy(np.stack([f["bgr"] for f in seq4])).cuda()
+    depth = torch.from_numpy(np.stack([f["depth"] for f in seq4])).cuda()
+    out = pipe.run(frames, depth, frame_count0=0)
+    torch.cuda.synchronize()
+    feats = vsctx.extract_batch([f["bgr"] for f in seq4])
+    n = out["n"].cpu().numpy()
+    kps = out["kps"].cpu().numpy().view(np.uint8)
+    for b in range(len(seq4)):
+        kb = kps[b].view(feats[b][0].dtype)[:n[b]]
+        assert _kp_equal(kb, feats[b][0])
+    ngood = out["ngood"].cpu().numpy()
+    assert ngood[0] == 0  # no frame before the first batch
+    for p in range(1, len(seq4)):  # pair p = frames (p-1, p), seed 42 + frame_count
+        _, good = vsctx.match_ratio(feats[p - 1][1], feats[p][1])
+        assert ngood[p] == len(good)
+        okp = bool(out["ok"][p].item())
+        k1, k2 = feats[p - 1][0], feats[p][0]
+        p1 = np.stack([k1["x"][good["query_idx"]], k1["y"][good["query_idx"]]], 1)
+        p2 = np.stack([k2["x"][good["train_idx"]], k2["y"][good["train_idx"]]], 1)
+        okh, Rh, th, dh = vsctx.ransac_3d3d(p1, p2, seq4[p - 1]["depth"], seq4[p]["depth"], seed=42 + p)
+        assert okp == okh
+        assert np.array_equal(out["diag"][p].cpu().numpy(), dh)
+        if okh:
+            assert np.max(np.abs(out["R"][p].cpu().numpy() - Rh.reshape(9))) <= 1e-12
+
+
+def test_profile_reports_stages(vsctx, seq4):
+    vsctx.profile(True)
+    vsctx.profile_reset()
+    vsctx.extract(seq4[0]["bgr"])
+    prof = vsctx.profile_read()
+    vsctx.profile(False)
+    for st in ["conv1a", "conv1b_pool", "head_a", "nms_rounds", "sample"]:
+        assert st in prof and prof[st][0] > 0

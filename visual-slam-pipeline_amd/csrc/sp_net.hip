@@ -1,0 +1,356 @@
+// sp_net.hip — SuperPoint network forward on gfx950 (replaces ONNX Runtime's Session::Run,
+// reference src/FeatureExtractor.cpp:107-124; topology SURVEY.md 8(a) A3).
+//
+// Layout: NHWC fp32 activations, frames batched along N.  Every 3x3 / 1x1 conv is an implicit
+// GEMM on the fp32 matrix cores (v_mfma_f32_32x32x2_f32, exact fp32 products, fp32 accumulate):
+//   M = output pixels (tiles of 8 rows x 32 columns, one 32-pixel row segment per MFMA block),
+//   N = output channels (64 per workgroup), K = k*k*Cin (Cin staged through LDS 16 at a time).
+// Bias, ReLU and the 2x2 max-pool are fused into the epilogue: the 32x32 accumulator keeps
+// horizontally adjacent pixels in adjacent registers of one lane and the two image rows of a
+// pool window in the same wave, so pooling never leaves registers.
+#include <hip/hip_runtime.h>
+
+#include "vs_internal.h"
+
+namespace vs {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+// ---------------------------------------------------------------------------------------------
+// A2: BGR u8 -> gray u8 (OpenCV fixed point) -> fp32 * (float)(1/255.0), zero-padded to Hp x Wp
+// (FeatureExtractor.cpp:63-67, 90-105).
+__global__ void k_gray_norm(const uint8_t* __restrict__ img, int channels, int h, int w, int Hp,
+                            int Wp, float* __restrict__ out, int total) {
+    int idx = blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= total) return;
+    int x = idx % Wp;
+    int t = idx / Wp;
+    int y = t % Hp;
+    int b = t / Hp;
+    float v = 0.0f;
+    if (x < w && y < h) {
+        const uint8_t* p = img + ((size_t)b * h * w + (size_t)y * w + x) * channels;
+        unsigned g;
+        if (channels == 3)
+            g = ((unsigned)p[0] * 1868u + (unsigned)p[1] * 9617u + (unsigned)p[2] * 4899u + (1u << 13)) >> 14;
+        else
+            g = p[0];
+        v = (float)g * (float)(1.0 / 255.0);
+    }
+    out[idx] = v;
+}
+
+// conv1a: 1 -> 64 channels, 3x3, ReLU.  K = 9 is too shallow for the matrix cores: one thread per
+// pixel, weights in LDS, 16 x 16-byte stores of the pixel's 64 channels.
+__global__ __launch_bounds__(256) void k_conv1a(const float* __restrict__ gray, const float* __restrict__ wt,
+                                                const float* __restrict__ bias, float* __restrict__ out,
+                                                int Hp, int Wp, int total) {
+    __shared__ float s_w[9 * 64 + 64];
+    for (int i = threadIdx.x; i < 9 * 64; i += blockDim.x) s_w[i] = wt[i];
+    if (threadIdx.x < 64) s_w[9 * 64 + threadIdx.x] = bias[threadIdx.x];
+    __syncthreads();
+    int idx = blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= total) return;
+    int x = idx % Wp;
+    int t = idx / Wp;
+    int y = t % Hp;
+    int b = t / Hp;
+    const float* g = gray + (size_t)b * Hp * Wp;
+    float v[9];
+#pragma unroll
+    for (int ky = 0; ky < 3; ky++)
+#pragma unroll
+        for (int kx = 0; kx < 3; kx++) {
+            int yy = y + ky - 1, xx = x + kx - 1;
+            v[ky * 3 + kx] = (yy >= 0 && yy < Hp && xx >= 0 && xx < Wp) ? g[(size_t)yy * Wp + xx] : 0.0f;
+        }
+    f32x4* o = reinterpret_cast<f32x4*>(out + (size_t)idx * 64);
+#pragma unroll
+    for (int q = 0; q < 16; q++) {
+        f32x4 r;
+#pragma unroll
+        for (int e = 0; e < 4; e++) {
+            int c = q * 4 + e;
+            float a = s_w[9 * 64 + c];
+#pragma unroll
+            for (int k = 0; k < 9; k++) a += v[k] * s_w[k * 64 + c];
+            r[e] = a > 0.0f ? a : 0.0f;
+        }
+        o[q] = r;
+    }
+}
+
+// Generic conv (KS = 3: 3x3 pad 1 over 8x32 spatial tiles; KS = 1: 1x1 over linear 256-pixel
+// tiles) on v_mfma_f32_32x32x2_f32.  256 threads = 4 waves; wave wv owns tile rows 2wv, 2wv+1
+// (two 32-pixel M blocks) x 64 output channels (two N blocks): four 32x32 accumulators.
+// LDS: s_in[CK][pixels] (channel-major: a half-wave reads 32 consecutive pixels, conflict free)
+//      s_w [k*k*CK][64] (a half-wave reads 32 consecutive output channels, conflict free).
+template <int KS>
+struct ConvGeom {
+    static constexpr int CK = (KS == 3) ? 16 : 32;
+    static constexpr int TW = 32, TH = 8;
+    static constexpr int PW = (KS == 3) ? TW + 2 : TW;
+    static constexpr int PH = (KS == 3) ? TH + 2 : TH;
+    static constexpr int NPIX = PW * PH;
+};
+
+template <int KS, bool POOL, int LAYER>
+__global__ __launch_bounds__(256, 2) void k_conv_mfma(
+    const float* __restrict__ in, int in_cstride, int in_coff, const float* __restrict__ wt,
+    const float* __restrict__ bias, int cin, int cout, int cout_pad, float* __restrict__ out,
+    int out_cstride, int out_coff, int B, int H, int W, int tiles_x, int tiles_y, int relu) {
+    using G = ConvGeom<KS>;
+    constexpr int CK = G::CK;
+    __shared__ float s_in[CK * G::NPIX];
+    __shared__ __attribute__((aligned(16))) float s_w[KS * KS * CK * 64];
+
+    const int tid = threadIdx.x;
+    const int wv = tid >> 6, lane = tid & 63, li = lane & 31, lh = lane >> 5;
+    const int n0 = blockIdx.y * 64;
+    int b = 0, y0 = 0, x0 = 0;
+    long m0 = 0;  // KS == 1: first linear pixel of the tile
+    const long M = (long)B * H * W;
+    if constexpr (KS == 3) {
+        int t = blockIdx.x;
+        int tx = t % tiles_x;
+        t /= tiles_x;
+        int ty = t % tiles_y;
+        b = t / tiles_y;
+        y0 = ty * G::TH;
+        x0 = tx * G::TW;
+    } else {
+        m0 = (long)blockIdx.x * 256;
+    }
+
+    f32x16 acc[2][2];
+#pragma unroll
+    for (int r = 0; r < 2; r++)
+#pragma unroll
+        for (int nb = 0; nb < 2; nb++)
+#pragma unroll
+            for (int e = 0; e < 16; e++) acc[r][nb][e] = 0.0f;
+
+    for (int c0 = 0; c0 < cin; c0 += CK) {
+        // ---- stage input pixels (16-byte loads of 4 channels) ----
+        constexpr int Q = CK / 4;
+        for (int idx = tid; idx < G::NPIX * Q; idx += 256) {
+            int p = idx / Q, q = idx - p * Q;
+            f32x4 v = {0.f, 0.f, 0.f, 0.f};
+            if constexpr (KS == 3) {
+                int py = p / G::PW, px = p - py * G::PW;
+                int gy = y0 - 1 + py, gx = x0 - 1 + px;
+                if (gy >= 0 && gy < H && gx >= 0 && gx < W)
+                    v = *reinterpret_cast<const f32x4*>(in + (((size_t)b * H + gy) * W + gx) * in_cstride + in_coff + c0 + 4 * q);
+            } else {
+                long m = m0 + p;
+                if (m < M) v = *reinterpret_cast<const f32x4*>(in + (size_t)m * in_cstride + in_coff + c0 + 4 * q);
+            }
+#pragma unroll
+            for (int e = 0; e < 4; e++) s_in[(4 * q + e) * G::NPIX + p] = v[e];
+        }
+        // ---- stage weights rows (kk, c) x 64 channels ----
+        for (int idx = tid; idx < KS * KS * CK * 16; idx += 256) {
+            int r = idx >> 4, q = idx & 15;
+            int kk = r / CK, c = r - kk * CK;
+            const f32x4 v = *reinterpret_cast<const f32x4*>(wt + ((size_t)kk * cin + c0 + c) * cout_pad + n0 + 4 * q);
+            *reinterpret_cast<f32x4*>(&s_w[r * 64 + 4 * q]) = v;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int kk = 0; kk < KS * KS; kk++) {
+            const int ky = kk / KS, kx = kk % KS;
+#pragma unroll
+            for (int cp = 0; cp < CK / 2; cp++) {
+                const int c = 2 * cp + lh;
+                const float* si = &s_in[c * G::NPIX];
+                float a0, a1;
+                if constexpr (KS == 3) {
+                    a0 = si[(2 * wv + 0 + ky) * G::PW + li + kx];
+                    a1 = si[(2 * wv + 1 + ky) * G::PW + li + kx];
+                } else {
+                    a0 = si[(2 * wv + 0) * 32 + li];
+                    a1 = si[(2 * wv + 1) * 32 + li];
+                }
+                const float b0 = s_w[(kk * CK + c) * 64 + li];
+                const float b1 = s_w[(kk * CK + c) * 64 + 32 + li];
+                acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b0, acc[0][0], 0, 0, 0);
+                acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b1, acc[0][1], 0, 0, 0);
+                acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b0, acc[1][0], 0, 0, 0);
+                acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b1, acc[1][1], 0, 0, 0);
+            }
+        }
+        __syncthreads();
+    }
+
+    // ---- epilogue: C/D map of 32x32 blocks: col (out channel) = lane&31,
+    //      row (pixel in the 32-segment) = (reg&3) + 8*(reg>>2) + 4*(lane>>5) ----
+#pragma unroll
+    for (int nb = 0; nb < 2; nb++) {
+        const int n = n0 + nb * 32 + li;
+        if (n >= cout) continue;
+        const float bv = bias[n];
+        if constexpr (POOL) {
+            const int y = y0 + 2 * wv;  // pool window rows y, y+1 live in acc[0], acc[1]
+            if (y >= H) continue;
+            const int Wo = W >> 1;
+#pragma unroll
+            for (int reg = 0; reg < 16; reg += 2) {
+                const int px = (reg & 3) + 8 * (reg >> 2) + 4 * lh;
+                const int x = x0 + px;
+                if (x >= W) continue;
+                float m = fmaxf(fmaxf(acc[0][nb][reg], acc[0][nb][reg + 1]), fmaxf(acc[1][nb][reg], acc[1][nb][reg + 1]));
+                m += bv;
+                if (relu) m = fmaxf(m, 0.0f);
+                out[(((size_t)b * (H >> 1) + (y >> 1)) * Wo + (x >> 1)) * out_cstride + out_coff + n] = m;
+            }
+        } else {
+#pragma unroll
+            for (int r = 0; r < 2; r++) {
+#pragma unroll
+                for (int reg = 0; reg < 16; reg++) {
+                    const int px = (reg & 3) + 8 * (reg >> 2) + 4 * lh;
+                    float v = acc[r][nb][reg] + bv;
+                    if (relu) v = fmaxf(v, 0.0f);
+                    if constexpr (KS == 3) {
+                        const int y = y0 + 2 * wv + r, x = x0 + px;
+                        if (y < H && x < W)
+                            out[(((size_t)b * H + y) * W + x) * out_cstride + out_coff + n] = v;
+                    } else {
+                        const long m = m0 + (2 * wv + r) * 32 + px;
+                        if (m < M) out[(size_t)m * out_cstride + out_coff + n] = v;
+                    }
+                }
+            }
+        }
+    }
+}
+
+// Descriptor head output: L2-normalise every pixel's 256 channels (MagicLeap export convention,
+// SURVEY.md 8(a) A3).  One wave per pixel, 16-byte loads, shuffle-tree sum of squares.
+__global__ __launch_bounds__(256) void k_desc_l2norm(float* __restrict__ d, long npix) {
+    long p = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+    int lane = threadIdx.x & 63;
+    if (p >= npix) return;
+    f32x4* row = reinterpret_cast<f32x4*>(d + (size_t)p * 256);
+    f32x4 v = row[lane];
+    float ss = v[0] * v[0] + v[1] * v[1] + v[2] * v[2] + v[3] * v[3];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) ss += __shfl_xor(ss, o);
+    float nrm = sqrtf(ss);
+    nrm = fmaxf(nrm, 1e-12f);
+    v[0] /= nrm; v[1] /= nrm; v[2] /= nrm; v[3] /= nrm;
+    row[lane] = v;
+}
+
+namespace {
+
+template <int KS, bool POOL, int LAYER>
+int launch_conv(const DevLayer& L, const float* in, int in_cstride, int in_coff, float* out,
+                int out_cstride, int out_coff, int B, int H, int W, int relu, hipStream_t s) {
+    using G = ConvGeom<KS>;
+    if (L.cin % G::CK != 0 || L.cout_pad % 64 != 0 || in_cstride % 4 || in_coff % 4) {
+        set_error("conv: unsupported channel geometry");
+        return VS_ERR_ARG;
+    }
+    int tiles_x = 1, tiles_y = 1;
+    long nblk;
+    if (KS == 3) {
+        tiles_x = (W + G::TW - 1) / G::TW;
+        tiles_y = (H + G::TH - 1) / G::TH;
+        nblk = (long)B * tiles_x * tiles_y;
+    } else {
+        nblk = ((long)B * H * W + 255) / 256;
+    }
+    if (POOL && ((H | W) & 1)) {
+        set_error("conv: pooled layer needs even H, W");
+        return VS_ERR_ARG;
+    }
+    dim3 grid((unsigned)nblk, L.cout_pad / 64);
+    hipLaunchKernelGGL((k_conv_mfma<KS, POOL, LAYER>), grid, dim3(256), 0, s, in, in_cstride, in_coff, L.w, L.b,
+                       L.cin, L.cout, L.cout_pad, out, out_cstride, out_coff, B, H, W, tiles_x, tiles_y, relu);
+    VS_HIP(hipGetLastError());
+    return VS_OK;
+}
+
+}  // namespace
+
+int sp_forward(vs_ctx* ctx, int B, const uint8_t* d_img, int channels, int h, int w, hipStream_t s) {
+    const int Hp = ((h + 7) / 8) * 8, Wp = ((w + 7) / 8) * 8;
+    const int hc = Hp / 8, wc = Wp / 8;
+    const size_t full = (size_t)B * Hp * Wp;
+    VS_CHECK(ctx->gray.ensure(full * sizeof(float)));
+    VS_CHECK(ctx->act0.ensure(full * 64 * sizeof(float)));
+    VS_CHECK(ctx->act1.ensure(full / 4 * 64 * sizeof(float)));
+    VS_CHECK(ctx->semi.ensure((size_t)B * hc * wc * kSemiCh * sizeof(float)));
+    VS_CHECK(ctx->dgrid.ensure((size_t)B * hc * wc * kDescDim * sizeof(float)));
+    float* gray = ctx->gray.as<float>();
+    float* a0 = ctx->act0.as<float>();
+    float* a1 = ctx->act1.as<float>();
+    const DevLayer* L = ctx->layers;
+    if (d_img) {
+        ProfScope ps(ctx, "gray_norm", s);
+        int total = (int)full;
+        hipLaunchKernelGGL(k_gray_norm, dim3((total + 255) / 256), dim3(256), 0, s, d_img, channels, h, w, Hp, Wp,
+                           gray, total);
+        VS_HIP(hipGetLastError());
+    }
+    {
+        ProfScope ps(ctx, "conv1a", s);
+        int total = (int)full;
+        hipLaunchKernelGGL(k_conv1a, dim3((total + 255) / 256), dim3(256), 0, s, gray, L[0].w, L[0].b, a0, Hp, Wp,
+                           total);
+        VS_HIP(hipGetLastError());
+    }
+    int H = Hp, W = Wp;
+    {
+        ProfScope ps(ctx, "conv1b_pool", s);
+        VS_CHECK((launch_conv<3, true, 1>(L[1], a0, 64, 0, a1, 64, 0, B, H, W, 1, s)));
+    }
+    H /= 2; W /= 2;
+    {
+        ProfScope ps(ctx, "conv2a", s);
+        VS_CHECK((launch_conv<3, false, 2>(L[2], a1, 64, 0, a0, 64, 0, B, H, W, 1, s)));
+    }
+    {
+        ProfScope ps(ctx, "conv2b_pool", s);
+        VS_CHECK((launch_conv<3, true, 3>(L[3], a0, 64, 0, a1, 64, 0, B, H, W, 1, s)));
+    }
+    H /= 2; W /= 2;
+    {
+        ProfScope ps(ctx, "conv3a", s);
+        VS_CHECK((launch_conv<3, false, 4>(L[4], a1, 64, 0, a0, 128, 0, B, H, W, 1, s)));
+    }
+    {
+        ProfScope ps(ctx, "conv3b_pool", s);
+        VS_CHECK((launch_conv<3, true, 5>(L[5], a0, 128, 0, a1, 128, 0, B, H, W, 1, s)));
+    }
+    H /= 2; W /= 2;
+    {
+        ProfScope ps(ctx, "conv4a", s);
+        VS_CHECK((launch_conv<3, false, 6>(L[6], a1, 128, 0, a0, 128, 0, B, H, W, 1, s)));
+    }
+    {
+        ProfScope ps(ctx, "conv4b", s);
+        VS_CHECK((launch_conv<3, false, 7>(L[7], a0, 128, 0, a1, 128, 0, B, H, W, 1, s)));
+    }
+    {
+        ProfScope ps(ctx, "head_a", s);  // convPa | convDa, 128 -> 512
+        VS_CHECK((launch_conv<3, false, 8>(ctx->head_a, a1, 128, 0, a0, 512, 0, B, H, W, 1, s)));
+    }
+    {
+        ProfScope ps(ctx, "head_b", s);  // convPb 256 -> 65 and convDb 256 -> 256 (1x1)
+        VS_CHECK((launch_conv<1, false, 9>(L[9], a0, 512, 0, ctx->semi.as<float>(), kSemiCh, 0, B, H, W, 0, s)));
+        VS_CHECK((launch_conv<1, false, 11>(L[11], a0, 512, 256, ctx->dgrid.as<float>(), kDescDim, 0, B, H, W, 0, s)));
+    }
+    {
+        ProfScope ps(ctx, "desc_l2norm", s);
+        long npix = (long)B * H * W;
+        hipLaunchKernelGGL(k_desc_l2norm, dim3((unsigned)((npix + 3) / 4)), dim3(256), 0, s, ctx->dgrid.as<float>(),
+                           npix);
+        VS_HIP(hipGetLastError());
+    }
+    return VS_OK;
+}
+
+}  // namespace vs

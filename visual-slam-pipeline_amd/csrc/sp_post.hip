@@ -1,0 +1,401 @@
+// sp_post.hip — SuperPoint post-processing on gfx950: heatmap decode, greedy NMS, descriptor
+// sampling (reference src/FeatureExtractor.cpp:126-206 and nms() :219-259).
+//
+// Compiled with -ffp-contract=off: every float expression keeps the reference's evaluation order
+// and IEEE rounding (division and sqrt correctly rounded), so the keypoints (pixel indices and
+// scores) and the sampled descriptors are bit-identical to the CPU restatement given the same
+// semi / desc tensors.
+//
+// NMS.  The reference sorts the candidates (score > 0.005) by score and greedily keeps a
+// candidate unless a kept one lies in its 9x9 window, stopping at 400.  Here the greedy set is
+// computed as a priority maximal independent set in parallel rounds over the dense heatmap: an
+// undecided pixel becomes kept when every higher-priority pixel of its window is already out,
+// and out when a kept pixel lies in its window.  States only move forward, so stale halo reads
+// are safe and the fixed point is exactly the sequential greedy set for the total order
+// (score desc, raster index asc).  The 400-cap then takes the 400 highest-priority kept pixels:
+// greedy decisions never depend on lower-priority candidates, so the capped greedy output is the
+// top 400 of the uncapped set.
+#include <hip/hip_runtime.h>
+
+#include "glibc_expf.h"
+#include "vs_internal.h"
+
+namespace vs {
+
+constexpr float kConfThresh = 0.005f;  // SP_CONFIDENCE_THRESHOLD (Config.h:40)
+constexpr int kRadius = 4;             // SP_NMS_RADIUS (Config.h:41)
+constexpr int kMaxKeypoints = 400;     // SP_MAX_KEYPOINTS (Config.h:42)
+constexpr int kNmsTile = 32;
+constexpr int kNmsReg = kNmsTile + 2 * kRadius;
+constexpr int kNmsMaxRounds = 48;
+
+enum : uint8_t { ST_UNDECIDED = 0, ST_KEPT = 1, ST_OUT = 2 };
+
+// ---------------------------------------------------------------------------------------------
+// A4 decode: one thread per 8x8 cell.  std::exp(float) is glibc's expf, which is not correctly
+// rounded; glibc_expf.h restates its algorithm instruction for instruction (checked exhaustively
+// against libm on the host by tests/test_oracle.py, and on the device through the decode parity
+// tests of tests/test_gpu_parity.py).
+__global__ __launch_bounds__(256) void k_decode(const float* __restrict__ semi, int hc, int wc, int B,
+                                                float* __restrict__ heat, uint8_t* __restrict__ state) {
+    int idx = blockIdx.x * blockDim.x + threadIdx.x;
+    int ncell = hc * wc;
+    if (idx >= B * ncell) return;
+    int b = idx / ncell, cidx = idx - b * ncell;
+    int cy = cidx / wc, cx = cidx - cy * wc;
+    const float* p = semi + (size_t)idx * kSemiCh;
+    float cell[kSemiCh];
+#pragma unroll
+    for (int c = 0; c < kSemiCh; c++) cell[c] = p[c];
+    float mx = cell[0];
+#pragma unroll
+    for (int c = 1; c < kSemiCh; c++) mx = (cell[c] > mx) ? cell[c] : mx;
+    float sum = 0.0f;
+#pragma unroll
+    for (int c = 0; c < kSemiCh; c++) {
+        cell[c] = vs_expf::glibc_expf(cell[c] - mx);
+        sum += cell[c];
+    }
+    const int Wp = wc * 8;
+    float* hb = heat + (size_t)b * ncell * 64;
+    uint8_t* sb = state + (size_t)b * ncell * 64;
+#pragma unroll
+    for (int c = 0; c < 64; c++) {
+        float v = __fdiv_rn(cell[c], sum);
+        size_t o = (size_t)(cy * 8 + c / 8) * Wp + cx * 8 + (c % 8);
+        hb[o] = v;
+        sb[o] = (v > kConfThresh) ? ST_UNDECIDED : ST_OUT;
+    }
+}
+
+// One NMS round over a 32x32 tile (+4 halo).  The tile iterates to its local fixed point, writes
+// its interior states back and flags the frame if anything is still undecided.
+// flags[r*B + b] != 0  <=>  frame b still had undecided pixels after round r-1.
+__global__ __launch_bounds__(256) void k_nms_round(const float* __restrict__ heat, uint8_t* __restrict__ state,
+                                                   int* __restrict__ flags, int r, int B, int Hp, int Wp,
+                                                   int tiles_x) {
+    const int b = blockIdx.y;
+    if (flags[r * B + b] == 0) return;
+    __shared__ float s_score[kNmsReg * kNmsReg];
+    __shared__ uint8_t s_state[kNmsReg * kNmsReg];
+    const int tx = blockIdx.x % tiles_x, ty = blockIdx.x / tiles_x;
+    const int gx0 = tx * kNmsTile - kRadius, gy0 = ty * kNmsTile - kRadius;
+    const float* hb = heat + (size_t)b * Hp * Wp;
+    uint8_t* sb = state + (size_t)b * Hp * Wp;
+    for (int i = threadIdx.x; i < kNmsReg * kNmsReg; i += 256) {
+        int ry = i / kNmsReg, rx = i - ry * kNmsReg;
+        int gy = gy0 + ry, gx = gx0 + rx;
+        bool in = gy >= 0 && gy < Hp && gx >= 0 && gx < Wp;
+        s_score[i] = in ? hb[(size_t)gy * Wp + gx] : 0.0f;
+        s_state[i] = in ? sb[(size_t)gy * Wp + gx] : ST_OUT;
+    }
+    __syncthreads();
+    // each thread owns 4 interior pixels
+    int own[4];
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        int k = threadIdx.x + 256 * j;
+        int iy = k / kNmsTile, ix = k - iy * kNmsTile;
+        own[j] = (iy + kRadius) * kNmsReg + ix + kRadius;
+    }
+    int changed;
+    do {
+        uint8_t ns[4];
+        int ch = 0;
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const int p = own[j];
+            ns[j] = s_state[p];
+            if (ns[j] != ST_UNDECIDED) continue;
+            const float sp = s_score[p];
+            bool kept_nb = false, blocked = false;
+            for (int dy = -kRadius; dy <= kRadius && !kept_nb; dy++) {
+                for (int dx = -kRadius; dx <= kRadius; dx++) {
+                    if (dx == 0 && dy == 0) continue;
+                    const int q = p + dy * kNmsReg + dx;
+                    const uint8_t sq = s_state[q];
+                    if (sq == ST_KEPT) {
+                        kept_nb = true;
+                        break;
+                    }
+                    if (sq == ST_UNDECIDED) {
+                        const float s = s_score[q];
+                        // q precedes p in raster order iff dy < 0 || (dy == 0 && dx < 0)
+                        if (s > sp || (s == sp && (dy < 0 || (dy == 0 && dx < 0)))) blocked = true;
+                    }
+                }
+            }
+            if (kept_nb) {
+                ns[j] = ST_OUT;
+                ch = 1;
+            } else if (!blocked) {
+                ns[j] = ST_KEPT;
+                ch = 1;
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < 4; j++) s_state[own[j]] = ns[j];
+        changed = __syncthreads_or(ch);
+    } while (changed);
+    int und = 0;
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        int k = threadIdx.x + 256 * j;
+        int iy = k / kNmsTile, ix = k - iy * kNmsTile;
+        int gy = gy0 + kRadius + iy, gx = gx0 + kRadius + ix;
+        if (gy < Hp && gx < Wp) {
+            uint8_t v = s_state[own[j]];
+            sb[(size_t)gy * Wp + gx] = v;
+            und |= (v == ST_UNDECIDED);
+        }
+    }
+    if (__syncthreads_or(und) && threadIdx.x == 0) flags[(r + 1) * B + b] = 1;
+}
+
+// Kept pixels -> 64-bit priority keys (score bits << 32 | ~raster index), unordered.
+__global__ __launch_bounds__(256) void k_nms_collect(const float* __restrict__ heat, const uint8_t* __restrict__ state,
+                                                     int Hp, int Wp, unsigned long long* __restrict__ keys,
+                                                     int* __restrict__ keycnt, int key_cap) {
+    const int b = blockIdx.y;
+    const int npx = Hp * Wp;
+    for (int i = blockIdx.x * 256 + threadIdx.x; i < npx; i += gridDim.x * 256) {
+        if (state[(size_t)b * npx + i] != ST_KEPT) continue;
+        float s = heat[(size_t)b * npx + i];
+        unsigned long long key = ((unsigned long long)__float_as_uint(s) << 32) | (unsigned)(0xFFFFFFFFu - (unsigned)i);
+        int slot = atomicAdd(&keycnt[b], 1);
+        if (slot < key_cap) keys[(size_t)b * key_cap + slot] = key;
+    }
+}
+
+// Top-K of the kept keys (exact MSB-first radix select over the 64-bit keys, which are unique),
+// bitonic sort of the K winners in descending priority, keypoint records, border erase
+// (FeatureExtractor.cpp:155-160).  One 1024-thread workgroup per frame.
+constexpr int kSelSort = 512;
+__global__ __launch_bounds__(1024) void k_nms_select(const unsigned long long* __restrict__ keys,
+                                                     const int* __restrict__ keycnt, int key_cap, int max_kp,
+                                                     int Wp, int h, int w, vs_keypoint* __restrict__ kps,
+                                                     int cap, int* __restrict__ nout, int* __restrict__ err) {
+    const int b = blockIdx.x;
+    __shared__ int hist[256];
+    __shared__ unsigned long long s_sel[kSelSort];
+    __shared__ int s_nsel;
+    __shared__ unsigned long long s_prefix, s_mask;
+    __shared__ int s_krem;
+    int nk = keycnt[b];
+    if (nk > key_cap) {
+        if (threadIdx.x == 0) atomicOr(err, 1);
+        nk = key_cap;
+    }
+    const unsigned long long* kb = keys + (size_t)b * key_cap;
+    const int K = nk < max_kp ? nk : max_kp;
+    unsigned long long kth = 0;
+    if (K > 0 && K < nk) {
+        if (threadIdx.x == 0) {
+            s_prefix = 0;
+            s_mask = 0;
+            s_krem = K;
+        }
+        for (int pass = 0; pass < 8; pass++) {
+            const int shift = 56 - 8 * pass;
+            if (threadIdx.x < 256) hist[threadIdx.x] = 0;
+            __syncthreads();
+            const unsigned long long pre = s_prefix, msk = s_mask;
+            for (int i = threadIdx.x; i < nk; i += blockDim.x) {
+                unsigned long long k = kb[i];
+                if ((k & msk) == pre) atomicAdd(&hist[(k >> shift) & 255], 1);
+            }
+            __syncthreads();
+            if (threadIdx.x == 0) {
+                int rem = s_krem, acc = 0, d = 255;
+                for (; d > 0; d--) {
+                    if (acc + hist[d] >= rem) break;
+                    acc += hist[d];
+                }
+                s_krem = rem - acc;
+                s_prefix = pre | ((unsigned long long)d << shift);
+                s_mask = msk | (255ull << shift);
+            }
+            __syncthreads();
+        }
+        kth = s_prefix;  // the K-th largest key
+    }
+    if (threadIdx.x == 0) s_nsel = 0;
+    for (int i = threadIdx.x; i < kSelSort; i += blockDim.x) s_sel[i] = 0;
+    __syncthreads();
+    for (int i = threadIdx.x; i < nk; i += blockDim.x) {
+        unsigned long long k = kb[i];
+        if (K > 0 && k >= kth) {
+            int slot = atomicAdd(&s_nsel, 1);
+            if (slot < kSelSort) s_sel[slot] = k;
+        }
+    }
+    __syncthreads();
+    // bitonic sort, descending (zero keys pad the tail)
+    for (int size = 2; size <= kSelSort; size <<= 1) {
+        for (int stride = size >> 1; stride > 0; stride >>= 1) {
+            for (int i = threadIdx.x; i < kSelSort; i += blockDim.x) {
+                int j = i ^ stride;
+                if (j > i) {
+                    bool desc = ((i & size) == 0);
+                    unsigned long long a = s_sel[i], c = s_sel[j];
+                    if (desc ? (a < c) : (a > c)) {
+                        s_sel[i] = c;
+                        s_sel[j] = a;
+                    }
+                }
+            }
+            __syncthreads();
+        }
+    }
+    if (threadIdx.x == 0) {
+        int n = 0;
+        for (int i = 0; i < K && n < cap; i++) {
+            unsigned long long k = s_sel[i];
+            unsigned idx = 0xFFFFFFFFu - (unsigned)(k & 0xFFFFFFFFull);
+            int x = (int)(idx % (unsigned)Wp), y = (int)(idx / (unsigned)Wp);
+            if (x >= w || y >= h) continue;
+            vs_keypoint kp;
+            kp.x = (float)x;
+            kp.y = (float)y;
+            kp.size = 8.0f;
+            kp.angle = -1.0f;
+            kp.response = __uint_as_float((unsigned)(k >> 32));
+            kp.octave = 0;
+            kp.class_id = -1;
+            kps[(size_t)b * cap + n] = kp;
+            n++;
+        }
+        nout[b] = n;
+    }
+}
+
+// A6: bilinear sampling of the normalised coarse grid + per-keypoint L2 normalisation.  One wave
+// per keypoint; each lane owns 4 channels; the sum of squares runs sequentially over c = 0..255
+// on lane 0 (the reference's order) from LDS.
+__global__ __launch_bounds__(256) void k_sample(const float* __restrict__ dgrid, int hc, int wc,
+                                                const vs_keypoint* __restrict__ kps, const int* __restrict__ nkp,
+                                                int cap, float* __restrict__ desc) {
+    __shared__ float s_v[4][256];
+    __shared__ float s_norm[4];
+    const int b = blockIdx.y;
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int i = blockIdx.x * 4 + wv;
+    const bool active = i < nkp[b];
+    float val[4] = {0, 0, 0, 0};
+    if (active) {
+        const vs_keypoint kp = kps[(size_t)b * cap + i];
+        float sx = kp.x / 8.0f;
+        float sy = kp.y / 8.0f;
+        int x0 = max(0, min((int)floorf(sx), wc - 1));
+        int y0 = max(0, min((int)floorf(sy), hc - 1));
+        int x1 = min(x0 + 1, wc - 1);
+        int y1 = min(y0 + 1, hc - 1);
+        float wx = sx - x0;
+        float wy = sy - y0;
+        const float* g = dgrid + (size_t)b * hc * wc * 256;
+        const float4 v00 = reinterpret_cast<const float4*>(g + ((size_t)y0 * wc + x0) * 256)[lane];
+        const float4 v01 = reinterpret_cast<const float4*>(g + ((size_t)y0 * wc + x1) * 256)[lane];
+        const float4 v10 = reinterpret_cast<const float4*>(g + ((size_t)y1 * wc + x0) * 256)[lane];
+        const float4 v11 = reinterpret_cast<const float4*>(g + ((size_t)y1 * wc + x1) * 256)[lane];
+        const float a00[4] = {v00.x, v00.y, v00.z, v00.w}, a01[4] = {v01.x, v01.y, v01.z, v01.w};
+        const float a10[4] = {v10.x, v10.y, v10.z, v10.w}, a11[4] = {v11.x, v11.y, v11.z, v11.w};
+#pragma unroll
+        for (int e = 0; e < 4; e++) {
+            val[e] = (1 - wy) * ((1 - wx) * a00[e] + wx * a01[e]) + wy * ((1 - wx) * a10[e] + wx * a11[e]);
+            s_v[wv][4 * lane + e] = val[e];
+        }
+    }
+    __syncthreads();
+    if (active && lane == 0) {
+        float nrm = 0;
+        for (int c = 0; c < 256; c++) {
+            float v = s_v[wv][c];
+            nrm += v * v;
+        }
+        s_norm[wv] = __fsqrt_rn(nrm);
+    }
+    __syncthreads();
+    if (active) {
+        const float nrm = s_norm[wv];
+        if (nrm > 1e-8f) {
+#pragma unroll
+            for (int e = 0; e < 4; e++) val[e] = __fdiv_rn(val[e], nrm);
+        }
+        float4 o = {val[0], val[1], val[2], val[3]};
+        reinterpret_cast<float4*>(desc + ((size_t)b * cap + i) * 256)[lane] = o;
+    }
+}
+
+int sp_postprocess(vs_ctx* ctx, int B, int hc, int wc, int h, int w, vs_keypoint* d_kps, float* d_desc,
+                   int* d_n, int cap, hipStream_t s) {
+    const int Hp = hc * 8, Wp = wc * 8;
+    const size_t npx = (size_t)B * Hp * Wp;
+    // Kept pixels are pairwise >= radius+1 apart (Chebyshev), so at most ceil(H/5)*ceil(W/5).
+    const int key_cap = ((Hp + kRadius) / (kRadius + 1)) * ((Wp + kRadius) / (kRadius + 1));
+    const int max_kp = cap < kMaxKeypoints ? cap : kMaxKeypoints;
+    VS_CHECK(ctx->heat.ensure(npx * sizeof(float)));
+    VS_CHECK(ctx->state.ensure(npx));
+    VS_CHECK(ctx->flags.ensure(((size_t)(kNmsMaxRounds + 1) * B + 1) * sizeof(int)));
+    VS_CHECK(ctx->keys.ensure((size_t)B * key_cap * sizeof(unsigned long long)));
+    VS_CHECK(ctx->keycnt.ensure((size_t)B * sizeof(int)));
+    int* flags = ctx->flags.as<int>();
+    int* err = flags + (size_t)(kNmsMaxRounds + 1) * B;
+    {
+        ProfScope ps(ctx, "decode", s);
+        int ncell = B * hc * wc;
+        hipLaunchKernelGGL(k_decode, dim3((ncell + 255) / 256), dim3(256), 0, s, ctx->semi.as<float>(), hc, wc, B,
+                           ctx->heat.as<float>(), ctx->state.as<uint8_t>());
+        VS_HIP(hipGetLastError());
+    }
+    {
+        ProfScope ps(ctx, "nms_rounds", s);
+        VS_HIP(hipMemsetAsync(flags, 0, ((size_t)(kNmsMaxRounds + 1) * B + 1) * sizeof(int), s));
+        // round 0 runs for every frame
+        VS_HIP(hipMemsetAsync(flags, 0x01, (size_t)B * sizeof(int), s));
+        const int tiles_x = (Wp + kNmsTile - 1) / kNmsTile, tiles_y = (Hp + kNmsTile - 1) / kNmsTile;
+        for (int r = 0; r < kNmsMaxRounds; r++) {
+            hipLaunchKernelGGL(k_nms_round, dim3(tiles_x * tiles_y, B), dim3(256), 0, s, ctx->heat.as<float>(),
+                               ctx->state.as<uint8_t>(), flags, r, B, Hp, Wp, tiles_x);
+        }
+        VS_HIP(hipGetLastError());
+    }
+    {
+        ProfScope ps(ctx, "nms_select", s);
+        VS_HIP(hipMemsetAsync(ctx->keycnt.p, 0, (size_t)B * sizeof(int), s));
+        hipLaunchKernelGGL(k_nms_collect, dim3(64, B), dim3(256), 0, s, ctx->heat.as<float>(), ctx->state.as<uint8_t>(),
+                           Hp, Wp, ctx->keys.as<unsigned long long>(), ctx->keycnt.as<int>(), key_cap);
+        hipLaunchKernelGGL(k_nms_select, dim3(B), dim3(1024), 0, s, ctx->keys.as<unsigned long long>(),
+                           ctx->keycnt.as<int>(), key_cap, max_kp, Wp, h, w, d_kps, cap, d_n, err);
+        VS_HIP(hipGetLastError());
+    }
+    {
+        ProfScope ps(ctx, "sample", s);
+        hipLaunchKernelGGL(k_sample, dim3((max_kp + 3) / 4, B), dim3(256), 0, s, ctx->dgrid.as<float>(), hc, wc,
+                           d_kps, d_n, cap, d_desc);
+        VS_HIP(hipGetLastError());
+    }
+    return VS_OK;
+}
+
+// Convergence check of the NMS rounds (host-synchronous; used by the host entry points and the
+// tests): returns VS_ERR_NOTCONV when a frame still had undecided pixels after the last round.
+int sp_postprocess_check(vs_ctx* ctx, int B, hipStream_t s) {
+    std::vector<int> f(B + 1);
+    int* flags = ctx->flags.as<int>();
+    VS_HIP(hipMemcpyAsync(f.data(), flags + (size_t)kNmsMaxRounds * B, B * sizeof(int), hipMemcpyDeviceToHost, s));
+    VS_HIP(hipMemcpyAsync(f.data() + B, flags + (size_t)(kNmsMaxRounds + 1) * B, sizeof(int), hipMemcpyDeviceToHost, s));
+    VS_HIP(hipStreamSynchronize(s));
+    for (int b = 0; b < B; b++)
+        if (f[b]) {
+            set_error("NMS did not converge within the round budget");
+            return VS_ERR_NOTCONV;
+        }
+    if (f[B]) {
+        set_error("NMS kept more pixels than the packing bound (internal error)");
+        return VS_ERR_CAPACITY;
+    }
+    return VS_OK;
+}
+
+}  // namespace vs

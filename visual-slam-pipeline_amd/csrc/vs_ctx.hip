@@ -1,0 +1,534 @@
+// vs_ctx.hip — the C ABI of libvslam_hip.so (include/vslam_abi.h): context, SuperPoint weights,
+// host entry points (synchronous, the reference's call semantics) and device-batched entry
+// points (enqueue only).  Each entry point cites the reference interface it replaces.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "vs_internal.h"
+
+namespace vs {
+
+static thread_local std::string g_err;
+void set_error(const std::string& msg) { g_err = msg; }
+
+const LayerDef kLayers[12] = {{"conv1a", 1, 64, 3},    {"conv1b", 64, 64, 3},   {"conv2a", 64, 64, 3},
+                              {"conv2b", 64, 64, 3},   {"conv3a", 64, 128, 3},  {"conv3b", 128, 128, 3},
+                              {"conv4a", 128, 128, 3}, {"conv4b", 128, 128, 3}, {"convPa", 128, 256, 3},
+                              {"convPb", 256, 65, 1},  {"convDa", 128, 256, 3}, {"convDb", 256, 256, 1}};
+
+int DevBuf::ensure(size_t n) {
+    if (n <= bytes && p) return VS_OK;
+    if (p) {
+        (void)hipFree(p);  // hipFree waits for outstanding device work
+        p = nullptr;
+        bytes = 0;
+    }
+    size_t alloc = n + n / 8 + 256;
+    if (hipMalloc(&p, alloc) != hipSuccess) {
+        p = nullptr;
+        set_error("hipMalloc of " + std::to_string(alloc) + " bytes failed");
+        return VS_ERR_NOMEM;
+    }
+    bytes = alloc;
+    return VS_OK;
+}
+
+void DevBuf::release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    bytes = 0;
+}
+
+// ---- profiling -------------------------------------------------------------------------------
+static hipEvent_t take_event(vs_ctx* c) {
+    if (!c->event_pool.empty()) {
+        hipEvent_t e = c->event_pool.back();
+        c->event_pool.pop_back();
+        return e;
+    }
+    hipEvent_t e = nullptr;
+    if (hipEventCreate(&e) != hipSuccess) return nullptr;
+    return e;
+}
+
+ProfScope::ProfScope(vs_ctx* c, const char* name, hipStream_t st) : ctx(c), stage(-1), s(st) {
+    if (!ctx->prof_on) return;
+    for (size_t i = 0; i < ctx->prof.size(); i++)
+        if (std::strcmp(ctx->prof[i].name, name) == 0) stage = (int)i;
+    if (stage < 0) {
+        ctx->prof.push_back(ProfStage{name});
+        stage = (int)ctx->prof.size() - 1;
+    }
+    e0 = take_event(ctx);
+    e1 = take_event(ctx);
+    if (e0) (void)hipEventRecord(e0, s);
+}
+
+ProfScope::~ProfScope() {
+    if (!ctx->prof_on || stage < 0 || !e0 || !e1) return;
+    (void)hipEventRecord(e1, s);
+    ctx->prof[stage].pending.emplace_back(e0, e1);
+    ctx->prof[stage].launches++;
+}
+
+// ---- synthetic weights: splitmix64 -> Box-Muller normals, He-normal scale ------------------
+static std::vector<float> synth_weights(uint64_t seed) {
+    uint64_t st = seed;
+    auto next = [&]() {
+        uint64_t z = (st += 0x9E3779B97F4A7C15ull);
+        z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+        z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+        return z ^ (z >> 31);
+    };
+    auto normal = [&]() {
+        double u1 = ((next() >> 11) + 1) * (1.0 / 9007199254740992.0);
+        double u2 = (next() >> 11) * (1.0 / 9007199254740992.0);
+        return std::sqrt(-2.0 * std::log(u1)) * std::cos(6.283185307179586 * u2);
+    };
+    std::vector<float> w;
+    for (const auto& L : kLayers) {
+        const double sd = std::sqrt(2.0 / (L.cin * L.k * L.k));
+        for (size_t i = 0; i < (size_t)L.cout * L.cin * L.k * L.k; i++) w.push_back((float)(normal() * sd));
+        for (int i = 0; i < L.cout; i++) w.push_back((float)(normal() * 0.05));
+    }
+    return w;
+}
+
+static size_t num_params() {
+    size_t n = 0;
+    for (const auto& L : kLayers) n += (size_t)L.cout * L.cin * L.k * L.k + L.cout;
+    return n;
+}
+
+// Canonical [Cout][Cin][k][k] -> device [k*k][Cin][cout_pad] (+ column offset for fused heads).
+static void to_dev_layout(const float* wsrc, const float* bsrc, const LayerDef& L, int cout_pad, int col_off,
+                          std::vector<float>& w, std::vector<float>& b) {
+    const int kk = L.k * L.k;
+    for (int co = 0; co < L.cout; co++) {
+        for (int ci = 0; ci < L.cin; ci++)
+            for (int k = 0; k < kk; k++)
+                w[((size_t)k * L.cin + ci) * cout_pad + col_off + co] = wsrc[((size_t)co * L.cin + ci) * kk + k];
+        b[col_off + co] = bsrc[co];
+    }
+}
+
+static int upload_layer(DevLayer& D, int cin, int cout, int cout_pad, int k, const std::vector<float>& w,
+                        const std::vector<float>& b) {
+    D.cin = cin;
+    D.cout = cout;
+    D.cout_pad = cout_pad;
+    D.k = k;
+    VS_HIP(hipMalloc(&D.w, w.size() * sizeof(float)));
+    VS_HIP(hipMalloc(&D.b, b.size() * sizeof(float)));
+    VS_HIP(hipMemcpy(D.w, w.data(), w.size() * sizeof(float), hipMemcpyHostToDevice));
+    VS_HIP(hipMemcpy(D.b, b.data(), b.size() * sizeof(float), hipMemcpyHostToDevice));
+    return VS_OK;
+}
+
+static int upload_weights(vs_ctx* ctx) {
+    const float* p = ctx->h_weights.data();
+    const float* wp[12];
+    const float* bp[12];
+    for (int i = 0; i < 12; i++) {
+        const LayerDef& L = kLayers[i];
+        wp[i] = p;
+        p += (size_t)L.cout * L.cin * L.k * L.k;
+        bp[i] = p;
+        p += L.cout;
+    }
+    for (int i = 0; i < 12; i++) {
+        if (i == 8 || i == 10) continue;  // convPa / convDa live in head_a
+        const LayerDef& L = kLayers[i];
+        const int cout_pad = ((L.cout + 63) / 64) * 64;
+        std::vector<float> w((size_t)L.k * L.k * L.cin * cout_pad, 0.0f), b(cout_pad, 0.0f);
+        to_dev_layout(wp[i], bp[i], L, cout_pad, 0, w, b);
+        VS_CHECK(upload_layer(ctx->layers[i], L.cin, L.cout, cout_pad, L.k, w, b));
+    }
+    {
+        const LayerDef& Pa = kLayers[8];
+        const LayerDef& Da = kLayers[10];
+        std::vector<float> w((size_t)9 * 128 * 512, 0.0f), b(512, 0.0f);
+        to_dev_layout(wp[8], bp[8], Pa, 512, 0, w, b);
+        to_dev_layout(wp[10], bp[10], Da, 512, 256, w, b);
+        VS_CHECK(upload_layer(ctx->head_a, 128, 512, 512, 3, w, b));
+    }
+    return VS_OK;
+}
+
+int sp_postprocess_check(vs_ctx* ctx, int B, hipStream_t s);  // sp_post.hip
+
+static hipStream_t pick(vs_ctx* ctx, void* stream) { return stream ? (hipStream_t)stream : ctx->stream; }
+
+template <class T>
+static int upload(DevBuf& buf, const T* src, size_t count, hipStream_t s) {
+    VS_CHECK(buf.ensure(count * sizeof(T)));
+    VS_HIP(hipMemcpyAsync(buf.p, src, count * sizeof(T), hipMemcpyHostToDevice, s));
+    return VS_OK;
+}
+
+}  // namespace vs
+
+using namespace vs;
+
+extern "C" {
+
+int vs_abi_version(void) { return VS_ABI_VERSION; }
+const char* vs_last_error(void) { return g_err.c_str(); }
+
+size_t vs_superpoint_num_params(void) { return num_params(); }
+
+int vs_create(int device, const char* weights_path, vs_ctx** out) {
+    VS_ARG(out, "vs_create: out is null");
+    *out = nullptr;
+    int ndev = 0;
+    VS_HIP(hipGetDeviceCount(&ndev));
+    VS_ARG(device >= 0 && device < ndev, "vs_create: no such device");
+    VS_HIP(hipSetDevice(device));
+    vs_ctx* ctx = new vs_ctx();
+    ctx->device = device;
+    if (weights_path) {
+        FILE* f = std::fopen(weights_path, "rb");
+        if (!f) {
+            delete ctx;
+            set_error(std::string("cannot open weights ") + weights_path);
+            return VS_ERR_IO;
+        }
+        uint32_t magic = 0, version = 0;
+        uint64_t count = 0;
+        bool okh = std::fread(&magic, 4, 1, f) == 1 && std::fread(&version, 4, 1, f) == 1 &&
+                   std::fread(&count, 8, 1, f) == 1;
+        if (!okh || magic != 0x57505356u || version != 1 || count != num_params()) {
+            std::fclose(f);
+            delete ctx;
+            set_error("malformed VSPW weight file");
+            return VS_ERR_IO;
+        }
+        ctx->h_weights.resize(count);
+        bool okd = std::fread(ctx->h_weights.data(), sizeof(float), count, f) == count;
+        std::fclose(f);
+        if (!okd) {
+            delete ctx;
+            set_error("truncated VSPW weight file");
+            return VS_ERR_IO;
+        }
+    } else {
+        ctx->h_weights = synth_weights(VS_SYNTH_WEIGHT_SEED);
+    }
+    if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete ctx;
+        set_error("hipStreamCreate failed");
+        return VS_ERR_HIP;
+    }
+    int rc = upload_weights(ctx);
+    if (rc != VS_OK) {
+        vs_destroy(ctx);
+        return rc;
+    }
+    *out = ctx;
+    return VS_OK;
+}
+
+void vs_destroy(vs_ctx* ctx) {
+    if (!ctx) return;
+    (void)hipSetDevice(ctx->device);
+    if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+    for (auto& L : ctx->layers) {
+        if (L.w) (void)hipFree(L.w);
+        if (L.b) (void)hipFree(L.b);
+    }
+    if (ctx->head_a.w) (void)hipFree(ctx->head_a.w);
+    if (ctx->head_a.b) (void)hipFree(ctx->head_a.b);
+    DevBuf* bufs[] = {&ctx->gray,  &ctx->act0,   &ctx->act1,   &ctx->semi,   &ctx->dgrid,  &ctx->heat,
+                      &ctx->state, &ctx->flags,  &ctx->keys,   &ctx->keycnt, &ctx->h_img,  &ctx->h_kps,
+                      &ctx->h_desc, &ctx->h_n,   &ctx->h_aux0, &ctx->h_aux1, &ctx->h_aux2, &ctx->h_aux3,
+                      &ctx->h_aux4, &ctx->h_aux5, &ctx->norms};
+    for (DevBuf* b : bufs) b->release();
+    for (auto& st : ctx->prof)
+        for (auto& pr : st.pending) {
+            (void)hipEventDestroy(pr.first);
+            (void)hipEventDestroy(pr.second);
+        }
+    for (hipEvent_t e : ctx->event_pool) (void)hipEventDestroy(e);
+    if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+    delete ctx;
+}
+
+void* vs_stream(vs_ctx* ctx) { return ctx ? (void*)ctx->stream : nullptr; }
+
+int vs_superpoint_get_weights(vs_ctx* ctx, float* out, size_t count) {
+    VS_ARG(ctx && out && count == ctx->h_weights.size(), "vs_superpoint_get_weights: bad arguments");
+    std::memcpy(out, ctx->h_weights.data(), count * sizeof(float));
+    return VS_OK;
+}
+
+int vs_superpoint_save_weights(vs_ctx* ctx, const char* path) {
+    VS_ARG(ctx && path, "vs_superpoint_save_weights: bad arguments");
+    FILE* f = std::fopen(path, "wb");
+    if (!f) {
+        set_error(std::string("cannot write ") + path);
+        return VS_ERR_IO;
+    }
+    uint32_t magic = 0x57505356u, version = 1;
+    uint64_t count = ctx->h_weights.size();
+    bool ok = std::fwrite(&magic, 4, 1, f) == 1 && std::fwrite(&version, 4, 1, f) == 1 &&
+              std::fwrite(&count, 8, 1, f) == 1 &&
+              std::fwrite(ctx->h_weights.data(), sizeof(float), count, f) == count;
+    std::fclose(f);
+    if (!ok) {
+        set_error("short write of weight file");
+        return VS_ERR_IO;
+    }
+    return VS_OK;
+}
+
+// ---- FeatureExtractor::extract (FeatureExtractor.cpp:49-81) -----------------------------------
+int vs_extract_batch_dev(vs_ctx* ctx, int B, const uint8_t* d_imgs, int h, int w, vs_keypoint* d_kps,
+                         float* d_desc, int* d_n, int cap, void* stream) {
+    VS_ARG(ctx && d_imgs && d_kps && d_desc && d_n, "vs_extract_batch_dev: null argument");
+    VS_ARG(B > 0 && h >= 8 && w >= 8 && cap >= 1, "vs_extract_batch_dev: bad sizes");
+    hipStream_t s = pick(ctx, stream);
+    VS_HIP(hipSetDevice(ctx->device));
+    VS_CHECK(sp_forward(ctx, B, d_imgs, 3, h, w, s));
+    const int hc = (h + 7) / 8, wc = (w + 7) / 8;
+    VS_CHECK(sp_postprocess(ctx, B, hc, wc, h, w, d_kps, d_desc, d_n, cap, s));
+    return VS_OK;
+}
+
+int vs_extract_batch(vs_ctx* ctx, int B, const uint8_t* const* imgs, int h, int w, int channels, size_t stride,
+                     vs_keypoint* kps, float* desc, int cap, int* n) {
+    VS_ARG(ctx && imgs && kps && desc && n, "vs_extract_batch: null argument");
+    VS_ARG(B > 0 && h >= 8 && w >= 8 && cap >= 1, "vs_extract_batch: bad sizes");
+    VS_ARG(channels == 3 || channels == 1, "vs_extract_batch: channels must be 1 or 3");
+    VS_ARG(stride >= (size_t)w * channels, "vs_extract_batch: stride too small");
+    VS_HIP(hipSetDevice(ctx->device));
+    hipStream_t s = ctx->stream;
+    const size_t frame = (size_t)h * w * channels;
+    std::vector<uint8_t> packed(frame * B);
+    for (int b = 0; b < B; b++) {
+        VS_ARG(imgs[b], "vs_extract_batch: null frame");
+        for (int y = 0; y < h; y++)
+            std::memcpy(&packed[b * frame + (size_t)y * w * channels], imgs[b] + (size_t)y * stride, (size_t)w * channels);
+    }
+    VS_CHECK(upload(ctx->h_img, packed.data(), packed.size(), s));
+    VS_CHECK(ctx->h_kps.ensure((size_t)B * cap * sizeof(vs_keypoint)));
+    VS_CHECK(ctx->h_desc.ensure((size_t)B * cap * 256 * sizeof(float)));
+    VS_CHECK(ctx->h_n.ensure((size_t)B * sizeof(int)));
+    VS_CHECK(sp_forward(ctx, B, ctx->h_img.as<uint8_t>(), channels, h, w, s));
+    const int hc = (h + 7) / 8, wc = (w + 7) / 8;
+    VS_CHECK(sp_postprocess(ctx, B, hc, wc, h, w, ctx->h_kps.as<vs_keypoint>(), ctx->h_desc.as<float>(),
+                            ctx->h_n.as<int>(), cap, s));
+    VS_CHECK(sp_postprocess_check(ctx, B, s));
+    VS_HIP(hipMemcpyAsync(n, ctx->h_n.p, (size_t)B * sizeof(int), hipMemcpyDeviceToHost, s));
+    VS_HIP(hipMemcpyAsync(kps, ctx->h_kps.p, (size_t)B * cap * sizeof(vs_keypoint), hipMemcpyDeviceToHost, s));
+    VS_HIP(hipMemcpyAsync(desc, ctx->h_desc.p, (size_t)B * cap * 256 * sizeof(float), hipMemcpyDeviceToHost, s));
+    VS_HIP(hipStreamSynchronize(s));
+    return VS_OK;
+}
+
+int vs_extract(vs_ctx* ctx, const uint8_t* img, int h, int w, int channels, size_t stride, vs_keypoint* kps,
+               float* desc, int cap, int* n) {
+    const uint8_t* imgs[1] = {img};
+    VS_ARG(img, "vs_extract: null image");
+    return vs_extract_batch(ctx, 1, imgs, h, w, channels, stride, kps, desc, cap, n);
+}
+
+// ---- stage isolation ----------------------------------------------------------------------------
+int vs_superpoint_forward(vs_ctx* ctx, const float* gray01, int h, int w, float* semi, float* desc_grid) {
+    VS_ARG(ctx && gray01 && semi && desc_grid, "vs_superpoint_forward: null argument");
+    VS_ARG(h >= 8 && w >= 8 && h % 8 == 0 && w % 8 == 0, "vs_superpoint_forward: h, w must be multiples of 8");
+    VS_HIP(hipSetDevice(ctx->device));
+    hipStream_t s = ctx->stream;
+    VS_CHECK(upload(ctx->gray, gray01, (size_t)h * w, s));
+    VS_CHECK(sp_forward(ctx, 1, nullptr, 1, h, w, s));
+    const int hc = h / 8, wc = w / 8, P = hc * wc;
+    std::vector<float> sm((size_t)P * kSemiCh), dg((size_t)P * kDescDim);
+    VS_HIP(hipMemcpyAsync(sm.data(), ctx->semi.p, sm.size() * sizeof(float), hipMemcpyDeviceToHost, s));
+    VS_HIP(hipMemcpyAsync(dg.data(), ctx->dgrid.p, dg.size() * sizeof(float), hipMemcpyDeviceToHost, s));
+    VS_HIP(hipStreamSynchronize(s));
+    for (int i = 0; i < P; i++) {
+        for (int c = 0; c < kSemiCh; c++) semi[(size_t)c * P + i] = sm[(size_t)i * kSemiCh + c];
+        for (int c = 0; c < kDescDim; c++) desc_grid[(size_t)c * P + i] = dg[(size_t)i * kDescDim + c];
+    }
+    return VS_OK;
+}
+
+int vs_postprocess(vs_ctx* ctx, const float* semi, const float* desc_grid, int hc, int wc, int h, int w,
+                   vs_keypoint* kps, float* desc, int cap, int* n) {
+    VS_ARG(ctx && semi && desc_grid && kps && desc && n, "vs_postprocess: null argument");
+    VS_ARG(hc > 0 && wc > 0 && h <= hc * 8 && w <= wc * 8 && cap >= 1, "vs_postprocess: bad sizes");
+    VS_HIP(hipSetDevice(ctx->device));
+    hipStream_t s = ctx->stream;
+    const int P = hc * wc;
+    std::vector<float> sm((size_t)P * kSemiCh), dg((size_t)P * kDescDim);
+    for (int i = 0; i < P; i++) {
+        for (int c = 0; c < kSemiCh; c++) sm[(size_t)i * kSemiCh + c] = semi[(size_t)c * P + i];
+        for (int c = 0; c < kDescDim; c++) dg[(size_t)i * kDescDim + c] = desc_grid[(size_t)c * P + i];
+    }
+    VS_CHECK(upload(ctx->semi, sm.data(), sm.size(), s));
+    VS_CHECK(upload(ctx->dgrid, dg.data(), dg.size(), s));
+    VS_CHECK(ctx->h_kps.ensure((size_t)cap * sizeof(vs_keypoint)));
+    VS_CHECK(ctx->h_desc.ensure((size_t)cap * 256 * sizeof(float)));
+    VS_CHECK(ctx->h_n.ensure(sizeof(int)));
+    VS_CHECK(sp_postprocess(ctx, 1, hc, wc, h, w, ctx->h_kps.as<vs_keypoint>(), ctx->h_desc.as<float>(),
+                            ctx->h_n.as<int>(), cap, s));
+    VS_CHECK(sp_postprocess_check(ctx, 1, s));
+    VS_HIP(hipMemcpyAsync(n, ctx->h_n.p, sizeof(int), hipMemcpyDeviceToHost, s));
+    VS_HIP(hipMemcpyAsync(kps, ctx->h_kps.p, (size_t)cap * sizeof(vs_keypoint), hipMemcpyDeviceToHost, s));
+    VS_HIP(hipMemcpyAsync(desc, ctx->h_desc.p, (size_t)cap * 256 * sizeof(float), hipMemcpyDeviceToHost, s));
+    VS_HIP(hipStreamSynchronize(s));
+    return VS_OK;
+}
+
+// ---- Slam::match_features (Slam.cpp:1140-1172) -------------------------------------------------
+int vs_match_pairs_dev(vs_ctx* ctx, int P, const int* d_pairs, int F, const float* d_desc, const int* d_n, int cap,
+                       float ratio, vs_match* d_raw, int* d_nraw, vs_match* d_good, int* d_ngood, void* stream) {
+    VS_ARG(ctx && d_pairs && d_desc && d_n && d_raw && d_nraw && d_good && d_ngood, "vs_match_pairs_dev: null");
+    VS_ARG(P >= 0 && F > 0 && cap >= 1, "vs_match_pairs_dev: bad sizes");
+    VS_HIP(hipSetDevice(ctx->device));
+    return match_pairs(ctx, P, d_pairs, F, d_desc, d_n, cap, ratio, d_raw, d_nraw, d_good, d_ngood, pick(ctx, stream));
+}
+
+int vs_match_ratio(vs_ctx* ctx, const float* desc1, int n1, const float* desc2, int n2, float ratio, vs_match* raw,
+                   int* n_raw, vs_match* good, int* n_good) {
+    VS_ARG(ctx && n_raw && n_good, "vs_match_ratio: null argument");
+    VS_ARG(n1 >= 0 && n2 >= 0, "vs_match_ratio: negative size");
+    VS_ARG((n1 == 0 || desc1) && (n2 == 0 || desc2), "vs_match_ratio: null descriptors");
+    *n_raw = 0;
+    *n_good = 0;
+    if (n1 == 0 || n2 < 2) return VS_OK;  // empty Mat / fewer than k=2 neighbours: no matches
+    VS_ARG(raw && good, "vs_match_ratio: null outputs");
+    VS_HIP(hipSetDevice(ctx->device));
+    hipStream_t s = ctx->stream;
+    const int cap = n1 > n2 ? n1 : n2;
+    VS_CHECK(ctx->h_desc.ensure((size_t)2 * cap * 256 * sizeof(float)));
+    float* dd = ctx->h_desc.as<float>();
+    VS_HIP(hipMemcpyAsync(dd, desc1, (size_t)n1 * 256 * sizeof(float), hipMemcpyHostToDevice, s));
+    VS_HIP(hipMemcpyAsync(dd + (size_t)cap * 256, desc2, (size_t)n2 * 256 * sizeof(float), hipMemcpyHostToDevice, s));
+    const int meta[4] = {n1, n2, 0, 1};  // n[0..1], pairs[0..1]
+    VS_CHECK(upload(ctx->h_n, meta, 4, s));
+    const int* d_n = ctx->h_n.as<int>();
+    VS_CHECK(ctx->h_aux0.ensure((size_t)2 * cap * sizeof(vs_match) + 2 * sizeof(int)));
+    vs_match* d_raw = ctx->h_aux0.as<vs_match>();
+    vs_match* d_good = d_raw + cap;
+    int* d_cnt = reinterpret_cast<int*>(d_good + cap);
+    VS_CHECK(match_pairs(ctx, 1, d_n + 2, 2, dd, d_n, cap, ratio, d_raw, d_cnt, d_good, d_cnt + 1, s));
+    int cnt[2];
+    VS_HIP(hipMemcpyAsync(cnt, d_cnt, sizeof(cnt), hipMemcpyDeviceToHost, s));
+    VS_HIP(hipStreamSynchronize(s));
+    *n_raw = cnt[0];
+    *n_good = cnt[1];
+    VS_HIP(hipMemcpyAsync(raw, d_raw, (size_t)cnt[0] * sizeof(vs_match), hipMemcpyDeviceToHost, s));
+    VS_HIP(hipMemcpyAsync(good, d_good, (size_t)cnt[1] * sizeof(vs_match), hipMemcpyDeviceToHost, s));
+    VS_HIP(hipStreamSynchronize(s));
+    return VS_OK;
+}
+
+// ---- Slam::estimate_motion_3d3d (Slam.cpp:214-375) -----------------------------------------------
+int vs_ransac_3d3d_pairs_dev(vs_ctx* ctx, int P, const int* d_pairs, const vs_keypoint* d_kps, int cap,
+                             const vs_match* d_good, const int* d_ngood, const float* d_depth, int h, int w,
+                             const double K[4], const uint32_t* d_seeds, int iters, double thr, double* d_R,
+                             double* d_t, int* d_ok, int* d_diag, void* stream) {
+    VS_ARG(ctx && d_pairs && d_kps && d_good && d_ngood && d_depth && K && d_seeds && d_R && d_t && d_ok && d_diag,
+           "vs_ransac_3d3d_pairs_dev: null argument");
+    VS_ARG(cap >= 1 && cap <= 512, "vs_ransac_3d3d_pairs_dev: cap must be in [1, 512]");
+    VS_HIP(hipSetDevice(ctx->device));
+    return ransac3d_pairs(ctx, P, d_pairs, d_kps, cap, d_good, d_ngood, d_depth, h, w, K, d_seeds, iters, thr, d_R,
+                          d_t, d_ok, d_diag, pick(ctx, stream));
+}
+
+int vs_ransac_3d3d(vs_ctx* ctx, const float* pts1, const float* pts2, int n, const float* depth1,
+                   const float* depth2, int h, int w, const double K[4], uint32_t seed, int iters, double thr,
+                   double R[9], double t[3], int* ok, int diag[4]) {
+    VS_ARG(ctx && depth1 && depth2 && K && R && t && ok, "vs_ransac_3d3d: null argument");
+    VS_ARG(n >= 0 && n <= 512, "vs_ransac_3d3d: n must be in [0, 512]");
+    VS_ARG(n == 0 || (pts1 && pts2), "vs_ransac_3d3d: null points");
+    VS_ARG(h > 0 && w > 0, "vs_ransac_3d3d: bad depth size");
+    VS_ARG(iters > 0 && iters <= 1024, "vs_ransac_3d3d: iters must be in [1, 1024]");
+    VS_HIP(hipSetDevice(ctx->device));
+    hipStream_t s = ctx->stream;
+    const int cap = n > 0 ? n : 1;
+    std::vector<vs_keypoint> kp((size_t)2 * cap);
+    std::vector<vs_match> gm(cap);
+    for (int i = 0; i < n; i++) {
+        kp[i] = {pts1[2 * i], pts1[2 * i + 1], 0, 0, 0, 0, 0};
+        kp[cap + i] = {pts2[2 * i], pts2[2 * i + 1], 0, 0, 0, 0, 0};
+        gm[i] = {i, i, 0, 0.0f};
+    }
+    VS_CHECK(upload(ctx->h_kps, kp.data(), kp.size(), s));
+    VS_CHECK(upload(ctx->h_aux0, gm.data(), gm.size(), s));
+    VS_CHECK(ctx->h_aux1.ensure((size_t)2 * h * w * sizeof(float)));
+    float* dd = ctx->h_aux1.as<float>();
+    VS_HIP(hipMemcpyAsync(dd, depth1, (size_t)h * w * sizeof(float), hipMemcpyHostToDevice, s));
+    VS_HIP(hipMemcpyAsync(dd + (size_t)h * w, depth2, (size_t)h * w * sizeof(float), hipMemcpyHostToDevice, s));
+    const int meta[4] = {0, 1, n, (int)seed};
+    VS_CHECK(upload(ctx->h_n, meta, 4, s));
+    VS_CHECK(ctx->h_aux2.ensure(12 * sizeof(double) + 5 * sizeof(int)));
+    double* dR = ctx->h_aux2.as<double>();
+    int* dres = reinterpret_cast<int*>(dR + 12);
+    const int* dm = ctx->h_n.as<int>();
+    VS_CHECK(ransac3d_pairs(ctx, 1, dm, ctx->h_kps.as<vs_keypoint>(), cap, ctx->h_aux0.as<vs_match>(), dm + 2, dd, h,
+                            w, K, reinterpret_cast<const uint32_t*>(dm + 3), iters, thr, dR, dR + 9, dres, dres + 1,
+                            s));
+    double rt[12];
+    int res[5];
+    VS_HIP(hipMemcpyAsync(rt, dR, sizeof(rt), hipMemcpyDeviceToHost, s));
+    VS_HIP(hipMemcpyAsync(res, dres, sizeof(res), hipMemcpyDeviceToHost, s));
+    VS_HIP(hipStreamSynchronize(s));
+    std::memcpy(R, rt, 9 * sizeof(double));
+    std::memcpy(t, rt + 9, 3 * sizeof(double));
+    *ok = res[0];
+    if (diag) std::memcpy(diag, res + 1, 4 * sizeof(int));
+    return VS_OK;
+}
+
+// ---- profiling ----------------------------------------------------------------------------------
+int vs_profile_enable(vs_ctx* ctx, int on) {
+    VS_ARG(ctx, "vs_profile_enable: null ctx");
+    ctx->prof_on = on != 0;
+    return VS_OK;
+}
+
+static int drain_profile(vs_ctx* ctx) {
+    for (auto& st : ctx->prof) {
+        for (auto& pr : st.pending) {
+            VS_HIP(hipEventSynchronize(pr.second));
+            float ms = 0;
+            VS_HIP(hipEventElapsedTime(&ms, pr.first, pr.second));
+            st.ms += ms;
+            ctx->event_pool.push_back(pr.first);
+            ctx->event_pool.push_back(pr.second);
+        }
+        st.pending.clear();
+    }
+    return VS_OK;
+}
+
+int vs_profile_reset(vs_ctx* ctx) {
+    VS_ARG(ctx, "vs_profile_reset: null ctx");
+    VS_CHECK(drain_profile(ctx));
+    for (auto& st : ctx->prof) {
+        st.ms = 0;
+        st.launches = 0;
+    }
+    return VS_OK;
+}
+
+int vs_profile_read(vs_ctx* ctx, int max_stages, const char** names, double* ms, int* launches, int* n_stages) {
+    VS_ARG(ctx && n_stages, "vs_profile_read: null argument");
+    VS_CHECK(drain_profile(ctx));
+    int n = (int)ctx->prof.size();
+    *n_stages = n;
+    for (int i = 0; i < n && i < max_stages; i++) {
+        if (names) names[i] = ctx->prof[i].name;
+        if (ms) ms[i] = ctx->prof[i].ms;
+        if (launches) launches[i] = ctx->prof[i].launches;
+    }
+    return VS_OK;
+}
+
+}  // extern "C"

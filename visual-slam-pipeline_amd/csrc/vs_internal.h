@@ -1,0 +1,125 @@
+// vs_internal.h — shared declarations of libvslam_hip.so's translation units (not installed).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "../../include/vslam_abi.h"
+
+namespace vs {
+
+// ---- errors ------------------------------------------------------------------------------
+void set_error(const std::string& msg);
+#define VS_HIP(call)                                                                  \
+    do {                                                                              \
+        hipError_t e_ = (call);                                                       \
+        if (e_ != hipSuccess) {                                                       \
+            ::vs::set_error(std::string(#call) + ": " + hipGetErrorString(e_));       \
+            return VS_ERR_HIP;                                                        \
+        }                                                                             \
+    } while (0)
+#define VS_CHECK(rc)                   \
+    do {                                \
+        int rc_ = (rc);                 \
+        if (rc_ != VS_OK) return rc_;   \
+    } while (0)
+#define VS_ARG(cond, msg)                         \
+    do {                                          \
+        if (!(cond)) {                            \
+            ::vs::set_error(msg);                 \
+            return VS_ERR_ARG;                    \
+        }                                         \
+    } while (0)
+
+// ---- SuperPoint network description ----------------------------------------------------
+// Canonical order (== the weight blob): conv1a conv1b conv2a conv2b conv3a conv3b conv4a conv4b
+// convPa convPb convDa convDb.
+struct LayerDef {
+    const char* name;
+    int cin, cout, k;
+};
+extern const LayerDef kLayers[12];
+constexpr int kDescDim = 256;
+constexpr int kSemiCh = 65;
+
+// Device copy of one layer's parameters in the layout the conv kernels read:
+// weight [k*k][cin][cout_pad] (cout fastest), bias [cout_pad]; padding columns are zero.
+struct DevLayer {
+    int cin, cout, cout_pad, k;
+    float* w = nullptr;
+    float* b = nullptr;
+};
+
+// ---- growable device scratch -------------------------------------------------------------
+struct DevBuf {
+    void* p = nullptr;
+    size_t bytes = 0;
+    int ensure(size_t n);  // grows (never shrinks); contents are not preserved
+    void release();
+    template <class T> T* as() const { return static_cast<T*>(p); }
+};
+
+// ---- profiling ------------------------------------------------------------------------------
+struct ProfStage {
+    const char* name;
+    double ms = 0;
+    int launches = 0;
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> pending;
+};
+
+}  // namespace vs
+
+struct vs_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    std::vector<float> h_weights;  // canonical blob
+    vs::DevLayer layers[12];
+    // convPa|convDa fused into one 128->512 conv (they share conv4b's output).
+    vs::DevLayer head_a;
+
+    // network activations (NHWC fp32) and post-processing scratch, sized per batch
+    vs::DevBuf gray, act0, act1, semi, dgrid, heat, state, flags, keys, keycnt;
+    // host-API staging
+    vs::DevBuf h_img, h_kps, h_desc, h_n, h_aux0, h_aux1, h_aux2, h_aux3, h_aux4, h_aux5;
+    vs::DevBuf norms;
+
+    bool prof_on = false;
+    std::vector<vs::ProfStage> prof;
+    std::vector<hipEvent_t> event_pool;
+};
+
+namespace vs {
+
+// profiling helpers (no-ops unless ctx->prof_on)
+struct ProfScope {
+    vs_ctx* ctx;
+    int stage;
+    hipStream_t s;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    ProfScope(vs_ctx* c, const char* name, hipStream_t st);
+    ~ProfScope();
+};
+
+// ---- stage launchers (return VS_OK or an error code; enqueue on `s` only) ------------------
+// Network: d_bgr is B x h x w x 3 u8 (or gray u8 when channels == 1, or nullptr when d_gray01
+// already holds B x h x w fp32 in [0,1]).  Produces ctx->semi [B][hc][wc][65] and ctx->dgrid
+// [B][hc][wc][256] (L2-normalised over channels).
+int sp_forward(vs_ctx* ctx, int B, const uint8_t* d_img, int channels, int h, int w,
+               hipStream_t s);
+// Post-processing: ctx->semi / ctx->dgrid -> keypoints, descriptors, counts.
+int sp_postprocess(vs_ctx* ctx, int B, int hc, int wc, int h, int w, vs_keypoint* d_kps,
+                   float* d_desc, int* d_n, int cap, hipStream_t s);
+// Matching
+int match_pairs(vs_ctx* ctx, int P, const int* d_pairs, int F, const float* d_desc,
+                const int* d_n, int cap, float ratio, vs_match* d_raw, int* d_nraw,
+                vs_match* d_good, int* d_ngood, hipStream_t s);
+// 3D-3D RANSAC
+int ransac3d_pairs(vs_ctx* ctx, int P, const int* d_pairs, const vs_keypoint* d_kps, int cap,
+                   const vs_match* d_good, const int* d_ngood, const float* d_depth, int h, int w,
+                   const double K[4], const uint32_t* d_seeds, int iters, double thr,
+                   double* d_R, double* d_t, int* d_ok, int* d_diag, hipStream_t s);
+
+}  // namespace vs

@@ -1,0 +1,175 @@
+"""Seeded synthetic TUM-like RGB-D sequence (SURVEY.md 8(d) "Synthetic inputs").
+
+A 6 x 5 x 3 m room whose walls, floor and ceiling carry band-limited value-noise texture plus
+random rectangles, seen by a pinhole camera K = (525, 525, 319.5, 239.5) (Config.h:14-17) moving
+along a Pioneer-like planar path (0.4 m above the floor, ~0.3 m/s, yaw rate <= 0.5 rad/s).
+Frames are BGR u8 640x480; depth is the TUM encoding (uint16 = round(z * 5000), 0 beyond 10 m,
+3 % random dropouts) converted to fp32 metres exactly as Frame::load_depth_image does
+(Frame.cpp:47-54: raw * (float)(1/5000), 0 where raw == 0).
+
+There is no network access and no TUM data in this image; the generator is the stand-in for
+rgbd_dataset_freiburg2_pioneer_slam3 (the reference's README sequence).  Camera convention is
+OpenCV's (x right, y down, z forward); world y points down as well, floor at y = +0.4.
+"""
+import numpy as np
+
+SEED = 20261015
+K_TUM = (525.0, 525.0, 319.5, 239.5)
+W, H = 640, 480
+
+# room: x in [-3, 3], z in [-2.5, 2.5], floor y = 0.4, ceiling y = -2.6
+_ROOM = dict(xmin=-3.0, xmax=3.0, zmin=-2.5, zmax=2.5, ymin=-2.6, ymax=0.4)
+
+
+def _hash2(ix, iy, seed):
+    h = (ix.astype(np.int64) * 374761393 + iy.astype(np.int64) * 668265263 + seed * 2246822519) & 0xFFFFFFFF
+    h = ((h ^ (h >> 13)) * 1274126177) & 0xFFFFFFFF
+    h = h ^ (h >> 16)
+    return (h & 0xFFFFFF).astype(np.float32) / np.float32(0xFFFFFF)
+
+
+def _value_noise(u, v, seed):
+    iu = np.floor(u)
+    iv = np.floor(v)
+    fu = (u - iu).astype(np.float32)
+    fv = (v - iv).astype(np.float32)
+    fu = fu * fu * (3 - 2 * fu)
+    fv = fv * fv * (3 - 2 * fv)
+    iu = iu.astype(np.int64)
+    iv = iv.astype(np.int64)
+    a = _hash2(iu, iv, seed)
+    b = _hash2(iu + 1, iv, seed)
+    c = _hash2(iu, iv + 1, seed)
+    d = _hash2(iu + 1, iv + 1, seed)
+    return (a * (1 - fu) + b * fu) * (1 - fv) + (c * (1 - fu) + d * fu) * fv
+
+
+class Scene:
+    """Six textured planes with per-plane rectangles and tints."""
+
+    def __init__(self, seed=SEED):
+        rng = np.random.default_rng(seed)
+        self.seed = seed
+        self.rects = []
+        self.tints = rng.uniform(0.55, 1.0, size=(6, 3)).astype(np.float32)
+        for _ in range(6):
+            n = 40
+            c = rng.uniform(-3.0, 3.0, size=(n, 2))
+            s = rng.uniform(0.08, 0.6, size=(n, 2))
+            val = rng.uniform(0.0, 1.0, size=n)
+            self.rects.append((c.astype(np.float32), s.astype(np.float32), val.astype(np.float32)))
+
+    def texture(self, plane, u, v):
+        t = np.zeros(u.shape, np.float32)
+        amp, freq, tot = 1.0, 2.0, 0.0
+        for o in range(6):
+            t += amp * _value_noise(u * freq, v * freq, self.seed + 101 * plane + o)
+            tot += amp
+            amp *= 0.5
+            freq *= 2.0
+        t = t / tot
+        c, s, val = self.rects[plane]
+        for k in range(len(val)):
+            m = (np.abs(u - c[k, 0]) < s[k, 0]) & (np.abs(v - c[k, 1]) < s[k, 1])
+            t = np.where(m, 0.35 * t + 0.65 * val[k], t)
+        return t
+
+    def render(self, R_wc, t_wc, K=K_TUM, w=W, h=H):
+        """R_wc, t_wc: camera->world pose.  Returns (bgr u8 HxWx3, z float64 HxW)."""
+        fx, fy, cx, cy = K
+        us, vs = np.meshgrid(np.arange(w, dtype=np.float64), np.arange(h, dtype=np.float64))
+        d_cam = np.stack([(us - cx) / fx, (vs - cy) / fy, np.ones_like(us)], axis=-1)  # z_cam = 1
+        d_w = d_cam @ np.asarray(R_wc).T
+        o = np.asarray(t_wc, np.float64).reshape(3)
+        best_t = np.full((h, w), np.inf)
+        best_p = np.full((h, w), -1, np.int32)
+        r = _ROOM
+        planes = [(0, r["xmin"]), (0, r["xmax"]), (1, r["ymin"]), (1, r["ymax"]), (2, r["zmin"]), (2, r["zmax"])]
+        for pi, (ax, val) in enumerate(planes):
+            with np.errstate(divide="ignore", invalid="ignore"):
+                tt = (val - o[ax]) / d_w[..., ax]
+            ok = (tt > 1e-6) & (tt < best_t)
+            best_t = np.where(ok, tt, best_t)
+            best_p = np.where(ok, pi, best_p)
+        P = o + d_w * best_t[..., None]
+        img = np.zeros((h, w, 3), np.float32)
+        for pi, (ax, _) in enumerate(planes):
+            m = best_p == pi
+            if not m.any():
+                continue
+            a1, a2 = [a for a in range(3) if a != ax]
+            tex = self.texture(pi, P[m][:, a1].astype(np.float32), P[m][:, a2].astype(np.float32))
+            img[m] = tex[:, None] * self.tints[pi][None, :]
+        bgr = np.clip(img * 255.0 + 0.5, 0, 255).astype(np.uint8)
+        return bgr, best_t  # with d_cam z = 1, the ray parameter is the camera depth
+
+
+def yaw_rotation(yaw):
+    c, s = np.cos(yaw), np.sin(yaw)
+    # rotation about the (downward) y axis; camera looks along +z at yaw 0
+    return np.array([[c, 0.0, s], [0.0, 1.0, 0.0], [-s, 0.0, c]])
+
+
+def trajectory(n, dt=1.0 / 10.0, speed=0.3, seed=SEED):
+    """n camera->world poses at spacing dt (default: every 3rd frame of a 30 Hz stream)."""
+    rng = np.random.default_rng(seed + 7)
+    poses = []
+    pos = np.array([0.0, 0.0, -1.0])
+    yaw = 0.0
+    omega = 0.0
+    for i in range(n):
+        poses.append((yaw_rotation(yaw), pos.copy()))
+        omega = np.clip(0.9 * omega + rng.normal(0, 0.08), -0.5, 0.5)
+        # steer back toward the room centre
+        to_c = -pos[[0, 2]]
+        heading = np.array([np.sin(yaw), np.cos(yaw)])
+        cross = heading[0] * to_c[1] - heading[1] * to_c[0]
+        if np.linalg.norm(to_c) > 1.2:
+            omega = np.clip(omega - 0.3 * np.sign(cross), -0.5, 0.5)
+        yaw += omega * dt
+        pos[0] += speed * dt * np.sin(yaw)
+        pos[2] += speed * dt * np.cos(yaw)
+    return poses
+
+
+def depth_tum(z, rng):
+    """TUM 16-bit depth of z metres, dropouts, then Frame::load_depth_image's fp32 conversion."""
+    raw = np.round(z * 5000.0)
+    raw = np.where((z > 10.0) | ~np.isfinite(z), 0, raw)
+    raw = np.clip(raw, 0, 65535).astype(np.uint16)
+    drop = rng.random(z.shape) < 0.03
+    raw[drop] = 0
+    depth = raw.astype(np.float32) * np.float32(1.0 / 5000.0)
+    depth[raw == 0] = 0.0
+    return depth
+
+
+def sequence(n, seed=SEED, dt=1.0 / 10.0):
+    """n frames: list of dicts {bgr, depth, R_wc, t_wc, timestamp}."""
+    scene = Scene(seed)
+    rng = np.random.default_rng(seed + 13)
+    out = []
+    for i, (R, t) in enumerate(trajectory(n, dt=dt, seed=seed)):
+        bgr, z = scene.render(R, t)
+        out.append(dict(bgr=bgr, depth=depth_tum(z, rng), R_wc=R, t_wc=t, timestamp=1311868164.0 + i * dt))
+    return out
+
+
+def random_descriptors(n, seed):
+    rng = np.random.default_rng(seed)
+    d = rng.standard_normal((n, 256)).astype(np.float32)
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    return d
+
+
+def frames(indices, n_total, seed=SEED, dt=1.0 / 10.0):
+    """Render only the given frame indices of an n_total-frame sequence (same poses/noise per index)."""
+    scene = Scene(seed)
+    poses = trajectory(n_total, dt=dt, seed=seed)
+    out = {}
+    for i in indices:
+        R, t = poses[i]
+        bgr, z = scene.render(R, t)
+        rng = np.random.default_rng((seed + 13) * 1000003 + i)
+        out[i] = dict(bgr=bgr, depth=depth_tum(z, rng), R_wc=R, t_wc=t, timestamp=1311868164.0 + i * dt)
+    return out

@@ -1,0 +1,245 @@
+"""ctypes binding of libvslam_hip.so (include/vslam_abi.h) for tests and bench.py.
+
+This is plumbing, not the product: every compute call goes through the C ABI into the HIP
+kernels.  Loading fails loudly when the shared library has not been built; there is no CPU
+fallback anywhere on this path.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+PKG_DIR = os.path.dirname(_HERE)
+LIB_PATH = os.path.join(PKG_DIR, "libvslam_hip.so")
+
+KEYPOINT_DTYPE = np.dtype([("x", "<f4"), ("y", "<f4"), ("size", "<f4"), ("angle", "<f4"),
+                           ("response", "<f4"), ("octave", "<i4"), ("class_id", "<i4")])
+MATCH_DTYPE = np.dtype([("query_idx", "<i4"), ("train_idx", "<i4"), ("img_idx", "<i4"),
+                        ("distance", "<f4")])
+assert KEYPOINT_DTYPE.itemsize == 28 and MATCH_DTYPE.itemsize == 16
+
+VS_OK = 0
+ERRORS = {-1: "VS_ERR_ARG", -2: "VS_ERR_HIP", -3: "VS_ERR_NOMEM", -4: "VS_ERR_IO",
+          -5: "VS_ERR_CAPACITY", -6: "VS_ERR_NOTCONV"}
+SP_MAX_KEYPOINTS = 400
+K_TUM = (525.0, 525.0, 319.5, 239.5)  # Config.h:14-17
+
+_P = ctypes.c_void_p
+_I = ctypes.c_int
+_SIG = {
+    "vs_abi_version": (_I, []),
+    "vs_last_error": (ctypes.c_char_p, []),
+    "vs_create": (_I, [_I, ctypes.c_char_p, ctypes.POINTER(_P)]),
+    "vs_destroy": (None, [_P]),
+    "vs_stream": (_P, [_P]),
+    "vs_superpoint_num_params": (ctypes.c_size_t, []),
+    "vs_superpoint_get_weights": (_I, [_P, _P, ctypes.c_size_t]),
+    "vs_superpoint_save_weights": (_I, [_P, ctypes.c_char_p]),
+    "vs_extract": (_I, [_P, _P, _I, _I, _I, ctypes.c_size_t, _P, _P, _I, _P]),
+    "vs_extract_batch": (_I, [_P, _I, _P, _I, _I, _I, ctypes.c_size_t, _P, _P, _I, _P]),
+    "vs_extract_batch_dev": (_I, [_P, _I, _P, _I, _I, _P, _P, _P, _I, _P]),
+    "vs_superpoint_forward": (_I, [_P, _P, _I, _I, _P, _P]),
+    "vs_postprocess": (_I, [_P, _P, _P, _I, _I, _I, _I, _P, _P, _I, _P]),
+    "vs_match_ratio": (_I, [_P, _P, _I, _P, _I, ctypes.c_float, _P, _P, _P, _P]),
+    "vs_match_pairs_dev": (_I, [_P, _I, _P, _I, _P, _P, _I, ctypes.c_float, _P, _P, _P, _P, _P]),
+    "vs_ransac_3d3d": (_I, [_P, _P, _P, _I, _P, _P, _I, _I, _P, ctypes.c_uint32, _I, ctypes.c_double,
+                            _P, _P, _P, _P]),
+    "vs_ransac_3d3d_pairs_dev": (_I, [_P, _I, _P, _P, _I, _P, _P, _P, _I, _I, _P, _P, _I,
+                                      ctypes.c_double, _P, _P, _P, _P, _P]),
+    "vs_profile_enable": (_I, [_P, _I]),
+    "vs_profile_reset": (_I, [_P]),
+    "vs_profile_read": (_I, [_P, _I, _P, _P, _P, _P]),
+}
+
+_lib = None
+
+
+def load_library(path=LIB_PATH):
+    """Load libvslam_hip.so; raise if it is missing (never fall back to a CPU path)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise RuntimeError(f"libvslam_hip.so not built at {path}: run __graft_entry__.build()")
+    lib = ctypes.CDLL(path)
+    for name, (res, args) in _SIG.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+class VSError(RuntimeError):
+    pass
+
+
+def _check(rc):
+    if rc != VS_OK:
+        msg = _lib.vs_last_error().decode(errors="replace")
+        raise VSError(f"{ERRORS.get(rc, rc)}: {msg}")
+
+
+def _ptr(a):
+    return a.ctypes.data_as(ctypes.c_void_p) if a is not None else None
+
+
+def _k_array(K):
+    return np.ascontiguousarray(np.asarray(K, dtype=np.float64).reshape(4))
+
+
+class Context:
+    """One vs_ctx: device scratch, SuperPoint weights and a HIP stream on one GPU."""
+
+    def __init__(self, device=0, weights_path=None):
+        self.lib = load_library()
+        h = ctypes.c_void_p()
+        wp = weights_path.encode() if weights_path else None
+        _check(self.lib.vs_create(device, wp, ctypes.byref(h)))
+        self.h = h
+
+    def close(self):
+        if self.h:
+            self.lib.vs_destroy(self.h)
+            self.h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def stream(self):
+        return self.lib.vs_stream(self.h)
+
+    # ---- weights ----
+    def weights(self):
+        n = self.lib.vs_superpoint_num_params()
+        out = np.empty(n, np.float32)
+        _check(self.lib.vs_superpoint_get_weights(self.h, _ptr(out), n))
+        return out
+
+    def save_weights(self, path):
+        _check(self.lib.vs_superpoint_save_weights(self.h, path.encode()))
+
+    # ---- FeatureExtractor::extract ----
+    def extract(self, img, cap=SP_MAX_KEYPOINTS):
+        img = np.ascontiguousarray(img, dtype=np.uint8)
+        h, w = img.shape[:2]
+        ch = 1 if img.ndim == 2 else img.shape[2]
+        kps = np.zeros(cap, KEYPOINT_DTYPE)
+        desc = np.zeros((cap, 256), np.float32)
+        n = ctypes.c_int(0)
+        _check(self.lib.vs_extract(self.h, _ptr(img), h, w, ch, img.strides[0], _ptr(kps), _ptr(desc), cap,
+                                   ctypes.byref(n)))
+        return kps[:n.value].copy(), desc[:n.value].copy()
+
+    def extract_batch(self, imgs, cap=SP_MAX_KEYPOINTS):
+        imgs = [np.ascontiguousarray(i, dtype=np.uint8) for i in imgs]
+        B = len(imgs)
+        h, w = imgs[0].shape[:2]
+        ch = 1 if imgs[0].ndim == 2 else imgs[0].shape[2]
+        ptrs = (ctypes.c_void_p * B)(*[i.ctypes.data for i in imgs])
+        kps = np.zeros((B, cap), KEYPOINT_DTYPE)
+        desc = np.zeros((B, cap, 256), np.float32)
+        n = np.zeros(B, np.int32)
+        _check(self.lib.vs_extract_batch(self.h, B, ctypes.cast(ptrs, ctypes.c_void_p), h, w, ch, imgs[0].strides[0],
+                                         _ptr(kps), _ptr(desc), cap, _ptr(n)))
+        return [(kps[b, :n[b]].copy(), desc[b, :n[b]].copy()) for b in range(B)]
+
+    def superpoint_forward(self, gray01):
+        g = np.ascontiguousarray(gray01, dtype=np.float32)
+        h, w = g.shape
+        semi = np.zeros((65, h // 8, w // 8), np.float32)
+        desc = np.zeros((256, h // 8, w // 8), np.float32)
+        _check(self.lib.vs_superpoint_forward(self.h, _ptr(g), h, w, _ptr(semi), _ptr(desc)))
+        return semi, desc
+
+    def postprocess(self, semi, desc_grid, h=None, w=None, cap=SP_MAX_KEYPOINTS):
+        semi = np.ascontiguousarray(semi, dtype=np.float32)
+        desc_grid = np.ascontiguousarray(desc_grid, dtype=np.float32)
+        hc, wc = semi.shape[1:]
+        h = hc * 8 if h is None else h
+        w = wc * 8 if w is None else w
+        kps = np.zeros(cap, KEYPOINT_DTYPE)
+        desc = np.zeros((cap, 256), np.float32)
+        n = ctypes.c_int(0)
+        _check(self.lib.vs_postprocess(self.h, _ptr(semi), _ptr(desc_grid), hc, wc, h, w, _ptr(kps), _ptr(desc), cap,
+                                       ctypes.byref(n)))
+        return kps[:n.value].copy(), desc[:n.value].copy()
+
+    # ---- Slam::match_features ----
+    def match_ratio(self, desc1, desc2, ratio=0.75):
+        d1 = np.ascontiguousarray(desc1, dtype=np.float32).reshape(-1, 256)
+        d2 = np.ascontiguousarray(desc2, dtype=np.float32).reshape(-1, 256)
+        n1, n2 = d1.shape[0], d2.shape[0]
+        raw = np.zeros(max(n1, 1), MATCH_DTYPE)
+        good = np.zeros(max(n1, 1), MATCH_DTYPE)
+        nr, ng = ctypes.c_int(0), ctypes.c_int(0)
+        _check(self.lib.vs_match_ratio(self.h, _ptr(d1), n1, _ptr(d2), n2, ratio, _ptr(raw), ctypes.byref(nr),
+                                       _ptr(good), ctypes.byref(ng)))
+        return raw[:nr.value].copy(), good[:ng.value].copy()
+
+    # ---- Slam::estimate_motion_3d3d ----
+    def ransac_3d3d(self, pts1, pts2, depth1, depth2, K=K_TUM, seed=42, iters=200, thr=0.05):
+        p1 = np.ascontiguousarray(pts1, dtype=np.float32).reshape(-1, 2)
+        p2 = np.ascontiguousarray(pts2, dtype=np.float32).reshape(-1, 2)
+        d1 = np.ascontiguousarray(depth1, dtype=np.float32)
+        d2 = np.ascontiguousarray(depth2, dtype=np.float32)
+        h, w = d1.shape
+        R = np.zeros(9, np.float64)
+        t = np.zeros(3, np.float64)
+        ok = ctypes.c_int(0)
+        diag = np.zeros(4, np.int32)
+        Ka = _k_array(K)
+        _check(self.lib.vs_ransac_3d3d(self.h, _ptr(p1), _ptr(p2), p1.shape[0], _ptr(d1), _ptr(d2), h, w, _ptr(Ka),
+                                       seed, iters, thr, _ptr(R), _ptr(t), ctypes.byref(ok), _ptr(diag)))
+        return bool(ok.value), R.reshape(3, 3), t, diag
+
+    # ---- device-batched entry points (pointers are ints, e.g. torch tensor.data_ptr()) ----
+    def extract_batch_dev(self, B, d_imgs, h, w, d_kps, d_desc, d_n, cap, stream=None):
+        _check(self.lib.vs_extract_batch_dev(self.h, B, d_imgs, h, w, d_kps, d_desc, d_n, cap, stream))
+
+    def match_pairs_dev(self, P, d_pairs, F, d_desc, d_n, cap, ratio, d_raw, d_nraw, d_good, d_ngood, stream=None):
+        _check(self.lib.vs_match_pairs_dev(self.h, P, d_pairs, F, d_desc, d_n, cap, ratio, d_raw, d_nraw, d_good,
+                                           d_ngood, stream))
+
+    def ransac_3d3d_pairs_dev(self, P, d_pairs, d_kps, cap, d_good, d_ngood, d_depth, h, w, K, d_seeds, iters, thr,
+                              d_R, d_t, d_ok, d_diag, stream=None):
+        Ka = _k_array(K)
+        _check(self.lib.vs_ransac_3d3d_pairs_dev(self.h, P, d_pairs, d_kps, cap, d_good, d_ngood, d_depth, h, w,
+                                                 _ptr(Ka), d_seeds, iters, thr, d_R, d_t, d_ok, d_diag, stream))
+
+    # ---- profiling ----
+    def profile(self, on=True):
+        _check(self.lib.vs_profile_enable(self.h, 1 if on else 0))
+
+    def profile_reset(self):
+        _check(self.lib.vs_profile_reset(self.h))
+
+    def profile_read(self):
+        n = ctypes.c_int(0)
+        _check(self.lib.vs_profile_read(self.h, 0, None, None, None, ctypes.byref(n)))
+        m = n.value
+        names = (ctypes.c_char_p * max(m, 1))()
+        ms = np.zeros(max(m, 1), np.float64)
+        launches = np.zeros(max(m, 1), np.int32)
+        _check(self.lib.vs_profile_read(self.h, m, ctypes.cast(names, ctypes.c_void_p), _ptr(ms), _ptr(launches),
+                                        ctypes.byref(n)))
+        return {names[i].decode(): (float(ms[i]), int(launches[i])) for i in range(m)}
+
+
+def exported_symbols_from_header(header_path):
+    """Function names declared in include/vslam_abi.h (for the export test)."""
+    import re
+    text = open(header_path).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(vs_[a-z0-9_]+)\s*\(", text)))

@@ -1,0 +1,126 @@
+"""Offline batched hot path on one GPU (and its multi-GPU frame-sharded form).
+
+Per step each rank takes B consecutive processed frames of a 640x480 RGB-D stream that already
+sit in HBM and runs, entirely through libvslam_hip.so:
+    FeatureExtractor::extract           (vs_extract_batch_dev: SuperPoint + decode + NMS + sample)
+    Slam::match_features(prev, cur)     (vs_match_pairs_dev: exact 2-NN + ratio 0.75)
+    Slam::estimate_motion_3d3d          (vs_ransac_3d3d_pairs_dev: 200-iteration 3D-3D RANSAC)
+for the B frame pairs (i-1, i) that end in its frames (Slam.cpp:838-955).  torch provides device
+memory, the stream and torch.distributed; it computes nothing.
+
+Multi-GPU: frames are sharded in contiguous blocks (rank r owns frames
+[r*B, (r+1)*B) of each step's N*B frames).  After extraction the per-frame feature records
+(count, 400 keypoints, 400x256 descriptors) are all-gathered over RCCL, which gives every rank the
+whole step's features (the SPCF-cache-like interchange the sequential tracker consumes) and gives
+rank r the neighbour frame r*B-1 its first pair needs.  Depth maps of a rank's block plus the one
+halo frame before it come with the input.
+"""
+import numpy as np
+import torch
+
+import vslam_abi as va
+
+KP_BYTES = va.KEYPOINT_DTYPE.itemsize
+M_BYTES = va.MATCH_DTYPE.itemsize
+
+
+class DevicePipeline:
+    def __init__(self, ctx, B, h=480, w=640, cap=va.SP_MAX_KEYPOINTS, K=va.K_TUM, iters=200, thr=0.05,
+                 ratio=0.75, rank=0, world=1, group=None):
+        self.ctx, self.B, self.h, self.w, self.cap = ctx, B, h, w, cap
+        self.K, self.iters, self.thr, self.ratio = K, iters, thr, ratio
+        self.rank, self.world, self.group = rank, world, group
+        dev = torch.device("cuda", torch.cuda.current_device())
+        F = B + 1  # slot 0 = the frame before this rank's block
+        self.kps = torch.zeros((F, cap * KP_BYTES), dtype=torch.uint8, device=dev)
+        self.desc = torch.zeros((F, cap, 256), dtype=torch.float32, device=dev)
+        self.n = torch.zeros(F, dtype=torch.int32, device=dev)
+        self.depth = torch.zeros((F, h, w), dtype=torch.float32, device=dev)
+        P = B
+        self.pairs = torch.tensor([[p, p + 1] for p in range(P)], dtype=torch.int32, device=dev)
+        self.raw = torch.zeros((P, cap * M_BYTES), dtype=torch.uint8, device=dev)
+        self.good = torch.zeros((P, cap * M_BYTES), dtype=torch.uint8, device=dev)
+        self.nraw = torch.zeros(P, dtype=torch.int32, device=dev)
+        self.ngood = torch.zeros(P, dtype=torch.int32, device=dev)
+        self.R = torch.zeros((P, 9), dtype=torch.float64, device=dev)
+        self.t = torch.zeros((P, 3), dtype=torch.float64, device=dev)
+        self.ok = torch.zeros(P, dtype=torch.int32, device=dev)
+        self.diag = torch.zeros((P, 4), dtype=torch.int32, device=dev)
+        self.seeds = torch.zeros(P, dtype=torch.int32, device=dev)
+        self._seed_base = torch.arange(P, dtype=torch.int64, device=dev)
+        if world > 1:
+            self.g_kps = torch.zeros((world * B, cap * KP_BYTES), dtype=torch.uint8, device=dev)
+            self.g_desc = torch.zeros((world * B, cap, 256), dtype=torch.float32, device=dev)
+            self.g_n = torch.zeros(world * B, dtype=torch.int32, device=dev)
+            self.carry_kps = torch.zeros(cap * KP_BYTES, dtype=torch.uint8, device=dev)
+            self.carry_desc = torch.zeros((cap, 256), dtype=torch.float32, device=dev)
+            self.carry_n = torch.zeros((), dtype=torch.int32, device=dev)
+
+    def _allgather_features(self):
+        import torch.distributed as dist
+        dist.all_gather_into_tensor(self.g_n, self.n[1:], group=self.group)
+        dist.all_gather_into_tensor(self.g_kps, self.kps[1:], group=self.group)
+        dist.all_gather_into_tensor(self.g_desc, self.desc[1:], group=self.group)
+
+    def run(self, frames, depth, frame_count0, depth_prev=None):
+        """frames: (B, h, w, 3) uint8 cuda, depth: (B, h, w) float32 cuda, frame_count0: global
+        processed-frame index of frames[0] (the RANSAC seed is 42 + frame_count, Slam.cpp:276).
+        depth_prev: depth of the frame before frames[0] (halo) when world > 1."""
+        B, h, w, cap = self.B, self.h, self.w, self.cap
+        assert frames.shape == (B, h, w, 3) and frames.dtype == torch.uint8 and frames.is_cuda
+        assert depth.shape == (B, h, w) and depth.dtype == torch.float32
+        s = torch.cuda.current_stream().cuda_stream
+        ctx = self.ctx
+        # carry the previous step's last frame into slot 0 (single GPU)
+        if self.world == 1:
+            self.kps[0].copy_(self.kps[B])
+            self.desc[0].copy_(self.desc[B])
+            self.n[0].copy_(self.n[B])
+            self.depth[0].copy_(self.depth[B])
+        elif depth_prev is not None:
+            self.depth[0].copy_(depth_prev)
+        self.depth[1:].copy_(depth)
+        ctx.extract_batch_dev(B, frames.data_ptr(), h, w, self.kps[1:].data_ptr(), self.desc[1:].data_ptr(),
+                              self.n[1:].data_ptr(), cap, s)
+        if self.world > 1:
+            self._allgather_features()
+            # neighbour frame before this block: rank-1's last frame, or (rank 0) the previous
+            # step's global last frame, which is still in slot 0's gathered copy from last step
+            if self.rank > 0:
+                j = self.rank * B - 1
+                self.kps[0].copy_(self.g_kps[j])
+                self.desc[0].copy_(self.g_desc[j])
+                self.n[0].copy_(self.g_n[j])
+            else:
+                # slot 0 of rank 0 still holds the previous step's global last frame (or n = 0)
+                self.kps[0].copy_(self.carry_kps)
+                self.desc[0].copy_(self.carry_desc)
+                self.n[0].copy_(self.carry_n)
+            self.carry_kps.copy_(self.g_kps[-1])
+            self.carry_desc.copy_(self.g_desc[-1])
+            self.carry_n.copy_(self.g_n[-1])
+        self.seeds.copy_((self._seed_base + (42 + frame_count0)).to(torch.int32))
+        ctx.match_pairs_dev(B, self.pairs.data_ptr(), B + 1, self.desc.data_ptr(), self.n.data_ptr(), cap,
+                            self.ratio, self.raw.data_ptr(), self.nraw.data_ptr(), self.good.data_ptr(),
+                            self.ngood.data_ptr(), s)
+        ctx.ransac_3d3d_pairs_dev(B, self.pairs.data_ptr(), self.kps.data_ptr(), cap, self.good.data_ptr(),
+                                  self.ngood.data_ptr(), self.depth.data_ptr(), h, w, self.K, self.seeds.data_ptr(),
+                                  self.iters, self.thr, self.R.data_ptr(), self.t.data_ptr(), self.ok.data_ptr(),
+                                  self.diag.data_ptr(), s)
+        return dict(kps=self.kps[1:], desc=self.desc[1:], n=self.n[1:], good=self.good, ngood=self.ngood,
+                    R=self.R, t=self.t, ok=self.ok, diag=self.diag)
+
+
+def compose_poses(R_rel, t_rel, ok, R0=None, t0=None):
+    """Host pose chain (Slam.cpp:963-964): R_new = R_ref R^T, t_new = t_ref - R_new t; a failed pair
+    keeps the previous pose (the reference then falls back to E-matrix motion, not modelled here)."""
+    R = np.eye(3) if R0 is None else R0.copy()
+    t = np.zeros(3) if t0 is None else t0.copy()
+    out = []
+    for Rr, tr, k in zip(R_rel, t_rel, ok):
+        if k:
+            Rn = R @ Rr.reshape(3, 3).T
+            t = t - Rn @ tr
+            R = Rn
+        out.append((R.copy(), t.copy()))
+    return out
