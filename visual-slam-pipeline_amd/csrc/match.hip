@@ -133,7 +133,7 @@ __global__ __launch_bounds__(256) void k_match(const int* __restrict__ pairs, co
     best.push(other.d0, other.j0);
     best.push(other.d1, other.j1);
     if (lh == 0 && qvalid) {
-        const float dist0 = __fsqrt_rn(best.d0), dist1 = __fsqrt_rn(best.d1);
+        const float dist0 = sqrt_rn(best.d0), dist1 = sqrt_rn(best.d1);
         vs_match m;
         m.query_idx = qj;
         m.train_idx = best.j0;

@@ -61,7 +61,7 @@ __global__ __launch_bounds__(256) void k_decode(const float* __restrict__ semi, 
     uint8_t* sb = state + (size_t)b * ncell * 64;
 #pragma unroll
     for (int c = 0; c < 64; c++) {
-        float v = __fdiv_rn(cell[c], sum);
+        float v = div_rn(cell[c], sum);
         size_t o = (size_t)(cy * 8 + c / 8) * Wp + cx * 8 + (c % 8);
         hb[o] = v;
         sb[o] = (v > kConfThresh) ? ST_UNDECIDED : ST_OUT;
@@ -313,14 +313,14 @@ __global__ __launch_bounds__(256) void k_sample(const float* __restrict__ dgrid,
             float v = s_v[wv][c];
             nrm += v * v;
         }
-        s_norm[wv] = __fsqrt_rn(nrm);
+        s_norm[wv] = sqrt_rn(nrm);
     }
     __syncthreads();
     if (active) {
         const float nrm = s_norm[wv];
         if (nrm > 1e-8f) {
 #pragma unroll
-            for (int e = 0; e < 4; e++) val[e] = __fdiv_rn(val[e], nrm);
+            for (int e = 0; e < 4; e++) val[e] = div_rn(val[e], nrm);
         }
         float4 o = {val[0], val[1], val[2], val[3]};
         reinterpret_cast<float4*>(desc + ((size_t)b * cap + i) * 256)[lane] = o;

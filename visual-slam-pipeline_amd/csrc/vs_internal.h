@@ -11,6 +11,14 @@
 
 namespace vs {
 
+// ---- IEEE-exact device math ---------------------------------------------------------------
+// gfx950's v_sqrt_f32 is not correctly rounded and __fsqrt_rn lowers to it; the f64 sqrt is
+// lowered with an fma refinement to the correctly rounded result, and rounding that to float is
+// exact for sqrt (53 >= 2*24 + 2), so this equals the host's sqrtf bit for bit.
+__device__ __forceinline__ float sqrt_rn(float x) { return (float)sqrt((double)x); }
+// __fdiv_rn lowers to the v_div_scale / v_div_fmas / v_div_fixup correctly rounded sequence.
+__device__ __forceinline__ float div_rn(float a, float b) { return __fdiv_rn(a, b); }
+
 // ---- errors ------------------------------------------------------------------------------
 void set_error(const std::string& msg);
 #define VS_HIP(call)                                                                  \

@@ -62,6 +62,13 @@ def load_library(path=LIB_PATH):
         return _lib
     if not os.path.exists(path):
         raise RuntimeError(f"libvslam_hip.so not built at {path}: run __graft_entry__.build()")
+    # torch bundles its own libamdhip64.so.7 (same SONAME as /opt/rocm's).  Whichever loads first
+    # serves the whole process; load torch's first so torch tensors and our kernels share one HIP
+    # runtime (when our library initialised /opt/rocm's copy first, torch found no GPU).
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     lib = ctypes.CDLL(path)
     for name, (res, args) in _SIG.items():
         fn = getattr(lib, name)
