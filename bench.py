@@ -44,6 +44,34 @@ LAYER_FLOPS = {
 }
 
 
+# profiling stage -> kernel symbol (as rocprofv3 reports it) of that stage's dominant launch
+STAGE_KERNEL = {
+    "conv1a": "vs::k_conv1a",
+    "conv1b_pool": "vs::k_conv_mfma<3, true, 1>",
+    "conv2a": "vs::k_conv_mfma<3, false, 2>",
+    "conv2b_pool": "vs::k_conv_mfma<3, true, 3>",
+    "conv3a": "vs::k_conv_mfma<3, false, 4>",
+    "conv3b_pool": "vs::k_conv_mfma<3, true, 5>",
+    "conv4a": "vs::k_conv_mfma<3, false, 6>",
+    "conv4b": "vs::k_conv_mfma<3, false, 7>",
+    "head_a": "vs::k_conv_mfma<3, false, 8>",
+}
+
+
+def pmc_traffic(kernel, batch):
+    """HBM bytes per launch of `kernel` from the committed PMC passes (profiles/pmc_traffic.json,
+    written by tools/summarize_profiles.py from rocprofv3 FETCH_SIZE / WRITE_SIZE runs of this same
+    bench at the same batch), or None when no matching measurement exists."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        doc = json.load(open(path))
+    except (OSError, ValueError):
+        return None, None
+    if doc.get("batch_frames") != batch or kernel not in doc.get("kernels", {}):
+        return None, None
+    return doc["kernels"][kernel]["hbm_bytes_per_launch"], doc.get("tag")
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -163,6 +191,7 @@ def main():
     net_ms = sum(v[0] for k, v in prof.items() if k in LAYER_FLOPS) / args.steps
     net_flops = sum(LAYER_FLOPS.values()) * B
     stage_ms = {k: round(v[0] / args.steps, 4) for k, v in sorted(prof.items(), key=lambda kv: -kv[1][0])}
+    traffic, traffic_tag = pmc_traffic(STAGE_KERNEL.get(dom, ""), B)
 
     result = None
     if rank == 0:
@@ -192,13 +221,15 @@ def main():
                 "parallelism": f"frame-sharded x{world}" + (" + RCCL all-gather of features" if world > 1 else ""),
             },
             "roofline": {
-                "kernel": f"k_conv_mfma ({dom})",
+                "kernel": f"{STAGE_KERNEL.get(dom, dom)} ({dom})",
                 "bound": "mfma",
                 "achieved": round(achieved, 3),
                 "peak": FP32_MFMA_PEAK_TFLOPS,
                 "unit": "TFLOP/s",
                 "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4),
-                "traffic": None,
+                "traffic": traffic,
+                "traffic_unit": "HBM bytes per launch (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE)",
+                "traffic_source": f"profiles/{traffic_tag}_pmc_traffic.json" if traffic_tag else None,
                 "avg_launch_ms": round(avg_s * 1e3, 4),
                 "flops_per_launch": flops_per_launch,
             },

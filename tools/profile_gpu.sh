@@ -1,0 +1,16 @@
+#!/bin/bash
+# rocprofv3 passes over bench.py (run on the GPU box from the repo root):
+#   1. kernel trace + stats (per-kernel durations; the summary committed under profiles/)
+#   2. FETCH_SIZE and 3. WRITE_SIZE in separate PMC passes (TCC slots; MI355X_MICROARCH.md)
+# Each pass has its own time limit and the chain stops at the first failure.
+export TMPDIR=/tmp
+R=$(pwd)
+OUT=$R/gpurun_out
+ARGS=${BENCH_ARGS:---steps 5 --warmup 1 --no-cpu-baseline}
+mkdir -p $OUT
+timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $OUT/prof_trace -o trace --output-format csv -- \
+    python3 $R/bench.py $ARGS > $OUT/prof_trace.log 2>&1 && echo "trace ok" &&
+timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d $OUT/prof_fetch -o fetch --output-format csv -- \
+    python3 $R/bench.py --steps 2 --warmup 1 --no-cpu-baseline > $OUT/prof_fetch.log 2>&1 && echo "fetch ok" &&
+timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d $OUT/prof_write -o write --output-format csv -- \
+    python3 $R/bench.py --steps 2 --warmup 1 --no-cpu-baseline > $OUT/prof_write.log 2>&1 && echo "write ok"

@@ -1,0 +1,67 @@
+"""Turn a tools/profile_gpu.sh run (gpurun_out/prof_*) into committed profile artefacts:
+
+  profiles/<tag>_kernel_stats.csv   rocprofv3 --kernel-trace --stats summary (verbatim)
+  profiles/<tag>_pmc_traffic.json   per-kernel HBM bytes per launch from the FETCH_SIZE / WRITE_SIZE
+                                    passes, with the gfx950 correction of MI355X_MICROARCH.md
+                                    "HBM": FETCH_SIZE counts half the bytes of a 16-B/lane streaming
+                                    read (x2); WRITE_SIZE is exact for 16-B/lane stores.
+  profiles/pmc_traffic.json         copy of the latest traffic file (read by bench.py)
+
+usage: python tools/summarize_profiles.py r01 [batch]
+"""
+import collections
+import csv
+import json
+import os
+import re
+import shutil
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+OUT = os.path.join(ROOT, "gpurun_out")
+PROF = os.path.join(ROOT, "profiles")
+
+
+def short(name):
+    m = re.match(r"(?:void )?([\w:]+(?:<[^>]*>)?)", name)
+    return m.group(1) if m else name[:80]
+
+
+def per_kernel(path, counter):
+    agg = collections.defaultdict(list)
+    for r in csv.DictReader(open(path)):
+        if r["Counter_Name"] == counter:
+            agg[short(r["Kernel_Name"])].append(float(r["Counter_Value"]) * 1024.0)
+    return {k: sum(v) / len(v) for k, v in agg.items()}
+
+
+def main():
+    tag = sys.argv[1]
+    batch = int(sys.argv[2]) if len(sys.argv) > 2 else 32
+    os.makedirs(PROF, exist_ok=True)
+    shutil.copy(os.path.join(OUT, "prof_trace", "trace_kernel_stats.csv"),
+                os.path.join(PROF, f"{tag}_kernel_stats.csv"))
+    fetch = per_kernel(os.path.join(OUT, "prof_fetch", "fetch_counter_collection.csv"), "FETCH_SIZE")
+    write = per_kernel(os.path.join(OUT, "prof_write", "write_counter_collection.csv"), "WRITE_SIZE")
+    stats = {}
+    for r in csv.DictReader(open(os.path.join(OUT, "prof_trace", "trace_kernel_stats.csv"))):
+        stats[short(r["Name"])] = float(r["AverageNs"])
+    kernels = {}
+    for k in sorted(set(fetch) | set(write)):
+        f = fetch.get(k, 0.0)
+        w = write.get(k, 0.0)
+        kernels[k] = {"fetch_bytes_raw": f, "fetch_bytes_corrected": 2.0 * f, "write_bytes": w,
+                      "hbm_bytes_per_launch": 2.0 * f + w, "avg_ns": stats.get(k)}
+    doc = {"tag": tag, "batch_frames": batch,
+           "note": "FETCH_SIZE x2 (gfx950 16-B/lane streaming-read correction), WRITE_SIZE as is; bytes per launch",
+           "kernels": kernels}
+    with open(os.path.join(PROF, f"{tag}_pmc_traffic.json"), "w") as fh:
+        json.dump(doc, fh, indent=1)
+    shutil.copy(os.path.join(PROF, f"{tag}_pmc_traffic.json"), os.path.join(PROF, "pmc_traffic.json"))
+    top = sorted(kernels.items(), key=lambda kv: -(kv[1]["avg_ns"] or 0))[:8]
+    for k, v in top:
+        print(f"{k:40s} avg {v['avg_ns'] or 0:12.0f} ns  hbm {v['hbm_bytes_per_launch'] / 1e9:8.3f} GB")
+
+
+if __name__ == "__main__":
+    main()
