@@ -31,8 +31,7 @@ HBM_PEAK_GBS = 8000.0
 
 # Algorithmic FLOPs of each SuperPoint layer per 640x480 frame (2 * MACs).
 LAYER_FLOPS = {
-    "conv1a": 2 * 480 * 640 * 64 * 1 * 9,
-    "conv1b_pool": 2 * 480 * 640 * 64 * 64 * 9,
+    "conv1_fused": 2 * 480 * 640 * 64 * 1 * 9 + 2 * 480 * 640 * 64 * 64 * 9,  # conv1a + conv1b (+pool)
     "conv2a": 2 * 240 * 320 * 64 * 64 * 9,
     "conv2b_pool": 2 * 240 * 320 * 64 * 64 * 9,
     "conv3a": 2 * 120 * 160 * 128 * 64 * 9,
@@ -46,8 +45,7 @@ LAYER_FLOPS = {
 
 # profiling stage -> kernel symbol (as rocprofv3 reports it) of that stage's dominant launch
 STAGE_KERNEL = {
-    "conv1a": "vs::k_conv1a",
-    "conv1b_pool": "vs::k_conv_mfma<3, true, 1>",
+    "conv1_fused": "vs::k_conv_mfma<3, true, 1, true>",
     "conv2a": "vs::k_conv_mfma<3, false, 2>",
     "conv2b_pool": "vs::k_conv_mfma<3, true, 3>",
     "conv3a": "vs::k_conv_mfma<3, false, 4>",

@@ -218,5 +218,5 @@ def test_profile_reports_stages(vsctx, seq4):
     vsctx.extract(seq4[0]["bgr"])
     prof = vsctx.profile_read()
     vsctx.profile(False)
-    for st in ["conv1a", "conv1b_pool", "head_a", "nms_rounds", "sample"]:
+    for st in ["conv1_fused", "conv2a", "head_a", "nms_rounds", "sample"]:
         assert st in prof and prof[st][0] > 0

@@ -41,46 +41,6 @@ __global__ void k_gray_norm(const uint8_t* __restrict__ img, int channels, int h
     out[idx] = v;
 }
 
-// conv1a: 1 -> 64 channels, 3x3, ReLU.  K = 9 is too shallow for the matrix cores: one thread per
-// pixel, weights in LDS, 16 x 16-byte stores of the pixel's 64 channels.
-__global__ __launch_bounds__(256) void k_conv1a(const float* __restrict__ gray, const float* __restrict__ wt,
-                                                const float* __restrict__ bias, float* __restrict__ out,
-                                                int Hp, int Wp, int total) {
-    __shared__ float s_w[9 * 64 + 64];
-    for (int i = threadIdx.x; i < 9 * 64; i += blockDim.x) s_w[i] = wt[i];
-    if (threadIdx.x < 64) s_w[9 * 64 + threadIdx.x] = bias[threadIdx.x];
-    __syncthreads();
-    int idx = blockIdx.x * blockDim.x + threadIdx.x;
-    if (idx >= total) return;
-    int x = idx % Wp;
-    int t = idx / Wp;
-    int y = t % Hp;
-    int b = t / Hp;
-    const float* g = gray + (size_t)b * Hp * Wp;
-    float v[9];
-#pragma unroll
-    for (int ky = 0; ky < 3; ky++)
-#pragma unroll
-        for (int kx = 0; kx < 3; kx++) {
-            int yy = y + ky - 1, xx = x + kx - 1;
-            v[ky * 3 + kx] = (yy >= 0 && yy < Hp && xx >= 0 && xx < Wp) ? g[(size_t)yy * Wp + xx] : 0.0f;
-        }
-    f32x4* o = reinterpret_cast<f32x4*>(out + (size_t)idx * 64);
-#pragma unroll
-    for (int q = 0; q < 16; q++) {
-        f32x4 r;
-#pragma unroll
-        for (int e = 0; e < 4; e++) {
-            int c = q * 4 + e;
-            float a = s_w[9 * 64 + c];
-#pragma unroll
-            for (int k = 0; k < 9; k++) a += v[k] * s_w[k * 64 + c];
-            r[e] = a > 0.0f ? a : 0.0f;
-        }
-        o[q] = r;
-    }
-}
-
 // Generic conv (KS = 3: 3x3 pad 1 over 8x32 spatial tiles; KS = 1: 1x1 over linear 256-pixel
 // tiles) on v_mfma_f32_32x32x2_f32.  256 threads = 4 waves; wave wv owns tile rows 2wv, 2wv+1
 // (two 32-pixel M blocks) x 64 output channels (two N blocks): four 32x32 accumulators.
@@ -95,15 +55,23 @@ struct ConvGeom {
     static constexpr int NPIX = PW * PH;
 };
 
-template <int KS, bool POOL, int LAYER>
+// FUSE1A (conv1b only): `in` is the fp32 gray plane [B][H][W]; the kernel recomputes conv1a
+// (1 -> 64, 3x3, ReLU) for each 16-channel chunk of its 10x34 input patch from a 12x36 gray patch
+// in LDS, so the 64-channel full-resolution conv1a activation never goes through HBM.  Patch
+// positions outside the image are conv1b's zero padding (0, not conv1a evaluated there).
+template <int KS, bool POOL, int LAYER, bool FUSE1A = false>
 __global__ __launch_bounds__(256, 2) void k_conv_mfma(
     const float* __restrict__ in, int in_cstride, int in_coff, const float* __restrict__ wt,
     const float* __restrict__ bias, int cin, int cout, int cout_pad, float* __restrict__ out,
-    int out_cstride, int out_coff, int B, int H, int W, int tiles_x, int tiles_y, int relu) {
+    int out_cstride, int out_coff, int B, int H, int W, int tiles_x, int tiles_y, int relu,
+    const float* __restrict__ w1a, const float* __restrict__ b1a) {
     using G = ConvGeom<KS>;
     constexpr int CK = G::CK;
     __shared__ float s_in[CK * G::NPIX];
     __shared__ __attribute__((aligned(16))) float s_w[KS * KS * CK * 64];
+    constexpr int GW = G::PW + 2, GH = G::PH + 2;  // gray patch for the fused conv1a
+    __shared__ float s_g[FUSE1A ? GW * GH : 1];
+    __shared__ float s_w1a[FUSE1A ? 10 * 64 : 1];   // 9 taps x 64 + bias
 
     const int tid = threadIdx.x;
     const int wv = tid >> 6, lane = tid & 63, li = lane & 31, lh = lane >> 5;
@@ -131,10 +99,41 @@ __global__ __launch_bounds__(256, 2) void k_conv_mfma(
 #pragma unroll
             for (int e = 0; e < 16; e++) acc[r][nb][e] = 0.0f;
 
+    if constexpr (FUSE1A) {
+        const float* g = in + (size_t)b * H * W;
+        for (int i = tid; i < GW * GH; i += 256) {
+            const int yy = i / GW, xx = i - yy * GW;
+            const int gy = y0 - 2 + yy, gx = x0 - 2 + xx;
+            s_g[i] = (gy >= 0 && gy < H && gx >= 0 && gx < W) ? g[(size_t)gy * W + gx] : 0.0f;
+        }
+        for (int i = tid; i < 9 * 64; i += 256) s_w1a[i] = w1a[i];
+        if (tid < 64) s_w1a[9 * 64 + tid] = b1a[tid];
+        __syncthreads();
+    }
+
     for (int c0 = 0; c0 < cin; c0 += CK) {
+        if constexpr (FUSE1A) {
+            // ---- conv1a for channels c0..c0+CK-1 at the 10x34 patch positions ----
+            for (int idx = tid; idx < G::NPIX * CK; idx += 256) {
+                const int c = idx / G::NPIX, p = idx - c * G::NPIX;
+                const int py = p / G::PW, px = p - py * G::PW;
+                const int gy = y0 - 1 + py, gx = x0 - 1 + px;
+                float a = 0.0f;
+                if (gy >= 0 && gy < H && gx >= 0 && gx < W) {
+                    a = s_w1a[9 * 64 + c0 + c];
+#pragma unroll
+                    for (int ky = 0; ky < 3; ky++)
+#pragma unroll
+                        for (int kx = 0; kx < 3; kx++)
+                            a += s_g[(py + ky) * GW + px + kx] * s_w1a[(ky * 3 + kx) * 64 + c0 + c];
+                    a = a > 0.0f ? a : 0.0f;
+                }
+                s_in[c * G::NPIX + p] = a;
+            }
+        }
         // ---- stage input pixels (16-byte loads of 4 channels) ----
         constexpr int Q = CK / 4;
-        for (int idx = tid; idx < G::NPIX * Q; idx += 256) {
+        for (int idx = tid; idx < (FUSE1A ? 0 : G::NPIX * Q); idx += 256) {
             int p = idx / Q, q = idx - p * Q;
             f32x4 v = {0.f, 0.f, 0.f, 0.f};
             if constexpr (KS == 3) {
@@ -245,11 +244,13 @@ __global__ __launch_bounds__(256) void k_desc_l2norm(float* __restrict__ d, long
 
 namespace {
 
-template <int KS, bool POOL, int LAYER>
+template <int KS, bool POOL, int LAYER, bool FUSE1A = false>
 int launch_conv(const DevLayer& L, const float* in, int in_cstride, int in_coff, float* out,
-                int out_cstride, int out_coff, int B, int H, int W, int relu, hipStream_t s) {
+                int out_cstride, int out_coff, int B, int H, int W, int relu, hipStream_t s,
+                const DevLayer* L1a = nullptr) {
     using G = ConvGeom<KS>;
-    if (L.cin % G::CK != 0 || L.cout_pad % 64 != 0 || in_cstride % 4 || in_coff % 4) {
+    if (L.cin % G::CK != 0 || L.cout_pad % 64 != 0 || (!FUSE1A && (in_cstride % 4 || in_coff % 4)) ||
+        (FUSE1A && !L1a)) {
         set_error("conv: unsupported channel geometry");
         return VS_ERR_ARG;
     }
@@ -267,8 +268,9 @@ int launch_conv(const DevLayer& L, const float* in, int in_cstride, int in_coff,
         return VS_ERR_ARG;
     }
     dim3 grid((unsigned)nblk, L.cout_pad / 64);
-    hipLaunchKernelGGL((k_conv_mfma<KS, POOL, LAYER>), grid, dim3(256), 0, s, in, in_cstride, in_coff, L.w, L.b,
-                       L.cin, L.cout, L.cout_pad, out, out_cstride, out_coff, B, H, W, tiles_x, tiles_y, relu);
+    hipLaunchKernelGGL((k_conv_mfma<KS, POOL, LAYER, FUSE1A>), grid, dim3(256), 0, s, in, in_cstride, in_coff, L.w,
+                       L.b, L.cin, L.cout, L.cout_pad, out, out_cstride, out_coff, B, H, W, tiles_x, tiles_y, relu,
+                       L1a ? L1a->w : nullptr, L1a ? L1a->b : nullptr);
     VS_HIP(hipGetLastError());
     return VS_OK;
 }
@@ -280,7 +282,8 @@ int sp_forward(vs_ctx* ctx, int B, const uint8_t* d_img, int channels, int h, in
     const int hc = Hp / 8, wc = Wp / 8;
     const size_t full = (size_t)B * Hp * Wp;
     VS_CHECK(ctx->gray.ensure(full * sizeof(float)));
-    VS_CHECK(ctx->act0.ensure(full * 64 * sizeof(float)));
+    // largest activations: the half-resolution 64-channel maps (conv1b+pool and conv2a outputs)
+    VS_CHECK(ctx->act0.ensure(full / 4 * 64 * sizeof(float)));
     VS_CHECK(ctx->act1.ensure(full / 4 * 64 * sizeof(float)));
     VS_CHECK(ctx->semi.ensure((size_t)B * hc * wc * kSemiCh * sizeof(float)));
     VS_CHECK(ctx->dgrid.ensure((size_t)B * hc * wc * kDescDim * sizeof(float)));
@@ -295,17 +298,10 @@ int sp_forward(vs_ctx* ctx, int B, const uint8_t* d_img, int channels, int h, in
                            gray, total);
         VS_HIP(hipGetLastError());
     }
-    {
-        ProfScope ps(ctx, "conv1a", s);
-        int total = (int)full;
-        hipLaunchKernelGGL(k_conv1a, dim3((total + 255) / 256), dim3(256), 0, s, gray, L[0].w, L[0].b, a0, Hp, Wp,
-                           total);
-        VS_HIP(hipGetLastError());
-    }
     int H = Hp, W = Wp;
     {
-        ProfScope ps(ctx, "conv1b_pool", s);
-        VS_CHECK((launch_conv<3, true, 1>(L[1], a0, 64, 0, a1, 64, 0, B, H, W, 1, s)));
+        ProfScope ps(ctx, "conv1_fused", s);  // conv1a + conv1b + ReLU + 2x2 pool in one kernel
+        VS_CHECK((launch_conv<3, true, 1, true>(L[1], gray, 1, 0, a1, 64, 0, B, H, W, 1, s, &L[0])));
     }
     H /= 2; W /= 2;
     {

@@ -71,81 +71,102 @@ __global__ __launch_bounds__(256) void k_decode(const float* __restrict__ semi, 
 // One NMS round over a 32x32 tile (+4 halo).  The tile iterates to its local fixed point, writes
 // its interior states back and flags the frame if anything is still undecided.
 // flags[r*B + b] != 0  <=>  frame b still had undecided pixels after round r-1.
+// Each local iteration evaluates, for every interior pixel, M = the 9x9 window max of the
+// undecided pixels' 64-bit priority keys (score bits << 32 | ~raster index, 0 when not undecided)
+// and K = the 9x9 window OR of the kept flags, both separable (9-wide row pass, then column pass)
+// in LDS.  An undecided pixel with K set is out; one whose own key equals M (nothing undecided
+// outranks it in its window) is kept.
+__device__ __forceinline__ unsigned long long nms_key(float s, unsigned raster) {
+    return ((unsigned long long)__float_as_uint(s) << 32) | (unsigned)(0xFFFFFFFFu - raster);
+}
+
 __global__ __launch_bounds__(256) void k_nms_round(const float* __restrict__ heat, uint8_t* __restrict__ state,
                                                    int* __restrict__ flags, int r, int B, int Hp, int Wp,
                                                    int tiles_x) {
     const int b = blockIdx.y;
     if (flags[r * B + b] == 0) return;
-    __shared__ float s_score[kNmsReg * kNmsReg];
-    __shared__ uint8_t s_state[kNmsReg * kNmsReg];
+    __shared__ unsigned long long s_key[kNmsReg * kNmsReg];
+    __shared__ unsigned long long s_rmax[kNmsReg * kNmsTile];
+    __shared__ uint8_t s_kept[kNmsReg * kNmsReg];
+    __shared__ uint8_t s_rkept[kNmsReg * kNmsTile];
     const int tx = blockIdx.x % tiles_x, ty = blockIdx.x / tiles_x;
     const int gx0 = tx * kNmsTile - kRadius, gy0 = ty * kNmsTile - kRadius;
     const float* hb = heat + (size_t)b * Hp * Wp;
     uint8_t* sb = state + (size_t)b * Hp * Wp;
     for (int i = threadIdx.x; i < kNmsReg * kNmsReg; i += 256) {
-        int ry = i / kNmsReg, rx = i - ry * kNmsReg;
-        int gy = gy0 + ry, gx = gx0 + rx;
-        bool in = gy >= 0 && gy < Hp && gx >= 0 && gx < Wp;
-        s_score[i] = in ? hb[(size_t)gy * Wp + gx] : 0.0f;
-        s_state[i] = in ? sb[(size_t)gy * Wp + gx] : ST_OUT;
+        const int ry = i / kNmsReg, rx = i - ry * kNmsReg;
+        const int gy = gy0 + ry, gx = gx0 + rx;
+        unsigned long long key = 0;
+        uint8_t kept = 0;
+        if (gy >= 0 && gy < Hp && gx >= 0 && gx < Wp) {
+            const uint8_t st = sb[(size_t)gy * Wp + gx];
+            if (st == ST_UNDECIDED) key = nms_key(hb[(size_t)gy * Wp + gx], (unsigned)(gy * Wp + gx));
+            kept = (st == ST_KEPT);
+        }
+        s_key[i] = key;
+        s_kept[i] = kept;
     }
     __syncthreads();
-    // each thread owns 4 interior pixels
-    int own[4];
-#pragma unroll
-    for (int j = 0; j < 4; j++) {
-        int k = threadIdx.x + 256 * j;
-        int iy = k / kNmsTile, ix = k - iy * kNmsTile;
-        own[j] = (iy + kRadius) * kNmsReg + ix + kRadius;
-    }
     int changed;
     do {
-        uint8_t ns[4];
+        // row pass: 40 region rows x 32 interior columns
+        for (int i = threadIdx.x; i < kNmsReg * kNmsTile; i += 256) {
+            const int ry = i / kNmsTile, ix = i - ry * kNmsTile;
+            const int base = ry * kNmsReg + ix;
+            unsigned long long m = s_key[base];
+            uint8_t k = s_kept[base];
+#pragma unroll
+            for (int d = 1; d <= 2 * kRadius; d++) {
+                const unsigned long long v = s_key[base + d];
+                m = v > m ? v : m;
+                k |= s_kept[base + d];
+            }
+            s_rmax[i] = m;
+            s_rkept[i] = k;
+        }
+        __syncthreads();
+        uint8_t dec[4];
         int ch = 0;
 #pragma unroll
         for (int j = 0; j < 4; j++) {
-            const int p = own[j];
-            ns[j] = s_state[p];
-            if (ns[j] != ST_UNDECIDED) continue;
-            const float sp = s_score[p];
-            bool kept_nb = false, blocked = false;
-            for (int dy = -kRadius; dy <= kRadius && !kept_nb; dy++) {
-                for (int dx = -kRadius; dx <= kRadius; dx++) {
-                    if (dx == 0 && dy == 0) continue;
-                    const int q = p + dy * kNmsReg + dx;
-                    const uint8_t sq = s_state[q];
-                    if (sq == ST_KEPT) {
-                        kept_nb = true;
-                        break;
-                    }
-                    if (sq == ST_UNDECIDED) {
-                        const float s = s_score[q];
-                        // q precedes p in raster order iff dy < 0 || (dy == 0 && dx < 0)
-                        if (s > sp || (s == sp && (dy < 0 || (dy == 0 && dx < 0)))) blocked = true;
-                    }
-                }
+            const int kk = threadIdx.x + 256 * j;
+            const int iy = kk / kNmsTile, ix = kk - iy * kNmsTile;
+            const unsigned long long key = s_key[(iy + kRadius) * kNmsReg + ix + kRadius];
+            dec[j] = 0;
+            if (key == 0) continue;
+            unsigned long long m = 0;
+            uint8_t k = 0;
+#pragma unroll
+            for (int d = 0; d <= 2 * kRadius; d++) {
+                const unsigned long long v = s_rmax[(iy + d) * kNmsTile + ix];
+                m = v > m ? v : m;
+                k |= s_rkept[(iy + d) * kNmsTile + ix];
             }
-            if (kept_nb) {
-                ns[j] = ST_OUT;
-                ch = 1;
-            } else if (!blocked) {
-                ns[j] = ST_KEPT;
-                ch = 1;
-            }
+            if (k) dec[j] = ST_OUT;
+            else if (m == key) dec[j] = ST_KEPT;
+            ch |= dec[j] != 0;
         }
         __syncthreads();
 #pragma unroll
-        for (int j = 0; j < 4; j++) s_state[own[j]] = ns[j];
+        for (int j = 0; j < 4; j++) {
+            if (!dec[j]) continue;
+            const int kk = threadIdx.x + 256 * j;
+            const int iy = kk / kNmsTile, ix = kk - iy * kNmsTile;
+            const int p = (iy + kRadius) * kNmsReg + ix + kRadius;
+            s_key[p] = 0;
+            if (dec[j] == ST_KEPT) s_kept[p] = 1;
+        }
         changed = __syncthreads_or(ch);
     } while (changed);
     int und = 0;
 #pragma unroll
     for (int j = 0; j < 4; j++) {
-        int k = threadIdx.x + 256 * j;
-        int iy = k / kNmsTile, ix = k - iy * kNmsTile;
-        int gy = gy0 + kRadius + iy, gx = gx0 + kRadius + ix;
+        const int kk = threadIdx.x + 256 * j;
+        const int iy = kk / kNmsTile, ix = kk - iy * kNmsTile;
+        const int gy = gy0 + kRadius + iy, gx = gx0 + kRadius + ix;
         if (gy < Hp && gx < Wp) {
-            uint8_t v = s_state[own[j]];
+            const int p = (iy + kRadius) * kNmsReg + ix + kRadius;
+            const uint8_t v = s_kept[p] ? ST_KEPT : (s_key[p] ? ST_UNDECIDED : ST_OUT);
             sb[(size_t)gy * Wp + gx] = v;
             und |= (v == ST_UNDECIDED);
         }
