@@ -7,7 +7,12 @@
 //   N = output channels (64 per workgroup), K = k*k*Cin (Cin staged through LDS 16 at a time).
 // Bias, ReLU and the 2x2 max-pool are fused into the epilogue: the 32x32 accumulator keeps
 // horizontally adjacent pixels in adjacent registers of one lane and the two image rows of a
-// pool window in the same wave, so pooling never leaves registers.
+// pool window in the same wave, so pooling never leaves registers.  conv1a (1 -> 64) is fused
+// into conv1b's input staging.
+//
+// Pipeline per channel chunk: the next chunk's input / weights are fetched into registers
+// (global loads, or the fused conv1a recompute) before the current chunk's MFMAs so their
+// latency hides under 288 MFMAs; the MFMA loop reads its LDS operands one k-step ahead.
 #include <hip/hip_runtime.h>
 
 #include "vs_internal.h"
@@ -67,6 +72,10 @@ __global__ __launch_bounds__(256, 2) void k_conv_mfma(
     const float* __restrict__ w1a, const float* __restrict__ b1a) {
     using G = ConvGeom<KS>;
     constexpr int CK = G::CK;
+    constexpr int Q = CK / 4;                                  // float4 per pixel and chunk
+    constexpr int NQ = (G::NPIX * Q + 255) / 256;              // input float4 per thread
+    constexpr int NW = (KS * KS * CK * 16 + 255) / 256;        // weight float4 per thread
+    constexpr int S = KS * KS * CK / 2;                        // MFMA k-steps per chunk
     __shared__ float s_in[CK * G::NPIX];
     __shared__ __attribute__((aligned(16))) float s_w[KS * KS * CK * 64];
     constexpr int GW = G::PW + 2, GH = G::PH + 2;  // gray patch for the fused conv1a
@@ -111,75 +120,142 @@ __global__ __launch_bounds__(256, 2) void k_conv_mfma(
         __syncthreads();
     }
 
-    for (int c0 = 0; c0 < cin; c0 += CK) {
+    f32x4 rin[FUSE1A ? 1 : NQ];
+    f32x4 rw[NW];
+    constexpr int NF = FUSE1A ? (G::NPIX * CK + 255) / 256 : 1;  // fused conv1a values per thread
+    float rf[NF];
+    // fused conv1a output j of this thread for the chunk starting at channel c0 (0 = zero padding)
+    auto conv1a_val = [&](int j, int c0) -> float {
+        const int idx = tid + 256 * j;
+        const int c = idx / G::NPIX, p = idx - c * G::NPIX;
+        const int py = p / G::PW, px = p - py * G::PW;
+        const int gy = y0 - 1 + py, gx = x0 - 1 + px;
+        float a = 0.0f;
+        if (idx < G::NPIX * CK && gy >= 0 && gy < H && gx >= 0 && gx < W) {
+            a = s_w1a[9 * 64 + c0 + c];
+#pragma unroll
+            for (int ky = 0; ky < 3; ky++)
+#pragma unroll
+                for (int kx = 0; kx < 3; kx++)
+                    a += s_g[(py + ky) * GW + px + kx] * s_w1a[(ky * 3 + kx) * 64 + c0 + c];
+            a = a > 0.0f ? a : 0.0f;
+        }
+        return a;
+    };
+
+    // global -> registers for the chunk starting at channel c0 (the fused conv1a input is computed
+    // at commit time instead: holding it in registers would spill)
+    auto fetch = [&](int c0) {
+        if constexpr (!FUSE1A) {
+#pragma unroll
+            for (int j = 0; j < NQ; j++) {
+                const int idx = tid + 256 * j;
+                const int p = idx / Q, q = idx - p * Q;
+                f32x4 v = {0.f, 0.f, 0.f, 0.f};
+                if (idx < G::NPIX * Q) {
+                    if constexpr (KS == 3) {
+                        const int py = p / G::PW, px = p - py * G::PW;
+                        const int gy = y0 - 1 + py, gx = x0 - 1 + px;
+                        if (gy >= 0 && gy < H && gx >= 0 && gx < W)
+                            v = *reinterpret_cast<const f32x4*>(in + (((size_t)b * H + gy) * W + gx) * in_cstride +
+                                                                in_coff + c0 + 4 * q);
+                    } else {
+                        const long m = m0 + p;
+                        if (m < M) v = *reinterpret_cast<const f32x4*>(in + (size_t)m * in_cstride + in_coff + c0 + 4 * q);
+                    }
+                }
+                rin[j] = v;
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < NW; j++) {
+            const int idx = tid + 256 * j;
+            if (idx < KS * KS * CK * 16) {
+                const int r = idx >> 4, q = idx & 15;
+                const int kk = r / CK, c = r - kk * CK;
+                rw[j] = *reinterpret_cast<const f32x4*>(wt + ((size_t)kk * cin + c0 + c) * cout_pad + n0 + 4 * q);
+            }
+        }
+    };
+    // registers -> LDS (fused: the conv1a values computed into rf during the previous MFMA loop)
+    auto commit = [&](int c0) {
+        (void)c0;
         if constexpr (FUSE1A) {
-            // ---- conv1a for channels c0..c0+CK-1 at the 10x34 patch positions ----
-            for (int idx = tid; idx < G::NPIX * CK; idx += 256) {
-                const int c = idx / G::NPIX, p = idx - c * G::NPIX;
-                const int py = p / G::PW, px = p - py * G::PW;
-                const int gy = y0 - 1 + py, gx = x0 - 1 + px;
-                float a = 0.0f;
-                if (gy >= 0 && gy < H && gx >= 0 && gx < W) {
-                    a = s_w1a[9 * 64 + c0 + c];
 #pragma unroll
-                    for (int ky = 0; ky < 3; ky++)
+            for (int j = 0; j < NF; j++) {
+                const int idx = tid + 256 * j;
+                if (idx < G::NPIX * CK) s_in[idx] = rf[j];  // idx = c * NPIX + p
+            }
+        } else {
 #pragma unroll
-                        for (int kx = 0; kx < 3; kx++)
-                            a += s_g[(py + ky) * GW + px + kx] * s_w1a[(ky * 3 + kx) * 64 + c0 + c];
-                    a = a > 0.0f ? a : 0.0f;
+            for (int j = 0; j < NQ; j++) {
+                const int idx = tid + 256 * j;
+                if (idx < G::NPIX * Q) {
+                    const int p = idx / Q, q = idx - p * Q;
+#pragma unroll
+                    for (int e = 0; e < 4; e++) s_in[(4 * q + e) * G::NPIX + p] = rin[j][e];
                 }
-                s_in[c * G::NPIX + p] = a;
             }
         }
-        // ---- stage input pixels (16-byte loads of 4 channels) ----
-        constexpr int Q = CK / 4;
-        for (int idx = tid; idx < (FUSE1A ? 0 : G::NPIX * Q); idx += 256) {
-            int p = idx / Q, q = idx - p * Q;
-            f32x4 v = {0.f, 0.f, 0.f, 0.f};
-            if constexpr (KS == 3) {
-                int py = p / G::PW, px = p - py * G::PW;
-                int gy = y0 - 1 + py, gx = x0 - 1 + px;
-                if (gy >= 0 && gy < H && gx >= 0 && gx < W)
-                    v = *reinterpret_cast<const f32x4*>(in + (((size_t)b * H + gy) * W + gx) * in_cstride + in_coff + c0 + 4 * q);
-            } else {
-                long m = m0 + p;
-                if (m < M) v = *reinterpret_cast<const f32x4*>(in + (size_t)m * in_cstride + in_coff + c0 + 4 * q);
-            }
 #pragma unroll
-            for (int e = 0; e < 4; e++) s_in[(4 * q + e) * G::NPIX + p] = v[e];
+        for (int j = 0; j < NW; j++) {
+            const int idx = tid + 256 * j;
+            if (idx < KS * KS * CK * 16) {
+                const int r = idx >> 4, q = idx & 15;
+                *reinterpret_cast<f32x4*>(&s_w[r * 64 + 4 * q]) = rw[j];
+            }
         }
-        // ---- stage weights rows (kk, c) x 64 channels ----
-        for (int idx = tid; idx < KS * KS * CK * 16; idx += 256) {
-            int r = idx >> 4, q = idx & 15;
-            int kk = r / CK, c = r - kk * CK;
-            const f32x4 v = *reinterpret_cast<const f32x4*>(wt + ((size_t)kk * cin + c0 + c) * cout_pad + n0 + 4 * q);
-            *reinterpret_cast<f32x4*>(&s_w[r * 64 + 4 * q]) = v;
+    };
+    // LDS operands of k-step s (s = kk * CK/2 + cp; lane half lh supplies channel 2cp + lh)
+    auto operands = [&](int s, float& a0, float& a1, float& b0, float& b1) {
+        const int kk = s / (CK / 2), cp = s - kk * (CK / 2);
+        const int ky = kk / KS, kx = kk - ky * KS;
+        const int c = 2 * cp + lh;
+        const float* si = &s_in[c * G::NPIX];
+        if constexpr (KS == 3) {
+            a0 = si[(2 * wv + 0 + ky) * G::PW + li + kx];
+            a1 = si[(2 * wv + 1 + ky) * G::PW + li + kx];
+        } else {
+            a0 = si[(2 * wv + 0) * 32 + li];
+            a1 = si[(2 * wv + 1) * 32 + li];
+        }
+        b0 = s_w[(kk * CK + c) * 64 + li];
+        b1 = s_w[(kk * CK + c) * 64 + 32 + li];
+    };
+
+    fetch(0);
+    if constexpr (FUSE1A) {
+#pragma unroll
+        for (int j = 0; j < NF; j++) rf[j] = conv1a_val(j, 0);
+    }
+    commit(0);
+    __syncthreads();
+    for (int c0 = 0; c0 < cin; c0 += CK) {
+        const bool more = c0 + CK < cin;
+        if (more) fetch(c0 + CK);
+        const int cnext = more ? c0 + CK : 0;  // fused conv1a: the next chunk, computed between MFMAs
+        float A0[2], A1[2], B0[2], B1[2];
+        operands(0, A0[0], A1[0], B0[0], B1[0]);
+#pragma unroll
+        for (int s = 0; s < S; s++) {
+            const int cur = s & 1, nxt = cur ^ 1;
+            if (s + 1 < S) operands(s + 1, A0[nxt], A1[nxt], B0[nxt], B1[nxt]);
+            if constexpr (FUSE1A) {
+                if (s % 3 == 1 && s / 3 < NF) rf[s / 3] = conv1a_val(s / 3, cnext);
+            }
+            // keep the next step's LDS reads ahead of this step's MFMAs (the scheduler otherwise
+            // sinks them to just before their consumers and exposes the LDS latency)
+            __builtin_amdgcn_sched_barrier(0);
+            acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(A0[cur], B0[cur], acc[0][0], 0, 0, 0);
+            acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(A0[cur], B1[cur], acc[0][1], 0, 0, 0);
+            acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(A1[cur], B0[cur], acc[1][0], 0, 0, 0);
+            acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(A1[cur], B1[cur], acc[1][1], 0, 0, 0);
         }
         __syncthreads();
-#pragma unroll
-        for (int kk = 0; kk < KS * KS; kk++) {
-            const int ky = kk / KS, kx = kk % KS;
-#pragma unroll
-            for (int cp = 0; cp < CK / 2; cp++) {
-                const int c = 2 * cp + lh;
-                const float* si = &s_in[c * G::NPIX];
-                float a0, a1;
-                if constexpr (KS == 3) {
-                    a0 = si[(2 * wv + 0 + ky) * G::PW + li + kx];
-                    a1 = si[(2 * wv + 1 + ky) * G::PW + li + kx];
-                } else {
-                    a0 = si[(2 * wv + 0) * 32 + li];
-                    a1 = si[(2 * wv + 1) * 32 + li];
-                }
-                const float b0 = s_w[(kk * CK + c) * 64 + li];
-                const float b1 = s_w[(kk * CK + c) * 64 + 32 + li];
-                acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b0, acc[0][0], 0, 0, 0);
-                acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b1, acc[0][1], 0, 0, 0);
-                acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b0, acc[1][0], 0, 0, 0);
-                acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b1, acc[1][1], 0, 0, 0);
-            }
+        if (more) {
+            commit(c0 + CK);
+            __syncthreads();
         }
-        __syncthreads();
     }
 
     // ---- epilogue: C/D map of 32x32 blocks: col (out channel) = lane&31,
