@@ -51,9 +51,9 @@ __global__ void k_gray_norm(const uint8_t* __restrict__ img, int channels, int h
 // (two 32-pixel M blocks) x 64 output channels (two N blocks): four 32x32 accumulators.
 // LDS: s_in[CK][pixels] (channel-major: a half-wave reads 32 consecutive pixels, conflict free)
 //      s_w [k*k*CK][64] (a half-wave reads 32 consecutive output channels, conflict free).
-template <int KS>
+template <int KS, int CKV = (KS == 3 ? 16 : 32)>
 struct ConvGeom {
-    static constexpr int CK = (KS == 3) ? 16 : 32;
+    static constexpr int CK = CKV;
     static constexpr int TW = 32, TH = 8;
     static constexpr int PW = (KS == 3) ? TW + 2 : TW;
     static constexpr int PH = (KS == 3) ? TH + 2 : TH;
@@ -64,13 +64,13 @@ struct ConvGeom {
 // (1 -> 64, 3x3, ReLU) for each 16-channel chunk of its 10x34 input patch from a 12x36 gray patch
 // in LDS, so the 64-channel full-resolution conv1a activation never goes through HBM.  Patch
 // positions outside the image are conv1b's zero padding (0, not conv1a evaluated there).
-template <int KS, bool POOL, int LAYER, bool FUSE1A = false>
-__global__ __launch_bounds__(256, 2) void k_conv_mfma(
+template <int KS, bool POOL, int LAYER, bool FUSE1A = false, int CKV = (KS == 3 ? 16 : 32)>
+__global__ __launch_bounds__(256, (KS == 3 && CKV == 32) ? 1 : 2) void k_conv_mfma(
     const float* __restrict__ in, int in_cstride, int in_coff, const float* __restrict__ wt,
     const float* __restrict__ bias, int cin, int cout, int cout_pad, float* __restrict__ out,
     int out_cstride, int out_coff, int B, int H, int W, int tiles_x, int tiles_y, int relu,
     const float* __restrict__ w1a, const float* __restrict__ b1a) {
-    using G = ConvGeom<KS>;
+    using G = ConvGeom<KS, CKV>;
     constexpr int CK = G::CK;
     constexpr int Q = CK / 4;                                  // float4 per pixel and chunk
     constexpr int NQ = (G::NPIX * Q + 255) / 256;              // input float4 per thread
@@ -320,11 +320,11 @@ __global__ __launch_bounds__(256) void k_desc_l2norm(float* __restrict__ d, long
 
 namespace {
 
-template <int KS, bool POOL, int LAYER, bool FUSE1A = false>
+template <int KS, bool POOL, int LAYER, bool FUSE1A = false, int CKV = (KS == 3 ? 16 : 32)>
 int launch_conv(const DevLayer& L, const float* in, int in_cstride, int in_coff, float* out,
                 int out_cstride, int out_coff, int B, int H, int W, int relu, hipStream_t s,
                 const DevLayer* L1a = nullptr) {
-    using G = ConvGeom<KS>;
+    using G = ConvGeom<KS, CKV>;
     if (L.cin % G::CK != 0 || L.cout_pad % 64 != 0 || (!FUSE1A && (in_cstride % 4 || in_coff % 4)) ||
         (FUSE1A && !L1a)) {
         set_error("conv: unsupported channel geometry");
@@ -344,11 +344,22 @@ int launch_conv(const DevLayer& L, const float* in, int in_cstride, int in_coff,
         return VS_ERR_ARG;
     }
     dim3 grid((unsigned)nblk, L.cout_pad / 64);
-    hipLaunchKernelGGL((k_conv_mfma<KS, POOL, LAYER, FUSE1A>), grid, dim3(256), 0, s, in, in_cstride, in_coff, L.w,
+    hipLaunchKernelGGL((k_conv_mfma<KS, POOL, LAYER, FUSE1A, CKV>), grid, dim3(256), 0, s, in, in_cstride, in_coff, L.w,
                        L.b, L.cin, L.cout, L.cout_pad, out, out_cstride, out_coff, B, H, W, tiles_x, tiles_y, relu,
                        L1a ? L1a->w : nullptr, L1a ? L1a->b : nullptr);
     VS_HIP(hipGetLastError());
     return VS_OK;
+}
+
+// 3x3 layers use a 16-channel chunk: 58.6 KB of LDS, two workgroups per CU, so one workgroup's
+// staging overlaps the other's MFMAs.  (A 32-channel chunk at one workgroup per CU measured
+// 1.5x slower end to end: 1306 vs 1952 frames/s, round 1.)
+template <bool POOL, int LAYER, bool FUSE1A = false>
+int conv3(vs_ctx* ctx, const DevLayer& L, const float* in, int in_cstride, int in_coff, float* out, int out_cstride,
+          int out_coff, int B, int H, int W, hipStream_t s, const DevLayer* L1a = nullptr) {
+    (void)ctx;
+    return launch_conv<3, POOL, LAYER, FUSE1A, 16>(L, in, in_cstride, in_coff, out, out_cstride, out_coff, B, H, W, 1,
+                                                   s, L1a);
 }
 
 }  // namespace
@@ -377,38 +388,38 @@ int sp_forward(vs_ctx* ctx, int B, const uint8_t* d_img, int channels, int h, in
     int H = Hp, W = Wp;
     {
         ProfScope ps(ctx, "conv1_fused", s);  // conv1a + conv1b + ReLU + 2x2 pool in one kernel
-        VS_CHECK((launch_conv<3, true, 1, true>(L[1], gray, 1, 0, a1, 64, 0, B, H, W, 1, s, &L[0])));
+        VS_CHECK((conv3<true, 1, true>(ctx, L[1], gray, 1, 0, a1, 64, 0, B, H, W, s, &L[0])));
     }
     H /= 2; W /= 2;
     {
         ProfScope ps(ctx, "conv2a", s);
-        VS_CHECK((launch_conv<3, false, 2>(L[2], a1, 64, 0, a0, 64, 0, B, H, W, 1, s)));
+        VS_CHECK((conv3<false, 2>(ctx, L[2], a1, 64, 0, a0, 64, 0, B, H, W, s)));
     }
     {
         ProfScope ps(ctx, "conv2b_pool", s);
-        VS_CHECK((launch_conv<3, true, 3>(L[3], a0, 64, 0, a1, 64, 0, B, H, W, 1, s)));
+        VS_CHECK((conv3<true, 3>(ctx, L[3], a0, 64, 0, a1, 64, 0, B, H, W, s)));
     }
     H /= 2; W /= 2;
     {
         ProfScope ps(ctx, "conv3a", s);
-        VS_CHECK((launch_conv<3, false, 4>(L[4], a1, 64, 0, a0, 128, 0, B, H, W, 1, s)));
+        VS_CHECK((conv3<false, 4>(ctx, L[4], a1, 64, 0, a0, 128, 0, B, H, W, s)));
     }
     {
         ProfScope ps(ctx, "conv3b_pool", s);
-        VS_CHECK((launch_conv<3, true, 5>(L[5], a0, 128, 0, a1, 128, 0, B, H, W, 1, s)));
+        VS_CHECK((conv3<true, 5>(ctx, L[5], a0, 128, 0, a1, 128, 0, B, H, W, s)));
     }
     H /= 2; W /= 2;
     {
         ProfScope ps(ctx, "conv4a", s);
-        VS_CHECK((launch_conv<3, false, 6>(L[6], a1, 128, 0, a0, 128, 0, B, H, W, 1, s)));
+        VS_CHECK((conv3<false, 6>(ctx, L[6], a1, 128, 0, a0, 128, 0, B, H, W, s)));
     }
     {
         ProfScope ps(ctx, "conv4b", s);
-        VS_CHECK((launch_conv<3, false, 7>(L[7], a0, 128, 0, a1, 128, 0, B, H, W, 1, s)));
+        VS_CHECK((conv3<false, 7>(ctx, L[7], a0, 128, 0, a1, 128, 0, B, H, W, s)));
     }
     {
         ProfScope ps(ctx, "head_a", s);  // convPa | convDa, 128 -> 512
-        VS_CHECK((launch_conv<3, false, 8>(ctx->head_a, a1, 128, 0, a0, 512, 0, B, H, W, 1, s)));
+        VS_CHECK((conv3<false, 8>(ctx, ctx->head_a, a1, 128, 0, a0, 512, 0, B, H, W, s)));
     }
     {
         ProfScope ps(ctx, "head_b", s);  // convPb 256 -> 65 and convDb 256 -> 256 (1x1)
