@@ -142,6 +142,39 @@ int vs_ransac_3d3d_pairs_dev(vs_ctx* ctx, int P, const int* d_pairs, const vs_ke
                              const uint32_t* d_seeds, int iters, double thr, double* d_R,
                              double* d_t, int* d_ok, int* d_diag, void* stream);
 
+/* ---- A11: Slam::track_local_map (Slam.cpp:380-469) -------------------------------------- */
+/* Map points: mp_pos n_mp x 3 fp64 (world), mp_desc n_mp x 256 fp32, mp_valid[i] = valid AND
+ * has a descriptor (Slam.cpp:417-418).  Keypoints/descriptors of the frame (n_kp <= 1024), its
+ * camera->world pose, K (the reference uses Config FX/FY/CX/CY) and image size (640 x 480 in the
+ * reference, Config.h:10-11).  kp_to_mp (n_kp) is updated in place (Frame::map_point_indices);
+ * *tracked = the reference's return value; the (map point, keypoint) pairs the reference passes
+ * to MapPoint::add_observation are returned in map-point order (first obs_cap of *n_obs). */
+int vs_track_local_map(vs_ctx* ctx, const double* mp_pos, const float* mp_desc,
+                       const uint8_t* mp_valid, int n_mp, const vs_keypoint* kps,
+                       const float* desc, int n_kp, const double R_world[9],
+                       const double t_world[3], const double K[4], int img_w, int img_h,
+                       int* kp_to_mp, int* tracked, int* obs_mp, int* obs_kp, int obs_cap,
+                       int* n_obs);
+/* Device variant (map resident in HBM); d_result[0] = tracked, d_result[1] = n_obs. */
+int vs_track_local_map_dev(vs_ctx* ctx, const double* d_mp_pos, const float* d_mp_desc,
+                           const uint8_t* d_mp_valid, int n_mp, const vs_keypoint* d_kps,
+                           const float* d_desc, int n_kp, const double R_world[9],
+                           const double t_world[3], const double K[4], int img_w, int img_h,
+                           int* d_kp_to_mp, int* d_obs_mp, int* d_obs_kp, int obs_cap,
+                           int* d_result, void* stream);
+
+/* ---- A13: Optimizer::optimize_pose (Optimizer.cpp:54-180) ------------------------------- */
+/* p3d n x 3 fp64 world points, p2d n x 2 fp32 pixels; R, t = camera->world pose in/out (the
+ * frame's pose is updated, Optimizer.cpp:166-168).  RMS reprojection error before/after; both 0
+ * and the pose untouched when n < 3 (Optimizer.cpp:60-62). */
+int vs_optimize_pose(vs_ctx* ctx, const double* p3d, const float* p2d, int n, const double K[4],
+                     double R[9], double t[3], double* rms_before, double* rms_after);
+/* nprob independent problems on device: points d_off[p] .. d_off[p+1]; d_R [p][9], d_t [p][3]
+ * in/out; d_res [p][4] = {rms_before, rms_after, iterations, accepted steps}; d_ok [p]. */
+int vs_optimize_pose_batch_dev(vs_ctx* ctx, int nprob, const double* d_p3d, const float* d_p2d,
+                               const int* d_off, const double K[4], double* d_R, double* d_t,
+                               double* d_res, int* d_ok, void* stream);
+
 /* ---- profiling ----------------------------------------------------------------------- */
 /* When enabled, every stage of the _dev pipelines brackets its launches with hipEvents on the
  * stream it runs on; vs_profile_read returns per-stage accumulated milliseconds and launch

@@ -33,6 +33,11 @@ _SIG = {
     "orc_match_ratio": (None, [_P, _I, _P, _I, ctypes.c_float, _P, _P, _P, _P]),
     "orc_match_ratio_f64": (None, [_P, _I, _P, _I, ctypes.c_float, _P, _P, _P, _P]),
     "orc_ransac_3d3d": (_I, [_P, _P, _I, _P, _P, _I, _I, _P, ctypes.c_uint32, _I, ctypes.c_double, _P, _P, _P]),
+    "orc_track_local_map": (_I, [_P, _P, _P, _I, _P, _P, _I, _P, _P, _P, _I, _I, _P, _P, _P, _I, _P]),
+    "orc_rodrigues_vec2mat": (None, [_P, _P]),
+    "orc_rodrigues_mat2vec": (None, [_P, _P]),
+    "orc_project_point": (None, [_P, _P, _P, _P, _P]),
+    "orc_optimize_pose": (_I, [_P, _P, _I, _P, _P, _P, _P, _P, _P]),
     "orc_mt19937": (None, [ctypes.c_uint32, _I, _P]),
     "orc_expf_array": (None, [_P, _I, _P]),
     "orc_expf_exhaustive_check": (ctypes.c_long, [ctypes.c_float, ctypes.c_float]),
@@ -165,6 +170,59 @@ def ransac_3d3d(pts1, pts2, depth1, depth2, K=(525.0, 525.0, 319.5, 239.5), seed
     ok = lib().orc_ransac_3d3d(_p(p1), _p(p2), p1.shape[0], _p(d1), _p(d2), d1.shape[0], d1.shape[1], _p(Ka), seed,
                                iters, thr, _p(R), _p(t), _p(diag))
     return bool(ok), R.reshape(3, 3), t, diag
+
+
+def track_local_map(mp_pos, mp_desc, mp_valid, kps, desc, R_world, t_world, K=(525.0, 525.0, 319.5, 239.5),
+                    img_w=640, img_h=480, kp_to_mp=None):
+    mp_pos = np.ascontiguousarray(mp_pos, np.float64).reshape(-1, 3)
+    mp_desc = np.ascontiguousarray(mp_desc, np.float32).reshape(-1, 256)
+    mp_valid = np.ascontiguousarray(mp_valid, np.uint8).reshape(-1)
+    kps = np.ascontiguousarray(kps, KEYPOINT_DTYPE)
+    desc = np.ascontiguousarray(desc, np.float32).reshape(-1, 256)
+    n_mp, n_kp = mp_pos.shape[0], len(kps)
+    kpmp = np.full(n_kp, -1, np.int32) if kp_to_mp is None else np.array(kp_to_mp, np.int32)
+    cap = max(n_mp, 1)
+    obs_mp = np.zeros(cap, np.int32)
+    obs_kp = np.zeros(cap, np.int32)
+    nobs = ctypes.c_int(0)
+    R = np.ascontiguousarray(R_world, np.float64).reshape(9)
+    t = np.ascontiguousarray(t_world, np.float64).reshape(3)
+    Ka = np.asarray(K, np.float64)
+    tracked = lib().orc_track_local_map(_p(mp_pos), _p(mp_desc), _p(mp_valid), n_mp, _p(kps), _p(desc), n_kp, _p(R),
+                                        _p(t), _p(Ka), img_w, img_h, _p(kpmp), _p(obs_mp), _p(obs_kp), cap,
+                                        ctypes.byref(nobs))
+    m = min(nobs.value, cap)
+    return tracked, kpmp, obs_mp[:m].copy(), obs_kp[:m].copy()
+
+
+def rodrigues(x):
+    x = np.ascontiguousarray(x, np.float64)
+    if x.size == 3:
+        out = np.zeros(9)
+        lib().orc_rodrigues_vec2mat(_p(x), _p(out))
+        return out.reshape(3, 3)
+    out = np.zeros(3)
+    lib().orc_rodrigues_mat2vec(_p(x.reshape(9)), _p(out))
+    return out
+
+
+def project_point(pw, R_world, t_world, K=(525.0, 525.0, 319.5, 239.5)):
+    uv = np.zeros(2)
+    lib().orc_project_point(_p(np.ascontiguousarray(pw, np.float64)), _p(np.ascontiguousarray(R_world, np.float64)),
+                            _p(np.ascontiguousarray(t_world, np.float64)), _p(np.asarray(K, np.float64)), _p(uv))
+    return uv
+
+
+def optimize_pose(p3d, p2d, R_world, t_world, K=(525.0, 525.0, 319.5, 239.5)):
+    P = np.ascontiguousarray(p3d, np.float64).reshape(-1, 3)
+    p2 = np.ascontiguousarray(p2d, np.float32).reshape(-1, 2)
+    R = np.array(R_world, np.float64).reshape(9)
+    t = np.array(t_world, np.float64).reshape(3)
+    eb, ea = ctypes.c_double(0), ctypes.c_double(0)
+    stats = np.zeros(3)
+    lib().orc_optimize_pose(_p(P), _p(p2), P.shape[0], _p(np.asarray(K, np.float64)), _p(R), _p(t), ctypes.byref(eb),
+                            ctypes.byref(ea), _p(stats))
+    return R.reshape(3, 3), t, eb.value, ea.value, stats
 
 
 def mt19937(seed, count):

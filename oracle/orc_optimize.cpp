@@ -1,0 +1,206 @@
+// orc_optimize.cpp — CPU restatement of Optimizer::project_point and Optimizer::optimize_pose
+// (reference src/Optimizer.cpp:26-48, 54-180).  TEST INFRASTRUCTURE ONLY (see oracle.h).
+//
+// External semantics restated (OpenCV 4.x, unpinned): cv::Rodrigues both directions (the R->r
+// direction without its SVD re-orthonormalisation, which moves an orthonormal R by O(1e-16));
+// cv::solve(DECOMP_CHOLESKY) as an LL^T factorisation that fails when a pivot drops below
+// DBL_EPSILON.  Matrix products sum left to right.
+#include <cfloat>
+#include <cmath>
+#include <vector>
+
+#include "oracle.h"
+
+extern "C" {
+
+void orc_rodrigues_vec2mat(const double r[3], double R[9]) {
+    double theta = std::sqrt(r[0] * r[0] + r[1] * r[1] + r[2] * r[2]);
+    if (theta < DBL_EPSILON) {
+        for (int i = 0; i < 9; i++) R[i] = (i % 4 == 0) ? 1.0 : 0.0;
+        return;
+    }
+    double c = std::cos(theta), s = std::sin(theta), c1 = 1.0 - c;
+    double itheta = theta ? 1.0 / theta : 0.0;
+    double rx = r[0] * itheta, ry = r[1] * itheta, rz = r[2] * itheta;
+    const double rrt[9] = {rx * rx, rx * ry, rx * rz, rx * ry, ry * ry, ry * rz, rx * rz, ry * rz, rz * rz};
+    const double rx_[9] = {0, -rz, ry, rz, 0, -rx, -ry, rx, 0};
+    for (int i = 0; i < 9; i++) R[i] = c * ((i % 4 == 0) ? 1.0 : 0.0) + c1 * rrt[i] + s * rx_[i];
+}
+
+void orc_rodrigues_mat2vec(const double R[9], double r[3]) {
+    double rx = R[7] - R[5], ry = R[2] - R[6], rz = R[3] - R[1];
+    double s = std::sqrt((rx * rx + ry * ry + rz * rz) * 0.25);
+    double c = (R[0] + R[4] + R[8] - 1) * 0.5;
+    c = c > 1. ? 1. : c < -1. ? -1. : c;
+    double theta = std::acos(c);
+    if (s < 1e-5) {
+        if (c > 0) {
+            r[0] = r[1] = r[2] = 0;
+            return;
+        }
+        double t = (R[0] + 1) * 0.5;
+        rx = std::sqrt(std::fmax(t, 0.));
+        t = (R[4] + 1) * 0.5;
+        ry = std::sqrt(std::fmax(t, 0.)) * (R[1] < 0 ? -1. : 1.);
+        t = (R[8] + 1) * 0.5;
+        rz = std::sqrt(std::fmax(t, 0.)) * (R[2] < 0 ? -1. : 1.);
+        if (std::fabs(rx) < std::fabs(ry) && std::fabs(rx) < std::fabs(rz) && (R[5] > 0) != (ry * rz > 0)) rz = -rz;
+        theta /= std::sqrt(rx * rx + ry * ry + rz * rz);
+        r[0] = rx * theta;
+        r[1] = ry * theta;
+        r[2] = rz * theta;
+        return;
+    }
+    double vth = 1 / (2 * s);
+    vth *= theta;
+    r[0] = rx * vth;
+    r[1] = ry * vth;
+    r[2] = rz * vth;
+}
+
+// Optimizer::project_point (Optimizer.cpp:26-48): R_world, t_world camera->world.
+void orc_project_point(const double pw[3], const double R[9], const double t[3], const double K[4], double uv[2]) {
+    double Rc[9], tc[3];
+    for (int i = 0; i < 3; i++)
+        for (int j = 0; j < 3; j++) Rc[i * 3 + j] = R[j * 3 + i];
+    for (int i = 0; i < 3; i++) tc[i] = -(Rc[i * 3 + 0] * t[0] + Rc[i * 3 + 1] * t[1] + Rc[i * 3 + 2] * t[2]);
+    double pc[3];
+    for (int i = 0; i < 3; i++) pc[i] = Rc[i * 3 + 0] * pw[0] + Rc[i * 3 + 1] * pw[1] + Rc[i * 3 + 2] * pw[2] + tc[i];
+    double z = pc[2];
+    if (z < 1e-6) {
+        uv[0] = -1;
+        uv[1] = -1;
+        return;
+    }
+    uv[0] = K[0] * pc[0] / z + K[2];
+    uv[1] = K[1] * pc[1] / z + K[3];
+}
+
+// LL^T solve of the n x n SPD system A x = b (A row-major, overwritten); 0 when not SPD.
+int orc_cholesky_solve(double* A, double* b, int n) {
+    for (int j = 0; j < n; j++) {
+        double s = A[j * n + j];
+        for (int k = 0; k < j; k++) s -= A[j * n + k] * A[j * n + k];
+        if (s < DBL_EPSILON) return 0;
+        double d = std::sqrt(s);
+        A[j * n + j] = d;
+        for (int i = j + 1; i < n; i++) {
+            double v = A[i * n + j];
+            for (int k = 0; k < j; k++) v -= A[i * n + k] * A[j * n + k];
+            A[i * n + j] = v / d;
+        }
+    }
+    for (int i = 0; i < n; i++) {
+        double v = b[i];
+        for (int k = 0; k < i; k++) v -= A[i * n + k] * b[k];
+        b[i] = v / A[i * n + i];
+    }
+    for (int i = n - 1; i >= 0; i--) {
+        double v = b[i];
+        for (int k = i + 1; k < n; k++) v -= A[k * n + i] * b[k];
+        b[i] = v / A[i * n + i];
+    }
+    return 1;
+}
+
+static double rms_err(const double* P, const float* p2, int n, const double R[9], const double t[3], const double K[4]) {
+    double e = 0;
+    for (int i = 0; i < n; i++) {
+        double uv[2];
+        orc_project_point(P + 3 * i, R, t, K, uv);
+        double dx = uv[0] - p2[2 * i], dy = uv[1] - p2[2 * i + 1];
+        e += dx * dx + dy * dy;
+    }
+    return std::sqrt(e / n);
+}
+
+// Optimizer::optimize_pose (Optimizer.cpp:54-180).  R, t (camera->world) in/out.
+// Returns 0 when the reference returns {0, 0} (n < 3), else 1; stats = {iterations run, accepted
+// steps, final lambda}.
+int orc_optimize_pose(const double* P, const float* p2, int n, const double K[4], double R[9], double t[3],
+                      double* err_before, double* err_after, double stats[3]) {
+    *err_before = *err_after = 0;
+    if (n < 3) return 0;
+    double rvec[3], tvec[3] = {t[0], t[1], t[2]};
+    orc_rodrigues_mat2vec(R, rvec);
+    *err_before = rms_err(P, p2, n, R, t, K);
+    double lambda = 1e-3;  // OPT_LM_LAMBDA (Config.h:105)
+    const double eps = 1e-6;
+    int iters = 0, accepted = 0;
+    std::vector<double> J((size_t)2 * n * 6), r((size_t)2 * n);
+    for (int iter = 0; iter < 10; iter++) {  // OPT_MAX_ITERATIONS (Config.h:103)
+        iters++;
+        double Rcur[9];
+        orc_rodrigues_vec2mat(rvec, Rcur);
+        double Rp[3][9];
+        for (int j = 0; j < 3; j++) {
+            double rp[3] = {rvec[0], rvec[1], rvec[2]};
+            rp[j] += eps;
+            orc_rodrigues_vec2mat(rp, Rp[j]);
+        }
+        for (int i = 0; i < n; i++) {
+            double uv[2];
+            orc_project_point(P + 3 * i, Rcur, tvec, K, uv);
+            r[2 * i] = uv[0] - p2[2 * i];
+            r[2 * i + 1] = uv[1] - p2[2 * i + 1];
+            for (int j = 0; j < 6; j++) {
+                double uvp[2];
+                if (j < 3) {
+                    orc_project_point(P + 3 * i, Rp[j], tvec, K, uvp);
+                } else {
+                    double tp[3] = {tvec[0], tvec[1], tvec[2]};
+                    tp[j - 3] += eps;
+                    orc_project_point(P + 3 * i, Rcur, tp, K, uvp);
+                }
+                J[(2 * i) * 6 + j] = (uvp[0] - uv[0]) / eps;
+                J[(2 * i + 1) * 6 + j] = (uvp[1] - uv[1]) / eps;
+            }
+        }
+        double JtJ[36] = {0}, Jtr[6] = {0};
+        for (int a = 0; a < 6; a++) {
+            for (int c = 0; c < 6; c++) {
+                double s = 0;
+                for (int k = 0; k < 2 * n; k++) s += J[k * 6 + a] * J[k * 6 + c];
+                JtJ[a * 6 + c] = s;
+            }
+            double s = 0;
+            for (int k = 0; k < 2 * n; k++) s += J[k * 6 + a] * r[k];
+            Jtr[a] = s;
+        }
+        for (int i = 0; i < 6; i++) JtJ[i * 6 + i] += lambda;
+        double delta[6];
+        for (int i = 0; i < 6; i++) delta[i] = -Jtr[i];
+        if (!orc_cholesky_solve(JtJ, delta, 6)) {
+            lambda *= 10;
+            continue;
+        }
+        double rv_new[3] = {rvec[0] + delta[0], rvec[1] + delta[1], rvec[2] + delta[2]};
+        double tv_new[3] = {tvec[0] + delta[3], tvec[1] + delta[4], tvec[2] + delta[5]};
+        double Rnew[9];
+        orc_rodrigues_vec2mat(rv_new, Rnew);
+        double error_new = rms_err(P, p2, n, Rnew, tv_new, K);
+        double current_error = rms_err(P, p2, n, Rcur, tvec, K);
+        if (error_new < current_error) {
+            for (int k = 0; k < 3; k++) {
+                rvec[k] = rv_new[k];
+                tvec[k] = tv_new[k];
+            }
+            lambda /= 2;
+            accepted++;
+        } else {
+            lambda *= 10;
+        }
+        if (std::fabs(current_error - error_new) < 1e-6) break;  // OPT_CONVERGENCE
+    }
+    orc_rodrigues_vec2mat(rvec, R);
+    for (int k = 0; k < 3; k++) t[k] = tvec[k];
+    *err_after = rms_err(P, p2, n, R, t, K);
+    if (stats) {
+        stats[0] = iters;
+        stats[1] = accepted;
+        stats[2] = lambda;
+    }
+    return 1;
+}
+
+}  // extern "C"

@@ -159,3 +159,84 @@ def rigid_scene(n, outlier_frac, seed, K=(525.0, 525.0, 319.5, 239.5), h=480, w=
         pts2.append((u2f, v2f))
         inl.append(is_in)
     return (np.array(pts1, np.float32), np.array(pts2, np.float32), depth1, depth2, R, t, np.array(inl))
+
+
+def track_local_map_py(mp_pos, mp_desc, mp_valid, kps_xy, desc, R, t, K=(525.0, 525.0, 319.5, 239.5), w=640, h=480):
+    """Slam.cpp:380-469 in pure Python (independent of the C oracle)."""
+    cell = 30
+    GW, GH = (w + cell - 1) // cell, (h + cell - 1) // cell
+    grid = [[] for _ in range(GW * GH)]
+    f32 = np.float32
+    for ki, (x, y) in enumerate(kps_xy):
+        gx = min(int(f32(x) / f32(cell)), GW - 1)
+        gy = min(int(f32(y) / f32(cell)), GH - 1)
+        if gx >= 0 and gy >= 0:
+            grid[gy * GW + gx].append(ki)
+    Rc = np.asarray(R, np.float64).reshape(3, 3).T
+    tw = np.asarray(t, np.float64).reshape(3)
+    tc = [-(Rc[i, 0] * tw[0] + Rc[i, 1] * tw[1] + Rc[i, 2] * tw[2]) for i in range(3)]
+    fx, fy, cx, cy = K
+    best_kp = [1e9] * len(kps_xy)
+    kp_to_mp = [-1] * len(kps_xy)
+    obs = []
+    for mp in range(len(mp_pos)):
+        if not mp_valid[mp]:
+            continue
+        x, y, z = (float(v) for v in mp_pos[mp])
+        px = Rc[0, 0] * x + Rc[0, 1] * y + Rc[0, 2] * z + tc[0]
+        py = Rc[1, 0] * x + Rc[1, 1] * y + Rc[1, 2] * z + tc[1]
+        pz = Rc[2, 0] * x + Rc[2, 1] * y + Rc[2, 2] * z + tc[2]
+        if pz < float(f32(0.1)) or pz > 50.0:
+            continue
+        u = fx * px / pz + cx
+        v = fy * py / pz + cy
+        if u < 0 or u >= w or v < 0 or v >= h:
+            continue
+        gx0, gy0 = max(0, int((u - 12.0) / cell)), max(0, int((v - 12.0) / cell))
+        gx1, gy1 = min(GW - 1, int((u + 12.0) / cell)), min(GH - 1, int((v + 12.0) / cell))
+        bk, bd = -1, 0.5
+        for gy in range(gy0, gy1 + 1):
+            for gx in range(gx0, gx1 + 1):
+                for ki in grid[gy * GW + gx]:
+                    dx, dy = u - float(kps_xy[ki][0]), v - float(kps_xy[ki][1])
+                    if dx * dx + dy * dy > 144.0:
+                        continue
+                    diff = (mp_desc[mp] - desc[ki]).astype(np.float32).astype(np.float64)
+                    s = 0.0
+                    for k in range(0, 256, 4):
+                        s += diff[k] * diff[k] + diff[k + 1] * diff[k + 1] + diff[k + 2] * diff[k + 2] + diff[k + 3] * diff[k + 3]
+                    d = float(np.sqrt(s))
+                    if d < bd:
+                        bd, bk = d, ki
+        if bk >= 0 and bd < best_kp[bk]:
+            kp_to_mp[bk] = mp
+            best_kp[bk] = bd
+            obs.append((mp, bk))
+    return len(obs), kp_to_mp, obs
+
+
+def synthetic_tracking_problem(n_kp, n_mp, seed, K=(525.0, 525.0, 319.5, 239.5), w=640, h=480):
+    """Keypoints + descriptors of a frame and a map whose points project near them (several map
+    points per keypoint, descriptor noise around the 0.5 threshold, invalid points, points behind
+    the camera / out of view), with the frame's camera->world pose."""
+    rng = np.random.default_rng(seed)
+    fx, fy, cx, cy = K
+    kxy = np.stack([rng.integers(0, w, n_kp), rng.integers(0, h, n_kp)], 1).astype(np.float32)
+    desc = rng.standard_normal((n_kp, 256)).astype(np.float32)
+    desc /= np.linalg.norm(desc, axis=1, keepdims=True)
+    R = rodrigues(rng.normal(size=3) * 0.3)
+    t = rng.normal(size=3)
+    pos, mdesc = [], []
+    for i in range(n_mp):
+        ki = int(rng.integers(0, n_kp))
+        u = kxy[ki, 0] + rng.normal() * 6.0
+        v = kxy[ki, 1] + rng.normal() * 6.0
+        z = rng.uniform(0.5, 8.0) if rng.random() > 0.02 else rng.choice([-1.0, 0.05, 60.0])
+        pc = np.array([(u - cx) * z / fx, (v - cy) * z / fy, z])
+        pos.append(R @ pc + t)  # camera -> world
+        d = desc[ki] + rng.normal(size=256).astype(np.float32) * rng.uniform(0.0, 0.04)
+        mdesc.append(d / np.linalg.norm(d))
+    pos = np.array(pos)
+    mdesc = np.array(mdesc, np.float32)
+    valid = (rng.random(n_mp) > 0.05).astype(np.uint8)
+    return kxy, desc, pos, mdesc, valid, R, t

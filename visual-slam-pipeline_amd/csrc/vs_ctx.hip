@@ -247,7 +247,7 @@ void vs_destroy(vs_ctx* ctx) {
     DevBuf* bufs[] = {&ctx->gray,  &ctx->act0,   &ctx->act1,   &ctx->semi,   &ctx->dgrid,  &ctx->heat,
                       &ctx->state, &ctx->flags,  &ctx->keys,   &ctx->keycnt, &ctx->h_img,  &ctx->h_kps,
                       &ctx->h_desc, &ctx->h_n,   &ctx->h_aux0, &ctx->h_aux1, &ctx->h_aux2, &ctx->h_aux3,
-                      &ctx->h_aux4, &ctx->h_aux5, &ctx->norms};
+                      &ctx->h_aux4, &ctx->h_aux5, &ctx->norms, &ctx->tlm};
     for (DevBuf* b : bufs) b->release();
     for (auto& st : ctx->prof)
         for (auto& pr : st.pending) {
@@ -484,6 +484,101 @@ int vs_ransac_3d3d(vs_ctx* ctx, const float* pts1, const float* pts2, int n, con
     std::memcpy(t, rt + 9, 3 * sizeof(double));
     *ok = res[0];
     if (diag) std::memcpy(diag, res + 1, 4 * sizeof(int));
+    return VS_OK;
+}
+
+// ---- Slam::track_local_map (Slam.cpp:380-469) ---------------------------------------------------
+int vs_track_local_map_dev(vs_ctx* ctx, const double* d_mp_pos, const float* d_mp_desc, const uint8_t* d_mp_valid,
+                           int n_mp, const vs_keypoint* d_kps, const float* d_desc, int n_kp, const double R_world[9],
+                           const double t_world[3], const double K[4], int img_w, int img_h, int* d_kp_to_mp,
+                           int* d_obs_mp, int* d_obs_kp, int obs_cap, int* d_result, void* stream) {
+    VS_ARG(ctx && R_world && t_world && K && d_kp_to_mp && d_result, "vs_track_local_map_dev: null argument");
+    VS_ARG(n_mp >= 0 && n_kp >= 0 && obs_cap >= 0, "vs_track_local_map_dev: negative size");
+    VS_ARG(n_mp == 0 || (d_mp_pos && d_mp_desc && d_mp_valid), "vs_track_local_map_dev: null map");
+    VS_ARG(n_kp == 0 || (d_kps && d_desc), "vs_track_local_map_dev: null keypoints");
+    VS_HIP(hipSetDevice(ctx->device));
+    return track_local_map(ctx, d_mp_pos, d_mp_desc, d_mp_valid, n_mp, d_kps, d_desc, n_kp, R_world, t_world, K, img_w,
+                           img_h, d_kp_to_mp, d_obs_mp, d_obs_kp, obs_cap, d_result, pick(ctx, stream));
+}
+
+int vs_track_local_map(vs_ctx* ctx, const double* mp_pos, const float* mp_desc, const uint8_t* mp_valid, int n_mp,
+                       const vs_keypoint* kps, const float* desc, int n_kp, const double R_world[9],
+                       const double t_world[3], const double K[4], int img_w, int img_h, int* kp_to_mp, int* tracked,
+                       int* obs_mp, int* obs_kp, int obs_cap, int* n_obs) {
+    VS_ARG(ctx && R_world && t_world && K && tracked && n_obs, "vs_track_local_map: null argument");
+    VS_ARG(n_mp >= 0 && n_kp >= 0 && obs_cap >= 0, "vs_track_local_map: negative size");
+    VS_ARG(n_kp == 0 || (kps && desc && kp_to_mp), "vs_track_local_map: null keypoints");
+    VS_ARG(n_mp == 0 || (mp_pos && mp_desc && mp_valid), "vs_track_local_map: null map");
+    VS_ARG(obs_cap == 0 || (obs_mp && obs_kp), "vs_track_local_map: null observation buffers");
+    *tracked = 0;
+    *n_obs = 0;
+    if (n_kp == 0) return VS_OK;  // Slam.cpp:384: no keypoints or descriptors -> 0
+    VS_HIP(hipSetDevice(ctx->device));
+    hipStream_t s = ctx->stream;
+    VS_CHECK(upload(ctx->h_aux0, mp_pos, (size_t)n_mp * 3 + 1, s));
+    VS_CHECK(upload(ctx->h_aux1, mp_desc, (size_t)n_mp * 256 + 4, s));
+    VS_CHECK(upload(ctx->h_aux2, mp_valid, (size_t)n_mp + 1, s));
+    VS_CHECK(upload(ctx->h_kps, kps, (size_t)n_kp, s));
+    VS_CHECK(upload(ctx->h_desc, desc, (size_t)n_kp * 256, s));
+    VS_CHECK(ctx->h_aux3.ensure(((size_t)n_kp + 2 + 2 * (size_t)obs_cap) * sizeof(int)));
+    int* d_kpmp = ctx->h_aux3.as<int>();
+    int* d_res = d_kpmp + n_kp;
+    int* d_obs = d_res + 2;
+    VS_HIP(hipMemcpyAsync(d_kpmp, kp_to_mp, (size_t)n_kp * sizeof(int), hipMemcpyHostToDevice, s));
+    VS_CHECK(track_local_map(ctx, ctx->h_aux0.as<double>(), ctx->h_aux1.as<float>(), ctx->h_aux2.as<uint8_t>(), n_mp,
+                             ctx->h_kps.as<vs_keypoint>(), ctx->h_desc.as<float>(), n_kp, R_world, t_world, K, img_w,
+                             img_h, d_kpmp, d_obs, d_obs + obs_cap, obs_cap, d_res, s));
+    int res[2];
+    VS_HIP(hipMemcpyAsync(kp_to_mp, d_kpmp, (size_t)n_kp * sizeof(int), hipMemcpyDeviceToHost, s));
+    VS_HIP(hipMemcpyAsync(res, d_res, sizeof(res), hipMemcpyDeviceToHost, s));
+    VS_HIP(hipStreamSynchronize(s));
+    *tracked = res[0];
+    *n_obs = res[1];
+    const int nc = res[1] < obs_cap ? res[1] : obs_cap;
+    if (nc > 0) {
+        VS_HIP(hipMemcpyAsync(obs_mp, d_obs, (size_t)nc * sizeof(int), hipMemcpyDeviceToHost, s));
+        VS_HIP(hipMemcpyAsync(obs_kp, d_obs + obs_cap, (size_t)nc * sizeof(int), hipMemcpyDeviceToHost, s));
+        VS_HIP(hipStreamSynchronize(s));
+    }
+    return VS_OK;
+}
+
+// ---- Optimizer::optimize_pose (Optimizer.cpp:54-180) ---------------------------------------------
+int vs_optimize_pose_batch_dev(vs_ctx* ctx, int nprob, const double* d_p3d, const float* d_p2d, const int* d_off,
+                               const double K[4], double* d_R, double* d_t, double* d_res, int* d_ok, void* stream) {
+    VS_ARG(ctx && K && d_off && d_R && d_t && d_res && d_ok, "vs_optimize_pose_batch_dev: null argument");
+    VS_HIP(hipSetDevice(ctx->device));
+    return optimize_pose(ctx, nprob, d_p3d, d_p2d, d_off, K, d_R, d_t, d_res, d_ok, pick(ctx, stream));
+}
+
+int vs_optimize_pose(vs_ctx* ctx, const double* p3d, const float* p2d, int n, const double K[4], double R[9],
+                     double t[3], double* rms_before, double* rms_after) {
+    VS_ARG(ctx && K && R && t && rms_before && rms_after, "vs_optimize_pose: null argument");
+    VS_ARG(n >= 0 && (n == 0 || (p3d && p2d)), "vs_optimize_pose: bad points");
+    *rms_before = *rms_after = 0;
+    if (n < 3) return VS_OK;  // Optimizer.cpp:60-62 returns {0, 0}
+    VS_HIP(hipSetDevice(ctx->device));
+    hipStream_t s = ctx->stream;
+    VS_CHECK(upload(ctx->h_aux0, p3d, (size_t)n * 3, s));
+    VS_CHECK(upload(ctx->h_aux1, p2d, (size_t)n * 2, s));
+    VS_CHECK(ctx->h_aux2.ensure(16 * sizeof(double) + 4 * sizeof(int)));
+    double* dR = ctx->h_aux2.as<double>();
+    int* dmeta = reinterpret_cast<int*>(dR + 16);
+    double Rt[12];
+    std::memcpy(Rt, R, 9 * sizeof(double));
+    std::memcpy(Rt + 9, t, 3 * sizeof(double));
+    const int off[2] = {0, n};
+    VS_HIP(hipMemcpyAsync(dR, Rt, sizeof(Rt), hipMemcpyHostToDevice, s));
+    VS_HIP(hipMemcpyAsync(dmeta, off, sizeof(off), hipMemcpyHostToDevice, s));
+    VS_CHECK(optimize_pose(ctx, 1, ctx->h_aux0.as<double>(), ctx->h_aux1.as<float>(), dmeta, K, dR, dR + 9, dR + 12,
+                           dmeta + 2, s));
+    double out[16];
+    VS_HIP(hipMemcpyAsync(out, dR, sizeof(out), hipMemcpyDeviceToHost, s));
+    VS_HIP(hipStreamSynchronize(s));
+    std::memcpy(R, out, 9 * sizeof(double));
+    std::memcpy(t, out + 9, 3 * sizeof(double));
+    *rms_before = out[12];
+    *rms_after = out[13];
     return VS_OK;
 }
 

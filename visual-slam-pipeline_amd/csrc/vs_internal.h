@@ -92,7 +92,7 @@ struct vs_ctx {
     vs::DevBuf gray, act0, act1, semi, dgrid, heat, state, flags, keys, keycnt;
     // host-API staging
     vs::DevBuf h_img, h_kps, h_desc, h_n, h_aux0, h_aux1, h_aux2, h_aux3, h_aux4, h_aux5;
-    vs::DevBuf norms;
+    vs::DevBuf norms, tlm;
 
     bool prof_on = false;
     std::vector<vs::ProfStage> prof;
@@ -129,5 +129,13 @@ int ransac3d_pairs(vs_ctx* ctx, int P, const int* d_pairs, const vs_keypoint* d_
                    const vs_match* d_good, const int* d_ngood, const float* d_depth, int h, int w,
                    const double K[4], const uint32_t* d_seeds, int iters, double thr,
                    double* d_R, double* d_t, int* d_ok, int* d_diag, hipStream_t s);
+// Local-map tracking (d_result = {tracked, observations})
+int track_local_map(vs_ctx* ctx, const double* d_mp_pos, const float* d_mp_desc, const uint8_t* d_mp_valid, int n_mp,
+                    const vs_keypoint* d_kps, const float* d_desc, int nkp, const double R[9], const double t[3],
+                    const double K[4], int img_w, int img_h, int* d_kp_to_mp, int* d_obs_mp, int* d_obs_kp,
+                    int obs_cap, int* d_result, hipStream_t s);
+// Pose LM, nprob problems with point ranges d_off[p]..d_off[p+1]
+int optimize_pose(vs_ctx* ctx, int nprob, const double* d_P, const float* d_p2, const int* d_off, const double K[4],
+                  double* d_R, double* d_t, double* d_res, int* d_ok, hipStream_t s);
 
 }  // namespace vs

@@ -47,6 +47,10 @@ _SIG = {
                             _P, _P, _P, _P]),
     "vs_ransac_3d3d_pairs_dev": (_I, [_P, _I, _P, _P, _I, _P, _P, _P, _I, _I, _P, _P, _I,
                                       ctypes.c_double, _P, _P, _P, _P, _P]),
+    "vs_track_local_map": (_I, [_P, _P, _P, _P, _I, _P, _P, _I, _P, _P, _P, _I, _I, _P, _P, _P, _P, _I, _P]),
+    "vs_track_local_map_dev": (_I, [_P, _P, _P, _P, _I, _P, _P, _I, _P, _P, _P, _I, _I, _P, _P, _P, _I, _P, _P]),
+    "vs_optimize_pose": (_I, [_P, _P, _P, _I, _P, _P, _P, _P, _P]),
+    "vs_optimize_pose_batch_dev": (_I, [_P, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
     "vs_profile_enable": (_I, [_P, _I]),
     "vs_profile_reset": (_I, [_P]),
     "vs_profile_read": (_I, [_P, _I, _P, _P, _P, _P]),
@@ -210,6 +214,41 @@ class Context:
         _check(self.lib.vs_ransac_3d3d(self.h, _ptr(p1), _ptr(p2), p1.shape[0], _ptr(d1), _ptr(d2), h, w, _ptr(Ka),
                                        seed, iters, thr, _ptr(R), _ptr(t), ctypes.byref(ok), _ptr(diag)))
         return bool(ok.value), R.reshape(3, 3), t, diag
+
+    # ---- Slam::track_local_map ----
+    def track_local_map(self, mp_pos, mp_desc, mp_valid, kps, desc, R_world, t_world, K=K_TUM, img_w=640, img_h=480,
+                        kp_to_mp=None, obs_cap=None):
+        mp_pos = np.ascontiguousarray(mp_pos, np.float64).reshape(-1, 3)
+        mp_desc = np.ascontiguousarray(mp_desc, np.float32).reshape(-1, 256)
+        mp_valid = np.ascontiguousarray(mp_valid, np.uint8).reshape(-1)
+        kps = np.ascontiguousarray(kps, KEYPOINT_DTYPE)
+        desc = np.ascontiguousarray(desc, np.float32).reshape(-1, 256)
+        n_mp, n_kp = mp_pos.shape[0], len(kps)
+        kpmp = np.full(n_kp, -1, np.int32) if kp_to_mp is None else np.array(kp_to_mp, np.int32)
+        cap = max(n_mp, 1) if obs_cap is None else obs_cap
+        obs_mp = np.zeros(max(cap, 1), np.int32)
+        obs_kp = np.zeros(max(cap, 1), np.int32)
+        tracked, nobs = ctypes.c_int(0), ctypes.c_int(0)
+        R = np.ascontiguousarray(R_world, np.float64).reshape(9)
+        t = np.ascontiguousarray(t_world, np.float64).reshape(3)
+        Ka = _k_array(K)
+        _check(self.lib.vs_track_local_map(self.h, _ptr(mp_pos), _ptr(mp_desc), _ptr(mp_valid), n_mp, _ptr(kps),
+                                           _ptr(desc), n_kp, _ptr(R), _ptr(t), _ptr(Ka), img_w, img_h, _ptr(kpmp),
+                                           ctypes.byref(tracked), _ptr(obs_mp), _ptr(obs_kp), cap, ctypes.byref(nobs)))
+        m = min(nobs.value, cap)
+        return tracked.value, kpmp, obs_mp[:m].copy(), obs_kp[:m].copy()
+
+    # ---- Optimizer::optimize_pose ----
+    def optimize_pose(self, p3d, p2d, R_world, t_world, K=K_TUM):
+        P = np.ascontiguousarray(p3d, np.float64).reshape(-1, 3)
+        p2 = np.ascontiguousarray(p2d, np.float32).reshape(-1, 2)
+        R = np.array(R_world, np.float64).reshape(9)
+        t = np.array(t_world, np.float64).reshape(3)
+        eb, ea = ctypes.c_double(0), ctypes.c_double(0)
+        Ka = _k_array(K)
+        _check(self.lib.vs_optimize_pose(self.h, _ptr(P), _ptr(p2), P.shape[0], _ptr(Ka), _ptr(R), _ptr(t),
+                                         ctypes.byref(eb), ctypes.byref(ea)))
+        return R.reshape(3, 3), t, eb.value, ea.value
 
     # ---- device-batched entry points (pointers are ints, e.g. torch tensor.data_ptr()) ----
     def extract_batch_dev(self, B, d_imgs, h, w, d_kps, d_desc, d_n, cap, stream=None):
