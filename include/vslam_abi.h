@@ -175,6 +175,26 @@ int vs_optimize_pose_batch_dev(vs_ctx* ctx, int nprob, const double* d_p3d, cons
                                const int* d_off, const double K[4], double* d_R, double* d_t,
                                double* d_res, int* d_ok, void* stream);
 
+/* ---- A10: Slam::solve_pnp (Slam.cpp:505-529) --------------------------------------------- */
+/* cv::solvePnPRansac(obj, img, K, no distortion, useExtrinsicGuess = false, ransac_iters,
+ * 8 px (Config.h:78), confidence 0.99) + the camera -> world conversion (Slam.cpp:521-526).
+ * obj_pts n x 3 fp32 (cv::Point3f), img_pts n x 2 fp32 (cv::Point2f); ransac_iters <=
+ * VS_PNP_MAX_ITERS.  *success = PnPResult.success (n >= min_inliers, RANSAC found a model and
+ * its inlier count >= min_inliers); R_world / t_world written on success; *inlier_count =
+ * inliers.rows; inlier_mask (n, nullable) = the RANSAC inliers; diag (nullable) = {RANSAC
+ * iterations run, winning iteration, LM iterations, LM accepted steps}. */
+#define VS_PNP_MAX_ITERS 2048
+int vs_solve_pnp(vs_ctx* ctx, const float* obj_pts, const float* img_pts, int n, const double K[4],
+                 int ransac_iters, int min_inliers, double R_world[9], double t_world[3],
+                 int* success, int* inlier_count, uint8_t* inlier_mask, int diag[4]);
+/* nprob problems on device (one workgroup each): points d_off[p] .. d_off[p+1] of d_obj / d_img;
+ * d_R [p][9], d_t [p][3] = world pose (written on success); d_stat [p][8] = {success, inliers,
+ * RANSAC iterations, winning iteration, LM iterations, LM accepted, n, 0}; d_mask [total points]
+ * = RANSAC inliers (required). */
+int vs_solve_pnp_batch_dev(vs_ctx* ctx, int nprob, const float* d_obj, const float* d_img,
+                           const int* d_off, const double K[4], int ransac_iters, int min_inliers,
+                           double* d_R, double* d_t, int* d_stat, uint8_t* d_mask, void* stream);
+
 /* ---- profiling ----------------------------------------------------------------------- */
 /* When enabled, every stage of the _dev pipelines brackets its launches with hipEvents on the
  * stream it runs on; vs_profile_read returns per-stage accumulated milliseconds and launch

@@ -38,6 +38,9 @@ _SIG = {
     "orc_rodrigues_mat2vec": (None, [_P, _P]),
     "orc_project_point": (None, [_P, _P, _P, _P, _P]),
     "orc_optimize_pose": (_I, [_P, _P, _I, _P, _P, _P, _P, _P, _P]),
+    "orc_epnp": (_I, [_P, _P, _I, _P, _P, _P]),
+    "orc_pnp_ransac": (_I, [_P, _P, _I, _P, _I, ctypes.c_double, ctypes.c_double, _P, _P, _P, _P, _P]),
+    "orc_solve_pnp": (_I, [_P, _P, _I, _P, _I, _I, _P, _P, _P]),
     "orc_mt19937": (None, [ctypes.c_uint32, _I, _P]),
     "orc_expf_array": (None, [_P, _I, _P]),
     "orc_expf_exhaustive_check": (ctypes.c_long, [ctypes.c_float, ctypes.c_float]),
@@ -223,6 +226,40 @@ def optimize_pose(p3d, p2d, R_world, t_world, K=(525.0, 525.0, 319.5, 239.5)):
     lib().orc_optimize_pose(_p(P), _p(p2), P.shape[0], _p(np.asarray(K, np.float64)), _p(R), _p(t), ctypes.byref(eb),
                             ctypes.byref(ea), _p(stats))
     return R.reshape(3, 3), t, eb.value, ea.value, stats
+
+
+def epnp(X, uv, K=(525.0, 525.0, 319.5, 239.5)):
+    """EPnP on all points: (ok, R world->camera, t)."""
+    X = np.ascontiguousarray(X, np.float64).reshape(-1, 3)
+    uv = np.ascontiguousarray(uv, np.float64).reshape(-1, 2)
+    R, t = np.zeros(9), np.zeros(3)
+    ok = lib().orc_epnp(_p(X), _p(uv), X.shape[0], _p(np.asarray(K, np.float64)), _p(R), _p(t))
+    return bool(ok), R.reshape(3, 3), t
+
+
+def pnp_ransac(obj, img, iters=100, thr=8.0, conf=0.99, K=(525.0, 525.0, 319.5, 239.5)):
+    """cv::solvePnPRansac restatement: (ok, rvec, tvec, n_inliers, mask, diag) in camera frame."""
+    P = np.ascontiguousarray(obj, np.float32).reshape(-1, 3)
+    p2 = np.ascontiguousarray(img, np.float32).reshape(-1, 2)
+    n = P.shape[0]
+    rv, tv = np.zeros(3), np.zeros(3)
+    mask = np.zeros(max(n, 1), np.uint8)
+    inl = ctypes.c_int(0)
+    diag = np.zeros(4, np.int32)
+    ok = lib().orc_pnp_ransac(_p(P), _p(p2), n, _p(np.asarray(K, np.float64)), iters, thr, conf, _p(rv), _p(tv),
+                              _p(mask), ctypes.byref(inl), _p(diag))
+    return bool(ok), rv, tv, inl.value, mask[:n].astype(bool), diag
+
+
+def solve_pnp(obj, img, ransac_iters=100, min_inliers=10, K=(525.0, 525.0, 319.5, 239.5)):
+    """Slam::solve_pnp restatement: (success, R_world, t_world, inlier_count)."""
+    P = np.ascontiguousarray(obj, np.float32).reshape(-1, 3)
+    p2 = np.ascontiguousarray(img, np.float32).reshape(-1, 2)
+    R, t = np.zeros(9), np.zeros(3)
+    inl = ctypes.c_int(0)
+    ok = lib().orc_solve_pnp(_p(P), _p(p2), P.shape[0], _p(np.asarray(K, np.float64)), ransac_iters, min_inliers,
+                             _p(R), _p(t), ctypes.byref(inl))
+    return bool(ok), R.reshape(3, 3), t, inl.value
 
 
 def mt19937(seed, count):

@@ -1,0 +1,174 @@
+"""CPU tests pinning the PnP restatement (A10, Slam::solve_pnp, reference src/Slam.cpp:505-529).
+
+OpenCV's solvePnPRansac is unpinned (no OpenCV in the image, no reference fixtures), so the
+oracle is pinned by known answers (noise-free scenes recover the pose to 1e-6, the inlier mask
+equals the ground-truth outlier labels) and by an independent Python replay of the RANSAC driver
+(cv::RNG subset stream, the max(best, modelPoints-1) acceptance rule and RANSACUpdateNumIters).
+"""
+import math
+
+import numpy as np
+import pytest
+
+import restate
+
+K = (525.0, 525.0, 319.5, 239.5)
+
+
+def pnp_problem(n, seed, noise=0.0, outlier_frac=0.0):
+    """n world points seen by a camera (world->camera R, t); returns obj (f32), img (f32),
+    R_cw, t_cw, and the outlier labels."""
+    rng = np.random.default_rng(seed)
+    R = restate.rodrigues(rng.normal(size=3) * 0.4)
+    t = rng.normal(size=3) * 0.5
+    pc = np.stack([rng.uniform(-2, 2, n), rng.uniform(-1.5, 1.5, n), rng.uniform(1.0, 8.0, n)], 1)
+    P = (pc - t) @ R  # world = R^T (pc - t)
+    uv = np.stack([K[0] * pc[:, 0] / pc[:, 2] + K[2], K[1] * pc[:, 1] / pc[:, 2] + K[3]], 1)
+    uv = uv + rng.normal(size=uv.shape) * noise
+    out = np.zeros(n, bool)
+    n_out = int(round(outlier_frac * n))
+    if n_out:
+        idx = rng.choice(n, n_out, replace=False)
+        out[idx] = True
+        uv[idx] = np.stack([rng.uniform(0, 640, n_out), rng.uniform(0, 480, n_out)], 1)
+        # keep labelled outliers genuinely outside the 8 px gate
+        d = np.hypot(*(uv[idx] - np.stack([K[0] * pc[idx, 0] / pc[idx, 2] + K[2],
+                                           K[1] * pc[idx, 1] / pc[idx, 2] + K[3]], 1)).T)
+        uv[idx[d < 20]] += 40.0
+    return P.astype(np.float32), uv.astype(np.float32), R, t, out
+
+
+def rot_angle(Ra, Rb):
+    c = (np.trace(Ra.T @ Rb) - 1) / 2
+    return math.acos(max(-1.0, min(1.0, c)))
+
+
+# ------------------------------------------------------------------------------------ EPnP
+@pytest.mark.parametrize("n,seed", [(4, 0), (5, 1), (6, 2), (20, 3), (400, 4)])
+def test_epnp_known_answer(oracle, n, seed):
+    # exact double inputs (no float rounding) so the solution must be exact to rounding
+    rng = np.random.default_rng(seed)
+    Rt = restate.rodrigues(rng.normal(size=3) * 0.4)
+    tt = rng.normal(size=3) * 0.5
+    pc = np.stack([rng.uniform(-2, 2, n), rng.uniform(-1.5, 1.5, n), rng.uniform(1.0, 8.0, n)], 1)
+    X = (pc - tt) @ Rt
+    img = np.stack([K[0] * pc[:, 0] / pc[:, 2] + K[2], K[1] * pc[:, 1] / pc[:, 2] + K[3]], 1)
+    ok, Re, te = oracle.epnp(X, img)
+    assert ok
+    # n = 4 leaves a 4-dimensional null space that 5 Gauss-Newton steps only approximate
+    # (OpenCV switches to P3P there); n >= 5 is exact to rounding
+    tol = 1e-3 if n == 4 else 1e-6
+    assert rot_angle(Re, Rt) < tol and np.max(np.abs(te - tt)) < tol
+    assert abs(np.linalg.det(Re) - 1) < 1e-9
+
+
+# --------------------------------------------------------------------------- cv::RNG replay
+def cv_rng(state=(1 << 64) - 1):
+    while True:
+        state = ((state & 0xFFFFFFFF) * 4164903690 + (state >> 32)) & ((1 << 64) - 1)
+        yield state & 0xFFFFFFFF
+
+
+def ransac_update_num_iters(p, ep, model_points, max_iters):
+    p, ep = min(max(p, 0.0), 1.0), min(max(ep, 0.0), 1.0)
+    num = max(1.0 - p, 2.2250738585072014e-308)
+    denom = 1.0 - (1.0 - ep) ** model_points
+    if denom < 2.2250738585072014e-308:
+        return 0
+    num, denom = math.log(num), math.log(denom)
+    if denom >= 0 or -num >= max_iters * (-denom):
+        return max_iters
+    return int(np.rint(num / denom))
+
+
+def reproj_err2(R, t, obj, img):
+    """PnPRansacCallback::computeError: projection in double, float output, float error."""
+    pc = obj.astype(np.float64) @ R.T + t
+    proj = np.stack([K[0] * (pc[:, 0] / pc[:, 2]) + K[2], K[1] * (pc[:, 1] / pc[:, 2]) + K[3]], 1).astype(np.float32)
+    d = img - proj
+    return (d[:, 0] * d[:, 0] + d[:, 1] * d[:, 1]).astype(np.float32)
+
+
+def ransac_replay(oracle, obj, img, iters, thr=8.0, conf=0.99):
+    n = len(obj)
+    g = cv_rng()
+    niters, best, best_iter, best_model = max(iters, 1), 0, -1, None
+    thr2 = np.float32(thr * thr)
+    it = 0
+    while it < niters:
+        idx = []
+        while len(idx) < 5:
+            v = next(g) % n
+            if v not in idx:
+                idx.append(v)
+        ok, R, t = oracle.epnp(obj[idx].astype(np.float64), img[idx].astype(np.float64))
+        if ok:
+            R = oracle.rodrigues(oracle.rodrigues(R))  # the model is stored as (rvec, tvec)
+            cnt = int((reproj_err2(R, t, obj, img) <= thr2).sum())
+            if cnt > max(best, 4):
+                best, best_iter, best_model = cnt, it, (R, t)
+                niters = ransac_update_num_iters(conf, (n - cnt) / n, 5, niters)
+        it += 1
+    mask = reproj_err2(*best_model, obj, img) <= thr2 if best_model else np.zeros(n, bool)
+    return it, best_iter, best, mask
+
+
+@pytest.mark.parametrize("n,seed,out,iters", [(30, 0, 0.3, 100), (200, 1, 0.5, 300), (60, 2, 0.5, 300), (40, 6, 0.7, 50),
+                                               (500, 3, 0.1, 100)])
+def test_pnp_ransac_matches_python_replay(oracle, n, seed, out, iters):
+    obj, img, R, t, outl = pnp_problem(n, seed, noise=0.5, outlier_frac=out)
+    ok, rv, tv, inl, mask, diag = oracle.pnp_ransac(obj, img, iters)
+    it, best_iter, best, mask_py = ransac_replay(oracle, obj, img, iters)
+    assert ok == (best > 0) and diag[0] == it and diag[1] == best_iter
+    if ok:
+        assert inl == best and np.array_equal(mask, mask_py)
+
+
+def test_rng_and_update_rule_values():
+    g = cv_rng()
+    first = [next(g) for _ in range(3)]
+    # state0 = 2^64-1: (2^32-1) * 4164903690 + (2^32-1)
+    s1 = ((0xFFFFFFFF * 4164903690 + 0xFFFFFFFF) & ((1 << 64) - 1))
+    assert first[0] == s1 & 0xFFFFFFFF
+    assert ransac_update_num_iters(0.99, 0.3, 5, 100) == 25  # log(0.01) / log(1 - 0.7^5) = 25.03
+    assert ransac_update_num_iters(0.99, 0.5, 5, 100) == 100  # 145 > the current budget
+    assert ransac_update_num_iters(0.99, 0.0, 5, 100) == 0 or ransac_update_num_iters(0.99, 0.0, 5, 100) == 1
+    assert ransac_update_num_iters(0.99, 0.99, 5, 100) == 100
+
+
+# --------------------------------------------------------------------------- solve_pnp
+@pytest.mark.parametrize("n,seed,out", [(50, 0, 0.0), (120, 1, 0.3), (300, 2, 0.5)])
+def test_solve_pnp_known_answer(oracle, n, seed, out):
+    obj, img, R, t, outl = pnp_problem(n, seed, outlier_frac=out)
+    ok, rv, tv, inl, mask, diag = oracle.pnp_ransac(obj, img, 300)
+    assert ok and np.array_equal(mask, ~outl) and inl == (~outl).sum()
+    success, Rw, tw, cnt = oracle.solve_pnp(obj, img, 300, 15)
+    assert success and cnt == inl
+    # world pose = inverse of the camera pose (Slam.cpp:524-525); float inputs -> ~1e-6
+    assert rot_angle(Rw, R.T) < 2e-6 and np.max(np.abs(tw - (-R.T @ t))) < 2e-5
+    assert diag[2] >= 1
+
+
+def test_solve_pnp_noise_refinement(oracle):
+    obj, img, R, t, outl = pnp_problem(400, 5, noise=1.0, outlier_frac=0.2)
+    ok, rv, tv, inl, mask, diag = oracle.pnp_ransac(obj, img, 100)
+    assert ok and diag[3] >= 1  # LM accepted at least one step
+    Rc = oracle.rodrigues(rv)
+    e = reproj_err2(Rc, tv, obj, img)[mask]
+    assert np.sqrt(e.mean()) < 1.6  # ~ sqrt(2) px for unit noise per axis
+    assert rot_angle(Rc, R) < 5e-3
+    assert not mask[outl].any()
+
+
+def test_solve_pnp_failures(oracle):
+    obj, img, R, t, _ = pnp_problem(9, 0)
+    assert oracle.solve_pnp(obj, img, 100, 10)[0] is False  # fewer points than min_inliers (:512)
+    rng = np.random.default_rng(0)
+    img_rand = np.stack([rng.uniform(0, 640, 40), rng.uniform(0, 480, 40)], 1).astype(np.float32)
+    obj2, _, _, _, _ = pnp_problem(40, 1)
+    s, _, _, cnt = oracle.solve_pnp(obj2, img_rand, 100, 15)
+    assert not s and cnt == 0
+    # n == 5: a single EPnP on all points, every point an inlier (OpenCV model_points == npoints)
+    obj5, img5, R5, t5, _ = pnp_problem(5, 3)
+    ok, rv, tv, inl, mask, diag = oracle.pnp_ransac(obj5, img5, 100)
+    assert ok and inl == 5 and mask.all() and diag[0] == 0

@@ -13,6 +13,7 @@
 
 #include <cfloat>
 
+#include "block_reduce.h"
 #include "vs_internal.h"
 
 namespace vs {
@@ -86,26 +87,6 @@ __device__ void project_dev(const CamPose& p, const double* pw, const double K[4
     }
     u = K[0] * pc[0] / z + K[2];
     v = K[1] * pc[1] / z + K[3];
-}
-
-// Deterministic block sum of N doubles per lane (256 lanes): shuffle tree, then the 4 waves.
-template <int N>
-__device__ void block_sum(double (&v)[N], double* s_red /*[4][N]*/, double (&out)[N]) {
-    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-#pragma unroll
-    for (int k = 0; k < N; k++) {
-        double x = v[k];
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o);
-        v[k] = x;
-    }
-    if (lane == 0)
-#pragma unroll
-        for (int k = 0; k < N; k++) s_red[wv * N + k] = v[k];
-    __syncthreads();
-#pragma unroll
-    for (int k = 0; k < N; k++) out[k] = ((s_red[k] + s_red[N + k]) + s_red[2 * N + k]) + s_red[3 * N + k];
-    __syncthreads();
 }
 
 __device__ int cholesky6(double* A, double* b) {

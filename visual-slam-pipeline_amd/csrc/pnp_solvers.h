@@ -1,0 +1,644 @@
+// pnp_solvers.h — host/device numerical kernels behind Slam::solve_pnp (reference
+// src/Slam.cpp:505-529 -> cv::solvePnPRansac, SOLVEPNP_ITERATIVE, useExtrinsicGuess = false).
+//
+// OpenCV 4.x semantics restated from its published algorithm (external, unpinned):
+//   * RANSAC registrator: cv::RNG((uint64)-1), 5-point subsets drawn with rejection of repeats,
+//     EPnP hypotheses, inlier iff the float squared reprojection error <= (float)(thr^2),
+//     a model replaces the best when its count exceeds max(best, modelPoints-1), iteration budget
+//     shrunk by RANSACUpdateNumIters(confidence, outlier ratio, 5, niters);
+//   * EPnP (Lepetit, Moreno-Noguer, Fua 2009): four control points from the PCA of the object
+//     points, barycentric coordinates, the 12x12 M^T M null space, the N = 4 / 2 / 3 beta
+//     approximations refined by 5 Gauss-Newton steps, the lowest reprojection error wins;
+//   * final refinement on the RANSAC inliers: Levenberg-Marquardt over (rvec, tvec) from the
+//     RANSAC model, Marquardt-scaled diagonal, lambda 1e-3 (/10 on success, x10 on failure),
+//     at most 20 iterations.
+// Everything is fp64 and written once for host (oracle/, the CPU restatement) and device
+// (pnp.hip) with identical operation order; the solver's correctness is pinned by known-answer
+// tests (tests/test_oracle_pnp.py), not by the oracle.
+#pragma once
+
+#include <float.h>
+#include <math.h>
+#include <stdint.h>
+
+#if defined(__HIPCC__)
+#define VS_HD __host__ __device__
+#else
+#define VS_HD
+#endif
+
+namespace vs_pnp {
+
+// ---------------------------------------------------------------------------- cv::RNG
+struct CvRng {
+    uint64_t state;
+    VS_HD explicit CvRng(uint64_t s) : state(s ? s : (uint64_t)-1) {}
+    VS_HD unsigned next() {
+        state = (uint64_t)(unsigned)state * 4164903690u + (unsigned)(state >> 32);
+        return (unsigned)state;
+    }
+    VS_HD int uniform(int a, int b) { return a == b ? a : (int)(next() % (unsigned)(b - a)) + a; }
+};
+
+// cv::RANSACUpdateNumIters
+VS_HD inline int ransac_update_num_iters(double p, double ep, int model_points, int max_iters) {
+    p = p > 0. ? p : 0.;
+    p = p < 1. ? p : 1.;
+    ep = ep > 0. ? ep : 0.;
+    ep = ep < 1. ? ep : 1.;
+    double num = (1. - p) > DBL_MIN ? (1. - p) : DBL_MIN;
+    double denom = 1. - pow(1. - ep, model_points);
+    if (denom < DBL_MIN) return 0;
+    num = log(num);
+    denom = log(denom);
+    if (denom >= 0 || -num >= max_iters * (-denom)) return max_iters;
+    return (int)lrint(num / denom);  // cvRound
+}
+
+// ------------------------------------------------------------- small dense linear algebra
+// Cyclic Jacobi eigen-decomposition of the symmetric n x n matrix A (row-major, destroyed):
+// w[k] eigenvalues in descending order, V[i*n + k] the k-th eigenvector (columns).
+template <int N>
+VS_HD void sym_eig(double* A, double* w, double* V) {
+    for (int i = 0; i < N; i++)
+        for (int j = 0; j < N; j++) V[i * N + j] = (i == j) ? 1.0 : 0.0;
+    double total = 0;
+    for (int i = 0; i < N * N; i++) total += A[i] * A[i];
+    for (int sweep = 0; sweep < 30; sweep++) {
+        double off = 0;
+        for (int p = 0; p < N; p++)
+            for (int q = p + 1; q < N; q++) off += A[p * N + q] * A[p * N + q];
+        if (!(off > 1e-32 * total)) break;
+        for (int p = 0; p < N - 1; p++)
+            for (int q = p + 1; q < N; q++) {
+                const double apq = A[p * N + q];
+                if (fabs(apq) < 1e-300) continue;
+                const double app = A[p * N + p], aqq = A[q * N + q];
+                const double theta = (aqq - app) / (2.0 * apq);
+                const double t = (theta >= 0 ? 1.0 : -1.0) / (fabs(theta) + sqrt(theta * theta + 1.0));
+                const double c = 1.0 / sqrt(t * t + 1.0), s = t * c;
+                for (int k = 0; k < N; k++) {
+                    const double akp = A[k * N + p], akq = A[k * N + q];
+                    A[k * N + p] = c * akp - s * akq;
+                    A[k * N + q] = s * akp + c * akq;
+                }
+                for (int k = 0; k < N; k++) {
+                    const double apk = A[p * N + k], aqk = A[q * N + k];
+                    A[p * N + k] = c * apk - s * aqk;
+                    A[q * N + k] = s * apk + c * aqk;
+                }
+                for (int k = 0; k < N; k++) {
+                    const double vkp = V[k * N + p], vkq = V[k * N + q];
+                    V[k * N + p] = c * vkp - s * vkq;
+                    V[k * N + q] = s * vkp + c * vkq;
+                }
+            }
+    }
+    for (int i = 0; i < N; i++) w[i] = A[i * N + i];
+    for (int i = 0; i < N - 1; i++) {  // selection sort, descending
+        int m = i;
+        for (int j = i + 1; j < N; j++)
+            if (w[j] > w[m]) m = j;
+        if (m != i) {
+            const double tw = w[i];
+            w[i] = w[m];
+            w[m] = tw;
+            for (int k = 0; k < N; k++) {
+                const double tv = V[k * N + i];
+                V[k * N + i] = V[k * N + m];
+                V[k * N + m] = tv;
+            }
+        }
+    }
+}
+
+// Least squares min ||A x - b|| for an M x N (M >= N) matrix by Householder QR (A, b destroyed).
+template <int M, int N>
+VS_HD void lstsq(double* A, double* b, double* x) {
+    for (int k = 0; k < N; k++) {
+        double nrm = 0;
+        for (int i = k; i < M; i++) nrm += A[i * N + k] * A[i * N + k];
+        nrm = sqrt(nrm);
+        if (nrm == 0) continue;
+        const double alpha = A[k * N + k] > 0 ? -nrm : nrm;
+        double v[M];
+        for (int i = 0; i < M; i++) v[i] = (i < k) ? 0.0 : A[i * N + k];
+        v[k] -= alpha;
+        double vv = 0;
+        for (int i = k; i < M; i++) vv += v[i] * v[i];
+        if (vv == 0) continue;
+        for (int j = k; j < N; j++) {
+            double d = 0;
+            for (int i = k; i < M; i++) d += v[i] * A[i * N + j];
+            const double f = 2.0 * d / vv;
+            for (int i = k; i < M; i++) A[i * N + j] -= f * v[i];
+        }
+        double d = 0;
+        for (int i = k; i < M; i++) d += v[i] * b[i];
+        const double f = 2.0 * d / vv;
+        for (int i = k; i < M; i++) b[i] -= f * v[i];
+    }
+    for (int k = N - 1; k >= 0; k--) {
+        double s = b[k];
+        for (int j = k + 1; j < N; j++) s -= A[k * N + j] * x[j];
+        x[k] = (A[k * N + k] != 0) ? s / A[k * N + k] : 0.0;
+    }
+}
+
+VS_HD inline double det3(const double* M) {
+    return M[0] * (M[4] * M[8] - M[5] * M[7]) - M[1] * (M[3] * M[8] - M[5] * M[6]) + M[2] * (M[3] * M[7] - M[4] * M[6]);
+}
+
+// R = argmin ||R A + t - B|| (Kabsch with reflection fix) from ABt = sum (b - cb)(a - ca)^T:
+// SVD: V from the symmetric eigen-decomposition of ABt^T ABt, u0 and u1 from ABt v0 and ABt v1
+// (Gram-Schmidt), u2 = u0 x u1.  With that u2, R = u0 v0^T + u1 v1^T + det(V) u2 v2^T is exactly
+// U diag(1, 1, det(U V^T)) V^T, and it never divides by the smallest singular value.
+VS_HD inline void rotation_from_cross(const double* ABt, double* R) {
+    double AtA[9];
+    for (int i = 0; i < 3; i++)
+        for (int j = 0; j < 3; j++) {
+            double s = 0;
+            for (int k = 0; k < 3; k++) s += ABt[k * 3 + i] * ABt[k * 3 + j];
+            AtA[i * 3 + j] = s;
+        }
+    double w[3], V[9];
+    sym_eig<3>(AtA, w, V);
+    double u[3][3];
+    for (int k = 0; k < 2; k++)
+        for (int i = 0; i < 3; i++)
+            u[k][i] = ABt[i * 3 + 0] * V[0 * 3 + k] + ABt[i * 3 + 1] * V[1 * 3 + k] + ABt[i * 3 + 2] * V[2 * 3 + k];
+    double n0 = sqrt(u[0][0] * u[0][0] + u[0][1] * u[0][1] + u[0][2] * u[0][2]);
+    n0 = n0 > 0 ? n0 : 1.0;
+    for (int i = 0; i < 3; i++) u[0][i] /= n0;
+    const double pr = u[0][0] * u[1][0] + u[0][1] * u[1][1] + u[0][2] * u[1][2];
+    for (int i = 0; i < 3; i++) u[1][i] -= pr * u[0][i];
+    double n1 = sqrt(u[1][0] * u[1][0] + u[1][1] * u[1][1] + u[1][2] * u[1][2]);
+    n1 = n1 > 0 ? n1 : 1.0;
+    for (int i = 0; i < 3; i++) u[1][i] /= n1;
+    u[2][0] = u[0][1] * u[1][2] - u[0][2] * u[1][1];
+    u[2][1] = u[0][2] * u[1][0] - u[0][0] * u[1][2];
+    u[2][2] = u[0][0] * u[1][1] - u[0][1] * u[1][0];
+    const double d = det3(V) < 0 ? -1.0 : 1.0;
+    for (int i = 0; i < 3; i++)
+        for (int j = 0; j < 3; j++)
+            R[i * 3 + j] = u[0][i] * V[j * 3 + 0] + u[1][i] * V[j * 3 + 1] + d * u[2][i] * V[j * 3 + 2];
+}
+
+// ----------------------------------------------------------------------------- Rodrigues
+VS_HD inline void rod_v2m(const double r[3], double R[9]) {
+    const double theta = sqrt(r[0] * r[0] + r[1] * r[1] + r[2] * r[2]);
+    if (theta < DBL_EPSILON) {
+        for (int i = 0; i < 9; i++) R[i] = (i % 4 == 0) ? 1.0 : 0.0;
+        return;
+    }
+    const double c = cos(theta), s = sin(theta), c1 = 1.0 - c;
+    const double it = 1.0 / theta;
+    const double x = r[0] * it, y = r[1] * it, z = r[2] * it;
+    const double rrt[9] = {x * x, x * y, x * z, x * y, y * y, y * z, x * z, y * z, z * z};
+    const double rx[9] = {0, -z, y, z, 0, -x, -y, x, 0};
+    for (int i = 0; i < 9; i++) R[i] = c * ((i % 4 == 0) ? 1.0 : 0.0) + c1 * rrt[i] + s * rx[i];
+}
+
+VS_HD inline void rod_m2v(const double R[9], double r[3]) {
+    double rx = R[7] - R[5], ry = R[2] - R[6], rz = R[3] - R[1];
+    const double s = sqrt((rx * rx + ry * ry + rz * rz) * 0.25);
+    double c = (R[0] + R[4] + R[8] - 1) * 0.5;
+    c = c > 1. ? 1. : c < -1. ? -1. : c;
+    double theta = acos(c);
+    if (s < 1e-5) {
+        if (c > 0) {
+            r[0] = r[1] = r[2] = 0;
+            return;
+        }
+        double t = (R[0] + 1) * 0.5;
+        rx = sqrt(fmax(t, 0.));
+        t = (R[4] + 1) * 0.5;
+        ry = sqrt(fmax(t, 0.)) * (R[1] < 0 ? -1. : 1.);
+        t = (R[8] + 1) * 0.5;
+        rz = sqrt(fmax(t, 0.)) * (R[2] < 0 ? -1. : 1.);
+        if (fabs(rx) < fabs(ry) && fabs(rx) < fabs(rz) && (R[5] > 0) != (ry * rz > 0)) rz = -rz;
+        theta /= sqrt(rx * rx + ry * ry + rz * rz);
+        r[0] = rx * theta;
+        r[1] = ry * theta;
+        r[2] = rz * theta;
+        return;
+    }
+    double vth = 1 / (2 * s);
+    vth *= theta;
+    r[0] = rx * vth;
+    r[1] = ry * vth;
+    r[2] = rz * vth;
+}
+
+// projection (world -> camera R, t; cv::projectPoints without distortion, double then float)
+struct Cam {
+    double fx, fy, cx, cy;
+};
+
+VS_HD inline void project(const double* R, const double* t, const Cam& K, double X, double Y, double Z, double& u,
+                          double& v) {
+    const double x = R[0] * X + R[1] * Y + R[2] * Z + t[0];
+    const double y = R[3] * X + R[4] * Y + R[5] * Z + t[1];
+    const double z = R[6] * X + R[7] * Y + R[8] * Z + t[2];
+    const double iz = z ? 1.0 / z : 1.0;
+    u = K.fx * (x * iz) + K.cx;
+    v = K.fy * (y * iz) + K.cy;
+}
+
+// float squared reprojection error (PnPRansacCallback::computeError)
+VS_HD inline float reproj_err2(const double* R, const double* t, const Cam& K, float X, float Y, float Z, float u,
+                               float v) {
+    double pu, pv;
+    project(R, t, K, X, Y, Z, pu, pv);
+    const float du = u - (float)pu, dv = v - (float)pv;
+    return du * du + dv * dv;
+}
+
+// ----------------------------------------------------------------------------------- EPnP
+// n >= 4 correspondences (object points X[3i..], image points u[2i..]).  Returns R (world ->
+// camera) and t; false if degenerate.
+template <int MAXN>
+VS_HD bool epnp(const double* X, const double* uv, int n, const Cam& K, double* Rout, double* tout) {
+    if (n < 4 || n > MAXN) return false;
+    // control points
+    double cw[4][3];
+    for (int j = 0; j < 3; j++) {
+        double s = 0;
+        for (int i = 0; i < n; i++) s += X[3 * i + j];
+        cw[0][j] = s / n;
+    }
+    double C[9];
+    for (int a = 0; a < 3; a++)
+        for (int b = 0; b < 3; b++) {
+            double s = 0;
+            for (int i = 0; i < n; i++) s += (X[3 * i + a] - cw[0][a]) * (X[3 * i + b] - cw[0][b]);
+            C[a * 3 + b] = s;
+        }
+    double dc[3], uc[9];
+    sym_eig<3>(C, dc, uc);
+    for (int i = 1; i < 4; i++) {
+        const double k = sqrt((dc[i - 1] > 0 ? dc[i - 1] : 0.0) / n);
+        for (int j = 0; j < 3; j++) cw[i][j] = cw[0][j] + k * uc[j * 3 + (i - 1)];
+    }
+    // barycentric coordinates: CC a = p - cw0 with CC columns cw_i - cw0
+    double CC[9];
+    for (int r = 0; r < 3; r++)
+        for (int c = 0; c < 3; c++) CC[r * 3 + c] = cw[c + 1][r] - cw[0][r];
+    const double det = det3(CC);
+    if (fabs(det) < 1e-300) return false;
+    double CI[9];
+    CI[0] = (CC[4] * CC[8] - CC[5] * CC[7]) / det;
+    CI[1] = (CC[2] * CC[7] - CC[1] * CC[8]) / det;
+    CI[2] = (CC[1] * CC[5] - CC[2] * CC[4]) / det;
+    CI[3] = (CC[5] * CC[6] - CC[3] * CC[8]) / det;
+    CI[4] = (CC[0] * CC[8] - CC[2] * CC[6]) / det;
+    CI[5] = (CC[2] * CC[3] - CC[0] * CC[5]) / det;
+    CI[6] = (CC[3] * CC[7] - CC[4] * CC[6]) / det;
+    CI[7] = (CC[1] * CC[6] - CC[0] * CC[7]) / det;
+    CI[8] = (CC[0] * CC[4] - CC[1] * CC[3]) / det;
+    double alphas[MAXN][4];
+    for (int i = 0; i < n; i++) {
+        const double p[3] = {X[3 * i] - cw[0][0], X[3 * i + 1] - cw[0][1], X[3 * i + 2] - cw[0][2]};
+        double a1 = CI[0] * p[0] + CI[1] * p[1] + CI[2] * p[2];
+        double a2 = CI[3] * p[0] + CI[4] * p[1] + CI[5] * p[2];
+        double a3 = CI[6] * p[0] + CI[7] * p[1] + CI[8] * p[2];
+        alphas[i][1] = a1;
+        alphas[i][2] = a2;
+        alphas[i][3] = a3;
+        alphas[i][0] = 1.0 - a1 - a2 - a3;
+    }
+    // M^T M accumulated row pair by row pair
+    double MtM[144];
+    for (int i = 0; i < 144; i++) MtM[i] = 0;
+    for (int i = 0; i < n; i++) {
+        double r0[12], r1[12];
+        for (int j = 0; j < 4; j++) {
+            const double a = alphas[i][j];
+            r0[3 * j] = a * K.fx;
+            r0[3 * j + 1] = 0.0;
+            r0[3 * j + 2] = a * (K.cx - uv[2 * i]);
+            r1[3 * j] = 0.0;
+            r1[3 * j + 1] = a * K.fy;
+            r1[3 * j + 2] = a * (K.cy - uv[2 * i + 1]);
+        }
+        for (int a = 0; a < 12; a++)
+            for (int b = 0; b < 12; b++) MtM[a * 12 + b] += r0[a] * r0[b] + r1[a] * r1[b];
+    }
+    double dm[12], um[144];
+    sym_eig<12>(MtM, dm, um);
+    // v[k] = eigenvector of the k-th smallest eigenvalue
+    double v[4][12];
+    for (int k = 0; k < 4; k++)
+        for (int i = 0; i < 12; i++) v[k][i] = um[i * 12 + (11 - k)];
+    // L_6x10 and rho
+    const int pa[6] = {0, 0, 0, 1, 1, 2}, pb[6] = {1, 2, 3, 2, 3, 3};
+    double L[6][10], rho[6];
+    for (int j = 0; j < 6; j++) {
+        double dv[4][3];
+        for (int k = 0; k < 4; k++)
+            for (int c = 0; c < 3; c++) dv[k][c] = v[k][3 * pa[j] + c] - v[k][3 * pb[j] + c];
+        auto dot = [&](int a, int b) { return dv[a][0] * dv[b][0] + dv[a][1] * dv[b][1] + dv[a][2] * dv[b][2]; };
+        L[j][0] = dot(0, 0);
+        L[j][1] = 2.0 * dot(0, 1);
+        L[j][2] = dot(1, 1);
+        L[j][3] = 2.0 * dot(0, 2);
+        L[j][4] = 2.0 * dot(1, 2);
+        L[j][5] = dot(2, 2);
+        L[j][6] = 2.0 * dot(0, 3);
+        L[j][7] = 2.0 * dot(1, 3);
+        L[j][8] = 2.0 * dot(2, 3);
+        L[j][9] = dot(3, 3);
+        const double dx = cw[pa[j]][0] - cw[pb[j]][0], dy = cw[pa[j]][1] - cw[pb[j]][1], dz = cw[pa[j]][2] - cw[pb[j]][2];
+        rho[j] = dx * dx + dy * dy + dz * dz;
+    }
+    double betas[3][4];
+    {  // N = 4: B11 B12 B13 B14
+        double A[24], b[6], x[4];
+        for (int j = 0; j < 6; j++) {
+            A[j * 4 + 0] = L[j][0];
+            A[j * 4 + 1] = L[j][1];
+            A[j * 4 + 2] = L[j][3];
+            A[j * 4 + 3] = L[j][6];
+            b[j] = rho[j];
+        }
+        lstsq<6, 4>(A, b, x);
+        if (x[0] < 0) {
+            const double b0 = sqrt(-x[0]);
+            betas[0][0] = b0;
+            betas[0][1] = b0 ? -x[1] / b0 : 0.0;
+            betas[0][2] = b0 ? -x[2] / b0 : 0.0;
+            betas[0][3] = b0 ? -x[3] / b0 : 0.0;
+        } else {
+            const double b0 = sqrt(x[0]);
+            betas[0][0] = b0;
+            betas[0][1] = b0 ? x[1] / b0 : 0.0;
+            betas[0][2] = b0 ? x[2] / b0 : 0.0;
+            betas[0][3] = b0 ? x[3] / b0 : 0.0;
+        }
+    }
+    {  // N = 2: B11 B12 B22
+        double A[18], b[6], x[3];
+        for (int j = 0; j < 6; j++) {
+            A[j * 3 + 0] = L[j][0];
+            A[j * 3 + 1] = L[j][1];
+            A[j * 3 + 2] = L[j][2];
+            b[j] = rho[j];
+        }
+        lstsq<6, 3>(A, b, x);
+        double b0, b1;
+        if (x[0] < 0) {
+            b0 = sqrt(-x[0]);
+            b1 = (x[2] < 0) ? sqrt(-x[2]) : 0.0;
+        } else {
+            b0 = sqrt(x[0]);
+            b1 = (x[2] > 0) ? sqrt(x[2]) : 0.0;
+        }
+        if (x[1] < 0) b0 = -b0;
+        betas[1][0] = b0;
+        betas[1][1] = b1;
+        betas[1][2] = 0.0;
+        betas[1][3] = 0.0;
+    }
+    {  // N = 3: B11 B12 B22 B13 B23
+        double A[30], b[6], x[5];
+        for (int j = 0; j < 6; j++) {
+            for (int c = 0; c < 5; c++) A[j * 5 + c] = L[j][c];
+            b[j] = rho[j];
+        }
+        lstsq<6, 5>(A, b, x);
+        double b0, b1;
+        if (x[0] < 0) {
+            b0 = sqrt(-x[0]);
+            b1 = (x[2] < 0) ? sqrt(-x[2]) : 0.0;
+        } else {
+            b0 = sqrt(x[0]);
+            b1 = (x[2] > 0) ? sqrt(x[2]) : 0.0;
+        }
+        if (x[1] < 0) b0 = -b0;
+        betas[2][0] = b0;
+        betas[2][1] = b1;
+        betas[2][2] = b0 ? x[3] / b0 : 0.0;
+        betas[2][3] = 0.0;
+    }
+    double best_err = 0;
+    bool have = false;
+    for (int s = 0; s < 3; s++) {
+        double* be = betas[s];
+        for (int it = 0; it < 5; it++) {  // Gauss-Newton on the 6 distance constraints
+            double A[24], b[6], x[4];
+            for (int j = 0; j < 6; j++) {
+                const double* l = L[j];
+                A[j * 4 + 0] = 2 * l[0] * be[0] + l[1] * be[1] + l[3] * be[2] + l[6] * be[3];
+                A[j * 4 + 1] = l[1] * be[0] + 2 * l[2] * be[1] + l[4] * be[2] + l[7] * be[3];
+                A[j * 4 + 2] = l[3] * be[0] + l[4] * be[1] + 2 * l[5] * be[2] + l[8] * be[3];
+                A[j * 4 + 3] = l[6] * be[0] + l[7] * be[1] + l[8] * be[2] + 2 * l[9] * be[3];
+                b[j] = rho[j] - (l[0] * be[0] * be[0] + l[1] * be[0] * be[1] + l[2] * be[1] * be[1] +
+                                 l[3] * be[0] * be[2] + l[4] * be[1] * be[2] + l[5] * be[2] * be[2] +
+                                 l[6] * be[0] * be[3] + l[7] * be[1] * be[3] + l[8] * be[2] * be[3] +
+                                 l[9] * be[3] * be[3]);
+            }
+            lstsq<6, 4>(A, b, x);
+            for (int k = 0; k < 4; k++) be[k] += x[k];
+        }
+        // camera coordinates of control and object points
+        double ccs[4][3];
+        for (int i = 0; i < 4; i++)
+            for (int c = 0; c < 3; c++)
+                ccs[i][c] = be[0] * v[0][3 * i + c] + be[1] * v[1][3 * i + c] + be[2] * v[2][3 * i + c] +
+                            be[3] * v[3][3 * i + c];
+        double pcs0z = alphas[0][0] * ccs[0][2] + alphas[0][1] * ccs[1][2] + alphas[0][2] * ccs[2][2] +
+                       alphas[0][3] * ccs[3][2];
+        const double sgn = pcs0z < 0 ? -1.0 : 1.0;
+        double pc0[3] = {0, 0, 0}, pw0[3] = {0, 0, 0};
+        for (int i = 0; i < n; i++)
+            for (int c = 0; c < 3; c++) {
+                pc0[c] += sgn * (alphas[i][0] * ccs[0][c] + alphas[i][1] * ccs[1][c] + alphas[i][2] * ccs[2][c] +
+                                 alphas[i][3] * ccs[3][c]);
+                pw0[c] += X[3 * i + c];
+            }
+        for (int c = 0; c < 3; c++) {
+            pc0[c] /= n;
+            pw0[c] /= n;
+        }
+        double ABt[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+        for (int i = 0; i < n; i++) {
+            double pc[3];
+            for (int c = 0; c < 3; c++)
+                pc[c] = sgn * (alphas[i][0] * ccs[0][c] + alphas[i][1] * ccs[1][c] + alphas[i][2] * ccs[2][c] +
+                               alphas[i][3] * ccs[3][c]) - pc0[c];
+            const double pw[3] = {X[3 * i] - pw0[0], X[3 * i + 1] - pw0[1], X[3 * i + 2] - pw0[2]};
+            for (int a = 0; a < 3; a++)
+                for (int b = 0; b < 3; b++) ABt[a * 3 + b] += pc[a] * pw[b];
+        }
+        double R[9], t[3];
+        rotation_from_cross(ABt, R);
+        for (int c = 0; c < 3; c++) t[c] = pc0[c] - (R[c * 3] * pw0[0] + R[c * 3 + 1] * pw0[1] + R[c * 3 + 2] * pw0[2]);
+        double err = 0;
+        for (int i = 0; i < n; i++) {
+            double u, vv;
+            project(R, t, K, X[3 * i], X[3 * i + 1], X[3 * i + 2], u, vv);
+            const double du = uv[2 * i] - u, dvv = uv[2 * i + 1] - vv;
+            err += sqrt(du * du + dvv * dvv);
+        }
+        err /= n;
+        if (!have || err < best_err) {
+            have = true;
+            best_err = err;
+            for (int k = 0; k < 9; k++) Rout[k] = R[k];
+            for (int k = 0; k < 3; k++) tout[k] = t[k];
+        }
+    }
+    return have;
+}
+
+// ------------------------------------------------------------ Levenberg-Marquardt refinement
+// Parameters p = (rvec, tvec), world -> camera.  Residuals r_i = project(X_i) - uv_i (double).
+// Rotation columns of J by central differences (step kLmStep) from seven shared rotations,
+// translation columns analytic.
+constexpr double kLmStep = 1e-6;
+constexpr int kLmMaxIters = 20;
+constexpr int kLmTerms = 28;  // 21 upper-triangular J^T J, 6 J^T r, 1 cost
+
+struct LmRots {
+    double R[7][9];  // R(r), R(r + h e0), R(r - h e0), R(r + h e1), ...
+};
+
+VS_HD inline void lm_rotations(const double* p, LmRots& L) {
+    rod_v2m(p, L.R[0]);
+    for (int k = 0; k < 3; k++) {
+        double rp[3] = {p[0], p[1], p[2]}, rm[3] = {p[0], p[1], p[2]};
+        rp[k] += kLmStep;
+        rm[k] -= kLmStep;
+        rod_v2m(rp, L.R[1 + 2 * k]);
+        rod_v2m(rm, L.R[2 + 2 * k]);
+    }
+}
+
+// Adds one correspondence's terms to acc[kLmTerms].
+VS_HD inline void lm_point(const LmRots& L, const double* t, const Cam& K, double X, double Y, double Z, double u,
+                           double v, double* acc) {
+    const double* R = L.R[0];
+    const double x = R[0] * X + R[1] * Y + R[2] * Z + t[0];
+    const double y = R[3] * X + R[4] * Y + R[5] * Z + t[1];
+    const double z = R[6] * X + R[7] * Y + R[8] * Z + t[2];
+    const double iz = z ? 1.0 / z : 1.0;
+    const double pu = K.fx * (x * iz) + K.cx, pv = K.fy * (y * iz) + K.cy;
+    const double ru = pu - u, rv = pv - v;
+    double ju[6], jv[6];
+    for (int k = 0; k < 3; k++) {
+        double up, vp, um, vm;
+        project(L.R[1 + 2 * k], t, K, X, Y, Z, up, vp);
+        project(L.R[2 + 2 * k], t, K, X, Y, Z, um, vm);
+        ju[k] = (up - um) / (2.0 * kLmStep);
+        jv[k] = (vp - vm) / (2.0 * kLmStep);
+    }
+    ju[3] = K.fx * iz;
+    ju[4] = 0.0;
+    ju[5] = -K.fx * x * iz * iz;
+    jv[3] = 0.0;
+    jv[4] = K.fy * iz;
+    jv[5] = -K.fy * y * iz * iz;
+    int k = 0;
+    for (int a = 0; a < 6; a++)
+        for (int c = a; c < 6; c++) acc[k++] += ju[a] * ju[c] + jv[a] * jv[c];
+    for (int a = 0; a < 6; a++) acc[21 + a] += ju[a] * ru + jv[a] * rv;
+    acc[27] += ru * ru + rv * rv;
+}
+
+// Solves (J^T J with its diagonal scaled by 1 + lambda) d = -J^T r by Cholesky; false if not SPD.
+VS_HD inline bool lm_solve(const double* acc, double lambda, double* d) {
+    double A[36];
+    int k = 0;
+    for (int a = 0; a < 6; a++)
+        for (int c = a; c < 6; c++) {
+            A[a * 6 + c] = acc[k];
+            A[c * 6 + a] = acc[k];
+            k++;
+        }
+    for (int a = 0; a < 6; a++) {
+        A[a * 6 + a] *= 1.0 + lambda;
+        d[a] = -acc[21 + a];
+    }
+    for (int j = 0; j < 6; j++) {
+        double s = A[j * 6 + j];
+        for (int q = 0; q < j; q++) s -= A[j * 6 + q] * A[j * 6 + q];
+        if (!(s > 0)) return false;
+        const double r = sqrt(s);
+        A[j * 6 + j] = r;
+        for (int i = j + 1; i < 6; i++) {
+            double w = A[i * 6 + j];
+            for (int q = 0; q < j; q++) w -= A[i * 6 + q] * A[j * 6 + q];
+            A[i * 6 + j] = w / r;
+        }
+    }
+    for (int i = 0; i < 6; i++) {
+        double w = d[i];
+        for (int q = 0; q < i; q++) w -= A[i * 6 + q] * d[q];
+        d[i] = w / A[i * 6 + i];
+    }
+    for (int i = 5; i >= 0; i--) {
+        double w = d[i];
+        for (int q = i + 1; q < 6; q++) w -= A[q * 6 + i] * d[q];
+        d[i] = w / A[i * 6 + i];
+    }
+    return true;
+}
+
+// LM control shared by the sequential (oracle) and workgroup (device) drivers.  The caller
+// evaluates acc at `cand` whenever step() returns 1 and then calls accept_or_reject().
+struct LmState {
+    double p[6], cand[6];
+    double acc[kLmTerms];  // terms at p
+    double lambda;
+    int iters, accepted, done;
+
+    VS_HD void init(const double* p0, const double* acc0) {
+        for (int i = 0; i < 6; i++) p[i] = cand[i] = p0[i];
+        for (int i = 0; i < kLmTerms; i++) acc[i] = acc0[i];
+        lambda = 1e-3;
+        iters = accepted = done = 0;
+    }
+    // 1: evaluate cand; 0: finished
+    VS_HD int step() {
+        while (!done && iters < kLmMaxIters) {
+            iters++;
+            double d[6];
+            if (!lm_solve(acc, lambda, d)) {
+                lambda *= 10;
+                continue;
+            }
+            double dn = 0, pn = 0;
+            for (int i = 0; i < 6; i++) {
+                dn += d[i] * d[i];
+                pn += p[i] * p[i];
+            }
+            if (sqrt(dn) <= DBL_EPSILON * sqrt(pn)) {
+                done = 1;
+                break;
+            }
+            for (int i = 0; i < 6; i++) cand[i] = p[i] + d[i];
+            return 1;
+        }
+        done = 1;
+        return 0;
+    }
+    VS_HD void accept_or_reject(const double* acc_cand) {
+        if (acc_cand[27] < acc[27]) {
+            double dn = 0, pn = 0;
+            for (int i = 0; i < 6; i++) {
+                dn += (cand[i] - p[i]) * (cand[i] - p[i]);
+                pn += cand[i] * cand[i];
+            }
+            for (int i = 0; i < 6; i++) p[i] = cand[i];
+            for (int i = 0; i < kLmTerms; i++) acc[i] = acc_cand[i];
+            lambda = lambda / 10 > 1e-15 ? lambda / 10 : 1e-15;
+            accepted++;
+            if (sqrt(dn) <= FLT_EPSILON * sqrt(pn)) done = 1;
+        } else {
+            lambda *= 10;
+            if (lambda > 1e16) done = 1;
+        }
+    }
+};
+
+}  // namespace vs_pnp

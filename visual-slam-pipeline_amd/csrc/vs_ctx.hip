@@ -582,6 +582,59 @@ int vs_optimize_pose(vs_ctx* ctx, const double* p3d, const float* p2d, int n, co
     return VS_OK;
 }
 
+int vs_solve_pnp_batch_dev(vs_ctx* ctx, int nprob, const float* d_obj, const float* d_img, const int* d_off,
+                           const double K[4], int ransac_iters, int min_inliers, double* d_R, double* d_t,
+                           int* d_stat, uint8_t* d_mask, void* stream) {
+    VS_ARG(ctx && K && d_off && d_R && d_t && d_stat && d_mask, "vs_solve_pnp_batch_dev: null argument");
+    VS_ARG(ransac_iters <= VS_PNP_MAX_ITERS, "vs_solve_pnp_batch_dev: ransac_iters > VS_PNP_MAX_ITERS");
+    VS_HIP(hipSetDevice(ctx->device));
+    return solve_pnp(ctx, nprob, d_obj, d_img, d_off, K, ransac_iters, min_inliers, d_R, d_t, d_stat, d_mask,
+                     pick(ctx, stream));
+}
+
+int vs_solve_pnp(vs_ctx* ctx, const float* obj_pts, const float* img_pts, int n, const double K[4], int ransac_iters,
+                 int min_inliers, double R_world[9], double t_world[3], int* success, int* inlier_count,
+                 uint8_t* inlier_mask, int diag[4]) {
+    VS_ARG(ctx && K && R_world && t_world && success && inlier_count, "vs_solve_pnp: null argument");
+    VS_ARG(n >= 0 && (n == 0 || (obj_pts && img_pts)), "vs_solve_pnp: bad points");
+    VS_ARG(ransac_iters <= VS_PNP_MAX_ITERS, "vs_solve_pnp: ransac_iters > VS_PNP_MAX_ITERS");
+    *success = 0;
+    *inlier_count = 0;
+    if (diag) diag[0] = diag[1] = diag[2] = diag[3] = 0;
+    if (n == 0) return VS_OK;
+    VS_HIP(hipSetDevice(ctx->device));
+    hipStream_t s = ctx->stream;
+    VS_CHECK(upload(ctx->h_aux0, obj_pts, (size_t)n * 3, s));
+    VS_CHECK(upload(ctx->h_aux1, img_pts, (size_t)n * 2, s));
+    VS_CHECK(ctx->h_aux2.ensure(12 * sizeof(double) + 12 * sizeof(int) + (size_t)n));
+    double* dRt = ctx->h_aux2.as<double>();
+    int* dmeta = reinterpret_cast<int*>(dRt + 12);  // off[2], stat[8]
+    uint8_t* dmask = reinterpret_cast<uint8_t*>(dmeta + 12);
+    const int off[2] = {0, n};
+    VS_HIP(hipMemcpyAsync(dmeta, off, sizeof(off), hipMemcpyHostToDevice, s));
+    VS_CHECK(solve_pnp(ctx, 1, ctx->h_aux0.as<float>(), ctx->h_aux1.as<float>(), dmeta, K, ransac_iters, min_inliers,
+                       dRt, dRt + 9, dmeta + 2, dmask, s));
+    double Rt[12];
+    int stat[8];
+    VS_HIP(hipMemcpyAsync(Rt, dRt, sizeof(Rt), hipMemcpyDeviceToHost, s));
+    VS_HIP(hipMemcpyAsync(stat, dmeta + 2, sizeof(stat), hipMemcpyDeviceToHost, s));
+    if (inlier_mask) VS_HIP(hipMemcpyAsync(inlier_mask, dmask, (size_t)n, hipMemcpyDeviceToHost, s));
+    VS_HIP(hipStreamSynchronize(s));
+    *success = stat[0];
+    *inlier_count = stat[0] ? stat[1] : 0;  // PnPResult.inlier_count stays 0 on failure (Slam.cpp:510)
+    if (stat[0]) {
+        std::memcpy(R_world, Rt, 9 * sizeof(double));
+        std::memcpy(t_world, Rt + 9, 3 * sizeof(double));
+    }
+    if (diag) {
+        diag[0] = stat[2];
+        diag[1] = stat[3];
+        diag[2] = stat[4];
+        diag[3] = stat[5];
+    }
+    return VS_OK;
+}
+
 // ---- profiling ----------------------------------------------------------------------------------
 int vs_profile_enable(vs_ctx* ctx, int on) {
     VS_ARG(ctx, "vs_profile_enable: null ctx");

@@ -137,5 +137,9 @@ int track_local_map(vs_ctx* ctx, const double* d_mp_pos, const float* d_mp_desc,
 // Pose LM, nprob problems with point ranges d_off[p]..d_off[p+1]
 int optimize_pose(vs_ctx* ctx, int nprob, const double* d_P, const float* d_p2, const int* d_off, const double K[4],
                   double* d_R, double* d_t, double* d_res, int* d_ok, hipStream_t s);
+// PnP RANSAC + LM, nprob problems with point ranges d_off[p]..d_off[p+1]
+int solve_pnp(vs_ctx* ctx, int nprob, const float* d_obj, const float* d_img, const int* d_off, const double K[4],
+              int ransac_iters, int min_inliers, double* d_R, double* d_t, int* d_stat, uint8_t* d_mask,
+              hipStream_t s);
 
 }  // namespace vs

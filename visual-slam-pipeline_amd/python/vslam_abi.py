@@ -51,6 +51,8 @@ _SIG = {
     "vs_track_local_map_dev": (_I, [_P, _P, _P, _P, _I, _P, _P, _I, _P, _P, _P, _I, _I, _P, _P, _P, _I, _P, _P]),
     "vs_optimize_pose": (_I, [_P, _P, _P, _I, _P, _P, _P, _P, _P]),
     "vs_optimize_pose_batch_dev": (_I, [_P, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
+    "vs_solve_pnp": (_I, [_P, _P, _P, _I, _P, _I, _I, _P, _P, _P, _P, _P, _P]),
+    "vs_solve_pnp_batch_dev": (_I, [_P, _I, _P, _P, _P, _P, _I, _I, _P, _P, _P, _P, _P]),
     "vs_profile_enable": (_I, [_P, _I]),
     "vs_profile_reset": (_I, [_P]),
     "vs_profile_read": (_I, [_P, _I, _P, _P, _P, _P]),
@@ -249,6 +251,28 @@ class Context:
         _check(self.lib.vs_optimize_pose(self.h, _ptr(P), _ptr(p2), P.shape[0], _ptr(Ka), _ptr(R), _ptr(t),
                                          ctypes.byref(eb), ctypes.byref(ea)))
         return R.reshape(3, 3), t, eb.value, ea.value
+
+    # ---- Slam::solve_pnp ----
+    def solve_pnp(self, obj_pts, img_pts, ransac_iters=100, min_inliers=10, K=K_TUM):
+        """Returns (success, R_world, t_world, inlier_count, inlier_mask, diag)."""
+        P = np.ascontiguousarray(obj_pts, np.float32).reshape(-1, 3)
+        p2 = np.ascontiguousarray(img_pts, np.float32).reshape(-1, 2)
+        n = P.shape[0]
+        R = np.zeros(9, np.float64)
+        t = np.zeros(3, np.float64)
+        ok, inl = ctypes.c_int(0), ctypes.c_int(0)
+        mask = np.zeros(max(n, 1), np.uint8)
+        diag = np.zeros(4, np.int32)
+        Ka = _k_array(K)
+        _check(self.lib.vs_solve_pnp(self.h, _ptr(P), _ptr(p2), n, _ptr(Ka), ransac_iters, min_inliers, _ptr(R),
+                                     _ptr(t), ctypes.byref(ok), ctypes.byref(inl), _ptr(mask), _ptr(diag)))
+        return bool(ok.value), R.reshape(3, 3), t, inl.value, mask[:n].astype(bool), diag
+
+    def solve_pnp_batch_dev(self, nprob, d_obj, d_img, d_off, ransac_iters, min_inliers, d_R, d_t, d_stat, d_mask,
+                            K=K_TUM, stream=None):
+        Ka = _k_array(K)
+        _check(self.lib.vs_solve_pnp_batch_dev(self.h, nprob, d_obj, d_img, d_off, _ptr(Ka), ransac_iters,
+                                               min_inliers, d_R, d_t, d_stat, d_mask, stream))
 
     # ---- device-batched entry points (pointers are ints, e.g. torch tensor.data_ptr()) ----
     def extract_batch_dev(self, B, d_imgs, h, w, d_kps, d_desc, d_n, cap, stream=None):
