@@ -195,6 +195,27 @@ int vs_solve_pnp_batch_dev(vs_ctx* ctx, int nprob, const float* d_obj, const flo
                            const int* d_off, const double K[4], int ransac_iters, int min_inliers,
                            double* d_R, double* d_t, int* d_stat, uint8_t* d_mask, void* stream);
 
+/* ---- A8: F-matrix verification (Slam.cpp:880-910, 1174-1187, 1217-1240) -------------------- */
+/* cv::findFundamentalMat(p1, p2, FM_RANSAC, thr, conf, max_iters) on one point set (n <=
+ * VS_FM_MAX_POINTS, interleaved xy fp32).  *ok = F non-empty (F row-major, F(3,3) = 1);
+ * mask (n, nullable) = inliers (all 0 when F is empty); diag (nullable) = {method 0 none /
+ * 1 seven-point / 2 RANSAC (n >= 15) / 3 LMedS (8..14), iterations run, winning iteration,
+ * inliers}. */
+#define VS_FM_MAX_POINTS 2048
+int vs_find_fundamental(vs_ctx* ctx, const float* p1, const float* p2, int n, double thr,
+                        double conf, int max_iters, double F[9], uint8_t* mask, int* ok,
+                        int diag[4]);
+/* Slam.cpp:880-910 for P frame pairs on device: matches d_good [p][cap] (query -> keypoints of
+ * slot d_pairs[2p], train -> slot d_pairs[2p+1], d_kps [slot][cap]) are verified with
+ * findFundamentalMat(FM_RANSAC, 3.0, 0.999); d_kept [p][cap] / d_nkept [p] = the surviving
+ * matches in order (all of them when F is empty); d_F [p][9] (zeros when empty); d_err [p][2] =
+ * {epipolar_error_before_, epipolar_error_after_}; d_diag [p][8] = {method, iterations,
+ * winning iteration, inliers, F ok, n, kept, 0}.  cap <= VS_FM_MAX_POINTS. */
+int vs_fmat_verify_pairs_dev(vs_ctx* ctx, int P, const int* d_pairs, const vs_keypoint* d_kps,
+                             int cap, const vs_match* d_good, const int* d_ngood, double* d_F,
+                             vs_match* d_kept, int* d_nkept, double* d_err, int* d_diag,
+                             void* stream);
+
 /* ---- profiling ----------------------------------------------------------------------- */
 /* When enabled, every stage of the _dev pipelines brackets its launches with hipEvents on the
  * stream it runs on; vs_profile_read returns per-stage accumulated milliseconds and launch

@@ -41,6 +41,9 @@ _SIG = {
     "orc_epnp": (_I, [_P, _P, _I, _P, _P, _P]),
     "orc_pnp_ransac": (_I, [_P, _P, _I, _P, _I, ctypes.c_double, ctypes.c_double, _P, _P, _P, _P, _P]),
     "orc_solve_pnp": (_I, [_P, _P, _I, _P, _I, _I, _P, _P, _P]),
+    "orc_find_fundamental": (_I, [_P, _P, _I, ctypes.c_double, ctypes.c_double, _I, _P, _P, _P]),
+    "orc_epipolar_error": (ctypes.c_double, [_P, _P, _I, _P]),
+    "orc_fmat_verify": (_I, [_P, _P, _P, _I, _P, _P, _P, _P, _P]),
     "orc_mt19937": (None, [ctypes.c_uint32, _I, _P]),
     "orc_expf_array": (None, [_P, _I, _P]),
     "orc_expf_exhaustive_check": (ctypes.c_long, [ctypes.c_float, ctypes.c_float]),
@@ -260,6 +263,39 @@ def solve_pnp(obj, img, ransac_iters=100, min_inliers=10, K=(525.0, 525.0, 319.5
     ok = lib().orc_solve_pnp(_p(P), _p(p2), P.shape[0], _p(np.asarray(K, np.float64)), ransac_iters, min_inliers,
                              _p(R), _p(t), ctypes.byref(inl))
     return bool(ok), R.reshape(3, 3), t, inl.value
+
+
+def find_fundamental(p1, p2, thr=3.0, conf=0.999, max_iters=1000):
+    """cv::findFundamentalMat(FM_RANSAC) restatement: (ok, F, mask, diag)."""
+    a = np.ascontiguousarray(p1, np.float32).reshape(-1, 2)
+    b = np.ascontiguousarray(p2, np.float32).reshape(-1, 2)
+    n = a.shape[0]
+    F = np.zeros(9)
+    mask = np.zeros(max(n, 1), np.uint8)
+    diag = np.zeros(4, np.int32)
+    ok = lib().orc_find_fundamental(_p(a), _p(b), n, thr, conf, max_iters, _p(F), _p(mask), _p(diag))
+    return bool(ok), F.reshape(3, 3), mask[:n].astype(bool), diag
+
+
+def epipolar_error(p1, p2, F):
+    a = np.ascontiguousarray(p1, np.float32).reshape(-1, 2)
+    b = np.ascontiguousarray(p2, np.float32).reshape(-1, 2)
+    return lib().orc_epipolar_error(_p(a), _p(b), a.shape[0], _p(np.ascontiguousarray(F, np.float64)))
+
+
+def fmat_verify(kp_ref, kp_cur, good):
+    """Slam.cpp:880-910: (F or None, kept match indices, [err_before, err_after], diag)."""
+    kr = np.ascontiguousarray(kp_ref, KEYPOINT_DTYPE)
+    kc = np.ascontiguousarray(kp_cur, KEYPOINT_DTYPE)
+    g = np.ascontiguousarray(good, MATCH_DTYPE)
+    n = len(g)
+    F = np.zeros(9)
+    keep = np.zeros(max(n, 1), np.int32)
+    err = np.zeros(2)
+    diag = np.zeros(4, np.int32)
+    ok = ctypes.c_int(0)
+    m = lib().orc_fmat_verify(_p(kr), _p(kc), _p(g), n, _p(F), _p(keep), _p(err), _p(diag), ctypes.byref(ok))
+    return (F.reshape(3, 3) if ok.value else None), keep[:m], err, diag
 
 
 def mt19937(seed, count):

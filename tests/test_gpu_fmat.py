@@ -1,0 +1,103 @@
+"""GPU parity for the F-matrix verification (A8, reference src/Slam.cpp:880-910) through the C ABI.
+
+The registrator outcome (method, iterations run, winning iteration, inlier count, inlier mask,
+the kept match list) must equal the oracle's exactly; F agrees to 1e-9 relative (device libm
+acos/cos/pow inside cv::solveCubic may differ from glibc in the last ulp) and the epipolar
+errors to 1e-12 relative (workgroup vs sequential summation order).  LMedS sets with n <= 13 are
+ill-posed (the median is an exactly fitted subset point), so only their structure is compared."""
+import numpy as np
+import pytest
+
+from test_oracle_fmat import two_view
+
+pytestmark = pytest.mark.gpu
+
+
+def _cmp_find(g, o, n):
+    ok_g, F_g, m_g, d_g = g
+    ok_o, F_o, m_o, d_o = o
+    assert d_g[0] == d_o[0]
+    if d_o[0] == 3 and n <= 13:
+        assert d_g[1] == d_o[1]
+        return
+    assert ok_g == ok_o and np.array_equal(d_g, d_o)
+    if ok_o:
+        assert np.array_equal(m_g, m_o)
+        assert np.max(np.abs(F_g - F_o)) <= 1e-9 * np.abs(F_o).max()
+
+
+@pytest.mark.parametrize("n,seed,noise,out", [(60, 0, 0.0, 0.0), (150, 1, 0.5, 0.3), (400, 2, 1.0, 0.5),
+                                              (2048, 3, 0.7, 0.2), (15, 4, 0.3, 0.0), (120, 5, 0.5, 0.6),
+                                              (14, 6, 0.5, 0.0), (10, 7, 0.5, 0.0), (7, 8, 0.0, 0.0)])
+def test_find_fundamental_matches_oracle(vsctx, oracle, n, seed, noise, out):
+    p1, p2, F, outl = two_view(n, seed, noise, out)
+    _cmp_find(vsctx.find_fundamental(p1, p2), oracle.find_fundamental(p1, p2), n)
+
+
+def test_find_fundamental_edges(vsctx, oracle):
+    p1, p2, F, _ = two_view(40, 9)
+    g = vsctx.find_fundamental(p1[:6], p2[:6])
+    assert not g[0] and g[3][0] == 0
+    assert not vsctx.find_fundamental(p1[:0], p2[:0])[0]
+    q1 = np.stack([np.linspace(0, 600, 30), np.linspace(0, 400, 30)], 1).astype(np.float32)
+    q2 = p2[:1].repeat(30, 0) + np.arange(30)[:, None].astype(np.float32)
+    _cmp_find(vsctx.find_fundamental(q1, q2), oracle.find_fundamental(q1, q2), 30)  # every subset degenerate
+    with pytest.raises(RuntimeError):
+        vsctx.find_fundamental(np.zeros((4096, 2), np.float32), np.zeros((4096, 2), np.float32))
+
+
+def _pairs_inputs(oracle, probs, cap=400):
+    """Two keypoint slots per problem (ref = 2p, cur = 2p+1); matches point into shuffled slots."""
+    P = len(probs)
+    kp_tab = np.zeros((2 * P, cap), oracle.KEYPOINT_DTYPE)
+    goods = np.zeros((P, cap), oracle.MATCH_DTYPE)
+    ngood = np.zeros(P, np.int32)
+    rng = np.random.default_rng(5)
+    for p, (p1, p2) in enumerate(probs):
+        n = len(p1)
+        qr, qc = rng.permutation(cap)[:n], rng.permutation(cap)[:n]
+        kp_tab[2 * p]["x"][qr], kp_tab[2 * p]["y"][qr] = p1[:, 0], p1[:, 1]
+        kp_tab[2 * p + 1]["x"][qc], kp_tab[2 * p + 1]["y"][qc] = p2[:, 0], p2[:, 1]
+        goods[p, :n]["query_idx"], goods[p, :n]["train_idx"] = qr, qc
+        ngood[p] = n
+    pairs = np.array([[2 * p, 2 * p + 1] for p in range(P)], np.int32)
+    return cap, pairs, kp_tab, goods, ngood
+
+
+def test_fmat_verify_pairs_dev_matches_oracle(vsctx, oracle):
+    import torch
+    probs = [two_view(n, 20 + i, noise, out)[:2] for i, (n, noise, out) in
+             enumerate([(300, 0.5, 0.3), (40, 1.0, 0.5), (14, 0.5, 0.0), (5, 0.0, 0.0), (400, 0.3, 0.1),
+                        (7, 0.0, 0.0), (100, 0.5, 0.7)])]
+    cap, pairs, kp_tab, goods2, ngood2 = _pairs_inputs(oracle, probs)
+    P = len(probs)
+    dev = lambda a: torch.from_numpy(np.ascontiguousarray(a).view(np.uint8)).cuda()  # noqa: E731
+    d_pairs, d_kps, d_good = dev(pairs), dev(kp_tab), dev(goods2)
+    d_ngood = dev(ngood2)
+    d_F = torch.zeros(P, 9, dtype=torch.float64, device="cuda")
+    d_kept = torch.zeros(P * cap * 16, dtype=torch.uint8, device="cuda")
+    d_nkept = torch.zeros(P, dtype=torch.int32, device="cuda")
+    d_err = torch.zeros(P, 2, dtype=torch.float64, device="cuda")
+    d_diag = torch.zeros(P, 8, dtype=torch.int32, device="cuda")
+    torch.cuda.synchronize()
+    vsctx.fmat_verify_pairs_dev(P, d_pairs.data_ptr(), d_kps.data_ptr(), cap, d_good.data_ptr(), d_ngood.data_ptr(),
+                                d_F.data_ptr(), d_kept.data_ptr(), d_nkept.data_ptr(), d_err.data_ptr(),
+                                d_diag.data_ptr())
+    torch.cuda.synchronize()
+    kept = d_kept.cpu().numpy().view(oracle.MATCH_DTYPE).reshape(P, cap)
+    nk, err, diag, Fg = d_nkept.cpu().numpy(), d_err.cpu().numpy(), d_diag.cpu().numpy(), d_F.cpu().numpy()
+    for p in range(P):
+        n = int(ngood2[p])
+        Fo, keep, err_o, diag_o = oracle.fmat_verify(kp_tab[2 * p], kp_tab[2 * p + 1], goods2[p, :n])
+        assert diag[p, 0] == diag_o[0] and diag[p, 5] == n
+        if diag_o[0] == 3 and n <= 13:
+            continue
+        assert (diag[p, 4] == 1) == (Fo is not None)
+        assert nk[p] == len(keep) and diag[p, 6] == len(keep)
+        assert np.array_equal(kept[p, :nk[p]], goods2[p, keep])
+        assert np.array_equal(diag[p, :4], diag_o)
+        if Fo is not None:
+            assert np.max(np.abs(Fg[p].reshape(3, 3) - Fo)) <= 1e-9 * np.abs(Fo).max()
+            assert np.allclose(err[p], err_o, rtol=1e-12, atol=0)
+        else:
+            assert (err[p] == 0).all()

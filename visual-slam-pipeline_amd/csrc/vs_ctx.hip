@@ -3,6 +3,7 @@
 // points (enqueue only).  Each entry point cites the reference interface it replaces.
 #include <hip/hip_runtime.h>
 
+#include <cfloat>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -631,6 +632,56 @@ int vs_solve_pnp(vs_ctx* ctx, const float* obj_pts, const float* img_pts, int n,
         diag[1] = stat[3];
         diag[2] = stat[4];
         diag[3] = stat[5];
+    }
+    return VS_OK;
+}
+
+int vs_fmat_verify_pairs_dev(vs_ctx* ctx, int P, const int* d_pairs, const vs_keypoint* d_kps, int cap,
+                             const vs_match* d_good, const int* d_ngood, double* d_F, vs_match* d_kept, int* d_nkept,
+                             double* d_err, int* d_diag, void* stream) {
+    VS_ARG(ctx && d_pairs && d_kps && d_good && d_ngood && d_F && d_kept && d_nkept && d_err && d_diag,
+           "vs_fmat_verify_pairs_dev: null argument");
+    VS_ARG(cap > 0 && cap <= VS_FM_MAX_POINTS, "vs_fmat_verify_pairs_dev: cap out of range");
+    VS_HIP(hipSetDevice(ctx->device));
+    return fmat_pairs(ctx, P, d_pairs, d_kps, cap, d_good, d_ngood, d_F, d_kept, d_nkept, d_err, d_diag,
+                      pick(ctx, stream));
+}
+
+int vs_find_fundamental(vs_ctx* ctx, const float* p1, const float* p2, int n, double thr, double conf, int max_iters,
+                        double F[9], uint8_t* mask, int* ok, int diag[4]) {
+    VS_ARG(ctx && F && ok, "vs_find_fundamental: null argument");
+    VS_ARG(n >= 0 && n <= VS_FM_MAX_POINTS && (n == 0 || (p1 && p2)), "vs_find_fundamental: bad points");
+    // findFundamentalMat's argument defaults (fundam.cpp)
+    if (thr <= 0) thr = 3;
+    if (conf < DBL_EPSILON || conf > 1 - DBL_EPSILON) conf = 0.99;
+    *ok = 0;
+    if (diag) diag[0] = diag[1] = diag[3] = 0, diag[2] = -1;
+    if (n == 0) return VS_OK;
+    VS_HIP(hipSetDevice(ctx->device));
+    hipStream_t s = ctx->stream;
+    VS_CHECK(upload(ctx->h_aux0, p1, (size_t)n * 2, s));
+    VS_CHECK(upload(ctx->h_aux1, p2, (size_t)n * 2, s));
+    VS_CHECK(ctx->h_aux2.ensure(11 * sizeof(double) + 12 * sizeof(int) + (size_t)n));
+    double* dF = ctx->h_aux2.as<double>();  // F[9], err[2]
+    int* dmeta = reinterpret_cast<int*>(dF + 11);  // off[2], diag[8]
+    uint8_t* dmask = reinterpret_cast<uint8_t*>(dmeta + 12);
+    const int off[2] = {0, n};
+    VS_HIP(hipMemcpyAsync(dmeta, off, sizeof(off), hipMemcpyHostToDevice, s));
+    VS_CHECK(fmat_points(ctx, 1, ctx->h_aux0.as<float>(), ctx->h_aux1.as<float>(), dmeta, thr, conf, max_iters, dF,
+                         dmask, dF + 9, dmeta + 2, s));
+    double Fh[9];
+    int dg[8];
+    VS_HIP(hipMemcpyAsync(Fh, dF, sizeof(Fh), hipMemcpyDeviceToHost, s));
+    VS_HIP(hipMemcpyAsync(dg, dmeta + 2, sizeof(dg), hipMemcpyDeviceToHost, s));
+    if (mask) VS_HIP(hipMemcpyAsync(mask, dmask, (size_t)n, hipMemcpyDeviceToHost, s));
+    VS_HIP(hipStreamSynchronize(s));
+    *ok = dg[4];
+    std::memcpy(F, Fh, sizeof(Fh));
+    if (diag) {
+        diag[0] = dg[0];
+        diag[1] = dg[1];
+        diag[2] = dg[2];
+        diag[3] = dg[3];
     }
     return VS_OK;
 }

@@ -141,5 +141,11 @@ int optimize_pose(vs_ctx* ctx, int nprob, const double* d_P, const float* d_p2, 
 int solve_pnp(vs_ctx* ctx, int nprob, const float* d_obj, const float* d_img, const int* d_off, const double K[4],
               int ransac_iters, int min_inliers, double* d_R, double* d_t, int* d_stat, uint8_t* d_mask,
               hipStream_t s);
+// F-matrix verification: per frame pair (pipeline) or per point set (ABI single problem)
+int fmat_pairs(vs_ctx* ctx, int P, const int* d_pairs, const vs_keypoint* d_kps, int cap, const vs_match* d_good,
+               const int* d_ngood, double* d_F, vs_match* d_kept, int* d_nkept, double* d_err, int* d_diag,
+               hipStream_t s);
+int fmat_points(vs_ctx* ctx, int P, const float* d_p1, const float* d_p2, const int* d_off, double thr, double conf,
+                int max_iters, double* d_F, uint8_t* d_mask, double* d_err, int* d_diag, hipStream_t s);
 
 }  // namespace vs

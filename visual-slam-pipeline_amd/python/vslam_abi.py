@@ -53,6 +53,8 @@ _SIG = {
     "vs_optimize_pose_batch_dev": (_I, [_P, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
     "vs_solve_pnp": (_I, [_P, _P, _P, _I, _P, _I, _I, _P, _P, _P, _P, _P, _P]),
     "vs_solve_pnp_batch_dev": (_I, [_P, _I, _P, _P, _P, _P, _I, _I, _P, _P, _P, _P, _P]),
+    "vs_find_fundamental": (_I, [_P, _P, _P, _I, ctypes.c_double, ctypes.c_double, _I, _P, _P, _P, _P]),
+    "vs_fmat_verify_pairs_dev": (_I, [_P, _I, _P, _P, _I, _P, _P, _P, _P, _P, _P, _P, _P]),
     "vs_profile_enable": (_I, [_P, _I]),
     "vs_profile_reset": (_I, [_P]),
     "vs_profile_read": (_I, [_P, _I, _P, _P, _P, _P]),
@@ -273,6 +275,25 @@ class Context:
         Ka = _k_array(K)
         _check(self.lib.vs_solve_pnp_batch_dev(self.h, nprob, d_obj, d_img, d_off, _ptr(Ka), ransac_iters,
                                                min_inliers, d_R, d_t, d_stat, d_mask, stream))
+
+    # ---- cv::findFundamentalMat (FM_RANSAC) ----
+    def find_fundamental(self, p1, p2, thr=3.0, conf=0.999, max_iters=1000):
+        """Returns (ok, F 3x3, inlier mask, diag)."""
+        a = np.ascontiguousarray(p1, np.float32).reshape(-1, 2)
+        b = np.ascontiguousarray(p2, np.float32).reshape(-1, 2)
+        n = a.shape[0]
+        F = np.zeros(9, np.float64)
+        mask = np.zeros(max(n, 1), np.uint8)
+        ok = ctypes.c_int(0)
+        diag = np.zeros(4, np.int32)
+        _check(self.lib.vs_find_fundamental(self.h, _ptr(a), _ptr(b), n, thr, conf, max_iters, _ptr(F), _ptr(mask),
+                                            ctypes.byref(ok), _ptr(diag)))
+        return bool(ok.value), F.reshape(3, 3), mask[:n].astype(bool), diag
+
+    def fmat_verify_pairs_dev(self, P, d_pairs, d_kps, cap, d_good, d_ngood, d_F, d_kept, d_nkept, d_err, d_diag,
+                              stream=None):
+        _check(self.lib.vs_fmat_verify_pairs_dev(self.h, P, d_pairs, d_kps, cap, d_good, d_ngood, d_F, d_kept,
+                                                 d_nkept, d_err, d_diag, stream))
 
     # ---- device-batched entry points (pointers are ints, e.g. torch tensor.data_ptr()) ----
     def extract_batch_dev(self, B, d_imgs, h, w, d_kps, d_desc, d_n, cap, stream=None):
