@@ -4,7 +4,8 @@ One "step" = B consecutive processed 640x480 RGB-D frames per GPU, already resid
 through the whole per-frame hot path by libvslam_hip.so:
     FeatureExtractor::extract   (SuperPoint fp32 network + decode + greedy NMS + descriptor sampling)
     Slam::match_features        (exact 2-NN + 0.75 ratio test, frame i-1 -> frame i)
-    Slam::estimate_motion_3d3d  (200-iteration 3D-3D RANSAC + refit)
+    F-matrix verification       (findFundamentalMat(FM_RANSAC, 3.0, 0.999) + ordered filtering)
+    Slam::estimate_motion_3d3d  (200-iteration 3D-3D RANSAC + refit, on the F-filtered matches)
 plus the host pose chain on the returned (R, t) (Slam.cpp:963-964).  With --gpus N > 1 the frames
 are sharded in contiguous blocks across N ranks (one process per GPU) and the per-frame feature
 records are all-gathered over RCCL each step (weak scaling: B frames per GPU per step).
@@ -83,7 +84,7 @@ def parse():
 
 def cpu_baseline(frames_list, nframes):
     """The CPU restatement (oracle/, test infrastructure) on a bounded sample of the same workload:
-    extract + match + 3D-3D RANSAC for consecutive frames, OpenMP network."""
+    extract + match + F verification + 3D-3D RANSAC for consecutive frames, OpenMP network."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle_py as oracle
     import vslam_abi
@@ -99,6 +100,8 @@ def cpu_baseline(frames_list, nframes):
         if prev is not None:
             (k1, d1, dep1) = prev
             _, good = oracle.match_ratio(d1, desc)
+            _, keep, _, _ = oracle.fmat_verify(k1, kps, good)
+            good = good[keep]
             p1 = np.stack([k1["x"][good["query_idx"]], k1["y"][good["query_idx"]]], 1)
             p2 = np.stack([kps["x"][good["train_idx"]], kps["y"][good["train_idx"]]], 1)
             oracle.ransac_3d3d(p1, p2, dep1, f["depth"], seed=42 + i)
@@ -106,7 +109,8 @@ def cpu_baseline(frames_list, nframes):
     dt = time.perf_counter() - t0
     return {"value": len(sample) / dt, "unit": "frames/s", "cores": threads, "kind": "port",
             "sample": f"{len(sample)} consecutive synthetic 640x480 RGB-D frames, oracle/ CPU restatement "
-                      f"(OpenMP fp32 SuperPoint, decode/NMS/sample, exact 2-NN match, 3D-3D RANSAC), "
+                      f"(OpenMP fp32 SuperPoint, decode/NMS/sample, exact 2-NN match, F-RANSAC "
+                      f"verification, 3D-3D RANSAC), "
                       f"{threads} threads, {dt:.1f} s"}
 
 
@@ -211,7 +215,7 @@ def main():
             "data": "synthetic (seeded 640x480 RGB-D room sequence, seeded He-normal SuperPoint weights)",
             "config": {
                 "workload": "config[1]: 640x480 RGB-D stream on 1xMI355X - HIP SuperPoint extract + "
-                            "ratio-test matching + 3D-3D RANSAC per processed frame",
+                            "ratio-test matching + F-RANSAC verification + 3D-3D RANSAC per processed frame",
                 "frames_per_gpu_per_step": B,
                 "resolution": "640x480",
                 "max_keypoints": 400,

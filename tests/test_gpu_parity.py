@@ -197,6 +197,8 @@ def test_device_pipeline_matches_host_entry_points(vsctx, seq4):
         kb = kps[b].view(feats[b][0].dtype)[:n[b]]
         assert _kp_equal(kb, feats[b][0])
     ngood = out["ngood"].cpu().numpy()
+    nkept = out["nkept"].cpu().numpy()
+    kept_all = out["kept"].cpu().numpy().view(np.uint8)
     assert ngood[0] == 0  # no frame before the first batch
     for p in range(1, len(seq4)):  # pair p = frames (p-1, p), seed 42 + frame_count
         _, good = vsctx.match_ratio(feats[p - 1][1], feats[p][1])
@@ -205,6 +207,13 @@ def test_device_pipeline_matches_host_entry_points(vsctx, seq4):
         k1, k2 = feats[p - 1][0], feats[p][0]
         p1 = np.stack([k1["x"][good["query_idx"]], k1["y"][good["query_idx"]]], 1)
         p2 = np.stack([k2["x"][good["train_idx"]], k2["y"][good["train_idx"]]], 1)
+        # F verification (Slam.cpp:880-910) filters the matches before the 3D-3D stage
+        okf, F, fmask, fdiag = vsctx.find_fundamental(p1, p2)
+        keep = np.flatnonzero(fmask) if okf else np.arange(len(good))
+        assert nkept[p] == len(keep)
+        assert np.array_equal(kept_all[p].view(good.dtype)[:nkept[p]], good[keep])
+        assert np.array_equal(out["fdiag"][p].cpu().numpy()[:4], fdiag)
+        p1, p2 = p1[keep], p2[keep]
         okh, Rh, th, dh = vsctx.ransac_3d3d(p1, p2, seq4[p - 1]["depth"], seq4[p]["depth"], seed=42 + p)
         assert okp == okh
         assert np.array_equal(out["diag"][p].cpu().numpy(), dh)

@@ -4,7 +4,10 @@ Per step each rank takes B consecutive processed frames of a 640x480 RGB-D strea
 sit in HBM and runs, entirely through libvslam_hip.so:
     FeatureExtractor::extract           (vs_extract_batch_dev: SuperPoint + decode + NMS + sample)
     Slam::match_features(prev, cur)     (vs_match_pairs_dev: exact 2-NN + ratio 0.75)
-    Slam::estimate_motion_3d3d          (vs_ransac_3d3d_pairs_dev: 200-iteration 3D-3D RANSAC)
+    F-matrix verification               (vs_fmat_verify_pairs_dev: findFundamentalMat(FM_RANSAC,
+                                         3.0, 0.999), matches filtered in order, epipolar errors)
+    Slam::estimate_motion_3d3d          (vs_ransac_3d3d_pairs_dev: 200-iteration 3D-3D RANSAC on
+                                         the F-filtered matches)
 for the B frame pairs (i-1, i) that end in its frames (Slam.cpp:838-955).  torch provides device
 memory, the stream and torch.distributed; it computes nothing.
 
@@ -42,6 +45,11 @@ class DevicePipeline:
         self.good = torch.zeros((P, cap * M_BYTES), dtype=torch.uint8, device=dev)
         self.nraw = torch.zeros(P, dtype=torch.int32, device=dev)
         self.ngood = torch.zeros(P, dtype=torch.int32, device=dev)
+        self.fkept = torch.zeros((P, cap * M_BYTES), dtype=torch.uint8, device=dev)
+        self.nfkept = torch.zeros(P, dtype=torch.int32, device=dev)
+        self.F = torch.zeros((P, 9), dtype=torch.float64, device=dev)
+        self.eperr = torch.zeros((P, 2), dtype=torch.float64, device=dev)
+        self.fdiag = torch.zeros((P, 8), dtype=torch.int32, device=dev)
         self.R = torch.zeros((P, 9), dtype=torch.float64, device=dev)
         self.t = torch.zeros((P, 3), dtype=torch.float64, device=dev)
         self.ok = torch.zeros(P, dtype=torch.int32, device=dev)
@@ -103,11 +111,15 @@ class DevicePipeline:
         ctx.match_pairs_dev(B, self.pairs.data_ptr(), B + 1, self.desc.data_ptr(), self.n.data_ptr(), cap,
                             self.ratio, self.raw.data_ptr(), self.nraw.data_ptr(), self.good.data_ptr(),
                             self.ngood.data_ptr(), s)
-        ctx.ransac_3d3d_pairs_dev(B, self.pairs.data_ptr(), self.kps.data_ptr(), cap, self.good.data_ptr(),
-                                  self.ngood.data_ptr(), self.depth.data_ptr(), h, w, self.K, self.seeds.data_ptr(),
+        ctx.fmat_verify_pairs_dev(B, self.pairs.data_ptr(), self.kps.data_ptr(), cap, self.good.data_ptr(),
+                                  self.ngood.data_ptr(), self.F.data_ptr(), self.fkept.data_ptr(),
+                                  self.nfkept.data_ptr(), self.eperr.data_ptr(), self.fdiag.data_ptr(), s)
+        ctx.ransac_3d3d_pairs_dev(B, self.pairs.data_ptr(), self.kps.data_ptr(), cap, self.fkept.data_ptr(),
+                                  self.nfkept.data_ptr(), self.depth.data_ptr(), h, w, self.K, self.seeds.data_ptr(),
                                   self.iters, self.thr, self.R.data_ptr(), self.t.data_ptr(), self.ok.data_ptr(),
                                   self.diag.data_ptr(), s)
         return dict(kps=self.kps[1:], desc=self.desc[1:], n=self.n[1:], good=self.good, ngood=self.ngood,
+                    kept=self.fkept, nkept=self.nfkept, F=self.F, eperr=self.eperr, fdiag=self.fdiag,
                     R=self.R, t=self.t, ok=self.ok, diag=self.diag)
 
 
