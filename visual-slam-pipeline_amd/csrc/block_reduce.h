@@ -6,9 +6,9 @@
 
 namespace vs {
 
-// Sum of N doubles per lane: xor-shuffle tree inside each wave, then the 4 wave partials in a
-// fixed order.  Every lane receives the totals in out[].  s_red holds 4 * N doubles.
-template <int N>
+// Sum of N doubles per lane over NW wave64s: xor-shuffle tree inside each wave, then the wave
+// partials in a fixed order.  Every lane receives the totals in out[].  s_red holds NW * N doubles.
+template <int N, int NW = 4>
 __device__ inline void block_sum(double (&v)[N], double* s_red, double (&out)[N]) {
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
 #pragma unroll
@@ -23,7 +23,12 @@ __device__ inline void block_sum(double (&v)[N], double* s_red, double (&out)[N]
         for (int k = 0; k < N; k++) s_red[wv * N + k] = v[k];
     __syncthreads();
 #pragma unroll
-    for (int k = 0; k < N; k++) out[k] = ((s_red[k] + s_red[N + k]) + s_red[2 * N + k]) + s_red[3 * N + k];
+    for (int k = 0; k < N; k++) {
+        double s = s_red[k];
+#pragma unroll
+        for (int w = 1; w < NW; w++) s += s_red[w * N + k];
+        out[k] = s;
+    }
     __syncthreads();
 }
 

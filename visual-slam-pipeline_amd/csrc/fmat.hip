@@ -3,15 +3,25 @@
 // 3.0, RANSAC_PROB = 0.999), mask filtering of good_matches in order, compute_epipolar_error
 // before and after :1217-1240).
 //
-// One workgroup (4 wave64s) per frame pair.  The registrators are sequential only through the
-// cv::RNG stream and the shrinking iteration budget, so iterations run in chunks of 256:
-// lane 0 draws the chunk's subsets (with the collinearity rejection, which depends on the data
-// only), every lane solves one 7-point subset and scores its up to three models (inlier count
-// for RANSAC, median error for LMedS), and lane 0 replays the acceptance rule over the chunk in
-// iteration order.  A chunk past the final budget is never drawn.  The winning subset is
-// re-solved for the final model (identical arithmetic), inliers are marked, the match list is
-// compacted in order, and both epipolar errors are reduced over the workgroup.  Numerical
-// kernels are shared with the CPU restatement (fmat_solvers.h, built with -ffp-contract=off).
+// One workgroup (8 wave64s) per frame pair.  The registrators are sequential only through the
+// cv::RNG stream and the shrinking iteration budget, so iterations run in chunks (64, 128, then
+// 256 hypotheses):
+//   * subsets: wave 0 steps the RNG on the scalar unit (lane k keeps state k of each block of
+//     64); all lanes reduce the draws modulo n; wave 0 assembles the 7-index subsets with the
+//     repeat rejection speculatively in parallel (lane l assumes the next 7-draw window; a
+//     ballot finds the first window with a repeat, which is assembled serially); all lanes test
+//     collinearity in parallel.  A collinear subset ends the chunk before it and the next chunk
+//     redraws it with the exact serial getSubset (attempt loop included), so the subsets are
+//     exactly OpenCV's;
+//   * hypotheses: one 7-point solve per lane, models in LDS;
+//   * RANSAC scoring in rounds of 8 hypotheses: wave w scores hypothesis r0 + w with its 64
+//     lanes sweeping the points (ballot + popcount, division-free exact gate of fm_inlier,
+//     early exit once a model can no longer beat the current best), then lane 0 replays the
+//     round in iteration order and the rounds stop at the shrinking budget; LMedS (n <= 14)
+//     scores per lane and replays per chunk.
+// Then inliers are marked, the match list is compacted in order and both epipolar errors are
+// reduced.  Numerical kernels are shared with the CPU restatement (fmat_solvers.h;
+// -ffp-contract=off).
 #include <hip/hip_runtime.h>
 
 #include "block_reduce.h"
@@ -23,18 +33,39 @@ namespace vs {
 using namespace vs_fm;
 
 constexpr int kFmMaxPts = VS_FM_MAX_POINTS;
-constexpr int kChunk = 256;
+constexpr int kMaxChunk = 256;
+constexpr int kThreads = 512;  // 8 wave64s: 2 per SIMD
+constexpr int kWaves = kThreads / 64;
+constexpr int kRawCap = 7 * kMaxChunk + 128;
+
+#ifdef VS_FM_PROFILE
+// phase cycle counters (profiling build only: make -C visual-slam-pipeline_amd prof)
+__device__ unsigned long long g_fm_cycles[8];
+#define FM_T0() long long _fm_t = clock64()
+#define FM_T(k)                                                              \
+    do {                                                                     \
+        if (threadIdx.x == 0) atomicAdd(&g_fm_cycles[k], clock64() - _fm_t); \
+        _fm_t = clock64();                                                   \
+    } while (0)
+#else
+#define FM_T0()
+#define FM_T(k)
+#endif
 
 struct FmShared {
     float p1[2 * kFmMaxPts], p2[2 * kFmMaxPts];
-    int subset[kChunk * 7];
-    int nmod[kChunk];
-    float score[kChunk * 3];  // RANSAC: inlier count; LMedS: median error
-    int scan[256];
+    uint64_t st[kRawCap];  // RNG state after raw draw r
+    int draw[kRawCap];     // (unsigned)state % n
+    int subset[kMaxChunk * 7];
+    int sub_end[kMaxChunk];  // raw position just past subset j
+    int coll[kMaxChunk];
+    double Fm[kMaxChunk * 3 * 9];
+    int nmod[kMaxChunk];
+    float score[kMaxChunk * 3];  // RANSAC: inlier count; LMedS: median error
+    int scan[kThreads];
     double F[9];
     uint64_t rng;
-    int best_subset[7];
-    int niters, best, best_k, best_iter, iter, fail_at, done, aborted, ok, chunk, inliers;
+    int niters, best, best_iter, iter, fail_at, done, aborted, ok, chunk, inliers, serial_next, raw_n, nchunk;
     double min_median;
 };
 
@@ -49,11 +80,131 @@ __device__ inline int solve_idx(const FmShared& S, const int* idx, double (*F)[9
     return run_7point(x1, y1, x2, y2, F);
 }
 
+__device__ inline bool subset_collinear(const FmShared& S, const int* idx) {
+    float x1[7], y1[7], x2[7], y2[7];
+    for (int i = 0; i < 7; i++) {
+        x1[i] = S.p1[2 * idx[i]];
+        y1[i] = S.p1[2 * idx[i] + 1];
+        x2[i] = S.p2[2 * idx[i]];
+        y2[i] = S.p2[2 * idx[i] + 1];
+    }
+    return have_collinear(x1, y1, 7) || have_collinear(x2, y2, 7);
+}
+
+// Draws the next chunk's subsets into S.subset and sets S.chunk (may be 0 when getSubset failed,
+// with S.fail_at set).  Called by all lanes.
+__device__ void draw_subsets(FmShared& S, int n, int base, int want, int attempts) {
+    const int tid = threadIdx.x;
+    if (S.serial_next) {  // exact serial getSubset (after a collinear rejection, or a stall)
+        if (tid == 0) {
+            CvRng rng(S.rng);
+            const bool found = get_subset(rng, S.p1, S.p2, n, attempts, S.subset);
+            S.rng = rng.state;
+            S.chunk = found ? 1 : 0;
+            if (!found) S.fail_at = base;
+            S.serial_next = 0;
+        }
+        __syncthreads();
+        return;
+    }
+    FM_T0();
+    const int lane = tid & 63;
+    const int R = min(kRawCap, (7 * want + 128 + 63) & ~63);
+    if (tid < 64) {  // wave 0, uniform: the generator runs on the scalar unit, lane k keeps state k
+        uint64_t s = S.rng;
+        for (int r0 = 0; r0 < R; r0 += 64) {
+            uint64_t mine = 0;
+            for (int k = 0; k < 64; k++) {
+                s = (uint64_t)(unsigned)s * 4164903690u + (unsigned)(s >> 32);
+                mine = lane == k ? s : mine;
+            }
+            S.st[r0 + lane] = mine;
+        }
+    }
+    __syncthreads();
+    for (int r = tid; r < R; r += blockDim.x) S.draw[r] = (int)((unsigned)S.st[r] % (unsigned)n);
+    __syncthreads();
+    FM_T(5);
+    if (tid < 64) {
+        // Repeat rejection in stream order, speculatively in parallel (wave 0): lane l assumes
+        // subset j + l is the 7 draws at pos + 7 l, which holds up to the first window that
+        // contains a repeat (ballot); that one subset is then assembled serially and the
+        // speculation resumes after it.  The result is exactly the sequential scan's.
+        int pos = 0, j = 0;
+        bool stalled = false;
+        while (j < want && !stalled) {
+            const int p = pos + 7 * lane;
+            bool ok = p + 7 <= R && j + lane < want;
+            int w[7];
+            VS_UNROLL
+            for (int q = 0; q < 7; q++) w[q] = ok ? S.draw[p + q] : -1;
+            VS_UNROLL
+            for (int a = 1; a < 7; a++)
+                VS_UNROLL
+                for (int b = 0; b < a; b++) ok = ok && w[a] != w[b];
+            const unsigned long long bad = __ballot(!ok);
+            const int f = bad ? __ffsll((long long)bad) - 1 : 64;
+            if (lane < f) {
+                VS_UNROLL
+                for (int q = 0; q < 7; q++) S.subset[7 * (j + lane) + q] = w[q];
+                S.sub_end[j + lane] = p + 7;
+            }
+            j += f;
+            pos += 7 * f;
+            if (f == 64 || j >= want) continue;
+            // serial assembly of subset j from pos (uniform across the wave)
+            int cur[7] = {-1, -1, -1, -1, -1, -1, -1};
+            int i = 0;
+            while (i < 7 && pos < R) {
+                const int v = S.draw[pos++];
+                bool dup = false;
+                VS_UNROLL
+                for (int q = 0; q < 7; q++) dup |= (q < i) & (cur[q] == v);
+                if (!dup) {
+                    VS_UNROLL
+                    for (int q = 0; q < 7; q++) cur[q] = (q == i) ? v : cur[q];
+                    i++;
+                }
+            }
+            if (i < 7) {  // the raw draws ran out: the chunk ends before subset j
+                stalled = true;
+                continue;
+            }
+            if (lane < 7) {
+                int val = cur[0];
+                VS_UNROLL
+                for (int q = 1; q < 7; q++) val = lane == q ? cur[q] : val;
+                S.subset[7 * j + lane] = val;
+            }
+            if (lane == 0) S.sub_end[j] = pos;
+            j++;
+        }
+        if (lane == 0) S.chunk = j;
+    }
+    __syncthreads();
+    FM_T(6);
+    for (int j = tid; j < S.chunk; j += blockDim.x) S.coll[j] = subset_collinear(S, S.subset + 7 * j);
+    __syncthreads();
+    FM_T(7);
+    if (tid == 0) {
+        int c = S.chunk;
+        for (int j = 0; j < S.chunk; j++)
+            if (S.coll[j]) {
+                c = j;
+                break;
+            }
+        if (c < S.chunk || c == 0) S.serial_next = 1;  // redraw subset c exactly (or make progress)
+        if (c > 0) S.rng = S.st[S.sub_end[c - 1] - 1];
+        S.chunk = c;
+    }
+    __syncthreads();
+}
+
 // Problem source: FROM_MATCHES = pairs of frames + keypoints + good matches (pipeline), else
 // point arrays with offsets (ABI single-problem path).
-// diag[p][8] = {method, iterations run, winning iteration, inliers, F ok, n, kept, 0}
+// diag[p][8] = {method, iterations run, winning iteration, inliers, F ok, n, kept, chunks}
 template <bool FROM_MATCHES>
-__global__ __launch_bounds__(256) void k_fmat(const int* __restrict__ pairs, const vs_keypoint* __restrict__ kps,
+__global__ __launch_bounds__(kThreads) void k_fmat(const int* __restrict__ pairs, const vs_keypoint* __restrict__ kps,
                                               int cap, const vs_match* __restrict__ good,
                                               const int* __restrict__ ngood, const float* __restrict__ pts1,
                                               const float* __restrict__ pts2, const int* __restrict__ off,
@@ -62,7 +213,8 @@ __global__ __launch_bounds__(256) void k_fmat(const int* __restrict__ pairs, con
                                               int* __restrict__ nkept, double* __restrict__ err,
                                               int* __restrict__ diag) {
     __shared__ FmShared S;
-    const int pb = blockIdx.x, tid = threadIdx.x;
+    __shared__ double red4[kWaves * 4];
+    const int pb = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     int n;
     const vs_match* gm = nullptr;
     if (FROM_MATCHES) {
@@ -87,64 +239,54 @@ __global__ __launch_bounds__(256) void k_fmat(const int* __restrict__ pairs, con
     }
     int* dg = diag + 8 * pb;
     const int method = n < 7 ? 0 : n == 7 ? 1 : n >= 15 ? 2 : 3;
+    const float thr2 = (float)(thr * thr);
     if (tid == 0) {
         S.rng = (uint64_t)-1;
         S.best = 0;
-        S.best_k = 0;
         S.best_iter = -1;
         S.iter = 0;
         S.fail_at = -1;
         S.done = method < 2;
         S.aborted = 0;
         S.ok = 0;
+        S.serial_next = 0;
+        S.nchunk = 0;
         S.min_median = DBL_MAX;
         S.niters = method == 2 ? (max_iters > 1 ? max_iters : 1) : 0;
         if (method == 3) {
             const int ni = vs_pnp::ransac_update_num_iters(conf, 0.45, 7, max_iters);
             S.niters = ni > 3 ? ni : 3;
         }
-        if (method == 1) {
-            const int all[7] = {0, 1, 2, 3, 4, 5, 6};
-            double Fs[3][9];
-            if (solve_idx(S, all, Fs) > 0) {
-                for (int k = 0; k < 9; k++) S.F[k] = Fs[0][k];
-                S.ok = 1;
-            }
+    }
+    __syncthreads();
+    if (method == 1 && tid == 0) {
+        const int all[7] = {0, 1, 2, 3, 4, 5, 6};
+        double Fs[3][9];
+        if (solve_idx(S, all, Fs) > 0) {
+            for (int k = 0; k < 9; k++) S.F[k] = Fs[0][k];
+            S.ok = 1;
         }
     }
     __syncthreads();
-    const float thr2 = (float)(thr * thr);
-    // ---- registrator loop, one chunk of iterations at a time ----
-    for (int base = 0; !S.done; base += kChunk) {
-        if (tid == 0) {
-            const int chunk = min(kChunk, S.niters - base);
-            CvRng rng(S.rng);
-            const int attempts = method == 2 ? 10000 : 1000;
-            int j = 0;
-            for (; j < chunk; j++)
-                if (!get_subset(rng, S.p1, S.p2, n, attempts, S.subset + 7 * j)) {
-                    S.fail_at = base + j;
-                    break;
-                }
-            S.rng = rng.state;
-            S.chunk = j;
-        }
-        __syncthreads();
+    // ---- registrator loop ----
+    while (!S.done) {
+        const int base = S.iter;
+        const int want = min(min(kMaxChunk, 64 << min(S.nchunk, 2)), S.niters - base);
+        draw_subsets(S, n, base, want, method == 2 ? 10000 : 1000);
+        FM_T0();
         const int chunk = S.chunk;
         if (tid < chunk) {
             double Fs[3][9];
             const int nm = solve_idx(S, S.subset + 7 * tid, Fs);
             S.nmod[tid] = nm;
-            for (int k = 0; k < nm; k++) {
-                if (method == 2) {
-                    int cnt = 0;
-                    for (int i = 0; i < n; i++)
-                        cnt += fm_error(Fs[k], S.p1[2 * i], S.p1[2 * i + 1], S.p2[2 * i], S.p2[2 * i + 1]) <= thr2;
-                    S.score[3 * tid + k] = (float)cnt;
-                } else {  // LMedS: n <= 14, median = element n/2 of the sorted errors
+            for (int k = 0; k < nm; k++)
+                for (int q = 0; q < 9; q++) S.Fm[(tid * 3 + k) * 9 + q] = Fs[k][q];
+            if (method == 3)  // LMedS: n <= 14, median = element n/2 of the sorted errors
+                for (int k = 0; k < nm; k++) {
                     float e[14];
                     for (int i = 0; i < n; i++) {
-                        const float v = fm_error(Fs[k], S.p1[2 * i], S.p1[2 * i + 1], S.p2[2 * i], S.p2[2 * i + 1]);
+                        const float v =
+                            fm_error(Fs[k], S.p1[2 * i], S.p1[2 * i + 1], S.p2[2 * i], S.p2[2 * i + 1]);
                         int q = i;
                         while (q > 0 && e[q - 1] > v) {
                             e[q] = e[q - 1];
@@ -154,52 +296,85 @@ __global__ __launch_bounds__(256) void k_fmat(const int* __restrict__ pairs, con
                     }
                     S.score[3 * tid + k] = e[n / 2];
                 }
-            }
         }
         __syncthreads();
-        if (tid == 0) {  // sequential replay of this chunk
+        FM_T(1);
+        if (method == 2) {
+            // Rounds of kWaves hypotheses: wave w scores hypothesis r0 + w (its lanes sweep the
+            // points), then lane 0 replays the round in iteration order.  A model whose count can
+            // no longer exceed max(best, 6) at the round's start stops early (it cannot be taken:
+            // the bar only rises during the replay); the round loop stops at the budget.
+            for (int r0 = 0; r0 < chunk; r0 += kWaves) {
+                const int h = r0 + wv;
+                if (h < chunk && base + h < S.niters) {
+                    const int bar = S.best > 6 ? S.best : 6;
+                    for (int k = 0; k < S.nmod[h]; k++) {
+                        const int m = 3 * h + k;
+                        double F[9];
+                        for (int q = 0; q < 9; q++) F[q] = S.Fm[m * 9 + q];
+                        int cnt = 0;
+                        for (int i0 = 0; i0 < n; i0 += 64) {
+                            const int i = i0 + lane;
+                            const bool in = i < n && fm_inlier(F, S.p1[2 * i], S.p1[2 * i + 1], S.p2[2 * i],
+                                                               S.p2[2 * i + 1], thr2);
+                            cnt += __popcll(__ballot(in));
+                            if (cnt + max(0, n - i0 - 64) <= bar) {
+                                cnt = -1;  // cannot be taken
+                                break;
+                            }
+                        }
+                        if (lane == 0) S.score[m] = (float)cnt;
+                    }
+                }
+                __syncthreads();
+                if (tid == 0) {
+                    int it = S.iter;
+                    for (int hh = r0; hh < min(r0 + kWaves, chunk) && it < S.niters; hh++, it++)
+                        for (int k = 0; k < S.nmod[hh]; k++) {
+                            const int m = 3 * hh + k;
+                            const int cnt = (int)S.score[m];
+                            if (cnt > (S.best > 6 ? S.best : 6)) {
+                                S.best = cnt;
+                                S.niters = vs_pnp::ransac_update_num_iters(conf, (double)(n - cnt) / n, 7, S.niters);
+                                S.best_iter = it;
+                                for (int q = 0; q < 9; q++) S.F[q] = S.Fm[m * 9 + q];
+                            }
+                        }
+                    S.iter = it;
+                }
+                __syncthreads();
+                if (S.iter >= S.niters) break;
+            }
+        } else if (tid == 0) {  // LMedS: fixed budget, replay the chunk
             int it = base;
             for (; it < base + chunk && it < S.niters; it++) {
                 const int h = it - base;
                 for (int k = 0; k < S.nmod[h]; k++) {
-                    if (method == 2) {
-                        const int cnt = (int)S.score[3 * h + k];
-                        if (cnt > (S.best > 6 ? S.best : 6)) {
-                            S.best = cnt;
-                            S.best_iter = it;
-                            S.best_k = k;
-                            for (int q = 0; q < 7; q++) S.best_subset[q] = S.subset[7 * h + q];
-                            S.niters = vs_pnp::ransac_update_num_iters(conf, (double)(n - cnt) / n, 7, S.niters);
-                        }
-                    } else {
-                        const double med = S.score[3 * h + k];
-                        if (med < S.min_median) {
-                            S.min_median = med;
-                            S.best_iter = it;
-                            S.best_k = k;
-                            for (int q = 0; q < 7; q++) S.best_subset[q] = S.subset[7 * h + q];
-                        }
+                    const int m = 3 * h + k;
+                    if (S.score[m] < S.min_median) {
+                        S.min_median = S.score[m];
+                        S.best_iter = it;
+                        for (int q = 0; q < 9; q++) S.F[q] = S.Fm[m * 9 + q];
                     }
                 }
             }
+            S.iter = it;
+        }
+        FM_T(2);
+        if (tid == 0) {
+            const int it = S.iter;
             if (S.fail_at >= 0 && it == S.fail_at) {  // getSubset failed at this iteration
                 if (it == 0) S.aborted = 1;
                 S.done = 1;
             }
             if (it >= S.niters) S.done = 1;
-            S.iter = it;
-            if (S.done && !S.aborted) {
-                const bool have = method == 2 ? S.best > 0 : S.min_median < DBL_MAX;
-                if (have) {
-                    double Fs[3][9];
-                    solve_idx(S, S.best_subset, Fs);
-                    for (int k = 0; k < 9; k++) S.F[k] = Fs[S.best_k][k];
-                    S.ok = 1;
-                }
-            }
+            S.nchunk++;
+            if (S.done && !S.aborted) S.ok = method == 2 ? S.best > 0 : S.min_median < DBL_MAX;
         }
         __syncthreads();
+        FM_T(3);
     }
+    FM_T0();
     // ---- inliers of the final model ----
     float gate = thr2;
     if (method == 3 && S.ok) {
@@ -211,13 +386,13 @@ __global__ __launch_bounds__(256) void k_fmat(const int* __restrict__ pairs, con
     double F[9];
     for (int k = 0; k < 9; k++) F[k] = S.F[k];
     // contiguous segment per lane so the compaction keeps the reference's order
-    const int per = (n + 255) / 256, lo = min(n, tid * per), hi = min(n, lo + per);
+    const int per = (n + kThreads - 1) / kThreads, lo = min(n, tid * per), hi = min(n, lo + per);
     int local = 0;
-    uint32_t bits = 0;  // per <= 8 since n <= 2048
+    uint32_t bits = 0;  // per <= 4 since n <= 2048
     for (int i = lo; i < hi; i++) {
         bool in = true;
         if (have_f && method != 1)
-            in = fm_error(F, S.p1[2 * i], S.p1[2 * i + 1], S.p2[2 * i], S.p2[2 * i + 1]) <= gate;
+            in = fm_inlier(F, S.p1[2 * i], S.p1[2 * i + 1], S.p2[2 * i], S.p2[2 * i + 1], gate);
         bits |= (uint32_t)in << (i - lo);
         local += in;
     }
@@ -225,7 +400,7 @@ __global__ __launch_bounds__(256) void k_fmat(const int* __restrict__ pairs, con
     __syncthreads();
     if (tid == 0) {
         int acc = 0;
-        for (int q = 0; q < 256; q++) {
+        for (int q = 0; q < kThreads; q++) {
             const int c = S.scan[q];
             S.scan[q] = acc;
             acc += c;
@@ -259,8 +434,8 @@ __global__ __launch_bounds__(256) void k_fmat(const int* __restrict__ pairs, con
             }
         }
     }
-    __shared__ double red4[4 * 4];
-    block_sum<4>(part, red4, tot);
+    block_sum<4, kWaves>(part, red4, tot);
+    FM_T(4);
     if (tid == 0) {
         const int kept_n = ok ? S.inliers : n;
         if (FROM_MATCHES) nkept[pb] = kept_n;
@@ -274,7 +449,7 @@ __global__ __launch_bounds__(256) void k_fmat(const int* __restrict__ pairs, con
         dg[4] = ok;
         dg[5] = n;
         dg[6] = kept_n;
-        dg[7] = 0;
+        dg[7] = S.nchunk;
     }
 }
 
@@ -284,7 +459,7 @@ int fmat_pairs(vs_ctx* ctx, int P, const int* d_pairs, const vs_keypoint* d_kps,
     if (P <= 0) return VS_OK;
     VS_ARG(cap <= kFmMaxPts, "fmat_pairs: cap above VS_FM_MAX_POINTS");
     ProfScope ps(ctx, "fmat_ransac", s);
-    hipLaunchKernelGGL(k_fmat<true>, dim3(P), dim3(256), 0, s, d_pairs, d_kps, cap, d_good, d_ngood, nullptr, nullptr,
+    hipLaunchKernelGGL(k_fmat<true>, dim3(P), dim3(kThreads), 0, s, d_pairs, d_kps, cap, d_good, d_ngood, nullptr, nullptr,
                        nullptr, 3.0, 0.999, 1000, d_F, nullptr, d_kept, d_nkept, d_err, d_diag);
     VS_HIP(hipGetLastError());
     return VS_OK;
@@ -294,10 +469,22 @@ int fmat_points(vs_ctx* ctx, int P, const float* d_p1, const float* d_p2, const 
                 int max_iters, double* d_F, uint8_t* d_mask, double* d_err, int* d_diag, hipStream_t s) {
     if (P <= 0) return VS_OK;
     ProfScope ps(ctx, "fmat_ransac", s);
-    hipLaunchKernelGGL(k_fmat<false>, dim3(P), dim3(256), 0, s, nullptr, nullptr, 0, nullptr, nullptr, d_p1, d_p2,
+    hipLaunchKernelGGL(k_fmat<false>, dim3(P), dim3(kThreads), 0, s, nullptr, nullptr, 0, nullptr, nullptr, d_p1, d_p2,
                        d_off, thr, conf, max_iters, d_F, d_mask, nullptr, nullptr, d_err, d_diag);
     VS_HIP(hipGetLastError());
     return VS_OK;
 }
 
 }  // namespace vs
+
+#ifdef VS_FM_PROFILE
+extern "C" int vs_debug_fm_cycles(unsigned long long* out, int reset) {
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(vs::g_fm_cycles), sizeof(unsigned long long) * 8) != hipSuccess)
+        return -1;
+    if (reset) {
+        unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(vs::g_fm_cycles), z, sizeof(z)) != hipSuccess) return -1;
+    }
+    return 0;
+}
+#endif

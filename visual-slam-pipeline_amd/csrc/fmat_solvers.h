@@ -160,19 +160,56 @@ VS_HD inline int run_7point(const float* x1, const float* y1, const float* x2, c
         a[i][7] = Y0;
         a[i][8] = 1;
     }
-    // null space of A: eigenvectors of A^T A for the two smallest eigenvalues
-    double AtA[81], w[9], V[81];
-    for (int r = 0; r < 9; r++)
-        for (int c = 0; c < 9; c++) {
-            double s = 0;
-            for (int i = 0; i < 7; i++) s += a[i][r] * a[i][c];
-            AtA[r * 9 + c] = s;
+    // 2-D null space of A by Gaussian elimination with partial pivoting (OpenCV takes the last two
+    // right singular vectors; any basis spans the same pencil and the F(3,3) = 1 normalisation
+    // below removes the basis).  Row swaps are selects so the unrolled matrix stays in registers.
+    VS_UNROLL
+    for (int k = 0; k < 7; k++) {
+        int p = k;
+        double big = fabs(a[k][k]);
+    VS_UNROLL
+        for (int r = k + 1; r < 7; r++) {
+            const double v = fabs(a[r][k]);
+            if (v > big) {
+                big = v;
+                p = r;
+            }
         }
-    vs_pnp::sym_eig<9>(AtA, w, V);
+        if (!(big > 1e-300)) return 0;  // rank-deficient subset
+    VS_UNROLL
+        for (int r = k + 1; r < 7; r++) {
+            const bool sw = r == p;
+    VS_UNROLL
+            for (int j = k; j < 9; j++) {
+                const double ak = a[k][j], ar = a[r][j];
+                a[k][j] = sw ? ar : ak;
+                a[r][j] = sw ? ak : ar;
+            }
+        }
+        const double inv = 1.0 / a[k][k];
+    VS_UNROLL
+        for (int r = k + 1; r < 7; r++) {
+            const double f = a[r][k] * inv;
+    VS_UNROLL
+            for (int j = k + 1; j < 9; j++) a[r][j] -= f * a[k][j];
+        }
+    }
+    // back substitution with the free unknowns (f[7], f[8]) = (1, 0) and (0, 1)
     double f1[9], f2[9];
-    for (int i = 0; i < 9; i++) {
-        f1[i] = V[i * 9 + 7];
-        f2[i] = V[i * 9 + 8];
+    f1[7] = 1;
+    f1[8] = 0;
+    f2[7] = 0;
+    f2[8] = 1;
+    VS_UNROLL
+    for (int k = 6; k >= 0; k--) {
+        double s1 = a[k][7], s2 = a[k][8];
+    VS_UNROLL
+        for (int j = k + 1; j < 7; j++) {
+            s1 += a[k][j] * f1[j];
+            s2 += a[k][j] * f2[j];
+        }
+        f1[k] = -s1 / a[k][k];
+        f2[k] = -s2 / a[k][k];
     }
     for (int i = 0; i < 9; i++) f1[i] -= f2[i];
     double c[4];
@@ -239,6 +276,28 @@ VS_HD inline float fm_error(const double* F, float x1, float y1, float x2, float
     const double d1 = x1 * a + y1 * b + c;
     const double e1 = d1 * d1 * s1, e2 = d2 * d2 * s2;
     return (float)(e1 > e2 ? e1 : e2);
+}
+
+// fm_error(F, ...) <= thr2, decided without the two divisions except within 1e-6 (relative) of
+// the gate, where the exact OpenCV rounding (double error, float cast) is evaluated.  Outside
+// that band the products' rounding (~1e-16) and the float cast (<= 6e-8) cannot change the
+// outcome, so the result is identical to the exact comparison for every input.
+VS_HD inline bool fm_inlier(const double* F, float x1, float y1, float x2, float y2, float thr2) {
+    double a = F[0] * x1 + F[1] * y1 + F[2];
+    double b = F[3] * x1 + F[4] * y1 + F[5];
+    double c = F[6] * x1 + F[7] * y1 + F[8];
+    const double q2 = a * a + b * b, d2 = x2 * a + y2 * b + c;
+    a = F[0] * x2 + F[3] * y2 + F[6];
+    b = F[1] * x2 + F[4] * y2 + F[7];
+    c = F[2] * x2 + F[5] * y2 + F[8];
+    const double q1 = a * a + b * b, d1 = x1 * a + y1 * b + c;
+    if (q1 > 0 && q2 > 0 && q1 < 1e300 && q2 < 1e300) {
+        const double e1 = d1 * d1, e2 = d2 * d2, t = thr2;
+        const double lo = t * (1.0 - 1e-6), hi = t * (1.0 + 1e-6);
+        if (e1 <= lo * q1 && e2 <= lo * q2) return true;
+        if (e1 >= hi * q1 || e2 >= hi * q2) return false;
+    }
+    return fm_error(F, x1, y1, x2, y2) <= thr2;
 }
 
 // one term of Slam::compute_epipolar_error (Slam.cpp:1226-1236); returns false when skipped

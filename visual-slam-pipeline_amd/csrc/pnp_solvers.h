@@ -23,8 +23,10 @@
 
 #if defined(__HIPCC__)
 #define VS_HD __host__ __device__
+#define VS_UNROLL _Pragma("unroll")
 #else
 #define VS_HD
+#define VS_UNROLL
 #endif
 
 namespace vs_pnp {
