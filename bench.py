@@ -46,14 +46,15 @@ LAYER_FLOPS = {
 
 # profiling stage -> kernel symbol (as rocprofv3 reports it) of that stage's dominant launch
 STAGE_KERNEL = {
-    "conv1_fused": "vs::k_conv_mfma<3, true, 1, true>",
-    "conv2a": "vs::k_conv_mfma<3, false, 2>",
-    "conv2b_pool": "vs::k_conv_mfma<3, true, 3>",
-    "conv3a": "vs::k_conv_mfma<3, false, 4>",
-    "conv3b_pool": "vs::k_conv_mfma<3, true, 5>",
-    "conv4a": "vs::k_conv_mfma<3, false, 6>",
-    "conv4b": "vs::k_conv_mfma<3, false, 7>",
-    "head_a": "vs::k_conv_mfma<3, false, 8>",
+    "conv1_fused": "vs::k_conv_mfma<3, true, 1, true, 16>",
+    "conv2a": "vs::k_conv_mfma<3, false, 2, false, 16>",
+    "conv2b_pool": "vs::k_conv_mfma<3, true, 3, false, 16>",
+    "conv3a": "vs::k_conv_mfma<3, false, 4, false, 16>",
+    "conv3b_pool": "vs::k_conv_mfma<3, true, 5, false, 16>",
+    "conv4a": "vs::k_conv_mfma<3, false, 6, false, 16>",
+    "conv4b": "vs::k_conv_mfma<3, false, 7, false, 16>",
+    "head_a": "vs::k_conv_mfma<3, false, 8, false, 16>",
+    "head_b": "vs::k_conv_mfma<1, false, 9, false, 32>",
 }
 
 
