@@ -83,6 +83,7 @@ int    vs_superpoint_save_weights(vs_ctx* ctx, const char* path);
  * row stride in bytes.  kps: cap records; desc: cap*256 floats; *n = keypoints written
  * (descending score order, reference NMS semantics).  cap must be >= 1; at most
  * min(cap, 400) keypoints are kept (SP_MAX_KEYPOINTS, Config.h:42). */
+#define VS_SP_MAX_KEYPOINTS 400
 int vs_extract(vs_ctx* ctx, const uint8_t* img, int h, int w, int channels, size_t stride,
                vs_keypoint* kps, float* desc, int cap, int* n);
 
@@ -200,11 +201,12 @@ int vs_solve_pnp_batch_dev(vs_ctx* ctx, int nprob, const float* d_obj, const flo
  * VS_FM_MAX_POINTS, interleaved xy fp32).  *ok = F non-empty (F row-major, F(3,3) = 1);
  * mask (n, nullable) = inliers (all 0 when F is empty); diag (nullable) = {method 0 none /
  * 1 seven-point / 2 RANSAC (n >= 15) / 3 LMedS (8..14), iterations run, winning iteration,
- * inliers}. */
+ * inliers}; err (nullable) = Slam::compute_epipolar_error over all points and over the inliers
+ * (0 when F is empty). */
 #define VS_FM_MAX_POINTS 2048
 int vs_find_fundamental(vs_ctx* ctx, const float* p1, const float* p2, int n, double thr,
                         double conf, int max_iters, double F[9], uint8_t* mask, int* ok,
-                        int diag[4]);
+                        int diag[4], double err[2]);
 /* Slam.cpp:880-910 for P frame pairs on device: matches d_good [p][cap] (query -> keypoints of
  * slot d_pairs[2p], train -> slot d_pairs[2p+1], d_kps [slot][cap]) are verified with
  * findFundamentalMat(FM_RANSAC, 3.0, 0.999); d_kept [p][cap] / d_nkept [p] = the surviving

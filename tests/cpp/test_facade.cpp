@@ -1,0 +1,168 @@
+// test_facade.cpp — exercises the C++ façade the way the reference's Slam uses FeatureExtractor,
+// match_features, the F verification, estimate_motion_3d3d, solve_pnp, track_local_map and
+// Optimizer::optimize_pose.  Built by `make -C visual-slam-pipeline_amd facade_test`, run on the
+// GPU by tests/test_gpu_facade.py.  Prints "FACADE OK" and exits 0 on success.
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "vslam_abi.h"
+#include "vslam_amd.hpp"
+
+using namespace vslam_amd;
+
+#define EXPECT(c)                                                       \
+    do {                                                                \
+        if (!(c)) {                                                     \
+            std::fprintf(stderr, "FAILED %s:%d: %s\n", __FILE__, __LINE__, #c); \
+            std::exit(1);                                               \
+        }                                                               \
+    } while (0)
+
+// smooth value-noise texture, BGR
+static float noise(int x, int y, int s) {
+    uint32_t h = (uint32_t)(x * 374761393 + y * 668265263 + s * 2246822519u);
+    h = (h ^ (h >> 13)) * 1274126177u;
+    return (float)((h ^ (h >> 16)) & 0xffff) / 65535.0f;
+}
+static float value_noise(float x, float y, int s) {
+    const int xi = (int)std::floor(x), yi = (int)std::floor(y);
+    const float fx = x - xi, fy = y - yi;
+    const float a = noise(xi, yi, s), b = noise(xi + 1, yi, s), c = noise(xi, yi + 1, s), d = noise(xi + 1, yi + 1, s);
+    return (a * (1 - fx) + b * fx) * (1 - fy) + (c * (1 - fx) + d * fx) * fy;
+}
+static std::vector<uint8_t> render(int w, int h, float dx, float dy) {
+    std::vector<uint8_t> img((size_t)w * h * 3);
+    for (int y = 0; y < h; y++)
+        for (int x = 0; x < w; x++) {
+            const float u = x + dx, v = y + dy;
+            const float t = 0.55f * value_noise(u / 23.f, v / 23.f, 1) + 0.3f * value_noise(u / 7.f, v / 7.f, 2) +
+                            0.15f * value_noise(u / 3.f, v / 3.f, 3);
+            const uint8_t g = (uint8_t)std::min(255.f, std::max(0.f, t * 255.f));
+            uint8_t* p = &img[((size_t)y * w + x) * 3];
+            p[0] = g;
+            p[1] = (uint8_t)(255 - g);
+            p[2] = (uint8_t)(g / 2 + 60);
+        }
+    return img;
+}
+
+int main() {
+    const int W = 640, H = 480;
+    const std::string cache = "/tmp/vslam_facade_test.spcf";
+    std::vector<uint8_t> im0 = render(W, H, 0, 0), im1 = render(W, H, 6, 3);
+    Image a{im0.data(), H, W, 3, (size_t)W * 3}, b{im1.data(), H, W, 3, (size_t)W * 3};
+
+    // ---- FeatureExtractor + SPCF cache (FeatureExtractor.cpp:49-81, 261-360) ----
+    FeatureExtractor fe;
+    EXPECT(fe.init(""));
+    EXPECT(fe.using_superpoint());
+    fe.set_cache_path(cache);
+    std::vector<KeyPoint> k0, k1;
+    Descriptors d0, d1;
+    fe.extract(a, k0, d0);
+    fe.extract(b, k1, d1);
+    EXPECT(k0.size() > 50 && k0.size() <= 400 && d0.rows == (int)k0.size());
+    {  // the façade returns exactly what the C ABI returns
+        std::vector<vs_keypoint> kc(400);
+        std::vector<float> dc(400 * 256);
+        int n = 0;
+        EXPECT(vs_extract(fe.context()->get(), im0.data(), H, W, 3, (size_t)W * 3, kc.data(), dc.data(), 400, &n) ==
+               VS_OK);
+        EXPECT(n == (int)k0.size());
+        EXPECT(std::memcmp(kc.data(), k0.data(), n * sizeof(vs_keypoint)) == 0);
+        EXPECT(std::memcmp(dc.data(), d0.data.data(), (size_t)n * 256 * 4) == 0);
+    }
+    EXPECT(fe.save_cache());
+    FeatureExtractor cached;  // never initialised: served from the cache only
+    cached.set_cache_path(cache);
+    EXPECT(cached.load_cache() && cached.cache_active() && cached.cache_size() == 2);
+    std::vector<KeyPoint> c0;
+    Descriptors cd0;
+    cached.extract(a, c0, cd0);
+    EXPECT(c0.size() == k0.size() && std::memcmp(c0.data(), k0.data(), k0.size() * sizeof(KeyPoint)) == 0);
+    EXPECT(cd0.data == d0.data);
+    cached.extract(b, c0, cd0);
+    bool threw = false;
+    try {
+        cached.extract(a, c0, cd0);  // index 2: cache miss and no GPU context -> fails loudly
+    } catch (const Error&) {
+        threw = true;
+    }
+    EXPECT(threw);
+
+    Context& ctx = *fe.context();
+    // ---- match_features + F verification (Slam.cpp:838-910) ----
+    std::vector<DMatch> raw;
+    std::vector<DMatch> good = match_features(ctx, d0, d1, &raw);
+    EXPECT(raw.size() == k0.size() && good.size() > 20 && good.size() <= raw.size());
+    std::vector<Point2f> p1, p2;
+    extract_matched_points(k0, k1, good, p1, p2);
+    const size_t n_good = good.size();
+    FundamentalResult fr = verify_fundamental(ctx, p1, p2, good);
+    EXPECT(fr.has_F && good.size() == p1.size() && good.size() <= n_good && good.size() >= 15);
+    EXPECT(fr.epipolar_error_after <= fr.epipolar_error_before);
+    // image shift (6, 3): a pure translation, matched points move by it
+    int shifted = 0;
+    for (size_t i = 0; i < p1.size(); i++)
+        shifted += std::fabs(p1[i].x - p2[i].x - 6.f) < 1.5f && std::fabs(p1[i].y - p2[i].y - 3.f) < 1.5f;
+    EXPECT(shifted >= (int)(0.8 * p1.size()));
+
+    // ---- estimate_motion_3d3d on a fronto-parallel plane at 2 m (Slam.cpp:214-375) ----
+    std::vector<float> plane((size_t)W * H, 2.0f);
+    DepthImage dp{plane.data(), H, W};
+    Mat33 R;
+    Vec3 t;
+    EXPECT(estimate_motion_3d3d(ctx, p1, p2, dp, dp, 42, R, t));
+    EXPECT(std::fabs(R[0] - 1) < 1e-2 && std::fabs(R[4] - 1) < 1e-2 && std::fabs(R[8] - 1) < 1e-2);
+    EXPECT(std::fabs(t[0] - (-6.0 * 2.0 / 525.0)) < 0.01 && std::fabs(t[1] - (-3.0 * 2.0 / 525.0)) < 0.01);
+
+    // ---- solve_pnp (Slam.cpp:505-529) on the plane's points seen by the second frame ----
+    std::vector<Point3f> obj;
+    std::vector<Point2f> img;
+    for (size_t i = 0; i < p1.size(); i++) {
+        const double z = 2.0;
+        obj.push_back({(float)((p1[i].x - 319.5) * z / 525.0), (float)((p1[i].y - 239.5) * z / 525.0), (float)z});
+        img.push_back(p2[i]);
+    }
+    PnPResult pnp = solve_pnp(ctx, obj, img, 100, 10);
+    EXPECT(pnp.success && pnp.inlier_count >= (int)(0.8 * obj.size()));
+    // camera moved by +(6, 3) px * z / f in x, y
+    EXPECT(std::fabs(pnp.t_world[0] - 6.0 * 2.0 / 525.0) < 0.01 && std::fabs(pnp.t_world[1] - 3.0 * 2.0 / 525.0) < 0.01);
+
+    // ---- Optimizer::optimize_pose from a perturbed pose (Optimizer.cpp:54-180) ----
+    std::vector<Point3d> P3;
+    for (const auto& o : obj) P3.push_back({o.x, o.y, o.z});
+    Mat33 Ro = pnp.R_world;
+    Vec3 to = {pnp.t_world[0] + 0.02, pnp.t_world[1] - 0.01, pnp.t_world[2] + 0.03};
+    Optimizer opt(ctx);
+    auto rms = opt.optimize_pose(Ro, to, P3, img);
+    EXPECT(rms.first > rms.second && rms.second < 2.0);
+
+    // ---- track_local_map: frame-0 keypoints as map points, tracked into frame 1 ----
+    std::vector<double> pos;
+    std::vector<float> mdesc;
+    std::vector<uint8_t> valid;
+    for (size_t i = 0; i < k0.size(); i++) {
+        const double z = 2.0;
+        pos.push_back((k0[i].pt.x - 319.5) * z / 525.0);
+        pos.push_back((k0[i].pt.y - 239.5) * z / 525.0);
+        pos.push_back(z);
+        mdesc.insert(mdesc.end(), d0.row((int)i), d0.row((int)i) + 256);
+        valid.push_back(1);
+    }
+    MapPointsView map{pos.data(), mdesc.data(), valid.data(), (int)k0.size()};
+    std::vector<int> kp_to_mp;
+    std::vector<std::pair<int, int>> obs;
+    const Mat33 I3 = {1, 0, 0, 0, 1, 0, 0, 0, 1};
+    const int tracked = track_local_map(ctx, map, k1, d1, I3, pnp.t_world, kp_to_mp, &obs);
+    EXPECT(tracked > 20 && (int)obs.size() == tracked && kp_to_mp.size() == k1.size());
+
+    std::remove(cache.c_str());
+    std::printf("FACADE OK keypoints=%zu good=%zu F-kept=%zu pnp_inliers=%d tracked=%d rms=%.4f->%.4f\n",
+                k0.size(), n_good, good.size(), pnp.inlier_count, tracked, rms.first, rms.second);
+    return 0;
+}

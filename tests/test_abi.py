@@ -40,3 +40,20 @@ def test_record_layouts_match_opencv():
     assert vslam_abi.KEYPOINT_DTYPE.itemsize == 28
     # cv::DMatch: int queryIdx, trainIdx, imgIdx, float distance
     assert vslam_abi.MATCH_DTYPE.itemsize == 16
+
+
+@pytest.mark.skipif(not os.path.exists(vslam_abi.LIB_PATH), reason="libvslam_hip.so not built")
+def test_cpp_facade_builds_and_links():
+    # the C++ host façade (host/vslam_amd.hpp) compiles against the C ABI and links the library;
+    # running it needs the GPU (tests/test_gpu_facade.py)
+    import subprocess
+    pkg = os.path.dirname(vslam_abi.LIB_PATH)
+    subprocess.run(["make", "-C", pkg, "-s", "facade_test"], check=True)
+    assert os.path.exists(os.path.join(pkg, "facade_test"))
+    lib = ctypes.CDLL(vslam_abi.LIB_PATH)
+    # façade symbols live in the same library (namespace vslam_amd)
+    out = subprocess.run(["nm", "-DC", vslam_abi.LIB_PATH], capture_output=True, text=True).stdout
+    for sym in ["vslam_amd::FeatureExtractor::extract", "vslam_amd::match_features", "vslam_amd::solve_pnp",
+                "vslam_amd::verify_fundamental", "vslam_amd::Optimizer::optimize_pose"]:
+        assert sym in out, sym
+    del lib

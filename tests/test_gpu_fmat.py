@@ -13,8 +13,8 @@ from test_oracle_fmat import two_view
 pytestmark = pytest.mark.gpu
 
 
-def _cmp_find(g, o, n):
-    ok_g, F_g, m_g, d_g = g
+def _cmp_find(g, o, n, p1=None, p2=None, oracle=None):
+    ok_g, F_g, m_g, d_g, err_g = g
     ok_o, F_o, m_o, d_o = o
     assert d_g[0] == d_o[0]
     if d_o[0] == 3 and n <= 13:
@@ -24,6 +24,12 @@ def _cmp_find(g, o, n):
     if ok_o:
         assert np.array_equal(m_g, m_o)
         assert np.max(np.abs(F_g - F_o)) <= 1e-9 * np.abs(F_o).max()
+        if oracle is not None:  # Slam::compute_epipolar_error over all points and over the inliers
+            e_all = oracle.epipolar_error(p1, p2, F_o)
+            e_in = oracle.epipolar_error(p1[m_o], p2[m_o], F_o)
+            assert np.allclose(err_g, [e_all, e_in], rtol=1e-7, atol=0)  # F agrees to 1e-9 rel
+    else:
+        assert (err_g == 0).all()
 
 
 @pytest.mark.parametrize("n,seed,noise,out", [(60, 0, 0.0, 0.0), (150, 1, 0.5, 0.3), (400, 2, 1.0, 0.5),
@@ -31,7 +37,7 @@ def _cmp_find(g, o, n):
                                               (14, 6, 0.5, 0.0), (10, 7, 0.5, 0.0), (7, 8, 0.0, 0.0)])
 def test_find_fundamental_matches_oracle(vsctx, oracle, n, seed, noise, out):
     p1, p2, F, outl = two_view(n, seed, noise, out)
-    _cmp_find(vsctx.find_fundamental(p1, p2), oracle.find_fundamental(p1, p2), n)
+    _cmp_find(vsctx.find_fundamental(p1, p2), oracle.find_fundamental(p1, p2), n, p1, p2, oracle)
 
 
 def test_find_fundamental_edges(vsctx, oracle):

@@ -208,7 +208,8 @@ def test_device_pipeline_matches_host_entry_points(vsctx, seq4):
         p1 = np.stack([k1["x"][good["query_idx"]], k1["y"][good["query_idx"]]], 1)
         p2 = np.stack([k2["x"][good["train_idx"]], k2["y"][good["train_idx"]]], 1)
         # F verification (Slam.cpp:880-910) filters the matches before the 3D-3D stage
-        okf, F, fmask, fdiag = vsctx.find_fundamental(p1, p2)
+        okf, F, fmask, fdiag, ferr = vsctx.find_fundamental(p1, p2)
+        assert np.allclose(out["eperr"][p].cpu().numpy(), ferr, rtol=1e-12, atol=0)
         keep = np.flatnonzero(fmask) if okf else np.arange(len(good))
         assert nkept[p] == len(keep)
         assert np.array_equal(kept_all[p].view(good.dtype)[:nkept[p]], good[keep])

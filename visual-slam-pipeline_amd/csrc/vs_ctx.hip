@@ -648,7 +648,7 @@ int vs_fmat_verify_pairs_dev(vs_ctx* ctx, int P, const int* d_pairs, const vs_ke
 }
 
 int vs_find_fundamental(vs_ctx* ctx, const float* p1, const float* p2, int n, double thr, double conf, int max_iters,
-                        double F[9], uint8_t* mask, int* ok, int diag[4]) {
+                        double F[9], uint8_t* mask, int* ok, int diag[4], double err[2]) {
     VS_ARG(ctx && F && ok, "vs_find_fundamental: null argument");
     VS_ARG(n >= 0 && n <= VS_FM_MAX_POINTS && (n == 0 || (p1 && p2)), "vs_find_fundamental: bad points");
     // findFundamentalMat's argument defaults (fundam.cpp)
@@ -656,6 +656,7 @@ int vs_find_fundamental(vs_ctx* ctx, const float* p1, const float* p2, int n, do
     if (conf < DBL_EPSILON || conf > 1 - DBL_EPSILON) conf = 0.99;
     *ok = 0;
     if (diag) diag[0] = diag[1] = diag[3] = 0, diag[2] = -1;
+    if (err) err[0] = err[1] = 0;
     if (n == 0) return VS_OK;
     VS_HIP(hipSetDevice(ctx->device));
     hipStream_t s = ctx->stream;
@@ -669,14 +670,18 @@ int vs_find_fundamental(vs_ctx* ctx, const float* p1, const float* p2, int n, do
     VS_HIP(hipMemcpyAsync(dmeta, off, sizeof(off), hipMemcpyHostToDevice, s));
     VS_CHECK(fmat_points(ctx, 1, ctx->h_aux0.as<float>(), ctx->h_aux1.as<float>(), dmeta, thr, conf, max_iters, dF,
                          dmask, dF + 9, dmeta + 2, s));
-    double Fh[9];
+    double Fh[11];  // F, err
     int dg[8];
     VS_HIP(hipMemcpyAsync(Fh, dF, sizeof(Fh), hipMemcpyDeviceToHost, s));
     VS_HIP(hipMemcpyAsync(dg, dmeta + 2, sizeof(dg), hipMemcpyDeviceToHost, s));
     if (mask) VS_HIP(hipMemcpyAsync(mask, dmask, (size_t)n, hipMemcpyDeviceToHost, s));
     VS_HIP(hipStreamSynchronize(s));
     *ok = dg[4];
-    std::memcpy(F, Fh, sizeof(Fh));
+    std::memcpy(F, Fh, 9 * sizeof(double));
+    if (err) {
+        err[0] = Fh[9];
+        err[1] = Fh[10];
+    }
     if (diag) {
         diag[0] = dg[0];
         diag[1] = dg[1];

@@ -1,0 +1,270 @@
+// vslam_amd.cpp — C++ façade over the C ABI (see vslam_amd.hpp).  Only bookkeeping lives here
+// (argument marshalling, the SPCF cache file, match filtering); all compute is in libvslam_hip.so.
+#include "vslam_amd.hpp"
+
+#include <algorithm>
+#include <cstring>
+#include <fstream>
+
+#include "vslam_abi.h"
+
+static_assert(sizeof(vslam_amd::KeyPoint) == sizeof(vs_keypoint), "KeyPoint must match vs_keypoint");
+static_assert(sizeof(vslam_amd::DMatch) == sizeof(vs_match), "DMatch must match vs_match");
+
+namespace vslam_amd {
+
+namespace {
+
+void check(int rc, const char* where) {
+    if (rc != VS_OK) throw Error(rc, std::string(where) + ": " + vs_last_error());
+}
+
+std::array<double, 4> kvec(const Intrinsics& K) { return {K.fx, K.fy, K.cx, K.cy}; }
+
+}  // namespace
+
+// ---------------------------------------------------------------------------------- Context
+Context::Context(int device, const std::string& weights_path) {
+    check(vs_create(device, weights_path.empty() ? nullptr : weights_path.c_str(), &h_), "vs_create");
+}
+
+Context::~Context() {
+    if (h_) vs_destroy(h_);
+}
+
+// ------------------------------------------------------------------------- FeatureExtractor
+FeatureExtractor::FeatureExtractor() = default;
+FeatureExtractor::~FeatureExtractor() = default;
+
+bool FeatureExtractor::init(const std::string& model_path, int device) {
+    try {
+        ctx_ = std::make_unique<Context>(device, model_path);
+        return true;
+    } catch (const Error&) {
+        ctx_.reset();
+        return false;
+    }
+}
+
+// FeatureExtractor::extract (FeatureExtractor.cpp:49-81): cache hit by sequential index, else
+// extract on the GPU and remember the result when a cache path is set.
+void FeatureExtractor::extract(const Image& image, std::vector<KeyPoint>& keypoints, Descriptors& descriptors) {
+    const int idx = extract_counter_++;
+    if (cache_loaded_) {
+        auto it = cache_.find(idx);
+        if (it != cache_.end()) {
+            keypoints = it->second.keypoints;
+            descriptors = it->second.descriptors;
+            return;
+        }
+    }
+    if (!ctx_) throw Error(VS_ERR_ARG, "FeatureExtractor::extract: not initialised (init() failed or not called)");
+    const int cap = VS_SP_MAX_KEYPOINTS;
+    keypoints.resize(cap);
+    descriptors.data.resize((size_t)cap * Descriptors::kCols);
+    int n = 0;
+    check(vs_extract(ctx_->get(), image.data, image.rows, image.cols, image.channels,
+                     image.step ? image.step : (size_t)image.cols * image.channels,
+                     reinterpret_cast<vs_keypoint*>(keypoints.data()), descriptors.data.data(), cap, &n),
+          "vs_extract");
+    keypoints.resize(n);
+    descriptors.rows = n;
+    descriptors.data.resize((size_t)n * Descriptors::kCols);
+    if (!cache_path_.empty()) cache_[idx] = CachedFeatures{keypoints, descriptors};
+}
+
+// SPCF cache file (FeatureExtractor.cpp:261-360): "SPCF" magic, version 1, entry count, then per
+// entry frame index, keypoint count, 7 x 4-byte keypoint fields, rows / cols / type (CV_32F = 5)
+// and the raw descriptor rows.
+bool FeatureExtractor::load_cache() {
+    if (cache_path_.empty()) return false;
+    std::ifstream ifs(cache_path_, std::ios::binary);
+    if (!ifs.is_open()) return false;
+    uint32_t magic = 0, version = 0, num_entries = 0;
+    ifs.read(reinterpret_cast<char*>(&magic), 4);
+    ifs.read(reinterpret_cast<char*>(&version), 4);
+    ifs.read(reinterpret_cast<char*>(&num_entries), 4);
+    if (!ifs || magic != 0x53504346u || version != 1) return false;
+    std::unordered_map<int, CachedFeatures> cache;
+    for (uint32_t e = 0; e < num_entries; e++) {
+        int32_t frame_idx = 0, num_kp = 0, rows = 0, cols = 0, type = 0;
+        ifs.read(reinterpret_cast<char*>(&frame_idx), 4);
+        ifs.read(reinterpret_cast<char*>(&num_kp), 4);
+        if (!ifs || num_kp < 0) return false;
+        CachedFeatures cf;
+        cf.keypoints.resize(num_kp);
+        ifs.read(reinterpret_cast<char*>(cf.keypoints.data()), (std::streamsize)num_kp * sizeof(KeyPoint));
+        ifs.read(reinterpret_cast<char*>(&rows), 4);
+        ifs.read(reinterpret_cast<char*>(&cols), 4);
+        ifs.read(reinterpret_cast<char*>(&type), 4);
+        if (!ifs) return false;
+        if (rows > 0 && cols > 0) {
+            if (cols != Descriptors::kCols || type != 5) return false;  // SuperPoint CV_32F rows
+            cf.descriptors.rows = rows;
+            cf.descriptors.data.resize((size_t)rows * cols);
+            ifs.read(reinterpret_cast<char*>(cf.descriptors.data.data()), (std::streamsize)rows * cols * 4);
+            if (!ifs) return false;
+        }
+        cache[frame_idx] = std::move(cf);
+    }
+    cache_ = std::move(cache);
+    cache_loaded_ = true;
+    return true;
+}
+
+bool FeatureExtractor::save_cache() {
+    if (cache_path_.empty() || cache_.empty()) return false;
+    std::ofstream ofs(cache_path_, std::ios::binary);
+    if (!ofs.is_open()) return false;
+    const uint32_t magic = 0x53504346u, version = 1, num_entries = (uint32_t)cache_.size();
+    ofs.write(reinterpret_cast<const char*>(&magic), 4);
+    ofs.write(reinterpret_cast<const char*>(&version), 4);
+    ofs.write(reinterpret_cast<const char*>(&num_entries), 4);
+    std::vector<int> indices;
+    indices.reserve(cache_.size());
+    for (const auto& kv : cache_) indices.push_back(kv.first);
+    std::sort(indices.begin(), indices.end());
+    for (int idx : indices) {
+        const CachedFeatures& cf = cache_.at(idx);
+        const int32_t frame_idx = idx, num_kp = (int32_t)cf.keypoints.size();
+        ofs.write(reinterpret_cast<const char*>(&frame_idx), 4);
+        ofs.write(reinterpret_cast<const char*>(&num_kp), 4);
+        ofs.write(reinterpret_cast<const char*>(cf.keypoints.data()), (std::streamsize)num_kp * sizeof(KeyPoint));
+        const int32_t rows = cf.descriptors.rows, cols = rows > 0 ? Descriptors::kCols : 0, type = rows > 0 ? 5 : 0;
+        ofs.write(reinterpret_cast<const char*>(&rows), 4);
+        ofs.write(reinterpret_cast<const char*>(&cols), 4);
+        ofs.write(reinterpret_cast<const char*>(&type), 4);
+        if (rows > 0)
+            ofs.write(reinterpret_cast<const char*>(cf.descriptors.data.data()), (std::streamsize)rows * cols * 4);
+    }
+    return (bool)ofs;
+}
+
+// ------------------------------------------------------------------------------ Slam methods
+std::vector<DMatch> match_features(Context& ctx, const Descriptors& desc1, const Descriptors& desc2,
+                                   std::vector<DMatch>* raw_matches_out) {
+    std::vector<DMatch> raw(std::max(desc1.rows, 1)), good(std::max(desc1.rows, 1));
+    int n_raw = 0, n_good = 0;
+    check(vs_match_ratio(ctx.get(), desc1.data.data(), desc1.rows, desc2.data.data(), desc2.rows, 0.75f,
+                         reinterpret_cast<vs_match*>(raw.data()), &n_raw, reinterpret_cast<vs_match*>(good.data()),
+                         &n_good),
+          "vs_match_ratio");
+    raw.resize(n_raw);
+    good.resize(n_good);
+    if (raw_matches_out) *raw_matches_out = std::move(raw);
+    return good;
+}
+
+void extract_matched_points(const std::vector<KeyPoint>& kp1, const std::vector<KeyPoint>& kp2,
+                            const std::vector<DMatch>& matches, std::vector<Point2f>& pts1,
+                            std::vector<Point2f>& pts2) {
+    pts1.clear();
+    pts2.clear();
+    pts1.reserve(matches.size());
+    pts2.reserve(matches.size());
+    for (const auto& m : matches) {
+        pts1.push_back(kp1[m.queryIdx].pt);
+        pts2.push_back(kp2[m.trainIdx].pt);
+    }
+}
+
+FundamentalResult verify_fundamental(Context& ctx, std::vector<Point2f>& pts1, std::vector<Point2f>& pts2,
+                                     std::vector<DMatch>& good_matches) {
+    FundamentalResult r;
+    const int n = (int)pts1.size();
+    if (pts2.size() != pts1.size() || good_matches.size() != pts1.size())
+        throw Error(VS_ERR_ARG, "verify_fundamental: pts1 / pts2 / good_matches sizes differ");
+    r.mask.assign(std::max(n, 1), 0);
+    int ok = 0, diag[4];
+    double err[2];
+    check(vs_find_fundamental(ctx.get(), reinterpret_cast<const float*>(pts1.data()),
+                              reinterpret_cast<const float*>(pts2.data()), n, 3.0, 0.999, 1000, r.F.data(),
+                              r.mask.data(), &ok, diag, err),
+          "vs_find_fundamental");
+    r.mask.resize(n);
+    r.has_F = ok != 0;
+    if (!r.has_F) return r;  // Slam.cpp:887, 892: nothing filtered without F
+    r.epipolar_error_before = err[0];
+    r.epipolar_error_after = err[1];
+    size_t w = 0;
+    for (int i = 0; i < n; i++)
+        if (r.mask[i]) {
+            pts1[w] = pts1[i];
+            pts2[w] = pts2[i];
+            good_matches[w] = good_matches[i];
+            w++;
+        }
+    pts1.resize(w);
+    pts2.resize(w);
+    good_matches.resize(w);
+    return r;
+}
+
+bool estimate_motion_3d3d(Context& ctx, const std::vector<Point2f>& pts1, const std::vector<Point2f>& pts2,
+                          const DepthImage& depth1, const DepthImage& depth2, uint32_t seed, Mat33& R_out,
+                          Vec3& t_out) {
+    if (pts1.size() != pts2.size()) throw Error(VS_ERR_ARG, "estimate_motion_3d3d: point counts differ");
+    if (depth1.rows != depth2.rows || depth1.cols != depth2.cols)
+        throw Error(VS_ERR_ARG, "estimate_motion_3d3d: depth sizes differ");
+    const auto K = kvec(ctx.K());
+    int ok = 0, diag[4];
+    check(vs_ransac_3d3d(ctx.get(), reinterpret_cast<const float*>(pts1.data()),
+                         reinterpret_cast<const float*>(pts2.data()), (int)pts1.size(), depth1.data, depth2.data,
+                         depth1.rows, depth1.cols, K.data(), seed, 200, 0.05, R_out.data(), t_out.data(), &ok,
+                         diag),
+          "vs_ransac_3d3d");
+    return ok != 0;
+}
+
+PnPResult solve_pnp(Context& ctx, const std::vector<Point3f>& obj_pts, const std::vector<Point2f>& img_pts,
+                    int ransac_iters, int min_inliers) {
+    if (obj_pts.size() != img_pts.size()) throw Error(VS_ERR_ARG, "solve_pnp: point counts differ");
+    PnPResult r;
+    const auto K = kvec(ctx.K());
+    int success = 0;
+    check(vs_solve_pnp(ctx.get(), reinterpret_cast<const float*>(obj_pts.data()),
+                       reinterpret_cast<const float*>(img_pts.data()), (int)obj_pts.size(), K.data(), ransac_iters,
+                       min_inliers, r.R_world.data(), r.t_world.data(), &success, &r.inlier_count, nullptr,
+                       nullptr),
+          "vs_solve_pnp");
+    r.success = success != 0;
+    return r;
+}
+
+int track_local_map(Context& ctx, const MapPointsView& map, const std::vector<KeyPoint>& keypoints,
+                    const Descriptors& descriptors, const Mat33& R_world, const Vec3& t_world,
+                    std::vector<int>& map_point_indices, std::vector<std::pair<int, int>>* observations, int img_w,
+                    int img_h) {
+    const int n_kp = (int)keypoints.size();
+    if (descriptors.rows != n_kp) throw Error(VS_ERR_ARG, "track_local_map: descriptor rows != keypoints");
+    map_point_indices.resize(n_kp, -1);
+    const auto K = kvec(ctx.K());
+    int tracked = 0, n_obs = 0;
+    const int obs_cap = n_kp;  // at most one observation per keypoint
+    std::vector<int> obs_mp(std::max(obs_cap, 1)), obs_kp(std::max(obs_cap, 1));
+    check(vs_track_local_map(ctx.get(), map.pos, map.desc, map.valid, map.n,
+                             reinterpret_cast<const vs_keypoint*>(keypoints.data()), descriptors.data.data(), n_kp,
+                             R_world.data(), t_world.data(), K.data(), img_w, img_h, map_point_indices.data(),
+                             &tracked, obs_mp.data(), obs_kp.data(), obs_cap, &n_obs),
+          "vs_track_local_map");
+    if (observations) {
+        observations->clear();
+        for (int i = 0; i < std::min(n_obs, obs_cap); i++) observations->emplace_back(obs_mp[i], obs_kp[i]);
+    }
+    return tracked;
+}
+
+std::pair<double, double> Optimizer::optimize_pose(Mat33& R_world, Vec3& t_world,
+                                                   const std::vector<Point3d>& points_3d,
+                                                   const std::vector<Point2f>& points_2d) {
+    if (points_3d.size() != points_2d.size()) throw Error(VS_ERR_ARG, "optimize_pose: point counts differ");
+    const auto K = kvec(ctx_.K());
+    double before = 0, after = 0;
+    check(vs_optimize_pose(ctx_.get(), reinterpret_cast<const double*>(points_3d.data()),
+                           reinterpret_cast<const float*>(points_2d.data()), (int)points_3d.size(), K.data(),
+                           R_world.data(), t_world.data(), &before, &after),
+          "vs_optimize_pose");
+    return {before, after};
+}
+
+}  // namespace vslam_amd

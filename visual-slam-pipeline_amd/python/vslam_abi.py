@@ -53,7 +53,7 @@ _SIG = {
     "vs_optimize_pose_batch_dev": (_I, [_P, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
     "vs_solve_pnp": (_I, [_P, _P, _P, _I, _P, _I, _I, _P, _P, _P, _P, _P, _P]),
     "vs_solve_pnp_batch_dev": (_I, [_P, _I, _P, _P, _P, _P, _I, _I, _P, _P, _P, _P, _P]),
-    "vs_find_fundamental": (_I, [_P, _P, _P, _I, ctypes.c_double, ctypes.c_double, _I, _P, _P, _P, _P]),
+    "vs_find_fundamental": (_I, [_P, _P, _P, _I, ctypes.c_double, ctypes.c_double, _I, _P, _P, _P, _P, _P]),
     "vs_fmat_verify_pairs_dev": (_I, [_P, _I, _P, _P, _I, _P, _P, _P, _P, _P, _P, _P, _P]),
     "vs_profile_enable": (_I, [_P, _I]),
     "vs_profile_reset": (_I, [_P]),
@@ -278,7 +278,7 @@ class Context:
 
     # ---- cv::findFundamentalMat (FM_RANSAC) ----
     def find_fundamental(self, p1, p2, thr=3.0, conf=0.999, max_iters=1000):
-        """Returns (ok, F 3x3, inlier mask, diag)."""
+        """Returns (ok, F 3x3, inlier mask, diag, [epipolar error all, inliers])."""
         a = np.ascontiguousarray(p1, np.float32).reshape(-1, 2)
         b = np.ascontiguousarray(p2, np.float32).reshape(-1, 2)
         n = a.shape[0]
@@ -286,9 +286,10 @@ class Context:
         mask = np.zeros(max(n, 1), np.uint8)
         ok = ctypes.c_int(0)
         diag = np.zeros(4, np.int32)
+        err = np.zeros(2, np.float64)
         _check(self.lib.vs_find_fundamental(self.h, _ptr(a), _ptr(b), n, thr, conf, max_iters, _ptr(F), _ptr(mask),
-                                            ctypes.byref(ok), _ptr(diag)))
-        return bool(ok.value), F.reshape(3, 3), mask[:n].astype(bool), diag
+                                            ctypes.byref(ok), _ptr(diag), _ptr(err)))
+        return bool(ok.value), F.reshape(3, 3), mask[:n].astype(bool), diag, err
 
     def fmat_verify_pairs_dev(self, P, d_pairs, d_kps, cap, d_good, d_ngood, d_F, d_kept, d_nkept, d_err, d_diag,
                               stream=None):

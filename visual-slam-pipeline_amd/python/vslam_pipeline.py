@@ -27,6 +27,45 @@ KP_BYTES = va.KEYPOINT_DTYPE.itemsize
 M_BYTES = va.MATCH_DTYPE.itemsize
 
 
+class FeatureExchange:
+    """Per-step interchange of per-frame feature records among frame-sharded ranks (SURVEY.md
+    8(e)).  Rank r extracts frames [rB, (r+1)B) of each step into slots 1..B of its tables; after
+    exchange() every rank holds the whole step's records (g_kps / g_desc / g_n, global frame
+    order) and slot 0 of its tables holds frame rB-1: rank r-1's last frame, or for rank 0 the
+    previous step's global last frame (count 0 before the first step).  Device-agnostic: the same
+    code runs over RCCL on MI355X and over gloo in the CPU tests."""
+
+    def __init__(self, B, cap, rank, world, group=None, device=None):
+        self.B, self.cap, self.rank, self.world, self.group = B, cap, rank, world, group
+        self.g_kps = torch.zeros((world * B, cap * KP_BYTES), dtype=torch.uint8, device=device)
+        self.g_desc = torch.zeros((world * B, cap, 256), dtype=torch.float32, device=device)
+        self.g_n = torch.zeros(world * B, dtype=torch.int32, device=device)
+        self.carry_kps = torch.zeros(cap * KP_BYTES, dtype=torch.uint8, device=device)
+        self.carry_desc = torch.zeros((cap, 256), dtype=torch.float32, device=device)
+        self.carry_n = torch.zeros((), dtype=torch.int32, device=device)
+
+    def exchange(self, kps, desc, n):
+        """kps (B+1, cap*28) u8, desc (B+1, cap, 256) f32, n (B+1,) i32; slots 1..B are this rank's
+        frames.  Fills slot 0 and returns the gathered step tables."""
+        import torch.distributed as dist
+        dist.all_gather_into_tensor(self.g_n, n[1:], group=self.group)
+        dist.all_gather_into_tensor(self.g_kps, kps[1:], group=self.group)
+        dist.all_gather_into_tensor(self.g_desc, desc[1:], group=self.group)
+        if self.rank > 0:
+            j = self.rank * self.B - 1
+            kps[0].copy_(self.g_kps[j])
+            desc[0].copy_(self.g_desc[j])
+            n[0].copy_(self.g_n[j])
+        else:
+            kps[0].copy_(self.carry_kps)
+            desc[0].copy_(self.carry_desc)
+            n[0].copy_(self.carry_n)
+        self.carry_kps.copy_(self.g_kps[-1])
+        self.carry_desc.copy_(self.g_desc[-1])
+        self.carry_n.copy_(self.g_n[-1])
+        return self.g_kps, self.g_desc, self.g_n
+
+
 class DevicePipeline:
     def __init__(self, ctx, B, h=480, w=640, cap=va.SP_MAX_KEYPOINTS, K=va.K_TUM, iters=200, thr=0.05,
                  ratio=0.75, rank=0, world=1, group=None):
@@ -56,19 +95,7 @@ class DevicePipeline:
         self.diag = torch.zeros((P, 4), dtype=torch.int32, device=dev)
         self.seeds = torch.zeros(P, dtype=torch.int32, device=dev)
         self._seed_base = torch.arange(P, dtype=torch.int64, device=dev)
-        if world > 1:
-            self.g_kps = torch.zeros((world * B, cap * KP_BYTES), dtype=torch.uint8, device=dev)
-            self.g_desc = torch.zeros((world * B, cap, 256), dtype=torch.float32, device=dev)
-            self.g_n = torch.zeros(world * B, dtype=torch.int32, device=dev)
-            self.carry_kps = torch.zeros(cap * KP_BYTES, dtype=torch.uint8, device=dev)
-            self.carry_desc = torch.zeros((cap, 256), dtype=torch.float32, device=dev)
-            self.carry_n = torch.zeros((), dtype=torch.int32, device=dev)
-
-    def _allgather_features(self):
-        import torch.distributed as dist
-        dist.all_gather_into_tensor(self.g_n, self.n[1:], group=self.group)
-        dist.all_gather_into_tensor(self.g_kps, self.kps[1:], group=self.group)
-        dist.all_gather_into_tensor(self.g_desc, self.desc[1:], group=self.group)
+        self.xchg = FeatureExchange(B, cap, rank, world, group, dev) if world > 1 else None
 
     def run(self, frames, depth, frame_count0, depth_prev=None):
         """frames: (B, h, w, 3) uint8 cuda, depth: (B, h, w) float32 cuda, frame_count0: global
@@ -91,22 +118,8 @@ class DevicePipeline:
         ctx.extract_batch_dev(B, frames.data_ptr(), h, w, self.kps[1:].data_ptr(), self.desc[1:].data_ptr(),
                               self.n[1:].data_ptr(), cap, s)
         if self.world > 1:
-            self._allgather_features()
-            # neighbour frame before this block: rank-1's last frame, or (rank 0) the previous
-            # step's global last frame, which is still in slot 0's gathered copy from last step
-            if self.rank > 0:
-                j = self.rank * B - 1
-                self.kps[0].copy_(self.g_kps[j])
-                self.desc[0].copy_(self.g_desc[j])
-                self.n[0].copy_(self.g_n[j])
-            else:
-                # slot 0 of rank 0 still holds the previous step's global last frame (or n = 0)
-                self.kps[0].copy_(self.carry_kps)
-                self.desc[0].copy_(self.carry_desc)
-                self.n[0].copy_(self.carry_n)
-            self.carry_kps.copy_(self.g_kps[-1])
-            self.carry_desc.copy_(self.g_desc[-1])
-            self.carry_n.copy_(self.g_n[-1])
+            # all-gather the step's feature records; slot 0 <- frame rank*B - 1
+            self.xchg.exchange(self.kps, self.desc, self.n)
         self.seeds.copy_((self._seed_base + (42 + frame_count0)).to(torch.int32))
         ctx.match_pairs_dev(B, self.pairs.data_ptr(), B + 1, self.desc.data_ptr(), self.n.data_ptr(), cap,
                             self.ratio, self.raw.data_ptr(), self.nraw.data_ptr(), self.good.data_ptr(),
