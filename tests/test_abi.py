@@ -57,3 +57,25 @@ def test_cpp_facade_builds_and_links():
                 "vslam_amd::verify_fundamental", "vslam_amd::Optimizer::optimize_pose"]:
         assert sym in out, sym
     del lib
+
+
+def test_vspw_weight_converter_roundtrip(tmp_path):
+    import sys
+    import numpy as np
+    import torch
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import superpoint_to_vspw as cv
+    assert cv.NUM_PARAMS == 1300865  # == vs_superpoint_num_params()
+    g = torch.Generator().manual_seed(0)
+    sd = {}
+    for name, ci, co, k in cv.LAYERS:
+        sd[name + ".weight"] = torch.randn(co, ci, k, k, generator=g)
+        sd[name + ".bias"] = torch.randn(co, generator=g)
+    torch.save(sd, tmp_path / "sp.pth")
+    import subprocess
+    subprocess.run([sys.executable, os.path.join(ROOT, "tools", "superpoint_to_vspw.py"), str(tmp_path / "sp.pth"),
+                    str(tmp_path / "sp.vspw")], check=True, capture_output=True)
+    blob = cv.read_vspw(tmp_path / "sp.vspw")
+    want = np.concatenate([np.concatenate([sd[n + ".weight"].numpy().ravel(), sd[n + ".bias"].numpy()])
+                           for n, *_ in cv.LAYERS])
+    assert np.array_equal(blob, want)
