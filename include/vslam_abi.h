@@ -218,6 +218,20 @@ int vs_fmat_verify_pairs_dev(vs_ctx* ctx, int P, const int* d_pairs, const vs_ke
                              vs_match* d_kept, int* d_nkept, double* d_err, int* d_diag,
                              void* stream);
 
+/* ---- A14: Optimizer::local_bundle_adjustment (Optimizer.cpp:187-599) --------------------- */
+/* The window as the reference gathers it (:205-244): N keyframe poses (camera -> world R_world
+ * [N][9], t_world [N][3]; poses 1..N-1 are written back, :584-588), M map points [M][3]
+ * (written back, :590-595) and n_obs observations (keyframe index, point index, u, v) in the
+ * reference's gather order (keyframe-major, keypoint order).  max_iter = 15 reproduces the
+ * reference (MAX_ITER, :294).  *err_before / *err_after = the returned RMS pair ({0, 0} and nothing
+ * written when N < 2, n_obs < 20 or M < 10); stats (nullable) = {LM iterations, accepted steps,
+ * ran}.  N <= VS_BA_MAX_KEYFRAMES. */
+#define VS_BA_MAX_KEYFRAMES 64
+int vs_local_ba(vs_ctx* ctx, int N, double* R_world, double* t_world, int M, double* points,
+                int n_obs, const int* obs_kf, const int* obs_pt, const double* obs_uv,
+                const double K[4], int max_iter, double* err_before, double* err_after,
+                int stats[3]);
+
 /* ---- profiling ----------------------------------------------------------------------- */
 /* When enabled, every stage of the _dev pipelines brackets its launches with hipEvents on the
  * stream it runs on; vs_profile_read returns per-stage accumulated milliseconds and launch

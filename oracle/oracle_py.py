@@ -44,6 +44,7 @@ _SIG = {
     "orc_find_fundamental": (_I, [_P, _P, _I, ctypes.c_double, ctypes.c_double, _I, _P, _P, _P]),
     "orc_epipolar_error": (ctypes.c_double, [_P, _P, _I, _P]),
     "orc_fmat_verify": (_I, [_P, _P, _P, _I, _P, _P, _P, _P, _P]),
+    "orc_local_ba": (_I, [_I, _P, _P, _I, _P, _I, _P, _P, _P, _P, _I, _P, _P, _P]),
     "orc_mt19937": (None, [ctypes.c_uint32, _I, _P]),
     "orc_expf_array": (None, [_P, _I, _P]),
     "orc_expf_exhaustive_check": (ctypes.c_long, [ctypes.c_float, ctypes.c_float]),
@@ -296,6 +297,21 @@ def fmat_verify(kp_ref, kp_cur, good):
     ok = ctypes.c_int(0)
     m = lib().orc_fmat_verify(_p(kr), _p(kc), _p(g), n, _p(F), _p(keep), _p(err), _p(diag), ctypes.byref(ok))
     return (F.reshape(3, 3) if ok.value else None), keep[:m], err, diag
+
+
+def local_ba(R, t, P, obs_kf, obs_pt, obs_uv, K=(525.0, 525.0, 319.5, 239.5), max_iter=15):
+    """Optimizer::local_bundle_adjustment restatement: (R', t', P', err_before, err_after, stats)."""
+    R = np.array(R, np.float64).reshape(-1, 9).copy()
+    t = np.array(t, np.float64).reshape(-1, 3).copy()
+    P = np.array(P, np.float64).reshape(-1, 3).copy()
+    kf = np.ascontiguousarray(obs_kf, np.int32)
+    pt = np.ascontiguousarray(obs_pt, np.int32)
+    uv = np.ascontiguousarray(obs_uv, np.float64).reshape(-1, 2)
+    eb, ea = ctypes.c_double(0), ctypes.c_double(0)
+    stats = np.zeros(3, np.int32)
+    lib().orc_local_ba(R.shape[0], _p(R), _p(t), P.shape[0], _p(P), len(kf), _p(kf), _p(pt), _p(uv),
+                       _p(np.asarray(K, np.float64)), max_iter, ctypes.byref(eb), ctypes.byref(ea), _p(stats))
+    return R.reshape(-1, 3, 3), t, P, eb.value, ea.value, stats
 
 
 def mt19937(seed, count):

@@ -1,0 +1,71 @@
+"""GPU parity for Optimizer::local_bundle_adjustment (A14, reference src/Optimizer.cpp:187-599).
+
+Same algorithm and per-element accumulation order on both sides (ba_solvers.h; chunked global
+sums); the remaining differences are last-ulp libm differences inside Rodrigues, so the LM
+trajectory (iterations, accepted steps) must match exactly and poses / points / RMS errors to
+1e-9 (relative for the errors)."""
+import numpy as np
+import pytest
+
+import restate
+from test_oracle_ba import ba_problem
+
+pytestmark = pytest.mark.gpu
+
+
+def windowed_problem(N, M, seed, span=5, noise=0.5, pert=0.03):
+    """Points visible from `span` consecutive keyframes (the sliding-window structure)."""
+    rng = np.random.default_rng(seed)
+    K = (525.0, 525.0, 319.5, 239.5)
+    Rs = np.array([restate.rodrigues(np.array([0.0, 0.03 * i, 0.0])) for i in range(N)])
+    ts = np.array([[0.2 * i, 0.0, 0.05 * i] for i in range(N)])
+    first = rng.integers(0, max(1, N - span + 1), M)
+    # place point j in front of keyframe first[j] + span // 2
+    kc = np.minimum(first + span // 2, N - 1)
+    pc = np.stack([rng.uniform(-1.5, 1.5, M), rng.uniform(-1.0, 1.0, M), rng.uniform(3.0, 6.0, M)], 1)
+    P = np.einsum("mij,mj->mi", Rs[kc], pc) + ts[kc]
+    kf, pt, uv = [], [], []
+    for i in range(N):
+        cam = (P - ts[i]) @ Rs[i]
+        u = K[0] * cam[:, 0] / cam[:, 2] + K[2]
+        v = K[1] * cam[:, 1] / cam[:, 2] + K[3]
+        vis = np.flatnonzero((first <= i) & (i < first + span) & (cam[:, 2] > 0.1) & (u > 0) & (u < 640) &
+                             (v > 0) & (v < 480))
+        for j in rng.permutation(vis):
+            kf.append(i)
+            pt.append(j)
+            uv.append([u[j] + rng.normal() * noise, v[j] + rng.normal() * noise])
+    P0 = P + rng.normal(size=P.shape) * pert
+    return Rs, ts, P, P0, np.array(kf, np.int32), np.array(pt, np.int32), np.array(uv)
+
+
+def _compare(g, o):
+    Rg, tg, Pg, ebg, eag, sg = g
+    Ro, to, Po, ebo, eao, so = o
+    assert np.array_equal(sg, so), (sg, so)
+    assert abs(ebg - ebo) <= 1e-9 * max(1.0, ebo) and abs(eag - eao) <= 1e-9 * max(1.0, eao)
+    assert np.max(np.abs(Pg - Po)) <= 1e-9 and np.max(np.abs(tg - to)) <= 1e-9 and np.max(np.abs(Rg - Ro)) <= 1e-9
+
+
+@pytest.mark.parametrize("args", [dict(N=5, M=120, seed=0), dict(N=4, M=60, seed=1, noise=0.3, pert=0.02, outliers=3),
+                                  dict(N=8, M=300, seed=2, noise=1.0, pert=0.1, outliers=10)])
+def test_local_ba_matches_oracle(vsctx, oracle, args):
+    R, t, P, P0, kf, pt, uv = ba_problem(**args)
+    _compare(vsctx.local_ba(R, t, P0, kf, pt, uv), oracle.local_ba(R, t, P0, kf, pt, uv))
+
+
+@pytest.mark.parametrize("N,M,seed", [(10, 2000, 3), (30, 6000, 4)])
+def test_local_ba_window_matches_oracle(vsctx, oracle, N, M, seed):
+    R, t, P, P0, kf, pt, uv = windowed_problem(N, M, seed)
+    g = vsctx.local_ba(R, t, P0, kf, pt, uv)
+    _compare(g, oracle.local_ba(R, t, P0, kf, pt, uv))
+    assert g[4] < g[3]
+
+
+def test_local_ba_bailouts_and_single_step(vsctx, oracle):
+    R, t, P, P0, kf, pt, uv = ba_problem(N=3, M=50, seed=3)
+    g = vsctx.local_ba(R, t, P0, kf[:19], pt[:19], uv[:19])
+    assert g[5][2] == 0 and g[3] == g[4] == 0 and np.array_equal(g[2], P0)
+    _compare(vsctx.local_ba(R, t, P0, kf, pt, uv, max_iter=1), oracle.local_ba(R, t, P0, kf, pt, uv, max_iter=1))
+    with pytest.raises(RuntimeError):
+        vsctx.local_ba(R, t, P0, kf, pt + 1000, uv)  # point index out of range

@@ -248,7 +248,7 @@ void vs_destroy(vs_ctx* ctx) {
     DevBuf* bufs[] = {&ctx->gray,  &ctx->act0,   &ctx->act1,   &ctx->semi,   &ctx->dgrid,  &ctx->heat,
                       &ctx->state, &ctx->flags,  &ctx->keys,   &ctx->keycnt, &ctx->h_img,  &ctx->h_kps,
                       &ctx->h_desc, &ctx->h_n,   &ctx->h_aux0, &ctx->h_aux1, &ctx->h_aux2, &ctx->h_aux3,
-                      &ctx->h_aux4, &ctx->h_aux5, &ctx->norms, &ctx->tlm};
+                      &ctx->h_aux4, &ctx->h_aux5, &ctx->norms, &ctx->tlm,  &ctx->ba};
     for (DevBuf* b : bufs) b->release();
     for (auto& st : ctx->prof)
         for (auto& pr : st.pending) {
@@ -689,6 +689,19 @@ int vs_find_fundamental(vs_ctx* ctx, const float* p1, const float* p2, int n, do
         diag[3] = dg[3];
     }
     return VS_OK;
+}
+
+int vs_local_ba(vs_ctx* ctx, int N, double* R_world, double* t_world, int M, double* points, int n_obs,
+                const int* obs_kf, const int* obs_pt, const double* obs_uv, const double K[4], int max_iter,
+                double* err_before, double* err_after, int stats[3]) {
+    VS_ARG(ctx && K && err_before && err_after, "vs_local_ba: null argument");
+    VS_ARG(N >= 0 && M >= 0 && n_obs >= 0, "vs_local_ba: negative size");
+    VS_ARG((N == 0 || (R_world && t_world)) && (M == 0 || points) &&
+               (n_obs == 0 || (obs_kf && obs_pt && obs_uv)),
+           "vs_local_ba: missing arrays");
+    VS_HIP(hipSetDevice(ctx->device));
+    return local_ba(ctx, N, R_world, t_world, M, points, n_obs, obs_kf, obs_pt, obs_uv, K, max_iter, err_before,
+                    err_after, stats);
 }
 
 // ---- profiling ----------------------------------------------------------------------------------

@@ -92,7 +92,7 @@ struct vs_ctx {
     vs::DevBuf gray, act0, act1, semi, dgrid, heat, state, flags, keys, keycnt;
     // host-API staging
     vs::DevBuf h_img, h_kps, h_desc, h_n, h_aux0, h_aux1, h_aux2, h_aux3, h_aux4, h_aux5;
-    vs::DevBuf norms, tlm;
+    vs::DevBuf norms, tlm, ba;
 
     bool prof_on = false;
     std::vector<vs::ProfStage> prof;
@@ -147,5 +147,8 @@ int fmat_pairs(vs_ctx* ctx, int P, const int* d_pairs, const vs_keypoint* d_kps,
                hipStream_t s);
 int fmat_points(vs_ctx* ctx, int P, const float* d_p1, const float* d_p2, const int* d_off, double thr, double conf,
                 int max_iters, double* d_F, uint8_t* d_mask, double* d_err, int* d_diag, hipStream_t s);
+// Local bundle adjustment over a gathered window (host arrays in/out, see vs_local_ba)
+int local_ba(vs_ctx* ctx, int N, double* R, double* t, int M, double* P, int n_obs, const int* okf, const int* opt,
+             const double* ouv, const double K4[4], int max_iter, double* err_before, double* err_after, int stats[3]);
 
 }  // namespace vs

@@ -55,6 +55,7 @@ _SIG = {
     "vs_solve_pnp_batch_dev": (_I, [_P, _I, _P, _P, _P, _P, _I, _I, _P, _P, _P, _P, _P]),
     "vs_find_fundamental": (_I, [_P, _P, _P, _I, ctypes.c_double, ctypes.c_double, _I, _P, _P, _P, _P, _P]),
     "vs_fmat_verify_pairs_dev": (_I, [_P, _I, _P, _P, _I, _P, _P, _P, _P, _P, _P, _P, _P]),
+    "vs_local_ba": (_I, [_P, _I, _P, _P, _I, _P, _I, _P, _P, _P, _P, _I, _P, _P, _P]),
     "vs_profile_enable": (_I, [_P, _I]),
     "vs_profile_reset": (_I, [_P]),
     "vs_profile_read": (_I, [_P, _I, _P, _P, _P, _P]),
@@ -275,6 +276,23 @@ class Context:
         Ka = _k_array(K)
         _check(self.lib.vs_solve_pnp_batch_dev(self.h, nprob, d_obj, d_img, d_off, _ptr(Ka), ransac_iters,
                                                min_inliers, d_R, d_t, d_stat, d_mask, stream))
+
+    # ---- Optimizer::local_bundle_adjustment ----
+    def local_ba(self, R, t, P, obs_kf, obs_pt, obs_uv, K=K_TUM, max_iter=15):
+        """Returns (R' [N,3,3], t' [N,3], P' [M,3], err_before, err_after, stats)."""
+        R = np.array(R, np.float64).reshape(-1, 9).copy()
+        t = np.array(t, np.float64).reshape(-1, 3).copy()
+        P = np.array(P, np.float64).reshape(-1, 3).copy()
+        kf = np.ascontiguousarray(obs_kf, np.int32)
+        pt = np.ascontiguousarray(obs_pt, np.int32)
+        uv = np.ascontiguousarray(obs_uv, np.float64).reshape(-1, 2)
+        eb, ea = ctypes.c_double(0), ctypes.c_double(0)
+        stats = np.zeros(3, np.int32)
+        Ka = _k_array(K)
+        _check(self.lib.vs_local_ba(self.h, R.shape[0], _ptr(R), _ptr(t), P.shape[0], _ptr(P), len(kf), _ptr(kf),
+                                    _ptr(pt), _ptr(uv), _ptr(Ka), max_iter, ctypes.byref(eb), ctypes.byref(ea),
+                                    _ptr(stats)))
+        return R.reshape(-1, 3, 3), t, P, eb.value, ea.value, stats
 
     # ---- cv::findFundamentalMat (FM_RANSAC) ----
     def find_fundamental(self, p1, p2, thr=3.0, conf=0.999, max_iters=1000):
