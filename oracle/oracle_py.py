@@ -45,6 +45,11 @@ _SIG = {
     "orc_epipolar_error": (ctypes.c_double, [_P, _P, _I, _P]),
     "orc_fmat_verify": (_I, [_P, _P, _P, _I, _P, _P, _P, _P, _P]),
     "orc_local_ba": (_I, [_I, _P, _P, _I, _P, _I, _P, _P, _P, _P, _I, _P, _P, _P]),
+    "orc_five_point": (_I, [_P, _P, _P]),
+    "orc_find_essential": (_I, [_P, _P, _I, _P, ctypes.c_double, ctypes.c_double, _I, _P, _P, _P]),
+    "orc_recover_pose": (_I, [_P, _P, _P, _I, _P, _P, _P, _P]),
+    "orc_estimate_motion": (_I, [_P, _P, _I, _P, _P, _P, _P, _P, _P]),
+    "orc_estimate_scale": (ctypes.c_double, [_P, _P, _I, _P, _P, _P, _P, _I, _I, _P]),
     "orc_mt19937": (None, [ctypes.c_uint32, _I, _P]),
     "orc_expf_array": (None, [_P, _I, _P]),
     "orc_expf_exhaustive_check": (ctypes.c_long, [ctypes.c_float, ctypes.c_float]),
@@ -312,6 +317,64 @@ def local_ba(R, t, P, obs_kf, obs_pt, obs_uv, K=(525.0, 525.0, 319.5, 239.5), ma
     lib().orc_local_ba(R.shape[0], _p(R), _p(t), P.shape[0], _p(P), len(kf), _p(kf), _p(pt), _p(uv),
                        _p(np.asarray(K, np.float64)), max_iter, ctypes.byref(eb), ctypes.byref(ea), _p(stats))
     return R.reshape(-1, 3, 3), t, P, eb.value, ea.value, stats
+
+
+_K = (525.0, 525.0, 319.5, 239.5)
+
+
+def five_point(q1, q2):
+    q1 = np.ascontiguousarray(q1, np.float64).reshape(5, 2)
+    q2 = np.ascontiguousarray(q2, np.float64).reshape(5, 2)
+    E = np.zeros((10, 9))
+    n = lib().orc_five_point(_p(q1), _p(q2), _p(E))
+    return E[:n].reshape(-1, 3, 3)
+
+
+def find_essential(p1, p2, K=_K, prob=0.999, thr=1.0, max_iters=1000):
+    a = np.ascontiguousarray(p1, np.float32).reshape(-1, 2)
+    b = np.ascontiguousarray(p2, np.float32).reshape(-1, 2)
+    n = a.shape[0]
+    E = np.zeros(9)
+    mask = np.zeros(max(n, 1), np.uint8)
+    diag = np.zeros(4, np.int32)
+    ok = lib().orc_find_essential(_p(a), _p(b), n, _p(np.asarray(K, np.float64)), prob, thr, max_iters, _p(E),
+                                  _p(mask), _p(diag))
+    return bool(ok), E.reshape(3, 3), mask[:n].astype(bool), diag
+
+
+def recover_pose(E, p1, p2, mask=None, K=_K):
+    a = np.ascontiguousarray(p1, np.float32).reshape(-1, 2)
+    b = np.ascontiguousarray(p2, np.float32).reshape(-1, 2)
+    n = a.shape[0]
+    m = np.ones(max(n, 1), np.uint8) if mask is None else np.ascontiguousarray(mask, np.uint8).copy()
+    R, t = np.zeros(9), np.zeros(3)
+    good = lib().orc_recover_pose(_p(np.ascontiguousarray(E, np.float64)), _p(a), _p(b), n,
+                                  _p(np.asarray(K, np.float64)), _p(m), _p(R), _p(t))
+    return good, R.reshape(3, 3), t, m[:n].astype(bool)
+
+
+def estimate_motion(p1, p2, K=_K):
+    """Slam::estimate_motion: (ok, R, t, mask, E inliers, recoverPose good)."""
+    a = np.ascontiguousarray(p1, np.float32).reshape(-1, 2)
+    b = np.ascontiguousarray(p2, np.float32).reshape(-1, 2)
+    n = a.shape[0]
+    R, t = np.zeros(9), np.zeros(3)
+    mask = np.zeros(max(n, 1), np.uint8)
+    inl, good = ctypes.c_int(0), ctypes.c_int(0)
+    ok = lib().orc_estimate_motion(_p(a), _p(b), n, _p(np.asarray(K, np.float64)), _p(R), _p(t), _p(mask),
+                                   ctypes.byref(inl), ctypes.byref(good))
+    return bool(ok), R.reshape(3, 3), t, mask[:n].astype(bool), inl.value, good.value
+
+
+def estimate_scale(p1, p2, R, t, depth1, depth2=None, K=_K):
+    a = np.ascontiguousarray(p1, np.float32).reshape(-1, 2)
+    b = np.ascontiguousarray(p2, np.float32).reshape(-1, 2)
+    d1 = np.ascontiguousarray(depth1, np.float32)
+    d2 = None if depth2 is None else np.ascontiguousarray(depth2, np.float32)
+    return lib().orc_estimate_scale(_p(a), _p(b), a.shape[0], _p(np.ascontiguousarray(R, np.float64)),
+                                    _p(np.ascontiguousarray(t, np.float64)), _p(d1),
+                                    None if d2 is None else _p(d2), d1.shape[0], d1.shape[1],
+                                    _p(np.asarray(K, np.float64)))
 
 
 def mt19937(seed, count):

@@ -1,0 +1,434 @@
+// emat_solvers.h — host/device kernels behind Slam::estimate_motion (reference src/Slam.cpp:
+// 1193-1213: cv::findEssentialMat(K, RANSAC, 0.999, 1.0 px) + cv::recoverPose) and the scale
+// estimators (:73-207).  OpenCV 4.x semantics restated from the published algorithms (external,
+// unpinned):
+//   * points normalised by K in double; RANSAC threshold 1.0 / ((fx + fy) / 2); model points 5;
+//     every subset accepted (no checkSubset); up to 10 models per subset;
+//   * 5-point solver (Nister 2004 / Stewenius): 4-D null space of the 5 x 9 epipolar system
+//     (orthonormal basis), the ten cubic constraints det(E) = 0 and 2 E E^T E - tr(E E^T) E = 0 in
+//     E = x E0 + y E1 + z E2 + E3, Gauss-Jordan on the 10 x 20 coefficient matrix in Nister's
+//     monomial order, the three <e> - z <f> rows, the degree-10 determinant, its real roots, then
+//     (x, y) from the null vector of B(z) and E normalised to unit Frobenius norm;
+//   * error: Sampson distance (x2' E x1)^2 / (|E x1|_12^2 + |E' x2|_12^2) as float;
+//   * recoverPose: decomposeEssentialMat (U, V sign-fixed; R1 = U W V^T, R2 = U W^T V^T, t = u3),
+//     linear triangulation (smallest right singular vector of the 4 x 4 DLT system), cheirality
+//     with distance threshold 50, ties resolved R1 t, R2 t, R1 -t, R2 -t in that order.
+// Numerical choices that differ from OpenCV's implementation (orthonormal basis from Gaussian
+// elimination + Gram-Schmidt instead of an SVD; real roots by derivative-interval bisection
+// instead of cv::solvePoly) yield the same E up to rounding; host and device share this code.
+#pragma once
+
+#include "pnp_solvers.h"
+
+namespace vs_em {
+
+constexpr int kMaxModels = 10;
+
+// Nister's monomial order over (x, y, z): x^3 y^3 x^2y xy^2 x^2z x^2 y^2z y^2 xyz xy | xz^2 xz x
+// yz^2 yz y z^3 z^2 z 1, indexed by exponents (a, b, c) -> position
+VS_HD inline int nister_index(int a, int b, int c) {
+    const int code = a * 16 + b * 4 + c;
+    switch (code) {
+        case 48: return 0;   // x3
+        case 12: return 1;   // y3
+        case 36: return 2;   // x2y
+        case 24: return 3;   // xy2
+        case 33: return 4;   // x2z
+        case 32: return 5;   // x2
+        case 9: return 6;    // y2z
+        case 8: return 7;    // y2
+        case 21: return 8;   // xyz
+        case 20: return 9;   // xy
+        case 18: return 10;  // xz2
+        case 17: return 11;  // xz
+        case 16: return 12;  // x
+        case 6: return 13;   // yz2
+        case 5: return 14;   // yz
+        case 4: return 15;   // y
+        case 3: return 16;   // z3
+        case 2: return 17;   // z2
+        case 1: return 18;   // z
+        default: return 19;  // 1
+    }
+}
+
+VS_HD inline double det3m(const double* A, const double* B, const double* C) {
+    // mixed determinant sum_sigma sgn A[0][s0] B[1][s1] C[2][s2]
+    return A[0] * (B[4] * C[8] - B[5] * C[7]) - A[1] * (B[3] * C[8] - B[5] * C[6]) + A[2] * (B[3] * C[7] - B[4] * C[6]);
+}
+
+// T(A, B, C) = 2 A B^T C - tr(A B^T) C  (9 entries)
+VS_HD inline void trilin(const double* A, const double* B, const double* C, double* T) {
+    double ABt[9];
+    for (int i = 0; i < 3; i++)
+        for (int j = 0; j < 3; j++) ABt[i * 3 + j] = A[i * 3] * B[j * 3] + A[i * 3 + 1] * B[j * 3 + 1] + A[i * 3 + 2] * B[j * 3 + 2];
+    const double tr = ABt[0] + ABt[4] + ABt[8];
+    for (int i = 0; i < 3; i++)
+        for (int j = 0; j < 3; j++)
+            T[i * 3 + j] = 2.0 * (ABt[i * 3] * C[j] + ABt[i * 3 + 1] * C[3 + j] + ABt[i * 3 + 2] * C[6 + j]) - tr * C[i * 3 + j];
+}
+
+// real roots of sum_k p[k] x^k (degree n <= 10) in ascending order; returns the count
+VS_HD inline double poly_eval(const double* p, int n, double x) {
+    double v = p[n];
+    for (int k = n - 1; k >= 0; k--) v = v * x + p[k];
+    return v;
+}
+
+VS_HD inline int poly_real_roots(const double* p_in, int n_in, double* roots) {
+    double p[11];
+    int n = n_in;
+    for (int k = 0; k <= n; k++) p[k] = p_in[k];
+    double amax = 0;
+    for (int k = 0; k <= n; k++) amax = fabs(p[k]) > amax ? fabs(p[k]) : amax;
+    while (n > 0 && fabs(p[n]) <= 1e-300 * amax) n--;  // exactly vanishing leading terms
+    if (n <= 0) return 0;
+    double bound = 0;
+    for (int k = 0; k < n; k++) {
+        const double r = fabs(p[k] / p[n]);
+        bound = r > bound ? r : bound;
+    }
+    bound += 1.0;
+    // derivatives d[m] = p^(m) for m = 0..n-1, each stored with its degree n - m
+    double d[11][11];
+    for (int k = 0; k <= n; k++) d[0][k] = p[k];
+    for (int m = 1; m < n; m++)
+        for (int k = 0; k <= n - m; k++) d[m][k] = d[m - 1][k + 1] * (double)(k + 1);
+    // roots of the degree-1 derivative, then upwards: each level's roots split the line into
+    // monotone intervals of the next level
+    double r[11];
+    int nr = 0;
+    for (int m = n - 1; m >= 0; m--) {
+        const int deg = n - m;
+        double cuts[12];
+        int nc = 0;
+        cuts[nc++] = -bound;
+        for (int i = 0; i < nr; i++)
+            if (r[i] > -bound && r[i] < bound) cuts[nc++] = r[i];
+        cuts[nc++] = bound;
+        double nr_new[11];
+        int cnt = 0;
+        for (int i = 0; i + 1 < nc; i++) {
+            double a = cuts[i], b = cuts[i + 1];
+            double fa = poly_eval(d[m], deg, a), fb = poly_eval(d[m], deg, b);
+            if (fa == 0) {
+                if (cnt == 0 || nr_new[cnt - 1] != a) nr_new[cnt++] = a;
+                continue;
+            }
+            if ((fa < 0) == (fb < 0)) continue;
+            for (int it = 0; it < 200; it++) {
+                const double mid = 0.5 * (a + b);
+                if (mid <= a || mid >= b) break;
+                const double fm = poly_eval(d[m], deg, mid);
+                if (fm == 0) {
+                    a = b = mid;
+                    break;
+                }
+                if ((fm < 0) == (fa < 0)) {
+                    a = mid;
+                    fa = fm;
+                } else {
+                    b = mid;
+                }
+            }
+            nr_new[cnt++] = 0.5 * (a + b);
+        }
+        for (int i = 0; i < cnt; i++) r[i] = nr_new[i];
+        nr = cnt;
+    }
+    for (int i = 0; i < nr; i++) roots[i] = r[i];
+    return nr;
+}
+
+// 5-point solver: q1, q2 = 5 normalised correspondences (x, y interleaved, double).  Returns the
+// number of essential matrices written to E[k][9] (row-major, unit Frobenius norm).
+VS_HD inline int five_point(const double* q1, const double* q2, double (*E)[9]) {
+    // epipolar rows: q2^T E q1 = 0 with e = (e11 e12 e13 e21 e22 e23 e31 e32 e33)
+    double Q[5][9];
+    for (int i = 0; i < 5; i++) {
+        const double x1 = q1[2 * i], y1 = q1[2 * i + 1], x2 = q2[2 * i], y2 = q2[2 * i + 1];
+        Q[i][0] = x1 * x2;
+        Q[i][1] = y1 * x2;
+        Q[i][2] = x2;
+        Q[i][3] = x1 * y2;
+        Q[i][4] = y1 * y2;
+        Q[i][5] = y2;
+        Q[i][6] = x1;
+        Q[i][7] = y1;
+        Q[i][8] = 1.0;
+    }
+    // null space by Gaussian elimination with partial pivoting (free unknowns 5..8)
+    for (int k = 0; k < 5; k++) {
+        int p = k;
+        for (int r = k + 1; r < 5; r++)
+            if (fabs(Q[r][k]) > fabs(Q[p][k])) p = r;
+        if (!(fabs(Q[p][k]) > 1e-300)) return 0;
+        if (p != k)
+            for (int j = 0; j < 9; j++) {
+                const double tmp = Q[k][j];
+                Q[k][j] = Q[p][j];
+                Q[p][j] = tmp;
+            }
+        for (int r = k + 1; r < 5; r++) {
+            const double f = Q[r][k] / Q[k][k];
+            for (int j = k; j < 9; j++) Q[r][j] -= f * Q[k][j];
+        }
+    }
+    double B[4][9];
+    for (int f = 0; f < 4; f++) {
+        for (int j = 5; j < 9; j++) B[f][j] = (j - 5 == f) ? 1.0 : 0.0;
+        for (int k = 4; k >= 0; k--) {
+            double s = 0;
+            for (int j = k + 1; j < 9; j++) s += Q[k][j] * B[f][j];
+            B[f][k] = -s / Q[k][k];
+        }
+    }
+    // orthonormal basis (modified Gram-Schmidt) -> E0..E3 in a generic position
+    for (int f = 0; f < 4; f++) {
+        for (int g = 0; g < f; g++) {
+            double dt = 0;
+            for (int j = 0; j < 9; j++) dt += B[f][j] * B[g][j];
+            for (int j = 0; j < 9; j++) B[f][j] -= dt * B[g][j];
+        }
+        double nn = 0;
+        for (int j = 0; j < 9; j++) nn += B[f][j] * B[f][j];
+        nn = sqrt(nn);
+        if (!(nn > 0)) return 0;
+        for (int j = 0; j < 9; j++) B[f][j] /= nn;
+    }
+    {  // rotate the basis by the orthogonal Hadamard / 2 so that E3 has no structural zero (with
+       // the elimination basis alone every E with e33 = 0 — e.g. R = I with a sideways baseline —
+       // would sit at infinity of x E0 + y E1 + z E2 + E3)
+        double H[4][9];
+        const double s[4][4] = {{1, 1, 1, 1}, {1, -1, 1, -1}, {1, 1, -1, -1}, {1, -1, -1, 1}};
+        for (int f = 0; f < 4; f++)
+            for (int j = 0; j < 9; j++)
+                H[f][j] = 0.5 * (s[f][0] * B[0][j] + s[f][1] * B[1][j] + s[f][2] * B[2][j] + s[f][3] * B[3][j]);
+        for (int f = 0; f < 4; f++)
+            for (int j = 0; j < 9; j++) B[f][j] = H[f][j];
+    }
+    // 10 x 20 coefficient matrix: row 0 = det(E), rows 1..9 = entries of 2 E E^T E - tr(E E^T) E;
+    // monomial lambda_i lambda_j lambda_k (i <= j <= k, lambda = (x, y, z, 1)) collects the
+    // symmetrised trilinear terms
+    double A[10][20];
+    for (int r = 0; r < 10; r++)
+        for (int c = 0; c < 20; c++) A[r][c] = 0;
+    for (int i = 0; i < 4; i++)
+        for (int j = i; j < 4; j++)
+            for (int k = j; k < 4; k++) {
+                int ex[4] = {0, 0, 0, 0};
+                ex[i]++;
+                ex[j]++;
+                ex[k]++;
+                const int col = nister_index(ex[0], ex[1], ex[2]);
+                // distinct permutations of (i, j, k)
+                int perm[6][3] = {{i, j, k}, {i, k, j}, {j, i, k}, {j, k, i}, {k, i, j}, {k, j, i}};
+                for (int pi = 0; pi < 6; pi++) {
+                    bool dup = false;
+                    for (int pj = 0; pj < pi; pj++)
+                        if (perm[pj][0] == perm[pi][0] && perm[pj][1] == perm[pi][1] && perm[pj][2] == perm[pi][2])
+                            dup = true;
+                    if (dup) continue;
+                    const double* Ea = B[perm[pi][0]];
+                    const double* Eb = B[perm[pi][1]];
+                    const double* Ec = B[perm[pi][2]];
+                    A[0][col] += det3m(Ea, Eb, Ec);
+                    double T[9];
+                    trilin(Ea, Eb, Ec, T);
+                    for (int e = 0; e < 9; e++) A[1 + e][col] += T[e];
+                }
+            }
+    // Gauss-Jordan on the first 10 columns
+    for (int k = 0; k < 10; k++) {
+        int p = k;
+        for (int r = k + 1; r < 10; r++)
+            if (fabs(A[r][k]) > fabs(A[p][k])) p = r;
+        if (!(fabs(A[p][k]) > 1e-300)) return 0;
+        if (p != k)
+            for (int c = 0; c < 20; c++) {
+                const double tmp = A[k][c];
+                A[k][c] = A[p][c];
+                A[p][c] = tmp;
+            }
+        const double inv = 1.0 / A[k][k];
+        for (int c = k; c < 20; c++) A[k][c] *= inv;
+        for (int r = 0; r < 10; r++) {
+            if (r == k) continue;
+            const double f = A[r][k];
+            if (f == 0) continue;
+            for (int c = k; c < 20; c++) A[r][c] -= f * A[k][c];
+        }
+    }
+    // B(z) rows <e> - z <f> over (x, y, 1): x-poly deg 3, y-poly deg 3, 1-poly deg 4 (coefficient
+    // arrays indexed by the power of z)
+    double bx[3][4], by[3][4], b1[3][5];
+    for (int i = 0; i < 3; i++) {
+        const double* e = &A[4 + 2 * i][10];
+        const double* f = &A[5 + 2 * i][10];
+        // rest monomials: xz^2 xz x yz^2 yz y z^3 z^2 z 1
+        bx[i][3] = -f[0];
+        bx[i][2] = e[0] - f[1];
+        bx[i][1] = e[1] - f[2];
+        bx[i][0] = e[2];
+        by[i][3] = -f[3];
+        by[i][2] = e[3] - f[4];
+        by[i][1] = e[4] - f[5];
+        by[i][0] = e[5];
+        b1[i][4] = -f[6];
+        b1[i][3] = e[6] - f[7];
+        b1[i][2] = e[7] - f[8];
+        b1[i][1] = e[8] - f[9];
+        b1[i][0] = e[9];
+    }
+    // det B(z) (degree 10) by cofactor expansion with polynomial products
+    auto pmul = [](const double* a, int na, const double* b, int nb, double* out) {
+        for (int k = 0; k <= na + nb; k++) out[k] = 0;
+        for (int i = 0; i <= na; i++)
+            for (int j = 0; j <= nb; j++) out[i + j] += a[i] * b[j];
+    };
+    double c[11];
+    for (int k = 0; k < 11; k++) c[k] = 0;
+    {
+        // det = bx0 (by1 b12 - b11 by2) - by0 (bx1 b12 - b11 bx2) + b10 (bx1 by2 - by1 bx2)
+        double t1[8], t2[8], m1[8], full[11];
+        pmul(by[1], 3, b1[2], 4, t1);
+        pmul(b1[1], 4, by[2], 3, t2);
+        for (int k = 0; k <= 7; k++) m1[k] = t1[k] - t2[k];
+        pmul(bx[0], 3, m1, 7, full);
+        for (int k = 0; k <= 10; k++) c[k] += full[k];
+        pmul(bx[1], 3, b1[2], 4, t1);
+        pmul(b1[1], 4, bx[2], 3, t2);
+        for (int k = 0; k <= 7; k++) m1[k] = t1[k] - t2[k];
+        pmul(by[0], 3, m1, 7, full);
+        for (int k = 0; k <= 10; k++) c[k] -= full[k];
+        double u1[7], u2[7], m2[7];
+        pmul(bx[1], 3, by[2], 3, u1);
+        pmul(by[1], 3, bx[2], 3, u2);
+        for (int k = 0; k <= 6; k++) m2[k] = u1[k] - u2[k];
+        pmul(b1[0], 4, m2, 6, full);
+        for (int k = 0; k <= 10; k++) c[k] += full[k];
+    }
+    double zr[10];
+    const int nz = poly_real_roots(c, 10, zr);
+    int count = 0;
+    for (int ri = 0; ri < nz && count < kMaxModels; ri++) {
+        const double z = zr[ri];
+        double Bz[3][3];
+        for (int i = 0; i < 3; i++) {
+            Bz[i][0] = poly_eval(bx[i], 3, z);
+            Bz[i][1] = poly_eval(by[i], 3, z);
+            Bz[i][2] = poly_eval(b1[i], 4, z);
+        }
+        // null vector of Bz: the largest cross product of two rows
+        double best[3] = {0, 0, 0}, bn = -1;
+        for (int a = 0; a < 3; a++)
+            for (int b = a + 1; b < 3; b++) {
+                const double cx = Bz[a][1] * Bz[b][2] - Bz[a][2] * Bz[b][1];
+                const double cy = Bz[a][2] * Bz[b][0] - Bz[a][0] * Bz[b][2];
+                const double cz = Bz[a][0] * Bz[b][1] - Bz[a][1] * Bz[b][0];
+                const double nn = cx * cx + cy * cy + cz * cz;
+                if (nn > bn) {
+                    bn = nn;
+                    best[0] = cx;
+                    best[1] = cy;
+                    best[2] = cz;
+                }
+            }
+        const double nrm = sqrt(bn > 0 ? bn : 0.0);
+        if (!(nrm > 0)) continue;
+        const double v0 = best[0] / nrm, v1 = best[1] / nrm, v2 = best[2] / nrm;
+        if (fabs(v2) < 1e-10) continue;
+        const double x = v0 / v2, y = v1 / v2;
+        double e[9], en = 0;
+        for (int q = 0; q < 9; q++) {
+            e[q] = B[0][q] * x + B[1][q] * y + B[2][q] * z + B[3][q];
+            en += e[q] * e[q];
+        }
+        en = sqrt(en);
+        if (!(en > 0)) continue;
+        for (int q = 0; q < 9; q++) E[count][q] = e[q] / en;
+        count++;
+    }
+    return count;
+}
+
+// EMEstimatorCallback::computeError (Sampson distance, float)
+VS_HD inline float sampson_err(const double* E, double x1, double y1, double x2, double y2) {
+    const double ex0 = E[0] * x1 + E[1] * y1 + E[2], ex1 = E[3] * x1 + E[4] * y1 + E[5],
+                 ex2 = E[6] * x1 + E[7] * y1 + E[8];
+    const double et0 = E[0] * x2 + E[3] * y2 + E[6], et1 = E[1] * x2 + E[4] * y2 + E[7];
+    const double x2tEx1 = x2 * ex0 + y2 * ex1 + ex2;
+    const double a = ex0 * ex0, b = ex1 * ex1, c = et0 * et0, d = et1 * et1;
+    return (float)(x2tEx1 * x2tEx1 / (a + b + c + d));
+}
+
+// cv::decomposeEssentialMat
+VS_HD inline void decompose_essential(const double* E, double* R1, double* R2, double* t) {
+    double AtA[9], w[3], V[9];
+    for (int i = 0; i < 3; i++)
+        for (int j = 0; j < 3; j++) AtA[i * 3 + j] = E[i] * E[j] + E[3 + i] * E[3 + j] + E[6 + i] * E[6 + j];
+    vs_pnp::sym_eig<3>(AtA, w, V);  // V columns: right singular vectors, descending
+    double U[9];
+    for (int k = 0; k < 2; k++) {  // u_k = E v_k / |E v_k|
+        double s[3], n = 0;
+        for (int i = 0; i < 3; i++) {
+            s[i] = E[i * 3] * V[k] + E[i * 3 + 1] * V[3 + k] + E[i * 3 + 2] * V[6 + k];
+            n += s[i] * s[i];
+        }
+        n = sqrt(n);
+        for (int i = 0; i < 3; i++) U[i * 3 + k] = n > 0 ? s[i] / n : 0.0;
+    }
+    {  // re-orthogonalise u1 against u0, u2 = u0 x u1 (the null direction of E^T)
+        double dt = U[0] * U[1] + U[3] * U[4] + U[6] * U[7], n = 0;
+        for (int i = 0; i < 3; i++) {
+            U[i * 3 + 1] -= dt * U[i * 3];
+            n += U[i * 3 + 1] * U[i * 3 + 1];
+        }
+        n = sqrt(n);
+        for (int i = 0; i < 3; i++) U[i * 3 + 1] = n > 0 ? U[i * 3 + 1] / n : 0.0;
+        U[2] = U[3] * U[7] - U[6] * U[4];
+        U[5] = U[6] * U[1] - U[0] * U[7];
+        U[8] = U[0] * U[4] - U[3] * U[1];
+    }
+    if (vs_pnp::det3(V) < 0)
+        for (int i = 0; i < 9; i++) V[i] = -V[i];
+    // W = [0 1 0; -1 0 0; 0 0 1]: U W = [-u1, u0, u2] ; U W^T = [u1, -u0, u2]
+    for (int i = 0; i < 3; i++)
+        for (int j = 0; j < 3; j++) {
+            // R = (U W) V^T: sum_k (UW)[i][k] V[j][k]
+            const double uw0 = -U[i * 3 + 1], uw1 = U[i * 3 + 0], uw2 = U[i * 3 + 2];
+            R1[i * 3 + j] = uw0 * V[j * 3 + 0] + uw1 * V[j * 3 + 1] + uw2 * V[j * 3 + 2];
+            const double uwt0 = U[i * 3 + 1], uwt1 = -U[i * 3 + 0];
+            R2[i * 3 + j] = uwt0 * V[j * 3 + 0] + uwt1 * V[j * 3 + 1] + uw2 * V[j * 3 + 2];
+        }
+    for (int i = 0; i < 3; i++) t[i] = U[i * 3 + 2];
+}
+
+// cheirality of one correspondence for camera P1 = [R | t] (P0 = [I | 0]): linear triangulation
+// and the two depth / distance tests of cv::recoverPose
+VS_HD inline bool cheiral_ok(const double* R, const double* t, double x1, double y1, double x2, double y2,
+                             double dist) {
+    double A[4][4];
+    for (int k = 0; k < 4; k++) {  // P0 rows: e_k
+        const double p0 = k == 0 ? 1.0 : 0.0, p1 = k == 1 ? 1.0 : 0.0, p2 = k == 2 ? 1.0 : 0.0;
+        A[0][k] = x1 * p2 - p0;
+        A[1][k] = y1 * p2 - p1;
+    }
+    for (int k = 0; k < 4; k++) {
+        const double q0 = k < 3 ? R[k] : t[0], q1 = k < 3 ? R[3 + k] : t[1], q2 = k < 3 ? R[6 + k] : t[2];
+        A[2][k] = x2 * q2 - q0;
+        A[3][k] = y2 * q2 - q1;
+    }
+    double AtA[16], w[4], V[16];
+    for (int i = 0; i < 4; i++)
+        for (int j = 0; j < 4; j++) AtA[i * 4 + j] = A[0][i] * A[0][j] + A[1][i] * A[1][j] + A[2][i] * A[2][j] + A[3][i] * A[3][j];
+    vs_pnp::sym_eig<4>(AtA, w, V);
+    const double Q0 = V[0 * 4 + 3], Q1 = V[1 * 4 + 3], Q2 = V[2 * 4 + 3], Q3 = V[3 * 4 + 3];
+    if (!(Q2 * Q3 > 0)) return false;
+    const double X = Q0 / Q3, Y = Q1 / Q3, Z = Q2 / Q3;
+    if (!(Z < dist)) return false;
+    const double Z2 = R[6] * X + R[7] * Y + R[8] * Z + t[2];
+    return Z2 > 0 && Z2 < dist;
+}
+
+}  // namespace vs_em
