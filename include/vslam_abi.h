@@ -218,6 +218,28 @@ int vs_fmat_verify_pairs_dev(vs_ctx* ctx, int P, const int* d_pairs, const vs_ke
                              vs_match* d_kept, int* d_nkept, double* d_err, int* d_diag,
                              void* stream);
 
+/* ---- A12: Slam::estimate_motion + depth scale (Slam.cpp:1193-1213, 73-207, used :965-984) ---- */
+/* cv::findEssentialMat(K, RANSAC, 0.999, 1.0 px) + cv::recoverPose + the >= 15 inlier and
+ * determinant checks on n <= VS_EM_MAX_POINTS pixel correspondences (interleaved xy fp32), then
+ * Slam::estimate_scale_from_depth with the reference depth map depth1 and the current depth2
+ * (h x w fp32 metres; depth2 NULL = single-depth variant, depth1 NULL = no scale).  *ok = the
+ * reference's return value; R, t (unit) = relative motion x2 = R x1 + t (written when ok);
+ * *scale = the estimate or -1 (the caller then falls back to its last good scale / MOTION_SCALE,
+ * Slam.cpp:976-980); diag (nullable) = {E found, RANSAC iterations, winning iteration, E inliers,
+ * recoverPose good, n, ran, 0}. */
+#define VS_EM_MAX_POINTS 1024
+int vs_estimate_motion(vs_ctx* ctx, const float* p1, const float* p2, int n, const double K[4],
+                       const float* depth1, const float* depth2, int h, int w, double R[9],
+                       double t[3], double* scale, int* ok, int diag[8]);
+/* Pipeline form on device: P frame pairs (d_pairs, keypoints d_kps [slot][cap], the F-verified
+ * matches d_kept [p][cap] / d_nkept, depth slots d_depth [slot][h][w]); pairs with d_skip[p] != 0
+ * (e.g. the 3D-3D result was ok) are skipped.  d_R [p][9], d_t [p][3], d_scale [p], d_ok [p],
+ * d_diag [p][8].  cap <= VS_EM_MAX_POINTS. */
+int vs_emat_motion_pairs_dev(vs_ctx* ctx, int P, const int* d_pairs, const vs_keypoint* d_kps,
+                             int cap, const vs_match* d_kept, const int* d_nkept, const int* d_skip,
+                             const float* d_depth, int h, int w, const double K[4], double* d_R,
+                             double* d_t, double* d_scale, int* d_ok, int* d_diag, void* stream);
+
 /* ---- A14: Optimizer::local_bundle_adjustment (Optimizer.cpp:187-599) --------------------- */
 /* The window as the reference gathers it (:205-244): N keyframe poses (camera -> world R_world
  * [N][9], t_world [N][3]; poses 1..N-1 are written back, :584-588), M map points [M][3]

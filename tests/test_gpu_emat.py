@@ -1,0 +1,49 @@
+"""GPU parity for Slam::estimate_motion + the depth scale (A12, reference src/Slam.cpp:1193-1213,
+73-207) through the C ABI.  The 5-point solver, Sampson scoring, recoverPose and the scale
+estimators use only correctly rounded operations (+ - * / sqrt), shared with the CPU restatement,
+so the outcome is compared exactly: RANSAC iterations, winning iteration, inlier and cheirality
+counts, R, t and the scale."""
+import numpy as np
+import pytest
+
+from test_oracle_emat import _depth_maps, two_view
+
+pytestmark = pytest.mark.gpu
+
+
+def _oracle_motion(oracle, p1, p2, d1, d2):
+    ok_e, E, mask, fdiag = oracle.find_essential(p1, p2)
+    ok, R, t, m, inl, good = oracle.estimate_motion(p1, p2)
+    sc = oracle.estimate_scale(p1, p2, R, t, d1, d2) if ok and d1 is not None else -1.0
+    return ok, R, t, sc, fdiag, inl, good
+
+
+@pytest.mark.parametrize("n,seed,noise,out,depth", [(80, 0, 0.3, 0.2, 2), (200, 1, 0.5, 0.4, 2), (40, 2, 0.2, 0.0, 1),
+                                                    (150, 3, 0.0, 0.3, 0), (400, 4, 0.7, 0.1, 2), (12, 5, 0.2, 0.5, 2)])
+def test_estimate_motion_matches_oracle(vsctx, oracle, n, seed, noise, out, depth):
+    p1, p2, R, t, X, outl = two_view(n, seed, noise=noise, outlier_frac=out)
+    d1, d2 = _depth_maps(X, R, t, p1, p2)
+    D1 = d1 if depth >= 1 else None
+    D2 = d2 if depth >= 2 else None
+    okg, Rg, tg, scg, dg = vsctx.estimate_motion(p1, p2, D1, D2)
+    oko, Ro, to, sco, fdiag, inl, good = _oracle_motion(oracle, p1, p2, D1, D2)
+    assert okg == oko
+    assert dg[1] == fdiag[0] and dg[2] == fdiag[1] and dg[5] == n
+    if fdiag[2] > 0:
+        assert dg[3] == inl
+    if oko:
+        assert dg[4] == good
+        assert np.array_equal(Rg, Ro) and np.array_equal(tg, to)
+        assert scg == sco
+
+
+def test_estimate_motion_edges(vsctx, oracle):
+    p1, p2, R, t, X, outl = two_view(30, 6)
+    assert not vsctx.estimate_motion(p1[:4], p2[:4])[0]
+    ok, Rg, tg, sc, dg = vsctx.estimate_motion(p1, p2)  # no depth -> scale -1
+    assert ok and sc == -1.0
+    rng = np.random.default_rng(0)
+    q = np.stack([rng.uniform(0, 640, 30), rng.uniform(0, 480, 30)], 1).astype(np.float32)
+    assert vsctx.estimate_motion(q, q[::-1].copy())[0] == oracle.estimate_motion(q, q[::-1].copy())[0]
+    with pytest.raises(RuntimeError):
+        vsctx.estimate_motion(np.zeros((2048, 2), np.float32), np.zeros((2048, 2), np.float32))

@@ -691,6 +691,59 @@ int vs_find_fundamental(vs_ctx* ctx, const float* p1, const float* p2, int n, do
     return VS_OK;
 }
 
+int vs_emat_motion_pairs_dev(vs_ctx* ctx, int P, const int* d_pairs, const vs_keypoint* d_kps, int cap,
+                             const vs_match* d_kept, const int* d_nkept, const int* d_skip, const float* d_depth, int h,
+                             int w, const double K[4], double* d_R, double* d_t, double* d_scale, int* d_ok, int* d_diag,
+                             void* stream) {
+    VS_ARG(ctx && d_pairs && d_kps && d_kept && d_nkept && d_depth && K && d_R && d_t && d_scale && d_ok && d_diag,
+           "vs_emat_motion_pairs_dev: null argument");
+    VS_ARG(cap > 0 && cap <= VS_EM_MAX_POINTS, "vs_emat_motion_pairs_dev: cap out of range");
+    VS_HIP(hipSetDevice(ctx->device));
+    return emat_pairs(ctx, P, d_pairs, d_kps, cap, d_kept, d_nkept, d_skip, d_depth, h, w, K, d_R, d_t, d_scale, d_ok,
+                      d_diag, pick(ctx, stream));
+}
+
+int vs_estimate_motion(vs_ctx* ctx, const float* p1, const float* p2, int n, const double K[4], const float* depth1,
+                       const float* depth2, int h, int w, double R[9], double t[3], double* scale, int* ok,
+                       int diag[8]) {
+    VS_ARG(ctx && K && R && t && scale && ok, "vs_estimate_motion: null argument");
+    VS_ARG(n >= 0 && n <= VS_EM_MAX_POINTS && (n == 0 || (p1 && p2)), "vs_estimate_motion: bad points");
+    VS_ARG(!depth1 || (h > 0 && w > 0), "vs_estimate_motion: bad depth size");
+    *ok = 0;
+    *scale = -1.0;
+    if (diag)
+        for (int k = 0; k < 8; k++) diag[k] = k == 2 ? -1 : 0;
+    if (n == 0) return VS_OK;
+    VS_HIP(hipSetDevice(ctx->device));
+    hipStream_t s = ctx->stream;
+    VS_CHECK(upload(ctx->h_aux0, p1, (size_t)n * 2, s));
+    VS_CHECK(upload(ctx->h_aux1, p2, (size_t)n * 2, s));
+    const size_t plane = depth1 ? (size_t)h * w : 0;
+    if (depth1) VS_CHECK(upload(ctx->h_aux3, depth1, plane, s));
+    if (depth1 && depth2) VS_CHECK(upload(ctx->h_aux4, depth2, plane, s));
+    VS_CHECK(ctx->h_aux2.ensure(13 * sizeof(double) + 12 * sizeof(int)));
+    double* dRt = ctx->h_aux2.as<double>();  // R[9], t[3], scale
+    int* dmeta = reinterpret_cast<int*>(dRt + 13);  // off[2], ok, diag[8]
+    const int off[2] = {0, n};
+    VS_HIP(hipMemcpyAsync(dmeta, off, sizeof(off), hipMemcpyHostToDevice, s));
+    VS_CHECK(emat_points(ctx, 1, ctx->h_aux0.as<float>(), ctx->h_aux1.as<float>(), dmeta,
+                         depth1 ? ctx->h_aux3.as<float>() : nullptr, depth1 && depth2 ? ctx->h_aux4.as<float>() : nullptr,
+                         h, w, K, dRt, dRt + 9, dRt + 12, dmeta + 2, dmeta + 3, s));
+    double hRt[13];
+    int hm[9];
+    VS_HIP(hipMemcpyAsync(hRt, dRt, sizeof(hRt), hipMemcpyDeviceToHost, s));
+    VS_HIP(hipMemcpyAsync(hm, dmeta + 2, sizeof(hm), hipMemcpyDeviceToHost, s));
+    VS_HIP(hipStreamSynchronize(s));
+    *ok = hm[0];
+    *scale = hRt[12];
+    if (hm[0]) {
+        std::memcpy(R, hRt, 9 * sizeof(double));
+        std::memcpy(t, hRt + 9, 3 * sizeof(double));
+    }
+    if (diag) std::memcpy(diag, hm + 1, 8 * sizeof(int));
+    return VS_OK;
+}
+
 int vs_local_ba(vs_ctx* ctx, int N, double* R_world, double* t_world, int M, double* points, int n_obs,
                 const int* obs_kf, const int* obs_pt, const double* obs_uv, const double K[4], int max_iter,
                 double* err_before, double* err_after, int stats[3]) {

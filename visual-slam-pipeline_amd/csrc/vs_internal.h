@@ -147,6 +147,13 @@ int fmat_pairs(vs_ctx* ctx, int P, const int* d_pairs, const vs_keypoint* d_kps,
                hipStream_t s);
 int fmat_points(vs_ctx* ctx, int P, const float* d_p1, const float* d_p2, const int* d_off, double thr, double conf,
                 int max_iters, double* d_F, uint8_t* d_mask, double* d_err, int* d_diag, hipStream_t s);
+// Essential-matrix motion + depth scale (A12): per frame pair (pipeline) or per point set
+int emat_pairs(vs_ctx* ctx, int P, const int* d_pairs, const vs_keypoint* d_kps, int cap, const vs_match* d_kept,
+               const int* d_nkept, const int* d_skip, const float* d_depth, int h, int w, const double K[4],
+               double* d_R, double* d_t, double* d_scale, int* d_ok, int* d_diag, hipStream_t s);
+int emat_points(vs_ctx* ctx, int P, const float* d_p1, const float* d_p2, const int* d_off, const float* d_depth1,
+                const float* d_depth2, int h, int w, const double K[4], double* d_R, double* d_t, double* d_scale,
+                int* d_ok, int* d_diag, hipStream_t s);
 // Local bundle adjustment over a gathered window (host arrays in/out, see vs_local_ba)
 int local_ba(vs_ctx* ctx, int N, double* R, double* t, int M, double* P, int n_obs, const int* okf, const int* opt,
              const double* ouv, const double K4[4], int max_iter, double* err_before, double* err_after, int stats[3]);

@@ -56,6 +56,8 @@ _SIG = {
     "vs_find_fundamental": (_I, [_P, _P, _P, _I, ctypes.c_double, ctypes.c_double, _I, _P, _P, _P, _P, _P]),
     "vs_fmat_verify_pairs_dev": (_I, [_P, _I, _P, _P, _I, _P, _P, _P, _P, _P, _P, _P, _P]),
     "vs_local_ba": (_I, [_P, _I, _P, _P, _I, _P, _I, _P, _P, _P, _P, _I, _P, _P, _P]),
+    "vs_estimate_motion": (_I, [_P, _P, _P, _I, _P, _P, _P, _I, _I, _P, _P, _P, _P, _P]),
+    "vs_emat_motion_pairs_dev": (_I, [_P, _I, _P, _P, _I, _P, _P, _P, _P, _I, _I, _P, _P, _P, _P, _P, _P, _P]),
     "vs_profile_enable": (_I, [_P, _I]),
     "vs_profile_reset": (_I, [_P]),
     "vs_profile_read": (_I, [_P, _I, _P, _P, _P, _P]),
@@ -276,6 +278,29 @@ class Context:
         Ka = _k_array(K)
         _check(self.lib.vs_solve_pnp_batch_dev(self.h, nprob, d_obj, d_img, d_off, _ptr(Ka), ransac_iters,
                                                min_inliers, d_R, d_t, d_stat, d_mask, stream))
+
+    # ---- Slam::estimate_motion + depth scale ----
+    def estimate_motion(self, p1, p2, depth1=None, depth2=None, K=K_TUM):
+        """Returns (ok, R, t (unit), scale, diag[8])."""
+        a = np.ascontiguousarray(p1, np.float32).reshape(-1, 2)
+        b = np.ascontiguousarray(p2, np.float32).reshape(-1, 2)
+        d1 = None if depth1 is None else np.ascontiguousarray(depth1, np.float32)
+        d2 = None if depth2 is None else np.ascontiguousarray(depth2, np.float32)
+        h, w = (d1.shape if d1 is not None else (0, 0))
+        R, t = np.zeros(9), np.zeros(3)
+        sc, ok = ctypes.c_double(0), ctypes.c_int(0)
+        diag = np.zeros(8, np.int32)
+        Ka = _k_array(K)
+        _check(self.lib.vs_estimate_motion(self.h, _ptr(a), _ptr(b), a.shape[0], _ptr(Ka),
+                                           None if d1 is None else _ptr(d1), None if d2 is None else _ptr(d2), h, w,
+                                           _ptr(R), _ptr(t), ctypes.byref(sc), ctypes.byref(ok), _ptr(diag)))
+        return bool(ok.value), R.reshape(3, 3), t, sc.value, diag
+
+    def emat_motion_pairs_dev(self, P, d_pairs, d_kps, cap, d_kept, d_nkept, d_skip, d_depth, h, w, d_R, d_t, d_scale,
+                              d_ok, d_diag, K=K_TUM, stream=None):
+        Ka = _k_array(K)
+        _check(self.lib.vs_emat_motion_pairs_dev(self.h, P, d_pairs, d_kps, cap, d_kept, d_nkept, d_skip, d_depth, h,
+                                                 w, _ptr(Ka), d_R, d_t, d_scale, d_ok, d_diag, stream))
 
     # ---- Optimizer::local_bundle_adjustment ----
     def local_ba(self, R, t, P, obs_kf, obs_pt, obs_uv, K=K_TUM, max_iter=15):
