@@ -6,6 +6,8 @@ through the whole per-frame hot path by libvslam_hip.so:
     Slam::match_features        (exact 2-NN + 0.75 ratio test, frame i-1 -> frame i)
     F-matrix verification       (findFundamentalMat(FM_RANSAC, 3.0, 0.999) + ordered filtering)
     Slam::estimate_motion_3d3d  (200-iteration 3D-3D RANSAC + refit, on the F-filtered matches)
+    Slam::estimate_motion       (5-point essential matrix + recoverPose + depth scale, for the pairs
+                                 whose 3D-3D estimate failed, Slam.cpp:965-984)
 plus the host pose chain on the returned (R, t) (Slam.cpp:963-964).  With --gpus N > 1 the frames
 are sharded in contiguous blocks across N ranks (one process per GPU) and the per-frame feature
 records are all-gathered over RCCL each step (weak scaling: B frames per GPU per step).
@@ -85,7 +87,8 @@ def parse():
 
 def cpu_baseline(frames_list, nframes):
     """The CPU restatement (oracle/, test infrastructure) on a bounded sample of the same workload:
-    extract + match + F verification + 3D-3D RANSAC for consecutive frames, OpenMP network."""
+    extract + match + F verification + 3D-3D RANSAC (+ the E-matrix fallback when it fails) for
+    consecutive frames, OpenMP network."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle_py as oracle
     import vslam_abi
@@ -105,13 +108,17 @@ def cpu_baseline(frames_list, nframes):
             good = good[keep]
             p1 = np.stack([k1["x"][good["query_idx"]], k1["y"][good["query_idx"]]], 1)
             p2 = np.stack([kps["x"][good["train_idx"]], kps["y"][good["train_idx"]]], 1)
-            oracle.ransac_3d3d(p1, p2, dep1, f["depth"], seed=42 + i)
+            ok3 = oracle.ransac_3d3d(p1, p2, dep1, f["depth"], seed=42 + i)[0]
+            if not ok3:  # Slam.cpp:965-984
+                ok_e, R_e, t_e = oracle.estimate_motion(p1, p2)[:3]
+                if ok_e:
+                    oracle.estimate_scale(p1, p2, R_e, t_e, dep1, f["depth"])
         prev = (kps, desc, f["depth"])
     dt = time.perf_counter() - t0
     return {"value": len(sample) / dt, "unit": "frames/s", "cores": threads, "kind": "port",
             "sample": f"{len(sample)} consecutive synthetic 640x480 RGB-D frames, oracle/ CPU restatement "
                       f"(OpenMP fp32 SuperPoint, decode/NMS/sample, exact 2-NN match, F-RANSAC "
-                      f"verification, 3D-3D RANSAC), "
+                      f"verification, 3D-3D RANSAC, E-matrix fallback), "
                       f"{threads} threads, {dt:.1f} s"}
 
 
@@ -122,7 +129,7 @@ def main():
 
     import synth
     import vslam_abi
-    from vslam_pipeline import DevicePipeline, compose_poses
+    from vslam_pipeline import DevicePipeline, PoseChain
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -147,15 +154,18 @@ def main():
     ctx = vslam_abi.Context(local if world > 1 else 0)
     pipe = DevicePipeline(ctx, B, H, W, rank=rank, world=world)
 
-    pose = [np.eye(3), np.zeros(3)]
+    chain = PoseChain()
+    n_emat = [0]
 
     def step(i):
         out = pipe.run(frames, depth, frame_count0=i * n_total + rank * B, depth_prev=depth_prev)
-        R = out["R"].cpu().numpy()  # small D2H: the host tracker consumes (R, t, ok)
-        t = out["t"].cpu().numpy()
-        ok = out["ok"].cpu().numpy()
-        chain = compose_poses(R, t, ok, pose[0], pose[1])
-        pose[0], pose[1] = chain[-1]
+        # small D2H: the host tracker consumes the per-pair motion (3D-3D or the E-matrix fallback)
+        R, t, ok = out["R"].cpu().numpy(), out["t"].cpu().numpy(), out["ok"].cpu().numpy()
+        eR, et = out["eR"].cpu().numpy(), out["et"].cpu().numpy()
+        esc, eok = out["escale"].cpu().numpy(), out["eok"].cpu().numpy()
+        for p in range(B):
+            chain.step(ok[p], R[p], t[p], eok[p], eR[p], et[p], esc[p])
+        n_emat[0] += int(eok.sum())
         return int(ok.sum())
 
     for i in range(args.warmup):
@@ -216,7 +226,8 @@ def main():
             "data": "synthetic (seeded 640x480 RGB-D room sequence, seeded He-normal SuperPoint weights)",
             "config": {
                 "workload": "config[1]: 640x480 RGB-D stream on 1xMI355X - HIP SuperPoint extract + "
-                            "ratio-test matching + F-RANSAC verification + 3D-3D RANSAC per processed frame",
+                            "ratio-test matching + F-RANSAC verification + 3D-3D RANSAC (E-matrix fallback) "
+                            "per processed frame",
                 "frames_per_gpu_per_step": B,
                 "resolution": "640x480",
                 "max_keypoints": 400,
@@ -239,6 +250,7 @@ def main():
             "network_tflops": round(net_flops / (net_ms / 1e3) / 1e12, 3),
             "stage_ms_per_step": stage_ms,
             "pairs_ok_3d3d": f"{n_ok}/{world * B * args.steps}" if world == 1 else None,
+            "pairs_emat_fallback": f"{n_emat[0]}/{world * B * (args.steps + args.warmup)}" if world == 1 else None,
             "cpu_baseline": cpu,
         }
         print(json.dumps(result), flush=True)

@@ -227,7 +227,7 @@ int vs_fmat_verify_pairs_dev(vs_ctx* ctx, int P, const int* d_pairs, const vs_ke
  * *scale = the estimate or -1 (the caller then falls back to its last good scale / MOTION_SCALE,
  * Slam.cpp:976-980); diag (nullable) = {E found, RANSAC iterations, winning iteration, E inliers,
  * recoverPose good, n, ran, 0}. */
-#define VS_EM_MAX_POINTS 1024
+#define VS_EM_MAX_POINTS 512
 int vs_estimate_motion(vs_ctx* ctx, const float* p1, const float* p2, int n, const double K[4],
                        const float* depth1, const float* depth2, int h, int w, double R[9],
                        double t[3], double* scale, int* ok, int diag[8]);

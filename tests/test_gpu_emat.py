@@ -46,4 +46,4 @@ def test_estimate_motion_edges(vsctx, oracle):
     q = np.stack([rng.uniform(0, 640, 30), rng.uniform(0, 480, 30)], 1).astype(np.float32)
     assert vsctx.estimate_motion(q, q[::-1].copy())[0] == oracle.estimate_motion(q, q[::-1].copy())[0]
     with pytest.raises(RuntimeError):
-        vsctx.estimate_motion(np.zeros((2048, 2), np.float32), np.zeros((2048, 2), np.float32))
+        vsctx.estimate_motion(np.zeros((1024, 2), np.float32), np.zeros((1024, 2), np.float32))

@@ -220,6 +220,13 @@ def test_device_pipeline_matches_host_entry_points(vsctx, seq4):
         assert np.array_equal(out["diag"][p].cpu().numpy(), dh)
         if okh:
             assert np.max(np.abs(out["R"][p].cpu().numpy() - Rh.reshape(9))) <= 1e-12
+            assert out["eok"][p].item() == 0 and out["ediag"][p, 5].item() == 0  # fallback skipped
+        else:  # Slam.cpp:965-984: the essential-matrix fallback with depth scale
+            oke, Re, te, sce, de = vsctx.estimate_motion(p1, p2, seq4[p - 1]["depth"], seq4[p]["depth"])
+            assert bool(out["eok"][p].item()) == oke
+            if oke:
+                assert np.array_equal(out["eR"][p].cpu().numpy(), Re.reshape(9))
+                assert np.array_equal(out["et"][p].cpu().numpy(), te) and out["escale"][p].item() == sce
 
 
 def test_profile_reports_stages(vsctx, seq4):

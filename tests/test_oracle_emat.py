@@ -54,7 +54,7 @@ def e_close(Ea, Eb, tol):
 
 @pytest.mark.parametrize("case", ["generic", "sideways_R_identity", "forward"])
 def test_five_point_known_answer(oracle, case):
-    rng = np.random.default_rng(hash(case) % 2 ** 32)
+    rng = np.random.default_rng(["generic", "sideways_R_identity", "forward"].index(case) + 11)
     if case == "generic":
         R, t = restate.rodrigues(rng.normal(size=3) * 0.2), rng.normal(size=3)
     elif case == "sideways_R_identity":  # e33 = 0: not representable with a fixed E3 coefficient basis
@@ -73,6 +73,22 @@ def test_five_point_known_answer(oracle, case):
         assert np.max(np.abs(2 * E @ E.T @ E - np.trace(E @ E.T) * E)) < 1e-9
         h1, h2 = np.c_[q1, np.ones(5)], np.c_[q2, np.ones(5)]
         assert np.max(np.abs(np.sum(h2 * (h1 @ E.T), 1))) < 1e-9
+
+
+def test_five_point_accuracy_sweep(oracle):
+    """300 random minimal problems: the true E is recovered to 1e-7 in >= 97% of them (the rest
+    are near-double roots of the degree-10 polynomial, still within 1e-3)."""
+    errs = []
+    for s in range(300):
+        rng = np.random.default_rng(s)
+        R, t = restate.rodrigues(rng.normal(size=3) * 0.2), rng.normal(size=3)
+        X = np.stack([rng.uniform(-2, 2, 5), rng.uniform(-2, 2, 5), rng.uniform(3, 6, 5)], 1)
+        X2 = X @ R.T + t
+        Es = oracle.five_point(X[:, :2] / X[:, 2:], X2[:, :2] / X2[:, 2:])
+        Et = skew(t) @ R
+        errs.append(min(next((tol for tol in (1e-7, 1e-3) if e_close(E, Et, tol)), 1.0) for E in Es))
+    errs = np.array(errs)
+    assert np.mean(errs <= 1e-7) >= 0.97 and np.all(errs <= 1e-3)
 
 
 def sampson(E, q1, q2):

@@ -4,7 +4,7 @@
 //
 // One workgroup (4 wave64s) per problem.  The reference runs this path when the 3D-3D estimate
 // fails (Slam.cpp:965-984), so in the pipeline a problem whose 3D-3D result is ok exits at once.
-// RANSAC: chunks of 64 subsets drawn by lane 0 with the cv::RNG stream (5 distinct indices, no
+// RANSAC: chunks of 32 subsets drawn by lane 0 with the cv::RNG stream (5 distinct indices, no
 // subset check), one 5-point solve per lane (up to 10 models, LDS), rounds of 4 hypotheses scored
 // by the waves (Sampson error, ballot counts, early exit below the current best) and replayed in
 // order by lane 0.  recoverPose: the cheirality test of every point under the four decompositions
@@ -20,7 +20,7 @@ namespace vs {
 using namespace vs_em;
 
 constexpr int kEmMaxPts = VS_EM_MAX_POINTS;
-constexpr int kEmChunk = 64;
+constexpr int kEmChunk = 32;  // one 5-point solve per lane of wave 0; workspace in LDS
 constexpr int kEmThreads = 256;
 constexpr int kEmWaves = kEmThreads / 64;
 
@@ -34,6 +34,7 @@ struct EmShared {
     double q1[2 * kEmMaxPts], q2[2 * kEmMaxPts];   // normalised
     int subset[kEmChunk * 5];
     double Em[kEmChunk * kMaxModels * 9];
+    double ws[kWsSize * kEmChunk];  // per-lane solver workspace, lane-interleaved
     int nmod[kEmChunk];
     int score[kEmChunk * kMaxModels];
     double sv[2 * kEmMaxPts];  // scale candidates (sorted)
@@ -138,9 +139,8 @@ __global__ __launch_bounds__(kEmThreads) void k_emat(const int* __restrict__ pai
         S.ok = 0;
         S.niters = 1000;
         if (n == 5) {  // count == modelPoints: a single kernel run, first model
-            double Es[kMaxModels][9];
-            if (five_point(S.q1, S.q2, Es) > 0) {
-                for (int k = 0; k < 9; k++) S.E[k] = Es[0][k];
+            if (five_point(S.q1, S.q2, S.Em, S.ws, kEmChunk) > 0) {
+                for (int k = 0; k < 9; k++) S.E[k] = S.Em[k];
                 S.ok = 1;
             }
         }
@@ -177,11 +177,7 @@ __global__ __launch_bounds__(kEmThreads) void k_emat(const int* __restrict__ pai
                 s2[2 * i] = S.q2[2 * k];
                 s2[2 * i + 1] = S.q2[2 * k + 1];
             }
-            double Es[kMaxModels][9];
-            const int nm = five_point(s1, s2, Es);
-            S.nmod[tid] = nm;
-            for (int k = 0; k < nm; k++)
-                for (int q = 0; q < 9; q++) S.Em[(tid * kMaxModels + k) * 9 + q] = Es[k][q];
+            S.nmod[tid] = five_point(s1, s2, &S.Em[tid * kMaxModels * 9], &S.ws[tid], kEmChunk);
         }
         __syncthreads();
         for (int r0 = 0; r0 < chunk; r0 += kEmWaves) {

@@ -75,51 +75,67 @@ VS_HD inline double poly_eval(const double* p, int n, double x) {
     return v;
 }
 
-VS_HD inline int poly_real_roots(const double* p_in, int n_in, double* roots) {
-    double p[11];
-    int n = n_in;
-    for (int k = 0; k <= n; k++) p[k] = p_in[k];
+// ---- workspace layout (doubles, element i at W[i * wst]): the device passes a lane-interleaved
+// LDS slice (conflict-free), the host a stack array with wst = 1 ----
+constexpr int kWsA = 0;       // 10 x 20 coefficient matrix
+constexpr int kWsP = 200;     // degree-10 polynomial
+constexpr int kWsD = 211;     // current derivative's coefficients
+constexpr int kWsR = 222;     // roots of the previous level / final roots
+constexpr int kWsC = 233;     // interval cuts
+constexpr int kWsN = 245;     // roots of the current level
+constexpr int kWsSize = 256;
+
+// real roots of sum_k P[k] x^k (degree <= 10, P in the workspace) in ascending order, written to
+// the workspace at kWsR; returns the count.  Each derivative level's roots split the line into
+// monotone intervals of the level above, which are bisected.
+VS_HD inline int poly_real_roots(double* W, int wst) {
+#define WS(i) W[(size_t)(i) * wst]
+    int n = 10;
     double amax = 0;
-    for (int k = 0; k <= n; k++) amax = fabs(p[k]) > amax ? fabs(p[k]) : amax;
-    while (n > 0 && fabs(p[n]) <= 1e-300 * amax) n--;  // exactly vanishing leading terms
+    for (int k = 0; k <= 10; k++) amax = fabs(WS(kWsP + k)) > amax ? fabs(WS(kWsP + k)) : amax;
+    while (n > 0 && fabs(WS(kWsP + n)) <= 1e-300 * amax) n--;  // exactly vanishing leading terms
     if (n <= 0) return 0;
+    const double lead = WS(kWsP + n);
     double bound = 0;
     for (int k = 0; k < n; k++) {
-        const double r = fabs(p[k] / p[n]);
+        const double r = fabs(WS(kWsP + k) / lead);
         bound = r > bound ? r : bound;
     }
     bound += 1.0;
-    // derivatives d[m] = p^(m) for m = 0..n-1, each stored with its degree n - m
-    double d[11][11];
-    for (int k = 0; k <= n; k++) d[0][k] = p[k];
-    for (int m = 1; m < n; m++)
-        for (int k = 0; k <= n - m; k++) d[m][k] = d[m - 1][k + 1] * (double)(k + 1);
-    // roots of the degree-1 derivative, then upwards: each level's roots split the line into
-    // monotone intervals of the next level
-    double r[11];
     int nr = 0;
     for (int m = n - 1; m >= 0; m--) {
         const int deg = n - m;
-        double cuts[12];
+        for (int k = 0; k <= deg; k++) {  // m-th derivative: P[k + m] (k + m)! / k!
+            double f = 1.0;
+            for (int q = 0; q < m; q++) f *= (double)(k + m - q);
+            WS(kWsD + k) = WS(kWsP + k + m) * f;
+        }
         int nc = 0;
-        cuts[nc++] = -bound;
-        for (int i = 0; i < nr; i++)
-            if (r[i] > -bound && r[i] < bound) cuts[nc++] = r[i];
-        cuts[nc++] = bound;
-        double nr_new[11];
+        WS(kWsC + nc++) = -bound;
+        for (int i = 0; i < nr; i++) {
+            const double ri = WS(kWsR + i);
+            if (ri > -bound && ri < bound) WS(kWsC + nc++) = ri;
+        }
+        WS(kWsC + nc++) = bound;
         int cnt = 0;
         for (int i = 0; i + 1 < nc; i++) {
-            double a = cuts[i], b = cuts[i + 1];
-            double fa = poly_eval(d[m], deg, a), fb = poly_eval(d[m], deg, b);
+            double a = WS(kWsC + i), b = WS(kWsC + i + 1);
+            auto ev = [&](double x) {
+                double v = WS(kWsD + deg);
+                for (int k = deg - 1; k >= 0; k--) v = v * x + WS(kWsD + k);
+                return v;
+            };
+            double fa = ev(a);
+            const double fb = ev(b);
             if (fa == 0) {
-                if (cnt == 0 || nr_new[cnt - 1] != a) nr_new[cnt++] = a;
+                if (cnt == 0 || WS(kWsN + cnt - 1) != a) WS(kWsN + cnt++) = a;
                 continue;
             }
             if ((fa < 0) == (fb < 0)) continue;
             for (int it = 0; it < 200; it++) {
                 const double mid = 0.5 * (a + b);
                 if (mid <= a || mid >= b) break;
-                const double fm = poly_eval(d[m], deg, mid);
+                const double fm = ev(mid);
                 if (fm == 0) {
                     a = b = mid;
                     break;
@@ -131,20 +147,24 @@ VS_HD inline int poly_real_roots(const double* p_in, int n_in, double* roots) {
                     b = mid;
                 }
             }
-            nr_new[cnt++] = 0.5 * (a + b);
+            WS(kWsN + cnt++) = 0.5 * (a + b);
         }
-        for (int i = 0; i < cnt; i++) r[i] = nr_new[i];
+        for (int i = 0; i < cnt; i++) WS(kWsR + i) = WS(kWsN + i);
         nr = cnt;
     }
-    for (int i = 0; i < nr; i++) roots[i] = r[i];
     return nr;
+#undef WS
 }
 
-// 5-point solver: q1, q2 = 5 normalised correspondences (x, y interleaved, double).  Returns the
-// number of essential matrices written to E[k][9] (row-major, unit Frobenius norm).
-VS_HD inline int five_point(const double* q1, const double* q2, double (*E)[9]) {
+// 5-point solver: q1, q2 = 5 normalised correspondences (x, y interleaved, double).  Writes up to
+// kMaxModels essential matrices to Eout[k * 9 + q] (row-major, unit Frobenius norm) and returns the
+// count.  W / wst: the workspace (kWsSize doubles).
+VS_HD inline int five_point(const double* q1, const double* q2, double* Eout, double* W, int wst) {
+#define WS(i) W[(size_t)(i) * wst]
+#define AA(r, c) WS(kWsA + (r) * 20 + (c))
     // epipolar rows: q2^T E q1 = 0 with e = (e11 e12 e13 e21 e22 e23 e31 e32 e33)
     double Q[5][9];
+    VS_UNROLL
     for (int i = 0; i < 5; i++) {
         const double x1 = q1[2 * i], y1 = q1[2 * i + 1], x2 = q2[2 * i], y2 = q2[2 * i + 1];
         Q[i][0] = x1 * x2;
@@ -157,43 +177,66 @@ VS_HD inline int five_point(const double* q1, const double* q2, double (*E)[9]) 
         Q[i][7] = y1;
         Q[i][8] = 1.0;
     }
-    // null space by Gaussian elimination with partial pivoting (free unknowns 5..8)
+    // null space by Gaussian elimination with partial pivoting (free unknowns 5..8); row swaps as
+    // selects so the unrolled matrix stays in registers
+    VS_UNROLL
     for (int k = 0; k < 5; k++) {
         int p = k;
+        double big = fabs(Q[k][k]);
+        VS_UNROLL
         for (int r = k + 1; r < 5; r++)
-            if (fabs(Q[r][k]) > fabs(Q[p][k])) p = r;
-        if (!(fabs(Q[p][k]) > 1e-300)) return 0;
-        if (p != k)
-            for (int j = 0; j < 9; j++) {
-                const double tmp = Q[k][j];
-                Q[k][j] = Q[p][j];
-                Q[p][j] = tmp;
+            if (fabs(Q[r][k]) > big) {
+                big = fabs(Q[r][k]);
+                p = r;
             }
+        if (!(big > 1e-300)) return 0;
+        VS_UNROLL
+        for (int r = k + 1; r < 5; r++) {
+            const bool sw = r == p;
+            VS_UNROLL
+            for (int j = k; j < 9; j++) {
+                const double qk = Q[k][j], qr = Q[r][j];
+                Q[k][j] = sw ? qr : qk;
+                Q[r][j] = sw ? qk : qr;
+            }
+        }
+        VS_UNROLL
         for (int r = k + 1; r < 5; r++) {
             const double f = Q[r][k] / Q[k][k];
+            VS_UNROLL
             for (int j = k; j < 9; j++) Q[r][j] -= f * Q[k][j];
         }
     }
     double B[4][9];
+    VS_UNROLL
     for (int f = 0; f < 4; f++) {
+        VS_UNROLL
         for (int j = 5; j < 9; j++) B[f][j] = (j - 5 == f) ? 1.0 : 0.0;
+        VS_UNROLL
         for (int k = 4; k >= 0; k--) {
             double s = 0;
+            VS_UNROLL
             for (int j = k + 1; j < 9; j++) s += Q[k][j] * B[f][j];
             B[f][k] = -s / Q[k][k];
         }
     }
-    // orthonormal basis (modified Gram-Schmidt) -> E0..E3 in a generic position
+    // orthonormal basis (modified Gram-Schmidt)
+    VS_UNROLL
     for (int f = 0; f < 4; f++) {
+        VS_UNROLL
         for (int g = 0; g < f; g++) {
             double dt = 0;
+            VS_UNROLL
             for (int j = 0; j < 9; j++) dt += B[f][j] * B[g][j];
+            VS_UNROLL
             for (int j = 0; j < 9; j++) B[f][j] -= dt * B[g][j];
         }
         double nn = 0;
+        VS_UNROLL
         for (int j = 0; j < 9; j++) nn += B[f][j] * B[f][j];
         nn = sqrt(nn);
         if (!(nn > 0)) return 0;
+        VS_UNROLL
         for (int j = 0; j < 9; j++) B[f][j] /= nn;
     }
     {  // rotate the basis by the orthogonal Hadamard / 2 so that E3 has no structural zero (with
@@ -201,84 +244,93 @@ VS_HD inline int five_point(const double* q1, const double* q2, double (*E)[9]) 
        // would sit at infinity of x E0 + y E1 + z E2 + E3)
         double H[4][9];
         const double s[4][4] = {{1, 1, 1, 1}, {1, -1, 1, -1}, {1, 1, -1, -1}, {1, -1, -1, 1}};
+        VS_UNROLL
         for (int f = 0; f < 4; f++)
+            VS_UNROLL
             for (int j = 0; j < 9; j++)
                 H[f][j] = 0.5 * (s[f][0] * B[0][j] + s[f][1] * B[1][j] + s[f][2] * B[2][j] + s[f][3] * B[3][j]);
+        VS_UNROLL
         for (int f = 0; f < 4; f++)
+            VS_UNROLL
             for (int j = 0; j < 9; j++) B[f][j] = H[f][j];
     }
     // 10 x 20 coefficient matrix: row 0 = det(E), rows 1..9 = entries of 2 E E^T E - tr(E E^T) E;
     // monomial lambda_i lambda_j lambda_k (i <= j <= k, lambda = (x, y, z, 1)) collects the
     // symmetrised trilinear terms
-    double A[10][20];
     for (int r = 0; r < 10; r++)
-        for (int c = 0; c < 20; c++) A[r][c] = 0;
+        for (int c = 0; c < 20; c++) AA(r, c) = 0;
+    VS_UNROLL
     for (int i = 0; i < 4; i++)
+        VS_UNROLL
         for (int j = i; j < 4; j++)
+            VS_UNROLL
             for (int k = j; k < 4; k++) {
                 int ex[4] = {0, 0, 0, 0};
                 ex[i]++;
                 ex[j]++;
                 ex[k]++;
                 const int col = nister_index(ex[0], ex[1], ex[2]);
-                // distinct permutations of (i, j, k)
-                int perm[6][3] = {{i, j, k}, {i, k, j}, {j, i, k}, {j, k, i}, {k, i, j}, {k, j, i}};
+                const int perm[6][3] = {{i, j, k}, {i, k, j}, {j, i, k}, {j, k, i}, {k, i, j}, {k, j, i}};
+                double acc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+                VS_UNROLL
                 for (int pi = 0; pi < 6; pi++) {
                     bool dup = false;
+                    VS_UNROLL
                     for (int pj = 0; pj < pi; pj++)
-                        if (perm[pj][0] == perm[pi][0] && perm[pj][1] == perm[pi][1] && perm[pj][2] == perm[pi][2])
-                            dup = true;
+                        dup |= perm[pj][0] == perm[pi][0] && perm[pj][1] == perm[pi][1] && perm[pj][2] == perm[pi][2];
                     if (dup) continue;
                     const double* Ea = B[perm[pi][0]];
                     const double* Eb = B[perm[pi][1]];
                     const double* Ec = B[perm[pi][2]];
-                    A[0][col] += det3m(Ea, Eb, Ec);
+                    acc[0] += det3m(Ea, Eb, Ec);
                     double T[9];
                     trilin(Ea, Eb, Ec, T);
-                    for (int e = 0; e < 9; e++) A[1 + e][col] += T[e];
+                    VS_UNROLL
+                    for (int e = 0; e < 9; e++) acc[1 + e] += T[e];
                 }
+                VS_UNROLL
+                for (int r = 0; r < 10; r++) AA(r, col) = acc[r];
             }
-    // Gauss-Jordan on the first 10 columns
+    // Gauss-Jordan on the first 10 columns (partial pivoting), in the workspace
     for (int k = 0; k < 10; k++) {
         int p = k;
         for (int r = k + 1; r < 10; r++)
-            if (fabs(A[r][k]) > fabs(A[p][k])) p = r;
-        if (!(fabs(A[p][k]) > 1e-300)) return 0;
+            if (fabs(AA(r, k)) > fabs(AA(p, k))) p = r;
+        if (!(fabs(AA(p, k)) > 1e-300)) return 0;
         if (p != k)
-            for (int c = 0; c < 20; c++) {
-                const double tmp = A[k][c];
-                A[k][c] = A[p][c];
-                A[p][c] = tmp;
+            for (int c = k; c < 20; c++) {
+                const double tmp = AA(k, c);
+                AA(k, c) = AA(p, c);
+                AA(p, c) = tmp;
             }
-        const double inv = 1.0 / A[k][k];
-        for (int c = k; c < 20; c++) A[k][c] *= inv;
+        const double inv = 1.0 / AA(k, k);
+        for (int c = k; c < 20; c++) AA(k, c) *= inv;
         for (int r = 0; r < 10; r++) {
             if (r == k) continue;
-            const double f = A[r][k];
+            const double f = AA(r, k);
             if (f == 0) continue;
-            for (int c = k; c < 20; c++) A[r][c] -= f * A[k][c];
+            for (int c = k; c < 20; c++) AA(r, c) -= f * AA(k, c);
         }
     }
     // B(z) rows <e> - z <f> over (x, y, 1): x-poly deg 3, y-poly deg 3, 1-poly deg 4 (coefficient
-    // arrays indexed by the power of z)
+    // arrays indexed by the power of z); rest monomials: xz^2 xz x yz^2 yz y z^3 z^2 z 1
     double bx[3][4], by[3][4], b1[3][5];
+    VS_UNROLL
     for (int i = 0; i < 3; i++) {
-        const double* e = &A[4 + 2 * i][10];
-        const double* f = &A[5 + 2 * i][10];
-        // rest monomials: xz^2 xz x yz^2 yz y z^3 z^2 z 1
-        bx[i][3] = -f[0];
-        bx[i][2] = e[0] - f[1];
-        bx[i][1] = e[1] - f[2];
-        bx[i][0] = e[2];
-        by[i][3] = -f[3];
-        by[i][2] = e[3] - f[4];
-        by[i][1] = e[4] - f[5];
-        by[i][0] = e[5];
-        b1[i][4] = -f[6];
-        b1[i][3] = e[6] - f[7];
-        b1[i][2] = e[7] - f[8];
-        b1[i][1] = e[8] - f[9];
-        b1[i][0] = e[9];
+        const int re = 4 + 2 * i, rf = 5 + 2 * i;
+        bx[i][3] = -AA(rf, 10);
+        bx[i][2] = AA(re, 10) - AA(rf, 11);
+        bx[i][1] = AA(re, 11) - AA(rf, 12);
+        bx[i][0] = AA(re, 12);
+        by[i][3] = -AA(rf, 13);
+        by[i][2] = AA(re, 13) - AA(rf, 14);
+        by[i][1] = AA(re, 14) - AA(rf, 15);
+        by[i][0] = AA(re, 15);
+        b1[i][4] = -AA(rf, 16);
+        b1[i][3] = AA(re, 16) - AA(rf, 17);
+        b1[i][2] = AA(re, 17) - AA(rf, 18);
+        b1[i][1] = AA(re, 18) - AA(rf, 19);
+        b1[i][0] = AA(re, 19);
     }
     // det B(z) (degree 10) by cofactor expansion with polynomial products
     auto pmul = [](const double* a, int na, const double* b, int nb, double* out) {
@@ -287,6 +339,7 @@ VS_HD inline int five_point(const double* q1, const double* q2, double (*E)[9]) 
             for (int j = 0; j <= nb; j++) out[i + j] += a[i] * b[j];
     };
     double c[11];
+    VS_UNROLL
     for (int k = 0; k < 11; k++) c[k] = 0;
     {
         // det = bx0 (by1 b12 - b11 by2) - by0 (bx1 b12 - b11 bx2) + b10 (bx1 by2 - by1 bx2)
@@ -308,20 +361,24 @@ VS_HD inline int five_point(const double* q1, const double* q2, double (*E)[9]) 
         pmul(b1[0], 4, m2, 6, full);
         for (int k = 0; k <= 10; k++) c[k] += full[k];
     }
-    double zr[10];
-    const int nz = poly_real_roots(c, 10, zr);
+    VS_UNROLL
+    for (int k = 0; k < 11; k++) WS(kWsP + k) = c[k];
+    const int nz = poly_real_roots(W, wst);
     int count = 0;
     for (int ri = 0; ri < nz && count < kMaxModels; ri++) {
-        const double z = zr[ri];
+        const double z = WS(kWsR + ri);
         double Bz[3][3];
+        VS_UNROLL
         for (int i = 0; i < 3; i++) {
-            Bz[i][0] = poly_eval(bx[i], 3, z);
-            Bz[i][1] = poly_eval(by[i], 3, z);
-            Bz[i][2] = poly_eval(b1[i], 4, z);
+            Bz[i][0] = ((bx[i][3] * z + bx[i][2]) * z + bx[i][1]) * z + bx[i][0];
+            Bz[i][1] = ((by[i][3] * z + by[i][2]) * z + by[i][1]) * z + by[i][0];
+            Bz[i][2] = (((b1[i][4] * z + b1[i][3]) * z + b1[i][2]) * z + b1[i][1]) * z + b1[i][0];
         }
         // null vector of Bz: the largest cross product of two rows
-        double best[3] = {0, 0, 0}, bn = -1;
+        double best0 = 0, best1 = 0, best2 = 0, bn = -1;
+        VS_UNROLL
         for (int a = 0; a < 3; a++)
+            VS_UNROLL
             for (int b = a + 1; b < 3; b++) {
                 const double cx = Bz[a][1] * Bz[b][2] - Bz[a][2] * Bz[b][1];
                 const double cy = Bz[a][2] * Bz[b][0] - Bz[a][0] * Bz[b][2];
@@ -329,27 +386,37 @@ VS_HD inline int five_point(const double* q1, const double* q2, double (*E)[9]) 
                 const double nn = cx * cx + cy * cy + cz * cz;
                 if (nn > bn) {
                     bn = nn;
-                    best[0] = cx;
-                    best[1] = cy;
-                    best[2] = cz;
+                    best0 = cx;
+                    best1 = cy;
+                    best2 = cz;
                 }
             }
         const double nrm = sqrt(bn > 0 ? bn : 0.0);
         if (!(nrm > 0)) continue;
-        const double v0 = best[0] / nrm, v1 = best[1] / nrm, v2 = best[2] / nrm;
+        const double v0 = best0 / nrm, v1 = best1 / nrm, v2 = best2 / nrm;
         if (fabs(v2) < 1e-10) continue;
         const double x = v0 / v2, y = v1 / v2;
         double e[9], en = 0;
+        VS_UNROLL
         for (int q = 0; q < 9; q++) {
             e[q] = B[0][q] * x + B[1][q] * y + B[2][q] * z + B[3][q];
             en += e[q] * e[q];
         }
         en = sqrt(en);
         if (!(en > 0)) continue;
-        for (int q = 0; q < 9; q++) E[count][q] = e[q] / en;
+        VS_UNROLL
+        for (int q = 0; q < 9; q++) Eout[count * 9 + q] = e[q] / en;
         count++;
     }
     return count;
+#undef AA
+#undef WS
+}
+
+// host convenience: the workspace on the stack
+inline int five_point(const double* q1, const double* q2, double (*E)[9]) {
+    double ws[kWsSize];
+    return five_point(q1, q2, &E[0][0], ws, 1);
 }
 
 // EMEstimatorCallback::computeError (Sampson distance, float)

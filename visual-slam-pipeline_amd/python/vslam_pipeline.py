@@ -93,6 +93,12 @@ class DevicePipeline:
         self.t = torch.zeros((P, 3), dtype=torch.float64, device=dev)
         self.ok = torch.zeros(P, dtype=torch.int32, device=dev)
         self.diag = torch.zeros((P, 4), dtype=torch.int32, device=dev)
+        # E-matrix fallback (Slam.cpp:965-984) for pairs whose 3D-3D estimate failed
+        self.eR = torch.zeros((P, 9), dtype=torch.float64, device=dev)
+        self.et = torch.zeros((P, 3), dtype=torch.float64, device=dev)
+        self.escale = torch.zeros(P, dtype=torch.float64, device=dev)
+        self.eok = torch.zeros(P, dtype=torch.int32, device=dev)
+        self.ediag = torch.zeros((P, 8), dtype=torch.int32, device=dev)
         self.seeds = torch.zeros(P, dtype=torch.int32, device=dev)
         self._seed_base = torch.arange(P, dtype=torch.int64, device=dev)
         self.xchg = FeatureExchange(B, cap, rank, world, group, dev) if world > 1 else None
@@ -131,21 +137,56 @@ class DevicePipeline:
                                   self.nfkept.data_ptr(), self.depth.data_ptr(), h, w, self.K, self.seeds.data_ptr(),
                                   self.iters, self.thr, self.R.data_ptr(), self.t.data_ptr(), self.ok.data_ptr(),
                                   self.diag.data_ptr(), s)
+        # Slam.cpp:965-984: pairs whose 3D-3D estimate failed fall back to the essential matrix
+        # with depth scale (the kernel skips pairs with ok != 0)
+        ctx.emat_motion_pairs_dev(B, self.pairs.data_ptr(), self.kps.data_ptr(), cap, self.fkept.data_ptr(),
+                                  self.nfkept.data_ptr(), self.ok.data_ptr(), self.depth.data_ptr(), h, w,
+                                  self.eR.data_ptr(), self.et.data_ptr(), self.escale.data_ptr(),
+                                  self.eok.data_ptr(), self.ediag.data_ptr(), K=self.K, stream=s)
         return dict(kps=self.kps[1:], desc=self.desc[1:], n=self.n[1:], good=self.good, ngood=self.ngood,
                     kept=self.fkept, nkept=self.nfkept, F=self.F, eperr=self.eperr, fdiag=self.fdiag,
-                    R=self.R, t=self.t, ok=self.ok, diag=self.diag)
+                    R=self.R, t=self.t, ok=self.ok, diag=self.diag, eR=self.eR, et=self.et, escale=self.escale,
+                    eok=self.eok, ediag=self.ediag)
 
 
-def compose_poses(R_rel, t_rel, ok, R0=None, t0=None):
-    """Host pose chain (Slam.cpp:963-964): R_new = R_ref R^T, t_new = t_ref - R_new t; a failed pair
-    keeps the previous pose (the reference then falls back to E-matrix motion, not modelled here)."""
-    R = np.eye(3) if R0 is None else R0.copy()
-    t = np.zeros(3) if t0 is None else t0.copy()
+MOTION_SCALE = 0.05  # Config.h:129
+
+
+class PoseChain:
+    """Host pose chain of Slam::process_frame (Slam.cpp:961-984): a 3D-3D result composes as
+    R_new = R_ref R^T, t_new = t_ref - R_new t; otherwise the essential-matrix result composes with
+    its depth scale (falling back to the last good scale, then MOTION_SCALE); a pair with neither
+    keeps the pose (the reference returns false for that frame)."""
+
+    def __init__(self, R0=None, t0=None):
+        self.R = np.eye(3) if R0 is None else np.array(R0, np.float64)
+        self.t = np.zeros(3) if t0 is None else np.array(t0, np.float64)
+        self.last_good_scale = -1.0
+
+    def step(self, ok3d, R3d, t3d, eok=0, eR=None, et=None, escale=-1.0):
+        if ok3d:
+            Rn = self.R @ np.asarray(R3d).reshape(3, 3).T
+            self.t = self.t - Rn @ np.asarray(t3d)
+            self.R = Rn
+        elif eok:
+            scale = escale
+            if scale <= 0:
+                scale = self.last_good_scale if self.last_good_scale > 0 else MOTION_SCALE
+            else:
+                self.last_good_scale = scale
+            Rn = self.R @ np.asarray(eR).reshape(3, 3).T
+            self.t = self.t - Rn @ (scale * np.asarray(et))
+            self.R = Rn
+        return self.R.copy(), self.t.copy()
+
+
+def compose_poses(R_rel, t_rel, ok, R0=None, t0=None, eR=None, et=None, escale=None, eok=None):
+    """Pose chain over a batch of pair results (see PoseChain)."""
+    chain = PoseChain(R0, t0)
     out = []
-    for Rr, tr, k in zip(R_rel, t_rel, ok):
-        if k:
-            Rn = R @ Rr.reshape(3, 3).T
-            t = t - Rn @ tr
-            R = Rn
-        out.append((R.copy(), t.copy()))
+    for p in range(len(ok)):
+        if eok is not None:
+            out.append(chain.step(ok[p], R_rel[p], t_rel[p], eok[p], eR[p], et[p], escale[p]))
+        else:
+            out.append(chain.step(ok[p], R_rel[p], t_rel[p]))
     return out
