@@ -8,7 +8,8 @@ through the whole per-frame hot path by libvslam_hip.so:
     Slam::estimate_motion_3d3d  (200-iteration 3D-3D RANSAC + refit, on the F-filtered matches)
     Slam::estimate_motion       (5-point essential matrix + recoverPose + depth scale, for the pairs
                                  whose 3D-3D estimate failed, Slam.cpp:965-984)
-plus the host pose chain on the returned (R, t) (Slam.cpp:963-964).  With --gpus N > 1 the frames
+plus the host pose chain on the returned (R, t) (Slam.cpp:963-964).  Steps are software-pipelined
+over two HIP streams (DevicePipeline): step i's pair geometry runs beside step i+1's network.  With --gpus N > 1 the frames
 are sharded in contiguous blocks across N ranks (one process per GPU) and the per-frame feature
 records are all-gathered over RCCL each step (weak scaling: B frames per GPU per step).
 
@@ -48,7 +49,7 @@ LAYER_FLOPS = {
 
 # profiling stage -> kernel symbol (as rocprofv3 reports it) of that stage's dominant launch
 STAGE_KERNEL = {
-    "conv1_fused": "vs::k_conv_mfma<3, true, 1, true, 16>",
+    "conv1_fused": "vs::k_conv3_db<true, 1, true>",
     "conv2a": "vs::k_conv_mfma<3, false, 2, false, 16>",
     "conv2b_pool": "vs::k_conv_mfma<3, true, 3, false, 16>",
     "conv3a": "vs::k_conv_mfma<3, false, 4, false, 16>",
@@ -82,6 +83,7 @@ def parse():
     ap.add_argument("--batch", type=int, default=32, help="frames per GPU per step")
     ap.add_argument("--cpu-frames", type=int, default=12, help="cpu_baseline sample size (processed frames)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--serial", action="store_true", help="wait for each step's geometry before the next network")
     return ap.parse_args()
 
 
@@ -157,19 +159,32 @@ def main():
     chain = PoseChain()
     n_emat = [0]
 
-    def step(i):
-        out = pipe.run(frames, depth, frame_count0=i * n_total + rank * B, depth_prev=depth_prev)
-        # small D2H: the host tracker consumes the per-pair motion (3D-3D or the E-matrix fallback)
-        R, t, ok = out["R"].cpu().numpy(), out["t"].cpu().numpy(), out["ok"].cpu().numpy()
-        eR, et = out["eR"].cpu().numpy(), out["et"].cpu().numpy()
-        esc, eok = out["escale"].cpu().numpy(), out["eok"].cpu().numpy()
+    def consume(S):
+        # small D2H (one packed pinned copy per step): the host tracker consumes the per-pair motion
+        # (3D-3D or the E-matrix fallback, Slam.cpp:961-984)
+        ok, R, t, eok, eR, et, esc = pipe.collect(S)
         for p in range(B):
             chain.step(ok[p], R[p], t[p], eok[p], eR[p], et[p], esc[p])
         n_emat[0] += int(eok.sum())
         return int(ok.sum())
 
-    for i in range(args.warmup):
-        step(i)
+    def run_steps(first, count):
+        # software pipeline: step i's network is enqueued before the host waits for step i-1's
+        # geometry, so the geometry of one step overlaps the network of the next
+        n_ok, pending = 0, None
+        for i in range(first, first + count):
+            S = pipe.submit(frames, depth, frame_count0=i * n_total + rank * B, depth_prev=depth_prev)
+            if args.serial:
+                n_ok += consume(S)
+                continue
+            if pending is not None:
+                n_ok += consume(pending)
+            pending = S
+        if pending is not None:
+            n_ok += consume(pending)
+        return n_ok
+
+    run_steps(0, args.warmup)
     torch.cuda.synchronize()
     ctx.profile(True)
     ctx.profile_reset()
@@ -177,9 +192,7 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    n_ok = 0
-    for i in range(args.steps):
-        n_ok += step(args.warmup + i)
+    n_ok = run_steps(args.warmup, args.steps)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()

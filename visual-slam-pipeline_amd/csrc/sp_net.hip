@@ -15,6 +15,9 @@
 // latency hides under 288 MFMAs; the MFMA loop reads its LDS operands one k-step ahead.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+#include <cstring>
+
 #include "vs_internal.h"
 
 namespace vs {
@@ -301,6 +304,221 @@ __global__ __launch_bounds__(256, (KS == 3 && CKV == 32) ? 1 : 2) void k_conv_mf
     }
 }
 
+// Double-buffered 3x3 conv: 8-channel chunks, s_in / s_w in two LDS buffers (63 KB with the fused
+// conv1a, two workgroups per CU), ONE barrier per chunk.  While chunk k's 36 k-steps run on the
+// matrix cores, chunk k+1 is staged into the other buffer: global loads issued at the top of the
+// chunk and written to LDS six k-steps before its end, or (FUSE1A) conv1a evaluated straight into
+// the buffer, one channel every four k-steps.  Nothing staged is held across the MFMA loop except
+// 8 float4 of loads, so the kernel fits two waves per SIMD without spilling.  Tiles, wave roles
+// and the epilogue (bias, ReLU, in-register 2x2 pool) are those of k_conv_mfma.
+template <bool POOL, int LAYER, bool FUSE1A>
+__global__ __launch_bounds__(256, 2) void k_conv3_db(
+    const float* __restrict__ in, int in_cstride, int in_coff, const float* __restrict__ wt,
+    const float* __restrict__ bias, int cin, int cout, int cout_pad, float* __restrict__ out,
+    int out_cstride, int out_coff, int B, int H, int W, int tiles_x, int tiles_y, int relu,
+    const float* __restrict__ w1a, const float* __restrict__ b1a) {
+    constexpr int CK = 8, TW = 32, TH = 8, PW = TW + 2, PH = TH + 2, NPIX = PW * PH;
+    constexpr int Q = CK / 4;                       // float4 per pixel and chunk
+    constexpr int NQ = (NPIX * Q + 255) / 256;      // input float4 per thread
+    constexpr int NWV = 9 * CK * 16;                // weight float4 per chunk
+    constexpr int NW = (NWV + 255) / 256;           // weight float4 per thread
+    constexpr int S = 9 * CK / 2;                   // MFMA k-steps per chunk
+    constexpr int GW = PW + 2, GH = PH + 2;         // gray patch for the fused conv1a
+    constexpr int SW = S - 6;                       // k-step at which staged loads go to LDS
+    static_assert(NPIX > 256 && NPIX <= 512 && 4 * (CK - 1) + 2 < S, "conv3_db geometry");
+    __shared__ float s_in[2][CK * NPIX];
+    __shared__ __attribute__((aligned(16))) float s_w[2][9 * CK * 64];
+    __shared__ float s_g[FUSE1A ? GW * GH : 1];
+    __shared__ __attribute__((aligned(16))) float s_w1a[FUSE1A ? 12 * 64 : 4];  // [channel][9 taps, bias, 0, 0]
+    __shared__ float s_trash[FUSE1A ? 256 : 1];      // sink of the masked second-pixel stores
+
+    const int tid = threadIdx.x;
+    const int wv = tid >> 6, lane = tid & 63, li = lane & 31, lh = lane >> 5;
+    const int n0 = blockIdx.y * 64;
+    int t = blockIdx.x;
+    const int tx = t % tiles_x;
+    t /= tiles_x;
+    const int ty = t % tiles_y;
+    const int b = t / tiles_y;
+    const int y0 = ty * TH, x0 = tx * TW;
+
+    f32x16 acc[2][2];
+#pragma unroll
+    for (int r = 0; r < 2; r++)
+#pragma unroll
+        for (int nb = 0; nb < 2; nb++)
+#pragma unroll
+            for (int e = 0; e < 16; e++) acc[r][nb][e] = 0.0f;
+
+    // fused conv1a: thread tid owns patch pixels tid and tid + 256 (< NPIX)
+    int gbase[2] = {0, 0};
+    bool gin[2] = {false, false};
+    if constexpr (FUSE1A) {
+        const float* g = in + (size_t)b * H * W;
+        for (int i = tid; i < GW * GH; i += 256) {
+            const int yy = i / GW, xx = i - yy * GW;
+            const int gy = y0 - 2 + yy, gx = x0 - 2 + xx;
+            s_g[i] = (gy >= 0 && gy < H && gx >= 0 && gx < W) ? g[(size_t)gy * W + gx] : 0.0f;
+        }
+        for (int i = tid; i < 12 * 64; i += 256) {
+            const int c = i / 12, k = i - c * 12;
+            s_w1a[i] = k < 9 ? w1a[k * 64 + c] : k == 9 ? b1a[c] : 0.0f;
+        }
+#pragma unroll
+        for (int i = 0; i < 2; i++) {
+            const int p = tid + 256 * i < NPIX ? tid + 256 * i : 0;
+            const int py = p / PW, px = p - py * PW;
+            const int gy = y0 - 1 + py, gx = x0 - 1 + px;
+            gin[i] = tid + 256 * i < NPIX && gy >= 0 && gy < H && gx >= 0 && gx < W;  // else zero padding
+            gbase[i] = py * GW + px;
+        }
+        __syncthreads();
+    }
+    // conv1a channel c0 + c (bias, taps row-major, ReLU) at this thread's pixels -> s_in[buf][c]
+    auto conv1a_chan = [&](int c, int c0, int buf) {
+        const f32x4* wp = reinterpret_cast<const f32x4*>(&s_w1a[(c0 + c) * 12]);
+        const f32x4 w0 = wp[0], w1 = wp[1], w2 = wp[2];
+        const float wk[10] = {w0[0], w0[1], w0[2], w0[3], w1[0], w1[1], w1[2], w1[3], w2[0], w2[1]};
+#pragma unroll
+        for (int i = 0; i < 2; i++) {
+            float a = wk[9];
+#pragma unroll
+            for (int k = 0; k < 9; k++) a += s_g[gbase[i] + (k / 3) * GW + k % 3] * wk[k];
+            a = a > 0.0f ? a : 0.0f;
+            float* dst = (i == 0 || tid + 256 < NPIX) ? &s_in[buf][c * NPIX + tid + 256 * i] : &s_trash[tid];
+            *dst = gin[i] ? a : 0.0f;
+        }
+    };
+
+    f32x4 rin[FUSE1A ? 1 : NQ];
+    f32x4 rw[NW];
+    auto fetch = [&](int c0) {
+        if constexpr (!FUSE1A) {
+#pragma unroll
+            for (int j = 0; j < NQ; j++) {
+                const int idx = tid + 256 * j;
+                const int p = idx / Q, q = idx - p * Q;
+                f32x4 v = {0.f, 0.f, 0.f, 0.f};
+                if (idx < NPIX * Q) {
+                    const int py = p / PW, px = p - py * PW;
+                    const int gy = y0 - 1 + py, gx = x0 - 1 + px;
+                    if (gy >= 0 && gy < H && gx >= 0 && gx < W)
+                        v = *reinterpret_cast<const f32x4*>(in + (((size_t)b * H + gy) * W + gx) * in_cstride + in_coff +
+                                                            c0 + 4 * q);
+                }
+                rin[j] = v;
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < NW; j++) {
+            const int idx = tid + 256 * j;
+            if (idx < NWV) {
+                const int r = idx >> 4, q = idx & 15;
+                const int kk = r / CK, c = r - kk * CK;
+                rw[j] = *reinterpret_cast<const f32x4*>(wt + ((size_t)kk * cin + c0 + c) * cout_pad + n0 + 4 * q);
+            }
+        }
+    };
+    auto stage = [&](int buf) {
+        if constexpr (!FUSE1A) {
+#pragma unroll
+            for (int j = 0; j < NQ; j++) {
+                const int idx = tid + 256 * j;
+                if (idx < NPIX * Q) {
+                    const int p = idx / Q, q = idx - p * Q;
+#pragma unroll
+                    for (int e = 0; e < 4; e++) s_in[buf][(4 * q + e) * NPIX + p] = rin[j][e];
+                }
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < NW; j++) {
+            const int idx = tid + 256 * j;
+            if (idx < NWV) {
+                const int r = idx >> 4, q = idx & 15;
+                *reinterpret_cast<f32x4*>(&s_w[buf][r * 64 + 4 * q]) = rw[j];
+            }
+        }
+    };
+
+    fetch(0);
+    if constexpr (FUSE1A) {
+#pragma unroll
+        for (int c = 0; c < CK; c++) conv1a_chan(c, 0, 0);
+    }
+    stage(0);
+    __syncthreads();
+    const int nchunk = cin / CK;
+    for (int k = 0; k < nchunk; k++) {
+        const int cur = k & 1, nxt = cur ^ 1;
+        const bool more = k + 1 < nchunk;
+        const int cn = (k + 1) * CK;
+        if (more) fetch(cn);
+        const float* si = s_in[cur];
+        const float* sw = s_w[cur];
+        auto operands = [&](int s, float& a0, float& a1, float& b0, float& b1) {
+            const int kk = s / (CK / 2), cp = s - kk * (CK / 2);
+            const int ky = kk / 3, kx = kk - ky * 3;
+            const int c = 2 * cp + lh;
+            a0 = si[c * NPIX + (2 * wv + 0 + ky) * PW + li + kx];
+            a1 = si[c * NPIX + (2 * wv + 1 + ky) * PW + li + kx];
+            b0 = sw[(kk * CK + c) * 64 + li];
+            b1 = sw[(kk * CK + c) * 64 + 32 + li];
+        };
+        float A0[2], A1[2], B0[2], B1[2];
+        operands(0, A0[0], A1[0], B0[0], B1[0]);
+#pragma unroll
+        for (int s = 0; s < S; s++) {
+            const int c_ = s & 1, n_ = c_ ^ 1;
+            if (s + 1 < S) operands(s + 1, A0[n_], A1[n_], B0[n_], B1[n_]);
+            if constexpr (FUSE1A) {
+                if (more && s % 4 == 2 && s / 4 < CK) conv1a_chan(s / 4, cn, nxt);
+            }
+            if (more && s == SW) stage(nxt);
+            __builtin_amdgcn_sched_barrier(0);
+            acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(A0[c_], B0[c_], acc[0][0], 0, 0, 0);
+            acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(A0[c_], B1[c_], acc[0][1], 0, 0, 0);
+            acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(A1[c_], B0[c_], acc[1][0], 0, 0, 0);
+            acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(A1[c_], B1[c_], acc[1][1], 0, 0, 0);
+        }
+        __syncthreads();
+    }
+
+#pragma unroll
+    for (int nb = 0; nb < 2; nb++) {
+        const int n = n0 + nb * 32 + li;
+        if (n >= cout) continue;
+        const float bv = bias[n];
+        if constexpr (POOL) {
+            const int y = y0 + 2 * wv;
+            if (y >= H) continue;
+            const int Wo = W >> 1;
+#pragma unroll
+            for (int reg = 0; reg < 16; reg += 2) {
+                const int px = (reg & 3) + 8 * (reg >> 2) + 4 * lh;
+                const int x = x0 + px;
+                if (x >= W) continue;
+                float m = fmaxf(fmaxf(acc[0][nb][reg], acc[0][nb][reg + 1]), fmaxf(acc[1][nb][reg], acc[1][nb][reg + 1]));
+                m += bv;
+                if (relu) m = fmaxf(m, 0.0f);
+                out[(((size_t)b * (H >> 1) + (y >> 1)) * Wo + (x >> 1)) * out_cstride + out_coff + n] = m;
+            }
+        } else {
+#pragma unroll
+            for (int r = 0; r < 2; r++) {
+#pragma unroll
+                for (int reg = 0; reg < 16; reg++) {
+                    const int px = (reg & 3) + 8 * (reg >> 2) + 4 * lh;
+                    float v = acc[r][nb][reg] + bv;
+                    if (relu) v = fmaxf(v, 0.0f);
+                    const int y = y0 + 2 * wv + r, x = x0 + px;
+                    if (y < H && x < W) out[(((size_t)b * H + y) * W + x) * out_cstride + out_coff + n] = v;
+                }
+            }
+        }
+    }
+}
+
 // Descriptor head output: L2-normalise every pixel's 256 channels (MagicLeap export convention,
 // SURVEY.md 8(a) A3).  One wave per pixel, 16-byte loads, shuffle-tree sum of squares.
 __global__ __launch_bounds__(256) void k_desc_l2norm(float* __restrict__ d, long npix) {
@@ -354,12 +572,36 @@ int launch_conv(const DevLayer& L, const float* in, int in_cstride, int in_coff,
 // 3x3 layers use a 16-channel chunk: 58.6 KB of LDS, two workgroups per CU, so one workgroup's
 // staging overlaps the other's MFMAs.  (A 32-channel chunk at one workgroup per CU measured
 // 1.5x slower end to end: 1306 vs 1952 frames/s, round 1.)
+// conv1 (fused conv1a) runs the double-buffered kernel: 6.56 vs 6.84 ms per 32 frames (round 1
+// A/B); the other 3x3 layers measured the same or 1-2% slower with it and keep the single-buffered
+// 16-channel kernel.  VS_CONV3=single selects the single-buffered conv1 too (A/B measurements).
+inline bool conv3_db_enabled() {
+    static const bool on = [] {
+        const char* e = std::getenv("VS_CONV3");
+        return !(e && std::strcmp(e, "single") == 0);
+    }();
+    return on;
+}
+
 template <bool POOL, int LAYER, bool FUSE1A = false>
 int conv3(vs_ctx* ctx, const DevLayer& L, const float* in, int in_cstride, int in_coff, float* out, int out_cstride,
           int out_coff, int B, int H, int W, hipStream_t s, const DevLayer* L1a = nullptr) {
     (void)ctx;
-    return launch_conv<3, POOL, LAYER, FUSE1A, 16>(L, in, in_cstride, in_coff, out, out_cstride, out_coff, B, H, W, 1,
-                                                   s, L1a);
+    if (!FUSE1A || !conv3_db_enabled())
+        return launch_conv<3, POOL, LAYER, FUSE1A, 16>(L, in, in_cstride, in_coff, out, out_cstride, out_coff, B, H,
+                                                       W, 1, s, L1a);
+    if (L.cin % 8 != 0 || L.cout_pad % 64 != 0 || (!FUSE1A && (in_cstride % 4 || in_coff % 4)) || (FUSE1A && !L1a) ||
+        (POOL && ((H | W) & 1))) {
+        set_error("conv3: unsupported geometry");
+        return VS_ERR_ARG;
+    }
+    const int tiles_x = (W + 31) / 32, tiles_y = (H + 7) / 8;
+    dim3 grid((unsigned)(B * tiles_x * tiles_y), L.cout_pad / 64);
+    hipLaunchKernelGGL((k_conv3_db<POOL, LAYER, FUSE1A>), grid, dim3(256), 0, s, in, in_cstride, in_coff, L.w, L.b,
+                       L.cin, L.cout, L.cout_pad, out, out_cstride, out_coff, B, H, W, tiles_x, tiles_y, 1,
+                       L1a ? L1a->w : nullptr, L1a ? L1a->b : nullptr);
+    VS_HIP(hipGetLastError());
+    return VS_OK;
 }
 
 }  // namespace

@@ -66,87 +66,137 @@ class FeatureExchange:
         return self.g_kps, self.g_desc, self.g_n
 
 
+class _StepSet:
+    """Device tables of one in-flight step (feature records of the block + halo slot, depth,
+    per-pair matches / F / motion results) plus pinned host copies of the per-pair motion."""
+
+    def __init__(self, B, h, w, cap, dev):
+        F = B + 1  # slot 0 = the frame before this rank's block
+        P = B
+        z = lambda *shape, dt=torch.int32: torch.zeros(shape, dtype=dt, device=dev)
+        self.kps, self.desc, self.n = z(F, cap * KP_BYTES, dt=torch.uint8), z(F, cap, 256, dt=torch.float32), z(F)
+        self.depth = z(F, h, w, dt=torch.float32)
+        self.raw, self.good = z(P, cap * M_BYTES, dt=torch.uint8), z(P, cap * M_BYTES, dt=torch.uint8)
+        self.nraw, self.ngood = z(P), z(P)
+        self.fkept, self.nfkept = z(P, cap * M_BYTES, dt=torch.uint8), z(P)
+        self.F, self.eperr, self.fdiag = z(P, 9, dt=torch.float64), z(P, 2, dt=torch.float64), z(P, 8)
+        self.R, self.t, self.ok, self.diag = z(P, 9, dt=torch.float64), z(P, 3, dt=torch.float64), z(P), z(P, 4)
+        # E-matrix fallback (Slam.cpp:965-984) for pairs whose 3D-3D estimate failed
+        self.eR, self.et = z(P, 9, dt=torch.float64), z(P, 3, dt=torch.float64)
+        self.escale, self.eok, self.ediag = z(P, dt=torch.float64), z(P), z(P, 8)
+        self.seeds = z(P)
+        self.motion = torch.zeros(P * 27, dtype=torch.float64, device=dev)  # R t ok eR et escale eok
+        self.host = torch.zeros(P * 27, dtype=torch.float64, pin_memory=True)
+        self.net_done = torch.cuda.Event()
+        self.geo_done = torch.cuda.Event()
+        self.geo_done.record()  # nothing pending on a fresh set
+
+
 class DevicePipeline:
+    """Two-stream software pipeline over the step's frames.  submit() enqueues step k's extraction
+    on the network stream and its pair geometry (match, F verification, 3D-3D RANSAC, E fallback)
+    on the geometry stream behind an event, into buffer set k % 2; collect() waits for that step's
+    geometry and returns its per-pair motion.  The geometry of step k (a few dozen workgroups)
+    therefore runs on the CUs the network of step k+1 leaves idle instead of serialising after it.
+    Set k % 2 is rewritten only after step k-2's geometry finished (event wait, no host sync)."""
+
     def __init__(self, ctx, B, h=480, w=640, cap=va.SP_MAX_KEYPOINTS, K=va.K_TUM, iters=200, thr=0.05,
                  ratio=0.75, rank=0, world=1, group=None):
         self.ctx, self.B, self.h, self.w, self.cap = ctx, B, h, w, cap
         self.K, self.iters, self.thr, self.ratio = K, iters, thr, ratio
         self.rank, self.world, self.group = rank, world, group
         dev = torch.device("cuda", torch.cuda.current_device())
-        F = B + 1  # slot 0 = the frame before this rank's block
-        self.kps = torch.zeros((F, cap * KP_BYTES), dtype=torch.uint8, device=dev)
-        self.desc = torch.zeros((F, cap, 256), dtype=torch.float32, device=dev)
-        self.n = torch.zeros(F, dtype=torch.int32, device=dev)
-        self.depth = torch.zeros((F, h, w), dtype=torch.float32, device=dev)
-        P = B
-        self.pairs = torch.tensor([[p, p + 1] for p in range(P)], dtype=torch.int32, device=dev)
-        self.raw = torch.zeros((P, cap * M_BYTES), dtype=torch.uint8, device=dev)
-        self.good = torch.zeros((P, cap * M_BYTES), dtype=torch.uint8, device=dev)
-        self.nraw = torch.zeros(P, dtype=torch.int32, device=dev)
-        self.ngood = torch.zeros(P, dtype=torch.int32, device=dev)
-        self.fkept = torch.zeros((P, cap * M_BYTES), dtype=torch.uint8, device=dev)
-        self.nfkept = torch.zeros(P, dtype=torch.int32, device=dev)
-        self.F = torch.zeros((P, 9), dtype=torch.float64, device=dev)
-        self.eperr = torch.zeros((P, 2), dtype=torch.float64, device=dev)
-        self.fdiag = torch.zeros((P, 8), dtype=torch.int32, device=dev)
-        self.R = torch.zeros((P, 9), dtype=torch.float64, device=dev)
-        self.t = torch.zeros((P, 3), dtype=torch.float64, device=dev)
-        self.ok = torch.zeros(P, dtype=torch.int32, device=dev)
-        self.diag = torch.zeros((P, 4), dtype=torch.int32, device=dev)
-        # E-matrix fallback (Slam.cpp:965-984) for pairs whose 3D-3D estimate failed
-        self.eR = torch.zeros((P, 9), dtype=torch.float64, device=dev)
-        self.et = torch.zeros((P, 3), dtype=torch.float64, device=dev)
-        self.escale = torch.zeros(P, dtype=torch.float64, device=dev)
-        self.eok = torch.zeros(P, dtype=torch.int32, device=dev)
-        self.ediag = torch.zeros((P, 8), dtype=torch.int32, device=dev)
-        self.seeds = torch.zeros(P, dtype=torch.int32, device=dev)
-        self._seed_base = torch.arange(P, dtype=torch.int64, device=dev)
+        self.sets = [_StepSet(B, h, w, cap, dev) for _ in range(2)]
+        self.k = 0
+        self.pairs = torch.tensor([[p, p + 1] for p in range(B)], dtype=torch.int32, device=dev)
+        self._seed_base = torch.arange(B, dtype=torch.int64, device=dev)
+        self.s_net = torch.cuda.Stream(device=dev)
+        self.s_geo = torch.cuda.Stream(device=dev)
         self.xchg = FeatureExchange(B, cap, rank, world, group, dev) if world > 1 else None
 
-    def run(self, frames, depth, frame_count0, depth_prev=None):
-        """frames: (B, h, w, 3) uint8 cuda, depth: (B, h, w) float32 cuda, frame_count0: global
+    def submit(self, frames, depth, frame_count0, depth_prev=None):
+        """Enqueue one step (no host synchronisation); returns the step's buffer set for collect().
+        frames: (B, h, w, 3) uint8 cuda, depth: (B, h, w) float32 cuda, frame_count0: global
         processed-frame index of frames[0] (the RANSAC seed is 42 + frame_count, Slam.cpp:276).
         depth_prev: depth of the frame before frames[0] (halo) when world > 1."""
         B, h, w, cap = self.B, self.h, self.w, self.cap
         assert frames.shape == (B, h, w, 3) and frames.dtype == torch.uint8 and frames.is_cuda
         assert depth.shape == (B, h, w) and depth.dtype == torch.float32
-        s = torch.cuda.current_stream().cuda_stream
+        S, prev = self.sets[self.k % 2], self.sets[(self.k + 1) % 2]
+        self.k += 1
         ctx = self.ctx
-        # carry the previous step's last frame into slot 0 (single GPU)
-        if self.world == 1:
-            self.kps[0].copy_(self.kps[B])
-            self.desc[0].copy_(self.desc[B])
-            self.n[0].copy_(self.n[B])
-            self.depth[0].copy_(self.depth[B])
-        elif depth_prev is not None:
-            self.depth[0].copy_(depth_prev)
-        self.depth[1:].copy_(depth)
-        ctx.extract_batch_dev(B, frames.data_ptr(), h, w, self.kps[1:].data_ptr(), self.desc[1:].data_ptr(),
-                              self.n[1:].data_ptr(), cap, s)
-        if self.world > 1:
-            # all-gather the step's feature records; slot 0 <- frame rank*B - 1
-            self.xchg.exchange(self.kps, self.desc, self.n)
-        self.seeds.copy_((self._seed_base + (42 + frame_count0)).to(torch.int32))
-        ctx.match_pairs_dev(B, self.pairs.data_ptr(), B + 1, self.desc.data_ptr(), self.n.data_ptr(), cap,
-                            self.ratio, self.raw.data_ptr(), self.nraw.data_ptr(), self.good.data_ptr(),
-                            self.ngood.data_ptr(), s)
-        ctx.fmat_verify_pairs_dev(B, self.pairs.data_ptr(), self.kps.data_ptr(), cap, self.good.data_ptr(),
-                                  self.ngood.data_ptr(), self.F.data_ptr(), self.fkept.data_ptr(),
-                                  self.nfkept.data_ptr(), self.eperr.data_ptr(), self.fdiag.data_ptr(), s)
-        ctx.ransac_3d3d_pairs_dev(B, self.pairs.data_ptr(), self.kps.data_ptr(), cap, self.fkept.data_ptr(),
-                                  self.nfkept.data_ptr(), self.depth.data_ptr(), h, w, self.K, self.seeds.data_ptr(),
-                                  self.iters, self.thr, self.R.data_ptr(), self.t.data_ptr(), self.ok.data_ptr(),
-                                  self.diag.data_ptr(), s)
-        # Slam.cpp:965-984: pairs whose 3D-3D estimate failed fall back to the essential matrix
-        # with depth scale (the kernel skips pairs with ok != 0)
-        ctx.emat_motion_pairs_dev(B, self.pairs.data_ptr(), self.kps.data_ptr(), cap, self.fkept.data_ptr(),
-                                  self.nfkept.data_ptr(), self.ok.data_ptr(), self.depth.data_ptr(), h, w,
-                                  self.eR.data_ptr(), self.et.data_ptr(), self.escale.data_ptr(),
-                                  self.eok.data_ptr(), self.ediag.data_ptr(), K=self.K, stream=s)
-        return dict(kps=self.kps[1:], desc=self.desc[1:], n=self.n[1:], good=self.good, ngood=self.ngood,
-                    kept=self.fkept, nkept=self.nfkept, F=self.F, eperr=self.eperr, fdiag=self.fdiag,
-                    R=self.R, t=self.t, ok=self.ok, diag=self.diag, eR=self.eR, et=self.et, escale=self.escale,
-                    eok=self.eok, ediag=self.ediag)
+        # inputs are produced on the caller's stream
+        self.s_net.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(self.s_net):
+            self.s_net.wait_event(S.geo_done)  # step k-2's geometry has released this set
+            s = self.s_net.cuda_stream
+            if self.world == 1:  # carry the previous step's last frame into slot 0
+                S.kps[0].copy_(prev.kps[B])
+                S.desc[0].copy_(prev.desc[B])
+                S.n[0].copy_(prev.n[B])
+                S.depth[0].copy_(prev.depth[B])
+            elif depth_prev is not None:
+                S.depth[0].copy_(depth_prev)
+            S.depth[1:].copy_(depth)
+            ctx.extract_batch_dev(B, frames.data_ptr(), h, w, S.kps[1:].data_ptr(), S.desc[1:].data_ptr(),
+                                  S.n[1:].data_ptr(), cap, s)
+            if self.world > 1:
+                # all-gather the step's feature records; slot 0 <- frame rank*B - 1
+                self.xchg.exchange(S.kps, S.desc, S.n)
+            S.net_done.record(self.s_net)
+        with torch.cuda.stream(self.s_geo):
+            self.s_geo.wait_event(S.net_done)
+            s = self.s_geo.cuda_stream
+            S.seeds.copy_((self._seed_base + (42 + frame_count0)).to(torch.int32))
+            ctx.match_pairs_dev(B, self.pairs.data_ptr(), B + 1, S.desc.data_ptr(), S.n.data_ptr(), cap,
+                                self.ratio, S.raw.data_ptr(), S.nraw.data_ptr(), S.good.data_ptr(),
+                                S.ngood.data_ptr(), s)
+            ctx.fmat_verify_pairs_dev(B, self.pairs.data_ptr(), S.kps.data_ptr(), cap, S.good.data_ptr(),
+                                      S.ngood.data_ptr(), S.F.data_ptr(), S.fkept.data_ptr(),
+                                      S.nfkept.data_ptr(), S.eperr.data_ptr(), S.fdiag.data_ptr(), s)
+            ctx.ransac_3d3d_pairs_dev(B, self.pairs.data_ptr(), S.kps.data_ptr(), cap, S.fkept.data_ptr(),
+                                      S.nfkept.data_ptr(), S.depth.data_ptr(), h, w, self.K, S.seeds.data_ptr(),
+                                      self.iters, self.thr, S.R.data_ptr(), S.t.data_ptr(), S.ok.data_ptr(),
+                                      S.diag.data_ptr(), s)
+            # Slam.cpp:965-984: pairs whose 3D-3D estimate failed fall back to the essential matrix
+            # with depth scale (the kernel skips pairs with ok != 0)
+            ctx.emat_motion_pairs_dev(B, self.pairs.data_ptr(), S.kps.data_ptr(), cap, S.fkept.data_ptr(),
+                                      S.nfkept.data_ptr(), S.ok.data_ptr(), S.depth.data_ptr(), h, w,
+                                      S.eR.data_ptr(), S.et.data_ptr(), S.escale.data_ptr(),
+                                      S.eok.data_ptr(), S.ediag.data_ptr(), K=self.K, stream=s)
+            # the host tracker's input: one packed D2H of the per-pair motion
+            torch.cat([S.R.view(-1), S.t.view(-1), S.ok.double(), S.eR.view(-1), S.et.view(-1), S.escale,
+                       S.eok.double()], out=S.motion)
+            S.host.copy_(S.motion, non_blocking=True)
+            S.geo_done.record(self.s_geo)
+        return S
+
+    def collect(self, S):
+        """Wait for a submitted step's geometry; returns (ok, R, t, eok, eR, et, escale) numpy."""
+        S.geo_done.synchronize()
+        P = self.B
+        h = S.host.numpy().copy()  # the pinned buffer is rewritten when this set is reused
+        o = [0]
+
+        def take(k):
+            v = h[o[0]:o[0] + k * P]
+            o[0] += k * P
+            return v.reshape(P, k) if k > 1 else v
+        R, t, ok, eR, et, esc, eok = take(9), take(3), take(1), take(9), take(3), take(1), take(1)
+        return ok.astype(np.int32), R, t, eok.astype(np.int32), eR, et, esc
+
+    @staticmethod
+    def outputs(S):
+        return dict(kps=S.kps[1:], desc=S.desc[1:], n=S.n[1:], good=S.good, ngood=S.ngood,
+                    kept=S.fkept, nkept=S.nfkept, F=S.F, eperr=S.eperr, fdiag=S.fdiag,
+                    R=S.R, t=S.t, ok=S.ok, diag=S.diag, eR=S.eR, et=S.et, escale=S.escale,
+                    eok=S.eok, ediag=S.ediag)
+
+    def run(self, frames, depth, frame_count0, depth_prev=None):
+        """One step, synchronously: the device tables of its buffer set after its geometry."""
+        S = self.submit(frames, depth, frame_count0, depth_prev)
+        S.geo_done.synchronize()
+        return self.outputs(S)
 
 
 MOTION_SCALE = 0.05  # Config.h:129
