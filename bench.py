@@ -49,14 +49,14 @@ LAYER_FLOPS = {
 
 # profiling stage -> kernel symbol (as rocprofv3 reports it) of that stage's dominant launch
 STAGE_KERNEL = {
-    "conv1_fused": "vs::k_conv3_db<true, 1, true>",
+    "conv1_fused": "vs::k_conv3_db<true, 1, true, false>",
     "conv2a": "vs::k_conv_mfma<3, false, 2, false, 16>",
     "conv2b_pool": "vs::k_conv_mfma<3, true, 3, false, 16>",
     "conv3a": "vs::k_conv_mfma<3, false, 4, false, 16>",
     "conv3b_pool": "vs::k_conv_mfma<3, true, 5, false, 16>",
-    "conv4a": "vs::k_conv_mfma<3, false, 6, false, 16>",
-    "conv4b": "vs::k_conv_mfma<3, false, 7, false, 16>",
-    "head_a": "vs::k_conv_mfma<3, false, 8, false, 16>",
+    "conv4a": "vs::k_conv3_db<false, 6, false, true>",
+    "conv4b": "vs::k_conv3_db<false, 7, false, true>",
+    "head_a": "vs::k_conv3_db<false, 8, false, true>",
     "head_b": "vs::k_conv_mfma<1, false, 9, false, 32>",
 }
 

@@ -96,6 +96,21 @@ int vs_extract_batch(vs_ctx* ctx, int B, const uint8_t* const* imgs, int h, int 
 int vs_extract_batch_dev(vs_ctx* ctx, int B, const uint8_t* d_imgs, int h, int w,
                          vs_keypoint* d_kps, float* d_desc, int* d_n, int cap, void* stream);
 
+/* The two halves of vs_extract_batch_dev, so a caller can overlap one batch's post-processing
+ * with the next batch's network on another stream.  Network: d_imgs (B BGR u8 frames) ->
+ * d_semi [B][H/8][W/8][VS_SEMI_CH] logits and d_dgrid [B][H/8][W/8][VS_DESC_DIM] L2-normalised
+ * coarse descriptors (channel-last; H, W rounded up to multiples of 8).  Post-processing (A4-A6:
+ * decode, NMS, top-k, border erase, descriptor sampling) reads them and writes d_kps / d_desc /
+ * d_n as vs_extract_batch_dev does.  Network scratch and post-processing scratch are disjoint in
+ * the context, so the two may run concurrently on different streams (one call of each at a time). */
+#define VS_SEMI_CH 65
+#define VS_DESC_DIM 256
+int vs_network_batch_dev(vs_ctx* ctx, int B, const uint8_t* d_imgs, int h, int w, float* d_semi,
+                         float* d_dgrid, void* stream);
+int vs_postprocess_batch_dev(vs_ctx* ctx, int B, const float* d_semi, const float* d_dgrid, int h,
+                             int w, vs_keypoint* d_kps, float* d_desc, int* d_n, int cap,
+                             void* stream);
+
 /* Stage isolation.  Network only: gray fp32 image (already /255 normalised, H x W) ->
  * semi [65][H/8][W/8] and desc [256][H/8][W/8], the ORT output layout
  * (FeatureExtractor.cpp:120-124,167-168).  H and W must be multiples of 8. */

@@ -35,6 +35,20 @@ def test_network_matches_torch_fp64(vsctx, seq4):
     assert np.max(np.abs(desc - td)) <= 2e-5
 
 
+@pytest.mark.parametrize("h,w", [(152, 200), (64, 96)])
+def test_network_other_geometries_match_torch_fp64(vsctx, h, w):
+    """Widths that are not multiples of 32 at every level: partial 8 x 32 tiles (conv1, pooled
+    layers) and the raster-order linear tiles (unpooled layers at W = 100, 50, 25 / 48, 24, 12)."""
+    from test_oracle import _torch_superpoint
+    rng = np.random.default_rng(h * w)
+    gray = rng.random((h, w), dtype=np.float32)
+    semi, desc = vsctx.superpoint_forward(gray)
+    ts, td = _torch_superpoint(vsctx.weights(), gray)
+    assert semi.shape == ts.shape and desc.shape == td.shape
+    assert np.max(np.abs(semi - ts)) <= 2e-4 * max(1.0, float(np.max(np.abs(ts))))
+    assert np.max(np.abs(desc - td)) <= 2e-5
+
+
 def test_network_matches_oracle_cpu_network(vsctx, oracle, seq4):
     w = vsctx.weights()
     gray = oracle.gray_to_f32(oracle.bgr_to_gray(seq4[1]["bgr"]))

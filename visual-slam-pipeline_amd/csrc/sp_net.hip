@@ -311,22 +311,30 @@ __global__ __launch_bounds__(256, (KS == 3 && CKV == 32) ? 1 : 2) void k_conv_mf
 // the buffer, one channel every four k-steps.  Nothing staged is held across the MFMA loop except
 // 8 float4 of loads, so the kernel fits two waves per SIMD without spilling.  Tiles, wave roles
 // and the epilogue (bias, ReLU, in-register 2x2 pool) are those of k_conv_mfma.
-template <bool POOL, int LAYER, bool FUSE1A>
+//
+// LIN (layers whose width is not a multiple of 32, e.g. the 80 x 60 conv4 / head layers of a
+// 640 x 480 frame): a tile is 256 CONSECUTIVE pixels of the image in raster order instead of an
+// 8 x 32 block, so no MFMA row is spent on columns past the image edge (8 x 32 tiles waste 22% of
+// the grid at W = 80).  The LDS patch holds the rows those pixels span plus the halo, full width
+// (tiles_y = patch rows, <= 640 patch pixels), and every lane addresses its own pixel in it.
+template <bool POOL, int LAYER, bool FUSE1A, bool LIN = false>
 __global__ __launch_bounds__(256, 2) void k_conv3_db(
     const float* __restrict__ in, int in_cstride, int in_coff, const float* __restrict__ wt,
     const float* __restrict__ bias, int cin, int cout, int cout_pad, float* __restrict__ out,
     int out_cstride, int out_coff, int B, int H, int W, int tiles_x, int tiles_y, int relu,
     const float* __restrict__ w1a, const float* __restrict__ b1a) {
     constexpr int CK = 8, TW = 32, TH = 8, PW = TW + 2, PH = TH + 2, NPIX = PW * PH;
+    constexpr int NPIXC = LIN ? 640 : NPIX;         // patch capacity
     constexpr int Q = CK / 4;                       // float4 per pixel and chunk
-    constexpr int NQ = (NPIX * Q + 255) / 256;      // input float4 per thread
+    constexpr int NQ = (NPIXC * Q + 255) / 256;     // input float4 per thread
     constexpr int NWV = 9 * CK * 16;                // weight float4 per chunk
     constexpr int NW = (NWV + 255) / 256;           // weight float4 per thread
     constexpr int S = 9 * CK / 2;                   // MFMA k-steps per chunk
     constexpr int GW = PW + 2, GH = PH + 2;         // gray patch for the fused conv1a
     constexpr int SW = S - 6;                       // k-step at which staged loads go to LDS
     static_assert(NPIX > 256 && NPIX <= 512 && 4 * (CK - 1) + 2 < S, "conv3_db geometry");
-    __shared__ float s_in[2][CK * NPIX];
+    static_assert(!LIN || (!POOL && !FUSE1A), "linear tiles: plain 3x3 layers only");
+    __shared__ float s_in[2][CK * NPIXC];
     __shared__ __attribute__((aligned(16))) float s_w[2][9 * CK * 64];
     __shared__ float s_g[FUSE1A ? GW * GH : 1];
     __shared__ __attribute__((aligned(16))) float s_w1a[FUSE1A ? 12 * 64 : 4];  // [channel][9 taps, bias, 0, 0]
@@ -335,12 +343,37 @@ __global__ __launch_bounds__(256, 2) void k_conv3_db(
     const int tid = threadIdx.x;
     const int wv = tid >> 6, lane = tid & 63, li = lane & 31, lh = lane >> 5;
     const int n0 = blockIdx.y * 64;
-    int t = blockIdx.x;
-    const int tx = t % tiles_x;
-    t /= tiles_x;
-    const int ty = t % tiles_y;
-    const int b = t / tiles_y;
-    const int y0 = ty * TH, x0 = tx * TW;
+    const int HW = H * W;
+    int b, y0, x0, m0 = 0;
+    if constexpr (LIN) {  // tiles_x = tiles per image, tiles_y = patch rows
+        b = blockIdx.x / tiles_x;
+        m0 = (blockIdx.x - b * tiles_x) * 256;
+        y0 = m0 / W;  // first image row of the tile
+        x0 = 0;
+    } else {
+        int t = blockIdx.x;
+        const int tx = t % tiles_x;
+        t /= tiles_x;
+        const int ty = t % tiles_y;
+        b = t / tiles_y;
+        y0 = ty * TH;
+        x0 = tx * TW;
+    }
+    const int pw = LIN ? W + 2 : PW;           // patch row pitch
+    const int npix = LIN ? pw * tiles_y : NPIX;  // patch pixels (per channel)
+    // A-operand base of this lane's pixel in the two M blocks (patch position of tap (0, 0))
+    int abase[2];
+#pragma unroll
+    for (int r = 0; r < 2; r++) {
+        if constexpr (LIN) {
+            int m = m0 + (2 * wv + r) * 32 + li;
+            m = m < HW ? m : HW - 1;  // past the image end: any in-patch pixel, never stored
+            const int y = m / W, x = m - y * W;
+            abase[r] = (y - y0) * pw + x;
+        } else {
+            abase[r] = (2 * wv + r) * PW + li;
+        }
+    }
 
     f32x16 acc[2][2];
 #pragma unroll
@@ -374,20 +407,35 @@ __global__ __launch_bounds__(256, 2) void k_conv3_db(
         }
         __syncthreads();
     }
-    // conv1a channel c0 + c (bias, taps row-major, ReLU) at this thread's pixels -> s_in[buf][c]
-    auto conv1a_chan = [&](int c, int c0, int buf) {
+    // the two pixels' 3x3 gray windows, in registers for the whole kernel
+    float gnb[2][9];
+#pragma unroll
+    for (int i = 0; i < 2; i++)
+#pragma unroll
+        for (int k = 0; k < 9; k++) gnb[i][k] = FUSE1A ? s_g[gbase[i] + (k / 3) * GW + k % 3] : 0.0f;
+    // conv1a channel c0 + c (ReLU) at pixel i from the taps + bias in wq (one broadcast 3 x 16 B
+    // read of s_w1a, issued two k-steps ahead of its use) -> s_in[buf][c]
+    auto w1a_load = [&](int c, int c0, f32x4* wq) {
         const f32x4* wp = reinterpret_cast<const f32x4*>(&s_w1a[(c0 + c) * 12]);
-        const f32x4 w0 = wp[0], w1 = wp[1], w2 = wp[2];
-        const float wk[10] = {w0[0], w0[1], w0[2], w0[3], w1[0], w1[1], w1[2], w1[3], w2[0], w2[1]};
+        wq[0] = wp[0];
+        wq[1] = wp[1];
+        wq[2] = wp[2];
+    };
+    auto conv1a_px = [&](int i, int c, int buf, const f32x4* wq) {
+        const float wk[10] = {wq[0][0], wq[0][1], wq[0][2], wq[0][3], wq[1][0],
+                              wq[1][1], wq[1][2], wq[1][3], wq[2][0], wq[2][1]};
+        float a = wk[9];
 #pragma unroll
-        for (int i = 0; i < 2; i++) {
-            float a = wk[9];
-#pragma unroll
-            for (int k = 0; k < 9; k++) a += s_g[gbase[i] + (k / 3) * GW + k % 3] * wk[k];
-            a = a > 0.0f ? a : 0.0f;
-            float* dst = (i == 0 || tid + 256 < NPIX) ? &s_in[buf][c * NPIX + tid + 256 * i] : &s_trash[tid];
-            *dst = gin[i] ? a : 0.0f;
-        }
+        for (int k = 0; k < 9; k++) a = __builtin_fmaf(gnb[i][k], wk[k], a);
+        a = a > 0.0f ? a : 0.0f;
+        float* dst = (i == 0 || tid + 256 < NPIX) ? &s_in[buf][c * NPIX + tid + 256 * i] : &s_trash[tid];
+        *dst = gin[i] ? a : 0.0f;
+    };
+    auto conv1a_chan = [&](int c, int c0, int buf) {
+        f32x4 wq[3];
+        w1a_load(c, c0, wq);
+        conv1a_px(0, c, buf, wq);
+        conv1a_px(1, c, buf, wq);
     };
 
     f32x4 rin[FUSE1A ? 1 : NQ];
@@ -399,8 +447,8 @@ __global__ __launch_bounds__(256, 2) void k_conv3_db(
                 const int idx = tid + 256 * j;
                 const int p = idx / Q, q = idx - p * Q;
                 f32x4 v = {0.f, 0.f, 0.f, 0.f};
-                if (idx < NPIX * Q) {
-                    const int py = p / PW, px = p - py * PW;
+                if (idx < npix * Q) {
+                    const int py = p / pw, px = p - py * pw;
                     const int gy = y0 - 1 + py, gx = x0 - 1 + px;
                     if (gy >= 0 && gy < H && gx >= 0 && gx < W)
                         v = *reinterpret_cast<const f32x4*>(in + (((size_t)b * H + gy) * W + gx) * in_cstride + in_coff +
@@ -424,10 +472,10 @@ __global__ __launch_bounds__(256, 2) void k_conv3_db(
 #pragma unroll
             for (int j = 0; j < NQ; j++) {
                 const int idx = tid + 256 * j;
-                if (idx < NPIX * Q) {
+                if (idx < npix * Q) {
                     const int p = idx / Q, q = idx - p * Q;
 #pragma unroll
-                    for (int e = 0; e < 4; e++) s_in[buf][(4 * q + e) * NPIX + p] = rin[j][e];
+                    for (int e = 0; e < 4; e++) s_in[buf][(4 * q + e) * npix + p] = rin[j][e];
                 }
             }
         }
@@ -460,24 +508,31 @@ __global__ __launch_bounds__(256, 2) void k_conv3_db(
             const int kk = s / (CK / 2), cp = s - kk * (CK / 2);
             const int ky = kk / 3, kx = kk - ky * 3;
             const int c = 2 * cp + lh;
-            a0 = si[c * NPIX + (2 * wv + 0 + ky) * PW + li + kx];
-            a1 = si[c * NPIX + (2 * wv + 1 + ky) * PW + li + kx];
+            a0 = si[c * npix + abase[0] + ky * pw + kx];
+            a1 = si[c * npix + abase[1] + ky * pw + kx];
             b0 = sw[(kk * CK + c) * 64 + li];
             b1 = sw[(kk * CK + c) * 64 + 32 + li];
         };
         float A0[2], A1[2], B0[2], B1[2];
         operands(0, A0[0], A1[0], B0[0], B1[0]);
+        f32x4 wq[3];
 #pragma unroll
         for (int s = 0; s < S; s++) {
             const int c_ = s & 1, n_ = c_ ^ 1;
             if (s + 1 < S) operands(s + 1, A0[n_], A1[n_], B0[n_], B1[n_]);
-            if constexpr (FUSE1A) {
-                if (more && s % 4 == 2 && s / 4 < CK) conv1a_chan(s / 4, cn, nxt);
-            }
+            // fused conv1a of the next chunk: channel s/4's taps are read at s % 4 == 0 and its two
+            // pixels evaluated at s % 4 == 2, each FMA chain issued behind an MFMA so it runs while
+            // the matrix core is busy
+            const bool c1a = FUSE1A && more && s / 4 < CK;
+            if (c1a && s % 4 == 0) w1a_load(s / 4, cn, wq);
             if (more && s == SW) stage(nxt);
             __builtin_amdgcn_sched_barrier(0);
             acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(A0[c_], B0[c_], acc[0][0], 0, 0, 0);
+            if (c1a && s % 4 == 2) conv1a_px(0, s / 4, nxt, wq);
+            __builtin_amdgcn_sched_barrier(0);
             acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(A0[c_], B1[c_], acc[0][1], 0, 0, 0);
+            if (c1a && s % 4 == 2) conv1a_px(1, s / 4, nxt, wq);
+            __builtin_amdgcn_sched_barrier(0);
             acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(A1[c_], B0[c_], acc[1][0], 0, 0, 0);
             acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(A1[c_], B1[c_], acc[1][1], 0, 0, 0);
         }
@@ -511,8 +566,13 @@ __global__ __launch_bounds__(256, 2) void k_conv3_db(
                     const int px = (reg & 3) + 8 * (reg >> 2) + 4 * lh;
                     float v = acc[r][nb][reg] + bv;
                     if (relu) v = fmaxf(v, 0.0f);
-                    const int y = y0 + 2 * wv + r, x = x0 + px;
-                    if (y < H && x < W) out[(((size_t)b * H + y) * W + x) * out_cstride + out_coff + n] = v;
+                    if constexpr (LIN) {
+                        const int m = m0 + (2 * wv + r) * 32 + px;
+                        if (m < HW) out[((size_t)b * HW + m) * out_cstride + out_coff + n] = v;
+                    } else {
+                        const int y = y0 + 2 * wv + r, x = x0 + px;
+                        if (y < H && x < W) out[(((size_t)b * H + y) * W + x) * out_cstride + out_coff + n] = v;
+                    }
                 }
             }
         }
@@ -587,7 +647,23 @@ template <bool POOL, int LAYER, bool FUSE1A = false>
 int conv3(vs_ctx* ctx, const DevLayer& L, const float* in, int in_cstride, int in_coff, float* out, int out_cstride,
           int out_coff, int B, int H, int W, hipStream_t s, const DevLayer* L1a = nullptr) {
     (void)ctx;
-    if (!FUSE1A || !conv3_db_enabled())
+    if constexpr (!FUSE1A) {
+        // linear tiles when 8 x 32 tiles would waste columns and the patch fits
+        const int lin_rows = (W - 1 + 255) / W + 1 + 2;
+        if (!POOL && W % 32 != 0 && lin_rows * (W + 2) <= 640 && conv3_db_enabled() && L.cin % 8 == 0 &&
+            L.cout_pad % 64 == 0 && in_cstride % 4 == 0 && in_coff % 4 == 0) {
+            const int tiles = (H * W + 255) / 256;
+            dim3 grid((unsigned)(B * tiles), L.cout_pad / 64);
+            hipLaunchKernelGGL((k_conv3_db<false, LAYER, false, true>), grid, dim3(256), 0, s, in, in_cstride, in_coff,
+                               L.w, L.b, L.cin, L.cout, L.cout_pad, out, out_cstride, out_coff, B, H, W, tiles,
+                               lin_rows, 1, nullptr, nullptr);
+            VS_HIP(hipGetLastError());
+            return VS_OK;
+        }
+        return launch_conv<3, POOL, LAYER, FUSE1A, 16>(L, in, in_cstride, in_coff, out, out_cstride, out_coff, B, H,
+                                                       W, 1, s, L1a);
+    } else {
+    if (!conv3_db_enabled())
         return launch_conv<3, POOL, LAYER, FUSE1A, 16>(L, in, in_cstride, in_coff, out, out_cstride, out_coff, B, H,
                                                        W, 1, s, L1a);
     if (L.cin % 8 != 0 || L.cout_pad % 64 != 0 || (!FUSE1A && (in_cstride % 4 || in_coff % 4)) || (FUSE1A && !L1a) ||
@@ -602,11 +678,13 @@ int conv3(vs_ctx* ctx, const DevLayer& L, const float* in, int in_cstride, int i
                        L1a ? L1a->w : nullptr, L1a ? L1a->b : nullptr);
     VS_HIP(hipGetLastError());
     return VS_OK;
+    }
 }
 
 }  // namespace
 
-int sp_forward(vs_ctx* ctx, int B, const uint8_t* d_img, int channels, int h, int w, hipStream_t s) {
+int sp_forward(vs_ctx* ctx, int B, const uint8_t* d_img, int channels, int h, int w, hipStream_t s, float* semi_out,
+               float* dgrid_out) {
     const int Hp = ((h + 7) / 8) * 8, Wp = ((w + 7) / 8) * 8;
     const int hc = Hp / 8, wc = Wp / 8;
     const size_t full = (size_t)B * Hp * Wp;
@@ -614,8 +692,14 @@ int sp_forward(vs_ctx* ctx, int B, const uint8_t* d_img, int channels, int h, in
     // largest activations: the half-resolution 64-channel maps (conv1b+pool and conv2a outputs)
     VS_CHECK(ctx->act0.ensure(full / 4 * 64 * sizeof(float)));
     VS_CHECK(ctx->act1.ensure(full / 4 * 64 * sizeof(float)));
-    VS_CHECK(ctx->semi.ensure((size_t)B * hc * wc * kSemiCh * sizeof(float)));
-    VS_CHECK(ctx->dgrid.ensure((size_t)B * hc * wc * kDescDim * sizeof(float)));
+    if (!semi_out) {
+        VS_CHECK(ctx->semi.ensure((size_t)B * hc * wc * kSemiCh * sizeof(float)));
+        semi_out = ctx->semi.as<float>();
+    }
+    if (!dgrid_out) {
+        VS_CHECK(ctx->dgrid.ensure((size_t)B * hc * wc * kDescDim * sizeof(float)));
+        dgrid_out = ctx->dgrid.as<float>();
+    }
     float* gray = ctx->gray.as<float>();
     float* a0 = ctx->act0.as<float>();
     float* a1 = ctx->act1.as<float>();
@@ -665,13 +749,13 @@ int sp_forward(vs_ctx* ctx, int B, const uint8_t* d_img, int channels, int h, in
     }
     {
         ProfScope ps(ctx, "head_b", s);  // convPb 256 -> 65 and convDb 256 -> 256 (1x1)
-        VS_CHECK((launch_conv<1, false, 9>(L[9], a0, 512, 0, ctx->semi.as<float>(), kSemiCh, 0, B, H, W, 0, s)));
-        VS_CHECK((launch_conv<1, false, 11>(L[11], a0, 512, 256, ctx->dgrid.as<float>(), kDescDim, 0, B, H, W, 0, s)));
+        VS_CHECK((launch_conv<1, false, 9>(L[9], a0, 512, 0, semi_out, kSemiCh, 0, B, H, W, 0, s)));
+        VS_CHECK((launch_conv<1, false, 11>(L[11], a0, 512, 256, dgrid_out, kDescDim, 0, B, H, W, 0, s)));
     }
     {
         ProfScope ps(ctx, "desc_l2norm", s);
         long npix = (long)B * H * W;
-        hipLaunchKernelGGL(k_desc_l2norm, dim3((unsigned)((npix + 3) / 4)), dim3(256), 0, s, ctx->dgrid.as<float>(),
+        hipLaunchKernelGGL(k_desc_l2norm, dim3((unsigned)((npix + 3) / 4)), dim3(256), 0, s, dgrid_out,
                            npix);
         VS_HIP(hipGetLastError());
     }

@@ -349,7 +349,9 @@ __global__ __launch_bounds__(256) void k_sample(const float* __restrict__ dgrid,
 }
 
 int sp_postprocess(vs_ctx* ctx, int B, int hc, int wc, int h, int w, vs_keypoint* d_kps, float* d_desc,
-                   int* d_n, int cap, hipStream_t s) {
+                   int* d_n, int cap, hipStream_t s, const float* semi, const float* dgrid) {
+    if (!semi) semi = ctx->semi.as<float>();
+    if (!dgrid) dgrid = ctx->dgrid.as<float>();
     const int Hp = hc * 8, Wp = wc * 8;
     const size_t npx = (size_t)B * Hp * Wp;
     // Kept pixels are pairwise >= radius+1 apart (Chebyshev), so at most ceil(H/5)*ceil(W/5).
@@ -365,7 +367,7 @@ int sp_postprocess(vs_ctx* ctx, int B, int hc, int wc, int h, int w, vs_keypoint
     {
         ProfScope ps(ctx, "decode", s);
         int ncell = B * hc * wc;
-        hipLaunchKernelGGL(k_decode, dim3((ncell + 255) / 256), dim3(256), 0, s, ctx->semi.as<float>(), hc, wc, B,
+        hipLaunchKernelGGL(k_decode, dim3((ncell + 255) / 256), dim3(256), 0, s, semi, hc, wc, B,
                            ctx->heat.as<float>(), ctx->state.as<uint8_t>());
         VS_HIP(hipGetLastError());
     }
@@ -392,7 +394,7 @@ int sp_postprocess(vs_ctx* ctx, int B, int hc, int wc, int h, int w, vs_keypoint
     }
     {
         ProfScope ps(ctx, "sample", s);
-        hipLaunchKernelGGL(k_sample, dim3((max_kp + 3) / 4, B), dim3(256), 0, s, ctx->dgrid.as<float>(), hc, wc,
+        hipLaunchKernelGGL(k_sample, dim3((max_kp + 3) / 4, B), dim3(256), 0, s, dgrid, hc, wc,
                            d_kps, d_n, cap, d_desc);
         VS_HIP(hipGetLastError());
     }

@@ -301,6 +301,23 @@ int vs_extract_batch_dev(vs_ctx* ctx, int B, const uint8_t* d_imgs, int h, int w
     return VS_OK;
 }
 
+int vs_network_batch_dev(vs_ctx* ctx, int B, const uint8_t* d_imgs, int h, int w, float* d_semi, float* d_dgrid,
+                         void* stream) {
+    VS_ARG(ctx && d_imgs && d_semi && d_dgrid, "vs_network_batch_dev: null argument");
+    VS_ARG(B > 0 && h >= 8 && w >= 8, "vs_network_batch_dev: bad sizes");
+    VS_HIP(hipSetDevice(ctx->device));
+    return sp_forward(ctx, B, d_imgs, 3, h, w, pick(ctx, stream), d_semi, d_dgrid);
+}
+
+int vs_postprocess_batch_dev(vs_ctx* ctx, int B, const float* d_semi, const float* d_dgrid, int h, int w,
+                             vs_keypoint* d_kps, float* d_desc, int* d_n, int cap, void* stream) {
+    VS_ARG(ctx && d_semi && d_dgrid && d_kps && d_desc && d_n, "vs_postprocess_batch_dev: null argument");
+    VS_ARG(B > 0 && h >= 8 && w >= 8 && cap >= 1, "vs_postprocess_batch_dev: bad sizes");
+    VS_HIP(hipSetDevice(ctx->device));
+    const int hc = (h + 7) / 8, wc = (w + 7) / 8;
+    return sp_postprocess(ctx, B, hc, wc, h, w, d_kps, d_desc, d_n, cap, pick(ctx, stream), d_semi, d_dgrid);
+}
+
 int vs_extract_batch(vs_ctx* ctx, int B, const uint8_t* const* imgs, int h, int w, int channels, size_t stride,
                      vs_keypoint* kps, float* desc, int cap, int* n) {
     VS_ARG(ctx && imgs && kps && desc && n, "vs_extract_batch: null argument");

@@ -115,11 +115,13 @@ struct ProfScope {
 // Network: d_bgr is B x h x w x 3 u8 (or gray u8 when channels == 1, or nullptr when d_gray01
 // already holds B x h x w fp32 in [0,1]).  Produces ctx->semi [B][hc][wc][65] and ctx->dgrid
 // [B][hc][wc][256] (L2-normalised over channels).
+// semi_out / dgrid_out (optional) replace ctx->semi / ctx->dgrid as the output tensors.
 int sp_forward(vs_ctx* ctx, int B, const uint8_t* d_img, int channels, int h, int w,
-               hipStream_t s);
-// Post-processing: ctx->semi / ctx->dgrid -> keypoints, descriptors, counts.
+               hipStream_t s, float* semi_out = nullptr, float* dgrid_out = nullptr);
+// Post-processing: semi / dgrid (default ctx->semi / ctx->dgrid) -> keypoints, descriptors, counts.
 int sp_postprocess(vs_ctx* ctx, int B, int hc, int wc, int h, int w, vs_keypoint* d_kps,
-                   float* d_desc, int* d_n, int cap, hipStream_t s);
+                   float* d_desc, int* d_n, int cap, hipStream_t s, const float* semi = nullptr,
+                   const float* dgrid = nullptr);
 // Matching
 int match_pairs(vs_ctx* ctx, int P, const int* d_pairs, int F, const float* d_desc,
                 const int* d_n, int cap, float ratio, vs_match* d_raw, int* d_nraw,

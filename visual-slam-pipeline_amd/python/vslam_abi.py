@@ -23,6 +23,8 @@ VS_OK = 0
 ERRORS = {-1: "VS_ERR_ARG", -2: "VS_ERR_HIP", -3: "VS_ERR_NOMEM", -4: "VS_ERR_IO",
           -5: "VS_ERR_CAPACITY", -6: "VS_ERR_NOTCONV"}
 SP_MAX_KEYPOINTS = 400
+SEMI_CH = 65  # VS_SEMI_CH
+DESC_DIM = 256  # VS_DESC_DIM
 K_TUM = (525.0, 525.0, 319.5, 239.5)  # Config.h:14-17
 
 _P = ctypes.c_void_p
@@ -39,6 +41,8 @@ _SIG = {
     "vs_extract": (_I, [_P, _P, _I, _I, _I, ctypes.c_size_t, _P, _P, _I, _P]),
     "vs_extract_batch": (_I, [_P, _I, _P, _I, _I, _I, ctypes.c_size_t, _P, _P, _I, _P]),
     "vs_extract_batch_dev": (_I, [_P, _I, _P, _I, _I, _P, _P, _P, _I, _P]),
+    "vs_network_batch_dev": (_I, [_P, _I, _P, _I, _I, _P, _P, _P]),
+    "vs_postprocess_batch_dev": (_I, [_P, _I, _P, _P, _I, _I, _P, _P, _P, _I, _P]),
     "vs_superpoint_forward": (_I, [_P, _P, _I, _I, _P, _P]),
     "vs_postprocess": (_I, [_P, _P, _P, _I, _I, _I, _I, _P, _P, _I, _P]),
     "vs_match_ratio": (_I, [_P, _P, _I, _P, _I, ctypes.c_float, _P, _P, _P, _P]),
@@ -342,6 +346,12 @@ class Context:
     # ---- device-batched entry points (pointers are ints, e.g. torch tensor.data_ptr()) ----
     def extract_batch_dev(self, B, d_imgs, h, w, d_kps, d_desc, d_n, cap, stream=None):
         _check(self.lib.vs_extract_batch_dev(self.h, B, d_imgs, h, w, d_kps, d_desc, d_n, cap, stream))
+
+    def network_batch_dev(self, B, d_imgs, h, w, d_semi, d_dgrid, stream=None):
+        _check(self.lib.vs_network_batch_dev(self.h, B, d_imgs, h, w, d_semi, d_dgrid, stream))
+
+    def postprocess_batch_dev(self, B, d_semi, d_dgrid, h, w, d_kps, d_desc, d_n, cap, stream=None):
+        _check(self.lib.vs_postprocess_batch_dev(self.h, B, d_semi, d_dgrid, h, w, d_kps, d_desc, d_n, cap, stream))
 
     def match_pairs_dev(self, P, d_pairs, F, d_desc, d_n, cap, ratio, d_raw, d_nraw, d_good, d_ngood, stream=None):
         _check(self.lib.vs_match_pairs_dev(self.h, P, d_pairs, F, d_desc, d_n, cap, ratio, d_raw, d_nraw, d_good,

@@ -2,7 +2,8 @@
 
 Per step each rank takes B consecutive processed frames of a 640x480 RGB-D stream that already
 sit in HBM and runs, entirely through libvslam_hip.so:
-    FeatureExtractor::extract           (vs_extract_batch_dev: SuperPoint + decode + NMS + sample)
+    FeatureExtractor::extract           (vs_network_batch_dev: SuperPoint, then
+                                         vs_postprocess_batch_dev: decode + NMS + sample)
     Slam::match_features(prev, cur)     (vs_match_pairs_dev: exact 2-NN + ratio 0.75)
     F-matrix verification               (vs_fmat_verify_pairs_dev: findFundamentalMat(FM_RANSAC,
                                          3.0, 0.999), matches filtered in order, epipolar errors)
@@ -76,6 +77,9 @@ class _StepSet:
         z = lambda *shape, dt=torch.int32: torch.zeros(shape, dtype=dt, device=dev)
         self.kps, self.desc, self.n = z(F, cap * KP_BYTES, dt=torch.uint8), z(F, cap, 256, dt=torch.float32), z(F)
         self.depth = z(F, h, w, dt=torch.float32)
+        hc, wc = (h + 7) // 8, (w + 7) // 8
+        self.semi = z(B, hc, wc, va.SEMI_CH, dt=torch.float32)  # network outputs of the block
+        self.dgrid = z(B, hc, wc, va.DESC_DIM, dt=torch.float32)
         self.raw, self.good = z(P, cap * M_BYTES, dt=torch.uint8), z(P, cap * M_BYTES, dt=torch.uint8)
         self.nraw, self.ngood = z(P), z(P)
         self.fkept, self.nfkept = z(P, cap * M_BYTES, dt=torch.uint8), z(P)
@@ -93,12 +97,13 @@ class _StepSet:
 
 
 class DevicePipeline:
-    """Two-stream software pipeline over the step's frames.  submit() enqueues step k's extraction
-    on the network stream and its pair geometry (match, F verification, 3D-3D RANSAC, E fallback)
-    on the geometry stream behind an event, into buffer set k % 2; collect() waits for that step's
-    geometry and returns its per-pair motion.  The geometry of step k (a few dozen workgroups)
-    therefore runs on the CUs the network of step k+1 leaves idle instead of serialising after it.
-    Set k % 2 is rewritten only after step k-2's geometry finished (event wait, no host sync)."""
+    """Two-stream software pipeline over the step's frames.  submit() enqueues step k's SuperPoint
+    network on the network stream, and its post-processing (decode, NMS, descriptor sampling) and
+    pair geometry (match, F verification, 3D-3D RANSAC, E fallback) on the geometry stream behind an
+    event, into buffer set k % 2; collect() waits for that step's geometry and returns its per-pair
+    motion.  Everything after the network (small grids, serial RANSAC replays) therefore runs on the
+    CUs the network of step k+1 leaves idle instead of serialising after it.  Set k % 2 is
+    rewritten only after step k-2's geometry finished (event wait, no host sync)."""
 
     def __init__(self, ctx, B, h=480, w=640, cap=va.SP_MAX_KEYPOINTS, K=va.K_TUM, iters=200, thr=0.05,
                  ratio=0.75, rank=0, world=1, group=None):
@@ -130,23 +135,25 @@ class DevicePipeline:
         with torch.cuda.stream(self.s_net):
             self.s_net.wait_event(S.geo_done)  # step k-2's geometry has released this set
             s = self.s_net.cuda_stream
-            if self.world == 1:  # carry the previous step's last frame into slot 0
-                S.kps[0].copy_(prev.kps[B])
-                S.desc[0].copy_(prev.desc[B])
-                S.n[0].copy_(prev.n[B])
+            if self.world == 1:  # carry the previous step's last depth map into slot 0
                 S.depth[0].copy_(prev.depth[B])
             elif depth_prev is not None:
                 S.depth[0].copy_(depth_prev)
             S.depth[1:].copy_(depth)
-            ctx.extract_batch_dev(B, frames.data_ptr(), h, w, S.kps[1:].data_ptr(), S.desc[1:].data_ptr(),
-                                  S.n[1:].data_ptr(), cap, s)
-            if self.world > 1:
-                # all-gather the step's feature records; slot 0 <- frame rank*B - 1
-                self.xchg.exchange(S.kps, S.desc, S.n)
+            ctx.network_batch_dev(B, frames.data_ptr(), h, w, S.semi.data_ptr(), S.dgrid.data_ptr(), s)
             S.net_done.record(self.s_net)
         with torch.cuda.stream(self.s_geo):
             self.s_geo.wait_event(S.net_done)
             s = self.s_geo.cuda_stream
+            ctx.postprocess_batch_dev(B, S.semi.data_ptr(), S.dgrid.data_ptr(), h, w, S.kps[1:].data_ptr(),
+                                      S.desc[1:].data_ptr(), S.n[1:].data_ptr(), cap, s)
+            if self.world == 1:  # carry the previous step's last frame into slot 0
+                S.kps[0].copy_(prev.kps[B])
+                S.desc[0].copy_(prev.desc[B])
+                S.n[0].copy_(prev.n[B])
+            else:
+                # all-gather the step's feature records; slot 0 <- frame rank*B - 1
+                self.xchg.exchange(S.kps, S.desc, S.n)
             S.seeds.copy_((self._seed_base + (42 + frame_count0)).to(torch.int32))
             ctx.match_pairs_dev(B, self.pairs.data_ptr(), B + 1, S.desc.data_ptr(), S.n.data_ptr(), cap,
                                 self.ratio, S.raw.data_ptr(), S.nraw.data_ptr(), S.good.data_ptr(),
