@@ -49,6 +49,19 @@ __global__ void k_gray_norm(const uint8_t* __restrict__ img, int channels, int h
     out[idx] = v;
 }
 
+// XCD-aware work order.  Workgroups are dealt round-robin to the 8 XCDs (block b and b + 8 share
+// one, and each XCD has its own L2), so the flat block index is remapped so that every XCD walks a
+// contiguous range of work items w = tile * ntiles + output-channel tile: the ntiles workgroups of
+// one spatial tile run back to back on one XCD and read its input patch through one L2 instead of
+// ntiles times from the fabric.  Falls back to the plain order when the grid is not a multiple of 8.
+__device__ inline void xcd_work(int ntiles, int& tile, int& nt) {
+    const int nblk = gridDim.x;
+    int w = blockIdx.x;
+    if ((nblk & 7) == 0) w = (w & 7) * (nblk >> 3) + (w >> 3);
+    tile = w / ntiles;
+    nt = w - tile * ntiles;
+}
+
 // Generic conv (KS = 3: 3x3 pad 1 over 8x32 spatial tiles; KS = 1: 1x1 over linear 256-pixel
 // tiles) on v_mfma_f32_32x32x2_f32.  256 threads = 4 waves; wave wv owns tile rows 2wv, 2wv+1
 // (two 32-pixel M blocks) x 64 output channels (two N blocks): four 32x32 accumulators.
@@ -87,12 +100,14 @@ __global__ __launch_bounds__(256, (KS == 3 && CKV == 32) ? 1 : 2) void k_conv_mf
 
     const int tid = threadIdx.x;
     const int wv = tid >> 6, lane = tid & 63, li = lane & 31, lh = lane >> 5;
-    const int n0 = blockIdx.y * 64;
+    int tile, nt;
+    xcd_work(cout_pad >> 6, tile, nt);
+    const int n0 = nt * 64;
     int b = 0, y0 = 0, x0 = 0;
     long m0 = 0;  // KS == 1: first linear pixel of the tile
     const long M = (long)B * H * W;
     if constexpr (KS == 3) {
-        int t = blockIdx.x;
+        int t = tile;
         int tx = t % tiles_x;
         t /= tiles_x;
         int ty = t % tiles_y;
@@ -100,7 +115,7 @@ __global__ __launch_bounds__(256, (KS == 3 && CKV == 32) ? 1 : 2) void k_conv_mf
         y0 = ty * G::TH;
         x0 = tx * G::TW;
     } else {
-        m0 = (long)blockIdx.x * 256;
+        m0 = (long)tile * 256;
     }
 
     f32x16 acc[2][2];
@@ -342,16 +357,18 @@ __global__ __launch_bounds__(256, 2) void k_conv3_db(
 
     const int tid = threadIdx.x;
     const int wv = tid >> 6, lane = tid & 63, li = lane & 31, lh = lane >> 5;
-    const int n0 = blockIdx.y * 64;
+    int tile, nt;
+    xcd_work(cout_pad >> 6, tile, nt);
+    const int n0 = nt * 64;
     const int HW = H * W;
     int b, y0, x0, m0 = 0;
     if constexpr (LIN) {  // tiles_x = tiles per image, tiles_y = patch rows
-        b = blockIdx.x / tiles_x;
-        m0 = (blockIdx.x - b * tiles_x) * 256;
+        b = tile / tiles_x;
+        m0 = (tile - b * tiles_x) * 256;
         y0 = m0 / W;  // first image row of the tile
         x0 = 0;
     } else {
-        int t = blockIdx.x;
+        int t = tile;
         const int tx = t % tiles_x;
         t /= tiles_x;
         const int ty = t % tiles_y;
@@ -621,7 +638,7 @@ int launch_conv(const DevLayer& L, const float* in, int in_cstride, int in_coff,
         set_error("conv: pooled layer needs even H, W");
         return VS_ERR_ARG;
     }
-    dim3 grid((unsigned)nblk, L.cout_pad / 64);
+    dim3 grid((unsigned)(nblk * (L.cout_pad / 64)));
     hipLaunchKernelGGL((k_conv_mfma<KS, POOL, LAYER, FUSE1A, CKV>), grid, dim3(256), 0, s, in, in_cstride, in_coff, L.w,
                        L.b, L.cin, L.cout, L.cout_pad, out, out_cstride, out_coff, B, H, W, tiles_x, tiles_y, relu,
                        L1a ? L1a->w : nullptr, L1a ? L1a->b : nullptr);
@@ -653,7 +670,7 @@ int conv3(vs_ctx* ctx, const DevLayer& L, const float* in, int in_cstride, int i
         if (!POOL && W % 32 != 0 && lin_rows * (W + 2) <= 640 && conv3_db_enabled() && L.cin % 8 == 0 &&
             L.cout_pad % 64 == 0 && in_cstride % 4 == 0 && in_coff % 4 == 0) {
             const int tiles = (H * W + 255) / 256;
-            dim3 grid((unsigned)(B * tiles), L.cout_pad / 64);
+            dim3 grid((unsigned)(B * tiles * (L.cout_pad / 64)));
             hipLaunchKernelGGL((k_conv3_db<false, LAYER, false, true>), grid, dim3(256), 0, s, in, in_cstride, in_coff,
                                L.w, L.b, L.cin, L.cout, L.cout_pad, out, out_cstride, out_coff, B, H, W, tiles,
                                lin_rows, 1, nullptr, nullptr);
@@ -672,7 +689,7 @@ int conv3(vs_ctx* ctx, const DevLayer& L, const float* in, int in_cstride, int i
         return VS_ERR_ARG;
     }
     const int tiles_x = (W + 31) / 32, tiles_y = (H + 7) / 8;
-    dim3 grid((unsigned)(B * tiles_x * tiles_y), L.cout_pad / 64);
+    dim3 grid((unsigned)(B * tiles_x * tiles_y * (L.cout_pad / 64)));
     hipLaunchKernelGGL((k_conv3_db<POOL, LAYER, FUSE1A>), grid, dim3(256), 0, s, in, in_cstride, in_coff, L.w, L.b,
                        L.cin, L.cout, L.cout_pad, out, out_cstride, out_coff, B, H, W, tiles_x, tiles_y, 1,
                        L1a ? L1a->w : nullptr, L1a ? L1a->b : nullptr);
