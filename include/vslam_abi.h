@@ -269,6 +269,49 @@ int vs_local_ba(vs_ctx* ctx, int N, double* R_world, double* t_world, int M, dou
                 const double K[4], int max_iter, double* err_before, double* err_after,
                 int stats[3]);
 
+/* ---- F1: the tracking loop, Slam::process_frame (Slam.cpp:809-1135) ---------------------- */
+/* A vs_slam is the reference's Slam object for the per-frame path: map, keyframes, EKF, RTS
+ * smoother (host/tracker.hpp restates the control flow; every arithmetic stage runs on the GPU
+ * through the context it was created on).  Images are 640 x 480 (Config.h:10-11), K is the
+ * reference's (Config.h:14-17).  Loop closure is not run: it only feeds the pose graph that the
+ * reference never optimises (Slam.cpp:1748 has no caller), so it cannot change a pose. */
+typedef struct vs_slam vs_slam;
+#define VS_SLAM_NSTATS 24
+/* max_batch: frames per vs_slam_process_batch_dev call (the device frame pool holds two batches). */
+int  vs_slam_create(vs_ctx* ctx, int max_batch, int h, int w, vs_slam** out);
+void vs_slam_destroy(vs_slam* slam);
+/* Slam::set_initial_pose (Slam.cpp:35-38). */
+int vs_slam_set_initial_pose(vs_slam* slam, const double R[9], const double t[3]);
+/* Slam::set_accelerometer_data + compute_gravity_direction (Slam.cpp:1580-1616, called as in
+ * main.cpp:1053-1066, i.e. after the initial pose): samples n x {timestamp, ax, ay, az}. */
+int vs_slam_set_accelerometer(vs_slam* slam, const double* samples, int n);
+/* B consecutive processed frames already in HBM (d_bgr B x h x w x 3 u8, d_depth B x h x w fp32
+ * metres or NULL) plus the host copies of the depth maps (h_depth[b], read during the call;
+ * NULL when d_depth is NULL), timestamps and frame ids (the image index, Frame::id).  Extracts all
+ * B frames in one batched SuperPoint pass, then runs Slam::process_frame on each in order;
+ * processed[b] = its return value. */
+int vs_slam_process_batch_dev(vs_slam* slam, int B, const uint8_t* d_bgr, const float* d_depth,
+                              const float* const* h_depth, const double* timestamps, const int* ids,
+                              int* processed);
+/* One frame from host features (e.g. a FeatureExtractor SPCF cache hit, FeatureExtractor.cpp:54-61):
+ * n_kp keypoints + n_kp x 256 descriptors, depth h x w fp32 metres (NULL = none). */
+int vs_slam_process_features(vs_slam* slam, int n_kp, const vs_keypoint* kps, const float* desc,
+                             const float* depth, double timestamp, int id, int* processed);
+/* Slam::run_rts_smoother (Slam.cpp:1761-1810). */
+int vs_slam_finish(vs_slam* slam);
+/* Map frames in insertion order (Map::get_all_frames): *n = count; the first cap entries of ids,
+ * timestamps, R (cap x 9, camera -> world) and t (cap x 3) are written (each nullable). */
+int vs_slam_trajectory(vs_slam* slam, int cap, int* ids, double* timestamps, double* R, double* t,
+                       int* n);
+/* {processed, rejected (< 30 keypoints), via 3D-3D, via E-matrix, E failed, bridge keyframes,
+ *  PnP recoveries, recoveries failed, stationary, keyframes, PnP refinements, periodic PnP,
+ *  tracked map points (sum), triangulated points, depth points, culled points, chains recomputed,
+ *  map points, valid map points, frame_count_, keyframe_count_, last match count, 0, 0} */
+int vs_slam_stats(vs_slam* slam, int* out, int cap);
+/* Map points (Map::map_points): *n = count; the first cap positions (world, x 3) and validity
+ * bytes are written (each nullable). */
+int vs_slam_map(vs_slam* slam, int cap, double* pos, uint8_t* valid, int* n);
+
 /* ---- profiling ----------------------------------------------------------------------- */
 /* When enabled, every stage of the _dev pipelines brackets its launches with hipEvents on the
  * stream it runs on; vs_profile_read returns per-stage accumulated milliseconds and launch

@@ -50,6 +50,15 @@ _SIG = {
     "orc_recover_pose": (_I, [_P, _P, _P, _I, _P, _P, _P, _P]),
     "orc_estimate_motion": (_I, [_P, _P, _I, _P, _P, _P, _P, _P, _P]),
     "orc_estimate_scale": (ctypes.c_double, [_P, _P, _I, _P, _P, _P, _P, _I, _I, _P]),
+    "orc_slam_create": (_P, []),
+    "orc_slam_destroy": (None, [_P]),
+    "orc_slam_set_initial_pose": (None, [_P, _P, _P]),
+    "orc_slam_set_accelerometer": (None, [_P, _P, _I]),
+    "orc_slam_process": (_I, [_P, _I, _P, _P, _P, ctypes.c_double, _I]),
+    "orc_slam_finish": (None, [_P]),
+    "orc_slam_trajectory": (_I, [_P, _I, _P, _P, _P, _P]),
+    "orc_slam_stats": (None, [_P, _P]),
+    "orc_slam_map": (_I, [_P, _I, _P, _P]),
     "orc_mt19937": (None, [ctypes.c_uint32, _I, _P]),
     "orc_expf_array": (None, [_P, _I, _P]),
     "orc_expf_exhaustive_check": (ctypes.c_long, [ctypes.c_float, ctypes.c_float]),
@@ -398,3 +407,62 @@ def expf_exhaustive_check(lo, hi):
 def expf_restated_check(lo, hi, use_fma=1):
     """Number of floats x in [lo, hi] (hi <= 0) where the product's glibc_expf.h differs from libm."""
     return lib().orc_expf_restated_check(lo, hi, use_fma)
+
+
+class Slam:
+    """The tracking loop (Slam::process_frame, host/tracker.hpp) over the CPU restatements: the
+    checker for vslam_abi.Slam (same features in, same trajectory / map / counters out)."""
+
+    def __init__(self):
+        self.h = lib().orc_slam_create()
+
+    def close(self):
+        if self.h:
+            lib().orc_slam_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set_initial_pose(self, R, t):
+        R = np.ascontiguousarray(R, np.float64).reshape(9)
+        t = np.ascontiguousarray(t, np.float64).reshape(3)
+        lib().orc_slam_set_initial_pose(self.h, _p(R), _p(t))
+
+    def set_accelerometer(self, samples):
+        a = np.ascontiguousarray(samples, np.float64).reshape(-1, 4)
+        lib().orc_slam_set_accelerometer(self.h, _p(a), a.shape[0])
+
+    def process(self, kps, desc, depth, timestamp, frame_id):
+        k = np.ascontiguousarray(kps, KEYPOINT_DTYPE)
+        d = np.ascontiguousarray(desc, np.float32).reshape(-1, 256)
+        dep = None if depth is None else np.ascontiguousarray(depth, np.float32)
+        return bool(lib().orc_slam_process(self.h, len(k), _p(k), _p(d), None if dep is None else _p(dep),
+                                           float(timestamp), int(frame_id)))
+
+    def finish(self):
+        lib().orc_slam_finish(self.h)
+
+    def trajectory(self):
+        n = lib().orc_slam_trajectory(self.h, 0, None, None, None, None)
+        ids = np.zeros(max(n, 1), np.int32)
+        ts = np.zeros(max(n, 1))
+        R = np.zeros((max(n, 1), 9))
+        t = np.zeros((max(n, 1), 3))
+        lib().orc_slam_trajectory(self.h, n, _p(ids), _p(ts), _p(R), _p(t))
+        return ids[:n], ts[:n], R[:n].reshape(-1, 3, 3), t[:n]
+
+    def stats(self):
+        out = np.zeros(24, np.int32)
+        lib().orc_slam_stats(self.h, _p(out))
+        return out
+
+    def map_points(self):
+        n = lib().orc_slam_map(self.h, 0, None, None)
+        pos = np.zeros((max(n, 1), 3))
+        valid = np.zeros(max(n, 1), np.uint8)
+        lib().orc_slam_map(self.h, n, _p(pos), _p(valid))
+        return pos[:n], valid[:n]

@@ -1,0 +1,127 @@
+"""CPU known-answer tests of the tracking loop restatement (host/tracker.hpp, Slam::process_frame,
+reference src/Slam.cpp:809-1135) instantiated over the oracle (oracle/orc_slam.cpp).
+
+Features are synthetic landmarks: points on the rendered room's surfaces, each with a fixed random
+256-d descriptor, projected into every frame with the ground-truth pose (sub-pixel noise, descriptor
+noise, occlusion test against the rendered depth).  With correct correspondences the reference's
+pipeline (ratio matching, F verification, 3D-3D RANSAC, EKF, local-map PnP, keyframes, RTS) must
+recover the synthetic trajectory to within a centimetre, and its bookkeeping must be consistent."""
+import numpy as np
+import pytest
+
+import ate
+import synth
+
+N_FRAMES = 10
+K = synth.K_TUM
+
+
+def landmark_features(seq, n_land=4000, seed=11):
+    rng = np.random.default_rng(seed)
+    fx, fy, cx, cy = K
+    # landmarks: random pixels of the frames back-projected with their depth and GT pose
+    pts = []
+    per = n_land // len(seq)
+    for f in seq:
+        u = rng.uniform(0, 639, per)
+        v = rng.uniform(0, 479, per)
+        z = f["depth"][np.round(v).astype(int), np.round(u).astype(int)].astype(np.float64)
+        ok = (z > 0.3) & (z < 4.5)
+        pc = np.stack([(u - cx) * z / fx, (v - cy) * z / fy, z], 1)[ok]
+        pts.append(pc @ f["R_wc"].T + f["t_wc"])
+    P = np.concatenate(pts)
+    D = rng.standard_normal((len(P), 256)).astype(np.float32)
+    D /= np.linalg.norm(D, axis=1, keepdims=True)
+    feats = []
+    kp_dtype = np.dtype([("x", "<f4"), ("y", "<f4"), ("size", "<f4"), ("angle", "<f4"), ("response", "<f4"),
+                         ("octave", "<i4"), ("class_id", "<i4")])
+    for f in seq:
+        pc = (P - f["t_wc"]) @ f["R_wc"]
+        z = pc[:, 2]
+        with np.errstate(divide="ignore", invalid="ignore"):
+            u = fx * pc[:, 0] / z + cx
+            v = fy * pc[:, 1] / z + cy
+        vis = (z > 0.2) & (u >= 1) & (u < 638) & (v >= 1) & (v < 478)
+        idx = np.nonzero(vis)[0]
+        dz = f["depth"][np.round(v[idx]).astype(int), np.round(u[idx]).astype(int)]
+        idx = idx[np.abs(dz - z[idx]) < 0.03]  # not occluded
+        idx = idx[rng.permutation(len(idx))[:400]]
+        k = np.zeros(len(idx), kp_dtype)
+        k["x"] = u[idx] + rng.normal(0, 0.3, len(idx))
+        k["y"] = v[idx] + rng.normal(0, 0.3, len(idx))
+        k["size"], k["angle"], k["response"], k["class_id"] = 8.0, -1.0, 0.5, -1
+        d = D[idx] + rng.normal(0, 0.02, (len(idx), 256)).astype(np.float32)
+        d /= np.linalg.norm(d, axis=1, keepdims=True)
+        feats.append((k, d.astype(np.float32)))
+    return feats
+
+
+@pytest.fixture(scope="module")
+def scene():
+    seq = synth.sequence(N_FRAMES)
+    return seq, landmark_features(seq)
+
+
+def test_oracle_tracker_recovers_synthetic_trajectory(oracle, scene):
+    seq, feats = scene
+    S = oracle.Slam()
+    done = [S.process(k, d, f["depth"], f["timestamp"], 3 * i) for i, (f, (k, d)) in enumerate(zip(seq, feats))]
+    assert all(done)
+    S.finish()
+    ids, ts, R, t = S.trajectory()
+    assert list(ids) == [3 * i for i in range(N_FRAMES)]
+    gt = np.array([f["t_wc"] for f in seq])
+    a = ate.compute_ate(ts, t, [f["timestamp"] for f in seq], gt)
+    assert a["n"] == N_FRAMES and a["ate_rmse"] < 0.01, a
+    # poses are relative to the first camera (Slam starts at identity, main.cpp:1065); the EKF
+    # (Slam.cpp:986-1047) starts at zero velocity and lags the measurements, so the raw path is
+    # shorter than the truth by a few cm over these 0.9 s (the similarity alignment above absorbs it)
+    R0, t0 = seq[0]["R_wc"], seq[0]["t_wc"]
+    rel = np.array([R0.T @ (f["t_wc"] - t0) for f in seq])
+    assert np.abs(t - rel).max() < 0.1
+    assert np.abs(t - rel)[:, :2].max() < 0.01  # lateral / vertical error stays sub-centimetre
+    st = S.stats()
+    processed, keyframes, map_points, map_valid = st[0], st[9], st[17], st[18]
+    assert processed == N_FRAMES and keyframes >= 2
+    assert 0 < map_valid <= map_points
+    pos, valid = S.map_points()
+    assert len(pos) == map_points and valid.sum() == map_valid and np.isfinite(pos).all()
+
+
+def test_oracle_tracker_rejected_first_frame(oracle, scene):
+    # Slam.cpp:820-823 keeps a frame with < MIN_MATCHES keypoints as last_frame_, so the next frame
+    # skips the first-frame initialisation (:826), matches the rejected frame (too few matches),
+    # finds no bridge (:847) and fails PnP recovery on the empty map (:560, returns -1); the frame
+    # after it matches that one and is tracked from its default identity pose.
+    seq, feats = scene
+    S = oracle.Slam()
+    k, d = feats[0]
+    assert not S.process(k[:5], d[:5], seq[0]["depth"], seq[0]["timestamp"], 0)
+    assert not S.process(*feats[1], seq[1]["depth"], seq[1]["timestamp"], 3)
+    assert S.process(*feats[2], seq[2]["depth"], seq[2]["timestamp"], 6)
+    ids, ts, R, t = S.trajectory()
+    assert list(ids) == [6]
+    st = S.stats()
+    assert (st[0], st[1], st[7], st[9]) == (1, 1, 1, 1)  # processed, rejected, recovery failed, keyframes
+    assert st[14] == st[17] > 0  # map points all from depth (create_points_from_depth)
+
+
+def test_oracle_tracker_first_frame(oracle, scene):
+    seq, feats = scene
+    S = oracle.Slam()
+    assert S.process(*feats[0], seq[0]["depth"], seq[0]["timestamp"], 0)  # :826-835
+    ids, ts, R, t = S.trajectory()
+    assert list(ids) == [0] and np.array_equal(R[0], np.eye(3)) and np.array_equal(t[0], np.zeros(3))
+    st = S.stats()
+    assert (st[0], st[9], st[17]) == (1, 1, 0)  # keyframe without map points (no depth points yet)
+
+
+def test_oracle_tracker_initial_pose(oracle, scene):
+    seq, feats = scene
+    S = oracle.Slam()
+    S.set_initial_pose(seq[0]["R_wc"], seq[0]["t_wc"])
+    for i, (f, (k, d)) in enumerate(zip(seq[:5], feats[:5])):
+        assert S.process(k, d, f["depth"], f["timestamp"], 3 * i)
+    ids, ts, R, t = S.trajectory()
+    gt = np.array([f["t_wc"] for f in seq[:5]])
+    assert np.abs(t - gt).max() < 0.05  # world frame = the given initial pose (EKF lag along the path)

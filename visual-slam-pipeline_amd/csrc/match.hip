@@ -62,10 +62,11 @@ __global__ __launch_bounds__(256) void k_desc_norms(const float* __restrict__ de
 
 constexpr int kTrainChunk = 64;
 
-__global__ __launch_bounds__(256) void k_match(const int* __restrict__ pairs, const float* __restrict__ desc,
-                                               const float* __restrict__ norms, const int* __restrict__ n,
-                                               int cap, float ratio, vs_match* __restrict__ raw,
-                                               uint8_t* __restrict__ good_flag) {
+__global__ __launch_bounds__(256) void k_match(const int* __restrict__ pairs, const float* __restrict__ descq,
+                                               const float* __restrict__ desct, const float* __restrict__ normsq,
+                                               const float* __restrict__ normst, const int* __restrict__ n,
+                                               int qstride, int tstride, int cap, float ratio,
+                                               vs_match* __restrict__ raw, uint8_t* __restrict__ good_flag) {
     __shared__ float s_t[256 * kTrainChunk];  // [k][m]
     __shared__ float s_nb[kTrainChunk];
     const int p = blockIdx.x;
@@ -76,12 +77,12 @@ __global__ __launch_bounds__(256) void k_match(const int* __restrict__ pairs, co
     const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63, li = lane & 31, lh = lane >> 5;
     const int qj = q0 + wv * 32 + li;
     const bool qvalid = qj < n1;
-    const float* Q = desc + ((size_t)qf * cap + (qvalid ? qj : 0)) * 256;
+    const float* Q = descq + ((size_t)qf * qstride + (qvalid ? qj : 0)) * 256;
     float qreg[128];
 #pragma unroll
     for (int s = 0; s < 128; s++) qreg[s] = qvalid ? Q[2 * s + lh] : 0.0f;
-    const float na = qvalid ? norms[(size_t)qf * cap + qj] : 0.0f;
-    const float* T = desc + (size_t)tf * cap * 256;
+    const float na = qvalid ? normsq[(size_t)qf * qstride + qj] : 0.0f;
+    const float* T = desct + (size_t)tf * tstride * 256;
     Best2 best;
     best.init();
     for (int t0 = 0; t0 < n2; t0 += kTrainChunk) {
@@ -96,7 +97,7 @@ __global__ __launch_bounds__(256) void k_match(const int* __restrict__ pairs, co
             s_t[(4 * k4 + 2) * kTrainChunk + m] = v.z;
             s_t[(4 * k4 + 3) * kTrainChunk + m] = v.w;
         }
-        if (tid < kTrainChunk) s_nb[tid] = (t0 + tid < n2) ? norms[(size_t)tf * cap + t0 + tid] : 0.0f;
+        if (tid < kTrainChunk) s_nb[tid] = (t0 + tid < n2) ? normst[(size_t)tf * tstride + t0 + tid] : 0.0f;
         __syncthreads();
         f32x16 acc0, acc1;
 #pragma unroll
@@ -181,6 +182,35 @@ __global__ __launch_bounds__(1024) void k_match_compact(const int* __restrict__ 
     }
 }
 
+// Norms of only the frames the P pairs reference (a pair out of a large frame pool): row r of
+// the 2P*cap grid is row r % cap of frame pairs[r / cap]; a frame named twice is written twice
+// with the same value.
+__global__ __launch_bounds__(256) void k_desc_norms_sel(const float* __restrict__ desc, const int* __restrict__ n,
+                                                        const int* __restrict__ pairs, int P, int cap,
+                                                        float* __restrict__ norms) {
+    long r = (long)blockIdx.x * 256 + threadIdx.x;
+    if (r >= (long)2 * P * cap) return;
+    const int f = pairs[r / cap], i = (int)(r % cap);
+    if (i >= n[f]) return;
+    const float4* p = reinterpret_cast<const float4*>(desc + ((size_t)f * cap + i) * 256);
+    float s = 0.0f;
+    for (int k4 = 0; k4 < 64; k4++) {
+        float4 v = p[k4];
+        s = fmaf(v.x, v.x, s);
+        s = fmaf(v.y, v.y, s);
+        s = fmaf(v.z, v.z, s);
+        s = fmaf(v.w, v.w, s);
+    }
+    norms[(size_t)f * cap + i] = s;
+}
+
+__global__ void k_set_meta(int* meta, int n1, int n2) {
+    meta[0] = 0;  // pairs = {0, 1}
+    meta[1] = 1;
+    meta[2] = n1;  // n = {n1, n2}
+    meta[3] = n2;
+}
+
 int match_pairs(vs_ctx* ctx, int P, const int* d_pairs, int F, const float* d_desc, const int* d_n, int cap,
                 float ratio, vs_match* d_raw, int* d_nraw, vs_match* d_good, int* d_ngood, hipStream_t s) {
     if (P <= 0) return VS_OK;
@@ -188,13 +218,45 @@ int match_pairs(vs_ctx* ctx, int P, const int* d_pairs, int F, const float* d_de
     float* norms = ctx->norms.as<float>();
     uint8_t* gflag = reinterpret_cast<uint8_t*>(norms + (size_t)F * cap);
     ProfScope ps(ctx, "match", s);
-    long rows = (long)F * cap;
-    hipLaunchKernelGGL(k_desc_norms, dim3((unsigned)((rows + 255) / 256)), dim3(256), 0, s, d_desc, d_n, F, cap, norms);
+    if (2 * P < F) {  // a few pairs out of a frame pool: only the referenced frames' norms
+        long rows = (long)2 * P * cap;
+        hipLaunchKernelGGL(k_desc_norms_sel, dim3((unsigned)((rows + 255) / 256)), dim3(256), 0, s, d_desc, d_n,
+                           d_pairs, P, cap, norms);
+    } else {
+        long rows = (long)F * cap;
+        hipLaunchKernelGGL(k_desc_norms, dim3((unsigned)((rows + 255) / 256)), dim3(256), 0, s, d_desc, d_n, F, cap,
+                           norms);
+    }
     VS_HIP(hipMemsetAsync(gflag, 0, (size_t)P * cap, s));
-    hipLaunchKernelGGL(k_match, dim3(P, (cap + 127) / 128), dim3(256), 0, s, d_pairs, d_desc, norms, d_n, cap, ratio,
-                       d_raw, gflag);
+    hipLaunchKernelGGL(k_match, dim3(P, (cap + 127) / 128), dim3(256), 0, s, d_pairs, d_desc, d_desc, norms, norms,
+                       d_n, cap, cap, cap, ratio, d_raw, gflag);
     hipLaunchKernelGGL(k_match_compact, dim3(P), dim3(1024), 0, s, d_pairs, d_n, cap, d_raw, gflag, d_nraw, d_good,
                        d_ngood);
+    VS_HIP(hipGetLastError());
+    return VS_OK;
+}
+
+// One query set against one train set held in separate arrays (PnP recovery: a frame's
+// descriptors against every valid map point, Slam.cpp:560-575).  Outputs are indexed by query
+// row (d_raw / d_good have n1 entries); d_counts = {n_raw, n_good}.
+int match_sets(vs_ctx* ctx, const float* d_q, int n1, const float* d_t, int n2, float ratio, vs_match* d_raw,
+               vs_match* d_good, int* d_counts, hipStream_t s) {
+    if (n1 <= 0) return VS_OK;
+    VS_CHECK(ctx->norms_sets.ensure(((size_t)n1 + n2) * sizeof(float) + (size_t)n1 + 64));
+    float* nq = ctx->norms_sets.as<float>();
+    float* nt = nq + n1;
+    int* meta = reinterpret_cast<int*>(nt + n2);
+    uint8_t* gflag = reinterpret_cast<uint8_t*>(meta + 4);
+    ProfScope ps(ctx, "match_map", s);
+    hipLaunchKernelGGL(k_set_meta, dim3(1), dim3(1), 0, s, meta, n1, n2);
+    // norms: query rows as "frame 0" of stride n1, train rows as "frame 1" read with stride 0
+    hipLaunchKernelGGL(k_desc_norms, dim3((unsigned)((n1 + 255) / 256)), dim3(256), 0, s, d_q, meta + 2, 1, n1, nq);
+    hipLaunchKernelGGL(k_desc_norms, dim3((unsigned)((n2 + 255) / 256)), dim3(256), 0, s, d_t, meta + 3, 1, n2, nt);
+    VS_HIP(hipMemsetAsync(gflag, 0, (size_t)n1, s));
+    hipLaunchKernelGGL(k_match, dim3(1, (n1 + 127) / 128), dim3(256), 0, s, meta, d_q, d_t, nq, nt, meta + 2, n1, 0,
+                       n1, ratio, d_raw, gflag);
+    hipLaunchKernelGGL(k_match_compact, dim3(1), dim3(1024), 0, s, meta, meta + 2, n1, d_raw, gflag, d_counts, d_good,
+                       d_counts + 1);
     VS_HIP(hipGetLastError());
     return VS_OK;
 }

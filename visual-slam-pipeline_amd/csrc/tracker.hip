@@ -1,0 +1,736 @@
+// tracker.hip — the GPU back end of the host tracking loop (host/tracker.hpp, a restatement of
+// Slam::process_frame, reference src/Slam.cpp:809-1135) and its C ABI (vs_slam_*).
+//
+// Device residency.  Every frame's features and depth live in HBM in a slot of a frame pool
+// ([slot][400] keypoints, [slot][400][256] descriptors, [slot][h][w] depth): two batch regions of
+// B slots each (a batch's frames are extracted straight into one region) plus persistent slots
+// that the tracker's live frames (last frame, last keyframe, reference frame) move into when
+// their batch region is about to be reused.  The map's point positions, validity bytes and
+// 256-d descriptors are mirrored in HBM and appended in place (descriptor rows are gathered
+// device-side from the creating frame's slot), so the per-frame O(map) work never crosses PCIe.
+//
+// Per processed frame the host issues: one fused chain (match -> F verification -> 3D-3D
+// RANSAC -> E-matrix fallback, one D2H of a packed 13 KB result block), local-map tracking
+// (one D2H of the index / observation block), PnP refinement, and for keyframes the keyframe
+// match, the visibility sweep and the map appends.  Everything runs on the context's stream.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <memory>
+#include <new>
+#include <vector>
+
+#include "../host/tracker.hpp"
+#include "vs_internal.h"
+
+namespace vs {
+
+int match_sets(vs_ctx* ctx, const float* d_q, int n1, const float* d_t, int n2, float ratio, vs_match* d_raw,
+               vs_match* d_good, int* d_counts, hipStream_t s);
+
+static_assert(sizeof(vs_trk::Keypoint) == sizeof(vs_keypoint), "keypoint layouts differ");
+static_assert(sizeof(vs_trk::Match) == sizeof(vs_match), "match layouts differ");
+
+constexpr int kCap = VS_SP_MAX_KEYPOINTS;
+constexpr int kPersist = 8;
+
+// dst[i] = src row rows[i] (256 floats), one 64-lane wave per row, float4 per lane
+__global__ __launch_bounds__(256) void k_gather_rows(const float* __restrict__ src, const int* __restrict__ rows,
+                                                     int k, float* __restrict__ dst) {
+    const int r = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (r >= k) return;
+    reinterpret_cast<float4*>(dst + (size_t)r * 256)[lane] =
+        reinterpret_cast<const float4*>(src + (size_t)rows[r] * 256)[lane];
+}
+
+// Visibility sweep (Slam.cpp:1089-1108): for every valid map point, Optimizer::project_point
+// (Optimizer.cpp:26-48) with the camera->world pose; bit 0 = inside the image (increase_visible),
+// bit 1 = some keypoint within TRACK_VISIBILITY_RADIUS (increase_found).  Keypoints sit in LDS.
+__global__ __launch_bounds__(256) void k_visibility(const double* __restrict__ pos, const uint8_t* __restrict__ valid,
+                                                    int n_mp, const vs_keypoint* __restrict__ kps, int nkp,
+                                                    double r0, double r1, double r2, double r3, double r4, double r5,
+                                                    double r6, double r7, double r8, double t0, double t1, double t2,
+                                                    double fx, double fy, double cx, double cy, int img_w, int img_h,
+                                                    uint8_t* __restrict__ flags) {
+    __shared__ float s_x[kCap], s_y[kCap];
+    for (int i = threadIdx.x; i < nkp; i += blockDim.x) {
+        s_x[i] = kps[i].x;
+        s_y[i] = kps[i].y;
+    }
+    __syncthreads();
+    const int m = blockIdx.x * blockDim.x + threadIdx.x;
+    if (m >= n_mp) return;
+    uint8_t f = 0;
+    if (valid[m]) {
+        // R_cam = R^T, t_cam = -R_cam t, pc = R_cam Pw + t_cam
+        const double tc0 = -(r0 * t0 + r3 * t1 + r6 * t2), tc1 = -(r1 * t0 + r4 * t1 + r7 * t2),
+                     tc2 = -(r2 * t0 + r5 * t1 + r8 * t2);
+        const double X = pos[3 * m], Y = pos[3 * m + 1], Z = pos[3 * m + 2];
+        const double z = (r2 * X + r5 * Y + r8 * Z) + tc2;
+        double u = -1, v = -1;
+        if (!(z < 1e-6)) {
+            u = fx * ((r0 * X + r3 * Y + r6 * Z) + tc0) / z + cx;
+            v = fy * ((r1 * X + r4 * Y + r7 * Z) + tc1) / z + cy;
+        }
+        if (u >= 0 && u < img_w && v >= 0 && v < img_h) {
+            f = 1;
+            const double rr = vs_trk::cfg::TRACK_VISIBILITY_RADIUS * vs_trk::cfg::TRACK_VISIBILITY_RADIUS;
+            for (int k = 0; k < nkp; k++) {
+                const double dx = u - s_x[k], dy = v - s_y[k];
+                if (dx * dx + dy * dy < rr) {
+                    f = 3;
+                    break;
+                }
+            }
+        }
+    }
+    flags[m] = f;
+}
+
+// Pinned bump allocator for small host<->device transfers; reset after every synchronisation.
+struct Pinned {
+    char* base = nullptr;
+    size_t cap = 0, used = 0;
+    ~Pinned() {
+        if (base) (void)hipHostFree(base);
+    }
+    int reserve(size_t n) {
+        if (n <= cap) return VS_OK;
+        if (base) (void)hipHostFree(base);
+        base = nullptr;
+        cap = 0;
+        used = 0;
+        size_t c = std::max(n, (size_t)1 << 20);
+        if (hipHostMalloc(&base, c, hipHostMallocDefault) != hipSuccess) {
+            set_error("hipHostMalloc failed");
+            return VS_ERR_NOMEM;
+        }
+        cap = c;
+        return VS_OK;
+    }
+    char* take(size_t n) {
+        size_t o = (used + 15) & ~(size_t)15;
+        if (o + n > cap) return nullptr;
+        used = o + n;
+        return base + o;
+    }
+};
+
+// Chain result block layout (device and pinned host copy):
+//   ints[32]: 0-1 pair slots, 2 seed, 3 nraw, 4 ngood, 5 nkept, 6 ok3d, 7 okE, 8-15 F diag,
+//             16-19 3D-3D diag, 20-27 E diag
+//   doubles[36]: 0-8 F, 9-10 epipolar errors, 11-19 R3, 20-22 t3, 23-31 RE, 32-34 tE, 35 scale
+//   good[cap], kept[cap], then raw[cap] (never copied back)
+constexpr size_t kChainInts = 0, kChainDbl = 128, kChainGood = 128 + 36 * 8;
+constexpr size_t kChainKept = kChainGood + (size_t)kCap * sizeof(vs_match);
+constexpr size_t kChainRaw = kChainKept + (size_t)kCap * sizeof(vs_match);
+constexpr size_t kChainBytes = kChainRaw + (size_t)kCap * sizeof(vs_match);
+
+struct GpuOps {
+    vs_ctx* ctx = nullptr;
+    hipStream_t s = nullptr;
+    int B = 0, h = 0, w = 0, S = 0, batch_region = 0;
+    double K[4] = {vs_trk::cfg::FX, vs_trk::cfg::FY, vs_trk::cfg::CX, vs_trk::cfg::CY};
+    DevBuf pool_kps, pool_desc, pool_n, pool_depth, semi, dgrid;
+    DevBuf chain_buf, work, rows_buf, map_pos, map_desc, map_valid, map_tmp;
+    int map_cap = 0, map_n = 0;
+    bool valid_dirty = false;
+    Pinned pin;
+    std::vector<vs_trk::Frame*> owner;  // persistent slot owners (slots 2B .. 2B + kPersist)
+    int err = VS_OK;                     // first error inside an Ops call (the tracker has no error channel)
+
+    vs_keypoint* kps_of(int slot) const { return pool_kps.as<vs_keypoint>() + (size_t)slot * kCap; }
+    float* desc_of(int slot) const { return pool_desc.as<float>() + (size_t)slot * kCap * 256; }
+    float* depth_of(int slot) const { return pool_depth.as<float>() + (size_t)slot * h * w; }
+
+    int init(vs_ctx* c, int max_batch, int hh, int ww) {
+        ctx = c;
+        s = ctx->stream;
+        B = max_batch;
+        h = hh;
+        w = ww;
+        S = 2 * B + kPersist;
+        VS_CHECK(pool_kps.ensure((size_t)S * kCap * sizeof(vs_keypoint)));
+        VS_CHECK(pool_desc.ensure((size_t)S * kCap * 256 * sizeof(float)));
+        VS_CHECK(pool_n.ensure((size_t)S * sizeof(int)));
+        VS_CHECK(pool_depth.ensure((size_t)S * h * w * sizeof(float)));
+        VS_HIP(hipMemsetAsync(pool_n.p, 0, (size_t)S * sizeof(int), s));
+        const int hc = (h + 7) / 8, wc = (w + 7) / 8;
+        VS_CHECK(semi.ensure((size_t)B * hc * wc * VS_SEMI_CH * sizeof(float)));
+        VS_CHECK(dgrid.ensure((size_t)B * hc * wc * VS_DESC_DIM * sizeof(float)));
+        VS_CHECK(chain_buf.ensure(kChainBytes));
+        VS_CHECK(pin.reserve((size_t)4 << 20));
+        owner.assign(kPersist, nullptr);
+        VS_CHECK(grow_map(1 << 16));
+        return VS_OK;
+    }
+
+    int sync() {
+        VS_HIP(hipStreamSynchronize(s));
+        pin.used = 0;
+        return VS_OK;
+    }
+    // pinned staging space; synchronises (and grows) when the area is exhausted
+    char* take(size_t n) {
+        char* p = pin.take(n);
+        if (p) return p;
+        if (failed(sync()) || failed(pin.reserve(n + 64))) return nullptr;
+        return pin.take(n);
+    }
+    int d2h(void* dst, const void* src, size_t bytes) {
+        VS_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, s));
+        return VS_OK;
+    }
+    // H2D of a host array through the pinned staging area
+    int upload(void* dst, const void* src, size_t bytes) {
+        if (bytes == 0) return VS_OK;
+        char* p = pin.take(bytes);
+        if (!p) {
+            VS_CHECK(sync());
+            VS_CHECK(pin.reserve(bytes + 64));
+            p = pin.take(bytes);
+        }
+        std::memcpy(p, src, bytes);
+        VS_HIP(hipMemcpyAsync(dst, p, bytes, hipMemcpyHostToDevice, s));
+        return VS_OK;
+    }
+
+    int grow_map(int need) {
+        if (need <= map_cap) return VS_OK;
+        int cap = std::max(need, map_cap * 2);
+        DevBuf np, nd, nv;
+        VS_CHECK(np.ensure((size_t)cap * 3 * sizeof(double)));
+        VS_CHECK(nd.ensure((size_t)cap * 256 * sizeof(float)));
+        VS_CHECK(nv.ensure((size_t)cap));
+        if (map_n > 0) {
+            VS_HIP(hipMemcpyAsync(np.p, map_pos.p, (size_t)map_n * 3 * sizeof(double), hipMemcpyDeviceToDevice, s));
+            VS_HIP(hipMemcpyAsync(nd.p, map_desc.p, (size_t)map_n * 256 * sizeof(float), hipMemcpyDeviceToDevice, s));
+            VS_HIP(hipMemcpyAsync(nv.p, map_valid.p, (size_t)map_n, hipMemcpyDeviceToDevice, s));
+        }
+        VS_HIP(hipStreamSynchronize(s));
+        map_pos.release();
+        map_desc.release();
+        map_valid.release();
+        map_pos = np;
+        map_desc = nd;
+        map_valid = nv;
+        np.p = nd.p = nv.p = nullptr;  // ownership moved
+        map_cap = cap;
+        return VS_OK;
+    }
+
+    int sync_valid(const vs_trk::Map& m) {
+        if (!valid_dirty) return VS_OK;
+        VS_CHECK(upload(map_valid.p, m.valid.data(), m.valid.size()));
+        valid_dirty = false;
+        return VS_OK;
+    }
+
+    // ---- frame slots -----------------------------------------------------------------------
+    int persistent_slot(vs_trk::Frame* f) {
+        for (int i = 0; i < kPersist; i++)
+            if (!owner[i]) {
+                owner[i] = f;
+                return 2 * B + i;
+            }
+        set_error("vs_slam: out of persistent frame slots");
+        return -1;
+    }
+    void release_slot(vs_trk::Frame* f) {
+        if (f->slot >= 2 * B) owner[f->slot - 2 * B] = nullptr;
+        f->slot = -1;
+    }
+    int copy_slot(int from, int to) {
+        VS_HIP(hipMemcpyAsync(kps_of(to), kps_of(from), kCap * sizeof(vs_keypoint), hipMemcpyDeviceToDevice, s));
+        VS_HIP(hipMemcpyAsync(desc_of(to), desc_of(from), (size_t)kCap * 256 * sizeof(float), hipMemcpyDeviceToDevice, s));
+        VS_HIP(hipMemcpyAsync(pool_n.as<int>() + to, pool_n.as<int>() + from, sizeof(int), hipMemcpyDeviceToDevice, s));
+        VS_HIP(hipMemcpyAsync(depth_of(to), depth_of(from), (size_t)h * w * sizeof(float), hipMemcpyDeviceToDevice, s));
+        return VS_OK;
+    }
+    // Host features (SPCF cache / caller-extracted) into a persistent slot.
+    int upload_frame(vs_trk::Frame& f, const float* desc) {
+        const int slot = persistent_slot(&f);
+        if (slot < 0) return VS_ERR_CAPACITY;
+        f.slot = slot;
+        const int n = (int)f.kps.size();
+        VS_CHECK(upload(kps_of(slot), f.kps.data(), (size_t)n * sizeof(vs_keypoint)));
+        VS_CHECK(upload(desc_of(slot), desc, (size_t)n * 256 * sizeof(float)));
+        VS_CHECK(upload(pool_n.as<int>() + slot, &n, sizeof(int)));
+        if (f.depth)
+            VS_CHECK(upload(depth_of(slot), f.depth, (size_t)h * w * sizeof(float)));
+        else
+            VS_HIP(hipMemsetAsync(depth_of(slot), 0, (size_t)h * w * sizeof(float), s));
+        return VS_OK;
+    }
+    // B frames already in HBM -> network + post-processing straight into batch region slots,
+    // depth copied beside them; keypoints come back to the host (the tracker's bookkeeping).
+    int extract_batch(std::vector<vs_trk::FramePtr>& frames, const uint8_t* d_bgr, const float* d_depth) {
+        const int nb = (int)frames.size();
+        const int s0 = batch_region * B;
+        batch_region ^= 1;
+        VS_CHECK(sp_forward(ctx, nb, d_bgr, 3, h, w, s, semi.as<float>(), dgrid.as<float>()));
+        VS_CHECK(sp_postprocess(ctx, nb, (h + 7) / 8, (w + 7) / 8, h, w, kps_of(s0), desc_of(s0),
+                                pool_n.as<int>() + s0, kCap, s, semi.as<float>(), dgrid.as<float>()));
+        if (d_depth)
+            VS_HIP(hipMemcpyAsync(depth_of(s0), d_depth, (size_t)nb * h * w * sizeof(float), hipMemcpyDeviceToDevice, s));
+        else
+            VS_HIP(hipMemsetAsync(depth_of(s0), 0, (size_t)nb * h * w * sizeof(float), s));
+        char* hk = pin.take((size_t)nb * kCap * sizeof(vs_keypoint) + (size_t)nb * sizeof(int));
+        if (!hk) {
+            VS_CHECK(sync());
+            VS_CHECK(pin.reserve((size_t)nb * kCap * (sizeof(vs_keypoint) + 4) + 64));
+            hk = pin.take((size_t)nb * kCap * sizeof(vs_keypoint) + (size_t)nb * sizeof(int));
+        }
+        int* hn = reinterpret_cast<int*>(hk + (size_t)nb * kCap * sizeof(vs_keypoint));
+        VS_HIP(hipMemcpyAsync(hk, kps_of(s0), (size_t)nb * kCap * sizeof(vs_keypoint), hipMemcpyDeviceToHost, s));
+        VS_HIP(hipMemcpyAsync(hn, pool_n.as<int>() + s0, (size_t)nb * sizeof(int), hipMemcpyDeviceToHost, s));
+        VS_HIP(hipStreamSynchronize(s));
+        for (int b = 0; b < nb; b++) {
+            const int n = hn[b];
+            if (n < 0 || n > kCap) {
+                set_error("vs_slam: keypoint count out of range");
+                return VS_ERR_CAPACITY;
+            }
+            const auto* kp = reinterpret_cast<const vs_trk::Keypoint*>(hk + (size_t)b * kCap * sizeof(vs_keypoint));
+            frames[b]->kps.assign(kp, kp + n);
+            frames[b]->mp_idx.assign(n, -1);
+            frames[b]->slot = s0 + b;
+        }
+        pin.used = 0;
+        return VS_OK;
+    }
+
+    // ---- Ops interface (host/tracker.hpp) ----------------------------------------------------
+    // Errors cannot propagate through the tracker (the reference has no error channel there):
+    // the first one is latched in `err`, results are emptied, and the C ABI reports it.
+    bool failed(int rc) {
+        if (rc != VS_OK && err == VS_OK) err = rc;
+        return rc != VS_OK;
+    }
+
+    int enqueue_match(int qslot, int tslot, float ratio, int* meta) {
+        const int pr[2] = {qslot, tslot};
+        VS_CHECK(upload(meta, pr, sizeof(pr)));
+        char* c = chain_buf.as<char>();
+        return match_pairs(ctx, 1, meta, S, pool_desc.as<float>(), pool_n.as<int>(), kCap, ratio,
+                           reinterpret_cast<vs_match*>(c + kChainRaw), meta + 3, reinterpret_cast<vs_match*>(c + kChainGood),
+                           meta + 4, s);
+    }
+
+    vs_trk::ChainResult chain_impl(const vs_trk::Frame& ref, const vs_trk::Frame& cur, uint32_t seed) {
+        vs_trk::ChainResult R;
+        char* c = chain_buf.as<char>();
+        int* di = reinterpret_cast<int*>(c + kChainInts);
+        double* dd = reinterpret_cast<double*>(c + kChainDbl);
+        vs_match* good = reinterpret_cast<vs_match*>(c + kChainGood);
+        vs_match* kept = reinterpret_cast<vs_match*>(c + kChainKept);
+        if (failed(upload(di + 2, &seed, sizeof(seed)))) return R;
+        if (failed(enqueue_match(ref.slot, cur.slot, vs_trk::cfg::L2_RATIO_THRESHOLD, di))) return R;
+        if (failed(fmat_pairs(ctx, 1, di, pool_kps.as<vs_keypoint>(), kCap, good, di + 4, dd, kept, di + 5, dd + 9,
+                              di + 8, s)))
+            return R;
+        if (failed(ransac3d_pairs(ctx, 1, di, pool_kps.as<vs_keypoint>(), kCap, kept, di + 5, pool_depth.as<float>(), h,
+                                  w, K, reinterpret_cast<const uint32_t*>(di + 2), 200, 0.05, dd + 11, dd + 20, di + 6,
+                                  di + 16, s)))
+            return R;
+        if (failed(emat_pairs(ctx, 1, di, pool_kps.as<vs_keypoint>(), kCap, kept, di + 5, di + 6, pool_depth.as<float>(),
+                              h, w, K, dd + 23, dd + 32, dd + 35, di + 7, di + 20, s)))
+            return R;
+        char* hc = take(kChainRaw);
+        if (!hc || failed(d2h(hc, c, kChainRaw)))
+            return R;
+        if (failed(sync())) return R;
+        const int* hi = reinterpret_cast<const int*>(hc + kChainInts);
+        const double* hd = reinterpret_cast<const double*>(hc + kChainDbl);
+        const auto* hg = reinterpret_cast<const vs_trk::Match*>(hc + kChainGood);
+        const auto* hk = reinterpret_cast<const vs_trk::Match*>(hc + kChainKept);
+        R.n_raw = hi[3];
+        R.good.assign(hg, hg + hi[4]);
+        R.kept.assign(hk, hk + hi[5]);
+        R.f_ok = hi[12] != 0;  // F diag[4] = F ok
+        R.epi_before = hd[9];
+        R.epi_after = hd[10];
+        R.ok3d = hi[6] != 0;
+        std::memcpy(R.R3.data(), hd + 11, 9 * sizeof(double));
+        std::memcpy(R.t3.data(), hd + 20, 3 * sizeof(double));
+        R.okE = !R.ok3d && hi[7] != 0;
+        std::memcpy(R.RE.data(), hd + 23, 9 * sizeof(double));
+        std::memcpy(R.tE.data(), hd + 32, 3 * sizeof(double));
+        R.scale = hd[35];
+        return R;
+    }
+    vs_trk::ChainResult chain(const vs_trk::Frame& ref, const vs_trk::Frame& cur, uint32_t seed) {
+        return chain_impl(ref, cur, seed);
+    }
+
+    std::vector<vs_trk::Match> match(const vs_trk::Frame& a, const vs_trk::Frame& b, float ratio) {
+        std::vector<vs_trk::Match> out;
+        char* c = chain_buf.as<char>();
+        int* di = reinterpret_cast<int*>(c + kChainInts);
+        if (failed(enqueue_match(a.slot, b.slot, ratio, di))) return out;
+        char* hc = take(kChainKept);
+        if (!hc || failed(d2h(hc, c, kChainKept)))
+            return out;
+        if (failed(sync())) return out;
+        const int ng = reinterpret_cast<const int*>(hc)[4];
+        const auto* hg = reinterpret_cast<const vs_trk::Match*>(hc + kChainGood);
+        out.assign(hg, hg + ng);
+        return out;
+    }
+
+    bool find_fundamental(const std::vector<float>& p1, const std::vector<float>& p2, std::vector<uint8_t>& mask) {
+        const int n = (int)(p1.size() / 2);
+        mask.assign(std::max(n, 1), 0);
+        double F[9];
+        int ok = 0;
+        if (failed(vs_find_fundamental(ctx, p1.data(), p2.data(), n, 3.0, 0.999, 1000, F, mask.data(), &ok, nullptr,
+                                       nullptr)))
+            return false;
+        return ok != 0;
+    }
+
+    vs_trk::ChainResult motion_points(const vs_trk::Frame& ref, const vs_trk::Frame& cur, const std::vector<float>& p1,
+                                      const std::vector<float>& p2, uint32_t seed) {
+        vs_trk::ChainResult R;
+        const int n = (int)(p1.size() / 2);
+        if (!ref.depth || !cur.depth) {  // the RGB-D tracker path; monocular callers use vs_estimate_motion
+            failed(VS_ERR_ARG);
+            set_error("vs_slam: post-stationary motion needs both depth maps on the host");
+            return R;
+        }
+        int ok = 0;
+        if (failed(vs_ransac_3d3d(ctx, p1.data(), p2.data(), n, ref.depth, cur.depth, h, w, K, seed, 200, 0.05,
+                                  R.R3.data(), R.t3.data(), &ok, nullptr)))
+            return R;
+        R.ok3d = ok != 0;
+        if (!R.ok3d) {
+            int eok = 0;
+            if (failed(vs_estimate_motion(ctx, p1.data(), p2.data(), n, K, ref.depth, cur.depth, h, w, R.RE.data(),
+                                          R.tE.data(), &R.scale, &eok, nullptr)))
+                return R;
+            R.okE = eok != 0;
+        }
+        return R;
+    }
+
+    // Observations can outnumber keypoints (a later map point may take a keypoint over with a
+    // smaller distance, Slam.cpp:460-465, and each takeover adds an observation): start with room
+    // for 4 per keypoint and rerun with the exact count when that is exceeded.
+    int track_local_map(vs_trk::Map& m, vs_trk::Frame& f, std::vector<std::pair<int, int>>& obs) {
+        obs.clear();
+        const int nkp = (int)f.kps.size();
+        if (failed(sync_valid(m))) return 0;
+        int obs_cap = std::max(4 * nkp, 64);
+        for (int attempt = 0; attempt < 2; attempt++) {
+            const int words = 2 + nkp + 2 * obs_cap;
+            if (failed(work.ensure((size_t)words * sizeof(int)))) return 0;
+            int* d = work.as<int>();
+            int* d_kpmp = d + 2;
+            int* d_obs = d + 2 + nkp;
+            if (failed(upload(d_kpmp, f.mp_idx.data(), (size_t)nkp * sizeof(int)))) return 0;
+            if (failed(::vs_track_local_map_dev(ctx, map_pos.as<double>(), map_desc.as<float>(),
+                                                map_valid.as<uint8_t>(), m.size(), kps_of(f.slot), desc_of(f.slot), nkp,
+                                                f.R.data(), f.t.data(), K, vs_trk::cfg::IMAGE_WIDTH,
+                                                vs_trk::cfg::IMAGE_HEIGHT, d_kpmp, d_obs, d_obs + obs_cap, obs_cap, d,
+                                                s)))
+                return 0;
+            int* hb = reinterpret_cast<int*>(take((size_t)words * sizeof(int)));
+            if (!hb || failed(d2h(hb, d, (size_t)words * sizeof(int))) || failed(sync())) return 0;
+            const int n_obs = hb[1];
+            if (n_obs > obs_cap) {  // rerun from the same inputs with room for every observation
+                obs_cap = n_obs;
+                continue;
+            }
+            std::memcpy(f.mp_idx.data(), hb + 2, (size_t)nkp * sizeof(int));
+            for (int i = 0; i < n_obs; i++) obs.emplace_back(hb[2 + nkp + i], hb[2 + nkp + obs_cap + i]);
+            return hb[0];
+        }
+        failed(VS_ERR_CAPACITY);
+        return 0;
+    }
+
+    vs_trk::PnPResult solve_pnp(const std::vector<float>& obj, const std::vector<float>& img, int iters, int min_inliers) {
+        vs_trk::PnPResult r;
+        int success = 0;
+        if (failed(vs_solve_pnp(ctx, obj.data(), img.data(), (int)(obj.size() / 3), K, iters, min_inliers,
+                                r.R_world.data(), r.t_world.data(), &success, &r.inlier_count, nullptr, nullptr)))
+            return r;
+        r.success = success != 0;
+        return r;
+    }
+
+    std::vector<std::pair<int, int>> match_map(const vs_trk::Map& m, const vs_trk::Frame& f, const std::vector<int>& ids,
+                                               float ratio) {
+        std::vector<std::pair<int, int>> out;
+        const int n1 = (int)f.kps.size(), n2 = (int)ids.size();
+        if (n1 == 0 || n2 < 2) return out;
+        const size_t tbytes = (size_t)n2 * 256 * sizeof(float), ibytes = (size_t)n2 * sizeof(int);
+        const size_t obytes = (size_t)2 * n1 * sizeof(vs_match) + 2 * sizeof(int);
+        if (failed(map_tmp.ensure(tbytes + ibytes + obytes))) return out;
+        float* d_t = map_tmp.as<float>();
+        int* d_ids = reinterpret_cast<int*>(map_tmp.as<char>() + tbytes);
+        vs_match* d_raw = reinterpret_cast<vs_match*>(map_tmp.as<char>() + tbytes + ibytes);
+        vs_match* d_good = d_raw + n1;
+        int* d_cnt = reinterpret_cast<int*>(d_good + n1);
+        if (failed(upload(d_ids, ids.data(), ibytes))) return out;
+        hipLaunchKernelGGL(k_gather_rows, dim3((n2 + 3) / 4), dim3(256), 0, s, map_desc.as<float>(), d_ids, n2, d_t);
+        if (failed(match_sets(ctx, desc_of(f.slot), n1, d_t, n2, ratio, d_raw, d_good, d_cnt, s))) return out;
+        char* hb = take((size_t)n1 * sizeof(vs_match) + 2 * sizeof(int));
+        if (!hb) return out;
+        if (failed(d2h(hb, d_cnt, 2 * sizeof(int))))
+            return out;
+        if (failed(d2h(hb + 2 * sizeof(int), d_good, (size_t)n1 * sizeof(vs_match))))
+            return out;
+        if (failed(sync())) return out;
+        const int ng = reinterpret_cast<const int*>(hb)[1];
+        const auto* g = reinterpret_cast<const vs_match*>(hb + 2 * sizeof(int));
+        for (int i = 0; i < ng; i++) out.emplace_back(g[i].query_idx, g[i].train_idx);
+        return out;
+    }
+
+    void map_append(const vs_trk::Map& m, int first, const vs_trk::Frame& src, const std::vector<int>& rows) {
+        const int k = (int)rows.size();
+        if (failed(grow_map(first + k))) return;
+        if (failed(upload(map_pos.as<double>() + (size_t)3 * first, m.pos.data() + (size_t)3 * first,
+                          (size_t)3 * k * sizeof(double))))
+            return;
+        if (failed(rows_buf.ensure((size_t)k * sizeof(int)))) return;
+        int* d_rows = rows_buf.as<int>();
+        if (failed(upload(d_rows, rows.data(), (size_t)k * sizeof(int)))) return;
+        hipLaunchKernelGGL(k_gather_rows, dim3((k + 3) / 4), dim3(256), 0, s, desc_of(src.slot), d_rows, k,
+                           map_desc.as<float>() + (size_t)first * 256);
+        if (failed(hipMemsetAsync(map_valid.as<uint8_t>() + first, 1, (size_t)k, s) == hipSuccess ? VS_OK : VS_ERR_HIP))
+            return;
+        map_n = first + k;
+        failed(sync());  // rows_buf is rewritten by the next append
+    }
+
+    void map_valid_changed() { valid_dirty = true; }
+
+    void visibility(const vs_trk::Map& m, const vs_trk::Frame& f, const vs_trk::M3& R, const vs_trk::V3& t,
+                    std::vector<uint8_t>& flags) {
+        const int n = m.size();
+        flags.assign(n, 0);
+        if (n == 0) return;
+        if (failed(sync_valid(m)) || failed(map_tmp.ensure((size_t)n))) return;
+        uint8_t* d_flags = map_tmp.as<uint8_t>();
+        hipLaunchKernelGGL(k_visibility, dim3((n + 255) / 256), dim3(256), 0, s, map_pos.as<double>(),
+                           map_valid.as<uint8_t>(), n, kps_of(f.slot), (int)f.kps.size(), R[0], R[1], R[2], R[3], R[4],
+                           R[5], R[6], R[7], R[8], t[0], t[1], t[2], K[0], K[1], K[2], K[3], vs_trk::cfg::IMAGE_WIDTH,
+                           vs_trk::cfg::IMAGE_HEIGHT, d_flags);
+        char* hb = take((size_t)n);
+        if (!hb) return;
+        if (failed(d2h(hb, d_flags, (size_t)n)))
+            return;
+        if (failed(sync())) return;
+        std::memcpy(flags.data(), hb, (size_t)n);
+    }
+};
+
+}  // namespace vs
+
+struct vs_slam {
+    vs::GpuOps ops;
+    std::unique_ptr<vs_trk::Tracker<vs::GpuOps>> trk;
+    std::vector<vs_trk::FramePtr> batch;  // frames of the batch being processed
+};
+
+using namespace vs;
+
+namespace {
+
+// After a batch (or a single frame): live frames still sitting in a batch-region slot move to
+// persistent slots; dead frames drop their device slot and host working data (the map keeps only
+// their pose for the trajectory).
+int settle(vs_slam* sl) {
+    GpuOps& o = sl->ops;
+    auto& T = *sl->trk;
+    for (int i = 0; i < kPersist; i++) {
+        vs_trk::Frame* f = o.owner[i];
+        if (f && !T.is_live(f)) {
+            o.release_slot(f);
+            f->kps.clear();
+            f->kps.shrink_to_fit();
+            f->mp_idx.clear();
+            f->mp_idx.shrink_to_fit();
+            f->depth_store = std::vector<float>();
+            f->depth = nullptr;
+        }
+    }
+    for (auto& f : sl->batch) {
+        if (T.is_live(f.get())) {
+            if (f->slot >= 0 && f->slot < 2 * o.B) {
+                const int to = o.persistent_slot(f.get());
+                if (to < 0) return VS_ERR_CAPACITY;
+                VS_CHECK(o.copy_slot(f->slot, to));
+                f->slot = to;
+            }
+        } else if (f->slot >= 0 && f->slot < 2 * o.B) {
+            f->slot = -1;
+            f->kps.clear();
+            f->kps.shrink_to_fit();
+            f->mp_idx.clear();
+            f->mp_idx.shrink_to_fit();
+            f->depth = nullptr;
+        }
+    }
+    T.retain_live_frames();  // live frames keep a host copy of their depth beyond the caller's buffer
+    sl->batch.clear();
+    return o.sync();
+}
+
+}  // namespace
+
+extern "C" {
+
+int vs_slam_create(vs_ctx* ctx, int max_batch, int h, int w, vs_slam** out) {
+    VS_ARG(ctx && out, "vs_slam_create: null argument");
+    VS_ARG(max_batch >= 1 && max_batch <= 256, "vs_slam_create: max_batch must be in [1, 256]");
+    VS_ARG(h == vs_trk::cfg::IMAGE_HEIGHT && w == vs_trk::cfg::IMAGE_WIDTH,
+           "vs_slam_create: the reference tracker is fixed to 640x480 (Config.h:10-11)");
+    *out = nullptr;
+    VS_HIP(hipSetDevice(ctx->device));
+    vs_slam* sl = new (std::nothrow) vs_slam();
+    if (!sl) return VS_ERR_NOMEM;
+    int rc = sl->ops.init(ctx, max_batch, h, w);
+    if (rc != VS_OK) {
+        delete sl;
+        return rc;
+    }
+    sl->trk = std::make_unique<vs_trk::Tracker<GpuOps>>(sl->ops);
+    *out = sl;
+    return VS_OK;
+}
+
+void vs_slam_destroy(vs_slam* sl) {
+    if (!sl) return;
+    (void)hipStreamSynchronize(sl->ops.s);
+    GpuOps& o = sl->ops;
+    DevBuf* bufs[] = {&o.pool_kps, &o.pool_desc, &o.pool_n, &o.pool_depth, &o.semi,      &o.dgrid,
+                      &o.chain_buf,    &o.work, &o.rows_buf,      &o.map_pos, &o.map_desc,  &o.map_valid, &o.map_tmp};
+    for (DevBuf* b : bufs) b->release();
+    delete sl;
+}
+
+int vs_slam_set_initial_pose(vs_slam* sl, const double R[9], const double t[3]) {
+    VS_ARG(sl && R && t, "vs_slam_set_initial_pose: null argument");
+    vs_trk::M3 Rm;
+    vs_trk::V3 tv;
+    std::memcpy(Rm.data(), R, sizeof(Rm));
+    std::memcpy(tv.data(), t, sizeof(tv));
+    sl->trk->set_initial_pose(Rm, tv);
+    return VS_OK;
+}
+
+int vs_slam_set_accelerometer(vs_slam* sl, const double* samples, int n) {
+    VS_ARG(sl && n >= 0 && (n == 0 || samples), "vs_slam_set_accelerometer: bad arguments");
+    std::vector<vs_trk::AccelSample> a(n);
+    for (int i = 0; i < n; i++) a[i] = {samples[4 * i], samples[4 * i + 1], samples[4 * i + 2], samples[4 * i + 3]};
+    sl->trk->set_accelerometer_data(std::move(a));
+    sl->trk->compute_gravity_direction();
+    return VS_OK;
+}
+
+int vs_slam_process_batch_dev(vs_slam* sl, int B, const uint8_t* d_bgr, const float* d_depth,
+                              const float* const* h_depth, const double* timestamps, const int* ids, int* processed) {
+    VS_ARG(sl && d_bgr && timestamps && ids && processed, "vs_slam_process_batch_dev: null argument");
+    VS_ARG(B >= 1 && B <= sl->ops.B, "vs_slam_process_batch_dev: B out of range");
+    VS_ARG(!d_depth == !h_depth, "vs_slam_process_batch_dev: depth must be given on both sides or neither");
+    GpuOps& o = sl->ops;
+    VS_HIP(hipSetDevice(o.ctx->device));
+    sl->batch.clear();
+    for (int b = 0; b < B; b++) {
+        auto f = std::make_shared<vs_trk::Frame>();
+        f->id = ids[b];
+        f->timestamp = timestamps[b];
+        f->dh = o.h;
+        f->dw = o.w;
+        f->depth = h_depth ? h_depth[b] : nullptr;
+        sl->batch.push_back(f);
+    }
+    VS_CHECK(o.extract_batch(sl->batch, d_bgr, d_depth));
+    for (int b = 0; b < B; b++) {
+        processed[b] = sl->trk->process_frame(sl->batch[b]) ? 1 : 0;
+        if (o.err != VS_OK) {
+            int rc = o.err;
+            o.err = VS_OK;
+            return rc;
+        }
+    }
+    return settle(sl);
+}
+
+int vs_slam_process_features(vs_slam* sl, int n_kp, const vs_keypoint* kps, const float* desc, const float* depth,
+                             double timestamp, int id, int* processed) {
+    VS_ARG(sl && processed && n_kp >= 0 && n_kp <= kCap, "vs_slam_process_features: bad arguments");
+    VS_ARG(n_kp == 0 || (kps && desc), "vs_slam_process_features: null features");
+    GpuOps& o = sl->ops;
+    VS_HIP(hipSetDevice(o.ctx->device));
+    auto f = std::make_shared<vs_trk::Frame>();
+    f->id = id;
+    f->timestamp = timestamp;
+    f->dh = o.h;
+    f->dw = o.w;
+    f->depth = depth;
+    const auto* kp = reinterpret_cast<const vs_trk::Keypoint*>(kps);
+    f->kps.assign(kp, kp + n_kp);
+    f->mp_idx.assign(n_kp, -1);
+    VS_CHECK(o.upload_frame(*f, desc));
+    *processed = sl->trk->process_frame(f) ? 1 : 0;
+    if (o.err != VS_OK) {
+        int rc = o.err;
+        o.err = VS_OK;
+        return rc;
+    }
+    sl->batch.assign(1, f);
+    return settle(sl);
+}
+
+int vs_slam_finish(vs_slam* sl) {
+    VS_ARG(sl, "vs_slam_finish: null argument");
+    sl->trk->run_rts_smoother();
+    return VS_OK;
+}
+
+int vs_slam_trajectory(vs_slam* sl, int cap, int* ids, double* timestamps, double* R, double* t, int* n) {
+    VS_ARG(sl && n, "vs_slam_trajectory: null argument");
+    const auto& fr = sl->trk->map().frames;
+    *n = (int)fr.size();
+    for (int i = 0; i < (int)fr.size() && i < cap; i++) {
+        if (ids) ids[i] = fr[i]->id;
+        if (timestamps) timestamps[i] = fr[i]->timestamp;
+        if (R) std::memcpy(R + 9 * i, fr[i]->R.data(), 9 * sizeof(double));
+        if (t) std::memcpy(t + 3 * i, fr[i]->t.data(), 3 * sizeof(double));
+    }
+    return VS_OK;
+}
+
+int vs_slam_stats(vs_slam* sl, int* out, int cap) {
+    VS_ARG(sl && out, "vs_slam_stats: null argument");
+    const auto& S = sl->trk->stats();
+    const auto& m = sl->trk->map();
+    int valid = 0;
+    for (uint8_t v : m.valid) valid += v;
+    const int v[VS_SLAM_NSTATS] = {S.processed,      S.rejected,       S.via_3d3d,       S.via_emat,
+                                   S.emat_failed,    S.bridges,        S.recoveries,     S.recovery_failed,
+                                   S.stationary,     S.keyframes,      S.pnp_refined,    S.periodic_pnp,
+                                   S.tracked_total,  S.triangulated,   S.depth_points,   S.culled,
+                                   S.chains_discarded, m.size(),       valid,            sl->trk->frame_count(),
+                                   sl->trk->keyframe_count(), sl->trk->last_match_count(), 0, 0};
+    for (int i = 0; i < cap && i < VS_SLAM_NSTATS; i++) out[i] = v[i];
+    return VS_OK;
+}
+
+int vs_slam_map(vs_slam* sl, int cap, double* pos, uint8_t* valid, int* n) {
+    VS_ARG(sl && n, "vs_slam_map: null argument");
+    const auto& m = sl->trk->map();
+    *n = m.size();
+    for (int i = 0; i < m.size() && i < cap; i++) {
+        if (pos) std::memcpy(pos + 3 * i, &m.pos[3 * i], 3 * sizeof(double));
+        if (valid) valid[i] = m.valid[i];
+    }
+    return VS_OK;
+}
+
+}  // extern "C"

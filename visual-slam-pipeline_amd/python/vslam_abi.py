@@ -62,6 +62,16 @@ _SIG = {
     "vs_local_ba": (_I, [_P, _I, _P, _P, _I, _P, _I, _P, _P, _P, _P, _I, _P, _P, _P]),
     "vs_estimate_motion": (_I, [_P, _P, _P, _I, _P, _P, _P, _I, _I, _P, _P, _P, _P, _P]),
     "vs_emat_motion_pairs_dev": (_I, [_P, _I, _P, _P, _I, _P, _P, _P, _P, _I, _I, _P, _P, _P, _P, _P, _P, _P]),
+    "vs_slam_create": (_I, [_P, _I, _I, _I, ctypes.POINTER(_P)]),
+    "vs_slam_destroy": (None, [_P]),
+    "vs_slam_set_initial_pose": (_I, [_P, _P, _P]),
+    "vs_slam_set_accelerometer": (_I, [_P, _P, _I]),
+    "vs_slam_process_batch_dev": (_I, [_P, _I, _P, _P, _P, _P, _P, _P]),
+    "vs_slam_process_features": (_I, [_P, _I, _P, _P, _P, ctypes.c_double, _I, _P]),
+    "vs_slam_finish": (_I, [_P]),
+    "vs_slam_trajectory": (_I, [_P, _I, _P, _P, _P, _P, _P]),
+    "vs_slam_stats": (_I, [_P, _P, _I]),
+    "vs_slam_map": (_I, [_P, _I, _P, _P, _P]),
     "vs_profile_enable": (_I, [_P, _I]),
     "vs_profile_reset": (_I, [_P]),
     "vs_profile_read": (_I, [_P, _I, _P, _P, _P, _P]),
@@ -380,6 +390,97 @@ class Context:
         _check(self.lib.vs_profile_read(self.h, m, ctypes.cast(names, ctypes.c_void_p), _ptr(ms), _ptr(launches),
                                         ctypes.byref(n)))
         return {names[i].decode(): (float(ms[i]), int(launches[i])) for i in range(m)}
+
+
+SLAM_STATS = ["processed", "rejected", "via_3d3d", "via_emat", "emat_failed", "bridges", "recoveries",
+              "recovery_failed", "stationary", "keyframes", "pnp_refined", "periodic_pnp", "tracked_total",
+              "triangulated", "depth_points", "culled", "chains_recomputed", "map_points", "map_valid",
+              "frame_count", "keyframe_count", "last_match_count"]
+
+
+class Slam:
+    """vs_slam: the reference's tracking loop (Slam::process_frame, Slam.cpp:809-1135) with every
+    arithmetic stage on the GPU of `ctx` (host/tracker.hpp + csrc/tracker.hip)."""
+
+    def __init__(self, ctx, max_batch=32, h=480, w=640):
+        self.ctx = ctx
+        self.lib = ctx.lib
+        hh = ctypes.c_void_p()
+        _check(self.lib.vs_slam_create(ctx.h, max_batch, h, w, ctypes.byref(hh)))
+        self.h = hh
+        self.max_batch = max_batch
+
+    def close(self):
+        if self.h:
+            self.lib.vs_slam_destroy(self.h)
+            self.h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def set_initial_pose(self, R, t):
+        R = np.ascontiguousarray(R, np.float64).reshape(9)
+        t = np.ascontiguousarray(t, np.float64).reshape(3)
+        _check(self.lib.vs_slam_set_initial_pose(self.h, _ptr(R), _ptr(t)))
+
+    def set_accelerometer(self, samples):
+        a = np.ascontiguousarray(samples, np.float64).reshape(-1, 4)
+        _check(self.lib.vs_slam_set_accelerometer(self.h, _ptr(a), a.shape[0]))
+
+    def process_batch_dev(self, B, d_bgr, d_depth, h_depths, timestamps, ids):
+        """d_bgr / d_depth: device pointers (ints); h_depths: list of B host fp32 depth arrays."""
+        hd = [np.ascontiguousarray(d, np.float32) for d in h_depths]
+        ptrs = (ctypes.c_void_p * B)(*[d.ctypes.data for d in hd])
+        ts = np.ascontiguousarray(timestamps, np.float64)
+        fid = np.ascontiguousarray(ids, np.int32)
+        out = np.zeros(B, np.int32)
+        _check(self.lib.vs_slam_process_batch_dev(self.h, B, d_bgr, d_depth, ctypes.cast(ptrs, ctypes.c_void_p),
+                                                  _ptr(ts), _ptr(fid), _ptr(out)))
+        return out.astype(bool)
+
+    def process_features(self, kps, desc, depth, timestamp, frame_id):
+        k = np.ascontiguousarray(kps, KEYPOINT_DTYPE)
+        d = np.ascontiguousarray(desc, np.float32).reshape(-1, 256)
+        dep = None if depth is None else np.ascontiguousarray(depth, np.float32)
+        out = ctypes.c_int(0)
+        _check(self.lib.vs_slam_process_features(self.h, len(k), _ptr(k), _ptr(d), None if dep is None else _ptr(dep),
+                                                 float(timestamp), int(frame_id), ctypes.byref(out)))
+        return bool(out.value)
+
+    def finish(self):
+        _check(self.lib.vs_slam_finish(self.h))
+
+    def trajectory(self):
+        n = ctypes.c_int(0)
+        _check(self.lib.vs_slam_trajectory(self.h, 0, None, None, None, None, ctypes.byref(n)))
+        m = n.value
+        ids = np.zeros(max(m, 1), np.int32)
+        ts = np.zeros(max(m, 1))
+        R = np.zeros((max(m, 1), 9))
+        t = np.zeros((max(m, 1), 3))
+        _check(self.lib.vs_slam_trajectory(self.h, m, _ptr(ids), _ptr(ts), _ptr(R), _ptr(t), ctypes.byref(n)))
+        return ids[:m], ts[:m], R[:m].reshape(-1, 3, 3), t[:m]
+
+    def stats(self):
+        out = np.zeros(24, np.int32)
+        _check(self.lib.vs_slam_stats(self.h, _ptr(out), 24))
+        return out
+
+    def stats_dict(self):
+        s = self.stats()
+        return {k: int(s[i]) for i, k in enumerate(SLAM_STATS)}
+
+    def map_points(self):
+        n = ctypes.c_int(0)
+        _check(self.lib.vs_slam_map(self.h, 0, None, None, ctypes.byref(n)))
+        m = n.value
+        pos = np.zeros((max(m, 1), 3))
+        valid = np.zeros(max(m, 1), np.uint8)
+        _check(self.lib.vs_slam_map(self.h, m, _ptr(pos), _ptr(valid), ctypes.byref(n)))
+        return pos[:m], valid[:m]
 
 
 def exported_symbols_from_header(header_path):
