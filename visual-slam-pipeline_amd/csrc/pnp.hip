@@ -26,12 +26,19 @@ using namespace vs_pnp;
 constexpr int kPnpMaxIters = VS_PNP_MAX_ITERS;
 
 struct PnpShared {
-    int subset[kPnpMaxIters * 5];
-    int count[kPnpMaxIters];  // -1: EPnP failed on the subset
     double red[4 * kLmTerms];
     LmState lm;
     double rv[3], tv[3];
     int best, best_iter, niters_run, go;
+};
+
+// Per-problem hypothesis table in global memory: subsets [iters][5], counts [iters] (-1 = EPnP
+// failed), models [iters][6] = (rvec, tvec).
+struct PnpHyp {
+    int* subset;
+    int* count;
+    double* model;
+    int stride;  // hypotheses per problem
 };
 
 __device__ inline bool epnp_subset(const float* obj, const float* img, const int* idx, int m, const Cam& K, double* rv,
@@ -52,12 +59,198 @@ __device__ inline bool epnp_subset(const float* obj, const float* img, const int
     return true;
 }
 
+__device__ inline bool pnp_problem_runs(int n, int min_inliers, int model_points) {
+    return !(n < min_inliers || n < 4) && n != model_points;
+}
+
+// 1. subsets of the initial budget from the cv::RNG stream (getSubset: repeats rejected); the
+//    stream does not depend on the models because checkSubset is trivially true for PnP.
+__global__ void k_pnp_subsets(const int* __restrict__ off, int niters0, int min_inliers, PnpHyp H) {
+    const int pb = blockIdx.x * blockDim.x + threadIdx.x;
+    if (pb >= (int)gridDim.x * (int)blockDim.x) return;
+    const int n = off[pb + 1] - off[pb];
+    const int model_points = n == 4 ? 4 : 5;
+    if (!pnp_problem_runs(n, min_inliers, model_points)) return;
+    CvRng rng((uint64_t)-1);
+    for (int it = 0; it < niters0; it++) {
+        int* idx = H.subset + ((size_t)pb * H.stride + it) * 5;
+        for (int i = 0; i < model_points; i++)
+            for (;;) {
+                idx[i] = rng.uniform(0, n);
+                int j = 0;
+                while (j < i && idx[j] != idx[i]) j++;
+                if (j == i) break;
+            }
+    }
+}
+
+// 2. one hypothesis per wave64 workgroup: EPnP on its subset with the 12 x 12 eigen-decomposition
+//    spread over the wave (LDS-resident, the same rotations and per-element arithmetic as the
+//    sequential sym_eig<12>, so the model is bit-identical to the host's), the three beta
+//    approximations on lanes 0-2, then the inlier count over all points by the whole wave.
+__global__ __launch_bounds__(64) void k_pnp_hyp(const float* __restrict__ obj_all, const float* __restrict__ img_all,
+                                                const int* __restrict__ off, double fx, double fy, double cx, double cy,
+                                                int niters0, float thr2, int min_inliers, PnpHyp H) {
+    __shared__ double sA[144], sV[144];
+    __shared__ double sX[15], sUV[10], sAl[5][4], sCw[4][3];
+    __shared__ double sTot, sOff, sErr[3], sRt[3][12];
+    __shared__ int sOk;
+    const int pb = blockIdx.x, h = blockIdx.y, lane = threadIdx.x;
+    const int o0 = off[pb], n = off[pb + 1] - o0;
+    const int model_points = n == 4 ? 4 : 5;
+    if (h >= niters0 || !pnp_problem_runs(n, min_inliers, model_points)) return;
+    const float* obj = obj_all + 3 * (size_t)o0;
+    const float* img = img_all + 2 * (size_t)o0;
+    const Cam K{fx, fy, cx, cy};
+    const int* idx = H.subset + ((size_t)pb * H.stride + h) * 5;
+    const int m = model_points;
+    if (lane < m) {
+        const int i = idx[lane];
+        sX[3 * lane] = obj[3 * i];
+        sX[3 * lane + 1] = obj[3 * i + 1];
+        sX[3 * lane + 2] = obj[3 * i + 2];
+        sUV[2 * lane] = img[2 * i];
+        sUV[2 * lane + 1] = img[2 * i + 1];
+    }
+    __syncthreads();
+    if (lane == 0) {
+        double cw[4][3], al[5][4];
+        sOk = epnp_control(sX, m, cw, al);
+        for (int i = 0; i < 4; i++)
+            for (int c = 0; c < 3; c++) sCw[i][c] = cw[i][c];
+        for (int i = 0; i < m; i++)
+            for (int j = 0; j < 4; j++) sAl[i][j] = al[i][j];
+    }
+    __syncthreads();
+    bool ok = sOk != 0;
+    if (ok) {
+        for (int e = lane; e < 144; e += 64) {
+            sA[e] = epnp_mtm(sAl, sUV, m, K, e / 12, e % 12);
+            sV[e] = (e / 12 == e % 12) ? 1.0 : 0.0;
+        }
+        __syncthreads();
+        // sym_eig<12> (pnp_solvers.h), wave-parallel over the 12 rows / columns of each rotation
+        if (lane == 0) {
+            double total = 0;
+            for (int i = 0; i < 144; i++) total += sA[i] * sA[i];
+            sTot = total;
+        }
+        __syncthreads();
+        const double total = sTot;
+        for (int sweep = 0; sweep < 30; sweep++) {
+            if (lane == 0) {
+                double o = 0;
+                for (int p = 0; p < 12; p++)
+                    for (int q = p + 1; q < 12; q++) o += sA[p * 12 + q] * sA[p * 12 + q];
+                sOff = o;
+            }
+            __syncthreads();
+            if (!(sOff > 1e-32 * total)) break;
+            for (int p = 0; p < 11; p++)
+                for (int q = p + 1; q < 12; q++) {
+                    const double apq = sA[p * 12 + q];
+                    if (fabs(apq) < 1e-300) continue;
+                    const double app = sA[p * 12 + p], aqq = sA[q * 12 + q];
+                    const double theta = (aqq - app) / (2.0 * apq);
+                    const double t = (theta >= 0 ? 1.0 : -1.0) / (fabs(theta) + sqrt(theta * theta + 1.0));
+                    const double c = 1.0 / sqrt(t * t + 1.0), s = t * c;
+                    __syncthreads();
+                    if (lane < 12) {
+                        const int k = lane;
+                        const double akp = sA[k * 12 + p], akq = sA[k * 12 + q];
+                        sA[k * 12 + p] = c * akp - s * akq;
+                        sA[k * 12 + q] = s * akp + c * akq;
+                    }
+                    __syncthreads();
+                    if (lane < 12) {
+                        const int k = lane;
+                        const double apk = sA[p * 12 + k], aqk = sA[q * 12 + k];
+                        sA[p * 12 + k] = c * apk - s * aqk;
+                        sA[q * 12 + k] = s * apk + c * aqk;
+                    } else if (lane >= 32 && lane < 44) {
+                        const int k = lane - 32;
+                        const double vkp = sV[k * 12 + p], vkq = sV[k * 12 + q];
+                        sV[k * 12 + p] = c * vkp - s * vkq;
+                        sV[k * 12 + q] = s * vkp + c * vkq;
+                    }
+                    __syncthreads();
+                }
+        }
+        if (lane == 0) {  // eigenvalues in descending order, columns of V swapped along (selection sort)
+            double w[12];
+            for (int i = 0; i < 12; i++) w[i] = sA[i * 12 + i];
+            for (int i = 0; i < 11; i++) {
+                int mx = i;
+                for (int j = i + 1; j < 12; j++)
+                    if (w[j] > w[mx]) mx = j;
+                if (mx != i) {
+                    const double tw = w[i];
+                    w[i] = w[mx];
+                    w[mx] = tw;
+                    for (int k = 0; k < 12; k++) {
+                        const double tv = sV[k * 12 + i];
+                        sV[k * 12 + i] = sV[k * 12 + mx];
+                        sV[k * 12 + mx] = tv;
+                    }
+                }
+            }
+        }
+        __syncthreads();
+        if (lane < 3) {  // one beta approximation per lane
+            double cw[4][3], v[4][12], L[6][10], rho[6], al[5][4], X[15], uv[10];
+            for (int i = 0; i < 4; i++)
+                for (int c = 0; c < 3; c++) cw[i][c] = sCw[i][c];
+            for (int i = 0; i < m; i++)
+                for (int j = 0; j < 4; j++) al[i][j] = sAl[i][j];
+            for (int i = 0; i < 3 * m; i++) X[i] = sX[i];
+            for (int i = 0; i < 2 * m; i++) uv[i] = sUV[i];
+            epnp_L_rho(sV, cw, v, L, rho);
+            double R[9], t[3];
+            sErr[lane] = epnp_variant(lane, L, rho, v, al, X, uv, m, K, R, t);
+            for (int k = 0; k < 9; k++) sRt[lane][k] = R[k];
+            for (int k = 0; k < 3; k++) sRt[lane][9 + k] = t[k];
+        }
+        __syncthreads();
+    }
+    // model = the first lowest-error approximation (epnp()), as (rvec, tvec)
+    double rv[3] = {0, 0, 0}, tv[3] = {0, 0, 0};
+    if (ok) {
+        int best = 0;
+        for (int v = 1; v < 3; v++)
+            if (sErr[v] < sErr[best]) best = v;
+        rod_m2v(sRt[best], rv);
+        for (int k = 0; k < 3; k++) tv[k] = sRt[best][9 + k];
+    }
+    int cnt = -1;
+    if (ok) {
+        double R[9];
+        rod_v2m(rv, R);
+        int c = 0;
+        for (int i = lane; i < n; i += 64)
+            c += reproj_err2(R, tv, K, obj[3 * i], obj[3 * i + 1], obj[3 * i + 2], img[2 * i], img[2 * i + 1]) <= thr2;
+        for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o);
+        cnt = c;
+    }
+    if (lane == 0) {
+        H.count[(size_t)pb * H.stride + h] = cnt;
+        double* mo = H.model + ((size_t)pb * H.stride + h) * 6;
+        for (int k = 0; k < 3; k++) {
+            mo[k] = rv[k];
+            mo[3 + k] = tv[k];
+        }
+    }
+}
+
+// 3-4. per problem: the sequential accept / RANSACUpdateNumIters replay over the counts (exactly
+// the hypotheses the OpenCV loop evaluates, in its order), the winner's inlier mask, and the LM
+// refinement with the 28 normal-equation sums reduced deterministically over the lanes.
 // stat[p][8] = {success, inliers, ransac iterations, best iteration, lm iterations, lm accepted, n, 0}
 __global__ __launch_bounds__(256) void k_pnp_ransac(const float* __restrict__ obj_all, const float* __restrict__ img_all,
                                                     const int* __restrict__ off, double fx, double fy, double cx,
                                                     double cy, int max_iters, float thr2, double conf,
-                                                    int min_inliers, double* __restrict__ Rw, double* __restrict__ tw,
-                                                    int* __restrict__ stat, uint8_t* __restrict__ mask_all) {
+                                                    int min_inliers, PnpHyp H, double* __restrict__ Rw,
+                                                    double* __restrict__ tw, int* __restrict__ stat,
+                                                    uint8_t* __restrict__ mask_all) {
     __shared__ PnpShared S;
     const int pb = blockIdx.x, tid = threadIdx.x;
     const int o0 = off[pb], n = off[pb + 1] - o0;
@@ -93,41 +286,11 @@ __global__ __launch_bounds__(256) void k_pnp_ransac(const float* __restrict__ ob
             S.lm.iters = S.lm.accepted = 0;
         }
     } else {
-        // 1. subsets (cv::RNG, getSubset)
-        if (tid == 0) {
-            CvRng rng((uint64_t)-1);
-            for (int it = 0; it < niters0; it++) {
-                int* idx = S.subset + 5 * it;
-                for (int i = 0; i < model_points; i++)
-                    for (;;) {
-                        idx[i] = rng.uniform(0, n);
-                        int j = 0;
-                        while (j < i && idx[j] != idx[i]) j++;
-                        if (j == i) break;
-                    }
-            }
-        }
-        __syncthreads();
-        // 2. hypotheses in parallel
-        for (int h = tid; h < niters0; h += blockDim.x) {
-            double rv[3], tv[3];
-            int cnt = -1;
-            if (epnp_subset(obj, img, S.subset + 5 * h, model_points, K, rv, tv)) {
-                double R[9];
-                rod_v2m(rv, R);
-                cnt = 0;
-                for (int i = 0; i < n; i++)
-                    cnt += reproj_err2(R, tv, K, obj[3 * i], obj[3 * i + 1], obj[3 * i + 2], img[2 * i],
-                                       img[2 * i + 1]) <= thr2;
-            }
-            S.count[h] = cnt;
-        }
-        __syncthreads();
-        // 3. sequential replay of the accept / update rule
+        const int* count = H.count + (size_t)pb * H.stride;
         if (tid == 0) {
             int niters = niters0, best = 0, best_iter = -1, it = 0;
             for (; it < niters; it++) {
-                const int c = S.count[it];
+                const int c = count[it];
                 if (c < 0) continue;
                 if (c > (best > model_points - 1 ? best : model_points - 1)) {
                     best = c;
@@ -138,7 +301,13 @@ __global__ __launch_bounds__(256) void k_pnp_ransac(const float* __restrict__ ob
             S.best = best;
             S.best_iter = best_iter;
             S.niters_run = it;
-            if (best > 0) epnp_subset(obj, img, S.subset + 5 * best_iter, model_points, K, S.rv, S.tv);
+            if (best > 0) {
+                const double* mo = H.model + ((size_t)pb * H.stride + best_iter) * 6;
+                for (int k = 0; k < 3; k++) {
+                    S.rv[k] = mo[k];
+                    S.tv[k] = mo[3 + k];
+                }
+            }
         }
         __syncthreads();
         if (tid == 0) {
@@ -207,8 +376,19 @@ int solve_pnp(vs_ctx* ctx, int nprob, const float* d_obj, const float* d_img, co
     ProfScope ps(ctx, "solve_pnp", s);
     const float thr = (float)8.0;  // Config::PNP_RANSAC_THRESHOLD passed as float (Slam.cpp:517)
     const float thr2 = (float)((double)thr * (double)thr);
+    const int niters0 = ransac_iters > 1 ? ransac_iters : 1;
+    const size_t per = (size_t)nprob * niters0;
+    VS_CHECK(ctx->pnp.ensure(per * (6 * sizeof(int) + 6 * sizeof(double))));
+    PnpHyp H;
+    H.model = ctx->pnp.as<double>();
+    H.subset = reinterpret_cast<int*>(H.model + per * 6);
+    H.count = H.subset + per * 5;
+    H.stride = niters0;
+    hipLaunchKernelGGL(k_pnp_subsets, dim3(nprob), dim3(1), 0, s, d_off, niters0, min_inliers, H);
+    hipLaunchKernelGGL(k_pnp_hyp, dim3(nprob, niters0), dim3(64), 0, s, d_obj, d_img, d_off, K[0], K[1], K[2], K[3],
+                       niters0, thr2, min_inliers, H);
     hipLaunchKernelGGL(k_pnp_ransac, dim3(nprob), dim3(256), 0, s, d_obj, d_img, d_off, K[0], K[1], K[2], K[3],
-                       ransac_iters, thr2, 0.99, min_inliers, d_R, d_t, d_stat, d_mask);
+                       ransac_iters, thr2, 0.99, min_inliers, H, d_R, d_t, d_stat, d_mask);
     VS_HIP(hipGetLastError());
     return VS_OK;
 }

@@ -257,13 +257,14 @@ VS_HD inline float reproj_err2(const double* R, const double* t, const Cam& K, f
 }
 
 // ----------------------------------------------------------------------------------- EPnP
-// n >= 4 correspondences (object points X[3i..], image points u[2i..]).  Returns R (world ->
-// camera) and t; false if degenerate.
-template <int MAXN>
-VS_HD bool epnp(const double* X, const double* uv, int n, const Cam& K, double* Rout, double* tout) {
-    if (n < 4 || n > MAXN) return false;
-    // control points
-    double cw[4][3];
+// Written as stages so the device can spread one hypothesis over a wave (pnp.hip): control
+// points and barycentric coordinates, one M^T M entry at a time (each entry's sum runs over the
+// points in order, as the host's row-pair accumulation does), the 12 x 12 eigen-decomposition,
+// the L_6x10 / rho system, and one beta approximation (N = 4 / 2 / 3) refined and turned into a
+// pose per call.  epnp() composes them sequentially; the device composes the same functions.
+
+// Control points cw (centroid + principal axes) and barycentric coordinates; false if degenerate.
+VS_HD inline bool epnp_control(const double* X, int n, double cw[4][3], double (*alphas)[4]) {
     for (int j = 0; j < 3; j++) {
         double s = 0;
         for (int i = 0; i < n; i++) s += X[3 * i + j];
@@ -298,7 +299,6 @@ VS_HD bool epnp(const double* X, const double* uv, int n, const Cam& K, double* 
     CI[6] = (CC[3] * CC[7] - CC[4] * CC[6]) / det;
     CI[7] = (CC[1] * CC[6] - CC[0] * CC[7]) / det;
     CI[8] = (CC[0] * CC[4] - CC[1] * CC[3]) / det;
-    double alphas[MAXN][4];
     for (int i = 0; i < n; i++) {
         const double p[3] = {X[3 * i] - cw[0][0], X[3 * i + 1] - cw[0][1], X[3 * i + 2] - cw[0][2]};
         double a1 = CI[0] * p[0] + CI[1] * p[1] + CI[2] * p[2];
@@ -309,32 +309,33 @@ VS_HD bool epnp(const double* X, const double* uv, int n, const Cam& K, double* 
         alphas[i][3] = a3;
         alphas[i][0] = 1.0 - a1 - a2 - a3;
     }
-    // M^T M accumulated row pair by row pair
-    double MtM[144];
-    for (int i = 0; i < 144; i++) MtM[i] = 0;
-    for (int i = 0; i < n; i++) {
-        double r0[12], r1[12];
-        for (int j = 0; j < 4; j++) {
-            const double a = alphas[i][j];
-            r0[3 * j] = a * K.fx;
-            r0[3 * j + 1] = 0.0;
-            r0[3 * j + 2] = a * (K.cx - uv[2 * i]);
-            r1[3 * j] = 0.0;
-            r1[3 * j + 1] = a * K.fy;
-            r1[3 * j + 2] = a * (K.cy - uv[2 * i + 1]);
-        }
-        for (int a = 0; a < 12; a++)
-            for (int b = 0; b < 12; b++) MtM[a * 12 + b] += r0[a] * r0[b] + r1[a] * r1[b];
-    }
-    double dm[12], um[144];
-    sym_eig<12>(MtM, dm, um);
-    // v[k] = eigenvector of the k-th smallest eigenvalue
-    double v[4][12];
+    return true;
+}
+
+// Row a of the two M rows of point i (M = [alpha_j fx, 0, alpha_j (cx - u)] / [0, alpha_j fy, ...]).
+VS_HD inline double epnp_m0(const double* al, double u, const Cam& K, int a) {
+    const double x = al[a / 3];
+    return (a % 3 == 0) ? x * K.fx : (a % 3 == 1) ? 0.0 : x * (K.cx - u);
+}
+VS_HD inline double epnp_m1(const double* al, double v, const Cam& K, int a) {
+    const double x = al[a / 3];
+    return (a % 3 == 0) ? 0.0 : (a % 3 == 1) ? x * K.fy : x * (K.cy - v);
+}
+// (M^T M)[a][b], accumulated over the points in order
+VS_HD inline double epnp_mtm(const double (*alphas)[4], const double* uv, int n, const Cam& K, int a, int b) {
+    double s = 0;
+    for (int i = 0; i < n; i++)
+        s += epnp_m0(alphas[i], uv[2 * i], K, a) * epnp_m0(alphas[i], uv[2 * i], K, b) +
+             epnp_m1(alphas[i], uv[2 * i + 1], K, a) * epnp_m1(alphas[i], uv[2 * i + 1], K, b);
+    return s;
+}
+
+// From the eigenvectors um (columns, descending eigenvalues): v[k] = eigenvector of the k-th
+// smallest eigenvalue, the L_6x10 matrix and the squared control point distances rho.
+VS_HD inline void epnp_L_rho(const double* um, const double cw[4][3], double v[4][12], double L[6][10], double rho[6]) {
     for (int k = 0; k < 4; k++)
         for (int i = 0; i < 12; i++) v[k][i] = um[i * 12 + (11 - k)];
-    // L_6x10 and rho
     const int pa[6] = {0, 0, 0, 1, 1, 2}, pb[6] = {1, 2, 3, 2, 3, 3};
-    double L[6][10], rho[6];
     for (int j = 0; j < 6; j++) {
         double dv[4][3];
         for (int k = 0; k < 4; k++)
@@ -353,8 +354,15 @@ VS_HD bool epnp(const double* X, const double* uv, int n, const Cam& K, double* 
         const double dx = cw[pa[j]][0] - cw[pb[j]][0], dy = cw[pa[j]][1] - cw[pb[j]][1], dz = cw[pa[j]][2] - cw[pb[j]][2];
         rho[j] = dx * dx + dy * dy + dz * dz;
     }
-    double betas[3][4];
-    {  // N = 4: B11 B12 B13 B14
+}
+
+// Beta approximation s (0: N = 4, 1: N = 2, 2: N = 3), 5 Gauss-Newton steps on the 6 distance
+// constraints, pose by Kabsch on the camera-frame points; returns the mean reprojection error.
+VS_HD inline double epnp_variant(int s, const double L[6][10], const double rho[6], const double v[4][12],
+                                 const double (*alphas)[4], const double* X, const double* uv, int n, const Cam& K,
+                                 double* R, double* t) {
+    double be[4];
+    if (s == 0) {  // N = 4: B11 B12 B13 B14
         double A[24], b[6], x[4];
         for (int j = 0; j < 6; j++) {
             A[j * 4 + 0] = L[j][0];
@@ -366,19 +374,18 @@ VS_HD bool epnp(const double* X, const double* uv, int n, const Cam& K, double* 
         lstsq<6, 4>(A, b, x);
         if (x[0] < 0) {
             const double b0 = sqrt(-x[0]);
-            betas[0][0] = b0;
-            betas[0][1] = b0 ? -x[1] / b0 : 0.0;
-            betas[0][2] = b0 ? -x[2] / b0 : 0.0;
-            betas[0][3] = b0 ? -x[3] / b0 : 0.0;
+            be[0] = b0;
+            be[1] = b0 ? -x[1] / b0 : 0.0;
+            be[2] = b0 ? -x[2] / b0 : 0.0;
+            be[3] = b0 ? -x[3] / b0 : 0.0;
         } else {
             const double b0 = sqrt(x[0]);
-            betas[0][0] = b0;
-            betas[0][1] = b0 ? x[1] / b0 : 0.0;
-            betas[0][2] = b0 ? x[2] / b0 : 0.0;
-            betas[0][3] = b0 ? x[3] / b0 : 0.0;
+            be[0] = b0;
+            be[1] = b0 ? x[1] / b0 : 0.0;
+            be[2] = b0 ? x[2] / b0 : 0.0;
+            be[3] = b0 ? x[3] / b0 : 0.0;
         }
-    }
-    {  // N = 2: B11 B12 B22
+    } else if (s == 1) {  // N = 2: B11 B12 B22
         double A[18], b[6], x[3];
         for (int j = 0; j < 6; j++) {
             A[j * 3 + 0] = L[j][0];
@@ -396,12 +403,11 @@ VS_HD bool epnp(const double* X, const double* uv, int n, const Cam& K, double* 
             b1 = (x[2] > 0) ? sqrt(x[2]) : 0.0;
         }
         if (x[1] < 0) b0 = -b0;
-        betas[1][0] = b0;
-        betas[1][1] = b1;
-        betas[1][2] = 0.0;
-        betas[1][3] = 0.0;
-    }
-    {  // N = 3: B11 B12 B22 B13 B23
+        be[0] = b0;
+        be[1] = b1;
+        be[2] = 0.0;
+        be[3] = 0.0;
+    } else {  // N = 3: B11 B12 B22 B13 B23
         double A[30], b[6], x[5];
         for (int j = 0; j < 6; j++) {
             for (int c = 0; c < 5; c++) A[j * 5 + c] = L[j][c];
@@ -417,72 +423,88 @@ VS_HD bool epnp(const double* X, const double* uv, int n, const Cam& K, double* 
             b1 = (x[2] > 0) ? sqrt(x[2]) : 0.0;
         }
         if (x[1] < 0) b0 = -b0;
-        betas[2][0] = b0;
-        betas[2][1] = b1;
-        betas[2][2] = b0 ? x[3] / b0 : 0.0;
-        betas[2][3] = 0.0;
+        be[0] = b0;
+        be[1] = b1;
+        be[2] = b0 ? x[3] / b0 : 0.0;
+        be[3] = 0.0;
     }
+    for (int it = 0; it < 5; it++) {  // Gauss-Newton on the 6 distance constraints
+        double A[24], b[6], x[4];
+        for (int j = 0; j < 6; j++) {
+            const double* l = L[j];
+            A[j * 4 + 0] = 2 * l[0] * be[0] + l[1] * be[1] + l[3] * be[2] + l[6] * be[3];
+            A[j * 4 + 1] = l[1] * be[0] + 2 * l[2] * be[1] + l[4] * be[2] + l[7] * be[3];
+            A[j * 4 + 2] = l[3] * be[0] + l[4] * be[1] + 2 * l[5] * be[2] + l[8] * be[3];
+            A[j * 4 + 3] = l[6] * be[0] + l[7] * be[1] + l[8] * be[2] + 2 * l[9] * be[3];
+            b[j] = rho[j] - (l[0] * be[0] * be[0] + l[1] * be[0] * be[1] + l[2] * be[1] * be[1] +
+                             l[3] * be[0] * be[2] + l[4] * be[1] * be[2] + l[5] * be[2] * be[2] +
+                             l[6] * be[0] * be[3] + l[7] * be[1] * be[3] + l[8] * be[2] * be[3] +
+                             l[9] * be[3] * be[3]);
+        }
+        lstsq<6, 4>(A, b, x);
+        for (int k = 0; k < 4; k++) be[k] += x[k];
+    }
+    // camera coordinates of control and object points
+    double ccs[4][3];
+    for (int i = 0; i < 4; i++)
+        for (int c = 0; c < 3; c++)
+            ccs[i][c] = be[0] * v[0][3 * i + c] + be[1] * v[1][3 * i + c] + be[2] * v[2][3 * i + c] +
+                        be[3] * v[3][3 * i + c];
+    double pcs0z = alphas[0][0] * ccs[0][2] + alphas[0][1] * ccs[1][2] + alphas[0][2] * ccs[2][2] +
+                   alphas[0][3] * ccs[3][2];
+    const double sgn = pcs0z < 0 ? -1.0 : 1.0;
+    double pc0[3] = {0, 0, 0}, pw0[3] = {0, 0, 0};
+    for (int i = 0; i < n; i++)
+        for (int c = 0; c < 3; c++) {
+            pc0[c] += sgn * (alphas[i][0] * ccs[0][c] + alphas[i][1] * ccs[1][c] + alphas[i][2] * ccs[2][c] +
+                             alphas[i][3] * ccs[3][c]);
+            pw0[c] += X[3 * i + c];
+        }
+    for (int c = 0; c < 3; c++) {
+        pc0[c] /= n;
+        pw0[c] /= n;
+    }
+    double ABt[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+    for (int i = 0; i < n; i++) {
+        double pc[3];
+        for (int c = 0; c < 3; c++)
+            pc[c] = sgn * (alphas[i][0] * ccs[0][c] + alphas[i][1] * ccs[1][c] + alphas[i][2] * ccs[2][c] +
+                           alphas[i][3] * ccs[3][c]) - pc0[c];
+        const double pw[3] = {X[3 * i] - pw0[0], X[3 * i + 1] - pw0[1], X[3 * i + 2] - pw0[2]};
+        for (int a = 0; a < 3; a++)
+            for (int b = 0; b < 3; b++) ABt[a * 3 + b] += pc[a] * pw[b];
+    }
+    rotation_from_cross(ABt, R);
+    for (int c = 0; c < 3; c++) t[c] = pc0[c] - (R[c * 3] * pw0[0] + R[c * 3 + 1] * pw0[1] + R[c * 3 + 2] * pw0[2]);
+    double err = 0;
+    for (int i = 0; i < n; i++) {
+        double u, vv;
+        project(R, t, K, X[3 * i], X[3 * i + 1], X[3 * i + 2], u, vv);
+        const double du = uv[2 * i] - u, dvv = uv[2 * i + 1] - vv;
+        err += sqrt(du * du + dvv * dvv);
+    }
+    return err / n;
+}
+
+// n >= 4 correspondences (object points X[3i..], image points u[2i..]).  Returns R (world ->
+// camera) and t; false if degenerate.  The lowest-error approximation wins (first on ties).
+template <int MAXN>
+VS_HD bool epnp(const double* X, const double* uv, int n, const Cam& K, double* Rout, double* tout) {
+    if (n < 4 || n > MAXN) return false;
+    double cw[4][3], alphas[MAXN][4];
+    if (!epnp_control(X, n, cw, alphas)) return false;
+    double MtM[144];
+    for (int a = 0; a < 12; a++)
+        for (int b = 0; b < 12; b++) MtM[a * 12 + b] = epnp_mtm(alphas, uv, n, K, a, b);
+    double dm[12], um[144];
+    sym_eig<12>(MtM, dm, um);
+    double v[4][12], L[6][10], rho[6];
+    epnp_L_rho(um, cw, v, L, rho);
     double best_err = 0;
     bool have = false;
     for (int s = 0; s < 3; s++) {
-        double* be = betas[s];
-        for (int it = 0; it < 5; it++) {  // Gauss-Newton on the 6 distance constraints
-            double A[24], b[6], x[4];
-            for (int j = 0; j < 6; j++) {
-                const double* l = L[j];
-                A[j * 4 + 0] = 2 * l[0] * be[0] + l[1] * be[1] + l[3] * be[2] + l[6] * be[3];
-                A[j * 4 + 1] = l[1] * be[0] + 2 * l[2] * be[1] + l[4] * be[2] + l[7] * be[3];
-                A[j * 4 + 2] = l[3] * be[0] + l[4] * be[1] + 2 * l[5] * be[2] + l[8] * be[3];
-                A[j * 4 + 3] = l[6] * be[0] + l[7] * be[1] + l[8] * be[2] + 2 * l[9] * be[3];
-                b[j] = rho[j] - (l[0] * be[0] * be[0] + l[1] * be[0] * be[1] + l[2] * be[1] * be[1] +
-                                 l[3] * be[0] * be[2] + l[4] * be[1] * be[2] + l[5] * be[2] * be[2] +
-                                 l[6] * be[0] * be[3] + l[7] * be[1] * be[3] + l[8] * be[2] * be[3] +
-                                 l[9] * be[3] * be[3]);
-            }
-            lstsq<6, 4>(A, b, x);
-            for (int k = 0; k < 4; k++) be[k] += x[k];
-        }
-        // camera coordinates of control and object points
-        double ccs[4][3];
-        for (int i = 0; i < 4; i++)
-            for (int c = 0; c < 3; c++)
-                ccs[i][c] = be[0] * v[0][3 * i + c] + be[1] * v[1][3 * i + c] + be[2] * v[2][3 * i + c] +
-                            be[3] * v[3][3 * i + c];
-        double pcs0z = alphas[0][0] * ccs[0][2] + alphas[0][1] * ccs[1][2] + alphas[0][2] * ccs[2][2] +
-                       alphas[0][3] * ccs[3][2];
-        const double sgn = pcs0z < 0 ? -1.0 : 1.0;
-        double pc0[3] = {0, 0, 0}, pw0[3] = {0, 0, 0};
-        for (int i = 0; i < n; i++)
-            for (int c = 0; c < 3; c++) {
-                pc0[c] += sgn * (alphas[i][0] * ccs[0][c] + alphas[i][1] * ccs[1][c] + alphas[i][2] * ccs[2][c] +
-                                 alphas[i][3] * ccs[3][c]);
-                pw0[c] += X[3 * i + c];
-            }
-        for (int c = 0; c < 3; c++) {
-            pc0[c] /= n;
-            pw0[c] /= n;
-        }
-        double ABt[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
-        for (int i = 0; i < n; i++) {
-            double pc[3];
-            for (int c = 0; c < 3; c++)
-                pc[c] = sgn * (alphas[i][0] * ccs[0][c] + alphas[i][1] * ccs[1][c] + alphas[i][2] * ccs[2][c] +
-                               alphas[i][3] * ccs[3][c]) - pc0[c];
-            const double pw[3] = {X[3 * i] - pw0[0], X[3 * i + 1] - pw0[1], X[3 * i + 2] - pw0[2]};
-            for (int a = 0; a < 3; a++)
-                for (int b = 0; b < 3; b++) ABt[a * 3 + b] += pc[a] * pw[b];
-        }
         double R[9], t[3];
-        rotation_from_cross(ABt, R);
-        for (int c = 0; c < 3; c++) t[c] = pc0[c] - (R[c * 3] * pw0[0] + R[c * 3 + 1] * pw0[1] + R[c * 3 + 2] * pw0[2]);
-        double err = 0;
-        for (int i = 0; i < n; i++) {
-            double u, vv;
-            project(R, t, K, X[3 * i], X[3 * i + 1], X[3 * i + 2], u, vv);
-            const double du = uv[2 * i] - u, dvv = uv[2 * i + 1] - vv;
-            err += sqrt(du * du + dvv * dvv);
-        }
-        err /= n;
+        const double err = epnp_variant(s, L, rho, v, alphas, X, uv, n, K, R, t);
         if (!have || err < best_err) {
             have = true;
             best_err = err;

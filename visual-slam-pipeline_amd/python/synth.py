@@ -173,3 +173,47 @@ def frames(indices, n_total, seed=SEED, dt=1.0 / 10.0):
         rng = np.random.default_rng((seed + 13) * 1000003 + i)
         out[i] = dict(bgr=bgr, depth=depth_tum(z, rng), R_wc=R, t_wc=t, timestamp=1311868164.0 + i * dt)
     return out
+
+
+def loop_trajectory(n=126, radius=0.6, seed=SEED):
+    """n camera->world poses evenly spaced on a closed circle (Pioneer-like: 0.4 m above the floor,
+    heading along the tangent; at 0.3 m/s and 10 processed frames/s a 0.6 m radius is a yaw rate of
+    0.5 rad/s and n = 126 frames per lap).  Pose n equals pose 0, so cycling the n rendered frames
+    is a continuous drive (timestamps keep increasing), for benchmark sequences of any length."""
+    rng = np.random.default_rng(seed + 29)
+    phase = rng.uniform(0, 2 * np.pi)
+    poses = []
+    for i in range(n):
+        a = phase + 2 * np.pi * i / n
+        pos = np.array([radius * np.cos(a), 0.0, radius * np.sin(a)])
+        # tangent direction (counter-clockwise) = camera forward (+z)
+        fwd = np.array([-np.sin(a), 0.0, np.cos(a)])
+        yaw = np.arctan2(fwd[0], fwd[2])
+        poses.append((yaw_rotation(yaw), pos))
+    return poses
+
+
+def _render_one(args):
+    i, R, t, seed = args
+    scene = Scene(seed)
+    bgr, z = scene.render(R, t)
+    rng = np.random.default_rng((seed + 17) * 1000003 + i)
+    return bgr, depth_tum(z, rng)
+
+
+def loop_sequence(n, seed=SEED, dt=1.0 / 10.0, workers=None):
+    """The n frames of loop_trajectory rendered (in a process pool when workers > 1):
+    dict(bgr [n,H,W,3] u8, depth [n,H,W] f32, R_wc [n,3,3], t_wc [n,3], dt)."""
+    poses = loop_trajectory(n, seed=seed)
+    jobs = [(i, R, t, seed) for i, (R, t) in enumerate(poses)]
+    if workers is None:
+        import os
+        workers = min(16, os.cpu_count() or 1, n)
+    if workers > 1:
+        import multiprocessing as mp
+        with mp.get_context("fork").Pool(workers) as pool:
+            out = pool.map(_render_one, jobs)
+    else:
+        out = [_render_one(j) for j in jobs]
+    return dict(bgr=np.stack([o[0] for o in out]), depth=np.stack([o[1] for o in out]),
+                R_wc=np.stack([p[0] for p in poses]), t_wc=np.stack([p[1] for p in poses]), dt=dt)
