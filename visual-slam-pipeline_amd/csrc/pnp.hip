@@ -73,7 +73,7 @@ __global__ void k_pnp_subsets(const int* __restrict__ off, int niters0, int min_
     if (!pnp_problem_runs(n, min_inliers, model_points)) return;
     CvRng rng((uint64_t)-1);
     for (int it = 0; it < niters0; it++) {
-        int* idx = H.subset + ((size_t)pb * H.stride + it) * 5;
+        int idx[5];  // drawn in registers, stored once
         for (int i = 0; i < model_points; i++)
             for (;;) {
                 idx[i] = rng.uniform(0, n);
@@ -81,6 +81,8 @@ __global__ void k_pnp_subsets(const int* __restrict__ off, int niters0, int min_
                 while (j < i && idx[j] != idx[i]) j++;
                 if (j == i) break;
             }
+        int* dst = H.subset + ((size_t)pb * H.stride + it) * 5;
+        for (int i = 0; i < model_points; i++) dst[i] = idx[i];
     }
 }
 

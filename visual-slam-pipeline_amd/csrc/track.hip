@@ -3,14 +3,17 @@
 // The reference walks every map point in order and, for the keypoints within 12 px of its
 // projection (30-px grid, :388-455), keeps the first strictly smaller L2 descriptor distance
 // below 0.5; the keypoint then takes the map point if that distance beats the keypoint's best so
-// far (:460-465).  Two phases:
-//   k_tlm_match    one lane per map point: projection, grid cells, candidate distances (fp64,
-//                  cv::norm's order: float differences, squares summed in groups of four), best
-//                  keypoint + distance — independent across map points, the HBM-bound part;
-//   k_tlm_resolve  the order-dependent assignment: candidates (map points with a best keypoint)
-//                  compacted in map-point order 1024 at a time and applied sequentially, which
-//                  yields exactly the reference's final kp->map-point table, tracked count and
-//                  (map point, keypoint) observation list in map-point order.
+// far (:460-465).  Phases (one stream, no host round trip):
+//   k_tlm_grid     the 30-px keypoint grid in keypoint order, built in LDS by one workgroup;
+//   k_tlm_cand     one lane per map point: projection, image / depth gates, the keypoints within
+//                  12 px in the reference's visiting order (the point's candidate list);
+//   k_tlm_dist     one lane per (map point, candidate): the fp64 L2 distance in cv::norm's order
+//                  (float differences, squares summed in groups of four) — the HBM-bound part;
+//   k_tlm_resolve  per map point the first strictly smaller distance below 0.5, then the
+//                  order-dependent assignment decided in parallel (a candidate wins iff its
+//                  distance is below every earlier candidate's for the same keypoint), giving
+//                  exactly the reference's kp->map-point table, tracked count and observation
+//                  list in map-point order.
 // Compiled with -ffp-contract=off: distances and projections equal the CPU restatement bit for bit.
 #include <hip/hip_runtime.h>
 
@@ -23,30 +26,36 @@ constexpr double kTlmRadius = 12;  // TRACK_SEARCH_RADIUS (Config.h:109)
 constexpr double kTlmDesc = 0.5;   // TRACK_DESC_THRESHOLD (Config.h:110)
 constexpr int kTlmMaxKp = 1024;
 
-// Keypoint grid: cells in keypoint order (counting sort on one lane; <= 1024 keypoints).
-__global__ void k_tlm_grid(const vs_keypoint* __restrict__ kps, int nkp, int GW, int GH, int* __restrict__ start,
-                           int* __restrict__ items) {
-    if (threadIdx.x != 0) return;
-    const int nc = GW * GH;
-    for (int c = 0; c <= nc; c++) start[c] = 0;
-    for (int ki = 0; ki < nkp; ki++) {
-        int gx = min((int)(kps[ki].x / kTlmCell), GW - 1);
-        int gy = min((int)(kps[ki].y / kTlmCell), GH - 1);
-        if (gx >= 0 && gy >= 0) start[gy * GW + gx + 1]++;
+// Keypoint grid (Slam.cpp:389-401): per-cell keypoint lists in keypoint order, built in LDS by one
+// workgroup: a keypoint's slot is its cell's prefix count plus the number of earlier keypoints in
+// the same cell (the order the reference's push_back produces).
+constexpr int kTlmMaxCells = 4096;
+__global__ __launch_bounds__(1024) void k_tlm_grid(const vs_keypoint* __restrict__ kps, int nkp, int GW, int GH,
+                                                   int* __restrict__ start, int* __restrict__ items) {
+    __shared__ int s_cell[kTlmMaxKp];
+    __shared__ int s_start[kTlmMaxCells + 1];
+    const int tid = threadIdx.x, nc = GW * GH;
+    for (int c = tid; c <= nc; c += blockDim.x) s_start[c] = 0;
+    __syncthreads();
+    for (int ki = tid; ki < nkp; ki += blockDim.x) {
+        const int gx = min((int)(kps[ki].x / kTlmCell), GW - 1);
+        const int gy = min((int)(kps[ki].y / kTlmCell), GH - 1);
+        const int c = (gx >= 0 && gy >= 0) ? gy * GW + gx : -1;
+        s_cell[ki] = c;
+        if (c >= 0) atomicAdd(&s_start[c + 1], 1);
     }
-    for (int c = 0; c < nc; c++) start[c + 1] += start[c];
-    // second pass places keypoints in order; reuse items[] write cursors from start[]
-    for (int ki = 0, filled = 0; ki < nkp; ki++) {
-        (void)filled;
-        int gx = min((int)(kps[ki].x / kTlmCell), GW - 1);
-        int gy = min((int)(kps[ki].y / kTlmCell), GH - 1);
-        if (gx >= 0 && gy >= 0) {
-            const int c = gy * GW + gx;
-            int pos = start[c];
-            while (items[pos] != -1) pos++;  // items pre-filled with -1
-            items[pos] = ki;
-        }
+    __syncthreads();
+    if (tid == 0)
+        for (int c = 0; c < nc; c++) s_start[c + 1] += s_start[c];
+    __syncthreads();
+    for (int ki = tid; ki < nkp; ki += blockDim.x) {
+        const int c = s_cell[ki];
+        if (c < 0) continue;
+        int rank = 0;
+        for (int kj = 0; kj < ki; kj++) rank += s_cell[kj] == c;
+        items[s_start[c] + rank] = ki;
     }
+    for (int c = tid; c <= nc; c += blockDim.x) start[c] = s_start[c];
 }
 
 __device__ double desc_l2_dev(const float* __restrict__ a, const float* __restrict__ b) {
@@ -66,16 +75,22 @@ struct TlmPose {
     double Rc[9], tc[3], fx, fy, cx, cy;
 };
 
-__global__ __launch_bounds__(256) void k_tlm_match(const double* __restrict__ mp_pos, const float* __restrict__ mp_desc,
-                                                   const uint8_t* __restrict__ mp_valid, int n_mp,
-                                                   const vs_keypoint* __restrict__ kps, const float* __restrict__ desc,
-                                                   const int* __restrict__ start, const int* __restrict__ items, int GW,
-                                                   int GH, int img_w, int img_h, TlmPose T, int* __restrict__ best_ki,
-                                                   double* __restrict__ best_d) {
+// Phase 1, one lane per map point: projection (:421-431) and the keypoints within the search
+// radius in the reference's visiting order (cells row by row, keypoints in insertion order,
+// :434-450), stored as the map point's candidate list.  A point with more candidates than slots
+// (not reachable with NMS-spaced keypoints, kept for safety) evaluates them itself and stores its
+// winner as its single candidate, whose distance phase 2 recomputes identically.
+constexpr int kTlmMaxCand = 40;
+__global__ __launch_bounds__(256) void k_tlm_cand(const double* __restrict__ mp_pos, const float* __restrict__ mp_desc,
+                                                  const uint8_t* __restrict__ mp_valid, int n_mp,
+                                                  const vs_keypoint* __restrict__ kps, const float* __restrict__ desc,
+                                                  const int* __restrict__ start, const int* __restrict__ items, int GW,
+                                                  int GH, int img_w, int img_h, TlmPose T, int* __restrict__ cnt,
+                                                  int* __restrict__ cand) {
     const int mp = blockIdx.x * 256 + threadIdx.x;
     if (mp >= n_mp) return;
-    int bk = -1;
-    double bd = kTlmDesc;
+    int c = 0;
+    int* my = cand + (size_t)mp * kTlmMaxCand;
     if (mp_valid[mp]) {
         const double x = mp_pos[3 * mp], y = mp_pos[3 * mp + 1], z = mp_pos[3 * mp + 2];
         const double* Rc = T.Rc;
@@ -90,76 +105,144 @@ __global__ __launch_bounds__(256) void k_tlm_match(const double* __restrict__ mp
                 const int gy0 = max(0, (int)((v - kTlmRadius) / kTlmCell));
                 const int gx1 = min(GW - 1, (int)((u + kTlmRadius) / kTlmCell));
                 const int gy1 = min(GH - 1, (int)((v + kTlmRadius) / kTlmCell));
-                const float* md = mp_desc + (size_t)mp * 256;
                 for (int gy = gy0; gy <= gy1; gy++)
                     for (int gx = gx0; gx <= gx1; gx++) {
-                        const int c = gy * GW + gx;
-                        for (int it = start[c]; it < start[c + 1]; it++) {
+                        const int cc = gy * GW + gx;
+                        for (int it = start[cc]; it < start[cc + 1]; it++) {
                             const int ki = items[it];
                             const double dx = u - (double)kps[ki].x, dy = v - (double)kps[ki].y;
                             if (dx * dx + dy * dy > kTlmRadius * kTlmRadius) continue;
-                            const double d = desc_l2_dev(md, desc + (size_t)ki * 256);
-                            if (d < bd) {
-                                bd = d;
-                                bk = ki;
-                            }
+                            if (c < kTlmMaxCand) my[c] = ki;
+                            c++;
                         }
                     }
+                if (c > kTlmMaxCand) {  // overflow: the sequential scan, winner only
+                    int bk = -1;
+                    double bd = kTlmDesc;
+                    const float* md = mp_desc + (size_t)mp * 256;
+                    for (int gy = gy0; gy <= gy1; gy++)
+                        for (int gx = gx0; gx <= gx1; gx++) {
+                            const int cc = gy * GW + gx;
+                            for (int it = start[cc]; it < start[cc + 1]; it++) {
+                                const int ki = items[it];
+                                const double dx = u - (double)kps[ki].x, dy = v - (double)kps[ki].y;
+                                if (dx * dx + dy * dy > kTlmRadius * kTlmRadius) continue;
+                                const double d = desc_l2_dev(md, desc + (size_t)ki * 256);
+                                if (d < bd) {
+                                    bd = d;
+                                    bk = ki;
+                                }
+                            }
+                        }
+                    c = 0;
+                    if (bk >= 0) my[c++] = bk;
+                }
             }
         }
     }
-    best_ki[mp] = bk;
-    best_d[mp] = bd;
+    cnt[mp] = c;
 }
 
-// Sequential assignment in map-point order (Slam.cpp:460-465).  One 1024-lane workgroup.
+// Phase 2: one lane per (map point, candidate): the cv::norm distance (:451).
+__global__ __launch_bounds__(256) void k_tlm_dist(const float* __restrict__ mp_desc, const float* __restrict__ desc,
+                                                  int n_mp, const int* __restrict__ cnt, const int* __restrict__ cand,
+                                                  double* __restrict__ dist) {
+    const long r = (long)blockIdx.x * 256 + threadIdx.x;
+    const int mp = (int)(r / kTlmMaxCand), j = (int)(r % kTlmMaxCand);
+    if (mp >= n_mp || j >= cnt[mp]) return;
+    dist[r] = desc_l2_dev(mp_desc + (size_t)mp * 256, desc + (size_t)cand[r] * 256);
+}
+
+// Assignment in map-point order (Slam.cpp:460-465), decided in parallel: keypoint ki's best
+// distance is a running minimum over the map points that chose it, so a candidate (map point m
+// with best keypoint ki, distance d) is applied — kp_to_mp[ki] = m, one tracked++ and one
+// add_observation — iff d is strictly below every earlier candidate's distance for ki.  Chunks
+// of 1024 candidates in map-point order: within a chunk each candidate compares against the
+// earlier ones for its keypoint and against the minimum carried from earlier chunks; winners
+// are compacted in order into the observation list.  One 1024-lane workgroup.
 // result[0] = tracked, result[1] = observations produced (all of them, even beyond obs_cap).
-__global__ __launch_bounds__(1024) void k_tlm_resolve(const int* __restrict__ best_ki, const double* __restrict__ best_d,
-                                                      int n_mp, int nkp, int* __restrict__ kp_to_mp,
+__global__ __launch_bounds__(1024) void k_tlm_resolve(const int* __restrict__ cnt, const int* __restrict__ cand,
+                                                      const double* __restrict__ dist, int n_mp, int nkp, int* __restrict__ kp_to_mp,
                                                       int* __restrict__ obs_mp, int* __restrict__ obs_kp, int obs_cap,
                                                       int* __restrict__ result) {
-    __shared__ double s_best[kTlmMaxKp];
+    __shared__ unsigned long long s_best[kTlmMaxKp];  // bits of the running minimum (d >= 0: order-preserving)
     __shared__ int s_kpmp[kTlmMaxKp];
-    __shared__ int s_cmp[1024];
+    __shared__ int s_cmp[1024], s_cki[1024];
+    __shared__ unsigned long long s_cd[1024];
     __shared__ int s_wcnt[16];
     __shared__ int s_nobs;
     const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
     for (int k = tid; k < nkp; k += 1024) {
-        s_best[k] = 1e9;
+        s_best[k] = (unsigned long long)__double_as_longlong(1e9);
         s_kpmp[k] = kp_to_mp[k];
     }
     if (tid == 0) s_nobs = 0;
     __syncthreads();
     for (int c0 = 0; c0 < n_mp; c0 += 1024) {
+        // phase 3 for this chunk: each map point's first strictly smaller distance below the
+        // threshold in visiting order (:439-456), then the chunk's candidates compacted in order
         const int mp = c0 + tid;
-        const bool cand = mp < n_mp && best_ki[mp] >= 0;
-        const unsigned long long bal = __ballot(cand);
-        if (lane == 0) s_wcnt[wv] = __popcll(bal);
-        __syncthreads();
-        int off = 0;
-        for (int k = 0; k < wv; k++) off += s_wcnt[k];
-        if (cand) s_cmp[off + __popcll(bal & ((1ull << lane) - 1ull))] = mp;
-        __syncthreads();
-        if (tid == 0) {
-            int nc = 0;
-            for (int k = 0; k < 16; k++) nc += s_wcnt[k];
-            int nobs = s_nobs;
-            for (int j = 0; j < nc; j++) {
-                const int m = s_cmp[j];
-                const int ki = best_ki[m];
-                const double d = best_d[m];
-                if (d < s_best[ki]) {
-                    s_kpmp[ki] = m;
-                    s_best[ki] = d;
-                    if (nobs < obs_cap) {
-                        obs_mp[nobs] = m;
-                        obs_kp[nobs] = ki;
-                    }
-                    nobs++;
+        int ki0 = -1;
+        double bd = kTlmDesc;
+        if (mp < n_mp) {
+            const int c = cnt[mp];
+            for (int j = 0; j < c; j++) {
+                const double d = dist[(size_t)mp * kTlmMaxCand + j];
+                if (d < bd) {
+                    bd = d;
+                    ki0 = cand[(size_t)mp * kTlmMaxCand + j];
                 }
             }
-            s_nobs = nobs;
         }
+        const bool cand_ok = ki0 >= 0;
+        unsigned long long bal = __ballot(cand_ok);
+        if (lane == 0) s_wcnt[wv] = __popcll(bal);
+        __syncthreads();
+        int off = 0, nc = 0;
+        for (int k = 0; k < 16; k++) {
+            if (k < wv) off += s_wcnt[k];
+            nc += s_wcnt[k];
+        }
+        if (cand_ok) {
+            const int j = off + __popcll(bal & ((1ull << lane) - 1ull));
+            s_cmp[j] = mp;
+            s_cki[j] = ki0;
+            s_cd[j] = (unsigned long long)__double_as_longlong(bd);
+        }
+        __syncthreads();
+        // winners: strictly below the carried minimum and below every earlier candidate of the keypoint
+        bool win = false;
+        int ki = -1;
+        unsigned long long d = 0;
+        if (tid < nc) {
+            ki = s_cki[tid];
+            d = s_cd[tid];
+            win = d < s_best[ki];
+            for (int j = 0; j < tid && win; j++)
+                if (s_cki[j] == ki && s_cd[j] <= d) win = false;
+        }
+        __syncthreads();
+        if (win) atomicMin(&s_best[ki], d);
+        bal = __ballot(win);
+        if (lane == 0) s_wcnt[wv] = __popcll(bal);
+        __syncthreads();
+        // the last winner of a keypoint has its smallest distance (winners strictly decrease)
+        if (win && s_best[ki] == d) s_kpmp[ki] = s_cmp[tid];
+        off = 0;
+        int nw = 0;
+        for (int k = 0; k < 16; k++) {
+            if (k < wv) off += s_wcnt[k];
+            nw += s_wcnt[k];
+        }
+        if (win) {
+            const int o = s_nobs + off + __popcll(bal & ((1ull << lane) - 1ull));
+            if (o < obs_cap) {
+                obs_mp[o] = s_cmp[tid];
+                obs_kp[o] = ki;
+            }
+        }
+        __syncthreads();
+        if (tid == 0) s_nobs += nw;
         __syncthreads();
     }
     for (int k = tid; k < nkp; k += 1024) kp_to_mp[k] = s_kpmp[k];
@@ -175,15 +258,18 @@ int track_local_map(vs_ctx* ctx, const double* d_mp_pos, const float* d_mp_desc,
                     int obs_cap, int* d_result, hipStream_t s) {
     VS_ARG(nkp >= 0 && nkp <= kTlmMaxKp, "track_local_map: at most 1024 keypoints");
     VS_ARG(img_w > 0 && img_h > 0, "track_local_map: bad image size");
+    VS_ARG(((img_w + kTlmCell - 1) / kTlmCell) * ((img_h + kTlmCell - 1) / kTlmCell) <= kTlmMaxCells,
+           "track_local_map: image too large for the keypoint grid");
     const int GW = (img_w + kTlmCell - 1) / kTlmCell, GH = (img_h + kTlmCell - 1) / kTlmCell;
     const size_t grid_bytes = (size_t)(GW * GH + 1) * sizeof(int) + (size_t)(nkp + 1) * sizeof(int);
-    const size_t per_mp = sizeof(int) + sizeof(double);
+    const size_t per_mp = sizeof(int) + (size_t)kTlmMaxCand * (sizeof(int) + sizeof(double));
     VS_CHECK(ctx->tlm.ensure(grid_bytes + 16 + (size_t)(n_mp + 1) * per_mp));
     char* base = static_cast<char*>(ctx->tlm.p);
     int* start = reinterpret_cast<int*>(base);
     int* items = start + GW * GH + 1;
-    double* best_d = reinterpret_cast<double*>(base + ((grid_bytes + 15) / 16) * 16);
-    int* best_ki = reinterpret_cast<int*>(best_d + n_mp + 1);
+    double* dist = reinterpret_cast<double*>(base + ((grid_bytes + 15) / 16) * 16);
+    int* cand = reinterpret_cast<int*>(dist + (size_t)(n_mp + 1) * kTlmMaxCand);
+    int* cnt = cand + (size_t)(n_mp + 1) * kTlmMaxCand;
     TlmPose T;
     for (int i = 0; i < 3; i++)
         for (int j = 0; j < 3; j++) T.Rc[i * 3 + j] = R[j * 3 + i];
@@ -194,12 +280,16 @@ int track_local_map(vs_ctx* ctx, const double* d_mp_pos, const float* d_mp_desc,
     T.cy = K[3];
     ProfScope ps(ctx, "track_local_map", s);
     VS_HIP(hipMemsetAsync(items, 0xff, (size_t)(nkp + 1) * sizeof(int), s));
-    if (nkp > 0) hipLaunchKernelGGL(k_tlm_grid, dim3(1), dim3(64), 0, s, d_kps, nkp, GW, GH, start, items);
+    if (nkp > 0) hipLaunchKernelGGL(k_tlm_grid, dim3(1), dim3(1024), 0, s, d_kps, nkp, GW, GH, start, items);
     else VS_HIP(hipMemsetAsync(start, 0, (size_t)(GW * GH + 1) * sizeof(int), s));
-    if (n_mp > 0)
-        hipLaunchKernelGGL(k_tlm_match, dim3((n_mp + 255) / 256), dim3(256), 0, s, d_mp_pos, d_mp_desc, d_mp_valid, n_mp,
-                           d_kps, d_desc, start, items, GW, GH, img_w, img_h, T, best_ki, best_d);
-    hipLaunchKernelGGL(k_tlm_resolve, dim3(1), dim3(1024), 0, s, best_ki, best_d, n_mp, nkp, d_kp_to_mp, d_obs_mp,
+    if (n_mp > 0) {
+        hipLaunchKernelGGL(k_tlm_cand, dim3((n_mp + 255) / 256), dim3(256), 0, s, d_mp_pos, d_mp_desc, d_mp_valid, n_mp,
+                           d_kps, d_desc, start, items, GW, GH, img_w, img_h, T, cnt, cand);
+        const long pairs = (long)n_mp * kTlmMaxCand;
+        hipLaunchKernelGGL(k_tlm_dist, dim3((unsigned)((pairs + 255) / 256)), dim3(256), 0, s, d_mp_desc, d_desc, n_mp,
+                           cnt, cand, dist);
+    }
+    hipLaunchKernelGGL(k_tlm_resolve, dim3(1), dim3(1024), 0, s, cnt, cand, dist, n_mp, nkp, d_kp_to_mp, d_obs_mp,
                        d_obs_kp, obs_cap, d_result);
     VS_HIP(hipGetLastError());
     return VS_OK;
