@@ -1,0 +1,37 @@
+"""Phase cycle breakdown of the local-BA Cholesky kernel (profiling build libvslam_hip_prof.so, built by
+`make -C visual-slam-pipeline_amd prof`): lane-0 clock64 deltas summed over the launches of one
+stress-window solve.  Phases: 0 panel load, 1 panel factorization, 2 write-back + trailing update,
+3 forward solve, 4 backward solve."""
+import ctypes
+import json
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+for p in ("visual-slam-pipeline_amd/python", "tests"):
+    sys.path.insert(0, os.path.join(ROOT, p))
+
+
+def main():
+    import vslam_abi as va
+    lib = va.load_library(os.path.join(ROOT, "visual-slam-pipeline_amd", "libvslam_hip_prof.so"))
+    lib.vs_debug_ba_cycles.argtypes = [ctypes.c_void_p, ctypes.c_int]
+    from test_gpu_ba import windowed_problem
+    R, t, P, P0, kf, pt, uv = windowed_problem(50, 10000, 7, span=3, noise=1.0, pert=0.05)
+    ctx = va.Context(0)
+    ctx.local_ba(R, t, P0, kf, pt, uv)
+    cyc = np.zeros(8, np.uint64)
+    lib.vs_debug_ba_cycles(cyc.ctypes.data, 1)
+    g = ctx.local_ba(R, t, P0, kf, pt, uv)
+    lib.vs_debug_ba_cycles(cyc.ctypes.data, 1)
+    names = ["panel_load", "panel_factor", "trailing", "fwd_solve", "bwd_solve"]
+    iters = int(g[5][0])
+    print(json.dumps({"lm_iterations": iters,
+                      "kcycles_per_solve": {names[k]: round(float(cyc[k]) / max(iters, 1) / 1e3, 1) for k in range(5)}}))
+    ctx.close()
+
+
+if __name__ == "__main__":
+    main()

@@ -73,39 +73,86 @@ __global__ void k_ba_obs(BaDev d) {
     ba_obs_terms(d.pc[d.okf[o]], d.P + 3 * (size_t)d.opt[o], d.ouv[2 * o], d.ouv[2 * o + 1], d.K, d.terms[o]);
 }
 
-// mode 0: total_cost from the terms; 1: new_cost (new params); 2: squared error (current params)
-__global__ void k_ba_chunk_sums(BaDev d, int mode, int check) {
+// mode 0: total_cost from the terms; 1: new_cost (new params); 2: squared error (current params).
+// One 256-lane workgroup per fixed chunk of kCostChunk observations: the per-observation terms in
+// parallel into LDS, then lane 0 sums them in observation order (the oracle's chunked order).
+__global__ __launch_bounds__(kCostChunk) void k_ba_chunk_sums(BaDev d, int mode, int check) {
     if (check) BA_LIVE(d);
-    const int c = blockIdx.x * blockDim.x + threadIdx.x;
-    if (c >= d.n_chunks) return;
+    __shared__ double s_v[kCostChunk];
+    const int c = blockIdx.x, t = threadIdx.x;
     const int o0 = c * kCostChunk, o1 = min(d.n_obs, o0 + kCostChunk);
-    double s = 0;
-    for (int o = o0; o < o1; o++) {
+    const int o = o0 + t;
+    double v = 0.0;
+    if (o < o1) {
         const double* P = (mode == 1 ? d.P_new : d.P) + 3 * (size_t)d.opt[o];
         if (mode == 0)
-            s += d.terms[o].valid ? d.terms[o].cost : 0.0;
+            v = d.terms[o].valid ? d.terms[o].cost : 0.0;
         else if (mode == 1)
-            s += ba_new_cost_term(d.pc_new[d.okf[o]], P, d.ouv[2 * o], d.ouv[2 * o + 1], d.K);
+            v = ba_new_cost_term(d.pc_new[d.okf[o]], P, d.ouv[2 * o], d.ouv[2 * o + 1], d.K);
         else
-            s += ba_sq_err_term(d.pc[d.okf[o]], P, d.ouv[2 * o], d.ouv[2 * o + 1], d.K);
+            v = ba_sq_err_term(d.pc[d.okf[o]], P, d.ouv[2 * o], d.ouv[2 * o + 1], d.K);
     }
-    d.chunk[c] = s;
+    s_v[t] = v;
+    __syncthreads();
+    if (t == 0) {
+        double sum = 0;
+        for (int k = 0; k < o1 - o0; k++) sum += s_v[k];
+        d.chunk[c] = sum;
+    }
 }
 
-__global__ void k_ba_kf_acc(BaDev d) {
+// Hpp, bp per keyframe in gather order (:407-451), one 64-lane workgroup per keyframe: lane
+// l < 21 owns upper-triangular element l of Hpp (mirrored), lanes 21..26 own bp — each element is
+// the same sequential sum over the keyframe's observations as in the oracle.  The observation
+// indices are staged 64 at a time so the term loads do not wait on index loads.
+__global__ __launch_bounds__(64) void k_ba_kf_acc(BaDev d) {
     BA_LIVE(d);
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    __shared__ double s_t[64][15];  // per staged observation: Jp (12), ru_w, rv_w, valid
+    const int i = blockIdx.x, l = threadIdx.x;
     if (i >= d.N) return;
-    double H[36], b[6];
-    for (int k = 0; k < 36; k++) H[k] = 0;
-    for (int k = 0; k < 6; k++) b[k] = 0;
-    for (int q = d.kf_off[i]; q < d.kf_off[i + 1]; q++) {
-        const ObsTerms& ot = d.terms[d.kf_obs[q]];
-        if (ot.valid) ba_add_pose(ot, H, b);
+    int r = 0, c = 0;
+    if (l < 21) {
+        int k = l;
+        while (k >= 6 - r) {
+            k -= 6 - r;
+            r++;
+        }
+        c = r + k;
+    } else {
+        r = l - 21;
     }
-    for (int k = 0; k < 6; k++) H[k * 6 + k] += kPoseDamp;
-    for (int k = 0; k < 36; k++) d.Hpp[36 * i + k] = H[k];
-    for (int k = 0; k < 6; k++) d.bp[6 * i + k] = b[k];
+    double acc = 0;
+    const int q0 = d.kf_off[i], q1 = d.kf_off[i + 1];
+    for (int qb = q0; qb < q1; qb += 64) {
+        if (qb + l < q1) {
+            const ObsTerms& ot = d.terms[d.kf_obs[qb + l]];
+            for (int k = 0; k < 6; k++) {
+                s_t[l][k] = ot.Jp[0][k];
+                s_t[l][6 + k] = ot.Jp[1][k];
+            }
+            s_t[l][12] = ot.ru_w;
+            s_t[l][13] = ot.rv_w;
+            s_t[l][14] = ot.valid ? 1.0 : 0.0;
+        }
+        __syncthreads();
+        const int m = min(64, q1 - qb);
+        if (l < 27)
+            for (int k = 0; k < m; k++) {
+                if (s_t[k][14] == 0.0) continue;
+                if (l < 21)
+                    acc += s_t[k][r] * s_t[k][c] + s_t[k][6 + r] * s_t[k][6 + c];
+                else
+                    acc += s_t[k][r] * s_t[k][12] + s_t[k][6 + r] * s_t[k][13];
+            }
+        __syncthreads();
+    }
+    if (l < 21) {
+        if (r == c) acc += kPoseDamp;
+        d.Hpp[36 * i + r * 6 + c] = acc;
+        d.Hpp[36 * i + c * 6 + r] = acc;
+    } else if (l < 27) {
+        d.bp[6 * i + r] = acc;
+    }
 }
 
 __global__ void k_ba_pt_acc(BaDev d) {
@@ -135,86 +182,281 @@ __global__ void k_ba_pt_acc(BaDev d) {
         for (int s = 0; s < np; s++) ba_schur_u(d.Hpm + 18 * (size_t)(p0 + s), Hi, d.U + 18 * (size_t)(p0 + s));
 }
 
-// grid: N*N workgroups of 64 threads; threads 0..35 own S_ab(r, c), threads 36..41 own b_a(r) on
-// the diagonal workgroups
+// grid: N*N workgroups of 64 threads; threads 0..35 own S_ab(r, c), threads 0..5 then own b_a(r)
+// on the diagonal workgroups.  The (U, Hpm, point) index lists are staged 64 at a time in LDS so
+// the products' loads do not wait on index loads; sums run over the lists in order (the oracle's).
 __global__ __launch_bounds__(64) void k_ba_schur(BaDev d) {
     BA_LIVE(d);
+    __shared__ double s_U[64][18], s_H[64][18];
+    __shared__ int s_ok[64];
     const int a = blockIdx.x / d.N, b = blockIdx.x % d.N, t = threadIdx.x;
     const int n = 6 * d.N;
     const double lam = d.ctl->lambda;
+    const int r = t / 6, c = t % 6;
+    double s = 0.0;
     if (t < 36) {
-        const int r = t / 6, c = t % 6;
-        double s = a == b ? d.Hpp[36 * a + r * 6 + c] : 0.0;
+        s = a == b ? d.Hpp[36 * a + r * 6 + c] : 0.0;
         if (a == b && r == c) s *= (1.0 + lam);
-        const int pair = a * d.N + b;
-        for (int q = d.ab_off[pair]; q < d.ab_off[pair + 1]; q++) {
-            if (!d.pvalid[d.ab_j[q]]) continue;
-            s -= ba_schur_s(d.U + 18 * (size_t)d.ab_u[q], d.Hpm + 18 * (size_t)d.ab_h[q], r, c);
-        }
-        d.S[(size_t)(6 * a + r) * n + 6 * b + c] = s;
-    } else if (t < 42 && a == b) {
-        const int r = t - 36;
-        double s = d.bp[6 * a + r];
-        for (int q = d.kb_off[a]; q < d.kb_off[a + 1]; q++) {
-            const int j = d.kb_j[q];
-            if (!d.pvalid[j]) continue;
-            s -= ba_schur_b(d.U + 18 * (size_t)d.kb_u[q], d.bm + 3 * (size_t)j, r);
-        }
-        d.bs[6 * a + r] = s;
     }
+    const int pair = a * d.N + b;
+    const int q0 = d.ab_off[pair], q1 = d.ab_off[pair + 1];
+    for (int qb = q0; qb < q1; qb += 64) {
+        const int q = qb + t;
+        if (q < q1) {
+            const double* U = d.U + 18 * (size_t)d.ab_u[q];
+            const double* Hh = d.Hpm + 18 * (size_t)d.ab_h[q];
+            for (int k = 0; k < 18; k++) {
+                s_U[t][k] = U[k];
+                s_H[t][k] = Hh[k];
+            }
+            s_ok[t] = d.pvalid[d.ab_j[q]];
+        }
+        __syncthreads();
+        const int m = min(64, q1 - qb);
+        if (t < 36)
+            for (int k = 0; k < m; k++)
+                if (s_ok[k]) s -= ba_schur_s(s_U[k], s_H[k], r, c);
+        __syncthreads();
+    }
+    if (t < 36) d.S[(size_t)(6 * a + r) * n + 6 * b + c] = s;
+    if (a != b) return;
+    double sb = t < 6 ? d.bp[6 * a + t] : 0.0;
+    const int k0 = d.kb_off[a], k1 = d.kb_off[a + 1];
+    for (int qb = k0; qb < k1; qb += 64) {
+        const int q = qb + t;
+        if (q < k1) {
+            const int j = d.kb_j[q];
+            const double* U = d.U + 18 * (size_t)d.kb_u[q];
+            for (int k = 0; k < 18; k++) s_U[t][k] = U[k];
+            for (int k = 0; k < 3; k++) s_H[t][k] = d.bm[3 * (size_t)j + k];
+            s_ok[t] = d.pvalid[j];
+        }
+        __syncthreads();
+        const int m = min(64, k1 - qb);
+        if (t < 6)
+            for (int k = 0; k < m; k++)
+                if (s_ok[k]) sb -= ba_schur_b(s_U[k], s_H[k], t);
+        __syncthreads();
+    }
+    if (t < 6) d.bs[6 * a + t] = sb;
 }
 
-// right-looking Cholesky of S (lower triangle) and S dp = -bs; order per element as the oracle
+// Right-looking Cholesky of S (lower triangle) and S dp = -bs, blocked, one workgroup:
+//   * 32-column panels staged in LDS; one thread per panel row; per column every thread takes
+//     the pivot sqrt itself and divides the column entries it needs on the fly, so one barrier
+//     per column suffices (the divided column is stored one step later, when nothing reads it);
+//   * the trailing lower triangle is updated by all waves in 4 x 4 register tiles;
+//   * both triangular solves are blocked the same way: the rows below (above) a finished block
+//     take that block's contributions in parallel, the 32 x 32 diagonal block is solved by one
+//     wave out of LDS.
+// Every element still receives its updates in the order of the oracle's sequential chol_solve
+// (orc_ba.cpp: ascending k for the factor and the forward solve, descending k for the backward
+// solve), so the factor and the solution are bit-identical.
+constexpr int kCholNB = 32;
+constexpr int kCholLd = kCholNB + 1;  // LDS row stride: rows one thread apart fall in different banks
+constexpr int kCholMaxN = 6 * VS_BA_MAX_KEYFRAMES;
+
+#ifdef VS_BA_PROFILE
+// phase cycle counters of k_ba_chol (profiling build only: make -C visual-slam-pipeline_amd prof)
+__device__ unsigned long long g_ba_cycles[8];
+#define BA_T0() long long _ba_t = clock64()
+#define BA_T(k)                                                               \
+    do {                                                                      \
+        if (threadIdx.x == 0) atomicAdd(&g_ba_cycles[k], clock64() - _ba_t);  \
+        _ba_t = clock64();                                                    \
+    } while (0)
+#else
+#define BA_T0()
+#define BA_T(k)
+#endif
+
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 __global__ __launch_bounds__(1024) void k_ba_chol(BaDev d) {
     BA_LIVE(d);
-    const int n = 6 * d.N, tid = threadIdx.x, nt = blockDim.x;
+    const int n = 6 * d.N, tid = threadIdx.x, nt = blockDim.x, lane = tid & 63;
     double* S = d.S;
-    double* x = d.dp;
+    __shared__ double Pn[kCholMaxN * kCholLd];  // panel rows K0..n-1 x columns K0..K0+nb-1
+    __shared__ double xs[kCholMaxN];
+    __shared__ double Db[kCholNB * kCholLd];  // diagonal block for the solves
+    __shared__ double Lc[kCholMaxN];           // the divided panel column of the current step
+    __shared__ double s_piv;
     __shared__ int bad;
-    __shared__ double piv;
     if (tid == 0) bad = 0;
-    for (int i = tid; i < n; i += nt) x[i] = -d.bs[i];
     __syncthreads();
-    for (int k = 0; k < n; k++) {
-        if (tid == 0) {
-            const double v = S[(size_t)k * n + k];
-            if (!(v > 0)) bad = 1;
-            piv = sqrt(v);
-            S[(size_t)k * n + k] = piv;
+    BA_T0();
+    for (int K0 = 0; K0 < n; K0 += kCholNB) {
+        const int nb = min(kCholNB, n - K0), rows = n - K0;
+        for (int e = tid; e < rows * nb; e += nt) {
+            const int r = e / nb, c = e % nb;
+            Pn[r * kCholLd + c] = S[(size_t)(K0 + r) * n + K0 + c];
         }
         __syncthreads();
+        BA_T(0);
+        // panel: thread r owns row r, held in registers (columns unrolled).  Step kk: the owner of
+        // row kk publishes the pivot sqrt; every row below divides its column-kk entry once and
+        // publishes it in Lc; then each row applies column kk to its columns kk+1.. .
+        double prow[kCholNB];
+        const bool own = tid < rows;
+#pragma unroll
+        for (int c = 0; c < kCholNB; c++) prow[c] = (own && c < nb) ? Pn[tid * kCholLd + c] : 0.0;
+        bool stop = false;
+#pragma unroll
+        for (int kk = 0; kk < kCholNB; kk++) {
+            if (kk < nb && !stop) {
+                if (tid == kk) {
+                    const double v = prow[kk];
+                    if (!(v > 0)) bad = 1;
+                    s_piv = sqrt(v);
+                    prow[kk] = s_piv;
+                }
+                __syncthreads();
+                stop = bad != 0;
+                if (!stop) {
+                    const double piv = s_piv;
+                    double lrk = 0.0;
+                    if (own && tid > kk) {
+                        lrk = prow[kk] / piv;
+                        prow[kk] = lrk;
+                        Lc[tid] = lrk;
+                    }
+                    __syncthreads();
+                    if (own && tid > kk) {
+#pragma unroll
+                        for (int c = kk + 1; c < kCholNB; c++)
+                            if (c < nb && c <= tid) prow[c] -= lrk * Lc[c];
+                    }
+                }
+            }
+        }
+        __syncthreads();
+        if (own && !bad)
+#pragma unroll
+            for (int c = 0; c < kCholNB; c++)
+                if (c < nb && c <= tid) Pn[tid * kCholLd + c] = prow[c];
+        __syncthreads();
+        BA_T(1);
         if (bad) break;
-        for (int i = k + 1 + tid; i < n; i += nt) S[(size_t)i * n + k] /= piv;
-        __syncthreads();
-        const int m = n - k - 1;  // trailing lower triangle, rows i = k+1.., cols j = k+1..i
-        const long tot = (long)m * (m + 1) / 2;
-        for (long e = tid; e < tot; e += nt) {
-            // e -> (ii, jj) with 0 <= jj <= ii < m
-            int ii = (int)((sqrt(8.0 * (double)e + 1.0) - 1.0) * 0.5);
-            while ((long)ii * (ii + 1) / 2 > e) ii--;
-            while ((long)(ii + 1) * (ii + 2) / 2 <= e) ii++;
-            const int jj = (int)(e - (long)ii * (ii + 1) / 2);
-            const int i = k + 1 + ii, j = k + 1 + jj;
-            S[(size_t)i * n + j] -= S[(size_t)i * n + k] * S[(size_t)j * n + k];
+        for (int e = tid; e < rows * nb; e += nt) {  // the factored L columns
+            const int r = e / nb, c = e % nb;
+            if (c <= r) S[(size_t)(K0 + r) * n + K0 + c] = Pn[r * kCholLd + c];
+        }
+        // trailing lower triangle (rows / columns K0 + nb ..), 4 x 4 tiles on or below the diagonal
+        const int base = nb, m = rows - nb;
+        const int mt = (m + 3) / 4;
+        const long tiles = (long)mt * (mt + 1) / 2;
+        for (long t = tid; t < tiles; t += nt) {
+            int ti = (int)((sqrt(8.0 * (double)t + 1.0) - 1.0) * 0.5);
+            while ((long)ti * (ti + 1) / 2 > t) ti--;
+            while ((long)(ti + 1) * (ti + 2) / 2 <= t) ti++;
+            const int tj = (int)(t - (long)ti * (ti + 1) / 2);
+            double acc[4][4];
+            int ri[4], cj[4];
+#pragma unroll
+            for (int x = 0; x < 4; x++) {
+                ri[x] = base + 4 * ti + x;
+                cj[x] = base + 4 * tj + x;
+            }
+#pragma unroll
+            for (int x = 0; x < 4; x++)
+#pragma unroll
+                for (int y = 0; y < 4; y++)
+                    acc[x][y] = (ri[x] < rows && cj[y] <= ri[x]) ? S[(size_t)(K0 + ri[x]) * n + K0 + cj[y]] : 0.0;
+            for (int kk = 0; kk < nb; kk++) {
+                double a[4], b[4];
+#pragma unroll
+                for (int x = 0; x < 4; x++) {
+                    a[x] = ri[x] < rows ? Pn[ri[x] * kCholLd + kk] : 0.0;
+                    b[x] = cj[x] < rows ? Pn[cj[x] * kCholLd + kk] : 0.0;
+                }
+#pragma unroll
+                for (int x = 0; x < 4; x++)
+#pragma unroll
+                    for (int y = 0; y < 4; y++) acc[x][y] -= a[x] * b[y];
+            }
+#pragma unroll
+            for (int x = 0; x < 4; x++)
+#pragma unroll
+                for (int y = 0; y < 4; y++)
+                    if (ri[x] < rows && cj[y] <= ri[x]) S[(size_t)(K0 + ri[x]) * n + K0 + cj[y]] = acc[x][y];
         }
         __syncthreads();
+        BA_T(2);
     }
     if (bad) {
         if (tid == 0) d.ctl->solved = 0;
         return;
     }
-    for (int k = 0; k < n; k++) {  // L y = b
-        if (tid == 0) x[k] /= S[(size_t)k * n + k];
+    // L y = -bs: block by block; y[i] = (b[i] - sum_{k < i} L[i][k] y[k]) / L[i][i], the sum in
+    // ascending k (the oracle's column sweep applies the same subtractions in the same order)
+    for (int i = tid; i < n; i += nt) xs[i] = -d.bs[i];
+    __syncthreads();
+    for (int K0 = 0; K0 < n; K0 += kCholNB) {
+        const int nb = min(kCholNB, n - K0);
+        for (int e = tid; e < nb * nb; e += nt) Db[(e / nb) * kCholLd + e % nb] = S[(size_t)(K0 + e / nb) * n + K0 + e % nb];
         __syncthreads();
-        for (int i = k + 1 + tid; i < n; i += nt) x[i] -= S[(size_t)i * n + k] * x[k];
+        if (tid < 64) {  // lane i holds x[K0 + i] and row i of the diagonal block
+            double x = lane < nb ? xs[K0 + lane] : 0.0;
+            double drow[kCholNB];
+#pragma unroll
+            for (int j = 0; j < kCholNB; j++) drow[j] = (lane < nb && j <= lane && j < nb) ? Db[lane * kCholLd + j] : 1.0;
+#pragma unroll
+            for (int k = 0; k < kCholNB; k++) {
+                if (k < nb) {
+                    const double q = x / drow[k];  // lane k: x[k] /= L[k][k]
+                    if (lane == k) x = q;
+                    const double xk = __shfl(q, k);
+                    if (lane > k && lane < nb) x -= drow[k] * xk;
+                }
+            }
+            if (lane < nb) xs[K0 + lane] = x;
+        }
+        __syncthreads();
+        for (int i = K0 + nb + tid; i < n; i += nt) {  // rows below take this block, ascending k
+            double s = xs[i];
+            const double* Li = S + (size_t)i * n + K0;
+            for (int k = 0; k < nb; k++) s -= Li[k] * xs[K0 + k];
+            xs[i] = s;
+        }
         __syncthreads();
     }
-    for (int k = n - 1; k >= 0; k--) {  // L^T x = y
-        if (tid == 0) x[k] /= S[(size_t)k * n + k];
+    BA_T(3);
+    // L^T x = y: blocks from the last; rows above take a finished block in descending k
+    const int nblk = (n + kCholNB - 1) / kCholNB;
+    for (int bI = nblk - 1; bI >= 0; bI--) {
+        const int K0 = bI * kCholNB, nb = min(kCholNB, n - K0);
+        for (int e = tid; e < nb * nb; e += nt) Db[(e / nb) * kCholLd + e % nb] = S[(size_t)(K0 + e / nb) * n + K0 + e % nb];
         __syncthreads();
-        for (int i = tid; i < k; i += nt) x[i] -= S[(size_t)k * n + i] * x[k];
+        if (tid < 64) {  // lane i holds x[K0 + i] and column i of the diagonal block
+            double x = lane < nb ? xs[K0 + lane] : 0.0;
+            double dcol[kCholNB];
+#pragma unroll
+            for (int j = 0; j < kCholNB; j++) dcol[j] = (lane < nb && j >= lane && j < nb) ? Db[j * kCholLd + lane] : 1.0;
+#pragma unroll
+            for (int kq = kCholNB - 1; kq >= 0; kq--) {
+                if (kq < nb) {
+                    const double q = x / dcol[kq];  // lane kq: x[kq] /= L[kq][kq]
+                    if (lane == kq) x = q;
+                    const double xk = __shfl(q, kq);
+                    if (lane < kq) x -= dcol[kq] * xk;
+                }
+            }
+            if (lane < nb) xs[K0 + lane] = x;
+        }
+        __syncthreads();
+        for (int i = tid; i < K0; i += nt) {
+            double s = xs[i];
+            for (int k = nb - 1; k >= 0; k--) s -= S[(size_t)(K0 + k) * n + i] * xs[K0 + k];
+            xs[i] = s;
+        }
         __syncthreads();
     }
+    BA_T(4);
+    for (int i = tid; i < n; i += nt) d.dp[i] = xs[i];
     if (tid == 0) d.ctl->solved = 1;
 }
 
@@ -483,25 +725,25 @@ int local_ba(vs_ctx* ctx, int N, double* R, double* t, int M, double* P, int n_o
         const int T = 256;
         hipLaunchKernelGGL(k_ba_init, dim3(cdiv(N, T)), dim3(T), 0, s, d, (const double*)(base + o_R));
         hipLaunchKernelGGL(k_ba_pose_cache, dim3(cdiv(N, T)), dim3(T), 0, s, d, 0, 0);
-        hipLaunchKernelGGL(k_ba_chunk_sums, dim3(cdiv(n_chunks, T)), dim3(T), 0, s, d, 2, 0);
+        hipLaunchKernelGGL(k_ba_chunk_sums, dim3(n_chunks), dim3(kCostChunk), 0, s, d, 2, 0);
         hipLaunchKernelGGL(k_ba_control, dim3(1), dim3(1), 0, s, d, 2);
         for (int it = 0; it < max_iter; it++) {
             hipLaunchKernelGGL(k_ba_pose_cache, dim3(cdiv(N, T)), dim3(T), 0, s, d, 0, 1);
             hipLaunchKernelGGL(k_ba_obs, dim3(cdiv(n_obs, T)), dim3(T), 0, s, d);
-            hipLaunchKernelGGL(k_ba_chunk_sums, dim3(cdiv(n_chunks, T)), dim3(T), 0, s, d, 0, 1);
+            hipLaunchKernelGGL(k_ba_chunk_sums, dim3(n_chunks), dim3(kCostChunk), 0, s, d, 0, 1);
             hipLaunchKernelGGL(k_ba_control, dim3(1), dim3(1), 0, s, d, 0);
-            hipLaunchKernelGGL(k_ba_kf_acc, dim3(cdiv(N, 64)), dim3(64), 0, s, d);
+            hipLaunchKernelGGL(k_ba_kf_acc, dim3(N), dim3(64), 0, s, d);
             hipLaunchKernelGGL(k_ba_pt_acc, dim3(cdiv(M, T)), dim3(T), 0, s, d);
             hipLaunchKernelGGL(k_ba_schur, dim3(N * N), dim3(64), 0, s, d);
             hipLaunchKernelGGL(k_ba_chol, dim3(1), dim3(1024), 0, s, d);
             hipLaunchKernelGGL(k_ba_update, dim3(cdiv(M + N, T)), dim3(T), 0, s, d);
             hipLaunchKernelGGL(k_ba_pose_cache, dim3(cdiv(N, T)), dim3(T), 0, s, d, 1, 1);
-            hipLaunchKernelGGL(k_ba_chunk_sums, dim3(cdiv(n_chunks, T)), dim3(T), 0, s, d, 1, 1);
+            hipLaunchKernelGGL(k_ba_chunk_sums, dim3(n_chunks), dim3(kCostChunk), 0, s, d, 1, 1);
             hipLaunchKernelGGL(k_ba_control, dim3(1), dim3(1), 0, s, d, 1);
             hipLaunchKernelGGL(k_ba_commit, dim3(cdiv(3 * M + 3 * N, T)), dim3(T), 0, s, d);
         }
         hipLaunchKernelGGL(k_ba_pose_cache, dim3(cdiv(N, T)), dim3(T), 0, s, d, 0, 0);
-        hipLaunchKernelGGL(k_ba_chunk_sums, dim3(cdiv(n_chunks, T)), dim3(T), 0, s, d, 2, 0);
+        hipLaunchKernelGGL(k_ba_chunk_sums, dim3(n_chunks), dim3(kCostChunk), 0, s, d, 2, 0);
         hipLaunchKernelGGL(k_ba_control, dim3(1), dim3(1), 0, s, d, 3);
         hipLaunchKernelGGL(k_ba_finish, dim3(cdiv(3 * M + N, T)), dim3(T), 0, s, d, (double*)(base + o_R),
                            (double*)(base + o_t), (double*)(base + o_Pn));
@@ -524,3 +766,14 @@ int local_ba(vs_ctx* ctx, int N, double* R, double* t, int M, double* P, int n_o
 }
 
 }  // namespace vs
+
+#ifdef VS_BA_PROFILE
+extern "C" int vs_debug_ba_cycles(unsigned long long* out, int reset) {
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(vs::g_ba_cycles), sizeof(unsigned long long) * 8) != hipSuccess) return -1;
+    if (reset) {
+        unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(vs::g_ba_cycles), z, sizeof(z)) != hipSuccess) return -1;
+    }
+    return 0;
+}
+#endif

@@ -73,16 +73,27 @@ __global__ void k_pnp_subsets(const int* __restrict__ off, int niters0, int min_
     if (!pnp_problem_runs(n, min_inliers, model_points)) return;
     CvRng rng((uint64_t)-1);
     for (int it = 0; it < niters0; it++) {
-        int idx[5];  // drawn in registers, stored once
-        for (int i = 0; i < model_points; i++)
-            for (;;) {
-                idx[i] = rng.uniform(0, n);
-                int j = 0;
-                while (j < i && idx[j] != idx[i]) j++;
-                if (j == i) break;
-            }
+        // getSubset's repeat rejection, unrolled so the subset stays in registers (a runtime
+        // index into a private array would live in scratch memory)
+        int idx[5] = {0, 0, 0, 0, 0};
+#pragma unroll
+        for (int i = 0; i < 5; i++) {
+            if (i < model_points)
+                for (;;) {
+                    const int v = rng.uniform(0, n);
+                    bool dup = false;
+#pragma unroll
+                    for (int j = 0; j < i; j++) dup |= idx[j] == v;
+                    if (!dup) {
+                        idx[i] = v;
+                        break;
+                    }
+                }
+        }
         int* dst = H.subset + ((size_t)pb * H.stride + it) * 5;
-        for (int i = 0; i < model_points; i++) dst[i] = idx[i];
+#pragma unroll
+        for (int i = 0; i < 5; i++)
+            if (i < model_points) dst[i] = idx[i];
     }
 }
 
