@@ -1,0 +1,201 @@
+"""Generate the committed golden fixtures (tests/golden/*.npz) for the per-frame hot path.
+
+The reference ships no tests, fixtures or golden vectors and cannot be built here (OpenCV, ONNX
+Runtime and g2o are absent), so these fixtures are NOT reference outputs.  They pin two things:
+
+  * known answers: every noise-free case below is checked at generation time against the ground
+    truth it was built from (the pose / fundamental matrix / map association is recovered), so a
+    fixture cannot silently record a wrong oracle;
+  * regressions: the oracle's outputs (oracle/, the CPU restatement of the reference, itself test
+    infrastructure) on seeded inputs, so the HIP path is checked against fixed vectors that do not
+    move when the oracle is edited.
+
+tests/test_golden.py replays every fixture through the oracle (CPU suite) and through
+libvslam_hip.so (GPU suite).  Run from the repo root:  python tests/golden/make_golden.py
+All files are plain npz (no pickled objects; structured keypoint / match records are numpy
+structured dtypes)."""
+import os
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+for p in (os.path.join(ROOT, "oracle"), os.path.join(ROOT, "tests")):
+    sys.path.insert(0, p)
+
+import oracle_py as oracle  # noqa: E402
+import restate  # noqa: E402
+
+
+def _rot_angle(Ra, Rb):
+    c = (np.trace(Ra.T @ Rb) - 1) / 2
+    return float(np.arccos(np.clip(c, -1.0, 1.0)))
+
+
+def _sparse(depth):
+    idx = np.flatnonzero(depth).astype(np.int32)
+    return idx, depth.reshape(-1)[idx].astype(np.float32)
+
+
+def _kps(kxy):
+    k = np.zeros(len(kxy), oracle.KEYPOINT_DTYPE)
+    k["x"], k["y"], k["size"], k["angle"], k["class_id"] = kxy[:, 0], kxy[:, 1], 8.0, -1.0, -1
+    return k
+
+
+def gen_postprocess():
+    """Slam feature extraction post-processing (FeatureExtractor.cpp decode / NMS / sampling) on a
+    random 8x12-cell grid with planted peaks, plateaus (exact ties) and a below-threshold field."""
+    rng = np.random.default_rng(101)
+    hc, wc = 8, 12
+    semi = rng.normal(size=(65, hc, wc)).astype(np.float32) * 2.0
+    semi[rng.integers(0, 64, 10), rng.integers(0, hc, 10), rng.integers(0, wc, 10)] = 9.0
+    semi[5, 3, 3] = semi[6, 3, 4] = 7.5  # tie
+    semi[:, 6:, :2] = -8.0               # dust-dominated cells: no keypoint
+    dgrid = rng.normal(size=(256, hc, wc)).astype(np.float32)
+    kps, desc = oracle.postprocess(semi, dgrid, max_kp=60)
+    assert 20 < len(kps) <= 60
+    return dict(semi=semi, dgrid=dgrid, max_kp=np.int32(60), kps=kps, desc=desc)
+
+
+def gen_match():
+    """Slam::match_features (Slam.cpp:367-378): exact 2-NN + ratio 0.75.  Half the queries have a
+    planted near-duplicate in the train set; one exact duplicate train row makes a tie."""
+    rng = np.random.default_rng(102)
+    d2 = rng.normal(size=(90, 256)).astype(np.float32)
+    d2 /= np.linalg.norm(d2, axis=1, keepdims=True)
+    d2[17] = d2[16]
+    src = rng.integers(0, 90, 35)
+    d1 = np.concatenate([d2[src] + rng.normal(size=(35, 256)).astype(np.float32) * 0.02,
+                         rng.normal(size=(35, 256)).astype(np.float32)])
+    d1 /= np.linalg.norm(d1, axis=1, keepdims=True)
+    d1 = d1.astype(np.float32)
+    raw, good = oracle.match_ratio(d1, d2)
+    # known answer: every planted pair whose source is not the duplicated row is a good match
+    gq = dict(zip(good["query_idx"], good["train_idx"]))
+    for q, s in enumerate(src):
+        if s not in (16, 17):
+            assert gq.get(q) == s
+    return dict(d1=d1, d2=d2, raw=raw, good=good)
+
+
+def gen_ransac3d():
+    """Slam::estimate_motion_3d3d (Slam.cpp:209-299): RANSAC over depth-backprojected pairs."""
+    out = {}
+    for tag, (n, of, seed, noise) in {"clean": (80, 0.0, 103, 0.0), "outl": (120, 0.35, 104, 0.003)}.items():
+        p1, p2, d1, d2, R, t, inl = restate.rigid_scene(n, of, seed, noise=noise)
+        ok, Ro, to, diag = oracle.ransac_3d3d(p1, p2, d1, d2)
+        assert ok
+        if noise == 0.0:
+            assert _rot_angle(Ro, R) < 1e-4 and np.max(np.abs(to - t)) < 1e-3
+        i1, v1 = _sparse(d1)
+        i2, v2 = _sparse(d2)
+        out.update({f"{tag}_p1": p1, f"{tag}_p2": p2, f"{tag}_d1i": i1, f"{tag}_d1v": v1, f"{tag}_d2i": i2,
+                    f"{tag}_d2v": v2, f"{tag}_ok": np.int32(ok), f"{tag}_R": Ro, f"{tag}_t": to, f"{tag}_diag": diag,
+                    f"{tag}_Rtrue": R, f"{tag}_ttrue": t})
+    return out
+
+
+def gen_fmat():
+    """cv::findFundamentalMat(FM_RANSAC, 3.0, 0.999) as Slam.cpp:880-910 calls it."""
+    from test_oracle_fmat import two_view
+    out = {}
+    for tag, (n, seed, noise, of) in {"clean": (60, 105, 0.0, 0.0), "outl": (150, 106, 0.5, 0.3)}.items():
+        p1, p2, F, outl = two_view(n, seed, noise, of)
+        ok, Fo, mask, diag = oracle.find_fundamental(p1, p2)
+        assert ok
+        if noise == 0.0:
+            assert oracle.epipolar_error(p1, p2, Fo) < 1e-3
+        out.update({f"{tag}_p1": p1, f"{tag}_p2": p2, f"{tag}_F": Fo, f"{tag}_mask": mask.astype(np.uint8),
+                    f"{tag}_diag": diag})
+    return out
+
+
+def gen_emat():
+    """Slam::estimate_motion (Slam.cpp:1193-1213) + estimate_scale_from_depth (Slam.cpp:73-207)."""
+    from test_oracle_emat import _depth_maps, two_view
+    out = {}
+    for tag, (n, seed, noise, of) in {"clean": (60, 107, 0.0, 0.0), "outl": (150, 108, 0.4, 0.3)}.items():
+        p1, p2, R, t, X, outl = two_view(n, seed, noise=noise, outlier_frac=of)
+        d1, d2 = _depth_maps(X, R, t, p1, p2)
+        ok_e, E, emask, fdiag = oracle.find_essential(p1, p2)
+        ok, Ro, to, mask, inl, good = oracle.estimate_motion(p1, p2)
+        assert ok
+        sc = oracle.estimate_scale(p1, p2, Ro, to, d1, d2)
+        if noise == 0.0:
+            assert _rot_angle(Ro, R) < 1e-6 and abs(sc * np.linalg.norm(to) - np.linalg.norm(t)) < 0.02
+        i1, v1 = _sparse(d1)
+        i2, v2 = _sparse(d2)
+        out.update({f"{tag}_p1": p1, f"{tag}_p2": p2, f"{tag}_d1i": i1, f"{tag}_d1v": v1, f"{tag}_d2i": i2,
+                    f"{tag}_d2v": v2, f"{tag}_R": Ro, f"{tag}_t": to, f"{tag}_scale": np.float64(sc),
+                    f"{tag}_fdiag": fdiag, f"{tag}_inl": np.int32(inl), f"{tag}_good": np.int32(good)})
+    return out
+
+
+def gen_pnp():
+    """Slam::solve_pnp (Slam.cpp:505-529): solvePnPRansac(EPnP) + LM refinement, world pose."""
+    from test_oracle_pnp import pnp_problem
+    out = {}
+    for tag, (n, seed, noise, of) in {"clean": (50, 109, 0.0, 0.0), "outl": (200, 110, 0.7, 0.4)}.items():
+        obj, img, R, t, outl = pnp_problem(n, seed, noise=noise, outlier_frac=of)
+        ok_r, rv, tv, inl_r, mask, diag = oracle.pnp_ransac(obj, img, 100)
+        succ, Rw, tw, cnt = oracle.solve_pnp(obj, img, 100, 10)
+        assert succ
+        if noise == 0.0:
+            assert _rot_angle(Rw, R.T) < 2e-6
+        out.update({f"{tag}_obj": obj, f"{tag}_img": img, f"{tag}_R": Rw, f"{tag}_t": tw, f"{tag}_cnt": np.int32(cnt),
+                    f"{tag}_mask": mask.astype(np.uint8), f"{tag}_diag": diag})
+    return out
+
+
+def gen_tlm():
+    """Slam::track_local_map (Slam.cpp:380-469): projection, 3x3-cell keypoint grid, distance gate,
+    per-keypoint resolution; a prior association on some keypoints."""
+    kxy, desc, pos, mdesc, valid, R, t = restate.synthetic_tracking_problem(80, 400, 111)
+    kps = _kps(kxy)
+    prior = np.full(80, -1, np.int32)
+    prior[::7] = 1000 + np.arange(len(prior[::7]), dtype=np.int32)
+    # known answer: without a prior, the independent pure-Python restatement agrees exactly
+    n0, kpmp0, om0, ok0 = oracle.track_local_map(pos, mdesc, valid, kps, desc, R, t)
+    py_n, py_kpmp, py_obs = restate.track_local_map_py(pos, mdesc, valid, kxy, desc, R, t)
+    assert n0 == py_n > 0 and np.array_equal(kpmp0, py_kpmp)
+    assert [tuple(o) for o in zip(om0, ok0)] == [tuple(o) for o in py_obs]
+    tracked, kpmp, obs_mp, obs_kp = oracle.track_local_map(pos, mdesc, valid, kps, desc, R, t, kp_to_mp=prior)
+    return dict(kps=kps, desc=desc, pos=pos, mdesc=mdesc, valid=valid, R=R, t=t, prior=prior,
+                tracked=np.int32(tracked), kpmp=kpmp, obs_mp=obs_mp, obs_kp=obs_kp)
+
+
+def gen_pose():
+    """Optimizer::optimize_pose (Optimizer.cpp:36-185): Gauss-Newton/LM with the Huber kernel."""
+    from test_oracle_tracking import pose_problem
+    P, uv, R, t, R0, t0 = pose_problem(300, 112, noise=0.5)
+    Ro, to, eb, ea, _ = oracle.optimize_pose(P, uv, R0, t0)
+    assert ea < eb and _rot_angle(Ro, R) < 2e-3
+    return dict(P=P, uv=uv, R0=R0, t0=t0, R=Ro, t=to, err=np.array([eb, ea]))
+
+
+def gen_ba():
+    """Optimizer::local_bundle_adjustment (Optimizer.cpp:187-599): Schur complement + Cholesky LM."""
+    from test_oracle_ba import ba_problem
+    R, t, P, P0, kf, pt, uv = ba_problem(N=6, M=150, seed=113, noise=0.5, pert=0.05, outliers=4)
+    Ro, to, Po, eb, ea, stats = oracle.local_ba(R, t, P0, kf, pt, uv)
+    assert ea < eb
+    return dict(R_in=np.asarray(R, np.float64), t_in=np.asarray(t, np.float64), P_in=P0, kf=kf, pt=pt, uv=uv,
+                R=Ro, t=to, P=Po, err=np.array([eb, ea]), stats=stats)
+
+
+GENERATORS = dict(postprocess=gen_postprocess, match=gen_match, ransac3d=gen_ransac3d, fmat=gen_fmat, emat=gen_emat,
+                  pnp=gen_pnp, tlm=gen_tlm, pose=gen_pose, ba=gen_ba)
+
+
+def main():
+    oracle.lib()
+    for name, fn in GENERATORS.items():
+        path = os.path.join(HERE, f"{name}.npz")
+        np.savez_compressed(path, **fn())
+        print(f"{name:12s} {os.path.getsize(path) / 1024:7.1f} KiB")
+
+
+if __name__ == "__main__":
+    main()
