@@ -306,7 +306,8 @@ int vs_slam_trajectory(vs_slam* slam, int cap, int* ids, double* timestamps, dou
 /* {processed, rejected (< 30 keypoints), via 3D-3D, via E-matrix, E failed, bridge keyframes,
  *  PnP recoveries, recoveries failed, stationary, keyframes, PnP refinements, periodic PnP,
  *  tracked map points (sum), triangulated points, depth points, culled points, chains recomputed,
- *  map points, valid map points, frame_count_, keyframe_count_, last match count, 0, 0} */
+ *  map points, valid map points, frame_count_, keyframe_count_, last match count,
+ *  F-RANSAC iterations (sum over chains), 0} */
 int vs_slam_stats(vs_slam* slam, int* out, int cap);
 /* Map points (Map::map_points): *n = count; the first cap positions (world, x 3) and validity
  * bytes are written (each nullable). */

@@ -21,6 +21,7 @@ MATCH_DTYPE = np.dtype([("query_idx", "<i4"), ("train_idx", "<i4"), ("img_idx", 
 _P = ctypes.c_void_p
 _I = ctypes.c_int
 _SIG = {
+    "orc_mwc_jump": (ctypes.c_uint64, [ctypes.c_uint64, _I]),
     "orc_bgr_to_gray": (None, [_P, _I, _I, ctypes.c_size_t, _P]),
     "orc_gray_to_f32": (None, [_P, _I, _I, _P]),
     "orc_superpoint_num_params": (ctypes.c_size_t, []),
@@ -384,6 +385,10 @@ def estimate_scale(p1, p2, R, t, depth1, depth2=None, K=_K):
                                     _p(np.ascontiguousarray(t, np.float64)), _p(d1),
                                     None if d2 is None else _p(d2), d1.shape[0], d1.shape[1],
                                     _p(np.asarray(K, np.float64)))
+
+
+def mwc_jump(s, k):
+    return int(lib().orc_mwc_jump(ctypes.c_uint64(s), k))
 
 
 def mt19937(seed, count):

@@ -186,3 +186,9 @@ extern "C" int orc_fmat_verify(const orc_keypoint* kp_ref, const orc_keypoint* k
     if (m > 0) err[1] = orc_epipolar_error(q1.data(), q2.data(), m, F);  // :903-905
     return m;
 }
+
+extern "C" uint64_t orc_mwc_jump(uint64_t s, int k) {
+    uint64_t pk = vs_pnp::kMwcR1;  // Mont(A^0)
+    for (int i = 0; i < k; i++) pk = vs_pnp::mwc_step(pk);
+    return vs_pnp::mwc_jump(s, k, pk);
+}

@@ -81,6 +81,7 @@ struct OracleOps {
                                       reinterpret_cast<const orc_match*>(R.good.data()), n, F, keep.data(), err, diag,
                                       &f_ok);
         R.f_ok = f_ok != 0;
+        R.f_iters = diag[1];
         R.epi_before = err[0];
         R.epi_after = err[1];
         for (int i = 0; i < m; i++) R.kept.push_back(R.good[keep[i]]);
@@ -258,7 +259,7 @@ void orc_slam_stats(void* h, int* out) {
                        S.bridges,     S.recoveries,   S.recovery_failed, S.stationary,   S.keyframes,
                        S.pnp_refined, S.periodic_pnp, S.tracked_total, S.triangulated,   S.depth_points,
                        S.culled,      S.chains_discarded, m.size(),   valid,             s->trk.frame_count(),
-                       s->trk.keyframe_count(), s->trk.last_match_count(), 0, 0};
+                       s->trk.keyframe_count(), s->trk.last_match_count(), S.f_iters, 0};
     std::memcpy(out, v, sizeof(v));
 }
 

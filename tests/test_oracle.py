@@ -21,6 +21,24 @@ def test_mt19937_known_answer(oracle):
     assert int(oracle.mt19937(5489, 10000)[-1]) == 4123659995
 
 
+def _mwc_steps(s, k):
+    for _ in range(k):
+        s = ((s & 0xFFFFFFFF) * 4164903690 + (s >> 32)) & 0xFFFFFFFFFFFFFFFF
+    return s
+
+
+def test_cv_rng_jump_ahead_equals_stepping(oracle):
+    """The device draws cv::RNG states out of order as s * A^k mod (A 2^32 - 1) (pnp_solvers.h);
+    every jump must equal plain sequential stepping of the multiply-with-carry generator."""
+    s1 = _mwc_steps(2 ** 64 - 1, 1)  # cv::RNG((uint64)-1) after its first draw
+    rng = np.random.default_rng(7)
+    starts = [s1, _mwc_steps(s1, 12345), 1, 2 ** 32, (4164903690 << 32) - 2]
+    starts += [int(v) for v in rng.integers(1, 2 ** 62, 5)]
+    for s in starts:
+        for k in (0, 1, 2, 63, 64, 65, 1000, 1919, 5000):
+            assert oracle.mwc_jump(s, k) == _mwc_steps(s, k), (s, k)
+
+
 def _random_semi(rng, hc, wc, scale=4.0):
     return (rng.standard_normal((65, hc, wc)) * scale).astype(np.float32)
 

@@ -1,0 +1,60 @@
+"""Phase breakdown of the F-matrix kernel inside the tracking loop (profiling build
+libvslam_hip_prof.so: `make -C visual-slam-pipeline_amd prof`).  Runs the closed-loop synthetic
+sequence through vs_slam like tools/bench_tracker.py and prints k_fmat's lane-0 clock64 phase
+cycles per launch (phases as tools/profile_fmat_phases.py)."""
+import ctypes
+import json
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "visual-slam-pipeline_amd", "python"))
+
+
+def main():
+    import torch
+
+    import synth
+    import vslam_abi as va
+    lib = va.load_library(os.path.join(ROOT, "visual-slam-pipeline_amd", "libvslam_hip_prof.so"))
+    lib.vs_debug_fm_cycles.argtypes = [ctypes.c_void_p, ctypes.c_int]
+    U, B, steps = 126, 32, 4
+    L = synth.loop_sequence(U)
+    dev = torch.device("cuda", 0)
+    wrap = np.concatenate([np.arange(U), np.arange(B)])
+    bgr = torch.from_numpy(L["bgr"][wrap]).to(dev)
+    dep = torch.from_numpy(L["depth"][wrap]).to(dev)
+    hdep = [L["depth"][i] for i in wrap]
+    ctx = va.Context(0)
+    S = va.Slam(ctx, max_batch=B)
+
+    def step(k):
+        g0 = k * B
+        i0 = g0 % U
+        return S.process_batch_dev(B, bgr[i0].data_ptr(), dep[i0].data_ptr(), hdep[i0:i0 + B],
+                                   [1311868164.0 + 0.1 * (g0 + j) for j in range(B)], [3 * (g0 + j) for j in range(B)])
+
+    step(0)
+    torch.cuda.synchronize()
+    cyc = np.zeros(8, np.uint64)
+    lib.vs_debug_fm_cycles(cyc.ctypes.data, 1)
+    ctx.profile(True)
+    ctx.profile_reset()
+    for k in range(1, 1 + steps):
+        step(k)
+    torch.cuda.synchronize()
+    lib.vs_debug_fm_cycles(cyc.ctypes.data, 1)
+    prof = ctx.profile_read()
+    calls = max(1, prof.get("fmat_ransac", (0, 1))[1])
+    names = ["-", "solve7", "score", "replay", "final", "rng+mod", "reject", "collinear"]
+    print(json.dumps({"fmat_launches": calls, "fmat_ms_per_launch": prof.get("fmat_ransac", (0, 1))[0] / calls,
+                      "kcycles_per_launch": {names[k]: round(float(cyc[k]) / calls / 1e3, 1) for k in range(1, 8)},
+                      "stats": S.stats_dict()}))
+    S.close()
+    ctx.close()
+
+
+if __name__ == "__main__":
+    main()

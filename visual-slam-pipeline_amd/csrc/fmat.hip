@@ -6,13 +6,14 @@
 // One workgroup (8 wave64s) per frame pair.  The registrators are sequential only through the
 // cv::RNG stream and the shrinking iteration budget, so iterations run in chunks (64, 128, then
 // 256 hypotheses):
-//   * subsets: wave 0 steps the RNG on the scalar unit (lane k keeps state k of each block of
-//     64); all lanes reduce the draws modulo n; wave 0 assembles the 7-index subsets with the
-//     repeat rejection speculatively in parallel (lane l assumes the next 7-draw window; a
-//     ballot finds the first window with a repeat, which is assembled serially); all lanes test
-//     collinearity in parallel.  A collinear subset ends the chunk before it and the next chunk
-//     redraws it with the exact serial getSubset (attempt loop included), so the subsets are
-//     exactly OpenCV's;
+//   * subsets: every lane computes raw draws out of order with the cv::RNG jump-ahead
+//     (pnp_solvers.h: state r = s1 * A^r mod (A 2^32 - 1), Mont(A^r) from a constant table) and
+//     reduces them modulo n; J0[p] = the end of the 7-distinct-draw attempt that would start at
+//     draw p (repeat rejection) for every p in parallel; pointer doubling (J_{k+1} = J_k o J_k)
+//     gives attempt t's start J0^t(0) in log2(chunk) lookups; attempts are assembled and tested
+//     for collinearity in parallel, and collinear attempts are dropped in order (getSubset's
+//     retry).  A chunk in which nothing is accepted falls back to the exact serial getSubset
+//     (attempt limit included), so the subsets are exactly OpenCV's;
 //   * hypotheses: one 7-point solve per lane, models in LDS;
 //   * RANSAC scoring in rounds of 8 hypotheses: wave w scores hypothesis r0 + w with its 64
 //     lanes sweeping the points (ballot + popcount, division-free exact gate of fm_inlier,
@@ -34,9 +35,25 @@ using namespace vs_fm;
 
 constexpr int kFmMaxPts = VS_FM_MAX_POINTS;
 constexpr int kMaxChunk = 256;
-constexpr int kThreads = 512;  // 8 wave64s: 2 per SIMD
+constexpr int kThreads = 256;  // 4 wave64s, one per SIMD: the 7-point solver needs > 128 VGPRs (spills to AGPRs, not scratch)
 constexpr int kWaves = kThreads / 64;
 constexpr int kRawCap = 7 * kMaxChunk + 128;
+constexpr int kLevels = 8;  // pointer-doubling levels: 2^8 >= kMaxChunk attempts
+
+// Mont(A^k), k < kRawCap: the generator stepped k times from the Montgomery one (pnp_solvers.h)
+struct MwcPow {
+    uint64_t v[kRawCap];
+};
+constexpr MwcPow make_mwc_pow() {
+    MwcPow t{};
+    uint64_t s = vs_pnp::kMwcR1;
+    for (int i = 0; i < kRawCap; i++) {
+        t.v[i] = s;
+        s = vs_pnp::mwc_step(s);
+    }
+    return t;
+}
+__constant__ MwcPow g_mwc_pow = make_mwc_pow();
 
 #ifdef VS_FM_PROFILE
 // phase cycle counters (profiling build only: make -C visual-slam-pipeline_amd prof)
@@ -54,18 +71,21 @@ __device__ unsigned long long g_fm_cycles[8];
 
 struct FmShared {
     float p1[2 * kFmMaxPts], p2[2 * kFmMaxPts];
-    uint64_t st[kRawCap];  // RNG state after raw draw r
-    int draw[kRawCap];     // (unsigned)state % n
+    int draw[kRawCap];  // (unsigned)state % n of raw draw r
     int subset[kMaxChunk * 7];
-    int sub_end[kMaxChunk];  // raw position just past subset j
+    int start[kMaxChunk];  // raw position of attempt t
     int coll[kMaxChunk];
-    double Fm[kMaxChunk * 3 * 9];
+    union {
+        double Fm[kMaxChunk * 3 * 9];
+        uint16_t J[kLevels][kRawCap + 2];  // attempt-end maps (subset drawing only)
+    };
     int nmod[kMaxChunk];
     float score[kMaxChunk * 3];  // RANSAC: inlier count; LMedS: median error
     int scan[kThreads];
     double F[9];
     uint64_t rng;
-    int niters, best, best_iter, iter, fail_at, done, aborted, ok, chunk, inliers, serial_next, raw_n, nchunk;
+    int niters, best, best_iter, iter, fail_at, done, aborted, ok, chunk, inliers, serial_next, nchunk, navail,
+        anycoll;
     double min_median;
 };
 
@@ -108,94 +128,101 @@ __device__ void draw_subsets(FmShared& S, int n, int base, int want, int attempt
         return;
     }
     FM_T0();
-    const int lane = tid & 63;
-    const int R = min(kRawCap, (7 * want + 128 + 63) & ~63);
-    if (tid < 64) {  // wave 0, uniform: the generator runs on the scalar unit, lane k keeps state k
-        uint64_t s = S.rng;
-        for (int r0 = 0; r0 < R; r0 += 64) {
-            uint64_t mine = 0;
-            for (int k = 0; k < 64; k++) {
-                s = (uint64_t)(unsigned)s * 4164903690u + (unsigned)(s >> 32);
-                mine = lane == k ? s : mine;
-            }
-            S.st[r0 + lane] = mine;
-        }
+    // raw draws: expected draws per attempt with repeat rejection = sum_{k<7} n / (n - k)
+    float per = 0.f;
+    for (int k = 0; k < 7; k++) per += (float)n / (float)(n - k);
+    const int R = min(kRawCap, (int)(want * per * 1.15f) + 64);
+    const uint64_t s1 = vs_pnp::mwc_step(S.rng);
+    for (int r = tid; r < R; r += kThreads)
+        S.draw[r] = (int)((unsigned)vs_pnp::mwc_jump(s1, r, g_mwc_pow.v[r]) % (unsigned)n);
+    if (tid == 0) {
+        S.navail = want;
+        S.anycoll = 0;
     }
     __syncthreads();
-    for (int r = tid; r < R; r += blockDim.x) S.draw[r] = (int)((unsigned)S.st[r] % (unsigned)n);
-    __syncthreads();
     FM_T(5);
-    if (tid < 64) {
-        // Repeat rejection in stream order, speculatively in parallel (wave 0): lane l assumes
-        // subset j + l is the 7 draws at pos + 7 l, which holds up to the first window that
-        // contains a repeat (ballot); that one subset is then assembled serially and the
-        // speculation resumes after it.  The result is exactly the sequential scan's.
-        int pos = 0, j = 0;
-        bool stalled = false;
-        while (j < want && !stalled) {
-            const int p = pos + 7 * lane;
-            bool ok = p + 7 <= R && j + lane < want;
-            int w[7];
-            VS_UNROLL
-            for (int q = 0; q < 7; q++) w[q] = ok ? S.draw[p + q] : -1;
-            VS_UNROLL
-            for (int a = 1; a < 7; a++)
-                VS_UNROLL
-                for (int b = 0; b < a; b++) ok = ok && w[a] != w[b];
-            const unsigned long long bad = __ballot(!ok);
-            const int f = bad ? __ffsll((long long)bad) - 1 : 64;
-            if (lane < f) {
-                VS_UNROLL
-                for (int q = 0; q < 7; q++) S.subset[7 * (j + lane) + q] = w[q];
-                S.sub_end[j + lane] = p + 7;
-            }
-            j += f;
-            pos += 7 * f;
-            if (f == 64 || j >= want) continue;
-            // serial assembly of subset j from pos (uniform across the wave)
+    // J0[p]: one past the 7th distinct draw from p (R + 1: the draws run out)
+    for (int p = tid; p <= R + 1; p += kThreads) {
+        int e = R + 1;
+        if (p < R) {
             int cur[7] = {-1, -1, -1, -1, -1, -1, -1};
-            int i = 0;
-            while (i < 7 && pos < R) {
-                const int v = S.draw[pos++];
+            int i = 0, q = p;
+            while (i < 7 && q < R) {
+                const int v = S.draw[q++];
                 bool dup = false;
                 VS_UNROLL
-                for (int q = 0; q < 7; q++) dup |= (q < i) & (cur[q] == v);
+                for (int k = 0; k < 7; k++) dup |= (k < i) & (cur[k] == v);
                 if (!dup) {
                     VS_UNROLL
-                    for (int q = 0; q < 7; q++) cur[q] = (q == i) ? v : cur[q];
+                    for (int k = 0; k < 7; k++) cur[k] = (k == i) ? v : cur[k];
                     i++;
                 }
             }
-            if (i < 7) {  // the raw draws ran out: the chunk ends before subset j
-                stalled = true;
-                continue;
-            }
-            if (lane < 7) {
-                int val = cur[0];
-                VS_UNROLL
-                for (int q = 1; q < 7; q++) val = lane == q ? cur[q] : val;
-                S.subset[7 * j + lane] = val;
-            }
-            if (lane == 0) S.sub_end[j] = pos;
-            j++;
+            if (i == 7) e = q;
         }
-        if (lane == 0) S.chunk = j;
+        S.J[0][p] = (uint16_t)e;
+    }
+    __syncthreads();
+    int L = 0;
+    while ((1 << L) < want) L++;
+    for (int k = 1; k < L; k++) {
+        for (int p = tid; p <= R + 1; p += kThreads) S.J[k][p] = S.J[k - 1][S.J[k - 1][p]];
+        __syncthreads();
+    }
+    for (int t = tid; t < want; t += kThreads) {  // attempt t starts at J0^t(0)
+        int p = 0;
+        for (int k = 0; k < L; k++)
+            if ((t >> k) & 1) p = S.J[k][p];
+        const bool avail = p < R && S.J[0][p] <= R;
+        S.start[t] = avail ? p : -1;
+        if (!avail) atomicMin(&S.navail, t);
     }
     __syncthreads();
     FM_T(6);
-    for (int j = tid; j < S.chunk; j += blockDim.x) S.coll[j] = subset_collinear(S, S.subset + 7 * j);
+    const int T = S.navail;
+    for (int t = tid; t < T; t += kThreads) {  // assemble attempt t, collinearity (getSubset's retry test)
+        int cur[7] = {-1, -1, -1, -1, -1, -1, -1};
+        int i = 0, q = S.start[t];
+        while (i < 7) {
+            const int v = S.draw[q++];
+            bool dup = false;
+            VS_UNROLL
+            for (int k = 0; k < 7; k++) dup |= (k < i) & (cur[k] == v);
+            if (!dup) {
+                VS_UNROLL
+                for (int k = 0; k < 7; k++) cur[k] = (k == i) ? v : cur[k];
+                i++;
+            }
+        }
+        VS_UNROLL
+        for (int k = 0; k < 7; k++) S.subset[7 * t + k] = cur[k];
+        const int c = subset_collinear(S, S.subset + 7 * t);
+        S.coll[t] = c;
+        if (c) S.anycoll = 1;
+    }
     __syncthreads();
     FM_T(7);
     if (tid == 0) {
-        int c = S.chunk;
-        for (int j = 0; j < S.chunk; j++)
-            if (S.coll[j]) {
-                c = j;
-                break;
+        int j = T, last = T - 1;
+        if (S.anycoll) {  // drop collinear attempts in order (rare)
+            j = 0;
+            last = -1;
+            for (int t = 0; t < T; t++) {
+                if (S.coll[t]) continue;
+                if (j != t)
+                    for (int k = 0; k < 7; k++) S.subset[7 * j + k] = S.subset[7 * t + k];
+                last = t;
+                j++;
             }
-        if (c < S.chunk || c == 0) S.serial_next = 1;  // redraw subset c exactly (or make progress)
-        if (c > 0) S.rng = S.st[S.sub_end[c - 1] - 1];
-        S.chunk = c;
+        }
+        if (j == 0) {  // nothing accepted: the exact serial getSubset draws the next subset
+            S.serial_next = 1;
+            S.chunk = 0;
+        } else {
+            const int P = S.J[0][S.start[last]];  // raw draws consumed
+            S.rng = vs_pnp::mwc_jump(s1, P - 1, g_mwc_pow.v[P - 1]);
+            S.chunk = j;
+        }
     }
     __syncthreads();
 }
@@ -261,9 +288,8 @@ __global__ __launch_bounds__(kThreads) void k_fmat(const int* __restrict__ pairs
     __syncthreads();
     if (method == 1 && tid == 0) {
         const int all[7] = {0, 1, 2, 3, 4, 5, 6};
-        double Fs[3][9];
-        if (solve_idx(S, all, Fs) > 0) {
-            for (int k = 0; k < 9; k++) S.F[k] = Fs[0][k];
+        if (solve_idx(S, all, reinterpret_cast<double(*)[9]>(S.Fm)) > 0) {
+            for (int k = 0; k < 9; k++) S.F[k] = S.Fm[k];
             S.ok = 1;
         }
     }
@@ -276,11 +302,11 @@ __global__ __launch_bounds__(kThreads) void k_fmat(const int* __restrict__ pairs
         FM_T0();
         const int chunk = S.chunk;
         if (tid < chunk) {
-            double Fs[3][9];
+            // the solver writes its models straight into LDS (no private array: dynamic model
+            // indices would put one in scratch)
+            double(*Fs)[9] = reinterpret_cast<double(*)[9]>(&S.Fm[tid * 27]);
             const int nm = solve_idx(S, S.subset + 7 * tid, Fs);
             S.nmod[tid] = nm;
-            for (int k = 0; k < nm; k++)
-                for (int q = 0; q < 9; q++) S.Fm[(tid * 3 + k) * 9 + q] = Fs[k][q];
             if (method == 3)  // LMedS: n <= 14, median = element n/2 of the sorted errors
                 for (int k = 0; k < nm; k++) {
                     float e[14];
@@ -388,7 +414,7 @@ __global__ __launch_bounds__(kThreads) void k_fmat(const int* __restrict__ pairs
     // contiguous segment per lane so the compaction keeps the reference's order
     const int per = (n + kThreads - 1) / kThreads, lo = min(n, tid * per), hi = min(n, lo + per);
     int local = 0;
-    uint32_t bits = 0;  // per <= 4 since n <= 2048
+    uint32_t bits = 0;  // per <= 8 since n <= 2048
     for (int i = lo; i < hi; i++) {
         bool in = true;
         if (have_f && method != 1)

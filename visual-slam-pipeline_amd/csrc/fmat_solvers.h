@@ -233,30 +233,37 @@ VS_HD inline int run_7point(const float* x1, const float* y1, const float* x2, c
     const int n = solve_cubic(c, r);
     if (n < 1 || n > 3) return n < 0 ? 0 : n;
     // T1 = [s1 0 -s1 m1cx; 0 s1 -s1 m1cy; 0 0 1], T2 likewise; F = T2^T Fn T1
-    for (int k = 0; k < n; k++) {
-        double lambda = r[k], mu = 1.;
-        double s = f1[8] * r[k] + f2[8];
-        double Fn[9];
-        if (fabs(s) > DBL_EPSILON) {
-            mu = 1. / s;
-            lambda *= mu;
-            Fn[8] = 1.;
-        } else {
-            Fn[8] = 0.;
-        }
-        for (int i = 0; i < 8; i++) Fn[i] = f1[i] * lambda + f2[i] * mu;
-        const double T1[9] = {scale1, 0, -scale1 * m1cx, 0, scale1, -scale1 * m1cy, 0, 0, 1};
-        const double T2[9] = {scale2, 0, -scale2 * m2cx, 0, scale2, -scale2 * m2cy, 0, 0, 1};
-        double tmp[9];
-        for (int i = 0; i < 3; i++)  // tmp = T2^T Fn
-            for (int j = 0; j < 3; j++)
-                tmp[i * 3 + j] = T2[0 * 3 + i] * Fn[0 * 3 + j] + T2[1 * 3 + i] * Fn[1 * 3 + j] + T2[2 * 3 + i] * Fn[2 * 3 + j];
-        for (int i = 0; i < 3; i++)  // F = tmp T1
-            for (int j = 0; j < 3; j++)
-                F[k][i * 3 + j] = tmp[i * 3 + 0] * T1[0 * 3 + j] + tmp[i * 3 + 1] * T1[1 * 3 + j] + tmp[i * 3 + 2] * T1[2 * 3 + j];
-        if (fabs(F[k][8]) > FLT_EPSILON) {
-            const double sc = 1. / F[k][8];
-            for (int i = 0; i < 9; i++) F[k][i] *= sc;
+    VS_UNROLL
+    for (int k = 0; k < 3; k++) {  // unrolled with a guard: constant indices keep F, r in registers
+        if (k < n) {
+            double lambda = r[k], mu = 1.;
+            double s = f1[8] * r[k] + f2[8];
+            double Fn[9];
+            if (fabs(s) > DBL_EPSILON) {
+                mu = 1. / s;
+                lambda *= mu;
+                Fn[8] = 1.;
+            } else {
+                Fn[8] = 0.;
+            }
+            for (int i = 0; i < 8; i++) Fn[i] = f1[i] * lambda + f2[i] * mu;
+            const double T1[9] = {scale1, 0, -scale1 * m1cx, 0, scale1, -scale1 * m1cy, 0, 0, 1};
+            const double T2[9] = {scale2, 0, -scale2 * m2cx, 0, scale2, -scale2 * m2cy, 0, 0, 1};
+            double tmp[9];
+            VS_UNROLL
+            for (int i = 0; i < 3; i++)  // tmp = T2^T Fn
+                VS_UNROLL
+                for (int j = 0; j < 3; j++)
+                    tmp[i * 3 + j] = T2[0 * 3 + i] * Fn[0 * 3 + j] + T2[1 * 3 + i] * Fn[1 * 3 + j] + T2[2 * 3 + i] * Fn[2 * 3 + j];
+            VS_UNROLL
+            for (int i = 0; i < 3; i++)  // F = tmp T1
+                VS_UNROLL
+                for (int j = 0; j < 3; j++)
+                    F[k][i * 3 + j] = tmp[i * 3 + 0] * T1[0 * 3 + j] + tmp[i * 3 + 1] * T1[1 * 3 + j] + tmp[i * 3 + 2] * T1[2 * 3 + j];
+            if (fabs(F[k][8]) > FLT_EPSILON) {
+                const double sc = 1. / F[k][8];
+                for (int i = 0; i < 9; i++) F[k][i] *= sc;
+            }
         }
     }
     return n;

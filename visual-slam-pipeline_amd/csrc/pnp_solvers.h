@@ -42,6 +42,50 @@ struct CvRng {
     VS_HD int uniform(int a, int b) { return a == b ? a : (int)(next() % (unsigned)(b - a)) + a; }
 };
 
+// Jump-ahead for cv::RNG.  One step s' = lo32(s) * A + hi32(s) is multiplication by A modulo
+// M = A * 2^32 - 1 (A * 2^32 == 1 mod M), for every state 1 <= s < M (all states after the first
+// step of (uint64)-1; the representation is the residue).  k steps = multiplication by A^k mod M,
+// done in Montgomery form (R = 2^64): kMwcR1 = 2^64 mod M is the Montgomery one, stepping the
+// generator k times from it gives Mont(A^k), and mwc_mont_mul(s, Mont(A^k)) = s * A^k mod M.
+constexpr uint64_t kMwcA = 4164903690u;
+constexpr uint64_t kMwcM = (kMwcA << 32) - 1;
+constexpr uint64_t kMwcR1 = 0 - kMwcM;  // 2^64 - M (M > 2^63)
+constexpr uint64_t mwc_neg_inv() {      // -M^-1 mod 2^64 by Newton's iteration
+    uint64_t x = kMwcM;                 // correct to 3 bits (M odd)
+    for (int i = 0; i < 6; i++) x *= 2 - kMwcM * x;
+    return 0 - x;
+}
+constexpr uint64_t kMwcMInv = mwc_neg_inv();
+
+VS_HD constexpr uint64_t mwc_step(uint64_t s) { return (uint64_t)(unsigned)s * kMwcA + (unsigned)(s >> 32); }
+
+VS_HD inline uint64_t mulhi64(uint64_t a, uint64_t b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __umul64hi(a, b);
+#else
+    return (uint64_t)(((unsigned __int128)a * b) >> 64);
+#endif
+}
+
+// x * y / 2^64 mod M for x, y < M (REDC; the 65-bit intermediate is < 2M)
+VS_HD inline uint64_t mwc_mont_mul(uint64_t x, uint64_t y) {
+    const uint64_t lo = x * y, hi = mulhi64(x, y);
+    const uint64_t q = lo * kMwcMInv;
+    const uint64_t qh = mulhi64(q, kMwcM);  // lo + q * M == 0 mod 2^64: carry iff lo != 0
+    const uint64_t u = hi + qh;
+    const bool c1 = u < hi;
+    const uint64_t v = u + (lo != 0);
+    const bool c2 = v < u;
+    return (c1 || c2 || v >= kMwcM) ? v - kMwcM : v;
+}
+
+// The state k steps after s, given mont_pow_k = Mont(A^k).  s may be any state reached by at least
+// one step (the first step of (uint64)-1 lands on M + 2^32 - A, above M: its residue is used; every
+// later state is its own residue).
+VS_HD inline uint64_t mwc_jump(uint64_t s, int k, uint64_t mont_pow_k) {
+    return k == 0 ? s : mwc_mont_mul(s >= kMwcM ? s - kMwcM : s, mont_pow_k);
+}
+
 // cv::RANSACUpdateNumIters
 VS_HD inline int ransac_update_num_iters(double p, double ep, int model_points, int max_iters) {
     p = p > 0. ? p : 0.;

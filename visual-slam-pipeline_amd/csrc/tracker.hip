@@ -349,6 +349,7 @@ struct GpuOps {
         R.good.assign(hg, hg + hi[4]);
         R.kept.assign(hk, hk + hi[5]);
         R.f_ok = hi[12] != 0;  // F diag[4] = F ok
+        R.f_iters = hi[9];     // F diag[1] = iterations run
         R.epi_before = hd[9];
         R.epi_after = hd[10];
         R.ok3d = hi[6] != 0;
@@ -717,7 +718,7 @@ int vs_slam_stats(vs_slam* sl, int* out, int cap) {
                                    S.stationary,     S.keyframes,      S.pnp_refined,    S.periodic_pnp,
                                    S.tracked_total,  S.triangulated,   S.depth_points,   S.culled,
                                    S.chains_discarded, m.size(),       valid,            sl->trk->frame_count(),
-                                   sl->trk->keyframe_count(), sl->trk->last_match_count(), 0, 0};
+                                   sl->trk->keyframe_count(), sl->trk->last_match_count(), S.f_iters, 0};
     for (int i = 0; i < cap && i < VS_SLAM_NSTATS; i++) out[i] = v[i];
     return VS_OK;
 }

@@ -152,6 +152,7 @@ struct ChainResult {
     M3 RE{};
     V3 tE{};
     double scale = -1.0;
+    int f_iters = 0;  // F-RANSAC iterations run (findFundamentalMat's registrator)
 };
 
 struct PnPResult {  // Slam::PnPResult
@@ -168,7 +169,7 @@ struct AccelSample {
 struct Stats {
     int processed = 0, rejected = 0, via_3d3d = 0, via_emat = 0, emat_failed = 0, bridges = 0, recoveries = 0,
         recovery_failed = 0, stationary = 0, keyframes = 0, pnp_refined = 0, periodic_pnp = 0, tracked_total = 0,
-        triangulated = 0, depth_points = 0, culled = 0, chains_discarded = 0;
+        triangulated = 0, depth_points = 0, culled = 0, chains_discarded = 0, f_iters = 0;
 };
 
 // ---- the tracker -----------------------------------------------------------------------------
@@ -233,6 +234,7 @@ class Tracker {
         // control flow reaches :880 with these matches
         ref_frame_ = (last_keyframe_ && last_keyframe_->has_desc()) ? last_keyframe_ : last_frame_;
         ChainResult C = ops_.chain(*ref_frame_, *frame, 42u + (uint32_t)frame_count_);
+        stats_.f_iters += C.f_iters;
         last_match_count_ = (int)C.good.size();
 
         // :847-872 bridge keyframe when keyframe matching is weak
@@ -253,6 +255,7 @@ class Tracker {
                 }
                 ref_frame_ = last_keyframe_;
                 C = ops_.chain(*ref_frame_, *frame, 42u + (uint32_t)frame_count_);
+                stats_.f_iters += C.f_iters;
                 last_match_count_ = (int)C.good.size();
             }
         }

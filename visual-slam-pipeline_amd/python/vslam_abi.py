@@ -395,7 +395,7 @@ class Context:
 SLAM_STATS = ["processed", "rejected", "via_3d3d", "via_emat", "emat_failed", "bridges", "recoveries",
               "recovery_failed", "stationary", "keyframes", "pnp_refined", "periodic_pnp", "tracked_total",
               "triangulated", "depth_points", "culled", "chains_recomputed", "map_points", "map_valid",
-              "frame_count", "keyframe_count", "last_match_count"]
+              "frame_count", "keyframe_count", "last_match_count", "f_ransac_iters"]
 
 
 class Slam:
