@@ -31,13 +31,34 @@ void model_rt(const double* rv, const double* tv, double* R, double* t) {
     for (int k = 0; k < 3; k++) t[k] = tv[k];
 }
 
+// The LM sums in the device's order (pnp.hip k_pnp_ransac: lane t of 256 accumulates the inliers
+// i = t mod 256 in index order; block_sum: xor butterfly inside each wave64, then waves 0..3 in
+// order), so the accept / stop decisions, which compare costs at rounding level near convergence,
+// are bit-identical.  OpenCV's own summation order (cvCalcMatMulDeriv + gemm) is unpinned either way.
 void lm_eval(const float* obj, const float* img, const std::vector<int>& idx, const Cam& K, const double* p,
              double* acc) {
+    constexpr int kLanes = 256;
     LmRots L;
     lm_rotations(p, L);
-    for (int k = 0; k < kLmTerms; k++) acc[k] = 0;
+    std::vector<double> part((size_t)kLanes * kLmTerms, 0.0);
     for (int i : idx)
-        lm_point(L, p + 3, K, obj[3 * i], obj[3 * i + 1], obj[3 * i + 2], img[2 * i], img[2 * i + 1], acc);
+        lm_point(L, p + 3, K, obj[3 * i], obj[3 * i + 1], obj[3 * i + 2], img[2 * i], img[2 * i + 1],
+                 &part[(size_t)(i % kLanes) * kLmTerms]);
+    for (int k = 0; k < kLmTerms; k++) {
+        double wsum[kLanes / 64];
+        for (int w = 0; w < kLanes / 64; w++) {
+            double v[64], nv[64];
+            for (int l = 0; l < 64; l++) v[l] = part[(size_t)(64 * w + l) * kLmTerms + k];
+            for (int o = 32; o > 0; o >>= 1) {
+                for (int l = 0; l < 64; l++) nv[l] = v[l] + v[l ^ o];
+                for (int l = 0; l < 64; l++) v[l] = nv[l];
+            }
+            wsum[w] = v[0];
+        }
+        double sacc = wsum[0];
+        for (int w = 1; w < kLanes / 64; w++) sacc += wsum[w];
+        acc[k] = sacc;
+    }
 }
 
 bool epnp_on(const float* obj, const float* img, const int* idx, int m, const Cam& K, double* rv, double* tv) {

@@ -1,7 +1,8 @@
 """Phase breakdown of the F-matrix kernel inside the tracking loop (profiling build
 libvslam_hip_prof.so: `make -C visual-slam-pipeline_amd prof`).  Runs the closed-loop synthetic
 sequence through vs_slam like tools/bench_tracker.py and prints k_fmat's lane-0 clock64 phase
-cycles per launch (phases as tools/profile_fmat_phases.py)."""
+cycles per launch (phases as tools/profile_fmat_phases.py), and k_pnp_hyp's phase cycles summed
+over a solve_pnp call's hypotheses (100 per call)."""
 import ctypes
 import json
 import os
@@ -20,6 +21,8 @@ def main():
     import vslam_abi as va
     lib = va.load_library(os.path.join(ROOT, "visual-slam-pipeline_amd", "libvslam_hip_prof.so"))
     lib.vs_debug_fm_cycles.argtypes = [ctypes.c_void_p, ctypes.c_int]
+    lib.vs_debug_pnp_cycles.argtypes = [ctypes.c_void_p, ctypes.c_int]
+    lib.vs_debug_r3_cycles.argtypes = [ctypes.c_void_p, ctypes.c_int]
     U, B, steps = 126, 32, 4
     L = synth.loop_sequence(U)
     dev = torch.device("cuda", 0)
@@ -39,18 +42,31 @@ def main():
     step(0)
     torch.cuda.synchronize()
     cyc = np.zeros(8, np.uint64)
+    pcyc = np.zeros(8, np.uint64)
+    rcyc = np.zeros(8, np.uint64)
     lib.vs_debug_fm_cycles(cyc.ctypes.data, 1)
+    lib.vs_debug_pnp_cycles(pcyc.ctypes.data, 1)
+    lib.vs_debug_r3_cycles(rcyc.ctypes.data, 1)
     ctx.profile(True)
     ctx.profile_reset()
     for k in range(1, 1 + steps):
         step(k)
     torch.cuda.synchronize()
     lib.vs_debug_fm_cycles(cyc.ctypes.data, 1)
+    lib.vs_debug_pnp_cycles(pcyc.ctypes.data, 1)
+    lib.vs_debug_r3_cycles(rcyc.ctypes.data, 1)
     prof = ctx.profile_read()
     calls = max(1, prof.get("fmat_ransac", (0, 1))[1])
     names = ["-", "solve7", "score", "replay", "final", "rng+mod", "reject", "collinear"]
     print(json.dumps({"fmat_launches": calls, "fmat_ms_per_launch": prof.get("fmat_ransac", (0, 1))[0] / calls,
                       "kcycles_per_launch": {names[k]: round(float(cyc[k]) / calls / 1e3, 1) for k in range(1, 8)},
+                      "pnp_hyp_kcycles_per_hypothesis_x100": {
+                          n: round(float(pcyc[k]) / max(1, prof.get("solve_pnp", (0, 1))[1]) / 1e3, 1)
+                          for k, n in enumerate(["load+control", "mtm", "jacobi", "sort", "variants", "count"])},
+                      "ransac3d_kcycles_per_launch": {
+                          n: round(float(rcyc[k]) / max(1, prof.get("ransac3d", (0, 1))[1]) / 1e3, 1)
+                          for k, n in enumerate(["backproject", "mt_init", "twists", "sampling", "hypotheses",
+                                                 "select", "refit"])},
                       "stats": S.stats_dict()}))
     S.close()
     ctx.close()

@@ -25,6 +25,20 @@ using namespace vs_pnp;
 
 constexpr int kPnpMaxIters = VS_PNP_MAX_ITERS;
 
+#ifdef VS_PNP_PROFILE
+// k_pnp_hyp phase cycle counters (profiling build only: make -C visual-slam-pipeline_amd prof)
+__device__ unsigned long long g_pnp_cycles[8];
+#define PNP_T0() long long _pn_t = clock64()
+#define PNP_T(k)                                                             \
+    do {                                                                     \
+        if (threadIdx.x == 0) atomicAdd(&g_pnp_cycles[k], clock64() - _pn_t); \
+        _pn_t = clock64();                                                   \
+    } while (0)
+#else
+#define PNP_T0()
+#define PNP_T(k)
+#endif
+
 struct PnpShared {
     double red[4 * kLmTerms];
     LmState lm;
@@ -98,8 +112,9 @@ __global__ void k_pnp_subsets(const int* __restrict__ off, int niters0, int min_
 }
 
 // 2. one hypothesis per wave64 workgroup: EPnP on its subset with the 12 x 12 eigen-decomposition
-//    spread over the wave (LDS-resident, the same rotations and per-element arithmetic as the
-//    sequential sym_eig<12>, so the model is bit-identical to the host's), the three beta
+//    spread over the wave (LDS-resident round-robin Jacobi: a round's 6 disjoint rotations run in
+//    parallel with the per-element arithmetic of the sequential sym_eig_rr<12>, so the model is
+//    bit-identical to the host's), the three beta
 //    approximations on lanes 0-2, then the inlier count over all points by the whole wave.
 __global__ __launch_bounds__(64) void k_pnp_hyp(const float* __restrict__ obj_all, const float* __restrict__ img_all,
                                                 const int* __restrict__ off, double fx, double fy, double cx, double cy,
@@ -107,7 +122,8 @@ __global__ __launch_bounds__(64) void k_pnp_hyp(const float* __restrict__ obj_al
     __shared__ double sA[144], sV[144];
     __shared__ double sX[15], sUV[10], sAl[5][4], sCw[4][3];
     __shared__ double sTot, sOff, sErr[3], sRt[3][12];
-    __shared__ int sOk;
+    __shared__ double sC[6], sS[6];
+    __shared__ int sOk, sP[6], sQ[6], sAct[6];
     const int pb = blockIdx.x, h = blockIdx.y, lane = threadIdx.x;
     const int o0 = off[pb], n = off[pb + 1] - o0;
     const int model_points = n == 4 ? 4 : 5;
@@ -117,6 +133,7 @@ __global__ __launch_bounds__(64) void k_pnp_hyp(const float* __restrict__ obj_al
     const Cam K{fx, fy, cx, cy};
     const int* idx = H.subset + ((size_t)pb * H.stride + h) * 5;
     const int m = model_points;
+    PNP_T0();
     if (lane < m) {
         const int i = idx[lane];
         sX[3 * lane] = obj[3 * i];
@@ -135,6 +152,7 @@ __global__ __launch_bounds__(64) void k_pnp_hyp(const float* __restrict__ obj_al
             for (int j = 0; j < 4; j++) sAl[i][j] = al[i][j];
     }
     __syncthreads();
+    PNP_T(0);
     bool ok = sOk != 0;
     if (ok) {
         for (int e = lane; e < 144; e += 64) {
@@ -142,13 +160,14 @@ __global__ __launch_bounds__(64) void k_pnp_hyp(const float* __restrict__ obj_al
             sV[e] = (e / 12 == e % 12) ? 1.0 : 0.0;
         }
         __syncthreads();
-        // sym_eig<12> (pnp_solvers.h), wave-parallel over the 12 rows / columns of each rotation
+        // sym_eig_rr<12> (pnp_solvers.h): the 6 disjoint rotations of each round in parallel
         if (lane == 0) {
             double total = 0;
             for (int i = 0; i < 144; i++) total += sA[i] * sA[i];
             sTot = total;
         }
         __syncthreads();
+        PNP_T(1);
         const double total = sTot;
         for (int sweep = 0; sweep < 30; sweep++) {
             if (lane == 0) {
@@ -159,36 +178,42 @@ __global__ __launch_bounds__(64) void k_pnp_hyp(const float* __restrict__ obj_al
             }
             __syncthreads();
             if (!(sOff > 1e-32 * total)) break;
-            for (int p = 0; p < 11; p++)
-                for (int q = p + 1; q < 12; q++) {
-                    const double apq = sA[p * 12 + q];
-                    if (fabs(apq) < 1e-300) continue;
-                    const double app = sA[p * 12 + p], aqq = sA[q * 12 + q];
-                    const double theta = (aqq - app) / (2.0 * apq);
-                    const double t = (theta >= 0 ? 1.0 : -1.0) / (fabs(theta) + sqrt(theta * theta + 1.0));
-                    const double c = 1.0 / sqrt(t * t + 1.0), s = t * c;
-                    __syncthreads();
-                    if (lane < 12) {
-                        const int k = lane;
-                        const double akp = sA[k * 12 + p], akq = sA[k * 12 + q];
-                        sA[k * 12 + p] = c * akp - s * akq;
-                        sA[k * 12 + q] = s * akp + c * akq;
-                    }
-                    __syncthreads();
-                    if (lane < 12) {
-                        const int k = lane;
-                        const double apk = sA[p * 12 + k], aqk = sA[q * 12 + k];
-                        sA[p * 12 + k] = c * apk - s * aqk;
-                        sA[q * 12 + k] = s * apk + c * aqk;
-                    } else if (lane >= 32 && lane < 44) {
-                        const int k = lane - 32;
-                        const double vkp = sV[k * 12 + p], vkq = sV[k * 12 + q];
-                        sV[k * 12 + p] = c * vkp - s * vkq;
-                        sV[k * 12 + q] = s * vkp + c * vkq;
-                    }
-                    __syncthreads();
+            for (int r = 0; r < 11; r++) {
+                if (lane < 6) {  // angles from the matrix as the round starts
+                    int p, q;
+                    rr_pair(12, r, lane, p, q);
+                    double c = 1.0, sn = 0.0;
+                    sAct[lane] = jacobi_angle(sA[p * 12 + p], sA[q * 12 + q], sA[p * 12 + q], c, sn);
+                    sC[lane] = c;
+                    sS[lane] = sn;
+                    sP[lane] = p;
+                    sQ[lane] = q;
                 }
+                __syncthreads();
+                for (int it = lane; it < 144; it += 64) {  // column rotations of A and of V
+                    const int mat = it / 72, k = (it % 72) / 12, i = it % 12;
+                    if (sAct[k]) {
+                        double* M = mat ? sV : sA;
+                        const int p = sP[k], q = sQ[k];
+                        const double aip = M[i * 12 + p], aiq = M[i * 12 + q];
+                        M[i * 12 + p] = sC[k] * aip - sS[k] * aiq;
+                        M[i * 12 + q] = sS[k] * aip + sC[k] * aiq;
+                    }
+                }
+                __syncthreads();
+                for (int it = lane; it < 72; it += 64) {  // row rotations of A
+                    const int k = it / 12, j = it % 12;
+                    if (sAct[k]) {
+                        const int p = sP[k], q = sQ[k];
+                        const double apj = sA[p * 12 + j], aqj = sA[q * 12 + j];
+                        sA[p * 12 + j] = sC[k] * apj - sS[k] * aqj;
+                        sA[q * 12 + j] = sS[k] * apj + sC[k] * aqj;
+                    }
+                }
+                __syncthreads();
+            }
         }
+        PNP_T(2);
         if (lane == 0) {  // eigenvalues in descending order, columns of V swapped along (selection sort)
             double w[12];
             for (int i = 0; i < 12; i++) w[i] = sA[i * 12 + i];
@@ -209,6 +234,7 @@ __global__ __launch_bounds__(64) void k_pnp_hyp(const float* __restrict__ obj_al
             }
         }
         __syncthreads();
+        PNP_T(3);
         if (lane < 3) {  // one beta approximation per lane
             double cw[4][3], v[4][12], L[6][10], rho[6], al[5][4], X[15], uv[10];
             for (int i = 0; i < 4; i++)
@@ -224,6 +250,7 @@ __global__ __launch_bounds__(64) void k_pnp_hyp(const float* __restrict__ obj_al
             for (int k = 0; k < 3; k++) sRt[lane][9 + k] = t[k];
         }
         __syncthreads();
+        PNP_T(4);
     }
     // model = the first lowest-error approximation (epnp()), as (rvec, tvec)
     double rv[3] = {0, 0, 0}, tv[3] = {0, 0, 0};
@@ -244,6 +271,7 @@ __global__ __launch_bounds__(64) void k_pnp_hyp(const float* __restrict__ obj_al
         for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o);
         cnt = c;
     }
+    PNP_T(5);
     if (lane == 0) {
         H.count[(size_t)pb * H.stride + h] = cnt;
         double* mo = H.model + ((size_t)pb * H.stride + h) * 6;
@@ -407,3 +435,15 @@ int solve_pnp(vs_ctx* ctx, int nprob, const float* d_obj, const float* d_img, co
 }
 
 }  // namespace vs
+
+#ifdef VS_PNP_PROFILE
+extern "C" int vs_debug_pnp_cycles(unsigned long long* out, int reset) {
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(vs::g_pnp_cycles), sizeof(unsigned long long) * 8) != hipSuccess)
+        return -1;
+    if (reset) {
+        unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(vs::g_pnp_cycles), z, sizeof(z)) != hipSuccess) return -1;
+    }
+    return 0;
+}
+#endif

@@ -158,6 +158,96 @@ VS_HD void sym_eig(double* A, double* w, double* V) {
     }
 }
 
+// Parallel-order Jacobi (even N): each sweep is N - 1 rounds of N / 2 disjoint rotations in the
+// round-robin (circle) order; a round takes every angle from the matrix as the round starts, then
+// applies all column rotations of A, all row rotations of A, and all column rotations of V.
+// Every element receives at most one column and one row update per round, so the device can run
+// a round's rotations in parallel and stay bit-identical to this sequential statement.  Same
+// stopping rule and output convention as sym_eig (used for the EPnP 12 x 12 MtM).
+VS_HD inline void rr_pair(int N, int r, int k, int& p, int& q) {
+    const int a = k == 0 ? N - 1 : (r + k) % (N - 1);
+    const int b = k == 0 ? r : (r - k + (N - 1)) % (N - 1);
+    p = a < b ? a : b;
+    q = a < b ? b : a;
+}
+
+VS_HD inline bool jacobi_angle(double app, double aqq, double apq, double& c, double& s) {
+    if (fabs(apq) < 1e-300) return false;
+    const double theta = (aqq - app) / (2.0 * apq);
+    const double t = (theta >= 0 ? 1.0 : -1.0) / (fabs(theta) + sqrt(theta * theta + 1.0));
+    c = 1.0 / sqrt(t * t + 1.0);
+    s = t * c;
+    return true;
+}
+
+template <int N>
+VS_HD void sym_eig_rr(double* A, double* w, double* V) {
+    static_assert(N % 2 == 0, "round-robin Jacobi needs an even order");
+    constexpr int H = N / 2;
+    for (int i = 0; i < N; i++)
+        for (int j = 0; j < N; j++) V[i * N + j] = (i == j) ? 1.0 : 0.0;
+    double total = 0;
+    for (int i = 0; i < N * N; i++) total += A[i] * A[i];
+    for (int sweep = 0; sweep < 30; sweep++) {
+        double off = 0;
+        for (int p = 0; p < N; p++)
+            for (int q = p + 1; q < N; q++) off += A[p * N + q] * A[p * N + q];
+        if (!(off > 1e-32 * total)) break;
+        for (int r = 0; r < N - 1; r++) {
+            int P[H], Q[H];
+            double C[H], S[H];
+            bool act[H];
+            for (int k = 0; k < H; k++) {
+                rr_pair(N, r, k, P[k], Q[k]);
+                act[k] = jacobi_angle(A[P[k] * N + P[k]], A[Q[k] * N + Q[k]], A[P[k] * N + Q[k]], C[k], S[k]);
+            }
+            for (int k = 0; k < H; k++) {
+                if (!act[k]) continue;
+                const int p = P[k], q = Q[k];
+                for (int i = 0; i < N; i++) {
+                    const double aip = A[i * N + p], aiq = A[i * N + q];
+                    A[i * N + p] = C[k] * aip - S[k] * aiq;
+                    A[i * N + q] = S[k] * aip + C[k] * aiq;
+                }
+            }
+            for (int k = 0; k < H; k++) {
+                if (!act[k]) continue;
+                const int p = P[k], q = Q[k];
+                for (int j = 0; j < N; j++) {
+                    const double apj = A[p * N + j], aqj = A[q * N + j];
+                    A[p * N + j] = C[k] * apj - S[k] * aqj;
+                    A[q * N + j] = S[k] * apj + C[k] * aqj;
+                }
+            }
+            for (int k = 0; k < H; k++) {
+                if (!act[k]) continue;
+                const int p = P[k], q = Q[k];
+                for (int i = 0; i < N; i++) {
+                    const double vip = V[i * N + p], viq = V[i * N + q];
+                    V[i * N + p] = C[k] * vip - S[k] * viq;
+                    V[i * N + q] = S[k] * vip + C[k] * viq;
+                }
+            }
+        }
+    }
+    for (int i = 0; i < N; i++) w[i] = A[i * N + i];
+    for (int i = 0; i < N - 1; i++) {  // selection sort, descending
+        int m = i;
+        for (int j = i + 1; j < N; j++)
+            if (w[j] > w[m]) m = j;
+        if (m != i) {
+            const double tw = w[i];
+            w[i] = w[m];
+            w[m] = tw;
+            for (int k = 0; k < N; k++) {
+                const double tv = V[k * N + i];
+                V[k * N + i] = V[k * N + m];
+                V[k * N + m] = tv;
+            }
+        }
+    }
+}
+
 // Least squares min ||A x - b|| for an M x N (M >= N) matrix by Householder QR (A, b destroyed).
 template <int M, int N>
 VS_HD void lstsq(double* A, double* b, double* x) {
@@ -541,7 +631,7 @@ VS_HD bool epnp(const double* X, const double* uv, int n, const Cam& K, double* 
     for (int a = 0; a < 12; a++)
         for (int b = 0; b < 12; b++) MtM[a * 12 + b] = epnp_mtm(alphas, uv, n, K, a, b);
     double dm[12], um[144];
-    sym_eig<12>(MtM, dm, um);
+    sym_eig_rr<12>(MtM, dm, um);
     double v[4][12], L[6][10], rho[6];
     epnp_L_rho(um, cw, v, L, rho);
     double best_err = 0;

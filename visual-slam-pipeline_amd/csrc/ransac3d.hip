@@ -21,6 +21,20 @@ constexpr int kMaxPts3d = 512;
 constexpr int kMaxIters3d = 1024;
 constexpr int kMtN = 624;
 
+#ifdef VS_R3_PROFILE
+// k_ransac3d phase cycle counters (profiling build only: make -C visual-slam-pipeline_amd prof)
+__device__ unsigned long long g_r3_cycles[8];
+#define R3_T0() long long _r3_t = clock64()
+#define R3_T(k)                                                             \
+    do {                                                                    \
+        if (threadIdx.x == 0) atomicAdd(&g_r3_cycles[k], clock64() - _r3_t); \
+        _r3_t = clock64();                                                  \
+    } while (0)
+#else
+#define R3_T0()
+#define R3_T(k)
+#endif
+
 struct D3 {
     double x, y, z;
 };
@@ -187,6 +201,7 @@ __global__ __launch_bounds__(256) void k_ransac3d(const int* __restrict__ pairs,
     const float* dep1 = depth + (size_t)rf * h * w;
     const float* dep2 = depth + (size_t)cf * h * w;
 
+    R3_T0();
     // ---- back-projection + order-preserving compaction (two 256-row chunks) ----
     if (tid == 0) s_N = 0;
     __syncthreads();
@@ -235,6 +250,7 @@ __global__ __launch_bounds__(256) void k_ransac3d(const int* __restrict__ pairs,
         return;
     }
 
+    R3_T(0);
     // ---- MT19937(seed): init_genrand on lane 0, two parallel twists = 1248 outputs ----
     if (tid == 0) {
         uint32_t x = seeds[p];
@@ -245,8 +261,10 @@ __global__ __launch_bounds__(256) void k_ransac3d(const int* __restrict__ pairs,
         }
     }
     __syncthreads();
+    R3_T(1);
     mt_twist_block(s_mt, s_nw, s_out);
     mt_twist_block(s_mt, s_nw, s_out + kMtN);
+    R3_T(2);
     if (tid == 0) {
         // the reference's sampling loop; beyond 1248 draws the lane keeps twisting on its own
         int c = 0;
@@ -273,6 +291,7 @@ __global__ __launch_bounds__(256) void k_ransac3d(const int* __restrict__ pairs,
         }
     }
     __syncthreads();
+    R3_T(3);
 
     // ---- hypotheses, one lane each; keep the first best per lane, then the first best overall ----
     int my_best = 0, my_it = INT_MAX;
@@ -289,6 +308,7 @@ __global__ __launch_bounds__(256) void k_ransac3d(const int* __restrict__ pairs,
     s_bc[tid] = my_best;
     s_bi[tid] = my_it;
     __syncthreads();
+    R3_T(4);
     if (tid == 0) {
         int bc = 0, bi = -1;
         for (int k = 0; k < (int)blockDim.x; k++) {
@@ -301,6 +321,7 @@ __global__ __launch_bounds__(256) void k_ransac3d(const int* __restrict__ pairs,
         s_best_it = bi;
     }
     __syncthreads();
+    R3_T(5);
     if (tid != 0) return;
     const int best_inliers = s_best_cnt, best_it = s_best_it;
     diag_out[4 * p + 0] = N;
@@ -344,6 +365,7 @@ __global__ __launch_bounds__(256) void k_ransac3d(const int* __restrict__ pairs,
     if (tn < 0.0001) ok = 0;
     if (fabs(det3_dev(R) - 1.0) > 0.01) ok = 0;
     ok_out[p] = ok;
+    R3_T(6);
 }
 
 int ransac3d_pairs(vs_ctx* ctx, int P, const int* d_pairs, const vs_keypoint* d_kps, int cap, const vs_match* d_good,
@@ -360,3 +382,15 @@ int ransac3d_pairs(vs_ctx* ctx, int P, const int* d_pairs, const vs_keypoint* d_
 }
 
 }  // namespace vs
+
+#ifdef VS_R3_PROFILE
+extern "C" int vs_debug_r3_cycles(unsigned long long* out, int reset) {
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(vs::g_r3_cycles), sizeof(unsigned long long) * 8) != hipSuccess)
+        return -1;
+    if (reset) {
+        unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(vs::g_r3_cycles), z, sizeof(z)) != hipSuccess) return -1;
+    }
+    return 0;
+}
+#endif
