@@ -123,7 +123,7 @@ __global__ __launch_bounds__(64) void k_pnp_hyp(const float* __restrict__ obj_al
     __shared__ double sX[15], sUV[10], sAl[5][4], sCw[4][3];
     __shared__ double sTot, sOff, sErr[3], sRt[3][12];
     __shared__ double sC[6], sS[6];
-    __shared__ int sOk, sP[6], sQ[6], sAct[6];
+    __shared__ int sOk, sAct[6];
     const int pb = blockIdx.x, h = blockIdx.y, lane = threadIdx.x;
     const int o0 = off[pb], n = off[pb + 1] - o0;
     const int model_points = n == 4 ? 4 : 5;
@@ -186,28 +186,52 @@ __global__ __launch_bounds__(64) void k_pnp_hyp(const float* __restrict__ obj_al
                     sAct[lane] = jacobi_angle(sA[p * 12 + p], sA[q * 12 + q], sA[p * 12 + q], c, sn);
                     sC[lane] = c;
                     sS[lane] = sn;
-                    sP[lane] = p;
-                    sQ[lane] = q;
                 }
                 __syncthreads();
-                for (int it = lane; it < 144; it += 64) {  // column rotations of A and of V
-                    const int mat = it / 72, k = (it % 72) / 12, i = it % 12;
-                    if (sAct[k]) {
-                        double* M = mat ? sV : sA;
-                        const int p = sP[k], q = sQ[k];
-                        const double aip = M[i * 12 + p], aiq = M[i * 12 + q];
-                        M[i * 12 + p] = sC[k] * aip - sS[k] * aiq;
-                        M[i * 12 + q] = sS[k] * aip + sC[k] * aiq;
-                    }
-                }
-                __syncthreads();
-                for (int it = lane; it < 72; it += 64) {  // row rotations of A
-                    const int k = it / 12, j = it % 12;
-                    if (sAct[k]) {
-                        const int p = sP[k], q = sQ[k];
-                        const double apj = sA[p * 12 + j], aqj = sA[q * 12 + j];
-                        sA[p * 12 + j] = sC[k] * apj - sS[k] * aqj;
-                        sA[q * 12 + j] = sS[k] * apj + sC[k] * aqj;
+                // One pass: the 2 x 2 block of A at (pair a rows i0 < i1, pair b columns j0 < j1)
+                // takes its column rotation (b) and then its row rotation (a) -- per element exactly
+                // the sequential statement's column-then-row order -- and each row of V its column
+                // rotations.
+                for (int it = lane; it < 36 + 72; it += 64) {
+                    if (it < 36) {
+                        const int a = it / 6, b = it % 6;
+                        int i0, i1, j0, j1;
+                        rr_pair(12, r, a, i0, i1);
+                        rr_pair(12, r, b, j0, j1);
+                        double x00 = sA[i0 * 12 + j0], x01 = sA[i0 * 12 + j1];
+                        double x10 = sA[i1 * 12 + j0], x11 = sA[i1 * 12 + j1];
+                        if (sAct[b]) {
+                            const double c = sC[b], sn = sS[b];
+                            const double y00 = c * x00 - sn * x01, y01 = sn * x00 + c * x01;
+                            const double y10 = c * x10 - sn * x11, y11 = sn * x10 + c * x11;
+                            x00 = y00;
+                            x01 = y01;
+                            x10 = y10;
+                            x11 = y11;
+                        }
+                        if (sAct[a]) {
+                            const double c = sC[a], sn = sS[a];
+                            const double y00 = c * x00 - sn * x10, y10 = sn * x00 + c * x10;
+                            const double y01 = c * x01 - sn * x11, y11 = sn * x01 + c * x11;
+                            x00 = y00;
+                            x01 = y01;
+                            x10 = y10;
+                            x11 = y11;
+                        }
+                        sA[i0 * 12 + j0] = x00;
+                        sA[i0 * 12 + j1] = x01;
+                        sA[i1 * 12 + j0] = x10;
+                        sA[i1 * 12 + j1] = x11;
+                    } else {
+                        const int v = it - 36, i = v / 6, b = v % 6;
+                        if (sAct[b]) {
+                            int j0, j1;
+                            rr_pair(12, r, b, j0, j1);
+                            const double c = sC[b], sn = sS[b];
+                            const double vp = sV[i * 12 + j0], vq = sV[i * 12 + j1];
+                            sV[i * 12 + j0] = c * vp - sn * vq;
+                            sV[i * 12 + j1] = sn * vp + c * vq;
+                        }
                     }
                 }
                 __syncthreads();
