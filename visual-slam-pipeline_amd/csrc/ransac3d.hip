@@ -4,12 +4,14 @@
 //   back-projection of the matched keypoints with round()-ed depth lookups and the (0.1, 10]
 //   depth gate, order preserved (:236-262); N >= 10 (:265);
 //   std::mt19937(42 + frame_count) sampling with the same rejection loops (:276-283) — the
-//   generator is a bit-exact MT19937 (parallel 3-phase twist into LDS, one lane consumes);
+//   generator is a bit-exact MT19937 (parallel 3-phase twist into LDS); the triples of all
+//   iterations are found at once (the draws an iteration starting at draw c consumes, for every
+//   c, then pointer doubling gives each iteration's first draw);
 //   every hypothesis (3-point Kabsch: centroids, cross-covariance, one-sided Jacobi SVD,
 //   reflection fix, t = c2 - R c1) and its inlier count over all N points runs on its own lane;
-//   the first strictly-best iteration wins (:313-317), >= 10 inliers (:320), the refit over all
-//   inliers runs sequentially on one lane in the reference's order (:324-358), then the sanity
-//   gates (:361-372).
+//   the first strictly-best iteration wins (:313-317, an exact max/min reduction), >= 10 inliers
+//   (:320), the refit over all inliers (:324-358) keeps each of its sums a sequential chain in
+//   the reference's order (one chain per lane), then the sanity gates (:361-372).
 // Compiled with -ffp-contract=off, so results equal the CPU restatement (tests/test_gpu_parity.py).
 #include <hip/hip_runtime.h>
 
