@@ -40,6 +40,7 @@ __device__ unsigned long long g_pnp_cycles[8];
 #endif
 
 struct PnpShared {
+    LmRots rots;
     double red[4 * kLmTerms];
     LmState lm;
     double rv[3], tv[3];
@@ -78,36 +79,127 @@ __device__ inline bool pnp_problem_runs(int n, int min_inliers, int model_points
 }
 
 // 1. subsets of the initial budget from the cv::RNG stream (getSubset: repeats rejected); the
-//    stream does not depend on the models because checkSubset is trivially true for PnP.
-__global__ void k_pnp_subsets(const int* __restrict__ off, int niters0, int min_inliers, PnpHyp H) {
-    const int pb = blockIdx.x * blockDim.x + threadIdx.x;
-    if (pb >= (int)gridDim.x * (int)blockDim.x) return;
+//    stream does not depend on the models because checkSubset is trivially true for PnP.  One
+//    workgroup per problem, up to 256 iterations per round: raw draws out of order with the
+//    cv::RNG jump-ahead (pnp_solvers.h), J0[p] = one past the 5th distinct draw from p for every
+//    p, pointer doubling for each iteration's first draw, subsets assembled in parallel.
+constexpr int kPnpRaw = 2048;
+constexpr int kPnpLevels = 8;  // 2^8 >= 256 iterations per round
+struct PnpMwcPow {
+    uint64_t v[kPnpRaw];
+};
+constexpr PnpMwcPow make_pnp_mwc_pow() {
+    PnpMwcPow t{};
+    uint64_t s = kMwcR1;
+    for (int i = 0; i < kPnpRaw; i++) {
+        t.v[i] = s;
+        s = mwc_step(s);
+    }
+    return t;
+}
+__constant__ PnpMwcPow g_pnp_mwc_pow = make_pnp_mwc_pow();
+
+__global__ __launch_bounds__(256) void k_pnp_subsets(const int* __restrict__ off, int niters0, int min_inliers,
+                                                     PnpHyp H) {
+    __shared__ int s_draw[kPnpRaw];
+    __shared__ uint16_t s_J[kPnpLevels][kPnpRaw + 2];
+    __shared__ int s_start[256];
+    __shared__ int s_navail;
+    __shared__ uint64_t s_rng;
+    const int pb = blockIdx.x, tid = threadIdx.x;
     const int n = off[pb + 1] - off[pb];
     const int model_points = n == 4 ? 4 : 5;
-    if (!pnp_problem_runs(n, min_inliers, model_points)) return;
-    CvRng rng((uint64_t)-1);
-    for (int it = 0; it < niters0; it++) {
-        // getSubset's repeat rejection, unrolled so the subset stays in registers (a runtime
-        // index into a private array would live in scratch memory)
-        int idx[5] = {0, 0, 0, 0, 0};
-#pragma unroll
-        for (int i = 0; i < 5; i++) {
-            if (i < model_points)
-                for (;;) {
-                    const int v = rng.uniform(0, n);
+    if (!pnp_problem_runs(n, min_inliers, model_points)) return;  // running problems have n > 5
+    float per = 0.f;
+    for (int k = 0; k < 5; k++) per += (float)n / (float)(n - k);
+    if (tid == 0) s_rng = (uint64_t)-1;
+    int base = 0;
+    while (base < niters0) {
+        const int want = min(256, niters0 - base);
+        const int R = min(kPnpRaw, (int)(want * per * 1.15f) + 64);
+        __syncthreads();
+        const uint64_t s1 = mwc_step(s_rng);
+        for (int r = tid; r < R; r += 256) s_draw[r] = (int)((unsigned)mwc_jump(s1, r, g_pnp_mwc_pow.v[r]) % (unsigned)n);
+        if (tid == 0) s_navail = want;
+        __syncthreads();
+        for (int p = tid; p <= R + 1; p += 256) {
+            int e = R + 1;
+            if (p < R) {
+                int cur[5] = {-1, -1, -1, -1, -1};
+                int i = 0, q = p;
+                while (i < 5 && q < R) {
+                    const int v = s_draw[q++];
                     bool dup = false;
 #pragma unroll
-                    for (int j = 0; j < i; j++) dup |= idx[j] == v;
+                    for (int k = 0; k < 5; k++) dup |= (k < i) & (cur[k] == v);
                     if (!dup) {
-                        idx[i] = v;
-                        break;
+#pragma unroll
+                        for (int k = 0; k < 5; k++) cur[k] = (k == i) ? v : cur[k];
+                        i++;
                     }
                 }
+                if (i == 5) e = q;
+            }
+            s_J[0][p] = (uint16_t)e;
         }
-        int* dst = H.subset + ((size_t)pb * H.stride + it) * 5;
+        __syncthreads();
+        int L = 0;
+        while ((1 << L) < want) L++;
+        for (int k = 1; k < L; k++) {
+            for (int p = tid; p <= R + 1; p += 256) s_J[k][p] = s_J[k - 1][s_J[k - 1][p]];
+            __syncthreads();
+        }
+        for (int t = tid; t < want; t += 256) {
+            int p = 0;
+            for (int k = 0; k < L; k++)
+                if ((t >> k) & 1) p = s_J[k][p];
+            const bool avail = p < R && s_J[0][p] <= R;
+            s_start[t] = avail ? p : -1;
+            if (!avail) atomicMin(&s_navail, t);
+        }
+        __syncthreads();
+        const int T = s_navail;
+        for (int t = tid; t < T; t += 256) {
+            int cur[5] = {-1, -1, -1, -1, -1};
+            int i = 0, q = s_start[t];
+            while (i < 5) {
+                const int v = s_draw[q++];
+                bool dup = false;
 #pragma unroll
-        for (int i = 0; i < 5; i++)
-            if (i < model_points) dst[i] = idx[i];
+                for (int k = 0; k < 5; k++) dup |= (k < i) & (cur[k] == v);
+                if (!dup) {
+#pragma unroll
+                    for (int k = 0; k < 5; k++) cur[k] = (k == i) ? v : cur[k];
+                    i++;
+                }
+            }
+            int* dst = H.subset + ((size_t)pb * H.stride + base + t) * 5;
+#pragma unroll
+            for (int k = 0; k < 5; k++) dst[k] = cur[k];
+        }
+        if (tid == 0) {
+            if (T > 0) {
+                const int P = s_J[0][s_start[T - 1]];  // raw draws consumed
+                s_rng = mwc_jump(s1, P - 1, g_pnp_mwc_pow.v[P - 1]);
+            } else {  // the window held no complete subset (not reachable for n > 5): one serially
+                CvRng rng(s_rng);
+                int cur[5] = {-1, -1, -1, -1, -1};
+                for (int i = 0; i < 5; i++)
+                    for (;;) {
+                        const int v = rng.uniform(0, n);
+                        bool dup = false;
+                        for (int k = 0; k < i; k++) dup |= cur[k] == v;
+                        if (!dup) {
+                            cur[i] = v;
+                            break;
+                        }
+                    }
+                int* dst = H.subset + ((size_t)pb * H.stride + base) * 5;
+                for (int k = 0; k < 5; k++) dst[k] = cur[k];
+                s_rng = rng.state;
+            }
+        }
+        base += T > 0 ? T : 1;
     }
 }
 
@@ -392,8 +484,14 @@ __global__ __launch_bounds__(256) void k_pnp_ransac(const float* __restrict__ ob
         // the previous candidate.
         double p[6] = {rv0[0], rv0[1], rv0[2], tv0[0], tv0[1], tv0[2]};
         for (bool first = true;; first = false) {
-            LmRots L;
-            lm_rotations(p, L);
+            // the 7 rotations of lm_rotations (R(r), R(r +- h e_k)), one per lane, shared via LDS
+            if (tid < 7) {
+                double r[3] = {p[0], p[1], p[2]};
+                if (tid > 0) r[(tid - 1) / 2] += ((tid - 1) % 2 == 0) ? kLmStep : -kLmStep;
+                rod_v2m(r, S.rots.R[tid]);
+            }
+            __syncthreads();
+            const LmRots& L = S.rots;
             double acc[kLmTerms], tot[kLmTerms];
             for (int k = 0; k < kLmTerms; k++) acc[k] = 0;
             for (int i = tid; i < n; i += blockDim.x)
@@ -449,7 +547,7 @@ int solve_pnp(vs_ctx* ctx, int nprob, const float* d_obj, const float* d_img, co
     H.subset = reinterpret_cast<int*>(H.model + per * 6);
     H.count = H.subset + per * 5;
     H.stride = niters0;
-    hipLaunchKernelGGL(k_pnp_subsets, dim3(nprob), dim3(1), 0, s, d_off, niters0, min_inliers, H);
+    hipLaunchKernelGGL(k_pnp_subsets, dim3(nprob), dim3(256), 0, s, d_off, niters0, min_inliers, H);
     hipLaunchKernelGGL(k_pnp_hyp, dim3(nprob, niters0), dim3(64), 0, s, d_obj, d_img, d_off, K[0], K[1], K[2], K[3],
                        niters0, thr2, min_inliers, H);
     hipLaunchKernelGGL(k_pnp_ransac, dim3(nprob), dim3(256), 0, s, d_obj, d_img, d_off, K[0], K[1], K[2], K[3],

@@ -167,6 +167,7 @@ __global__ __launch_bounds__(1024) void k_tlm_resolve(const int* __restrict__ cn
                                                       int* __restrict__ result) {
     __shared__ unsigned long long s_best[kTlmMaxKp];  // bits of the running minimum (d >= 0: order-preserving)
     __shared__ int s_kpmp[kTlmMaxKp];
+    __shared__ int s_first[kTlmMaxKp];  // first candidate of a keypoint within the chunk
     __shared__ int s_cmp[1024], s_cki[1024];
     __shared__ unsigned long long s_cd[1024];
     __shared__ int s_wcnt[16];
@@ -175,6 +176,7 @@ __global__ __launch_bounds__(1024) void k_tlm_resolve(const int* __restrict__ cn
     for (int k = tid; k < nkp; k += 1024) {
         s_best[k] = (unsigned long long)__double_as_longlong(1e9);
         s_kpmp[k] = kp_to_mp[k];
+        s_first[k] = INT_MAX;
     }
     if (tid == 0) s_nobs = 0;
     __syncthreads();
@@ -208,9 +210,11 @@ __global__ __launch_bounds__(1024) void k_tlm_resolve(const int* __restrict__ cn
             s_cmp[j] = mp;
             s_cki[j] = ki0;
             s_cd[j] = (unsigned long long)__double_as_longlong(bd);
+            atomicMin(&s_first[ki0], j);
         }
         __syncthreads();
-        // winners: strictly below the carried minimum and below every earlier candidate of the keypoint
+        // winners: strictly below the carried minimum and below every earlier candidate of the
+        // keypoint (only candidates from the keypoint's first one on can share it)
         bool win = false;
         int ki = -1;
         unsigned long long d = 0;
@@ -218,10 +222,11 @@ __global__ __launch_bounds__(1024) void k_tlm_resolve(const int* __restrict__ cn
             ki = s_cki[tid];
             d = s_cd[tid];
             win = d < s_best[ki];
-            for (int j = 0; j < tid && win; j++)
+            for (int j = s_first[ki]; j < tid && win; j++)
                 if (s_cki[j] == ki && s_cd[j] <= d) win = false;
         }
         __syncthreads();
+        if (tid < nc) s_first[ki] = INT_MAX;  // every reader is past the barrier above
         if (win) atomicMin(&s_best[ki], d);
         bal = __ballot(win);
         if (lane == 0) s_wcnt[wv] = __popcll(bal);
