@@ -15,6 +15,8 @@
 // match, the visibility sweep and the map appends.  Everything runs on the context's stream.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include <algorithm>
 #include <cstring>
 #include <memory>
@@ -127,9 +129,17 @@ constexpr size_t kChainKept = kChainGood + (size_t)kCap * sizeof(vs_match);
 constexpr size_t kChainRaw = kChainKept + (size_t)kCap * sizeof(vs_match);
 constexpr size_t kChainBytes = kChainRaw + (size_t)kCap * sizeof(vs_match);
 
+// Frames per extraction chunk: the batch's network + post-processing runs chunk by chunk on the
+// extraction stream while the tracker consumes the chunks already done (process_batch_dev).
+constexpr int kXChunk = 8;
+
 struct GpuOps {
     vs_ctx* ctx = nullptr;
-    hipStream_t s = nullptr;
+    hipStream_t s = nullptr;   // tracking stream (the context's stream is swapped to it during vs_slam calls)
+    hipStream_t xs = nullptr;  // extraction stream
+    bool own_streams = false;
+    std::vector<hipEvent_t> xev;  // one per extraction chunk
+    Pinned xpin;                  // keypoints / counts of the batch being extracted
     int B = 0, h = 0, w = 0, S = 0, batch_region = 0;
     double K[4] = {vs_trk::cfg::FX, vs_trk::cfg::FY, vs_trk::cfg::CX, vs_trk::cfg::CY};
     DevBuf pool_kps, pool_desc, pool_n, pool_depth, semi, dgrid;
@@ -144,9 +154,48 @@ struct GpuOps {
     float* desc_of(int slot) const { return pool_desc.as<float>() + (size_t)slot * kCap * 256; }
     float* depth_of(int slot) const { return pool_depth.as<float>() + (size_t)slot * h * w; }
 
+    // Two streams on disjoint CU sets: the latency-bound tracking kernels keep VS_SLAM_TRACK_CUS
+    // (default 32) CUs to themselves, so they never queue behind the network's long-running
+    // workgroups, and the next chunks' network runs on the rest meanwhile.  Plain streams when
+    // the CU-mask extension is unavailable.
+    int make_streams() {
+        int ncu = 0;
+        VS_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, ctx->device));
+        const char* env = std::getenv("VS_SLAM_TRACK_CUS");
+        const int tcu = env ? std::atoi(env) : 32;
+        bool masked = false;
+        if (tcu > 0 && ncu >= 2 * tcu) {
+            const int words = (ncu + 31) / 32;
+            std::vector<uint32_t> tm(words, 0u), xm(words, 0u);
+            for (int cu = 0; cu < ncu; cu++) (cu < tcu ? tm : xm)[cu / 32] |= 1u << (cu % 32);
+            masked = hipExtStreamCreateWithCUMask(&s, words, tm.data()) == hipSuccess;
+            if (masked && hipExtStreamCreateWithCUMask(&xs, words, xm.data()) != hipSuccess) {
+                (void)hipStreamDestroy(s);
+                s = nullptr;
+                masked = false;
+            }
+        }
+        if (!masked) {
+            VS_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+            VS_HIP(hipStreamCreateWithFlags(&xs, hipStreamNonBlocking));
+        }
+        own_streams = true;
+        return VS_OK;
+    }
+    void destroy_streams() {
+        if (!own_streams) return;
+        (void)hipStreamSynchronize(xs);
+        (void)hipStreamSynchronize(s);
+        for (hipEvent_t e : xev) (void)hipEventDestroy(e);
+        xev.clear();
+        (void)hipStreamDestroy(xs);
+        (void)hipStreamDestroy(s);
+        own_streams = false;
+    }
+
     int init(vs_ctx* c, int max_batch, int hh, int ww) {
         ctx = c;
-        s = ctx->stream;
+        VS_CHECK(make_streams());
         B = max_batch;
         h = hh;
         w = ww;
@@ -264,29 +313,52 @@ struct GpuOps {
         return VS_OK;
     }
     // B frames already in HBM -> network + post-processing straight into batch region slots,
-    // depth copied beside them; keypoints come back to the host (the tracker's bookkeeping).
+    // depth copied beside them, keypoints back to pinned host memory, kXChunk frames at a time on
+    // the extraction stream; chunk c's event marks its slots and host keypoints ready.  Enqueue
+    // only: wait_chunk() hands a chunk to the tracker.
     int extract_batch(std::vector<vs_trk::FramePtr>& frames, const uint8_t* d_bgr, const float* d_depth) {
         const int nb = (int)frames.size();
         const int s0 = batch_region * B;
         batch_region ^= 1;
-        VS_CHECK(sp_forward(ctx, nb, d_bgr, 3, h, w, s, semi.as<float>(), dgrid.as<float>()));
-        VS_CHECK(sp_postprocess(ctx, nb, (h + 7) / 8, (w + 7) / 8, h, w, kps_of(s0), desc_of(s0),
-                                pool_n.as<int>() + s0, kCap, s, semi.as<float>(), dgrid.as<float>()));
-        if (d_depth)
-            VS_HIP(hipMemcpyAsync(depth_of(s0), d_depth, (size_t)nb * h * w * sizeof(float), hipMemcpyDeviceToDevice, s));
-        else
-            VS_HIP(hipMemsetAsync(depth_of(s0), 0, (size_t)nb * h * w * sizeof(float), s));
-        char* hk = pin.take((size_t)nb * kCap * sizeof(vs_keypoint) + (size_t)nb * sizeof(int));
-        if (!hk) {
-            VS_CHECK(sync());
-            VS_CHECK(pin.reserve((size_t)nb * kCap * (sizeof(vs_keypoint) + 4) + 64));
-            hk = pin.take((size_t)nb * kCap * sizeof(vs_keypoint) + (size_t)nb * sizeof(int));
+        const int nch = (nb + kXChunk - 1) / kXChunk;
+        while ((int)xev.size() < nch) {
+            hipEvent_t e;
+            VS_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+            xev.push_back(e);
         }
+        VS_CHECK(xpin.reserve((size_t)nb * kCap * sizeof(vs_keypoint) + (size_t)nb * sizeof(int) + 64));
+        char* hk = xpin.base;
         int* hn = reinterpret_cast<int*>(hk + (size_t)nb * kCap * sizeof(vs_keypoint));
-        VS_HIP(hipMemcpyAsync(hk, kps_of(s0), (size_t)nb * kCap * sizeof(vs_keypoint), hipMemcpyDeviceToHost, s));
-        VS_HIP(hipMemcpyAsync(hn, pool_n.as<int>() + s0, (size_t)nb * sizeof(int), hipMemcpyDeviceToHost, s));
-        VS_HIP(hipStreamSynchronize(s));
-        for (int b = 0; b < nb; b++) {
+        const int hc = (h + 7) / 8, wc = (w + 7) / 8;
+        for (int c = 0; c < nch; c++) {
+            const int f0 = c * kXChunk, m = std::min(kXChunk, nb - f0);
+            VS_CHECK(sp_forward(ctx, m, d_bgr + (size_t)f0 * h * w * 3, 3, h, w, xs, semi.as<float>(),
+                                dgrid.as<float>()));
+            VS_CHECK(sp_postprocess(ctx, m, hc, wc, h, w, kps_of(s0 + f0), desc_of(s0 + f0), pool_n.as<int>() + s0 + f0,
+                                    kCap, xs, semi.as<float>(), dgrid.as<float>()));
+            if (d_depth)
+                VS_HIP(hipMemcpyAsync(depth_of(s0 + f0), d_depth + (size_t)f0 * h * w, (size_t)m * h * w * sizeof(float),
+                                      hipMemcpyDeviceToDevice, xs));
+            else
+                VS_HIP(hipMemsetAsync(depth_of(s0 + f0), 0, (size_t)m * h * w * sizeof(float), xs));
+            VS_HIP(hipMemcpyAsync(hk + (size_t)f0 * kCap * sizeof(vs_keypoint), kps_of(s0 + f0),
+                                  (size_t)m * kCap * sizeof(vs_keypoint), hipMemcpyDeviceToHost, xs));
+            VS_HIP(hipMemcpyAsync(hn + f0, pool_n.as<int>() + s0 + f0, (size_t)m * sizeof(int), hipMemcpyDeviceToHost, xs));
+            VS_HIP(hipEventRecord(xev[c], xs));
+        }
+        for (int b = 0; b < nb; b++) frames[b]->slot = s0 + b;
+        return VS_OK;
+    }
+    // Chunk c of the batch is extracted: its keypoints to the frames, and the tracking stream
+    // ordered after it.
+    int wait_chunk(std::vector<vs_trk::FramePtr>& frames, int c) {
+        const int nb = (int)frames.size();
+        const int f0 = c * kXChunk, m = std::min(kXChunk, nb - f0);
+        VS_HIP(hipEventSynchronize(xev[c]));
+        VS_HIP(hipStreamWaitEvent(s, xev[c], 0));
+        const char* hk = xpin.base;
+        const int* hn = reinterpret_cast<const int*>(hk + (size_t)nb * kCap * sizeof(vs_keypoint));
+        for (int b = f0; b < f0 + m; b++) {
             const int n = hn[b];
             if (n < 0 || n > kCap) {
                 set_error("vs_slam: keypoint count out of range");
@@ -295,9 +367,7 @@ struct GpuOps {
             const auto* kp = reinterpret_cast<const vs_trk::Keypoint*>(hk + (size_t)b * kCap * sizeof(vs_keypoint));
             frames[b]->kps.assign(kp, kp + n);
             frames[b]->mp_idx.assign(n, -1);
-            frames[b]->slot = s0 + b;
         }
-        pin.used = 0;
         return VS_OK;
     }
 
@@ -541,6 +611,15 @@ using namespace vs;
 
 namespace {
 
+// The context's stream is the tracking stream for the duration of a vs_slam call, so the vs_*
+// entry points the back end calls enqueue behind the tracker's own kernels.
+struct CtxStream {
+    vs_ctx* c;
+    hipStream_t old;
+    CtxStream(vs_ctx* cc, hipStream_t st) : c(cc), old(cc->stream) { c->stream = st; }
+    ~CtxStream() { c->stream = old; }
+};
+
 // After a batch (or a single frame): live frames still sitting in a batch-region slot move to
 // persistent slots; dead frames drop their device slot and host working data (the map keeps only
 // their pose for the trajectory).
@@ -606,8 +685,8 @@ int vs_slam_create(vs_ctx* ctx, int max_batch, int h, int w, vs_slam** out) {
 
 void vs_slam_destroy(vs_slam* sl) {
     if (!sl) return;
-    (void)hipStreamSynchronize(sl->ops.s);
     GpuOps& o = sl->ops;
+    o.destroy_streams();
     DevBuf* bufs[] = {&o.pool_kps, &o.pool_desc, &o.pool_n, &o.pool_depth, &o.semi,      &o.dgrid,
                       &o.chain_buf,    &o.work, &o.rows_buf,      &o.map_pos, &o.map_desc,  &o.map_valid, &o.map_tmp};
     for (DevBuf* b : bufs) b->release();
@@ -640,6 +719,7 @@ int vs_slam_process_batch_dev(vs_slam* sl, int B, const uint8_t* d_bgr, const fl
     VS_ARG(!d_depth == !h_depth, "vs_slam_process_batch_dev: depth must be given on both sides or neither");
     GpuOps& o = sl->ops;
     VS_HIP(hipSetDevice(o.ctx->device));
+    CtxStream use(o.ctx, o.s);
     sl->batch.clear();
     for (int b = 0; b < B; b++) {
         auto f = std::make_shared<vs_trk::Frame>();
@@ -650,14 +730,19 @@ int vs_slam_process_batch_dev(vs_slam* sl, int B, const uint8_t* d_bgr, const fl
         f->depth = h_depth ? h_depth[b] : nullptr;
         sl->batch.push_back(f);
     }
-    VS_CHECK(o.extract_batch(sl->batch, d_bgr, d_depth));
-    for (int b = 0; b < B; b++) {
+    int rc = o.extract_batch(sl->batch, d_bgr, d_depth);
+    for (int b = 0; b < B && rc == VS_OK; b++) {
+        if (b % kXChunk == 0) rc = o.wait_chunk(sl->batch, b / kXChunk);
+        if (rc != VS_OK) break;
         processed[b] = sl->trk->process_frame(sl->batch[b]) ? 1 : 0;
         if (o.err != VS_OK) {
-            int rc = o.err;
+            rc = o.err;
             o.err = VS_OK;
-            return rc;
         }
+    }
+    if (rc != VS_OK) {
+        (void)hipStreamSynchronize(o.xs);  // nothing may still write the pool after an error
+        return rc;
     }
     return settle(sl);
 }
@@ -668,6 +753,7 @@ int vs_slam_process_features(vs_slam* sl, int n_kp, const vs_keypoint* kps, cons
     VS_ARG(n_kp == 0 || (kps && desc), "vs_slam_process_features: null features");
     GpuOps& o = sl->ops;
     VS_HIP(hipSetDevice(o.ctx->device));
+    CtxStream use(o.ctx, o.s);
     auto f = std::make_shared<vs_trk::Frame>();
     f->id = id;
     f->timestamp = timestamp;
