@@ -15,6 +15,8 @@
 // match, the visibility sweep and the map appends.  Everything runs on the context's stream.
 #include <hip/hip_runtime.h>
 
+#include <chrono>
+#include <cstdio>
 #include <cstdlib>
 
 #include <algorithm>
@@ -133,8 +135,36 @@ constexpr size_t kChainBytes = kChainRaw + (size_t)kCap * sizeof(vs_match);
 // extraction stream while the tracker consumes the chunks already done (process_batch_dev).
 constexpr int kXChunk = 8;
 
+// Host-side wall time per back-end operation (VS_SLAM_HOST_PROFILE=1: printed to stderr when the
+// vs_slam is destroyed); the rest of process_frame is the tracker's own host logic.
+enum HostOp { kHChain, kHMatch, kHFmat, kHMotion, kHTlm, kHPnp, kHMatchMap, kHAppend, kHVis, kHFrame, kHWait, kHOps };
+static const char* const kHostOpNames[kHOps] = {"chain", "match", "find_fundamental", "motion_points",
+                                                "track_local_map", "solve_pnp", "match_map", "map_append",
+                                                "visibility", "process_frame (total)", "extract wait"};
+struct HostProf {
+    bool on = false;
+    long skip = 64;  // frames before counting starts (first launches load code objects)
+    double ms[kHOps] = {};
+    long n[kHOps] = {};
+};
+struct HostTimer {
+    HostProf& p;
+    int k;
+    std::chrono::steady_clock::time_point t0;
+    HostTimer(HostProf& pp, int kk) : p(pp), k(kk) {
+        if (p.on) t0 = std::chrono::steady_clock::now();
+    }
+    ~HostTimer() {
+        if (!p.on) return;
+        p.ms[k] += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+        p.n[k]++;
+    }
+};
+
 struct GpuOps {
     vs_ctx* ctx = nullptr;
+    HostProf hprof;
+    bool hprof_armed = false;
     hipStream_t s = nullptr;   // tracking stream (the context's stream is swapped to it during vs_slam calls)
     hipStream_t xs = nullptr;  // extraction stream
     bool own_streams = false;
@@ -196,6 +226,9 @@ struct GpuOps {
     int init(vs_ctx* c, int max_batch, int hh, int ww) {
         ctx = c;
         VS_CHECK(make_streams());
+        const char* hp = std::getenv("VS_SLAM_HOST_PROFILE");
+        hprof.on = hp && hp[0] == '1';
+        if (hprof.on) hprof.on = false, hprof.skip = 64, hprof_armed = true;
         B = max_batch;
         h = hh;
         w = ww;
@@ -212,6 +245,9 @@ struct GpuOps {
         VS_CHECK(pin.reserve((size_t)4 << 20));
         owner.assign(kPersist, nullptr);
         VS_CHECK(grow_map(1 << 16));
+        // map-sized scratch up front (a later growth would wait for the extraction stream too)
+        VS_CHECK(map_tmp.ensure((size_t)1 << 20));
+        VS_CHECK(work.ensure((size_t)1 << 20));
         return VS_OK;
     }
 
@@ -352,6 +388,7 @@ struct GpuOps {
     // Chunk c of the batch is extracted: its keypoints to the frames, and the tracking stream
     // ordered after it.
     int wait_chunk(std::vector<vs_trk::FramePtr>& frames, int c) {
+        HostTimer ht(hprof, kHWait);
         const int nb = (int)frames.size();
         const int f0 = c * kXChunk, m = std::min(kXChunk, nb - f0);
         VS_HIP(hipEventSynchronize(xev[c]));
@@ -432,10 +469,12 @@ struct GpuOps {
         return R;
     }
     vs_trk::ChainResult chain(const vs_trk::Frame& ref, const vs_trk::Frame& cur, uint32_t seed) {
+        HostTimer ht(hprof, kHChain);
         return chain_impl(ref, cur, seed);
     }
 
     std::vector<vs_trk::Match> match(const vs_trk::Frame& a, const vs_trk::Frame& b, float ratio) {
+        HostTimer ht(hprof, kHMatch);
         std::vector<vs_trk::Match> out;
         char* c = chain_buf.as<char>();
         int* di = reinterpret_cast<int*>(c + kChainInts);
@@ -451,6 +490,7 @@ struct GpuOps {
     }
 
     bool find_fundamental(const std::vector<float>& p1, const std::vector<float>& p2, std::vector<uint8_t>& mask) {
+        HostTimer ht(hprof, kHFmat);
         const int n = (int)(p1.size() / 2);
         mask.assign(std::max(n, 1), 0);
         double F[9];
@@ -463,6 +503,7 @@ struct GpuOps {
 
     vs_trk::ChainResult motion_points(const vs_trk::Frame& ref, const vs_trk::Frame& cur, const std::vector<float>& p1,
                                       const std::vector<float>& p2, uint32_t seed) {
+        HostTimer ht(hprof, kHMotion);
         vs_trk::ChainResult R;
         const int n = (int)(p1.size() / 2);
         if (!ref.depth || !cur.depth) {  // the RGB-D tracker path; monocular callers use vs_estimate_motion
@@ -489,6 +530,7 @@ struct GpuOps {
     // smaller distance, Slam.cpp:460-465, and each takeover adds an observation): start with room
     // for 4 per keypoint and rerun with the exact count when that is exceeded.
     int track_local_map(vs_trk::Map& m, vs_trk::Frame& f, std::vector<std::pair<int, int>>& obs) {
+        HostTimer ht(hprof, kHTlm);
         obs.clear();
         const int nkp = (int)f.kps.size();
         if (failed(sync_valid(m))) return 0;
@@ -522,6 +564,7 @@ struct GpuOps {
     }
 
     vs_trk::PnPResult solve_pnp(const std::vector<float>& obj, const std::vector<float>& img, int iters, int min_inliers) {
+        HostTimer ht(hprof, kHPnp);
         vs_trk::PnPResult r;
         int success = 0;
         if (failed(vs_solve_pnp(ctx, obj.data(), img.data(), (int)(obj.size() / 3), K, iters, min_inliers,
@@ -533,6 +576,7 @@ struct GpuOps {
 
     std::vector<std::pair<int, int>> match_map(const vs_trk::Map& m, const vs_trk::Frame& f, const std::vector<int>& ids,
                                                float ratio) {
+        HostTimer ht(hprof, kHMatchMap);
         std::vector<std::pair<int, int>> out;
         const int n1 = (int)f.kps.size(), n2 = (int)ids.size();
         if (n1 == 0 || n2 < 2) return out;
@@ -561,6 +605,7 @@ struct GpuOps {
     }
 
     void map_append(const vs_trk::Map& m, int first, const vs_trk::Frame& src, const std::vector<int>& rows) {
+        HostTimer ht(hprof, kHAppend);
         const int k = (int)rows.size();
         if (failed(grow_map(first + k))) return;
         if (failed(upload(map_pos.as<double>() + (size_t)3 * first, m.pos.data() + (size_t)3 * first,
@@ -581,6 +626,7 @@ struct GpuOps {
 
     void visibility(const vs_trk::Map& m, const vs_trk::Frame& f, const vs_trk::M3& R, const vs_trk::V3& t,
                     std::vector<uint8_t>& flags) {
+        HostTimer ht(hprof, kHVis);
         const int n = m.size();
         flags.assign(n, 0);
         if (n == 0) return;
@@ -686,6 +732,11 @@ int vs_slam_create(vs_ctx* ctx, int max_batch, int h, int w, vs_slam** out) {
 void vs_slam_destroy(vs_slam* sl) {
     if (!sl) return;
     GpuOps& o = sl->ops;
+    if (o.hprof.on)
+        for (int k = 0; k < kHOps; k++)
+            if (o.hprof.n[k])
+                std::fprintf(stderr, "vs_slam host %-22s %8ld calls %10.3f ms  %8.1f us/call\n", kHostOpNames[k],
+                             o.hprof.n[k], o.hprof.ms[k], 1e3 * o.hprof.ms[k] / o.hprof.n[k]);
     o.destroy_streams();
     DevBuf* bufs[] = {&o.pool_kps, &o.pool_desc, &o.pool_n, &o.pool_depth, &o.semi,      &o.dgrid,
                       &o.chain_buf,    &o.work, &o.rows_buf,      &o.map_pos, &o.map_desc,  &o.map_valid, &o.map_tmp};
@@ -734,7 +785,11 @@ int vs_slam_process_batch_dev(vs_slam* sl, int B, const uint8_t* d_bgr, const fl
     for (int b = 0; b < B && rc == VS_OK; b++) {
         if (b % kXChunk == 0) rc = o.wait_chunk(sl->batch, b / kXChunk);
         if (rc != VS_OK) break;
-        processed[b] = sl->trk->process_frame(sl->batch[b]) ? 1 : 0;
+        if (o.hprof_armed && --o.hprof.skip < 0) o.hprof.on = true, o.hprof_armed = false;
+        {
+            HostTimer ht(o.hprof, kHFrame);
+            processed[b] = sl->trk->process_frame(sl->batch[b]) ? 1 : 0;
+        }
         if (o.err != VS_OK) {
             rc = o.err;
             o.err = VS_OK;

@@ -3,6 +3,8 @@
 // points (enqueue only).  Each entry point cites the reference interface it replaces.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include <cfloat>
 #include <cmath>
 #include <cstdio>
@@ -25,12 +27,14 @@ const LayerDef kLayers[12] = {{"conv1a", 1, 64, 3},    {"conv1b", 64, 64, 3},   
 
 int DevBuf::ensure(size_t n) {
     if (n <= bytes && p) return VS_OK;
+    // Geometric growth: buffers that follow the map (tracking scratch) reallocate O(log n) times,
+    // and each hipFree waits for all outstanding device work, including other streams'.
+    size_t alloc = std::max(n + n / 8 + 256, 2 * bytes);
     if (p) {
         (void)hipFree(p);  // hipFree waits for outstanding device work
         p = nullptr;
         bytes = 0;
     }
-    size_t alloc = n + n / 8 + 256;
     if (hipMalloc(&p, alloc) != hipSuccess) {
         p = nullptr;
         set_error("hipMalloc of " + std::to_string(alloc) + " bytes failed");
