@@ -131,9 +131,12 @@ constexpr size_t kChainKept = kChainGood + (size_t)kCap * sizeof(vs_match);
 constexpr size_t kChainRaw = kChainKept + (size_t)kCap * sizeof(vs_match);
 constexpr size_t kChainBytes = kChainRaw + (size_t)kCap * sizeof(vs_match);
 
-// Frames per extraction chunk: the batch's network + post-processing runs chunk by chunk on the
-// extraction stream while the tracker consumes the chunks already done (process_batch_dev).
+// Extraction chunks: the batch's network + post-processing runs chunk by chunk on the extraction
+// stream while the tracker consumes the chunks already done (process_batch_dev).  The first chunk
+// is small (nothing hides its latency) and the sizes grow by ~1.5x up to kXChunk, about as fast as
+// tracking a chunk outlasts extracting the next.
 constexpr int kXChunk = 8;
+constexpr int kXFirst = 2;
 
 // Host-side wall time per back-end operation (VS_SLAM_HOST_PROFILE=1: printed to stderr when the
 // vs_slam is destroyed); the rest of process_frame is the tracker's own host logic.
@@ -169,6 +172,8 @@ struct GpuOps {
     hipStream_t xs = nullptr;  // extraction stream
     bool own_streams = false;
     std::vector<hipEvent_t> xev;  // one per extraction chunk
+    std::vector<int> xch;         // chunk boundaries (frame index of each chunk's first frame, then nb)
+    int first_chunk = kXFirst;    // VS_SLAM_FIRST_CHUNK overrides
     Pinned xpin;                  // keypoints / counts of the batch being extracted
     int B = 0, h = 0, w = 0, S = 0, batch_region = 0;
     double K[4] = {vs_trk::cfg::FX, vs_trk::cfg::FY, vs_trk::cfg::CX, vs_trk::cfg::CY};
@@ -226,6 +231,7 @@ struct GpuOps {
     int init(vs_ctx* c, int max_batch, int hh, int ww) {
         ctx = c;
         VS_CHECK(make_streams());
+        if (const char* fc = std::getenv("VS_SLAM_FIRST_CHUNK")) first_chunk = std::max(1, std::min(kXChunk, std::atoi(fc)));
         const char* hp = std::getenv("VS_SLAM_HOST_PROFILE");
         hprof.on = hp && hp[0] == '1';
         if (hprof.on) hprof.on = false, hprof.skip = 64, hprof_armed = true;
@@ -356,7 +362,10 @@ struct GpuOps {
         const int nb = (int)frames.size();
         const int s0 = batch_region * B;
         batch_region ^= 1;
-        const int nch = (nb + kXChunk - 1) / kXChunk;
+        xch.assign(1, 0);
+        for (int c = first_chunk; xch.back() < nb; c = std::min(kXChunk, (3 * c + 1) / 2))
+            xch.push_back(std::min(nb, xch.back() + c));
+        const int nch = (int)xch.size() - 1;
         while ((int)xev.size() < nch) {
             hipEvent_t e;
             VS_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
@@ -367,7 +376,7 @@ struct GpuOps {
         int* hn = reinterpret_cast<int*>(hk + (size_t)nb * kCap * sizeof(vs_keypoint));
         const int hc = (h + 7) / 8, wc = (w + 7) / 8;
         for (int c = 0; c < nch; c++) {
-            const int f0 = c * kXChunk, m = std::min(kXChunk, nb - f0);
+            const int f0 = xch[c], m = xch[c + 1] - xch[c];
             VS_CHECK(sp_forward(ctx, m, d_bgr + (size_t)f0 * h * w * 3, 3, h, w, xs, semi.as<float>(),
                                 dgrid.as<float>()));
             VS_CHECK(sp_postprocess(ctx, m, hc, wc, h, w, kps_of(s0 + f0), desc_of(s0 + f0), pool_n.as<int>() + s0 + f0,
@@ -390,7 +399,7 @@ struct GpuOps {
     int wait_chunk(std::vector<vs_trk::FramePtr>& frames, int c) {
         HostTimer ht(hprof, kHWait);
         const int nb = (int)frames.size();
-        const int f0 = c * kXChunk, m = std::min(kXChunk, nb - f0);
+        const int f0 = xch[c], m = xch[c + 1] - xch[c];
         VS_HIP(hipEventSynchronize(xev[c]));
         VS_HIP(hipStreamWaitEvent(s, xev[c], 0));
         const char* hk = xpin.base;
@@ -782,8 +791,8 @@ int vs_slam_process_batch_dev(vs_slam* sl, int B, const uint8_t* d_bgr, const fl
         sl->batch.push_back(f);
     }
     int rc = o.extract_batch(sl->batch, d_bgr, d_depth);
-    for (int b = 0; b < B && rc == VS_OK; b++) {
-        if (b % kXChunk == 0) rc = o.wait_chunk(sl->batch, b / kXChunk);
+    for (int b = 0, c = 0; b < B && rc == VS_OK; b++) {
+        if (b == o.xch[c]) rc = o.wait_chunk(sl->batch, c++);
         if (rc != VS_OK) break;
         if (o.hprof_armed && --o.hprof.skip < 0) o.hprof.on = true, o.hprof_armed = false;
         {
