@@ -20,7 +20,9 @@ frames, matches consecutive pairs and runs F verification + 3D-3D (+E) per pair 
 with N > 1 the per-frame feature records are all-gathered over RCCL every step.
 
 roofline — the dominant throughput-bound kernel (the fused SuperPoint conv1, fp32 MFMA) measured
-with HIP events on its stream during the timed region; the latency-bound tracking stages are
+with HIP events on its stream during the timed region (the tracker extracts each batch in growing
+chunks on its own stream and CU set, overlapped with tracking; FLOPs per launch = per-frame FLOPs x
+frames per launch); the latency-bound tracking stages are
 reported per frame in stage_ms_per_frame.  cpu_baseline — the oracle (CPU restatement: OpenMP
 SuperPoint + the same tracking loop over the CPU stages) on a bounded prefix of the same sequence.
 
@@ -250,13 +252,18 @@ def main():
     conv = {k: v for k, v in prof.items() if k in LAYER_FLOPS}
     dom = max(conv, key=lambda k: conv[k][0])
     dom_ms, dom_launches = conv[dom]
+    # the tracker extracts each batch in chunks (2, 3, 5, 8, 8, 6 frames at B = 32) overlapped
+    # with tracking, so a launch covers frames_timed / launches frames on average
     avg_s = dom_ms / 1e3 / dom_launches
-    flops_per_launch = LAYER_FLOPS[dom] * B
+    frames_per_launch = frames_timed / dom_launches
+    flops_per_launch = LAYER_FLOPS[dom] * frames_per_launch
     achieved = flops_per_launch / avg_s / 1e12
     net_ms = sum(v[0] for k, v in prof.items() if k in LAYER_FLOPS)
     net_flops = sum(LAYER_FLOPS.values()) * frames_timed
     stage_ms = {k: round(v[0] / frames_timed, 4) for k, v in sorted(prof.items(), key=lambda kv: -kv[1][0])}
     traffic, traffic_tag = pmc_traffic(STAGE_KERNEL.get(dom, ""), B)
+    if traffic is not None:  # PMC pass at B frames per launch -> bytes per average launch here
+        traffic = traffic / B * frames_per_launch
 
     fe = None
     if not args.no_frontend and args.frontend_steps > 0:
@@ -301,10 +308,14 @@ def main():
                 "unit": "TFLOP/s",
                 "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4),
                 "traffic": traffic,
-                "traffic_unit": "HBM bytes per launch (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE)",
+                "traffic_unit": "HBM bytes per launch (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE of the B-frame "
+                                "PMC pass, per frame x frames per launch)",
                 "traffic_source": f"profiles/{traffic_tag}_pmc_traffic.json" if traffic_tag else None,
                 "avg_launch_ms": round(avg_s * 1e3, 4),
-                "flops_per_launch": flops_per_launch,
+                "frames_per_launch": round(frames_per_launch, 3),
+                "flops_per_launch": round(flops_per_launch),
+                "note": "network on the extraction stream's CU set (all CUs but VS_SLAM_TRACK_CUS = 32), "
+                        "overlapped with tracking; peak is the whole chip's",
             },
             "network_tflops": round(net_flops / (net_ms / 1e3) / 1e12, 3),
             "stage_ms_per_frame": stage_ms,
