@@ -178,7 +178,7 @@ struct GpuOps {
     int B = 0, h = 0, w = 0, S = 0, batch_region = 0;
     double K[4] = {vs_trk::cfg::FX, vs_trk::cfg::FY, vs_trk::cfg::CX, vs_trk::cfg::CY};
     DevBuf pool_kps, pool_desc, pool_n, pool_depth, semi, dgrid;
-    DevBuf chain_buf, work, rows_buf, map_pos, map_desc, map_valid, map_tmp;
+    DevBuf chain_buf, work, rows_buf, map_pos, map_desc, map_valid, map_tmp, pnp_io;
     int map_cap = 0, map_n = 0;
     bool valid_dirty = false;
     Pinned pin;
@@ -441,8 +441,12 @@ struct GpuOps {
         double* dd = reinterpret_cast<double*>(c + kChainDbl);
         vs_match* good = reinterpret_cast<vs_match*>(c + kChainGood);
         vs_match* kept = reinterpret_cast<vs_match*>(c + kChainKept);
-        if (failed(upload(di + 2, &seed, sizeof(seed)))) return R;
-        if (failed(enqueue_match(ref.slot, cur.slot, vs_trk::cfg::L2_RATIO_THRESHOLD, di))) return R;
+        const int hdr[3] = {ref.slot, cur.slot, (int)seed};  // pair slots + RANSAC seed, one upload
+        if (failed(upload(di, hdr, sizeof(hdr)))) return R;
+        if (failed(match_pairs(ctx, 1, di, S, pool_desc.as<float>(), pool_n.as<int>(), kCap,
+                               vs_trk::cfg::L2_RATIO_THRESHOLD, reinterpret_cast<vs_match*>(c + kChainRaw), di + 3,
+                               good, di + 4, s)))
+            return R;
         if (failed(fmat_pairs(ctx, 1, di, pool_kps.as<vs_keypoint>(), kCap, good, di + 4, dd, kept, di + 5, dd + 9,
                               di + 8, s)))
             return R;
@@ -572,14 +576,46 @@ struct GpuOps {
         return 0;
     }
 
+    // Slam::solve_pnp on the device: one packed pinned upload (offsets, object and image points),
+    // the PnP kernels, one packed download of (R, t, status).
     vs_trk::PnPResult solve_pnp(const std::vector<float>& obj, const std::vector<float>& img, int iters, int min_inliers) {
         HostTimer ht(hprof, kHPnp);
         vs_trk::PnPResult r;
-        int success = 0;
-        if (failed(vs_solve_pnp(ctx, obj.data(), img.data(), (int)(obj.size() / 3), K, iters, min_inliers,
-                                r.R_world.data(), r.t_world.data(), &success, &r.inlier_count, nullptr, nullptr)))
+        const int n = (int)(obj.size() / 3);
+        if (n == 0) return r;
+        if (iters > VS_PNP_MAX_ITERS) {
+            failed(VS_ERR_ARG);
             return r;
-        r.success = success != 0;
+        }
+        const size_t in_bytes = 16 + (size_t)n * 5 * sizeof(float);
+        const size_t in_pad = (in_bytes + 15) & ~(size_t)15;
+        const size_t out_bytes = 12 * sizeof(double) + 8 * sizeof(int);
+        if (failed(pnp_io.ensure(in_pad + out_bytes + (size_t)n))) return r;
+        char* d = pnp_io.as<char>();
+        char* hb = take(in_bytes);
+        if (!hb) return r;
+        const int off[4] = {0, n, 0, 0};
+        std::memcpy(hb, off, 16);
+        std::memcpy(hb + 16, obj.data(), (size_t)n * 3 * sizeof(float));
+        std::memcpy(hb + 16 + (size_t)n * 3 * sizeof(float), img.data(), (size_t)n * 2 * sizeof(float));
+        if (failed(hipMemcpyAsync(d, hb, in_bytes, hipMemcpyHostToDevice, s) == hipSuccess ? VS_OK : VS_ERR_HIP))
+            return r;
+        double* dRt = reinterpret_cast<double*>(d + in_pad);
+        int* dstat = reinterpret_cast<int*>(dRt + 12);
+        if (failed(vs::solve_pnp(ctx, 1, reinterpret_cast<const float*>(d + 16),
+                                 reinterpret_cast<const float*>(d + 16 + (size_t)n * 3 * sizeof(float)),
+                                 reinterpret_cast<const int*>(d), K, iters, min_inliers, dRt, dRt + 9, dstat,
+                                 reinterpret_cast<uint8_t*>(dstat + 8), s)))
+            return r;
+        char* ho = take(out_bytes);
+        if (!ho || failed(d2h(ho, dRt, out_bytes)) || failed(sync())) return r;
+        const int* st = reinterpret_cast<const int*>(ho + 12 * sizeof(double));
+        r.success = st[0] != 0;
+        r.inlier_count = st[0] ? st[1] : 0;  // PnPResult.inlier_count stays 0 on failure (Slam.cpp:510)
+        if (r.success) {
+            std::memcpy(r.R_world.data(), ho, 9 * sizeof(double));
+            std::memcpy(r.t_world.data(), ho + 9 * sizeof(double), 3 * sizeof(double));
+        }
         return r;
     }
 
@@ -748,7 +784,8 @@ void vs_slam_destroy(vs_slam* sl) {
                              o.hprof.n[k], o.hprof.ms[k], 1e3 * o.hprof.ms[k] / o.hprof.n[k]);
     o.destroy_streams();
     DevBuf* bufs[] = {&o.pool_kps, &o.pool_desc, &o.pool_n, &o.pool_depth, &o.semi,      &o.dgrid,
-                      &o.chain_buf,    &o.work, &o.rows_buf,      &o.map_pos, &o.map_desc,  &o.map_valid, &o.map_tmp};
+                      &o.chain_buf,    &o.work, &o.rows_buf,      &o.map_pos, &o.map_desc,  &o.map_valid, &o.map_tmp,
+                      &o.pnp_io};
     for (DevBuf* b : bufs) b->release();
     delete sl;
 }
