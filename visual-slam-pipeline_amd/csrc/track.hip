@@ -156,106 +156,209 @@ __global__ __launch_bounds__(256) void k_tlm_dist(const float* __restrict__ mp_d
 // Assignment in map-point order (Slam.cpp:460-465), decided in parallel: keypoint ki's best
 // distance is a running minimum over the map points that chose it, so a candidate (map point m
 // with best keypoint ki, distance d) is applied — kp_to_mp[ki] = m, one tracked++ and one
-// add_observation — iff d is strictly below every earlier candidate's distance for ki.  Chunks
-// of 1024 candidates in map-point order: within a chunk each candidate compares against the
-// earlier ones for its keypoint and against the minimum carried from earlier chunks; winners
-// are compacted in order into the observation list.  One 1024-lane workgroup.
+// add_observation — iff d is strictly below every earlier candidate's distance for ki.
 // result[0] = tracked, result[1] = observations produced (all of them, even beyond obs_cap).
-__global__ __launch_bounds__(1024) void k_tlm_resolve(const int* __restrict__ cnt, const int* __restrict__ cand,
-                                                      const double* __restrict__ dist, int n_mp, int nkp, int* __restrict__ kp_to_mp,
-                                                      int* __restrict__ obs_mp, int* __restrict__ obs_kp, int obs_cap,
-                                                      int* __restrict__ result) {
-    __shared__ unsigned long long s_best[kTlmMaxKp];  // bits of the running minimum (d >= 0: order-preserving)
-    __shared__ int s_kpmp[kTlmMaxKp];
-    __shared__ int s_first[kTlmMaxKp];  // first candidate of a keypoint within the chunk
-    __shared__ int s_cmp[1024], s_cki[1024];
-    __shared__ unsigned long long s_cd[1024];
-    __shared__ int s_wcnt[16];
-    __shared__ int s_nobs;
-    const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
-    for (int k = tid; k < nkp; k += 1024) {
-        s_best[k] = (unsigned long long)__double_as_longlong(1e9);
-        s_kpmp[k] = kp_to_mp[k];
-        s_first[k] = INT_MAX;
+//
+// Phase 3a, one lane per map point: its first strictly smaller distance below the threshold in
+// visiting order (:439-456) -> (keypoint or -1, distance).
+// Also the map point's rank among its block's candidates and the block's candidate count, so the
+// resolve kernel places every candidate in map-point order without a serial scan.
+__global__ __launch_bounds__(256) void k_tlm_best(const int* __restrict__ cnt, const int* __restrict__ cand,
+                                                  const double* __restrict__ dist, int n_mp, int* __restrict__ best_ki,
+                                                  double* __restrict__ best_d, int* __restrict__ rank,
+                                                  int* __restrict__ blkcnt) {
+    __shared__ int s_w[4];
+    const int mp = blockIdx.x * 256 + threadIdx.x, wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    int ki0 = -1;
+    double bd = kTlmDesc;
+    if (mp < n_mp) {
+        const int c = cnt[mp];
+        for (int j = 0; j < c; j++) {
+            const double d = dist[(size_t)mp * kTlmMaxCand + j];
+            if (d < bd) {
+                bd = d;
+                ki0 = cand[(size_t)mp * kTlmMaxCand + j];
+            }
+        }
     }
-    if (tid == 0) s_nobs = 0;
+    const unsigned long long bal = __ballot(ki0 >= 0);
+    if (lane == 0) s_w[wv] = __popcll(bal);
     __syncthreads();
-    for (int c0 = 0; c0 < n_mp; c0 += 1024) {
-        // phase 3 for this chunk: each map point's first strictly smaller distance below the
-        // threshold in visiting order (:439-456), then the chunk's candidates compacted in order
-        const int mp = c0 + tid;
-        int ki0 = -1;
-        double bd = kTlmDesc;
-        if (mp < n_mp) {
-            const int c = cnt[mp];
-            for (int j = 0; j < c; j++) {
-                const double d = dist[(size_t)mp * kTlmMaxCand + j];
-                if (d < bd) {
-                    bd = d;
-                    ki0 = cand[(size_t)mp * kTlmMaxCand + j];
-                }
-            }
-        }
-        const bool cand_ok = ki0 >= 0;
-        unsigned long long bal = __ballot(cand_ok);
-        if (lane == 0) s_wcnt[wv] = __popcll(bal);
-        __syncthreads();
-        int off = 0, nc = 0;
-        for (int k = 0; k < 16; k++) {
-            if (k < wv) off += s_wcnt[k];
-            nc += s_wcnt[k];
-        }
-        if (cand_ok) {
-            const int j = off + __popcll(bal & ((1ull << lane) - 1ull));
-            s_cmp[j] = mp;
-            s_cki[j] = ki0;
-            s_cd[j] = (unsigned long long)__double_as_longlong(bd);
-            atomicMin(&s_first[ki0], j);
-        }
-        __syncthreads();
-        // winners: strictly below the carried minimum and below every earlier candidate of the
-        // keypoint (only candidates from the keypoint's first one on can share it)
-        bool win = false;
-        int ki = -1;
-        unsigned long long d = 0;
-        if (tid < nc) {
-            ki = s_cki[tid];
-            d = s_cd[tid];
-            win = d < s_best[ki];
-            for (int j = s_first[ki]; j < tid && win; j++)
-                if (s_cki[j] == ki && s_cd[j] <= d) win = false;
-        }
-        __syncthreads();
-        if (tid < nc) s_first[ki] = INT_MAX;  // every reader is past the barrier above
-        if (win) atomicMin(&s_best[ki], d);
-        bal = __ballot(win);
-        if (lane == 0) s_wcnt[wv] = __popcll(bal);
-        __syncthreads();
-        // the last winner of a keypoint has its smallest distance (winners strictly decrease)
-        if (win && s_best[ki] == d) s_kpmp[ki] = s_cmp[tid];
-        off = 0;
-        int nw = 0;
-        for (int k = 0; k < 16; k++) {
-            if (k < wv) off += s_wcnt[k];
-            nw += s_wcnt[k];
-        }
-        if (win) {
-            const int o = s_nobs + off + __popcll(bal & ((1ull << lane) - 1ull));
-            if (o < obs_cap) {
-                obs_mp[o] = s_cmp[tid];
-                obs_kp[o] = ki;
-            }
-        }
-        __syncthreads();
-        if (tid == 0) s_nobs += nw;
-        __syncthreads();
+    int off = 0;
+    for (int k = 0; k < wv; k++) off += s_w[k];
+    if (mp < n_mp) {
+        best_ki[mp] = ki0;
+        best_d[mp] = bd;
+        rank[mp] = off + __popcll(bal & ((1ull << lane) - 1ull));
     }
-    for (int k = tid; k < nkp; k += 1024) kp_to_mp[k] = s_kpmp[k];
-    if (tid == 0) {
-        result[0] = s_nobs;  // each record is one tracked++ and one add_observation
-        result[1] = s_nobs;
+    if (threadIdx.x == 0) blkcnt[blockIdx.x] = s_w[0] + s_w[1] + s_w[2] + s_w[3];
+}
+
+constexpr int kTlmCandBuf = 4096;  // candidates buffered in LDS between resolve passes
+constexpr int kTlmMaxBlk = 4096;  // map points / 256 handled by the direct placement
+
+struct TlmResolveShared {
+    unsigned long long best[kTlmMaxKp];  // bits of the running minimum (d >= 0: order-preserving)
+    int kpmp[kTlmMaxKp];
+    int first[kTlmMaxKp];  // first buffered candidate of a keypoint in the current pass
+    int cmp[kTlmCandBuf], cki[kTlmCandBuf];
+    unsigned long long cd[kTlmCandBuf];
+    int pre[kTlmMaxBlk];
+    int wcnt[16];
+    int nobs, nc, total;
+};
+
+// One pass over the nc buffered candidates (map-point order): winners are strictly below the
+// carried minimum and below every earlier buffered candidate of the keypoint (a keypoint's
+// candidates start at its first one); the last winner of a keypoint has its smallest distance
+// (winners strictly decrease); observations are compacted in candidate order.
+__device__ void tlm_resolve_pass(TlmResolveShared& S, int nc, int* __restrict__ obs_mp, int* __restrict__ obs_kp,
+                                 int obs_cap) {
+    const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
+    bool win[kTlmCandBuf / 1024];
+#pragma unroll
+    for (int r = 0; r < kTlmCandBuf / 1024; r++) {
+        const int t = r * 1024 + tid;
+        win[r] = false;
+        if (t < nc) {
+            const int ki = S.cki[t];
+            const unsigned long long d = S.cd[t];
+            bool w = d < S.best[ki];
+            for (int j = S.first[ki]; j < t && w; j++)
+                if (S.cki[j] == ki && S.cd[j] <= d) w = false;
+            win[r] = w;
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < kTlmCandBuf / 1024; r++) {
+        const int t = r * 1024 + tid;
+        if (t < nc) {
+            S.first[S.cki[t]] = INT_MAX;  // every reader is past the barrier above
+            if (win[r]) atomicMin(&S.best[S.cki[t]], S.cd[t]);
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < kTlmCandBuf / 1024; r++) {
+        if (r * 1024 >= nc) break;  // uniform
+        const int t = r * 1024 + tid;
+        const bool w = win[r];
+        if (w && S.best[S.cki[t]] == S.cd[t]) S.kpmp[S.cki[t]] = S.cmp[t];
+        const unsigned long long wb = __ballot(w);
+        if (lane == 0) S.wcnt[wv] = __popcll(wb);
+        __syncthreads();
+        int o = S.nobs, nw = 0;
+        for (int k = 0; k < 16; k++) {
+            if (k < wv) o += S.wcnt[k];
+            nw += S.wcnt[k];
+        }
+        if (w) {
+            o += __popcll(wb & ((1ull << lane) - 1ull));
+            if (o < obs_cap) {
+                obs_mp[o] = S.cmp[t];
+                obs_kp[o] = S.cki[t];
+            }
+        }
+        __syncthreads();
+        if (tid == 0) S.nobs += nw;
+        __syncthreads();
     }
 }
+
+// Phase 3b: the assignment in map-point order (Slam.cpp:460-465).  The candidates (k_tlm_best)
+// go to an LDS buffer in map-point order -- directly at block prefix + rank when they all fit,
+// else 1024 map points at a time with a pass whenever the buffer could overflow.
+__global__ __launch_bounds__(1024) void k_tlm_resolve(const int* __restrict__ best_ki, const double* __restrict__ best_d,
+                                                      const int* __restrict__ rank, const int* __restrict__ blkcnt,
+                                                      int n_mp, int nkp, int* __restrict__ kp_to_mp,
+                                                      int* __restrict__ obs_mp, int* __restrict__ obs_kp, int obs_cap,
+                                                      int* __restrict__ result) {
+    __shared__ TlmResolveShared S;
+    const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
+    const int nblk = (n_mp + 255) / 256;
+    for (int k = tid; k < nkp; k += 1024) {
+        S.best[k] = (unsigned long long)__double_as_longlong(1e9);
+        S.kpmp[k] = kp_to_mp[k];
+        S.first[k] = INT_MAX;
+    }
+    if (tid == 0) {
+        S.nobs = S.nc = 0;
+        S.total = INT_MAX;
+    }
+    if (nblk <= kTlmMaxBlk) {
+        for (int b = tid; b < nblk; b += 1024) S.pre[b] = blkcnt[b];
+        __syncthreads();
+        if (tid == 0) {
+            int acc = 0;
+            for (int b = 0; b < nblk; b++) {
+                const int c = S.pre[b];
+                S.pre[b] = acc;
+                acc += c;
+            }
+            S.total = acc;
+        }
+    }
+    __syncthreads();
+    if (S.total <= kTlmCandBuf) {
+        for (int m0 = 0; m0 < n_mp; m0 += 16 * 1024) {
+            int kis[16];  // all loads of the round issued before any is used (latency, not bandwidth)
+#pragma unroll
+            for (int u = 0; u < 16; u++) {
+                const int mp = m0 + u * 1024 + tid;
+                kis[u] = mp < n_mp ? best_ki[mp] : -1;
+            }
+#pragma unroll
+            for (int u = 0; u < 16; u++) {
+                const int mp = m0 + u * 1024 + tid;
+                if (kis[u] < 0) continue;
+                const int j = S.pre[mp >> 8] + rank[mp];
+                S.cmp[j] = mp;
+                S.cki[j] = kis[u];
+                S.cd[j] = (unsigned long long)__double_as_longlong(best_d[mp]);
+                atomicMin(&S.first[kis[u]], j);
+            }
+        }
+        __syncthreads();
+        tlm_resolve_pass(S, S.total, obs_mp, obs_kp, obs_cap);
+    } else {
+        for (int c0 = 0; c0 < n_mp; c0 += 1024) {
+            const int mp = c0 + tid;
+            const int ki0 = mp < n_mp ? best_ki[mp] : -1;
+            const bool cand_ok = ki0 >= 0;
+            const unsigned long long bal = __ballot(cand_ok);
+            if (lane == 0) S.wcnt[wv] = __popcll(bal);
+            __syncthreads();
+            int off = S.nc, add = 0;
+            for (int k = 0; k < 16; k++) {
+                if (k < wv) off += S.wcnt[k];
+                add += S.wcnt[k];
+            }
+            if (cand_ok) {
+                const int j = off + __popcll(bal & ((1ull << lane) - 1ull));
+                S.cmp[j] = mp;
+                S.cki[j] = ki0;
+                S.cd[j] = (unsigned long long)__double_as_longlong(best_d[mp]);
+                atomicMin(&S.first[ki0], j);
+            }
+            __syncthreads();
+            const int nc = S.nc + add;
+            if (tid == 0) S.nc = nc;
+            __syncthreads();
+            if (nc + 1024 <= kTlmCandBuf && c0 + 1024 < n_mp) continue;  // uniform
+            tlm_resolve_pass(S, nc, obs_mp, obs_kp, obs_cap);
+            if (tid == 0) S.nc = 0;
+            __syncthreads();
+        }
+    }
+    __syncthreads();
+    for (int k = tid; k < nkp; k += 1024) kp_to_mp[k] = S.kpmp[k];
+    if (tid == 0) {
+        result[0] = S.nobs;  // each record is one tracked++ and one add_observation
+        result[1] = S.nobs;
+    }
+}
+
 
 int track_local_map(vs_ctx* ctx, const double* d_mp_pos, const float* d_mp_desc, const uint8_t* d_mp_valid, int n_mp,
                     const vs_keypoint* d_kps, const float* d_desc, int nkp, const double R[9], const double t[3],
@@ -267,14 +370,20 @@ int track_local_map(vs_ctx* ctx, const double* d_mp_pos, const float* d_mp_desc,
            "track_local_map: image too large for the keypoint grid");
     const int GW = (img_w + kTlmCell - 1) / kTlmCell, GH = (img_h + kTlmCell - 1) / kTlmCell;
     const size_t grid_bytes = (size_t)(GW * GH + 1) * sizeof(int) + (size_t)(nkp + 1) * sizeof(int);
-    const size_t per_mp = sizeof(int) + (size_t)kTlmMaxCand * (sizeof(int) + sizeof(double));
-    VS_CHECK(ctx->tlm.ensure(grid_bytes + 16 + (size_t)(n_mp + 1) * per_mp));
+    const size_t per_mp = 3 * sizeof(int) + sizeof(double) + (size_t)kTlmMaxCand * (sizeof(int) + sizeof(double));
+    const int nblk = (n_mp + 255) / 256;
+    VS_CHECK(ctx->tlm.ensure(grid_bytes + 64 + (size_t)(n_mp + 1) * per_mp + (size_t)(nblk + 1) * sizeof(int)));
     char* base = static_cast<char*>(ctx->tlm.p);
     int* start = reinterpret_cast<int*>(base);
     int* items = start + GW * GH + 1;
     double* dist = reinterpret_cast<double*>(base + ((grid_bytes + 15) / 16) * 16);
     int* cand = reinterpret_cast<int*>(dist + (size_t)(n_mp + 1) * kTlmMaxCand);
     int* cnt = cand + (size_t)(n_mp + 1) * kTlmMaxCand;
+    int* best_ki = cnt + (n_mp + 1);
+    int* rank = best_ki + (n_mp + 1);
+    int* blkcnt = rank + (n_mp + 1);
+    double* best_d =
+        reinterpret_cast<double*>(base + (((size_t)(reinterpret_cast<char*>(blkcnt + nblk + 1) - base) + 15) / 16) * 16);
     TlmPose T;
     for (int i = 0; i < 3; i++)
         for (int j = 0; j < 3; j++) T.Rc[i * 3 + j] = R[j * 3 + i];
@@ -294,8 +403,11 @@ int track_local_map(vs_ctx* ctx, const double* d_mp_pos, const float* d_mp_desc,
         hipLaunchKernelGGL(k_tlm_dist, dim3((unsigned)((pairs + 255) / 256)), dim3(256), 0, s, d_mp_desc, d_desc, n_mp,
                            cnt, cand, dist);
     }
-    hipLaunchKernelGGL(k_tlm_resolve, dim3(1), dim3(1024), 0, s, cnt, cand, dist, n_mp, nkp, d_kp_to_mp, d_obs_mp,
-                       d_obs_kp, obs_cap, d_result);
+    if (n_mp > 0)
+        hipLaunchKernelGGL(k_tlm_best, dim3(nblk), dim3(256), 0, s, cnt, cand, dist, n_mp, best_ki, best_d, rank,
+                           blkcnt);
+    hipLaunchKernelGGL(k_tlm_resolve, dim3(1), dim3(1024), 0, s, best_ki, best_d, rank, blkcnt, n_mp, nkp, d_kp_to_mp,
+                       d_obs_mp, d_obs_kp, obs_cap, d_result);
     VS_HIP(hipGetLastError());
     return VS_OK;
 }
