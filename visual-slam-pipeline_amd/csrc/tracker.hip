@@ -138,6 +138,42 @@ constexpr size_t kChainBytes = kChainRaw + (size_t)kCap * sizeof(vs_match);
 constexpr int kXChunk = 8;
 constexpr int kXFirst = 2;
 
+// The PnP input of Slam::refine_pose_via_local_pnp (tracked_points, :1408-1420) straight from the
+// local-map tracking result: keypoints (in order) whose map point is valid, as float object
+// points and image points; io = [off {0, n, 0, 0} | obj cap x 3 | img cap x 2].  One workgroup.
+__global__ __launch_bounds__(1024) void k_pnp_gather(const int* __restrict__ kpmp, int nkp, const double* __restrict__ pos,
+                                                     const uint8_t* __restrict__ valid, int n_mp,
+                                                     const vs_keypoint* __restrict__ kps, int cap, float* __restrict__ io) {
+    __shared__ int s_w[16];
+    const int i = threadIdx.x, wv = i >> 6, lane = i & 63;
+    const int id = i < nkp ? kpmp[i] : -1;
+    const bool use = id >= 0 && id < n_mp && valid[id];
+    const unsigned long long bal = __ballot(use);
+    if (lane == 0) s_w[wv] = __popcll(bal);
+    __syncthreads();
+    int o = 0, n = 0;
+    for (int k = 0; k < 16; k++) {
+        if (k < wv) o += s_w[k];
+        n += s_w[k];
+    }
+    float* obj = io + 4;
+    float* img = obj + 3 * cap;
+    if (use) {
+        o += __popcll(bal & ((1ull << lane) - 1ull));
+        obj[3 * o] = (float)pos[3 * id];
+        obj[3 * o + 1] = (float)pos[3 * id + 1];
+        obj[3 * o + 2] = (float)pos[3 * id + 2];
+        img[2 * o] = kps[i].x;
+        img[2 * o + 1] = kps[i].y;
+    }
+    if (i == 0) {
+        int* off = reinterpret_cast<int*>(io);
+        off[0] = 0;
+        off[1] = n;
+        off[2] = off[3] = 0;
+    }
+}
+
 // Host-side wall time per back-end operation (VS_SLAM_HOST_PROFILE=1: printed to stderr when the
 // vs_slam is destroyed); the rest of process_frame is the tracker's own host logic.
 enum HostOp { kHChain, kHMatch, kHFmat, kHMotion, kHTlm, kHPnp, kHMatchMap, kHAppend, kHVis, kHFrame, kHWait, kHOps };
@@ -168,6 +204,10 @@ struct GpuOps {
     vs_ctx* ctx = nullptr;
     HostProf hprof;
     bool hprof_armed = false;
+    // speculative PnP of the tracked points, run right behind local-map tracking (see solve_pnp)
+    bool spec_valid = false;
+    vs_trk::PnPResult spec;
+    std::vector<float> spec_obj, spec_img;
     hipStream_t s = nullptr;   // tracking stream (the context's stream is swapped to it during vs_slam calls)
     hipStream_t xs = nullptr;  // extraction stream
     bool own_streams = false;
@@ -561,8 +601,45 @@ struct GpuOps {
                                                 vs_trk::cfg::IMAGE_HEIGHT, d_kpmp, d_obs, d_obs + obs_cap, obs_cap, d,
                                                 s)))
                 return 0;
+            // Speculatively, the refinement's PnP on the tracked points right behind it (the
+            // tracker calls solve_pnp on exactly these next, Slam.cpp:1057-1059; solve_pnp checks).
+            spec_valid = false;
+            const int cap = std::max(nkp, 1);
+            const size_t io_bytes = 16 + (size_t)cap * 5 * sizeof(float), io_pad = (io_bytes + 15) & ~(size_t)15;
+            const size_t spec_bytes = io_pad + 12 * sizeof(double) + 8 * sizeof(int);
+            char* hs = nullptr;
+            if (nkp > 0 && nkp <= 1024 && pnp_io.ensure(spec_bytes + (size_t)cap) == VS_OK) {
+                char* io = pnp_io.as<char>();
+                hipLaunchKernelGGL(k_pnp_gather, dim3(1), dim3(1024), 0, s, d_kpmp, nkp, map_pos.as<double>(),
+                                   map_valid.as<uint8_t>(), m.size(), kps_of(f.slot), cap, reinterpret_cast<float*>(io));
+                double* dRt = reinterpret_cast<double*>(io + io_pad);
+                int* dstat = reinterpret_cast<int*>(dRt + 12);
+                if (vs::solve_pnp(ctx, 1, reinterpret_cast<const float*>(io + 16),
+                                  reinterpret_cast<const float*>(io + 16 + (size_t)cap * 3 * sizeof(float)),
+                                  reinterpret_cast<const int*>(io), K, 100, 10, dRt, dRt + 9, dstat,
+                                  reinterpret_cast<uint8_t*>(dstat + 8), s) == VS_OK) {
+                    hs = take(spec_bytes);
+                    if (hs && failed(d2h(hs, io, spec_bytes))) hs = nullptr;
+                }
+            }
             int* hb = reinterpret_cast<int*>(take((size_t)words * sizeof(int)));
             if (!hb || failed(d2h(hb, d, (size_t)words * sizeof(int))) || failed(sync())) return 0;
+            if (hs) {
+                const int n = reinterpret_cast<const int*>(hs)[1];
+                const float* so = reinterpret_cast<const float*>(hs + 16);
+                spec_obj.assign(so, so + (size_t)3 * n);
+                spec_img.assign(so + (size_t)3 * cap, so + (size_t)3 * cap + (size_t)2 * n);
+                const double* Rt = reinterpret_cast<const double*>(hs + io_pad);
+                const int* st = reinterpret_cast<const int*>(Rt + 12);
+                spec = vs_trk::PnPResult();
+                spec.success = n > 0 && st[0] != 0;
+                spec.inlier_count = spec.success ? st[1] : 0;
+                if (spec.success) {
+                    std::memcpy(spec.R_world.data(), Rt, 9 * sizeof(double));
+                    std::memcpy(spec.t_world.data(), Rt + 9, 3 * sizeof(double));
+                }
+                spec_valid = true;
+            }
             const int n_obs = hb[1];
             if (n_obs > obs_cap) {  // rerun from the same inputs with room for every observation
                 obs_cap = n_obs;
@@ -580,6 +657,10 @@ struct GpuOps {
     // the PnP kernels, one packed download of (R, t, status).
     vs_trk::PnPResult solve_pnp(const std::vector<float>& obj, const std::vector<float>& img, int iters, int min_inliers) {
         HostTimer ht(hprof, kHPnp);
+        if (spec_valid) {  // the speculative run had exactly these inputs: its result is this call's
+            spec_valid = false;
+            if (iters == 100 && min_inliers == 10 && obj == spec_obj && img == spec_img) return spec;
+        }
         vs_trk::PnPResult r;
         const int n = (int)(obj.size() / 3);
         if (n == 0) return r;
