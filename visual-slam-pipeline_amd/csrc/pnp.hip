@@ -1,16 +1,19 @@
 // pnp.hip — Slam::solve_pnp (reference src/Slam.cpp:505-529: cv::solvePnPRansac, 8 px,
 // confidence 0.99, then R_world = R_cam^T, t_world = -R_cam^T tvec) on gfx950.
 //
-// One workgroup (4 wave64s) per PnP problem; a batch of problems (frames, or the periodic /
-// recovery / loop callers) is one grid.  The OpenCV RANSAC loop is sequential only through its
-// adaptive iteration budget, and that budget only shrinks, so the workgroup
-//   1. draws every subset of the initial budget with the cv::RNG stream (lane 0; the stream does
-//      not depend on the models because checkSubset is trivially true for PnP),
-//   2. solves the EPnP hypotheses and counts their inliers in parallel, one hypothesis per lane,
-//   3. replays the accept / RANSACUpdateNumIters sequence on lane 0 over the counts — exactly
-//      the hypotheses the sequential loop would have evaluated, in its order,
-//   4. re-solves the winning subset, marks the inliers, and refines (rvec, tvec) with the LM of
-//      pnp_solvers.h, the 28 normal-equation sums reduced deterministically over the lanes.
+// A batch of problems (frames, or the periodic / recovery / loop callers) is one grid per stage.
+// The OpenCV RANSAC loop is sequential only through its adaptive iteration budget, and that
+// budget only shrinks, so
+//   1. k_pnp_subsets draws every subset of the initial budget from the cv::RNG stream (one
+//      workgroup per problem; jump-ahead + pointer doubling, the stream does not depend on the
+//      models because checkSubset is trivially true for PnP),
+//   2. k_pnp_hyp solves the EPnP hypotheses and counts their inliers, one wave64 per hypothesis
+//      (solving only a first wave of 16 and the rest on demand was tried: with this data the
+//      budget rarely ends inside 16 iterations, and the two serialized waves cost 50 % more),
+//   3. k_pnp_ransac replays the accept / RANSACUpdateNumIters sequence over the counts — exactly
+//      the hypotheses the sequential loop would have evaluated, in its order — marks the winner's
+//      inliers and refines (rvec, tvec) with the LM of pnp_solvers.h, the 28 normal-equation sums
+//      reduced in a fixed lane / butterfly order that the oracle restates.
 // Numerical kernels are shared with the CPU restatement (pnp_solvers.h; this file is built
 // with -ffp-contract=off like the oracle).
 #include <hip/hip_runtime.h>
