@@ -217,8 +217,7 @@ __global__ __launch_bounds__(64) void k_pnp_hyp(const float* __restrict__ obj_al
     __shared__ double sA[144], sV[144];
     __shared__ double sX[15], sUV[10], sAl[5][4], sCw[4][3];
     __shared__ double sTot, sOff, sErr[3], sRt[3][12];
-    __shared__ double sC[6], sS[6];
-    __shared__ int sOk, sAct[6];
+    __shared__ int sOk;
     const int pb = blockIdx.x, h = blockIdx.y, lane = threadIdx.x;
     const int o0 = off[pb], n = off[pb + 1] - o0;
     const int model_points = n == 4 ? 4 : 5;
@@ -273,61 +272,75 @@ __global__ __launch_bounds__(64) void k_pnp_hyp(const float* __restrict__ obj_al
             }
             __syncthreads();
             if (!(sOff > 1e-32 * total)) break;
+            // Each lane of 0..35 keeps one 2 x 2 block of A in registers for the round: (pair a rows
+            // i0 < i1, pair b columns j0 < j1), a = lane / 6, b = lane % 6.  The diagonal-block lanes
+            // (a == b) compute the round's angles from their registers and shuffle them out; every
+            // block takes its column rotation (b) and then its row rotation (a) -- per element exactly
+            // the sequential statement's column-then-row order; V's rows take their column rotations
+            // in LDS; the blocks go back to the LDS matrix and the next round's blocks are read.
+            const int ba = lane / 6, bb = lane % 6;
+            const bool blk = lane < 36;
+            int i0, i1, j0, j1;
+            double x00 = 0, x01 = 0, x10 = 0, x11 = 0;
+            if (blk) {
+                rr_pair(12, 0, ba, i0, i1);
+                rr_pair(12, 0, bb, j0, j1);
+                x00 = sA[i0 * 12 + j0];
+                x01 = sA[i0 * 12 + j1];
+                x10 = sA[i1 * 12 + j0];
+                x11 = sA[i1 * 12 + j1];
+            }
             for (int r = 0; r < 11; r++) {
-                if (lane < 6) {  // angles from the matrix as the round starts
-                    int p, q;
-                    rr_pair(12, r, lane, p, q);
-                    double c = 1.0, sn = 0.0;
-                    sAct[lane] = jacobi_angle(sA[p * 12 + p], sA[q * 12 + q], sA[p * 12 + q], c, sn);
-                    sC[lane] = c;
-                    sS[lane] = sn;
+                double c = 1.0, sn = 0.0;
+                int act = 0;
+                if (blk && ba == bb) act = jacobi_angle(x00, x11, x01, c, sn);  // (A[p][p], A[q][q], A[p][q])
+                const double ca = __shfl(c, 7 * ba), sa = __shfl(sn, 7 * ba);
+                const double cb = __shfl(c, 7 * bb), sb = __shfl(sn, 7 * bb);
+                const int acta = __shfl(act, 7 * ba), actb = __shfl(act, 7 * bb);
+                if (blk) {
+                    if (actb) {
+                        const double y00 = cb * x00 - sb * x01, y01 = sb * x00 + cb * x01;
+                        const double y10 = cb * x10 - sb * x11, y11 = sb * x10 + cb * x11;
+                        x00 = y00;
+                        x01 = y01;
+                        x10 = y10;
+                        x11 = y11;
+                    }
+                    if (acta) {
+                        const double y00 = ca * x00 - sa * x10, y10 = sa * x00 + ca * x10;
+                        const double y01 = ca * x01 - sa * x11, y11 = sa * x01 + ca * x11;
+                        x00 = y00;
+                        x01 = y01;
+                        x10 = y10;
+                        x11 = y11;
+                    }
+                    sA[i0 * 12 + j0] = x00;
+                    sA[i0 * 12 + j1] = x01;
+                    sA[i1 * 12 + j0] = x10;
+                    sA[i1 * 12 + j1] = x11;
+                }
+#pragma unroll
+                for (int u = 0; u < 2; u++) {  // V's rows: column rotation of pair b (items lane, lane + 64)
+                    const int v = lane + 64 * u, vi = v / 6, vb = v % 6;
+                    // shuffles with every lane active; the item's own guard comes after
+                    const double cv = __shfl(c, 7 * vb), sv = __shfl(sn, 7 * vb);
+                    const int av = __shfl(act, 7 * vb);
+                    if (v < 72 && av) {
+                        int k0, k1;
+                        rr_pair(12, r, vb, k0, k1);
+                        const double vp = sV[vi * 12 + k0], vq = sV[vi * 12 + k1];
+                        sV[vi * 12 + k0] = cv * vp - sv * vq;
+                        sV[vi * 12 + k1] = sv * vp + cv * vq;
+                    }
                 }
                 __syncthreads();
-                // One pass: the 2 x 2 block of A at (pair a rows i0 < i1, pair b columns j0 < j1)
-                // takes its column rotation (b) and then its row rotation (a) -- per element exactly
-                // the sequential statement's column-then-row order -- and each row of V its column
-                // rotations.
-                for (int it = lane; it < 36 + 72; it += 64) {
-                    if (it < 36) {
-                        const int a = it / 6, b = it % 6;
-                        int i0, i1, j0, j1;
-                        rr_pair(12, r, a, i0, i1);
-                        rr_pair(12, r, b, j0, j1);
-                        double x00 = sA[i0 * 12 + j0], x01 = sA[i0 * 12 + j1];
-                        double x10 = sA[i1 * 12 + j0], x11 = sA[i1 * 12 + j1];
-                        if (sAct[b]) {
-                            const double c = sC[b], sn = sS[b];
-                            const double y00 = c * x00 - sn * x01, y01 = sn * x00 + c * x01;
-                            const double y10 = c * x10 - sn * x11, y11 = sn * x10 + c * x11;
-                            x00 = y00;
-                            x01 = y01;
-                            x10 = y10;
-                            x11 = y11;
-                        }
-                        if (sAct[a]) {
-                            const double c = sC[a], sn = sS[a];
-                            const double y00 = c * x00 - sn * x10, y10 = sn * x00 + c * x10;
-                            const double y01 = c * x01 - sn * x11, y11 = sn * x01 + c * x11;
-                            x00 = y00;
-                            x01 = y01;
-                            x10 = y10;
-                            x11 = y11;
-                        }
-                        sA[i0 * 12 + j0] = x00;
-                        sA[i0 * 12 + j1] = x01;
-                        sA[i1 * 12 + j0] = x10;
-                        sA[i1 * 12 + j1] = x11;
-                    } else {
-                        const int v = it - 36, i = v / 6, b = v % 6;
-                        if (sAct[b]) {
-                            int j0, j1;
-                            rr_pair(12, r, b, j0, j1);
-                            const double c = sC[b], sn = sS[b];
-                            const double vp = sV[i * 12 + j0], vq = sV[i * 12 + j1];
-                            sV[i * 12 + j0] = c * vp - sn * vq;
-                            sV[i * 12 + j1] = sn * vp + c * vq;
-                        }
-                    }
+                if (blk && r + 1 < 11) {  // the next round's block
+                    rr_pair(12, r + 1, ba, i0, i1);
+                    rr_pair(12, r + 1, bb, j0, j1);
+                    x00 = sA[i0 * 12 + j0];
+                    x01 = sA[i0 * 12 + j1];
+                    x10 = sA[i1 * 12 + j0];
+                    x11 = sA[i1 * 12 + j1];
                 }
                 __syncthreads();
             }
