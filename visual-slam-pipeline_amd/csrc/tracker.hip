@@ -133,10 +133,11 @@ constexpr size_t kChainBytes = kChainRaw + (size_t)kCap * sizeof(vs_match);
 
 // Extraction chunks: the batch's network + post-processing runs chunk by chunk on the extraction
 // stream while the tracker consumes the chunks already done (process_batch_dev).  The first chunk
-// is small (nothing hides its latency) and the sizes grow by ~1.5x up to kXChunk, about as fast as
-// tracking a chunk outlasts extracting the next.
+// is small (nothing hides its latency) and the sizes grow by ~1.3x up to kXChunk (3, 4, 5, 7, 8, 5
+// at B = 32), about as fast as tracking a chunk outlasts extracting the next (A/B on one box:
+// 3 / 1.3x 1016, 2 / 1.2x 1011, 2 / 1.5x 991, 1 / 1.5x 959 frames/s).
 constexpr int kXChunk = 8;
-constexpr int kXFirst = 2;
+constexpr int kXFirst = 3;
 
 // The PnP input of Slam::refine_pose_via_local_pnp (tracked_points, :1408-1420) straight from the
 // local-map tracking result: keypoints (in order) whose map point is valid, as float object
@@ -214,6 +215,7 @@ struct GpuOps {
     std::vector<hipEvent_t> xev;  // one per extraction chunk
     std::vector<int> xch;         // chunk boundaries (frame index of each chunk's first frame, then nb)
     int first_chunk = kXFirst;    // VS_SLAM_FIRST_CHUNK overrides
+    int chunk_growth = 13;        // next chunk = this one x growth / 10 (VS_SLAM_CHUNK_GROWTH overrides)
     Pinned xpin;                  // keypoints / counts of the batch being extracted
     int B = 0, h = 0, w = 0, S = 0, batch_region = 0;
     double K[4] = {vs_trk::cfg::FX, vs_trk::cfg::FY, vs_trk::cfg::CX, vs_trk::cfg::CY};
@@ -272,6 +274,7 @@ struct GpuOps {
         ctx = c;
         VS_CHECK(make_streams());
         if (const char* fc = std::getenv("VS_SLAM_FIRST_CHUNK")) first_chunk = std::max(1, std::min(kXChunk, std::atoi(fc)));
+        if (const char* g = std::getenv("VS_SLAM_CHUNK_GROWTH")) chunk_growth = std::max(10, std::min(40, std::atoi(g)));
         const char* hp = std::getenv("VS_SLAM_HOST_PROFILE");
         hprof.on = hp && hp[0] == '1';
         if (hprof.on) hprof.on = false, hprof.skip = 64, hprof_armed = true;
@@ -403,7 +406,7 @@ struct GpuOps {
         const int s0 = batch_region * B;
         batch_region ^= 1;
         xch.assign(1, 0);
-        for (int c = first_chunk; xch.back() < nb; c = std::min(kXChunk, (3 * c + 1) / 2))
+        for (int c = first_chunk; xch.back() < nb; c = std::min(kXChunk, std::max(c + 1, (c * chunk_growth + 5) / 10)))
             xch.push_back(std::min(nb, xch.back() + c));
         const int nch = (int)xch.size() - 1;
         while ((int)xev.size() < nch) {
