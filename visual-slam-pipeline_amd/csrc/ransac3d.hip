@@ -202,7 +202,7 @@ __global__ __launch_bounds__(256) void k_ransac3d(const int* __restrict__ pairs,
     __shared__ uint16_t s_J[kLevels3d][kDraws3d + 2];  // attempt-end maps (pointer doubling)
     __shared__ int s_start[kMaxIters3d];
     __shared__ int s_navail;
-    __shared__ uint16_t s_idx[kMaxPts3d];
+    __shared__ double s_in[6][kMaxPts3d];  // inlier coordinates for the refit
     const int p = blockIdx.x;
     const int rf = pairs[2 * p], cf = pairs[2 * p + 1];
     const int n = min(ngood[p], kMaxPts3d);
@@ -356,7 +356,8 @@ __global__ __launch_bounds__(256) void k_ransac3d(const int* __restrict__ pairs,
         double R[9], t[3];
         hypothesis_dev(sP1, sP2, s_samp[3 * it], s_samp[3 * it + 1], s_samp[3 * it + 2], R, t);
         int inl = 0;
-        for (int j = 0; j < N; j++) inl += inlier_dev(R, t, sP1[j], sP2[j], thr);
+#pragma unroll 4
+        for (int j = 0; j < N; j++) inl += inlier_dev(R, t, sP1[j], sP2[j], thr);  // unrolled: loads run ahead
         if (inl > my_best) {
             my_best = inl;
             my_it = it;
@@ -401,7 +402,15 @@ __global__ __launch_bounds__(256) void k_ransac3d(const int* __restrict__ pairs,
             __syncthreads();
             int off = s_N;
             for (int k = 0; k < wv; k++) off += s_wcnt[k];
-            if (in) s_idx[off + __popcll(bal & ((1ull << lane) - 1ull))] = (uint16_t)j;
+            if (in) {  // the inliers' coordinates, compacted in index order (coordinate-major)
+                const int q = off + __popcll(bal & ((1ull << lane) - 1ull));
+                s_in[0][q] = sP1[j].x;
+                s_in[1][q] = sP1[j].y;
+                s_in[2][q] = sP1[j].z;
+                s_in[3][q] = sP2[j].x;
+                s_in[4][q] = sP2[j].y;
+                s_in[5][q] = sP2[j].z;
+            }
             __syncthreads();
             if (tid == 0) s_N += s_wcnt[0] + s_wcnt[1] + s_wcnt[2] + s_wcnt[3];
             __syncthreads();
@@ -421,30 +430,23 @@ __global__ __launch_bounds__(256) void k_ransac3d(const int* __restrict__ pairs,
     // the inliers in index order, one chain per lane (6 centroid coordinates, then 9 entries of H)
     const int cnt = s_N;
     double sum = 0;
-    if (tid < 6) {
-        const D3* P = tid < 3 ? sP1 : sP2;
-        const int c = tid % 3;
+    if (tid < 6) {  // c1.x, c1.y, c1.z, c2.x, c2.y, c2.z: each a sequential chain in index order
+        const double* col = s_in[tid];
 #pragma unroll 8
-        for (int q = 0; q < cnt; q++) {  // unrolled: the loads run ahead of the sequential sum
-            const D3 v = P[s_idx[q]];
-            sum += c == 0 ? v.x : c == 1 ? v.y : v.z;
-        }
+        for (int q = 0; q < cnt; q++) sum += col[q];
     }
     D3 c1, c2;
     c1.x = __shfl(sum, 0) / cnt; c1.y = __shfl(sum, 1) / cnt; c1.z = __shfl(sum, 2) / cnt;
     c2.x = __shfl(sum, 3) / cnt; c2.y = __shfl(sum, 4) / cnt; c2.z = __shfl(sum, 5) / cnt;
     double hs = 0;
-    if (tid < 9) {
+    if (tid < 9) {  // H[r][c] = sum (p1_r - c1_r)(p2_c - c2_c), sequential in index order
         const int r = tid / 3, c = tid % 3;
         const double m1 = r == 0 ? c1.x : r == 1 ? c1.y : c1.z;
         const double m2 = c == 0 ? c2.x : c == 1 ? c2.y : c2.z;
+        const double* ca = s_in[r];
+        const double* cb = s_in[3 + c];
 #pragma unroll 8
-        for (int q = 0; q < cnt; q++) {
-            const int j = s_idx[q];
-            const double a = (r == 0 ? sP1[j].x : r == 1 ? sP1[j].y : sP1[j].z) - m1;
-            const double b = (c == 0 ? sP2[j].x : c == 1 ? sP2[j].y : sP2[j].z) - m2;
-            hs += a * b;
-        }
+        for (int q = 0; q < cnt; q++) hs += (ca[q] - m1) * (cb[q] - m2);
     }
     double H[9];
 #pragma unroll
