@@ -190,7 +190,8 @@ __global__ __launch_bounds__(256) void k_ransac3d(const int* __restrict__ pairs,
                                                   int cap, const vs_match* __restrict__ good,
                                                   const int* __restrict__ ngood, const float* __restrict__ depth,
                                                   int h, int w, double fx, double fy, double cx, double cy,
-                                                  const uint32_t* __restrict__ seeds, int iters, double thr,
+                                                  const uint32_t* __restrict__ seeds,
+                                                  const uint32_t* __restrict__ mt_init, int iters, double thr,
                                                   double* __restrict__ R_out, double* __restrict__ t_out,
                                                   int* __restrict__ ok_out, int* __restrict__ diag_out) {
     __shared__ D3 sP1[kMaxPts3d], sP2[kMaxPts3d];
@@ -260,8 +261,11 @@ __global__ __launch_bounds__(256) void k_ransac3d(const int* __restrict__ pairs,
     }
 
     R3_T(0);
-    // ---- MT19937(seed): init_genrand on lane 0, two parallel twists = 1248 outputs ----
-    if (tid == 0) {
+    // ---- MT19937(seed): init_genrand (given by the caller, or on lane 0), two parallel twists =
+    // 1248 outputs ----
+    if (mt_init) {
+        for (int i = tid; i < kMtN; i += blockDim.x) s_mt[i] = mt_init[(size_t)p * kMtN + i];
+    } else if (tid == 0) {
         uint32_t x = seeds[p];
         s_mt[0] = x;
         for (int i = 1; i < kMtN; i++) {
@@ -473,12 +477,12 @@ __global__ __launch_bounds__(256) void k_ransac3d(const int* __restrict__ pairs,
 int ransac3d_pairs(vs_ctx* ctx, int P, const int* d_pairs, const vs_keypoint* d_kps, int cap, const vs_match* d_good,
                    const int* d_ngood, const float* d_depth, int h, int w, const double K[4],
                    const uint32_t* d_seeds, int iters, double thr, double* d_R, double* d_t, int* d_ok, int* d_diag,
-                   hipStream_t s) {
+                   hipStream_t s, const uint32_t* d_mt_init) {
     if (P <= 0) return VS_OK;
     VS_ARG(iters > 0 && iters <= kMaxIters3d, "ransac_3d3d: iters must be in [1, 1024]");
     ProfScope ps(ctx, "ransac3d", s);
     hipLaunchKernelGGL(k_ransac3d, dim3(P), dim3(256), 0, s, d_pairs, d_kps, cap, d_good, d_ngood, d_depth, h, w, K[0],
-                       K[1], K[2], K[3], d_seeds, iters, thr, d_R, d_t, d_ok, d_diag);
+                       K[1], K[2], K[3], d_seeds, d_mt_init, iters, thr, d_R, d_t, d_ok, d_diag);
     VS_HIP(hipGetLastError());
     return VS_OK;
 }

@@ -220,7 +220,7 @@ struct GpuOps {
     int B = 0, h = 0, w = 0, S = 0, batch_region = 0;
     double K[4] = {vs_trk::cfg::FX, vs_trk::cfg::FY, vs_trk::cfg::CX, vs_trk::cfg::CY};
     DevBuf pool_kps, pool_desc, pool_n, pool_depth, semi, dgrid;
-    DevBuf chain_buf, work, rows_buf, map_pos, map_desc, map_valid, map_tmp, pnp_io;
+    DevBuf chain_buf, work, rows_buf, map_pos, map_desc, map_valid, map_tmp, pnp_io, hdr_buf;
     int map_cap = 0, map_n = 0;
     bool valid_dirty = false;
     Pinned pin;
@@ -484,20 +484,29 @@ struct GpuOps {
         double* dd = reinterpret_cast<double*>(c + kChainDbl);
         vs_match* good = reinterpret_cast<vs_match*>(c + kChainGood);
         vs_match* kept = reinterpret_cast<vs_match*>(c + kChainKept);
-        const int hdr[3] = {ref.slot, cur.slot, (int)seed};  // pair slots + RANSAC seed, one upload
-        if (failed(upload(di, hdr, sizeof(hdr)))) return R;
-        if (failed(match_pairs(ctx, 1, di, S, pool_desc.as<float>(), pool_n.as<int>(), kCap,
+        // one upload: pair slots, the 3D-3D seed and its MT19937 init_genrand state (624 serial
+        // steps, cheaper on the host than on one GPU lane)
+        uint32_t hdr[4 + 624];
+        hdr[0] = (uint32_t)ref.slot;
+        hdr[1] = (uint32_t)cur.slot;
+        hdr[2] = seed;
+        hdr[3] = 0;
+        hdr[4] = seed;
+        for (int i = 1; i < 624; i++) hdr[4 + i] = 1812433253u * (hdr[3 + i] ^ (hdr[3 + i] >> 30)) + (uint32_t)i;
+        if (failed(hdr_buf.ensure(sizeof(hdr))) || failed(upload(hdr_buf.p, hdr, sizeof(hdr)))) return R;
+        const int* dh = hdr_buf.as<int>();
+        if (failed(match_pairs(ctx, 1, dh, S, pool_desc.as<float>(), pool_n.as<int>(), kCap,
                                vs_trk::cfg::L2_RATIO_THRESHOLD, reinterpret_cast<vs_match*>(c + kChainRaw), di + 3,
                                good, di + 4, s)))
             return R;
-        if (failed(fmat_pairs(ctx, 1, di, pool_kps.as<vs_keypoint>(), kCap, good, di + 4, dd, kept, di + 5, dd + 9,
+        if (failed(fmat_pairs(ctx, 1, dh, pool_kps.as<vs_keypoint>(), kCap, good, di + 4, dd, kept, di + 5, dd + 9,
                               di + 8, s)))
             return R;
-        if (failed(ransac3d_pairs(ctx, 1, di, pool_kps.as<vs_keypoint>(), kCap, kept, di + 5, pool_depth.as<float>(), h,
-                                  w, K, reinterpret_cast<const uint32_t*>(di + 2), 200, 0.05, dd + 11, dd + 20, di + 6,
-                                  di + 16, s)))
+        if (failed(ransac3d_pairs(ctx, 1, dh, pool_kps.as<vs_keypoint>(), kCap, kept, di + 5, pool_depth.as<float>(), h,
+                                  w, K, reinterpret_cast<const uint32_t*>(dh + 2), 200, 0.05, dd + 11, dd + 20, di + 6,
+                                  di + 16, s, reinterpret_cast<const uint32_t*>(dh + 4))))
             return R;
-        if (failed(emat_pairs(ctx, 1, di, pool_kps.as<vs_keypoint>(), kCap, kept, di + 5, di + 6, pool_depth.as<float>(),
+        if (failed(emat_pairs(ctx, 1, dh, pool_kps.as<vs_keypoint>(), kCap, kept, di + 5, di + 6, pool_depth.as<float>(),
                               h, w, K, dd + 23, dd + 32, dd + 35, di + 7, di + 20, s)))
             return R;
         char* hc = take(kChainRaw);
@@ -869,7 +878,7 @@ void vs_slam_destroy(vs_slam* sl) {
     o.destroy_streams();
     DevBuf* bufs[] = {&o.pool_kps, &o.pool_desc, &o.pool_n, &o.pool_depth, &o.semi,      &o.dgrid,
                       &o.chain_buf,    &o.work, &o.rows_buf,      &o.map_pos, &o.map_desc,  &o.map_valid, &o.map_tmp,
-                      &o.pnp_io};
+                      &o.pnp_io,       &o.hdr_buf};
     for (DevBuf* b : bufs) b->release();
     delete sl;
 }

@@ -130,7 +130,8 @@ int match_pairs(vs_ctx* ctx, int P, const int* d_pairs, int F, const float* d_de
 int ransac3d_pairs(vs_ctx* ctx, int P, const int* d_pairs, const vs_keypoint* d_kps, int cap,
                    const vs_match* d_good, const int* d_ngood, const float* d_depth, int h, int w,
                    const double K[4], const uint32_t* d_seeds, int iters, double thr,
-                   double* d_R, double* d_t, int* d_ok, int* d_diag, hipStream_t s);
+                   double* d_R, double* d_t, int* d_ok, int* d_diag, hipStream_t s,
+                   const uint32_t* d_mt_init = nullptr);  // [P][624] init_genrand states (optional)
 // Local-map tracking (d_result = {tracked, observations})
 int track_local_map(vs_ctx* ctx, const double* d_mp_pos, const float* d_mp_desc, const uint8_t* d_mp_valid, int n_mp,
                     const vs_keypoint* d_kps, const float* d_desc, int nkp, const double R[9], const double t[3],
