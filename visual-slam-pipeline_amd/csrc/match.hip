@@ -227,8 +227,18 @@ __global__ void k_set_meta(int* meta, int n1, int n2) {
     meta[3] = n2;
 }
 
+int desc_norms(vs_ctx* ctx, int F, const float* d_desc, const int* d_n, int cap, float* d_norms, hipStream_t s) {
+    (void)ctx;
+    const long rows = (long)F * cap;
+    if (rows <= 0) return VS_OK;
+    hipLaunchKernelGGL(k_desc_norms, dim3((unsigned)((rows + 255) / 256)), dim3(256), 0, s, d_desc, d_n, F, cap, d_norms);
+    VS_HIP(hipGetLastError());
+    return VS_OK;
+}
+
 int match_pairs(vs_ctx* ctx, int P, const int* d_pairs, int F, const float* d_desc, const int* d_n, int cap,
-                float ratio, vs_match* d_raw, int* d_nraw, vs_match* d_good, int* d_ngood, hipStream_t s) {
+                float ratio, vs_match* d_raw, int* d_nraw, vs_match* d_good, int* d_ngood, hipStream_t s,
+                const float* d_norms) {
     if (P <= 0) return VS_OK;
     const int nslices = (cap + kTrainChunk - 1) / kTrainChunk;
     const size_t norm_bytes = ((size_t)F * cap * sizeof(float) + 255) & ~(size_t)255;
@@ -236,7 +246,9 @@ int match_pairs(vs_ctx* ctx, int P, const int* d_pairs, int F, const float* d_de
     float* norms = ctx->norms.as<float>();
     Part2* part = reinterpret_cast<Part2*>(ctx->norms.as<uint8_t>() + norm_bytes);
     ProfScope ps(ctx, "match", s);
-    if (2 * P < F) {  // a few pairs out of a frame pool: only the referenced frames' norms
+    if (d_norms) {  // the caller keeps the frames' row norms
+        norms = const_cast<float*>(d_norms);
+    } else if (2 * P < F) {  // a few pairs out of a frame pool: only the referenced frames' norms
         long rows = (long)2 * P * cap;
         hipLaunchKernelGGL(k_desc_norms_sel, dim3((unsigned)((rows + 255) / 256)), dim3(256), 0, s, d_desc, d_n,
                            d_pairs, P, cap, norms);

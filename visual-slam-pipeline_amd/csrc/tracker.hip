@@ -219,7 +219,7 @@ struct GpuOps {
     Pinned xpin;                  // keypoints / counts of the batch being extracted
     int B = 0, h = 0, w = 0, S = 0, batch_region = 0;
     double K[4] = {vs_trk::cfg::FX, vs_trk::cfg::FY, vs_trk::cfg::CX, vs_trk::cfg::CY};
-    DevBuf pool_kps, pool_desc, pool_n, pool_depth, semi, dgrid;
+    DevBuf pool_kps, pool_desc, pool_n, pool_depth, pool_norms, semi, dgrid;
     DevBuf chain_buf, work, rows_buf, map_pos, map_desc, map_valid, map_tmp, pnp_io, hdr_buf;
     int map_cap = 0, map_n = 0;
     bool valid_dirty = false;
@@ -230,6 +230,7 @@ struct GpuOps {
     vs_keypoint* kps_of(int slot) const { return pool_kps.as<vs_keypoint>() + (size_t)slot * kCap; }
     float* desc_of(int slot) const { return pool_desc.as<float>() + (size_t)slot * kCap * 256; }
     float* depth_of(int slot) const { return pool_depth.as<float>() + (size_t)slot * h * w; }
+    float* norms_of(int slot) const { return pool_norms.as<float>() + (size_t)slot * kCap; }
 
     // Two streams on disjoint CU sets: the latency-bound tracking kernels keep VS_SLAM_TRACK_CUS
     // (default 32) CUs to themselves, so they never queue behind the network's long-running
@@ -286,6 +287,7 @@ struct GpuOps {
         VS_CHECK(pool_desc.ensure((size_t)S * kCap * 256 * sizeof(float)));
         VS_CHECK(pool_n.ensure((size_t)S * sizeof(int)));
         VS_CHECK(pool_depth.ensure((size_t)S * h * w * sizeof(float)));
+        VS_CHECK(pool_norms.ensure((size_t)S * kCap * sizeof(float)));
         VS_HIP(hipMemsetAsync(pool_n.p, 0, (size_t)S * sizeof(int), s));
         const int hc = (h + 7) / 8, wc = (w + 7) / 8;
         VS_CHECK(semi.ensure((size_t)B * hc * wc * VS_SEMI_CH * sizeof(float)));
@@ -380,6 +382,7 @@ struct GpuOps {
         VS_HIP(hipMemcpyAsync(desc_of(to), desc_of(from), (size_t)kCap * 256 * sizeof(float), hipMemcpyDeviceToDevice, s));
         VS_HIP(hipMemcpyAsync(pool_n.as<int>() + to, pool_n.as<int>() + from, sizeof(int), hipMemcpyDeviceToDevice, s));
         VS_HIP(hipMemcpyAsync(depth_of(to), depth_of(from), (size_t)h * w * sizeof(float), hipMemcpyDeviceToDevice, s));
+        VS_HIP(hipMemcpyAsync(norms_of(to), norms_of(from), kCap * sizeof(float), hipMemcpyDeviceToDevice, s));
         return VS_OK;
     }
     // Host features (SPCF cache / caller-extracted) into a persistent slot.
@@ -391,6 +394,7 @@ struct GpuOps {
         VS_CHECK(upload(kps_of(slot), f.kps.data(), (size_t)n * sizeof(vs_keypoint)));
         VS_CHECK(upload(desc_of(slot), desc, (size_t)n * 256 * sizeof(float)));
         VS_CHECK(upload(pool_n.as<int>() + slot, &n, sizeof(int)));
+        VS_CHECK(desc_norms(ctx, 1, desc_of(slot), pool_n.as<int>() + slot, kCap, norms_of(slot), s));
         if (f.depth)
             VS_CHECK(upload(depth_of(slot), f.depth, (size_t)h * w * sizeof(float)));
         else
@@ -424,6 +428,8 @@ struct GpuOps {
                                 dgrid.as<float>()));
             VS_CHECK(sp_postprocess(ctx, m, hc, wc, h, w, kps_of(s0 + f0), desc_of(s0 + f0), pool_n.as<int>() + s0 + f0,
                                     kCap, xs, semi.as<float>(), dgrid.as<float>()));
+            // descriptor row norms once per frame (matching reuses them for every pair)
+            VS_CHECK(desc_norms(ctx, m, desc_of(s0 + f0), pool_n.as<int>() + s0 + f0, kCap, norms_of(s0 + f0), xs));
             if (d_depth)
                 VS_HIP(hipMemcpyAsync(depth_of(s0 + f0), d_depth + (size_t)f0 * h * w, (size_t)m * h * w * sizeof(float),
                                       hipMemcpyDeviceToDevice, xs));
@@ -474,7 +480,7 @@ struct GpuOps {
         char* c = chain_buf.as<char>();
         return match_pairs(ctx, 1, meta, S, pool_desc.as<float>(), pool_n.as<int>(), kCap, ratio,
                            reinterpret_cast<vs_match*>(c + kChainRaw), meta + 3, reinterpret_cast<vs_match*>(c + kChainGood),
-                           meta + 4, s);
+                           meta + 4, s, pool_norms.as<float>());
     }
 
     vs_trk::ChainResult chain_impl(const vs_trk::Frame& ref, const vs_trk::Frame& cur, uint32_t seed) {
@@ -497,7 +503,7 @@ struct GpuOps {
         const int* dh = hdr_buf.as<int>();
         if (failed(match_pairs(ctx, 1, dh, S, pool_desc.as<float>(), pool_n.as<int>(), kCap,
                                vs_trk::cfg::L2_RATIO_THRESHOLD, reinterpret_cast<vs_match*>(c + kChainRaw), di + 3,
-                               good, di + 4, s)))
+                               good, di + 4, s, pool_norms.as<float>())))
             return R;
         if (failed(fmat_pairs(ctx, 1, dh, pool_kps.as<vs_keypoint>(), kCap, good, di + 4, dd, kept, di + 5, dd + 9,
                               di + 8, s)))
@@ -876,7 +882,7 @@ void vs_slam_destroy(vs_slam* sl) {
                 std::fprintf(stderr, "vs_slam host %-22s %8ld calls %10.3f ms  %8.1f us/call\n", kHostOpNames[k],
                              o.hprof.n[k], o.hprof.ms[k], 1e3 * o.hprof.ms[k] / o.hprof.n[k]);
     o.destroy_streams();
-    DevBuf* bufs[] = {&o.pool_kps, &o.pool_desc, &o.pool_n, &o.pool_depth, &o.semi,      &o.dgrid,
+    DevBuf* bufs[] = {&o.pool_kps, &o.pool_desc, &o.pool_n, &o.pool_depth, &o.pool_norms, &o.semi, &o.dgrid,
                       &o.chain_buf,    &o.work, &o.rows_buf,      &o.map_pos, &o.map_desc,  &o.map_valid, &o.map_tmp,
                       &o.pnp_io,       &o.hdr_buf};
     for (DevBuf* b : bufs) b->release();

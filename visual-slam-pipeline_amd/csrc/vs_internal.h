@@ -125,7 +125,10 @@ int sp_postprocess(vs_ctx* ctx, int B, int hc, int wc, int h, int w, vs_keypoint
 // Matching
 int match_pairs(vs_ctx* ctx, int P, const int* d_pairs, int F, const float* d_desc,
                 const int* d_n, int cap, float ratio, vs_match* d_raw, int* d_nraw,
-                vs_match* d_good, int* d_ngood, hipStream_t s);
+                vs_match* d_good, int* d_ngood, hipStream_t s,
+                const float* d_norms = nullptr);  // [F][cap] row norms when already known
+// Sequential-fmaf squared norms of the descriptor rows of F frames ([F][cap], rows >= n[f] untouched).
+int desc_norms(vs_ctx* ctx, int F, const float* d_desc, const int* d_n, int cap, float* d_norms, hipStream_t s);
 // 3D-3D RANSAC
 int ransac3d_pairs(vs_ctx* ctx, int P, const int* d_pairs, const vs_keypoint* d_kps, int cap,
                    const vs_match* d_good, const int* d_ngood, const float* d_depth, int h, int w,
