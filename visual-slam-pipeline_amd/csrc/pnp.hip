@@ -371,13 +371,18 @@ __global__ __launch_bounds__(64) void k_pnp_hyp(const float* __restrict__ obj_al
             double cw[4][3], v[4][12], L[6][10], rho[6], al[5][4], X[15], uv[10];
             for (int i = 0; i < 4; i++)
                 for (int c = 0; c < 3; c++) cw[i][c] = sCw[i][c];
-            for (int i = 0; i < m; i++)
-                for (int j = 0; j < 4; j++) al[i][j] = sAl[i][j];
-            for (int i = 0; i < 3 * m; i++) X[i] = sX[i];
-            for (int i = 0; i < 2 * m; i++) uv[i] = sUV[i];
+            // constant bounds (m <= 5): the copies unroll and the arrays stay in registers
+#pragma unroll
+            for (int i = 0; i < 5; i++)
+#pragma unroll
+                for (int j = 0; j < 4; j++) al[i][j] = i < m ? sAl[i][j] : 0.0;
+#pragma unroll
+            for (int i = 0; i < 15; i++) X[i] = i < 3 * m ? sX[i] : 0.0;
+#pragma unroll
+            for (int i = 0; i < 10; i++) uv[i] = i < 2 * m ? sUV[i] : 0.0;
             epnp_L_rho(sV, cw, v, L, rho);
             double R[9], t[3];
-            sErr[lane] = epnp_variant(lane, L, rho, v, al, X, uv, m, K, R, t);
+            sErr[lane] = epnp_variant<5>(lane, L, rho, v, al, X, uv, m, K, R, t);
             for (int k = 0; k < 9; k++) sRt[lane][k] = R[k];
             for (int k = 0; k < 3; k++) sRt[lane][9 + k] = t[k];
         }

@@ -492,6 +492,10 @@ VS_HD inline void epnp_L_rho(const double* um, const double cw[4][3], double v[4
 
 // Beta approximation s (0: N = 4, 1: N = 2, 2: N = 3), 5 Gauss-Newton steps on the 6 distance
 // constraints, pose by Kabsch on the camera-frame points; returns the mean reprojection error.
+// MAXN bounds n at compile time: the point loops run to MAXN with an i < n guard (the same
+// operations in the same order), so on the device (MAXN = 5) they unroll and the arrays stay in
+// registers instead of scratch.
+template <int MAXN>
 VS_HD inline double epnp_variant(int s, const double L[6][10], const double rho[6], const double v[4][12],
                                  const double (*alphas)[4], const double* X, const double* uv, int n, const Cam& K,
                                  double* R, double* t) {
@@ -588,8 +592,10 @@ VS_HD inline double epnp_variant(int s, const double L[6][10], const double rho[
                    alphas[0][3] * ccs[3][2];
     const double sgn = pcs0z < 0 ? -1.0 : 1.0;
     double pc0[3] = {0, 0, 0}, pw0[3] = {0, 0, 0};
-    for (int i = 0; i < n; i++)
-        for (int c = 0; c < 3; c++) {
+    VS_UNROLL
+    for (int i = 0; i < MAXN; i++)
+        if (i < n)
+            for (int c = 0; c < 3; c++) {
             pc0[c] += sgn * (alphas[i][0] * ccs[0][c] + alphas[i][1] * ccs[1][c] + alphas[i][2] * ccs[2][c] +
                              alphas[i][3] * ccs[3][c]);
             pw0[c] += X[3 * i + c];
@@ -599,7 +605,9 @@ VS_HD inline double epnp_variant(int s, const double L[6][10], const double rho[
         pw0[c] /= n;
     }
     double ABt[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
-    for (int i = 0; i < n; i++) {
+    VS_UNROLL
+    for (int i = 0; i < MAXN; i++) {
+        if (i >= n) continue;
         double pc[3];
         for (int c = 0; c < 3; c++)
             pc[c] = sgn * (alphas[i][0] * ccs[0][c] + alphas[i][1] * ccs[1][c] + alphas[i][2] * ccs[2][c] +
@@ -611,7 +619,9 @@ VS_HD inline double epnp_variant(int s, const double L[6][10], const double rho[
     rotation_from_cross(ABt, R);
     for (int c = 0; c < 3; c++) t[c] = pc0[c] - (R[c * 3] * pw0[0] + R[c * 3 + 1] * pw0[1] + R[c * 3 + 2] * pw0[2]);
     double err = 0;
-    for (int i = 0; i < n; i++) {
+    VS_UNROLL
+    for (int i = 0; i < MAXN; i++) {
+        if (i >= n) continue;
         double u, vv;
         project(R, t, K, X[3 * i], X[3 * i + 1], X[3 * i + 2], u, vv);
         const double du = uv[2 * i] - u, dvv = uv[2 * i + 1] - vv;
@@ -638,7 +648,7 @@ VS_HD bool epnp(const double* X, const double* uv, int n, const Cam& K, double* 
     bool have = false;
     for (int s = 0; s < 3; s++) {
         double R[9], t[3];
-        const double err = epnp_variant(s, L, rho, v, alphas, X, uv, n, K, R, t);
+        const double err = epnp_variant<MAXN>(s, L, rho, v, alphas, X, uv, n, K, R, t);
         if (!have || err < best_err) {
             have = true;
             best_err = err;
