@@ -31,7 +31,9 @@ constexpr int kTlmMaxKp = 1024;
 // the same cell (the order the reference's push_back produces).
 constexpr int kTlmMaxCells = 4096;
 __global__ __launch_bounds__(1024) void k_tlm_grid(const vs_keypoint* __restrict__ kps, int nkp, int GW, int GH,
-                                                   int* __restrict__ start, int* __restrict__ items) {
+                                                   int* __restrict__ start, int* __restrict__ items,
+                                                   int* __restrict__ work_n) {
+    if (threadIdx.x == 0) *work_n = 0;  // the candidate work list of this call (k_tlm_cand appends)
     __shared__ int s_cell[kTlmMaxKp];
     __shared__ int s_start[kTlmMaxCells + 1];
     const int tid = threadIdx.x, nc = GW * GH;
@@ -86,12 +88,13 @@ __global__ __launch_bounds__(256) void k_tlm_cand(const double* __restrict__ mp_
                                                   const vs_keypoint* __restrict__ kps, const float* __restrict__ desc,
                                                   const int* __restrict__ start, const int* __restrict__ items, int GW,
                                                   int GH, int img_w, int img_h, TlmPose T, int* __restrict__ cnt,
-                                                  int* __restrict__ cand) {
+                                                  int* __restrict__ cand, int* __restrict__ work,
+                                                  int* __restrict__ work_n) {
     const int mp = blockIdx.x * 256 + threadIdx.x;
-    if (mp >= n_mp) return;
+    const int lane = threadIdx.x & 63;
     int c = 0;
-    int* my = cand + (size_t)mp * kTlmMaxCand;
-    if (mp_valid[mp]) {
+    int* my = cand + (size_t)min(mp, n_mp - 1) * kTlmMaxCand;
+    if (mp < n_mp && mp_valid[mp]) {
         const double x = mp_pos[3 * mp], y = mp_pos[3 * mp + 1], z = mp_pos[3 * mp + 2];
         const double* Rc = T.Rc;
         const double px = Rc[0] * x + Rc[1] * y + Rc[2] * z + T.tc[0];
@@ -140,17 +143,32 @@ __global__ __launch_bounds__(256) void k_tlm_cand(const double* __restrict__ mp_
             }
         }
     }
-    cnt[mp] = c;
+    if (mp < n_mp) cnt[mp] = c;
+    // append this map point's (map point, slot) pairs to the distance work list: one atomic per
+    // wave (the list order is irrelevant: every distance lands at its own slot)
+    int incl = c;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(incl, o);
+        if (lane >= o) incl += y;
+    }
+    const int total = __shfl(incl, 63);
+    int base = 0;
+    if (lane == 63 && total > 0) base = atomicAdd(work_n, total);
+    base = __shfl(base, 63);
+    for (int j = 0; j < c; j++) work[base + incl - c + j] = mp * kTlmMaxCand + j;
 }
 
-// Phase 2: one lane per (map point, candidate): the cv::norm distance (:451).
+// Phase 2: the cv::norm distance (:451) of every (map point, candidate) pair on the work list,
+// grid-stride (the list holds only real candidates, a few per visible map point).
 __global__ __launch_bounds__(256) void k_tlm_dist(const float* __restrict__ mp_desc, const float* __restrict__ desc,
-                                                  int n_mp, const int* __restrict__ cnt, const int* __restrict__ cand,
-                                                  double* __restrict__ dist) {
-    const long r = (long)blockIdx.x * 256 + threadIdx.x;
-    const int mp = (int)(r / kTlmMaxCand), j = (int)(r % kTlmMaxCand);
-    if (mp >= n_mp || j >= cnt[mp]) return;
-    dist[r] = desc_l2_dev(mp_desc + (size_t)mp * 256, desc + (size_t)cand[r] * 256);
+                                                  const int* __restrict__ cand, const int* __restrict__ work,
+                                                  const int* __restrict__ work_n, double* __restrict__ dist) {
+    const int n = *work_n;
+    for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
+        const int r = work[i];
+        dist[r] = desc_l2_dev(mp_desc + (size_t)(r / kTlmMaxCand) * 256, desc + (size_t)cand[r] * 256);
+    }
 }
 
 // Assignment in map-point order (Slam.cpp:460-465), decided in parallel: keypoint ki's best
@@ -370,9 +388,9 @@ int track_local_map(vs_ctx* ctx, const double* d_mp_pos, const float* d_mp_desc,
            "track_local_map: image too large for the keypoint grid");
     const int GW = (img_w + kTlmCell - 1) / kTlmCell, GH = (img_h + kTlmCell - 1) / kTlmCell;
     const size_t grid_bytes = (size_t)(GW * GH + 1) * sizeof(int) + (size_t)(nkp + 1) * sizeof(int);
-    const size_t per_mp = 3 * sizeof(int) + sizeof(double) + (size_t)kTlmMaxCand * (sizeof(int) + sizeof(double));
+    const size_t per_mp = 3 * sizeof(int) + sizeof(double) + (size_t)kTlmMaxCand * (2 * sizeof(int) + sizeof(double));
     const int nblk = (n_mp + 255) / 256;
-    VS_CHECK(ctx->tlm.ensure(grid_bytes + 64 + (size_t)(n_mp + 1) * per_mp + (size_t)(nblk + 1) * sizeof(int)));
+    VS_CHECK(ctx->tlm.ensure(grid_bytes + 64 + (size_t)(n_mp + 1) * per_mp + (size_t)(nblk + 2) * sizeof(int)));
     char* base = static_cast<char*>(ctx->tlm.p);
     int* start = reinterpret_cast<int*>(base);
     int* items = start + GW * GH + 1;
@@ -381,9 +399,11 @@ int track_local_map(vs_ctx* ctx, const double* d_mp_pos, const float* d_mp_desc,
     int* cnt = cand + (size_t)(n_mp + 1) * kTlmMaxCand;
     int* best_ki = cnt + (n_mp + 1);
     int* rank = best_ki + (n_mp + 1);
-    int* blkcnt = rank + (n_mp + 1);
+    int* work_n = rank + (n_mp + 1);
+    int* blkcnt = work_n + 1;
+    int* work = blkcnt + nblk + 1;
     double* best_d =
-        reinterpret_cast<double*>(base + (((size_t)(reinterpret_cast<char*>(blkcnt + nblk + 1) - base) + 15) / 16) * 16);
+        reinterpret_cast<double*>(base + (((size_t)(reinterpret_cast<char*>(work + (size_t)(n_mp + 1) * kTlmMaxCand) - base) + 15) / 16) * 16);
     TlmPose T;
     for (int i = 0; i < 3; i++)
         for (int j = 0; j < 3; j++) T.Rc[i * 3 + j] = R[j * 3 + i];
@@ -394,14 +414,16 @@ int track_local_map(vs_ctx* ctx, const double* d_mp_pos, const float* d_mp_desc,
     T.cy = K[3];
     ProfScope ps(ctx, "track_local_map", s);
     VS_HIP(hipMemsetAsync(items, 0xff, (size_t)(nkp + 1) * sizeof(int), s));
-    if (nkp > 0) hipLaunchKernelGGL(k_tlm_grid, dim3(1), dim3(1024), 0, s, d_kps, nkp, GW, GH, start, items);
-    else VS_HIP(hipMemsetAsync(start, 0, (size_t)(GW * GH + 1) * sizeof(int), s));
+    if (nkp > 0) {
+        hipLaunchKernelGGL(k_tlm_grid, dim3(1), dim3(1024), 0, s, d_kps, nkp, GW, GH, start, items, work_n);
+    } else {
+        VS_HIP(hipMemsetAsync(start, 0, (size_t)(GW * GH + 1) * sizeof(int), s));
+        VS_HIP(hipMemsetAsync(work_n, 0, sizeof(int), s));
+    }
     if (n_mp > 0) {
         hipLaunchKernelGGL(k_tlm_cand, dim3((n_mp + 255) / 256), dim3(256), 0, s, d_mp_pos, d_mp_desc, d_mp_valid, n_mp,
-                           d_kps, d_desc, start, items, GW, GH, img_w, img_h, T, cnt, cand);
-        const long pairs = (long)n_mp * kTlmMaxCand;
-        hipLaunchKernelGGL(k_tlm_dist, dim3((unsigned)((pairs + 255) / 256)), dim3(256), 0, s, d_mp_desc, d_desc, n_mp,
-                           cnt, cand, dist);
+                           d_kps, d_desc, start, items, GW, GH, img_w, img_h, T, cnt, cand, work, work_n);
+        hipLaunchKernelGGL(k_tlm_dist, dim3(128), dim3(256), 0, s, d_mp_desc, d_desc, cand, work, work_n, dist);
     }
     if (n_mp > 0)
         hipLaunchKernelGGL(k_tlm_best, dim3(nblk), dim3(256), 0, s, cnt, cand, dist, n_mp, best_ki, best_d, rank,
