@@ -214,11 +214,14 @@ __global__ __launch_bounds__(256) void k_tlm_best(const int* __restrict__ cnt, c
 
 constexpr int kTlmCandBuf = 4096;  // candidates buffered in LDS between resolve passes
 constexpr int kTlmMaxBlk = 4096;  // map points / 256 handled by the direct placement
+constexpr int kTlmBucket = 8;     // per-keypoint candidate bucket of a resolve pass
 
 struct TlmResolveShared {
     unsigned long long best[kTlmMaxKp];  // bits of the running minimum (d >= 0: order-preserving)
     int kpmp[kTlmMaxKp];
     int first[kTlmMaxKp];  // first buffered candidate of a keypoint in the current pass
+    int bcnt[kTlmMaxKp];   // candidates of a keypoint in the current pass
+    int bkt[kTlmMaxKp][kTlmBucket];  // their buffer indices (any order) while they fit
     int cmp[kTlmCandBuf], cki[kTlmCandBuf];
     unsigned long long cd[kTlmCandBuf];
     int pre[kTlmMaxBlk];
@@ -233,6 +236,17 @@ struct TlmResolveShared {
 __device__ void tlm_resolve_pass(TlmResolveShared& S, int nc, int* __restrict__ obs_mp, int* __restrict__ obs_kp,
                                  int obs_cap) {
     const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
+    // each keypoint's candidates into its bucket (unordered: the test below compares positions)
+#pragma unroll
+    for (int r = 0; r < kTlmCandBuf / 1024; r++) {
+        const int t = r * 1024 + tid;
+        if (t < nc) {
+            const int ki = S.cki[t];
+            const int slot = atomicAdd(&S.bcnt[ki], 1);
+            if (slot < kTlmBucket) S.bkt[ki][slot] = t;
+        }
+    }
+    __syncthreads();
     bool win[kTlmCandBuf / 1024];
 #pragma unroll
     for (int r = 0; r < kTlmCandBuf / 1024; r++) {
@@ -242,8 +256,16 @@ __device__ void tlm_resolve_pass(TlmResolveShared& S, int nc, int* __restrict__ 
             const int ki = S.cki[t];
             const unsigned long long d = S.cd[t];
             bool w = d < S.best[ki];
-            for (int j = S.first[ki]; j < t && w; j++)
-                if (S.cki[j] == ki && S.cd[j] <= d) w = false;
+            const int nb = S.bcnt[ki];
+            if (nb <= kTlmBucket) {  // the keypoint's other candidates: earlier and not larger -> loses
+                for (int k = 0; k < nb && w; k++) {
+                    const int j = S.bkt[ki][k];
+                    if (j < t && S.cd[j] <= d) w = false;
+                }
+            } else {
+                for (int j = S.first[ki]; j < t && w; j++)
+                    if (S.cki[j] == ki && S.cd[j] <= d) w = false;
+            }
             win[r] = w;
         }
     }
@@ -253,6 +275,7 @@ __device__ void tlm_resolve_pass(TlmResolveShared& S, int nc, int* __restrict__ 
         const int t = r * 1024 + tid;
         if (t < nc) {
             S.first[S.cki[t]] = INT_MAX;  // every reader is past the barrier above
+            S.bcnt[S.cki[t]] = 0;
             if (win[r]) atomicMin(&S.best[S.cki[t]], S.cd[t]);
         }
     }
@@ -299,6 +322,7 @@ __global__ __launch_bounds__(1024) void k_tlm_resolve(const int* __restrict__ be
         S.best[k] = (unsigned long long)__double_as_longlong(1e9);
         S.kpmp[k] = kp_to_mp[k];
         S.first[k] = INT_MAX;
+        S.bcnt[k] = 0;
     }
     if (tid == 0) {
         S.nobs = S.nc = 0;
