@@ -19,6 +19,12 @@ frontend_batch — BASELINE config[3], offline batch: each rank extracts its blo
 frames, matches consecutive pairs and runs F verification + 3D-3D (+E) per pair (DevicePipeline);
 with N > 1 the per-frame feature records are all-gathered over RCCL every step.
 
+monocular_hd — BASELINE config[4] without the depth network: a synthetic 1280x720 stream (the build's
+HD camera synth.K_HD) through the same front end with no depth: extract + match + F verification +
+essential-matrix RANSAC / recoverPose per pair, poses chained at the reference's fallback scale
+(Slam.cpp:976-980), ATE after sim(3) alignment.  MiDaS (DepthEstimator.cpp) is not built: its
+weights are not shipped and the reference never consumes its output.
+
 roofline — the dominant throughput-bound kernel (the fused SuperPoint conv1, fp32 MFMA) measured
 with HIP events on its stream during the timed region (the tracker extracts each batch in growing
 chunks on its own stream and CU set, overlapped with tracking; FLOPs per launch = per-frame FLOPs x
@@ -98,6 +104,7 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--frontend-steps", type=int, default=6, help="timed steps of the config[3] batch front end")
     ap.add_argument("--no-frontend", action="store_true")
+    ap.add_argument("--mono-steps", type=int, default=4, help="timed steps of the config[4] monocular HD stream")
     return ap.parse_args()
 
 
@@ -170,6 +177,73 @@ def frontend_batch(ctx, L, B, rank, world, steps, warmup):
             "workload": "config[3] offline batch: per-GPU SuperPoint extract + ratio matching + F-RANSAC + 3D-3D "
                         "RANSAC (E fallback) over consecutive frame pairs, no tracking state",
             "parallelism": f"frame-sharded x{world}" + (" + RCCL all-gather of feature records" if world > 1 else "")}
+
+
+def monocular_hd(ctx, B, rank, world, steps, warmup, workers):
+    """BASELINE config[4] (depth-less): frame-sharded 1280x720 extract + match + F + E per pair."""
+    import torch
+    import torch.distributed as dist
+
+    import ate
+    import synth
+    from vslam_pipeline import DevicePipeline, PoseChain
+    t_r = time.perf_counter()
+    Lh = synth.loop_sequence(LOOP_FRAMES, workers=workers, K=synth.K_HD, w=synth.W_HD, h=synth.H_HD)
+    render_s = time.perf_counter() - t_r
+    U = LOOP_FRAMES
+    n_total = world * B
+    dev = torch.device("cuda", torch.cuda.current_device())
+    bgr = torch.from_numpy(Lh["bgr"]).to(dev)
+    del Lh["bgr"], Lh["depth"]
+    pipe = DevicePipeline(ctx, B, synth.H_HD, synth.W_HD, K=synth.K_HD, rank=rank, world=world, monocular=True)
+    chain, est, gidx = PoseChain(), [], []
+
+    def run(first, count, track):
+        pending = None
+
+        def take(S, i):
+            ok, R, t, eok, eR, et, esc = pipe.collect(S)
+            if track and world == 1:
+                for p in range(B):
+                    est.append(chain.step(ok[p], R[p], t[p], eok[p], eR[p], et[p], esc[p])[1])
+                    gidx.append((i * n_total + p) % U)
+        for i in range(first, first + count):
+            idx = torch.tensor([(i * n_total + rank * B + j) % U for j in range(B)], device=dev)
+            S = pipe.submit(bgr.index_select(0, idx), None, frame_count0=i * n_total + rank * B)
+            if pending is not None:
+                take(*pending)
+            pending = (S, i)
+        if pending is not None:
+            take(*pending)
+
+    run(0, warmup, False)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    run(warmup, steps, True)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    if world > 1:
+        tt = torch.tensor([el], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        el = float(tt.item())
+    res = {"value": round(world * B * steps / el, 3), "unit": "frames/s", "ms_per_step": round(el / steps * 1e3, 3),
+           "steps": steps, "frames_per_gpu_per_step": B, "resolution": "1280x720", "K": list(synth.K_HD),
+           "workload": "config[4] monocular stream without the MiDaS network: per-GPU SuperPoint extract + ratio "
+                       "matching + F-RANSAC + essential-matrix RANSAC / recoverPose over consecutive frame pairs, "
+                       "scale-less (MOTION_SCALE) pose chain; the device-side gather of the batch frames is inside the step",
+           "parallelism": f"frame-sharded x{world}" + (" + RCCL all-gather of feature records" if world > 1 else ""),
+           "render_s": round(render_s, 1)}
+    if world == 1 and est:
+        ts = np.arange(len(est), dtype=np.float64)
+        a = ate.compute_ate(ts, np.array(est), ts, Lh["t_wc"][np.array(gidx)])
+        res["ate_rmse_m"] = round(a["ate_rmse"], 4)
+        res["ate_note"] = "sim(3)-aligned (monocular: scale unobservable), first-pair pose chain per timed window"
+    return res
 
 
 def main():
@@ -269,6 +343,10 @@ def main():
     if not args.no_frontend and args.frontend_steps > 0:
         fe = frontend_batch(ctx, L, B, rank, world, args.frontend_steps, 2)
 
+    mono = None
+    if args.mono_steps > 0:
+        mono = monocular_hd(ctx, B, rank, world, args.mono_steps, 1, workers)
+
     if rank == 0:
         cpu = None
         if not args.no_cpu_baseline and world == 1:
@@ -320,6 +398,7 @@ def main():
             "network_tflops": round(net_flops / (net_ms / 1e3) / 1e12, 3),
             "stage_ms_per_frame": stage_ms,
             "frontend_batch": fe,
+            "monocular_hd": mono,
             "cpu_baseline": cpu,
         }
         print(json.dumps(result), flush=True)

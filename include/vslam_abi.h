@@ -247,7 +247,8 @@ int vs_estimate_motion(vs_ctx* ctx, const float* p1, const float* p2, int n, con
                        const float* depth1, const float* depth2, int h, int w, double R[9],
                        double t[3], double* scale, int* ok, int diag[8]);
 /* Pipeline form on device: P frame pairs (d_pairs, keypoints d_kps [slot][cap], the F-verified
- * matches d_kept [p][cap] / d_nkept, depth slots d_depth [slot][h][w]); pairs with d_skip[p] != 0
+ * matches d_kept [p][cap] / d_nkept, depth slots d_depth [slot][h][w], or NULL for a monocular
+ * stream: no scale, *d_scale = -1, BASELINE config[4]); pairs with d_skip[p] != 0
  * (e.g. the 3D-3D result was ok) are skipped.  d_R [p][9], d_t [p][3], d_scale [p], d_ok [p],
  * d_diag [p][8].  cap <= VS_EM_MAX_POINTS. */
 int vs_emat_motion_pairs_dev(vs_ctx* ctx, int P, const int* d_pairs, const vs_keypoint* d_kps,

@@ -107,8 +107,8 @@ __global__ __launch_bounds__(kEmThreads) void k_emat(const int* __restrict__ pai
             S.px2[2 * i] = kc[m.train_idx].x;
             S.px2[2 * i + 1] = kc[m.train_idx].y;
         }
-        d1 = depth + (size_t)pairs[2 * pb] * h * w;
-        d2 = depth + (size_t)pairs[2 * pb + 1] * h * w;
+        d1 = depth ? depth + (size_t)pairs[2 * pb] * h * w : nullptr;  // null: monocular, no scale
+        d2 = depth ? depth + (size_t)pairs[2 * pb + 1] * h * w : nullptr;
     } else {
         const int o0 = off[pb];
         n = off[pb + 1] - o0;

@@ -716,8 +716,9 @@ int vs_emat_motion_pairs_dev(vs_ctx* ctx, int P, const int* d_pairs, const vs_ke
                              const vs_match* d_kept, const int* d_nkept, const int* d_skip, const float* d_depth, int h,
                              int w, const double K[4], double* d_R, double* d_t, double* d_scale, int* d_ok, int* d_diag,
                              void* stream) {
-    VS_ARG(ctx && d_pairs && d_kps && d_kept && d_nkept && d_depth && K && d_R && d_t && d_scale && d_ok && d_diag,
+    VS_ARG(ctx && d_pairs && d_kps && d_kept && d_nkept && K && d_R && d_t && d_scale && d_ok && d_diag,
            "vs_emat_motion_pairs_dev: null argument");
+    VS_ARG(!d_depth || (h > 0 && w > 0), "vs_emat_motion_pairs_dev: bad depth size");
     VS_ARG(cap > 0 && cap <= VS_EM_MAX_POINTS, "vs_emat_motion_pairs_dev: cap out of range");
     VS_HIP(hipSetDevice(ctx->device));
     return emat_pairs(ctx, P, d_pairs, d_kps, cap, d_kept, d_nkept, d_skip, d_depth, h, w, K, d_R, d_t, d_scale, d_ok,

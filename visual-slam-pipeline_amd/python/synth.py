@@ -16,6 +16,11 @@ import numpy as np
 SEED = 20261015
 K_TUM = (525.0, 525.0, 319.5, 239.5)
 W, H = 640, 480
+# 1280x720 camera of the monocular stream (BASELINE config[4]); the reference hard-codes the TUM K
+# (Config.h:14-17), so this one is the build's own: the TUM horizontal field of view at twice the
+# focal length, principal point at the centre
+K_HD = (1050.0, 1050.0, 639.5, 359.5)
+W_HD, H_HD = 1280, 720
 
 # room: x in [-3, 3], z in [-2.5, 2.5], floor y = 0.4, ceiling y = -2.6
 _ROOM = dict(xmin=-3.0, xmax=3.0, zmin=-2.5, zmax=2.5, ymin=-2.6, ymax=0.4)
@@ -194,18 +199,19 @@ def loop_trajectory(n=126, radius=0.6, seed=SEED):
 
 
 def _render_one(args):
-    i, R, t, seed = args
+    i, R, t, seed, K, w, h = args
     scene = Scene(seed)
-    bgr, z = scene.render(R, t)
+    bgr, z = scene.render(R, t, K=K, w=w, h=h)
     rng = np.random.default_rng((seed + 17) * 1000003 + i)
     return bgr, depth_tum(z, rng)
 
 
-def loop_sequence(n, seed=SEED, dt=1.0 / 10.0, workers=None):
+def loop_sequence(n, seed=SEED, dt=1.0 / 10.0, workers=None, K=K_TUM, w=W, h=H):
     """The n frames of loop_trajectory rendered (in a process pool when workers > 1):
-    dict(bgr [n,H,W,3] u8, depth [n,H,W] f32, R_wc [n,3,3], t_wc [n,3], dt)."""
+    dict(bgr [n,h,w,3] u8, depth [n,h,w] f32, R_wc [n,3,3], t_wc [n,3], dt).  K, w, h select the
+    camera (default the TUM 640x480 one; K_HD, 1280, 720 for the monocular stream of config[4])."""
     poses = loop_trajectory(n, seed=seed)
-    jobs = [(i, R, t, seed) for i, (R, t) in enumerate(poses)]
+    jobs = [(i, R, t, seed, K, w, h) for i, (R, t) in enumerate(poses)]
     if workers is None:
         import os
         workers = min(16, os.cpu_count() or 1, n)

@@ -71,12 +71,12 @@ class _StepSet:
     """Device tables of one in-flight step (feature records of the block + halo slot, depth,
     per-pair matches / F / motion results) plus pinned host copies of the per-pair motion."""
 
-    def __init__(self, B, h, w, cap, dev):
+    def __init__(self, B, h, w, cap, dev, with_depth=True):
         F = B + 1  # slot 0 = the frame before this rank's block
         P = B
         z = lambda *shape, dt=torch.int32: torch.zeros(shape, dtype=dt, device=dev)
         self.kps, self.desc, self.n = z(F, cap * KP_BYTES, dt=torch.uint8), z(F, cap, 256, dt=torch.float32), z(F)
-        self.depth = z(F, h, w, dt=torch.float32)
+        self.depth = z(F, h, w, dt=torch.float32) if with_depth else None  # None: monocular stream
         hc, wc = (h + 7) // 8, (w + 7) // 8
         self.semi = z(B, hc, wc, va.SEMI_CH, dt=torch.float32)  # network outputs of the block
         self.dgrid = z(B, hc, wc, va.DESC_DIM, dt=torch.float32)
@@ -101,17 +101,21 @@ class DevicePipeline:
     network on the network stream, and its post-processing (decode, NMS, descriptor sampling) and
     pair geometry (match, F verification, 3D-3D RANSAC, E fallback) on the geometry stream behind an
     event, into buffer set k % 2; collect() waits for that step's geometry and returns its per-pair
-    motion.  Everything after the network (small grids, serial RANSAC replays) therefore runs on the
+    motion.  monocular=True is the depth-less stream of BASELINE config[4]: no depth tables, no 3D-3D
+    RANSAC (the reference's estimate_motion_3d3d finds no depth-valid correspondence there), and the
+    essential-matrix estimate of every pair with scale -1 (PoseChain falls back to the last good
+    scale, then MOTION_SCALE, Slam.cpp:976-980).  Everything after the network (small grids, serial RANSAC replays) therefore runs on the
     CUs the network of step k+1 leaves idle instead of serialising after it.  Set k % 2 is
     rewritten only after step k-2's geometry finished (event wait, no host sync)."""
 
     def __init__(self, ctx, B, h=480, w=640, cap=va.SP_MAX_KEYPOINTS, K=va.K_TUM, iters=200, thr=0.05,
-                 ratio=0.75, rank=0, world=1, group=None):
+                 ratio=0.75, rank=0, world=1, group=None, monocular=False):
         self.ctx, self.B, self.h, self.w, self.cap = ctx, B, h, w, cap
+        self.monocular = monocular
         self.K, self.iters, self.thr, self.ratio = K, iters, thr, ratio
         self.rank, self.world, self.group = rank, world, group
         dev = torch.device("cuda", torch.cuda.current_device())
-        self.sets = [_StepSet(B, h, w, cap, dev) for _ in range(2)]
+        self.sets = [_StepSet(B, h, w, cap, dev, with_depth=not monocular) for _ in range(2)]
         self.k = 0
         self.pairs = torch.tensor([[p, p + 1] for p in range(B)], dtype=torch.int32, device=dev)
         self._seed_base = torch.arange(B, dtype=torch.int64, device=dev)
@@ -126,7 +130,10 @@ class DevicePipeline:
         depth_prev: depth of the frame before frames[0] (halo) when world > 1."""
         B, h, w, cap = self.B, self.h, self.w, self.cap
         assert frames.shape == (B, h, w, 3) and frames.dtype == torch.uint8 and frames.is_cuda
-        assert depth.shape == (B, h, w) and depth.dtype == torch.float32
+        if self.monocular:
+            assert depth is None, "monocular pipeline: no depth"
+        else:
+            assert depth.shape == (B, h, w) and depth.dtype == torch.float32
         S, prev = self.sets[self.k % 2], self.sets[(self.k + 1) % 2]
         self.k += 1
         ctx = self.ctx
@@ -135,11 +142,15 @@ class DevicePipeline:
         with torch.cuda.stream(self.s_net):
             self.s_net.wait_event(S.geo_done)  # step k-2's geometry has released this set
             s = self.s_net.cuda_stream
-            if self.world == 1:  # carry the previous step's last depth map into slot 0
+            if self.monocular:
+                pass
+            elif self.world == 1:  # carry the previous step's last depth map into slot 0
                 S.depth[0].copy_(prev.depth[B])
-            elif depth_prev is not None:
-                S.depth[0].copy_(depth_prev)
-            S.depth[1:].copy_(depth)
+                S.depth[1:].copy_(depth)
+            else:
+                if depth_prev is not None:
+                    S.depth[0].copy_(depth_prev)
+                S.depth[1:].copy_(depth)
             ctx.network_batch_dev(B, frames.data_ptr(), h, w, S.semi.data_ptr(), S.dgrid.data_ptr(), s)
             S.net_done.record(self.s_net)
         with torch.cuda.stream(self.s_geo):
@@ -161,14 +172,16 @@ class DevicePipeline:
             ctx.fmat_verify_pairs_dev(B, self.pairs.data_ptr(), S.kps.data_ptr(), cap, S.good.data_ptr(),
                                       S.ngood.data_ptr(), S.F.data_ptr(), S.fkept.data_ptr(),
                                       S.nfkept.data_ptr(), S.eperr.data_ptr(), S.fdiag.data_ptr(), s)
-            ctx.ransac_3d3d_pairs_dev(B, self.pairs.data_ptr(), S.kps.data_ptr(), cap, S.fkept.data_ptr(),
-                                      S.nfkept.data_ptr(), S.depth.data_ptr(), h, w, self.K, S.seeds.data_ptr(),
-                                      self.iters, self.thr, S.R.data_ptr(), S.t.data_ptr(), S.ok.data_ptr(),
-                                      S.diag.data_ptr(), s)
+            if not self.monocular:  # monocular: S.ok stays 0, every pair takes the E path
+                ctx.ransac_3d3d_pairs_dev(B, self.pairs.data_ptr(), S.kps.data_ptr(), cap, S.fkept.data_ptr(),
+                                          S.nfkept.data_ptr(), S.depth.data_ptr(), h, w, self.K,
+                                          S.seeds.data_ptr(), self.iters, self.thr, S.R.data_ptr(), S.t.data_ptr(),
+                                          S.ok.data_ptr(), S.diag.data_ptr(), s)
             # Slam.cpp:965-984: pairs whose 3D-3D estimate failed fall back to the essential matrix
             # with depth scale (the kernel skips pairs with ok != 0)
             ctx.emat_motion_pairs_dev(B, self.pairs.data_ptr(), S.kps.data_ptr(), cap, S.fkept.data_ptr(),
-                                      S.nfkept.data_ptr(), S.ok.data_ptr(), S.depth.data_ptr(), h, w,
+                                      S.nfkept.data_ptr(), S.ok.data_ptr(),
+                                      None if self.monocular else S.depth.data_ptr(), h, w,
                                       S.eR.data_ptr(), S.et.data_ptr(), S.escale.data_ptr(),
                                       S.eok.data_ptr(), S.ediag.data_ptr(), K=self.K, stream=s)
             # the host tracker's input: one packed D2H of the per-pair motion
