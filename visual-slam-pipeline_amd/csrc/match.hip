@@ -99,21 +99,33 @@ __global__ __launch_bounds__(256) void k_match(const int* __restrict__ pairs, co
     if (tid < kTrainChunk) s_nb[tid] = (t0 + tid < n2) ? normst[(size_t)tf * tstride + t0 + tid] : 0.0f;
     const float* Q = descq + ((size_t)qf * qstride + (qvalid ? qj : 0)) * 256;
     float qreg[128];
+    const bool wlive = q0 + wv * 32 < n1;  // wave-uniform
 #pragma unroll
-    for (int s = 0; s < 128; s++) qreg[s] = qvalid ? Q[2 * s + lh] : 0.0f;
+    for (int s = 0; s < 128; s++) qreg[s] = (qvalid && wlive) ? Q[2 * s + lh] : 0.0f;
     const float na = qvalid ? normsq[(size_t)qf * qstride + qj] : 0.0f;
     __syncthreads();
+    // padding is not computed: a wave whose 32 queries are all past n1 leaves (no barrier follows),
+    // and the upper 32 train rows of a slice are skipped when all of them are past n2
+    if (q0 + wv * 32 >= n1) return;
     Best2 best;
     best.init();
     f32x16 acc0, acc1;
 #pragma unroll
     for (int e = 0; e < 16; e++) acc0[e] = acc1[e] = 0.0f;
+    if (t0 + 32 < n2) {
 #pragma unroll
-    for (int s = 0; s < 128; s++) {
-        const float a0 = s_t[(2 * s + lh) * kTrainChunk + li];
-        const float a1 = s_t[(2 * s + lh) * kTrainChunk + 32 + li];
-        acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, qreg[s], acc0, 0, 0, 0);
-        acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, qreg[s], acc1, 0, 0, 0);
+        for (int s = 0; s < 128; s++) {
+            const float a0 = s_t[(2 * s + lh) * kTrainChunk + li];
+            const float a1 = s_t[(2 * s + lh) * kTrainChunk + 32 + li];
+            acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, qreg[s], acc0, 0, 0, 0);
+            acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, qreg[s], acc1, 0, 0, 0);
+        }
+    } else {
+#pragma unroll
+        for (int s = 0; s < 128; s++) {
+            const float a0 = s_t[(2 * s + lh) * kTrainChunk + li];
+            acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, qreg[s], acc0, 0, 0, 0);
+        }
     }
     // C/D: col = query (lane&31), row = train (reg&3) + 8*(reg>>2) + 4*(lane>>5)
 #pragma unroll
