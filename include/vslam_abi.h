@@ -323,6 +323,12 @@ int vs_profile_reset(vs_ctx* ctx);
 int vs_profile_read(vs_ctx* ctx, int max_stages, const char** names, double* ms, int* launches,
                     int* n_stages);
 
+/* ---- test support -------------------------------------------------------------------- */
+/* The device's correctly rounded fp64 functions (csrc/cr_math.h, used by Rodrigues, the 7-point
+ * cubic and RANSACUpdateNumIters) on n host inputs: op 0 sin(a), 1 cos(a), 2 acos(a), 3 log(a),
+ * 4 pow(a, b) (b may be NULL for ops 0-3).  Synchronous; out has n entries. */
+int vs_selftest_crmath(vs_ctx* ctx, int op, int n, const double* a, const double* b, double* out);
+
 #ifdef __cplusplus
 }
 #endif

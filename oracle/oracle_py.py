@@ -64,6 +64,7 @@ _SIG = {
     "orc_expf_array": (None, [_P, _I, _P]),
     "orc_expf_exhaustive_check": (ctypes.c_long, [ctypes.c_float, ctypes.c_float]),
     "orc_expf_restated_check": (ctypes.c_long, [ctypes.c_float, ctypes.c_float, ctypes.c_int]),
+    "orc_crmath": (None, [ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
 }
 
 _lib = None
@@ -401,6 +402,18 @@ def expf(x):
     x = np.ascontiguousarray(x, np.float32)
     out = np.zeros_like(x)
     lib().orc_expf_array(_p(x), x.size, _p(out))
+    return out
+
+
+CRMATH_OPS = {"sin": 0, "cos": 1, "acos": 2, "log": 3, "pow": 4}
+
+
+def crmath(op, a, b=None):
+    """Correctly rounded sin / cos / acos / log / pow (libquadmath, rounded to double)."""
+    a = np.ascontiguousarray(a, np.float64)
+    b = a if b is None else np.ascontiguousarray(b, np.float64)
+    out = np.zeros_like(a)
+    lib().orc_crmath(CRMATH_OPS[op], a.size, _p(a), _p(b), _p(out))
     return out
 
 

@@ -4,6 +4,7 @@
 // stage (OracleOps below).  tests/ run the GPU tracker (vs_slam_*, libvslam_hip.so) and this one
 // on the same features and compare trajectories, map sizes and decision counters; bench.py may
 // time it as the CPU baseline.  The product never links this file.
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <vector>
@@ -177,6 +178,14 @@ struct OrcSlam {
     OracleOps ops;
     vs_trk::Tracker<OracleOps> trk{ops};
     std::vector<vs_trk::FramePtr> holding;  // frames that still own features / depth
+    FILE* trace = nullptr;                  // VS_TRACE_ORACLE=path: stage trace (debugging aid)
+    OrcSlam() {
+        if (const char* p = std::getenv("VS_TRACE_ORACLE")) trace = std::fopen(p, "w");
+        trk.set_trace(trace);
+    }
+    ~OrcSlam() {
+        if (trace) std::fclose(trace);
+    }
 };
 
 }  // namespace

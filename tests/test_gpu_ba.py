@@ -3,7 +3,7 @@
 Same algorithm and per-element accumulation order on both sides (ba_solvers.h; chunked global
 sums); the remaining differences are last-ulp libm differences inside Rodrigues, so the LM
 trajectory (iterations, accepted steps) must match exactly and poses / points / RMS errors to
-1e-9 (relative for the errors)."""
+1e-9 (relative for the errors and for points, to their distance)."""
 import numpy as np
 import pytest
 
@@ -44,7 +44,11 @@ def _compare(g, o):
     Ro, to, Po, ebo, eao, so = o
     assert np.array_equal(sg, so), (sg, so)
     assert abs(ebg - ebo) <= 1e-9 * max(1.0, ebo) and abs(eag - eao) <= 1e-9 * max(1.0, eao)
-    assert np.max(np.abs(Pg - Po)) <= 1e-9 and np.max(np.abs(tg - to)) <= 1e-9 and np.max(np.abs(Rg - Ro)) <= 1e-9
+    # points: 1e-9 relative to their distance (the 50 KF / 10k window has weakly constrained
+    # points 16 m out whose last-ulp Rodrigues differences grow to ~8e-9 m)
+    tol = 1e-9 * np.maximum(1.0, np.linalg.norm(Po, axis=1))[:, None]
+    assert np.all(np.abs(Pg - Po) <= tol), np.max(np.abs(Pg - Po))
+    assert np.max(np.abs(tg - to)) <= 1e-9 and np.max(np.abs(Rg - Ro)) <= 1e-9
 
 
 @pytest.mark.parametrize("args", [dict(N=5, M=120, seed=0), dict(N=4, M=60, seed=1, noise=0.3, pert=0.02, outliers=3),
@@ -54,9 +58,12 @@ def test_local_ba_matches_oracle(vsctx, oracle, args):
     _compare(vsctx.local_ba(R, t, P0, kf, pt, uv), oracle.local_ba(R, t, P0, kf, pt, uv))
 
 
-@pytest.mark.parametrize("N,M,seed", [(10, 2000, 3), (30, 6000, 4)])
-def test_local_ba_window_matches_oracle(vsctx, oracle, N, M, seed):
-    R, t, P, P0, kf, pt, uv = windowed_problem(N, M, seed)
+# (50, 10000, span 3, 1 px, 5 cm): BASELINE config[2], the 50-keyframe / 10k-MapPoint stress
+# window exactly as tools/bench_ba.py times it
+@pytest.mark.parametrize("N,M,seed,kw", [(10, 2000, 3, {}), (30, 6000, 4, {}), (50, 10000, 5, {}),
+                                         (50, 10000, 7, dict(span=3, noise=1.0, pert=0.05))])
+def test_local_ba_window_matches_oracle(vsctx, oracle, N, M, seed, kw):
+    R, t, P, P0, kf, pt, uv = windowed_problem(N, M, seed, **kw)
     g = vsctx.local_ba(R, t, P0, kf, pt, uv)
     _compare(g, oracle.local_ba(R, t, P0, kf, pt, uv))
     assert g[4] < g[3]

@@ -146,6 +146,48 @@ def test_match_edges_and_ties(vsctx, oracle):
         assert _match_equal(rg, ro) and _match_equal(gg, go)
 
 
+@pytest.mark.parametrize("P", [3, 40])
+def test_match_pairs_batched_bit_exact(vsctx, oracle, P):
+    """One vs_match_pairs_dev launch over P pairs of a frame pool (P = 40 takes the 64 x 64
+    workgroup tile, P = 3 the 32 x 32 one), ragged counts incl. empty / single-row frames and a
+    frame paired with itself; every pair's lists must equal the oracle's."""
+    import synth
+    import torch
+    cap = 400
+    F = P + 2
+    rng = np.random.default_rng(P)
+    n = rng.integers(300, cap + 1, F).astype(np.int32)
+    n[1], n[2], n[3] = 0, 1, 2
+    desc = np.zeros((F, cap, 256), np.float32)
+    for f in range(F):
+        desc[f, :n[f]] = synth.random_descriptors(int(n[f]), 100 + f)
+        if f and n[f] > 50 and n[f - 1] > 50:  # planted neighbours of the previous frame
+            desc[f, :50] = desc[f - 1, :50] + 0.1 * synth.random_descriptors(50, 900 + f)
+    pairs = [(f, f + 1) for f in range(P)]
+    pairs[-1] = (F - 1, F - 1)
+    pairs = np.array(pairs, np.int32)
+    dev = torch.device("cuda", 0)
+    d_desc = torch.from_numpy(desc).to(dev)
+    d_n = torch.from_numpy(n).to(dev)
+    d_pairs = torch.from_numpy(pairs).to(dev)
+    raw = torch.zeros((P, cap, 4), dtype=torch.int32, device=dev)
+    good = torch.zeros_like(raw)
+    nraw = torch.full((P,), -1, dtype=torch.int32, device=dev)
+    ngood = torch.full((P,), -1, dtype=torch.int32, device=dev)
+    for rep in range(2):  # the second launch reuses the keys / counters the first left reset
+        torch.cuda.synchronize()
+        vsctx.match_pairs_dev(P, d_pairs.data_ptr(), F, d_desc.data_ptr(), d_n.data_ptr(), cap, 0.75,
+                              raw.data_ptr(), nraw.data_ptr(), good.data_ptr(), ngood.data_ptr())
+        torch.cuda.synchronize()
+        rh, gh = raw.cpu().numpy(), good.cpu().numpy()
+        nr, ng = nraw.cpu().numpy(), ngood.cpu().numpy()
+        for p, (a, b) in enumerate(pairs):
+            ro, go = oracle.match_ratio(desc[a, :n[a]], desc[b, :n[b]])
+            assert nr[p] == len(ro) and ng[p] == len(go), (p, nr[p], len(ro), ng[p], len(go))
+            assert np.array_equal(rh[p, :nr[p]].view(np.uint8).ravel(), ro.view(np.uint8).ravel()), p
+            assert np.array_equal(gh[p, :ng[p]].view(np.uint8).ravel(), go.view(np.uint8).ravel()), p
+
+
 def test_match_bit_exact_real_descriptors(vsctx, oracle, seq4):
     feats = vsctx.extract_batch([f["bgr"] for f in seq4])
     for i in range(3):

@@ -1,0 +1,100 @@
+"""GPU parity of the tracking loop at the bench's own settings (SURVEY.md 8(f)
+F1: Slam::process_frame, reference src/Slam.cpp:809-1135, restated in host/tracker.hpp).
+
+bench.py runs vs_slam_process_batch_dev with B = 32 frames per call, the default extraction chunk
+schedule (3, 4, 5, 7, 8, 5) on its own CU-masked stream and the default VS_SLAM_TRACK_CUS, over the
+126-frame closed loop replayed with continuing timestamps.  This test runs exactly that for 416
+frames (3.3 laps, map past 20k points) and the oracle tracker (oracle/orc_slam.cpp: the same control
+flow over the CPU restatements) on the same GPU features, and compares decision counters, the whole
+trajectory and the map."""
+import numpy as np
+import pytest
+import torch
+
+import ate
+import synth
+import vslam_abi
+
+pytestmark = pytest.mark.gpu
+
+LOOP = 126
+B = 32
+STEPS = 13          # 416 frames
+T0 = 1311868164.0
+
+
+@pytest.fixture(scope="module")
+def loop():
+    return synth.loop_sequence(LOOP, workers=8)
+
+
+@pytest.fixture(scope="module")
+def loop_feats(vsctx, loop):
+    out = []
+    for i in range(0, LOOP, 32):
+        out += vsctx.extract_batch(list(loop["bgr"][i:i + 32]))
+    return out
+
+
+@pytest.fixture(scope="module")
+def gpu_run(vsctx, loop):
+    dev = torch.device("cuda", 0)
+    wrap = np.concatenate([np.arange(LOOP), np.arange(B)])
+    bgr = torch.from_numpy(loop["bgr"][wrap]).to(dev)
+    dep = torch.from_numpy(loop["depth"][wrap]).to(dev)
+    hdep = [loop["depth"][i] for i in wrap]
+    torch.cuda.synchronize()
+    with vslam_abi.Slam(vsctx, max_batch=B) as S:
+        done = []
+        for k in range(STEPS):
+            g0 = k * B
+            i0 = g0 % LOOP
+            done += S.process_batch_dev(B, bgr[i0].data_ptr(), dep[i0].data_ptr(), hdep[i0:i0 + B],
+                                        [T0 + 0.1 * (g0 + j) for j in range(B)],
+                                        [3 * (g0 + j) for j in range(B)]).tolist()
+        traj_raw = S.trajectory()
+        S.finish()
+        return done, S.stats(), traj_raw, S.trajectory(), S.map_points()
+
+
+@pytest.fixture(scope="module")
+def oracle_run(oracle, loop, loop_feats):
+    S = oracle.Slam()
+    done = []
+    for g in range(STEPS * B):
+        k, d = loop_feats[g % LOOP]
+        done.append(S.process(k, d, loop["depth"][g % LOOP], T0 + 0.1 * g, 3 * g))
+    traj_raw = S.trajectory()
+    S.finish()
+    out = done, S.stats(), traj_raw, S.trajectory(), S.map_points()
+    S.close()
+    return out
+
+
+def test_bench_scale_tracker_matches_oracle(gpu_run, oracle_run, loop):
+    g, o = gpu_run, oracle_run
+    stats = dict(zip(vslam_abi.SLAM_STATS, g[1].tolist()))
+    ostats = dict(zip(vslam_abi.SLAM_STATS, o[1].tolist()))
+    assert g[0] == o[0]
+    assert stats == ostats, (stats, ostats)
+    assert stats["processed"] == STEPS * B
+    assert stats["map_points"] > 20000, stats
+    for (gi, gts, gR, gt), (oi, ots, oR, ot) in [(g[2], o[2]), (g[3], o[3])]:
+        assert np.array_equal(gi, oi) and np.array_equal(gts, ots)
+        np.testing.assert_allclose(gR, oR, rtol=0, atol=1e-7)
+        np.testing.assert_allclose(gt, ot, rtol=0, atol=1e-7)
+    (gp, gv), (op, ov) = g[4], o[4]
+    assert np.array_equal(gv, ov)
+    np.testing.assert_allclose(gp, op, rtol=0, atol=1e-7)
+
+
+def test_bench_scale_ate_is_the_algorithms(gpu_run, oracle_run, loop):
+    """The ATE and sim(3) scale of the bench sequence are properties of the restated algorithm
+    (random SuperPoint weights), not of the GPU path: both trackers give the same numbers."""
+    res = []
+    for run in (gpu_run, oracle_run):
+        ids, ts, R, t = run[3]
+        gi = np.round((ts - T0) / 0.1).astype(int) % LOOP
+        res.append(ate.compute_ate(ts, t, ts, loop["t_wc"][gi]))
+    assert abs(res[0]["ate_rmse"] - res[1]["ate_rmse"]) < 1e-6, res
+    assert abs(res[0]["scale"] - res[1]["scale"]) < 1e-6, res

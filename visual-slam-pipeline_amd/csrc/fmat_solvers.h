@@ -102,16 +102,16 @@ VS_HD inline int solve_cubic(const double* c, double* x) {
         const double Qcubed = Q * Q * Q;
         double d = Qcubed - R * R;
         if (d >= 0) {
-            const double theta = acos(R / sqrt(Qcubed));
+            const double theta = vs_cr::acos(R / sqrt(Qcubed));
             const double sqrtQ = sqrt(Q);
             const double t0 = -2 * sqrtQ, t1 = theta * (1. / 3), t2 = a1 * (1. / 3);
-            x[0] = t0 * cos(t1) - t2;
-            x[1] = t0 * cos(t1 + (2. * M_PI / 3)) - t2;
-            x[2] = t0 * cos(t1 + (4. * M_PI / 3)) - t2;
+            x[0] = t0 * vs_cr::cos(t1) - t2;
+            x[1] = t0 * vs_cr::cos(t1 + (2. * M_PI / 3)) - t2;
+            x[2] = t0 * vs_cr::cos(t1 + (4. * M_PI / 3)) - t2;
             n = 3;
         } else {
             d = sqrt(-d);
-            double e = pow(d + fabs(R), 1. / 3);
+            double e = vs_cr::pow(d + fabs(R), 1. / 3);
             if (R > 0) e = -e;
             x[0] = (e + Q / e) - a1 * (1. / 3);
             n = 1;

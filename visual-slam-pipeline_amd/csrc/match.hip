@@ -2,22 +2,36 @@
 //
 // Exact L2 2-NN + Lowe ratio test.  The reference's FLANN kd-tree search is approximate; the
 // exact 2-NN it approximates is the only definable semantics (DESIGN.md "Matching"):
-//   dot(q, t) on the fp32 matrix cores: v_mfma_f32_32x32x2_f32 accumulates k = 2s, 2s+1 per
-//   instruction as a k-ordered fp32 fmaf chain, so chaining s = 0..127 gives exactly the
+//   dot(q, t) on the fp32 matrix cores: v_mfma_f32_16x16x4_f32 accumulates k = 4s .. 4s+3 per
+//   instruction as a k-ordered fp32 fmaf chain, so chaining s = 0..63 gives exactly the
 //   sequential fmaf chain over k = 0..255 that the CPU oracle computes;
 //   d2 = max((na + nb) - 2*dot, 0) with the row norms as sequential fmaf chains;
 //   best / second = the two smallest (d2, train index) pairs; distance = sqrtf(d2);
 //   good iff sqrtf(d0) < ratio * sqrtf(d1).
 // Pair lists are therefore bit-identical to the oracle.
 //
-// Mapping: A operand = 32 train rows (M), B operand = 32 query rows (N).  A workgroup owns 128
-// query rows (one 32-row N block per wave, its K = 256 values held in 128 VGPRs) and one slice of
-// 64 train rows staged through LDS (k-major, conflict free); the grid is pairs x query blocks x
-// train slices, so even a single pair spreads over tens of CUs.  The accumulator puts one query
-// per lane and 16 train rows per register set, so the slice's top-2 is per-lane register work,
-// merged with the partner half-wave by one shuffle.  The compaction kernel merges the slices'
-// top-2 per query (a total order on (d2, train index), so the merge order cannot matter), then
-// applies the ratio test and compacts in query order.
+// One launch per call (any number of pairs):
+//   * grid = pairs x query blocks x train blocks, linearised so that the 8-block round-robin XCD
+//     placement gives each XCD a contiguous range of pairs (one pair's descriptors stay in one L2);
+//   * a workgroup (4 waves, 2 x 2) owns 2WQ queries x 2WT train rows and stages them through LDS in
+//     k-chunks of 64 with one-chunk register prefetch: coalesced 16 B global loads of 16
+//     consecutive k per thread, a 4 x 4 register transpose, and 16 B LDS stores into rows padded to
+//     72 floats, so every MFMA fragment (lane i, k-group g) is one conflict-free ds_read_b128 that
+//     carries four consecutive MFMA steps;
+//   * each wave chains (WQ/16) x (WT/16) independent 16x16 accumulators over the 64 steps (the
+//     16x16x4 MFMA issues every 32 cycles with a 40-cycle dependent latency, so >= 2 chains per
+//     wave, or >= 2 waves per SIMD, keep the matrix pipe busy);
+//   * row norms: either the caller's (computed once per frame) or sequential fmaf chains over the
+//     staged chunks, one thread per row, interleaved with the MFMAs;
+//   * the per-query top-2 of a wave is merged across train blocks with 64-bit atomicMin on keys
+//     (d2 bits << 32 | train index; d2 >= +0 so the bits order like the floats, and the index
+//     breaks ties toward the lower index): best0 keeps the minimum and the key it displaces (or
+//     the rejected candidate) goes to best1, so best1 ends as the minimum over everything except
+//     best0 — the exact top-2 of the union, independent of arrival order;
+//   * the last workgroup of a pair to arrive (a device-scope counter; every atomic of the earlier
+//     workgroups has returned before their arrival) reads and resets the keys with atomicExch,
+//     applies the ratio test and compacts the good rows in query order.  Keys and counters are
+//     left reset for the next launch.
 #include <hip/hip_runtime.h>
 
 #include <climits>
@@ -26,23 +40,9 @@
 
 namespace vs {
 
-typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-struct Best2 {
-    float d0, d1;
-    int j0, j1;
-    __device__ void init() {
-        d0 = d1 = __int_as_float(0x7f800000);
-        j0 = j1 = INT_MAX;
-    }
-    __device__ void push(float d, int j) {
-        if (d < d0 || (d == d0 && j < j0)) {
-            d1 = d0; j1 = j0; d0 = d; j0 = j;
-        } else if (d < d1 || (d == d1 && j < j1)) {
-            d1 = d; j1 = j;
-        }
-    }
-};
+constexpr unsigned long long kNoKey = ~0ull;
 
 // Sequential fmaf-chain squared norm of every descriptor row of F frames.
 __global__ __launch_bounds__(256) void k_desc_norms(const float* __restrict__ desc, const int* __restrict__ n,
@@ -63,131 +63,252 @@ __global__ __launch_bounds__(256) void k_desc_norms(const float* __restrict__ de
     norms[r] = s;
 }
 
-constexpr int kTrainChunk = 64;
-
-struct Part2 {  // a train slice's top-2 for one query
-    float d0, d1;
-    int j0, j1;
-};
-
-__global__ __launch_bounds__(256) void k_match(const int* __restrict__ pairs, const float* __restrict__ descq,
-                                               const float* __restrict__ desct, const float* __restrict__ normsq,
-                                               const float* __restrict__ normst, const int* __restrict__ n,
-                                               int qstride, int tstride, int cap, int nslices,
-                                               Part2* __restrict__ part) {
-    __shared__ float s_t[256 * kTrainChunk];  // [k][m]
-    __shared__ float s_nb[kTrainChunk];
-    const int p = blockIdx.x;
-    const int qf = pairs[2 * p], tf = pairs[2 * p + 1];
-    const int n1 = n[qf], n2 = n[tf];
-    const int q0 = blockIdx.y * 128, t0 = blockIdx.z * kTrainChunk;
-    if (q0 >= n1 || n2 < 2 || t0 >= n2) return;
-    const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63, li = lane & 31, lh = lane >> 5;
-    const int qj = q0 + wv * 32 + li;
-    const bool qvalid = qj < n1;
-    const float* T = desct + (size_t)tf * tstride * 256;
-    // stage the slice's train rows, k-major; lanes walk rows so LDS writes are conflict free
-    for (int idx = tid; idx < kTrainChunk * 64; idx += 256) {
-        int m = idx & (kTrainChunk - 1), k4 = idx / kTrainChunk;
-        float4 v = {0.f, 0.f, 0.f, 0.f};
-        if (t0 + m < n2) v = reinterpret_cast<const float4*>(T + (size_t)(t0 + m) * 256)[k4];
-        s_t[(4 * k4 + 0) * kTrainChunk + m] = v.x;
-        s_t[(4 * k4 + 1) * kTrainChunk + m] = v.y;
-        s_t[(4 * k4 + 2) * kTrainChunk + m] = v.z;
-        s_t[(4 * k4 + 3) * kTrainChunk + m] = v.w;
-    }
-    if (tid < kTrainChunk) s_nb[tid] = (t0 + tid < n2) ? normst[(size_t)tf * tstride + t0 + tid] : 0.0f;
-    const float* Q = descq + ((size_t)qf * qstride + (qvalid ? qj : 0)) * 256;
-    float qreg[128];
-    const bool wlive = q0 + wv * 32 < n1;  // wave-uniform
-#pragma unroll
-    for (int s = 0; s < 128; s++) qreg[s] = (qvalid && wlive) ? Q[2 * s + lh] : 0.0f;
-    const float na = qvalid ? normsq[(size_t)qf * qstride + qj] : 0.0f;
-    __syncthreads();
-    // padding is not computed: a wave whose 32 queries are all past n1 leaves (no barrier follows),
-    // and the upper 32 train rows of a slice are skipped when all of them are past n2
-    if (q0 + wv * 32 >= n1) return;
-    Best2 best;
-    best.init();
-    f32x16 acc0, acc1;
-#pragma unroll
-    for (int e = 0; e < 16; e++) acc0[e] = acc1[e] = 0.0f;
-    if (t0 + 32 < n2) {
-#pragma unroll
-        for (int s = 0; s < 128; s++) {
-            const float a0 = s_t[(2 * s + lh) * kTrainChunk + li];
-            const float a1 = s_t[(2 * s + lh) * kTrainChunk + 32 + li];
-            acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, qreg[s], acc0, 0, 0, 0);
-            acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, qreg[s], acc1, 0, 0, 0);
-        }
-    } else {
-#pragma unroll
-        for (int s = 0; s < 128; s++) {
-            const float a0 = s_t[(2 * s + lh) * kTrainChunk + li];
-            acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, qreg[s], acc0, 0, 0, 0);
-        }
-    }
-    // C/D: col = query (lane&31), row = train (reg&3) + 8*(reg>>2) + 4*(lane>>5)
-#pragma unroll
-    for (int reg = 0; reg < 16; reg++) {
-        const int mr = (reg & 3) + 8 * (reg >> 2) + 4 * lh;
-        if (t0 + mr < n2) {
-            float s = na + s_nb[mr];
-            float d = s - 2.0f * acc0[reg];
-            best.push(d < 0.0f ? 0.0f : d, t0 + mr);
-        }
-        if (t0 + 32 + mr < n2) {
-            float s = na + s_nb[32 + mr];
-            float d = s - 2.0f * acc1[reg];
-            best.push(d < 0.0f ? 0.0f : d, t0 + 32 + mr);
-        }
-    }
-    // merge the two half-waves that saw disjoint train rows of the same query
-    Best2 other;
-    other.d0 = __shfl_xor(best.d0, 32);
-    other.d1 = __shfl_xor(best.d1, 32);
-    other.j0 = __shfl_xor(best.j0, 32);
-    other.j1 = __shfl_xor(best.j1, 32);
-    best.push(other.d0, other.j0);
-    best.push(other.d1, other.j1);
-    if (lh == 0 && qvalid) part[((size_t)p * nslices + blockIdx.z) * cap + qj] = {best.d0, best.d1, best.j0, best.j1};
+__device__ __forceinline__ unsigned long long shfl_xor_u64(unsigned long long v, int m) {
+    const unsigned lo = __shfl_xor((unsigned)v, m), hi = __shfl_xor((unsigned)(v >> 32), m);
+    return ((unsigned long long)hi << 32) | lo;
 }
 
-// Per query: merge the train slices' top-2, distance = sqrtf(d2), ratio test (Slam.cpp:1151-1157);
-// then the order-preserving compaction of the good rows (query order).
-__global__ __launch_bounds__(1024) void k_match_compact(const int* __restrict__ pairs, const int* __restrict__ n,
-                                                        int cap, int nslices, float ratio,
-                                                        const Part2* __restrict__ part, vs_match* __restrict__ raw,
-                                                        int* __restrict__ nraw, vs_match* __restrict__ good,
-                                                        int* __restrict__ ngood) {
-    __shared__ int s_wave[16];
-    __shared__ int s_base;
-    const int p = blockIdx.x;
-    const int n1 = n[pairs[2 * p]], n2 = n[pairs[2 * p + 1]];
-    const int rows = (n2 >= 2) ? n1 : 0;
-    const int used = (n2 + kTrainChunk - 1) / kTrainChunk;
-    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    if (threadIdx.x == 0) s_base = 0;
+// top-2 of a set of distinct keys (k0 < k1), branch-free
+__device__ __forceinline__ void push2(unsigned long long& k0, unsigned long long& k1, unsigned long long k) {
+    const unsigned long long lo = k < k0 ? k : k0, hi = k < k0 ? k0 : k;
+    k1 = hi < k1 ? hi : k1;
+    k0 = lo;
+}
+
+struct MatchArgs {
+    const int* pairs;      // [P][2] (query frame, train frame)
+    const float* descq;    // query frames, row stride 256 floats, frame stride qstride rows
+    const float* desct;    // train frames (tstride 0: one set)
+    const float* normsq;   // optional caller norms, same indexing as the rows
+    const float* normst;
+    const int* n;          // rows per frame
+    int qstride, tstride;
+    int qblocks, tblocks;  // grid extents per pair (capacity)
+    int work, per_xcd;     // P * qblocks * tblocks; blocks per XCD range
+    float ratio;
+    unsigned long long* keys;  // [P][2][kcap]
+    int kcap;
+    unsigned* cnt;             // [P] arrival counters
+    vs_match* raw;             // [P][ostride]
+    int* nraw;
+    vs_match* good;
+    int* ngood;
+    int ostride;
+};
+
+template <int WQ, int WT, int KC, bool NORMS>
+__global__ __launch_bounds__(256) void k_match(MatchArgs a) {
+    constexpr int TQ = 2 * WQ, TT = 2 * WT, R = TQ + TT;
+    constexpr int FQ = WQ / 16, FT = WT / 16;
+    constexpr int NC = 256 / KC;           // staged chunks
+    constexpr int NB = NC > 1 ? 2 : 1;     // LDS buffers
+    constexpr int RS4 = KC / 4 + 2;        // row stride in float4: KC + 8 floats = 8 mod 64 dwords
+    constexpr int GR = KC / 16;            // 16-k groups per row and chunk
+    constexpr int GPT = R * GR / 256;      // groups per thread and chunk
+    constexpr int NR = R / 4;              // norm rows per wave
+    __shared__ float4 sbuf[NB][R * RS4];
+    __shared__ float s_norm[R];
+    __shared__ int s_wave[4];
+    __shared__ int s_last, s_base;
+
+    // linear work index: XCD x (= blockIdx % 8 under round-robin placement) takes a contiguous range
+    const int L = (blockIdx.x & 7) * a.per_xcd + (blockIdx.x >> 3);
+    if (L >= a.work) return;
+    const int per_pair = a.qblocks * a.tblocks;
+    const int p = L / per_pair, r0 = L - p * per_pair;
+    const int qb = r0 / a.tblocks, tb = r0 - qb * a.tblocks;
+    const int qf = a.pairs[2 * p], tf = a.pairs[2 * p + 1];
+    const int n1 = a.n[qf], n2 = a.n[tf];
+    const int tid = threadIdx.x;
+    if (n1 <= 0 || n2 < 2) {  // empty Mat / fewer than k = 2 neighbours: no matches (Slam.cpp:1151-1153)
+        if (qb == 0 && tb == 0 && tid == 0) {
+            a.nraw[p] = 0;
+            a.ngood[p] = 0;
+        }
+        return;
+    }
+    const int nq = (n1 + TQ - 1) / TQ, nt = (n2 + TT - 1) / TT;
+    if (qb >= nq || tb >= nt) return;
+    const int q0 = qb * TQ, t0 = tb * TT;
+    const float* Q = a.descq + (size_t)qf * a.qstride * 256;
+    const float* T = a.desct + (size_t)tf * a.tstride * 256;
+
+    // staging: group G = tid + 256 u -> LDS row G / GR, 16 consecutive k at (G % GR) * 16 of the chunk.
+    // Rows past n1 / n2 re-read the last valid row (their results are never used), so every load
+    // is unconditional and the compiler keeps all of them in flight together.
+    const float4* src[GPT];
+#pragma unroll
+    for (int u = 0; u < GPT; u++) {
+        const int G = tid + 256 * u, row = G / GR, q4 = G % GR;
+        const float* base = row < TQ ? Q + (size_t)min(q0 + row, n1 - 1) * 256
+                                     : T + (size_t)min(t0 + row - TQ, n2 - 1) * 256;
+        src[u] = reinterpret_cast<const float4*>(base) + 4 * q4;
+    }
+    float4 reg[GPT][4];
+    auto load = [&](int c) {
+#pragma unroll
+        for (int u = 0; u < GPT; u++)
+#pragma unroll
+            for (int j = 0; j < 4; j++) reg[u][j] = src[u][(KC / 4) * c + j];
+    };
+    // position 4g + j of a 16-k group holds k = 4j + g: the fragment of lane group g is one float4
+    auto store = [&](int buf) {
+#pragma unroll
+        for (int u = 0; u < GPT; u++) {
+            const int G = tid + 256 * u, row = G / GR, q4 = G % GR;
+            float4* d = &sbuf[buf][row * RS4 + 4 * q4];
+            d[0] = make_float4(reg[u][0].x, reg[u][1].x, reg[u][2].x, reg[u][3].x);
+            d[1] = make_float4(reg[u][0].y, reg[u][1].y, reg[u][2].y, reg[u][3].y);
+            d[2] = make_float4(reg[u][0].z, reg[u][1].z, reg[u][2].z, reg[u][3].z);
+            d[3] = make_float4(reg[u][0].w, reg[u][1].w, reg[u][2].w, reg[u][3].w);
+        }
+    };
+
+    const int wv = tid >> 6, lane = tid & 63, li = lane & 15, lg = lane >> 4;
+    const int wq = wv & 1, wt = wv >> 1;
+    const int qrow0 = wq * WQ, trow0 = TQ + wt * WT;  // LDS rows of this wave's fragments
+    f32x4 acc[FT][FQ];
+#pragma unroll
+    for (int x = 0; x < FT; x++)
+#pragma unroll
+        for (int y = 0; y < FQ; y++) acc[x][y] = f32x4{0.f, 0.f, 0.f, 0.f};
+    // NORMS == false: lane < NR of each wave chains the squared norm of LDS row wv * NR + lane (the
+    // same share per wave, so no wave reaches the chunk barrier late)
+    const int nrow = wv * NR + lane;
+    const bool nthread = !NORMS && lane < NR;
+    float nrm = 0.0f;
+
+    if (NORMS && tid < R) {
+        const float* nsrc = tid < TQ ? a.normsq + (size_t)qf * a.qstride + q0 + tid
+                                     : a.normst + (size_t)tf * a.tstride + t0 + tid - TQ;
+        const bool ok = tid < TQ ? q0 + tid < n1 : t0 + tid - TQ < n2;
+        s_norm[tid] = ok ? *nsrc : 0.0f;
+    }
+    load(0);
+    store(0);
     __syncthreads();
-    for (int c0 = 0; c0 < rows; c0 += 1024) {
-        const int i = c0 + threadIdx.x;
+#pragma unroll
+    for (int c = 0; c < NC; c++) {  // unrolled: no loop-carried copies of the prefetch registers
+        const int buf = NB > 1 ? (c & 1) : 0;
+        if (c + 1 < NC) load(c + 1);
+        // keep the transposing register moves of store() below the MFMAs: hoisted here they would
+        // wait for the loads just issued
+        __builtin_amdgcn_sched_barrier(0);
+        const float4* sb = sbuf[buf];
+#pragma unroll
+        for (int qd = 0; qd < KC / 16; qd++) {
+            float4 fa[FT], fb[FQ];
+#pragma unroll
+            for (int x = 0; x < FT; x++) fa[x] = sb[(trow0 + 16 * x + li) * RS4 + 4 * qd + lg];
+#pragma unroll
+            for (int y = 0; y < FQ; y++) fb[y] = sb[(qrow0 + 16 * y + li) * RS4 + 4 * qd + lg];
+#pragma unroll
+            for (int x = 0; x < FT; x++)
+#pragma unroll
+                for (int y = 0; y < FQ; y++) acc[x][y] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[x].x, fb[y].x, acc[x][y], 0, 0, 0);
+#pragma unroll
+            for (int x = 0; x < FT; x++)
+#pragma unroll
+                for (int y = 0; y < FQ; y++) acc[x][y] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[x].y, fb[y].y, acc[x][y], 0, 0, 0);
+#pragma unroll
+            for (int x = 0; x < FT; x++)
+#pragma unroll
+                for (int y = 0; y < FQ; y++) acc[x][y] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[x].z, fb[y].z, acc[x][y], 0, 0, 0);
+#pragma unroll
+            for (int x = 0; x < FT; x++)
+#pragma unroll
+                for (int y = 0; y < FQ; y++) acc[x][y] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[x].w, fb[y].w, acc[x][y], 0, 0, 0);
+            if (nthread) {
+                // k = 16 qd + m sits at float4 (m & 3), component (m >> 2)
+                float4 v[4];
+#pragma unroll
+                for (int g = 0; g < 4; g++) v[g] = sb[nrow * RS4 + 4 * qd + g];
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    nrm = fmaf(v[0][j], v[0][j], nrm);
+                    nrm = fmaf(v[1][j], v[1][j], nrm);
+                    nrm = fmaf(v[2][j], v[2][j], nrm);
+                    nrm = fmaf(v[3][j], v[3][j], nrm);
+                }
+            }
+        }
+        if (c + 1 < NC) {
+            __builtin_amdgcn_sched_barrier(0);
+            if (NB == 1) __syncthreads();
+            store(NB > 1 ? (buf ^ 1) : 0);
+        } else if (nthread) {
+            s_norm[nrow] = nrm;
+        }
+        __syncthreads();
+    }
+
+    // ---- per-wave top-2 per query: D[train 4 lg + e][query li] of each 16 x 16 fragment ----
+    unsigned long long mine0 = kNoKey, mine1 = kNoKey;  // the fragment this lane group publishes
+#pragma unroll
+    for (int y = 0; y < FQ; y++) {
+        const float na = s_norm[qrow0 + 16 * y + li];
+        unsigned long long k0 = kNoKey, k1 = kNoKey;
+#pragma unroll
+        for (int x = 0; x < FT; x++)
+#pragma unroll
+            for (int e = 0; e < 4; e++) {
+                const int tr = wt * WT + 16 * x + 4 * lg + e;  // train row within the block
+                const float s = na + s_norm[TQ + tr];
+                float d = s - 2.0f * acc[x][y][e];
+                d = d < 0.0f ? 0.0f : d;
+                const unsigned long long key = ((unsigned long long)__float_as_uint(d) << 32) | (unsigned)(t0 + tr);
+                push2(k0, k1, t0 + tr < n2 ? key : kNoKey);
+            }
+#pragma unroll
+        for (int m = 16; m <= 32; m <<= 1) {
+            const unsigned long long o0 = shfl_xor_u64(k0, m), o1 = shfl_xor_u64(k1, m);
+            const unsigned long long lo = k0 < o0 ? k0 : o0, hi = k0 < o0 ? o0 : k0;
+            const unsigned long long m1 = k1 < o1 ? k1 : o1;
+            k0 = lo;
+            k1 = hi < m1 ? hi : m1;
+        }
+        if (lg == y) {
+            mine0 = k0;
+            mine1 = k1;
+        }
+    }
+    const int qi = q0 + qrow0 + 16 * lg + li;
+    unsigned long long* B0 = a.keys + (size_t)p * 2 * a.kcap;
+    unsigned long long* B1 = B0 + a.kcap;
+    if (lg < FQ && qi < n1 && mine0 != kNoKey) {
+        if (mine1 != kNoKey) atomicMin(B1 + qi, mine1);
+        const unsigned long long old = atomicMin(B0 + qi, mine0);
+        atomicMin(B1 + qi, old > mine0 ? old : mine0);
+    }
+    // every atomic of this workgroup has been performed (acknowledged) before it arrives
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) s_last = atomicAdd(a.cnt + p, 1u) == (unsigned)(nq * nt - 1);
+    __syncthreads();
+    if (!s_last) return;
+
+    // ---- last arrival: ratio test + order-preserving compaction (Slam.cpp:1151-1157) ----
+    if (tid == 0) {
+        s_base = 0;
+        atomicExch(a.cnt + p, 0u);
+    }
+    __syncthreads();
+    vs_match* raw = a.raw + (size_t)p * a.ostride;
+    vs_match* good = a.good + (size_t)p * a.ostride;
+    for (int c0 = 0; c0 < n1; c0 += 256) {
+        const int i = c0 + tid;
         bool f = false;
         vs_match m;
-        if (i < rows) {
-            Best2 best;
-            best.init();
-            for (int z = 0; z < used; z++) {
-                const Part2 q = part[((size_t)p * nslices + z) * cap + i];
-                best.push(q.d0, q.j0);
-                best.push(q.d1, q.j1);
-            }
-            const float dist0 = sqrt_rn(best.d0), dist1 = sqrt_rn(best.d1);
+        if (i < n1) {
+            const unsigned long long k0 = atomicExch(B0 + i, kNoKey), k1 = atomicExch(B1 + i, kNoKey);
+            const float dist0 = sqrt_rn(__uint_as_float((unsigned)(k0 >> 32)));
+            const float dist1 = sqrt_rn(__uint_as_float((unsigned)(k1 >> 32)));
             m.query_idx = i;
-            m.train_idx = best.j0;
+            m.train_idx = (int)(unsigned)k0;
             m.img_idx = 0;
             m.distance = dist0;
-            raw[(size_t)p * cap + i] = m;
-            f = dist0 < ratio * dist1;
+            raw[i] = m;
+            f = dist0 < a.ratio * dist1;
         }
         const unsigned long long bal = __ballot(f);
         const int before = __popcll(bal & ((1ull << lane) - 1ull));
@@ -195,41 +316,15 @@ __global__ __launch_bounds__(1024) void k_match_compact(const int* __restrict__ 
         __syncthreads();
         int off = s_base;
         for (int k = 0; k < wv; k++) off += s_wave[k];
-        if (f) good[(size_t)p * cap + off + before] = m;
+        if (f) good[off + before] = m;
         __syncthreads();
-        if (threadIdx.x == 0) {
-            int tot = 0;
-            for (int k = 0; k < 16; k++) tot += s_wave[k];
-            s_base += tot;
-        }
+        if (tid == 0) s_base += s_wave[0] + s_wave[1] + s_wave[2] + s_wave[3];
         __syncthreads();
     }
-    if (threadIdx.x == 0) {
-        nraw[p] = rows;
-        ngood[p] = s_base;
+    if (tid == 0) {
+        a.nraw[p] = n1;
+        a.ngood[p] = s_base;
     }
-}
-
-// Norms of only the frames the P pairs reference (a pair out of a large frame pool): row r of
-// the 2P*cap grid is row r % cap of frame pairs[r / cap]; a frame named twice is written twice
-// with the same value.
-__global__ __launch_bounds__(256) void k_desc_norms_sel(const float* __restrict__ desc, const int* __restrict__ n,
-                                                        const int* __restrict__ pairs, int P, int cap,
-                                                        float* __restrict__ norms) {
-    long r = (long)blockIdx.x * 256 + threadIdx.x;
-    if (r >= (long)2 * P * cap) return;
-    const int f = pairs[r / cap], i = (int)(r % cap);
-    if (i >= n[f]) return;
-    const float4* p = reinterpret_cast<const float4*>(desc + ((size_t)f * cap + i) * 256);
-    float s = 0.0f;
-    for (int k4 = 0; k4 < 64; k4++) {
-        float4 v = p[k4];
-        s = fmaf(v.x, v.x, s);
-        s = fmaf(v.y, v.y, s);
-        s = fmaf(v.z, v.z, s);
-        s = fmaf(v.w, v.w, s);
-    }
-    norms[(size_t)f * cap + i] = s;
 }
 
 __global__ void k_set_meta(int* meta, int n1, int n2) {
@@ -248,31 +343,65 @@ int desc_norms(vs_ctx* ctx, int F, const float* d_desc, const int* d_n, int cap,
     return VS_OK;
 }
 
+// Keys ([P][2][kcap], all ones) and arrival counters ([P], zero) that every k_match launch leaves
+// reset; (re)initialised only when a buffer grows.
+static int match_state(vs_ctx* ctx, int P, int kcap, unsigned long long** keys, unsigned** cnt, hipStream_t s) {
+    void* kp = ctx->match_keys.p;
+    VS_CHECK(ctx->match_keys.ensure((size_t)P * 2 * kcap * sizeof(unsigned long long)));
+    if (ctx->match_keys.p != kp) VS_HIP(hipMemsetAsync(ctx->match_keys.p, 0xFF, ctx->match_keys.bytes, s));
+    void* cp = ctx->match_cnt.p;
+    VS_CHECK(ctx->match_cnt.ensure((size_t)P * sizeof(unsigned)));
+    if (ctx->match_cnt.p != cp) VS_HIP(hipMemsetAsync(ctx->match_cnt.p, 0, ctx->match_cnt.bytes, s));
+    *keys = ctx->match_keys.as<unsigned long long>();
+    *cnt = ctx->match_cnt.as<unsigned>();
+    return VS_OK;
+}
+
+template <int WQ, int WT, int KC>
+static void launch_tile(MatchArgs& a, int P, int cap_q, int cap_t, bool norms, hipStream_t s) {
+    a.qblocks = (cap_q + 2 * WQ - 1) / (2 * WQ);
+    a.tblocks = (cap_t + 2 * WT - 1) / (2 * WT);
+    a.work = P * a.qblocks * a.tblocks;
+    a.per_xcd = (a.work + 7) / 8;
+    const unsigned blocks = (unsigned)(8 * a.per_xcd);
+    if (norms)
+        hipLaunchKernelGGL((k_match<WQ, WT, KC, true>), dim3(blocks), dim3(256), 0, s, a);
+    else
+        hipLaunchKernelGGL((k_match<WQ, WT, KC, false>), dim3(blocks), dim3(256), 0, s, a);
+}
+
+// Tile choice: 64 x 64 workgroups (4 chains per wave, k staged in 64-wide chunks, two buffers)
+// when the problem fills the chip several times, else 32 x 32 workgroups (one 16 x 16 chain per
+// wave, all of k loaded at once: one memory round trip before the MFMAs) for latency.
+static void launch(MatchArgs& a, int P, int cap_q, int cap_t, bool norms, hipStream_t s) {
+    const long tiles32 = (long)P * ((cap_q + 31) / 32) * ((cap_t + 31) / 32);
+    if (tiles32 > 2048)
+        launch_tile<32, 32, 64>(a, P, cap_q, cap_t, norms, s);
+    else
+        launch_tile<16, 16, 256>(a, P, cap_q, cap_t, norms, s);
+}
+
 int match_pairs(vs_ctx* ctx, int P, const int* d_pairs, int F, const float* d_desc, const int* d_n, int cap,
                 float ratio, vs_match* d_raw, int* d_nraw, vs_match* d_good, int* d_ngood, hipStream_t s,
                 const float* d_norms) {
+    (void)F;
     if (P <= 0) return VS_OK;
-    const int nslices = (cap + kTrainChunk - 1) / kTrainChunk;
-    const size_t norm_bytes = ((size_t)F * cap * sizeof(float) + 255) & ~(size_t)255;
-    VS_CHECK(ctx->norms.ensure(norm_bytes + (size_t)P * nslices * cap * sizeof(Part2)));
-    float* norms = ctx->norms.as<float>();
-    Part2* part = reinterpret_cast<Part2*>(ctx->norms.as<uint8_t>() + norm_bytes);
+    MatchArgs a{};
+    VS_CHECK(match_state(ctx, P, cap, &a.keys, &a.cnt, s));
     ProfScope ps(ctx, "match", s);
-    if (d_norms) {  // the caller keeps the frames' row norms
-        norms = const_cast<float*>(d_norms);
-    } else if (2 * P < F) {  // a few pairs out of a frame pool: only the referenced frames' norms
-        long rows = (long)2 * P * cap;
-        hipLaunchKernelGGL(k_desc_norms_sel, dim3((unsigned)((rows + 255) / 256)), dim3(256), 0, s, d_desc, d_n,
-                           d_pairs, P, cap, norms);
-    } else {
-        long rows = (long)F * cap;
-        hipLaunchKernelGGL(k_desc_norms, dim3((unsigned)((rows + 255) / 256)), dim3(256), 0, s, d_desc, d_n, F, cap,
-                           norms);
-    }
-    hipLaunchKernelGGL(k_match, dim3(P, (cap + 127) / 128, nslices), dim3(256), 0, s, d_pairs, d_desc, d_desc, norms,
-                       norms, d_n, cap, cap, cap, nslices, part);
-    hipLaunchKernelGGL(k_match_compact, dim3(P), dim3(1024), 0, s, d_pairs, d_n, cap, nslices, ratio, part, d_raw,
-                       d_nraw, d_good, d_ngood);
+    a.pairs = d_pairs;
+    a.descq = a.desct = d_desc;
+    a.normsq = a.normst = d_norms;
+    a.n = d_n;
+    a.qstride = a.tstride = cap;
+    a.ratio = ratio;
+    a.kcap = cap;
+    a.raw = d_raw;
+    a.nraw = d_nraw;
+    a.good = d_good;
+    a.ngood = d_ngood;
+    a.ostride = cap;
+    launch(a, P, cap, cap, d_norms != nullptr, s);
     VS_HIP(hipGetLastError());
     return VS_OK;
 }
@@ -283,25 +412,27 @@ int match_pairs(vs_ctx* ctx, int P, const int* d_pairs, int F, const float* d_de
 int match_sets(vs_ctx* ctx, const float* d_q, int n1, const float* d_t, int n2, float ratio, vs_match* d_raw,
                vs_match* d_good, int* d_counts, hipStream_t s) {
     if (n1 <= 0) return VS_OK;
-    const int nslices = (n2 + kTrainChunk - 1) / kTrainChunk;
-    const size_t head = (((size_t)n1 + n2) * sizeof(float) + 4 * sizeof(int) + 255) & ~(size_t)255;
-    VS_CHECK(ctx->norms_sets.ensure(head + (size_t)(nslices > 0 ? nslices : 1) * n1 * sizeof(Part2)));
-    float* nq = ctx->norms_sets.as<float>();
-    float* nt = nq + n1;
-    int* meta = reinterpret_cast<int*>(nt + n2);
-    Part2* part = reinterpret_cast<Part2*>(ctx->norms_sets.as<uint8_t>() + head);
+    VS_CHECK(ctx->norms_sets.ensure(256));
+    int* meta = ctx->norms_sets.as<int>();
+    MatchArgs a{};
+    VS_CHECK(match_state(ctx, 1, n1, &a.keys, &a.cnt, s));
     ProfScope ps(ctx, "match_map", s);
     hipLaunchKernelGGL(k_set_meta, dim3(1), dim3(1), 0, s, meta, n1, n2);
-    // norms: query rows as "frame 0" of stride n1, train rows as "frame 1" read with stride 0
-    hipLaunchKernelGGL(k_desc_norms, dim3((unsigned)((n1 + 255) / 256)), dim3(256), 0, s, d_q, meta + 2, 1, n1, nq);
-    if (n2 > 0)
-        hipLaunchKernelGGL(k_desc_norms, dim3((unsigned)((n2 + 255) / 256)), dim3(256), 0, s, d_t, meta + 3, 1, n2,
-                           nt);
-    if (nslices > 0)
-        hipLaunchKernelGGL(k_match, dim3(1, (n1 + 127) / 128, nslices), dim3(256), 0, s, meta, d_q, d_t, nq, nt,
-                           meta + 2, n1, 0, n1, nslices, part);
-    hipLaunchKernelGGL(k_match_compact, dim3(1), dim3(1024), 0, s, meta, meta + 2, n1, nslices, ratio, part, d_raw,
-                       d_counts, d_good, d_counts + 1);
+    // query rows as "frame 0" of stride n1, train rows as "frame 1" read with stride 0
+    a.pairs = meta;
+    a.descq = d_q;
+    a.desct = d_t;
+    a.n = meta + 2;
+    a.qstride = n1;
+    a.tstride = 0;
+    a.ratio = ratio;
+    a.kcap = n1;
+    a.raw = d_raw;
+    a.nraw = d_counts;
+    a.good = d_good;
+    a.ngood = d_counts + 1;
+    a.ostride = n1;
+    launch(a, 1, n1, n2 > 0 ? n2 : 1, false, s);
     VS_HIP(hipGetLastError());
     return VS_OK;
 }

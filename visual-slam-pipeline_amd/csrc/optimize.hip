@@ -14,6 +14,7 @@
 #include <cfloat>
 
 #include "block_reduce.h"
+#include "cr_math.h"
 #include "vs_internal.h"
 
 namespace vs {
@@ -24,7 +25,7 @@ __device__ void rodrigues_v2m(const double r[3], double R[9]) {
         for (int i = 0; i < 9; i++) R[i] = (i % 4 == 0) ? 1.0 : 0.0;
         return;
     }
-    const double c = cos(theta), s = sin(theta), c1 = 1.0 - c;
+    const double c = vs_cr::cos(theta), s = vs_cr::sin(theta), c1 = 1.0 - c;
     const double itheta = theta ? 1.0 / theta : 0.0;
     const double rx = r[0] * itheta, ry = r[1] * itheta, rz = r[2] * itheta;
     const double rrt[9] = {rx * rx, rx * ry, rx * rz, rx * ry, ry * ry, ry * rz, rx * rz, ry * rz, rz * rz};
@@ -37,7 +38,7 @@ __device__ void rodrigues_m2v(const double R[9], double r[3]) {
     const double s = sqrt((rx * rx + ry * ry + rz * rz) * 0.25);
     double c = (R[0] + R[4] + R[8] - 1) * 0.5;
     c = c > 1. ? 1. : c < -1. ? -1. : c;
-    double theta = acos(c);
+    double theta = vs_cr::acos(c);
     if (s < 1e-5) {
         if (c > 0) {
             r[0] = r[1] = r[2] = 0;

@@ -21,6 +21,8 @@
 #include <math.h>
 #include <stdint.h>
 
+#include "cr_math.h"  // correctly rounded sin / cos / acos / log / pow (host == device)
+
 #if defined(__HIPCC__)
 #define VS_HD __host__ __device__
 #define VS_UNROLL _Pragma("unroll")
@@ -93,10 +95,10 @@ VS_HD inline int ransac_update_num_iters(double p, double ep, int model_points, 
     ep = ep > 0. ? ep : 0.;
     ep = ep < 1. ? ep : 1.;
     double num = (1. - p) > DBL_MIN ? (1. - p) : DBL_MIN;
-    double denom = 1. - pow(1. - ep, model_points);
+    double denom = 1. - vs_cr::pow(1. - ep, model_points);
     if (denom < DBL_MIN) return 0;
-    num = log(num);
-    denom = log(denom);
+    num = vs_cr::log(num);
+    denom = vs_cr::log(denom);
     if (denom >= 0 || -num >= max_iters * (-denom)) return max_iters;
     return (int)lrint(num / denom);  // cvRound
 }
@@ -327,7 +329,7 @@ VS_HD inline void rod_v2m(const double r[3], double R[9]) {
         for (int i = 0; i < 9; i++) R[i] = (i % 4 == 0) ? 1.0 : 0.0;
         return;
     }
-    const double c = cos(theta), s = sin(theta), c1 = 1.0 - c;
+    const double c = vs_cr::cos(theta), s = vs_cr::sin(theta), c1 = 1.0 - c;
     const double it = 1.0 / theta;
     const double x = r[0] * it, y = r[1] * it, z = r[2] * it;
     const double rrt[9] = {x * x, x * y, x * z, x * y, y * y, y * z, x * z, y * z, z * z};
@@ -340,7 +342,7 @@ VS_HD inline void rod_m2v(const double R[9], double r[3]) {
     const double s = sqrt((rx * rx + ry * ry + rz * rz) * 0.25);
     double c = (R[0] + R[4] + R[8] - 1) * 0.5;
     c = c > 1. ? 1. : c < -1. ? -1. : c;
-    double theta = acos(c);
+    double theta = vs_cr::acos(c);
     if (s < 1e-5) {
         if (c > 0) {
             r[0] = r[1] = r[2] = 0;

@@ -795,6 +795,7 @@ struct vs_slam {
     vs::GpuOps ops;
     std::unique_ptr<vs_trk::Tracker<vs::GpuOps>> trk;
     std::vector<vs_trk::FramePtr> batch;  // frames of the batch being processed
+    FILE* trace = nullptr;                // VS_TRACE_GPU=path: stage trace (debugging aid)
 };
 
 using namespace vs;
@@ -869,6 +870,8 @@ int vs_slam_create(vs_ctx* ctx, int max_batch, int h, int w, vs_slam** out) {
         return rc;
     }
     sl->trk = std::make_unique<vs_trk::Tracker<GpuOps>>(sl->ops);
+    if (const char* p = std::getenv("VS_TRACE_GPU")) sl->trace = std::fopen(p, "w");
+    sl->trk->set_trace(sl->trace);
     *out = sl;
     return VS_OK;
 }
@@ -886,6 +889,7 @@ void vs_slam_destroy(vs_slam* sl) {
                       &o.chain_buf,    &o.work, &o.rows_buf,      &o.map_pos, &o.map_desc,  &o.map_valid, &o.map_tmp,
                       &o.pnp_io,       &o.hdr_buf};
     for (DevBuf* b : bufs) b->release();
+    if (sl->trace) std::fclose(sl->trace);
     delete sl;
 }
 

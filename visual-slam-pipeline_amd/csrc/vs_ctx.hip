@@ -13,6 +13,7 @@
 #include <string>
 #include <vector>
 
+#include "cr_math.h"
 #include "vs_internal.h"
 
 namespace vs {
@@ -181,6 +182,25 @@ static int upload(DevBuf& buf, const T* src, size_t count, hipStream_t s) {
 
 using namespace vs;
 
+namespace vs {
+// test support: the device's correctly rounded functions (cr_math.h) on an array
+__global__ void k_crmath(int op, int n, const double* __restrict__ a, const double* __restrict__ b,
+                         double* __restrict__ out) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const double x = a[i];
+    double r;
+    switch (op) {
+        case 0: r = vs_cr::sin(x); break;
+        case 1: r = vs_cr::cos(x); break;
+        case 2: r = vs_cr::acos(x); break;
+        case 3: r = vs_cr::log(x); break;
+        default: r = vs_cr::pow(x, b[i]); break;
+    }
+    out[i] = r;
+}
+}  // namespace vs
+
 extern "C" {
 
 int vs_abi_version(void) { return VS_ABI_VERSION; }
@@ -252,7 +272,7 @@ void vs_destroy(vs_ctx* ctx) {
     DevBuf* bufs[] = {&ctx->gray,  &ctx->act0,   &ctx->act1,   &ctx->semi,   &ctx->dgrid,  &ctx->heat,
                       &ctx->state, &ctx->flags,  &ctx->keys,   &ctx->keycnt, &ctx->h_img,  &ctx->h_kps,
                       &ctx->h_desc, &ctx->h_n,   &ctx->h_aux0, &ctx->h_aux1, &ctx->h_aux2, &ctx->h_aux3,
-                      &ctx->h_aux4, &ctx->h_aux5, &ctx->norms, &ctx->norms_sets, &ctx->tlm, &ctx->ba, &ctx->pnp};
+                      &ctx->h_aux4, &ctx->h_aux5, &ctx->match_keys, &ctx->match_cnt, &ctx->norms_sets, &ctx->tlm, &ctx->ba, &ctx->pnp};
     for (DevBuf* b : bufs) b->release();
     for (auto& st : ctx->prof)
         for (auto& pr : st.pending) {
@@ -821,6 +841,23 @@ int vs_profile_read(vs_ctx* ctx, int max_stages, const char** names, double* ms,
         if (ms) ms[i] = ctx->prof[i].ms;
         if (launches) launches[i] = ctx->prof[i].launches;
     }
+    return VS_OK;
+}
+
+int vs_selftest_crmath(vs_ctx* ctx, int op, int n, const double* a, const double* b, double* out) {
+    VS_ARG(ctx && a && out && n >= 0 && op >= 0 && op <= 4 && (op < 4 || b), "vs_selftest_crmath: bad argument");
+    if (n == 0) return VS_OK;
+    VS_HIP(hipSetDevice(ctx->device));
+    hipStream_t s = ctx->stream;
+    const size_t bytes = (size_t)n * sizeof(double);
+    VS_CHECK(ctx->h_aux0.ensure(3 * bytes));
+    double* d = ctx->h_aux0.as<double>();
+    VS_HIP(hipMemcpyAsync(d, a, bytes, hipMemcpyHostToDevice, s));
+    if (b) VS_HIP(hipMemcpyAsync(d + n, b, bytes, hipMemcpyHostToDevice, s));
+    hipLaunchKernelGGL(k_crmath, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, op, n, d, b ? d + n : d, d + 2 * (size_t)n);
+    VS_HIP(hipGetLastError());
+    VS_HIP(hipMemcpyAsync(out, d + 2 * (size_t)n, bytes, hipMemcpyDeviceToHost, s));
+    VS_HIP(hipStreamSynchronize(s));
     return VS_OK;
 }
 

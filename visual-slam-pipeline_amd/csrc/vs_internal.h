@@ -92,7 +92,7 @@ struct vs_ctx {
     vs::DevBuf gray, act0, act1, semi, dgrid, heat, state, flags, keys, keycnt;
     // host-API staging
     vs::DevBuf h_img, h_kps, h_desc, h_n, h_aux0, h_aux1, h_aux2, h_aux3, h_aux4, h_aux5;
-    vs::DevBuf norms, norms_sets, tlm, ba, pnp;
+    vs::DevBuf match_keys, match_cnt, norms_sets, tlm, ba, pnp;
 
     bool prof_on = false;
     std::vector<vs::ProfStage> prof;

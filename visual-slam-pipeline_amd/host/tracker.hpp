@@ -26,6 +26,7 @@
 #include <array>
 #include <cmath>
 #include <cstdint>
+#include <cstdio>
 #include <cstring>
 #include <memory>
 #include <utility>
@@ -183,6 +184,9 @@ class Tracker {
         t_world_ = t;
     }
     void set_accelerometer_data(std::vector<AccelSample> d) { accel_ = std::move(d); }  // :1580-1582
+    // Debugging aid: one line per stage result (hex floats) so that two back ends' runs can be
+    // diffed to the first differing stage (tools/debug_tracker_divergence.py --trace).
+    void set_trace(FILE* f) { trace_ = f; }
 
     // Slam::compute_gravity_direction (Slam.cpp:1587-1616)
     void compute_gravity_direction() {
@@ -236,6 +240,7 @@ class Tracker {
         ChainResult C = ops_.chain(*ref_frame_, *frame, 42u + (uint32_t)frame_count_);
         stats_.f_iters += C.f_iters;
         last_match_count_ = (int)C.good.size();
+        trace_chain(frame->id, C);
 
         // :847-872 bridge keyframe when keyframe matching is weak
         if (last_match_count_ < cfg::MIN_MATCHES && last_frame_ && last_frame_ != ref_frame_) {
@@ -316,6 +321,7 @@ class Tracker {
             stats_.chains_discarded++;
             C = ops_.motion_points(*ref_frame_, *frame, p1, p2, 42u + (uint32_t)frame_count_);
         }
+        if (recompute_motion) trace_chain(frame->id, C);
         const bool use_3d3d = C.ok3d;
         const M3 R_ref = ref_frame_->R;
         const V3 t_ref = ref_frame_->t;
@@ -385,10 +391,15 @@ class Tracker {
         frame->R = R_world_;
         frame->t = t_world_;
         map_.frames.push_back(frame);
+        trace_pose(frame->id, "motion+ekf", R_world_, t_world_);
 
         // :1057-1059 local map tracking + PnP refinement
         const int tracked = track_local_map(frame);
+        if (trace_)
+            std::fprintf(trace_, "%d tlm %d %016llx\n", frame->id, tracked,
+                         (unsigned long long)fnv(frame->mp_idx.data(), frame->mp_idx.size() * sizeof(int)));
         refine_pose_via_local_pnp(frame, tracked);
+        trace_pose(frame->id, "refined", R_world_, t_world_);
 
         // :1061-1070 proactive keyframe.  Deviation: the reference dereferences last_keyframe_
         // unconditionally here, which is null when the first frame was rejected (:820-823 keeps it
@@ -484,6 +495,28 @@ class Tracker {
     bool last_pnp() const { return last_pnp_; }
 
    private:
+    FILE* trace_ = nullptr;
+    static uint64_t fnv(const void* p, size_t n) {
+        uint64_t h = 1469598103934665603ull;
+        for (size_t i = 0; i < n; i++) h = (h ^ static_cast<const uint8_t*>(p)[i]) * 1099511628211ull;
+        return h;
+    }
+    void trace_pose(int id, const char* tag, const M3& R, const V3& t) const {
+        if (!trace_) return;
+        if (id >= 0) std::fprintf(trace_, "%d %s", id, tag);
+        for (double v : R) std::fprintf(trace_, " %a", v);
+        for (double v : t) std::fprintf(trace_, " %a", v);
+        std::fprintf(trace_, "\n");
+    }
+    void trace_chain(int id, const ChainResult& C) const {
+        if (!trace_) return;
+        std::fprintf(trace_, "%d chain raw=%d good=%d/%016llx fok=%d fit=%d kept=%d epi=%a/%a ok3d=%d okE=%d sc=%a\n", id,
+                     C.n_raw, (int)C.good.size(), (unsigned long long)fnv(C.good.data(), C.good.size() * sizeof(Match)),
+                     (int)C.f_ok, C.f_iters, (int)C.kept.size(), C.epi_before, C.epi_after, (int)C.ok3d, (int)C.okE,
+                     C.scale);
+        if (C.ok3d) trace_pose(id, "r3d", C.R3, C.t3);
+        if (C.okE) trace_pose(id, "rE", C.RE, C.tE);
+    }
     struct Snapshot {
         double x_pred[6], P_pred[36], x_filt[6], P_filt[36];
         double dt;
@@ -611,7 +644,14 @@ class Tracker {
     PnPResult solve_pnp(const std::vector<float>& obj, const std::vector<float>& img, int iters, int min_inliers) {
         PnPResult r;
         if ((int)(obj.size() / 3) < min_inliers) return r;  // :512
-        return ops_.solve_pnp(obj, img, iters, min_inliers);
+        r = ops_.solve_pnp(obj, img, iters, min_inliers);
+        if (trace_) {
+            std::fprintf(trace_, "pnp n=%d in=%016llx/%016llx ok=%d inl=%d", (int)(obj.size() / 3),
+                         (unsigned long long)fnv(obj.data(), obj.size() * 4), (unsigned long long)fnv(img.data(), img.size() * 4),
+                         (int)r.success, r.inlier_count);
+            trace_pose(-1, "", r.R_world, r.t_world);
+        }
+        return r;
     }
 
     // Slam::run_pnp (:1477-1522)

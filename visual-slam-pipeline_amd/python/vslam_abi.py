@@ -31,6 +31,7 @@ _P = ctypes.c_void_p
 _I = ctypes.c_int
 _SIG = {
     "vs_abi_version": (_I, []),
+    "vs_selftest_crmath": (_I, [_P, _I, _I, _P, _P, _P]),
     "vs_last_error": (ctypes.c_char_p, []),
     "vs_create": (_I, [_I, ctypes.c_char_p, ctypes.POINTER(_P)]),
     "vs_destroy": (None, [_P]),
@@ -151,6 +152,17 @@ class Context:
     @property
     def stream(self):
         return self.lib.vs_stream(self.h)
+
+    # ---- test support ----
+    def crmath(self, op, a, b=None):
+        """The device's correctly rounded fp64 functions (cr_math.h) on host arrays."""
+        ops = {"sin": 0, "cos": 1, "acos": 2, "log": 3, "pow": 4}
+        a = np.ascontiguousarray(a, np.float64)
+        bb = None if b is None else np.ascontiguousarray(b, np.float64)
+        out = np.zeros_like(a)
+        _check(self.lib.vs_selftest_crmath(self.h, ops[op], a.size, _ptr(a), None if bb is None else _ptr(bb),
+                                           _ptr(out)))
+        return out
 
     # ---- weights ----
     def weights(self):
