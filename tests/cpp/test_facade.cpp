@@ -1,11 +1,12 @@
 // test_facade.cpp — exercises the C++ façade the way the reference's Slam uses FeatureExtractor,
-// match_features, the F verification, estimate_motion_3d3d, solve_pnp, track_local_map and
-// Optimizer::optimize_pose.  Built by `make -C visual-slam-pipeline_amd facade_test`, run on the
+// Frame, match_features, the F verification, estimate_motion_3d3d, solve_pnp, track_local_map,
+// Map / MapPoint and Optimizer (project_point, optimize_pose, local_bundle_adjustment).  Built by `make -C visual-slam-pipeline_amd facade_test`, run on the
 // GPU by tests/test_gpu_facade.py.  Prints "FACADE OK" and exits 0 on success.
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <memory>
 #include <string>
 #include <vector>
 
@@ -170,8 +171,88 @@ int main() {
     const int tracked = track_local_map(ctx, map, k1, d1, I3, t1, kp_to_mp, &obs);
     EXPECT(tracked > 20 && (int)obs.size() == tracked && kp_to_mp.size() == k1.size());
 
+    // ---- Frame::detect_features (Frame.cpp:33-38) + depth (Frame.cpp:47-54) ----
+    FeatureExtractor fe2;
+    EXPECT(fe2.init(""));
+    auto f0 = std::make_shared<Frame>(0, a, 1311868164.0), f1 = std::make_shared<Frame>(3, b, 1311868164.1);
+    f0->detect_features(fe2);
+    f1->detect_features(fe2);
+    EXPECT(f0->is_processed() && f0->keypoints().size() == k0.size());
+    EXPECT(std::memcmp(f0->keypoints().data(), k0.data(), k0.size() * sizeof(KeyPoint)) == 0);
+    EXPECT(f0->descriptors().data == d0.data && f1->descriptors().data == d1.data);
+    EXPECT(f0->map_point_indices().size() == k0.size() && f0->map_point_indices()[0] == -1);
+    Frame empty(7, Image{}, 0.0);
+    empty.detect_features(fe2);  // no image: untouched, like a failed imread
+    EXPECT(!empty.is_processed() && empty.keypoints().empty());
+    std::vector<uint16_t> raw_depth((size_t)W * H, 10000);  // 2 m in TUM units (x 5000)
+    raw_depth[5] = 0;
+    f0->load_depth_image(raw_depth.data(), H, W);
+    EXPECT(f0->has_real_depth() && f0->depth_map().data[0] == 2.0f && f0->depth_map().data[5] == 0.0f);
+
+    // ---- Optimizer::project_point (Optimizer.cpp:26-48) ----
+    const Point2d pp = Optimizer::project_point({0.1, -0.2, 2.0}, I3, {0.0, 0.0, 0.0}, ctx.K());
+    EXPECT(std::fabs(pp.x - (525.0 * 0.05 + 319.5)) < 1e-12 && std::fabs(pp.y - (-525.0 * 0.1 + 239.5)) < 1e-12);
+    EXPECT(Optimizer::project_point({0.0, 0.0, -1.0}, I3, {0.0, 0.0, 0.0}, ctx.K()).x == -1.0);
+
+    // ---- Map + Optimizer::local_bundle_adjustment (Optimizer.cpp:187-599) over the two views:
+    // frame-0 keypoints as map points on the z = 2 plane (perturbed), observed by both keyframes ----
+    Map m;
+    f0->set_keyframe(true);
+    f1->set_keyframe(true);
+    f0->set_pose(I3, {0.0, 0.0, 0.0});
+    f1->set_pose(I3, t1);
+    m.add_frame(f0);
+    m.add_frame(f1);
+    for (size_t i = 0; i < k0.size(); i++) {
+        const double dz = 0.01 * (double)((i * 13) % 7 - 3);
+        MapPoint mp((int)i, {pos[3 * i] * (1 + dz / 2), pos[3 * i + 1] * (1 + dz / 2), pos[3 * i + 2] + dz}, d0.row((int)i));
+        m.add_map_point(mp);
+        f0->map_point_indices()[i] = (int)i;
+    }
+    f1->map_point_indices() = kp_to_mp;  // the local-map tracking result
+    std::vector<Point3d> before_pts;
+    for (const auto& mp : m.map_points()) before_pts.push_back(mp.position());
+    // the same window through the C ABI directly: the façade must gather it exactly like this
+    std::vector<double> Rw = {1, 0, 0, 0, 1, 0, 0, 0, 1, 1, 0, 0, 0, 1, 0, 0, 0, 1}, tw2 = {0, 0, 0, t1[0], t1[1], t1[2]};
+    std::vector<double> P;
+    std::vector<int> okf, opt_pt, seen(k0.size(), -1);
+    std::vector<double> ouv;
+    int nloc = 0;
+    for (int ki = 0; ki < 2; ki++) {
+        const Frame& f = ki ? *f1 : *f0;
+        for (size_t kp = 0; kp < f.map_point_indices().size(); kp++) {
+            const int id = f.map_point_indices()[kp];
+            if (id < 0) continue;
+            if (seen[id] < 0) {
+                seen[id] = nloc++;
+                P.insert(P.end(), {before_pts[id].x, before_pts[id].y, before_pts[id].z});
+            }
+            okf.push_back(ki);
+            opt_pt.push_back(seen[id]);
+            ouv.insert(ouv.end(), {(double)f.keypoints()[kp].pt.x, (double)f.keypoints()[kp].pt.y});
+        }
+    }
+    const double Kv[4] = {525.0, 525.0, 319.5, 239.5};
+    double eb = 0, ea = 0;
+    EXPECT(vs_local_ba(ctx.get(), 2, Rw.data(), tw2.data(), nloc, P.data(), (int)okf.size(), okf.data(), opt_pt.data(),
+                       ouv.data(), Kv, 15, &eb, &ea, nullptr) == VS_OK);
+    Optimizer opt2(*fe2.context());
+    const auto ba = opt2.local_bundle_adjustment(m, 10);
+    EXPECT(ba.first == eb && ba.second == ea && ba.second < ba.first);
+    for (size_t i = 0; i < k0.size(); i++) {  // points written back in place (:590-595)
+        const Point3d q = m.map_points()[i].position();
+        const int l = seen[i];
+        EXPECT(l >= 0 && q.x == P[3 * l] && q.y == P[3 * l + 1] && q.z == P[3 * l + 2]);
+    }
+    EXPECT(f0->get_translation()[0] == 0.0 && f0->get_rotation()[0] == 1.0);  // keyframe 0 fixed
+    EXPECT(f1->get_translation()[0] == tw2[3] && f1->get_translation()[2] == tw2[5]);  // pose 1 written back
+    m.map_points()[0].set_valid(false);
+    Map tiny;
+    tiny.add_frame(f0);
+    EXPECT(opt2.local_bundle_adjustment(tiny, 10) == std::make_pair(0.0, 0.0));  // < 2 keyframes (:222)
+
     std::remove(cache.c_str());
-    std::printf("FACADE OK keypoints=%zu good=%zu F-kept=%zu pnp_inliers=%d tracked=%d rms=%.4f->%.4f\n",
-                k0.size(), n_good, good.size(), pnp.inlier_count, tracked, rms.first, rms.second);
+    std::printf("FACADE OK keypoints=%zu good=%zu F-kept=%zu pnp_inliers=%d tracked=%d rms=%.4f->%.4f ba=%.4f->%.4f\n",
+                k0.size(), n_good, good.size(), pnp.inlier_count, tracked, rms.first, rms.second, ba.first, ba.second);
     return 0;
 }

@@ -1,6 +1,8 @@
 """Runs the C++ façade program (tests/cpp/test_facade.cpp) on the GPU: FeatureExtractor with the
-SPCF cache, match_features, F verification, estimate_motion_3d3d, solve_pnp, Optimizer::
-optimize_pose and track_local_map through libvslam_hip.so, called the way the reference calls them."""
+SPCF cache, Frame::detect_features / load_depth_image, match_features, F verification,
+estimate_motion_3d3d, solve_pnp, track_local_map, Map / MapPoint and Optimizer::project_point /
+optimize_pose / local_bundle_adjustment (window gather + write-back, checked against vs_local_ba on
+the same window) through libvslam_hip.so, called the way the reference calls them."""
 import os
 import subprocess
 

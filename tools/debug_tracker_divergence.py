@@ -106,3 +106,7 @@ def diff_traces(pg, po):
 if __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "--diff":
     diff_traces(sys.argv[2], sys.argv[3])
     sys.exit(0)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,7 +1,13 @@
-set -o pipefail
 export PYTHONUNBUFFERED=1
 export TMPDIR=/tmp
-timeout -k 10 120 python -u -m pytest -x -q --timeout 100 --timeout-method thread tests/test_gpu_crmath.py > gpurun_out/t6a.log 2>&1 && \
-timeout -k 10 120 python -u tools/bench_match.py --pairs 1,8,32,128,512 > gpurun_out/bm6.log 2>&1 && \
-timeout -k 10 400 python -u tools/debug_tracker_divergence.py --loop 416 --batch 32 --tol 0 --after 2 --trace gpurun_out/tr6 > gpurun_out/div6.log 2>&1 ; \
-timeout -k 10 700 python -u -m pytest -q --timeout 300 --timeout-method thread -m gpu tests/ > gpurun_out/t6.log 2>&1
+timeout -k 10 400 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_tracker.py tests/test_gpu_tracker_bench.py tests/test_gpu_parity.py -k "match or tracker" > gpurun_out/t9.log 2>&1
+echo "tests exit $?" >> gpurun_out/t9.log
+for v in default large2 small; do
+  if [ $v = default ]; then unset VS_MATCH_TILE; else export VS_MATCH_TILE=$v; fi
+  echo "== $v" >> gpurun_out/bm9.log
+  timeout -k 10 120 python -u tools/bench_match.py --pairs 1,8,32,128,512 >> gpurun_out/bm9.log 2>&1 || break
+done
+unset VS_MATCH_TILE
+timeout -k 10 200 python -u bench.py --steps 10 --warmup 3 --no-cpu-baseline --frontend-steps 0 --mono-steps 0 > gpurun_out/bench9a.log 2>&1
+VS_MATCH_TILE=large timeout -k 10 200 python -u bench.py --steps 10 --warmup 3 --no-cpu-baseline --frontend-steps 0 --mono-steps 0 > gpurun_out/bench9b.log 2>&1
+echo done

@@ -35,6 +35,8 @@
 #include <hip/hip_runtime.h>
 
 #include <climits>
+#include <cstdlib>
+#include <cstring>
 
 #include "vs_internal.h"
 
@@ -96,12 +98,12 @@ struct MatchArgs {
     int ostride;
 };
 
-template <int WQ, int WT, int KC, bool NORMS>
+template <int WQ, int WT, int KC, int NBUF, bool NORMS>
 __global__ __launch_bounds__(256) void k_match(MatchArgs a) {
     constexpr int TQ = 2 * WQ, TT = 2 * WT, R = TQ + TT;
     constexpr int FQ = WQ / 16, FT = WT / 16;
     constexpr int NC = 256 / KC;           // staged chunks
-    constexpr int NB = NC > 1 ? 2 : 1;     // LDS buffers
+    constexpr int NB = NC > 1 ? NBUF : 1;  // LDS buffers (1: a second barrier per chunk, half the LDS)
     constexpr int RS4 = KC / 4 + 2;        // row stride in float4: KC + 8 floats = 8 mod 64 dwords
     constexpr int GR = KC / 16;            // 16-k groups per row and chunk
     constexpr int GPT = R * GR / 256;      // groups per thread and chunk
@@ -167,6 +169,12 @@ __global__ __launch_bounds__(256) void k_match(MatchArgs a) {
     const int wv = tid >> 6, lane = tid & 63, li = lane & 15, lg = lane >> 4;
     const int wq = wv & 1, wt = wv >> 1;
     const int qrow0 = wq * WQ, trow0 = TQ + wt * WT;  // LDS rows of this wave's fragments
+    // fragments entirely past n1 / n2 are not computed (wave-uniform)
+    bool vq[FQ], vt[FT];
+#pragma unroll
+    for (int y = 0; y < FQ; y++) vq[y] = q0 + qrow0 + 16 * y < n1;
+#pragma unroll
+    for (int x = 0; x < FT; x++) vt[x] = t0 + wt * WT + 16 * x < n2;
     f32x4 acc[FT][FQ];
 #pragma unroll
     for (int x = 0; x < FT; x++)
@@ -205,19 +213,23 @@ __global__ __launch_bounds__(256) void k_match(MatchArgs a) {
 #pragma unroll
             for (int x = 0; x < FT; x++)
 #pragma unroll
-                for (int y = 0; y < FQ; y++) acc[x][y] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[x].x, fb[y].x, acc[x][y], 0, 0, 0);
+                for (int y = 0; y < FQ; y++)
+                    if (vt[x] && vq[y]) acc[x][y] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[x].x, fb[y].x, acc[x][y], 0, 0, 0);
 #pragma unroll
             for (int x = 0; x < FT; x++)
 #pragma unroll
-                for (int y = 0; y < FQ; y++) acc[x][y] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[x].y, fb[y].y, acc[x][y], 0, 0, 0);
+                for (int y = 0; y < FQ; y++)
+                    if (vt[x] && vq[y]) acc[x][y] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[x].y, fb[y].y, acc[x][y], 0, 0, 0);
 #pragma unroll
             for (int x = 0; x < FT; x++)
 #pragma unroll
-                for (int y = 0; y < FQ; y++) acc[x][y] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[x].z, fb[y].z, acc[x][y], 0, 0, 0);
+                for (int y = 0; y < FQ; y++)
+                    if (vt[x] && vq[y]) acc[x][y] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[x].z, fb[y].z, acc[x][y], 0, 0, 0);
 #pragma unroll
             for (int x = 0; x < FT; x++)
 #pragma unroll
-                for (int y = 0; y < FQ; y++) acc[x][y] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[x].w, fb[y].w, acc[x][y], 0, 0, 0);
+                for (int y = 0; y < FQ; y++)
+                    if (vt[x] && vq[y]) acc[x][y] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[x].w, fb[y].w, acc[x][y], 0, 0, 0);
             if (nthread) {
                 // k = 16 qd + m sits at float4 (m & 3), component (m >> 2)
                 float4 v[4];
@@ -357,7 +369,7 @@ static int match_state(vs_ctx* ctx, int P, int kcap, unsigned long long** keys, 
     return VS_OK;
 }
 
-template <int WQ, int WT, int KC>
+template <int WQ, int WT, int KC, int NBUF>
 static void launch_tile(MatchArgs& a, int P, int cap_q, int cap_t, bool norms, hipStream_t s) {
     a.qblocks = (cap_q + 2 * WQ - 1) / (2 * WQ);
     a.tblocks = (cap_t + 2 * WT - 1) / (2 * WT);
@@ -365,20 +377,25 @@ static void launch_tile(MatchArgs& a, int P, int cap_q, int cap_t, bool norms, h
     a.per_xcd = (a.work + 7) / 8;
     const unsigned blocks = (unsigned)(8 * a.per_xcd);
     if (norms)
-        hipLaunchKernelGGL((k_match<WQ, WT, KC, true>), dim3(blocks), dim3(256), 0, s, a);
+        hipLaunchKernelGGL((k_match<WQ, WT, KC, NBUF, true>), dim3(blocks), dim3(256), 0, s, a);
     else
-        hipLaunchKernelGGL((k_match<WQ, WT, KC, false>), dim3(blocks), dim3(256), 0, s, a);
+        hipLaunchKernelGGL((k_match<WQ, WT, KC, NBUF, false>), dim3(blocks), dim3(256), 0, s, a);
 }
 
-// Tile choice: 64 x 64 workgroups (4 chains per wave, k staged in 64-wide chunks, two buffers)
-// when the problem fills the chip several times, else 32 x 32 workgroups (one 16 x 16 chain per
-// wave, all of k loaded at once: one memory round trip before the MFMAs) for latency.
+// Tile choice: 64 x 64 workgroups (4 chains per wave, k staged in 64-wide chunks through one LDS
+// buffer: 37 KB, four workgroups per CU) when the problem fills the chip several times, else
+// 32 x 32 workgroups (one 16 x 16 chain per wave, all of k loaded at once: one memory round trip
+// before the MFMAs) for latency.  VS_MATCH_TILE = small | large | large2 overrides (experiments).
 static void launch(MatchArgs& a, int P, int cap_q, int cap_t, bool norms, hipStream_t s) {
+    static const char* force = std::getenv("VS_MATCH_TILE");
     const long tiles32 = (long)P * ((cap_q + 31) / 32) * ((cap_t + 31) / 32);
-    if (tiles32 > 2048)
-        launch_tile<32, 32, 64>(a, P, cap_q, cap_t, norms, s);
+    const bool large = force ? std::strncmp(force, "large", 5) == 0 : tiles32 > 2048;
+    if (large && force && std::strcmp(force, "large2") == 0)
+        launch_tile<32, 32, 64, 2>(a, P, cap_q, cap_t, norms, s);
+    else if (large)
+        launch_tile<32, 32, 64, 1>(a, P, cap_q, cap_t, norms, s);
     else
-        launch_tile<16, 16, 256>(a, P, cap_q, cap_t, norms, s);
+        launch_tile<16, 16, 256, 1>(a, P, cap_q, cap_t, norms, s);
 }
 
 int match_pairs(vs_ctx* ctx, int P, const int* d_pairs, int F, const float* d_desc, const int* d_n, int cap,

@@ -9,7 +9,10 @@
 //   estimate_motion_3d3d  Slam.h:133-137          (Slam.cpp:214-375)
 //   solve_pnp / PnPResult Slam.h:120-131          (Slam.cpp:505-529)
 //   track_local_map       Slam.h:96               (Slam.cpp:380-469)
-//   Optimizer::optimize_pose  Optimizer.h:31-35   (Optimizer.cpp:54-180)
+//   Frame                 Frame.h:12-72           (Frame.cpp: detect_features :33-38, depth :47-54)
+//   MapPoint / Map        MapPoint.h:8-48, Map.h:10-40 (the containers local BA gathers from)
+//   Optimizer::project_point / optimize_pose / local_bundle_adjustment
+//                         Optimizer.h:24-38       (Optimizer.cpp:26-48, 54-180, 187-599)
 //
 // OpenCV types are replaced by layout-compatible PODs (KeyPoint == cv::KeyPoint, DMatch ==
 // cv::DMatch, Descriptors == an N x 256 CV_32F cv::Mat).  Every compute call goes to the GPU
@@ -20,6 +23,7 @@
 #include <cfloat>
 #include <cstdint>
 #include <memory>
+#include <mutex>
 #include <stdexcept>
 #include <string>
 #include <unordered_map>
@@ -189,13 +193,141 @@ int track_local_map(Context& ctx, const MapPointsView& map, const std::vector<Ke
                     std::vector<int>& map_point_indices, std::vector<std::pair<int, int>>* observations = nullptr,
                     int img_w = 640, int img_h = 480);
 
-// Optimizer (Optimizer.h): the pose-only LM.  The frame's camera->world pose is updated in
-// place; returns {rms before, rms after} ({0, 0} and untouched when fewer than 3 points).
+// Frame (Frame.h:12-72): image, features, depth, camera->world pose, keyframe flag and
+// map_point_indices.  The reference constructs from a file path (cv::imread + cvtColor,
+// Frame.cpp:19-30); decoding is out of scope here, so the caller hands over the decoded 8-bit
+// image (copied) — or none, which leaves the frame without features like a failed imread.
+class FeatureExtractor;
+class Frame {
+   public:
+    Frame() = default;
+    Frame(int id, const Image& image, double timestamp = 0.0);
+    // Frame::detect_features (Frame.cpp:33-38): extract, then map_point_indices = -1 per keypoint
+    void detect_features(FeatureExtractor& extractor);
+    // Frame::load_depth_image (Frame.cpp:47-54) from the decoded 16-bit TUM depth PNG:
+    // depth = raw / 5000 m (Config.h:28), raw == 0 -> 0 (invalid)
+    void load_depth_image(const uint16_t* raw, int rows, int cols, size_t step_bytes = 0);
+    void set_depth_map(const DepthImage& depth);  // Frame::set_depth_map (copied)
+    bool has_real_depth() const { return has_real_depth_; }
+    DepthImage depth_map() const { return {depth_.data(), has_real_depth_ ? rows_ : 0, has_real_depth_ ? cols_ : 0}; }
+
+    Mat33 get_rotation() const { return R_; }
+    Vec3 get_translation() const { return t_; }
+    std::array<double, 16> get_pose() const;  // Frame::get_pose (Frame.cpp:100-105): 4x4 [R t; 0 1]
+    void set_rotation(const Mat33& R) { R_ = R; }
+    void set_translation(const Vec3& t) { t_ = t; }
+    void set_pose(const Mat33& R, const Vec3& t) {
+        R_ = R;
+        t_ = t;
+    }
+    int id() const { return id_; }
+    double timestamp() const { return timestamp_; }
+    Image image() const { return {pixels_.data(), rows_, cols_, channels_, (size_t)cols_ * channels_}; }
+    const std::vector<KeyPoint>& keypoints() const { return keypoints_; }
+    const Descriptors& descriptors() const { return descriptors_; }
+    bool is_processed() const { return processed_; }
+    bool is_keyframe() const { return is_keyframe_; }
+    void set_keyframe(bool kf) { is_keyframe_ = kf; }
+    std::vector<int>& map_point_indices() { return map_point_indices_; }
+    const std::vector<int>& map_point_indices() const { return map_point_indices_; }
+
+   private:
+    int id_ = -1;
+    double timestamp_ = 0.0;
+    std::vector<uint8_t> pixels_;
+    int rows_ = 0, cols_ = 0, channels_ = 3;
+    std::vector<KeyPoint> keypoints_;
+    Descriptors descriptors_;
+    std::vector<float> depth_;
+    Mat33 R_{1, 0, 0, 0, 1, 0, 0, 0, 1};
+    Vec3 t_{0, 0, 0};
+    bool processed_ = false, is_keyframe_ = false, has_real_depth_ = false;
+    std::vector<int> map_point_indices_;
+};
+
+// MapPoint (MapPoint.h:8-48)
+class MapPoint {
+   public:
+    MapPoint() = default;
+    MapPoint(int id, const Point3d& position, const float* descriptor /* 256, nullable */);
+    int id() const { return id_; }
+    Point3d position() const { return position_; }
+    void set_position(const Point3d& p) { position_ = p; }
+    const std::vector<float>& descriptor() const { return descriptor_; }
+    void add_observation(int frame_id, int keypoint_idx) { observations_.emplace_back(frame_id, keypoint_idx); }
+    const std::vector<std::pair<int, int>>& observations() const { return observations_; }
+    int observation_count() const { return (int)observations_.size(); }
+    bool is_valid() const { return valid_; }
+    void set_valid(bool v) { valid_ = v; }
+    void increase_visible(int n = 1) { visible_count_ += n; }
+    void increase_found(int n = 1) { found_count_ += n; }
+    float get_found_ratio() const { return visible_count_ > 0 ? (float)found_count_ / visible_count_ : 0.0f; }
+    int visible_count() const { return visible_count_; }
+    int found_count() const { return found_count_; }
+    void set_first_kf_id(int id) { first_kf_id_ = id; }
+    int first_kf_id() const { return first_kf_id_; }
+
+   private:
+    int id_ = -1;
+    Point3d position_;
+    std::vector<std::pair<int, int>> observations_;
+    std::vector<float> descriptor_;
+    bool valid_ = true;
+    int visible_count_ = 0, found_count_ = 0, first_kf_id_ = 0;
+};
+
+// Map (Map.h:10-40): frames in insertion order, map points, one mutex
+class Map {
+   public:
+    void add_frame(std::shared_ptr<Frame> f) {
+        std::lock_guard<std::mutex> lock(mutex_);
+        frames_.push_back(std::move(f));
+    }
+    void add_map_point(const MapPoint& mp) {
+        std::lock_guard<std::mutex> lock(mutex_);
+        map_points_.push_back(mp);
+    }
+    std::shared_ptr<Frame> get_frame(int id) const;
+    std::vector<std::shared_ptr<Frame>> get_all_frames() const {
+        std::lock_guard<std::mutex> lock(mutex_);
+        return frames_;
+    }
+    int frame_count() const {
+        std::lock_guard<std::mutex> lock(mutex_);
+        return (int)frames_.size();
+    }
+    std::vector<std::shared_ptr<Frame>> get_keyframes() const;
+    std::vector<MapPoint>& map_points() { return map_points_; }
+    const std::vector<MapPoint>& map_points() const { return map_points_; }
+    std::vector<std::shared_ptr<Frame>>& frames_direct() { return frames_; }
+    std::mutex& mutex() { return mutex_; }
+
+   private:
+    std::vector<std::shared_ptr<Frame>> frames_;
+    std::vector<MapPoint> map_points_;
+    mutable std::mutex mutex_;
+};
+
+// Optimizer (Optimizer.h:22-48) over the GPU context.  Loop correction / pose graph optimisation
+// (g2o) are out of scope.
 class Optimizer {
    public:
     explicit Optimizer(Context& ctx) : ctx_(ctx) {}
+    // Optimizer::project_point (Optimizer.cpp:26-48): world point -> pixel for a camera->world pose;
+    // (-1, -1) behind the camera (z < 1e-6).  Host arithmetic, the reference's expression order.
+    static Point2d project_point(const Point3d& pw, const Mat33& R_world, const Vec3& t_world, const Intrinsics& K);
+    // the pose-only LM (Optimizer.cpp:54-180).  The pose is updated in place; returns {rms before,
+    // rms after} ({0, 0} and untouched when fewer than 3 points).
     std::pair<double, double> optimize_pose(Mat33& R_world, Vec3& t_world, const std::vector<Point3d>& points_3d,
                                             const std::vector<Point2f>& points_2d);
+    // the reference's signature: the frame's pose is read and written (Optimizer.cpp:166-168)
+    std::pair<double, double> optimize_pose(const std::shared_ptr<Frame>& frame, const std::vector<Point3d>& points_3d,
+                                            const std::vector<Point2f>& points_2d);
+    // Optimizer::local_bundle_adjustment (Optimizer.cpp:187-599): the window gather under the map
+    // mutex (:205-244: the last window_size keyframes, their valid map points in first-seen order,
+    // observations keyframe-major in keypoint order), Schur-complement LM on the GPU (vs_local_ba),
+    // write-back of poses 1..N-1 and of the points under the mutex (:580-596).  {0, 0} on bail-out.
+    std::pair<double, double> local_bundle_adjustment(Map& map, int window_size = 10);
 
    private:
     Context& ctx_;
