@@ -382,20 +382,20 @@ static void launch_tile(MatchArgs& a, int P, int cap_q, int cap_t, bool norms, h
         hipLaunchKernelGGL((k_match<WQ, WT, KC, NBUF, false>), dim3(blocks), dim3(256), 0, s, a);
 }
 
-// Tile choice: 64 x 64 workgroups (4 chains per wave, k staged in 64-wide chunks through one LDS
-// buffer: 37 KB, four workgroups per CU) when the problem fills the chip several times, else
-// 32 x 32 workgroups (one 16 x 16 chain per wave, all of k loaded at once: one memory round trip
-// before the MFMAs) for latency.  VS_MATCH_TILE = small | large | large2 overrides (experiments).
+// Tile: 64 x 64 workgroups (4 chains per wave, k staged in 64-wide chunks through one LDS buffer:
+// 37 KB, four workgroups per CU).  Measured against 32 x 32 workgroups with all of k loaded at once
+// (one 16 x 16 chain per wave) and against two LDS buffers (two workgroups per CU): the 64 x 64
+// single-buffer tile is faster from 8 pairs up and inside the tracker (32 CUs, one pair), and within
+// 15 % at one pair on the whole chip.  VS_MATCH_TILE = small | large2 selects the others
+// (experiments; profiles/r02_match_variants.jsonl).
 static void launch(MatchArgs& a, int P, int cap_q, int cap_t, bool norms, hipStream_t s) {
     static const char* force = std::getenv("VS_MATCH_TILE");
-    const long tiles32 = (long)P * ((cap_q + 31) / 32) * ((cap_t + 31) / 32);
-    const bool large = force ? std::strncmp(force, "large", 5) == 0 : tiles32 > 2048;
-    if (large && force && std::strcmp(force, "large2") == 0)
-        launch_tile<32, 32, 64, 2>(a, P, cap_q, cap_t, norms, s);
-    else if (large)
-        launch_tile<32, 32, 64, 1>(a, P, cap_q, cap_t, norms, s);
-    else
+    if (force && std::strcmp(force, "small") == 0)
         launch_tile<16, 16, 256, 1>(a, P, cap_q, cap_t, norms, s);
+    else if (force && std::strcmp(force, "large2") == 0)
+        launch_tile<32, 32, 64, 2>(a, P, cap_q, cap_t, norms, s);
+    else
+        launch_tile<32, 32, 64, 1>(a, P, cap_q, cap_t, norms, s);
 }
 
 int match_pairs(vs_ctx* ctx, int P, const int* d_pairs, int F, const float* d_desc, const int* d_n, int cap,
