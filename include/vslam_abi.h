@@ -92,7 +92,10 @@ int vs_extract_batch(vs_ctx* ctx, int B, const uint8_t* const* imgs, int h, int 
                      size_t stride, vs_keypoint* kps, float* desc, int cap, int* n);
 
 /* B frames, device buffers (offline batch mode): d_imgs is B contiguous H x W x 3 BGR u8
- * frames; outputs d_kps [B][cap], d_desc [B][cap][256], d_n [B]. */
+ * frames; outputs d_kps [B][cap], d_desc [B][cap][256], d_n [B].  Enqueue only (no host sync):
+ * a frame whose NMS could not be completed on the device (its undecided pixels exceed the
+ * finishing pass's list) gets d_n[b] = VS_ERR_NOTCONV and no keypoints; every consumer of d_n in
+ * this library (matching, the tracker) treats a negative count as an error / empty frame. */
 int vs_extract_batch_dev(vs_ctx* ctx, int B, const uint8_t* d_imgs, int h, int w,
                          vs_keypoint* d_kps, float* d_desc, int* d_n, int cap, void* stream);
 

@@ -59,6 +59,7 @@ _SIG = {
     "orc_slam_finish": (None, [_P]),
     "orc_slam_trajectory": (_I, [_P, _I, _P, _P, _P, _P]),
     "orc_slam_stats": (None, [_P, _P]),
+    "orc_slam_stage_seconds": (ctypes.c_int, [_P, _P, ctypes.c_int]),
     "orc_slam_map": (_I, [_P, _I, _P, _P]),
     "orc_mt19937": (None, [ctypes.c_uint32, _I, _P]),
     "orc_expf_array": (None, [_P, _I, _P]),
@@ -477,6 +478,14 @@ class Slam:
         out = np.zeros(24, np.int32)
         lib().orc_slam_stats(self.h, _p(out))
         return out
+
+    STAGES = ("match", "fmat_ransac", "motion_3d3d_emat", "track_local_map", "solve_pnp", "match_map", "visibility")
+
+    def stage_seconds(self):
+        """CPU seconds per tracking stage so far (orc_slam_stage_seconds)."""
+        out = np.zeros(len(self.STAGES))
+        k = lib().orc_slam_stage_seconds(self.h, _p(out), len(out))
+        return dict(zip(self.STAGES[:k], out[:k].tolist()))
 
     def map_points(self):
         n = lib().orc_slam_map(self.h, 0, None, None)

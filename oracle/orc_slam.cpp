@@ -4,6 +4,7 @@
 // stage (OracleOps below).  tests/ run the GPU tracker (vs_slam_*, libvslam_hip.so) and this one
 // on the same features and compare trajectories, map sizes and decision counters; bench.py may
 // time it as the CPU baseline.  The product never links this file.
+#include <chrono>
 #include <cstdlib>
 #include <cstring>
 #include <memory>
@@ -21,7 +22,18 @@ using vs_trk::Match;
 static_assert(sizeof(vs_trk::Keypoint) == sizeof(orc_keypoint), "keypoint layouts differ");
 static_assert(sizeof(vs_trk::Match) == sizeof(orc_match), "match layouts differ");
 
+// Per-stage CPU seconds (for the CPU baseline's per-stage split; order = orc_slam_stage_seconds)
+enum Stage { kMatch, kFmat, kMotion, kTrackLocalMap, kPnP, kMatchMap, kVisibility, kNStage };
+
+struct StageTimer {
+    double* acc;
+    std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
+    explicit StageTimer(double* a) : acc(a) {}
+    ~StageTimer() { *acc += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count(); }
+};
+
 struct OracleOps {
+    double sec[kNStage] = {};
     double K[4] = {vs_trk::cfg::FX, vs_trk::cfg::FY, vs_trk::cfg::CX, vs_trk::cfg::CY};
     int h = vs_trk::cfg::IMAGE_HEIGHT, w = vs_trk::cfg::IMAGE_WIDTH;
     std::vector<float> map_desc;  // M x 256
@@ -34,6 +46,7 @@ struct OracleOps {
     }
 
     std::vector<Match> match(const Frame& a, const Frame& b, float ratio) {
+        StageTimer st(&sec[kMatch]);
         const int n1 = (int)a.kps.size(), n2 = (int)b.kps.size();
         std::vector<Match> raw(std::max(n1, 1)), good(std::max(n1, 1));
         int nr = 0, ng = 0;
@@ -56,6 +69,7 @@ struct OracleOps {
     // 3D-3D (Slam.cpp:955), then estimate_motion + estimate_scale_from_depth (:965-984)
     void motion(const Frame& ref, const Frame& cur, const std::vector<float>& p1, const std::vector<float>& p2,
                 uint32_t seed, vs_trk::ChainResult& R) {
+        StageTimer st(&sec[kMotion]);
         const int n = (int)(p1.size() / 2);
         int diag[4];
         R.ok3d = orc_ransac_3d3d(p1.data(), p2.data(), n, depth_or_zero(ref), depth_or_zero(cur), h, w, K, seed, 200,
@@ -77,14 +91,17 @@ struct OracleOps {
         double F[9], err[2];
         int diag[4], f_ok = 0;
         std::vector<int> keep(std::max(n, 1));
-        const int m = orc_fmat_verify(reinterpret_cast<const orc_keypoint*>(ref.kps.data()),
-                                      reinterpret_cast<const orc_keypoint*>(cur.kps.data()),
-                                      reinterpret_cast<const orc_match*>(R.good.data()), n, F, keep.data(), err, diag,
-                                      &f_ok);
-        R.f_ok = f_ok != 0;
-        R.f_iters = diag[1];
-        R.epi_before = err[0];
-        R.epi_after = err[1];
+        int m;
+        {
+            StageTimer st(&sec[kFmat]);
+            m = orc_fmat_verify(reinterpret_cast<const orc_keypoint*>(ref.kps.data()),
+                                reinterpret_cast<const orc_keypoint*>(cur.kps.data()),
+                                reinterpret_cast<const orc_match*>(R.good.data()), n, F, keep.data(), err, diag, &f_ok);
+            R.f_ok = f_ok != 0;
+            R.f_iters = diag[1];
+            R.epi_before = err[0];
+            R.epi_after = err[1];
+        }
         for (int i = 0; i < m; i++) R.kept.push_back(R.good[keep[i]]);
         std::vector<float> p1, p2;
         points(ref, cur, R.kept, p1, p2);
@@ -93,6 +110,7 @@ struct OracleOps {
     }
 
     bool find_fundamental(const std::vector<float>& p1, const std::vector<float>& p2, std::vector<uint8_t>& mask) {
+        StageTimer st(&sec[kFmat]);
         const int n = (int)(p1.size() / 2);
         mask.assign(std::max(n, 1), 0);
         double F[9];
@@ -108,6 +126,7 @@ struct OracleOps {
     }
 
     int track_local_map(Map& m, Frame& f, std::vector<std::pair<int, int>>& obs) {
+        StageTimer st(&sec[kTrackLocalMap]);
         const int nkp = (int)f.kps.size(), nmp = m.size();
         const int cap = std::max(nmp, 1);
         std::vector<int> om(cap), ok(cap);
@@ -123,6 +142,7 @@ struct OracleOps {
     }
 
     vs_trk::PnPResult solve_pnp(const std::vector<float>& obj, const std::vector<float>& img, int iters, int min_inliers) {
+        StageTimer st(&sec[kPnP]);
         vs_trk::PnPResult r;
         int inl = 0;
         r.success = orc_solve_pnp(obj.data(), img.data(), (int)(obj.size() / 3), K, iters, min_inliers,
@@ -132,6 +152,7 @@ struct OracleOps {
     }
 
     std::vector<std::pair<int, int>> match_map(const Map&, const Frame& f, const std::vector<int>& ids, float ratio) {
+        StageTimer st(&sec[kMatchMap]);
         std::vector<std::pair<int, int>> out;
         const int n1 = (int)f.kps.size(), n2 = (int)ids.size();
         std::vector<float> t((size_t)n2 * 256);
@@ -154,6 +175,7 @@ struct OracleOps {
 
     // Slam.cpp:1089-1108 with Optimizer::project_point
     void visibility(const Map& m, const Frame& f, const vs_trk::M3& R, const vs_trk::V3& t, std::vector<uint8_t>& flags) {
+        StageTimer st(&sec[kVisibility]);
         flags.assign(m.size(), 0);
         const double rr = vs_trk::cfg::TRACK_VISIBILITY_RADIUS * vs_trk::cfg::TRACK_VISIBILITY_RADIUS;
         for (int i = 0; i < m.size(); i++) {
@@ -280,6 +302,15 @@ int orc_slam_map(void* h, int cap, double* pos, uint8_t* valid) {
         if (valid) valid[i] = m.valid[i];
     }
     return m.size();
+}
+
+// Seconds spent in each stage so far: match, fmat, motion (3D-3D / E), track_local_map, solve_pnp,
+// match_map, visibility.  Returns the number of stages written (at most n).
+int orc_slam_stage_seconds(void* h, double* out, int n) {
+    const auto& ops = static_cast<OrcSlam*>(h)->ops;
+    const int k = n < kNStage ? n : kNStage;
+    for (int i = 0; i < k; i++) out[i] = ops.sec[i];
+    return k;
 }
 
 }  // extern "C"

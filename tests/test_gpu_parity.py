@@ -321,3 +321,58 @@ def test_profile_reports_stages(vsctx, seq4):
     vsctx.profile(False)
     for st in ["conv1_fused", "conv2a", "head_a", "nms_rounds", "sample"]:
         assert st in prof and prof[st][0] > 0
+
+
+# --------------------------------------------- NMS beyond the tile-round budget
+def _unit_grid(hc, wc, seed):
+    dg = np.random.default_rng(seed).standard_normal((256, hc, wc)).astype(np.float32)
+    return dg / np.linalg.norm(dg, axis=0, keepdims=True)
+
+
+@pytest.mark.parametrize("case", ["serpentine", "gradient"])
+def test_postprocess_long_dependency_chains(vsctx, oracle, case):
+    """Heatmaps the 8 tile rounds cannot settle (tests/nms_cases.py: a ~4900-pixel chain through
+    every tile, thousands of priority-MIS rounds; a whole-frame score gradient): k_nms_finish
+    completes them and the keypoints equal the oracle's sequential greedy NMS bit for bit."""
+    import nms_cases
+    hc, wc = 60, 80
+    semi = nms_cases.serpentine_semi(hc, wc)[0] if case == "serpentine" else nms_cases.gradient_semi(hc, wc)
+    dg = _unit_grid(hc, wc, 5)
+    kg, dgpu = vsctx.postprocess(semi, dg)
+    ko, do = oracle.postprocess(semi, dg, order_mode=1)
+    assert _kp_equal(kg, ko) and _bits_equal(dgpu, do)
+    assert len(kg) == 400
+    if case == "serpentine":  # the top of the chain: every other pixel, 8 apart, along row 2
+        assert np.array_equal(kg["x"][:80], np.arange(0, 640, 8)) and np.all(kg["y"][:80] == 2)
+
+
+def test_postprocess_round_cap_is_reported(vsctx, monkeypatch):
+    """A frame that reaches k_nms_finish's round cap is an error, never a silent keypoint list:
+    VS_ERR_NOTCONV from the host entry point, d_n[b] = VS_ERR_NOTCONV (no keypoints) for that
+    frame alone on the enqueue-only device path.  The cap is lowered to 2 rounds here
+    (VS_NMS_FINISH_ROUNDS, a test knob) so the serpentine chain reaches it."""
+    import torch
+    import nms_cases
+    import vslam_abi
+    hc, wc = 60, 80
+    semi_s, _ = nms_cases.serpentine_semi(hc, wc)
+    rng = np.random.default_rng(3)
+    semi_r = (rng.standard_normal((65, hc, wc)) * 3).astype(np.float32)
+    dg = _unit_grid(hc, wc, 6)
+    monkeypatch.setenv("VS_NMS_FINISH_ROUNDS", "2")
+    with pytest.raises(vslam_abi.VSError, match="NOTCONV"):
+        vsctx.postprocess(semi_s, dg)
+    dev = torch.device("cuda", 0)
+    semi = torch.from_numpy(np.stack([semi_s, semi_r]).transpose(0, 2, 3, 1).copy()).to(dev)
+    grid = torch.from_numpy(np.stack([dg, dg]).transpose(0, 2, 3, 1).copy()).to(dev)
+    cap = 400
+    kps = torch.zeros((2, cap, 7), dtype=torch.int32, device=dev)
+    desc = torch.zeros((2, cap, 256), dtype=torch.float32, device=dev)
+    n = torch.full((2,), 12345, dtype=torch.int32, device=dev)
+    vsctx.postprocess_batch_dev(2, semi.data_ptr(), grid.data_ptr(), hc * 8, wc * 8, kps.data_ptr(),
+                                desc.data_ptr(), n.data_ptr(), cap)
+    torch.cuda.synchronize()
+    assert n.tolist() == [vslam_abi.VS_ERR_NOTCONV, 400]
+    monkeypatch.delenv("VS_NMS_FINISH_ROUNDS")
+    kg, _ = vsctx.postprocess(semi_r, dg)
+    assert np.array_equal(kps[1].cpu().numpy().view(np.uint8).reshape(-1)[:kg.nbytes], kg.view(np.uint8).reshape(-1))

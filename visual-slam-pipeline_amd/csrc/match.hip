@@ -37,12 +37,22 @@
 #include <climits>
 #include <cstdlib>
 #include <cstring>
+#include <type_traits>
 
 #include "vs_internal.h"
 
 namespace vs {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+// f(integral_constant<int, I>) for I = B .. E-1, unrolled at compile time
+template <int B, int E, class F>
+__device__ __forceinline__ void static_for(F&& f) {
+    if constexpr (B < E) {
+        f(std::integral_constant<int, B>{});
+        static_for<B + 1, E>(f);
+    }
+}
 
 constexpr unsigned long long kNoKey = ~0ull;
 
@@ -98,7 +108,7 @@ struct MatchArgs {
     int ostride;
 };
 
-template <int WQ, int WT, int KC, int NBUF, bool NORMS>
+template <int WQ, int WT, int KC, int NBUF, int PD, bool NORMS>
 __global__ __launch_bounds__(256) void k_match(MatchArgs a) {
     constexpr int TQ = 2 * WQ, TT = 2 * WT, R = TQ + TT;
     constexpr int FQ = WQ / 16, FT = WT / 16;
@@ -146,23 +156,31 @@ __global__ __launch_bounds__(256) void k_match(MatchArgs a) {
                                      : T + (size_t)min(t0 + row - TQ, n2 - 1) * 256;
         src[u] = reinterpret_cast<const float4*>(base) + 4 * q4;
     }
-    float4 reg[GPT][4];
-    auto load = [&](int c) {
+    // PD chunks in flight in registers (slot c % PD holds chunk c): PD = 1 overlaps one chunk's
+    // loads with the previous chunk's MFMAs (throughput shape, many workgroups per CU); PD = NC
+    // issues every load of the tile up front, so a lone workgroup pays one memory latency instead
+    // of one per chunk (latency shape: a single pair on the tracker's CU set).
+    // (compile-time chunk indices throughout — static_for — so the ring stays in registers)
+    float4 reg[PD][GPT][4];
+    auto load = [&](auto cc) {
+        constexpr int c = decltype(cc)::value;
 #pragma unroll
         for (int u = 0; u < GPT; u++)
 #pragma unroll
-            for (int j = 0; j < 4; j++) reg[u][j] = src[u][(KC / 4) * c + j];
+            for (int j = 0; j < 4; j++) reg[c % PD][u][j] = src[u][(KC / 4) * c + j];
     };
     // position 4g + j of a 16-k group holds k = 4j + g: the fragment of lane group g is one float4
-    auto store = [&](int buf) {
+    auto store = [&](auto cc, int buf) {
+        constexpr int c = decltype(cc)::value;
+        const float4(&r)[GPT][4] = reg[c % PD];
 #pragma unroll
         for (int u = 0; u < GPT; u++) {
             const int G = tid + 256 * u, row = G / GR, q4 = G % GR;
             float4* d = &sbuf[buf][row * RS4 + 4 * q4];
-            d[0] = make_float4(reg[u][0].x, reg[u][1].x, reg[u][2].x, reg[u][3].x);
-            d[1] = make_float4(reg[u][0].y, reg[u][1].y, reg[u][2].y, reg[u][3].y);
-            d[2] = make_float4(reg[u][0].z, reg[u][1].z, reg[u][2].z, reg[u][3].z);
-            d[3] = make_float4(reg[u][0].w, reg[u][1].w, reg[u][2].w, reg[u][3].w);
+            d[0] = make_float4(r[u][0].x, r[u][1].x, r[u][2].x, r[u][3].x);
+            d[1] = make_float4(r[u][0].y, r[u][1].y, r[u][2].y, r[u][3].y);
+            d[2] = make_float4(r[u][0].z, r[u][1].z, r[u][2].z, r[u][3].z);
+            d[3] = make_float4(r[u][0].w, r[u][1].w, r[u][2].w, r[u][3].w);
         }
     };
 
@@ -175,6 +193,7 @@ __global__ __launch_bounds__(256) void k_match(MatchArgs a) {
     for (int y = 0; y < FQ; y++) vq[y] = q0 + qrow0 + 16 * y < n1;
 #pragma unroll
     for (int x = 0; x < FT; x++) vt[x] = t0 + wt * WT + 16 * x < n2;
+    const bool full = q0 + qrow0 + WQ <= n1 && t0 + wt * WT + WT <= n2;
     f32x4 acc[FT][FQ];
 #pragma unroll
     for (int x = 0; x < FT; x++)
@@ -186,19 +205,21 @@ __global__ __launch_bounds__(256) void k_match(MatchArgs a) {
     const bool nthread = !NORMS && lane < NR;
     float nrm = 0.0f;
 
+    // caller's norms: loaded before the staging loads, stored to LDS after them (vmcnt is in order)
+    float cnorm = 0.0f;
     if (NORMS && tid < R) {
-        const float* nsrc = tid < TQ ? a.normsq + (size_t)qf * a.qstride + q0 + tid
-                                     : a.normst + (size_t)tf * a.tstride + t0 + tid - TQ;
-        const bool ok = tid < TQ ? q0 + tid < n1 : t0 + tid - TQ < n2;
-        s_norm[tid] = ok ? *nsrc : 0.0f;
+        const float* nsrc = tid < TQ ? a.normsq + (size_t)qf * a.qstride + min(q0 + tid, n1 - 1)
+                                     : a.normst + (size_t)tf * a.tstride + min(t0 + tid - TQ, n2 - 1);
+        cnorm = *nsrc;
     }
-    load(0);
-    store(0);
+    static_for<0, (PD < NC ? PD : NC)>([&](auto cc) { load(cc); });
+    store(std::integral_constant<int, 0>{}, 0);
+    if (NORMS && tid < R) s_norm[tid] = cnorm;
     __syncthreads();
-#pragma unroll
-    for (int c = 0; c < NC; c++) {  // unrolled: no loop-carried copies of the prefetch registers
+    static_for<0, NC>([&](auto cc) {  // unrolled: no loop-carried copies of the prefetch registers
+        constexpr int c = decltype(cc)::value;
         const int buf = NB > 1 ? (c & 1) : 0;
-        if (c + 1 < NC) load(c + 1);
+        if constexpr (c + PD < NC) load(std::integral_constant<int, c + PD>{});
         // keep the transposing register moves of store() below the MFMAs: hoisted here they would
         // wait for the loads just issued
         __builtin_amdgcn_sched_barrier(0);
@@ -210,26 +231,25 @@ __global__ __launch_bounds__(256) void k_match(MatchArgs a) {
             for (int x = 0; x < FT; x++) fa[x] = sb[(trow0 + 16 * x + li) * RS4 + 4 * qd + lg];
 #pragma unroll
             for (int y = 0; y < FQ; y++) fb[y] = sb[(qrow0 + 16 * y + li) * RS4 + 4 * qd + lg];
+            // all fragments valid (every interior workgroup): straight-line MFMAs; else per-fragment
+            if (full) {
 #pragma unroll
-            for (int x = 0; x < FT; x++)
+                for (int j = 0; j < 4; j++)
 #pragma unroll
-                for (int y = 0; y < FQ; y++)
-                    if (vt[x] && vq[y]) acc[x][y] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[x].x, fb[y].x, acc[x][y], 0, 0, 0);
+                    for (int x = 0; x < FT; x++)
 #pragma unroll
-            for (int x = 0; x < FT; x++)
+                        for (int y = 0; y < FQ; y++)
+                            acc[x][y] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[x][j], fb[y][j], acc[x][y], 0, 0, 0);
+            } else {
 #pragma unroll
-                for (int y = 0; y < FQ; y++)
-                    if (vt[x] && vq[y]) acc[x][y] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[x].y, fb[y].y, acc[x][y], 0, 0, 0);
+                for (int j = 0; j < 4; j++)
 #pragma unroll
-            for (int x = 0; x < FT; x++)
+                    for (int x = 0; x < FT; x++)
 #pragma unroll
-                for (int y = 0; y < FQ; y++)
-                    if (vt[x] && vq[y]) acc[x][y] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[x].z, fb[y].z, acc[x][y], 0, 0, 0);
-#pragma unroll
-            for (int x = 0; x < FT; x++)
-#pragma unroll
-                for (int y = 0; y < FQ; y++)
-                    if (vt[x] && vq[y]) acc[x][y] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[x].w, fb[y].w, acc[x][y], 0, 0, 0);
+                        for (int y = 0; y < FQ; y++)
+                            if (vt[x] && vq[y])
+                                acc[x][y] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[x][j], fb[y][j], acc[x][y], 0, 0, 0);
+            }
             if (nthread) {
                 // k = 16 qd + m sits at float4 (m & 3), component (m >> 2)
                 float4 v[4];
@@ -244,15 +264,15 @@ __global__ __launch_bounds__(256) void k_match(MatchArgs a) {
                 }
             }
         }
-        if (c + 1 < NC) {
+        if constexpr (c + 1 < NC) {
             __builtin_amdgcn_sched_barrier(0);
             if (NB == 1) __syncthreads();
-            store(NB > 1 ? (buf ^ 1) : 0);
-        } else if (nthread) {
-            s_norm[nrow] = nrm;
+            store(std::integral_constant<int, c + 1>{}, NB > 1 ? (buf ^ 1) : 0);
+        } else {
+            if (nthread) s_norm[nrow] = nrm;
         }
         __syncthreads();
-    }
+    });
 
     // ---- per-wave top-2 per query: D[train 4 lg + e][query li] of each 16 x 16 fragment ----
     unsigned long long mine0 = kNoKey, mine1 = kNoKey;  // the fragment this lane group publishes
@@ -369,7 +389,7 @@ static int match_state(vs_ctx* ctx, int P, int kcap, unsigned long long** keys, 
     return VS_OK;
 }
 
-template <int WQ, int WT, int KC, int NBUF>
+template <int WQ, int WT, int KC, int NBUF, int PD = 1>
 static void launch_tile(MatchArgs& a, int P, int cap_q, int cap_t, bool norms, hipStream_t s) {
     a.qblocks = (cap_q + 2 * WQ - 1) / (2 * WQ);
     a.tblocks = (cap_t + 2 * WT - 1) / (2 * WT);
@@ -377,35 +397,48 @@ static void launch_tile(MatchArgs& a, int P, int cap_q, int cap_t, bool norms, h
     a.per_xcd = (a.work + 7) / 8;
     const unsigned blocks = (unsigned)(8 * a.per_xcd);
     if (norms)
-        hipLaunchKernelGGL((k_match<WQ, WT, KC, NBUF, true>), dim3(blocks), dim3(256), 0, s, a);
+        hipLaunchKernelGGL((k_match<WQ, WT, KC, NBUF, PD, true>), dim3(blocks), dim3(256), 0, s, a);
     else
-        hipLaunchKernelGGL((k_match<WQ, WT, KC, NBUF, false>), dim3(blocks), dim3(256), 0, s, a);
+        hipLaunchKernelGGL((k_match<WQ, WT, KC, NBUF, PD, false>), dim3(blocks), dim3(256), 0, s, a);
 }
 
-// Tile: 64 x 64 workgroups (4 chains per wave, k staged in 64-wide chunks through one LDS buffer:
-// 37 KB, four workgroups per CU).  Measured against 32 x 32 workgroups with all of k loaded at once
-// (one 16 x 16 chain per wave) and against two LDS buffers (two workgroups per CU): the 64 x 64
-// single-buffer tile is faster from 8 pairs up and inside the tracker (32 CUs, one pair), and within
-// 15 % at one pair on the whole chip.  VS_MATCH_TILE = small | large2 selects the others
-// (experiments; profiles/r02_match_variants.jsonl).
+// Tile: 64 x 64 workgroups (4 chains per wave, k staged in 32-wide chunks through one LDS buffer:
+// 21 KB, seven waves per SIMD).  Measured (profiles/r02_match_variants.jsonl, r02 sweep) against
+// 32 x 32 workgroups with all of k loaded at once (one 16 x 16 chain per wave), 64-wide chunks
+// (37 KB, four workgroups per CU) and two LDS buffers of either width: the 32-wide single buffer is
+// the fastest from 8 pairs up (54 % of the fp32 MFMA peak at 512 pairs, 35 % at 32) and ties at one
+// pair.  Issuing all eight chunks' loads up front (PD = 8) does not shorten a lone pair (19.2 vs
+// 18.5 us per launch, r02 sweep): the single-pair time is not the per-chunk load latency.
+// VS_MATCH_TILE = small | k64 | k64d | k32d | deep selects the others (experiments).
 static void launch(MatchArgs& a, int P, int cap_q, int cap_t, bool norms, hipStream_t s) {
     static const char* force = std::getenv("VS_MATCH_TILE");
     if (force && std::strcmp(force, "small") == 0)
         launch_tile<16, 16, 256, 1>(a, P, cap_q, cap_t, norms, s);
-    else if (force && std::strcmp(force, "large2") == 0)
-        launch_tile<32, 32, 64, 2>(a, P, cap_q, cap_t, norms, s);
-    else
+    else if (force && std::strcmp(force, "k64") == 0)
         launch_tile<32, 32, 64, 1>(a, P, cap_q, cap_t, norms, s);
+    else if (force && std::strcmp(force, "k64d") == 0)
+        launch_tile<32, 32, 64, 2>(a, P, cap_q, cap_t, norms, s);
+    else if (force && std::strcmp(force, "k32d") == 0)
+        launch_tile<32, 32, 32, 2>(a, P, cap_q, cap_t, norms, s);
+    else if (force && std::strcmp(force, "deep") == 0)  // every chunk's loads issued up front
+        launch_tile<32, 32, 32, 1, 8>(a, P, cap_q, cap_t, norms, s);
+    else
+        launch_tile<32, 32, 32, 1>(a, P, cap_q, cap_t, norms, s);
 }
 
 int match_pairs(vs_ctx* ctx, int P, const int* d_pairs, int F, const float* d_desc, const int* d_n, int cap,
                 float ratio, vs_match* d_raw, int* d_nraw, vs_match* d_good, int* d_ngood, hipStream_t s,
                 const float* d_norms) {
-    (void)F;
     if (P <= 0) return VS_OK;
     MatchArgs a{};
     VS_CHECK(match_state(ctx, P, cap, &a.keys, &a.cnt, s));
     ProfScope ps(ctx, "match", s);
+    static const bool pre_norms = std::getenv("VS_MATCH_NORMS") != nullptr;  // experiment: norms first
+    if (!d_norms && pre_norms) {
+        VS_CHECK(ctx->norms_sets.ensure(((size_t)F * cap * sizeof(float) + 255) & ~(size_t)255));
+        VS_CHECK(desc_norms(ctx, F, d_desc, d_n, cap, ctx->norms_sets.as<float>(), s));
+        d_norms = ctx->norms_sets.as<float>();
+    }
     a.pairs = d_pairs;
     a.descq = a.desct = d_desc;
     a.normsq = a.normst = d_norms;

@@ -15,7 +15,17 @@
 // (score desc, raster index asc).  The 400-cap then takes the 400 highest-priority kept pixels:
 // greedy decisions never depend on lower-priority candidates, so the capped greedy output is the
 // top 400 of the uncapped set.
+//
+// Round budget: a fixed number of tile rounds (kNmsRounds launches; each iterates its tile to a
+// local fixed point) settles typical heatmaps; whatever is still undecided afterwards (a dependency
+// chain crossing many tile borders) is finished by k_nms_finish, one workgroup per frame running
+// the same priority-MIS rule over a compact list of the remaining pixels until none is left.  The
+// result is the greedy set for every input; a frame that reaches k_nms_finish's round cap (only an
+// adversarial dependency chain thousands of pixels long can) is reported (count = VS_ERR_NOTCONV
+// on the device paths, VS_ERR_NOTCONV from the host entry points), never a wrong keypoint list.
 #include <hip/hip_runtime.h>
+
+#include <cstdlib>
 
 #include "glibc_expf.h"
 #include "vs_internal.h"
@@ -27,7 +37,8 @@ constexpr int kRadius = 4;             // SP_NMS_RADIUS (Config.h:41)
 constexpr int kMaxKeypoints = 400;     // SP_MAX_KEYPOINTS (Config.h:42)
 constexpr int kNmsTile = 32;
 constexpr int kNmsReg = kNmsTile + 2 * kRadius;
-constexpr int kNmsMaxRounds = 48;
+constexpr int kNmsMaxRounds = 8;          // tile-round launches before k_nms_finish
+constexpr int kFinishMaxRounds = 1 << 14; // k_nms_finish's round cap (VS_NMS_FINISH_ROUNDS overrides)
 
 enum : uint8_t { ST_UNDECIDED = 0, ST_KEPT = 1, ST_OUT = 2 };
 
@@ -174,6 +185,64 @@ __global__ __launch_bounds__(256) void k_nms_round(const float* __restrict__ hea
     if (__syncthreads_or(und) && threadIdx.x == 0) flags[(r + 1) * B + b] = 1;
 }
 
+// Finishes the NMS of frames the tile rounds left undecided (flags[R * B + b] != 0), one workgroup
+// per frame: the frame's undecided pixels are listed once, then each round walks the list, decides
+// what it can with the tile rounds' rule (out if a kept pixel is in the window, kept if no
+// undecided window pixel outranks it), stores the decision at once and compacts the rest into the
+// other list ([B][2][npx] scratch).  Deciding in place is safe for the same reason stale halo reads
+// are: states only move forward and a decided state is final.  Every round decides at least the
+// highest-priority undecided pixel, so the loop ends; max_rounds bounds adversarial dependency
+// chains, ferr[b] = 1 reports hitting it.
+__global__ __launch_bounds__(1024) void k_nms_finish(const float* __restrict__ heat, uint8_t* __restrict__ state,
+                                                     const int* __restrict__ flags, int R, int B, int Hp, int Wp,
+                                                     int* __restrict__ lists, int max_rounds, int* __restrict__ ferr) {
+    const int b = blockIdx.x;
+    if (flags[R * B + b] == 0) return;
+    __shared__ int s_n[2];
+    const int npx = Hp * Wp;
+    const float* hb = heat + (size_t)b * npx;
+    uint8_t* sb = state + (size_t)b * npx;
+    int* lst[2] = {lists + (size_t)b * 2 * npx, lists + (size_t)b * 2 * npx + npx};
+    if (threadIdx.x == 0) s_n[0] = 0;
+    __syncthreads();
+    for (int i = threadIdx.x; i < npx; i += blockDim.x)
+        if (sb[i] == ST_UNDECIDED) lst[0][atomicAdd(&s_n[0], 1)] = i;
+    __syncthreads();
+    int cur = 0;
+    for (int round = 0; round < max_rounds; round++) {
+        const int n = s_n[cur];
+        if (n == 0) return;
+        if (threadIdx.x == 0) s_n[cur ^ 1] = 0;
+        __syncthreads();
+        for (int i = threadIdx.x; i < n; i += blockDim.x) {
+            const int p = lst[cur][i], py = p / Wp, px = p - py * Wp;
+            const unsigned long long key = nms_key(hb[p], (unsigned)p);
+            bool kept_near = false, blocked = false;
+            for (int dy = -kRadius; dy <= kRadius && !kept_near; dy++) {
+                const int y = py + dy;
+                if (y < 0 || y >= Hp) continue;
+                for (int dx = -kRadius; dx <= kRadius; dx++) {
+                    const int x = px + dx;
+                    if (x < 0 || x >= Wp || (dx == 0 && dy == 0)) continue;
+                    const int q = y * Wp + x;
+                    const uint8_t st = sb[q];
+                    if (st == ST_KEPT) {
+                        kept_near = true;
+                        break;
+                    }
+                    if (st == ST_UNDECIDED && nms_key(hb[q], (unsigned)q) > key) blocked = true;
+                }
+            }
+            if (kept_near) sb[p] = ST_OUT;
+            else if (!blocked) sb[p] = ST_KEPT;
+            else lst[cur ^ 1][atomicAdd(&s_n[cur ^ 1], 1)] = p;
+        }
+        __syncthreads();
+        cur ^= 1;
+    }
+    if (threadIdx.x == 0 && s_n[cur] != 0) ferr[b] = 1;
+}
+
 // Kept pixels -> 64-bit priority keys (score bits << 32 | ~raster index), unordered.
 __global__ __launch_bounds__(256) void k_nms_collect(const float* __restrict__ heat, const uint8_t* __restrict__ state,
                                                      int Hp, int Wp, unsigned long long* __restrict__ keys,
@@ -196,8 +265,13 @@ constexpr int kSelSort = 512;
 __global__ __launch_bounds__(1024) void k_nms_select(const unsigned long long* __restrict__ keys,
                                                      const int* __restrict__ keycnt, int key_cap, int max_kp,
                                                      int Wp, int h, int w, vs_keypoint* __restrict__ kps,
-                                                     int cap, int* __restrict__ nout, int* __restrict__ err) {
+                                                     int cap, int* __restrict__ nout, int* __restrict__ err,
+                                                     const int* __restrict__ ferr) {
     const int b = blockIdx.x;
+    if (ferr[b]) {  // NMS not finished: no keypoints, a negative count that every consumer rejects
+        if (threadIdx.x == 0) nout[b] = VS_ERR_NOTCONV;
+        return;
+    }
     __shared__ int hist[256];
     __shared__ unsigned long long s_sel[kSelSort];
     __shared__ int s_nsel;
@@ -359,11 +433,16 @@ int sp_postprocess(vs_ctx* ctx, int B, int hc, int wc, int h, int w, vs_keypoint
     const int max_kp = cap < kMaxKeypoints ? cap : kMaxKeypoints;
     VS_CHECK(ctx->heat.ensure(npx * sizeof(float)));
     VS_CHECK(ctx->state.ensure(npx));
-    VS_CHECK(ctx->flags.ensure(((size_t)(kNmsMaxRounds + 1) * B + 1) * sizeof(int)));
+    // flags: [rounds + 1][B] undecided-after-round, then the capacity word, then ferr [B]
+    VS_CHECK(ctx->flags.ensure(((size_t)(kNmsMaxRounds + 2) * B + 1) * sizeof(int)));
+    VS_CHECK(ctx->nms_list.ensure(npx * 2 * sizeof(int)));
+    const char* fr_env = getenv("VS_NMS_FINISH_ROUNDS");  // test knob: forces the error path
+    const int finish_rounds = fr_env && atoi(fr_env) > 0 ? atoi(fr_env) : kFinishMaxRounds;
     VS_CHECK(ctx->keys.ensure((size_t)B * key_cap * sizeof(unsigned long long)));
     VS_CHECK(ctx->keycnt.ensure((size_t)B * sizeof(int)));
     int* flags = ctx->flags.as<int>();
     int* err = flags + (size_t)(kNmsMaxRounds + 1) * B;
+    int* ferr = err + 1;
     {
         ProfScope ps(ctx, "decode", s);
         int ncell = B * hc * wc;
@@ -373,7 +452,7 @@ int sp_postprocess(vs_ctx* ctx, int B, int hc, int wc, int h, int w, vs_keypoint
     }
     {
         ProfScope ps(ctx, "nms_rounds", s);
-        VS_HIP(hipMemsetAsync(flags, 0, ((size_t)(kNmsMaxRounds + 1) * B + 1) * sizeof(int), s));
+        VS_HIP(hipMemsetAsync(flags, 0, ((size_t)(kNmsMaxRounds + 2) * B + 1) * sizeof(int), s));
         // round 0 runs for every frame
         VS_HIP(hipMemsetAsync(flags, 0x01, (size_t)B * sizeof(int), s));
         const int tiles_x = (Wp + kNmsTile - 1) / kNmsTile, tiles_y = (Hp + kNmsTile - 1) / kNmsTile;
@@ -381,6 +460,8 @@ int sp_postprocess(vs_ctx* ctx, int B, int hc, int wc, int h, int w, vs_keypoint
             hipLaunchKernelGGL(k_nms_round, dim3(tiles_x * tiles_y, B), dim3(256), 0, s, ctx->heat.as<float>(),
                                ctx->state.as<uint8_t>(), flags, r, B, Hp, Wp, tiles_x);
         }
+        hipLaunchKernelGGL(k_nms_finish, dim3(B), dim3(1024), 0, s, ctx->heat.as<float>(), ctx->state.as<uint8_t>(),
+                           flags, kNmsMaxRounds, B, Hp, Wp, ctx->nms_list.as<int>(), finish_rounds, ferr);
         VS_HIP(hipGetLastError());
     }
     {
@@ -389,7 +470,7 @@ int sp_postprocess(vs_ctx* ctx, int B, int hc, int wc, int h, int w, vs_keypoint
         hipLaunchKernelGGL(k_nms_collect, dim3(64, B), dim3(256), 0, s, ctx->heat.as<float>(), ctx->state.as<uint8_t>(),
                            Hp, Wp, ctx->keys.as<unsigned long long>(), ctx->keycnt.as<int>(), key_cap);
         hipLaunchKernelGGL(k_nms_select, dim3(B), dim3(1024), 0, s, ctx->keys.as<unsigned long long>(),
-                           ctx->keycnt.as<int>(), key_cap, max_kp, Wp, h, w, d_kps, cap, d_n, err);
+                           ctx->keycnt.as<int>(), key_cap, max_kp, Wp, h, w, d_kps, cap, d_n, err, ferr);
         VS_HIP(hipGetLastError());
     }
     {
@@ -401,20 +482,21 @@ int sp_postprocess(vs_ctx* ctx, int B, int hc, int wc, int h, int w, vs_keypoint
     return VS_OK;
 }
 
-// Convergence check of the NMS rounds (host-synchronous; used by the host entry points and the
-// tests): returns VS_ERR_NOTCONV when a frame still had undecided pixels after the last round.
+// Completion check of the NMS (host-synchronous; used by the host entry points and the tests):
+// VS_ERR_NOTCONV when k_nms_finish could not complete a frame (list or round cap), VS_ERR_CAPACITY
+// when the packing bound was exceeded (internal error).
 int sp_postprocess_check(vs_ctx* ctx, int B, hipStream_t s) {
     std::vector<int> f(B + 1);
     int* flags = ctx->flags.as<int>();
-    VS_HIP(hipMemcpyAsync(f.data(), flags + (size_t)kNmsMaxRounds * B, B * sizeof(int), hipMemcpyDeviceToHost, s));
-    VS_HIP(hipMemcpyAsync(f.data() + B, flags + (size_t)(kNmsMaxRounds + 1) * B, sizeof(int), hipMemcpyDeviceToHost, s));
+    VS_HIP(hipMemcpyAsync(f.data(), flags + (size_t)(kNmsMaxRounds + 1) * B, (B + 1) * sizeof(int),
+                          hipMemcpyDeviceToHost, s));
     VS_HIP(hipStreamSynchronize(s));
-    for (int b = 0; b < B; b++)
+    for (int b = 1; b <= B; b++)
         if (f[b]) {
-            set_error("NMS did not converge within the round budget");
+            set_error("NMS: a frame reached the finishing pass's round cap");
             return VS_ERR_NOTCONV;
         }
-    if (f[B]) {
+    if (f[0]) {
         set_error("NMS kept more pixels than the packing bound (internal error)");
         return VS_ERR_CAPACITY;
     }

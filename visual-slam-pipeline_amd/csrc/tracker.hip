@@ -455,6 +455,10 @@ struct GpuOps {
         const int* hn = reinterpret_cast<const int*>(hk + (size_t)nb * kCap * sizeof(vs_keypoint));
         for (int b = f0; b < f0 + m; b++) {
             const int n = hn[b];
+            if (n == VS_ERR_NOTCONV) {
+                set_error("vs_slam: NMS could not be completed for a frame");
+                return VS_ERR_NOTCONV;
+            }
             if (n < 0 || n > kCap) {
                 set_error("vs_slam: keypoint count out of range");
                 return VS_ERR_CAPACITY;

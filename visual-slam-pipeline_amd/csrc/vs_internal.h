@@ -89,7 +89,7 @@ struct vs_ctx {
     vs::DevLayer head_a;
 
     // network activations (NHWC fp32) and post-processing scratch, sized per batch
-    vs::DevBuf gray, act0, act1, semi, dgrid, heat, state, flags, keys, keycnt;
+    vs::DevBuf gray, act0, act1, semi, dgrid, heat, state, flags, keys, keycnt, nms_list;
     // host-API staging
     vs::DevBuf h_img, h_kps, h_desc, h_n, h_aux0, h_aux1, h_aux2, h_aux3, h_aux4, h_aux5;
     vs::DevBuf match_keys, match_cnt, norms_sets, tlm, ba, pnp;

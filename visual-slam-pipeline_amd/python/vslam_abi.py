@@ -20,6 +20,8 @@ MATCH_DTYPE = np.dtype([("query_idx", "<i4"), ("train_idx", "<i4"), ("img_idx", 
 assert KEYPOINT_DTYPE.itemsize == 28 and MATCH_DTYPE.itemsize == 16
 
 VS_OK = 0
+VS_ERR_CAPACITY = -5
+VS_ERR_NOTCONV = -6
 ERRORS = {-1: "VS_ERR_ARG", -2: "VS_ERR_HIP", -3: "VS_ERR_NOMEM", -4: "VS_ERR_IO",
           -5: "VS_ERR_CAPACITY", -6: "VS_ERR_NOTCONV"}
 SP_MAX_KEYPOINTS = 400
