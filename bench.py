@@ -94,6 +94,29 @@ def pmc_traffic(kernel, batch):
     return doc["kernels"][kernel]["hbm_bytes_per_launch"], doc.get("tag")
 
 
+def progress(msg):
+    """A line on stderr per phase (a profiled run stays visibly alive; stdout keeps the one JSON line)."""
+    print(f"[bench] {time.strftime('%H:%M:%S')} {msg}", file=sys.stderr, flush=True)
+
+
+def match_roofline(ms_launches, pairs_per_launch, cus, where):
+    """The descriptor matcher (k_match, one launch per call) against the fp32 MFMA peak: 2 n^2 256
+    FLOP per pair at n = 400 keypoints (every synthetic frame reaches SP_MAX_KEYPOINTS), HIP-event
+    time on the stream the kernel runs on.  The peak is scaled to the CUs the launch may use."""
+    if not ms_launches or not ms_launches[1]:
+        return None
+    ms, launches = ms_launches
+    avg_s = ms / 1e3 / launches
+    flops = 2.0 * 400 * 400 * 256 * pairs_per_launch
+    peak = FP32_MFMA_PEAK_TFLOPS * cus / 256
+    ach = flops / avg_s / 1e12
+    return {"where": where, "kernel": "vs::k_match<2, 2, 32, 32, 32, 1, 1, NORMS> (64 x 64 tiles)", "bound": "mfma",
+            "achieved": round(ach, 3), "peak": round(peak, 2), "unit": "TFLOP/s", "frac": round(ach / peak, 4),
+            "cus": cus, "pairs_per_launch": pairs_per_launch, "avg_launch_us": round(avg_s * 1e6, 2),
+            "us_per_pair": round(avg_s * 1e6 / pairs_per_launch, 2), "launches": launches,
+            "flops_per_launch": flops}
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -120,13 +143,26 @@ def cpu_baseline(L, nframes):
     with vslam_abi.Context(0) as ctx:
         weights = ctx.weights()
     S = oracle.Slam()
-    t0 = time.perf_counter()
+    t_ext = t_trk = 0.0
     for g in range(nframes):
+        t0 = time.perf_counter()
         kps, desc = oracle.extract(weights, L["bgr"][g], nthreads=threads)
+        t1 = time.perf_counter()
         S.process(kps, desc, L["depth"][g], T0 + 0.1 * g, 3 * g)
-    dt = time.perf_counter() - t0
+        t_ext += t1 - t0
+        t_trk += time.perf_counter() - t1
+    dt = t_ext + t_trk
+    stages = {k: round(v / nframes * 1e3, 4) for k, v in S.stage_seconds().items()}
     S.close()
-    return {"value": nframes / dt, "unit": "frames/s", "cores": threads, "kind": "port",
+    model = "unknown"
+    try:
+        model = next(ln.split(":", 1)[1].strip() for ln in open("/proc/cpuinfo") if ln.startswith("model name"))
+    except (OSError, StopIteration):
+        pass
+    return {"value": nframes / dt, "unit": "frames/s", "cores": threads, "kind": "port", "cpu_model": model,
+            "ms_per_frame": {"extract": round(t_ext / nframes * 1e3, 3), "track": round(t_trk / nframes * 1e3, 3),
+                             **stages},
+            "full_table": "profiles/r02_cpu_baseline.json (200 frames at 1, 4, 16 threads; tools/cpu_baseline.py)",
             "sample": f"first {nframes} frames of the same synthetic 640x480 RGB-D sequence through the oracle/ "
                       f"CPU restatement (OpenMP fp32 SuperPoint + decode/NMS/sample, then Slam::process_frame with "
                       f"exact 2-NN matching, F-RANSAC, 3D-3D RANSAC / E fallback, EKF, local-map tracking, PnP, "
@@ -162,18 +198,22 @@ def frontend_batch(ctx, L, B, rank, world, steps, warmup):
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    ctx.profile(True)
+    ctx.profile_reset()
     t0 = time.perf_counter()
     run(warmup, steps)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     el = time.perf_counter() - t0
+    prof = ctx.profile_read()
+    ctx.profile(False)
     if world > 1:
         tt = torch.tensor([el], dtype=torch.float64, device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         el = float(tt.item())
     return {"value": round(world * B * steps / el, 3), "unit": "frames/s", "ms_per_step": round(el / steps * 1e3, 3),
-            "steps": steps, "frames_per_gpu_per_step": B,
+            "_match": prof.get("match"), "steps": steps, "frames_per_gpu_per_step": B,
             "workload": "config[3] offline batch: per-GPU SuperPoint extract + ratio matching + F-RANSAC + 3D-3D "
                         "RANSAC (E fallback) over consecutive frame pairs, no tracking state",
             "parallelism": f"frame-sharded x{world}" + (" + RCCL all-gather of feature records" if world > 1 else "")}
@@ -286,6 +326,7 @@ def main():
         return slam.process_batch_dev(B, bgr[i0].data_ptr(), dep[i0].data_ptr(), hdep[i0:i0 + B],
                                       [T0 + 0.1 * (g0 + j) for j in range(B)], [3 * (g0 + j) for j in range(B)])
 
+    progress(f"sequence rendered, tracker ready; {args.warmup} warmup steps")
     torch.cuda.synchronize()
     for k in range(args.warmup):
         step(k)
@@ -304,6 +345,7 @@ def main():
     elapsed = time.perf_counter() - t0
     prof = ctx.profile_read()
     ctx.profile(False)
+    progress(f"timed region done: {args.steps} steps in {elapsed:.2f} s")
     if world > 1:
         tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
@@ -339,17 +381,26 @@ def main():
     if traffic is not None:  # PMC pass at B frames per launch -> bytes per average launch here
         traffic = traffic / B * frames_per_launch
 
+    track_cus = int(os.environ.get("VS_SLAM_TRACK_CUS", "32"))
+    mroof = {"tracker": match_roofline(prof.get("match"), 1, track_cus,
+                                       "tracking loop: one pair (frame vs reference keyframe) per launch on the "
+                                       f"tracker's {track_cus}-CU stream (overlapped with extraction on the rest)")}
     fe = None
+    progress("config[3] batch front end")
     if not args.no_frontend and args.frontend_steps > 0:
         fe = frontend_batch(ctx, L, B, rank, world, args.frontend_steps, 2)
+        mroof["frontend_batch"] = match_roofline(fe.pop("_match"), B, 256,
+                                                 f"config[3] batch front end: {B} consecutive pairs per launch, whole chip")
 
     mono = None
+    progress("config[4] monocular HD stream")
     if args.mono_steps > 0:
         mono = monocular_hd(ctx, B, rank, world, args.mono_steps, 1, workers)
 
     if rank == 0:
         cpu = None
         if not args.no_cpu_baseline and world == 1:
+            progress("cpu baseline")
             cpu = cpu_baseline(L, args.cpu_frames)
         result = {
             "metric": METRIC,
@@ -395,6 +446,7 @@ def main():
                 "note": "network on the extraction stream's CU set (all CUs but VS_SLAM_TRACK_CUS = 32), "
                         "overlapped with tracking; peak is the whole chip's",
             },
+            "match_roofline": mroof,
             "network_tflops": round(net_flops / (net_ms / 1e3) / 1e12, 3),
             "stage_ms_per_frame": stage_ms,
             "frontend_batch": fe,

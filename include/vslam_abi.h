@@ -317,6 +317,34 @@ int vs_slam_stats(vs_slam* slam, int* out, int cap);
  * bytes are written (each nullable). */
 int vs_slam_map(vs_slam* slam, int cap, double* pos, uint8_t* valid, int* n);
 
+/* ---- F2: the SPCF feature cache as the batch interchange (FeatureExtractor.cpp:261-381) ---
+ * Byte layout of the reference's save_cache / load_cache: u32 magic 0x53504346 ("SPCF"),
+ * u32 version 1, u32 entry count, then per entry i32 frame_idx, i32 num_kp, num_kp x 28-B
+ * keypoint records (x, y, size, angle, response f32, octave, class_id i32 == vs_keypoint),
+ * i32 rows, cols, type (CV_32F = 5; 0, 0, 0 for an empty cv::Mat) and rows x cols fp32
+ * descriptors.  The reference keys entries by the sequential extract-call index
+ * (FeatureExtractor.cpp:52-61) and writes them sorted by it. */
+
+/* Writes F frames (host buffers kps [F][cap], desc [F][cap][256], n [F]) as entries frame_idx[f].
+ * append == 0 creates the file; append != 0 adds the entries to an existing file (header count
+ * updated; a missing file is created).  A frame with n == 0 is written as the reference writes an
+ * empty extraction (rows = cols = type = 0).  n[f] < 0 or > cap: VS_ERR_ARG. */
+int vs_spcf_write(const char* path, int F, const int* frame_idx, const vs_keypoint* kps, const float* desc,
+                  const int* n, int cap, int append);
+
+/* The same from device buffers (vs_extract_batch_dev's outputs): copied on `stream`, then
+ * written (synchronous). */
+int vs_spcf_write_dev(vs_ctx* ctx, const char* path, int F, const int* frame_idx, const vs_keypoint* d_kps,
+                      const float* d_desc, const int* d_n, int cap, int append, void* stream);
+
+/* Reads an SPCF file.  *count = number of distinct frame indices (a repeated index keeps its last
+ * entry, as the reference's map assignment does).  With non-null buffers (max_frames entries of
+ * kps [cap], desc [cap][256]) the entries are returned sorted by frame index.  Bad magic / version,
+ * a truncated file or a non-CV_32F / non-256-column descriptor matrix: VS_ERR_IO; more entries than
+ * max_frames or keypoints than cap: VS_ERR_CAPACITY. */
+int vs_spcf_read(const char* path, int max_frames, int cap, int* frame_idx, vs_keypoint* kps, float* desc, int* n,
+                 int* count);
+
 /* ---- profiling ----------------------------------------------------------------------- */
 /* When enabled, every stage of the _dev pipelines brackets its launches with hipEvents on the
  * stream it runs on; vs_profile_read returns per-stage accumulated milliseconds and launch

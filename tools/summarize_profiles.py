@@ -6,6 +6,10 @@
                                     "HBM": FETCH_SIZE counts half the bytes of a 16-B/lane streaming
                                     read (x2); WRITE_SIZE is exact for 16-B/lane stores.
   profiles/pmc_traffic.json         copy of the latest traffic file (read by bench.py)
+  profiles/<tag>_mfma_util.json     per-kernel matrix-core utilisation from the MFMA passes:
+                                    SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x GRBM_GUI_ACTIVE / 8)
+                                    (GRBM_GUI_ACTIVE is summed over the 8 XCDs; MI355X_MICROARCH.md)
+  profiles/<tag>_match_kernel_stats.csv  kernel trace of tools/bench_match.py (1, 32, 512 pairs)
 
 usage: python tools/summarize_profiles.py r01 [batch]
 """
@@ -35,6 +39,33 @@ def per_kernel(path, counter):
     return {k: sum(v) / len(v) for k, v in agg.items()}
 
 
+def per_dispatch(path):
+    """{dispatch: (kernel, grid/wg, {counter: value})} from a --pmc csv (values summed per dispatch)."""
+    out = {}
+    for r in csv.DictReader(open(path)):
+        d = r["Dispatch_Id"]
+        k, cs = out.setdefault(d, (short(r["Kernel_Name"]), {}))[:2]
+        cs[r["Counter_Name"]] = cs.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
+    return out
+
+
+def mfma_util(path, label):
+    agg = collections.defaultdict(lambda: collections.defaultdict(list))
+    for d, (k, cs) in per_dispatch(path).items():
+        for cn, v in cs.items():
+            agg[k][cn].append(v)
+    res = {}
+    for k, cs in agg.items():
+        busy = sum(cs["SQ_VALU_MFMA_BUSY_CYCLES"]) / len(cs["SQ_VALU_MFMA_BUSY_CYCLES"])
+        gui = sum(cs["GRBM_GUI_ACTIVE"]) / len(cs["GRBM_GUI_ACTIVE"])
+        if busy <= 0 or gui <= 0:
+            continue
+        res[k] = {"source": label, "dispatches": len(cs["GRBM_GUI_ACTIVE"]), "mfma_busy_cycles": busy,
+                  "grbm_gui_active": gui, "sq_busy_cycles": sum(cs.get("SQ_BUSY_CYCLES", [0])) / len(cs["GRBM_GUI_ACTIVE"]),
+                  "mfma_util": busy / (1024.0 * gui / 8.0)}
+    return res
+
+
 def main():
     tag = sys.argv[1]
     batch = int(sys.argv[2]) if len(sys.argv) > 2 else 32
@@ -58,6 +89,20 @@ def main():
     with open(os.path.join(PROF, f"{tag}_pmc_traffic.json"), "w") as fh:
         json.dump(doc, fh, indent=1)
     shutil.copy(os.path.join(PROF, f"{tag}_pmc_traffic.json"), os.path.join(PROF, "pmc_traffic.json"))
+    util = {}
+    for sub, name, label in (("prof_mfma", "mfma", "bench.py"), ("prof_match_mfma", "match_mfma", "tools/bench_match.py")):
+        path = os.path.join(OUT, sub, f"{name}_counter_collection.csv")
+        if os.path.exists(path):
+            util.update(mfma_util(path, label))
+    if util:
+        with open(os.path.join(PROF, f"{tag}_mfma_util.json"), "w") as fh:
+            json.dump({"tag": tag, "formula": "SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x GRBM_GUI_ACTIVE / 8)",
+                       "kernels": util}, fh, indent=1)
+        for k, v in sorted(util.items(), key=lambda kv: -kv[1]["mfma_busy_cycles"])[:8]:
+            print(f"{k:40s} mfma util {v['mfma_util']:.3f} ({v['source']})")
+    mt = os.path.join(OUT, "prof_match", "match_kernel_stats.csv")
+    if os.path.exists(mt):
+        shutil.copy(mt, os.path.join(PROF, f"{tag}_match_kernel_stats.csv"))
     top = sorted(kernels.items(), key=lambda kv: -(kv[1]["avg_ns"] or 0))[:8]
     for k, v in top:
         print(f"{k:40s} avg {v['avg_ns'] or 0:12.0f} ns  hbm {v['hbm_bytes_per_launch'] / 1e9:8.3f} GB")

@@ -108,19 +108,27 @@ struct MatchArgs {
     int ostride;
 };
 
-template <int WQ, int WT, int KC, int NBUF, int PD, bool NORMS>
-__global__ __launch_bounds__(256) void k_match(MatchArgs a) {
-    constexpr int TQ = 2 * WQ, TT = 2 * WT, R = TQ + TT;
+// Workgroup = NWQ x NWT waves, each owning WQ queries x WT train rows (FQ x FT 16 x 16 MFMA
+// chains), so a workgroup covers TQ = NWQ WQ queries x TT = NWT WT train rows.
+// ABL: phase ablation for latency studies (VS_MATCH_ABLATE; results are not matches): 0 = the
+// product kernel, 1 = stop after the k-loop, 2 = no MFMAs in the k-loop, 3 = stop after the
+// prologue's first chunk.
+template <int NWQ, int NWT, int WQ, int WT, int KC, int NBUF, int PD, bool NORMS, int ABL = 0>
+__global__ __launch_bounds__(64 * NWQ * NWT) void k_match(MatchArgs a) {
+    constexpr int NW = NWQ * NWT, NTH = 64 * NW;
+    constexpr int TQ = NWQ * WQ, TT = NWT * WT, R = TQ + TT;
     constexpr int FQ = WQ / 16, FT = WT / 16;
     constexpr int NC = 256 / KC;           // staged chunks
     constexpr int NB = NC > 1 ? NBUF : 1;  // LDS buffers (1: a second barrier per chunk, half the LDS)
-    constexpr int RS4 = KC / 4 + 2;        // row stride in float4: KC + 8 floats = 8 mod 64 dwords
+    constexpr int RS4 = KC / 4 + 2;        // row stride in float4 (KC + 8 floats)
     constexpr int GR = KC / 16;            // 16-k groups per row and chunk
-    constexpr int GPT = R * GR / 256;      // groups per thread and chunk
-    constexpr int NR = R / 4;              // norm rows per wave
+    constexpr int GPT = R * GR / NTH;      // groups per thread and chunk
+    constexpr int NR = R / NW;             // norm rows per wave
+    static_assert(GPT * NTH == R * GR && NR * NW == R && NR <= 64, "staging / norm split");
     __shared__ float4 sbuf[NB][R * RS4];
     __shared__ float s_norm[R];
-    __shared__ int s_wave[4];
+    __shared__ unsigned long long s_top[NWT > 1 ? NWT : 1][TQ][2];
+    __shared__ int s_wave[NW];
     __shared__ int s_last, s_base;
 
     // linear work index: XCD x (= blockIdx % 8 under round-robin placement) takes a contiguous range
@@ -145,22 +153,20 @@ __global__ __launch_bounds__(256) void k_match(MatchArgs a) {
     const float* Q = a.descq + (size_t)qf * a.qstride * 256;
     const float* T = a.desct + (size_t)tf * a.tstride * 256;
 
-    // staging: group G = tid + 256 u -> LDS row G / GR, 16 consecutive k at (G % GR) * 16 of the chunk.
-    // Rows past n1 / n2 re-read the last valid row (their results are never used), so every load
-    // is unconditional and the compiler keeps all of them in flight together.
+    // staging: group G = tid + NTH u -> LDS row G / GR, 16 consecutive k at (G % GR) * 16 of the
+    // chunk.  Rows past n1 / n2 re-read the last valid row (their results are never used), so every
+    // load is unconditional and the compiler keeps all of them in flight together.
     const float4* src[GPT];
 #pragma unroll
     for (int u = 0; u < GPT; u++) {
-        const int G = tid + 256 * u, row = G / GR, q4 = G % GR;
+        const int G = tid + NTH * u, row = G / GR, q4 = G % GR;
         const float* base = row < TQ ? Q + (size_t)min(q0 + row, n1 - 1) * 256
                                      : T + (size_t)min(t0 + row - TQ, n2 - 1) * 256;
         src[u] = reinterpret_cast<const float4*>(base) + 4 * q4;
     }
     // PD chunks in flight in registers (slot c % PD holds chunk c): PD = 1 overlaps one chunk's
-    // loads with the previous chunk's MFMAs (throughput shape, many workgroups per CU); PD = NC
-    // issues every load of the tile up front, so a lone workgroup pays one memory latency instead
-    // of one per chunk (latency shape: a single pair on the tracker's CU set).
-    // (compile-time chunk indices throughout — static_for — so the ring stays in registers)
+    // loads with the previous chunk's MFMAs; PD = NC issues every load of the tile up front
+    // (compile-time chunk indices throughout — static_for — so the ring stays in registers).
     float4 reg[PD][GPT][4];
     auto load = [&](auto cc) {
         constexpr int c = decltype(cc)::value;
@@ -175,7 +181,7 @@ __global__ __launch_bounds__(256) void k_match(MatchArgs a) {
         const float4(&r)[GPT][4] = reg[c % PD];
 #pragma unroll
         for (int u = 0; u < GPT; u++) {
-            const int G = tid + 256 * u, row = G / GR, q4 = G % GR;
+            const int G = tid + NTH * u, row = G / GR, q4 = G % GR;
             float4* d = &sbuf[buf][row * RS4 + 4 * q4];
             d[0] = make_float4(r[u][0].x, r[u][1].x, r[u][2].x, r[u][3].x);
             d[1] = make_float4(r[u][0].y, r[u][1].y, r[u][2].y, r[u][3].y);
@@ -185,7 +191,7 @@ __global__ __launch_bounds__(256) void k_match(MatchArgs a) {
     };
 
     const int wv = tid >> 6, lane = tid & 63, li = lane & 15, lg = lane >> 4;
-    const int wq = wv & 1, wt = wv >> 1;
+    const int wq = wv % NWQ, wt = wv / NWQ;
     const int qrow0 = wq * WQ, trow0 = TQ + wt * WT;  // LDS rows of this wave's fragments
     // fragments entirely past n1 / n2 are not computed (wave-uniform)
     bool vq[FQ], vt[FT];
@@ -216,6 +222,10 @@ __global__ __launch_bounds__(256) void k_match(MatchArgs a) {
     store(std::integral_constant<int, 0>{}, 0);
     if (NORMS && tid < R) s_norm[tid] = cnorm;
     __syncthreads();
+    if constexpr (ABL == 3) {
+        if (sbuf[0][tid].x == 1234.5f) a.raw[0].distance = sbuf[0][tid].y;
+        return;
+    }
     static_for<0, NC>([&](auto cc) {  // unrolled: no loop-carried copies of the prefetch registers
         constexpr int c = decltype(cc)::value;
         const int buf = NB > 1 ? (c & 1) : 0;
@@ -232,7 +242,12 @@ __global__ __launch_bounds__(256) void k_match(MatchArgs a) {
 #pragma unroll
             for (int y = 0; y < FQ; y++) fb[y] = sb[(qrow0 + 16 * y + li) * RS4 + 4 * qd + lg];
             // all fragments valid (every interior workgroup): straight-line MFMAs; else per-fragment
-            if (full) {
+            if constexpr (ABL == 2) {
+#pragma unroll
+                for (int x = 0; x < FT; x++)
+#pragma unroll
+                    for (int y = 0; y < FQ; y++) acc[x][y][0] += fa[x][0] * fb[y][0];
+            } else if (full) {
 #pragma unroll
                 for (int j = 0; j < 4; j++)
 #pragma unroll
@@ -273,9 +288,20 @@ __global__ __launch_bounds__(256) void k_match(MatchArgs a) {
         }
         __syncthreads();
     });
+    if constexpr (ABL == 1) {
+        float t = 0.0f;
+#pragma unroll
+        for (int x = 0; x < FT; x++)
+#pragma unroll
+            for (int y = 0; y < FQ; y++) t += acc[x][y][0] + acc[x][y][1] + acc[x][y][2] + acc[x][y][3];
+        if (t == 1234.5f) a.raw[0].distance = t;
+        return;
+    }
 
-    // ---- per-wave top-2 per query: D[train 4 lg + e][query li] of each 16 x 16 fragment ----
-    unsigned long long mine0 = kNoKey, mine1 = kNoKey;  // the fragment this lane group publishes
+    // ---- per-wave top-2 per query over the wave's WT train rows: D[train 4 lg + e][query li] of
+    // each 16 x 16 fragment, merged over e, x and (shuffles) the lane groups; NWT > 1 merges the
+    // waves of a query block through LDS ----
+    unsigned long long w0[FQ], w1[FQ];
 #pragma unroll
     for (int y = 0; y < FQ; y++) {
         const float na = s_norm[qrow0 + 16 * y + li];
@@ -299,18 +325,59 @@ __global__ __launch_bounds__(256) void k_match(MatchArgs a) {
             k0 = lo;
             k1 = hi < m1 ? hi : m1;
         }
-        if (lg == y) {
+        w0[y] = k0;
+        w1[y] = k1;
+    }
+    unsigned long long mine0 = kNoKey, mine1 = kNoKey;  // the query this thread publishes
+    int ql = -1;                                        // its row within the query block
+    if constexpr (NWT == 1) {
+        // lane group lg publishes fragments y = lg, lg + 4, ... (one query per lane and pass)
+#pragma unroll
+        for (int y = 0; y < FQ; y++)
+            if ((y & 3) == lg && y < 4) {
+                mine0 = w0[y];
+                mine1 = w1[y];
+                ql = qrow0 + 16 * y + li;
+            }
+    } else {
+        if (lg == 0) {
+#pragma unroll
+            for (int y = 0; y < FQ; y++) {
+                s_top[wt][qrow0 + 16 * y + li][0] = w0[y];
+                s_top[wt][qrow0 + 16 * y + li][1] = w1[y];
+            }
+        }
+        __syncthreads();
+        if (tid < TQ) {
+            unsigned long long k0 = s_top[0][tid][0], k1 = s_top[0][tid][1];
+#pragma unroll
+            for (int w = 1; w < NWT; w++) {
+                const unsigned long long o0 = s_top[w][tid][0], o1 = s_top[w][tid][1];
+                const unsigned long long lo = k0 < o0 ? k0 : o0, hi = k0 < o0 ? o0 : k0;
+                const unsigned long long m1 = k1 < o1 ? k1 : o1;
+                k0 = lo;
+                k1 = hi < m1 ? hi : m1;
+            }
             mine0 = k0;
             mine1 = k1;
+            ql = tid;
         }
     }
-    const int qi = q0 + qrow0 + 16 * lg + li;
     unsigned long long* B0 = a.keys + (size_t)p * 2 * a.kcap;
     unsigned long long* B1 = B0 + a.kcap;
-    if (lg < FQ && qi < n1 && mine0 != kNoKey) {
-        if (mine1 != kNoKey) atomicMin(B1 + qi, mine1);
-        const unsigned long long old = atomicMin(B0 + qi, mine0);
-        atomicMin(B1 + qi, old > mine0 ? old : mine0);
+    auto publish = [&](int qloc, unsigned long long m0, unsigned long long m1) {
+        const int qi = q0 + qloc;
+        if (qloc >= 0 && qi < n1 && m0 != kNoKey) {
+            if (m1 != kNoKey) atomicMin(B1 + qi, m1);
+            const unsigned long long old = atomicMin(B0 + qi, m0);
+            atomicMin(B1 + qi, old > m0 ? old : m0);
+        }
+    };
+    publish(ql, mine0, mine1);
+    if constexpr (NWT == 1 && FQ > 4) {  // fragments 4.. (one more pass)
+#pragma unroll
+        for (int y = 4; y < FQ; y++)
+            if ((y & 3) == lg) publish(qrow0 + 16 * y + li, w0[y], w1[y]);
     }
     // every atomic of this workgroup has been performed (acknowledged) before it arrives
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -327,7 +394,7 @@ __global__ __launch_bounds__(256) void k_match(MatchArgs a) {
     __syncthreads();
     vs_match* raw = a.raw + (size_t)p * a.ostride;
     vs_match* good = a.good + (size_t)p * a.ostride;
-    for (int c0 = 0; c0 < n1; c0 += 256) {
+    for (int c0 = 0; c0 < n1; c0 += NTH) {
         const int i = c0 + tid;
         bool f = false;
         vs_match m;
@@ -350,7 +417,11 @@ __global__ __launch_bounds__(256) void k_match(MatchArgs a) {
         for (int k = 0; k < wv; k++) off += s_wave[k];
         if (f) good[off + before] = m;
         __syncthreads();
-        if (tid == 0) s_base += s_wave[0] + s_wave[1] + s_wave[2] + s_wave[3];
+        if (tid == 0) {
+            int tot = 0;
+            for (int k = 0; k < NW; k++) tot += s_wave[k];
+            s_base += tot;
+        }
         __syncthreads();
     }
     if (tid == 0) {
@@ -389,41 +460,52 @@ static int match_state(vs_ctx* ctx, int P, int kcap, unsigned long long** keys, 
     return VS_OK;
 }
 
-template <int WQ, int WT, int KC, int NBUF, int PD = 1>
+template <int NWQ, int NWT, int WQ, int WT, int KC, int NBUF, int PD = 1>
 static void launch_tile(MatchArgs& a, int P, int cap_q, int cap_t, bool norms, hipStream_t s) {
-    a.qblocks = (cap_q + 2 * WQ - 1) / (2 * WQ);
-    a.tblocks = (cap_t + 2 * WT - 1) / (2 * WT);
+    constexpr int TQ = NWQ * WQ, TT = NWT * WT, NTH = 64 * NWQ * NWT;
+    a.qblocks = (cap_q + TQ - 1) / TQ;
+    a.tblocks = (cap_t + TT - 1) / TT;
     a.work = P * a.qblocks * a.tblocks;
     a.per_xcd = (a.work + 7) / 8;
     const unsigned blocks = (unsigned)(8 * a.per_xcd);
+    static const char* abl = std::getenv("VS_MATCH_ABLATE");  // latency study only
+    if (abl && PD == 1) {
+        const int m = std::atoi(abl);
+        if (m == 1) hipLaunchKernelGGL((k_match<NWQ, NWT, WQ, WT, KC, NBUF, PD, false, 1>), dim3(blocks), dim3(NTH), 0, s, a);
+        if (m == 2) hipLaunchKernelGGL((k_match<NWQ, NWT, WQ, WT, KC, NBUF, PD, false, 2>), dim3(blocks), dim3(NTH), 0, s, a);
+        if (m == 3) hipLaunchKernelGGL((k_match<NWQ, NWT, WQ, WT, KC, NBUF, PD, false, 3>), dim3(blocks), dim3(NTH), 0, s, a);
+        if (m >= 1 && m <= 3) return;
+    }
     if (norms)
-        hipLaunchKernelGGL((k_match<WQ, WT, KC, NBUF, PD, true>), dim3(blocks), dim3(256), 0, s, a);
+        hipLaunchKernelGGL((k_match<NWQ, NWT, WQ, WT, KC, NBUF, PD, true>), dim3(blocks), dim3(NTH), 0, s, a);
     else
-        hipLaunchKernelGGL((k_match<WQ, WT, KC, NBUF, PD, false>), dim3(blocks), dim3(256), 0, s, a);
+        hipLaunchKernelGGL((k_match<NWQ, NWT, WQ, WT, KC, NBUF, PD, false>), dim3(blocks), dim3(NTH), 0, s, a);
 }
 
-// Tile: 64 x 64 workgroups (4 chains per wave, k staged in 32-wide chunks through one LDS buffer:
-// 21 KB, seven waves per SIMD).  Measured (profiles/r02_match_variants.jsonl, r02 sweep) against
-// 32 x 32 workgroups with all of k loaded at once (one 16 x 16 chain per wave), 64-wide chunks
-// (37 KB, four workgroups per CU) and two LDS buffers of either width: the 32-wide single buffer is
-// the fastest from 8 pairs up (54 % of the fp32 MFMA peak at 512 pairs, 35 % at 32) and ties at one
-// pair.  Issuing all eight chunks' loads up front (PD = 8) does not shorten a lone pair (19.2 vs
-// 18.5 us per launch, r02 sweep): the single-pair time is not the per-chunk load latency.
-// VS_MATCH_TILE = small | k64 | k64d | k32d | deep selects the others (experiments).
+// Tile (r02 sweeps, profiles/r02_match_variants.jsonl): 64 x 64 workgroups of 2 x 2 waves, each
+// wave 32 x 32 (four 16 x 16 chains), k staged in 32-wide chunks through one LDS buffer (23 KB,
+// seven waves per SIMD).  Fragments wholly past n are skipped, so 400 keypoints cost no padded
+// MFMA work.  Measured against: all of k in LDS at once (32 x 32 workgroups), 64-wide chunks,
+// double buffering, every chunk's loads issued up front (PD = 8: no faster at one pair, so the
+// lone-pair time is not per-chunk load latency), and 80 x 80 workgroups of five waves (no padding
+// and 5 instead of 7 stagings per row, but five waves on four SIMDs: 13-16 % slower).
+// VS_MATCH_TILE = small | k64 | k64d | k32d | deep | t80 selects those (experiments).
 static void launch(MatchArgs& a, int P, int cap_q, int cap_t, bool norms, hipStream_t s) {
     static const char* force = std::getenv("VS_MATCH_TILE");
     if (force && std::strcmp(force, "small") == 0)
-        launch_tile<16, 16, 256, 1>(a, P, cap_q, cap_t, norms, s);
+        launch_tile<2, 2, 16, 16, 256, 1>(a, P, cap_q, cap_t, norms, s);
     else if (force && std::strcmp(force, "k64") == 0)
-        launch_tile<32, 32, 64, 1>(a, P, cap_q, cap_t, norms, s);
+        launch_tile<2, 2, 32, 32, 64, 1>(a, P, cap_q, cap_t, norms, s);
     else if (force && std::strcmp(force, "k64d") == 0)
-        launch_tile<32, 32, 64, 2>(a, P, cap_q, cap_t, norms, s);
+        launch_tile<2, 2, 32, 32, 64, 2>(a, P, cap_q, cap_t, norms, s);
     else if (force && std::strcmp(force, "k32d") == 0)
-        launch_tile<32, 32, 32, 2>(a, P, cap_q, cap_t, norms, s);
-    else if (force && std::strcmp(force, "deep") == 0)  // every chunk's loads issued up front
-        launch_tile<32, 32, 32, 1, 8>(a, P, cap_q, cap_t, norms, s);
+        launch_tile<2, 2, 32, 32, 32, 2>(a, P, cap_q, cap_t, norms, s);
+    else if (force && std::strcmp(force, "deep") == 0)
+        launch_tile<2, 2, 32, 32, 32, 1, 8>(a, P, cap_q, cap_t, norms, s);
+    else if (force && std::strcmp(force, "t80") == 0)
+        launch_tile<5, 1, 16, 80, 32, 1>(a, P, cap_q, cap_t, norms, s);
     else
-        launch_tile<32, 32, 32, 1>(a, P, cap_q, cap_t, norms, s);
+        launch_tile<2, 2, 32, 32, 32, 1>(a, P, cap_q, cap_t, norms, s);
 }
 
 int match_pairs(vs_ctx* ctx, int P, const int* d_pairs, int F, const float* d_desc, const int* d_n, int cap,

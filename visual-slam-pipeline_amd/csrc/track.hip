@@ -228,6 +228,8 @@ struct TlmResolveShared {
     int wcnt[16];
     int nobs, nc, total;
 };
+// ~132 KB: one workgroup per CU within gfx950's 160 KB of LDS (this kernel is written for gfx950 only)
+static_assert(sizeof(TlmResolveShared) <= 160 * 1024, "k_tlm_resolve's shared state exceeds gfx950's 160 KB LDS");
 
 // One pass over the nc buffered candidates (map-point order): winners are strictly below the
 // carried minimum and below every earlier buffered candidate of the keypoint (a keypoint's

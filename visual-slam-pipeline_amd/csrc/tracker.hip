@@ -681,7 +681,10 @@ struct GpuOps {
         HostTimer ht(hprof, kHPnp);
         if (spec_valid) {  // the speculative run had exactly these inputs: its result is this call's
             spec_valid = false;
-            if (iters == 100 && min_inliers == 10 && obj == spec_obj && img == spec_img) return spec;
+            const auto same = [](const std::vector<float>& a, const std::vector<float>& b) {  // bit-exact
+                return a.size() == b.size() && std::memcmp(a.data(), b.data(), a.size() * sizeof(float)) == 0;
+            };
+            if (iters == 100 && min_inliers == 10 && same(obj, spec_obj) && same(img, spec_img)) return spec;
         }
         vs_trk::PnPResult r;
         const int n = (int)(obj.size() / 3);

@@ -4,7 +4,6 @@
 
 #include <algorithm>
 #include <cstring>
-#include <fstream>
 
 #include "vslam_abi.h"
 
@@ -73,39 +72,27 @@ void FeatureExtractor::extract(const Image& image, std::vector<KeyPoint>& keypoi
     if (!cache_path_.empty()) cache_[idx] = CachedFeatures{keypoints, descriptors};
 }
 
-// SPCF cache file (FeatureExtractor.cpp:261-360): "SPCF" magic, version 1, entry count, then per
-// entry frame index, keypoint count, 7 x 4-byte keypoint fields, rows / cols / type (CV_32F = 5)
-// and the raw descriptor rows.
+// SPCF cache file (FeatureExtractor.cpp:261-381) through the library's reader / writer
+// (vs_spcf_read / vs_spcf_write: the reference's byte layout, entries sorted by index).
 bool FeatureExtractor::load_cache() {
     if (cache_path_.empty()) return false;
-    std::ifstream ifs(cache_path_, std::ios::binary);
-    if (!ifs.is_open()) return false;
-    uint32_t magic = 0, version = 0, num_entries = 0;
-    ifs.read(reinterpret_cast<char*>(&magic), 4);
-    ifs.read(reinterpret_cast<char*>(&version), 4);
-    ifs.read(reinterpret_cast<char*>(&num_entries), 4);
-    if (!ifs || magic != 0x53504346u || version != 1) return false;
+    int count = 0;
+    if (vs_spcf_read(cache_path_.c_str(), 0, 0, nullptr, nullptr, nullptr, nullptr, &count) != VS_OK) return false;
+    const int cap = VS_SP_MAX_KEYPOINTS;
+    std::vector<int> idx(count), n(count);
+    std::vector<KeyPoint> kps((size_t)count * cap);
+    std::vector<float> desc((size_t)count * cap * Descriptors::kCols);
+    if (count > 0 && vs_spcf_read(cache_path_.c_str(), count, cap, idx.data(), reinterpret_cast<vs_keypoint*>(kps.data()),
+                                  desc.data(), n.data(), &count) != VS_OK)
+        return false;
     std::unordered_map<int, CachedFeatures> cache;
-    for (uint32_t e = 0; e < num_entries; e++) {
-        int32_t frame_idx = 0, num_kp = 0, rows = 0, cols = 0, type = 0;
-        ifs.read(reinterpret_cast<char*>(&frame_idx), 4);
-        ifs.read(reinterpret_cast<char*>(&num_kp), 4);
-        if (!ifs || num_kp < 0) return false;
+    for (int e = 0; e < count; e++) {
         CachedFeatures cf;
-        cf.keypoints.resize(num_kp);
-        ifs.read(reinterpret_cast<char*>(cf.keypoints.data()), (std::streamsize)num_kp * sizeof(KeyPoint));
-        ifs.read(reinterpret_cast<char*>(&rows), 4);
-        ifs.read(reinterpret_cast<char*>(&cols), 4);
-        ifs.read(reinterpret_cast<char*>(&type), 4);
-        if (!ifs) return false;
-        if (rows > 0 && cols > 0) {
-            if (cols != Descriptors::kCols || type != 5) return false;  // SuperPoint CV_32F rows
-            cf.descriptors.rows = rows;
-            cf.descriptors.data.resize((size_t)rows * cols);
-            ifs.read(reinterpret_cast<char*>(cf.descriptors.data.data()), (std::streamsize)rows * cols * 4);
-            if (!ifs) return false;
-        }
-        cache[frame_idx] = std::move(cf);
+        cf.keypoints.assign(kps.begin() + (size_t)e * cap, kps.begin() + (size_t)e * cap + n[e]);
+        cf.descriptors.rows = n[e];
+        cf.descriptors.data.assign(desc.begin() + (size_t)e * cap * Descriptors::kCols,
+                                   desc.begin() + ((size_t)e * cap + n[e]) * Descriptors::kCols);
+        cache[idx[e]] = std::move(cf);
     }
     cache_ = std::move(cache);
     cache_loaded_ = true;
@@ -114,30 +101,21 @@ bool FeatureExtractor::load_cache() {
 
 bool FeatureExtractor::save_cache() {
     if (cache_path_.empty() || cache_.empty()) return false;
-    std::ofstream ofs(cache_path_, std::ios::binary);
-    if (!ofs.is_open()) return false;
-    const uint32_t magic = 0x53504346u, version = 1, num_entries = (uint32_t)cache_.size();
-    ofs.write(reinterpret_cast<const char*>(&magic), 4);
-    ofs.write(reinterpret_cast<const char*>(&version), 4);
-    ofs.write(reinterpret_cast<const char*>(&num_entries), 4);
     std::vector<int> indices;
     indices.reserve(cache_.size());
     for (const auto& kv : cache_) indices.push_back(kv.first);
     std::sort(indices.begin(), indices.end());
-    for (int idx : indices) {
+    bool first = true;
+    for (int idx : indices) {  // one entry at a time: no second copy of the whole cache
         const CachedFeatures& cf = cache_.at(idx);
-        const int32_t frame_idx = idx, num_kp = (int32_t)cf.keypoints.size();
-        ofs.write(reinterpret_cast<const char*>(&frame_idx), 4);
-        ofs.write(reinterpret_cast<const char*>(&num_kp), 4);
-        ofs.write(reinterpret_cast<const char*>(cf.keypoints.data()), (std::streamsize)num_kp * sizeof(KeyPoint));
-        const int32_t rows = cf.descriptors.rows, cols = rows > 0 ? Descriptors::kCols : 0, type = rows > 0 ? 5 : 0;
-        ofs.write(reinterpret_cast<const char*>(&rows), 4);
-        ofs.write(reinterpret_cast<const char*>(&cols), 4);
-        ofs.write(reinterpret_cast<const char*>(&type), 4);
-        if (rows > 0)
-            ofs.write(reinterpret_cast<const char*>(cf.descriptors.data.data()), (std::streamsize)rows * cols * 4);
+        const int n = (int)cf.keypoints.size();
+        if (cf.descriptors.rows != n) return false;
+        if (vs_spcf_write(cache_path_.c_str(), 1, &idx, reinterpret_cast<const vs_keypoint*>(cf.keypoints.data()),
+                          cf.descriptors.data.data(), &n, n, first ? 0 : 1) != VS_OK)
+            return false;
+        first = false;
     }
-    return (bool)ofs;
+    return true;
 }
 
 // ------------------------------------------------------------------------------ Slam methods

@@ -75,6 +75,9 @@ _SIG = {
     "vs_slam_trajectory": (_I, [_P, _I, _P, _P, _P, _P, _P]),
     "vs_slam_stats": (_I, [_P, _P, _I]),
     "vs_slam_map": (_I, [_P, _I, _P, _P, _P]),
+    "vs_spcf_write": (_I, [ctypes.c_char_p, _I, _P, _P, _P, _P, _I, _I]),
+    "vs_spcf_write_dev": (_I, [_P, ctypes.c_char_p, _I, _P, _P, _P, _P, _I, _I, _P]),
+    "vs_spcf_read": (_I, [ctypes.c_char_p, _I, _I, _P, _P, _P, _P, _P]),
     "vs_profile_enable": (_I, [_P, _I]),
     "vs_profile_reset": (_I, [_P]),
     "vs_profile_read": (_I, [_P, _I, _P, _P, _P, _P]),
@@ -388,6 +391,13 @@ class Context:
                                                  _ptr(Ka), d_seeds, iters, thr, d_R, d_t, d_ok, d_diag, stream))
 
     # ---- profiling ----
+    def spcf_write_dev(self, path, frame_idx, F, d_kps, d_desc, d_n, cap, append=False, stream=None):
+        """vs_extract_batch_dev outputs (device pointers) -> SPCF entries frame_idx[f]."""
+        idx = np.ascontiguousarray(frame_idx, np.int32)
+        assert idx.shape == (F,)
+        _check(self.lib.vs_spcf_write_dev(self.h, os.fsencode(path), F, _ptr(idx), d_kps, d_desc, d_n, cap,
+                                          int(append), stream))
+
     def profile(self, on=True):
         _check(self.lib.vs_profile_enable(self.h, 1 if on else 0))
 
@@ -503,3 +513,32 @@ def exported_symbols_from_header(header_path):
     text = open(header_path).read()
     text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
     return sorted(set(re.findall(r"\b(vs_[a-z0-9_]+)\s*\(", text)))
+
+
+# ---- F2: SPCF feature cache (FeatureExtractor.cpp:261-381) -------------------------------------
+def spcf_write(path, frame_idx, kps, desc, n, append=False):
+    """Host arrays: kps [F][cap] KEYPOINT_DTYPE, desc [F][cap][256] f32, n [F]; entries frame_idx[f]."""
+    load_library()
+    kps = np.ascontiguousarray(kps, KEYPOINT_DTYPE)
+    desc = np.ascontiguousarray(desc, np.float32)
+    n = np.ascontiguousarray(n, np.int32)
+    idx = np.ascontiguousarray(frame_idx, np.int32)
+    F, cap = kps.shape[:2]
+    assert desc.shape == (F, cap, DESC_DIM) and n.shape == (F,) and idx.shape == (F,)
+    _check(_lib.vs_spcf_write(os.fsencode(path), F, _ptr(idx), _ptr(kps), _ptr(desc), _ptr(n), cap, int(append)))
+
+
+def spcf_read(path, cap=SP_MAX_KEYPOINTS):
+    """-> (frame_idx [E], kps [E][cap], desc [E][cap][256], n [E]), sorted by frame index."""
+    load_library()
+    cnt = ctypes.c_int(0)
+    _check(_lib.vs_spcf_read(os.fsencode(path), 0, cap, None, None, None, None, ctypes.byref(cnt)))
+    E = cnt.value
+    idx = np.zeros(max(E, 1), np.int32)
+    kps = np.zeros((max(E, 1), cap), KEYPOINT_DTYPE)
+    desc = np.zeros((max(E, 1), cap, DESC_DIM), np.float32)
+    n = np.zeros(max(E, 1), np.int32)
+    if E:
+        _check(_lib.vs_spcf_read(os.fsencode(path), E, cap, _ptr(idx), _ptr(kps), _ptr(desc), _ptr(n),
+                                 ctypes.byref(cnt)))
+    return idx[:E], kps[:E], desc[:E], n[:E]

@@ -18,6 +18,11 @@ Multi-GPU: frames are sharded in contiguous blocks (rank r owns
 whole step's features (the SPCF-cache-like interchange the sequential tracker consumes) and gives
 rank r the neighbour frame r*B-1 its first pair needs.  Depth maps of a rank's block plus the one
 halo frame before it come with the input.
+
+F2 (SPCF as the batch interchange, FeatureExtractor.cpp:261-381): with spcf_path set, collect()
+appends every step's feature records — the whole gathered step on rank 0 when world > 1 — to an
+SPCF cache keyed by the global processed-frame index (the reference's sequential extract index,
+FeatureExtractor.cpp:52), which vs_slam_process_features then replays (tests/test_gpu_spcf.py).
 """
 import numpy as np
 import torch
@@ -71,7 +76,7 @@ class _StepSet:
     """Device tables of one in-flight step (feature records of the block + halo slot, depth,
     per-pair matches / F / motion results) plus pinned host copies of the per-pair motion."""
 
-    def __init__(self, B, h, w, cap, dev, with_depth=True):
+    def __init__(self, B, h, w, cap, dev, with_depth=True, gathered=0):
         F = B + 1  # slot 0 = the frame before this rank's block
         P = B
         z = lambda *shape, dt=torch.int32: torch.zeros(shape, dtype=dt, device=dev)
@@ -89,6 +94,10 @@ class _StepSet:
         self.eR, self.et = z(P, 9, dt=torch.float64), z(P, 3, dt=torch.float64)
         self.escale, self.eok, self.ediag = z(P, dt=torch.float64), z(P), z(P, 8)
         self.seeds = z(P)
+        self.fc0 = 0
+        if gathered:  # a copy of the step's all-gathered records (SPCF writing, world > 1)
+            self.g_kps, self.g_desc = z(gathered, cap * KP_BYTES, dt=torch.uint8), z(gathered, cap, 256, dt=torch.float32)
+            self.g_n = z(gathered)
         self.motion = torch.zeros(P * 27, dtype=torch.float64, device=dev)  # R t ok eR et escale eok
         self.host = torch.zeros(P * 27, dtype=torch.float64, pin_memory=True)
         self.net_done = torch.cuda.Event()
@@ -109,13 +118,15 @@ class DevicePipeline:
     rewritten only after step k-2's geometry finished (event wait, no host sync)."""
 
     def __init__(self, ctx, B, h=480, w=640, cap=va.SP_MAX_KEYPOINTS, K=va.K_TUM, iters=200, thr=0.05,
-                 ratio=0.75, rank=0, world=1, group=None, monocular=False):
+                 ratio=0.75, rank=0, world=1, group=None, monocular=False, spcf_path=None):
         self.ctx, self.B, self.h, self.w, self.cap = ctx, B, h, w, cap
         self.monocular = monocular
         self.K, self.iters, self.thr, self.ratio = K, iters, thr, ratio
         self.rank, self.world, self.group = rank, world, group
         dev = torch.device("cuda", torch.cuda.current_device())
-        self.sets = [_StepSet(B, h, w, cap, dev, with_depth=not monocular) for _ in range(2)]
+        self.spcf_path, self._spcf_open = spcf_path, False
+        gathered = world * B if (spcf_path and world > 1 and rank == 0) else 0
+        self.sets = [_StepSet(B, h, w, cap, dev, with_depth=not monocular, gathered=gathered) for _ in range(2)]
         self.k = 0
         self.pairs = torch.tensor([[p, p + 1] for p in range(B)], dtype=torch.int32, device=dev)
         self._seed_base = torch.arange(B, dtype=torch.int64, device=dev)
@@ -136,6 +147,7 @@ class DevicePipeline:
             assert depth.shape == (B, h, w) and depth.dtype == torch.float32
         S, prev = self.sets[self.k % 2], self.sets[(self.k + 1) % 2]
         self.k += 1
+        S.fc0 = frame_count0
         ctx = self.ctx
         # inputs are produced on the caller's stream
         self.s_net.wait_stream(torch.cuda.current_stream())
@@ -164,7 +176,11 @@ class DevicePipeline:
                 S.n[0].copy_(prev.n[B])
             else:
                 # all-gather the step's feature records; slot 0 <- frame rank*B - 1
-                self.xchg.exchange(S.kps, S.desc, S.n)
+                gk, gd, gn = self.xchg.exchange(S.kps, S.desc, S.n)
+                if hasattr(S, "g_kps"):
+                    S.g_kps.copy_(gk)
+                    S.g_desc.copy_(gd)
+                    S.g_n.copy_(gn)
             S.seeds.copy_((self._seed_base + (42 + frame_count0)).to(torch.int32))
             ctx.match_pairs_dev(B, self.pairs.data_ptr(), B + 1, S.desc.data_ptr(), S.n.data_ptr(), cap,
                                 self.ratio, S.raw.data_ptr(), S.nraw.data_ptr(), S.good.data_ptr(),
@@ -194,6 +210,8 @@ class DevicePipeline:
     def collect(self, S):
         """Wait for a submitted step's geometry; returns (ok, R, t, eok, eR, et, escale) numpy."""
         S.geo_done.synchronize()
+        if self.spcf_path is not None and self.rank == 0:
+            self._write_spcf(S)
         P = self.B
         h = S.host.numpy().copy()  # the pinned buffer is rewritten when this set is reused
         o = [0]
@@ -204,6 +222,17 @@ class DevicePipeline:
             return v.reshape(P, k) if k > 1 else v
         R, t, ok, eR, et, esc, eok = take(9), take(3), take(1), take(9), take(3), take(1), take(1)
         return ok.astype(np.int32), R, t, eok.astype(np.int32), eR, et, esc
+
+    def _write_spcf(self, S):
+        if self.world > 1:
+            kps, desc, n, first = S.g_kps, S.g_desc, S.g_n, S.fc0  # rank 0's block starts the step
+        else:
+            kps, desc, n, first = S.kps[1:], S.desc[1:], S.n[1:], S.fc0
+        F = n.shape[0]
+        # the step's tables are complete (geo_done waited); the library's own stream does the copies
+        self.ctx.spcf_write_dev(self.spcf_path, np.arange(first, first + F), F, kps.data_ptr(), desc.data_ptr(),
+                                n.data_ptr(), self.cap, append=self._spcf_open)
+        self._spcf_open = True
 
     @staticmethod
     def outputs(S):
