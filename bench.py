@@ -128,6 +128,9 @@ def parse():
     ap.add_argument("--frontend-steps", type=int, default=6, help="timed steps of the config[3] batch front end")
     ap.add_argument("--no-frontend", action="store_true")
     ap.add_argument("--mono-steps", type=int, default=4, help="timed steps of the config[4] monocular HD stream")
+    ap.add_argument("--render-workers", type=int, default=0,
+                    help="processes rendering the synthetic sequence (0: min(16, cpus / ranks); 1 under rocprofv3 "
+                         "--pmc, whose preloaded library has initialised the GPU before the fork)")
     return ap.parse_args()
 
 
@@ -212,8 +215,21 @@ def frontend_batch(ctx, L, B, rank, world, steps, warmup):
         tt = torch.tensor([el], dtype=torch.float64, device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         el = float(tt.item())
+    # the matcher alone on the last step's resident descriptors (B consecutive pairs per launch, whole chip):
+    # inside the pipeline it shares the CUs with the next step's network
+    S = pipe.sets[(pipe.k - 1) % 2]
+    cap = S.desc.shape[1]
+    sm = torch.cuda.current_stream().cuda_stream
+    ctx.profile(True)
+    ctx.profile_reset()
+    for _ in range(20):
+        ctx.match_pairs_dev(B, pipe.pairs.data_ptr(), B + 1, S.desc.data_ptr(), S.n.data_ptr(), cap, 0.75,
+                            S.raw.data_ptr(), S.nraw.data_ptr(), S.good.data_ptr(), S.ngood.data_ptr(), sm)
+    torch.cuda.synchronize()
+    alone = ctx.profile_read().get("match")
+    ctx.profile(False)
     return {"value": round(world * B * steps / el, 3), "unit": "frames/s", "ms_per_step": round(el / steps * 1e3, 3),
-            "_match": prof.get("match"), "steps": steps, "frames_per_gpu_per_step": B,
+            "_match": alone, "_match_in_pipeline": prof.get("match"), "steps": steps, "frames_per_gpu_per_step": B,
             "workload": "config[3] offline batch: per-GPU SuperPoint extract + ratio matching + F-RANSAC + 3D-3D "
                         "RANSAC (E fallback) over consecutive frame pairs, no tracking state",
             "parallelism": f"frame-sharded x{world}" + (" + RCCL all-gather of feature records" if world > 1 else "")}
@@ -307,7 +323,7 @@ def main():
     dev = torch.device("cuda", torch.cuda.current_device())
 
     # one lap of the closed-loop path; rank r starts its sequence 16 r frames further along
-    workers = max(1, min(16, (os.cpu_count() or 1) // max(world, 1)))
+    workers = args.render_workers or max(1, min(16, (os.cpu_count() or 1) // max(world, 1)))
     L0 = synth.loop_sequence(LOOP_FRAMES, workers=workers)
     U = LOOP_FRAMES
     roll = (16 * rank) % U
@@ -327,9 +343,17 @@ def main():
                                       [T0 + 0.1 * (g0 + j) for j in range(B)], [3 * (g0 + j) for j in range(B)])
 
     progress(f"sequence rendered, tracker ready; {args.warmup} warmup steps")
+    def run_steps(k0, k1):
+        # each batch's extraction is prefetched behind the previous batch's (vs_slam_prefetch_batch_dev),
+        # never across the warmup / timed boundary: every timed batch is extracted inside the timed region
+        for k in range(k0, k1):
+            if k + 1 < k1:
+                i1 = ((k + 1) * B) % U
+                slam.prefetch_batch_dev(B, bgr[i1].data_ptr(), dep[i1].data_ptr())
+            step(k)
+
     torch.cuda.synchronize()
-    for k in range(args.warmup):
-        step(k)
+    run_steps(0, args.warmup)
     torch.cuda.synchronize()
     ctx.profile(True)
     ctx.profile_reset()
@@ -337,8 +361,7 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for k in range(args.warmup, args.warmup + args.steps):
-        step(k)
+    run_steps(args.warmup, args.warmup + args.steps)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -390,7 +413,11 @@ def main():
     if not args.no_frontend and args.frontend_steps > 0:
         fe = frontend_batch(ctx, L, B, rank, world, args.frontend_steps, 2)
         mroof["frontend_batch"] = match_roofline(fe.pop("_match"), B, 256,
-                                                 f"config[3] batch front end: {B} consecutive pairs per launch, whole chip")
+                                                 f"config[3] batch front end's last step: {B} consecutive pairs per "
+                                                 "launch on the resident descriptors, alone on the whole chip")
+        inp = fe.pop("_match_in_pipeline")
+        if mroof["frontend_batch"] and inp and inp[1]:
+            mroof["frontend_batch"]["in_pipeline_avg_launch_us"] = round(inp[0] * 1e3 / inp[1], 2)
 
     mono = None
     progress("config[4] monocular HD stream")

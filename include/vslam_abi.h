@@ -297,6 +297,11 @@ int vs_slam_set_accelerometer(vs_slam* slam, const double* samples, int n);
 int vs_slam_process_batch_dev(vs_slam* slam, int B, const uint8_t* d_bgr, const float* d_depth,
                               const float* const* h_depth, const double* timestamps, const int* ids,
                               int* processed);
+/* The frames of the NEXT vs_slam_process_batch_dev call (same B, d_bgr, d_depth), given before the
+ * current one: the next call's extraction is enqueued right behind the current batch's, so it runs
+ * while the current batch is tracked.  The buffers must stay unchanged until that call; a next
+ * call with other buffers waits for the prefetch and extracts its own frames. */
+int vs_slam_prefetch_batch_dev(vs_slam* slam, int B, const uint8_t* d_bgr, const float* d_depth);
 /* One frame from host features (e.g. a FeatureExtractor SPCF cache hit, FeatureExtractor.cpp:54-61):
  * n_kp keypoints + n_kp x 256 descriptors, depth h x w fp32 metres (NULL = none). */
 int vs_slam_process_features(vs_slam* slam, int n_kp, const vs_keypoint* kps, const float* desc,
@@ -316,6 +321,28 @@ int vs_slam_stats(vs_slam* slam, int* out, int cap);
 /* Map points (Map::map_points): *n = count; the first cap positions (world, x 3) and validity
  * bytes are written (each nullable). */
 int vs_slam_map(vs_slam* slam, int cap, double* pos, uint8_t* valid, int* n);
+
+/* ---- F3: DepthEstimator::estimate (DepthEstimator.cpp:39-112), MiDaS v2.1-small ---------------
+ * The midas_v21_small_256 network (EfficientNet-Lite3 encoder, features 64, expand, non-negative)
+ * with the reference's pre-processing (INTER_LINEAR resize to 256 x 256, 1/255, per-channel
+ * mean / std on the BGR planes as :54-67 writes it) and post-processing (INTER_LINEAR resize back,
+ * min-max normalisation when the range exceeds 1e-6, :96-109).  The reference never consumes the
+ * result; BASELINE config[4] runs it per frame. */
+typedef struct vs_midas vs_midas;
+/* weights_path: a VSMW file (tools/midas_to_vsmw.py converts a MiDaS state_dict, BatchNorm folded)
+ * or NULL for seeded He-normal weights. */
+int vs_midas_create(vs_ctx* ctx, const char* weights_path, vs_midas** out);
+void vs_midas_destroy(vs_midas* m);
+size_t vs_midas_num_params(void);
+double vs_midas_flops_per_frame(void);
+int vs_midas_get_weights(vs_midas* m, float* out, size_t count);
+/* B frames d_bgr [B][h][w][3] u8 -> d_depth [B][h][w] fp32 in [0, 1] (enqueue only). */
+int vs_midas_estimate_dev(vs_midas* m, int B, const uint8_t* d_bgr, int h, int w, float* d_depth, void* stream);
+/* The three stages separately (tests): d_input [B][256][256][3] fp32 (NHWC, normalised),
+ * d_out [B][256][256] the network's output, d_depth as above. */
+int vs_midas_preprocess_dev(vs_midas* m, int B, const uint8_t* d_bgr, int h, int w, float* d_input, void* stream);
+int vs_midas_forward_dev(vs_midas* m, int B, const float* d_input, float* d_out, void* stream);
+int vs_midas_postprocess_dev(vs_midas* m, int B, const float* d_small, int h, int w, float* d_depth, void* stream);
 
 /* ---- F2: the SPCF feature cache as the batch interchange (FeatureExtractor.cpp:261-381) ---
  * Byte layout of the reference's save_cache / load_cache: u32 magic 0x53504346 ("SPCF"),

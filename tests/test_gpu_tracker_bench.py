@@ -1,9 +1,10 @@
 """GPU parity of the tracking loop at the bench's own settings (SURVEY.md 8(f)
 F1: Slam::process_frame, reference src/Slam.cpp:809-1135, restated in host/tracker.hpp).
 
-bench.py runs vs_slam_process_batch_dev with B = 32 frames per call, the default extraction chunk
-schedule (3, 4, 5, 7, 8, 5) on its own CU-masked stream and the default VS_SLAM_TRACK_CUS, over the
-126-frame closed loop replayed with continuing timestamps.  This test runs exactly that for 416
+bench.py runs vs_slam_process_batch_dev with B = 32 frames per call, each batch's extraction
+prefetched behind the previous batch's (vs_slam_prefetch_batch_dev), the default extraction chunk
+schedule (3, 4, 5, 7, 8, 5) on its own CU-masked stream, the speculative next-frame chain and the
+default VS_SLAM_TRACK_CUS, over the 126-frame closed loop replayed with continuing timestamps.  This test runs exactly that for 416
 frames (3.3 laps, map past 20k points) and the oracle tracker (oracle/orc_slam.cpp: the same control
 flow over the CPU restatements) on the same GPU features, and compares decision counters, the whole
 trajectory and the map bit for bit: every stage is bit-exact against its CPU restatement, and the
@@ -53,6 +54,9 @@ def gpu_run(vsctx, loop):
         for k in range(STEPS):
             g0 = k * B
             i0 = g0 % LOOP
+            if k + 1 < STEPS:  # as bench.py: the next batch extracted behind this one
+                i1 = (g0 + B) % LOOP
+                S.prefetch_batch_dev(B, bgr[i1].data_ptr(), dep[i1].data_ptr())
             done += S.process_batch_dev(B, bgr[i0].data_ptr(), dep[i0].data_ptr(), hdep[i0:i0 + B],
                                         [T0 + 0.1 * (g0 + j) for j in range(B)],
                                         [3 * (g0 + j) for j in range(B)]).tolist()
@@ -99,3 +103,31 @@ def test_bench_scale_ate_is_the_algorithms(gpu_run, oracle_run, loop):
         gi = np.round((ts - T0) / 0.1).astype(int) % LOOP
         res.append(ate.compute_ate(ts, t, ts, loop["t_wc"][gi]))
     assert res[0]["ate_rmse"] == res[1]["ate_rmse"] and res[0]["scale"] == res[1]["scale"], res
+
+
+def test_stale_prefetch_is_discarded(vsctx, loop):
+    """A prefetch hint whose buffers the next call does not use is waited for and dropped: the run
+    equals one without hints (and the region it held is reused correctly afterwards)."""
+    dev = torch.device("cuda", 0)
+    Bs = 16
+    bgr = torch.from_numpy(loop["bgr"][:4 * Bs]).to(dev)
+    dep = torch.from_numpy(loop["depth"][:4 * Bs]).to(dev)
+    other = bgr.clone()
+    res = []
+    for hints in (False, True):
+        with vslam_abi.Slam(vsctx, max_batch=Bs) as S:
+            for k in range(4):
+                g0 = k * Bs
+                if hints and k == 1:  # a hint for buffers the next call will not pass
+                    S.prefetch_batch_dev(Bs, other[g0 + Bs].data_ptr(), dep[g0 + Bs].data_ptr())
+                if hints and k == 2:  # a matching hint
+                    S.prefetch_batch_dev(Bs, bgr[g0 + Bs].data_ptr(), dep[g0 + Bs].data_ptr())
+                S.process_batch_dev(Bs, bgr[g0].data_ptr(), dep[g0].data_ptr(), list(loop["depth"][g0:g0 + Bs]),
+                                    [T0 + 0.1 * (g0 + j) for j in range(Bs)], [3 * (g0 + j) for j in range(Bs)])
+            S.finish()
+            res.append((S.stats(), S.trajectory(), S.map_points()))
+    assert np.array_equal(res[0][0], res[1][0])
+    for a, b in zip(res[0][1], res[1][1]):
+        assert np.array_equal(a, b)
+    for a, b in zip(res[0][2], res[1][2]):
+        assert np.array_equal(a, b)

@@ -510,10 +510,15 @@ static void launch(MatchArgs& a, int P, int cap_q, int cap_t, bool norms, hipStr
 
 int match_pairs(vs_ctx* ctx, int P, const int* d_pairs, int F, const float* d_desc, const int* d_n, int cap,
                 float ratio, vs_match* d_raw, int* d_nraw, vs_match* d_good, int* d_ngood, hipStream_t s,
-                const float* d_norms) {
+                const float* d_norms, unsigned long long* d_keys, unsigned* d_cnt) {
     if (P <= 0) return VS_OK;
     MatchArgs a{};
-    VS_CHECK(match_state(ctx, P, cap, &a.keys, &a.cnt, s));
+    if (d_keys && d_cnt) {  // the caller's own key / counter state (all ones / zero, left reset)
+        a.keys = d_keys;
+        a.cnt = d_cnt;
+    } else {
+        VS_CHECK(match_state(ctx, P, cap, &a.keys, &a.cnt, s));
+    }
     ProfScope ps(ctx, "match", s);
     static const bool pre_norms = std::getenv("VS_MATCH_NORMS") != nullptr;  // experiment: norms first
     if (!d_norms && pre_norms) {

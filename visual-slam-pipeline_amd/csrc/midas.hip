@@ -1,0 +1,804 @@
+// midas.hip — DepthEstimator::estimate (reference src/DepthEstimator.cpp:39-112) on gfx950: the
+// MiDaS v2.1-small network (the published midas_v21_small_256 topology: MidasNet_small with an
+// EfficientNet-Lite3 encoder, features = 64, expand = True, non-negative output) as hand-written
+// NHWC fp32 kernels, with the reference's pre- and post-processing around it.
+//
+//   pre   cv::resize(image, 256 x 256) (INTER_LINEAR, 8-bit fixed point: the SIMD row formula of
+//         OpenCV's VResizeLinearVec_32s8u, which covers whole 256-pixel rows), convertTo(1/255),
+//         (c - mean[c]) / std[c] per BGR channel as the reference writes it (:54-67)
+//   net   encoder: TF-"same"-padded stem and depthwise stride-2 convolutions (timm tf_ models),
+//         inverted residual blocks (1x1 expand + ReLU6, depthwise k x k + ReLU6, 1x1 project,
+//         identity skip), BatchNorm folded into the convolutions; decoder: 3x3 "rn" projections,
+//         four FeatureFusionBlock_custom (two residual conv units, x2 bilinear align_corners,
+//         1x1 out conv), output head (3x3 conv, x2 bilinear, 3x3 conv + ReLU, 1x1 conv + ReLU)
+//   post  cv::resize back to the frame size (INTER_LINEAR, float), minMaxLoc, (d - min) / (max -
+//         min) when the range exceeds 1e-6 (:96-109)
+//
+// Dense convolutions (3x3 and 1x1, 99 % of the FLOPs) are implicit GEMMs on the fp32 matrix cores:
+// a workgroup computes 64 output pixels x 64 output channels with v_mfma_f32_16x16x4_f32 (2 x 2
+// waves, four 16 x 16 chains each) over K = k*k*Cin in chunks of 16 input channels of one tap,
+// staged through LDS; bias, activation, an input-side ReLU (residual conv units) and up to two
+// residual adds are fused.  Depthwise convolutions and the resizes are HBM/L2-bound elementwise
+// kernels with channel-vectorised (float4) NHWC accesses.
+//
+// The reference never consumes this output (Frame::estimate_depth has no caller);
+// it is built for BASELINE config[4].  Weights: seeded He-normal (no checkpoint ships with the
+// reference, README.md:43) or a VSMW file written by tools/midas_to_vsmw.py from a MiDaS
+// state_dict (BatchNorm folded there).
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <vector>
+
+#include "vs_internal.h"
+
+namespace vs {
+namespace midas {
+
+constexpr int kIn = 256;  // Config::MIDAS_INPUT_SIZE (Config.h:45)
+enum Kind : int { K_CONV = 0, K_DW = 1, K_UP = 2 };
+enum Act : int { A_NONE = 0, A_RELU = 1, A_RELU6 = 2 };
+
+// Canonical weights per layer: conv [cout][cin][k][k] then [cout] bias; depthwise [c][k][k] then
+// [c] bias (BatchNorm folded).
+struct LayerDef {
+    int kind, cin, cout, k;
+    bool bias;  // the scratch "rn" projections have none
+};
+
+struct Step {
+    int kind;
+    int layer = -1;
+    int in = -1, out = -1, res1 = -1, res2 = -1;
+    int H = 0, W = 0, C = 0, Ho = 0, Wo = 0, Co = 0;
+    int k = 1, stride = 1, pad_t = 0, pad_l = 0;
+    int act = A_NONE;
+    bool pre_relu = false, align_corners = false;
+};
+
+// The network as data: layer definitions (canonical weight order) and the step program over
+// SSA tensors (tensor t has tdims[t] = {H, W, C}).
+struct Net {
+    std::vector<LayerDef> layers;
+    std::vector<Step> steps;
+    std::vector<int> tdims;  // 3 per tensor
+    int input = -1, output = -1;
+
+    int tensor(int H, int W, int C) {
+        tdims.insert(tdims.end(), {H, W, C});
+        return (int)tdims.size() / 3 - 1;
+    }
+    int Hof(int t) const { return tdims[3 * t]; }
+    int Wof(int t) const { return tdims[3 * t + 1]; }
+    int Cof(int t) const { return tdims[3 * t + 2]; }
+    // TF "same" padding (timm Conv2dSame): total = max((ceil(i/s) - 1) s + k - i, 0), begin = total / 2
+    static int same_begin(int i, int k, int s) {
+        const int o = (i + s - 1) / s;
+        const int total = std::max((o - 1) * s + k - i, 0);
+        return total / 2;
+    }
+    int conv(int in, int cout, int k, int stride, int act, bool tf_same, bool bias = true, int res1 = -1,
+             int res2 = -1, bool pre_relu = false) {
+        Step st;
+        st.kind = K_CONV;
+        st.layer = (int)layers.size();
+        layers.push_back({K_CONV, Cof(in), cout, k, bias});
+        st.in = in;
+        st.H = Hof(in), st.W = Wof(in), st.C = Cof(in);
+        st.k = k, st.stride = stride;
+        st.Ho = (st.H + stride - 1) / stride, st.Wo = (st.W + stride - 1) / stride, st.Co = cout;
+        st.pad_t = tf_same ? same_begin(st.H, k, stride) : k / 2;
+        st.pad_l = tf_same ? same_begin(st.W, k, stride) : k / 2;
+        st.act = act, st.res1 = res1, st.res2 = res2, st.pre_relu = pre_relu;
+        st.out = tensor(st.Ho, st.Wo, cout);
+        steps.push_back(st);
+        return st.out;
+    }
+    int dw(int in, int k, int stride) {
+        Step st;
+        st.kind = K_DW;
+        st.layer = (int)layers.size();
+        layers.push_back({K_DW, Cof(in), Cof(in), k, true});
+        st.in = in;
+        st.H = Hof(in), st.W = Wof(in), st.C = st.Co = Cof(in);
+        st.k = k, st.stride = stride;
+        st.Ho = (st.H + stride - 1) / stride, st.Wo = (st.W + stride - 1) / stride;
+        st.pad_t = same_begin(st.H, k, stride);
+        st.pad_l = same_begin(st.W, k, stride);
+        st.act = A_RELU6;
+        st.out = tensor(st.Ho, st.Wo, st.C);
+        steps.push_back(st);
+        return st.out;
+    }
+    int up(int in, bool align_corners) {
+        Step st;
+        st.kind = K_UP;
+        st.in = in;
+        st.H = Hof(in), st.W = Wof(in), st.C = st.Co = Cof(in);
+        st.Ho = 2 * st.H, st.Wo = 2 * st.W;
+        st.align_corners = align_corners;
+        st.out = tensor(st.Ho, st.Wo, st.C);
+        steps.push_back(st);
+        return st.out;
+    }
+    // timm InvertedResidual (exp ratio 6, no SE in the Lite models): 1x1 expand + BN + ReLU6,
+    // depthwise + BN + ReLU6, 1x1 project + BN, identity skip when stride 1 and cin == cout
+    int ir(int in, int cout, int k, int stride) {
+        const int cin = Cof(in);
+        int x = conv(in, cin * 6, 1, 1, A_RELU6, false);
+        x = dw(x, k, stride);
+        return conv(x, cout, 1, 1, A_NONE, false, true, stride == 1 && cin == cout ? in : -1);
+    }
+    // ResidualConvUnit_custom (bn = False): conv2(relu(conv1(relu(x)))) + x  [+ extra]
+    int rcu(int x, int extra = -1) {
+        const int c = Cof(x);
+        const int h = conv(x, c, 3, 1, A_RELU, false, true, -1, -1, /*pre_relu=*/true);
+        return conv(h, c, 3, 1, A_NONE, false, true, x, extra);
+    }
+    // FeatureFusionBlock_custom: out = xs0 [+ rcu1(xs1)]; rcu2; x2 bilinear (align_corners); 1x1 out
+    int fusion(int xs0, int xs1, int out_ch) {
+        int o = xs1 >= 0 ? rcu(xs1, xs0) : xs0;
+        o = rcu(o);
+        o = up(o, true);
+        return conv(o, out_ch, 1, 1, A_NONE, false);
+    }
+
+    void build() {
+        input = tensor(kIn, kIn, 3);
+        // EfficientNet-Lite3 (tf_efficientnet_lite3): stem 32, stages
+        // DS(24) | IR k3 s2 32 x3 | IR k5 s2 48 x3 | IR k3 s2 96 x5 | IR k5 s1 136 x5 | IR k5 s2 232 x6 | IR k3 s1 384 x1
+        int x = conv(input, 32, 3, 2, A_RELU6, true);
+        x = dw(x, 3, 1);  // DepthwiseSeparable: dw 3x3 + BN + ReLU6, pw 1x1 + BN (no act, no skip 32 -> 24)
+        x = conv(x, 24, 1, 1, A_NONE, false);
+        struct Stage {
+            int c, k, s, n;
+        };
+        const Stage stages[6] = {{32, 3, 2, 3}, {48, 5, 2, 3}, {96, 3, 2, 5}, {136, 5, 1, 5}, {232, 5, 2, 6}, {384, 3, 1, 1}};
+        int skip[4];
+        for (int si = 0; si < 6; si++) {
+            for (int r = 0; r < stages[si].n; r++) x = ir(x, stages[si].c, stages[si].k, r == 0 ? stages[si].s : 1);
+            if (si == 0) skip[0] = x;  // layer1 = stem + blocks[0:2]   (32 @ 64^2)
+            if (si == 1) skip[1] = x;  // layer2 = blocks[2:3]          (48 @ 32^2)
+            if (si == 3) skip[2] = x;  // layer3 = blocks[3:5]          (136 @ 16^2)
+            if (si == 5) skip[3] = x;  // layer4 = blocks[5:9]          (384 @ 8^2)
+        }
+        // scratch.layerN_rn: 3x3, no bias, to 64 / 128 / 256 / 512 (expand)
+        const int rn1 = conv(skip[0], 64, 3, 1, A_NONE, false, false);
+        const int rn2 = conv(skip[1], 128, 3, 1, A_NONE, false, false);
+        const int rn3 = conv(skip[2], 256, 3, 1, A_NONE, false, false);
+        const int rn4 = conv(skip[3], 512, 3, 1, A_NONE, false, false);
+        const int p4 = fusion(rn4, -1, 256);
+        const int p3 = fusion(p4, rn3, 128);
+        const int p2 = fusion(p3, rn2, 64);
+        const int p1 = fusion(p2, rn1, 64);  // refinenet1: no expand
+        // output_conv: 3x3 64 -> 32, x2 bilinear (align_corners False), 3x3 32 -> 32 + ReLU, 1x1 32 -> 1 + ReLU
+        int o = conv(p1, 32, 3, 1, A_NONE, false);
+        o = up(o, false);
+        o = conv(o, 32, 3, 1, A_RELU, false);
+        output = conv(o, 1, 1, 1, A_RELU, false);
+    }
+    size_t num_params() const {
+        size_t n = 0;
+        for (const auto& L : layers)
+            n += (size_t)(L.kind == K_DW ? L.cout * L.k * L.k : L.cout * L.cin * L.k * L.k) + (L.bias ? L.cout : 0);
+        return n;
+    }
+    double flops() const {  // per frame (2 x MACs of the convolutions)
+        double f = 0;
+        for (const auto& st : steps) {
+            if (st.kind == K_CONV) f += 2.0 * st.Ho * st.Wo * st.Co * st.C * st.k * st.k;
+            if (st.kind == K_DW) f += 2.0 * st.Ho * st.Wo * st.C * st.k * st.k;
+        }
+        return f;
+    }
+};
+
+const Net& net() {
+    static Net n = [] {
+        Net m;
+        m.build();
+        return m;
+    }();
+    return n;
+}
+
+// ---- kernels --------------------------------------------------------------------------------
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ float activate(float v, int act) {
+    if (act == A_RELU) return v > 0.f ? v : 0.f;
+    if (act == A_RELU6) return v > 0.f ? (v < 6.f ? v : 6.f) : 0.f;
+    return v;
+}
+
+// OpenCV resize coefficient (resizeGeneric_, INTER_LINEAR): f = (float)((d + 0.5) * scale - 0.5),
+// s = floor(f), f -= s, clamped to the source; fixed point saturate_cast<short>(f * 2048)
+struct Lin {
+    int s0, s1;
+    float f;
+};
+__device__ __forceinline__ Lin lin_coef(int d, double scale, int n) {
+    float f = (float)((d + 0.5) * scale - 0.5);
+    int s = (int)floorf(f);
+    f -= (float)s;
+    if (s < 0) {
+        f = 0.f;
+        s = 0;
+    }
+    if (s >= n - 1) {
+        f = 0.f;
+        s = n - 1;
+    }
+    return {s, s + 1 < n ? s + 1 : n - 1, f};
+}
+__device__ __forceinline__ int fix11(float v) {  // saturate_cast<short>(v * INTER_RESIZE_COEF_SCALE)
+    return (int)rintf(v * 2048.0f);
+}
+
+// pre: B BGR u8 frames (h x w) -> B x 256 x 256 x 3 fp32, normalised (DepthEstimator.cpp:54-67)
+__global__ __launch_bounds__(256) void k_mid_pre(const uint8_t* __restrict__ bgr, int h, int w, int B,
+                                                 float* __restrict__ out) {
+    const int idx = blockIdx.x * 256 + threadIdx.x;
+    if (idx >= B * kIn * kIn) return;
+    const int b = idx / (kIn * kIn), p = idx - b * kIn * kIn, y = p / kIn, x = p - y * kIn;
+    const Lin cx = lin_coef(x, 1.0 / ((double)kIn / w), w), cy = lin_coef(y, 1.0 / ((double)kIn / h), h);
+    const int a0 = fix11(1.f - cx.f), a1 = fix11(cx.f), b0 = fix11(1.f - cy.f), b1 = fix11(cy.f);
+    const uint8_t* im = bgr + (size_t)b * h * w * 3;
+    const uint8_t* r0 = im + (size_t)cy.s0 * w * 3;
+    const uint8_t* r1 = im + (size_t)cy.s1 * w * 3;
+    // (float)(1/255.0); 1/std and -mean/std in double, then float (MatExpr -> convertTo, fma)
+    const float mean[3] = {0.485f, 0.456f, 0.406f}, sd[3] = {0.229f, 0.224f, 0.225f};
+    float* o = out + (size_t)idx * 3;
+#pragma unroll
+    for (int c = 0; c < 3; c++) {
+        const int h0 = r0[cx.s0 * 3 + c] * a0 + r0[cx.s1 * 3 + c] * a1;
+        const int h1 = r1[cx.s0 * 3 + c] * a0 + r1[cx.s1 * 3 + c] * a1;
+        // VResizeLinearVec_32s8u: (mulhi16(h0 >> 4, b0) + mulhi16(h1 >> 4, b1) + 2) >> 2, saturated
+        int v = ((((h0 >> 4) * b0) >> 16) + (((h1 >> 4) * b1) >> 16) + 2) >> 2;
+        v = v < 0 ? 0 : (v > 255 ? 255 : v);
+        const float f = (float)v * (float)(1.0 / 255.0);
+        const double is = 1.0 / (double)sd[c];
+        o[c] = fmaf(f, (float)is, (float)(-(double)mean[c] * is));
+    }
+}
+
+// Dense convolution as an implicit GEMM on the fp32 matrix cores (see file header).
+// in [B][H][W][C], w [k*k][C][CoP] (CoP = Co rounded up to 64), out / res [B][Ho][Wo][Co].
+struct ConvArgs {
+    const float* in;
+    const float* w;
+    const float* bias;  // nullptr: none
+    const float* res1;
+    const float* res2;
+    float* out;
+    int B, H, W, C, Ho, Wo, Co, CoP, k, stride, pad_t, pad_l, act, pre_relu;
+};
+
+constexpr int kCT = 64;  // output pixels x channels per workgroup
+constexpr int kCK = 16;  // input channels per K chunk
+constexpr int kAS = kCK + 4;  // LDS row stride of the pixel operand (floats)
+
+__global__ __launch_bounds__(256) void k_mid_conv(ConvArgs a) {
+    __shared__ float sA[kCT * kAS];   // [pixel][16 k] (k permuted for float4 fragments)
+    __shared__ float sB[kCT * kAS];   // [cout][16 k]
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, li = lane & 15, lg = lane >> 4;
+    const int npix = a.B * a.Ho * a.Wo;
+    const int p0 = blockIdx.x * kCT, n0 = blockIdx.y * kCT;
+    // staging roles: 256 threads x 4 k each: pixel / cout row r = tid / 4, k quad q = tid % 4
+    const int r = tid >> 2, q = tid & 3;
+    const int gp = p0 + r;
+    int b = 0, oy = 0, ox = 0;
+    const bool pvalid = gp < npix;
+    if (pvalid) {
+        b = gp / (a.Ho * a.Wo);
+        const int rem = gp - b * a.Ho * a.Wo;
+        oy = rem / a.Wo;
+        ox = rem - oy * a.Wo;
+    }
+    const int wq = wv & 1, wt = wv >> 1;  // wave: pixels wq*32.., couts wt*32..
+    f32x4 acc[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; i++)
+#pragma unroll
+        for (int j = 0; j < 2; j++) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const int nchunk = (a.C + kCK - 1) / kCK;
+    for (int tap = 0; tap < a.k * a.k; tap++) {
+        const int ky = tap / a.k, kx = tap - ky * a.k;
+        const int iy = oy * a.stride - a.pad_t + ky, ix = ox * a.stride - a.pad_l + kx;
+        const bool inb = pvalid && iy >= 0 && iy < a.H && ix >= 0 && ix < a.W;
+        const float* src = a.in + (((size_t)b * a.H + (inb ? iy : 0)) * a.W + (inb ? ix : 0)) * a.C;
+        for (int ch = 0; ch < nchunk; ch++) {
+            const int c0 = ch * kCK + 4 * q;
+            // pixel operand: 4 consecutive input channels of this tap
+            float v[4];
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                const float t = (inb && c0 + j < a.C) ? src[c0 + j] : 0.f;
+                v[j] = a.pre_relu ? (t > 0.f ? t : 0.f) : t;
+            }
+            // weight operand: cout n0 + r, the same 4 channels
+            const int co = n0 + r;
+            float u[4];
+#pragma unroll
+            for (int j = 0; j < 4; j++)
+                u[j] = (c0 + j < a.C) ? a.w[((size_t)tap * a.C + c0 + j) * a.CoP + co] : 0.f;
+            __syncthreads();
+            // k = 4 q + j -> position 4 j + q (a lane group g reads k = g, 4 + g, 8 + g, 12 + g)
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                sA[r * kAS + 4 * j + q] = v[j];
+                sB[r * kAS + 4 * j + q] = u[j];
+            }
+            __syncthreads();
+            float4 fa[2], fb[2];
+#pragma unroll
+            for (int i = 0; i < 2; i++) {
+                fa[i] = *reinterpret_cast<const float4*>(&sA[(wq * 32 + 16 * i + li) * kAS + 4 * lg]);
+                fb[i] = *reinterpret_cast<const float4*>(&sB[(wt * 32 + 16 * i + li) * kAS + 4 * lg]);
+            }
+#pragma unroll
+            for (int j = 0; j < 4; j++)
+#pragma unroll
+                for (int i = 0; i < 2; i++)
+#pragma unroll
+                    for (int m = 0; m < 2; m++)
+                        acc[i][m] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[i][j], fb[m][j], acc[i][m], 0, 0, 0);
+        }
+    }
+    // D[pixel 4 lg + e][cout li] of fragment (i, m)
+#pragma unroll
+    for (int i = 0; i < 2; i++)
+#pragma unroll
+        for (int m = 0; m < 2; m++) {
+            const int co = n0 + wt * 32 + 16 * m + li;
+            if (co >= a.Co) continue;
+            const float bv = a.bias ? a.bias[co] : 0.f;
+#pragma unroll
+            for (int e = 0; e < 4; e++) {
+                const int gpix = p0 + wq * 32 + 16 * i + 4 * lg + e;
+                if (gpix >= npix) continue;
+                const size_t o = (size_t)gpix * a.Co + co;
+                float v = activate(acc[i][m][e] + bv, a.act);
+                if (a.res1) v = v + a.res1[o];
+                if (a.res2) v = a.res2[o] + v;
+                a.out[o] = v;
+            }
+        }
+}
+
+// Depthwise k x k, stride s, TF-same padding, bias + ReLU6; one thread per (pixel, 4 channels).
+__global__ __launch_bounds__(256) void k_mid_dw(const float* __restrict__ in, const float* __restrict__ w,
+                                                const float* __restrict__ bias, float* __restrict__ out, int B, int H,
+                                                int W, int C, int Ho, int Wo, int k, int stride, int pad_t, int pad_l) {
+    const int C4 = C / 4;
+    const long idx = (long)blockIdx.x * 256 + threadIdx.x;
+    if (idx >= (long)B * Ho * Wo * C4) return;
+    const int c4 = (int)(idx % C4);
+    const long pix = idx / C4;
+    const int ox = (int)(pix % Wo), oy = (int)((pix / Wo) % Ho), b = (int)(pix / ((long)Wo * Ho));
+    float4 s = reinterpret_cast<const float4*>(bias)[c4];
+    for (int ky = 0; ky < k; ky++) {
+        const int iy = oy * stride - pad_t + ky;
+        if (iy < 0 || iy >= H) continue;
+        for (int kx = 0; kx < k; kx++) {
+            const int ix = ox * stride - pad_l + kx;
+            if (ix < 0 || ix >= W) continue;
+            const float4 v = reinterpret_cast<const float4*>(in + (((size_t)b * H + iy) * W + ix) * C)[c4];
+            const float4 g = reinterpret_cast<const float4*>(w + (size_t)(ky * k + kx) * C)[c4];
+            s.x = fmaf(v.x, g.x, s.x);
+            s.y = fmaf(v.y, g.y, s.y);
+            s.z = fmaf(v.z, g.z, s.z);
+            s.w = fmaf(v.w, g.w, s.w);
+        }
+    }
+    s.x = activate(s.x, A_RELU6);
+    s.y = activate(s.y, A_RELU6);
+    s.z = activate(s.z, A_RELU6);
+    s.w = activate(s.w, A_RELU6);
+    reinterpret_cast<float4*>(out)[idx] = s;
+}
+
+// x2 bilinear upsampling (torch interpolate, mode "bilinear"), NHWC, 4 channels per thread.
+__global__ __launch_bounds__(256) void k_mid_up(const float* __restrict__ in, float* __restrict__ out, int B, int H,
+                                                int W, int C, int align_corners) {
+    const int C4 = C / 4, Ho = 2 * H, Wo = 2 * W;
+    const long idx = (long)blockIdx.x * 256 + threadIdx.x;
+    if (idx >= (long)B * Ho * Wo * C4) return;
+    const int c4 = (int)(idx % C4);
+    const long pix = idx / C4;
+    const int ox = (int)(pix % Wo), oy = (int)((pix / Wo) % Ho), b = (int)(pix / ((long)Wo * Ho));
+    float sy, sx;
+    if (align_corners) {
+        sy = Ho > 1 ? (float)(H - 1) / (float)(Ho - 1) * oy : 0.f;
+        sx = Wo > 1 ? (float)(W - 1) / (float)(Wo - 1) * ox : 0.f;
+    } else {
+        sy = fmaxf((oy + 0.5f) * 0.5f - 0.5f, 0.f);
+        sx = fmaxf((ox + 0.5f) * 0.5f - 0.5f, 0.f);
+    }
+    const int y0 = (int)sy, x0 = (int)sx;
+    const int y1 = y0 + (y0 < H - 1), x1 = x0 + (x0 < W - 1);
+    const float ly = sy - y0, lx = sx - x0, hy = 1.f - ly, hx = 1.f - lx;
+    const float4* p = reinterpret_cast<const float4*>(in) + (size_t)b * H * W * C4;
+    const float4 v00 = p[((size_t)y0 * W + x0) * C4 + c4], v01 = p[((size_t)y0 * W + x1) * C4 + c4];
+    const float4 v10 = p[((size_t)y1 * W + x0) * C4 + c4], v11 = p[((size_t)y1 * W + x1) * C4 + c4];
+    float4 o;
+    o.x = hy * (hx * v00.x + lx * v01.x) + ly * (hx * v10.x + lx * v11.x);
+    o.y = hy * (hx * v00.y + lx * v01.y) + ly * (hx * v10.y + lx * v11.y);
+    o.z = hy * (hx * v00.z + lx * v01.z) + ly * (hx * v10.z + lx * v11.z);
+    o.w = hy * (hx * v00.w + lx * v01.w) + ly * (hx * v10.w + lx * v11.w);
+    reinterpret_cast<float4*>(out)[idx] = o;
+}
+
+// post: the 1-channel 256^2 output resized to h x w (float INTER_LINEAR, the same coefficients
+// without fixed point) with per-block min / max partials.
+__global__ __launch_bounds__(256) void k_mid_post(const float* __restrict__ d, int B, int h, int w,
+                                                  float* __restrict__ out, float* __restrict__ part) {
+    __shared__ float smin[256], smax[256];
+    const int b = blockIdx.y;
+    const int idx = blockIdx.x * 256 + threadIdx.x;
+    float mn = INFINITY, mx = -INFINITY;
+    if (idx < h * w) {
+        const int y = idx / w, x = idx - y * w;
+        const Lin cx = lin_coef(x, 1.0 / ((double)w / kIn), kIn), cy = lin_coef(y, 1.0 / ((double)h / kIn), kIn);
+        const float* s = d + (size_t)b * kIn * kIn;
+        const float a0 = 1.f - cx.f, a1 = cx.f, b0 = 1.f - cy.f, b1 = cy.f;
+        const float r0 = s[cy.s0 * kIn + cx.s0] * a0 + s[cy.s0 * kIn + cx.s1] * a1;
+        const float r1 = s[cy.s1 * kIn + cx.s0] * a0 + s[cy.s1 * kIn + cx.s1] * a1;
+        const float v = r0 * b0 + r1 * b1;
+        out[(size_t)b * h * w + idx] = v;
+        mn = mx = v;
+    }
+    smin[threadIdx.x] = mn;
+    smax[threadIdx.x] = mx;
+    __syncthreads();
+    for (int o = 128; o > 0; o >>= 1) {
+        if (threadIdx.x < o) {
+            smin[threadIdx.x] = fminf(smin[threadIdx.x], smin[threadIdx.x + o]);
+            smax[threadIdx.x] = fmaxf(smax[threadIdx.x], smax[threadIdx.x + o]);
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        part[((size_t)b * gridDim.x + blockIdx.x) * 2] = smin[0];
+        part[((size_t)b * gridDim.x + blockIdx.x) * 2 + 1] = smax[0];
+    }
+}
+
+// minMaxLoc over the partials, then (d - min) / (max - min) when max - min > 1e-6 (convertTo with
+// alpha = 1 / range, beta = -min / range, as the MatExpr evaluates): one workgroup row per frame.
+__global__ __launch_bounds__(256) void k_mid_norm(float* __restrict__ out, const float* __restrict__ part, int nparts,
+                                                  int n) {
+    __shared__ float smin[256], smax[256];
+    const int b = blockIdx.y;
+    float mn = INFINITY, mx = -INFINITY;
+    for (int i = threadIdx.x; i < nparts; i += 256) {
+        mn = fminf(mn, part[((size_t)b * nparts + i) * 2]);
+        mx = fmaxf(mx, part[((size_t)b * nparts + i) * 2 + 1]);
+    }
+    smin[threadIdx.x] = mn;
+    smax[threadIdx.x] = mx;
+    __syncthreads();
+    for (int o = 128; o > 0; o >>= 1) {
+        if (threadIdx.x < o) {
+            smin[threadIdx.x] = fminf(smin[threadIdx.x], smin[threadIdx.x + o]);
+            smax[threadIdx.x] = fmaxf(smax[threadIdx.x], smax[threadIdx.x + o]);
+        }
+        __syncthreads();
+    }
+    const double lo = smin[0], hi = smax[0];
+    if (!(hi - lo > 1e-6)) return;
+    const double sc = 1.0 / (hi - lo);
+    const float al = (float)sc, be = (float)(-lo * sc);
+    float* o = out + (size_t)b * n;
+    for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) o[i] = fmaf(o[i], al, be);
+}
+
+// ---- weights --------------------------------------------------------------------------------
+std::vector<float> synth(uint64_t seed) {
+    uint64_t st = seed;
+    auto next = [&]() {
+        uint64_t z = (st += 0x9E3779B97F4A7C15ull);
+        z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+        z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+        return z ^ (z >> 31);
+    };
+    auto normal = [&]() {
+        double u1 = ((next() >> 11) + 1) * (1.0 / 9007199254740992.0);
+        double u2 = (next() >> 11) * (1.0 / 9007199254740992.0);
+        return std::sqrt(-2.0 * std::log(u1)) * std::cos(6.283185307179586 * u2);
+    };
+    std::vector<float> w;
+    for (const auto& L : net().layers) {
+        const int fan_in = (L.kind == K_DW ? 1 : L.cin) * L.k * L.k;
+        const double sd = std::sqrt(2.0 / fan_in);
+        const size_t nw = (size_t)(L.kind == K_DW ? L.cout : L.cout * L.cin) * L.k * L.k;
+        for (size_t i = 0; i < nw; i++) w.push_back((float)(normal() * sd));
+        if (L.bias)
+            for (int i = 0; i < L.cout; i++) w.push_back((float)(normal() * 0.05));
+    }
+    return w;
+}
+
+struct DevW {
+    float* w = nullptr;
+    float* b = nullptr;
+    int cop = 0;
+};
+
+}  // namespace midas
+}  // namespace vs
+
+struct vs_midas {
+    vs_ctx* ctx = nullptr;
+    std::vector<float> h_weights;
+    std::vector<vs::midas::DevW> dev;
+    std::vector<vs::DevBuf> slots;  // activation slots (reused by last use)
+    std::vector<int> slot_of;       // tensor -> slot
+    std::vector<size_t> slot_elems; // floats per frame per slot
+    vs::DevBuf input, post_part;
+    int batch_cap = 0;
+};
+
+namespace vs {
+namespace midas {
+
+static int upload(vs_midas* m) {
+    const Net& N = net();
+    const float* p = m->h_weights.data();
+    m->dev.resize(N.layers.size());
+    for (size_t i = 0; i < N.layers.size(); i++) {
+        const LayerDef& L = N.layers[i];
+        DevW& D = m->dev[i];
+        const int kk = L.k * L.k;
+        if (L.kind == K_DW) {
+            std::vector<float> w((size_t)kk * L.cout), b(L.cout, 0.f);
+            for (int c = 0; c < L.cout; c++)
+                for (int t = 0; t < kk; t++) w[(size_t)t * L.cout + c] = p[(size_t)c * kk + t];
+            p += (size_t)L.cout * kk;
+            for (int c = 0; c < L.cout; c++) b[c] = p[c];
+            p += L.cout;
+            VS_HIP(hipMalloc(&D.w, w.size() * sizeof(float)));
+            VS_HIP(hipMalloc(&D.b, b.size() * sizeof(float)));
+            VS_HIP(hipMemcpy(D.w, w.data(), w.size() * sizeof(float), hipMemcpyHostToDevice));
+            VS_HIP(hipMemcpy(D.b, b.data(), b.size() * sizeof(float), hipMemcpyHostToDevice));
+        } else {
+            D.cop = (L.cout + kCT - 1) / kCT * kCT;
+            std::vector<float> w((size_t)kk * L.cin * D.cop, 0.f), b(D.cop, 0.f);
+            for (int co = 0; co < L.cout; co++)
+                for (int ci = 0; ci < L.cin; ci++)
+                    for (int t = 0; t < kk; t++) w[((size_t)t * L.cin + ci) * D.cop + co] = p[((size_t)co * L.cin + ci) * kk + t];
+            p += (size_t)L.cout * L.cin * kk;
+            if (L.bias) {
+                for (int c = 0; c < L.cout; c++) b[c] = p[c];
+                p += L.cout;
+            }
+            VS_HIP(hipMalloc(&D.w, w.size() * sizeof(float)));
+            VS_HIP(hipMemcpy(D.w, w.data(), w.size() * sizeof(float), hipMemcpyHostToDevice));
+            if (L.bias) {
+                VS_HIP(hipMalloc(&D.b, b.size() * sizeof(float)));
+                VS_HIP(hipMemcpy(D.b, b.data(), b.size() * sizeof(float), hipMemcpyHostToDevice));
+            }
+        }
+    }
+    return VS_OK;
+}
+
+// tensor -> slot assignment by last use (a slot is reused once its tensor is dead)
+static void plan(vs_midas* m) {
+    const Net& N = net();
+    const int nt = (int)N.tdims.size() / 3;
+    std::vector<int> last(nt, -1);
+    for (int i = 0; i < (int)N.steps.size(); i++) {
+        const Step& s = N.steps[i];
+        for (int t : {s.in, s.res1, s.res2})
+            if (t >= 0) last[t] = i;
+    }
+    last[N.output] = (int)N.steps.size();
+    m->slot_of.assign(nt, -1);
+    std::vector<int> free_slots;
+    m->slot_of[N.input] = -2;  // the input lives in m->input
+    auto grab = [&](int t) {
+        const size_t need = (size_t)N.Hof(t) * N.Wof(t) * N.Cof(t);
+        int best = -1;
+        for (size_t j = 0; j < free_slots.size(); j++)
+            if (best < 0 || m->slot_elems[free_slots[j]] < m->slot_elems[free_slots[best]]) best = (int)j;
+        int slot;
+        if (best >= 0) {
+            slot = free_slots[best];
+            free_slots.erase(free_slots.begin() + best);
+        } else {
+            slot = (int)m->slot_elems.size();
+            m->slot_elems.push_back(0);
+        }
+        m->slot_elems[slot] = std::max(m->slot_elems[slot], need);
+        m->slot_of[t] = slot;
+    };
+    for (int i = 0; i < (int)N.steps.size(); i++) {
+        const Step& s = N.steps[i];
+        grab(s.out);
+        for (int t : {s.in, s.res1, s.res2})
+            if (t >= 0 && last[t] == i && m->slot_of[t] >= 0) free_slots.push_back(m->slot_of[t]);
+    }
+    m->slots.resize(m->slot_elems.size());
+}
+
+static float* tensor_ptr(vs_midas* m, int t) {
+    const int s = m->slot_of[t];
+    return s == -2 ? m->input.as<float>() : m->slots[s].as<float>();
+}
+
+static int ensure_batch(vs_midas* m, int B) {
+    if (B <= m->batch_cap) return VS_OK;
+    for (size_t i = 0; i < m->slots.size(); i++) VS_CHECK(m->slots[i].ensure((size_t)B * m->slot_elems[i] * sizeof(float)));
+    VS_CHECK(m->input.ensure((size_t)B * kIn * kIn * 3 * sizeof(float)));
+    m->batch_cap = B;
+    return VS_OK;
+}
+
+// network: m->input [B][256][256][3] -> returns the output tensor pointer [B][256][256]
+static int forward(vs_midas* m, int B, hipStream_t s, float** out) {
+    const Net& N = net();
+    VS_CHECK(ensure_batch(m, B));
+    ProfScope ps(m->ctx, "midas_net", s);
+    for (const Step& st : N.steps) {
+        if (st.kind == K_CONV) {
+            ConvArgs a{};
+            a.in = tensor_ptr(m, st.in);
+            a.w = m->dev[st.layer].w;
+            a.bias = m->dev[st.layer].b;
+            a.res1 = st.res1 >= 0 ? tensor_ptr(m, st.res1) : nullptr;
+            a.res2 = st.res2 >= 0 ? tensor_ptr(m, st.res2) : nullptr;
+            a.out = tensor_ptr(m, st.out);
+            a.B = B, a.H = st.H, a.W = st.W, a.C = st.C, a.Ho = st.Ho, a.Wo = st.Wo, a.Co = st.Co;
+            a.CoP = m->dev[st.layer].cop, a.k = st.k, a.stride = st.stride, a.pad_t = st.pad_t, a.pad_l = st.pad_l;
+            a.act = st.act, a.pre_relu = st.pre_relu;
+            const int npix = B * st.Ho * st.Wo;
+            hipLaunchKernelGGL(k_mid_conv, dim3((npix + kCT - 1) / kCT, a.CoP / kCT), dim3(256), 0, s, a);
+        } else if (st.kind == K_DW) {
+            const long n = (long)B * st.Ho * st.Wo * (st.C / 4);
+            hipLaunchKernelGGL(k_mid_dw, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, tensor_ptr(m, st.in),
+                               m->dev[st.layer].w, m->dev[st.layer].b, tensor_ptr(m, st.out), B, st.H, st.W, st.C,
+                               st.Ho, st.Wo, st.k, st.stride, st.pad_t, st.pad_l);
+        } else {
+            const long n = (long)B * st.Ho * st.Wo * (st.C / 4);
+            hipLaunchKernelGGL(k_mid_up, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, tensor_ptr(m, st.in),
+                               tensor_ptr(m, st.out), B, st.H, st.W, st.C, st.align_corners ? 1 : 0);
+        }
+    }
+    VS_HIP(hipGetLastError());
+    *out = tensor_ptr(m, N.output);
+    return VS_OK;
+}
+
+static int preprocess(vs_midas* m, int B, const uint8_t* d_bgr, int h, int w, hipStream_t s) {
+    VS_CHECK(ensure_batch(m, B));
+    ProfScope ps(m->ctx, "midas_pre", s);
+    const int n = B * kIn * kIn;
+    hipLaunchKernelGGL(k_mid_pre, dim3((n + 255) / 256), dim3(256), 0, s, d_bgr, h, w, B, m->input.as<float>());
+    VS_HIP(hipGetLastError());
+    return VS_OK;
+}
+
+static int postprocess(vs_midas* m, int B, const float* d_small, int h, int w, float* d_out, hipStream_t s) {
+    ProfScope ps(m->ctx, "midas_post", s);
+    const int nb = (h * w + 255) / 256;
+    VS_CHECK(m->post_part.ensure((size_t)B * nb * 2 * sizeof(float)));
+    hipLaunchKernelGGL(k_mid_post, dim3(nb, B), dim3(256), 0, s, d_small, B, h, w, d_out, m->post_part.as<float>());
+    hipLaunchKernelGGL(k_mid_norm, dim3(64, B), dim3(256), 0, s, d_out, m->post_part.as<float>(), nb, h * w);
+    VS_HIP(hipGetLastError());
+    return VS_OK;
+}
+
+}  // namespace midas
+}  // namespace vs
+
+using namespace vs;
+
+extern "C" {
+
+size_t vs_midas_num_params(void) { return midas::net().num_params(); }
+
+double vs_midas_flops_per_frame(void) { return midas::net().flops(); }
+
+int vs_midas_create(vs_ctx* ctx, const char* weights_path, vs_midas** out) {
+    VS_ARG(ctx && out, "vs_midas_create: null argument");
+    *out = nullptr;
+    VS_HIP(hipSetDevice(ctx->device));
+    auto* m = new (std::nothrow) vs_midas();
+    if (!m) return VS_ERR_NOMEM;
+    m->ctx = ctx;
+    const size_t np = midas::net().num_params();
+    if (weights_path) {
+        FILE* f = std::fopen(weights_path, "rb");
+        if (!f) {
+            delete m;
+            set_error(std::string("cannot open MiDaS weights ") + weights_path);
+            return VS_ERR_IO;
+        }
+        uint32_t magic = 0, version = 0;
+        uint64_t count = 0;
+        const bool okh = std::fread(&magic, 4, 1, f) == 1 && std::fread(&version, 4, 1, f) == 1 &&
+                         std::fread(&count, 8, 1, f) == 1;
+        if (!okh || magic != 0x574D5356u || version != 1 || count != np) {  // "VSMW"
+            std::fclose(f);
+            delete m;
+            set_error("malformed VSMW weight file");
+            return VS_ERR_IO;
+        }
+        m->h_weights.resize(np);
+        const bool okd = std::fread(m->h_weights.data(), sizeof(float), np, f) == np;
+        std::fclose(f);
+        if (!okd) {
+            delete m;
+            set_error("truncated VSMW weight file");
+            return VS_ERR_IO;
+        }
+    } else {
+        m->h_weights = midas::synth(VS_SYNTH_WEIGHT_SEED + 1);
+    }
+    int rc = midas::upload(m);
+    if (rc != VS_OK) {
+        vs_midas_destroy(m);
+        return rc;
+    }
+    midas::plan(m);
+    *out = m;
+    return VS_OK;
+}
+
+void vs_midas_destroy(vs_midas* m) {
+    if (!m) return;
+    (void)hipDeviceSynchronize();
+    for (auto& D : m->dev) {
+        if (D.w) (void)hipFree(D.w);
+        if (D.b) (void)hipFree(D.b);
+    }
+    for (auto& b : m->slots) b.release();
+    m->input.release();
+    m->post_part.release();
+    delete m;
+}
+
+int vs_midas_get_weights(vs_midas* m, float* out, size_t count) {
+    VS_ARG(m && out && count == m->h_weights.size(), "vs_midas_get_weights: bad arguments");
+    std::memcpy(out, m->h_weights.data(), count * sizeof(float));
+    return VS_OK;
+}
+
+int vs_midas_estimate_dev(vs_midas* m, int B, const uint8_t* d_bgr, int h, int w, float* d_depth, void* stream) {
+    VS_ARG(m && d_bgr && d_depth && B >= 1 && h >= 2 && w >= 2, "vs_midas_estimate_dev: bad arguments");
+    hipStream_t s = stream ? static_cast<hipStream_t>(stream) : m->ctx->stream;
+    VS_CHECK(midas::preprocess(m, B, d_bgr, h, w, s));
+    float* small = nullptr;
+    VS_CHECK(midas::forward(m, B, s, &small));
+    return midas::postprocess(m, B, small, h, w, d_depth, s);
+}
+
+int vs_midas_preprocess_dev(vs_midas* m, int B, const uint8_t* d_bgr, int h, int w, float* d_input, void* stream) {
+    VS_ARG(m && d_bgr && d_input && B >= 1 && h >= 2 && w >= 2, "vs_midas_preprocess_dev: bad arguments");
+    hipStream_t s = stream ? static_cast<hipStream_t>(stream) : m->ctx->stream;
+    VS_CHECK(midas::preprocess(m, B, d_bgr, h, w, s));
+    VS_HIP(hipMemcpyAsync(d_input, m->input.p, (size_t)B * 256 * 256 * 3 * sizeof(float), hipMemcpyDeviceToDevice, s));
+    return VS_OK;
+}
+
+int vs_midas_forward_dev(vs_midas* m, int B, const float* d_input, float* d_out, void* stream) {
+    VS_ARG(m && d_input && d_out && B >= 1, "vs_midas_forward_dev: bad arguments");
+    hipStream_t s = stream ? static_cast<hipStream_t>(stream) : m->ctx->stream;
+    VS_CHECK(midas::ensure_batch(m, B));
+    VS_HIP(hipMemcpyAsync(m->input.p, d_input, (size_t)B * 256 * 256 * 3 * sizeof(float), hipMemcpyDeviceToDevice, s));
+    float* small = nullptr;
+    VS_CHECK(midas::forward(m, B, s, &small));
+    VS_HIP(hipMemcpyAsync(d_out, small, (size_t)B * 256 * 256 * sizeof(float), hipMemcpyDeviceToDevice, s));
+    return VS_OK;
+}
+
+int vs_midas_postprocess_dev(vs_midas* m, int B, const float* d_small, int h, int w, float* d_depth, void* stream) {
+    VS_ARG(m && d_small && d_depth && B >= 1 && h >= 2 && w >= 2, "vs_midas_postprocess_dev: bad arguments");
+    hipStream_t s = stream ? static_cast<hipStream_t>(stream) : m->ctx->stream;
+    return midas::postprocess(m, B, d_small, h, w, d_depth, s);
+}
+
+}  // extern "C"

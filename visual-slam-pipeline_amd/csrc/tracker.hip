@@ -130,6 +130,9 @@ constexpr size_t kChainInts = 0, kChainDbl = 128, kChainGood = 128 + 36 * 8;
 constexpr size_t kChainKept = kChainGood + (size_t)kCap * sizeof(vs_match);
 constexpr size_t kChainRaw = kChainKept + (size_t)kCap * sizeof(vs_match);
 constexpr size_t kChainBytes = kChainRaw + (size_t)kCap * sizeof(vs_match);
+// chain header: pair slots, the 3D-3D seed, 0, then its MT19937 init_genrand state
+constexpr int kHdrWords = 4 + 624;
+constexpr size_t kHdrBytes = kHdrWords * sizeof(uint32_t);
 
 // Extraction chunks: the batch's network + post-processing runs chunk by chunk on the extraction
 // stream while the tracker consumes the chunks already done (process_batch_dev).  The first chunk
@@ -177,10 +180,11 @@ __global__ __launch_bounds__(1024) void k_pnp_gather(const int* __restrict__ kpm
 
 // Host-side wall time per back-end operation (VS_SLAM_HOST_PROFILE=1: printed to stderr when the
 // vs_slam is destroyed); the rest of process_frame is the tracker's own host logic.
-enum HostOp { kHChain, kHMatch, kHFmat, kHMotion, kHTlm, kHPnp, kHMatchMap, kHAppend, kHVis, kHFrame, kHWait, kHOps };
+enum HostOp { kHChain, kHMatch, kHFmat, kHMotion, kHTlm, kHPnp, kHMatchMap, kHAppend, kHVis, kHFrame, kHWait, kHSpec, kHOps };
 static const char* const kHostOpNames[kHOps] = {"chain", "match", "find_fundamental", "motion_points",
                                                 "track_local_map", "solve_pnp", "match_map", "map_append",
-                                                "visibility", "process_frame (total)", "extract wait"};
+                                                "visibility", "process_frame (total)", "extract wait",
+                                                "chain: speculation wait"};
 struct HostProf {
     bool on = false;
     long skip = 64;  // frames before counting starts (first launches load code objects)
@@ -211,12 +215,45 @@ struct GpuOps {
     std::vector<float> spec_obj, spec_img;
     hipStream_t s = nullptr;   // tracking stream (the context's stream is swapped to it during vs_slam calls)
     hipStream_t xs = nullptr;  // extraction stream
+    // Speculative front chain of the batch's next frame (see chain()): its own stream on the tracking
+    // CU set, result block, header, matcher key state and pinned host block [header | result].
+    hipStream_t s2 = nullptr;
+    hipEvent_t cspec_ev = nullptr;
+    DevBuf chain_buf2, hdr_buf2, mstate2;
+    Pinned cpin;
+    struct ChainSpec {
+        bool valid = false;
+        const vs_trk::Frame* cur = nullptr;
+        int ref_slot = -1, cur_slot = -1;
+        uint32_t seed = 0;
+    } cspec;
+    bool cspec_on = true;                       // VS_SLAM_SPEC_CHAIN=0 disables
+    const vs_trk::Frame* next_frame = nullptr;  // the batch's next frame (process_batch_dev)
+    hipEvent_t next_ready = nullptr;            // its extraction chunk's event
+    long cspec_hits = 0, cspec_launched = 0;
     bool own_streams = false;
-    std::vector<hipEvent_t> xev;  // one per extraction chunk
-    std::vector<int> xch;         // chunk boundaries (frame index of each chunk's first frame, then nb)
+    // One extraction in flight or in use: chunk boundaries (frame index of each chunk's first frame,
+    // then nb), one event per chunk, the pinned keypoints / counts, the batch region it writes and
+    // the caller's frame buffers.  Two sets: the batch being tracked and the next one, prefetched
+    // (vs_slam_prefetch_batch_dev) into the other region while this one is tracked.
+    struct XBatch {
+        std::vector<int> ch;
+        std::vector<hipEvent_t> ev;
+        Pinned pin;
+        int region = 0, nb = 0;
+        const uint8_t* bgr = nullptr;
+        const float* depth = nullptr;
+        bool pending = false;  // prefetched, not yet claimed by a process_batch_dev call
+    } xb[2];
+    int xcur = 0;                      // the set of the batch being tracked
+    struct {
+        int nb = 0;
+        const uint8_t* bgr = nullptr;
+        const float* depth = nullptr;
+    } hint;                            // the next batch, to prefetch behind the current one
+
     int first_chunk = kXFirst;    // VS_SLAM_FIRST_CHUNK overrides
     int chunk_growth = 13;        // next chunk = this one x growth / 10 (VS_SLAM_CHUNK_GROWTH overrides)
-    Pinned xpin;                  // keypoints / counts of the batch being extracted
     int B = 0, h = 0, w = 0, S = 0, batch_region = 0;
     double K[4] = {vs_trk::cfg::FX, vs_trk::cfg::FY, vs_trk::cfg::CX, vs_trk::cfg::CY};
     DevBuf pool_kps, pool_desc, pool_n, pool_depth, pool_norms, semi, dgrid;
@@ -252,11 +289,19 @@ struct GpuOps {
                 s = nullptr;
                 masked = false;
             }
+            if (masked && hipExtStreamCreateWithCUMask(&s2, words, tm.data()) != hipSuccess) {
+                (void)hipStreamDestroy(s);
+                (void)hipStreamDestroy(xs);
+                s = xs = nullptr;
+                masked = false;
+            }
         }
         if (!masked) {
             VS_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
             VS_HIP(hipStreamCreateWithFlags(&xs, hipStreamNonBlocking));
+            VS_HIP(hipStreamCreateWithFlags(&s2, hipStreamNonBlocking));
         }
+        VS_HIP(hipEventCreateWithFlags(&cspec_ev, hipEventDisableTiming));
         own_streams = true;
         return VS_OK;
     }
@@ -264,10 +309,15 @@ struct GpuOps {
         if (!own_streams) return;
         (void)hipStreamSynchronize(xs);
         (void)hipStreamSynchronize(s);
-        for (hipEvent_t e : xev) (void)hipEventDestroy(e);
-        xev.clear();
+        (void)hipStreamSynchronize(s2);
+        for (auto& X : xb) {
+            for (hipEvent_t e : X.ev) (void)hipEventDestroy(e);
+            X.ev.clear();
+        }
+        (void)hipEventDestroy(cspec_ev);
         (void)hipStreamDestroy(xs);
         (void)hipStreamDestroy(s);
+        (void)hipStreamDestroy(s2);
         own_streams = false;
     }
 
@@ -293,6 +343,14 @@ struct GpuOps {
         VS_CHECK(semi.ensure((size_t)B * hc * wc * VS_SEMI_CH * sizeof(float)));
         VS_CHECK(dgrid.ensure((size_t)B * hc * wc * VS_DESC_DIM * sizeof(float)));
         VS_CHECK(chain_buf.ensure(kChainBytes));
+        VS_CHECK(chain_buf2.ensure(kChainBytes));
+        VS_CHECK(hdr_buf.ensure(kHdrBytes));
+        VS_CHECK(hdr_buf2.ensure(kHdrBytes));
+        VS_CHECK(mstate2.ensure(2 * kCap * sizeof(unsigned long long) + 256));
+        VS_HIP(hipMemsetAsync(mstate2.p, 0xFF, 2 * kCap * sizeof(unsigned long long), s));
+        VS_HIP(hipMemsetAsync(mstate2.as<char>() + 2 * kCap * sizeof(unsigned long long), 0, 256, s));
+        VS_CHECK(cpin.reserve(kHdrBytes + kChainRaw + 64));
+        if (const char* e = std::getenv("VS_SLAM_SPEC_CHAIN")) cspec_on = e[0] != '0';
         VS_CHECK(pin.reserve((size_t)4 << 20));
         owner.assign(kPersist, nullptr);
         VS_CHECK(grow_map(1 << 16));
@@ -405,25 +463,28 @@ struct GpuOps {
     // depth copied beside them, keypoints back to pinned host memory, kXChunk frames at a time on
     // the extraction stream; chunk c's event marks its slots and host keypoints ready.  Enqueue
     // only: wait_chunk() hands a chunk to the tracker.
-    int extract_batch(std::vector<vs_trk::FramePtr>& frames, const uint8_t* d_bgr, const float* d_depth) {
-        const int nb = (int)frames.size();
-        const int s0 = batch_region * B;
+    int enqueue_extraction(XBatch& X, int nb, const uint8_t* d_bgr, const float* d_depth) {
+        X.region = batch_region;
         batch_region ^= 1;
-        xch.assign(1, 0);
-        for (int c = first_chunk; xch.back() < nb; c = std::min(kXChunk, std::max(c + 1, (c * chunk_growth + 5) / 10)))
-            xch.push_back(std::min(nb, xch.back() + c));
-        const int nch = (int)xch.size() - 1;
-        while ((int)xev.size() < nch) {
+        X.nb = nb;
+        X.bgr = d_bgr;
+        X.depth = d_depth;
+        const int s0 = X.region * B;
+        X.ch.assign(1, 0);
+        for (int c = first_chunk; X.ch.back() < nb; c = std::min(kXChunk, std::max(c + 1, (c * chunk_growth + 5) / 10)))
+            X.ch.push_back(std::min(nb, X.ch.back() + c));
+        const int nch = (int)X.ch.size() - 1;
+        while ((int)X.ev.size() < nch) {
             hipEvent_t e;
             VS_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-            xev.push_back(e);
+            X.ev.push_back(e);
         }
-        VS_CHECK(xpin.reserve((size_t)nb * kCap * sizeof(vs_keypoint) + (size_t)nb * sizeof(int) + 64));
-        char* hk = xpin.base;
+        VS_CHECK(X.pin.reserve((size_t)nb * kCap * sizeof(vs_keypoint) + (size_t)nb * sizeof(int) + 64));
+        char* hk = X.pin.base;
         int* hn = reinterpret_cast<int*>(hk + (size_t)nb * kCap * sizeof(vs_keypoint));
         const int hc = (h + 7) / 8, wc = (w + 7) / 8;
         for (int c = 0; c < nch; c++) {
-            const int f0 = xch[c], m = xch[c + 1] - xch[c];
+            const int f0 = X.ch[c], m = X.ch[c + 1] - X.ch[c];
             VS_CHECK(sp_forward(ctx, m, d_bgr + (size_t)f0 * h * w * 3, 3, h, w, xs, semi.as<float>(),
                                 dgrid.as<float>()));
             VS_CHECK(sp_postprocess(ctx, m, hc, wc, h, w, kps_of(s0 + f0), desc_of(s0 + f0), pool_n.as<int>() + s0 + f0,
@@ -438,9 +499,35 @@ struct GpuOps {
             VS_HIP(hipMemcpyAsync(hk + (size_t)f0 * kCap * sizeof(vs_keypoint), kps_of(s0 + f0),
                                   (size_t)m * kCap * sizeof(vs_keypoint), hipMemcpyDeviceToHost, xs));
             VS_HIP(hipMemcpyAsync(hn + f0, pool_n.as<int>() + s0 + f0, (size_t)m * sizeof(int), hipMemcpyDeviceToHost, xs));
-            VS_HIP(hipEventRecord(xev[c], xs));
+            VS_HIP(hipEventRecord(X.ev[c], xs));
         }
-        for (int b = 0; b < nb; b++) frames[b]->slot = s0 + b;
+        return VS_OK;
+    }
+    // The batch's extraction: the one prefetched for exactly these buffers, or enqueued now; then the
+    // hinted next batch is prefetched behind it into the other region (free: the previous batch's
+    // live frames moved to persistent slots when it settled).
+    int extract_batch(std::vector<vs_trk::FramePtr>& frames, const uint8_t* d_bgr, const float* d_depth) {
+        const int nb = (int)frames.size();
+        XBatch& P = xb[xcur ^ 1];
+        if (P.pending && !(P.bgr == d_bgr && P.depth == d_depth && P.nb == nb)) {
+            VS_HIP(hipStreamSynchronize(xs));  // a stale prefetch: let it land, its region is free again
+            P.pending = false;
+            batch_region = P.region;
+        }
+        xcur ^= 1;
+        XBatch& X = xb[xcur];
+        if (X.pending) {
+            X.pending = false;
+        } else {
+            VS_CHECK(enqueue_extraction(X, nb, d_bgr, d_depth));
+        }
+        for (int b = 0; b < nb; b++) frames[b]->slot = X.region * B + b;
+        if (hint.nb > 0) {
+            XBatch& N = xb[xcur ^ 1];
+            VS_CHECK(enqueue_extraction(N, hint.nb, hint.bgr, hint.depth));
+            N.pending = true;
+            hint.nb = 0;
+        }
         return VS_OK;
     }
     // Chunk c of the batch is extracted: its keypoints to the frames, and the tracking stream
@@ -448,10 +535,11 @@ struct GpuOps {
     int wait_chunk(std::vector<vs_trk::FramePtr>& frames, int c) {
         HostTimer ht(hprof, kHWait);
         const int nb = (int)frames.size();
-        const int f0 = xch[c], m = xch[c + 1] - xch[c];
-        VS_HIP(hipEventSynchronize(xev[c]));
-        VS_HIP(hipStreamWaitEvent(s, xev[c], 0));
-        const char* hk = xpin.base;
+        const XBatch& X = xb[xcur];
+        const int f0 = X.ch[c], m = X.ch[c + 1] - X.ch[c];
+        VS_HIP(hipEventSynchronize(X.ev[c]));
+        VS_HIP(hipStreamWaitEvent(s, X.ev[c], 0));
+        const char* hk = X.pin.base;
         const int* hn = reinterpret_cast<const int*>(hk + (size_t)nb * kCap * sizeof(vs_keypoint));
         for (int b = f0; b < f0 + m; b++) {
             const int n = hn[b];
@@ -487,42 +575,41 @@ struct GpuOps {
                            meta + 4, s, pool_norms.as<float>());
     }
 
-    vs_trk::ChainResult chain_impl(const vs_trk::Frame& ref, const vs_trk::Frame& cur, uint32_t seed) {
-        vs_trk::ChainResult R;
-        char* c = chain_buf.as<char>();
-        int* di = reinterpret_cast<int*>(c + kChainInts);
-        double* dd = reinterpret_cast<double*>(c + kChainDbl);
-        vs_match* good = reinterpret_cast<vs_match*>(c + kChainGood);
-        vs_match* kept = reinterpret_cast<vs_match*>(c + kChainKept);
-        // one upload: pair slots, the 3D-3D seed and its MT19937 init_genrand state (624 serial
-        // steps, cheaper on the host than on one GPU lane)
-        uint32_t hdr[4 + 624];
-        hdr[0] = (uint32_t)ref.slot;
-        hdr[1] = (uint32_t)cur.slot;
+    // one header: pair slots, the 3D-3D seed and its MT19937 init_genrand state (624 serial steps,
+    // cheaper on the host than on one GPU lane)
+    static void fill_hdr(uint32_t* hdr, int ref_slot, int cur_slot, uint32_t seed) {
+        hdr[0] = (uint32_t)ref_slot;
+        hdr[1] = (uint32_t)cur_slot;
         hdr[2] = seed;
         hdr[3] = 0;
         hdr[4] = seed;
         for (int i = 1; i < 624; i++) hdr[4 + i] = 1812433253u * (hdr[3 + i] ^ (hdr[3 + i] >> 30)) + (uint32_t)i;
-        if (failed(hdr_buf.ensure(sizeof(hdr))) || failed(upload(hdr_buf.p, hdr, sizeof(hdr)))) return R;
-        const int* dh = hdr_buf.as<int>();
-        if (failed(match_pairs(ctx, 1, dh, S, pool_desc.as<float>(), pool_n.as<int>(), kCap,
-                               vs_trk::cfg::L2_RATIO_THRESHOLD, reinterpret_cast<vs_match*>(c + kChainRaw), di + 3,
-                               good, di + 4, s, pool_norms.as<float>())))
-            return R;
-        if (failed(fmat_pairs(ctx, 1, dh, pool_kps.as<vs_keypoint>(), kCap, good, di + 4, dd, kept, di + 5, dd + 9,
-                              di + 8, s)))
-            return R;
-        if (failed(ransac3d_pairs(ctx, 1, dh, pool_kps.as<vs_keypoint>(), kCap, kept, di + 5, pool_depth.as<float>(), h,
-                                  w, K, reinterpret_cast<const uint32_t*>(dh + 2), 200, 0.05, dd + 11, dd + 20, di + 6,
-                                  di + 16, s, reinterpret_cast<const uint32_t*>(dh + 4))))
-            return R;
-        if (failed(emat_pairs(ctx, 1, dh, pool_kps.as<vs_keypoint>(), kCap, kept, di + 5, di + 6, pool_depth.as<float>(),
-                              h, w, K, dd + 23, dd + 32, dd + 35, di + 7, di + 20, s)))
-            return R;
-        char* hc = take(kChainRaw);
-        if (!hc || failed(d2h(hc, c, kChainRaw)))
-            return R;
-        if (failed(sync())) return R;
+    }
+    // match -> F verification -> 3D-3D -> E fallback for the pair in the header, on stream st, into
+    // the result block cbuf, copied back to hout (pinned); keys / cnt: the matcher's key state
+    // (nullptr: the context's)
+    int enqueue_chain(hipStream_t st, char* cbuf, int* dh, const uint32_t* hhdr, char* hout, unsigned long long* keys,
+                      unsigned* cnt) {
+        int* di = reinterpret_cast<int*>(cbuf + kChainInts);
+        double* dd = reinterpret_cast<double*>(cbuf + kChainDbl);
+        vs_match* good = reinterpret_cast<vs_match*>(cbuf + kChainGood);
+        vs_match* kept = reinterpret_cast<vs_match*>(cbuf + kChainKept);
+        VS_HIP(hipMemcpyAsync(dh, hhdr, kHdrBytes, hipMemcpyHostToDevice, st));
+        VS_CHECK(match_pairs(ctx, 1, dh, S, pool_desc.as<float>(), pool_n.as<int>(), kCap, vs_trk::cfg::L2_RATIO_THRESHOLD,
+                             reinterpret_cast<vs_match*>(cbuf + kChainRaw), di + 3, good, di + 4, st,
+                             pool_norms.as<float>(), keys, cnt));
+        VS_CHECK(fmat_pairs(ctx, 1, dh, pool_kps.as<vs_keypoint>(), kCap, good, di + 4, dd, kept, di + 5, dd + 9, di + 8,
+                            st));
+        VS_CHECK(ransac3d_pairs(ctx, 1, dh, pool_kps.as<vs_keypoint>(), kCap, kept, di + 5, pool_depth.as<float>(), h, w,
+                                K, reinterpret_cast<const uint32_t*>(dh + 2), 200, 0.05, dd + 11, dd + 20, di + 6, di + 16,
+                                st, reinterpret_cast<const uint32_t*>(dh + 4)));
+        VS_CHECK(emat_pairs(ctx, 1, dh, pool_kps.as<vs_keypoint>(), kCap, kept, di + 5, di + 6, pool_depth.as<float>(), h,
+                            w, K, dd + 23, dd + 32, dd + 35, di + 7, di + 20, st));
+        VS_HIP(hipMemcpyAsync(hout, cbuf, kChainRaw, hipMemcpyDeviceToHost, st));
+        return VS_OK;
+    }
+    static vs_trk::ChainResult parse_chain(const char* hc) {
+        vs_trk::ChainResult R;
         const int* hi = reinterpret_cast<const int*>(hc + kChainInts);
         const double* hd = reinterpret_cast<const double*>(hc + kChainDbl);
         const auto* hg = reinterpret_cast<const vs_trk::Match*>(hc + kChainGood);
@@ -543,9 +630,61 @@ struct GpuOps {
         R.scale = hd[35];
         return R;
     }
+    vs_trk::ChainResult chain_impl(const vs_trk::Frame& ref, const vs_trk::Frame& cur, uint32_t seed) {
+        uint32_t* hh = reinterpret_cast<uint32_t*>(take(kHdrBytes));
+        if (!hh) return vs_trk::ChainResult();
+        fill_hdr(hh, ref.slot, cur.slot, seed);
+        char* hc = take(kChainRaw);
+        if (!hc || failed(enqueue_chain(s, chain_buf.as<char>(), hdr_buf.as<int>(), hh, hc, nullptr, nullptr)) ||
+            failed(sync()))
+            return vs_trk::ChainResult();
+        return parse_chain(hc);
+    }
+    // The chain of the batch's next frame against this call's reference frame with the next seed,
+    // on s2 beside this frame's local-map tracking and PnP: it is the next frame's chain whenever
+    // this frame neither becomes a keyframe nor is rejected (the reference frame and the processed
+    // count then carry over, Slam.cpp:838, 276).  chain() uses it only when slots and seed match.
+    int launch_spec_chain(int ref_slot, const vs_trk::Frame& nxt, uint32_t seed) {
+        VS_HIP(hipEventSynchronize(cspec_ev));  // the previous speculation released cpin / chain_buf2
+        uint32_t* hh = reinterpret_cast<uint32_t*>(cpin.base);
+        fill_hdr(hh, ref_slot, nxt.slot, seed);
+        if (next_ready) VS_HIP(hipStreamWaitEvent(s2, next_ready, 0));  // its extraction chunk
+        unsigned long long* keys = mstate2.as<unsigned long long>();
+        unsigned* cnt = reinterpret_cast<unsigned*>(mstate2.as<char>() + 2 * kCap * sizeof(unsigned long long));
+        VS_CHECK(enqueue_chain(s2, chain_buf2.as<char>(), hdr_buf2.as<int>(), hh, cpin.base + kHdrBytes, keys, cnt));
+        VS_HIP(hipEventRecord(cspec_ev, s2));
+        cspec.valid = true;
+        cspec.cur = &nxt;
+        cspec.ref_slot = ref_slot;
+        cspec.cur_slot = nxt.slot;
+        cspec.seed = seed;
+        cspec_launched++;
+        return VS_OK;
+    }
     vs_trk::ChainResult chain(const vs_trk::Frame& ref, const vs_trk::Frame& cur, uint32_t seed) {
         HostTimer ht(hprof, kHChain);
-        return chain_impl(ref, cur, seed);
+        vs_trk::ChainResult R;
+        const bool hit = cspec.valid && cspec.cur == &cur && cspec.ref_slot == ref.slot && cspec.cur_slot == cur.slot &&
+                         cspec.seed == seed;
+        cspec.valid = false;
+        if (hit) {
+            HostTimer hw(hprof, kHSpec);
+            if (failed(hipEventSynchronize(cspec_ev) == hipSuccess ? VS_OK : VS_ERR_HIP)) return R;
+            R = parse_chain(cpin.base + kHdrBytes);
+            cspec_hits++;
+        } else {
+            R = chain_impl(ref, cur, seed);
+        }
+        // The next frame's reference is this one's unless this frame becomes a keyframe, which the
+        // rules of Slam.cpp:1061-1072 / is_keyframe (:1360) predict from the frame-id gap and this
+        // chain's match count; a wrong guess only costs the speculation.
+        if (cspec_on && err == VS_OK && next_frame && next_frame != &cur && next_frame->slot >= 0 && ref.slot >= 0) {
+            const int ng = (int)R.good.size(), gap = cur.id - ref.id;
+            const bool kf = (gap >= vs_trk::cfg::KF_MIN_FRAME_GAP && ng >= vs_trk::cfg::KF_MIN_MATCHES) ||
+                            (ng < 2 * vs_trk::cfg::MIN_MATCHES && gap >= 5);
+            failed(launch_spec_chain(kf && cur.slot >= 0 ? cur.slot : ref.slot, *next_frame, seed + 1u));
+        }
+        return R;
     }
 
     std::vector<vs_trk::Match> match(const vs_trk::Frame& a, const vs_trk::Frame& b, float ratio) {
@@ -824,6 +963,7 @@ struct CtxStream {
 int settle(vs_slam* sl) {
     GpuOps& o = sl->ops;
     auto& T = *sl->trk;
+    VS_HIP(hipStreamWaitEvent(o.s, o.cspec_ev, 0));  // a discarded speculation still reads the pool
     for (int i = 0; i < kPersist; i++) {
         vs_trk::Frame* f = o.owner[i];
         if (f && !T.is_live(f)) {
@@ -891,10 +1031,12 @@ void vs_slam_destroy(vs_slam* sl) {
             if (o.hprof.n[k])
                 std::fprintf(stderr, "vs_slam host %-22s %8ld calls %10.3f ms  %8.1f us/call\n", kHostOpNames[k],
                              o.hprof.n[k], o.hprof.ms[k], 1e3 * o.hprof.ms[k] / o.hprof.n[k]);
+    if (o.hprof.on)
+        std::fprintf(stderr, "vs_slam speculative chains: %ld launched, %ld used\n", o.cspec_launched, o.cspec_hits);
     o.destroy_streams();
     DevBuf* bufs[] = {&o.pool_kps, &o.pool_desc, &o.pool_n, &o.pool_depth, &o.pool_norms, &o.semi, &o.dgrid,
                       &o.chain_buf,    &o.work, &o.rows_buf,      &o.map_pos, &o.map_desc,  &o.map_valid, &o.map_tmp,
-                      &o.pnp_io,       &o.hdr_buf};
+                      &o.pnp_io,       &o.hdr_buf, &o.chain_buf2, &o.hdr_buf2, &o.mstate2};
     for (DevBuf* b : bufs) b->release();
     if (sl->trace) std::fclose(sl->trace);
     delete sl;
@@ -919,6 +1061,15 @@ int vs_slam_set_accelerometer(vs_slam* sl, const double* samples, int n) {
     return VS_OK;
 }
 
+int vs_slam_prefetch_batch_dev(vs_slam* sl, int B, const uint8_t* d_bgr, const float* d_depth) {
+    VS_ARG(sl && d_bgr, "vs_slam_prefetch_batch_dev: null argument");
+    VS_ARG(B >= 1 && B <= sl->ops.B, "vs_slam_prefetch_batch_dev: B out of range");
+    sl->ops.hint.nb = B;
+    sl->ops.hint.bgr = d_bgr;
+    sl->ops.hint.depth = d_depth;
+    return VS_OK;
+}
+
 int vs_slam_process_batch_dev(vs_slam* sl, int B, const uint8_t* d_bgr, const float* d_depth,
                               const float* const* h_depth, const double* timestamps, const int* ids, int* processed) {
     VS_ARG(sl && d_bgr && timestamps && ids && processed, "vs_slam_process_batch_dev: null argument");
@@ -939,8 +1090,12 @@ int vs_slam_process_batch_dev(vs_slam* sl, int B, const uint8_t* d_bgr, const fl
     }
     int rc = o.extract_batch(sl->batch, d_bgr, d_depth);
     for (int b = 0, c = 0; b < B && rc == VS_OK; b++) {
-        if (b == o.xch[c]) rc = o.wait_chunk(sl->batch, c++);
+        const auto& X = o.xb[o.xcur];
+        if (b == X.ch[c]) rc = o.wait_chunk(sl->batch, c++);
         if (rc != VS_OK) break;
+        // the next frame and its chunk's event, for the speculative chain (chain())
+        o.next_frame = b + 1 < B ? sl->batch[b + 1].get() : nullptr;
+        o.next_ready = b + 1 < B ? X.ev[b + 1 == X.ch[c] ? c : c - 1] : nullptr;
         if (o.hprof_armed && --o.hprof.skip < 0) o.hprof.on = true, o.hprof_armed = false;
         {
             HostTimer ht(o.hprof, kHFrame);
@@ -951,8 +1106,12 @@ int vs_slam_process_batch_dev(vs_slam* sl, int B, const uint8_t* d_bgr, const fl
             o.err = VS_OK;
         }
     }
+    o.next_frame = nullptr;
+    o.next_ready = nullptr;
+    o.cspec.valid = false;
     if (rc != VS_OK) {
         (void)hipStreamSynchronize(o.xs);  // nothing may still write the pool after an error
+        (void)hipStreamSynchronize(o.s2);
         return rc;
     }
     return settle(sl);

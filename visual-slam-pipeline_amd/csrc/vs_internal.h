@@ -126,7 +126,8 @@ int sp_postprocess(vs_ctx* ctx, int B, int hc, int wc, int h, int w, vs_keypoint
 int match_pairs(vs_ctx* ctx, int P, const int* d_pairs, int F, const float* d_desc,
                 const int* d_n, int cap, float ratio, vs_match* d_raw, int* d_nraw,
                 vs_match* d_good, int* d_ngood, hipStream_t s,
-                const float* d_norms = nullptr);  // [F][cap] row norms when already known
+                const float* d_norms = nullptr, unsigned long long* d_keys = nullptr,
+                unsigned* d_cnt = nullptr);  // [F][cap] row norms when already known
 // Sequential-fmaf squared norms of the descriptor rows of F frames ([F][cap], rows >= n[f] untouched).
 int desc_norms(vs_ctx* ctx, int F, const float* d_desc, const int* d_n, int cap, float* d_norms, hipStream_t s);
 // 3D-3D RANSAC

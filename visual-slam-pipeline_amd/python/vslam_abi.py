@@ -70,6 +70,7 @@ _SIG = {
     "vs_slam_set_initial_pose": (_I, [_P, _P, _P]),
     "vs_slam_set_accelerometer": (_I, [_P, _P, _I]),
     "vs_slam_process_batch_dev": (_I, [_P, _I, _P, _P, _P, _P, _P, _P]),
+    "vs_slam_prefetch_batch_dev": (_I, [_P, _I, _P, _P]),
     "vs_slam_process_features": (_I, [_P, _I, _P, _P, _P, ctypes.c_double, _I, _P]),
     "vs_slam_finish": (_I, [_P]),
     "vs_slam_trajectory": (_I, [_P, _I, _P, _P, _P, _P, _P]),
@@ -464,6 +465,10 @@ class Slam:
         _check(self.lib.vs_slam_process_batch_dev(self.h, B, d_bgr, d_depth, ctypes.cast(ptrs, ctypes.c_void_p),
                                                   _ptr(ts), _ptr(fid), _ptr(out)))
         return out.astype(bool)
+
+    def prefetch_batch_dev(self, B, d_bgr, d_depth):
+        """The next process_batch_dev call's device frames: extracted behind the current batch."""
+        _check(self.lib.vs_slam_prefetch_batch_dev(self.h, B, d_bgr, d_depth))
 
     def process_features(self, kps, desc, depth, timestamp, frame_id):
         k = np.ascontiguousarray(kps, KEYPOINT_DTYPE)
