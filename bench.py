@@ -19,11 +19,12 @@ frontend_batch — BASELINE config[3], offline batch: each rank extracts its blo
 frames, matches consecutive pairs and runs F verification + 3D-3D (+E) per pair (DevicePipeline);
 with N > 1 the per-frame feature records are all-gathered over RCCL every step.
 
-monocular_hd — BASELINE config[4] without the depth network: a synthetic 1280x720 stream (the build's
-HD camera synth.K_HD) through the same front end with no depth: extract + match + F verification +
-essential-matrix RANSAC / recoverPose per pair, poses chained at the reference's fallback scale
-(Slam.cpp:976-980), ATE after sim(3) alignment.  MiDaS (DepthEstimator.cpp) is not built: its
-weights are not shipped and the reference never consumes its output.
+monocular_hd — BASELINE config[4]: a synthetic 1280x720 stream (the build's HD camera synth.K_HD)
+through DepthEstimator::estimate (MiDaS v2.1-small at 256x256, seeded weights: the reference ships
+none; its output is kept but, as in the reference, not consumed) and the front end with no depth:
+extract + match + F verification + essential-matrix RANSAC / recoverPose per pair, poses chained at
+the reference's fallback scale (Slam.cpp:976-980), ATE after sim(3) alignment; MiDaS has its own
+roofline line (midas.roofline).
 
 roofline — the dominant throughput-bound kernel (the fused SuperPoint conv1, fp32 MFMA) measured
 with HIP events on its stream during the timed region (the tracker extracts each batch in growing
@@ -251,7 +252,10 @@ def monocular_hd(ctx, B, rank, world, steps, warmup, workers):
     dev = torch.device("cuda", torch.cuda.current_device())
     bgr = torch.from_numpy(Lh["bgr"]).to(dev)
     del Lh["bgr"], Lh["depth"]
-    pipe = DevicePipeline(ctx, B, synth.H_HD, synth.W_HD, K=synth.K_HD, rank=rank, world=world, monocular=True)
+    import vslam_abi
+    midas = vslam_abi.Midas(ctx)  # DepthEstimator (MiDaS v2.1-small, seeded weights) per frame
+    pipe = DevicePipeline(ctx, B, synth.H_HD, synth.W_HD, K=synth.K_HD, rank=rank, world=world, monocular=True,
+                          midas=midas)
     chain, est, gidx = PoseChain(), [], []
 
     def run(first, count, track):
@@ -277,23 +281,45 @@ def monocular_hd(ctx, B, rank, world, steps, warmup, workers):
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    ctx.profile(True)
+    ctx.profile_reset()
     t0 = time.perf_counter()
     run(warmup, steps, True)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     el = time.perf_counter() - t0
+    prof = ctx.profile_read()
+    ctx.profile(False)
+    midas.close()
     if world > 1:
         tt = torch.tensor([el], dtype=torch.float64, device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         el = float(tt.item())
     res = {"value": round(world * B * steps / el, 3), "unit": "frames/s", "ms_per_step": round(el / steps * 1e3, 3),
            "steps": steps, "frames_per_gpu_per_step": B, "resolution": "1280x720", "K": list(synth.K_HD),
-           "workload": "config[4] monocular stream without the MiDaS network: per-GPU SuperPoint extract + ratio "
-                       "matching + F-RANSAC + essential-matrix RANSAC / recoverPose over consecutive frame pairs, "
-                       "scale-less (MOTION_SCALE) pose chain; the device-side gather of the batch frames is inside the step",
+           "workload": "config[4] monocular stream: per-GPU MiDaS v2.1-small depth (DepthEstimator) + SuperPoint "
+                       "extract + ratio matching + F-RANSAC + essential-matrix RANSAC / recoverPose over consecutive "
+                       "frame pairs, scale-less (MOTION_SCALE) pose chain; the device-side gather of the batch frames "
+                       "is inside the step",
            "parallelism": f"frame-sharded x{world}" + (" + RCCL all-gather of feature records" if world > 1 else ""),
            "render_s": round(render_s, 1)}
+    mn = prof.get("midas_net")
+    if mn and mn[1]:
+        avg_s = mn[0] / 1e3 / mn[1]
+        fl = vslam_abi.Midas.flops_per_frame() * B
+        res["midas"] = {
+            "what": "DepthEstimator::estimate per frame (DepthEstimator.cpp:39-112): MiDaS v2.1-small at 256x256 "
+                    "(seeded weights) with the reference's resize / normalisation around it; output kept, not "
+                    "consumed (as in the reference)",
+            "roofline": {"kernel": "midas_net (all k_mid_conv / k_mid_dw / k_mid_up launches of one batch)",
+                         "bound": "mfma", "achieved": round(fl / avg_s / 1e12, 3), "peak": FP32_MFMA_PEAK_TFLOPS,
+                         "unit": "TFLOP/s", "frac": round(fl / avg_s / 1e12 / FP32_MFMA_PEAK_TFLOPS, 4),
+                         "flops_per_frame": vslam_abi.Midas.flops_per_frame(), "frames_per_launch": B,
+                         "avg_batch_ms": round(avg_s * 1e3, 3),
+                         "note": "shares the chip with the pipeline's SuperPoint network and geometry streams"},
+            "stage_ms_per_frame": {k: round(prof[k][0] / (B * steps), 4) for k in ("midas_pre", "midas_net", "midas_post")
+                                   if k in prof}}
     if world == 1 and est:
         ts = np.arange(len(est), dtype=np.float64)
         a = ate.compute_ate(ts, np.array(est), ts, Lh["t_wc"][np.array(gidx)])

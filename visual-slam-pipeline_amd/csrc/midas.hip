@@ -29,6 +29,7 @@
 
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -615,9 +616,11 @@ static void plan(vs_midas* m) {
         m->slot_elems[slot] = std::max(m->slot_elems[slot], need);
         m->slot_of[t] = slot;
     };
+    const bool keep_all = std::getenv("VS_MIDAS_KEEP_TENSORS") != nullptr;  // debugging: every tensor its own slot
     for (int i = 0; i < (int)N.steps.size(); i++) {
         const Step& s = N.steps[i];
         grab(s.out);
+        if (keep_all) continue;
         for (int t : {s.in, s.res1, s.res2})
             if (t >= 0 && last[t] == i && m->slot_of[t] >= 0) free_slots.push_back(m->slot_of[t]);
     }
@@ -793,6 +796,20 @@ int vs_midas_forward_dev(vs_midas* m, int B, const float* d_input, float* d_out,
     VS_CHECK(midas::forward(m, B, s, &small));
     VS_HIP(hipMemcpyAsync(d_out, small, (size_t)B * 256 * 256 * sizeof(float), hipMemcpyDeviceToDevice, s));
     return VS_OK;
+}
+
+// Debugging (VS_MIDAS_KEEP_TENSORS set at create): frame 0 of the output tensor of step i after
+// the last forward ([Ho][Wo][Co] floats); returns the element count, or < 0.
+long vs_midas_debug_step(vs_midas* m, int i, float* out) {
+    const auto& N = midas::net();
+    if (!m || i < 0 || i >= (int)N.steps.size()) return VS_ERR_ARG;
+    const auto& st = N.steps[i];
+    const long n = (long)st.Ho * st.Wo * st.Co;
+    if (out) {
+        VS_HIP(hipDeviceSynchronize());
+        VS_HIP(hipMemcpy(out, midas::tensor_ptr(m, st.out), n * sizeof(float), hipMemcpyDeviceToHost));
+    }
+    return n;
 }
 
 int vs_midas_postprocess_dev(vs_midas* m, int B, const float* d_small, int h, int w, float* d_depth, void* stream) {

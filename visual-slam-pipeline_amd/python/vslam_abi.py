@@ -76,7 +76,16 @@ _SIG = {
     "vs_slam_trajectory": (_I, [_P, _I, _P, _P, _P, _P, _P]),
     "vs_slam_stats": (_I, [_P, _P, _I]),
     "vs_slam_map": (_I, [_P, _I, _P, _P, _P]),
-    "vs_spcf_write": (_I, [ctypes.c_char_p, _I, _P, _P, _P, _P, _I, _I]),
+    "vs_midas_create": (_I, [_P, ctypes.c_char_p, ctypes.POINTER(_P)]),
+    "vs_midas_destroy": (None, [_P]),
+    "vs_midas_num_params": (ctypes.c_size_t, []),
+    "vs_midas_flops_per_frame": (ctypes.c_double, []),
+    "vs_midas_get_weights": (_I, [_P, _P, ctypes.c_size_t]),
+    "vs_midas_estimate_dev": (_I, [_P, _I, _P, _I, _I, _P, _P]),
+    "vs_midas_preprocess_dev": (_I, [_P, _I, _P, _I, _I, _P, _P]),
+    "vs_midas_forward_dev": (_I, [_P, _I, _P, _P, _P]),
+    "vs_midas_postprocess_dev": (_I, [_P, _I, _P, _I, _I, _P, _P]),
+    "vs_spcf_write": (ctypes.c_int, [ctypes.c_char_p, _I, _P, _P, _P, _P, _I, _I]),
     "vs_spcf_write_dev": (_I, [_P, ctypes.c_char_p, _I, _P, _P, _P, _P, _I, _I, _P]),
     "vs_spcf_read": (_I, [ctypes.c_char_p, _I, _I, _P, _P, _P, _P, _P]),
     "vs_profile_enable": (_I, [_P, _I]),
@@ -547,3 +556,60 @@ def spcf_read(path, cap=SP_MAX_KEYPOINTS):
         _check(_lib.vs_spcf_read(os.fsencode(path), E, cap, _ptr(idx), _ptr(kps), _ptr(desc), _ptr(n),
                                  ctypes.byref(cnt)))
     return idx[:E], kps[:E], desc[:E], n[:E]
+
+
+# ---- F3: DepthEstimator (MiDaS v2.1-small) ----------------------------------------------------
+class Midas:
+    """vs_midas: DepthEstimator::estimate (DepthEstimator.cpp:39-112) on the GPU.  Device entry
+    points take device pointers (ints); weights() returns the canonical flat weights (per layer
+    [cout][cin][k][k] + [cout] bias, depthwise [c][k][k] + [c]; tests/midas_ref.py reads them)."""
+
+    def __init__(self, ctx, weights_path=None):
+        self.ctx = ctx
+        self.lib = ctx.lib
+        h = ctypes.c_void_p()
+        _check(self.lib.vs_midas_create(ctx.h, None if weights_path is None else os.fsencode(weights_path),
+                                        ctypes.byref(h)))
+        self.h = h
+
+    def close(self):
+        if self.h:
+            self.lib.vs_midas_destroy(self.h)
+            self.h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    @staticmethod
+    def num_params():
+        return int(load_library().vs_midas_num_params())
+
+    @staticmethod
+    def flops_per_frame():
+        return float(load_library().vs_midas_flops_per_frame())
+
+    def weights(self):
+        w = np.zeros(self.num_params(), np.float32)
+        _check(self.lib.vs_midas_get_weights(self.h, _ptr(w), w.size))
+        return w
+
+    def save_weights(self, path):
+        w = self.weights()
+        with open(path, "wb") as f:
+            f.write(np.array([0x574D5356, 1], "<u4").tobytes() + np.array([w.size], "<u8").tobytes())
+            f.write(w.astype("<f4").tobytes())
+
+    def estimate_dev(self, B, d_bgr, h, w, d_depth, stream=None):
+        _check(self.lib.vs_midas_estimate_dev(self.h, B, d_bgr, h, w, d_depth, stream))
+
+    def preprocess_dev(self, B, d_bgr, h, w, d_input, stream=None):
+        _check(self.lib.vs_midas_preprocess_dev(self.h, B, d_bgr, h, w, d_input, stream))
+
+    def forward_dev(self, B, d_input, d_out, stream=None):
+        _check(self.lib.vs_midas_forward_dev(self.h, B, d_input, d_out, stream))
+
+    def postprocess_dev(self, B, d_small, h, w, d_depth, stream=None):
+        _check(self.lib.vs_midas_postprocess_dev(self.h, B, d_small, h, w, d_depth, stream))

@@ -118,15 +118,20 @@ class DevicePipeline:
     rewritten only after step k-2's geometry finished (event wait, no host sync)."""
 
     def __init__(self, ctx, B, h=480, w=640, cap=va.SP_MAX_KEYPOINTS, K=va.K_TUM, iters=200, thr=0.05,
-                 ratio=0.75, rank=0, world=1, group=None, monocular=False, spcf_path=None):
+                 ratio=0.75, rank=0, world=1, group=None, monocular=False, spcf_path=None, midas=None):
         self.ctx, self.B, self.h, self.w, self.cap = ctx, B, h, w, cap
         self.monocular = monocular
         self.K, self.iters, self.thr, self.ratio = K, iters, thr, ratio
         self.rank, self.world, self.group = rank, world, group
         dev = torch.device("cuda", torch.cuda.current_device())
         self.spcf_path, self._spcf_open = spcf_path, False
+        # config[4]: DepthEstimator::estimate (MiDaS v2.1-small) per frame on the network stream,
+        # into S.mdepth [B][h][w] (kept, not consumed — as in the reference, SURVEY.md §2)
+        self.midas = midas
         gathered = world * B if (spcf_path and world > 1 and rank == 0) else 0
         self.sets = [_StepSet(B, h, w, cap, dev, with_depth=not monocular, gathered=gathered) for _ in range(2)]
+        for S in self.sets:
+            S.mdepth = torch.zeros((B, h, w), dtype=torch.float32, device=dev) if midas is not None else None
         self.k = 0
         self.pairs = torch.tensor([[p, p + 1] for p in range(B)], dtype=torch.int32, device=dev)
         self._seed_base = torch.arange(B, dtype=torch.int64, device=dev)
@@ -149,8 +154,14 @@ class DevicePipeline:
         self.k += 1
         S.fc0 = frame_count0
         ctx = self.ctx
-        # inputs are produced on the caller's stream
+        # inputs are produced on the caller's stream; the caching allocator must not hand their
+        # memory out again before the pipeline's streams are done with them
         self.s_net.wait_stream(torch.cuda.current_stream())
+        frames.record_stream(self.s_net)
+        if depth is not None:
+            depth.record_stream(self.s_net)
+        if depth_prev is not None:
+            depth_prev.record_stream(self.s_net)
         with torch.cuda.stream(self.s_net):
             self.s_net.wait_event(S.geo_done)  # step k-2's geometry has released this set
             s = self.s_net.cuda_stream
@@ -165,6 +176,8 @@ class DevicePipeline:
                 S.depth[1:].copy_(depth)
             ctx.network_batch_dev(B, frames.data_ptr(), h, w, S.semi.data_ptr(), S.dgrid.data_ptr(), s)
             S.net_done.record(self.s_net)
+            if self.midas is not None:  # after the features: the geometry never waits for it
+                self.midas.estimate_dev(B, frames.data_ptr(), h, w, S.mdepth.data_ptr(), s)
         with torch.cuda.stream(self.s_geo):
             self.s_geo.wait_event(S.net_done)
             s = self.s_geo.cuda_stream
