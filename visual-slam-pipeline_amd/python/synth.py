@@ -223,3 +223,39 @@ def loop_sequence(n, seed=SEED, dt=1.0 / 10.0, workers=None, K=K_TUM, w=W, h=H):
         out = [_render_one(j) for j in jobs]
     return dict(bgr=np.stack([o[0] for o in out]), depth=np.stack([o[1] for o in out]),
                 R_wc=np.stack([p[0] for p in poses]), t_wc=np.stack([p[1] for p in poses]), dt=dt)
+
+
+def stationary_sequence(n_move1=25, n_hold=12, n_move2=20, seed=SEED, dt=1.0 / 10.0, workers=None, rate=100.0):
+    """A drive along the loop that stops for n_hold frames (the camera holds the pose of the last
+    moving frame; depth noise still differs per frame) and then continues, with an accelerometer
+    stream for Slam::set_accelerometer_data (Slam.cpp:1580-1651): samples {t, ax, ay, az} at `rate`
+    Hz, gravity 9.81 m/s^2 along -y of the device, per-sample vibration of 0.02 m/s^2 while held
+    and 0.6 m/s^2 while driving (the stationarity test thresholds the std of |a| at 0.15 over
+    +-0.1 s).  Returns dict(bgr, depth, R_wc, t_wc, timestamps, accel, moving)."""
+    loop = loop_trajectory(126, seed=seed)
+    idx = list(range(n_move1)) + [n_move1 - 1] * n_hold + list(range(n_move1, n_move1 + n_move2))
+    poses = [loop[i] for i in idx]
+    jobs = [(j, R, t, seed, K_TUM, W, H) for j, (R, t) in enumerate(poses)]
+    if workers is None:
+        import os
+        workers = min(16, os.cpu_count() or 1, len(jobs))
+    if workers > 1:
+        import multiprocessing as mp
+        with mp.get_context("fork").Pool(workers) as pool:
+            out = pool.map(_render_one, jobs)
+    else:
+        out = [_render_one(j) for j in jobs]
+    n = len(idx)
+    ts = np.arange(n) * dt
+    moving = np.ones(n, bool)
+    moving[n_move1:n_move1 + n_hold] = False
+    t_hold0, t_hold1 = ts[n_move1] - 0.5 * dt, ts[n_move1 + n_hold - 1] + 0.5 * dt
+    rng = np.random.default_rng(seed + 71)
+    ta = np.arange(-0.5, ts[-1] + 0.5, 1.0 / rate)
+    held = (ta >= t_hold0) & (ta <= t_hold1)
+    sd = np.where(held, 0.02, 0.6)
+    acc = np.stack([ta, rng.standard_normal(ta.size) * sd, -9.81 + rng.standard_normal(ta.size) * sd,
+                    rng.standard_normal(ta.size) * sd], axis=1)
+    return dict(bgr=np.stack([o[0] for o in out]), depth=np.stack([o[1] for o in out]),
+                R_wc=np.stack([p[0] for p in poses]), t_wc=np.stack([p[1] for p in poses]), timestamps=ts,
+                accel=acc, moving=moving)
