@@ -63,6 +63,9 @@ def main():
                       "pnp_hyp_kcycles_per_hypothesis_x100": {
                           n: round(float(pcyc[k]) / max(1, prof.get("solve_pnp", (0, 1))[1]) / 1e3, 1)
                           for k, n in enumerate(["load+control", "mtm", "jacobi", "sort", "variants", "count"])},
+                      "pnp_ransac_kcycles_per_call": {
+                          n: round(float(pcyc[k]) / max(1, prof.get("solve_pnp", (0, 1))[1]) / 1e3, 1)
+                          for k, n in ((6, "replay"), (7, "inliers+lm"))},
                       "ransac3d_kcycles_per_launch": {
                           n: round(float(rcyc[k]) / max(1, prof.get("ransac3d", (0, 1))[1]) / 1e3, 1)
                           for k, n in enumerate(["backproject", "mt_init", "twists", "sampling", "hypotheses",

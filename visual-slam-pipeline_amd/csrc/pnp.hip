@@ -465,6 +465,7 @@ __global__ __launch_bounds__(256) void k_pnp_ransac(const float* __restrict__ ob
         }
     } else {
         const int* count = H.count + (size_t)pb * H.stride;
+        PNP_T0();
         if (tid == 0) {
             int niters = niters0, best = 0, best_iter = -1, it = 0;
             for (; it < niters; it++) {
@@ -488,6 +489,7 @@ __global__ __launch_bounds__(256) void k_pnp_ransac(const float* __restrict__ ob
             }
         }
         __syncthreads();
+        PNP_T(6);
         if (tid == 0) {
             st[2] = S.niters_run;
             st[3] = S.best_iter;
@@ -530,6 +532,7 @@ __global__ __launch_bounds__(256) void k_pnp_ransac(const float* __restrict__ ob
             if (!S.go) break;
             for (int k = 0; k < 6; k++) p[k] = S.lm.cand[k];
         }
+        PNP_T(7);
     }
     // outputs: Slam.cpp:519-526
     if (tid == 0) {
