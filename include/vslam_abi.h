@@ -344,6 +344,36 @@ int vs_midas_preprocess_dev(vs_midas* m, int B, const uint8_t* d_bgr, int h, int
 int vs_midas_forward_dev(vs_midas* m, int B, const float* d_input, float* d_out, void* stream);
 int vs_midas_postprocess_dev(vs_midas* m, int B, const float* d_small, int h, int w, float* d_depth, void* stream);
 
+/* ---- (e) the offline frame-sharded front end (BASELINE config[3]) ---------------
+ * One process per GPU; per step each rank extracts its B frames, the step's feature records are
+ * all-gathered over RCCL (xGMI), and the B frame pairs ending in the rank's frames go through
+ * match_features, F verification, 3D-3D RANSAC and the E fallback (Slam.cpp:838-984).  The C form
+ * of python/vslam_pipeline.DevicePipeline, with bit-identical results.  RCCL is loaded at run time
+ * (librccl.so.1); a one-rank batch does not need it. */
+#define VS_BATCH_ID_BYTES 128 /* == NCCL_UNIQUE_ID_BYTES */
+typedef struct vs_batch vs_batch;
+typedef struct {
+    int ok3d;                  /* estimate_motion_3d3d succeeded (R3, t3: pose of frame p+1 vs p) */
+    double R3[9], t3[3];
+    int okE;                   /* the essential-matrix fallback succeeded (only when ok3d == 0) */
+    double RE[9], tE[3], scale; /* scale: estimate_scale_from_depth, -1 when unavailable */
+    int n_good, n_kept;        /* ratio-test matches, F-verified matches */
+} vs_pair_motion;
+/* Rank 0 creates the communicator id and distributes the VS_BATCH_ID_BYTES bytes (MPI, a file...). */
+int vs_batch_unique_id(void* id);
+/* world == 1: id may be NULL (no communicator; with an id, one rank runs the exchange path). */
+int vs_batch_create(vs_ctx* ctx, int B, int h, int w, int rank, int world, const void* id, vs_batch** out);
+void vs_batch_destroy(vs_batch* b);
+/* One step (synchronous): this rank's B frames d_bgr [B][h][w][3] u8 and depth [B][h][w] metres,
+ * d_depth_prev the depth of frame rank * B - 1 (world > 1; NULL for the first step of rank 0),
+ * frame_count0 the processed-frame index of d_bgr[0] (RANSAC seed 42 + index, Slam.cpp:276);
+ * out[p] = motion of pair (frame p - 1, frame p) of the block, p = 0..B-1. */
+int vs_batch_step_dev(vs_batch* b, const uint8_t* d_bgr, const float* d_depth, const float* d_depth_prev,
+                      int frame_count0, vs_pair_motion* out, void* stream);
+/* The last step's feature records on the device (with a communicator: all ranks' frames in global
+ * order; without: this rank's), e.g. for vs_spcf_write_dev. */
+int vs_batch_features_dev(vs_batch* b, const vs_keypoint** d_kps, const float** d_desc, const int** d_n, int* frames);
+
 /* ---- F2: the SPCF feature cache as the batch interchange (FeatureExtractor.cpp:261-381) ---
  * Byte layout of the reference's save_cache / load_cache: u32 magic 0x53504346 ("SPCF"),
  * u32 version 1, u32 entry count, then per entry i32 frame_idx, i32 num_kp, num_kp x 28-B

@@ -31,6 +31,17 @@ int main(int argc, char** argv) {
         chk(3, vs_cr::log(y), logq(y));
         chk(4, vs_cr::pow(y, p * 0.5), powq(y, p * 0.5));
         chk(4, vs_cr::pow(u, 5.0), powq(u, 5.0));  // RANSACUpdateNumIters: (1 - ep)^modelPoints
+        chk(4, vs_cr::pow(u, 7.0), powq(u, 7.0));  // the F-matrix registrator's 7-point subsets
+        chk(4, vs_cr::pow(y, (double)(2 + i % 7)), powq(y, (double)(2 + i % 7)));
+        double sn, cs;  // sincos = (sin, cos); arguments near the table knots j/64 and near k pi/4
+        const double knot = std::ldexp(std::floor(U(g) * 100) - 50, -6) + (U(g) - 0.5) * 1e-12;
+        vs_cr::sincos(knot, sn, cs);
+        chk(0, sn, sinq(knot));
+        chk(1, cs, cosq(knot));
+        const double q4 = (std::floor(U(g) * 16) - 8) * 0.7853981633974483 + (U(g) - 0.5) * 1e-9;
+        vs_cr::sincos(q4, sn, cs);
+        chk(0, sn, sinq(q4));
+        chk(1, cs, cosq(q4));
     }
     std::printf("mismatches sin %ld cos %ld acos %ld log %ld pow %ld over %d draws\n", bad[0], bad[1], bad[2], bad[3],
                 bad[4], N);

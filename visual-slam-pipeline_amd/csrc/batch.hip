@@ -1,0 +1,277 @@
+// batch.hip — the offline, frame-sharded front end (BASELINE config[3]) behind the
+// C ABI, for a C/C++ driver such as the reference's main.cpp:1036-1311: per step each rank
+// extracts its B frames (FeatureExtractor::extract), the step's feature records are all-gathered
+// over RCCL so that every rank holds the whole step (the SPCF-like interchange a sequential
+// tracker consumes) and rank r the neighbour frame rB - 1, then the B frame pairs that end in
+// the rank's frames go through Slam::match_features, the F-matrix verification, the 3D-3D RANSAC
+// and its essential-matrix fallback (Slam.cpp:838-984).  The same stages and inputs as
+// python/vslam_pipeline.DevicePipeline, so both give bit-identical pair motions
+// (tests/test_gpu_batch.py).
+//
+// RCCL is resolved at run time (dlopen of librccl.so.1, the process's already-loaded copy when
+// torch or the host application has one), so the library carries no link-time RCCL dependency and
+// a one-rank batch needs none at all.
+#include <dlfcn.h>
+#include <hip/hip_runtime.h>
+
+#include <cstring>
+#include <vector>
+
+#include "vs_internal.h"
+
+namespace {
+
+// The RCCL entry points used here (rccl.h ABI: ncclUniqueId is 128 opaque bytes, enums as int)
+typedef struct {
+    char internal[VS_BATCH_ID_BYTES];
+} RcclId;
+typedef void* RcclComm;
+struct Rccl {
+    void* so = nullptr;
+    int (*get_unique_id)(RcclId*) = nullptr;
+    int (*comm_init_rank)(RcclComm*, int, RcclId, int) = nullptr;
+    int (*all_gather)(const void*, void*, size_t, int, RcclComm, hipStream_t) = nullptr;
+    int (*comm_destroy)(RcclComm) = nullptr;
+    const char* (*error_string)(int) = nullptr;
+};
+constexpr int kRcclChar = 0;  // ncclInt8 / ncclChar
+
+int load_rccl(Rccl& r) {
+    if (r.so) return VS_OK;
+    void* so = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+    if (!so) so = dlopen("librccl.so", RTLD_NOW | RTLD_GLOBAL);
+    if (!so) {
+        vs::set_error("vs_batch: librccl.so not found (needed for world > 1)");
+        return VS_ERR_IO;
+    }
+    r.get_unique_id = reinterpret_cast<int (*)(RcclId*)>(dlsym(so, "ncclGetUniqueId"));
+    r.comm_init_rank = reinterpret_cast<int (*)(RcclComm*, int, RcclId, int)>(dlsym(so, "ncclCommInitRank"));
+    r.all_gather = reinterpret_cast<int (*)(const void*, void*, size_t, int, RcclComm, hipStream_t)>(
+        dlsym(so, "ncclAllGather"));
+    r.comm_destroy = reinterpret_cast<int (*)(RcclComm)>(dlsym(so, "ncclCommDestroy"));
+    r.error_string = reinterpret_cast<const char* (*)(int)>(dlsym(so, "ncclGetErrorString"));
+    if (!r.get_unique_id || !r.comm_init_rank || !r.all_gather || !r.comm_destroy) {
+        vs::set_error("vs_batch: librccl.so lacks the expected entry points");
+        return VS_ERR_IO;
+    }
+    r.so = so;
+    return VS_OK;
+}
+Rccl g_rccl;
+
+#define VS_RCCL(call)                                                                                  \
+    do {                                                                                               \
+        const int rc_ = (call);                                                                        \
+        if (rc_ != 0) {                                                                                \
+            ::vs::set_error(std::string("RCCL: ") + (g_rccl.error_string ? g_rccl.error_string(rc_) : "error")); \
+            return VS_ERR_HIP;                                                                         \
+        }                                                                                              \
+    } while (0)
+
+template <class T>
+T* alloc(std::vector<void*>& owned, size_t count) {  // zeroed; a failure leaves a null in `owned`
+    void* p = nullptr;
+    if (hipMalloc(&p, count * sizeof(T)) != hipSuccess) p = nullptr;
+    owned.push_back(p);
+    if (p) (void)hipMemset(p, 0, count * sizeof(T));
+    return static_cast<T*>(p);
+}
+
+}  // namespace
+
+struct vs_batch {
+    vs_ctx* ctx = nullptr;
+    int B = 0, h = 0, w = 0, rank = 0, world = 1, cap = VS_SP_MAX_KEYPOINTS, steps = 0;
+    RcclComm comm = nullptr;
+    std::vector<void*> owned;
+    // slot 0 = the frame before this rank's block, slots 1..B = its frames
+    vs_keypoint* kps = nullptr;
+    float *desc = nullptr, *depth = nullptr, *semi = nullptr, *dgrid = nullptr;
+    int* n = nullptr;
+    // the step's gathered records (world > 1): [world * B]
+    vs_keypoint* g_kps = nullptr;
+    float* g_desc = nullptr;
+    int* g_n = nullptr;
+    // per pair
+    int *pairs = nullptr, *nraw = nullptr, *ngood = nullptr, *nkept = nullptr, *fdiag = nullptr, *ok = nullptr,
+        *diag = nullptr, *eok = nullptr, *ediag = nullptr;
+    uint32_t* seeds = nullptr;
+    vs_match *raw = nullptr, *good = nullptr, *kept = nullptr;
+    double *F = nullptr, *eperr = nullptr, *R = nullptr, *t = nullptr, *eR = nullptr, *et = nullptr, *escale = nullptr;
+    std::vector<uint32_t> h_seeds;
+};
+
+extern "C" {
+
+int vs_batch_unique_id(void* id) {
+    VS_ARG(id, "vs_batch_unique_id: null argument");
+    VS_CHECK(load_rccl(g_rccl));
+    RcclId u;
+    VS_RCCL(g_rccl.get_unique_id(&u));
+    std::memcpy(id, &u, sizeof(u));
+    return VS_OK;
+}
+
+int vs_batch_create(vs_ctx* ctx, int B, int h, int w, int rank, int world, const void* id, vs_batch** out) {
+    VS_ARG(ctx && out && B >= 1 && h >= 16 && w >= 16, "vs_batch_create: bad arguments");
+    VS_ARG(world >= 1 && rank >= 0 && rank < world, "vs_batch_create: bad rank / world");
+    VS_ARG(world == 1 || id, "vs_batch_create: world > 1 needs the communicator id of vs_batch_unique_id");
+    *out = nullptr;
+    VS_HIP(hipSetDevice(ctx->device));
+    auto* b = new (std::nothrow) vs_batch();
+    if (!b) return VS_ERR_NOMEM;
+    b->ctx = ctx, b->B = B, b->h = h, b->w = w, b->rank = rank, b->world = world;
+    const int F = B + 1, cap = b->cap, hc = (h + 7) / 8, wc = (w + 7) / 8;
+    auto& o = b->owned;
+    b->kps = alloc<vs_keypoint>(o, (size_t)F * cap);
+    b->desc = alloc<float>(o, (size_t)F * cap * 256);
+    b->n = alloc<int>(o, F);
+    b->depth = alloc<float>(o, (size_t)F * h * w);
+    b->semi = alloc<float>(o, (size_t)B * hc * wc * VS_SEMI_CH);
+    b->dgrid = alloc<float>(o, (size_t)B * hc * wc * VS_DESC_DIM);
+    if (id) {
+        b->g_kps = alloc<vs_keypoint>(o, (size_t)world * B * cap);
+        b->g_desc = alloc<float>(o, (size_t)world * B * cap * 256);
+        b->g_n = alloc<int>(o, (size_t)world * B);
+    }
+    b->pairs = alloc<int>(o, 2 * B);
+    b->seeds = alloc<uint32_t>(o, B);
+    b->raw = alloc<vs_match>(o, (size_t)B * cap);
+    b->good = alloc<vs_match>(o, (size_t)B * cap);
+    b->kept = alloc<vs_match>(o, (size_t)B * cap);
+    b->nraw = alloc<int>(o, B), b->ngood = alloc<int>(o, B), b->nkept = alloc<int>(o, B);
+    b->F = alloc<double>(o, 9 * B), b->eperr = alloc<double>(o, 2 * B), b->fdiag = alloc<int>(o, 8 * B);
+    b->R = alloc<double>(o, 9 * B), b->t = alloc<double>(o, 3 * B), b->ok = alloc<int>(o, B), b->diag = alloc<int>(o, 4 * B);
+    b->eR = alloc<double>(o, 9 * B), b->et = alloc<double>(o, 3 * B), b->escale = alloc<double>(o, B);
+    b->eok = alloc<int>(o, B), b->ediag = alloc<int>(o, 8 * B);
+    for (void* p : o)
+        if (!p) {
+            vs_batch_destroy(b);
+            vs::set_error("vs_batch_create: device allocation failed");
+            return VS_ERR_NOMEM;
+        }
+    std::vector<int> pr(2 * B);
+    for (int p = 0; p < B; p++) pr[2 * p] = p, pr[2 * p + 1] = p + 1;  // pair p = (slot p, slot p + 1)
+    VS_HIP(hipMemcpy(b->pairs, pr.data(), pr.size() * sizeof(int), hipMemcpyHostToDevice));
+    b->h_seeds.resize(B);
+    if (id) {  // a communicator (also for one rank: the exchange path, tests)
+        int rc = load_rccl(g_rccl);
+        RcclId u;
+        std::memcpy(&u, id, sizeof(u));
+        if (rc == VS_OK && g_rccl.comm_init_rank(&b->comm, world, u, rank) != 0) {
+            vs::set_error("vs_batch_create: ncclCommInitRank failed");
+            rc = VS_ERR_HIP;
+        }
+        if (rc != VS_OK) {
+            vs_batch_destroy(b);
+            return rc;
+        }
+    }
+    *out = b;
+    return VS_OK;
+}
+
+void vs_batch_destroy(vs_batch* b) {
+    if (!b) return;
+    (void)hipDeviceSynchronize();
+    if (b->comm && g_rccl.comm_destroy) (void)g_rccl.comm_destroy(b->comm);
+    for (void* p : b->owned)
+        if (p) (void)hipFree(p);
+    delete b;
+}
+
+int vs_batch_step_dev(vs_batch* b, const uint8_t* d_bgr, const float* d_depth, const float* d_depth_prev,
+                      int frame_count0, vs_pair_motion* out, void* stream) {
+    VS_ARG(b && d_bgr && d_depth && out, "vs_batch_step_dev: null argument");
+    vs_ctx* ctx = b->ctx;
+    hipStream_t s = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
+    const int B = b->B, h = b->h, w = b->w, cap = b->cap;
+    const size_t plane = (size_t)h * w, rec_k = (size_t)cap, rec_d = (size_t)cap * 256;
+    // depth: slot 0 = the frame before the block (the caller's halo, or the previous step's last)
+    const bool xchg = b->comm != nullptr;
+    if (xchg && d_depth_prev)
+        VS_HIP(hipMemcpyAsync(b->depth, d_depth_prev, plane * sizeof(float), hipMemcpyDeviceToDevice, s));
+    else if (!xchg)
+        VS_HIP(hipMemcpyAsync(b->depth, b->depth + (size_t)B * plane, plane * sizeof(float), hipMemcpyDeviceToDevice, s));
+    VS_HIP(hipMemcpyAsync(b->depth + plane, d_depth, (size_t)B * plane * sizeof(float), hipMemcpyDeviceToDevice, s));
+    // features: the previous step's last frame into slot 0 first (no communicator: the carry)
+    if (!xchg) {
+        VS_HIP(hipMemcpyAsync(b->kps, b->kps + (size_t)B * rec_k, rec_k * sizeof(vs_keypoint), hipMemcpyDeviceToDevice, s));
+        VS_HIP(hipMemcpyAsync(b->desc, b->desc + (size_t)B * rec_d, rec_d * sizeof(float), hipMemcpyDeviceToDevice, s));
+        VS_HIP(hipMemcpyAsync(b->n, b->n + B, sizeof(int), hipMemcpyDeviceToDevice, s));
+    }
+    VS_CHECK(vs_network_batch_dev(ctx, B, d_bgr, h, w, b->semi, b->dgrid, s));
+    VS_CHECK(vs_postprocess_batch_dev(ctx, B, b->semi, b->dgrid, h, w, b->kps + rec_k, b->desc + rec_d, b->n + 1, cap, s));
+    if (xchg) {
+        // all-gather the step's records; slot 0 <- frame rank * B - 1 (rank 0: the previous step's
+        // global last frame, still in g_* from that step)
+        if (b->rank == 0) {
+            if (b->steps > 0) {
+                const size_t last = (size_t)b->world * B - 1;
+                VS_HIP(hipMemcpyAsync(b->kps, b->g_kps + last * rec_k, rec_k * sizeof(vs_keypoint), hipMemcpyDeviceToDevice, s));
+                VS_HIP(hipMemcpyAsync(b->desc, b->g_desc + last * rec_d, rec_d * sizeof(float), hipMemcpyDeviceToDevice, s));
+                VS_HIP(hipMemcpyAsync(b->n, b->g_n + last, sizeof(int), hipMemcpyDeviceToDevice, s));
+            } else {
+                VS_HIP(hipMemsetAsync(b->n, 0, sizeof(int), s));
+            }
+        }
+        VS_RCCL(g_rccl.all_gather(b->n + 1, b->g_n, (size_t)B * sizeof(int), kRcclChar, b->comm, s));
+        VS_RCCL(g_rccl.all_gather(b->kps + rec_k, b->g_kps, (size_t)B * rec_k * sizeof(vs_keypoint), kRcclChar, b->comm, s));
+        VS_RCCL(g_rccl.all_gather(b->desc + rec_d, b->g_desc, (size_t)B * rec_d * sizeof(float), kRcclChar, b->comm, s));
+        if (b->rank > 0) {
+            const size_t j = (size_t)b->rank * B - 1;
+            VS_HIP(hipMemcpyAsync(b->kps, b->g_kps + j * rec_k, rec_k * sizeof(vs_keypoint), hipMemcpyDeviceToDevice, s));
+            VS_HIP(hipMemcpyAsync(b->desc, b->g_desc + j * rec_d, rec_d * sizeof(float), hipMemcpyDeviceToDevice, s));
+            VS_HIP(hipMemcpyAsync(b->n, b->g_n + j, sizeof(int), hipMemcpyDeviceToDevice, s));
+        }
+    }
+    // the RANSAC seed of pair p is 42 + its processed-frame index (Slam.cpp:276)
+    for (int p = 0; p < B; p++) b->h_seeds[p] = (uint32_t)(42 + frame_count0 + p);
+    VS_HIP(hipMemcpyAsync(b->seeds, b->h_seeds.data(), B * sizeof(uint32_t), hipMemcpyHostToDevice, s));
+    const double K[4] = {525.0, 525.0, 319.5, 239.5};  // Config.h:14-17
+    VS_CHECK(vs_match_pairs_dev(ctx, B, b->pairs, B + 1, b->desc, b->n, cap, 0.75f, b->raw, b->nraw, b->good, b->ngood, s));
+    VS_CHECK(vs_fmat_verify_pairs_dev(ctx, B, b->pairs, b->kps, cap, b->good, b->ngood, b->F, b->kept, b->nkept,
+                                      b->eperr, b->fdiag, s));
+    VS_CHECK(vs_ransac_3d3d_pairs_dev(ctx, B, b->pairs, b->kps, cap, b->kept, b->nkept, b->depth, h, w, K, b->seeds, 200,
+                                      0.05, b->R, b->t, b->ok, b->diag, s));
+    VS_CHECK(vs_emat_motion_pairs_dev(ctx, B, b->pairs, b->kps, cap, b->kept, b->nkept, b->ok, b->depth, h, w, K, b->eR,
+                                      b->et, b->escale, b->eok, b->ediag, s));
+    std::vector<double> R(9 * B), t(3 * B), eR(9 * B), et(3 * B), sc(B);
+    std::vector<int> ok(B), eok(B), ng(B), nk(B);
+    VS_HIP(hipMemcpyAsync(R.data(), b->R, R.size() * sizeof(double), hipMemcpyDeviceToHost, s));
+    VS_HIP(hipMemcpyAsync(t.data(), b->t, t.size() * sizeof(double), hipMemcpyDeviceToHost, s));
+    VS_HIP(hipMemcpyAsync(eR.data(), b->eR, eR.size() * sizeof(double), hipMemcpyDeviceToHost, s));
+    VS_HIP(hipMemcpyAsync(et.data(), b->et, et.size() * sizeof(double), hipMemcpyDeviceToHost, s));
+    VS_HIP(hipMemcpyAsync(sc.data(), b->escale, sc.size() * sizeof(double), hipMemcpyDeviceToHost, s));
+    VS_HIP(hipMemcpyAsync(ok.data(), b->ok, B * sizeof(int), hipMemcpyDeviceToHost, s));
+    VS_HIP(hipMemcpyAsync(eok.data(), b->eok, B * sizeof(int), hipMemcpyDeviceToHost, s));
+    VS_HIP(hipMemcpyAsync(ng.data(), b->ngood, B * sizeof(int), hipMemcpyDeviceToHost, s));
+    VS_HIP(hipMemcpyAsync(nk.data(), b->nkept, B * sizeof(int), hipMemcpyDeviceToHost, s));
+    VS_HIP(hipStreamSynchronize(s));
+    for (int p = 0; p < B; p++) {
+        vs_pair_motion& m = out[p];
+        m.ok3d = ok[p];
+        std::memcpy(m.R3, &R[9 * p], sizeof(m.R3));
+        std::memcpy(m.t3, &t[3 * p], sizeof(m.t3));
+        m.okE = eok[p];
+        std::memcpy(m.RE, &eR[9 * p], sizeof(m.RE));
+        std::memcpy(m.tE, &et[3 * p], sizeof(m.tE));
+        m.scale = sc[p];
+        m.n_good = ng[p];
+        m.n_kept = nk[p];
+    }
+    b->steps++;
+    return VS_OK;
+}
+
+int vs_batch_features_dev(vs_batch* b, const vs_keypoint** d_kps, const float** d_desc, const int** d_n, int* frames) {
+    VS_ARG(b && d_kps && d_desc && d_n && frames, "vs_batch_features_dev: null argument");
+    if (b->comm) {
+        *d_kps = b->g_kps, *d_desc = b->g_desc, *d_n = b->g_n, *frames = b->world * b->B;
+    } else {
+        *d_kps = b->kps + b->cap, *d_desc = b->desc + (size_t)b->cap * 256, *d_n = b->n + 1, *frames = b->B;
+    }
+    return VS_OK;
+}
+
+}  // extern "C"

@@ -14,10 +14,13 @@
 // Implementation (device and the product's host code): double-double arithmetic (fma-exact
 // products) with ~2^-100 relative error before the final rounding, so the rounded result is the
 // correctly rounded one except within 2^-100 of a rounding midpoint (probability ~2^-47 per call).
-//   sin / cos: x - k pi/2 with a triple-double pi/2, Taylor series of degree 29 / 28 on |r| <= pi/4;
+//   sin / cos: x - k pi/2 with a triple-double pi/2, then r = j/64 + b with a 53-entry double-double
+//         table of sin / cos (j/64), Taylor series of degree 13 / 12 on |b| <= 1/128 and the
+//         addition formulas (sincos shares the reduction);
 //   acos: pi/2 - asin(c) for |c| <= 1/2, 2 asin(sqrt((1 -+ c) / 2)) beyond, asin by one
 //         double-double Newton step on sin from the libm estimate;
-//   log: one Newton step on exp from the libm estimate; pow(y, p) = exp(p log y);
+//   log: one Newton step on exp from the libm estimate; pow(y, p) = exp(p log y), integer
+//         exponents 2..8 by binary powering;
 //   exp: k ln2 reduction (triple-double ln2), /32, degree-14 Taylor, five squarings.
 // The oracle (oracle/, test infrastructure) compiles this header with VS_CR_QUADMATH: the same
 // functions from libquadmath's binary128 routines rounded to double — an independent
@@ -38,6 +41,10 @@
 namespace vs_cr {
 inline double sin(double x) { return (double)sinq((__float128)x); }
 inline double cos(double x) { return (double)cosq((__float128)x); }
+inline void sincos(double x, double& sn, double& cs) {
+    sn = sin(x);
+    cs = cos(x);
+}
 inline double acos(double x) { return (double)acosq((__float128)x); }
 inline double log(double x) { return (double)logq((__float128)x); }
 inline double pow(double y, double p) { return (double)powq((__float128)y, (__float128)p); }
@@ -112,24 +119,102 @@ VS_CR_HD inline dd inv_fact(int n) {
     return {t[n][0], t[n][1]};
 }
 
-// sin(r), cos(r) for |r| <= pi/4 (+ rounding slack): Horner in u = r^2 with signs (-1)^k
-VS_CR_HD inline dd sin_poly(dd r) {  // r * sum_{k=0}^{14} (-1)^k u^k / (2k+1)!
-    const dd u = mul(r, r);
-    dd p = inv_fact(29);
-    for (int k = 13; k >= 0; k--) {
+// sin(j/64), cos(j/64) as double-doubles, j = 0..52 (libquadmath: hi = RN(q), lo = RN(q - hi))
+#define VS_CR_SINCOS64 \
+    { \
+    {0x0p+0, 0x0p+0, 0x1p+0, 0x0p+0}, \
+    {0x1.fffaaaaeeeed5p-7, -0x1.2ab639a9f0776p-63, 0x1.fff000155549fp-1, 0x1.28a28a03a5ef3p-55}, \
+    {0x1.ffeaaaeeee86fp-6, -0x1.cd406fb224ae2p-60, 0x1.ffc00155527d3p-1, -0x1.3b54492d89b5bp-55}, \
+    {0x1.7fdc01032fba9p-5, -0x1.599bdf46e997ap-59, 0x1.ff7006bfdf99fp-1, -0x1.8b3b560648d5fp-56}, \
+    {0x1.ffaaaeeed4edbp-5, -0x1.2d16d32684b69p-59, 0x1.ff0015549f4d3p-1, 0x1.328387b99426fp-55}, \
+    {0x1.3facb12d1755bp-4, -0x1.921915299468bp-58, 0x1.fe7034129ef6fp-1, -0x1.cbf4337c96f96p-57}, \
+    {0x1.7f701032550e4p-4, 0x1.afc2d1800501ap-60, 0x1.fdc06bf7e6b9bp-1, 0x1.31902b535f8dbp-55}, \
+    {0x1.bf1b78568391dp-4, 0x1.e91841dea4cc8p-58, 0x1.fcf0c800e99b1p-1, 0x1.ea3d786d186acp-57}, \
+    {0x1.feaaeee86ee36p-4, -0x1.afcb2bcc6f03bp-59, 0x1.fc015527d5bd3p-1, 0x1.b68f35094efb8p-55}, \
+    {0x1.1f0d3d7afceafp-3, -0x1.6ef95099769a5p-57, 0x1.faf22263c4bd3p-1, -0x1.52ace133a2769p-58}, \
+    {0x1.3eb312c5d66cbp-3, 0x1.47d666b66cb91p-57, 0x1.f9c340a7cc428p-1, 0x1.c5b6b063b7462p-55}, \
+    {0x1.5e44fcfa126f3p-3, -0x1.6f443063f89b6p-57, 0x1.f874c2e1eecf6p-1, -0x1.c6514e1332b16p-55}, \
+    {0x1.7dc102fbaf2b5p-3, 0x1.5ab50e23c97c3p-59, 0x1.f706bdf9ece1cp-1, -0x1.698c80c36dcb4p-55}, \
+    {0x1.9d252d0cec312p-3, 0x1.9c43d80b1137dp-58, 0x1.f57948cff6797p-1, 0x1.e3a0d3e03b1d4p-57}, \
+    {0x1.bc6f84edc6199p-3, 0x1.9c1a56a7b0cabp-57, 0x1.f3cc7c3b3d16ep-1, -0x1.21a3ad28a3494p-57}, \
+    {0x1.db9e15fb5a5dp-3, -0x1.32e20d6cc6fc2p-57, 0x1.f20073086649fp-1, 0x1.b940416c1984bp-56}, \
+    {0x1.faaeed4f31577p-3, -0x1.15d88508e32b8p-57, 0x1.f01549f7deea1p-1, 0x1.d3c1e99e5cafdp-55}, \
+    {0x1.0cd00cef36436p-2, -0x1.9fb0a0c93e2b4p-56, 0x1.ee0b1fbc0f11cp-1, -0x1.bfd2380bbc3b1p-59}, \
+    {0x1.1c37d64c6b876p-2, 0x1.46076fe0dcff4p-56, 0x1.ebe214f76efa8p-1, -0x1.02f9f12ba543ep-55}, \
+    {0x1.2b8ddc43eb49fp-2, 0x1.1553899f2d807p-57, 0x1.e99a4c3a7cd83p-1, -0x1.2264b1bc53ce8p-55}, \
+    {0x1.3ad129769d3d8p-2, 0x1.03d550487839ap-63, 0x1.e733ea0193d4p-1, -0x1.6428b3546ce13p-55}, \
+    {0x1.4a00c9b0f3d2p-2, 0x1.823ba6bb08eadp-56, 0x1.e4af14b2a449cp-1, -0x1.68ca02e8a6833p-55}, \
+    {0x1.591bc9fa2f597p-2, 0x1.7c74bac3fe0cbp-57, 0x1.e20bf49acd6c1p-1, -0x1.660aec7ef636cp-58}, \
+    {0x1.682138a38d7f7p-2, -0x1.d889202444aadp-56, 0x1.df4ab3ebd875ep-1, -0x1.e2d8a7e6736c4p-55}, \
+    {0x1.7710255764214p-2, -0x1.6ead7314bb6cep-57, 0x1.dc6b7eb995912p-1, 0x1.4b364776dcd35p-58}, \
+    {0x1.85e7a12826949p-2, 0x1.8a40e9b5facep-56, 0x1.d96e82f71a9dcp-1, 0x1.ff61bd5d2039dp-55}, \
+    {0x1.94a6be9f546c5p-2, -0x1.69ce13e683f58p-56, 0x1.d653f073e404p-1, -0x1.76236434bec37p-55}, \
+    {0x1.a34c91cc50ccap-2, -0x1.a310e3b50cecdp-58, 0x1.d31bf8d8d7c06p-1, 0x1.e60dd3089cbddp-56}, \
+    {0x1.b1d8305321617p-2, -0x1.ae242cb99f519p-56, 0x1.cfc6cfa52ad9fp-1, 0x1.8b5b5508f2a0dp-55}, \
+    {0x1.c048b17b140a3p-2, 0x1.19fe6757e9fa6p-57, 0x1.cc54aa2b2972ep-1, 0x1.4ee162ba83a98p-57}, \
+    {0x1.ce9d2e3d4a51fp-2, -0x1.2fc8a12dae298p-57, 0x1.c8c5bf8ce1a84p-1, 0x1.ab3d1a1590123p-56}, \
+    {0x1.dcd4c15329c9ap-2, 0x1.0d4c6e171fd9ap-56, 0x1.c51a48b8b175ep-1, -0x1.1bbb43b9aa88p-57}, \
+    {0x1.eaee8744b05fp-2, -0x1.789b43c9b027cp-58, 0x1.c1528065b7d5p-1, -0x1.892111312e828p-55}, \
+    {0x1.f8e99e76abc97p-2, 0x1.9d950af2d00a3p-58, 0x1.bd6ea310294f5p-1, 0x1.31bbcc88c109dp-56}, \
+    {0x1.0362939c69955p-1, -0x1.2d8cd78397b01p-55, 0x1.b96eeef58840ep-1, 0x1.45a3cc78fadep-58}, \
+    {0x1.0a4021e9e1001p-1, -0x1.6f643a13914f6p-55, 0x1.b553a410c104ep-1, 0x1.8ff7947027a16p-58}, \
+    {0x1.110d0c4b69c3bp-1, 0x1.d918998809981p-55, 0x1.b11d04162a4c6p-1, 0x1.1dd561efbc0c2p-56}, \
+    {0x1.17c8e5f2eedbp-1, 0x1.35e57102e2488p-57, 0x1.accb526f69de5p-1, 0x1.8fb6a8dd6b6ccp-55}, \
+    {0x1.1e7343236574cp-1, 0x1.22a3fa4f41d5ap-56, 0x1.a85ed4373e02dp-1, 0x1.9be06385ec792p-57}, \
+    {0x1.250bb93788bbbp-1, 0x1.ea3d02457bccep-56, 0x1.a3d7d0352bdcfp-1, -0x1.68dbaeca19669p-55}, \
+    {0x1.2b91dea88421ep-1, -0x1.fa371db216abp-55, 0x1.9f368ed912f85p-1, -0x1.1d200c5791606p-55}, \
+    {0x1.32054b148bc4fp-1, 0x1.f6b42095a135bp-55, 0x1.9a7b5a36a6514p-1, 0x1.722cfcc9fa7a9p-55}, \
+    {0x1.386597456282bp-1, -0x1.10fada93b07a8p-56, 0x1.95a67e00cb1fdp-1, -0x1.0befda21f862dp-55}, \
+    {0x1.3eb25d36cd53ap-1, -0x1.be570e1570fcp-58, 0x1.90b84784ddaf7p-1, -0x1.0feb10ab93b87p-56}, \
+    {0x1.44eb381cf386bp-1, -0x1.3ed6c1e6a5505p-55, 0x1.8bb105a5dc9p-1, 0x1.863e03e9474c1p-55}, \
+    {0x1.4b0fc46aab761p-1, 0x1.0da05738cc59cp-61, 0x1.869108d77a6c6p-1, 0x1.338ffe2bfe9ddp-56}, \
+    {0x1.511f9fd7b351cp-1, -0x1.5c0e861c48831p-55, 0x1.8158a31916d5dp-1, -0x1.de8b90b8228dep-57}, \
+    {0x1.571a6966d59b3p-1, 0x1.c843b4d0fb197p-58, 0x1.7c0827f09e54fp-1, -0x1.c73d6d72aee68p-57}, \
+    {0x1.5cffc16bf8f0dp-1, 0x1.96cb370eb578ap-55, 0x1.769fec655211fp-1, -0x1.827d5cf8c68c5p-57}, \
+    {0x1.62cf49921ac79p-1, -0x1.edd9855b6241ap-55, 0x1.712046fa77678p-1, 0x1.425b0a5029c81p-55}, \
+    {0x1.6888a4e134b2fp-1, -0x1.6b7d37644d5e6p-55, 0x1.6b898fa9efb5dp-1, 0x1.15ac786ccf4b2p-56}, \
+    {0x1.6e2b77c40bde1p-1, -0x1.0e729857fad53p-56, 0x1.65dc1fdeb8cbap-1, -0x1.97c1b47337c77p-58}, \
+    {0x1.73b7680dea578p-1, -0x1.2248306dc12a2p-56, 0x1.6018526f563dfp-1, 0x1.46ca5e0e432dp-55} \
+    }
+#if defined(__HIPCC__)
+__device__ __constant__ const double kSinCos64Dev[53][4] = VS_CR_SINCOS64;
+#endif
+inline constexpr double kSinCos64[53][4] = VS_CR_SINCOS64;
+
+// sin(b), cos(b) for |b| <= 1/128 (+ slack): Taylor to b^13 / b^12 (terms below 2^-113)
+VS_CR_HD inline dd sin_small(dd b) {  // b * sum_{k=0}^{6} (-1)^k u^k / (2k+1)!
+    const dd u = mul(b, b);
+    dd p = inv_fact(13);
+    for (int k = 5; k >= 0; k--) {
         p = mul(p, u);
         p = (k & 1) ? sub(p, inv_fact(2 * k + 1)) : add(p, inv_fact(2 * k + 1));
     }
-    return mul(p, r);
+    return mul(p, b);
 }
-VS_CR_HD inline dd cos_poly(dd r) {  // sum_{k=0}^{14} (-1)^k u^k / (2k)!
-    const dd u = mul(r, r);
-    dd p = inv_fact(28);
-    for (int k = 13; k >= 0; k--) {
+VS_CR_HD inline dd cos_small(dd b) {  // sum_{k=0}^{6} (-1)^k u^k / (2k)!
+    const dd u = mul(b, b);
+    dd p = inv_fact(12);
+    for (int k = 5; k >= 0; k--) {
         p = mul(p, u);
         p = (k & 1) ? sub(p, inv_fact(2 * k)) : add(p, inv_fact(2 * k));
     }
     return p;
+}
+// sin(r), cos(r) for |r| <= pi/4: r = a + b with a = j/64 (table), |b| <= 1/128 (the subtraction
+// r.hi - a is exact), then the addition formulas in double-double
+VS_CR_HD inline void sincos_poly(dd r, dd& sn, dd& cs) {
+    const double j = ::rint(r.hi * 64.0);
+    const int ji = (int)::fabs(j);
+#if defined(__HIP_DEVICE_COMPILE__)
+    const double* t = kSinCos64Dev[ji];
+#else
+    const double* t = kSinCos64[ji];
+#endif
+    const dd sa{j < 0 ? -t[0] : t[0], j < 0 ? -t[1] : t[1]}, ca{t[2], t[3]};
+    const dd b = two_sum(r.hi - j * 0x1p-6, r.lo);
+    const dd sb = sin_small(b), cb = cos_small(b);
+    sn = add(mul(sa, cb), mul(ca, sb));
+    cs = sub(mul(ca, cb), mul(sa, sb));
 }
 
 // x = k pi/2 + r, |r| <= pi/4; valid for |x| < 2^20
@@ -142,28 +227,35 @@ VS_CR_HD inline dd reduce_pio2(double x, int& q) {
     return r;
 }
 
-VS_CR_HD inline dd sin_dd(double x) {
+VS_CR_HD inline void sincos_dd(double x, dd& sn, dd& cs) {
     int q;
     const dd r = reduce_pio2(x, q);
+    dd s0, c0;
+    sincos_poly(r, s0, c0);
     switch (q) {
-        case 0: return sin_poly(r);
-        case 1: return cos_poly(r);
-        case 2: return neg(sin_poly(r));
-        default: return neg(cos_poly(r));
+        case 0: sn = s0, cs = c0; break;
+        case 1: sn = c0, cs = neg(s0); break;
+        case 2: sn = neg(s0), cs = neg(c0); break;
+        default: sn = neg(c0), cs = s0; break;
     }
 }
-VS_CR_HD inline dd cos_dd(double x) {
-    int q;
-    const dd r = reduce_pio2(x, q);
-    switch (q) {
-        case 0: return cos_poly(r);
-        case 1: return neg(sin_poly(r));
-        case 2: return neg(cos_poly(r));
-        default: return sin_poly(r);
-    }
+VS_CR_HD inline dd sin_dd(double x) {
+    dd s, c;
+    sincos_dd(x, s, c);
+    return s;
 }
 VS_CR_HD inline double sin(double x) { return round_dd(sin_dd(x)); }
-VS_CR_HD inline double cos(double x) { return round_dd(cos_dd(x)); }
+VS_CR_HD inline double cos(double x) {
+    dd s, c;
+    sincos_dd(x, s, c);
+    return round_dd(c);
+}
+VS_CR_HD inline void sincos(double x, double& sn, double& cs) {
+    dd s, c;
+    sincos_dd(x, s, c);
+    sn = round_dd(s);
+    cs = round_dd(c);
+}
 
 // sqrt of a double as a double-double
 VS_CR_HD inline dd sqrt_dd(double s) {
@@ -217,6 +309,16 @@ VS_CR_HD inline double log(double y) {
 VS_CR_HD inline double pow(double y, double p) {
     if (y == 1.0 || p == 0.0) return 1.0;
     if (!(y > 0.0) || y > 1.7976931348623157e308) return ::pow(y, p);
+    if (p >= 2.0 && p <= 8.0 && p == ::rint(p) && y > 0x1p-100 && y < 0x1p100) {
+        // small integer powers (RANSACUpdateNumIters' (1 - ep)^model_points) by binary powering in
+        // double-double: relative error ~2^-103, as the exp / log route
+        dd r{1.0, 0.0}, b{y, 0.0};
+        for (int e = (int)p; e > 0; e >>= 1) {
+            if (e & 1) r = mul(r, b);
+            if (e > 1) b = mul(b, b);
+        }
+        return round_dd(r);
+    }
     const dd z = mul_d(log_dd(y), p);
     if (z.hi > 709.0 || z.hi < -708.0) return ::pow(y, p);
     return round_dd(exp_dd(z));

@@ -447,14 +447,15 @@ int desc_norms(vs_ctx* ctx, int F, const float* d_desc, const int* d_n, int cap,
 }
 
 // Keys ([P][2][kcap], all ones) and arrival counters ([P], zero) that every k_match launch leaves
-// reset; (re)initialised only when a buffer grows.
+// reset; (re)initialised only when a buffer grows.  Growth is detected on the size: a freed and
+// reallocated buffer can come back at the same address with an uninitialised tail.
 static int match_state(vs_ctx* ctx, int P, int kcap, unsigned long long** keys, unsigned** cnt, hipStream_t s) {
-    void* kp = ctx->match_keys.p;
+    const size_t kb = ctx->match_keys.bytes;
     VS_CHECK(ctx->match_keys.ensure((size_t)P * 2 * kcap * sizeof(unsigned long long)));
-    if (ctx->match_keys.p != kp) VS_HIP(hipMemsetAsync(ctx->match_keys.p, 0xFF, ctx->match_keys.bytes, s));
-    void* cp = ctx->match_cnt.p;
+    if (ctx->match_keys.bytes != kb) VS_HIP(hipMemsetAsync(ctx->match_keys.p, 0xFF, ctx->match_keys.bytes, s));
+    const size_t cb = ctx->match_cnt.bytes;
     VS_CHECK(ctx->match_cnt.ensure((size_t)P * sizeof(unsigned)));
-    if (ctx->match_cnt.p != cp) VS_HIP(hipMemsetAsync(ctx->match_cnt.p, 0, ctx->match_cnt.bytes, s));
+    if (ctx->match_cnt.bytes != cb) VS_HIP(hipMemsetAsync(ctx->match_cnt.p, 0, ctx->match_cnt.bytes, s));
     *keys = ctx->match_keys.as<unsigned long long>();
     *cnt = ctx->match_cnt.as<unsigned>();
     return VS_OK;

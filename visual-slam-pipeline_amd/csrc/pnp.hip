@@ -468,13 +468,14 @@ __global__ __launch_bounds__(256) void k_pnp_ransac(const float* __restrict__ ob
         PNP_T0();
         if (tid == 0) {
             int niters = niters0, best = 0, best_iter = -1, it = 0;
+            const double log_num = ransac_log_num(conf);
             for (; it < niters; it++) {
                 const int c = count[it];
                 if (c < 0) continue;
                 if (c > (best > model_points - 1 ? best : model_points - 1)) {
                     best = c;
                     best_iter = it;
-                    niters = ransac_update_num_iters(conf, (double)(n - c) / n, model_points, niters);
+                    niters = ransac_update_num_iters_ln(log_num, (double)(n - c) / n, model_points, niters);
                 }
             }
             S.best = best;

@@ -89,18 +89,25 @@ VS_HD inline uint64_t mwc_jump(uint64_t s, int k, uint64_t mont_pow_k) {
 }
 
 // cv::RANSACUpdateNumIters
-VS_HD inline int ransac_update_num_iters(double p, double ep, int model_points, int max_iters) {
+// log(max(1 - p, DBL_MIN)) of RANSACUpdateNumIters (p clamped to [0, 1]): constant per caller,
+// so replay loops compute it once
+VS_HD inline double ransac_log_num(double p) {
     p = p > 0. ? p : 0.;
     p = p < 1. ? p : 1.;
+    return vs_cr::log((1. - p) > DBL_MIN ? (1. - p) : DBL_MIN);
+}
+VS_HD inline int ransac_update_num_iters_ln(double log_num, double ep, int model_points, int max_iters) {
     ep = ep > 0. ? ep : 0.;
     ep = ep < 1. ? ep : 1.;
-    double num = (1. - p) > DBL_MIN ? (1. - p) : DBL_MIN;
     double denom = 1. - vs_cr::pow(1. - ep, model_points);
     if (denom < DBL_MIN) return 0;
-    num = vs_cr::log(num);
+    const double num = log_num;
     denom = vs_cr::log(denom);
     if (denom >= 0 || -num >= max_iters * (-denom)) return max_iters;
     return (int)lrint(num / denom);  // cvRound
+}
+VS_HD inline int ransac_update_num_iters(double p, double ep, int model_points, int max_iters) {
+    return ransac_update_num_iters_ln(ransac_log_num(p), ep, model_points, max_iters);
 }
 
 // ------------------------------------------------------------- small dense linear algebra
@@ -329,7 +336,9 @@ VS_HD inline void rod_v2m(const double r[3], double R[9]) {
         for (int i = 0; i < 9; i++) R[i] = (i % 4 == 0) ? 1.0 : 0.0;
         return;
     }
-    const double c = vs_cr::cos(theta), s = vs_cr::sin(theta), c1 = 1.0 - c;
+    double s, c;
+    vs_cr::sincos(theta, s, c);  // one reduction for both (correctly rounded each)
+    const double c1 = 1.0 - c;
     const double it = 1.0 / theta;
     const double x = r[0] * it, y = r[1] * it, z = r[2] * it;
     const double rrt[9] = {x * x, x * y, x * z, x * y, y * y, y * z, x * z, y * z, z * z};

@@ -85,6 +85,11 @@ _SIG = {
     "vs_midas_preprocess_dev": (_I, [_P, _I, _P, _I, _I, _P, _P]),
     "vs_midas_forward_dev": (_I, [_P, _I, _P, _P, _P]),
     "vs_midas_postprocess_dev": (_I, [_P, _I, _P, _I, _I, _P, _P]),
+    "vs_batch_unique_id": (_I, [_P]),
+    "vs_batch_create": (_I, [_P, _I, _I, _I, _I, _I, _P, ctypes.POINTER(_P)]),
+    "vs_batch_destroy": (None, [_P]),
+    "vs_batch_step_dev": (_I, [_P, _P, _P, _P, _I, _P, _P]),
+    "vs_batch_features_dev": (_I, [_P, _P, _P, _P, _P]),
     "vs_spcf_write": (ctypes.c_int, [ctypes.c_char_p, _I, _P, _P, _P, _P, _I, _I]),
     "vs_spcf_write_dev": (_I, [_P, ctypes.c_char_p, _I, _P, _P, _P, _P, _I, _I, _P]),
     "vs_spcf_read": (_I, [ctypes.c_char_p, _I, _I, _P, _P, _P, _P, _P]),
@@ -613,3 +618,48 @@ class Midas:
 
     def postprocess_dev(self, B, d_small, h, w, d_depth, stream=None):
         _check(self.lib.vs_midas_postprocess_dev(self.h, B, d_small, h, w, d_depth, stream))
+
+
+# ---- (e) the offline frame-sharded front end in C (vs_batch) ----------------------------------
+class PairMotion(ctypes.Structure):
+    _fields_ = [("ok3d", ctypes.c_int), ("R3", ctypes.c_double * 9), ("t3", ctypes.c_double * 3),
+                ("okE", ctypes.c_int), ("RE", ctypes.c_double * 9), ("tE", ctypes.c_double * 3),
+                ("scale", ctypes.c_double), ("n_good", ctypes.c_int), ("n_kept", ctypes.c_int)]
+
+
+def batch_unique_id():
+    buf = ctypes.create_string_buffer(128)
+    _check(load_library().vs_batch_unique_id(buf))
+    return buf.raw
+
+
+class Batch:
+    """vs_batch: DevicePipeline's stages behind the C ABI (one rank per process; world > 1 over RCCL)."""
+
+    def __init__(self, ctx, B, h=480, w=640, rank=0, world=1, uid=None):
+        self.lib = ctx.lib
+        self.B = B
+        h_ = ctypes.c_void_p()
+        idb = None if uid is None else ctypes.create_string_buffer(uid, 128)
+        _check(self.lib.vs_batch_create(ctx.h, B, h, w, rank, world, idb, ctypes.byref(h_)))
+        self.h = h_
+
+    def close(self):
+        if self.h:
+            self.lib.vs_batch_destroy(self.h)
+            self.h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def step_dev(self, d_bgr, d_depth, d_depth_prev, frame_count0, stream=None):
+        out = (PairMotion * self.B)()
+        _check(self.lib.vs_batch_step_dev(self.h, d_bgr, d_depth, d_depth_prev, frame_count0, out, stream))
+        return dict(ok=np.array([m.ok3d for m in out], np.int32), R=np.array([list(m.R3) for m in out]),
+                    t=np.array([list(m.t3) for m in out]), eok=np.array([m.okE for m in out], np.int32),
+                    eR=np.array([list(m.RE) for m in out]), et=np.array([list(m.tE) for m in out]),
+                    escale=np.array([m.scale for m in out]), n_good=np.array([m.n_good for m in out]),
+                    n_kept=np.array([m.n_kept for m in out]))
