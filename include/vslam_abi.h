@@ -402,6 +402,45 @@ int vs_spcf_write_dev(vs_ctx* ctx, const char* path, int F, const int* frame_idx
 int vs_spcf_read(const char* path, int max_frames, int cap, int* frame_idx, vs_keypoint* kps, float* desc, int* n,
                  int* count);
 
+/* ---- F4: dense voxel fusion (main.cpp:1081-1146, dense_map.ply :1463-1474) -------------------
+ * Every processed frame with real depth is back-projected on a pixel_step grid with its pose at
+ * processing time; a point joins the cloud the first time its voxel (floor(p / voxel_size) per
+ * axis) is seen, in the reference's insertion order (frame, then row-major grid).  The cloud lives
+ * in HBM (a voxel hash table of 2^table_log2 slots plus max_points x 3 fp64).  Voxel coordinates
+ * must lie in [-2^20, 2^20) (+-20 km at 2 cm); beyond that, a full table or more than max_points
+ * points, vs_dense_size reports VS_ERR_CAPACITY. */
+typedef struct vs_dense vs_dense;
+typedef struct vs_dense_config {
+    int pixel_step;     /* Config::DENSE_PIXEL_STEP (8) */
+    double max_depth;   /* Config::DENSE_MAX_DEPTH (5.0 m) */
+    double voxel_size;  /* Config::DENSE_VOXEL_SIZE (0.02 m) */
+    double fx, fy, cx, cy;
+    double origin[3];   /* main.cpp's origin_offset (0, 0, 0) */
+    int table_log2;     /* hash table slots (default 24) */
+    long long max_points; /* cloud capacity (default 8 Mi points) */
+} vs_dense_config;
+void vs_dense_default_config(vs_dense_config* cfg);
+/* cfg NULL = the reference's Config values. */
+int vs_dense_create(vs_ctx* ctx, const vs_dense_config* cfg, vs_dense** out);
+void vs_dense_destroy(vs_dense* d);
+int vs_dense_reset(vs_dense* d, void* stream);
+/* nf frames in insertion order: d_depth[f] a device h x w fp32 depth map (metres), R (nf x 9,
+ * camera -> world, row-major) and t (nf x 3) on the host.  Enqueue only. */
+int vs_dense_integrate_dev(vs_dense* d, int nf, const float* const* d_depth, int h, int w, const double* R,
+                           const double* t, void* stream);
+/* Synchronises with the last integrate; *n = points in the cloud. */
+int vs_dense_size(vs_dense* d, long long* n);
+/* The first min(cap, n) points (x, y, z fp64) to host memory; *n = points in the cloud. */
+int vs_dense_points(vs_dense* d, long long cap, double* xyz, long long* n);
+/* The cloud in HBM ([max_points][3] fp64; valid after vs_dense_size). */
+const double* vs_dense_points_dev(vs_dense* d);
+/* dense_map.ply as main.cpp:1463-1474 writes it (ascii, 6 decimals). */
+int vs_dense_write_ply(vs_dense* d, const char* path);
+/* Attach a dense cloud to a tracker: every frame vs_slam_process_batch_dev / _features reports as
+ * processed and that has depth is integrated with its pose right after Slam::process_frame, as the
+ * reference's main loop does (NULL detaches). */
+int vs_slam_attach_dense(vs_slam* slam, vs_dense* d);
+
 /* ---- profiling ----------------------------------------------------------------------- */
 /* When enabled, every stage of the _dev pipelines brackets its launches with hipEvents on the
  * stream it runs on; vs_profile_read returns per-stage accumulated milliseconds and launch

@@ -66,6 +66,10 @@ _SIG = {
     "orc_expf_exhaustive_check": (ctypes.c_long, [ctypes.c_float, ctypes.c_float]),
     "orc_expf_restated_check": (ctypes.c_long, [ctypes.c_float, ctypes.c_float, ctypes.c_int]),
     "orc_crmath": (None, [ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
+    "orc_dense_create": (_P, [_I] + [ctypes.c_double] * 9),
+    "orc_dense_destroy": (None, [_P]),
+    "orc_dense_integrate": (None, [_P, _P, _I, _I, _P, _P]),
+    "orc_dense_points": (ctypes.c_longlong, [_P, _P, ctypes.c_longlong]),
 }
 
 _lib = None
@@ -426,6 +430,35 @@ def expf_exhaustive_check(lo, hi):
 def expf_restated_check(lo, hi, use_fma=1):
     """Number of floats x in [lo, hi] (hi <= 0) where the product's glibc_expf.h differs from libm."""
     return lib().orc_expf_restated_check(lo, hi, use_fma)
+
+
+class Dense:
+    """Dense voxel fusion (main.cpp:1081-1139), sequential: the checker for vslam_abi.Dense."""
+
+    def __init__(self, pixel_step=8, max_depth=5.0, voxel_size=0.02, K=(525.0, 525.0, 319.5, 239.5),
+                 origin=(0.0, 0.0, 0.0)):
+        self.h = lib().orc_dense_create(pixel_step, max_depth, voxel_size, *K, *origin)
+
+    def close(self):
+        if self.h:
+            lib().orc_dense_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        self.close()
+
+    def integrate(self, depth, R, t):
+        """One processed frame: depth [h, w] float32 metres, R [3, 3] camera -> world, t [3]."""
+        depth = np.ascontiguousarray(depth, np.float32)
+        R = np.ascontiguousarray(R, np.float64)
+        t = np.ascontiguousarray(t, np.float64)
+        lib().orc_dense_integrate(self.h, _p(depth), depth.shape[0], depth.shape[1], _p(R), _p(t))
+
+    def points(self):
+        n = lib().orc_dense_points(self.h, None, 0)
+        out = np.zeros((n, 3), np.float64)
+        lib().orc_dense_points(self.h, _p(out), n)
+        return out
 
 
 class Slam:

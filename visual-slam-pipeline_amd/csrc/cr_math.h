@@ -15,8 +15,8 @@
 // products) with ~2^-100 relative error before the final rounding, so the rounded result is the
 // correctly rounded one except within 2^-100 of a rounding midpoint (probability ~2^-47 per call).
 //   sin / cos: x - k pi/2 with a triple-double pi/2, then r = j/64 + b with a 53-entry double-double
-//         table of sin / cos (j/64), Taylor series of degree 13 / 12 on |b| <= 1/128 and the
-//         addition formulas (sincos shares the reduction);
+//         table of sin / cos (j/64), Taylor series of degree 13 / 12 on |b| <= 1/128 (terms past
+//         u^3 in plain double) and the addition formulas (sincos shares the reduction);
 //   acos: pi/2 - asin(c) for |c| <= 1/2, 2 asin(sqrt((1 -+ c) / 2)) beyond, asin by one
 //         double-double Newton step on sin from the libm estimate;
 //   log: one Newton step on exp from the libm estimate; pow(y, p) = exp(p log y), integer
@@ -181,24 +181,27 @@ __device__ __constant__ const double kSinCos64Dev[53][4] = VS_CR_SINCOS64;
 #endif
 inline constexpr double kSinCos64[53][4] = VS_CR_SINCOS64;
 
-// sin(b), cos(b) for |b| <= 1/128 (+ slack): Taylor to b^13 / b^12 (terms below 2^-113)
+// sin(b), cos(b) for |b| <= 1/128 (+ slack): Taylor to b^13 / b^12.  With u = b^2 <= 2^-14 the
+// terms from u^4 on are below 2^-68 relative, so they are summed in plain double (error < 2^-120)
+// and only the first four steps of the Horner chain run in double-double.
 VS_CR_HD inline dd sin_small(dd b) {  // b * sum_{k=0}^{6} (-1)^k u^k / (2k+1)!
     const dd u = mul(b, b);
-    dd p = inv_fact(13);
-    for (int k = 5; k >= 0; k--) {
-        p = mul(p, u);
-        p = (k & 1) ? sub(p, inv_fact(2 * k + 1)) : add(p, inv_fact(2 * k + 1));
-    }
+    const double ud = u.hi;
+    const double tl = inv_fact(9).hi + ud * (-inv_fact(11).hi + ud * inv_fact(13).hi);
+    dd p = sub(mul_d(u, tl), inv_fact(7));
+    p = add(mul(p, u), inv_fact(5));
+    p = sub(mul(p, u), inv_fact(3));
+    p = add(mul(p, u), dd{1.0, 0.0});
     return mul(p, b);
 }
 VS_CR_HD inline dd cos_small(dd b) {  // sum_{k=0}^{6} (-1)^k u^k / (2k)!
     const dd u = mul(b, b);
-    dd p = inv_fact(12);
-    for (int k = 5; k >= 0; k--) {
-        p = mul(p, u);
-        p = (k & 1) ? sub(p, inv_fact(2 * k)) : add(p, inv_fact(2 * k));
-    }
-    return p;
+    const double ud = u.hi;
+    const double tl = inv_fact(8).hi + ud * (-inv_fact(10).hi + ud * inv_fact(12).hi);
+    dd p = sub(mul_d(u, tl), inv_fact(6));
+    p = add(mul(p, u), inv_fact(4));
+    p = sub(mul(p, u), inv_fact(2));
+    return add(mul(p, u), dd{1.0, 0.0});
 }
 // sin(r), cos(r) for |r| <= pi/4: r = a + b with a = j/64 (table), |b| <= 1/128 (the subtraction
 // r.hi - a is exact), then the addition formulas in double-double

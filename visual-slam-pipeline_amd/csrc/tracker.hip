@@ -942,6 +942,10 @@ struct vs_slam {
     std::unique_ptr<vs_trk::Tracker<vs::GpuOps>> trk;
     std::vector<vs_trk::FramePtr> batch;  // frames of the batch being processed
     FILE* trace = nullptr;                // VS_TRACE_GPU=path: stage trace (debugging aid)
+    // dense fusion (main.cpp:1116-1139): processed frames with depth, pose right after process_frame
+    vs_dense* dense = nullptr;
+    std::vector<const float*> dense_depth;
+    std::vector<double> dense_R, dense_t;
 };
 
 using namespace vs;
@@ -957,13 +961,29 @@ struct CtxStream {
     ~CtxStream() { c->stream = old; }
 };
 
-// After a batch (or a single frame): live frames still sitting in a batch-region slot move to
-// persistent slots; dead frames drop their device slot and host working data (the map keeps only
-// their pose for the trajectory).
+// main.cpp:1116-1118: a processed frame with real depth joins the dense cloud with its pose now
+void dense_record(vs_slam* sl, const vs_trk::Frame& f) {
+    if (!sl->dense || !f.depth || f.slot < 0) return;
+    sl->dense_depth.push_back(sl->ops.depth_of(f.slot));
+    sl->dense_R.insert(sl->dense_R.end(), f.R.begin(), f.R.end());
+    sl->dense_t.insert(sl->dense_t.end(), f.t.begin(), f.t.end());
+}
+
+// After a batch (or a single frame): the recorded frames are fused into the dense cloud (before
+// any slot moves), live frames still sitting in a batch-region slot move to persistent slots; dead
+// frames drop their device slot and host working data (the map keeps only their pose for the
+// trajectory).
 int settle(vs_slam* sl) {
     GpuOps& o = sl->ops;
     auto& T = *sl->trk;
     VS_HIP(hipStreamWaitEvent(o.s, o.cspec_ev, 0));  // a discarded speculation still reads the pool
+    if (sl->dense && !sl->dense_depth.empty()) {
+        VS_CHECK(vs_dense_integrate_dev(sl->dense, (int)sl->dense_depth.size(), sl->dense_depth.data(), o.h, o.w,
+                                        sl->dense_R.data(), sl->dense_t.data(), o.s));
+        sl->dense_depth.clear();
+        sl->dense_R.clear();
+        sl->dense_t.clear();
+    }
     for (int i = 0; i < kPersist; i++) {
         vs_trk::Frame* f = o.owner[i];
         if (f && !T.is_live(f)) {
@@ -1101,6 +1121,7 @@ int vs_slam_process_batch_dev(vs_slam* sl, int B, const uint8_t* d_bgr, const fl
             HostTimer ht(o.hprof, kHFrame);
             processed[b] = sl->trk->process_frame(sl->batch[b]) ? 1 : 0;
         }
+        if (processed[b]) dense_record(sl, *sl->batch[b]);
         if (o.err != VS_OK) {
             rc = o.err;
             o.err = VS_OK;
@@ -1112,6 +1133,9 @@ int vs_slam_process_batch_dev(vs_slam* sl, int B, const uint8_t* d_bgr, const fl
     if (rc != VS_OK) {
         (void)hipStreamSynchronize(o.xs);  // nothing may still write the pool after an error
         (void)hipStreamSynchronize(o.s2);
+        sl->dense_depth.clear();
+        sl->dense_R.clear();
+        sl->dense_t.clear();
         return rc;
     }
     return settle(sl);
@@ -1140,8 +1164,18 @@ int vs_slam_process_features(vs_slam* sl, int n_kp, const vs_keypoint* kps, cons
         o.err = VS_OK;
         return rc;
     }
+    if (*processed) dense_record(sl, *f);
     sl->batch.assign(1, f);
     return settle(sl);
+}
+
+int vs_slam_attach_dense(vs_slam* sl, vs_dense* d) {
+    VS_ARG(sl, "vs_slam_attach_dense: null argument");
+    sl->dense = d;
+    sl->dense_depth.clear();
+    sl->dense_R.clear();
+    sl->dense_t.clear();
+    return VS_OK;
 }
 
 int vs_slam_finish(vs_slam* sl) {

@@ -93,6 +93,16 @@ _SIG = {
     "vs_spcf_write": (ctypes.c_int, [ctypes.c_char_p, _I, _P, _P, _P, _P, _I, _I]),
     "vs_spcf_write_dev": (_I, [_P, ctypes.c_char_p, _I, _P, _P, _P, _P, _I, _I, _P]),
     "vs_spcf_read": (_I, [ctypes.c_char_p, _I, _I, _P, _P, _P, _P, _P]),
+    "vs_dense_default_config": (None, [_P]),
+    "vs_dense_create": (_I, [_P, _P, ctypes.POINTER(_P)]),
+    "vs_dense_destroy": (None, [_P]),
+    "vs_dense_reset": (_I, [_P, _P]),
+    "vs_dense_integrate_dev": (_I, [_P, _I, _P, _I, _I, _P, _P, _P]),
+    "vs_dense_size": (_I, [_P, ctypes.POINTER(ctypes.c_longlong)]),
+    "vs_dense_points": (_I, [_P, ctypes.c_longlong, _P, ctypes.POINTER(ctypes.c_longlong)]),
+    "vs_dense_points_dev": (_P, [_P]),
+    "vs_dense_write_ply": (_I, [_P, ctypes.c_char_p]),
+    "vs_slam_attach_dense": (_I, [_P, _P]),
     "vs_profile_enable": (_I, [_P, _I]),
     "vs_profile_reset": (_I, [_P]),
     "vs_profile_read": (_I, [_P, _I, _P, _P, _P, _P]),
@@ -516,6 +526,11 @@ class Slam:
         s = self.stats()
         return {k: int(s[i]) for i, k in enumerate(SLAM_STATS)}
 
+    def attach_dense(self, dense):
+        """Fuse every processed frame with depth into `dense` (a Dense, or None to detach)."""
+        _check(self.lib.vs_slam_attach_dense(self.h, None if dense is None else dense.h))
+        self._dense = dense  # keep it alive while attached
+
     def map_points(self):
         n = ctypes.c_int(0)
         _check(self.lib.vs_slam_map(self.h, 0, None, None, ctypes.byref(n)))
@@ -561,6 +576,70 @@ def spcf_read(path, cap=SP_MAX_KEYPOINTS):
         _check(_lib.vs_spcf_read(os.fsencode(path), E, cap, _ptr(idx), _ptr(kps), _ptr(desc), _ptr(n),
                                  ctypes.byref(cnt)))
     return idx[:E], kps[:E], desc[:E], n[:E]
+
+
+# ---- F4: dense voxel fusion (main.cpp:1081-1146) ----------------------------------------------
+class DenseConfig(ctypes.Structure):
+    _fields_ = [("pixel_step", ctypes.c_int), ("max_depth", ctypes.c_double), ("voxel_size", ctypes.c_double),
+                ("fx", ctypes.c_double), ("fy", ctypes.c_double), ("cx", ctypes.c_double), ("cy", ctypes.c_double),
+                ("origin", ctypes.c_double * 3), ("table_log2", ctypes.c_int), ("max_points", ctypes.c_longlong)]
+
+
+class Dense:
+    """vs_dense: the reference main loop's dense cloud (first point per 2 cm voxel) in HBM."""
+
+    def __init__(self, ctx, **overrides):
+        self.ctx = ctx
+        self.lib = ctx.lib
+        cfg = DenseConfig()
+        self.lib.vs_dense_default_config(ctypes.byref(cfg))
+        for k, v in overrides.items():
+            if k == "origin":
+                cfg.origin[:] = [float(x) for x in v]
+            else:
+                setattr(cfg, k, v)
+        self.cfg = cfg
+        h = ctypes.c_void_p()
+        _check(self.lib.vs_dense_create(ctx.h, ctypes.byref(cfg), ctypes.byref(h)))
+        self.h = h
+
+    def close(self):
+        if self.h:
+            self.lib.vs_dense_destroy(self.h)
+            self.h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def reset(self, stream=None):
+        _check(self.lib.vs_dense_reset(self.h, stream))
+
+    def integrate_dev(self, d_depths, h, w, R, t, stream=None):
+        """d_depths: list of device pointers (ints) to h x w fp32 maps; R [n, 3, 3], t [n, 3] host."""
+        n = len(d_depths)
+        ptrs = (ctypes.c_void_p * max(n, 1))(*d_depths)
+        R = np.ascontiguousarray(R, np.float64).reshape(n, 9)
+        t = np.ascontiguousarray(t, np.float64).reshape(n, 3)
+        _check(self.lib.vs_dense_integrate_dev(self.h, n, ctypes.cast(ptrs, ctypes.c_void_p), h, w, _ptr(R), _ptr(t),
+                                               stream))
+
+    def size(self):
+        n = ctypes.c_longlong(0)
+        _check(self.lib.vs_dense_size(self.h, ctypes.byref(n)))
+        return n.value
+
+    def points(self):
+        m = self.size()
+        out = np.zeros((max(m, 1), 3), np.float64)
+        n = ctypes.c_longlong(0)
+        _check(self.lib.vs_dense_points(self.h, m, _ptr(out), ctypes.byref(n)))
+        return out[:m]
+
+    def write_ply(self, path):
+        _check(self.lib.vs_dense_write_ply(self.h, os.fsencode(path)))
 
 
 # ---- F3: DepthEstimator (MiDaS v2.1-small) ----------------------------------------------------
