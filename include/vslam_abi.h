@@ -277,8 +277,9 @@ int vs_local_ba(vs_ctx* ctx, int N, double* R_world, double* t_world, int M, dou
 /* A vs_slam is the reference's Slam object for the per-frame path: map, keyframes, EKF, RTS
  * smoother (host/tracker.hpp restates the control flow; every arithmetic stage runs on the GPU
  * through the context it was created on).  Images are 640 x 480 (Config.h:10-11), K is the
- * reference's (Config.h:14-17).  Loop closure is not run: it only feeds the pose graph that the
- * reference never optimises (Slam.cpp:1748 has no caller), so it cannot change a pose. */
+ * reference's (Config.h:14-17).  Loop closure runs as the reference's does (loop edges and PGO
+ * constraints, vs_slam_loops); like the reference it never changes a pose (the pose graph is never
+ * optimised: Slam.cpp:1748 has no caller). */
 typedef struct vs_slam vs_slam;
 #define VS_SLAM_NSTATS 24
 /* max_batch: frames per vs_slam_process_batch_dev call (the device frame pool holds two batches). */
@@ -318,6 +319,11 @@ int vs_slam_trajectory(vs_slam* slam, int cap, int* ids, double* timestamps, dou
  *  map points, valid map points, frame_count_, keyframe_count_, last match count,
  *  F-RANSAC iterations (sum over chains), 0} */
 int vs_slam_stats(vs_slam* slam, int* out, int cap);
+/* Loop closures (Slam::handle_loop_closure, Slam.cpp:730-798, every 200 keyframes): loop edges
+ * (matched keyframe id, frame id; Slam::loop_edges_) and the PGO constraints of verified loops
+ * (16 doubles each: from id, to id, R_rel[9], t_rel[3], trans_sigma, rot_sigma); the first cap of
+ * each are written (buffers nullable).  stats[23] = LoopCloser::loop_count(). */
+int vs_slam_loops(vs_slam* slam, int cap, int* edges, double* constraints, int* n_edges, int* n_constraints);
 /* Map points (Map::map_points): *n = count; the first cap positions (world, x 3) and validity
  * bytes are written (each nullable). */
 int vs_slam_map(vs_slam* slam, int cap, double* pos, uint8_t* valid, int* n);

@@ -61,6 +61,7 @@ _SIG = {
     "orc_slam_stats": (None, [_P, _P]),
     "orc_slam_stage_seconds": (ctypes.c_int, [_P, _P, ctypes.c_int]),
     "orc_slam_map": (_I, [_P, _I, _P, _P]),
+    "orc_slam_loops": (_I, [_P, _I, _P, _P, _P]),
     "orc_mt19937": (None, [ctypes.c_uint32, _I, _P]),
     "orc_expf_array": (None, [_P, _I, _P]),
     "orc_expf_exhaustive_check": (ctypes.c_long, [ctypes.c_float, ctypes.c_float]),
@@ -526,3 +527,14 @@ class Slam:
         valid = np.zeros(max(n, 1), np.uint8)
         lib().orc_slam_map(self.h, n, _p(pos), _p(valid))
         return pos[:n], valid[:n]
+
+    def loops(self):
+        """(edges [E, 2] (matched frame id, frame id), constraints [C, 16] = from, to, R_rel[9],
+        t_rel[3], trans_sigma, rot_sigma) of Slam::handle_loop_closure."""
+        ne = ctypes.c_int(0)
+        nc = lib().orc_slam_loops(self.h, 0, None, None, ctypes.byref(ne))
+        cap = max(ne.value, nc, 1)
+        e = np.zeros((cap, 2), np.int32)
+        c = np.zeros((cap, 16))
+        lib().orc_slam_loops(self.h, cap, _p(e), _p(c), ctypes.byref(ne))
+        return e[:ne.value], c[:nc]

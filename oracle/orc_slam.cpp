@@ -151,6 +151,27 @@ struct OracleOps {
         return r;
     }
 
+    // LoopCloser::detect's per-keyframe evaluation (LoopCloser.cpp:50-76): knnMatch + ratio 0.75,
+    // then findEssentialMat(RANSAC, 0.999, 1.0) on the matched pixels and its inlier count
+    std::vector<vs_trk::LoopEval> loop_eval(const Frame& cur, const std::vector<const Frame*>& kfs) {
+        std::vector<vs_trk::LoopEval> out(kfs.size());
+        for (size_t i = 0; i < kfs.size(); i++) {
+            const std::vector<Match> good = match(cur, *kfs[i], vs_trk::cfg::L2_RATIO_THRESHOLD);
+            out[i].n_good = (int)good.size();
+            if (out[i].n_good < vs_trk::cfg::MIN_MATCHES) continue;
+            StageTimer st(&sec[kMotion]);
+            std::vector<float> p1, p2;
+            points(cur, *kfs[i], good, p1, p2);
+            const int n = (int)(p1.size() / 2);
+            std::vector<uint8_t> mask(std::max(n, 1));
+            double R[9], t[3];
+            int inl = 0, g = 0;
+            orc_estimate_motion(p1.data(), p2.data(), n, K, R, t, mask.data(), &inl, &g);
+            out[i].inliers = inl;
+        }
+        return out;
+    }
+
     std::vector<std::pair<int, int>> match_map(const Map&, const Frame& f, const std::vector<int>& ids, float ratio) {
         StageTimer st(&sec[kMatchMap]);
         std::vector<std::pair<int, int>> out;
@@ -255,8 +276,10 @@ int orc_slam_process(void* h, int n_kp, const orc_keypoint* kps, const float* de
             g->own_depth();
             keep.push_back(g);
         } else {
-            g->desc = std::vector<float>();
-            g->kps = std::vector<vs_trk::Keypoint>();
+            if (!g->keyframe) {  // keyframes keep their features for loop closure (LoopCloser.cpp:43-48)
+                g->desc = std::vector<float>();
+                g->kps = std::vector<vs_trk::Keypoint>();
+            }
             g->mp_idx = std::vector<int>();
             g->depth = nullptr;
             g->depth_store = std::vector<float>();
@@ -290,8 +313,31 @@ void orc_slam_stats(void* h, int* out) {
                        S.bridges,     S.recoveries,   S.recovery_failed, S.stationary,   S.keyframes,
                        S.pnp_refined, S.periodic_pnp, S.tracked_total, S.triangulated,   S.depth_points,
                        S.culled,      S.chains_discarded, m.size(),   valid,             s->trk.frame_count(),
-                       s->trk.keyframe_count(), s->trk.last_match_count(), S.f_iters, 0};
+                       s->trk.keyframe_count(), s->trk.last_match_count(), S.f_iters, s->trk.loop_count()};
     std::memcpy(out, v, sizeof(v));
+}
+
+// Loop edges (matched frame id, frame id) and PGO constraints {from, to, R_rel[9], t_rel[3],
+// trans_sigma, rot_sigma} (16 doubles each): returns the constraint count; *n_edges = edge count.
+int orc_slam_loops(void* h, int cap, int* edges, double* cons, int* n_edges) {
+    const auto& T = static_cast<OrcSlam*>(h)->trk;
+    const auto& E = T.loop_edges();
+    const auto& C = T.loop_constraints();
+    *n_edges = (int)E.size();
+    for (int i = 0; i < (int)E.size() && i < cap && edges; i++) {
+        edges[2 * i] = E[i].first;
+        edges[2 * i + 1] = E[i].second;
+    }
+    for (int i = 0; i < (int)C.size() && i < cap && cons; i++) {
+        double* c = cons + 16 * i;
+        c[0] = C[i].from_id;
+        c[1] = C[i].to_id;
+        std::memcpy(c + 2, C[i].R_rel.data(), 9 * sizeof(double));
+        std::memcpy(c + 11, C[i].t_rel.data(), 3 * sizeof(double));
+        c[14] = C[i].trans_sigma;
+        c[15] = C[i].rot_sigma;
+    }
+    return (int)C.size();
 }
 
 // Map point positions and validity (for map-level comparisons): returns the count.

@@ -4,8 +4,9 @@ F1: Slam::process_frame, reference src/Slam.cpp:809-1135, restated in host/track
 bench.py runs vs_slam_process_batch_dev with B = 32 frames per call, each batch's extraction
 prefetched behind the previous batch's (vs_slam_prefetch_batch_dev), the default extraction chunk
 schedule (3, 4, 5, 7, 8, 5) on its own CU-masked stream, the speculative next-frame chain and the
-default VS_SLAM_TRACK_CUS, over the 126-frame closed loop replayed with continuing timestamps.  This test runs exactly that for 416
-frames (3.3 laps, map past 20k points) and the oracle tracker (oracle/orc_slam.cpp: the same control
+default VS_SLAM_TRACK_CUS, over the 126-frame closed loop replayed with continuing timestamps.  This test runs exactly that for
+the bench's 800 frames (6.3 laps, map past 30k points, 200+ keyframes so that loop closure runs,
+Slam.cpp:1084-1086) and the oracle tracker (oracle/orc_slam.cpp: the same control
 flow over the CPU restatements) on the same GPU features, and compares decision counters, the whole
 trajectory and the map bit for bit: every stage is bit-exact against its CPU restatement, and the
 fp64 transcendental functions both sides use (Rodrigues, the 7-point cubic, RANSACUpdateNumIters)
@@ -24,7 +25,7 @@ pytestmark = pytest.mark.gpu
 
 LOOP = 126
 B = 32
-STEPS = 13          # 416 frames
+STEPS = 25          # 800 frames, as bench.py
 T0 = 1311868164.0
 
 
@@ -62,7 +63,7 @@ def gpu_run(vsctx, loop):
                                         [3 * (g0 + j) for j in range(B)]).tolist()
         traj_raw = S.trajectory()
         S.finish()
-        return done, S.stats(), traj_raw, S.trajectory(), S.map_points()
+        return done, S.stats(), traj_raw, S.trajectory(), S.map_points(), S.loops()
 
 
 @pytest.fixture(scope="module")
@@ -74,7 +75,7 @@ def oracle_run(oracle, loop, loop_feats):
         done.append(S.process(k, d, loop["depth"][g % LOOP], T0 + 0.1 * g, 3 * g))
     traj_raw = S.trajectory()
     S.finish()
-    out = done, S.stats(), traj_raw, S.trajectory(), S.map_points()
+    out = done, S.stats(), traj_raw, S.trajectory(), S.map_points(), S.loops()
     S.close()
     return out
 
@@ -92,6 +93,21 @@ def test_bench_scale_tracker_matches_oracle(gpu_run, oracle_run, loop):
         assert np.array_equal(gR, oR) and np.array_equal(gt, ot)
     (gp, gv), (op, ov) = g[4], o[4]
     assert np.array_equal(gv, ov) and np.array_equal(gp, op)
+
+
+def test_bench_scale_loop_closure_matches_oracle(gpu_run, oracle_run):
+    """LoopCloser::detect + Slam::handle_loop_closure (LoopCloser.cpp:16-100, Slam.cpp:730-798) at
+    keyframe 200: the batched candidate evaluation on the GPU (one match launch over every 5th
+    keyframe 200+ ids back, one E-RANSAC launch) finds the same loop as the oracle's sequential
+    loop, and the PnP-verified constraint is identical bit for bit.  The synthetic sequence is a
+    closed loop, so a loop must be found."""
+    (ge, gc), (oe, oc) = gpu_run[5], oracle_run[5]
+    stats = dict(zip(vslam_abi.SLAM_STATS, gpu_run[1].tolist()))
+    assert stats["keyframe_count"] >= 200 and stats["loop_count"] >= 1, stats
+    assert np.array_equal(ge, oe) and ge.shape[0] == stats["loop_count"]
+    assert np.array_equal(gc.view(np.uint64), oc.view(np.uint64))
+    for e in ge:
+        assert e[1] - e[0] >= 200  # LC_MIN_FRAME_GAP in frame ids
 
 
 def test_bench_scale_ate_is_the_algorithms(gpu_run, oracle_run, loop):

@@ -180,11 +180,11 @@ __global__ __launch_bounds__(1024) void k_pnp_gather(const int* __restrict__ kpm
 
 // Host-side wall time per back-end operation (VS_SLAM_HOST_PROFILE=1: printed to stderr when the
 // vs_slam is destroyed); the rest of process_frame is the tracker's own host logic.
-enum HostOp { kHChain, kHMatch, kHFmat, kHMotion, kHTlm, kHPnp, kHMatchMap, kHAppend, kHVis, kHFrame, kHWait, kHSpec, kHOps };
+enum HostOp { kHChain, kHMatch, kHFmat, kHMotion, kHTlm, kHPnp, kHMatchMap, kHAppend, kHVis, kHFrame, kHWait, kHSpec, kHLoop, kHOps };
 static const char* const kHostOpNames[kHOps] = {"chain", "match", "find_fundamental", "motion_points",
                                                 "track_local_map", "solve_pnp", "match_map", "map_append",
                                                 "visibility", "process_frame (total)", "extract wait",
-                                                "chain: speculation wait"};
+                                                "chain: speculation wait", "loop_eval"};
 struct HostProf {
     bool on = false;
     long skip = 64;  // frames before counting starts (first launches load code objects)
@@ -262,6 +262,11 @@ struct GpuOps {
     bool valid_dirty = false;
     Pinned pin;
     std::vector<vs_trk::Frame*> owner;  // persistent slot owners (slots 2B .. 2B + kPersist)
+    // Keyframe feature archive (loop closure reads keyframes long after their slots are gone):
+    // [arch_cap][kCap] keypoints, [arch_cap][kCap][256] descriptors, [arch_cap] counts.
+    DevBuf arch_kps, arch_desc, arch_n;
+    int arch_cap = 0, arch_used = 0;
+    DevBuf lc_buf;  // loop-closure candidate pool and outputs
     int err = VS_OK;                     // first error inside an Ops call (the tracker has no error channel)
 
     vs_keypoint* kps_of(int slot) const { return pool_kps.as<vs_keypoint>() + (size_t)slot * kCap; }
@@ -864,6 +869,117 @@ struct GpuOps {
         return r;
     }
 
+    int grow_archive(int need) {
+        if (need <= arch_cap) return VS_OK;
+        const int cap = std::max(need, std::max(16, 2 * arch_cap));
+        DevBuf nk, nd, nn;
+        VS_CHECK(nk.ensure((size_t)cap * kCap * sizeof(vs_keypoint)));
+        VS_CHECK(nd.ensure((size_t)cap * kCap * 256 * sizeof(float)));
+        VS_CHECK(nn.ensure((size_t)cap * sizeof(int)));
+        if (arch_used > 0) {
+            VS_HIP(hipMemcpyAsync(nk.p, arch_kps.p, (size_t)arch_used * kCap * sizeof(vs_keypoint), hipMemcpyDeviceToDevice, s));
+            VS_HIP(hipMemcpyAsync(nd.p, arch_desc.p, (size_t)arch_used * kCap * 256 * sizeof(float), hipMemcpyDeviceToDevice, s));
+            VS_HIP(hipMemcpyAsync(nn.p, arch_n.p, (size_t)arch_used * sizeof(int), hipMemcpyDeviceToDevice, s));
+        }
+        VS_HIP(hipStreamSynchronize(s));
+        arch_kps.release();
+        arch_desc.release();
+        arch_n.release();
+        arch_kps = nk;
+        arch_desc = nd;
+        arch_n = nn;
+        nk.p = nd.p = nn.p = nullptr;  // ownership moved
+        arch_cap = cap;
+        return VS_OK;
+    }
+    // A keyframe's features into the archive (at settle, while its pool slot is still intact)
+    int archive(vs_trk::Frame* f) {
+        if (f->kf_slot >= 0 || f->slot < 0) return VS_OK;
+        VS_CHECK(grow_archive(arch_used + 1));
+        const int a = arch_used++;
+        VS_HIP(hipMemcpyAsync(arch_kps.as<vs_keypoint>() + (size_t)a * kCap, kps_of(f->slot), kCap * sizeof(vs_keypoint),
+                              hipMemcpyDeviceToDevice, s));
+        VS_HIP(hipMemcpyAsync(arch_desc.as<float>() + (size_t)a * kCap * 256, desc_of(f->slot),
+                              (size_t)kCap * 256 * sizeof(float), hipMemcpyDeviceToDevice, s));
+        VS_HIP(hipMemcpyAsync(arch_n.as<int>() + a, pool_n.as<int>() + f->slot, sizeof(int), hipMemcpyDeviceToDevice, s));
+        f->kf_slot = a;
+        return VS_OK;
+    }
+
+    // LoopCloser::detect's candidate evaluation (LoopCloser.cpp:50-76) for all candidates at once:
+    // the current frame and the candidates gathered into one pool (keyframes from the archive, or
+    // from their pool slot within the batch that made them), one match_pairs launch over the P
+    // (current, keyframe) pairs, one E-RANSAC launch over their good lists, one read-back.
+    std::vector<vs_trk::LoopEval> loop_eval(const vs_trk::Frame& cur, const std::vector<const vs_trk::Frame*>& kfs) {
+        HostTimer ht(hprof, kHLoop);
+        const int P = (int)kfs.size(), F = P + 1;
+        std::vector<vs_trk::LoopEval> out(P);
+        if (P == 0 || cur.slot < 0) return out;
+        auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
+        const size_t kb = al((size_t)F * kCap * sizeof(vs_keypoint)), db = al((size_t)F * kCap * 256 * sizeof(float));
+        const size_t nb = al((size_t)F * sizeof(int)), pb = al((size_t)2 * P * sizeof(int));
+        const size_t mb = al((size_t)P * kCap * sizeof(vs_match)), cb = al((size_t)P * sizeof(int));
+        const size_t rb = al((size_t)P * 16 * sizeof(double)), gb = al((size_t)P * 8 * sizeof(int));
+        if (failed(lc_buf.ensure(kb + db + nb + pb + 2 * mb + 3 * cb + rb + gb))) return out;
+        char* base = lc_buf.as<char>();
+        auto* d_kps = reinterpret_cast<vs_keypoint*>(base);
+        auto* d_desc = reinterpret_cast<float*>(base + kb);
+        auto* d_n = reinterpret_cast<int*>(base + kb + db);
+        auto* d_pairs = reinterpret_cast<int*>(base + kb + db + nb);
+        auto* d_raw = reinterpret_cast<vs_match*>(base + kb + db + nb + pb);
+        auto* d_good = reinterpret_cast<vs_match*>(base + kb + db + nb + pb + mb);
+        char* tail = base + kb + db + nb + pb + 2 * mb;
+        auto* d_nraw = reinterpret_cast<int*>(tail);
+        auto* d_ngood = reinterpret_cast<int*>(tail + cb);
+        auto* d_ok = reinterpret_cast<int*>(tail + 2 * cb);
+        auto* d_Rt = reinterpret_cast<double*>(tail + 3 * cb);  // R [P][9] | t [P][3] | scale [P]
+        auto* d_diag = reinterpret_cast<int*>(tail + 3 * cb + rb);
+        auto gather = [&](int dst, const vs_keypoint* k, const float* d, const int* n) -> int {
+            VS_HIP(hipMemcpyAsync(d_kps + (size_t)dst * kCap, k, kCap * sizeof(vs_keypoint), hipMemcpyDeviceToDevice, s));
+            VS_HIP(hipMemcpyAsync(d_desc + (size_t)dst * kCap * 256, d, (size_t)kCap * 256 * sizeof(float),
+                                  hipMemcpyDeviceToDevice, s));
+            VS_HIP(hipMemcpyAsync(d_n + dst, n, sizeof(int), hipMemcpyDeviceToDevice, s));
+            return VS_OK;
+        };
+        if (failed(gather(0, kps_of(cur.slot), desc_of(cur.slot), pool_n.as<int>() + cur.slot))) return out;
+        std::vector<int> pairs(2 * P);
+        for (int i = 0; i < P; i++) {
+            const vs_trk::Frame* k = kfs[i];
+            int rc;
+            if (k->kf_slot >= 0)
+                rc = gather(i + 1, arch_kps.as<vs_keypoint>() + (size_t)k->kf_slot * kCap,
+                            arch_desc.as<float>() + (size_t)k->kf_slot * kCap * 256, arch_n.as<int>() + k->kf_slot);
+            else if (k->slot >= 0)
+                rc = gather(i + 1, kps_of(k->slot), desc_of(k->slot), pool_n.as<int>() + k->slot);
+            else {
+                set_error("vs_slam: a loop-closure keyframe has no device features");
+                rc = VS_ERR_CAPACITY;
+            }
+            if (failed(rc)) return out;
+            pairs[2 * i] = 0;
+            pairs[2 * i + 1] = i + 1;
+        }
+        if (failed(upload(d_pairs, pairs.data(), pairs.size() * sizeof(int)))) return out;
+        if (failed(match_pairs(ctx, P, d_pairs, F, d_desc, d_n, kCap, vs_trk::cfg::L2_RATIO_THRESHOLD, d_raw, d_nraw,
+                               d_good, d_ngood, s)))
+            return out;
+        if (failed(emat_pairs(ctx, P, d_pairs, d_kps, kCap, d_good, d_ngood, nullptr, nullptr, h, w, K, d_Rt,
+                              d_Rt + 9 * P, d_Rt + 12 * P, d_ok, d_diag, s)))
+            return out;
+        char* hb = take((size_t)P * 9 * sizeof(int));
+        if (!hb) return out;
+        if (failed(d2h(hb, d_ngood, (size_t)P * sizeof(int))) ||
+            failed(d2h(hb + (size_t)P * sizeof(int), d_diag, (size_t)P * 8 * sizeof(int))) || failed(sync()))
+            return out;
+        const int* ng = reinterpret_cast<const int*>(hb);
+        const int* dg = ng + P;
+        for (int i = 0; i < P; i++) {
+            out[i].n_good = ng[i];
+            out[i].inliers = dg[8 * i + 3];
+        }
+        return out;
+    }
+
     std::vector<std::pair<int, int>> match_map(const vs_trk::Map& m, const vs_trk::Frame& f, const std::vector<int>& ids,
                                                float ratio) {
         HostTimer ht(hprof, kHMatchMap);
@@ -977,6 +1093,8 @@ int settle(vs_slam* sl) {
     GpuOps& o = sl->ops;
     auto& T = *sl->trk;
     VS_HIP(hipStreamWaitEvent(o.s, o.cspec_ev, 0));  // a discarded speculation still reads the pool
+    for (const auto& f : T.map().frames)  // new keyframes' features into the archive (loop closure)
+        if (f->keyframe && f->kf_slot < 0 && f->slot >= 0) VS_CHECK(o.archive(f.get()));
     if (sl->dense && !sl->dense_depth.empty()) {
         VS_CHECK(vs_dense_integrate_dev(sl->dense, (int)sl->dense_depth.size(), sl->dense_depth.data(), o.h, o.w,
                                         sl->dense_R.data(), sl->dense_t.data(), o.s));
@@ -988,8 +1106,10 @@ int settle(vs_slam* sl) {
         vs_trk::Frame* f = o.owner[i];
         if (f && !T.is_live(f)) {
             o.release_slot(f);
-            f->kps.clear();
-            f->kps.shrink_to_fit();
+            if (!f->keyframe) {  // keyframes keep their host keypoints (LoopCloser.cpp:48 checks them)
+                f->kps.clear();
+                f->kps.shrink_to_fit();
+            }
             f->mp_idx.clear();
             f->mp_idx.shrink_to_fit();
             f->depth_store = std::vector<float>();
@@ -1006,8 +1126,10 @@ int settle(vs_slam* sl) {
             }
         } else if (f->slot >= 0 && f->slot < 2 * o.B) {
             f->slot = -1;
-            f->kps.clear();
-            f->kps.shrink_to_fit();
+            if (!f->keyframe) {
+                f->kps.clear();
+                f->kps.shrink_to_fit();
+            }
             f->mp_idx.clear();
             f->mp_idx.shrink_to_fit();
             f->depth = nullptr;
@@ -1056,7 +1178,8 @@ void vs_slam_destroy(vs_slam* sl) {
     o.destroy_streams();
     DevBuf* bufs[] = {&o.pool_kps, &o.pool_desc, &o.pool_n, &o.pool_depth, &o.pool_norms, &o.semi, &o.dgrid,
                       &o.chain_buf,    &o.work, &o.rows_buf,      &o.map_pos, &o.map_desc,  &o.map_valid, &o.map_tmp,
-                      &o.pnp_io,       &o.hdr_buf, &o.chain_buf2, &o.hdr_buf2, &o.mstate2};
+                      &o.pnp_io,       &o.hdr_buf, &o.chain_buf2, &o.hdr_buf2, &o.mstate2,
+                      &o.arch_kps,     &o.arch_desc, &o.arch_n,   &o.lc_buf};
     for (DevBuf* b : bufs) b->release();
     if (sl->trace) std::fclose(sl->trace);
     delete sl;
@@ -1208,8 +1331,31 @@ int vs_slam_stats(vs_slam* sl, int* out, int cap) {
                                    S.stationary,     S.keyframes,      S.pnp_refined,    S.periodic_pnp,
                                    S.tracked_total,  S.triangulated,   S.depth_points,   S.culled,
                                    S.chains_discarded, m.size(),       valid,            sl->trk->frame_count(),
-                                   sl->trk->keyframe_count(), sl->trk->last_match_count(), S.f_iters, 0};
+                                   sl->trk->keyframe_count(), sl->trk->last_match_count(), S.f_iters,
+                                   sl->trk->loop_count()};
     for (int i = 0; i < cap && i < VS_SLAM_NSTATS; i++) out[i] = v[i];
+    return VS_OK;
+}
+
+int vs_slam_loops(vs_slam* sl, int cap, int* edges, double* constraints, int* n_edges, int* n_constraints) {
+    VS_ARG(sl && n_edges && n_constraints, "vs_slam_loops: null argument");
+    const auto& E = sl->trk->loop_edges();
+    const auto& C = sl->trk->loop_constraints();
+    *n_edges = (int)E.size();
+    *n_constraints = (int)C.size();
+    for (int i = 0; i < (int)E.size() && i < cap && edges; i++) {
+        edges[2 * i] = E[i].first;
+        edges[2 * i + 1] = E[i].second;
+    }
+    for (int i = 0; i < (int)C.size() && i < cap && constraints; i++) {
+        double* c = constraints + 16 * i;
+        c[0] = C[i].from_id;
+        c[1] = C[i].to_id;
+        std::memcpy(c + 2, C[i].R_rel.data(), 9 * sizeof(double));
+        std::memcpy(c + 11, C[i].t_rel.data(), 3 * sizeof(double));
+        c[14] = C[i].trans_sigma;
+        c[15] = C[i].rot_sigma;
+    }
     return VS_OK;
 }
 

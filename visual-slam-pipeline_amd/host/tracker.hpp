@@ -17,9 +17,12 @@
 // matching against the map (:546-575), local-map tracking (:380-469), PnP (:505-529) and the
 // O(map points x keypoints) visibility sweep (:1089-1108).
 //
-// Deliberate omissions: loop closure (:1083-1086, 727-798) only appends PGO
-// constraints that nothing consumes (run_posthoc_pgo has no caller), so it never changes a pose;
-// local BA is disabled in the reference (Config.h:99).  The ORB fallback is out of scope.
+// Loop closure (F4: Slam::handle_loop_closure :730-798 with LoopCloser::detect, LoopCloser.cpp:16-100,
+// every LC_CHECK_INTERVAL keyframes, :1084-1086) records loop edges and PGO constraints; like the
+// reference it never changes a pose (run_posthoc_pgo has no caller).  Its back-end op evaluates every
+// candidate keyframe at once (one batched match + E-RANSAC).  Keyframes keep their features for it.
+// Deliberate omissions: local BA is disabled in the reference (Config.h:99).  The
+// ORB fallback is out of scope.
 #pragma once
 
 #include <algorithm>
@@ -52,6 +55,8 @@ constexpr int KF_MIN_FRAME_GAP = 10, KF_MIN_MATCHES = 50;
 constexpr double TRACK_VISIBILITY_RADIUS = 8.0;
 constexpr float CULL_FOUND_RATIO_YOUNG = 0.15f, CULL_FOUND_RATIO_OLD = 0.30f;
 constexpr double MOTION_SCALE = 0.05;
+constexpr int LC_MIN_FRAME_GAP = 200, LC_MIN_INLIERS = 30, LC_CHECK_INTERVAL = 200, LC_NEARBY_FRAME_RANGE = 30;
+constexpr double LC_MAX_JUMP = 0.5, LC_MIN_JUMP = 0.01, PGO_LC_TRANS_SIGMA = 0.03, PGO_LC_ROT_SIGMA = 0.01;
 constexpr double EKF_SIGMA_VIS_3D3D = 0.04, EKF_SIGMA_VIS_EMAT = 0.10, EKF_SIGMA_HEIGHT = 0.01,
                  EKF_PROCESS_ACCEL = 1.0, EKF_VEL_DECAY = 0.95, EKF_INNOV_GATE = 0.3, EKF_MAX_STEP = 0.10;
 }  // namespace cfg
@@ -103,6 +108,7 @@ struct Frame {
     bool keyframe = false;
     std::vector<int> mp_idx;           // Frame::map_point_indices
     int slot = -1;                     // back-end handle (device feature / depth slot)
+    int kf_slot = -1;                  // back-end handle of a keyframe's archived features (loop closure)
     bool has_depth() const { return depth != nullptr; }
     bool has_desc() const { return !kps.empty(); }  // descriptors are empty iff there are no keypoints
     float depth_at(int py, int px) const { return depth[(size_t)py * dw + px]; }
@@ -163,6 +169,21 @@ struct PnPResult {  // Slam::PnPResult
     int inlier_count = 0;
 };
 
+// Slam.h LoopConstraint (PGO edge from a verified loop, Slam.cpp:788-797)
+struct LoopConstraint {
+    int from_id = -1, to_id = -1;
+    M3 R_rel{};
+    V3 t_rel{};
+    double trans_sigma = 0, rot_sigma = 0;
+};
+
+// One loop-closure candidate as LoopCloser::detect sees it (LoopCloser.cpp:50-76): ratio-test
+// matches of the current frame against the keyframe, and the inliers of findEssentialMat on them
+// (0 when E is empty).
+struct LoopEval {
+    int n_good = 0, inliers = 0;
+};
+
 struct AccelSample {
     double timestamp, ax, ay, az;
 };
@@ -215,6 +236,7 @@ class Tracker {
     bool process_frame(const FramePtr& frame) {
         if (!frame) return false;
         last_pnp_ = false;
+        last_loop_ = false;  // :813
         if ((int)frame->kps.size() < cfg::MIN_MATCHES) {  // :820-823
             last_frame_ = frame;
             stats_.rejected++;
@@ -422,7 +444,7 @@ class Tracker {
             stats_.keyframes++;
             setup_new_keyframe(frame);
             if (keyframe_count_ % cfg::PNP_INTERVAL == 0) run_pnp(frame);
-            // :1084-1086 loop closure: omitted, it only feeds the never-run pose graph (header note)
+            if (keyframe_count_ % cfg::LC_CHECK_INTERVAL == 0) handle_loop_closure(frame);  // :1084-1086
             visibility_sweep(frame);  // :1088-1108
             if (keyframe_count_ % 3 == 0) cull_by_found_ratio();  // :1110-1126
             last_keyframe_ = frame;
@@ -493,6 +515,10 @@ class Tracker {
     double reproj_error_before() const { return reproj_error_before_; }
     double reproj_error_after() const { return reproj_error_after_; }
     bool last_pnp() const { return last_pnp_; }
+    bool last_was_loop() const { return last_loop_; }
+    int loop_count() const { return loop_count_; }
+    const std::vector<std::pair<int, int>>& loop_edges() const { return loop_edges_; }  // (matched id, frame id)
+    const std::vector<LoopConstraint>& loop_constraints() const { return loop_constraints_; }
 
    private:
     FILE* trace_ = nullptr;
@@ -652,6 +678,76 @@ class Tracker {
             trace_pose(-1, "", r.R_world, r.t_world);
         }
         return r;
+    }
+
+    // Slam::handle_loop_closure (:730-798) with LoopCloser::detect (LoopCloser.cpp:16-100)
+    void handle_loop_closure(const FramePtr& frame) {
+        // ---- LoopCloser::detect ----
+        if (!frame->has_desc()) return;  // :23
+        std::vector<const Frame*> kfs;   // Map::get_keyframes (Map.cpp:40-47)
+        for (const FramePtr& f : map_.frames)
+            if (f->keyframe) kfs.push_back(f.get());
+        if (kfs.size() < 2) return;  // :26
+        std::vector<const Frame*> cand;  // :44-49 every 5th keyframe at least LC_MIN_FRAME_GAP ids back
+        int checked = 0;
+        for (const Frame* kf : kfs) {
+            if (frame->id - kf->id < cfg::LC_MIN_FRAME_GAP) continue;
+            if (!kf->has_desc()) continue;
+            checked++;
+            if (checked % 5 != 0) continue;
+            cand.push_back(kf);
+        }
+        if (cand.empty()) return;
+        const std::vector<LoopEval> ev = ops_.loop_eval(*frame, cand);
+        int best = -1, best_inliers = 0;
+        for (size_t i = 0; i < cand.size(); i++) {  // :51-88
+            if (ev[i].n_good < cfg::MIN_MATCHES) continue;
+            if (ev[i].inliers < cfg::LC_MIN_INLIERS) continue;  // E.empty() gives 0 inliers
+            if (ev[i].inliers > best_inliers) {
+                best_inliers = ev[i].inliers;
+                best = (int)i;
+            }
+        }
+        if (best < 0 || best_inliers < cfg::LC_MIN_INLIERS) return;  // :91
+        loop_count_++;
+        const Frame* matched = cand[best];
+        if (trace_) std::fprintf(trace_, "%d loop %d inliers %d\n", frame->id, matched->id, best_inliers);
+        // ---- handle_loop_closure ----
+        last_loop_ = true;
+        loop_edges_.emplace_back(matched->id, frame->id);
+        std::vector<int> ids;  // :743-761 valid map points observed within LC_NEARBY_FRAME_RANGE ids
+        for (int i = 0; i < map_.size(); i++) {
+            if (!map_.valid[i]) continue;
+            for (const auto& ob : map_.obs[i])
+                if (std::abs(ob.first - matched->id) < cfg::LC_NEARBY_FRAME_RANGE) {
+                    ids.push_back(i);
+                    break;
+                }
+        }
+        std::vector<float> obj, img;
+        if ((int)ids.size() >= 20 && frame->has_desc()) {  // :763-775 FLANN 2-NN (exact here) + ratio 0.7
+            const auto pairs = ops_.match_map(map_, *frame, ids, cfg::FLANN_RATIO_THRESHOLD);
+            for (const auto& q : pairs) {
+                const int id = ids[q.second];
+                obj.insert(obj.end(), {(float)map_.pos[3 * id], (float)map_.pos[3 * id + 1], (float)map_.pos[3 * id + 2]});
+                img.insert(img.end(), {frame->kps[q.first].x, frame->kps[q.first].y});
+            }
+        }
+        const PnPResult pnp = solve_pnp(obj, img, 300, 15);  // :779-780
+        if (!pnp.success) return;
+        const V3 d{pnp.t_world[0] - t_world_[0], pnp.t_world[1] - t_world_[1], pnp.t_world[2] - t_world_[2]};
+        const double jump = norm3(d);
+        if (jump >= cfg::LC_MAX_JUMP || jump <= cfg::LC_MIN_JUMP) return;  // :782-783
+        LoopConstraint c;  // :788-797
+        c.from_id = matched->id;
+        c.to_id = frame->id;
+        const M3 Rft = tr(matched->R);
+        c.R_rel = mul(Rft, pnp.R_world);
+        c.t_rel = mulv(Rft, V3{pnp.t_world[0] - matched->t[0], pnp.t_world[1] - matched->t[1],
+                               pnp.t_world[2] - matched->t[2]});
+        c.trans_sigma = cfg::PGO_LC_TRANS_SIGMA;
+        c.rot_sigma = cfg::PGO_LC_ROT_SIGMA;
+        loop_constraints_.push_back(c);
     }
 
     // Slam::run_pnp (:1477-1522)
@@ -1146,6 +1242,10 @@ class Tracker {
     V3 t_world_{0, 0, 0};
     FramePtr last_frame_, last_keyframe_, ref_frame_;
     int frame_count_ = 0, keyframe_count_ = 0, last_match_count_ = 0;
+    bool last_loop_ = false;
+    int loop_count_ = 0;  // LoopCloser::loop_count_
+    std::vector<std::pair<int, int>> loop_edges_;
+    std::vector<LoopConstraint> loop_constraints_;
     double epipolar_error_before_ = 0, epipolar_error_after_ = 0, reproj_error_before_ = 0, reproj_error_after_ = 0;
     bool last_pnp_ = false;
     double last_good_scale_ = -1.0;

@@ -103,6 +103,7 @@ _SIG = {
     "vs_dense_points_dev": (_P, [_P]),
     "vs_dense_write_ply": (_I, [_P, ctypes.c_char_p]),
     "vs_slam_attach_dense": (_I, [_P, _P]),
+    "vs_slam_loops": (_I, [_P, _I, _P, _P, _P, _P]),
     "vs_profile_enable": (_I, [_P, _I]),
     "vs_profile_reset": (_I, [_P]),
     "vs_profile_read": (_I, [_P, _I, _P, _P, _P, _P]),
@@ -444,7 +445,7 @@ class Context:
 SLAM_STATS = ["processed", "rejected", "via_3d3d", "via_emat", "emat_failed", "bridges", "recoveries",
               "recovery_failed", "stationary", "keyframes", "pnp_refined", "periodic_pnp", "tracked_total",
               "triangulated", "depth_points", "culled", "chains_recomputed", "map_points", "map_valid",
-              "frame_count", "keyframe_count", "last_match_count", "f_ransac_iters"]
+              "frame_count", "keyframe_count", "last_match_count", "f_ransac_iters", "loop_count"]
 
 
 class Slam:
@@ -525,6 +526,17 @@ class Slam:
     def stats_dict(self):
         s = self.stats()
         return {k: int(s[i]) for i, k in enumerate(SLAM_STATS)}
+
+    def loops(self):
+        """(edges [E, 2] (matched keyframe id, frame id), constraints [C, 16] = from, to, R_rel[9],
+        t_rel[3], trans_sigma, rot_sigma): Slam::handle_loop_closure's loop edges and PGO constraints."""
+        ne, nc = ctypes.c_int(0), ctypes.c_int(0)
+        _check(self.lib.vs_slam_loops(self.h, 0, None, None, ctypes.byref(ne), ctypes.byref(nc)))
+        cap = max(ne.value, nc.value, 1)
+        e = np.zeros((cap, 2), np.int32)
+        c = np.zeros((cap, 16))
+        _check(self.lib.vs_slam_loops(self.h, cap, _ptr(e), _ptr(c), ctypes.byref(ne), ctypes.byref(nc)))
+        return e[:ne.value], c[:nc.value]
 
     def attach_dense(self, dense):
         """Fuse every processed frame with depth into `dense` (a Dense, or None to detach)."""
