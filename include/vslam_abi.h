@@ -447,6 +447,26 @@ int vs_dense_write_ply(vs_dense* d, const char* path);
  * reference's main loop does (NULL detaches). */
 int vs_slam_attach_dense(vs_slam* slam, vs_dense* d);
 
+/* ---- F4: Optimizer::pose_graph_optimize (Optimizer.cpp:654-863), g2o LM restated -------------
+ * N keyframe poses (camera -> world, R [N][9] row-major, t [N][3], keyframe order; the first is
+ * fixed), odometry edges between consecutive keyframes from these poses, L loop constraints
+ * (vertex indices lc_from / lc_to, measurement R_rel [L][9] / t_rel [L][3], sigmas [L][2] =
+ * {trans, rot}), and, when gravity is non-NULL, a height prior g . t = height on every vertex.
+ * Nothing happens for N < 3, or with no loops and no prior (as the reference returns 0).
+ * R / t are overwritten with the optimised poses.  stats (nullable) = {iterations, accepted steps,
+ * trials, loop edges}; chi2 (nullable) = {before, after, final lambda}.  Synchronous. */
+int vs_pose_graph_optimize(vs_ctx* ctx, int N, double* R, double* t, int L, const int* lc_from, const int* lc_to,
+                           const double* lc_R, const double* lc_t, const double* lc_sigma, const double* gravity,
+                           double height, int iterations, int stats[4], double chi2[3]);
+/* Optimizer.cpp:829-859: map point i moves with keyframe kf[i] (-1: unchanged) by
+ * new_k * old_k^-1; pos [M][3] in place.  Synchronous. */
+int vs_pgo_transform_points(vs_ctx* ctx, int N, const double* R_old, const double* t_old, const double* R_new,
+                            const double* t_new, int M, const int* kf, double* pos);
+/* Slam::run_posthoc_pgo (Slam.cpp:1748-1755): the pose graph over the tracker's keyframes with its
+ * loop constraints and height prior, then the non-keyframe translations and map points corrected
+ * as Optimizer.cpp:780-859 does.  *loop_edges = pose_graph_optimize's return value. */
+int vs_slam_run_posthoc_pgo(vs_slam* slam, int* loop_edges);
+
 /* ---- profiling ----------------------------------------------------------------------- */
 /* When enabled, every stage of the _dev pipelines brackets its launches with hipEvents on the
  * stream it runs on; vs_profile_read returns per-stage accumulated milliseconds and launch

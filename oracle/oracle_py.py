@@ -62,6 +62,9 @@ _SIG = {
     "orc_slam_stage_seconds": (ctypes.c_int, [_P, _P, ctypes.c_int]),
     "orc_slam_map": (_I, [_P, _I, _P, _P]),
     "orc_slam_loops": (_I, [_P, _I, _P, _P, _P]),
+    "orc_slam_run_posthoc_pgo": (_I, [_P]),
+    "orc_pose_graph": (_I, [_I, _P, _P, _I, _P, _P, _P, _P, _P, _P, ctypes.c_double, _I, _P, _P]),
+    "orc_pgo_transform_points": (None, [_I, _P, _P, _P, _P, _I, _P, _P]),
     "orc_mt19937": (None, [ctypes.c_uint32, _I, _P]),
     "orc_expf_array": (None, [_P, _I, _P]),
     "orc_expf_exhaustive_check": (ctypes.c_long, [ctypes.c_float, ctypes.c_float]),
@@ -433,6 +436,25 @@ def expf_restated_check(lo, hi, use_fma=1):
     return lib().orc_expf_restated_check(lo, hi, use_fma)
 
 
+def pose_graph(R, t, loops=(), gravity=None, height=0.0, iters=20):
+    """Optimizer::pose_graph_optimize restated (dense): R [N, 3, 3], t [N, 3] keyframe poses; loops =
+    [(from, to, R_rel, t_rel, trans_sigma, rot_sigma)].  -> (R, t, stats [4], chi2 [3])."""
+    R = np.ascontiguousarray(R, np.float64).copy()
+    t = np.ascontiguousarray(t, np.float64).copy()
+    L = len(loops)
+    lf = np.array([l[0] for l in loops] + [0], np.int32)
+    lt_ = np.array([l[1] for l in loops] + [0], np.int32)
+    lR = np.ascontiguousarray(np.array([np.asarray(l[2], np.float64).reshape(9) for l in loops] + [np.zeros(9)]))
+    ltv = np.ascontiguousarray(np.array([np.asarray(l[3], np.float64).reshape(3) for l in loops] + [np.zeros(3)]))
+    ls = np.ascontiguousarray(np.array([[l[4], l[5]] for l in loops] + [[1.0, 1.0]], np.float64))
+    g = None if gravity is None else np.ascontiguousarray(gravity, np.float64)
+    st = np.zeros(4, np.int32)
+    ch = np.zeros(3)
+    lib().orc_pose_graph(R.shape[0], _p(R), _p(t), L, _p(lf), _p(lt_), _p(lR), _p(ltv), _p(ls), _p(g), float(height),
+                         iters, _p(st), _p(ch))
+    return R, t, st, ch
+
+
 class Dense:
     """Dense voxel fusion (main.cpp:1081-1139), sequential: the checker for vslam_abi.Dense."""
 
@@ -527,6 +549,9 @@ class Slam:
         valid = np.zeros(max(n, 1), np.uint8)
         lib().orc_slam_map(self.h, n, _p(pos), _p(valid))
         return pos[:n], valid[:n]
+
+    def run_posthoc_pgo(self):
+        return lib().orc_slam_run_posthoc_pgo(self.h)
 
     def loops(self):
         """(edges [E, 2] (matched frame id, frame id), constraints [C, 16] = from, to, R_rel[9],

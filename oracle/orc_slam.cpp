@@ -172,6 +172,43 @@ struct OracleOps {
         return out;
     }
 
+    void pose_graph(std::vector<vs_trk::M3>& R, std::vector<vs_trk::V3>& t, const std::vector<vs_trk::PgoLoop>& loops,
+                    const vs_trk::V3* gravity, double height, int iters) {
+        const int N = (int)R.size(), L = (int)loops.size();
+        std::vector<double> Rf((size_t)N * 9), tf((size_t)N * 3), lR(9 * L + 1), lt(3 * L + 1), ls(2 * L + 1);
+        std::vector<int> lf(L + 1), lto(L + 1);
+        for (int i = 0; i < N; i++) {
+            std::memcpy(&Rf[9 * i], R[i].data(), 72);
+            std::memcpy(&tf[3 * i], t[i].data(), 24);
+        }
+        for (int l = 0; l < L; l++) {
+            lf[l] = loops[l].from;
+            lto[l] = loops[l].to;
+            std::memcpy(&lR[9 * l], loops[l].R.data(), 72);
+            std::memcpy(&lt[3 * l], loops[l].t.data(), 24);
+            ls[2 * l] = loops[l].trans_sigma;
+            ls[2 * l + 1] = loops[l].rot_sigma;
+        }
+        orc_pose_graph(N, Rf.data(), tf.data(), L, lf.data(), lto.data(), lR.data(), lt.data(), ls.data(),
+                       gravity ? gravity->data() : nullptr, height, iters, nullptr, nullptr);
+        for (int i = 0; i < N; i++) {
+            std::memcpy(R[i].data(), &Rf[9 * i], 72);
+            std::memcpy(t[i].data(), &tf[3 * i], 24);
+        }
+    }
+    void pgo_points(const std::vector<vs_trk::M3>& Ro, const std::vector<vs_trk::V3>& to, const std::vector<vs_trk::M3>& Rn,
+                    const std::vector<vs_trk::V3>& tn, const std::vector<int>& kf, Map& m) {
+        const int N = (int)Ro.size();
+        std::vector<double> a((size_t)N * 9), b((size_t)N * 3), c((size_t)N * 9), d((size_t)N * 3);
+        for (int i = 0; i < N; i++) {
+            std::memcpy(&a[9 * i], Ro[i].data(), 72);
+            std::memcpy(&b[3 * i], to[i].data(), 24);
+            std::memcpy(&c[9 * i], Rn[i].data(), 72);
+            std::memcpy(&d[3 * i], tn[i].data(), 24);
+        }
+        orc_pgo_transform_points(N, a.data(), b.data(), c.data(), d.data(), m.size(), kf.data(), m.pos.data());
+    }
+
     std::vector<std::pair<int, int>> match_map(const Map&, const Frame& f, const std::vector<int>& ids, float ratio) {
         StageTimer st(&sec[kMatchMap]);
         std::vector<std::pair<int, int>> out;
@@ -290,6 +327,8 @@ int orc_slam_process(void* h, int n_kp, const orc_keypoint* kps, const float* de
 }
 
 void orc_slam_finish(void* h) { static_cast<OrcSlam*>(h)->trk.run_rts_smoother(); }
+
+int orc_slam_run_posthoc_pgo(void* h) { return static_cast<OrcSlam*>(h)->trk.run_posthoc_pgo(); }
 
 int orc_slam_trajectory(void* h, int cap, int* ids, double* ts, double* R, double* t) {
     const auto& fr = static_cast<OrcSlam*>(h)->trk.map().frames;

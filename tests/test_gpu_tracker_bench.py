@@ -63,7 +63,9 @@ def gpu_run(vsctx, loop):
                                         [3 * (g0 + j) for j in range(B)]).tolist()
         traj_raw = S.trajectory()
         S.finish()
-        return done, S.stats(), traj_raw, S.trajectory(), S.map_points(), S.loops()
+        out = done, S.stats(), traj_raw, S.trajectory(), S.map_points(), S.loops()
+        n_pgo = S.run_posthoc_pgo()  # Slam::run_posthoc_pgo over the found loop(s)
+        return out + ((n_pgo, S.trajectory(), S.map_points()),)
 
 
 @pytest.fixture(scope="module")
@@ -76,6 +78,8 @@ def oracle_run(oracle, loop, loop_feats):
     traj_raw = S.trajectory()
     S.finish()
     out = done, S.stats(), traj_raw, S.trajectory(), S.map_points(), S.loops()
+    n_pgo = S.run_posthoc_pgo()
+    out = out + ((n_pgo, S.trajectory(), S.map_points()),)
     S.close()
     return out
 
@@ -108,6 +112,20 @@ def test_bench_scale_loop_closure_matches_oracle(gpu_run, oracle_run):
     assert np.array_equal(gc.view(np.uint64), oc.view(np.uint64))
     for e in ge:
         assert e[1] - e[0] >= 200  # LC_MIN_FRAME_GAP in frame ids
+
+
+def test_bench_scale_posthoc_pgo_matches_oracle(gpu_run, oracle_run):
+    """Slam::run_posthoc_pgo (Slam.cpp:1748-1755 -> Optimizer.cpp:654-863) over the bench run's
+    keyframes and verified loop constraint(s): the GPU pose graph (block-skyline LM) and the
+    oracle's dense one give the same keyframe / frame poses and map points to 1e-7 (numeric-Jacobian
+noise, tests/test_gpu_pgo.py)."""
+    (gn, (gi, _, gR, gt), (gp, gv)), (on, (oi, _, oR, ot), (op, ov)) = gpu_run[6], oracle_run[6]
+    assert gn == on
+    assert np.array_equal(gi, oi) and np.array_equal(gv, ov)
+    assert np.abs(gR - oR).max() < 1e-7 and np.abs(gt - ot).max() < 1e-7
+    assert np.abs(gp - op).max() < 1e-6  # map points up to ~10 m from their keyframe
+    if gn:  # a loop constraint moved the trajectory
+        assert np.abs(gt - gpu_run[3][3]).max() > 1e-6
 
 
 def test_bench_scale_ate_is_the_algorithms(gpu_run, oracle_run, loop):

@@ -324,6 +324,7 @@ int vs_dense_integrate_dev(vs_dense* d, int nf, const float* const* d_depth, int
     a.slot = d->scratch.as<int>();
     a.bcnt = reinterpret_cast<int*>(d->scratch.as<char>() + slot_b);
     a.boff = reinterpret_cast<long long*>(d->scratch.as<char>() + slot_b + cnt_b);
+    ProfScope ps(d->ctx, "dense_fusion", s);
     for (int f0 = 0; f0 < nf; f0 += kDF) {
         DenseFrames F{};
         a.nf = std::min(kDF, nf - f0);

@@ -980,6 +980,52 @@ struct GpuOps {
         return out;
     }
 
+    // Optimizer::pose_graph_optimize's solve (Optimizer.cpp:677-778) on the GPU (csrc/pgo.hip)
+    void pose_graph(std::vector<vs_trk::M3>& R, std::vector<vs_trk::V3>& t, const std::vector<vs_trk::PgoLoop>& loops,
+                    const vs_trk::V3* gravity, double height, int iters) {
+        const int N = (int)R.size(), L = (int)loops.size();
+        std::vector<double> Rf((size_t)N * 9), tf((size_t)N * 3), lR((size_t)L * 9 + 1), lt((size_t)L * 3 + 1),
+            ls((size_t)L * 2 + 1);
+        std::vector<int> lf(L + 1), lto(L + 1);
+        for (int i = 0; i < N; i++) {
+            std::memcpy(&Rf[9 * i], R[i].data(), 72);
+            std::memcpy(&tf[3 * i], t[i].data(), 24);
+        }
+        for (int l = 0; l < L; l++) {
+            lf[l] = loops[l].from;
+            lto[l] = loops[l].to;
+            std::memcpy(&lR[9 * l], loops[l].R.data(), 72);
+            std::memcpy(&lt[3 * l], loops[l].t.data(), 24);
+            ls[2 * l] = loops[l].trans_sigma;
+            ls[2 * l + 1] = loops[l].rot_sigma;
+        }
+        if (failed(vs_pose_graph_optimize(ctx, N, Rf.data(), tf.data(), L, lf.data(), lto.data(), lR.data(), lt.data(),
+                                          ls.data(), gravity ? gravity->data() : nullptr, height, iters, nullptr,
+                                          nullptr)))
+            return;
+        for (int i = 0; i < N; i++) {
+            std::memcpy(R[i].data(), &Rf[9 * i], 72);
+            std::memcpy(t[i].data(), &tf[3 * i], 24);
+        }
+    }
+    void pgo_points(const std::vector<vs_trk::M3>& Ro, const std::vector<vs_trk::V3>& to, const std::vector<vs_trk::M3>& Rn,
+                    const std::vector<vs_trk::V3>& tn, const std::vector<int>& kf, vs_trk::Map& m) {
+        const int N = (int)Ro.size(), M = m.size();
+        if (M == 0) return;
+        std::vector<double> a((size_t)N * 9), b((size_t)N * 3), c((size_t)N * 9), d((size_t)N * 3);
+        for (int i = 0; i < N; i++) {
+            std::memcpy(&a[9 * i], Ro[i].data(), 72);
+            std::memcpy(&b[3 * i], to[i].data(), 24);
+            std::memcpy(&c[9 * i], Rn[i].data(), 72);
+            std::memcpy(&d[3 * i], tn[i].data(), 24);
+        }
+        if (failed(vs_pgo_transform_points(ctx, N, a.data(), b.data(), c.data(), d.data(), M, kf.data(), m.pos.data())))
+            return;
+        // the device copy of the map follows (tracking after a PGO sees the corrected points)
+        if (failed(upload(map_pos.as<double>(), m.pos.data(), (size_t)M * 3 * sizeof(double)))) return;
+        failed(sync());
+    }
+
     std::vector<std::pair<int, int>> match_map(const vs_trk::Map& m, const vs_trk::Frame& f, const std::vector<int>& ids,
                                                float ratio) {
         HostTimer ht(hprof, kHMatchMap);
@@ -1298,6 +1344,21 @@ int vs_slam_attach_dense(vs_slam* sl, vs_dense* d) {
     sl->dense_depth.clear();
     sl->dense_R.clear();
     sl->dense_t.clear();
+    return VS_OK;
+}
+
+int vs_slam_run_posthoc_pgo(vs_slam* sl, int* loop_edges) {
+    VS_ARG(sl, "vs_slam_run_posthoc_pgo: null argument");
+    GpuOps& o = sl->ops;
+    VS_HIP(hipSetDevice(o.ctx->device));
+    CtxStream use(o.ctx, o.s);
+    const int n = sl->trk->run_posthoc_pgo();
+    if (loop_edges) *loop_edges = n;
+    if (o.err != VS_OK) {
+        const int rc = o.err;
+        o.err = VS_OK;
+        return rc;
+    }
     return VS_OK;
 }
 

@@ -177,6 +177,14 @@ struct LoopConstraint {
     double trans_sigma = 0, rot_sigma = 0;
 };
 
+// A loop constraint as the pose graph takes it: keyframe indices instead of frame ids
+struct PgoLoop {
+    int from = -1, to = -1;
+    M3 R{};
+    V3 t{};
+    double trans_sigma = 0, rot_sigma = 0;
+};
+
 // One loop-closure candidate as LoopCloser::detect sees it (LoopCloser.cpp:50-76): ratio-test
 // matches of the current frame against the keyframe, and the inliers of findEssentialMat on them
 // (0 when E is empty).
@@ -453,6 +461,76 @@ class Tracker {
         frame_count_++;
         stats_.processed++;
         return true;
+    }
+
+    // Slam::run_posthoc_pgo (Slam.cpp:1748-1755) -> Optimizer::pose_graph_optimize (Optimizer.cpp:654-863):
+    // the back end optimises the keyframe graph (g2o LM, 20 iterations) and moves the map points;
+    // the keyframe / non-keyframe pose bookkeeping (:789-827) is restated here.  Returns the number
+    // of loop edges added.
+    int run_posthoc_pgo() {
+        if (!has_initial_height_ && loop_constraints_.empty()) return 0;  // :1749-1751
+        const bool prior = has_initial_height_ && has_gravity_;          // has_height_prior && !gravity.empty()
+        std::vector<Frame*> kfs;
+        for (const FramePtr& f : map_.frames)
+            if (f->keyframe) kfs.push_back(f.get());
+        const int N = (int)kfs.size();
+        if (N < 3) return 0;  // :670
+        auto kf_index = [&](int id) {
+            for (int i = 0; i < N; i++)
+                if (kfs[i]->id == id) return i;
+            return -1;
+        };
+        std::vector<PgoLoop> loops;
+        for (const LoopConstraint& c : loop_constraints_) {  // :723-755
+            const int a = kf_index(c.from_id), b = kf_index(c.to_id);
+            if (a < 0 || b < 0) continue;
+            loops.push_back({a, b, c.R_rel, c.t_rel, c.trans_sigma, c.rot_sigma});
+        }
+        if (loops.empty() && !prior) return 0;  // :775
+        std::vector<M3> R_old(N), R_new(N);
+        std::vector<V3> t_old(N), t_new(N);
+        for (int i = 0; i < N; i++) {
+            R_old[i] = R_new[i] = kfs[i]->R;
+            t_old[i] = t_new[i] = kfs[i]->t;
+        }
+        ops_.pose_graph(R_new, t_new, loops, prior ? &gravity_ : nullptr, initial_height_, 20);  // :777-778
+        for (int i = 0; i < N; i++) {  // :789-793
+            kfs[i]->R = R_new[i];
+            kfs[i]->t = t_new[i];
+        }
+        for (const FramePtr& f : map_.frames) {  // :795-827 non-keyframes: interpolated translation shift
+            if (f->keyframe) continue;
+            const int fid = f->id;
+            int prev = -1, next = -1;
+            for (int i = 0; i < N; i++) {
+                if (kfs[i]->id <= fid) prev = i;
+                if (kfs[i]->id > fid && next < 0) next = i;
+            }
+            if (prev < 0) continue;
+            if (next < 0) next = prev;
+            double alpha = 0.0;
+            if (prev != next) alpha = (double)(fid - kfs[prev]->id) / (double)(kfs[next]->id - kfs[prev]->id);
+            for (int k = 0; k < 3; k++) {
+                const double dp = t_new[prev][k] - t_old[prev][k], dn = t_new[next][k] - t_old[next][k];
+                f->t[k] += (1.0 - alpha) * dp + alpha * dn;
+            }
+        }
+        std::vector<int> pkf(map_.size(), -1);  // :829-851 each valid point's keyframe
+        for (int i = 0; i < map_.size(); i++) {
+            if (!map_.valid[i] || map_.obs[i].empty()) continue;
+            const int ofid = map_.obs[i][0].first;
+            int k = kf_index(ofid);
+            if (k < 0) {
+                int best = 1 << 30;
+                for (int q = 0; q < N; q++) {
+                    const int d = std::abs(kfs[q]->id - ofid);
+                    if (d < best) best = d, k = q;
+                }
+            }
+            pkf[i] = k;
+        }
+        ops_.pgo_points(R_old, t_old, R_new, t_new, pkf, map_);  // :852-858
+        return (int)loops.size();
     }
 
     // Slam::run_rts_smoother (Slam.cpp:1761-1810)

@@ -104,6 +104,9 @@ _SIG = {
     "vs_dense_write_ply": (_I, [_P, ctypes.c_char_p]),
     "vs_slam_attach_dense": (_I, [_P, _P]),
     "vs_slam_loops": (_I, [_P, _I, _P, _P, _P, _P]),
+    "vs_pose_graph_optimize": (_I, [_P, _I, _P, _P, _I, _P, _P, _P, _P, _P, _P, ctypes.c_double, _I, _P, _P]),
+    "vs_pgo_transform_points": (_I, [_P, _I, _P, _P, _P, _P, _I, _P, _P]),
+    "vs_slam_run_posthoc_pgo": (_I, [_P, _P]),
     "vs_profile_enable": (_I, [_P, _I]),
     "vs_profile_reset": (_I, [_P]),
     "vs_profile_read": (_I, [_P, _I, _P, _P, _P, _P]),
@@ -538,6 +541,12 @@ class Slam:
         _check(self.lib.vs_slam_loops(self.h, cap, _ptr(e), _ptr(c), ctypes.byref(ne), ctypes.byref(nc)))
         return e[:ne.value], c[:nc.value]
 
+    def run_posthoc_pgo(self):
+        """Slam::run_posthoc_pgo (Slam.cpp:1748-1755) on the GPU: returns the loop edges added."""
+        n = ctypes.c_int(0)
+        _check(self.lib.vs_slam_run_posthoc_pgo(self.h, ctypes.byref(n)))
+        return n.value
+
     def attach_dense(self, dense):
         """Fuse every processed frame with depth into `dense` (a Dense, or None to detach)."""
         _check(self.lib.vs_slam_attach_dense(self.h, None if dense is None else dense.h))
@@ -588,6 +597,27 @@ def spcf_read(path, cap=SP_MAX_KEYPOINTS):
         _check(_lib.vs_spcf_read(os.fsencode(path), E, cap, _ptr(idx), _ptr(kps), _ptr(desc), _ptr(n),
                                  ctypes.byref(cnt)))
     return idx[:E], kps[:E], desc[:E], n[:E]
+
+
+# ---- F4: Optimizer::pose_graph_optimize (Optimizer.cpp:654-863) ---------------------------------
+def pose_graph_optimize(ctx, R, t, loops=(), gravity=None, height=0.0, iters=20):
+    """GPU g2o-LM pose graph: R [N, 3, 3], t [N, 3] keyframe poses (camera -> world); loops =
+    [(from, to, R_rel, t_rel, trans_sigma, rot_sigma)].  -> (R, t, stats [4], chi2 [3])."""
+    R = np.ascontiguousarray(R, np.float64).copy()
+    t = np.ascontiguousarray(t, np.float64).copy()
+    L = len(loops)
+    lf = np.array([l[0] for l in loops] + [0], np.int32)
+    lt_ = np.array([l[1] for l in loops] + [0], np.int32)
+    lR = np.ascontiguousarray(np.array([np.asarray(l[2], np.float64).reshape(9) for l in loops] + [np.zeros(9)]))
+    ltv = np.ascontiguousarray(np.array([np.asarray(l[3], np.float64).reshape(3) for l in loops] + [np.zeros(3)]))
+    ls = np.ascontiguousarray(np.array([[l[4], l[5]] for l in loops] + [[1.0, 1.0]], np.float64))
+    g = None if gravity is None else np.ascontiguousarray(gravity, np.float64)
+    st = np.zeros(4, np.int32)
+    ch = np.zeros(3)
+    _check(ctx.lib.vs_pose_graph_optimize(ctx.h, R.shape[0], _ptr(R), _ptr(t), L, _ptr(lf), _ptr(lt_), _ptr(lR),
+                                          _ptr(ltv), _ptr(ls), None if g is None else _ptr(g), float(height), iters,
+                                          _ptr(st), _ptr(ch)))
+    return R, t, st, ch
 
 
 # ---- F4: dense voxel fusion (main.cpp:1081-1146) ----------------------------------------------
