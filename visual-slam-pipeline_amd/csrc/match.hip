@@ -461,6 +461,12 @@ static int match_state(vs_ctx* ctx, int P, int kcap, unsigned long long** keys, 
     return VS_OK;
 }
 
+int match_reserve(vs_ctx* ctx, int P, int cap, hipStream_t s) {
+    unsigned long long* keys;
+    unsigned* cnt;
+    return match_state(ctx, P, cap, &keys, &cnt, s);
+}
+
 template <int NWQ, int NWT, int WQ, int WT, int KC, int NBUF, int PD = 1>
 static void launch_tile(MatchArgs& a, int P, int cap_q, int cap_t, bool norms, hipStream_t s) {
     constexpr int TQ = NWQ * WQ, TT = NWT * WT, NTH = 64 * NWQ * NWT;

@@ -217,7 +217,7 @@ __global__ __launch_bounds__(64) void k_pnp_hyp(const float* __restrict__ obj_al
     __shared__ double sA[144], sV[144];
     __shared__ double sX[15], sUV[10], sAl[5][4], sCw[4][3];
     __shared__ double sTot, sOff, sErr[3], sRt[3][12];
-    __shared__ int sOk;
+    __shared__ int sOk, sPerm[12];
     const int pb = blockIdx.x, h = blockIdx.y, lane = threadIdx.x;
     const int o0 = off[pb], n = off[pb + 1] - o0;
     const int model_points = n == 4 ? 4 : 5;
@@ -346,23 +346,56 @@ __global__ __launch_bounds__(64) void k_pnp_hyp(const float* __restrict__ obj_al
             }
         }
         PNP_T(2);
-        if (lane == 0) {  // eigenvalues in descending order, columns of V swapped along (selection sort)
+        // eigenvalues in descending order, columns of V swapped along (sym_eig_rr's selection
+        // sort): lane 0 runs the sort on the eigenvalues and a column index, the wave moves the
+        // columns once (the same moves as swapping them step by step)
+        if (lane == 0) {
             double w[12];
-            for (int i = 0; i < 12; i++) w[i] = sA[i * 12 + i];
+            int pm[12];
+#pragma unroll
+            for (int i = 0; i < 12; i++) {
+                w[i] = sA[i * 12 + i];
+                pm[i] = i;
+            }
+#pragma unroll
             for (int i = 0; i < 11; i++) {
                 int mx = i;
+                double wm = w[i];
+#pragma unroll
                 for (int j = i + 1; j < 12; j++)
-                    if (w[j] > w[mx]) mx = j;
-                if (mx != i) {
-                    const double tw = w[i];
-                    w[i] = w[mx];
-                    w[mx] = tw;
-                    for (int k = 0; k < 12; k++) {
-                        const double tv = sV[k * 12 + i];
-                        sV[k * 12 + i] = sV[k * 12 + mx];
-                        sV[k * 12 + mx] = tv;
+                    if (w[j] > wm) {
+                        mx = j;
+                        wm = w[j];
                     }
-                }
+                // swap entries i and mx with compile-time indices only (the arrays stay in registers)
+                int pmx = pm[i];
+#pragma unroll
+                for (int j = i + 1; j < 12; j++) pmx = j == mx ? pm[j] : pmx;
+#pragma unroll
+                for (int j = i + 1; j < 12; j++)
+                    if (j == mx) {
+                        w[j] = w[i];
+                        pm[j] = pm[i];
+                    }
+                w[i] = wm;
+                pm[i] = pmx;
+            }
+#pragma unroll
+            for (int i = 0; i < 12; i++) sPerm[i] = pm[i];
+        }
+        __syncthreads();
+        {
+            double tv[3];
+#pragma unroll
+            for (int u = 0; u < 3; u++) {
+                const int e = lane + 64 * u;
+                if (e < 144) tv[u] = sV[(e / 12) * 12 + sPerm[e % 12]];
+            }
+            __syncthreads();
+#pragma unroll
+            for (int u = 0; u < 3; u++) {
+                const int e = lane + 64 * u;
+                if (e < 144) sV[e] = tv[u];
             }
         }
         __syncthreads();
@@ -430,6 +463,7 @@ __global__ __launch_bounds__(256) void k_pnp_ransac(const float* __restrict__ ob
                                                     double* __restrict__ tw, int* __restrict__ stat,
                                                     uint8_t* __restrict__ mask_all) {
     __shared__ PnpShared S;
+    __shared__ double s_lden[kPnpMaxIters];
     const int pb = blockIdx.x, tid = threadIdx.x;
     const int o0 = off[pb], n = off[pb + 1] - o0;
     const float* obj = obj_all + 3 * (size_t)o0;
@@ -466,6 +500,13 @@ __global__ __launch_bounds__(256) void k_pnp_ransac(const float* __restrict__ ob
     } else {
         const int* count = H.count + (size_t)pb * H.stride;
         PNP_T0();
+        // every hypothesis' outlier-ratio term at once (it depends on its count only), then the
+        // sequential accept / budget replay reads them
+        for (int it = tid; it < niters0; it += blockDim.x) {
+            const int c = count[it];
+            s_lden[it] = c >= 0 ? ransac_log_denom((double)(n - c) / n, model_points) : 0.0;
+        }
+        __syncthreads();
         if (tid == 0) {
             int niters = niters0, best = 0, best_iter = -1, it = 0;
             const double log_num = ransac_log_num(conf);
@@ -475,7 +516,7 @@ __global__ __launch_bounds__(256) void k_pnp_ransac(const float* __restrict__ ob
                 if (c > (best > model_points - 1 ? best : model_points - 1)) {
                     best = c;
                     best_iter = it;
-                    niters = ransac_update_num_iters_ln(log_num, (double)(n - c) / n, model_points, niters);
+                    niters = ransac_update_from_denom(log_num, s_lden[it], niters);
                 }
             }
             S.best = best;

@@ -96,15 +96,24 @@ VS_HD inline double ransac_log_num(double p) {
     p = p < 1. ? p : 1.;
     return vs_cr::log((1. - p) > DBL_MIN ? (1. - p) : DBL_MIN);
 }
-VS_HD inline int ransac_update_num_iters_ln(double log_num, double ep, int model_points, int max_iters) {
+// RANSACUpdateNumIters in two parts: the outlier-ratio term log(1 - (1 - ep)^m), which does not
+// depend on the running budget (a device evaluates it for every hypothesis at once; +inf marks
+// OpenCV's denom < DBL_MIN exit), and the budget update from it.
+VS_HD inline double ransac_log_denom(double ep, int model_points) {
     ep = ep > 0. ? ep : 0.;
     ep = ep < 1. ? ep : 1.;
-    double denom = 1. - vs_cr::pow(1. - ep, model_points);
-    if (denom < DBL_MIN) return 0;
+    const double denom = 1. - vs_cr::pow(1. - ep, model_points);
+    if (denom < DBL_MIN) return HUGE_VAL;
+    return vs_cr::log(denom);
+}
+VS_HD inline int ransac_update_from_denom(double log_num, double denom, int max_iters) {
+    if (denom == HUGE_VAL) return 0;
     const double num = log_num;
-    denom = vs_cr::log(denom);
     if (denom >= 0 || -num >= max_iters * (-denom)) return max_iters;
     return (int)lrint(num / denom);  // cvRound
+}
+VS_HD inline int ransac_update_num_iters_ln(double log_num, double ep, int model_points, int max_iters) {
+    return ransac_update_from_denom(log_num, ransac_log_denom(ep, model_points), max_iters);
 }
 VS_HD inline int ransac_update_num_iters(double p, double ep, int model_points, int max_iters) {
     return ransac_update_num_iters_ln(ransac_log_num(p), ep, model_points, max_iters);

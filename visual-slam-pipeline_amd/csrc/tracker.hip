@@ -38,6 +38,31 @@ static_assert(sizeof(vs_trk::Match) == sizeof(vs_match), "match layouts differ")
 
 constexpr int kCap = VS_SP_MAX_KEYPOINTS;
 constexpr int kPersist = 8;
+constexpr int kArchInit = 512;   // keyframes the feature archive holds before it first grows
+constexpr int kLoopPairs = 128;  // loop candidates reserved up front (kArchInit / 5 + slack)
+
+// Loop-closure candidate pool: frame f of the pool = the keypoints / descriptors / count at src[f]
+// (archive rows or pool slots); grid (F, slices), float4 copies.
+struct FrameSrc {
+    const vs_keypoint* k;
+    const float* d;
+    const int* n;
+};
+__global__ __launch_bounds__(256) void k_gather_frames(const FrameSrc* __restrict__ src, vs_keypoint* __restrict__ kps,
+                                                       float* __restrict__ desc, int* __restrict__ n) {
+    const int f = blockIdx.x;
+    const FrameSrc S = src[f];
+    const float4* sd = reinterpret_cast<const float4*>(S.d);
+    float4* dd = reinterpret_cast<float4*>(desc + (size_t)f * kCap * 256);
+    for (int i = blockIdx.y * 256 + threadIdx.x; i < kCap * 64; i += gridDim.y * 256) dd[i] = sd[i];
+    if (blockIdx.y == 0) {
+        constexpr int kw = kCap * (int)sizeof(vs_keypoint) / 4;
+        const int* sk = reinterpret_cast<const int*>(S.k);
+        int* dk = reinterpret_cast<int*>(kps + (size_t)f * kCap);
+        for (int i = threadIdx.x; i < kw; i += 256) dk[i] = sk[i];
+        if (threadIdx.x == 0) n[f] = *S.n;
+    }
+}
 
 // dst[i] = src row rows[i] (256 floats), one 64-lane wave per row, float4 per lane
 __global__ __launch_bounds__(256) void k_gather_rows(const float* __restrict__ src, const int* __restrict__ rows,
@@ -231,6 +256,13 @@ struct GpuOps {
     const vs_trk::Frame* next_frame = nullptr;  // the batch's next frame (process_batch_dev)
     hipEvent_t next_ready = nullptr;            // its extraction chunk's event
     long cspec_hits = 0, cspec_launched = 0;
+    struct SpecReq {  // the speculation chain() decided on, launched by flush_spec()
+        bool pending = false;
+        int ref_slot = -1, nxt_slot = -1;
+        const vs_trk::Frame* nxt = nullptr;
+        uint32_t seed = 0;
+        hipEvent_t ready = nullptr;
+    } spec_req;
     bool own_streams = false;
     // One extraction in flight or in use: chunk boundaries (frame index of each chunk's first frame,
     // then nb), one event per chunk, the pinned keypoints / counts, the batch region it writes and
@@ -359,9 +391,25 @@ struct GpuOps {
         VS_CHECK(pin.reserve((size_t)4 << 20));
         owner.assign(kPersist, nullptr);
         VS_CHECK(grow_map(1 << 16));
-        // map-sized scratch up front (a later growth would wait for the extraction stream too)
-        VS_CHECK(map_tmp.ensure((size_t)1 << 20));
+        // map-sized scratch up front (a later growth would wait for the extraction stream too):
+        // map_tmp holds the gathered descriptors of PnP-recovery / loop-closure map matching (1 KB per
+        // candidate map point; 64 MB = 65k points, the size grow_map starts with)
+        VS_CHECK(map_tmp.ensure((size_t)64 << 20));
         VS_CHECK(work.ensure((size_t)1 << 20));
+        VS_CHECK(pnp_io.ensure((size_t)1 << 20));
+        VS_CHECK(rows_buf.ensure((size_t)64 << 10));
+        // the context's per-stage scratch at its largest in-loop size: local-map tracking for 200k
+        // map points, PnP hypothesis tables for the largest RANSAC budget (loop closure: 300)
+        VS_CHECK(ctx->tlm.ensure((size_t)64 << 20));
+        VS_CHECK(ctx->pnp.ensure((size_t)4 * VS_PNP_MAX_ITERS * (6 * sizeof(int) + 6 * sizeof(double))));
+        // Loop closure (every 200 keyframes, candidates every 5th keyframe >= 200 ids back,
+        // LoopCloser.cpp:44-49): the keyframe archive for kArchInit keyframes (215 MB of HBM), the
+        // candidate pool and the matcher key state for kLoopPairs candidates, reserved here because
+        // every hipFree inside the loop waits for the extraction stream as well.
+        VS_CHECK(grow_archive(kArchInit));
+        VS_CHECK(lc_buf.ensure(LcLayout(kLoopPairs).total));
+        VS_CHECK(match_reserve(ctx, kLoopPairs, kCap, s));
+        VS_HIP(hipStreamSynchronize(s));
         return VS_OK;
     }
 
@@ -649,11 +697,11 @@ struct GpuOps {
     // on s2 beside this frame's local-map tracking and PnP: it is the next frame's chain whenever
     // this frame neither becomes a keyframe nor is rejected (the reference frame and the processed
     // count then carry over, Slam.cpp:838, 276).  chain() uses it only when slots and seed match.
-    int launch_spec_chain(int ref_slot, const vs_trk::Frame& nxt, uint32_t seed) {
+    int launch_spec_chain(int ref_slot, const vs_trk::Frame& nxt, uint32_t seed, hipEvent_t ready) {
         VS_HIP(hipEventSynchronize(cspec_ev));  // the previous speculation released cpin / chain_buf2
         uint32_t* hh = reinterpret_cast<uint32_t*>(cpin.base);
         fill_hdr(hh, ref_slot, nxt.slot, seed);
-        if (next_ready) VS_HIP(hipStreamWaitEvent(s2, next_ready, 0));  // its extraction chunk
+        if (ready) VS_HIP(hipStreamWaitEvent(s2, ready, 0));  // its extraction chunk
         unsigned long long* keys = mstate2.as<unsigned long long>();
         unsigned* cnt = reinterpret_cast<unsigned*>(mstate2.as<char>() + 2 * kCap * sizeof(unsigned long long));
         VS_CHECK(enqueue_chain(s2, chain_buf2.as<char>(), hdr_buf2.as<int>(), hh, cpin.base + kHdrBytes, keys, cnt));
@@ -683,13 +731,29 @@ struct GpuOps {
         // The next frame's reference is this one's unless this frame becomes a keyframe, which the
         // rules of Slam.cpp:1061-1072 / is_keyframe (:1360) predict from the frame-id gap and this
         // chain's match count; a wrong guess only costs the speculation.
+        // The launch itself (~40 us of HIP calls) is deferred until this frame's local-map tracking
+        // and PnP are enqueued (flush_spec), so it overlaps them instead of delaying them.
+        spec_req.pending = false;
         if (cspec_on && err == VS_OK && next_frame && next_frame != &cur && next_frame->slot >= 0 && ref.slot >= 0) {
             const int ng = (int)R.good.size(), gap = cur.id - ref.id;
             const bool kf = (gap >= vs_trk::cfg::KF_MIN_FRAME_GAP && ng >= vs_trk::cfg::KF_MIN_MATCHES) ||
                             (ng < 2 * vs_trk::cfg::MIN_MATCHES && gap >= 5);
-            failed(launch_spec_chain(kf && cur.slot >= 0 ? cur.slot : ref.slot, *next_frame, seed + 1u));
+            spec_req.pending = true;
+            spec_req.ref_slot = kf && cur.slot >= 0 ? cur.slot : ref.slot;
+            spec_req.nxt = next_frame;
+            spec_req.nxt_slot = next_frame->slot;
+            spec_req.seed = seed + 1u;
+            spec_req.ready = next_ready;
         }
         return R;
+    }
+    // Launches the speculative chain chain() asked for, if its frames still sit in the same slots;
+    // called once the frame's tracking kernels are enqueued, and at the end of every frame.
+    void flush_spec() {
+        if (!spec_req.pending) return;
+        spec_req.pending = false;
+        if (err != VS_OK || spec_req.nxt->slot != spec_req.nxt_slot) return;
+        failed(launch_spec_chain(spec_req.ref_slot, *spec_req.nxt, spec_req.seed, spec_req.ready));
     }
 
     std::vector<vs_trk::Match> match(const vs_trk::Frame& a, const vs_trk::Frame& b, float ratio) {
@@ -789,7 +853,9 @@ struct GpuOps {
                 }
             }
             int* hb = reinterpret_cast<int*>(take((size_t)words * sizeof(int)));
-            if (!hb || failed(d2h(hb, d, (size_t)words * sizeof(int))) || failed(sync())) return 0;
+            if (!hb || failed(d2h(hb, d, (size_t)words * sizeof(int)))) return 0;
+            flush_spec();  // the next frame's chain, launched while these kernels run
+            if (failed(sync())) return 0;
             if (hs) {
                 const int n = reinterpret_cast<const int*>(hs)[1];
                 const float* so = reinterpret_cast<const float*>(hs + 16);
@@ -892,6 +958,25 @@ struct GpuOps {
         arch_cap = cap;
         return VS_OK;
     }
+    // loop_eval's candidate pool for P candidates: [P + 1] frames (keypoints, descriptors, counts),
+    // pairs, raw / good lists, counts, E-RANSAC outputs
+    struct LcLayout {
+        size_t kb, db, nb, pb, mb, cb, rb, gb, sb, total;
+        explicit LcLayout(int P) {
+            auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
+            const size_t F = (size_t)P + 1;
+            kb = al(F * kCap * sizeof(vs_keypoint));
+            db = al(F * kCap * 256 * sizeof(float));
+            nb = al(F * sizeof(int));
+            pb = al((size_t)2 * P * sizeof(int));
+            mb = al((size_t)P * kCap * sizeof(vs_match));
+            cb = al((size_t)P * sizeof(int));
+            rb = al((size_t)P * 16 * sizeof(double));
+            gb = al((size_t)P * 8 * sizeof(int));
+            sb = al(F * sizeof(FrameSrc));
+            total = kb + db + nb + pb + 2 * mb + 3 * cb + rb + gb + sb;
+        }
+    };
     // A keyframe's features into the archive (at settle, while its pool slot is still intact)
     int archive(vs_trk::Frame* f) {
         if (f->kf_slot >= 0 || f->slot < 0) return VS_OK;
@@ -915,12 +1000,9 @@ struct GpuOps {
         const int P = (int)kfs.size(), F = P + 1;
         std::vector<vs_trk::LoopEval> out(P);
         if (P == 0 || cur.slot < 0) return out;
-        auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
-        const size_t kb = al((size_t)F * kCap * sizeof(vs_keypoint)), db = al((size_t)F * kCap * 256 * sizeof(float));
-        const size_t nb = al((size_t)F * sizeof(int)), pb = al((size_t)2 * P * sizeof(int));
-        const size_t mb = al((size_t)P * kCap * sizeof(vs_match)), cb = al((size_t)P * sizeof(int));
-        const size_t rb = al((size_t)P * 16 * sizeof(double)), gb = al((size_t)P * 8 * sizeof(int));
-        if (failed(lc_buf.ensure(kb + db + nb + pb + 2 * mb + 3 * cb + rb + gb))) return out;
+        const LcLayout Lb(P);
+        const size_t kb = Lb.kb, db = Lb.db, nb = Lb.nb, pb = Lb.pb, mb = Lb.mb, cb = Lb.cb, rb = Lb.rb;
+        if (failed(lc_buf.ensure(Lb.total)) || failed(match_reserve(ctx, P, kCap, s))) return out;
         char* base = lc_buf.as<char>();
         auto* d_kps = reinterpret_cast<vs_keypoint*>(base);
         auto* d_desc = reinterpret_cast<float*>(base + kb);
@@ -934,31 +1016,28 @@ struct GpuOps {
         auto* d_ok = reinterpret_cast<int*>(tail + 2 * cb);
         auto* d_Rt = reinterpret_cast<double*>(tail + 3 * cb);  // R [P][9] | t [P][3] | scale [P]
         auto* d_diag = reinterpret_cast<int*>(tail + 3 * cb + rb);
-        auto gather = [&](int dst, const vs_keypoint* k, const float* d, const int* n) -> int {
-            VS_HIP(hipMemcpyAsync(d_kps + (size_t)dst * kCap, k, kCap * sizeof(vs_keypoint), hipMemcpyDeviceToDevice, s));
-            VS_HIP(hipMemcpyAsync(d_desc + (size_t)dst * kCap * 256, d, (size_t)kCap * 256 * sizeof(float),
-                                  hipMemcpyDeviceToDevice, s));
-            VS_HIP(hipMemcpyAsync(d_n + dst, n, sizeof(int), hipMemcpyDeviceToDevice, s));
-            return VS_OK;
-        };
-        if (failed(gather(0, kps_of(cur.slot), desc_of(cur.slot), pool_n.as<int>() + cur.slot))) return out;
+        // the pool: one gather launch from a table of source rows (archive or pool slot)
+        std::vector<FrameSrc> src(F);
+        src[0] = {kps_of(cur.slot), desc_of(cur.slot), pool_n.as<int>() + cur.slot};
         std::vector<int> pairs(2 * P);
         for (int i = 0; i < P; i++) {
             const vs_trk::Frame* k = kfs[i];
-            int rc;
             if (k->kf_slot >= 0)
-                rc = gather(i + 1, arch_kps.as<vs_keypoint>() + (size_t)k->kf_slot * kCap,
-                            arch_desc.as<float>() + (size_t)k->kf_slot * kCap * 256, arch_n.as<int>() + k->kf_slot);
+                src[i + 1] = {arch_kps.as<vs_keypoint>() + (size_t)k->kf_slot * kCap,
+                              arch_desc.as<float>() + (size_t)k->kf_slot * kCap * 256, arch_n.as<int>() + k->kf_slot};
             else if (k->slot >= 0)
-                rc = gather(i + 1, kps_of(k->slot), desc_of(k->slot), pool_n.as<int>() + k->slot);
+                src[i + 1] = {kps_of(k->slot), desc_of(k->slot), pool_n.as<int>() + k->slot};
             else {
                 set_error("vs_slam: a loop-closure keyframe has no device features");
-                rc = VS_ERR_CAPACITY;
+                failed(VS_ERR_CAPACITY);
+                return out;
             }
-            if (failed(rc)) return out;
             pairs[2 * i] = 0;
             pairs[2 * i + 1] = i + 1;
         }
+        auto* d_src = reinterpret_cast<FrameSrc*>(tail + 3 * cb + rb + Lb.gb);
+        if (failed(upload(d_src, src.data(), src.size() * sizeof(FrameSrc)))) return out;
+        hipLaunchKernelGGL(k_gather_frames, dim3(F, 8), dim3(256), 0, s, d_src, d_kps, d_desc, d_n);
         if (failed(upload(d_pairs, pairs.data(), pairs.size() * sizeof(int)))) return out;
         if (failed(match_pairs(ctx, P, d_pairs, F, d_desc, d_n, kCap, vs_trk::cfg::L2_RATIO_THRESHOLD, d_raw, d_nraw,
                                d_good, d_ngood, s)))
@@ -1071,7 +1150,8 @@ struct GpuOps {
         if (failed(hipMemsetAsync(map_valid.as<uint8_t>() + first, 1, (size_t)k, s) == hipSuccess ? VS_OK : VS_ERR_HIP))
             return;
         map_n = first + k;
-        failed(sync());  // rows_buf is rewritten by the next append
+        // no synchronisation: the next append's upload into rows_buf is ordered behind this gather on
+        // the same stream, and the pinned staging it came from is recycled only at a sync()
     }
 
     void map_valid_changed() { valid_dirty = true; }
@@ -1290,6 +1370,7 @@ int vs_slam_process_batch_dev(vs_slam* sl, int B, const uint8_t* d_bgr, const fl
             HostTimer ht(o.hprof, kHFrame);
             processed[b] = sl->trk->process_frame(sl->batch[b]) ? 1 : 0;
         }
+        o.flush_spec();  // a frame that tracked no local map still launches its speculation
         if (processed[b]) dense_record(sl, *sl->batch[b]);
         if (o.err != VS_OK) {
             rc = o.err;
@@ -1299,6 +1380,7 @@ int vs_slam_process_batch_dev(vs_slam* sl, int B, const uint8_t* d_bgr, const fl
     o.next_frame = nullptr;
     o.next_ready = nullptr;
     o.cspec.valid = false;
+    o.spec_req.pending = false;
     if (rc != VS_OK) {
         (void)hipStreamSynchronize(o.xs);  // nothing may still write the pool after an error
         (void)hipStreamSynchronize(o.s2);

@@ -128,6 +128,9 @@ int match_pairs(vs_ctx* ctx, int P, const int* d_pairs, int F, const float* d_de
                 vs_match* d_good, int* d_ngood, hipStream_t s,
                 const float* d_norms = nullptr, unsigned long long* d_keys = nullptr,
                 unsigned* d_cnt = nullptr);  // [F][cap] row norms when already known
+// Sizes the context's matcher key state for P pairs of cap rows up front (no allocation inside
+// a later match_pairs of at most that size).
+int match_reserve(vs_ctx* ctx, int P, int cap, hipStream_t s);
 // Sequential-fmaf squared norms of the descriptor rows of F frames ([F][cap], rows >= n[f] untouched).
 int desc_norms(vs_ctx* ctx, int F, const float* d_desc, const int* d_n, int cap, float* d_norms, hipStream_t s);
 // 3D-3D RANSAC
