@@ -239,7 +239,11 @@ struct GpuOps {
     vs_trk::PnPResult spec;
     std::vector<float> spec_obj, spec_img;
     hipStream_t s = nullptr;   // tracking stream (the context's stream is swapped to it during vs_slam calls)
-    hipStream_t xs = nullptr;  // extraction stream
+    hipStream_t xs = nullptr;  // extraction stream (the network)
+    // post-processing stream on the extraction CU set: a chunk's decode / NMS / sampling / copies run
+    // here while the network of the next chunk already runs on xs
+    hipStream_t xp = nullptr;
+    hipEvent_t region_done[2] = {nullptr, nullptr};  // last post-processing that read a region's network output
     // Speculative front chain of the batch's next frame (see chain()): its own stream on the tracking
     // CU set, result block, header, matcher key state and pinned host block [header | result].
     hipStream_t s2 = nullptr;
@@ -270,7 +274,8 @@ struct GpuOps {
     // (vs_slam_prefetch_batch_dev) into the other region while this one is tracked.
     struct XBatch {
         std::vector<int> ch;
-        std::vector<hipEvent_t> ev;
+        std::vector<hipEvent_t> ev;   // chunk c post-processed (xp)
+        std::vector<hipEvent_t> net;  // chunk c's network done (xs)
         Pinned pin;
         int region = 0, nb = 0;
         const uint8_t* bgr = nullptr;
@@ -332,12 +337,21 @@ struct GpuOps {
                 s = xs = nullptr;
                 masked = false;
             }
+            if (masked && hipExtStreamCreateWithCUMask(&xp, words, xm.data()) != hipSuccess) {
+                (void)hipStreamDestroy(s);
+                (void)hipStreamDestroy(xs);
+                (void)hipStreamDestroy(s2);
+                s = xs = s2 = nullptr;
+                masked = false;
+            }
         }
         if (!masked) {
             VS_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
             VS_HIP(hipStreamCreateWithFlags(&xs, hipStreamNonBlocking));
             VS_HIP(hipStreamCreateWithFlags(&s2, hipStreamNonBlocking));
+            VS_HIP(hipStreamCreateWithFlags(&xp, hipStreamNonBlocking));
         }
+        for (auto& e : region_done) VS_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
         VS_HIP(hipEventCreateWithFlags(&cspec_ev, hipEventDisableTiming));
         own_streams = true;
         return VS_OK;
@@ -345,14 +359,19 @@ struct GpuOps {
     void destroy_streams() {
         if (!own_streams) return;
         (void)hipStreamSynchronize(xs);
+        (void)hipStreamSynchronize(xp);
         (void)hipStreamSynchronize(s);
         (void)hipStreamSynchronize(s2);
+        for (auto& e : region_done) (void)hipEventDestroy(e);
         for (auto& X : xb) {
             for (hipEvent_t e : X.ev) (void)hipEventDestroy(e);
+            for (hipEvent_t e : X.net) (void)hipEventDestroy(e);
             X.ev.clear();
+            X.net.clear();
         }
         (void)hipEventDestroy(cspec_ev);
         (void)hipStreamDestroy(xs);
+        (void)hipStreamDestroy(xp);
         (void)hipStreamDestroy(s);
         (void)hipStreamDestroy(s2);
         own_streams = false;
@@ -377,8 +396,10 @@ struct GpuOps {
         VS_CHECK(pool_norms.ensure((size_t)S * kCap * sizeof(float)));
         VS_HIP(hipMemsetAsync(pool_n.p, 0, (size_t)S * sizeof(int), s));
         const int hc = (h + 7) / 8, wc = (w + 7) / 8;
-        VS_CHECK(semi.ensure((size_t)B * hc * wc * VS_SEMI_CH * sizeof(float)));
-        VS_CHECK(dgrid.ensure((size_t)B * hc * wc * VS_DESC_DIM * sizeof(float)));
+        // network outputs per batch region (2 B frames): a chunk's post-processing reads its own
+        // frames' rows while later chunks (and the prefetched batch) write theirs
+        VS_CHECK(semi.ensure((size_t)2 * B * hc * wc * VS_SEMI_CH * sizeof(float)));
+        VS_CHECK(dgrid.ensure((size_t)2 * B * hc * wc * VS_DESC_DIM * sizeof(float)));
         VS_CHECK(chain_buf.ensure(kChainBytes));
         VS_CHECK(chain_buf2.ensure(kChainBytes));
         VS_CHECK(hdr_buf.ensure(kHdrBytes));
@@ -528,32 +549,41 @@ struct GpuOps {
             X.ch.push_back(std::min(nb, X.ch.back() + c));
         const int nch = (int)X.ch.size() - 1;
         while ((int)X.ev.size() < nch) {
-            hipEvent_t e;
+            hipEvent_t e, en;
             VS_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+            VS_HIP(hipEventCreateWithFlags(&en, hipEventDisableTiming));
             X.ev.push_back(e);
+            X.net.push_back(en);
         }
         VS_CHECK(X.pin.reserve((size_t)nb * kCap * sizeof(vs_keypoint) + (size_t)nb * sizeof(int) + 64));
         char* hk = X.pin.base;
         int* hn = reinterpret_cast<int*>(hk + (size_t)nb * kCap * sizeof(vs_keypoint));
         const int hc = (h + 7) / 8, wc = (w + 7) / 8;
+        // the region's previous batch has finished reading its network outputs
+        VS_HIP(hipStreamWaitEvent(xs, region_done[X.region], 0));
+        const size_t semi_f = (size_t)hc * wc * VS_SEMI_CH, dgrid_f = (size_t)hc * wc * VS_DESC_DIM;
         for (int c = 0; c < nch; c++) {
             const int f0 = X.ch[c], m = X.ch[c + 1] - X.ch[c];
-            VS_CHECK(sp_forward(ctx, m, d_bgr + (size_t)f0 * h * w * 3, 3, h, w, xs, semi.as<float>(),
-                                dgrid.as<float>()));
+            float* sm = semi.as<float>() + (size_t)(s0 + f0) * semi_f;
+            float* dg = dgrid.as<float>() + (size_t)(s0 + f0) * dgrid_f;
+            VS_CHECK(sp_forward(ctx, m, d_bgr + (size_t)f0 * h * w * 3, 3, h, w, xs, sm, dg));
+            VS_HIP(hipEventRecord(X.net[c], xs));
+            VS_HIP(hipStreamWaitEvent(xp, X.net[c], 0));
             VS_CHECK(sp_postprocess(ctx, m, hc, wc, h, w, kps_of(s0 + f0), desc_of(s0 + f0), pool_n.as<int>() + s0 + f0,
-                                    kCap, xs, semi.as<float>(), dgrid.as<float>()));
+                                    kCap, xp, sm, dg));
             // descriptor row norms once per frame (matching reuses them for every pair)
-            VS_CHECK(desc_norms(ctx, m, desc_of(s0 + f0), pool_n.as<int>() + s0 + f0, kCap, norms_of(s0 + f0), xs));
+            VS_CHECK(desc_norms(ctx, m, desc_of(s0 + f0), pool_n.as<int>() + s0 + f0, kCap, norms_of(s0 + f0), xp));
             if (d_depth)
                 VS_HIP(hipMemcpyAsync(depth_of(s0 + f0), d_depth + (size_t)f0 * h * w, (size_t)m * h * w * sizeof(float),
-                                      hipMemcpyDeviceToDevice, xs));
+                                      hipMemcpyDeviceToDevice, xp));
             else
-                VS_HIP(hipMemsetAsync(depth_of(s0 + f0), 0, (size_t)m * h * w * sizeof(float), xs));
+                VS_HIP(hipMemsetAsync(depth_of(s0 + f0), 0, (size_t)m * h * w * sizeof(float), xp));
             VS_HIP(hipMemcpyAsync(hk + (size_t)f0 * kCap * sizeof(vs_keypoint), kps_of(s0 + f0),
-                                  (size_t)m * kCap * sizeof(vs_keypoint), hipMemcpyDeviceToHost, xs));
-            VS_HIP(hipMemcpyAsync(hn + f0, pool_n.as<int>() + s0 + f0, (size_t)m * sizeof(int), hipMemcpyDeviceToHost, xs));
-            VS_HIP(hipEventRecord(X.ev[c], xs));
+                                  (size_t)m * kCap * sizeof(vs_keypoint), hipMemcpyDeviceToHost, xp));
+            VS_HIP(hipMemcpyAsync(hn + f0, pool_n.as<int>() + s0 + f0, (size_t)m * sizeof(int), hipMemcpyDeviceToHost, xp));
+            VS_HIP(hipEventRecord(X.ev[c], xp));
         }
+        VS_HIP(hipEventRecord(region_done[X.region], xp));
         return VS_OK;
     }
     // The batch's extraction: the one prefetched for exactly these buffers, or enqueued now; then the
@@ -564,6 +594,7 @@ struct GpuOps {
         XBatch& P = xb[xcur ^ 1];
         if (P.pending && !(P.bgr == d_bgr && P.depth == d_depth && P.nb == nb)) {
             VS_HIP(hipStreamSynchronize(xs));  // a stale prefetch: let it land, its region is free again
+            VS_HIP(hipStreamSynchronize(xp));
             P.pending = false;
             batch_region = P.region;
         }
@@ -1383,6 +1414,7 @@ int vs_slam_process_batch_dev(vs_slam* sl, int B, const uint8_t* d_bgr, const fl
     o.spec_req.pending = false;
     if (rc != VS_OK) {
         (void)hipStreamSynchronize(o.xs);  // nothing may still write the pool after an error
+        (void)hipStreamSynchronize(o.xp);
         (void)hipStreamSynchronize(o.s2);
         sl->dense_depth.clear();
         sl->dense_R.clear();
