@@ -59,7 +59,7 @@ struct PnpHyp {
     int stride;  // hypotheses per problem
 };
 
-__device__ inline bool epnp_subset(const float* obj, const float* img, const int* idx, int m, const Cam& K, double* rv,
+__device__ __attribute__((noinline)) bool epnp_subset(const float* obj, const float* img, const int* idx, int m, const Cam& K, double* rv,
                                    double* tv) {
     double X[15], uv[10];
     for (int j = 0; j < m; j++) {
@@ -250,7 +250,7 @@ __global__ __launch_bounds__(64) void k_pnp_hyp(const float* __restrict__ obj_al
     bool ok = sOk != 0;
     if (ok) {
         for (int e = lane; e < 144; e += 64) {
-            sA[e] = epnp_mtm(sAl, sUV, m, K, e / 12, e % 12);
+            sA[e] = epnp_mtm<5>(sAl, sUV, m, K, e / 12, e % 12);
             sV[e] = (e / 12 == e % 12) ? 1.0 : 0.0;
         }
         __syncthreads();
@@ -545,8 +545,8 @@ __global__ __launch_bounds__(256) void k_pnp_ransac(const float* __restrict__ ob
             mask[i] = reproj_err2(R, tv0, K, obj[3 * i], obj[3 * i + 1], obj[3 * i + 2], img[2 * i], img[2 * i + 1]) <=
                       thr2;
         // (each lane re-reads only the mask entries it wrote itself)
-        // Thread 0 owns S.lm; block_sum's barriers order its updates after every lane has read
-        // the previous candidate.
+        // Thread 0 owns S.lm; the barrier after its update orders it after every lane's read of the
+        // previous candidate, and the next reduction's writes to S.red after its reads.
         double p[6] = {rv0[0], rv0[1], rv0[2], tv0[0], tv0[1], tv0[2]};
         for (bool first = true;; first = false) {
             // the 7 rotations of lm_rotations (R(r), R(r +- h e_k)), one per lane, shared via LDS
@@ -562,7 +562,7 @@ __global__ __launch_bounds__(256) void k_pnp_ransac(const float* __restrict__ ob
             for (int i = tid; i < n; i += blockDim.x)
                 if (mask[i])
                     lm_point(L, p + 3, K, obj[3 * i], obj[3 * i + 1], obj[3 * i + 2], img[2 * i], img[2 * i + 1], acc);
-            block_sum<kLmTerms>(acc, S.red, tot);
+            block_sum_to0<kLmTerms>(acc, S.red, tot);  // tot valid on thread 0 (its only reader)
             if (tid == 0) {
                 if (first)
                     S.lm.init(p, tot);

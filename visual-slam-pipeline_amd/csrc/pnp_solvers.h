@@ -476,10 +476,14 @@ VS_HD inline double epnp_m1(const double* al, double v, const Cam& K, int a) {
     return (a % 3 == 0) ? 0.0 : (a % 3 == 1) ? x * K.fy : x * (K.cy - v);
 }
 // (M^T M)[a][b], accumulated over the points in order
+// (MAXN bounds n at compile time so the device unrolls the point loop, as in epnp_variant)
+template <int MAXN>
 VS_HD inline double epnp_mtm(const double (*alphas)[4], const double* uv, int n, const Cam& K, int a, int b) {
     double s = 0;
-    for (int i = 0; i < n; i++)
-        s += epnp_m0(alphas[i], uv[2 * i], K, a) * epnp_m0(alphas[i], uv[2 * i], K, b) +
+    VS_UNROLL
+    for (int i = 0; i < MAXN; i++)
+        if (i < n)
+            s += epnp_m0(alphas[i], uv[2 * i], K, a) * epnp_m0(alphas[i], uv[2 * i], K, b) +
              epnp_m1(alphas[i], uv[2 * i + 1], K, a) * epnp_m1(alphas[i], uv[2 * i + 1], K, b);
     return s;
 }
@@ -659,7 +663,7 @@ VS_HD bool epnp(const double* X, const double* uv, int n, const Cam& K, double* 
     if (!epnp_control(X, n, cw, alphas)) return false;
     double MtM[144];
     for (int a = 0; a < 12; a++)
-        for (int b = 0; b < 12; b++) MtM[a * 12 + b] = epnp_mtm(alphas, uv, n, K, a, b);
+        for (int b = 0; b < 12; b++) MtM[a * 12 + b] = epnp_mtm<MAXN>(alphas, uv, n, K, a, b);
     double dm[12], um[144];
     sym_eig_rr<12>(MtM, dm, um);
     double v[4][12], L[6][10], rho[6];

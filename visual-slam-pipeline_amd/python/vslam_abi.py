@@ -11,7 +11,8 @@ import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 PKG_DIR = os.path.dirname(_HERE)
-LIB_PATH = os.path.join(PKG_DIR, "libvslam_hip.so")
+# VS_LIB_PATH: another build of the same library (A/B timing experiments only)
+LIB_PATH = os.environ.get("VS_LIB_PATH") or os.path.join(PKG_DIR, "libvslam_hip.so")
 
 KEYPOINT_DTYPE = np.dtype([("x", "<f4"), ("y", "<f4"), ("size", "<f4"), ("angle", "<f4"),
                            ("response", "<f4"), ("octave", "<i4"), ("class_id", "<i4")])
