@@ -56,6 +56,19 @@ struct OracleOps {
         return good;
     }
 
+    // match() and the DLT of every good match (the tracker triangulates from them)
+    std::vector<Match> match_dlt(const Frame& a, const Frame& b, float ratio, const double P1[12], const double P2[12],
+                                 std::vector<std::array<float, 4>>& X4) {
+        std::vector<Match> m = match(a, b, ratio);
+        X4.resize(m.size());
+        for (size_t i = 0; i < m.size(); i++) {
+            const auto& ka = a.kps[m[i].query_idx];
+            const auto& kb = b.kps[m[i].train_idx];
+            vs_pnp::dlt_point(P1, P2, ka.x, ka.y, kb.x, kb.y, X4[i].data());
+        }
+        return m;
+    }
+
     static void points(const Frame& a, const Frame& b, const std::vector<Match>& m, std::vector<float>& p1,
                        std::vector<float>& p2) {
         p1.clear();

@@ -266,6 +266,13 @@ VS_HD void sym_eig_rr(double* A, double* w, double* V) {
     }
 }
 
+// cv::triangulatePoints for one correspondence (OpenCV's icvTriangulatePoints restated: the 4x4
+// DLT system, its right singular vector of the smallest singular value -- here the eigenvector of
+// A^T A -- stored as float like the CV_32F pts4D of Slam.cpp:1276-1277).  Shared by the host
+// tracker restatement and the GPU back end's per-match kernel.
+VS_HD inline void dlt_point(const double P1[12], const double P2[12], float x1, float y1, float x2, float y2,
+                            float X[4]);
+
 // Least squares min ||A x - b|| for an M x N (M >= N) matrix by Householder QR (A, b destroyed).
 template <int M, int N>
 VS_HD void lstsq(double* A, double* b, double* x) {
@@ -832,5 +839,26 @@ struct LmState {
         }
     }
 };
+
+VS_HD inline void dlt_point(const double P1[12], const double P2[12], float x1, float y1, float x2, float y2,
+                            float X[4]) {
+    double A[16];
+    const double* Ps[2] = {P1, P2};
+    const double xs[2] = {x1, x2}, ys[2] = {y1, y2};
+    for (int j = 0; j < 2; j++)
+        for (int k = 0; k < 4; k++) {
+            A[(2 * j) * 4 + k] = xs[j] * Ps[j][8 + k] - Ps[j][k];
+            A[(2 * j + 1) * 4 + k] = ys[j] * Ps[j][8 + k] - Ps[j][4 + k];
+        }
+    double AtA[16], w[4], V[16];
+    for (int i = 0; i < 4; i++)
+        for (int j = 0; j < 4; j++) {
+            double s = 0;
+            for (int k = 0; k < 4; k++) s += A[k * 4 + i] * A[k * 4 + j];
+            AtA[i * 4 + j] = s;
+        }
+    sym_eig<4>(AtA, w, V);
+    for (int i = 0; i < 4; i++) X[i] = (float)V[i * 4 + 3];
+}
 
 }  // namespace vs_pnp

@@ -64,6 +64,22 @@ __global__ __launch_bounds__(256) void k_gather_frames(const FrameSrc* __restric
     }
 }
 
+// Triangulation inputs (Slam::triangulate_points, Slam.cpp:1265-1277): the DLT solution of every
+// good match of a keyframe match, one lane per match, right behind the matcher.
+struct DltProj {
+    double P1[12], P2[12];
+};
+__global__ __launch_bounds__(64) void k_dlt(const vs_match* __restrict__ good, const int* __restrict__ ng,
+                                            const vs_keypoint* __restrict__ ka, const vs_keypoint* __restrict__ kb,
+                                            DltProj P, float4* __restrict__ X) {
+    const int i = blockIdx.x * 64 + threadIdx.x;
+    if (i >= *ng) return;
+    const vs_match m = good[i];
+    float x[4];
+    vs_pnp::dlt_point(P.P1, P.P2, ka[m.query_idx].x, ka[m.query_idx].y, kb[m.train_idx].x, kb[m.train_idx].y, x);
+    X[i] = make_float4(x[0], x[1], x[2], x[3]);
+}
+
 // dst[i] = src row rows[i] (256 floats), one 64-lane wave per row, float4 per lane
 __global__ __launch_bounds__(256) void k_gather_rows(const float* __restrict__ src, const int* __restrict__ rows,
                                                      int k, float* __restrict__ dst) {
@@ -304,6 +320,7 @@ struct GpuOps {
     DevBuf arch_kps, arch_desc, arch_n;
     int arch_cap = 0, arch_used = 0;
     DevBuf lc_buf;  // loop-closure candidate pool and outputs
+    DevBuf dlt_buf;  // [kCap] DLT solutions of a keyframe match (match_dlt)
     int err = VS_OK;                     // first error inside an Ops call (the tracker has no error channel)
 
     vs_keypoint* kps_of(int slot) const { return pool_kps.as<vs_keypoint>() + (size_t)slot * kCap; }
@@ -320,18 +337,24 @@ struct GpuOps {
         VS_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, ctx->device));
         const char* env = std::getenv("VS_SLAM_TRACK_CUS");
         const int tcu = env ? std::atoi(env) : 32;
+        // VS_SLAM_SPEC_CUS > 0: the speculative chain gets CUs of its own, carved from the
+        // extraction set (default 0: it shares the tracking CUs)
+        const char* senv = std::getenv("VS_SLAM_SPEC_CUS");
+        const int scu = senv ? std::max(0, std::atoi(senv)) : 0;
         bool masked = false;
-        if (tcu > 0 && ncu >= 2 * tcu) {
+        if (tcu > 0 && ncu >= 2 * (tcu + scu)) {
             const int words = (ncu + 31) / 32;
-            std::vector<uint32_t> tm(words, 0u), xm(words, 0u);
-            for (int cu = 0; cu < ncu; cu++) (cu < tcu ? tm : xm)[cu / 32] |= 1u << (cu % 32);
+            std::vector<uint32_t> tm(words, 0u), xm(words, 0u), sm(words, 0u);
+            for (int cu = 0; cu < ncu; cu++)
+                (cu < tcu ? tm : cu < tcu + scu ? sm : xm)[cu / 32] |= 1u << (cu % 32);
+            if (scu == 0) sm = tm;
             masked = hipExtStreamCreateWithCUMask(&s, words, tm.data()) == hipSuccess;
             if (masked && hipExtStreamCreateWithCUMask(&xs, words, xm.data()) != hipSuccess) {
                 (void)hipStreamDestroy(s);
                 s = nullptr;
                 masked = false;
             }
-            if (masked && hipExtStreamCreateWithCUMask(&s2, words, tm.data()) != hipSuccess) {
+            if (masked && hipExtStreamCreateWithCUMask(&s2, words, sm.data()) != hipSuccess) {
                 (void)hipStreamDestroy(s);
                 (void)hipStreamDestroy(xs);
                 s = xs = nullptr;
@@ -418,6 +441,7 @@ struct GpuOps {
         VS_CHECK(map_tmp.ensure((size_t)64 << 20));
         VS_CHECK(work.ensure((size_t)1 << 20));
         VS_CHECK(pnp_io.ensure((size_t)1 << 20));
+        VS_CHECK(dlt_buf.ensure((size_t)kCap * sizeof(float4)));
         VS_CHECK(rows_buf.ensure((size_t)64 << 10));
         // the context's per-stage scratch at its largest in-loop size: local-map tracking for 200k
         // map points, PnP hypothesis tables for the largest RANSAC budget (loop closure: 300)
@@ -800,6 +824,33 @@ struct GpuOps {
         const int ng = reinterpret_cast<const int*>(hc)[4];
         const auto* hg = reinterpret_cast<const vs_trk::Match*>(hc + kChainGood);
         out.assign(hg, hg + ng);
+        return out;
+    }
+
+    // match() plus the DLT of every good match (triangulation input) in the same round trip
+    std::vector<vs_trk::Match> match_dlt(const vs_trk::Frame& a, const vs_trk::Frame& b, float ratio, const double P1[12],
+                                         const double P2[12], std::vector<std::array<float, 4>>& X4) {
+        HostTimer ht(hprof, kHMatch);
+        std::vector<vs_trk::Match> out;
+        X4.clear();
+        char* c = chain_buf.as<char>();
+        int* di = reinterpret_cast<int*>(c + kChainInts);
+        if (failed(enqueue_match(a.slot, b.slot, ratio, di))) return out;
+        DltProj P;
+        std::memcpy(P.P1, P1, sizeof(P.P1));
+        std::memcpy(P.P2, P2, sizeof(P.P2));
+        float4* dX = dlt_buf.as<float4>();
+        hipLaunchKernelGGL(k_dlt, dim3((kCap + 63) / 64), dim3(64), 0, s, reinterpret_cast<const vs_match*>(c + kChainGood),
+                           di + 4, kps_of(a.slot), kps_of(b.slot), P, dX);
+        char* hc = take(kChainKept + (size_t)kCap * sizeof(float4));
+        if (!hc || failed(d2h(hc, c, kChainKept)) || failed(d2h(hc + kChainKept, dX, (size_t)kCap * sizeof(float4))))
+            return out;
+        if (failed(sync())) return out;
+        const int ng = reinterpret_cast<const int*>(hc)[4];
+        const auto* hg = reinterpret_cast<const vs_trk::Match*>(hc + kChainGood);
+        out.assign(hg, hg + ng);
+        X4.resize(ng);
+        std::memcpy(X4.data(), hc + kChainKept, (size_t)ng * sizeof(float4));
         return out;
     }
 
@@ -1336,7 +1387,7 @@ void vs_slam_destroy(vs_slam* sl) {
     DevBuf* bufs[] = {&o.pool_kps, &o.pool_desc, &o.pool_n, &o.pool_depth, &o.pool_norms, &o.semi, &o.dgrid,
                       &o.chain_buf,    &o.work, &o.rows_buf,      &o.map_pos, &o.map_desc,  &o.map_valid, &o.map_tmp,
                       &o.pnp_io,       &o.hdr_buf, &o.chain_buf2, &o.hdr_buf2, &o.mstate2,
-                      &o.arch_kps,     &o.arch_desc, &o.arch_n,   &o.lc_buf};
+                      &o.arch_kps,     &o.arch_desc, &o.arch_n,   &o.lc_buf,    &o.dlt_buf};
     for (DevBuf* b : bufs) b->release();
     if (sl->trace) std::fclose(sl->trace);
     delete sl;

@@ -282,8 +282,7 @@ class Tracker {
                     stats_.keyframes++;
                     stats_.bridges++;
                     if (last_keyframe_) {
-                        auto bridge = ops_.match(*last_keyframe_, *last_frame_, cfg::L2_RATIO_THRESHOLD);
-                        if ((int)bridge.size() >= cfg::MIN_MATCHES) triangulate_points(last_keyframe_, last_frame_, bridge);
+                        match_and_triangulate(last_keyframe_, last_frame_);
                     }
                     create_points_from_depth(last_frame_);
                     last_keyframe_ = last_frame_;
@@ -982,43 +981,16 @@ class Tracker {
 
     // Slam::setup_new_keyframe (:699-725); local BA is disabled (Config.h:99)
     void setup_new_keyframe(const FramePtr& frame) {
-        if (last_keyframe_) {
-            auto kfm = ops_.match(*last_keyframe_, *frame, cfg::L2_RATIO_THRESHOLD);
-            if ((int)kfm.size() >= cfg::MIN_MATCHES) triangulate_points(last_keyframe_, frame, kfm);
-        }
+        if (last_keyframe_) match_and_triangulate(last_keyframe_, frame);
         create_points_from_depth(frame);
         cull_map_points(frame);
     }
 
-    // cv::triangulatePoints for one correspondence (OpenCV's icvTriangulatePoints restated: the
-    // 4x4 DLT system, its right singular vector of the smallest singular value — here the
-    // eigenvector of A^T A — stored as float like the CV_32F pts4D of Slam.cpp:1276-1277).
-    static void dlt_point(const double P1[12], const double P2[12], float x1, float y1, float x2, float y2, float X[4]) {
-        double A[16];
-        const double* Ps[2] = {P1, P2};
-        const double xs[2] = {x1, x2}, ys[2] = {y1, y2};
-        for (int j = 0; j < 2; j++)
-            for (int k = 0; k < 4; k++) {
-                A[(2 * j) * 4 + k] = xs[j] * Ps[j][8 + k] - Ps[j][k];
-                A[(2 * j + 1) * 4 + k] = ys[j] * Ps[j][8 + k] - Ps[j][4 + k];
-            }
-        double AtA[16], w[4], V[16];
-        for (int i = 0; i < 4; i++)
-            for (int j = 0; j < 4; j++) {
-                double s = 0;
-                for (int k = 0; k < 4; k++) s += A[k * 4 + i] * A[k * 4 + j];
-                AtA[i * 4 + j] = s;
-            }
-        vs_pnp::sym_eig<4>(AtA, w, V);
-        for (int i = 0; i < 4; i++) X[i] = (float)V[i * 4 + 3];
-    }
-
-    // Slam::triangulate_points (:1246-1356)
-    void triangulate_points(const FramePtr& f1, const FramePtr& f2, const std::vector<Match>& matches) {
-        const M3 R1c = tr(f1->R), R2c = tr(f2->R);
-        const V3 m1 = mulv(R1c, f1->t), m2 = mulv(R2c, f2->t);
+    // The projection matrices K [R | t] of two frames (Slam.cpp:1255-1262)
+    static void proj_mats(const Frame& f1, const Frame& f2, double P1[12], double P2[12]) {
+        const M3 R1c = tr(f1.R), R2c = tr(f2.R);
+        const V3 m1 = mulv(R1c, f1.t), m2 = mulv(R2c, f2.t);
         const V3 t1c{-m1[0], -m1[1], -m1[2]}, t2c{-m2[0], -m2[1], -m2[2]};
-        double P1[12], P2[12];  // K [R | t]
         const double K[9] = {cfg::FX, 0, cfg::CX, 0, cfg::FY, cfg::CY, 0, 0, 1};
         for (int i = 0; i < 3; i++)
             for (int j = 0; j < 4; j++) {
@@ -1030,6 +1002,25 @@ class Tracker {
                 P1[i * 4 + j] = s1;
                 P2[i * 4 + j] = s2;
             }
+    }
+
+    // match(f1, f2) then triangulate_points on the good matches when there are enough
+    // (Slam.cpp:713-716, :859-862).  The back end returns the DLT solution of every good match
+    // with the matches (vs_trk::dlt_point; on the GPU one launch behind the matcher, one round trip).
+    void match_and_triangulate(const FramePtr& f1, const FramePtr& f2) {
+        double P1[12], P2[12];
+        proj_mats(*f1, *f2, P1, P2);
+        std::vector<std::array<float, 4>> X4;
+        const auto m = ops_.match_dlt(*f1, *f2, cfg::L2_RATIO_THRESHOLD, P1, P2, X4);
+        if ((int)m.size() >= cfg::MIN_MATCHES) triangulate_points(f1, f2, m, X4);
+    }
+
+    // Slam::triangulate_points (:1246-1356), with the DLT of match i in X4[i]
+    void triangulate_points(const FramePtr& f1, const FramePtr& f2, const std::vector<Match>& matches,
+                            const std::vector<std::array<float, 4>>& X4all) {
+        const M3 R1c = tr(f1->R), R2c = tr(f2->R);
+        const V3 m1 = mulv(R1c, f1->t), m2 = mulv(R2c, f2->t);
+        const V3 t1c{-m1[0], -m1[1], -m1[2]}, t2c{-m2[0], -m2[1], -m2[2]};
         if (matches.size() < 5) return;
         const bool use_real_depth = f2->has_depth();
         std::vector<int> rows;
@@ -1037,8 +1028,7 @@ class Tracker {
         for (size_t i = 0; i < matches.size(); i++) {
             const Keypoint& a = f1->kps[matches[i].query_idx];
             const Keypoint& b = f2->kps[matches[i].train_idx];
-            float X4[4];
-            dlt_point(P1, P2, a.x, a.y, b.x, b.y, X4);
+            const float* X4 = X4all[i].data();
             const float w = X4[3];
             if (std::abs(w) < 1e-6) continue;
             double pt[3] = {X4[0] / w, X4[1] / w, X4[2] / w};
