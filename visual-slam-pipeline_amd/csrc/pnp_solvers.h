@@ -120,6 +120,23 @@ VS_HD inline int ransac_update_num_iters(double p, double ep, int model_points, 
 }
 
 // ------------------------------------------------------------- small dense linear algebra
+// The Jacobi rotation (c, s) that zeroes A[p][q]: with d = A[q][q] - A[p][p], h = 2 A[p][q],
+// r = |(d, h)|, the classic t = tan = sgn(d) h / (|d| + r) gives c = 1 / sqrt(1 + t^2) =
+// (|d| + r) / w and s = t c = sgn(d) h / w with w = sqrt(2 r (|d| + r)): two square roots and two
+// independent divisions (the textbook form chains three divisions and two roots; on the device
+// that chain is each Jacobi round's latency).  No cancellation: every sum adds non-negative terms.
+// Rotations with |A[p][q]| < 1e-150 are skipped (h^2 stays a normal number).
+VS_HD inline bool jacobi_angle(double app, double aqq, double apq, double& c, double& s) {
+    if (fabs(apq) < 1e-150) return false;
+    const double d = aqq - app, h = 2.0 * apq;
+    const double r = sqrt(d * d + h * h);
+    const double u = fabs(d) + r;
+    const double w = sqrt(2.0 * r * u);
+    c = u / w;
+    s = (d >= 0 ? h : -h) / w;
+    return true;
+}
+
 // Cyclic Jacobi eigen-decomposition of the symmetric n x n matrix A (row-major, destroyed):
 // w[k] eigenvalues in descending order, V[i*n + k] the k-th eigenvector (columns).
 template <int N>
@@ -135,12 +152,8 @@ VS_HD void sym_eig(double* A, double* w, double* V) {
         if (!(off > 1e-32 * total)) break;
         for (int p = 0; p < N - 1; p++)
             for (int q = p + 1; q < N; q++) {
-                const double apq = A[p * N + q];
-                if (fabs(apq) < 1e-300) continue;
-                const double app = A[p * N + p], aqq = A[q * N + q];
-                const double theta = (aqq - app) / (2.0 * apq);
-                const double t = (theta >= 0 ? 1.0 : -1.0) / (fabs(theta) + sqrt(theta * theta + 1.0));
-                const double c = 1.0 / sqrt(t * t + 1.0), s = t * c;
+                double c, s;
+                if (!jacobi_angle(A[p * N + p], A[q * N + q], A[p * N + q], c, s)) continue;
                 for (int k = 0; k < N; k++) {
                     const double akp = A[k * N + p], akq = A[k * N + q];
                     A[k * N + p] = c * akp - s * akq;
@@ -189,14 +202,6 @@ VS_HD inline void rr_pair(int N, int r, int k, int& p, int& q) {
     q = a < b ? b : a;
 }
 
-VS_HD inline bool jacobi_angle(double app, double aqq, double apq, double& c, double& s) {
-    if (fabs(apq) < 1e-300) return false;
-    const double theta = (aqq - app) / (2.0 * apq);
-    const double t = (theta >= 0 ? 1.0 : -1.0) / (fabs(theta) + sqrt(theta * theta + 1.0));
-    c = 1.0 / sqrt(t * t + 1.0);
-    s = t * c;
-    return true;
-}
 
 template <int N>
 VS_HD void sym_eig_rr(double* A, double* w, double* V) {
