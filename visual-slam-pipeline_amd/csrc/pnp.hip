@@ -276,20 +276,27 @@ __global__ __launch_bounds__(64) void k_pnp_hyp(const float* __restrict__ obj_al
             // i0 < i1, pair b columns j0 < j1), a = lane / 6, b = lane % 6.  The diagonal-block lanes
             // (a == b) compute the round's angles from their registers and shuffle them out; every
             // block takes its column rotation (b) and then its row rotation (a) -- per element exactly
-            // the sequential statement's column-then-row order; V's rows take their column rotations
-            // in LDS; the blocks go back to the LDS matrix and the next round's blocks are read.
+            // the sequential statement's column-then-row order; V's rows 2a, 2a + 1 take the column
+            // rotation of pair b in the same lane; the blocks go back to the LDS matrix and the next
+            // round's blocks are read.
             const int ba = lane / 6, bb = lane % 6;
             const bool blk = lane < 36;
             int i0, i1, j0, j1;
-            double x00 = 0, x01 = 0, x10 = 0, x11 = 0;
-            if (blk) {
-                rr_pair(12, 0, ba, i0, i1);
-                rr_pair(12, 0, bb, j0, j1);
+            double x00 = 0, x01 = 0, x10 = 0, x11 = 0, p0 = 0, q0 = 0, p1 = 0, q1 = 0;
+            // the round's A block and the V entries (rows 2a, 2a + 1 at the block's columns)
+            auto load_blk = [&](int r) {
+                rr_pair(12, r, ba, i0, i1);
+                rr_pair(12, r, bb, j0, j1);
                 x00 = sA[i0 * 12 + j0];
                 x01 = sA[i0 * 12 + j1];
                 x10 = sA[i1 * 12 + j0];
                 x11 = sA[i1 * 12 + j1];
-            }
+                p0 = sV[(2 * ba) * 12 + j0];
+                q0 = sV[(2 * ba) * 12 + j1];
+                p1 = sV[(2 * ba + 1) * 12 + j0];
+                q1 = sV[(2 * ba + 1) * 12 + j1];
+            };
+            if (blk) load_blk(0);
             for (int r = 0; r < 11; r++) {
                 double c = 1.0, sn = 0.0;
                 int act = 0;
@@ -319,29 +326,16 @@ __global__ __launch_bounds__(64) void k_pnp_hyp(const float* __restrict__ obj_al
                     sA[i1 * 12 + j0] = x10;
                     sA[i1 * 12 + j1] = x11;
                 }
-#pragma unroll
-                for (int u = 0; u < 2; u++) {  // V's rows: column rotation of pair b (items lane, lane + 64)
-                    const int v = lane + 64 * u, vi = v / 6, vb = v % 6;
-                    // shuffles with every lane active; the item's own guard comes after
-                    const double cv = __shfl(c, 7 * vb), sv = __shfl(sn, 7 * vb);
-                    const int av = __shfl(act, 7 * vb);
-                    if (v < 72 && av) {
-                        int k0, k1;
-                        rr_pair(12, r, vb, k0, k1);
-                        const double vp = sV[vi * 12 + k0], vq = sV[vi * 12 + k1];
-                        sV[vi * 12 + k0] = cv * vp - sv * vq;
-                        sV[vi * 12 + k1] = sv * vp + cv * vq;
-                    }
+                // V's rows 2a, 2a + 1 at this block's column pair b take the column rotation the
+                // lane already holds for A (each V entry once per round, no shuffles)
+                if (blk && actb) {
+                    sV[(2 * ba) * 12 + j0] = cb * p0 - sb * q0;
+                    sV[(2 * ba) * 12 + j1] = sb * p0 + cb * q0;
+                    sV[(2 * ba + 1) * 12 + j0] = cb * p1 - sb * q1;
+                    sV[(2 * ba + 1) * 12 + j1] = sb * p1 + cb * q1;
                 }
                 __syncthreads();
-                if (blk && r + 1 < 11) {  // the next round's block
-                    rr_pair(12, r + 1, ba, i0, i1);
-                    rr_pair(12, r + 1, bb, j0, j1);
-                    x00 = sA[i0 * 12 + j0];
-                    x01 = sA[i0 * 12 + j1];
-                    x10 = sA[i1 * 12 + j0];
-                    x11 = sA[i1 * 12 + j1];
-                }
+                if (blk && r + 1 < 11) load_blk(r + 1);  // the next round's block
                 __syncthreads();
             }
         }
