@@ -284,9 +284,19 @@ __global__ __launch_bounds__(64) void k_pnp_hyp(const float* __restrict__ obj_al
             int i0, i1, j0, j1;
             double x00 = 0, x01 = 0, x10 = 0, x11 = 0, p0 = 0, q0 = 0, p1 = 0, q1 = 0;
             // the round's A block and the V entries (rows 2a, 2a + 1 at the block's columns)
+            int pk[11];  // the lane's round pairs, packed 4 bits each (rounds unrolled: static indices)
+#pragma unroll
+            for (int r = 0; r < 11; r++) {
+                int a0, a1, b0, b1;
+                rr_pair(12, r, ba, a0, a1);
+                rr_pair(12, r, bb, b0, b1);
+                pk[r] = a0 | a1 << 4 | b0 << 8 | b1 << 12;
+            }
             auto load_blk = [&](int r) {
-                rr_pair(12, r, ba, i0, i1);
-                rr_pair(12, r, bb, j0, j1);
+                i0 = pk[r] & 15;
+                i1 = (pk[r] >> 4) & 15;
+                j0 = (pk[r] >> 8) & 15;
+                j1 = pk[r] >> 12;
                 x00 = sA[i0 * 12 + j0];
                 x01 = sA[i0 * 12 + j1];
                 x10 = sA[i1 * 12 + j0];
@@ -297,6 +307,7 @@ __global__ __launch_bounds__(64) void k_pnp_hyp(const float* __restrict__ obj_al
                 q1 = sV[(2 * ba + 1) * 12 + j1];
             };
             if (blk) load_blk(0);
+#pragma unroll
             for (int r = 0; r < 11; r++) {
                 double c = 1.0, sn = 0.0;
                 int act = 0;
