@@ -47,8 +47,33 @@ __global__ __launch_bounds__(1024) void k_tlm_grid(const vs_keypoint* __restrict
         if (c >= 0) atomicAdd(&s_start[c + 1], 1);
     }
     __syncthreads();
-    if (tid == 0)
-        for (int c = 0; c < nc; c++) s_start[c + 1] += s_start[c];
+    // s_start[c + 1] += s_start[c] over the cells: every thread takes 4 consecutive cells, the
+    // threads' totals are scanned across the workgroup (integer sums: any order is exact)
+    __shared__ int s_wsum[16];
+    {
+        const int c0 = 4 * tid;
+        int v[4], run = 0;
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            v[k] = c0 + k < nc ? s_start[c0 + k + 1] : 0;
+            run += v[k];
+            v[k] = run;  // inclusive within the thread
+        }
+        const int lane = tid & 63, wv = tid >> 6;
+        int incl = run;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int y = __shfl_up(incl, o);
+            if (lane >= o) incl += y;
+        }
+        if (lane == 63) s_wsum[wv] = incl;
+        __syncthreads();
+        int before = incl - run;  // exclusive within the wave
+        for (int w = 0; w < wv; w++) before += s_wsum[w];
+#pragma unroll
+        for (int k = 0; k < 4; k++)
+            if (c0 + k < nc) s_start[c0 + k + 1] = before + v[k];
+    }
     __syncthreads();
     for (int ki = tid; ki < nkp; ki += blockDim.x) {
         const int c = s_cell[ki];
@@ -90,6 +115,21 @@ __global__ __launch_bounds__(256) void k_tlm_cand(const double* __restrict__ mp_
                                                   int GH, int img_w, int img_h, TlmPose T, int* __restrict__ cnt,
                                                   int* __restrict__ cand, int* __restrict__ work,
                                                   int* __restrict__ work_n) {
+    // the keypoint grid and the keypoint coordinates in LDS (one coalesced pass; every lookup of
+    // the candidate scan then stays on chip)
+    __shared__ int s_start[kTlmMaxCells + 1];
+    __shared__ int s_items[kTlmMaxKp];
+    __shared__ float2 s_xy[kTlmMaxKp];
+    const int nc = GW * GH;
+    for (int i = threadIdx.x; i <= nc; i += 256) s_start[i] = start[i];
+    __syncthreads();
+    const int nit = s_start[nc];
+    for (int i = threadIdx.x; i < nit; i += 256) {
+        const int ki = items[i];
+        s_items[i] = ki;
+        s_xy[ki] = make_float2(kps[ki].x, kps[ki].y);
+    }
+    __syncthreads();
     const int mp = blockIdx.x * 256 + threadIdx.x;
     const int lane = threadIdx.x & 63;
     int c = 0;
@@ -111,9 +151,9 @@ __global__ __launch_bounds__(256) void k_tlm_cand(const double* __restrict__ mp_
                 for (int gy = gy0; gy <= gy1; gy++)
                     for (int gx = gx0; gx <= gx1; gx++) {
                         const int cc = gy * GW + gx;
-                        for (int it = start[cc]; it < start[cc + 1]; it++) {
-                            const int ki = items[it];
-                            const double dx = u - (double)kps[ki].x, dy = v - (double)kps[ki].y;
+                        for (int it = s_start[cc]; it < s_start[cc + 1]; it++) {
+                            const int ki = s_items[it];
+                            const double dx = u - (double)s_xy[ki].x, dy = v - (double)s_xy[ki].y;
                             if (dx * dx + dy * dy > kTlmRadius * kTlmRadius) continue;
                             if (c < kTlmMaxCand) my[c] = ki;
                             c++;
@@ -126,9 +166,9 @@ __global__ __launch_bounds__(256) void k_tlm_cand(const double* __restrict__ mp_
                     for (int gy = gy0; gy <= gy1; gy++)
                         for (int gx = gx0; gx <= gx1; gx++) {
                             const int cc = gy * GW + gx;
-                            for (int it = start[cc]; it < start[cc + 1]; it++) {
-                                const int ki = items[it];
-                                const double dx = u - (double)kps[ki].x, dy = v - (double)kps[ki].y;
+                            for (int it = s_start[cc]; it < s_start[cc + 1]; it++) {
+                                const int ki = s_items[it];
+                                const double dx = u - (double)s_xy[ki].x, dy = v - (double)s_xy[ki].y;
                                 if (dx * dx + dy * dy > kTlmRadius * kTlmRadius) continue;
                                 const double d = desc_l2_dev(md, desc + (size_t)ki * 256);
                                 if (d < bd) {
