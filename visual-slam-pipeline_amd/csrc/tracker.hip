@@ -176,12 +176,14 @@ constexpr int kHdrWords = 4 + 624;
 constexpr size_t kHdrBytes = kHdrWords * sizeof(uint32_t);
 
 // Extraction chunks: the batch's network + post-processing runs chunk by chunk on the extraction
-// stream while the tracker consumes the chunks already done (process_batch_dev).  The first chunk
-// is small (nothing hides its latency) and the sizes grow by ~1.3x up to kXChunk (3, 4, 5, 7, 8, 5
-// at B = 32), about as fast as tracking a chunk outlasts extracting the next (A/B on one box:
-// 3 / 1.3x 1016, 2 / 1.2x 1011, 2 / 1.5x 991, 1 / 1.5x 959 frames/s).
-constexpr int kXChunk = 8;
-constexpr int kXFirst = 3;
+// streams while the tracker consumes the chunks already done (process_batch_dev).  Sizes grow from
+// the first chunk by VS_SLAM_CHUNK_GROWTH / 10 up to kXChunk.  Round 1 (tracking-bound, no
+// prefetch) wanted a small first chunk (3, 4, 5, 7, 8, 5 at B = 32); with the next batch prefetched
+// behind the current one and the tracker faster than the network, larger chunks win because the
+// network's small layers (60 x 80 conv4 / heads) fill the chip better (A/B on one box, 4 rounds:
+// 3 / 1.3x 1624, 5 / 1.5x 1629, 8 8 8 8 1688 frames/s).
+constexpr int kXChunk = 16;
+constexpr int kXFirst = 8;
 
 // The PnP input of Slam::refine_pose_via_local_pnp (tracked_points, :1408-1420) straight from the
 // local-map tracking result: keypoints (in order) whose map point is valid, as float object
