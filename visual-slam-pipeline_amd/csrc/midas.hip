@@ -282,13 +282,17 @@ constexpr int kCK = 16;  // input channels per K chunk
 constexpr int kAS = kCK + 4;  // LDS row stride of the pixel operand (floats)
 
 __global__ __launch_bounds__(256) void k_mid_conv(ConvArgs a) {
-    __shared__ float sA[kCT * kAS];   // [pixel][16 k] (k permuted for float4 fragments)
-    __shared__ float sB[kCT * kAS];   // [cout][16 k]
+    __shared__ float sA[2][kCT * kAS];  // [pixel][16 k] (k permuted for float4 fragments), double-buffered
+    __shared__ float sB[2][kCT * kAS];  // [cout][16 k]
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, li = lane & 15, lg = lane >> 4;
     const int npix = a.B * a.Ho * a.Wo;
     const int p0 = blockIdx.x * kCT, n0 = blockIdx.y * kCT;
-    // staging roles: 256 threads x 4 k each: pixel / cout row r = tid / 4, k quad q = tid % 4
+    // staging roles.  Pixel operand: pixel r = tid / 4 reads 4 consecutive channels (quad q = tid % 4),
+    // so 4 neighbouring threads cover 16 contiguous channels of one pixel.  Weight operand: cout
+    // co = tid % 64 for channel quad kq = tid / 64, so neighbouring threads read neighbouring couts
+    // of one [tap][channel] row (coalesced).
     const int r = tid >> 2, q = tid & 3;
+    const int co = tid & 63, kq = tid >> 6;
     const int gp = p0 + r;
     int b = 0, oy = 0, ox = 0;
     const bool pvalid = gp < npix;
@@ -298,6 +302,7 @@ __global__ __launch_bounds__(256) void k_mid_conv(ConvArgs a) {
         oy = rem / a.Wo;
         ox = rem - oy * a.Wo;
     }
+    const bool vec = (a.C & 3) == 0;
     const int wq = wv & 1, wt = wv >> 1;  // wave: pixels wq*32.., couts wt*32..
     f32x4 acc[2][2];
 #pragma unroll
@@ -305,48 +310,64 @@ __global__ __launch_bounds__(256) void k_mid_conv(ConvArgs a) {
 #pragma unroll
         for (int j = 0; j < 2; j++) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
     const int nchunk = (a.C + kCK - 1) / kCK;
-    for (int tap = 0; tap < a.k * a.k; tap++) {
+    const int T = a.k * a.k * nchunk;  // (tap, channel chunk) steps
+    float v[4], u[4];
+    // operands of step t into registers (global loads; issued one step ahead of their MFMAs)
+    auto fetch = [&](int t) {
+        const int tap = t / nchunk, ch = t - tap * nchunk;
         const int ky = tap / a.k, kx = tap - ky * a.k;
         const int iy = oy * a.stride - a.pad_t + ky, ix = ox * a.stride - a.pad_l + kx;
         const bool inb = pvalid && iy >= 0 && iy < a.H && ix >= 0 && ix < a.W;
         const float* src = a.in + (((size_t)b * a.H + (inb ? iy : 0)) * a.W + (inb ? ix : 0)) * a.C;
-        for (int ch = 0; ch < nchunk; ch++) {
-            const int c0 = ch * kCK + 4 * q;
-            // pixel operand: 4 consecutive input channels of this tap
-            float v[4];
+        const int c0 = ch * kCK + 4 * q;
+        if (vec) {
+            const float4 t4 = (inb && c0 < a.C) ? *reinterpret_cast<const float4*>(src + c0) : make_float4(0.f, 0.f, 0.f, 0.f);
+            v[0] = t4.x;
+            v[1] = t4.y;
+            v[2] = t4.z;
+            v[3] = t4.w;
+        } else {
 #pragma unroll
-            for (int j = 0; j < 4; j++) {
-                const float t = (inb && c0 + j < a.C) ? src[c0 + j] : 0.f;
-                v[j] = a.pre_relu ? (t > 0.f ? t : 0.f) : t;
-            }
-            // weight operand: cout n0 + r, the same 4 channels
-            const int co = n0 + r;
-            float u[4];
-#pragma unroll
-            for (int j = 0; j < 4; j++)
-                u[j] = (c0 + j < a.C) ? a.w[((size_t)tap * a.C + c0 + j) * a.CoP + co] : 0.f;
-            __syncthreads();
-            // k = 4 q + j -> position 4 j + q (a lane group g reads k = g, 4 + g, 8 + g, 12 + g)
-#pragma unroll
-            for (int j = 0; j < 4; j++) {
-                sA[r * kAS + 4 * j + q] = v[j];
-                sB[r * kAS + 4 * j + q] = u[j];
-            }
-            __syncthreads();
-            float4 fa[2], fb[2];
-#pragma unroll
-            for (int i = 0; i < 2; i++) {
-                fa[i] = *reinterpret_cast<const float4*>(&sA[(wq * 32 + 16 * i + li) * kAS + 4 * lg]);
-                fb[i] = *reinterpret_cast<const float4*>(&sB[(wt * 32 + 16 * i + li) * kAS + 4 * lg]);
-            }
-#pragma unroll
-            for (int j = 0; j < 4; j++)
-#pragma unroll
-                for (int i = 0; i < 2; i++)
-#pragma unroll
-                    for (int m = 0; m < 2; m++)
-                        acc[i][m] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[i][j], fb[m][j], acc[i][m], 0, 0, 0);
+            for (int j = 0; j < 4; j++) v[j] = (inb && c0 + j < a.C) ? src[c0 + j] : 0.f;
         }
+        if (a.pre_relu)
+#pragma unroll
+            for (int j = 0; j < 4; j++) v[j] = v[j] > 0.f ? v[j] : 0.f;
+        const int cw = ch * kCK + 4 * kq;
+#pragma unroll
+        for (int j = 0; j < 4; j++) u[j] = (cw + j < a.C) ? a.w[((size_t)tap * a.C + cw + j) * a.CoP + n0 + co] : 0.f;
+    };
+    // k = 4 q + j -> position 4 j + q (a lane group g reads k = g, 4 + g, 8 + g, 12 + g)
+    auto stage = [&](int buf) {
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            sA[buf][r * kAS + 4 * j + q] = v[j];
+            sB[buf][co * kAS + 4 * j + kq] = u[j];
+        }
+    };
+    fetch(0);
+    stage(0);
+    __syncthreads();
+    for (int t = 0; t < T; t++) {
+        const int cur = t & 1;
+        if (t + 1 < T) fetch(t + 1);
+        float4 fa[2], fb[2];
+#pragma unroll
+        for (int i = 0; i < 2; i++) {
+            fa[i] = *reinterpret_cast<const float4*>(&sA[cur][(wq * 32 + 16 * i + li) * kAS + 4 * lg]);
+            fb[i] = *reinterpret_cast<const float4*>(&sB[cur][(wt * 32 + 16 * i + li) * kAS + 4 * lg]);
+        }
+#pragma unroll
+        for (int j = 0; j < 4; j++)
+#pragma unroll
+            for (int i = 0; i < 2; i++)
+#pragma unroll
+                for (int m = 0; m < 2; m++)
+                    acc[i][m] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[i][j], fb[m][j], acc[i][m], 0, 0, 0);
+        // the other buffer was last read in step t - 1, which every wave finished before the
+        // barrier that ended it
+        if (t + 1 < T) stage(cur ^ 1);
+        __syncthreads();
     }
     // D[pixel 4 lg + e][cout li] of fragment (i, m)
 #pragma unroll
