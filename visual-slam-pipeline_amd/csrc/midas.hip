@@ -390,6 +390,26 @@ __global__ __launch_bounds__(256) void k_mid_conv(ConvArgs a) {
         }
 }
 
+// 1 x 1 convolution to a single output channel (the head's last layer, 32 -> 1 at the full
+// 256 x 256): one thread per pixel, a plain dot product over the channels.  On the implicit GEMM it
+// would occupy a 64-wide output tile for one channel (63/64 of the MFMA work padding).
+__global__ __launch_bounds__(256) void k_mid_conv_co1(ConvArgs a) {
+    const int p = blockIdx.x * 256 + threadIdx.x;
+    const int npix = a.B * a.Ho * a.Wo;
+    if (p >= npix) return;
+    const float* src = a.in + (size_t)p * a.C;
+    float s = 0.f;
+    for (int c = 0; c < a.C; c++) {
+        float t = src[c];
+        if (a.pre_relu) t = t > 0.f ? t : 0.f;
+        s = fmaf(t, a.w[(size_t)c * a.CoP], s);
+    }
+    float v = activate(s + (a.bias ? a.bias[0] : 0.f), a.act);
+    if (a.res1) v = v + a.res1[p];
+    if (a.res2) v = a.res2[p] + v;
+    a.out[p] = v;
+}
+
 // Depthwise k x k, stride s, TF-same padding, bias + ReLU6; one thread per (pixel, 4 channels).
 __global__ __launch_bounds__(256) void k_mid_dw(const float* __restrict__ in, const float* __restrict__ w,
                                                 const float* __restrict__ bias, float* __restrict__ out, int B, int H,
@@ -679,7 +699,10 @@ static int forward(vs_midas* m, int B, hipStream_t s, float** out) {
             a.CoP = m->dev[st.layer].cop, a.k = st.k, a.stride = st.stride, a.pad_t = st.pad_t, a.pad_l = st.pad_l;
             a.act = st.act, a.pre_relu = st.pre_relu;
             const int npix = B * st.Ho * st.Wo;
-            hipLaunchKernelGGL(k_mid_conv, dim3((npix + kCT - 1) / kCT, a.CoP / kCT), dim3(256), 0, s, a);
+            if (st.Co == 1 && st.k == 1 && st.stride == 1)
+                hipLaunchKernelGGL(k_mid_conv_co1, dim3((npix + 255) / 256), dim3(256), 0, s, a);
+            else
+                hipLaunchKernelGGL(k_mid_conv, dim3((npix + kCT - 1) / kCT, a.CoP / kCT), dim3(256), 0, s, a);
         } else if (st.kind == K_DW) {
             const long n = (long)B * st.Ho * st.Wo * (st.C / 4);
             hipLaunchKernelGGL(k_mid_dw, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, tensor_ptr(m, st.in),
