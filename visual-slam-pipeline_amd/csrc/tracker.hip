@@ -343,13 +343,18 @@ struct GpuOps {
         // extraction set (default 0: it shares the tracking CUs)
         const char* senv = std::getenv("VS_SLAM_SPEC_CUS");
         const int scu = senv ? std::max(0, std::atoi(senv)) : 0;
+        // VS_SLAM_POST_CUS > 0: the extraction post-processing (xp) gets CUs of its own, taken from
+        // the network's set (default 0: it shares the network's CUs)
+        const char* penv = std::getenv("VS_SLAM_POST_CUS");
+        const int pcu = penv ? std::max(0, std::atoi(penv)) : 0;
         bool masked = false;
-        if (tcu > 0 && ncu >= 2 * (tcu + scu)) {
+        if (tcu > 0 && ncu >= 2 * (tcu + scu + pcu)) {
             const int words = (ncu + 31) / 32;
-            std::vector<uint32_t> tm(words, 0u), xm(words, 0u), sm(words, 0u);
+            std::vector<uint32_t> tm(words, 0u), xm(words, 0u), sm(words, 0u), pm(words, 0u);
             for (int cu = 0; cu < ncu; cu++)
-                (cu < tcu ? tm : cu < tcu + scu ? sm : xm)[cu / 32] |= 1u << (cu % 32);
+                (cu < tcu ? tm : cu < tcu + scu ? sm : cu < tcu + scu + pcu ? pm : xm)[cu / 32] |= 1u << (cu % 32);
             if (scu == 0) sm = tm;
+            if (pcu == 0) pm = xm;
             masked = hipExtStreamCreateWithCUMask(&s, words, tm.data()) == hipSuccess;
             if (masked && hipExtStreamCreateWithCUMask(&xs, words, xm.data()) != hipSuccess) {
                 (void)hipStreamDestroy(s);
@@ -362,7 +367,7 @@ struct GpuOps {
                 s = xs = nullptr;
                 masked = false;
             }
-            if (masked && hipExtStreamCreateWithCUMask(&xp, words, xm.data()) != hipSuccess) {
+            if (masked && hipExtStreamCreateWithCUMask(&xp, words, pm.data()) != hipSuccess) {
                 (void)hipStreamDestroy(s);
                 (void)hipStreamDestroy(xs);
                 (void)hipStreamDestroy(s2);
@@ -903,8 +908,16 @@ struct GpuOps {
         if (failed(sync_valid(m))) return 0;
         int obs_cap = std::max(4 * nkp, 64);
         for (int attempt = 0; attempt < 2; attempt++) {
+            // one device block, read back with ONE copy: [tracking words | speculative PnP io + result]
             const int words = 2 + nkp + 2 * obs_cap;
-            if (failed(work.ensure((size_t)words * sizeof(int)))) return 0;
+            const size_t wbytes = ((size_t)words * sizeof(int) + 255) & ~(size_t)255;
+            spec_valid = false;
+            const int cap = std::max(nkp, 1);
+            const size_t io_bytes = 16 + (size_t)cap * 5 * sizeof(float), io_pad = (io_bytes + 15) & ~(size_t)15;
+            const size_t spec_bytes = io_pad + 12 * sizeof(double) + 8 * sizeof(int);
+            const bool spec_on = nkp > 0 && nkp <= 1024;
+            const size_t total = wbytes + (spec_on ? spec_bytes + (size_t)cap : 0);
+            if (failed(work.ensure(total))) return 0;
             int* d = work.as<int>();
             int* d_kpmp = d + 2;
             int* d_obs = d + 2 + nkp;
@@ -917,27 +930,23 @@ struct GpuOps {
                 return 0;
             // Speculatively, the refinement's PnP on the tracked points right behind it (the
             // tracker calls solve_pnp on exactly these next, Slam.cpp:1057-1059; solve_pnp checks).
-            spec_valid = false;
-            const int cap = std::max(nkp, 1);
-            const size_t io_bytes = 16 + (size_t)cap * 5 * sizeof(float), io_pad = (io_bytes + 15) & ~(size_t)15;
-            const size_t spec_bytes = io_pad + 12 * sizeof(double) + 8 * sizeof(int);
-            char* hs = nullptr;
-            if (nkp > 0 && nkp <= 1024 && pnp_io.ensure(spec_bytes + (size_t)cap) == VS_OK) {
-                char* io = pnp_io.as<char>();
+            bool spec_run = false;
+            if (spec_on) {
+                char* io = work.as<char>() + wbytes;
                 hipLaunchKernelGGL(k_pnp_gather, dim3(1), dim3(1024), 0, s, d_kpmp, nkp, map_pos.as<double>(),
                                    map_valid.as<uint8_t>(), m.size(), kps_of(f.slot), cap, reinterpret_cast<float*>(io));
                 double* dRt = reinterpret_cast<double*>(io + io_pad);
                 int* dstat = reinterpret_cast<int*>(dRt + 12);
-                if (vs::solve_pnp(ctx, 1, reinterpret_cast<const float*>(io + 16),
-                                  reinterpret_cast<const float*>(io + 16 + (size_t)cap * 3 * sizeof(float)),
-                                  reinterpret_cast<const int*>(io), K, 100, 10, dRt, dRt + 9, dstat,
-                                  reinterpret_cast<uint8_t*>(dstat + 8), s) == VS_OK) {
-                    hs = take(spec_bytes);
-                    if (hs && failed(d2h(hs, io, spec_bytes))) hs = nullptr;
-                }
+                spec_run = vs::solve_pnp(ctx, 1, reinterpret_cast<const float*>(io + 16),
+                                         reinterpret_cast<const float*>(io + 16 + (size_t)cap * 3 * sizeof(float)),
+                                         reinterpret_cast<const int*>(io), K, 100, 10, dRt, dRt + 9, dstat,
+                                         reinterpret_cast<uint8_t*>(dstat + 8), s) == VS_OK;
             }
-            int* hb = reinterpret_cast<int*>(take((size_t)words * sizeof(int)));
-            if (!hb || failed(d2h(hb, d, (size_t)words * sizeof(int)))) return 0;
+            const size_t rb = wbytes + (spec_run ? spec_bytes : 0);
+            char* hall = take(rb);
+            if (!hall || failed(d2h(hall, work.p, rb))) return 0;
+            int* hb = reinterpret_cast<int*>(hall);
+            char* hs = spec_run ? hall + wbytes : nullptr;
             flush_spec();  // the next frame's chain, launched while these kernels run
             if (failed(sync())) return 0;
             if (hs) {
