@@ -15,6 +15,10 @@
 // match, the visibility sweep and the map appends.  Everything runs on the context's stream.
 #include <hip/hip_runtime.h>
 
+#include <condition_variable>
+#include <functional>
+#include <thread>
+
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -248,8 +252,76 @@ struct HostTimer {
     }
 };
 
+// One helper thread that enqueues the NEXT batch's extraction (≈ 200 HIP calls: per chunk the
+// network layers, post-processing, copies and events) while the caller's thread goes on tracking
+// the current batch.  One task at a time; join() waits for it and hands its error over.
+struct AsyncEnqueue {
+    std::thread th;
+    std::mutex mu;
+    std::condition_variable cv;
+    std::function<int()> task;
+    bool has_task = false, busy = false, quit = false;
+    int rc = VS_OK;
+    std::string err;
+    void start(int device) {
+        th = std::thread([this, device] {
+            (void)hipSetDevice(device);
+            for (;;) {
+                std::function<int()> t;
+                {
+                    std::unique_lock<std::mutex> lk(mu);
+                    cv.wait(lk, [&] { return has_task || quit; });
+                    if (!has_task) return;
+                    t = std::move(task);
+                    has_task = false;
+                    busy = true;
+                }
+                const int r = t();
+                const std::string e = r != VS_OK ? std::string(vs_last_error()) : std::string();
+                {
+                    std::lock_guard<std::mutex> lk(mu);
+                    if (r != VS_OK && rc == VS_OK) {
+                        rc = r;
+                        err = e;
+                    }
+                    busy = false;
+                }
+                cv.notify_all();
+            }
+        });
+    }
+    void submit(std::function<int()> f) {
+        {
+            std::lock_guard<std::mutex> lk(mu);
+            task = std::move(f);
+            has_task = true;
+        }
+        cv.notify_all();
+    }
+    int join() {
+        std::unique_lock<std::mutex> lk(mu);
+        cv.wait(lk, [&] { return !has_task && !busy; });
+        const int r = rc;
+        rc = VS_OK;
+        if (r != VS_OK) set_error("vs_slam: next-batch extraction: " + err);
+        return r;
+    }
+    void stop() {
+        if (!th.joinable()) return;
+        (void)join();
+        {
+            std::lock_guard<std::mutex> lk(mu);
+            quit = true;
+        }
+        cv.notify_all();
+        th.join();
+    }
+};
+
 struct GpuOps {
     vs_ctx* ctx = nullptr;
+    AsyncEnqueue aq;
+    bool async_enqueue = true;  // VS_SLAM_ASYNC_ENQUEUE=0: enqueue the next batch on the caller's thread
     HostProf hprof;
     bool hprof_armed = false;
     // speculative PnP of the tracked points, run right behind local-map tracking (see solve_pnp)
@@ -387,6 +459,7 @@ struct GpuOps {
         return VS_OK;
     }
     void destroy_streams() {
+        aq.stop();  // no enqueue may still be running when the streams go
         if (!own_streams) return;
         (void)hipStreamSynchronize(xs);
         (void)hipStreamSynchronize(xp);
@@ -410,6 +483,8 @@ struct GpuOps {
     int init(vs_ctx* c, int max_batch, int hh, int ww) {
         ctx = c;
         VS_CHECK(make_streams());
+        if (const char* e = std::getenv("VS_SLAM_ASYNC_ENQUEUE")) async_enqueue = e[0] != '0';
+        if (async_enqueue) aq.start(ctx->device);
         if (const char* fc = std::getenv("VS_SLAM_FIRST_CHUNK")) first_chunk = std::max(1, std::min(kXChunk, std::atoi(fc)));
         if (const char* g = std::getenv("VS_SLAM_CHUNK_GROWTH")) chunk_growth = std::max(10, std::min(40, std::atoi(g)));
         const char* hp = std::getenv("VS_SLAM_HOST_PROFILE");
@@ -621,6 +696,7 @@ struct GpuOps {
     // hinted next batch is prefetched behind it into the other region (free: the previous batch's
     // live frames moved to persistent slots when it settled).
     int extract_batch(std::vector<vs_trk::FramePtr>& frames, const uint8_t* d_bgr, const float* d_depth) {
+        VS_CHECK(aq.join());  // the previous call's prefetch enqueue has finished touching xs / xp / xb
         const int nb = (int)frames.size();
         XBatch& P = xb[xcur ^ 1];
         if (P.pending && !(P.bgr == d_bgr && P.depth == d_depth && P.nb == nb)) {
@@ -639,9 +715,15 @@ struct GpuOps {
         for (int b = 0; b < nb; b++) frames[b]->slot = X.region * B + b;
         if (hint.nb > 0) {
             XBatch& N = xb[xcur ^ 1];
-            VS_CHECK(enqueue_extraction(N, hint.nb, hint.bgr, hint.depth));
             N.pending = true;
+            const int hnb = hint.nb;
+            const uint8_t* hb = hint.bgr;
+            const float* hd = hint.depth;
             hint.nb = 0;
+            if (async_enqueue)
+                aq.submit([this, &N, hnb, hb, hd] { return enqueue_extraction(N, hnb, hb, hd); });
+            else
+                VS_CHECK(enqueue_extraction(N, hnb, hb, hd));
         }
         return VS_OK;
     }
@@ -1475,6 +1557,7 @@ int vs_slam_process_batch_dev(vs_slam* sl, int B, const uint8_t* d_bgr, const fl
     o.cspec.valid = false;
     o.spec_req.pending = false;
     if (rc != VS_OK) {
+        (void)o.aq.join();
         (void)hipStreamSynchronize(o.xs);  // nothing may still write the pool after an error
         (void)hipStreamSynchronize(o.xp);
         (void)hipStreamSynchronize(o.s2);

@@ -65,6 +65,7 @@ static hipEvent_t take_event(vs_ctx* c) {
 
 ProfScope::ProfScope(vs_ctx* c, const char* name, hipStream_t st) : ctx(c), stage(-1), s(st) {
     if (!ctx->prof_on) return;
+    std::lock_guard<std::mutex> lk(ctx->prof_mu);
     for (size_t i = 0; i < ctx->prof.size(); i++)
         if (std::strcmp(ctx->prof[i].name, name) == 0) stage = (int)i;
     if (stage < 0) {
@@ -78,6 +79,7 @@ ProfScope::ProfScope(vs_ctx* c, const char* name, hipStream_t st) : ctx(c), stag
 
 ProfScope::~ProfScope() {
     if (!ctx->prof_on || stage < 0 || !e0 || !e1) return;
+    std::lock_guard<std::mutex> lk(ctx->prof_mu);
     (void)hipEventRecord(e1, s);
     ctx->prof[stage].pending.emplace_back(e0, e1);
     ctx->prof[stage].launches++;
@@ -807,6 +809,7 @@ int vs_profile_enable(vs_ctx* ctx, int on) {
 }
 
 static int drain_profile(vs_ctx* ctx) {
+    std::lock_guard<std::mutex> lk(ctx->prof_mu);
     for (auto& st : ctx->prof) {
         for (auto& pr : st.pending) {
             VS_HIP(hipEventSynchronize(pr.second));

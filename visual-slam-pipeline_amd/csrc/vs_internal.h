@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -97,6 +98,7 @@ struct vs_ctx {
     bool prof_on = false;
     std::vector<vs::ProfStage> prof;
     std::vector<hipEvent_t> event_pool;
+    std::mutex prof_mu;  // a vs_slam enqueues its next batch's extraction from a helper thread
 };
 
 namespace vs {
