@@ -332,13 +332,15 @@ __global__ __launch_bounds__(256, (KS == 3 && CKV == 32) ? 1 : 2) void k_conv_mf
 // 8 x 32 block, so no MFMA row is spent on columns past the image edge (8 x 32 tiles waste 22% of
 // the grid at W = 80).  The LDS patch holds the rows those pixels span plus the halo, full width
 // (tiles_y = patch rows, <= 640 patch pixels), and every lane addresses its own pixel in it.
-template <bool POOL, int LAYER, bool FUSE1A, bool LIN = false>
-__global__ __launch_bounds__(256, 2) void k_conv3_db(
+template <bool POOL, int LAYER, bool FUSE1A, bool LIN = false, int CKT = 8>
+__global__ __launch_bounds__(256, CKT == 4 ? 3 : 2) void k_conv3_db(
     const float* __restrict__ in, int in_cstride, int in_coff, const float* __restrict__ wt,
     const float* __restrict__ bias, int cin, int cout, int cout_pad, float* __restrict__ out,
     int out_cstride, int out_coff, int B, int H, int W, int tiles_x, int tiles_y, int relu,
     const float* __restrict__ w1a, const float* __restrict__ b1a) {
-    constexpr int CK = 8, TW = 32, TH = 8, PW = TW + 2, PH = TH + 2, NPIX = PW * PH;
+    // CKT input channels per chunk: 8 (two workgroups per CU), or 4 (about half the LDS, three
+    // workgroups per CU, twice the chunk barriers)
+    constexpr int CK = CKT, TW = 32, TH = 8, PW = TW + 2, PH = TH + 2, NPIX = PW * PH;
     constexpr int NPIXC = LIN ? 640 : NPIX;         // patch capacity
     constexpr int Q = CK / 4;                       // float4 per pixel and chunk
     constexpr int NQ = (NPIXC * Q + 255) / 256;     // input float4 per thread
@@ -690,9 +692,22 @@ int conv3(vs_ctx* ctx, const DevLayer& L, const float* in, int in_cstride, int i
     }
     const int tiles_x = (W + 31) / 32, tiles_y = (H + 7) / 8;
     dim3 grid((unsigned)(B * tiles_x * tiles_y * (L.cout_pad / 64)));
-    hipLaunchKernelGGL((k_conv3_db<POOL, LAYER, FUSE1A>), grid, dim3(256), 0, s, in, in_cstride, in_coff, L.w, L.b,
-                       L.cin, L.cout, L.cout_pad, out, out_cstride, out_coff, B, H, W, tiles_x, tiles_y, 1,
-                       L1a ? L1a->w : nullptr, L1a ? L1a->b : nullptr);
+    // The fused conv1 runs with 4-channel chunks: three workgroups per CU instead of two (35 KB of
+    // LDS, 145 VGPRs) hide its chunk barriers and prologue better (same-box A/B over 5 + 3 runs: conv1
+    // 97.6-99.5 -> 102.4-103.1 TFLOP/s, 0.63 -> 0.65-0.66 of the whole-chip fp32 MFMA peak; end to end
+    // equal).  VS_CONV1_CK=8 restores 8-channel chunks.
+    static const int ck = [] {
+        const char* e = std::getenv("VS_CONV1_CK");
+        return e ? std::atoi(e) : 4;
+    }();
+    if (FUSE1A && ck == 4)
+        hipLaunchKernelGGL((k_conv3_db<POOL, LAYER, FUSE1A, false, 4>), grid, dim3(256), 0, s, in, in_cstride, in_coff,
+                           L.w, L.b, L.cin, L.cout, L.cout_pad, out, out_cstride, out_coff, B, H, W, tiles_x, tiles_y,
+                           1, L1a ? L1a->w : nullptr, L1a ? L1a->b : nullptr);
+    else
+        hipLaunchKernelGGL((k_conv3_db<POOL, LAYER, FUSE1A>), grid, dim3(256), 0, s, in, in_cstride, in_coff, L.w, L.b,
+                           L.cin, L.cout, L.cout_pad, out, out_cstride, out_coff, B, H, W, tiles_x, tiles_y, 1,
+                           L1a ? L1a->w : nullptr, L1a ? L1a->b : nullptr);
     VS_HIP(hipGetLastError());
     return VS_OK;
     }
