@@ -81,7 +81,7 @@ struct ConvGeom {
 // in LDS, so the 64-channel full-resolution conv1a activation never goes through HBM.  Patch
 // positions outside the image are conv1b's zero padding (0, not conv1a evaluated there).
 template <int KS, bool POOL, int LAYER, bool FUSE1A = false, int CKV = (KS == 3 ? 16 : 32)>
-__global__ __launch_bounds__(256, (KS == 3 && CKV == 32) ? 1 : 2) void k_conv_mfma(
+__global__ __launch_bounds__(256, (KS == 3 && CKV == 32) ? 1 : (CKV == 8 ? 3 : 2)) void k_conv_mfma(
     const float* __restrict__ in, int in_cstride, int in_coff, const float* __restrict__ wt,
     const float* __restrict__ bias, int cin, int cout, int cout_pad, float* __restrict__ out,
     int out_cstride, int out_coff, int B, int H, int W, int tiles_x, int tiles_y, int relu,
@@ -679,6 +679,16 @@ int conv3(vs_ctx* ctx, const DevLayer& L, const float* in, int in_cstride, int i
             VS_HIP(hipGetLastError());
             return VS_OK;
         }
+        // conv2a / conv2b / conv3a / conv3b: 8-channel chunks, three workgroups per CU (29 KB LDS, 146
+        // VGPRs) instead of 16-channel chunks at two (same-box A/B over 4 runs each: the four layers
+        // 0.1997 -> 0.1920 ms per frame).  VS_CONV_CK=16 restores 16-channel chunks.
+        static const int ck = [] {
+            const char* e = std::getenv("VS_CONV_CK");
+            return e ? std::atoi(e) : 8;
+        }();
+        if (ck == 8)
+            return launch_conv<3, POOL, LAYER, FUSE1A, 8>(L, in, in_cstride, in_coff, out, out_cstride, out_coff, B, H,
+                                                          W, 1, s, L1a);
         return launch_conv<3, POOL, LAYER, FUSE1A, 16>(L, in, in_cstride, in_coff, out, out_cstride, out_coff, B, H,
                                                        W, 1, s, L1a);
     } else {
