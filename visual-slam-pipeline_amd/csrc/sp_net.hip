@@ -673,9 +673,21 @@ int conv3(vs_ctx* ctx, const DevLayer& L, const float* in, int in_cstride, int i
             L.cout_pad % 64 == 0 && in_cstride % 4 == 0 && in_coff % 4 == 0) {
             const int tiles = (H * W + 255) / 256;
             dim3 grid((unsigned)(B * tiles * (L.cout_pad / 64)));
-            hipLaunchKernelGGL((k_conv3_db<false, LAYER, false, true>), grid, dim3(256), 0, s, in, in_cstride, in_coff,
-                               L.w, L.b, L.cin, L.cout, L.cout_pad, out, out_cstride, out_coff, B, H, W, tiles,
-                               lin_rows, 1, nullptr, nullptr);
+            // conv4a / conv4b / the fused head: 4-channel chunks, three workgroups per CU (39 KB LDS, 134
+            // VGPRs; same-box A/B over 3 runs each: the three layers 0.1051 -> 0.0993 ms per frame).
+            // VS_CONV_LIN_CK=8 restores 8-channel chunks.
+            static const int ck = [] {
+                const char* e = std::getenv("VS_CONV_LIN_CK");
+                return e ? std::atoi(e) : 4;
+            }();
+            if (ck == 4)
+                hipLaunchKernelGGL((k_conv3_db<false, LAYER, false, true, 4>), grid, dim3(256), 0, s, in, in_cstride,
+                                   in_coff, L.w, L.b, L.cin, L.cout, L.cout_pad, out, out_cstride, out_coff, B, H, W,
+                                   tiles, lin_rows, 1, nullptr, nullptr);
+            else
+                hipLaunchKernelGGL((k_conv3_db<false, LAYER, false, true>), grid, dim3(256), 0, s, in, in_cstride,
+                                   in_coff, L.w, L.b, L.cin, L.cout, L.cout_pad, out, out_cstride, out_coff, B, H, W,
+                                   tiles, lin_rows, 1, nullptr, nullptr);
             VS_HIP(hipGetLastError());
             return VS_OK;
         }
