@@ -81,7 +81,7 @@ struct ConvGeom {
 // in LDS, so the 64-channel full-resolution conv1a activation never goes through HBM.  Patch
 // positions outside the image are conv1b's zero padding (0, not conv1a evaluated there).
 template <int KS, bool POOL, int LAYER, bool FUSE1A = false, int CKV = (KS == 3 ? 16 : 32)>
-__global__ __launch_bounds__(256, (KS == 3 && CKV == 32) ? 1 : (CKV == 8 ? 3 : 2)) void k_conv_mfma(
+__global__ __launch_bounds__(256, (KS == 3 && CKV == 32) ? 1 : ((CKV == 8 || (KS == 1 && CKV == 16)) ? 3 : 2)) void k_conv_mfma(
     const float* __restrict__ in, int in_cstride, int in_coff, const float* __restrict__ wt,
     const float* __restrict__ bias, int cin, int cout, int cout_pad, float* __restrict__ out,
     int out_cstride, int out_coff, int B, int H, int W, int tiles_x, int tiles_y, int relu,
@@ -803,8 +803,20 @@ int sp_forward(vs_ctx* ctx, int B, const uint8_t* d_img, int channels, int h, in
     }
     {
         ProfScope ps(ctx, "head_b", s);  // convPb 256 -> 65 and convDb 256 -> 256 (1x1)
-        VS_CHECK((launch_conv<1, false, 9>(L[9], a0, 512, 0, semi_out, kSemiCh, 0, B, H, W, 0, s)));
-        VS_CHECK((launch_conv<1, false, 11>(L[11], a0, 512, 256, dgrid_out, kDescDim, 0, B, H, W, 0, s)));
+        // the 1x1 heads (convPb, convDb) with 16-channel chunks, three workgroups per CU (20 KB LDS, 130
+        // VGPRs; same-box A/B over 3 runs each: 0.0191-0.0206 -> 0.0162 ms per frame).
+        // VS_CONV1X1_CK=32 restores 32-channel chunks.
+        static const int ck1 = [] {
+            const char* e = std::getenv("VS_CONV1X1_CK");
+            return e ? std::atoi(e) : 16;
+        }();
+        if (ck1 == 16) {
+            VS_CHECK((launch_conv<1, false, 9, false, 16>(L[9], a0, 512, 0, semi_out, kSemiCh, 0, B, H, W, 0, s)));
+            VS_CHECK((launch_conv<1, false, 11, false, 16>(L[11], a0, 512, 256, dgrid_out, kDescDim, 0, B, H, W, 0, s)));
+        } else {
+            VS_CHECK((launch_conv<1, false, 9>(L[9], a0, 512, 0, semi_out, kSemiCh, 0, B, H, W, 0, s)));
+            VS_CHECK((launch_conv<1, false, 11>(L[11], a0, 512, 256, dgrid_out, kDescDim, 0, B, H, W, 0, s)));
+        }
     }
     {
         ProfScope ps(ctx, "desc_l2norm", s);
