@@ -51,6 +51,9 @@ sys.path.insert(0, os.path.join(ROOT, "visual-slam-pipeline_amd", "python"))
 METRIC = "frames/sec end-to-end on TUM 640x480 at 1/2/4/8 MI355X; ATE RMSE vs ref"
 H, W = 480, 640
 FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: dense fp32 (v_mfma_f32_32x32x2_f32) peak
+# conv1's minimum HBM traffic per frame: the fp32 gray input read once (480 x 640 x 4 B) and the
+# pooled 240 x 320 x 64 fp32 output written once
+CONV1_MIN_BYTES_PER_FRAME = 480 * 640 * 4 + 240 * 320 * 64 * 4
 LOOP_FRAMES = 126               # one lap of synth.loop_trajectory (0.3 m/s, 10 processed frames/s)
 T0 = 1311868164.0               # TUM-like timestamps, 0.1 s per processed frame (FRAME_STEP = 3)
 
@@ -67,32 +70,63 @@ LAYER_FLOPS = {
     "head_b": 2 * 60 * 80 * (65 + 256) * 256,
 }
 
-# profiling stage -> kernel symbol (as rocprofv3 reports it) of that stage's dominant launch
+# profiling stage -> symbol prefix (as rocprofv3 reports it) of that stage's dominant kernel; the
+# template argument list continues after the prefix (e.g. the chunk width: "<true, 1, true, false, 4>")
 STAGE_KERNEL = {
-    "conv1_fused": "vs::k_conv3_db<true, 1, true, false>",
-    "conv2a": "vs::k_conv_mfma<3, false, 2, false, 16>",
-    "conv2b_pool": "vs::k_conv_mfma<3, true, 3, false, 16>",
-    "conv3a": "vs::k_conv_mfma<3, false, 4, false, 16>",
-    "conv3b_pool": "vs::k_conv_mfma<3, true, 5, false, 16>",
-    "conv4a": "vs::k_conv3_db<false, 6, false, true>",
-    "conv4b": "vs::k_conv3_db<false, 7, false, true>",
-    "head_a": "vs::k_conv3_db<false, 8, false, true>",
-    "head_b": "vs::k_conv_mfma<1, false, 9, false, 32>",
+    "conv1_fused": "vs::k_conv3_db<true, 1, true, false",
+    "conv2a": "vs::k_conv_mfma<3, false, 2, false",
+    "conv2b_pool": "vs::k_conv_mfma<3, true, 3, false",
+    "conv3a": "vs::k_conv_mfma<3, false, 4, false",
+    "conv3b_pool": "vs::k_conv_mfma<3, true, 5, false",
+    "conv4a": "vs::k_conv3_db<false, 6, false, true",
+    "conv4b": "vs::k_conv3_db<false, 7, false, true",
+    "head_a": "vs::k_conv3_db<false, 8, false, true",
+    "head_b": "vs::k_conv_mfma<1, false, 9, false",
 }
 
 
-def pmc_traffic(kernel, batch):
-    """HBM bytes per launch of `kernel` from the committed PMC passes (profiles/pmc_traffic.json,
-    written by tools/summarize_profiles.py from rocprofv3 FETCH_SIZE / WRITE_SIZE runs at the same
-    batch), or None when no matching measurement exists."""
+def kernel_matches(name, prefix):
+    """rocprof kernel `name` is the kernel `prefix` names (the prefix ends inside the template list)."""
+    return name.startswith(prefix) and name[len(prefix):len(prefix) + 1] in (",", ">")
+
+
+def pmc_traffic(prefix):
+    """HBM bytes per FRAME of the kernel `prefix` names, from the committed PMC passes
+    (profiles/pmc_traffic.json, written by tools/summarize_profiles.py from rocprofv3 FETCH_SIZE /
+    WRITE_SIZE runs in which every launch of that kernel covered the same number of frames), or None."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         doc = json.load(open(path))
     except (OSError, ValueError):
-        return None, None
-    if doc.get("batch_frames") != batch or kernel not in doc.get("kernels", {}):
-        return None, None
-    return doc["kernels"][kernel]["hbm_bytes_per_launch"], doc.get("tag")
+        return None, None, None
+    fpl = doc.get("frames_per_launch")
+    for name, k in doc.get("kernels", {}).items():
+        if kernel_matches(name, prefix) and fpl:
+            return k["hbm_bytes_per_launch"] / fpl, doc.get("tag"), fpl
+    return None, None, None
+
+
+def launch_plan(gpus, environ, argv):
+    """--gpus N: ("run", None) when this process is one rank of an N-rank job (or N == 1);
+    ("spawn", cmd) when N > 1 and no launcher started us (WORLD_SIZE unset): the caller starts
+    torch.distributed.run with N ranks as a child process, before any GPU call, and relays its
+    output and exit code; ("error", msg) when WORLD_SIZE is set and differs from N."""
+    if gpus < 1:
+        return "error", f"--gpus must be >= 1 (got {gpus})"
+    ws = environ.get("WORLD_SIZE")
+    if ws is not None:
+        if int(ws) != gpus:
+            return "error", f"--gpus {gpus} but WORLD_SIZE={ws}: the launcher and the flag disagree"
+        return "run", None
+    if gpus == 1:
+        return "run", None
+    import socket
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + list(argv)
+    return "spawn", cmd
 
 
 def progress(msg):
@@ -128,6 +162,7 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--frontend-steps", type=int, default=6, help="timed steps of the config[3] batch front end")
     ap.add_argument("--no-frontend", action="store_true")
+    ap.add_argument("--ba-reps", type=int, default=5, help="timed calls of the config[2] local-BA window (0: skip)")
     ap.add_argument("--mono-steps", type=int, default=4, help="timed steps of the config[4] monocular HD stream")
     ap.add_argument("--render-workers", type=int, default=0,
                     help="processes rendering the synthetic sequence (0: min(16, cpus / ranks); 1 under rocprofv3 "
@@ -135,13 +170,22 @@ def parse():
     return ap.parse_args()
 
 
-def cpu_baseline(L, nframes):
+def cpu_baseline(L, nframes, ba=None):
     """The CPU restatement (oracle/, test infrastructure) on the first `nframes` frames of the same
     sequence: OpenMP SuperPoint + decode/NMS/sample, then the same tracking loop (host/tracker.hpp)
-    over the CPU stages."""
+    over the CPU stages; and, given the config[2] window `ba`, the CPU local BA on one thread."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle_py as oracle
     import vslam_abi
+    ba_cpu = None
+    if ba is not None:
+        R, t, P0, kf, pt, uv, iters = ba
+        t0 = time.perf_counter()
+        o = oracle.local_ba(R, t, P0, kf, pt, uv)
+        ms = (time.perf_counter() - t0) * 1e3
+        ba_cpu = {"ms_per_call": round(ms, 3), "ms_per_iteration": round(ms / max(int(o[5][0]), 1), 3), "threads": 1,
+                  "lm_iterations": int(o[5][0]), "same_lm_trajectory_as_gpu": int(o[5][0]) == iters,
+                  "kind": "port", "what": "oracle/orc_ba.cpp (the CPU restatement of Optimizer.cpp:187-599)"}
     threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
     threads = max(1, min(threads, 16, os.cpu_count() or 1))
     with vslam_abi.Context(0) as ctx:
@@ -164,6 +208,7 @@ def cpu_baseline(L, nframes):
     except (OSError, StopIteration):
         pass
     return {"value": nframes / dt, "unit": "frames/s", "cores": threads, "kind": "port", "cpu_model": model,
+            "local_ba": ba_cpu,
             "ms_per_frame": {"extract": round(t_ext / nframes * 1e3, 3), "track": round(t_trk / nframes * 1e3, 3),
                              **stages},
             "full_table": "profiles/r02_cpu_baseline.json (200 frames at 1, 4, 16 threads; tools/cpu_baseline.py)",
@@ -171,6 +216,48 @@ def cpu_baseline(L, nframes):
                       f"CPU restatement (OpenMP fp32 SuperPoint + decode/NMS/sample, then Slam::process_frame with "
                       f"exact 2-NN matching, F-RANSAC, 3D-3D RANSAC / E fallback, EKF, local-map tracking, PnP, "
                       f"keyframes), {threads} threads, {dt:.1f} s"}
+
+
+BA_WINDOW = dict(N=50, M=10000, seed=7, span=3, noise=1.0, pert=0.05)  # SURVEY.md 8(d) BA stress
+
+
+def ba_bytes_per_iteration(N, M, n_obs):
+    """Algorithmic HBM bytes of one local-BA LM iteration: per observation
+    the pixel + indices read (24 B) and its 6x3 pose-point block written (144 B); per point its
+    position read and written (48 B) and its 3x3 block + gradient (96 B); the 6N x 6N Schur system
+    written once and read once by the factorisation (16 B per entry)."""
+    return n_obs * (24 + 144) + M * (48 + 96) + (6 * N) ** 2 * 16
+
+
+def local_ba(ctx, reps):
+    """BASELINE config[2]: Optimizer::local_bundle_adjustment (Optimizer.cpp:187-599) on the 50-keyframe
+    / 10k-point stress window through vs_local_ba (host arrays in and out, as the reference's call)."""
+    import synth
+    w = BA_WINDOW
+    R, t, P, P0, kf, pt, uv = synth.ba_window(w["N"], w["M"], w["seed"], span=w["span"], noise=w["noise"],
+                                              pert=w["pert"])
+    g = ctx.local_ba(R, t, P0, kf, pt, uv)  # warm-up: code objects, scratch
+    ctx.profile(True)
+    ctx.profile_reset()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        g = ctx.local_ba(R, t, P0, kf, pt, uv)
+    ms = (time.perf_counter() - t0) / reps * 1e3
+    prof = ctx.profile_read()
+    ctx.profile(False)
+    iters = int(g[5][0])
+    bpi = ba_bytes_per_iteration(w["N"], w["M"], len(kf))
+    res = {"workload": "config[2] local-BA stress window: 50 keyframes / 10k map points / span 3, 1 px noise, 5 cm "
+                       "point perturbation (synth.ba_window seed 7), vs_local_ba (Schur complement, blocked "
+                       "Cholesky, LM control on the device)",
+           "observations": int(len(kf)), "lm_iterations": iters, "accepted_steps": int(g[5][1]),
+           "rms_before": round(g[3], 6), "rms_after": round(g[4], 6), "reps": reps,
+           "ms_per_call": round(ms, 3), "ms_per_iteration": round(ms / max(iters, 1), 4),
+           "roofline": {"bound": "latency (hbm reported)", "algorithmic_bytes_per_iteration": bpi,
+                        "achieved": round(bpi / (ms / max(iters, 1) / 1e3) / 1e9, 3), "peak": 8000.0,
+                        "unit": "GB/s", "frac": round(bpi / (ms / max(iters, 1) / 1e3) / 8e12, 6)},
+           "stage_ms_per_call": {k: round(v[0] / reps, 4) for k, v in prof.items()}}
+    return res, (R, t, P0, kf, pt, uv, iters)
 
 
 def frontend_batch(ctx, L, B, rank, world, steps, warmup):
@@ -330,6 +417,14 @@ def monocular_hd(ctx, B, rank, world, steps, warmup, workers):
 
 def main():
     args = parse()
+    mode, what = launch_plan(args.gpus, os.environ, sys.argv[1:])
+    if mode == "error":
+        print(f"bench.py: {what}", file=sys.stderr, flush=True)
+        sys.exit(2)
+    if mode == "spawn":  # no GPU has been touched in this process: the ranks are children
+        import subprocess
+        progress(f"launching {args.gpus} ranks: {' '.join(what)}")
+        sys.exit(subprocess.run(what).returncode)
     import torch
     import torch.distributed as dist
 
@@ -420,8 +515,8 @@ def main():
     conv = {k: v for k, v in prof.items() if k in LAYER_FLOPS}
     dom = max(conv, key=lambda k: conv[k][0])
     dom_ms, dom_launches = conv[dom]
-    # the tracker extracts each batch in chunks (2, 3, 5, 8, 8, 6 frames at B = 32) overlapped
-    # with tracking, so a launch covers frames_timed / launches frames on average
+    # the tracker extracts each batch in even chunks (8, 8, 8, 8 frames at B = 32, tracker.hip
+    # enqueue_extraction) overlapped with tracking: a launch covers frames_timed / launches frames
     avg_s = dom_ms / 1e3 / dom_launches
     frames_per_launch = frames_timed / dom_launches
     flops_per_launch = LAYER_FLOPS[dom] * frames_per_launch
@@ -429,9 +524,8 @@ def main():
     net_ms = sum(v[0] for k, v in prof.items() if k in LAYER_FLOPS)
     net_flops = sum(LAYER_FLOPS.values()) * frames_timed
     stage_ms = {k: round(v[0] / frames_timed, 4) for k, v in sorted(prof.items(), key=lambda kv: -kv[1][0])}
-    traffic, traffic_tag = pmc_traffic(STAGE_KERNEL.get(dom, ""), B)
-    if traffic is not None:  # PMC pass at B frames per launch -> bytes per average launch here
-        traffic = traffic / B * frames_per_launch
+    traffic_pf, traffic_tag, traffic_fpl = pmc_traffic(STAGE_KERNEL.get(dom, ""))
+    traffic = round(traffic_pf * frames_per_launch) if traffic_pf is not None else None
 
     track_cus = int(os.environ.get("VS_SLAM_TRACK_CUS", "32"))
     mroof = {"tracker": match_roofline(prof.get("match"), 1, track_cus,
@@ -453,11 +547,18 @@ def main():
     if args.mono_steps > 0:
         mono = monocular_hd(ctx, B, rank, world, args.mono_steps, 1, workers)
 
+    lba, lba_problem = None, None
+    if args.ba_reps > 0:
+        progress("config[2] local BA stress window")
+        lba, lba_problem = local_ba(ctx, args.ba_reps)
+
     if rank == 0:
         cpu = None
         if not args.no_cpu_baseline and world == 1:
             progress("cpu baseline")
-            cpu = cpu_baseline(L, args.cpu_frames)
+            cpu = cpu_baseline(L, args.cpu_frames, lba_problem)
+            if lba is not None and cpu.get("local_ba"):
+                lba["cpu_ms_per_call_1thread"] = cpu["local_ba"]["ms_per_call"]
         result = {
             "metric": METRIC,
             "value": round(value, 3),
@@ -495,9 +596,12 @@ def main():
                 "unit": "TFLOP/s",
                 "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4),
                 "traffic": traffic,
-                "traffic_unit": "HBM bytes per launch (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE of the B-frame "
-                                "PMC pass, per frame x frames per launch)",
+                "traffic_unit": "HBM bytes per launch (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE per frame, from a PMC "
+                                "pass whose launches all covered traffic_pmc_frames_per_launch frames, x frames per "
+                                "launch here)",
                 "traffic_source": f"profiles/{traffic_tag}_pmc_traffic.json" if traffic_tag else None,
+                "traffic_pmc_frames_per_launch": traffic_fpl,
+                "algorithmic_bytes_per_launch": round(CONV1_MIN_BYTES_PER_FRAME * frames_per_launch),
                 "avg_launch_ms": round(avg_s * 1e3, 4),
                 "frames_per_launch": round(frames_per_launch, 3),
                 "flops_per_launch": round(flops_per_launch),
@@ -509,6 +613,7 @@ def main():
             "stage_ms_per_frame": stage_ms,
             "frontend_batch": fe,
             "monocular_hd": mono,
+            "local_ba": lba,
             "cpu_baseline": cpu,
         }
         print(json.dumps(result), flush=True)

@@ -467,6 +467,15 @@ int vs_pgo_transform_points(vs_ctx* ctx, int N, const double* R_old, const doubl
  * as Optimizer.cpp:780-859 does.  *loop_edges = pose_graph_optimize's return value. */
 int vs_slam_run_posthoc_pgo(vs_slam* slam, int* loop_edges);
 
+/* ---- NMS tie accounting (FeatureExtractor.cpp:238-259: std::sort, unstable) ------------------
+ * Every post-processed frame on this context (vs_extract*, vs_postprocess*, a vs_slam's batches)
+ * adds to four totals: out = {frames, frames with a tie, window ties (output keypoints with an
+ * equal-score candidate inside their 9x9 window), cut ties (the 400th and 401st kept pixel score
+ * the same)}.  A frame with no tie gives the reference's keypoints for any order of equal scores,
+ * std::sort's included; the build breaks ties by raster index.  reset != 0 zeroes the totals.
+ * Synchronises the device. */
+int vs_nms_tie_stats(vs_ctx* ctx, long long out[4], int reset);
+
 /* ---- profiling ----------------------------------------------------------------------- */
 /* When enabled, every stage of the _dev pipelines brackets its launches with hipEvents on the
  * stream it runs on; vs_profile_read returns per-stage accumulated milliseconds and launch

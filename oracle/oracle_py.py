@@ -28,6 +28,7 @@ _SIG = {
     "orc_superpoint_forward": (_I, [_P, _P, _I, _I, _P, _P, _I]),
     "orc_decode_heatmap": (None, [_P, _I, _I, _P]),
     "orc_nms": (_I, [_P, _I, _I, _I, _I, ctypes.c_float, _I, _I, _I, _P, _P, _P]),
+    "orc_nms_ties": (None, [_P, _I, _I, ctypes.c_float, _I, _I, _P]),
     "orc_sample_descriptors": (None, [_P, _I, _I, _P, _I, _P]),
     "orc_postprocess": (_I, [_P, _P, _I, _I, _I, _I, _I, _I, _P, _P]),
     "orc_extract": (_I, [_P, _P, _I, _I, ctypes.c_size_t, _I, _I, _P, _P]),
@@ -145,6 +146,14 @@ def nms(heat, h=None, w=None, thr=0.005, radius=4, max_kp=400, order_mode=1):
     n = lib().orc_nms(_p(heat), hp, wp, h, w, thr, radius, max_kp, order_mode, _p(out), ctypes.byref(nc),
                       ctypes.byref(nt))
     return out[:n].copy(), nc.value, nt.value
+
+
+def nms_ties(heat, thr=0.005, radius=4, max_kp=400):
+    """(window ties, cut tie) of the heatmap's greedy NMS (orc_nms_ties)."""
+    heat = np.ascontiguousarray(heat, np.float32)
+    out = np.zeros(2, np.int32)
+    lib().orc_nms_ties(_p(heat), heat.shape[0], heat.shape[1], thr, radius, max_kp, _p(out))
+    return int(out[0]), int(out[1])
 
 
 def sample_descriptors(desc_grid, kps):

@@ -102,6 +102,48 @@ int orc_nms(const float* heatmap, int hp, int wp, int h, int w, float thr, int r
     return n;
 }
 
+// The ties that can make std::sort's output (FeatureExtractor.cpp:238-239, unstable) differ from
+// the raster-order tie break used here (sp_post.hip header): over the stable greedy's kept sequence
+// (uncapped), out[0] = selected pixels (the first min(max_kp, kept) of it) with an equal-score
+// candidate in their (2 radius + 1)^2 window, out[1] = 1 when the max_kp-th and the next kept pixel
+// score the same.  Both zero => every order of equal scores gives the same output.
+void orc_nms_ties(const float* heatmap, int hp, int wp, float thr, int radius, int max_kp, int* out) {
+    std::vector<Candidate> candidates;
+    for (int y = 0; y < hp; y++)
+        for (int x = 0; x < wp; x++) {
+            float val = heatmap[(size_t)y * wp + x];
+            if (val > thr) candidates.push_back({val, x, y});
+        }
+    std::stable_sort(candidates.begin(), candidates.end(),
+                     [](const Candidate& a, const Candidate& b) { return a.score > b.score; });
+    std::vector<uint8_t> suppressed((size_t)hp * wp, 0);
+    std::vector<Candidate> kept;
+    for (const auto& c : candidates) {
+        if (suppressed[(size_t)c.y * wp + c.x]) continue;
+        kept.push_back(c);
+        for (int dy = -radius; dy <= radius; dy++)
+            for (int dx = -radius; dx <= radius; dx++) {
+                int ny = c.y + dy, nx = c.x + dx;
+                if (ny >= 0 && ny < hp && nx >= 0 && nx < wp) suppressed[(size_t)ny * wp + nx] = 1;
+            }
+    }
+    const int K = std::min<int>(max_kp, (int)kept.size());
+    int window = 0;
+    for (int i = 0; i < K; i++) {
+        const Candidate& c = kept[i];
+        bool tie = false;
+        for (int dy = -radius; dy <= radius; dy++)
+            for (int dx = -radius; dx <= radius; dx++) {
+                int ny = c.y + dy, nx = c.x + dx;
+                if ((dx || dy) && ny >= 0 && ny < hp && nx >= 0 && nx < wp && heatmap[(size_t)ny * wp + nx] == c.score)
+                    tie = true;
+            }
+        window += tie;
+    }
+    out[0] = window;
+    out[1] = (K > 0 && (int)kept.size() > K && kept[K - 1].score == kept[K].score) ? 1 : 0;
+}
+
 // FeatureExtractor.cpp:167-206: bilinear sample of the coarse descriptor grid, expression
 // order kept, then sequential sum of squares, sqrtf, divide when norm > 1e-8f.
 void orc_sample_descriptors(const float* desc_data, int Hc, int Wc, const orc_keypoint* kps,

@@ -42,6 +42,59 @@ def greedy_nms(heat, thr=0.005, radius=4, max_kp=400, stable=True):
     return out
 
 
+def greedy_kept(heat, thr=0.005, radius=4, order=None):
+    """The greedy's whole kept sequence (no cap); `order` (optional) is a permutation of the
+    candidates' raster list used to break exact score ties (default: raster order)."""
+    H, W = heat.shape
+    ys, xs = np.nonzero(heat > np.float32(thr))
+    scores = heat[ys, xs]
+    tb = np.arange(len(ys)) if order is None else np.asarray(order)
+    seq = np.lexsort((tb, -scores))
+    sup = np.zeros((H, W), bool)
+    out = []
+    for i in seq:
+        y, x = ys[i], xs[i]
+        if sup[y, x]:
+            continue
+        out.append((int(x), int(y), float(scores[i])))
+        sup[max(0, y - radius):y + radius + 1, max(0, x - radius):x + radius + 1] = True
+    return out
+
+
+def nms_ties(heat, thr=0.005, radius=4, max_kp=400):
+    """(window ties, cut tie): selected keypoints with an equal-score candidate in their window,
+    and whether the max_kp-th and the next kept pixel score the same (sp_post.hip header)."""
+    H, W = heat.shape
+    kept = greedy_kept(heat, thr, radius)
+    K = min(max_kp, len(kept))
+    window = 0
+    for x, y, sc in kept[:K]:
+        win = heat[max(0, y - radius):y + radius + 1, max(0, x - radius):x + radius + 1]
+        window += int((win == np.float32(sc)).sum() > 1)
+    cut = int(0 < K < len(kept) and kept[K - 1][2] == kept[K][2])
+    return window, cut
+
+
+def nms_floor(heat, thr=0.005, radius=4, max_kp=400):
+    """The GPU's score floor (sp_post.hip k_nms_lmax / k_nms_floor): the max_kp-th largest score
+    among strict local maxima (every other candidate in the window scores lower), 0 with fewer."""
+    H, W = heat.shape
+    c = np.where(heat > np.float32(thr), heat, np.float32(0))
+    p = np.pad(c, radius)
+    mx = np.zeros_like(c)
+    eq = np.zeros((H, W), np.int32)
+    for dy in range(2 * radius + 1):
+        for dx in range(2 * radius + 1):
+            mx = np.maximum(mx, p[dy:dy + H, dx:dx + W])
+    for dy in range(2 * radius + 1):
+        for dx in range(2 * radius + 1):
+            eq += p[dy:dy + H, dx:dx + W] == c
+    lm = c[(c > 0) & (c == mx) & (eq == 1)]
+    if len(lm) < max_kp:
+        return np.float32(0)
+    return np.sort(lm)[::-1][max_kp - 1]
+
+
 def mis_rounds_nms(heat, thr=0.005, radius=4, max_kp=400):
     """The GPU's algorithm (sp_post.hip), in global Jacobi rounds over the dense heatmap:
     undecided -> kept when no undecided higher-priority pixel is in the window and no kept one,

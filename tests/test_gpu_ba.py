@@ -7,36 +7,15 @@ trajectory (iterations, accepted steps) must match exactly and poses / points / 
 import numpy as np
 import pytest
 
-import restate
+import synth
 from test_oracle_ba import ba_problem
 
 pytestmark = pytest.mark.gpu
 
 
 def windowed_problem(N, M, seed, span=5, noise=0.5, pert=0.03):
-    """Points visible from `span` consecutive keyframes (the sliding-window structure)."""
-    rng = np.random.default_rng(seed)
-    K = (525.0, 525.0, 319.5, 239.5)
-    Rs = np.array([restate.rodrigues(np.array([0.0, 0.03 * i, 0.0])) for i in range(N)])
-    ts = np.array([[0.2 * i, 0.0, 0.05 * i] for i in range(N)])
-    first = rng.integers(0, max(1, N - span + 1), M)
-    # place point j in front of keyframe first[j] + span // 2
-    kc = np.minimum(first + span // 2, N - 1)
-    pc = np.stack([rng.uniform(-1.5, 1.5, M), rng.uniform(-1.0, 1.0, M), rng.uniform(3.0, 6.0, M)], 1)
-    P = np.einsum("mij,mj->mi", Rs[kc], pc) + ts[kc]
-    kf, pt, uv = [], [], []
-    for i in range(N):
-        cam = (P - ts[i]) @ Rs[i]
-        u = K[0] * cam[:, 0] / cam[:, 2] + K[2]
-        v = K[1] * cam[:, 1] / cam[:, 2] + K[3]
-        vis = np.flatnonzero((first <= i) & (i < first + span) & (cam[:, 2] > 0.1) & (u > 0) & (u < 640) &
-                             (v > 0) & (v < 480))
-        for j in rng.permutation(vis):
-            kf.append(i)
-            pt.append(j)
-            uv.append([u[j] + rng.normal() * noise, v[j] + rng.normal() * noise])
-    P0 = P + rng.normal(size=P.shape) * pert
-    return Rs, ts, P, P0, np.array(kf, np.int32), np.array(pt, np.int32), np.array(uv)
+    """Points visible from `span` consecutive keyframes (the sliding-window structure; synth.ba_window)."""
+    return synth.ba_window(N, M, seed, span=span, noise=noise, pert=pert)
 
 
 def _compare(g, o):

@@ -377,3 +377,60 @@ def test_postprocess_round_cap_is_reported(vsctx, monkeypatch):
     monkeypatch.delenv("VS_NMS_FINISH_ROUNDS")
     kg, _ = vsctx.postprocess(semi_r, dg)
     assert np.array_equal(kps[1].cpu().numpy().view(np.uint8).reshape(-1)[:kg.nbytes], kg.view(np.uint8).reshape(-1))
+
+
+# ------------------------------------------ NMS ties vs the reference's std::sort
+def _tie_delta(ctx, before):
+    after = ctx.tie_stats()
+    return after["window_ties"] - before["window_ties"], after["cut_ties"] - before["cut_ties"]
+
+
+def test_nms_tie_counts_and_literal_std_sort(vsctx, oracle):
+    """SURVEY hard part (i).  For camera frames of the synthetic sequence and for tie-heavy
+    (quantised) heatmaps: the GPU's per-frame tie counts equal the oracle's (orc_nms_ties), and the
+    GPU keypoints are compared with the literal std::sort path of the oracle (order_mode=0, the
+    reference's unstable sort under libstdc++).  A frame whose keypoints differ from std::sort's
+    must carry a counted tie; the mismatch and tie counts are recorded in
+    gpurun_out/nms_literal_sort.json."""
+    import json
+    import os
+
+    import synth
+    seq = synth.loop_sequence(24, workers=8)
+    cases = [("camera", oracle.gray_to_f32(oracle.bgr_to_gray(img))) for img in seq["bgr"]]
+    rng = np.random.default_rng(21)
+    for q in (4, 16, 64):
+        semi = np.round(rng.standard_normal((65, 60, 80)).astype(np.float32) * 3 * q) / q
+        cases.append((f"quantised/{q}", semi.astype(np.float32)))
+    dg_q = _unit_grid(60, 80, 9)
+    rec = {"frames": 0, "mismatch_vs_std_sort": 0, "frames_with_tie": 0, "window_ties": 0, "cut_ties": 0,
+           "mismatch_without_tie": 0, "by_kind": {}}
+    for kind, x in cases:
+        if kind == "camera":
+            semi, dg = vsctx.superpoint_forward(x)
+        else:
+            semi, dg = x, dg_q
+        before = vsctx.tie_stats()
+        kg, _ = vsctx.postprocess(semi, dg)
+        w, c = _tie_delta(vsctx, before)
+        assert (w, c) == oracle.nms_ties(oracle.decode_heatmap(semi)), kind
+        ko_stable, _ = oracle.postprocess(semi, dg, order_mode=1)
+        assert _kp_equal(kg, ko_stable)
+        ko_lit, _ = oracle.postprocess(semi, dg, order_mode=0)
+        differ = not _kp_equal(kg, ko_lit)
+        rec["frames"] += 1
+        rec["mismatch_vs_std_sort"] += differ
+        rec["frames_with_tie"] += (w + c) > 0
+        rec["window_ties"] += w
+        rec["cut_ties"] += c
+        rec["mismatch_without_tie"] += differ and (w + c) == 0
+        k = rec["by_kind"].setdefault(kind.split("/")[0], {"frames": 0, "mismatch": 0, "tie_frames": 0})
+        k["frames"] += 1
+        k["mismatch"] += differ
+        k["tie_frames"] += (w + c) > 0
+    os.makedirs("gpurun_out", exist_ok=True)
+    with open(os.path.join("gpurun_out", "nms_literal_sort.json"), "w") as fh:
+        json.dump(rec, fh, indent=1)
+    print("nms literal std::sort:", rec)
+    assert rec["mismatch_without_tie"] == 0
+    assert rec["by_kind"]["quantised"]["tie_frames"] > 0  # the tie path is exercised

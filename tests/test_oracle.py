@@ -84,14 +84,67 @@ def test_parallel_mis_rounds_equal_sequential_greedy(oracle, seed, max_kp):
     assert rounds >= 1
 
 
-def test_nms_sort_order_only_matters_for_ties(oracle):
-    rng = np.random.default_rng(7)
-    heat = rng.random((64, 80), dtype=np.float32) * np.float32(0.05)
-    a, _, tied = oracle.nms(heat, order_mode=0)
-    b, _, _ = oracle.nms(heat, order_mode=1)
-    assert tied == 0 or True
-    if tied == 0:
-        assert _kp_tuples(a) == _kp_tuples(b)
+def _tie_heat(rng, h, w, levels, scale=0.05):
+    heat = rng.random((h, w), dtype=np.float32) * np.float32(scale)
+    if levels:
+        heat = (np.round(heat * levels) / levels).astype(np.float32)  # exact ties
+    return heat
+
+
+@pytest.mark.parametrize("seed", range(10))
+@pytest.mark.parametrize("max_kp", [400, 20])
+def test_nms_tie_stats_oracle_matches_numpy(oracle, seed, max_kp):
+    rng = np.random.default_rng(300 + seed)
+    heat = _tie_heat(rng, 40, 64, [0, 60, 400, 4000][seed % 4])
+    assert oracle.nms_ties(heat, max_kp=max_kp) == restate.nms_ties(heat, max_kp=max_kp)
+
+
+@pytest.mark.parametrize("seed", range(24))
+def test_nms_tie_free_frames_are_order_independent(oracle, seed):
+    """SURVEY hard part (i): the reference's std::sort is unstable.  When a frame has no window tie
+    and no cut tie, EVERY order of equal scores gives the same keypoints — the literal std::sort
+    (order_mode=0) and random tie orders included; a difference needs a counted tie."""
+    rng = np.random.default_rng(400 + seed)
+    max_kp = [400, 25, 60][seed % 3]
+    heat = _tie_heat(rng, 48, 64, [0, 40, 150, 2000][seed % 4], scale=[0.05, 0.02][seed % 2])
+    window, cut = oracle.nms_ties(heat, max_kp=max_kp)
+    stable = _kp_tuples(oracle.nms(heat, max_kp=max_kp, order_mode=1)[0])
+    lit = _kp_tuples(oracle.nms(heat, max_kp=max_kp, order_mode=0)[0])
+    n = int((heat > np.float32(0.005)).sum())
+    others = [restate.greedy_kept(heat, order=rng.permutation(n))[:max_kp] for _ in range(4)]
+    if window == 0 and cut == 0:
+        assert lit == stable and all(o == stable for o in others)
+    elif lit != stable or any(o != stable for o in others):
+        assert window + cut > 0
+
+
+def test_nms_ties_detected_when_they_decide(oracle):
+    # two equal scores side by side: which one is kept depends on the order -> a window tie
+    heat = np.zeros((20, 20), np.float32)
+    heat[5, 5] = heat[5, 7] = 0.5
+    assert oracle.nms_ties(heat) == (1, 0)
+    # the 2nd and 3rd kept pixel score the same with max_kp = 2 -> a cut tie
+    heat = np.zeros((20, 40), np.float32)
+    heat[2, 2], heat[2, 15], heat[2, 30] = 0.9, 0.5, 0.5
+    assert oracle.nms_ties(heat, max_kp=2) == (0, 1)
+    assert oracle.nms_ties(heat, max_kp=3) == (0, 0)
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_nms_score_floor_keeps_the_greedy_output(seed):
+    """The GPU prunes pixels below F = the max_kp-th largest strict-local-maximum score before the
+    MIS rounds (sp_post.hip): the greedy's top max_kp is unchanged, for dense and sparse heatmaps,
+    with exact ties, and at caps above the number of local maxima (no floor)."""
+    rng = np.random.default_rng(500 + seed)
+    max_kp = [400, 30, 5, 100][seed % 4]
+    heat = _tie_heat(rng, 64, 96, [0, 100, 0, 1000][seed % 4], scale=[0.03, 0.5, 0.01, 0.2][seed % 4])
+    if seed >= 8:  # sparse blobs (a camera frame's shape)
+        heat = np.where(rng.random(heat.shape) < 0.05, heat * 10, np.float32(0.001)).astype(np.float32)
+    F = restate.nms_floor(heat, max_kp=max_kp)
+    pruned = np.where(heat >= F, heat, np.float32(0)).astype(np.float32)
+    assert restate.greedy_nms(pruned, max_kp=max_kp) == restate.greedy_nms(heat, max_kp=max_kp)
+    if F > 0:
+        assert (heat >= F).sum() < (heat > np.float32(0.005)).sum()
 
 
 def test_nms_border_erase_and_empty(oracle):
@@ -214,3 +267,14 @@ def test_oracle_ransac_3d3d_failures(oracle):
     p1, p2, d1, d2, R, t, inl = restate.rigid_scene(60, 0.0, 10, trans=(0.3, 0.0, 0.0))
     ok, _, te, diag = oracle.ransac_3d3d(p1, p2, d1, d2)
     assert not ok and diag[3] == 60 and np.allclose(te, t, atol=1e-5)
+
+
+def test_nms_score_floor_full_frame_dense():
+    # a random-weight SuperPoint heatmap's shape: nearly every pixel a candidate, ~1/81 of them
+    # strict local maxima; the floor leaves a small fraction of the candidates undecided
+    rng = np.random.default_rng(77)
+    heat = (rng.random((240, 320), dtype=np.float32) * np.float32(0.03)).astype(np.float32)
+    F = restate.nms_floor(heat)
+    assert F > 0 and (heat >= F).sum() < 0.05 * (heat > np.float32(0.005)).sum()
+    pruned = np.where(heat >= F, heat, np.float32(0)).astype(np.float32)
+    assert restate.greedy_nms(pruned) == restate.greedy_nms(heat)

@@ -11,7 +11,7 @@
                                     (GRBM_GUI_ACTIVE is summed over the 8 XCDs; MI355X_MICROARCH.md)
   profiles/<tag>_match_kernel_stats.csv  kernel trace of tools/bench_match.py (1, 32, 512 pairs)
 
-usage: python tools/summarize_profiles.py r01 [batch]
+usage: python tools/summarize_profiles.py r03 [frames_per_launch (default 8, the tracker's chunk)]
 """
 import collections
 import csv
@@ -31,11 +31,21 @@ def short(name):
     return m.group(1) if m else name[:80]
 
 
-def per_kernel(path, counter):
-    agg = collections.defaultdict(list)
+def per_kernel(path, counter, grids=None):
+    """Mean counter value x 1024 per dispatch of each kernel (FETCH_SIZE / WRITE_SIZE are KB); the
+    distinct grid sizes of each kernel's dispatches go to `grids` (one size = one launch shape)."""
+    per_disp = collections.defaultdict(float)
+    names = {}
     for r in csv.DictReader(open(path)):
         if r["Counter_Name"] == counter:
-            agg[short(r["Kernel_Name"])].append(float(r["Counter_Value"]) * 1024.0)
+            d = r.get("Dispatch_Id") or str(len(names))
+            per_disp[d] += float(r["Counter_Value"]) * 1024.0
+            names[d] = short(r["Kernel_Name"])
+            if grids is not None and r.get("Grid_Size"):
+                grids.setdefault(names[d], set()).add(r["Grid_Size"])
+    agg = collections.defaultdict(list)
+    for d, v in per_disp.items():
+        agg[names[d]].append(v)
     return {k: sum(v) / len(v) for k, v in agg.items()}
 
 
@@ -68,12 +78,13 @@ def mfma_util(path, label):
 
 def main():
     tag = sys.argv[1]
-    batch = int(sys.argv[2]) if len(sys.argv) > 2 else 32
+    batch = int(sys.argv[2]) if len(sys.argv) > 2 else 8
     os.makedirs(PROF, exist_ok=True)
     shutil.copy(os.path.join(OUT, "prof_trace", "trace_kernel_stats.csv"),
                 os.path.join(PROF, f"{tag}_kernel_stats.csv"))
-    fetch = per_kernel(os.path.join(OUT, "prof_fetch", "fetch_counter_collection.csv"), "FETCH_SIZE")
-    write = per_kernel(os.path.join(OUT, "prof_write", "write_counter_collection.csv"), "WRITE_SIZE")
+    grids = {}
+    fetch = per_kernel(os.path.join(OUT, "prof_fetch", "fetch_counter_collection.csv"), "FETCH_SIZE", grids)
+    write = per_kernel(os.path.join(OUT, "prof_write", "write_counter_collection.csv"), "WRITE_SIZE", grids)
     stats = {}
     for r in csv.DictReader(open(os.path.join(OUT, "prof_trace", "trace_kernel_stats.csv"))):
         stats[short(r["Name"])] = float(r["AverageNs"])
@@ -82,9 +93,12 @@ def main():
         f = fetch.get(k, 0.0)
         w = write.get(k, 0.0)
         kernels[k] = {"fetch_bytes_raw": f, "fetch_bytes_corrected": 2.0 * f, "write_bytes": w,
-                      "hbm_bytes_per_launch": 2.0 * f + w, "avg_ns": stats.get(k)}
-    doc = {"tag": tag, "batch_frames": batch,
-           "note": "FETCH_SIZE x2 (gfx950 16-B/lane streaming-read correction), WRITE_SIZE as is; bytes per launch",
+                      "hbm_bytes_per_launch": 2.0 * f + w, "avg_ns": stats.get(k),
+                      "grid_sizes": sorted(grids.get(k, ()))}
+    doc = {"tag": tag, "frames_per_launch": batch,
+           "note": "FETCH_SIZE x2 (gfx950 16-B/lane streaming-read correction), WRITE_SIZE as is; bytes per launch. "
+                   "Taken from bench.py --no-frontend --mono-steps 0: every SuperPoint launch is one tracker "
+                   "extraction chunk of frames_per_launch frames (one grid size per network kernel)",
            "kernels": kernels}
     with open(os.path.join(PROF, f"{tag}_pmc_traffic.json"), "w") as fh:
         json.dump(doc, fh, indent=1)

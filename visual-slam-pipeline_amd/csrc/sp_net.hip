@@ -739,6 +739,7 @@ int conv3(vs_ctx* ctx, const DevLayer& L, const float* in, int in_cstride, int i
 
 int sp_forward(vs_ctx* ctx, int B, const uint8_t* d_img, int channels, int h, int w, hipStream_t s, float* semi_out,
                float* dgrid_out) {
+    VS_CHECK(scratch_order(ctx, s));
     const int Hp = ((h + 7) / 8) * 8, Wp = ((w + 7) / 8) * 8;
     const int hc = Hp / 8, wc = Wp / 8;
     const size_t full = (size_t)B * Hp * Wp;

@@ -16,6 +16,15 @@
 // greedy decisions never depend on lower-priority candidates, so the capped greedy output is the
 // top 400 of the uncapped set.
 //
+// Score floor (round 3).  A strict local maximum (every other candidate of its window scores
+// lower) is kept by the greedy whatever else happens.  So when a frame has at least 400 of them,
+// the 400th kept pixel scores at least the 400th-largest strict-local-maximum score F, and no
+// pixel scoring below F can be output or influence a pixel that can: those pixels start out
+// decided (out).  k_nms_lmax lists the strict local maxima, k_nms_floor selects F per frame.  On
+// a camera frame (and on random-weight heatmaps, where nearly every pixel is a candidate) this
+// leaves a few hundred to a few thousand undecided pixels per frame, so the rounds converge in one
+// or two iterations and only tiles with undecided pixels run at all.
+//
 // Round budget: a fixed number of tile rounds (kNmsRounds launches; each iterates its tile to a
 // local fixed point) settles typical heatmaps; whatever is still undecided afterwards (a dependency
 // chain crossing many tile borders) is finished by k_nms_finish, one workgroup per frame running
@@ -23,6 +32,14 @@
 // result is the greedy set for every input; a frame that reaches k_nms_finish's round cap (only an
 // adversarial dependency chain thousands of pixels long can) is reported (count = VS_ERR_NOTCONV
 // on the device paths, VS_ERR_NOTCONV from the host entry points), never a wrong keypoint list.
+//
+// Ties.  The reference sorts with std::sort (unstable); the order used here breaks exact score
+// ties by raster index.  The output can differ from the reference's only through an exact tie that
+// the greedy actually resolves: two candidates of equal score within one 9x9 window of which one is
+// kept, or equal scores on both sides of the 400 cut.  k_nms_select counts both per frame (an
+// output keypoint with an equal-score candidate in its window; the 400th and 401st kept pixel
+// scoring the same) into the context's tie totals (vs_nms_tie_stats): when both are zero the
+// output equals the reference's for ANY order of equal scores, std::sort's included.
 #include <hip/hip_runtime.h>
 
 #include <cstdlib>
@@ -37,7 +54,7 @@ constexpr int kRadius = 4;             // SP_NMS_RADIUS (Config.h:41)
 constexpr int kMaxKeypoints = 400;     // SP_MAX_KEYPOINTS (Config.h:42)
 constexpr int kNmsTile = 32;
 constexpr int kNmsReg = kNmsTile + 2 * kRadius;
-constexpr int kNmsMaxRounds = 8;          // tile-round launches before k_nms_finish
+constexpr int kNmsMaxRounds = 4;          // tile-round launches before k_nms_finish
 constexpr int kFinishMaxRounds = 1 << 14; // k_nms_finish's round cap (VS_NMS_FINISH_ROUNDS overrides)
 
 enum : uint8_t { ST_UNDECIDED = 0, ST_KEPT = 1, ST_OUT = 2 };
@@ -48,7 +65,7 @@ enum : uint8_t { ST_UNDECIDED = 0, ST_KEPT = 1, ST_OUT = 2 };
 // against libm on the host by tests/test_oracle.py, and on the device through the decode parity
 // tests of tests/test_gpu_parity.py).
 __global__ __launch_bounds__(256) void k_decode(const float* __restrict__ semi, int hc, int wc, int B,
-                                                float* __restrict__ heat, uint8_t* __restrict__ state) {
+                                                float* __restrict__ heat) {
     int idx = blockIdx.x * blockDim.x + threadIdx.x;
     int ncell = hc * wc;
     if (idx >= B * ncell) return;
@@ -69,110 +86,242 @@ __global__ __launch_bounds__(256) void k_decode(const float* __restrict__ semi, 
     }
     const int Wp = wc * 8;
     float* hb = heat + (size_t)b * ncell * 64;
-    uint8_t* sb = state + (size_t)b * ncell * 64;
 #pragma unroll
-    for (int c = 0; c < 64; c++) {
-        float v = div_rn(cell[c], sum);
-        size_t o = (size_t)(cy * 8 + c / 8) * Wp + cx * 8 + (c % 8);
-        hb[o] = v;
-        sb[o] = (v > kConfThresh) ? ST_UNDECIDED : ST_OUT;
+    for (int c = 0; c < 64; c += 4) {
+        float4 v;
+        v.x = div_rn(cell[c], sum);
+        v.y = div_rn(cell[c + 1], sum);
+        v.z = div_rn(cell[c + 2], sum);
+        v.w = div_rn(cell[c + 3], sum);
+        *reinterpret_cast<float4*>(hb + (size_t)(cy * 8 + c / 8) * Wp + cx * 8 + (c % 8)) = v;
     }
 }
 
+// 9-wide windows over a (32 + 8)^2 LDS region of 32-bit score keys: row pass (40 region rows x 32
+// interior columns), then the column pass per interior pixel.  u32 score bits order like the
+// scores (all candidates are > 0).
+constexpr int kNmsThreads = 256;
+
+// Strict local maxima of the candidate heatmap -> per-frame list of their score bits (any order).
+// One workgroup per 32x32 tile.
+__global__ __launch_bounds__(kNmsThreads) void k_nms_lmax(const float* __restrict__ heat, int B, int Hp, int Wp,
+                                                          int tiles_x, unsigned* __restrict__ lm,
+                                                          int* __restrict__ lmcnt, int lm_cap) {
+    const int b = blockIdx.y;
+    __shared__ unsigned s_key[kNmsReg * kNmsReg];
+    __shared__ unsigned s_rmax[kNmsReg * kNmsTile];
+    const int tx = blockIdx.x % tiles_x, ty = blockIdx.x / tiles_x;
+    const int gx0 = tx * kNmsTile - kRadius, gy0 = ty * kNmsTile - kRadius;
+    const float* hb = heat + (size_t)b * Hp * Wp;
+    for (int i = threadIdx.x; i < kNmsReg * kNmsReg; i += kNmsThreads) {
+        const int ry = i / kNmsReg, rx = i - ry * kNmsReg;
+        const int gy = gy0 + ry, gx = gx0 + rx;
+        unsigned key = 0;
+        if (gy >= 0 && gy < Hp && gx >= 0 && gx < Wp) {
+            const float v = hb[(size_t)gy * Wp + gx];
+            key = v > kConfThresh ? __float_as_uint(v) : 0u;
+        }
+        s_key[i] = key;
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < kNmsReg * kNmsTile; i += kNmsThreads) {
+        const int ry = i / kNmsTile, ix = i - ry * kNmsTile;
+        const unsigned* r = s_key + ry * kNmsReg + ix;
+        unsigned m = r[0];
+#pragma unroll
+        for (int d = 1; d <= 2 * kRadius; d++) m = max(m, r[d]);
+        s_rmax[i] = m;
+    }
+    __syncthreads();
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int j = 0; j < kNmsTile * kNmsTile / kNmsThreads; j++) {
+        const int kk = threadIdx.x + kNmsThreads * j;
+        const int iy = kk / kNmsTile, ix = kk - iy * kNmsTile;
+        const unsigned key = s_key[(iy + kRadius) * kNmsReg + ix + kRadius];
+        bool lmx = false;
+        if (key != 0 && gy0 + kRadius + iy < Hp && gx0 + kRadius + ix < Wp) {
+            unsigned m = 0;
+#pragma unroll
+            for (int d = 0; d <= 2 * kRadius; d++) m = max(m, s_rmax[(iy + d) * kNmsTile + ix]);
+            if (m == key) {  // the window maximum: strict unless another window pixel scores the same
+                int eq = 0;
+                for (int dy = 0; dy <= 2 * kRadius; dy++)
+                    for (int dx = 0; dx <= 2 * kRadius; dx++) eq += s_key[(iy + dy) * kNmsReg + ix + dx] == key;
+                lmx = eq == 1;
+            }
+        }
+        const unsigned long long bal = __ballot(lmx);
+        if (bal) {
+            const int leader = __ffsll((long long)bal) - 1;
+            int base = 0;
+            if (lane == leader) base = atomicAdd(&lmcnt[b], __popcll(bal));
+            base = __shfl(base, leader);
+            const int o = base + __popcll(bal & ((1ull << lane) - 1ull));
+            if (lmx && o < lm_cap) lm[(size_t)b * lm_cap + o] = key;
+        }
+    }
+}
+
+// Per frame: F = the max_kp-th largest strict-local-maximum score (bits), or 0 (no floor) when the
+// frame has fewer strict local maxima.  Exact MSB-first radix select, one workgroup per frame.
+__global__ __launch_bounds__(kNmsThreads) void k_nms_floor(const unsigned* __restrict__ lm, const int* __restrict__ lmcnt,
+                                                           int lm_cap, int max_kp, unsigned* __restrict__ floor_bits) {
+    const int b = blockIdx.x;
+    __shared__ int hist[256];
+    __shared__ unsigned s_prefix, s_mask;
+    __shared__ int s_krem;
+    const int n = min(lmcnt[b], lm_cap);
+    if (n < max_kp) {
+        if (threadIdx.x == 0) floor_bits[b] = 0u;
+        return;
+    }
+    const unsigned* l = lm + (size_t)b * lm_cap;
+    if (threadIdx.x == 0) {
+        s_prefix = 0;
+        s_mask = 0;
+        s_krem = max_kp;
+    }
+    for (int pass = 0; pass < 4; pass++) {
+        const int shift = 24 - 8 * pass;
+        hist[threadIdx.x] = 0;
+        __syncthreads();
+        const unsigned pre = s_prefix, msk = s_mask;
+        for (int i = threadIdx.x; i < n; i += kNmsThreads) {
+            const unsigned k = l[i];
+            if ((k & msk) == pre) atomicAdd(&hist[(k >> shift) & 255], 1);
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            int rem = s_krem, acc = 0, d = 255;
+            for (; d > 0; d--) {
+                if (acc + hist[d] >= rem) break;
+                acc += hist[d];
+            }
+            s_krem = rem - acc;
+            s_prefix = pre | ((unsigned)d << shift);
+            s_mask = msk | (255u << shift);
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) floor_bits[b] = s_prefix;
+}
+
 // One NMS round over a 32x32 tile (+4 halo).  The tile iterates to its local fixed point, writes
-// its interior states back and flags the frame if anything is still undecided.
-// flags[r*B + b] != 0  <=>  frame b still had undecided pixels after round r-1.
+// its interior states back and flags itself (and its frame) if anything is still undecided.
+// tflags[r][b][tile] != 0  <=>  the tile's interior still had undecided pixels after round r-1
+// (round 0: every tile); flags[r*B + b] != 0  <=>  some tile of frame b did.  Round 0 derives the
+// initial states from the heatmap and the frame's floor (undecided iff score > 0.005 and >= F).
 // Each local iteration evaluates, for every interior pixel, M = the 9x9 window max of the
-// undecided pixels' 64-bit priority keys (score bits << 32 | ~raster index, 0 when not undecided)
-// and K = the 9x9 window OR of the kept flags, both separable (9-wide row pass, then column pass)
-// in LDS.  An undecided pixel with K set is out; one whose own key equals M (nothing undecided
-// outranks it in its window) is kept.
+// undecided pixels' score bits (0 when not undecided) and K = the 9x9 window OR of the kept
+// flags, both separable in LDS.  An undecided pixel with K set is out; one whose own score is
+// below M is blocked; one whose score equals M is kept unless an equal-score undecided pixel
+// precedes it in raster order inside its window (the total order's tie break).
 __device__ __forceinline__ unsigned long long nms_key(float s, unsigned raster) {
     return ((unsigned long long)__float_as_uint(s) << 32) | (unsigned)(0xFFFFFFFFu - raster);
 }
 
-__global__ __launch_bounds__(256) void k_nms_round(const float* __restrict__ heat, uint8_t* __restrict__ state,
-                                                   int* __restrict__ flags, int r, int B, int Hp, int Wp,
-                                                   int tiles_x) {
+__global__ __launch_bounds__(kNmsThreads) void k_nms_round(const float* __restrict__ heat, uint8_t* __restrict__ state,
+                                                           int* __restrict__ flags, uint8_t* __restrict__ tflags,
+                                                           const unsigned* __restrict__ floor_bits, int r, int B,
+                                                           int Hp, int Wp, int tiles_x, int ntiles) {
     const int b = blockIdx.y;
     if (flags[r * B + b] == 0) return;
-    __shared__ unsigned long long s_key[kNmsReg * kNmsReg];
-    __shared__ unsigned long long s_rmax[kNmsReg * kNmsTile];
+    if (r > 0 && tflags[((size_t)r * B + b) * ntiles + blockIdx.x] == 0) return;
+    __shared__ unsigned s_key[kNmsReg * kNmsReg];
+    __shared__ unsigned s_rmax[kNmsReg * kNmsTile];
     __shared__ uint8_t s_kept[kNmsReg * kNmsReg];
     __shared__ uint8_t s_rkept[kNmsReg * kNmsTile];
     const int tx = blockIdx.x % tiles_x, ty = blockIdx.x / tiles_x;
     const int gx0 = tx * kNmsTile - kRadius, gy0 = ty * kNmsTile - kRadius;
     const float* hb = heat + (size_t)b * Hp * Wp;
     uint8_t* sb = state + (size_t)b * Hp * Wp;
-    for (int i = threadIdx.x; i < kNmsReg * kNmsReg; i += 256) {
+    const unsigned fl = floor_bits[b];
+    int any = 0;
+    for (int i = threadIdx.x; i < kNmsReg * kNmsReg; i += kNmsThreads) {
         const int ry = i / kNmsReg, rx = i - ry * kNmsReg;
         const int gy = gy0 + ry, gx = gx0 + rx;
-        unsigned long long key = 0;
+        unsigned key = 0;
         uint8_t kept = 0;
         if (gy >= 0 && gy < Hp && gx >= 0 && gx < Wp) {
-            const uint8_t st = sb[(size_t)gy * Wp + gx];
-            if (st == ST_UNDECIDED) key = nms_key(hb[(size_t)gy * Wp + gx], (unsigned)(gy * Wp + gx));
+            const float v = hb[(size_t)gy * Wp + gx];
+            uint8_t st;
+            if (r == 0)  // halo pixels of other tiles: their round-0 state, derived the same way
+                st = (v > kConfThresh && __float_as_uint(v) >= fl) ? ST_UNDECIDED : ST_OUT;
+            else
+                st = sb[(size_t)gy * Wp + gx];
+            if (st == ST_UNDECIDED) key = __float_as_uint(v);
             kept = (st == ST_KEPT);
         }
         s_key[i] = key;
         s_kept[i] = kept;
+        any |= key != 0 && ry >= kRadius && ry < kRadius + kNmsTile && rx >= kRadius && rx < kRadius + kNmsTile;
     }
-    __syncthreads();
-    int changed;
-    do {
-        // row pass: 40 region rows x 32 interior columns
-        for (int i = threadIdx.x; i < kNmsReg * kNmsTile; i += 256) {
-            const int ry = i / kNmsTile, ix = i - ry * kNmsTile;
-            const int base = ry * kNmsReg + ix;
-            unsigned long long m = s_key[base];
-            uint8_t k = s_kept[base];
+    if (__syncthreads_or(any)) {
+        int changed;
+        do {
+            for (int i = threadIdx.x; i < kNmsReg * kNmsTile; i += kNmsThreads) {
+                const int ry = i / kNmsTile, ix = i - ry * kNmsTile;
+                const int base = ry * kNmsReg + ix;
+                unsigned m = s_key[base];
+                uint8_t k = s_kept[base];
 #pragma unroll
-            for (int d = 1; d <= 2 * kRadius; d++) {
-                const unsigned long long v = s_key[base + d];
-                m = v > m ? v : m;
-                k |= s_kept[base + d];
+                for (int d = 1; d <= 2 * kRadius; d++) {
+                    m = max(m, s_key[base + d]);
+                    k |= s_kept[base + d];
+                }
+                s_rmax[i] = m;
+                s_rkept[i] = k;
             }
-            s_rmax[i] = m;
-            s_rkept[i] = k;
-        }
-        __syncthreads();
-        uint8_t dec[4];
-        int ch = 0;
+            __syncthreads();
+            uint8_t dec[kNmsTile * kNmsTile / kNmsThreads];
+            int ch = 0;
 #pragma unroll
-        for (int j = 0; j < 4; j++) {
-            const int kk = threadIdx.x + 256 * j;
-            const int iy = kk / kNmsTile, ix = kk - iy * kNmsTile;
-            const unsigned long long key = s_key[(iy + kRadius) * kNmsReg + ix + kRadius];
-            dec[j] = 0;
-            if (key == 0) continue;
-            unsigned long long m = 0;
-            uint8_t k = 0;
+            for (int j = 0; j < kNmsTile * kNmsTile / kNmsThreads; j++) {
+                const int kk = threadIdx.x + kNmsThreads * j;
+                const int iy = kk / kNmsTile, ix = kk - iy * kNmsTile;
+                const unsigned key = s_key[(iy + kRadius) * kNmsReg + ix + kRadius];
+                dec[j] = 0;
+                if (key == 0) continue;
+                unsigned m = 0;
+                uint8_t k = 0;
 #pragma unroll
-            for (int d = 0; d <= 2 * kRadius; d++) {
-                const unsigned long long v = s_rmax[(iy + d) * kNmsTile + ix];
-                m = v > m ? v : m;
-                k |= s_rkept[(iy + d) * kNmsTile + ix];
+                for (int d = 0; d <= 2 * kRadius; d++) {
+                    m = max(m, s_rmax[(iy + d) * kNmsTile + ix]);
+                    k |= s_rkept[(iy + d) * kNmsTile + ix];
+                }
+                if (k) {
+                    dec[j] = ST_OUT;
+                } else if (m == key) {
+                    // equal-score undecided pixels earlier in raster order (rows above, then left)
+                    bool first = true;
+                    for (int d = 0; d < kRadius * (2 * kRadius + 1) + kRadius && first; d++) {
+                        const int dy = d / (2 * kRadius + 1), dx = d - dy * (2 * kRadius + 1);
+                        first = s_key[(iy + dy) * kNmsReg + ix + dx] != key;
+                    }
+                    if (first) dec[j] = ST_KEPT;
+                }
+                ch |= dec[j] != 0;
             }
-            if (k) dec[j] = ST_OUT;
-            else if (m == key) dec[j] = ST_KEPT;
-            ch |= dec[j] != 0;
-        }
-        __syncthreads();
+            __syncthreads();
 #pragma unroll
-        for (int j = 0; j < 4; j++) {
-            if (!dec[j]) continue;
-            const int kk = threadIdx.x + 256 * j;
-            const int iy = kk / kNmsTile, ix = kk - iy * kNmsTile;
-            const int p = (iy + kRadius) * kNmsReg + ix + kRadius;
-            s_key[p] = 0;
-            if (dec[j] == ST_KEPT) s_kept[p] = 1;
-        }
-        changed = __syncthreads_or(ch);
-    } while (changed);
+            for (int j = 0; j < kNmsTile * kNmsTile / kNmsThreads; j++) {
+                if (!dec[j]) continue;
+                const int kk = threadIdx.x + kNmsThreads * j;
+                const int iy = kk / kNmsTile, ix = kk - iy * kNmsTile;
+                const int p = (iy + kRadius) * kNmsReg + ix + kRadius;
+                s_key[p] = 0;
+                if (dec[j] == ST_KEPT) s_kept[p] = 1;
+            }
+            changed = __syncthreads_or(ch);
+        } while (changed);
+    } else if (r > 0) {
+        return;  // nothing undecided inside any more: nothing to write
+    }
     int und = 0;
 #pragma unroll
-    for (int j = 0; j < 4; j++) {
-        const int kk = threadIdx.x + 256 * j;
+    for (int j = 0; j < kNmsTile * kNmsTile / kNmsThreads; j++) {
+        const int kk = threadIdx.x + kNmsThreads * j;
         const int iy = kk / kNmsTile, ix = kk - iy * kNmsTile;
         const int gy = gy0 + kRadius + iy, gx = gx0 + kRadius + ix;
         if (gy < Hp && gx < Wp) {
@@ -182,7 +331,12 @@ __global__ __launch_bounds__(256) void k_nms_round(const float* __restrict__ hea
             und |= (v == ST_UNDECIDED);
         }
     }
-    if (__syncthreads_or(und) && threadIdx.x == 0) flags[(r + 1) * B + b] = 1;
+    // only a tile with undecided interior pixels has anything to do next round (its neighbours'
+    // decisions reach it through the halo it reloads)
+    if (__syncthreads_or(und) && threadIdx.x == 0) {
+        tflags[((size_t)(r + 1) * B + b) * ntiles + blockIdx.x] = 1;
+        flags[(r + 1) * B + b] = 1;
+    }
 }
 
 // Finishes the NMS of frames the tile rounds left undecided (flags[R * B + b] != 0), one workgroup
@@ -260,13 +414,17 @@ __global__ __launch_bounds__(256) void k_nms_collect(const float* __restrict__ h
 
 // Top-K of the kept keys (exact MSB-first radix select over the 64-bit keys, which are unique),
 // bitonic sort of the K winners in descending priority, keypoint records, border erase
-// (FeatureExtractor.cpp:155-160).  One 1024-thread workgroup per frame.
+// (FeatureExtractor.cpp:155-160), and the frame's tie accounting (see the header): window ties =
+// selected pixels with an equal-score candidate in their 9x9 window, cut tie = the K-th and the
+// (K+1)-th kept pixel score the same.  ties[b] = {window, cut}; totals += {frames, frames with a
+// tie, window ties, cut ties}.  One 1024-thread workgroup per frame.
 constexpr int kSelSort = 512;
 __global__ __launch_bounds__(1024) void k_nms_select(const unsigned long long* __restrict__ keys,
                                                      const int* __restrict__ keycnt, int key_cap, int max_kp,
-                                                     int Wp, int h, int w, vs_keypoint* __restrict__ kps,
+                                                     int Wp, int Hp, int h, int w, vs_keypoint* __restrict__ kps,
                                                      int cap, int* __restrict__ nout, int* __restrict__ err,
-                                                     const int* __restrict__ ferr) {
+                                                     const int* __restrict__ ferr, const float* __restrict__ heat,
+                                                     int* __restrict__ ties, unsigned long long* __restrict__ totals) {
     const int b = blockIdx.x;
     if (ferr[b]) {  // NMS not finished: no keypoints, a negative count that every consumer rejects
         if (threadIdx.x == 0) nout[b] = VS_ERR_NOTCONV;
@@ -274,8 +432,8 @@ __global__ __launch_bounds__(1024) void k_nms_select(const unsigned long long* _
     }
     __shared__ int hist[256];
     __shared__ unsigned long long s_sel[kSelSort];
-    __shared__ int s_nsel;
-    __shared__ unsigned long long s_prefix, s_mask;
+    __shared__ int s_nsel, s_wties;
+    __shared__ unsigned long long s_prefix, s_mask, s_next;
     __shared__ int s_krem;
     int nk = keycnt[b];
     if (nk > key_cap) {
@@ -315,7 +473,11 @@ __global__ __launch_bounds__(1024) void k_nms_select(const unsigned long long* _
         }
         kth = s_prefix;  // the K-th largest key
     }
-    if (threadIdx.x == 0) s_nsel = 0;
+    if (threadIdx.x == 0) {
+        s_nsel = 0;
+        s_wties = 0;
+        s_next = 0;
+    }
     for (int i = threadIdx.x; i < kSelSort; i += blockDim.x) s_sel[i] = 0;
     __syncthreads();
     for (int i = threadIdx.x; i < nk; i += blockDim.x) {
@@ -323,7 +485,29 @@ __global__ __launch_bounds__(1024) void k_nms_select(const unsigned long long* _
         if (K > 0 && k >= kth) {
             int slot = atomicAdd(&s_nsel, 1);
             if (slot < kSelSort) s_sel[slot] = k;
+        } else if (K > 0) {
+            atomicMax(&s_next, k);  // the (K+1)-th kept key
         }
+    }
+    __syncthreads();
+    // window ties of the selected pixels (each lane one pixel, 80 heatmap reads)
+    if ((int)threadIdx.x < K && (int)threadIdx.x < kSelSort) {
+        const unsigned long long k = s_sel[threadIdx.x];
+        const unsigned idx = 0xFFFFFFFFu - (unsigned)(k & 0xFFFFFFFFull);
+        const int px = (int)(idx % (unsigned)Wp), py = (int)(idx / (unsigned)Wp);
+        const unsigned sc = (unsigned)(k >> 32);
+        const float* hb = heat + (size_t)b * Hp * Wp;
+        bool tie = false;
+        for (int dy = -kRadius; dy <= kRadius; dy++) {
+            const int y = py + dy;
+            if (y < 0 || y >= Hp) continue;
+            for (int dx = -kRadius; dx <= kRadius; dx++) {
+                const int x = px + dx;
+                if (x < 0 || x >= Wp || (dx == 0 && dy == 0)) continue;
+                tie |= __float_as_uint(hb[(size_t)y * Wp + x]) == sc;
+            }
+        }
+        if (tie) atomicAdd(&s_wties, 1);
     }
     __syncthreads();
     // bitonic sort, descending (zero keys pad the tail)
@@ -362,6 +546,14 @@ __global__ __launch_bounds__(1024) void k_nms_select(const unsigned long long* _
             n++;
         }
         nout[b] = n;
+        const int wt = s_wties;
+        const int ct = (K > 0 && K < nk && (s_next >> 32) == (kth >> 32)) ? 1 : 0;
+        ties[2 * b] = wt;
+        ties[2 * b + 1] = ct;
+        atomicAdd(&totals[0], 1ull);
+        atomicAdd(&totals[1], (wt || ct) ? 1ull : 0ull);
+        atomicAdd(&totals[2], (unsigned long long)wt);
+        atomicAdd(&totals[3], (unsigned long long)ct);
     }
 }
 
@@ -424,41 +616,57 @@ __global__ __launch_bounds__(256) void k_sample(const float* __restrict__ dgrid,
 
 int sp_postprocess(vs_ctx* ctx, int B, int hc, int wc, int h, int w, vs_keypoint* d_kps, float* d_desc,
                    int* d_n, int cap, hipStream_t s, const float* semi, const float* dgrid) {
+    VS_CHECK(scratch_order(ctx, s));
     if (!semi) semi = ctx->semi.as<float>();
     if (!dgrid) dgrid = ctx->dgrid.as<float>();
     const int Hp = hc * 8, Wp = wc * 8;
     const size_t npx = (size_t)B * Hp * Wp;
-    // Kept pixels are pairwise >= radius+1 apart (Chebyshev), so at most ceil(H/5)*ceil(W/5).
+    // Kept pixels (and strict local maxima) are pairwise >= radius+1 apart (Chebyshev), so at most
+    // ceil(H/5)*ceil(W/5).
     const int key_cap = ((Hp + kRadius) / (kRadius + 1)) * ((Wp + kRadius) / (kRadius + 1));
     const int max_kp = cap < kMaxKeypoints ? cap : kMaxKeypoints;
+    const int tiles_x = (Wp + kNmsTile - 1) / kNmsTile, tiles_y = (Hp + kNmsTile - 1) / kNmsTile;
+    const int ntiles = tiles_x * tiles_y;
     VS_CHECK(ctx->heat.ensure(npx * sizeof(float)));
     VS_CHECK(ctx->state.ensure(npx));
-    // flags: [rounds + 1][B] undecided-after-round, then the capacity word, then ferr [B]
-    VS_CHECK(ctx->flags.ensure(((size_t)(kNmsMaxRounds + 2) * B + 1) * sizeof(int)));
+    // flags (ints): [rounds + 1][B] undecided-after-round, the capacity word, ferr [B], keycnt [B],
+    // lmcnt [B], floor [B], ties [B][2]; then tile flags (bytes) [rounds + 1][B][ntiles]
+    const size_t nflag = (size_t)(kNmsMaxRounds + 1) * B + 1 + 6 * (size_t)B;
+    VS_CHECK(ctx->flags.ensure(nflag * sizeof(int) + (size_t)(kNmsMaxRounds + 1) * B * ntiles));
     VS_CHECK(ctx->nms_list.ensure(npx * 2 * sizeof(int)));
     const char* fr_env = getenv("VS_NMS_FINISH_ROUNDS");  // test knob: forces the error path
     const int finish_rounds = fr_env && atoi(fr_env) > 0 ? atoi(fr_env) : kFinishMaxRounds;
     VS_CHECK(ctx->keys.ensure((size_t)B * key_cap * sizeof(unsigned long long)));
-    VS_CHECK(ctx->keycnt.ensure((size_t)B * sizeof(int)));
+    VS_CHECK(ctx->lmax.ensure((size_t)B * key_cap * sizeof(unsigned)));  // strict local maxima
+    if (!ctx->tie_totals.p) {
+        VS_CHECK(ctx->tie_totals.ensure(4 * sizeof(unsigned long long)));
+        VS_HIP(hipMemsetAsync(ctx->tie_totals.p, 0, 4 * sizeof(unsigned long long), s));
+    }
     int* flags = ctx->flags.as<int>();
     int* err = flags + (size_t)(kNmsMaxRounds + 1) * B;
     int* ferr = err + 1;
+    int* keycnt = ferr + B;
+    int* lmcnt = keycnt + B;
+    unsigned* floor_bits = reinterpret_cast<unsigned*>(lmcnt + B);
+    int* ties = lmcnt + 2 * B;
+    uint8_t* tflags = reinterpret_cast<uint8_t*>(flags + nflag);
+    unsigned* lm = ctx->lmax.as<unsigned>();
     {
         ProfScope ps(ctx, "decode", s);
         int ncell = B * hc * wc;
-        hipLaunchKernelGGL(k_decode, dim3((ncell + 255) / 256), dim3(256), 0, s, semi, hc, wc, B,
-                           ctx->heat.as<float>(), ctx->state.as<uint8_t>());
+        hipLaunchKernelGGL(k_decode, dim3((ncell + 255) / 256), dim3(256), 0, s, semi, hc, wc, B, ctx->heat.as<float>());
         VS_HIP(hipGetLastError());
     }
     {
         ProfScope ps(ctx, "nms_rounds", s);
-        VS_HIP(hipMemsetAsync(flags, 0, ((size_t)(kNmsMaxRounds + 2) * B + 1) * sizeof(int), s));
-        // round 0 runs for every frame
-        VS_HIP(hipMemsetAsync(flags, 0x01, (size_t)B * sizeof(int), s));
-        const int tiles_x = (Wp + kNmsTile - 1) / kNmsTile, tiles_y = (Hp + kNmsTile - 1) / kNmsTile;
+        VS_HIP(hipMemsetAsync(flags, 0, nflag * sizeof(int) + (size_t)(kNmsMaxRounds + 1) * B * ntiles, s));
+        VS_HIP(hipMemsetAsync(flags, 0x01, (size_t)B * sizeof(int), s));  // round 0 runs for every frame
+        hipLaunchKernelGGL(k_nms_lmax, dim3(ntiles, B), dim3(kNmsThreads), 0, s, ctx->heat.as<float>(), B, Hp, Wp,
+                           tiles_x, lm, lmcnt, key_cap);
+        hipLaunchKernelGGL(k_nms_floor, dim3(B), dim3(kNmsThreads), 0, s, lm, lmcnt, key_cap, max_kp, floor_bits);
         for (int r = 0; r < kNmsMaxRounds; r++) {
-            hipLaunchKernelGGL(k_nms_round, dim3(tiles_x * tiles_y, B), dim3(256), 0, s, ctx->heat.as<float>(),
-                               ctx->state.as<uint8_t>(), flags, r, B, Hp, Wp, tiles_x);
+            hipLaunchKernelGGL(k_nms_round, dim3(ntiles, B), dim3(kNmsThreads), 0, s, ctx->heat.as<float>(),
+                               ctx->state.as<uint8_t>(), flags, tflags, floor_bits, r, B, Hp, Wp, tiles_x, ntiles);
         }
         hipLaunchKernelGGL(k_nms_finish, dim3(B), dim3(1024), 0, s, ctx->heat.as<float>(), ctx->state.as<uint8_t>(),
                            flags, kNmsMaxRounds, B, Hp, Wp, ctx->nms_list.as<int>(), finish_rounds, ferr);
@@ -466,11 +674,11 @@ int sp_postprocess(vs_ctx* ctx, int B, int hc, int wc, int h, int w, vs_keypoint
     }
     {
         ProfScope ps(ctx, "nms_select", s);
-        VS_HIP(hipMemsetAsync(ctx->keycnt.p, 0, (size_t)B * sizeof(int), s));
-        hipLaunchKernelGGL(k_nms_collect, dim3(64, B), dim3(256), 0, s, ctx->heat.as<float>(), ctx->state.as<uint8_t>(),
-                           Hp, Wp, ctx->keys.as<unsigned long long>(), ctx->keycnt.as<int>(), key_cap);
-        hipLaunchKernelGGL(k_nms_select, dim3(B), dim3(1024), 0, s, ctx->keys.as<unsigned long long>(),
-                           ctx->keycnt.as<int>(), key_cap, max_kp, Wp, h, w, d_kps, cap, d_n, err, ferr);
+        hipLaunchKernelGGL(k_nms_collect, dim3(16, B), dim3(256), 0, s, ctx->heat.as<float>(), ctx->state.as<uint8_t>(),
+                           Hp, Wp, ctx->keys.as<unsigned long long>(), keycnt, key_cap);
+        hipLaunchKernelGGL(k_nms_select, dim3(B), dim3(1024), 0, s, ctx->keys.as<unsigned long long>(), keycnt, key_cap,
+                           max_kp, Wp, Hp, h, w, d_kps, cap, d_n, err, ferr, ctx->heat.as<float>(), ties,
+                           ctx->tie_totals.as<unsigned long long>());
         VS_HIP(hipGetLastError());
     }
     {

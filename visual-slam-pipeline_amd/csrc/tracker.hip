@@ -180,12 +180,13 @@ constexpr int kHdrWords = 4 + 624;
 constexpr size_t kHdrBytes = kHdrWords * sizeof(uint32_t);
 
 // Extraction chunks: the batch's network + post-processing runs chunk by chunk on the extraction
-// streams while the tracker consumes the chunks already done (process_batch_dev).  Sizes grow from
-// the first chunk by VS_SLAM_CHUNK_GROWTH / 10 up to kXChunk.  Round 1 (tracking-bound, no
-// prefetch) wanted a small first chunk (3, 4, 5, 7, 8, 5 at B = 32); with the next batch prefetched
-// behind the current one and the tracker faster than the network, larger chunks win because the
-// network's small layers (60 x 80 conv4 / heads) fill the chip better (A/B on one box, 4 rounds:
-// 3 / 1.3x 1624, 5 / 1.5x 1629, 8 8 8 8 1688 frames/s).
+// streams while the tracker consumes the chunks already done (process_batch_dev).  The batch is
+// split evenly into ceil(nb / chunk) chunks (8, 8, 8, 8 at B = 32; 8, 8, 7, 7 at 30: never a
+// short tail chunk that runs the whole network for one frame).  Round 1 (tracking-bound, no
+// prefetch) wanted a small first chunk; with the next batch prefetched behind the current one and
+// the tracker faster than the network, larger chunks win because the network's small layers
+// (60 x 80 conv4 / heads) fill the chip better (same-box A/B, 4 rounds: 3, 4, 5, 7, 8, 5 -> 1624;
+// 8, 8, 8, 8 -> 1688 frames/s).  VS_SLAM_CHUNK (1..kXChunk) sets the target chunk size.
 constexpr int kXChunk = 16;
 constexpr int kXFirst = 8;
 
@@ -334,6 +335,7 @@ struct GpuOps {
     // here while the network of the next chunk already runs on xs
     hipStream_t xp = nullptr;
     hipEvent_t region_done[2] = {nullptr, nullptr};  // last post-processing that read a region's network output
+    hipEvent_t xdone = nullptr;  // the last extraction enqueued (ctx->scratch_busy while this vs_slam lives)
     // Speculative front chain of the batch's next frame (see chain()): its own stream on the tracking
     // CU set, result block, header, matcher key state and pinned host block [header | result].
     hipStream_t s2 = nullptr;
@@ -379,8 +381,7 @@ struct GpuOps {
         const float* depth = nullptr;
     } hint;                            // the next batch, to prefetch behind the current one
 
-    int first_chunk = kXFirst;    // VS_SLAM_FIRST_CHUNK overrides
-    int chunk_growth = 13;        // next chunk = this one x growth / 10 (VS_SLAM_CHUNK_GROWTH overrides)
+    int chunk = kXFirst;          // target frames per extraction chunk (VS_SLAM_CHUNK overrides)
     int B = 0, h = 0, w = 0, S = 0, batch_region = 0;
     double K[4] = {vs_trk::cfg::FX, vs_trk::cfg::FY, vs_trk::cfg::CX, vs_trk::cfg::CY};
     DevBuf pool_kps, pool_desc, pool_n, pool_depth, pool_norms, semi, dgrid;
@@ -455,6 +456,12 @@ struct GpuOps {
         }
         for (auto& e : region_done) VS_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
         VS_HIP(hipEventCreateWithFlags(&cspec_ev, hipEventDisableTiming));
+        VS_HIP(hipEventCreateWithFlags(&xdone, hipEventDisableTiming));
+        // the extraction streams share the context's network / NMS scratch: any other stream that
+        // uses it waits for the last extraction enqueued here (vs::scratch_order)
+        ctx->scratch_busy = xdone;
+        ctx->scratch_owner[0] = xs;
+        ctx->scratch_owner[1] = xp;
         own_streams = true;
         return VS_OK;
     }
@@ -465,6 +472,11 @@ struct GpuOps {
         (void)hipStreamSynchronize(xp);
         (void)hipStreamSynchronize(s);
         (void)hipStreamSynchronize(s2);
+        if (ctx->scratch_busy == xdone) {
+            ctx->scratch_busy = nullptr;
+            ctx->scratch_owner[0] = ctx->scratch_owner[1] = nullptr;
+        }
+        (void)hipEventDestroy(xdone);
         for (auto& e : region_done) (void)hipEventDestroy(e);
         for (auto& X : xb) {
             for (hipEvent_t e : X.ev) (void)hipEventDestroy(e);
@@ -485,8 +497,7 @@ struct GpuOps {
         VS_CHECK(make_streams());
         if (const char* e = std::getenv("VS_SLAM_ASYNC_ENQUEUE")) async_enqueue = e[0] != '0';
         if (async_enqueue) aq.start(ctx->device);
-        if (const char* fc = std::getenv("VS_SLAM_FIRST_CHUNK")) first_chunk = std::max(1, std::min(kXChunk, std::atoi(fc)));
-        if (const char* g = std::getenv("VS_SLAM_CHUNK_GROWTH")) chunk_growth = std::max(10, std::min(40, std::atoi(g)));
+        if (const char* fc = std::getenv("VS_SLAM_CHUNK")) chunk = std::max(1, std::min(kXChunk, std::atoi(fc)));
         const char* hp = std::getenv("VS_SLAM_HOST_PROFILE");
         hprof.on = hp && hp[0] == '1';
         if (hprof.on) hprof.on = false, hprof.skip = 64, hprof_armed = true;
@@ -640,7 +651,7 @@ struct GpuOps {
         return VS_OK;
     }
     // B frames already in HBM -> network + post-processing straight into batch region slots,
-    // depth copied beside them, keypoints back to pinned host memory, kXChunk frames at a time on
+    // depth copied beside them, keypoints back to pinned host memory, one chunk (<= kXChunk frames) at a time on
     // the extraction stream; chunk c's event marks its slots and host keypoints ready.  Enqueue
     // only: wait_chunk() hands a chunk to the tracker.
     int enqueue_extraction(XBatch& X, int nb, const uint8_t* d_bgr, const float* d_depth) {
@@ -651,8 +662,8 @@ struct GpuOps {
         X.depth = d_depth;
         const int s0 = X.region * B;
         X.ch.assign(1, 0);
-        for (int c = first_chunk; X.ch.back() < nb; c = std::min(kXChunk, std::max(c + 1, (c * chunk_growth + 5) / 10)))
-            X.ch.push_back(std::min(nb, X.ch.back() + c));
+        const int nch_even = (nb + chunk - 1) / chunk;  // even split, no short tail chunk
+        for (int c = 0; c < nch_even; c++) X.ch.push_back(X.ch.back() + nb / nch_even + (c < nb % nch_even ? 1 : 0));
         const int nch = (int)X.ch.size() - 1;
         while ((int)X.ev.size() < nch) {
             hipEvent_t e, en;
@@ -690,6 +701,7 @@ struct GpuOps {
             VS_HIP(hipEventRecord(X.ev[c], xp));
         }
         VS_HIP(hipEventRecord(region_done[X.region], xp));
+        VS_HIP(hipEventRecord(xdone, xp));  // covers xs too (xp waited for every chunk's network)
         return VS_OK;
     }
     // The batch's extraction: the one prefetched for exactly these buffers, or enqueued now; then the
@@ -715,15 +727,20 @@ struct GpuOps {
         for (int b = 0; b < nb; b++) frames[b]->slot = X.region * B + b;
         if (hint.nb > 0) {
             XBatch& N = xb[xcur ^ 1];
-            N.pending = true;
             const int hnb = hint.nb;
             const uint8_t* hb = hint.bgr;
             const float* hd = hint.depth;
             hint.nb = 0;
+            // pending only once the whole enqueue succeeded: a half-built prefetch is never claimed
+            auto task = [this, &N, hnb, hb, hd] {
+                const int r = enqueue_extraction(N, hnb, hb, hd);
+                N.pending = r == VS_OK;
+                return r;
+            };
             if (async_enqueue)
-                aq.submit([this, &N, hnb, hb, hd] { return enqueue_extraction(N, hnb, hb, hd); });
+                aq.submit(task);
             else
-                VS_CHECK(enqueue_extraction(N, hnb, hb, hd));
+                VS_CHECK(task());
         }
         return VS_OK;
     }
@@ -1556,11 +1573,17 @@ int vs_slam_process_batch_dev(vs_slam* sl, int B, const uint8_t* d_bgr, const fl
     o.next_ready = nullptr;
     o.cspec.valid = false;
     o.spec_req.pending = false;
+    // The helper's next-batch enqueue has finished before the call returns, so no thread of this
+    // vs_slam touches the context's scratch once the caller has it back; the prefetched batch's
+    // device work is ordered before the caller's own use of that scratch by vs::scratch_order.
+    const int rj = o.aq.join();
+    if (rc == VS_OK) rc = rj;
     if (rc != VS_OK) {
-        (void)o.aq.join();
         (void)hipStreamSynchronize(o.xs);  // nothing may still write the pool after an error
         (void)hipStreamSynchronize(o.xp);
         (void)hipStreamSynchronize(o.s2);
+        o.xb[o.xcur ^ 1].pending = false;  // a prefetch that failed (or raced an error) is dropped
+        o.batch_region = o.xb[o.xcur].region ^ 1;
         sl->dense_depth.clear();
         sl->dense_R.clear();
         sl->dense_t.clear();

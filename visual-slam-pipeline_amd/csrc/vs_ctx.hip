@@ -171,6 +171,12 @@ static int upload_weights(vs_ctx* ctx) {
 
 int sp_postprocess_check(vs_ctx* ctx, int B, hipStream_t s);  // sp_post.hip
 
+int scratch_order(vs_ctx* ctx, hipStream_t s) {
+    if (!ctx->scratch_busy || s == ctx->scratch_owner[0] || s == ctx->scratch_owner[1]) return VS_OK;
+    VS_HIP(hipStreamWaitEvent(s, ctx->scratch_busy, 0));
+    return VS_OK;
+}
+
 static hipStream_t pick(vs_ctx* ctx, void* stream) { return stream ? (hipStream_t)stream : ctx->stream; }
 
 template <class T>
@@ -274,7 +280,8 @@ void vs_destroy(vs_ctx* ctx) {
     DevBuf* bufs[] = {&ctx->gray,  &ctx->act0,   &ctx->act1,   &ctx->semi,   &ctx->dgrid,  &ctx->heat,
                       &ctx->state, &ctx->flags,  &ctx->keys,   &ctx->keycnt, &ctx->h_img,  &ctx->h_kps,
                       &ctx->h_desc, &ctx->h_n,   &ctx->h_aux0, &ctx->h_aux1, &ctx->h_aux2, &ctx->h_aux3,
-                      &ctx->h_aux4, &ctx->h_aux5, &ctx->match_keys, &ctx->match_cnt, &ctx->nms_list, &ctx->norms_sets, &ctx->tlm, &ctx->ba, &ctx->pnp};
+                      &ctx->h_aux4, &ctx->h_aux5, &ctx->match_keys, &ctx->match_cnt, &ctx->nms_list, &ctx->norms_sets, &ctx->tlm, &ctx->ba, &ctx->pnp,
+                      &ctx->lmax, &ctx->tie_totals};
     for (DevBuf* b : bufs) b->release();
     for (auto& st : ctx->prof)
         for (auto& pr : st.pending) {
@@ -802,6 +809,20 @@ int vs_local_ba(vs_ctx* ctx, int N, double* R_world, double* t_world, int M, dou
 }
 
 // ---- profiling ----------------------------------------------------------------------------------
+int vs_nms_tie_stats(vs_ctx* ctx, long long out[4], int reset) {
+    VS_ARG(ctx && out, "vs_nms_tie_stats: null argument");
+    VS_HIP(hipSetDevice(ctx->device));
+    unsigned long long t[4] = {0, 0, 0, 0};
+    if (ctx->tie_totals.p) {
+        // every stream that post-processes on this context (a vs_slam's extraction streams included)
+        VS_HIP(hipDeviceSynchronize());
+        VS_HIP(hipMemcpy(t, ctx->tie_totals.p, sizeof(t), hipMemcpyDeviceToHost));
+        if (reset) VS_HIP(hipMemset(ctx->tie_totals.p, 0, sizeof(t)));
+    }
+    for (int i = 0; i < 4; i++) out[i] = (long long)t[i];
+    return VS_OK;
+}
+
 int vs_profile_enable(vs_ctx* ctx, int on) {
     VS_ARG(ctx, "vs_profile_enable: null ctx");
     ctx->prof_on = on != 0;

@@ -94,11 +94,18 @@ struct vs_ctx {
     // host-API staging
     vs::DevBuf h_img, h_kps, h_desc, h_n, h_aux0, h_aux1, h_aux2, h_aux3, h_aux4, h_aux5;
     vs::DevBuf match_keys, match_cnt, norms_sets, tlm, ba, pnp;
+    vs::DevBuf lmax;        // NMS: strict local maxima (score bits) per frame
+    vs::DevBuf tie_totals;  // NMS tie accounting since the last reset: {frames, frames with a tie, window, cut}
 
     bool prof_on = false;
     std::vector<vs::ProfStage> prof;
     std::vector<hipEvent_t> event_pool;
     std::mutex prof_mu;  // a vs_slam enqueues its next batch's extraction from a helper thread
+    // A vs_slam's extraction streams use the scratch above (gray .. nms_list) asynchronously, also
+    // after its call returned (the prefetched next batch).  Work on any other stream that uses that
+    // scratch first waits for scratch_busy (the last extraction it enqueued); null without a vs_slam.
+    hipEvent_t scratch_busy = nullptr;
+    hipStream_t scratch_owner[2] = {nullptr, nullptr};
 };
 
 namespace vs {
@@ -112,6 +119,10 @@ struct ProfScope {
     ProfScope(vs_ctx* c, const char* name, hipStream_t st);
     ~ProfScope();
 };
+
+// Orders work on stream s that uses the context's network / NMS scratch after a vs_slam's
+// in-flight extraction (no-op on the vs_slam's own extraction streams and without one).
+int scratch_order(vs_ctx* ctx, hipStream_t s);
 
 // ---- stage launchers (return VS_OK or an error code; enqueue on `s` only) ------------------
 // Network: d_bgr is B x h x w x 3 u8 (or gray u8 when channels == 1, or nullptr when d_gray01

@@ -259,3 +259,40 @@ def stationary_sequence(n_move1=25, n_hold=12, n_move2=20, seed=SEED, dt=1.0 / 1
     return dict(bgr=np.stack([o[0] for o in out]), depth=np.stack([o[1] for o in out]),
                 R_wc=np.stack([p[0] for p in poses]), t_wc=np.stack([p[1] for p in poses]), timestamps=ts,
                 accel=acc, moving=moving)
+
+
+def _rodrigues_y(a):
+    """Rotation by angle a about the camera y axis (the planar sweep of the BA stress window)."""
+    c, s_ = np.cos(a), np.sin(a)
+    k = np.array([0.0, 1.0, 0.0])
+    Kx = np.array([[0, -k[2], k[1]], [k[2], 0, -k[0]], [-k[1], k[0], 0]])
+    return np.eye(3) + s_ * Kx + (1 - c) * Kx @ Kx
+
+
+def ba_window(N, M, seed, span=5, noise=0.5, pert=0.03):
+    """BASELINE config[2]'s local-BA stress window: N keyframes along a sweep,
+    M points each visible from `span` consecutive keyframes (the sliding-window structure), pixel
+    noise `noise`, points perturbed by `pert` m.  Returns R, t (world-from-camera), true points,
+    perturbed points, observation keyframe / point indices and pixels."""
+    rng = np.random.default_rng(seed)
+    K = (525.0, 525.0, 319.5, 239.5)
+    Rs = np.array([_rodrigues_y(0.03 * i) if i else np.eye(3) for i in range(N)])
+    ts = np.array([[0.2 * i, 0.0, 0.05 * i] for i in range(N)])
+    first = rng.integers(0, max(1, N - span + 1), M)
+    # place point j in front of keyframe first[j] + span // 2
+    kc = np.minimum(first + span // 2, N - 1)
+    pc = np.stack([rng.uniform(-1.5, 1.5, M), rng.uniform(-1.0, 1.0, M), rng.uniform(3.0, 6.0, M)], 1)
+    P = np.einsum("mij,mj->mi", Rs[kc], pc) + ts[kc]
+    kf, pt, uv = [], [], []
+    for i in range(N):
+        cam = (P - ts[i]) @ Rs[i]
+        u = K[0] * cam[:, 0] / cam[:, 2] + K[2]
+        v = K[1] * cam[:, 1] / cam[:, 2] + K[3]
+        vis = np.flatnonzero((first <= i) & (i < first + span) & (cam[:, 2] > 0.1) & (u > 0) & (u < 640) &
+                             (v > 0) & (v < 480))
+        for j in rng.permutation(vis):
+            kf.append(i)
+            pt.append(j)
+            uv.append([u[j] + rng.normal() * noise, v[j] + rng.normal() * noise])
+    P0 = P + rng.normal(size=P.shape) * pert
+    return Rs, ts, P, P0, np.array(kf, np.int32), np.array(pt, np.int32), np.array(uv)

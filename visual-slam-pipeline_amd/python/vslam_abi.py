@@ -109,6 +109,7 @@ _SIG = {
     "vs_pgo_transform_points": (_I, [_P, _I, _P, _P, _P, _P, _I, _P, _P]),
     "vs_slam_run_posthoc_pgo": (_I, [_P, _P]),
     "vs_profile_enable": (_I, [_P, _I]),
+    "vs_nms_tie_stats": (_I, [_P, _P, _I]),
     "vs_profile_reset": (_I, [_P]),
     "vs_profile_read": (_I, [_P, _I, _P, _P, _P, _P]),
 }
@@ -427,6 +428,13 @@ class Context:
         assert idx.shape == (F,)
         _check(self.lib.vs_spcf_write_dev(self.h, os.fsencode(path), F, _ptr(idx), d_kps, d_desc, d_n, cap,
                                           int(append), stream))
+
+    def tie_stats(self, reset=False):
+        """NMS tie totals since the last reset: frames, frames with a tie, window ties, cut ties
+        (vs_nms_tie_stats)."""
+        out = np.zeros(4, np.int64)
+        _check(self.lib.vs_nms_tie_stats(self.h, _ptr(out), 1 if reset else 0))
+        return dict(zip(("frames", "frames_with_tie", "window_ties", "cut_ties"), (int(v) for v in out)))
 
     def profile(self, on=True):
         _check(self.lib.vs_profile_enable(self.h, 1 if on else 0))
