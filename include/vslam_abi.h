@@ -63,9 +63,11 @@ int         vs_abi_version(void);
 const char* vs_last_error(void);
 
 /* Replaces FeatureExtractor::init (FeatureExtractor.h:18, FeatureExtractor.cpp:22-44).
- * superpoint_weights: path of a VSPW weight file (see vs_superpoint_save_weights), or NULL
- * for the seeded synthetic He-normal weights (seed VS_SYNTH_WEIGHT_SEED).  Unlike the
- * reference, a failure is reported (VS_ERR_IO) instead of silently switching to ORB. */
+ * superpoint_weights: the reference's own model file (models/superpoint_v1.onnx, Slam.cpp:28-31:
+ * an ONNX SuperPoint export, read by the library's protobuf reader and mapped through the graph's
+ * Conv nodes), a VSPW weight file (see vs_superpoint_save_weights), or NULL for the seeded
+ * synthetic He-normal weights (seed VS_SYNTH_WEIGHT_SEED).  Unlike the reference, a failure is
+ * reported (VS_ERR_IO, vs_last_error) instead of silently switching to ORB. */
 #define VS_SYNTH_WEIGHT_SEED 20261015ull
 int  vs_create(int device, const char* superpoint_weights, vs_ctx** out);
 void vs_destroy(vs_ctx* ctx);
@@ -76,6 +78,12 @@ void* vs_stream(vs_ctx* ctx); /* the context's hipStream_t */
  * conv4a conv4b convPa convPb convDa convDb).  Used by tests to build the fp32 torch reference. */
 size_t vs_superpoint_num_params(void);
 int    vs_superpoint_get_weights(vs_ctx* ctx, float* out, size_t count);
+/* Host only (no device needed): the canonical weights (count = vs_superpoint_num_params()) read
+ * from an ONNX SuperPoint export — the file FeatureExtractor::init hands to ONNX Runtime
+ * (FeatureExtractor.cpp:22-44) — mapped through the graph's Conv nodes; and the seeded synthetic
+ * weights vs_create(…, NULL, …) uses. */
+int    vs_superpoint_onnx_weights(const char* onnx_path, float* out, size_t count);
+int    vs_superpoint_synth_weights(float* out, size_t count);
 int    vs_superpoint_save_weights(vs_ctx* ctx, const char* path);
 
 /* ---- A1-A6: FeatureExtractor::extract (FeatureExtractor.cpp:49-81, 87-207, 219-259) ---- */
@@ -335,13 +343,19 @@ int vs_slam_map(vs_slam* slam, int cap, double* pos, uint8_t* valid, int* n);
  * min-max normalisation when the range exceeds 1e-6, :96-109).  The reference never consumes the
  * result; BASELINE config[4] runs it per frame. */
 typedef struct vs_midas vs_midas;
-/* weights_path: a VSMW file (tools/midas_to_vsmw.py converts a MiDaS state_dict, BatchNorm folded)
- * or NULL for seeded He-normal weights. */
+/* weights_path: the reference's own model file (models/midas_v21_small_256.onnx, Slam.cpp:30-31:
+ * Conv nodes in graph order, BatchNormalization folded), a VSMW file (tools/midas_to_vsmw.py
+ * converts a MiDaS state_dict, BatchNorm folded) or NULL for seeded He-normal weights. */
 int vs_midas_create(vs_ctx* ctx, const char* weights_path, vs_midas** out);
 void vs_midas_destroy(vs_midas* m);
 size_t vs_midas_num_params(void);
 double vs_midas_flops_per_frame(void);
 int vs_midas_get_weights(vs_midas* m, float* out, size_t count);
+/* Host only: canonical MiDaS weights from an ONNX export of midas_v21_small_256 (the file
+ * DepthEstimator::init hands to ONNX Runtime, DepthEstimator.cpp:15-36; BatchNormalization folded)
+ * and the seeded synthetic weights vs_midas_create(…, NULL, …) uses. */
+int vs_midas_onnx_weights(const char* onnx_path, float* out, size_t count);
+int vs_midas_synth_weights(float* out, size_t count);
 /* B frames d_bgr [B][h][w][3] u8 -> d_depth [B][h][w] fp32 in [0, 1] (enqueue only). */
 int vs_midas_estimate_dev(vs_midas* m, int B, const uint8_t* d_bgr, int h, int w, float* d_depth, void* stream);
 /* The three stages separately (tests): d_input [B][256][256][3] fp32 (NHWC, normalised),

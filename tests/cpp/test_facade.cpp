@@ -171,6 +171,22 @@ int main() {
     const int tracked = track_local_map(ctx, map, k1, d1, I3, t1, kp_to_mp, &obs);
     EXPECT(tracked > 20 && (int)obs.size() == tracked && kp_to_mp.size() == k1.size());
 
+    // ---- FeatureExtractor::init on the reference's model file (Slam.cpp:29: model_dir +
+    // "/superpoint_v1.onnx"): an ONNX export of the same weights gives the same features ----
+    if (const char* onnx = std::getenv("VS_FACADE_SUPERPOINT_ONNX")) {
+        FeatureExtractor fx;
+        EXPECT(fx.init(onnx));
+        EXPECT(fx.using_superpoint());
+        std::vector<KeyPoint> kx;
+        Descriptors dx;
+        fx.extract(a, kx, dx);
+        EXPECT(kx.size() == k0.size() && std::memcmp(kx.data(), k0.data(), k0.size() * sizeof(KeyPoint)) == 0);
+        EXPECT(dx.rows == d0.rows && dx.data == d0.data);
+        FeatureExtractor fbad;
+        EXPECT(!fbad.init(std::string(onnx) + ".missing"));  // reported, as the reference's init returns false
+        std::printf("facade: FeatureExtractor::init(%s) ok\n", onnx);
+    }
+
     // ---- Frame::detect_features (Frame.cpp:33-38) + depth (Frame.cpp:47-54) ----
     FeatureExtractor fe2;
     EXPECT(fe2.init(""));

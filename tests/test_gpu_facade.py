@@ -13,8 +13,14 @@ pytestmark = pytest.mark.gpu
 PKG = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "visual-slam-pipeline_amd")
 
 
-def test_cpp_facade_program():
+def test_cpp_facade_program(tmp_path):
+    import onnx_writer
+    import vslam_abi
+    onnx = tmp_path / "superpoint_v1.onnx"  # FeatureExtractor::init on the reference's kind of model file
+    onnx.write_bytes(onnx_writer.superpoint_model(vslam_abi.superpoint_synth_weights()))
     subprocess.run(["make", "-C", PKG, "-s", "facade_test"], check=True)
-    r = subprocess.run([os.path.join(PKG, "facade_test")], capture_output=True, text=True, timeout=300)
+    env = dict(os.environ, VS_FACADE_SUPERPOINT_ONNX=str(onnx))
+    r = subprocess.run([os.path.join(PKG, "facade_test")], capture_output=True, text=True, timeout=300, env=env)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "FACADE OK" in r.stdout, r.stdout
+    assert "FeatureExtractor::init(" in r.stdout, r.stdout

@@ -34,6 +34,7 @@
 #include <vector>
 
 #include "vs_internal.h"
+#include "../host/onnx_weights.h"
 
 namespace vs {
 namespace midas {
@@ -563,6 +564,28 @@ std::vector<float> synth(uint64_t seed) {
     return w;
 }
 
+// The canonical weights from an ONNX export of midas_v21_small_256: the graph's convolutions in
+// node order (BatchNormalization folded) checked layer by layer against the network's definition.
+bool from_onnx(const char* path, std::vector<float>& w, std::string& err) {
+    const Net& N = net();
+    std::vector<vs_onnx::LayerSpec> spec(N.layers.size());
+    std::vector<int> stride(N.layers.size(), 1);
+    for (const Step& st : N.steps)
+        if (st.layer >= 0) stride[st.layer] = st.stride;
+    for (size_t l = 0; l < N.layers.size(); l++) {
+        const LayerDef& L = N.layers[l];
+        spec[l] = {L.kind == K_DW, L.cin, L.cout, L.k, stride[l], L.bias};
+    }
+    vs_onnx::Model model;
+    if (!vs_onnx::load(path, model, err)) return false;
+    if (!vs_onnx::midas_weights(model, spec, w, err)) return false;
+    if (w.size() != N.num_params()) {
+        err = "MiDaS graph: parameter count mismatch";
+        return false;
+    }
+    return true;
+}
+
 struct DevW {
     float* w = nullptr;
     float* b = nullptr;
@@ -747,6 +770,25 @@ extern "C" {
 
 size_t vs_midas_num_params(void) { return midas::net().num_params(); }
 
+int vs_midas_onnx_weights(const char* path, float* out, size_t count) {
+    VS_ARG(path && out && count == midas::net().num_params(), "vs_midas_onnx_weights: bad arguments");
+    std::vector<float> w;
+    std::string err;
+    if (!midas::from_onnx(path, w, err)) {
+        set_error("vs_midas_onnx_weights: " + err);
+        return VS_ERR_IO;
+    }
+    std::memcpy(out, w.data(), count * sizeof(float));
+    return VS_OK;
+}
+
+int vs_midas_synth_weights(float* out, size_t count) {
+    VS_ARG(out && count == midas::net().num_params(), "vs_midas_synth_weights: bad arguments");
+    const std::vector<float> w = midas::synth(VS_SYNTH_WEIGHT_SEED + 1);
+    std::memcpy(out, w.data(), count * sizeof(float));
+    return VS_OK;
+}
+
 double vs_midas_flops_per_frame(void) { return midas::net().flops(); }
 
 int vs_midas_create(vs_ctx* ctx, const char* weights_path, vs_midas** out) {
@@ -757,7 +799,15 @@ int vs_midas_create(vs_ctx* ctx, const char* weights_path, vs_midas** out) {
     if (!m) return VS_ERR_NOMEM;
     m->ctx = ctx;
     const size_t np = midas::net().num_params();
-    if (weights_path) {
+    if (weights_path && vs_onnx::looks_like_onnx(weights_path)) {
+        // the reference's own model file (DepthEstimator.cpp:15-36: models/midas_v21_small_256.onnx)
+        std::string err;
+        if (!midas::from_onnx(weights_path, m->h_weights, err)) {
+            delete m;
+            set_error("vs_midas_create: " + err);
+            return VS_ERR_IO;
+        }
+    } else if (weights_path) {
         FILE* f = std::fopen(weights_path, "rb");
         if (!f) {
             delete m;

@@ -15,6 +15,7 @@
 
 #include "cr_math.h"
 #include "vs_internal.h"
+#include "../host/onnx_weights.h"
 
 namespace vs {
 
@@ -216,6 +217,26 @@ const char* vs_last_error(void) { return g_err.c_str(); }
 
 size_t vs_superpoint_num_params(void) { return num_params(); }
 
+int vs_superpoint_onnx_weights(const char* path, float* out, size_t count) {
+    VS_ARG(path && out && count == num_params(), "vs_superpoint_onnx_weights: bad arguments");
+    std::string err;
+    vs_onnx::Model model;
+    std::vector<float> w;
+    if (!vs_onnx::load(path, model, err) || !vs_onnx::superpoint_weights(model, w, err)) {
+        set_error("vs_superpoint_onnx_weights: " + err);
+        return VS_ERR_IO;
+    }
+    std::memcpy(out, w.data(), count * sizeof(float));
+    return VS_OK;
+}
+
+int vs_superpoint_synth_weights(float* out, size_t count) {
+    VS_ARG(out && count == num_params(), "vs_superpoint_synth_weights: bad arguments");
+    const std::vector<float> w = synth_weights(VS_SYNTH_WEIGHT_SEED);
+    std::memcpy(out, w.data(), count * sizeof(float));
+    return VS_OK;
+}
+
 int vs_create(int device, const char* weights_path, vs_ctx** out) {
     VS_ARG(out, "vs_create: out is null");
     *out = nullptr;
@@ -225,7 +246,17 @@ int vs_create(int device, const char* weights_path, vs_ctx** out) {
     VS_HIP(hipSetDevice(device));
     vs_ctx* ctx = new vs_ctx();
     ctx->device = device;
-    if (weights_path) {
+    if (weights_path && vs_onnx::looks_like_onnx(weights_path)) {
+        // the reference's own model file (FeatureExtractor.cpp:22-44: models/superpoint_v1.onnx)
+        std::string err;
+        vs_onnx::Model model;
+        if (!vs_onnx::load(weights_path, model, err) || !vs_onnx::superpoint_weights(model, ctx->h_weights, err) ||
+            ctx->h_weights.size() != num_params()) {
+            delete ctx;
+            set_error("vs_create: " + (err.empty() ? std::string("SuperPoint parameter count mismatch") : err));
+            return VS_ERR_IO;
+        }
+    } else if (weights_path) {
         FILE* f = std::fopen(weights_path, "rb");
         if (!f) {
             delete ctx;

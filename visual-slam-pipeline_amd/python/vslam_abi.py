@@ -110,6 +110,10 @@ _SIG = {
     "vs_slam_run_posthoc_pgo": (_I, [_P, _P]),
     "vs_profile_enable": (_I, [_P, _I]),
     "vs_nms_tie_stats": (_I, [_P, _P, _I]),
+    "vs_superpoint_onnx_weights": (_I, [ctypes.c_char_p, _P, ctypes.c_size_t]),
+    "vs_superpoint_synth_weights": (_I, [_P, ctypes.c_size_t]),
+    "vs_midas_onnx_weights": (_I, [ctypes.c_char_p, _P, ctypes.c_size_t]),
+    "vs_midas_synth_weights": (_I, [_P, ctypes.c_size_t]),
     "vs_profile_reset": (_I, [_P]),
     "vs_profile_read": (_I, [_P, _I, _P, _P, _P, _P]),
 }
@@ -152,6 +156,36 @@ def _check(rc):
 
 def _ptr(a):
     return a.ctypes.data_as(ctypes.c_void_p) if a is not None else None
+
+
+def superpoint_onnx_weights(path):
+    """Canonical SuperPoint weights read from an ONNX export (host only, vs_superpoint_onnx_weights)."""
+    lib = load_library()
+    out = np.zeros(lib.vs_superpoint_num_params(), np.float32)
+    _check(lib.vs_superpoint_onnx_weights(os.fsencode(path), _ptr(out), out.size))
+    return out
+
+
+def superpoint_synth_weights():
+    lib = load_library()
+    out = np.zeros(lib.vs_superpoint_num_params(), np.float32)
+    _check(lib.vs_superpoint_synth_weights(_ptr(out), out.size))
+    return out
+
+
+def midas_onnx_weights(path):
+    """Canonical MiDaS v2.1-small weights from an ONNX export (host only, vs_midas_onnx_weights)."""
+    lib = load_library()
+    out = np.zeros(lib.vs_midas_num_params(), np.float32)
+    _check(lib.vs_midas_onnx_weights(os.fsencode(path), _ptr(out), out.size))
+    return out
+
+
+def midas_synth_weights():
+    lib = load_library()
+    out = np.zeros(lib.vs_midas_num_params(), np.float32)
+    _check(lib.vs_midas_synth_weights(_ptr(out), out.size))
+    return out
 
 
 def _k_array(K):
