@@ -122,9 +122,10 @@ __global__ __launch_bounds__(64 * NWQ * NWT) void k_match(MatchArgs a) {
     constexpr int NB = NC > 1 ? NBUF : 1;  // LDS buffers (1: a second barrier per chunk, half the LDS)
     constexpr int RS4 = KC / 4 + 2;        // row stride in float4 (KC + 8 floats)
     constexpr int GR = KC / 16;            // 16-k groups per row and chunk
-    constexpr int GPT = R * GR / NTH;      // groups per thread and chunk
+    constexpr int GPT = (R * GR + NTH - 1) / NTH;  // groups per thread and chunk (the last may be partial)
+    constexpr bool GPART = GPT * NTH != R * GR;
     constexpr int NR = R / NW;             // norm rows per wave
-    static_assert(GPT * NTH == R * GR && NR * NW == R && NR <= 64, "staging / norm split");
+    static_assert(NR * NW == R && NR <= 64, "norm split");
     __shared__ float4 sbuf[NB][R * RS4];
     __shared__ float s_norm[R];
     __shared__ unsigned long long s_top[NWT > 1 ? NWT : 1][TQ][2];
@@ -159,7 +160,7 @@ __global__ __launch_bounds__(64 * NWQ * NWT) void k_match(MatchArgs a) {
     const float4* src[GPT];
 #pragma unroll
     for (int u = 0; u < GPT; u++) {
-        const int G = tid + NTH * u, row = G / GR, q4 = G % GR;
+        const int G = min(tid + NTH * u, R * GR - 1), row = G / GR, q4 = G % GR;
         const float* base = row < TQ ? Q + (size_t)min(q0 + row, n1 - 1) * 256
                                      : T + (size_t)min(t0 + row - TQ, n2 - 1) * 256;
         src[u] = reinterpret_cast<const float4*>(base) + 4 * q4;
@@ -182,6 +183,7 @@ __global__ __launch_bounds__(64 * NWQ * NWT) void k_match(MatchArgs a) {
 #pragma unroll
         for (int u = 0; u < GPT; u++) {
             const int G = tid + NTH * u, row = G / GR, q4 = G % GR;
+            if (GPART && u == GPT - 1 && G >= R * GR) continue;  // (loaded a duplicate group; not stored)
             float4* d = &sbuf[buf][row * RS4 + 4 * q4];
             d[0] = make_float4(r[u][0].x, r[u][1].x, r[u][2].x, r[u][3].x);
             d[1] = make_float4(r[u][0].y, r[u][1].y, r[u][2].y, r[u][3].y);
@@ -511,6 +513,16 @@ static void launch(MatchArgs& a, int P, int cap_q, int cap_t, bool norms, hipStr
         launch_tile<2, 2, 32, 32, 32, 1, 8>(a, P, cap_q, cap_t, norms, s);
     else if (force && std::strcmp(force, "t80") == 0)
         launch_tile<5, 1, 16, 80, 32, 1>(a, P, cap_q, cap_t, norms, s);
+    else if (force && std::strcmp(force, "q32t64") == 0)
+        launch_tile<1, 4, 32, 16, 32, 1>(a, P, cap_q, cap_t, norms, s);
+    else if (force && std::strcmp(force, "q32t32") == 0)
+        launch_tile<2, 2, 16, 16, 32, 1>(a, P, cap_q, cap_t, norms, s);
+    else if (force && std::strcmp(force, "q64t32") == 0)
+        launch_tile<2, 2, 32, 16, 32, 1>(a, P, cap_q, cap_t, norms, s);
+    else if (force && std::strcmp(force, "w8") == 0)
+        launch_tile<2, 4, 32, 16, 32, 1>(a, P, cap_q, cap_t, norms, s);
+    else if (force && std::strcmp(force, "w8k64") == 0)
+        launch_tile<2, 4, 32, 16, 64, 1>(a, P, cap_q, cap_t, norms, s);
     else
         launch_tile<2, 2, 32, 32, 32, 1>(a, P, cap_q, cap_t, norms, s);
 }
