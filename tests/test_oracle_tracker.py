@@ -125,3 +125,33 @@ def test_oracle_tracker_initial_pose(oracle, scene):
     ids, ts, R, t = S.trajectory()
     gt = np.array([f["t_wc"] for f in seq[:5]])
     assert np.abs(t - gt).max() < 0.05  # world frame = the given initial pose (EKF lag along the path)
+
+
+def test_oracle_tracker_pnp_recovery_succeeds():
+    """Slam::try_pnp_recovery's success branch (Slam.cpp:535-613): on the loop's second lap one
+    frame sees only landmarks the recent frames never observed but the same place's first-lap
+    keyframes did (tests/landmarks.py): no ratio matches against the reference keyframe or the last
+    frame, enough against the map, so PnP(300, 15) recovers the pose, the frame becomes a keyframe
+    with depth points and the EKF restarts at it; the trajectory stays on the ground truth."""
+    import oracle_py as oracle
+    import landmarks
+    L = synth.loop_sequence(126, workers=8)
+    n, kj = 134, 131
+    feats, _ = landmarks.recovery_sequence(L, n, kj)
+    S = oracle.Slam()
+    T0 = 1311868164.0
+    before = after = None
+    for g in range(n):
+        if g == kj:
+            before = S.stats().copy()
+        assert S.process(*feats[g], L["depth"][g % 126], T0 + 0.1 * g, 3 * g)
+        if g == kj:
+            after = S.stats().copy()
+    st = S.stats()
+    assert (before[6], after[6], st[6], st[7]) == (0, 1, 1, 0)  # recovered at frame kj, no failure
+    assert after[9] == before[9] + 1 and after[14] > before[14]  # a keyframe with depth points
+    S.finish()
+    ids, ts, R, t = S.trajectory()
+    gi = np.round((ts - T0) / 0.1).astype(int) % 126
+    a = ate.compute_ate(ts, t, ts, L["t_wc"][gi])
+    assert a["ate_rmse"] < 0.03, a
