@@ -427,8 +427,9 @@ int vs_spcf_read(const char* path, int max_frames, int cap, int* frame_idx, vs_k
  * processing time; a point joins the cloud the first time its voxel (floor(p / voxel_size) per
  * axis) is seen, in the reference's insertion order (frame, then row-major grid).  The cloud lives
  * in HBM (a voxel hash table of 2^table_log2 slots plus max_points x 3 fp64).  Voxel coordinates
- * must lie in [-2^20, 2^20) (+-20 km at 2 cm); beyond that, a full table or more than max_points
- * points, vs_dense_size reports VS_ERR_CAPACITY. */
+ * within [-2^20, 2^20) (+-20 km at 2 cm) are keyed exactly, farther ones (a diverged pose) by a
+ * 63-bit hash of the three ints; a full table or more than max_points points: vs_dense_size
+ * reports VS_ERR_CAPACITY.  vs_dense_write_ply writes no file for an empty cloud. */
 typedef struct vs_dense vs_dense;
 typedef struct vs_dense_config {
     int pixel_step;     /* Config::DENSE_PIXEL_STEP (8) */

@@ -3,7 +3,7 @@
 same order (integer voxel keys and the reference's fp64 expressions, no contraction), across
 integrate calls of 1, 5 and 40 frames (two launch groups), repeated frames, rejected depths; the
 PLY text equals the reference's std::fixed / setprecision(6) output; overflow of the cloud, the
-table or the packable voxel range is reported, never silent; a tracker with a cloud attached fuses
+table is reported, never silent; voxels far outside the packed range join the cloud like any other; a tracker with a cloud attached fuses
 every processed frame with its pose right after Slam::process_frame."""
 import numpy as np
 import pytest
@@ -76,11 +76,31 @@ def test_dense_overflow_is_reported(vsctx):
         _gpu_integrate(D, frames)
         with pytest.raises(vslam_abi.VSError, match="VS_ERR_CAPACITY"):
             D.size()
-    far = [(np.full((480, 640), 1.0, np.float32), np.eye(3), np.array([1e5, 0.0, 0.0]))]
-    with vslam_abi.Dense(vsctx, table_log2=12, max_points=1024) as D:
+
+
+
+def test_dense_far_voxels_join_the_cloud(vsctx, oracle, tmp_path):
+    """Voxels beyond the packed +-2^20 range (a diverged pose 100 km / 1e12 m out, and a NaN pose
+    whose voxels are INT_MIN as x86 (int)floor gives) join the cloud in order like any other, as
+    the reference's unordered_set inserts them (ADVICE r02): no global failure, the PLY is written;
+    an empty cloud writes no PLY (main.cpp:1462)."""
+    frames = _frames(3, 480, 640, 9)
+    far = [(frames[0][0], np.eye(3), np.array([1e5, 0.0, 0.0])), frames[1],
+           (frames[2][0], np.eye(3), np.array([1e12, -3e11, 7e10])),
+           (frames[2][0], np.eye(3), np.array([np.nan, 0.0, 0.0]))]
+    O = oracle.Dense()
+    for f in far:
+        O.integrate(*f)
+    with vslam_abi.Dense(vsctx, table_log2=20, max_points=1 << 18) as D:
         _gpu_integrate(D, far)
-        with pytest.raises(vslam_abi.VSError, match="VS_ERR_CAPACITY"):
-            D.size()
+        got, ref = D.points(), O.points()
+        assert got.shape == ref.shape and got.shape[0] > 0
+        assert np.array_equal(got.view(np.uint64), ref.view(np.uint64))
+        D.write_ply(tmp_path / "far.ply")
+        assert (tmp_path / "far.ply").exists()
+    with vslam_abi.Dense(vsctx, table_log2=12, max_points=1024) as D:
+        D.write_ply(tmp_path / "empty.ply")
+    assert not (tmp_path / "empty.ply").exists()
 
 
 def test_tracker_fuses_processed_frames(vsctx, oracle):

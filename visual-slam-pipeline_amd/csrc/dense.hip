@@ -35,7 +35,7 @@ constexpr int kDF = 32;                           // frames per launch group (ke
 constexpr unsigned long long kEmpty = ~0ull;
 constexpr int kPackBits = 21;
 constexpr int kPackLim = 1 << (kPackBits - 1);    // voxel coordinates in [-2^20, 2^20)
-constexpr unsigned kErrTable = 1u, kErrCapacity = 2u, kErrRange = 4u;
+constexpr unsigned kErrTable = 1u, kErrCapacity = 2u;
 
 struct DenseFrames {
     const float* depth[kDF];
@@ -107,8 +107,16 @@ __global__ __launch_bounds__(256) void k_dense_insert(DenseArgs a, DenseFrames F
             key = (key << kPackBits) | ((unsigned long long)(unsigned)vox[k] & ((1ull << kPackBits) - 1));
         }
         if (!packable) {
-            atomicOr(a.err, kErrRange);
-        } else {
+            // Outside +-2^20 voxels (a diverged pose; INT_MIN from NaN / overflow): the reference
+            // still inserts the (int, int, int) tuple.  Such voxels get a 63-bit hash of all 96 bits
+            // with the top bit set — disjoint from the packed keys (top bit 0), unique unless two
+            // out-of-range voxels collide in 63 bits (documented).
+            unsigned long long hv = mix64(((unsigned long long)(unsigned)vox[0] << 32) | (unsigned)vox[1]);
+            hv = mix64(hv ^ (unsigned long long)(unsigned)vox[2] ^ 0x9E3779B97F4A7C15ull);
+            key = (hv & 0x7FFFFFFFFFFFFFFFull) | 0x8000000000000000ull;
+            if (key == kEmpty) key ^= 1ull;
+        }
+        {
             const unsigned long long stamp = a.seq0 + (unsigned long long)g;
             unsigned long long h = mix64(key) & a.mask;
             for (unsigned long long probe = 0; probe <= a.mask; probe++) {
@@ -364,10 +372,6 @@ int vs_dense_size(vs_dense* d, long long* n) {
         set_error("vs_dense: more points than max_points");
         return VS_ERR_CAPACITY;
     }
-    if (st.err & kErrRange) {
-        set_error("vs_dense: a voxel coordinate is outside the packable range [-2^20, 2^20)");
-        return VS_ERR_CAPACITY;
-    }
     return VS_OK;
 }
 
@@ -386,6 +390,7 @@ int vs_dense_write_ply(vs_dense* d, const char* path) {
     VS_ARG(d && path, "vs_dense_write_ply: null argument");
     long long n = 0;
     VS_CHECK(vs_dense_size(d, &n));
+    if (n == 0) return VS_OK;  // main.cpp:1462: no file for an empty cloud
     std::vector<double> p((size_t)n * 3);
     if (n > 0) VS_HIP(hipMemcpy(p.data(), d->cloud.p, p.size() * sizeof(double), hipMemcpyDeviceToHost));
     FILE* f = std::fopen(path, "w");
