@@ -385,13 +385,18 @@ int vs_batch_unique_id(void* id);
 int vs_batch_create(vs_ctx* ctx, int B, int h, int w, int rank, int world, const void* id, vs_batch** out);
 void vs_batch_destroy(vs_batch* b);
 /* One step (synchronous): this rank's B frames d_bgr [B][h][w][3] u8 and depth [B][h][w] metres,
- * d_depth_prev the depth of frame rank * B - 1 (world > 1; NULL for the first step of rank 0),
- * frame_count0 the processed-frame index of d_bgr[0] (RANSAC seed 42 + index, Slam.cpp:276);
- * out[p] = motion of pair (frame p - 1, frame p) of the block, p = 0..B-1. */
+ * d_depth_prev the depth of frame rank * B - 1 (required with a communicator except on rank 0's
+ * first step: VS_ERR_ARG otherwise), frame_count0 the processed-frame index of d_bgr[0] (RANSAC
+ * seed 42 + index, Slam.cpp:276); out[p] = motion of pair (frame p - 1, frame p) of the block,
+ * p = 0..B-1.  The neighbour frame's features arrive over a point-to-point ring (ncclSend /
+ * ncclRecv: one record per rank per step), or from the all-gather in gather mode. */
 int vs_batch_step_dev(vs_batch* b, const uint8_t* d_bgr, const float* d_depth, const float* d_depth_prev,
                       int frame_count0, vs_pair_motion* out, void* stream);
-/* The last step's feature records on the device (with a communicator: all ranks' frames in global
- * order; without: this rank's), e.g. for vs_spcf_write_dev. */
+/* Gather mode (on != 0, with a communicator): every step all-gathers all ranks' records, so that
+ * vs_batch_features_dev returns the whole step (rank 0 writing the SPCF cache).  Default: off. */
+int vs_batch_set_gather(vs_batch* b, int on);
+/* The last step's feature records on the device (gather mode: all ranks' frames in global order;
+ * otherwise this rank's), e.g. for vs_spcf_write_dev. */
 int vs_batch_features_dev(vs_batch* b, const vs_keypoint** d_kps, const float** d_desc, const int** d_n, int* frames);
 
 /* ---- F2: the SPCF feature cache as the batch interchange (FeatureExtractor.cpp:261-381) ---
@@ -484,12 +489,13 @@ int vs_slam_run_posthoc_pgo(vs_slam* slam, int* loop_edges);
 
 /* ---- NMS tie accounting (FeatureExtractor.cpp:238-259: std::sort, unstable) ------------------
  * Every post-processed frame on this context (vs_extract*, vs_postprocess*, a vs_slam's batches)
- * adds to four totals: out = {frames, frames with a tie, window ties (output keypoints with an
+ * adds to five totals: out = {frames, frames with a tie, window ties (output keypoints with an
  * equal-score candidate inside their 9x9 window), cut ties (the 400th and 401st kept pixel score
- * the same)}.  A frame with no tie gives the reference's keypoints for any order of equal scores,
- * std::sort's included; the build breaks ties by raster index.  reset != 0 zeroes the totals.
- * Synchronises the device. */
-int vs_nms_tie_stats(vs_ctx* ctx, long long out[4], int reset);
+ * the same), order ties (output keypoints sharing their score with another output keypoint)}.
+ * Without window and cut ties the keypoint set is the reference's for any order of equal scores,
+ * std::sort's included; without order ties also their order in the list.  The build breaks ties
+ * by raster index.  reset != 0 zeroes the totals.  Synchronises the device. */
+int vs_nms_tie_stats(vs_ctx* ctx, long long out[5], int reset);
 
 /* ---- profiling ----------------------------------------------------------------------- */
 /* When enabled, every stage of the _dev pipelines brackets its launches with hipEvents on the

@@ -149,11 +149,11 @@ def nms(heat, h=None, w=None, thr=0.005, radius=4, max_kp=400, order_mode=1):
 
 
 def nms_ties(heat, thr=0.005, radius=4, max_kp=400):
-    """(window ties, cut tie) of the heatmap's greedy NMS (orc_nms_ties)."""
+    """(window ties, cut tie, order ties) of the heatmap's greedy NMS (orc_nms_ties)."""
     heat = np.ascontiguousarray(heat, np.float32)
-    out = np.zeros(2, np.int32)
+    out = np.zeros(3, np.int32)
     lib().orc_nms_ties(_p(heat), heat.shape[0], heat.shape[1], thr, radius, max_kp, _p(out))
-    return int(out[0]), int(out[1])
+    return int(out[0]), int(out[1]), int(out[2])
 
 
 def sample_descriptors(desc_grid, kps):

@@ -106,7 +106,9 @@ int orc_nms(const float* heatmap, int hp, int wp, int h, int w, float thr, int r
 // the raster-order tie break used here (sp_post.hip header): over the stable greedy's kept sequence
 // (uncapped), out[0] = selected pixels (the first min(max_kp, kept) of it) with an equal-score
 // candidate in their (2 radius + 1)^2 window, out[1] = 1 when the max_kp-th and the next kept pixel
-// score the same.  Both zero => every order of equal scores gives the same output.
+// score the same, out[2] = selected keypoints sharing their score with another selected one.
+// out[0] = out[1] = 0 => every order of equal scores gives the same keypoint set; all three zero =>
+// the same list.
 void orc_nms_ties(const float* heatmap, int hp, int wp, float thr, int radius, int max_kp, int* out) {
     std::vector<Candidate> candidates;
     for (int y = 0; y < hp; y++)
@@ -142,6 +144,12 @@ void orc_nms_ties(const float* heatmap, int hp, int wp, float thr, int radius, i
     }
     out[0] = window;
     out[1] = (K > 0 && (int)kept.size() > K && kept[K - 1].score == kept[K].score) ? 1 : 0;
+    // order ties: selected keypoints sharing their exact score with another selected one — the
+    // set is order-independent, their order in the output list is not
+    int order = 0;
+    for (int i = 0; i < K; i++)
+        order += (i > 0 && kept[i - 1].score == kept[i].score) || (i + 1 < K && kept[i + 1].score == kept[i].score);
+    out[2] = order;
 }
 
 // FeatureExtractor.cpp:167-206: bilinear sample of the coarse descriptor grid, expression

@@ -62,8 +62,9 @@ def greedy_kept(heat, thr=0.005, radius=4, order=None):
 
 
 def nms_ties(heat, thr=0.005, radius=4, max_kp=400):
-    """(window ties, cut tie): selected keypoints with an equal-score candidate in their window,
-    and whether the max_kp-th and the next kept pixel score the same (sp_post.hip header)."""
+    """(window ties, cut tie, order ties): selected keypoints with an equal-score candidate in their
+    window, whether the max_kp-th and the next kept pixel score the same, and selected keypoints
+    sharing their score with another selected one (sp_post.hip header)."""
     H, W = heat.shape
     kept = greedy_kept(heat, thr, radius)
     K = min(max_kp, len(kept))
@@ -72,7 +73,9 @@ def nms_ties(heat, thr=0.005, radius=4, max_kp=400):
         win = heat[max(0, y - radius):y + radius + 1, max(0, x - radius):x + radius + 1]
         window += int((win == np.float32(sc)).sum() > 1)
     cut = int(0 < K < len(kept) and kept[K - 1][2] == kept[K][2])
-    return window, cut
+    sc = [k[2] for k in kept[:K]]
+    order = sum(1 for i in range(K) if (i > 0 and sc[i - 1] == sc[i]) or (i + 1 < K and sc[i + 1] == sc[i]))
+    return window, cut, order
 
 
 def nms_floor(heat, thr=0.005, radius=4, max_kp=400):

@@ -1,8 +1,8 @@
 """The offline frame-sharded front end behind the C ABI (vs_batch_*, csrc/batch.hip; BASELINE
 config[3]) against python/vslam_pipeline.DevicePipeline on the same frames: every
 pair motion (3D-3D and E results, match counts) bit for bit, without a communicator (the carry of
-the previous step's last frame) and with a one-rank RCCL communicator (the all-gather / halo
-exchange path with the previous step's last depth as the halo).  More ranks need more GPUs than the
+the previous step's last frame) and with a one-rank RCCL communicator (the halo ring and the all-gather
+exchange paths with the previous step's last depth as the halo).  More ranks need more GPUs than the
 test box has; the exchange logic itself is the one the gloo tests cover for DevicePipeline."""
 import numpy as np
 import pytest
@@ -40,12 +40,24 @@ def pipeline_results(vsctx, frames):
     return res
 
 
-@pytest.mark.parametrize("with_comm", [False, True])
-def test_batch_c_abi_equals_device_pipeline(vsctx, frames, pipeline_results, with_comm):
+@pytest.mark.parametrize("mode", ["none", "ring", "gather"])
+def test_batch_c_abi_equals_device_pipeline(vsctx, frames, pipeline_results, mode):
     dev = torch.device("cuda", 0)
     bgr, dep = frames
+    with_comm = mode != "none"
     uid = vslam_abi.batch_unique_id() if with_comm else None
     with vslam_abi.Batch(vsctx, B, uid=uid) as bt:
+        if mode == "gather":
+            bt.set_gather(True)
+        if with_comm:  # a communicator needs the neighbour's depth after rank 0's first step
+            with pytest.raises(vslam_abi.VSError, match="d_depth_prev"):
+                fr0 = torch.from_numpy(bgr[:B]).to(dev)
+                de0 = torch.from_numpy(dep[:B]).to(dev)
+                bt.step_dev(fr0.data_ptr(), de0.data_ptr(), None, 0, torch.cuda.current_stream().cuda_stream)
+                bt.step_dev(fr0.data_ptr(), de0.data_ptr(), None, B, torch.cuda.current_stream().cuda_stream)
+    with vslam_abi.Batch(vsctx, B, uid=vslam_abi.batch_unique_id() if with_comm else None) as bt:
+        if mode == "gather":
+            bt.set_gather(True)
         prev = None
         for k in range(STEPS):
             fr = torch.from_numpy(bgr[k * B:(k + 1) * B]).to(dev)

@@ -22,7 +22,7 @@ def _frame_value(step, g):
     return float(1000 * step + g + 1)
 
 
-def _worker(rank, world, port, errq):
+def _worker(rank, world, port, errq, gather=True):
     try:
         import torch.distributed as dist
 
@@ -30,7 +30,7 @@ def _worker(rank, world, port, errq):
         os.environ["MASTER_ADDR"] = "127.0.0.1"
         os.environ["MASTER_PORT"] = str(port)
         dist.init_process_group("gloo", rank=rank, world_size=world)
-        x = FeatureExchange(B, CAP, rank, world, device="cpu")
+        x = FeatureExchange(B, CAP, rank, world, device="cpu", gather=gather)
         kps = torch.zeros((B + 1, CAP * KP_BYTES), dtype=torch.uint8)
         desc = torch.zeros((B + 1, CAP, 256), dtype=torch.float32)
         n = torch.zeros(B + 1, dtype=torch.int32)
@@ -41,12 +41,15 @@ def _worker(rank, world, port, errq):
                 desc[1 + b].fill_(v)
                 kps[1 + b].fill_(int(v) % 251)
                 n[1 + b] = int(v) % 400
-            g_kps, g_desc, g_n = x.exchange(kps, desc, n)
-            # gathered tables: the whole step in global frame order
-            for g in range(world * B):
-                v = _frame_value(step, g)
-                assert float(g_desc[g, 0, 0]) == v and int(g_n[g]) == int(v) % 400
-                assert int(g_kps[g, 0]) == int(v) % 251
+            got = x.exchange(kps, desc, n)
+            if gather:  # gathered tables: the whole step in global frame order
+                g_kps, g_desc, g_n = got
+                for g in range(world * B):
+                    v = _frame_value(step, g)
+                    assert float(g_desc[g, 0, 0]) == v and int(g_n[g]) == int(v) % 400
+                    assert int(g_kps[g, 0]) == int(v) % 251
+            else:
+                assert got is None
             # slot 0 = frame rank*B - 1 (previous step's global last frame for rank 0)
             if rank > 0:
                 want = _frame_value(step, rank * B - 1)
@@ -66,11 +69,13 @@ def _worker(rank, world, port, errq):
         raise
 
 
-def test_feature_exchange_world2_gloo():
+@pytest.mark.parametrize("world,gather", [(2, True), (2, False), (3, False)])
+def test_feature_exchange_gloo(world, gather):
+    """All-gather (SPCF consumer) and the default halo ring (one record per rank per step)."""
     ctx = mp.get_context("spawn")
     errq = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, errq)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, errq, gather)) for r in range(world)]
     for p in procs:
         p.start()
     for p in procs:

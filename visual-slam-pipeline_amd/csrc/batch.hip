@@ -1,8 +1,10 @@
 // batch.hip — the offline, frame-sharded front end (BASELINE config[3]) behind the
 // C ABI, for a C/C++ driver such as the reference's main.cpp:1036-1311: per step each rank
-// extracts its B frames (FeatureExtractor::extract), the step's feature records are all-gathered
-// over RCCL so that every rank holds the whole step (the SPCF-like interchange a sequential
-// tracker consumes) and rank r the neighbour frame rB - 1, then the B frame pairs that end in
+// extracts its B frames (FeatureExtractor::extract), rank r receives the neighbour frame rB - 1's
+// record over RCCL (a ring: each rank sends its last record to rank r + 1, one 420 KB record per
+// rank per step; rank 0 keeps what rank world - 1 sent as the next step's neighbour), or — with
+// vs_batch_set_gather, for an SPCF writer — the step's records are all-gathered so that every rank
+// holds the whole step (the interchange a sequential tracker consumes); then the B frame pairs that end in
 // the rank's frames go through Slam::match_features, the F-matrix verification, the 3D-3D RANSAC
 // and its essential-matrix fallback (Slam.cpp:838-984).  The same stages and inputs as
 // python/vslam_pipeline.DevicePipeline, so both give bit-identical pair motions
@@ -31,6 +33,10 @@ struct Rccl {
     int (*get_unique_id)(RcclId*) = nullptr;
     int (*comm_init_rank)(RcclComm*, int, RcclId, int) = nullptr;
     int (*all_gather)(const void*, void*, size_t, int, RcclComm, hipStream_t) = nullptr;
+    int (*send)(const void*, size_t, int, int, RcclComm, hipStream_t) = nullptr;
+    int (*recv)(void*, size_t, int, int, RcclComm, hipStream_t) = nullptr;
+    int (*group_start)() = nullptr;
+    int (*group_end)() = nullptr;
     int (*comm_destroy)(RcclComm) = nullptr;
     const char* (*error_string)(int) = nullptr;
 };
@@ -49,8 +55,13 @@ int load_rccl(Rccl& r) {
     r.all_gather = reinterpret_cast<int (*)(const void*, void*, size_t, int, RcclComm, hipStream_t)>(
         dlsym(so, "ncclAllGather"));
     r.comm_destroy = reinterpret_cast<int (*)(RcclComm)>(dlsym(so, "ncclCommDestroy"));
+    r.send = reinterpret_cast<int (*)(const void*, size_t, int, int, RcclComm, hipStream_t)>(dlsym(so, "ncclSend"));
+    r.recv = reinterpret_cast<int (*)(void*, size_t, int, int, RcclComm, hipStream_t)>(dlsym(so, "ncclRecv"));
+    r.group_start = reinterpret_cast<int (*)()>(dlsym(so, "ncclGroupStart"));
+    r.group_end = reinterpret_cast<int (*)()>(dlsym(so, "ncclGroupEnd"));
     r.error_string = reinterpret_cast<const char* (*)(int)>(dlsym(so, "ncclGetErrorString"));
-    if (!r.get_unique_id || !r.comm_init_rank || !r.all_gather || !r.comm_destroy) {
+    if (!r.get_unique_id || !r.comm_init_rank || !r.all_gather || !r.comm_destroy || !r.send || !r.recv ||
+        !r.group_start || !r.group_end) {
         vs::set_error("vs_batch: librccl.so lacks the expected entry points");
         return VS_ERR_IO;
     }
@@ -82,16 +93,21 @@ T* alloc(std::vector<void*>& owned, size_t count) {  // zeroed; a failure leaves
 struct vs_batch {
     vs_ctx* ctx = nullptr;
     int B = 0, h = 0, w = 0, rank = 0, world = 1, cap = VS_SP_MAX_KEYPOINTS, steps = 0;
+    bool gather = false;  // all-gather the whole step (vs_batch_set_gather) instead of the halo ring
     RcclComm comm = nullptr;
     std::vector<void*> owned;
     // slot 0 = the frame before this rank's block, slots 1..B = its frames
     vs_keypoint* kps = nullptr;
     float *desc = nullptr, *depth = nullptr, *semi = nullptr, *dgrid = nullptr;
     int* n = nullptr;
-    // the step's gathered records (world > 1): [world * B]
+    // the step's gathered records (gather mode): [world * B]
     vs_keypoint* g_kps = nullptr;
     float* g_desc = nullptr;
     int* g_n = nullptr;
+    // halo ring: the record received from rank r - 1, and rank 0's carry (next step's slot 0)
+    vs_keypoint *rx_kps = nullptr, *carry_kps = nullptr;
+    float *rx_desc = nullptr, *carry_desc = nullptr;
+    int *rx_n = nullptr, *carry_n = nullptr;
     // per pair
     int *pairs = nullptr, *nraw = nullptr, *ngood = nullptr, *nkept = nullptr, *fdiag = nullptr, *ok = nullptr,
         *diag = nullptr, *eok = nullptr, *ediag = nullptr;
@@ -130,9 +146,9 @@ int vs_batch_create(vs_ctx* ctx, int B, int h, int w, int rank, int world, const
     b->semi = alloc<float>(o, (size_t)B * hc * wc * VS_SEMI_CH);
     b->dgrid = alloc<float>(o, (size_t)B * hc * wc * VS_DESC_DIM);
     if (id) {
-        b->g_kps = alloc<vs_keypoint>(o, (size_t)world * B * cap);
-        b->g_desc = alloc<float>(o, (size_t)world * B * cap * 256);
-        b->g_n = alloc<int>(o, (size_t)world * B);
+        b->rx_kps = alloc<vs_keypoint>(o, cap), b->carry_kps = alloc<vs_keypoint>(o, cap);
+        b->rx_desc = alloc<float>(o, (size_t)cap * 256), b->carry_desc = alloc<float>(o, (size_t)cap * 256);
+        b->rx_n = alloc<int>(o, 1), b->carry_n = alloc<int>(o, 1);
     }
     b->pairs = alloc<int>(o, 2 * B);
     b->seeds = alloc<uint32_t>(o, B);
@@ -189,8 +205,14 @@ int vs_batch_step_dev(vs_batch* b, const uint8_t* d_bgr, const float* d_depth, c
     const size_t plane = (size_t)h * w, rec_k = (size_t)cap, rec_d = (size_t)cap * 256;
     // depth: slot 0 = the frame before the block (the caller's halo, or the previous step's last)
     const bool xchg = b->comm != nullptr;
+    // with a communicator the neighbour frame's depth comes from the caller (it is the rank's input
+    // halo); only rank 0's very first step has no neighbour (never a stale plane)
+    VS_ARG(!xchg || d_depth_prev || (b->rank == 0 && b->steps == 0),
+           "vs_batch_step_dev: d_depth_prev (frame rank * B - 1) is required with a communicator");
     if (xchg && d_depth_prev)
         VS_HIP(hipMemcpyAsync(b->depth, d_depth_prev, plane * sizeof(float), hipMemcpyDeviceToDevice, s));
+    else if (xchg)
+        VS_HIP(hipMemsetAsync(b->depth, 0, plane * sizeof(float), s));
     else if (!xchg)
         VS_HIP(hipMemcpyAsync(b->depth, b->depth + (size_t)B * plane, plane * sizeof(float), hipMemcpyDeviceToDevice, s));
     VS_HIP(hipMemcpyAsync(b->depth + plane, d_depth, (size_t)B * plane * sizeof(float), hipMemcpyDeviceToDevice, s));
@@ -203,26 +225,44 @@ int vs_batch_step_dev(vs_batch* b, const uint8_t* d_bgr, const float* d_depth, c
     VS_CHECK(vs_network_batch_dev(ctx, B, d_bgr, h, w, b->semi, b->dgrid, s));
     VS_CHECK(vs_postprocess_batch_dev(ctx, B, b->semi, b->dgrid, h, w, b->kps + rec_k, b->desc + rec_d, b->n + 1, cap, s));
     if (xchg) {
-        // all-gather the step's records; slot 0 <- frame rank * B - 1 (rank 0: the previous step's
-        // global last frame, still in g_* from that step)
-        if (b->rank == 0) {
-            if (b->steps > 0) {
-                const size_t last = (size_t)b->world * B - 1;
-                VS_HIP(hipMemcpyAsync(b->kps, b->g_kps + last * rec_k, rec_k * sizeof(vs_keypoint), hipMemcpyDeviceToDevice, s));
-                VS_HIP(hipMemcpyAsync(b->desc, b->g_desc + last * rec_d, rec_d * sizeof(float), hipMemcpyDeviceToDevice, s));
-                VS_HIP(hipMemcpyAsync(b->n, b->g_n + last, sizeof(int), hipMemcpyDeviceToDevice, s));
-            } else {
-                VS_HIP(hipMemsetAsync(b->n, 0, sizeof(int), s));
-            }
+        const size_t kb = rec_k * sizeof(vs_keypoint), db = rec_d * sizeof(float);
+        if (b->gather) {
+            // all-gather the step's records; the neighbour record is frame rank * B - 1 of the
+            // gathered step (rank 0: the global last frame, next step's neighbour)
+            VS_RCCL(g_rccl.all_gather(b->n + 1, b->g_n, (size_t)B * sizeof(int), kRcclChar, b->comm, s));
+            VS_RCCL(g_rccl.all_gather(b->kps + rec_k, b->g_kps, (size_t)B * kb, kRcclChar, b->comm, s));
+            VS_RCCL(g_rccl.all_gather(b->desc + rec_d, b->g_desc, (size_t)B * db, kRcclChar, b->comm, s));
+            const size_t j = ((size_t)b->rank * B + (size_t)b->world * B - 1) % ((size_t)b->world * B);
+            VS_HIP(hipMemcpyAsync(b->rx_kps, b->g_kps + j * rec_k, kb, hipMemcpyDeviceToDevice, s));
+            VS_HIP(hipMemcpyAsync(b->rx_desc, b->g_desc + j * rec_d, db, hipMemcpyDeviceToDevice, s));
+            VS_HIP(hipMemcpyAsync(b->rx_n, b->g_n + j, sizeof(int), hipMemcpyDeviceToDevice, s));
+        } else if (b->world == 1) {  // a one-rank ring: the record goes to itself
+            VS_HIP(hipMemcpyAsync(b->rx_kps, b->kps + (size_t)B * rec_k, kb, hipMemcpyDeviceToDevice, s));
+            VS_HIP(hipMemcpyAsync(b->rx_desc, b->desc + (size_t)B * rec_d, db, hipMemcpyDeviceToDevice, s));
+            VS_HIP(hipMemcpyAsync(b->rx_n, b->n + B, sizeof(int), hipMemcpyDeviceToDevice, s));
+        } else {
+            // ring: last record to rank + 1, the neighbour's from rank - 1 (three sends, three receives)
+            const int nxt = (b->rank + 1) % b->world, prv = (b->rank + b->world - 1) % b->world;
+            VS_RCCL(g_rccl.group_start());
+            VS_RCCL(g_rccl.send(b->kps + (size_t)B * rec_k, kb, kRcclChar, nxt, b->comm, s));
+            VS_RCCL(g_rccl.send(b->desc + (size_t)B * rec_d, db, kRcclChar, nxt, b->comm, s));
+            VS_RCCL(g_rccl.send(b->n + B, sizeof(int), kRcclChar, nxt, b->comm, s));
+            VS_RCCL(g_rccl.recv(b->rx_kps, kb, kRcclChar, prv, b->comm, s));
+            VS_RCCL(g_rccl.recv(b->rx_desc, db, kRcclChar, prv, b->comm, s));
+            VS_RCCL(g_rccl.recv(b->rx_n, sizeof(int), kRcclChar, prv, b->comm, s));
+            VS_RCCL(g_rccl.group_end());
         }
-        VS_RCCL(g_rccl.all_gather(b->n + 1, b->g_n, (size_t)B * sizeof(int), kRcclChar, b->comm, s));
-        VS_RCCL(g_rccl.all_gather(b->kps + rec_k, b->g_kps, (size_t)B * rec_k * sizeof(vs_keypoint), kRcclChar, b->comm, s));
-        VS_RCCL(g_rccl.all_gather(b->desc + rec_d, b->g_desc, (size_t)B * rec_d * sizeof(float), kRcclChar, b->comm, s));
-        if (b->rank > 0) {
-            const size_t j = (size_t)b->rank * B - 1;
-            VS_HIP(hipMemcpyAsync(b->kps, b->g_kps + j * rec_k, rec_k * sizeof(vs_keypoint), hipMemcpyDeviceToDevice, s));
-            VS_HIP(hipMemcpyAsync(b->desc, b->g_desc + j * rec_d, rec_d * sizeof(float), hipMemcpyDeviceToDevice, s));
-            VS_HIP(hipMemcpyAsync(b->n, b->g_n + j, sizeof(int), hipMemcpyDeviceToDevice, s));
+        if (b->rank > 0) {  // slot 0 <- rank - 1's last frame of this step
+            VS_HIP(hipMemcpyAsync(b->kps, b->rx_kps, kb, hipMemcpyDeviceToDevice, s));
+            VS_HIP(hipMemcpyAsync(b->desc, b->rx_desc, db, hipMemcpyDeviceToDevice, s));
+            VS_HIP(hipMemcpyAsync(b->n, b->rx_n, sizeof(int), hipMemcpyDeviceToDevice, s));
+        } else {  // slot 0 <- the previous step's global last frame (none before the first step)
+            VS_HIP(hipMemcpyAsync(b->kps, b->carry_kps, kb, hipMemcpyDeviceToDevice, s));
+            VS_HIP(hipMemcpyAsync(b->desc, b->carry_desc, db, hipMemcpyDeviceToDevice, s));
+            VS_HIP(hipMemcpyAsync(b->n, b->carry_n, sizeof(int), hipMemcpyDeviceToDevice, s));
+            VS_HIP(hipMemcpyAsync(b->carry_kps, b->rx_kps, kb, hipMemcpyDeviceToDevice, s));
+            VS_HIP(hipMemcpyAsync(b->carry_desc, b->rx_desc, db, hipMemcpyDeviceToDevice, s));
+            VS_HIP(hipMemcpyAsync(b->carry_n, b->rx_n, sizeof(int), hipMemcpyDeviceToDevice, s));
         }
     }
     // the RANSAC seed of pair p is 42 + its processed-frame index (Slam.cpp:276)
@@ -264,9 +304,27 @@ int vs_batch_step_dev(vs_batch* b, const uint8_t* d_bgr, const float* d_depth, c
     return VS_OK;
 }
 
+int vs_batch_set_gather(vs_batch* b, int on) {
+    VS_ARG(b, "vs_batch_set_gather: null argument");
+    if (!on || b->gather || !b->comm) {
+        b->gather = on && b->comm;
+        return VS_OK;
+    }
+    const size_t n = (size_t)b->world * b->B;
+    b->g_kps = alloc<vs_keypoint>(b->owned, n * b->cap);
+    b->g_desc = alloc<float>(b->owned, n * b->cap * 256);
+    b->g_n = alloc<int>(b->owned, n);
+    if (!b->g_kps || !b->g_desc || !b->g_n) {
+        vs::set_error("vs_batch_set_gather: device allocation failed");
+        return VS_ERR_NOMEM;
+    }
+    b->gather = true;
+    return VS_OK;
+}
+
 int vs_batch_features_dev(vs_batch* b, const vs_keypoint** d_kps, const float** d_desc, const int** d_n, int* frames) {
     VS_ARG(b && d_kps && d_desc && d_n && frames, "vs_batch_features_dev: null argument");
-    if (b->comm) {
+    if (b->comm && b->gather) {
         *d_kps = b->g_kps, *d_desc = b->g_desc, *d_n = b->g_n, *frames = b->world * b->B;
     } else {
         *d_kps = b->kps + b->cap, *d_desc = b->desc + (size_t)b->cap * 256, *d_n = b->n + 1, *frames = b->B;

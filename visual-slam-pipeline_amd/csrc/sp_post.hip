@@ -34,12 +34,14 @@
 // on the device paths, VS_ERR_NOTCONV from the host entry points), never a wrong keypoint list.
 //
 // Ties.  The reference sorts with std::sort (unstable); the order used here breaks exact score
-// ties by raster index.  The output can differ from the reference's only through an exact tie that
-// the greedy actually resolves: two candidates of equal score within one 9x9 window of which one is
-// kept, or equal scores on both sides of the 400 cut.  k_nms_select counts both per frame (an
-// output keypoint with an equal-score candidate in its window; the 400th and 401st kept pixel
-// scoring the same) into the context's tie totals (vs_nms_tie_stats): when both are zero the
-// output equals the reference's for ANY order of equal scores, std::sort's included.
+// ties by raster index.  The keypoint SET can differ from the reference's only through an exact tie
+// that the greedy actually resolves: two candidates of equal score within one 9x9 window of which
+// one is kept, or equal scores on both sides of the 400 cut; the keypoint LIST order additionally
+// through output keypoints that share a score.  k_nms_select counts all three per frame (an output
+// keypoint with an equal-score candidate in its window; the 400th and 401st kept pixel scoring the
+// same; output keypoints sharing their score) into the context's tie totals (vs_nms_tie_stats):
+// when all are zero the output list equals the reference's for ANY order of equal scores,
+// std::sort's included (tests/test_oracle.py pins the claim on the CPU restatement).
 #include <hip/hip_runtime.h>
 
 #include <cstdlib>
@@ -416,8 +418,9 @@ __global__ __launch_bounds__(256) void k_nms_collect(const float* __restrict__ h
 // bitonic sort of the K winners in descending priority, keypoint records, border erase
 // (FeatureExtractor.cpp:155-160), and the frame's tie accounting (see the header): window ties =
 // selected pixels with an equal-score candidate in their 9x9 window, cut tie = the K-th and the
-// (K+1)-th kept pixel score the same.  ties[b] = {window, cut}; totals += {frames, frames with a
-// tie, window ties, cut ties}.  One 1024-thread workgroup per frame.
+// (K+1)-th kept pixel score the same, order ties = selected keypoints sharing their score with
+// another selected one.  ties[b] = {window, cut, order}; totals += {frames, frames with a tie,
+// window ties, cut ties, order ties}.  One 1024-thread workgroup per frame.
 constexpr int kSelSort = 512;
 __global__ __launch_bounds__(1024) void k_nms_select(const unsigned long long* __restrict__ keys,
                                                      const int* __restrict__ keycnt, int key_cap, int max_kp,
@@ -548,12 +551,19 @@ __global__ __launch_bounds__(1024) void k_nms_select(const unsigned long long* _
         nout[b] = n;
         const int wt = s_wties;
         const int ct = (K > 0 && K < nk && (s_next >> 32) == (kth >> 32)) ? 1 : 0;
-        ties[2 * b] = wt;
-        ties[2 * b + 1] = ct;
+        int ot = 0;  // selected keypoints sharing their score with another one (list order)
+        for (int i = 0; i < K && i < kSelSort; i++) {
+            const unsigned sc = (unsigned)(s_sel[i] >> 32);
+            ot += (i > 0 && (unsigned)(s_sel[i - 1] >> 32) == sc) || (i + 1 < K && (unsigned)(s_sel[i + 1] >> 32) == sc);
+        }
+        ties[3 * b] = wt;
+        ties[3 * b + 1] = ct;
+        ties[3 * b + 2] = ot;
         atomicAdd(&totals[0], 1ull);
-        atomicAdd(&totals[1], (wt || ct) ? 1ull : 0ull);
+        atomicAdd(&totals[1], (wt || ct || ot) ? 1ull : 0ull);
         atomicAdd(&totals[2], (unsigned long long)wt);
         atomicAdd(&totals[3], (unsigned long long)ct);
+        atomicAdd(&totals[4], (unsigned long long)ot);
     }
 }
 
@@ -630,8 +640,8 @@ int sp_postprocess(vs_ctx* ctx, int B, int hc, int wc, int h, int w, vs_keypoint
     VS_CHECK(ctx->heat.ensure(npx * sizeof(float)));
     VS_CHECK(ctx->state.ensure(npx));
     // flags (ints): [rounds + 1][B] undecided-after-round, the capacity word, ferr [B], keycnt [B],
-    // lmcnt [B], floor [B], ties [B][2]; then tile flags (bytes) [rounds + 1][B][ntiles]
-    const size_t nflag = (size_t)(kNmsMaxRounds + 1) * B + 1 + 6 * (size_t)B;
+    // lmcnt [B], floor [B], ties [B][3]; then tile flags (bytes) [rounds + 1][B][ntiles]
+    const size_t nflag = (size_t)(kNmsMaxRounds + 1) * B + 1 + 7 * (size_t)B;
     VS_CHECK(ctx->flags.ensure(nflag * sizeof(int) + (size_t)(kNmsMaxRounds + 1) * B * ntiles));
     VS_CHECK(ctx->nms_list.ensure(npx * 2 * sizeof(int)));
     const char* fr_env = getenv("VS_NMS_FINISH_ROUNDS");  // test knob: forces the error path
@@ -639,8 +649,8 @@ int sp_postprocess(vs_ctx* ctx, int B, int hc, int wc, int h, int w, vs_keypoint
     VS_CHECK(ctx->keys.ensure((size_t)B * key_cap * sizeof(unsigned long long)));
     VS_CHECK(ctx->lmax.ensure((size_t)B * key_cap * sizeof(unsigned)));  // strict local maxima
     if (!ctx->tie_totals.p) {
-        VS_CHECK(ctx->tie_totals.ensure(4 * sizeof(unsigned long long)));
-        VS_HIP(hipMemsetAsync(ctx->tie_totals.p, 0, 4 * sizeof(unsigned long long), s));
+        VS_CHECK(ctx->tie_totals.ensure(5 * sizeof(unsigned long long)));
+        VS_HIP(hipMemsetAsync(ctx->tie_totals.p, 0, 5 * sizeof(unsigned long long), s));
     }
     int* flags = ctx->flags.as<int>();
     int* err = flags + (size_t)(kNmsMaxRounds + 1) * B;

@@ -840,17 +840,17 @@ int vs_local_ba(vs_ctx* ctx, int N, double* R_world, double* t_world, int M, dou
 }
 
 // ---- profiling ----------------------------------------------------------------------------------
-int vs_nms_tie_stats(vs_ctx* ctx, long long out[4], int reset) {
+int vs_nms_tie_stats(vs_ctx* ctx, long long out[5], int reset) {
     VS_ARG(ctx && out, "vs_nms_tie_stats: null argument");
     VS_HIP(hipSetDevice(ctx->device));
-    unsigned long long t[4] = {0, 0, 0, 0};
+    unsigned long long t[5] = {0, 0, 0, 0, 0};
     if (ctx->tie_totals.p) {
         // every stream that post-processes on this context (a vs_slam's extraction streams included)
         VS_HIP(hipDeviceSynchronize());
         VS_HIP(hipMemcpy(t, ctx->tie_totals.p, sizeof(t), hipMemcpyDeviceToHost));
         if (reset) VS_HIP(hipMemset(ctx->tie_totals.p, 0, sizeof(t)));
     }
-    for (int i = 0; i < 4; i++) out[i] = (long long)t[i];
+    for (int i = 0; i < 5; i++) out[i] = (long long)t[i];
     return VS_OK;
 }
 

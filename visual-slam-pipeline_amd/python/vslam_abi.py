@@ -91,6 +91,7 @@ _SIG = {
     "vs_batch_destroy": (None, [_P]),
     "vs_batch_step_dev": (_I, [_P, _P, _P, _P, _I, _P, _P]),
     "vs_batch_features_dev": (_I, [_P, _P, _P, _P, _P]),
+    "vs_batch_set_gather": (_I, [_P, _I]),
     "vs_spcf_write": (ctypes.c_int, [ctypes.c_char_p, _I, _P, _P, _P, _P, _I, _I]),
     "vs_spcf_write_dev": (_I, [_P, ctypes.c_char_p, _I, _P, _P, _P, _P, _I, _I, _P]),
     "vs_spcf_read": (_I, [ctypes.c_char_p, _I, _I, _P, _P, _P, _P, _P]),
@@ -464,11 +465,11 @@ class Context:
                                           int(append), stream))
 
     def tie_stats(self, reset=False):
-        """NMS tie totals since the last reset: frames, frames with a tie, window ties, cut ties
+        """NMS tie totals since the last reset: frames, frames with a tie, window, cut and order ties
         (vs_nms_tie_stats)."""
-        out = np.zeros(4, np.int64)
+        out = np.zeros(5, np.int64)
         _check(self.lib.vs_nms_tie_stats(self.h, _ptr(out), 1 if reset else 0))
-        return dict(zip(("frames", "frames_with_tie", "window_ties", "cut_ties"), (int(v) for v in out)))
+        return dict(zip(("frames", "frames_with_tie", "window_ties", "cut_ties", "order_ties"), (int(v) for v in out)))
 
     def profile(self, on=True):
         _check(self.lib.vs_profile_enable(self.h, 1 if on else 0))
@@ -818,6 +819,10 @@ class Batch:
 
     def __exit__(self, *a):
         self.close()
+
+    def set_gather(self, on=True):
+        """All-gather every step's records (for an SPCF writer) instead of the halo ring."""
+        _check(self.lib.vs_batch_set_gather(self.h, 1 if on else 0))
 
     def step_dev(self, d_bgr, d_depth, d_depth_prev, frame_count0, stream=None):
         out = (PairMotion * self.B)()

@@ -36,40 +36,67 @@ M_BYTES = va.MATCH_DTYPE.itemsize
 class FeatureExchange:
     """Per-step interchange of per-frame feature records among frame-sharded ranks (SURVEY.md
     8(e)).  Rank r extracts frames [rB, (r+1)B) of each step into slots 1..B of its tables; after
-    exchange() every rank holds the whole step's records (g_kps / g_desc / g_n, global frame
-    order) and slot 0 of its tables holds frame rB-1: rank r-1's last frame, or for rank 0 the
-    previous step's global last frame (count 0 before the first step).  Device-agnostic: the same
-    code runs over RCCL on MI355X and over gloo in the CPU tests."""
+    exchange() slot 0 of its tables holds frame rB-1: rank r-1's last frame, or for rank 0 the
+    previous step's global last frame (count 0 before the first step).
 
-    def __init__(self, B, cap, rank, world, group=None, device=None):
-        self.B, self.cap, self.rank, self.world, self.group = B, cap, rank, world, group
-        self.g_kps = torch.zeros((world * B, cap * KP_BYTES), dtype=torch.uint8, device=device)
-        self.g_desc = torch.zeros((world * B, cap, 256), dtype=torch.float32, device=device)
-        self.g_n = torch.zeros(world * B, dtype=torch.int32, device=device)
+    gather=False (the default): a ring halo exchange — every rank sends its last record to rank
+    r+1 (mod world) and receives one record from rank r-1, one 420 KB record per rank per step
+    over xGMI point-to-point (rank 0 keeps what it receives as next step's slot 0).  gather=True
+    (an SPCF consumer on rank 0 needs the whole step): all-gather of the step's records, after
+    which every rank also holds g_kps / g_desc / g_n in global frame order.  Device-agnostic: the
+    same code runs over RCCL on MI355X and over gloo in the CPU tests."""
+
+    def __init__(self, B, cap, rank, world, group=None, device=None, gather=False):
+        self.B, self.cap, self.rank, self.world, self.group, self.gather = B, cap, rank, world, group, gather
+        if gather:
+            self.g_kps = torch.zeros((world * B, cap * KP_BYTES), dtype=torch.uint8, device=device)
+            self.g_desc = torch.zeros((world * B, cap, 256), dtype=torch.float32, device=device)
+            self.g_n = torch.zeros(world * B, dtype=torch.int32, device=device)
         self.carry_kps = torch.zeros(cap * KP_BYTES, dtype=torch.uint8, device=device)
         self.carry_desc = torch.zeros((cap, 256), dtype=torch.float32, device=device)
-        self.carry_n = torch.zeros((), dtype=torch.int32, device=device)
+        self.carry_n = torch.zeros(1, dtype=torch.int32, device=device)
+        self.rx_kps = torch.zeros_like(self.carry_kps)
+        self.rx_desc = torch.zeros_like(self.carry_desc)
+        self.rx_n = torch.zeros_like(self.carry_n)
+
+    def _peer(self, r):
+        import torch.distributed as dist
+        return dist.get_global_rank(self.group, r) if self.group is not None else r
 
     def exchange(self, kps, desc, n):
         """kps (B+1, cap*28) u8, desc (B+1, cap, 256) f32, n (B+1,) i32; slots 1..B are this rank's
-        frames.  Fills slot 0 and returns the gathered step tables."""
+        frames.  Fills slot 0; returns the gathered step tables (gather=True) or None."""
         import torch.distributed as dist
-        dist.all_gather_into_tensor(self.g_n, n[1:], group=self.group)
-        dist.all_gather_into_tensor(self.g_kps, kps[1:], group=self.group)
-        dist.all_gather_into_tensor(self.g_desc, desc[1:], group=self.group)
-        if self.rank > 0:
-            j = self.rank * self.B - 1
-            kps[0].copy_(self.g_kps[j])
-            desc[0].copy_(self.g_desc[j])
-            n[0].copy_(self.g_n[j])
+        if self.gather:
+            dist.all_gather_into_tensor(self.g_n, n[1:], group=self.group)
+            dist.all_gather_into_tensor(self.g_kps, kps[1:], group=self.group)
+            dist.all_gather_into_tensor(self.g_desc, desc[1:], group=self.group)
+            self.rx_kps.copy_(self.g_kps[(self.rank * self.B - 1) % (self.world * self.B)])
+            self.rx_desc.copy_(self.g_desc[(self.rank * self.B - 1) % (self.world * self.B)])
+            self.rx_n.copy_(self.g_n[(self.rank * self.B - 1) % (self.world * self.B)].reshape(1))
         else:
+            nxt, prv = self._peer((self.rank + 1) % self.world), self._peer((self.rank - 1) % self.world)
+            last = self.B
+            ops = [dist.P2POp(dist.isend, kps[last].contiguous(), nxt, self.group),
+                   dist.P2POp(dist.isend, desc[last].contiguous(), nxt, self.group),
+                   dist.P2POp(dist.isend, n[last:last + 1].contiguous(), nxt, self.group),
+                   dist.P2POp(dist.irecv, self.rx_kps, prv, self.group),
+                   dist.P2POp(dist.irecv, self.rx_desc, prv, self.group),
+                   dist.P2POp(dist.irecv, self.rx_n, prv, self.group)]
+            for w in dist.batch_isend_irecv(ops):
+                w.wait()
+        if self.rank > 0:  # rank r-1's last frame of this step
+            kps[0].copy_(self.rx_kps)
+            desc[0].copy_(self.rx_desc)
+            n[0:1].copy_(self.rx_n)
+        else:  # the previous step's global last frame; this step's (from rank world-1) for the next
             kps[0].copy_(self.carry_kps)
             desc[0].copy_(self.carry_desc)
-            n[0].copy_(self.carry_n)
-        self.carry_kps.copy_(self.g_kps[-1])
-        self.carry_desc.copy_(self.g_desc[-1])
-        self.carry_n.copy_(self.g_n[-1])
-        return self.g_kps, self.g_desc, self.g_n
+            n[0:1].copy_(self.carry_n)
+            self.carry_kps.copy_(self.rx_kps)
+            self.carry_desc.copy_(self.rx_desc)
+            self.carry_n.copy_(self.rx_n)
+        return (self.g_kps, self.g_desc, self.g_n) if self.gather else None
 
 
 class _StepSet:
@@ -137,7 +164,9 @@ class DevicePipeline:
         self._seed_base = torch.arange(B, dtype=torch.int64, device=dev)
         self.s_net = torch.cuda.Stream(device=dev)
         self.s_geo = torch.cuda.Stream(device=dev)
-        self.xchg = FeatureExchange(B, cap, rank, world, group, dev) if world > 1 else None
+        # the whole step is gathered only for an SPCF file (rank 0 writes every frame's record);
+        # otherwise each rank needs just its halo frame (ring point-to-point)
+        self.xchg = FeatureExchange(B, cap, rank, world, group, dev, gather=bool(spcf_path)) if world > 1 else None
 
     def submit(self, frames, depth, frame_count0, depth_prev=None):
         """Enqueue one step (no host synchronisation); returns the step's buffer set for collect().
@@ -188,9 +217,10 @@ class DevicePipeline:
                 S.desc[0].copy_(prev.desc[B])
                 S.n[0].copy_(prev.n[B])
             else:
-                # all-gather the step's feature records; slot 0 <- frame rank*B - 1
-                gk, gd, gn = self.xchg.exchange(S.kps, S.desc, S.n)
-                if hasattr(S, "g_kps"):
+                # slot 0 <- frame rank*B - 1 (halo ring; the whole step gathered for SPCF)
+                gathered = self.xchg.exchange(S.kps, S.desc, S.n)
+                if gathered is not None and hasattr(S, "g_kps"):
+                    gk, gd, gn = gathered
                     S.g_kps.copy_(gk)
                     S.g_desc.copy_(gd)
                     S.g_n.copy_(gn)
