@@ -54,6 +54,9 @@ FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: dense fp32 (v_mfma_f32_32
 # conv1's minimum HBM traffic per frame: the fp32 gray input read once (480 x 640 x 4 B) and the
 # pooled 240 x 320 x 64 fp32 output written once
 CONV1_MIN_BYTES_PER_FRAME = 480 * 640 * 4 + 240 * 320 * 64 * 4
+# post-processing algorithmic bytes per frame: semi read 1,248,000 + 400 x 4 taps x
+# 1 KB descriptor gathers 1,638,400 + heatmap write and read 1,228,800 + 420,800 of records out
+POST_BYTES_PER_FRAME = 1248000 + 1638400 + 1228800 + 420800
 LOOP_FRAMES = 126               # one lap of synth.loop_trajectory (0.3 m/s, 10 processed frames/s)
 T0 = 1311868164.0               # TUM-like timestamps, 0.1 s per processed frame (FRAME_STEP = 3)
 
@@ -316,8 +319,33 @@ def frontend_batch(ctx, L, B, rank, world, steps, warmup):
     torch.cuda.synchronize()
     alone = ctx.profile_read().get("match")
     ctx.profile(False)
+    # post-processing alone (decode + NMS + top-K + sampling) on the same step's network outputs,
+    # whole chip: in the pipelines it queues behind the network's workgroups on the same CUs
+    h, w = H, W
+    ctx.postprocess_batch_dev(B, S.semi.data_ptr(), S.dgrid.data_ptr(), h, w, S.kps[1:].data_ptr(),
+                              S.desc[1:].data_ptr(), S.n[1:].data_ptr(), cap, sm)
+    torch.cuda.synchronize()
+    ctx.profile(True)
+    ctx.profile_reset()
+    reps = 10
+    for _ in range(reps):
+        ctx.postprocess_batch_dev(B, S.semi.data_ptr(), S.dgrid.data_ptr(), h, w, S.kps[1:].data_ptr(),
+                                  S.desc[1:].data_ptr(), S.n[1:].data_ptr(), cap, sm)
+    torch.cuda.synchronize()
+    pp = ctx.profile_read()
+    ctx.profile(False)
+    post_ms = sum(pp[k][0] for k in ("decode", "nms_rounds", "nms_select", "sample") if k in pp) / (reps * B)
+    post = {"what": "FeatureExtractor.cpp:126-259 after the network (decode, greedy NMS, top-400, border erase, "
+                    "descriptor sampling) on one step's resident semi / descriptor grids, alone on the whole chip",
+            "frames_per_launch": B, "ms_per_frame": round(post_ms, 5),
+            "stage_ms_per_frame": {k: round(pp[k][0] / (reps * B), 5) for k in ("decode", "nms_rounds", "nms_select",
+                                                                                "sample") if k in pp},
+            "roofline": {"bound": "hbm", "algorithmic_bytes_per_frame": POST_BYTES_PER_FRAME,
+                         "achieved": round(POST_BYTES_PER_FRAME / (post_ms / 1e3) / 1e9, 2), "peak": 8000.0,
+                         "unit": "GB/s", "frac": round(POST_BYTES_PER_FRAME / (post_ms / 1e3) / 8e12, 5)}}
     return {"value": round(world * B * steps / el, 3), "unit": "frames/s", "ms_per_step": round(el / steps * 1e3, 3),
             "_match": alone, "_match_in_pipeline": prof.get("match"), "steps": steps, "frames_per_gpu_per_step": B,
+            "postprocess_alone": post,
             "workload": "config[3] offline batch: per-GPU SuperPoint extract + ratio matching + F-RANSAC + 3D-3D "
                         "RANSAC (E fallback) over consecutive frame pairs, no tracking state",
             "parallelism": f"frame-sharded x{world}" + (" + RCCL all-gather of feature records" if world > 1 else "")}

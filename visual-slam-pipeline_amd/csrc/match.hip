@@ -499,6 +499,10 @@ static void launch_tile(MatchArgs& a, int P, int cap_q, int cap_t, bool norms, h
 // lone-pair time is not per-chunk load latency), and 80 x 80 workgroups of five waves (no padding
 // and 5 instead of 7 stagings per row, but five waves on four SIMDs: 13-16 % slower).
 // VS_MATCH_TILE = small | k64 | k64d | k32d | deep | t80 selects those (experiments).
+// r03 sweep (profiles/r03b_match_sweep.json, kernel durations alone on the chip, 400 x 400 pairs):
+// one pair 16.3 us with 64 x 64 tiles vs 10.9 us with 32 x 32 (q32t32, four 16 x 16 waves), which
+// loses at 32 pairs (52.3 vs 43.0 us) and 512 (0.39 vs 0.51 of the fp32 MFMA peak); 32 x 64 /
+// 64 x 32 tiles and 8-wave 64 x 64 workgroups sit in between.  So P <= 2 takes 32 x 32 tiles.
 static void launch(MatchArgs& a, int P, int cap_q, int cap_t, bool norms, hipStream_t s) {
     static const char* force = std::getenv("VS_MATCH_TILE");
     if (force && std::strcmp(force, "small") == 0)
@@ -523,6 +527,10 @@ static void launch(MatchArgs& a, int P, int cap_q, int cap_t, bool norms, hipStr
         launch_tile<2, 4, 32, 16, 32, 1>(a, P, cap_q, cap_t, norms, s);
     else if (force && std::strcmp(force, "w8k64") == 0)
         launch_tile<2, 4, 32, 16, 64, 1>(a, P, cap_q, cap_t, norms, s);
+    else if (force && std::strcmp(force, "default") == 0)
+        launch_tile<2, 2, 32, 32, 32, 1>(a, P, cap_q, cap_t, norms, s);
+    else if (P <= 2)  // one or two pairs: 32 x 32 tiles (169 workgroups per 400 x 400 pair) fill the CUs
+        launch_tile<2, 2, 16, 16, 32, 1>(a, P, cap_q, cap_t, norms, s);
     else
         launch_tile<2, 2, 32, 32, 32, 1>(a, P, cap_q, cap_t, norms, s);
 }

@@ -435,7 +435,8 @@ __global__ __launch_bounds__(1024) void k_nms_select(const unsigned long long* _
     }
     __shared__ int hist[256];
     __shared__ unsigned long long s_sel[kSelSort];
-    __shared__ int s_nsel, s_wties;
+    __shared__ int s_nsel;
+    __shared__ int s_wk[16], s_ww[16], s_wo[16];
     __shared__ unsigned long long s_prefix, s_mask, s_next;
     __shared__ int s_krem;
     int nk = keycnt[b];
@@ -478,7 +479,6 @@ __global__ __launch_bounds__(1024) void k_nms_select(const unsigned long long* _
     }
     if (threadIdx.x == 0) {
         s_nsel = 0;
-        s_wties = 0;
         s_next = 0;
     }
     for (int i = threadIdx.x; i < kSelSort; i += blockDim.x) s_sel[i] = 0;
@@ -491,26 +491,6 @@ __global__ __launch_bounds__(1024) void k_nms_select(const unsigned long long* _
         } else if (K > 0) {
             atomicMax(&s_next, k);  // the (K+1)-th kept key
         }
-    }
-    __syncthreads();
-    // window ties of the selected pixels (each lane one pixel, 80 heatmap reads)
-    if ((int)threadIdx.x < K && (int)threadIdx.x < kSelSort) {
-        const unsigned long long k = s_sel[threadIdx.x];
-        const unsigned idx = 0xFFFFFFFFu - (unsigned)(k & 0xFFFFFFFFull);
-        const int px = (int)(idx % (unsigned)Wp), py = (int)(idx / (unsigned)Wp);
-        const unsigned sc = (unsigned)(k >> 32);
-        const float* hb = heat + (size_t)b * Hp * Wp;
-        bool tie = false;
-        for (int dy = -kRadius; dy <= kRadius; dy++) {
-            const int y = py + dy;
-            if (y < 0 || y >= Hp) continue;
-            for (int dx = -kRadius; dx <= kRadius; dx++) {
-                const int x = px + dx;
-                if (x < 0 || x >= Wp || (dx == 0 && dy == 0)) continue;
-                tie |= __float_as_uint(hb[(size_t)y * Wp + x]) == sc;
-            }
-        }
-        if (tie) atomicAdd(&s_wties, 1);
     }
     __syncthreads();
     // bitonic sort, descending (zero keys pad the tail)
@@ -530,32 +510,57 @@ __global__ __launch_bounds__(1024) void k_nms_select(const unsigned long long* _
             __syncthreads();
         }
     }
+    // keypoint records in priority order with the border erase, one selected pixel per thread
+    // (order-preserving ballot compaction), and the frame's window / order ties
+    const int i = threadIdx.x, lane = i & 63, wv = i >> 6;
+    bool keep = false, wtie = false, otie = false;
+    vs_keypoint kp;
+    if (i < K && i < kSelSort) {
+        const unsigned long long k = s_sel[i];
+        const unsigned idx = 0xFFFFFFFFu - (unsigned)(k & 0xFFFFFFFFull);
+        const int px = (int)(idx % (unsigned)Wp), py = (int)(idx / (unsigned)Wp);
+        const unsigned sc = (unsigned)(k >> 32);
+        keep = !(px >= w || py >= h);
+        kp.x = (float)px;
+        kp.y = (float)py;
+        kp.size = 8.0f;
+        kp.angle = -1.0f;
+        kp.response = __uint_as_float(sc);
+        kp.octave = 0;
+        kp.class_id = -1;
+        otie = (i > 0 && (unsigned)(s_sel[i - 1] >> 32) == sc) || (i + 1 < K && (unsigned)(s_sel[i + 1] >> 32) == sc);
+        const float* hb = heat + (size_t)b * Hp * Wp;
+        for (int dy = -kRadius; dy <= kRadius; dy++) {
+            const int y = py + dy;
+            if (y < 0 || y >= Hp) continue;
+            for (int dx = -kRadius; dx <= kRadius; dx++) {
+                const int x = px + dx;
+                if (x < 0 || x >= Wp || (dx == 0 && dy == 0)) continue;
+                wtie |= __float_as_uint(hb[(size_t)y * Wp + x]) == sc;
+            }
+        }
+    }
+    const unsigned long long bk = __ballot(keep), bw = __ballot(wtie), bo = __ballot(otie);
+    if (lane == 0) {
+        s_wk[wv] = __popcll(bk);
+        s_ww[wv] = __popcll(bw);
+        s_wo[wv] = __popcll(bo);
+    }
+    __syncthreads();
+    if (keep) {
+        int off = __popcll(bk & ((1ull << lane) - 1ull));
+        for (int k2 = 0; k2 < wv; k2++) off += s_wk[k2];
+        kps[(size_t)b * cap + off] = kp;
+    }
     if (threadIdx.x == 0) {
-        int n = 0;
-        for (int i = 0; i < K && n < cap; i++) {
-            unsigned long long k = s_sel[i];
-            unsigned idx = 0xFFFFFFFFu - (unsigned)(k & 0xFFFFFFFFull);
-            int x = (int)(idx % (unsigned)Wp), y = (int)(idx / (unsigned)Wp);
-            if (x >= w || y >= h) continue;
-            vs_keypoint kp;
-            kp.x = (float)x;
-            kp.y = (float)y;
-            kp.size = 8.0f;
-            kp.angle = -1.0f;
-            kp.response = __uint_as_float((unsigned)(k >> 32));
-            kp.octave = 0;
-            kp.class_id = -1;
-            kps[(size_t)b * cap + n] = kp;
-            n++;
+        int n = 0, wt = 0, ot = 0;
+        for (int k2 = 0; k2 < 16; k2++) {
+            n += s_wk[k2];
+            wt += s_ww[k2];
+            ot += s_wo[k2];
         }
         nout[b] = n;
-        const int wt = s_wties;
         const int ct = (K > 0 && K < nk && (s_next >> 32) == (kth >> 32)) ? 1 : 0;
-        int ot = 0;  // selected keypoints sharing their score with another one (list order)
-        for (int i = 0; i < K && i < kSelSort; i++) {
-            const unsigned sc = (unsigned)(s_sel[i] >> 32);
-            ot += (i > 0 && (unsigned)(s_sel[i - 1] >> 32) == sc) || (i + 1 < K && (unsigned)(s_sel[i + 1] >> 32) == sc);
-        }
         ties[3 * b] = wt;
         ties[3 * b + 1] = ct;
         ties[3 * b + 2] = ot;
