@@ -27,9 +27,10 @@ the reference's fallback scale (Slam.cpp:976-980), ATE after sim(3) alignment; M
 roofline line (midas.roofline).
 
 roofline — the dominant throughput-bound kernel (the fused SuperPoint conv1, fp32 MFMA) measured
-with HIP events on its stream during the timed region (the tracker extracts each batch in growing
-chunks on its own stream and CU set, overlapped with tracking; FLOPs per launch = per-frame FLOPs x
-frames per launch); the latency-bound tracking stages are
+with HIP events on its stream during the timed region (the tracker extracts each batch in even
+chunks of 8 frames on its own stream and CU set, overlapped with tracking; FLOPs per launch =
+per-frame FLOPs x frames per launch; traffic per launch = the single-chunk-size PMC pass's bytes per
+frame x frames per launch); the latency-bound tracking stages are
 reported per frame in stage_ms_per_frame.  cpu_baseline — the oracle (CPU restatement: OpenMP
 SuperPoint + the same tracking loop over the CPU stages) on a bounded prefix of the same sequence.
 
@@ -212,6 +213,10 @@ def cpu_baseline(L, nframes, ba=None):
         pass
     return {"value": nframes / dt, "unit": "frames/s", "cores": threads, "kind": "port", "cpu_model": model,
             "local_ba": ba_cpu,
+            "caveats": "a restatement, not the reference binary (OpenCV / ONNX Runtime / g2o are absent): the network "
+                       "is the oracle's OpenMP fp32 direct convolution, not ONNX Runtime's MLAS (SURVEY.md 8(d)); "
+                       "matching is the exact 2-NN FLANN approximates, AVX2-vectorised and bit-identical to the GPU "
+                       "(the reference's randomized kd-tree: ~2-5 ms per 400 x 400 pair, SURVEY.md A7)",
             "ms_per_frame": {"extract": round(t_ext / nframes * 1e3, 3), "track": round(t_trk / nframes * 1e3, 3),
                              **stages},
             "full_table": "profiles/r02_cpu_baseline.json (200 frames at 1, 4, 16 threads; tools/cpu_baseline.py)",
@@ -259,7 +264,7 @@ def local_ba(ctx, reps):
            "roofline": {"bound": "latency (hbm reported)", "algorithmic_bytes_per_iteration": bpi,
                         "achieved": round(bpi / (ms / max(iters, 1) / 1e3) / 1e9, 3), "peak": 8000.0,
                         "unit": "GB/s", "frac": round(bpi / (ms / max(iters, 1) / 1e3) / 8e12, 6)},
-           "stage_ms_per_call": {k: round(v[0] / reps, 4) for k, v in prof.items()}}
+           "stage_ms_per_call": {k: round(v[0] / reps, 4) for k, v in prof.items() if v[1]}}
     return res, (R, t, P0, kf, pt, uv, iters)
 
 
@@ -506,6 +511,7 @@ def main():
     torch.cuda.synchronize()
     run_steps(0, args.warmup)
     torch.cuda.synchronize()
+    ctx.tie_stats(reset=True)
     ctx.profile(True)
     ctx.profile_reset()
     if world > 1:
@@ -519,6 +525,7 @@ def main():
     elapsed = time.perf_counter() - t0
     prof = ctx.profile_read()
     ctx.profile(False)
+    ties = ctx.tie_stats()  # the timed frames' NMS ties (after the timed region: it synchronises)
     progress(f"timed region done: {args.steps} steps in {elapsed:.2f} s")
     if world > 1:
         tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
@@ -615,6 +622,10 @@ def main():
             "ate": {"rank0_rmse_m": round(a["ate_rmse"], 4), "scale": round(a["scale"], 4), "frames": a["n"],
                     "reference": "Umeyama sim(3) alignment as main.cpp:258-332, synthetic ground truth"},
             "tracker_stats": stats,
+            "nms_ties": dict(ties, note="per timed frame (vs_nms_tie_stats): window / cut ties can change the keypoint "
+                                        "set vs the reference's unstable std::sort (FeatureExtractor.cpp:238), order "
+                                        "ties only the order of equal-score keypoints in the list; zero = identical "
+                                        "for any tie order"),
             "dense_cloud_points": dense_points,
             "roofline": {
                 "kernel": f"{STAGE_KERNEL.get(dom, dom)} ({dom})",

@@ -33,6 +33,7 @@ _SIG = {
     "orc_postprocess": (_I, [_P, _P, _I, _I, _I, _I, _I, _I, _P, _P]),
     "orc_extract": (_I, [_P, _P, _I, _I, ctypes.c_size_t, _I, _I, _P, _P]),
     "orc_match_ratio": (None, [_P, _I, _P, _I, ctypes.c_float, _P, _P, _P, _P]),
+    "orc_match_ratio_scalar": (None, [_P, _I, _P, _I, ctypes.c_float, _P, _P, _P, _P]),
     "orc_match_ratio_f64": (None, [_P, _I, _P, _I, ctypes.c_float, _P, _P, _P, _P]),
     "orc_ransac_3d3d": (_I, [_P, _P, _I, _P, _P, _I, _I, _P, ctypes.c_uint32, _I, ctypes.c_double, _P, _P, _P]),
     "orc_track_local_map": (_I, [_P, _P, _P, _I, _P, _P, _I, _P, _P, _P, _I, _I, _P, _P, _P, _I, _P]),
@@ -187,14 +188,14 @@ def extract(weights, bgr, max_kp=400, nthreads=0):
     return kps[:n].copy(), desc[:n].copy()
 
 
-def match_ratio(d1, d2, ratio=0.75, f64=False):
+def match_ratio(d1, d2, ratio=0.75, f64=False, scalar=False):
     d1 = np.ascontiguousarray(d1, np.float32).reshape(-1, 256)
     d2 = np.ascontiguousarray(d2, np.float32).reshape(-1, 256)
     n1, n2 = d1.shape[0], d2.shape[0]
     raw = np.zeros(max(n1, 1), MATCH_DTYPE)
     good = np.zeros(max(n1, 1), MATCH_DTYPE)
     nr, ng = ctypes.c_int(0), ctypes.c_int(0)
-    fn = lib().orc_match_ratio_f64 if f64 else lib().orc_match_ratio
+    fn = lib().orc_match_ratio_f64 if f64 else lib().orc_match_ratio_scalar if scalar else lib().orc_match_ratio
     fn(_p(d1), n1, _p(d2), n2, ratio, _p(raw), ctypes.byref(nr), _p(good), ctypes.byref(ng))
     return raw[:nr.value].copy(), good[:ng.value].copy()
 

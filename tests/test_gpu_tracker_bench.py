@@ -3,7 +3,7 @@ F1: Slam::process_frame, reference src/Slam.cpp:809-1135, restated in host/track
 
 bench.py runs vs_slam_process_batch_dev with B = 32 frames per call, each batch's extraction
 prefetched behind the previous batch's (vs_slam_prefetch_batch_dev), the default extraction chunk
-schedule (3, 4, 5, 7, 8, 5) on its own CU-masked stream, the speculative next-frame chain and the
+schedule (even chunks of 8: 8, 8, 8, 8) on its own CU-masked stream, the speculative next-frame chain and the
 default VS_SLAM_TRACK_CUS, over the 126-frame closed loop replayed with continuing timestamps.  This test runs exactly that for
 the bench's 800 frames (6.3 laps, map past 30k points, 200+ keyframes so that loop closure runs,
 Slam.cpp:1084-1086) and the oracle tracker (oracle/orc_slam.cpp: the same control

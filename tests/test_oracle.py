@@ -281,3 +281,20 @@ def test_nms_score_floor_full_frame_dense():
     assert F > 0 and (heat >= F).sum() < 0.05 * (heat > np.float32(0.005)).sum()
     pruned = np.where(heat >= F, heat, np.float32(0)).astype(np.float32)
     assert restate.greedy_nms(pruned) == restate.greedy_nms(heat)
+
+
+@pytest.mark.parametrize("n1,n2,seed", [(400, 400, 1), (37, 513, 2), (1, 2, 3), (300, 33, 4)])
+def test_oracle_vector_matcher_equals_scalar(oracle, n1, n2, seed):
+    """The AVX2 path of orc_match_ratio (eight fmaf chains per register) == the scalar fmaf loops
+    bit for bit, including planted near-duplicates and exact ties."""
+    import synth
+    d1 = synth.random_descriptors(n1, seed)
+    d2 = synth.random_descriptors(n2, seed + 100)
+    k = min(n1, n2) // 2
+    d2[:k] = d1[:k] + 0.01 * synth.random_descriptors(k, seed + 200)
+    if n2 > 3:
+        d2[-1] = d2[0]  # an exact duplicate train row: the lower index wins
+    a = oracle.match_ratio(d1, d2)
+    b = oracle.match_ratio(d1, d2, scalar=True)
+    for x, y in zip(a, b):
+        assert np.array_equal(x.view(np.uint8), y.view(np.uint8))
