@@ -79,8 +79,10 @@ def nms_ties(heat, thr=0.005, radius=4, max_kp=400):
 
 
 def nms_floor(heat, thr=0.005, radius=4, max_kp=400):
-    """The GPU's score floor (sp_post.hip k_nms_lmax / k_nms_floor): the max_kp-th largest score
-    among strict local maxima (every other candidate in the window scores lower), 0 with fewer."""
+    """The score floor's exact value: the max_kp-th largest score among strict local maxima (every
+    other candidate in the window scores lower), 0 with fewer.  The GPU (sp_post.hip k_nms_lmax /
+    k_nms_floor) uses a lower bound of it (the lower edge of its 2^-7-octave histogram bin), which
+    prunes a subset of what this value prunes."""
     H, W = heat.shape
     c = np.where(heat > np.float32(thr), heat, np.float32(0))
     p = np.pad(c, radius)

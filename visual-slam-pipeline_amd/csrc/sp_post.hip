@@ -20,7 +20,9 @@
 // lower) is kept by the greedy whatever else happens.  So when a frame has at least 400 of them,
 // the 400th kept pixel scores at least the 400th-largest strict-local-maximum score F, and no
 // pixel scoring below F can be output or influence a pixel that can: those pixels start out
-// decided (out).  k_nms_lmax lists the strict local maxima, k_nms_floor selects F per frame.  On
+// decided (out).  k_nms_lmax histograms the strict local maxima's scores (2^-7-octave bins) and
+// k_nms_floor takes the lower edge of the bin holding the 400th largest — a lower bound of F, so
+// the argument holds and at most one bin's width more pixels stay undecided.  On
 // a camera frame (and on random-weight heatmaps, where nearly every pixel is a candidate) this
 // leaves a few hundred to a few thousand undecided pixels per frame, so the rounds converge in one
 // or two iterations and only tiles with undecided pixels run at all.
@@ -104,17 +106,28 @@ __global__ __launch_bounds__(256) void k_decode(const float* __restrict__ semi, 
 // scores (all candidates are > 0).
 constexpr int kNmsThreads = 256;
 
-// Strict local maxima of the candidate heatmap -> per-frame list of their score bits (any order).
-// One workgroup per 32x32 tile.
+// Strict local maxima of the candidate heatmap -> a per-frame histogram of their scores: bin =
+// (score bits >> 16) - kFloorBin0, i.e. 2^-7-octave bins over [2^-11, 2) (every candidate scores
+// in (0.005, 1]).  One workgroup per 32x32 tile; an LDS histogram per workgroup, flushed with one
+// global atomic per touched bin (same-address atomics per local maximum would serialise in L2).
+constexpr int kFloorBins = 2048;
+constexpr unsigned kFloorBin0 = 0x3A00u;  // bits >> 16 of 2^-11
+__device__ __forceinline__ int floor_bin(unsigned key) {
+    const int bin = (int)(key >> 16) - (int)kFloorBin0;
+    return bin < 0 ? 0 : bin >= kFloorBins ? kFloorBins - 1 : bin;
+}
+
 __global__ __launch_bounds__(kNmsThreads) void k_nms_lmax(const float* __restrict__ heat, int B, int Hp, int Wp,
-                                                          int tiles_x, unsigned* __restrict__ lm,
-                                                          int* __restrict__ lmcnt, int lm_cap) {
+                                                          int tiles_x, int* __restrict__ hist) {
     const int b = blockIdx.y;
     __shared__ unsigned s_key[kNmsReg * kNmsReg];
     __shared__ unsigned s_rmax[kNmsReg * kNmsTile];
+    __shared__ int s_hist[kFloorBins];
+    __shared__ int s_any;
     const int tx = blockIdx.x % tiles_x, ty = blockIdx.x / tiles_x;
     const int gx0 = tx * kNmsTile - kRadius, gy0 = ty * kNmsTile - kRadius;
     const float* hb = heat + (size_t)b * Hp * Wp;
+    if (threadIdx.x == 0) s_any = 0;
     for (int i = threadIdx.x; i < kNmsReg * kNmsReg; i += kNmsThreads) {
         const int ry = i / kNmsReg, rx = i - ry * kNmsReg;
         const int gy = gy0 + ry, gx = gx0 + rx;
@@ -125,6 +138,7 @@ __global__ __launch_bounds__(kNmsThreads) void k_nms_lmax(const float* __restric
         }
         s_key[i] = key;
     }
+    for (int i = threadIdx.x; i < kFloorBins; i += kNmsThreads) s_hist[i] = 0;
     __syncthreads();
     for (int i = threadIdx.x; i < kNmsReg * kNmsTile; i += kNmsThreads) {
         const int ry = i / kNmsTile, ix = i - ry * kNmsTile;
@@ -135,13 +149,11 @@ __global__ __launch_bounds__(kNmsThreads) void k_nms_lmax(const float* __restric
         s_rmax[i] = m;
     }
     __syncthreads();
-    const int lane = threadIdx.x & 63;
 #pragma unroll
     for (int j = 0; j < kNmsTile * kNmsTile / kNmsThreads; j++) {
         const int kk = threadIdx.x + kNmsThreads * j;
         const int iy = kk / kNmsTile, ix = kk - iy * kNmsTile;
         const unsigned key = s_key[(iy + kRadius) * kNmsReg + ix + kRadius];
-        bool lmx = false;
         if (key != 0 && gy0 + kRadius + iy < Hp && gx0 + kRadius + ix < Wp) {
             unsigned m = 0;
 #pragma unroll
@@ -150,63 +162,59 @@ __global__ __launch_bounds__(kNmsThreads) void k_nms_lmax(const float* __restric
                 int eq = 0;
                 for (int dy = 0; dy <= 2 * kRadius; dy++)
                     for (int dx = 0; dx <= 2 * kRadius; dx++) eq += s_key[(iy + dy) * kNmsReg + ix + dx] == key;
-                lmx = eq == 1;
+                if (eq == 1) {
+                    atomicAdd(&s_hist[floor_bin(key)], 1);
+                    s_any = 1;
+                }
             }
         }
-        const unsigned long long bal = __ballot(lmx);
-        if (bal) {
-            const int leader = __ffsll((long long)bal) - 1;
-            int base = 0;
-            if (lane == leader) base = atomicAdd(&lmcnt[b], __popcll(bal));
-            base = __shfl(base, leader);
-            const int o = base + __popcll(bal & ((1ull << lane) - 1ull));
-            if (lmx && o < lm_cap) lm[(size_t)b * lm_cap + o] = key;
-        }
     }
+    __syncthreads();
+    if (!s_any) return;
+    int* hg = hist + (size_t)b * kFloorBins;
+    for (int i = threadIdx.x; i < kFloorBins; i += kNmsThreads)
+        if (s_hist[i]) atomicAdd(&hg[i], s_hist[i]);
 }
 
-// Per frame: F = the max_kp-th largest strict-local-maximum score (bits), or 0 (no floor) when the
-// frame has fewer strict local maxima.  Exact MSB-first radix select, one workgroup per frame.
-__global__ __launch_bounds__(kNmsThreads) void k_nms_floor(const unsigned* __restrict__ lm, const int* __restrict__ lmcnt,
-                                                           int lm_cap, int max_kp, unsigned* __restrict__ floor_bits) {
-    const int b = blockIdx.x;
-    __shared__ int hist[256];
-    __shared__ unsigned s_prefix, s_mask;
-    __shared__ int s_krem;
-    const int n = min(lmcnt[b], lm_cap);
-    if (n < max_kp) {
-        if (threadIdx.x == 0) floor_bits[b] = 0u;
-        return;
+// Per frame: F = the lower edge of the histogram bin that holds the max_kp-th largest strict-local-
+// maximum score (a lower bound of that score, so at least max_kp strict local maxima score >= F),
+// or 0 (no floor) with fewer.  One workgroup per frame: a suffix scan over the bins from the top.
+__global__ __launch_bounds__(kNmsThreads) void k_nms_floor(const int* __restrict__ hist, int max_kp,
+                                                           unsigned* __restrict__ floor_bits) {
+    constexpr int PER = kFloorBins / kNmsThreads;  // bins per thread (thread 0 owns the top bins)
+    const int b = blockIdx.x, t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    const int* h = hist + (size_t)b * kFloorBins;
+    int v[PER], tot = 0;
+#pragma unroll
+    for (int k = 0; k < PER; k++) {  // thread t owns bins hi(t) down to hi(t) - PER + 1, top first
+        v[k] = h[kFloorBins - 1 - (t * PER + k)];
+        tot += v[k];
     }
-    const unsigned* l = lm + (size_t)b * lm_cap;
-    if (threadIdx.x == 0) {
-        s_prefix = 0;
-        s_mask = 0;
-        s_krem = max_kp;
+    int incl = tot;  // inclusive scan over threads in descending-bin order
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(incl, o);
+        if (lane >= o) incl += y;
     }
-    for (int pass = 0; pass < 4; pass++) {
-        const int shift = 24 - 8 * pass;
-        hist[threadIdx.x] = 0;
-        __syncthreads();
-        const unsigned pre = s_prefix, msk = s_mask;
-        for (int i = threadIdx.x; i < n; i += kNmsThreads) {
-            const unsigned k = l[i];
-            if ((k & msk) == pre) atomicAdd(&hist[(k >> shift) & 255], 1);
+    __shared__ int s_w[kNmsThreads / 64];
+    __shared__ unsigned s_floor;
+    if (lane == 63) s_w[wv] = incl;
+    if (t == 0) s_floor = 0u;
+    __syncthreads();
+    int before = incl - tot;
+    for (int w = 0; w < wv; w++) before += s_w[w];
+    // the thread whose range crosses max_kp names the bin
+    if (before < max_kp && before + tot >= max_kp) {
+        int run = before;
+#pragma unroll
+        for (int k = 0; k < PER; k++) {
+            if (run < max_kp && run + v[k] >= max_kp)
+                s_floor = (unsigned)(kFloorBins - 1 - (t * PER + k) + (int)kFloorBin0) << 16;
+            run += v[k];
         }
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            int rem = s_krem, acc = 0, d = 255;
-            for (; d > 0; d--) {
-                if (acc + hist[d] >= rem) break;
-                acc += hist[d];
-            }
-            s_krem = rem - acc;
-            s_prefix = pre | ((unsigned)d << shift);
-            s_mask = msk | (255u << shift);
-        }
-        __syncthreads();
     }
-    if (threadIdx.x == 0) floor_bits[b] = s_prefix;
+    __syncthreads();
+    if (t == 0) floor_bits[b] = s_floor;
 }
 
 // One NMS round over a 32x32 tile (+4 halo).  The tile iterates to its local fixed point, writes
@@ -405,12 +413,22 @@ __global__ __launch_bounds__(256) void k_nms_collect(const float* __restrict__ h
                                                      int* __restrict__ keycnt, int key_cap) {
     const int b = blockIdx.y;
     const int npx = Hp * Wp;
-    for (int i = blockIdx.x * 256 + threadIdx.x; i < npx; i += gridDim.x * 256) {
-        if (state[(size_t)b * npx + i] != ST_KEPT) continue;
-        float s = heat[(size_t)b * npx + i];
-        unsigned long long key = ((unsigned long long)__float_as_uint(s) << 32) | (unsigned)(0xFFFFFFFFu - (unsigned)i);
-        int slot = atomicAdd(&keycnt[b], 1);
-        if (slot < key_cap) keys[(size_t)b * key_cap + slot] = key;
+    const int lane = threadIdx.x & 63;
+    for (int i0 = blockIdx.x * 256; i0 < npx; i0 += gridDim.x * 256) {  // (uniform trip count per wave)
+        const int i = i0 + threadIdx.x;
+        const bool kept = i < npx && state[(size_t)b * npx + i] == ST_KEPT;
+        const unsigned long long bal = __ballot(kept);  // one atomic per wave
+        if (!bal) continue;
+        const int leader = __ffsll((long long)bal) - 1;
+        int base = 0;
+        if (lane == leader) base = atomicAdd(&keycnt[b], __popcll(bal));
+        base = __shfl(base, leader);
+        if (kept) {
+            const float s = heat[(size_t)b * npx + i];
+            const unsigned long long key = ((unsigned long long)__float_as_uint(s) << 32) | (unsigned)(0xFFFFFFFFu - (unsigned)i);
+            const int slot = base + __popcll(bal & ((1ull << lane) - 1ull));
+            if (slot < key_cap) keys[(size_t)b * key_cap + slot] = key;
+        }
     }
 }
 
@@ -645,14 +663,14 @@ int sp_postprocess(vs_ctx* ctx, int B, int hc, int wc, int h, int w, vs_keypoint
     VS_CHECK(ctx->heat.ensure(npx * sizeof(float)));
     VS_CHECK(ctx->state.ensure(npx));
     // flags (ints): [rounds + 1][B] undecided-after-round, the capacity word, ferr [B], keycnt [B],
-    // lmcnt [B], floor [B], ties [B][3]; then tile flags (bytes) [rounds + 1][B][ntiles]
-    const size_t nflag = (size_t)(kNmsMaxRounds + 1) * B + 1 + 7 * (size_t)B;
+    // floor [B], ties [B][3], the floor histograms [B][kFloorBins]; then tile flags (bytes)
+    // [rounds + 1][B][ntiles]
+    const size_t nflag = (size_t)(kNmsMaxRounds + 1) * B + 1 + 6 * (size_t)B + (size_t)B * kFloorBins;
     VS_CHECK(ctx->flags.ensure(nflag * sizeof(int) + (size_t)(kNmsMaxRounds + 1) * B * ntiles));
     VS_CHECK(ctx->nms_list.ensure(npx * 2 * sizeof(int)));
     const char* fr_env = getenv("VS_NMS_FINISH_ROUNDS");  // test knob: forces the error path
     const int finish_rounds = fr_env && atoi(fr_env) > 0 ? atoi(fr_env) : kFinishMaxRounds;
     VS_CHECK(ctx->keys.ensure((size_t)B * key_cap * sizeof(unsigned long long)));
-    VS_CHECK(ctx->lmax.ensure((size_t)B * key_cap * sizeof(unsigned)));  // strict local maxima
     if (!ctx->tie_totals.p) {
         VS_CHECK(ctx->tie_totals.ensure(5 * sizeof(unsigned long long)));
         VS_HIP(hipMemsetAsync(ctx->tie_totals.p, 0, 5 * sizeof(unsigned long long), s));
@@ -661,11 +679,10 @@ int sp_postprocess(vs_ctx* ctx, int B, int hc, int wc, int h, int w, vs_keypoint
     int* err = flags + (size_t)(kNmsMaxRounds + 1) * B;
     int* ferr = err + 1;
     int* keycnt = ferr + B;
-    int* lmcnt = keycnt + B;
-    unsigned* floor_bits = reinterpret_cast<unsigned*>(lmcnt + B);
-    int* ties = lmcnt + 2 * B;
+    unsigned* floor_bits = reinterpret_cast<unsigned*>(keycnt + B);
+    int* ties = keycnt + 2 * B;
+    int* fhist = ties + 3 * B;
     uint8_t* tflags = reinterpret_cast<uint8_t*>(flags + nflag);
-    unsigned* lm = ctx->lmax.as<unsigned>();
     {
         ProfScope ps(ctx, "decode", s);
         int ncell = B * hc * wc;
@@ -677,8 +694,8 @@ int sp_postprocess(vs_ctx* ctx, int B, int hc, int wc, int h, int w, vs_keypoint
         VS_HIP(hipMemsetAsync(flags, 0, nflag * sizeof(int) + (size_t)(kNmsMaxRounds + 1) * B * ntiles, s));
         VS_HIP(hipMemsetAsync(flags, 0x01, (size_t)B * sizeof(int), s));  // round 0 runs for every frame
         hipLaunchKernelGGL(k_nms_lmax, dim3(ntiles, B), dim3(kNmsThreads), 0, s, ctx->heat.as<float>(), B, Hp, Wp,
-                           tiles_x, lm, lmcnt, key_cap);
-        hipLaunchKernelGGL(k_nms_floor, dim3(B), dim3(kNmsThreads), 0, s, lm, lmcnt, key_cap, max_kp, floor_bits);
+                           tiles_x, fhist);
+        hipLaunchKernelGGL(k_nms_floor, dim3(B), dim3(kNmsThreads), 0, s, fhist, max_kp, floor_bits);
         for (int r = 0; r < kNmsMaxRounds; r++) {
             hipLaunchKernelGGL(k_nms_round, dim3(ntiles, B), dim3(kNmsThreads), 0, s, ctx->heat.as<float>(),
                                ctx->state.as<uint8_t>(), flags, tflags, floor_bits, r, B, Hp, Wp, tiles_x, ntiles);

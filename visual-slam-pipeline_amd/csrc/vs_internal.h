@@ -94,7 +94,6 @@ struct vs_ctx {
     // host-API staging
     vs::DevBuf h_img, h_kps, h_desc, h_n, h_aux0, h_aux1, h_aux2, h_aux3, h_aux4, h_aux5;
     vs::DevBuf match_keys, match_cnt, norms_sets, tlm, ba, pnp;
-    vs::DevBuf lmax;        // NMS: strict local maxima (score bits) per frame
     vs::DevBuf tie_totals;  // NMS tie accounting since the last reset: {frames, frames with a tie, window, cut, order}
 
     bool prof_on = false;
