@@ -407,28 +407,41 @@ __global__ __launch_bounds__(1024) void k_nms_finish(const float* __restrict__ h
     if (threadIdx.x == 0 && s_n[cur] != 0) ferr[b] = 1;
 }
 
-// Kept pixels -> 64-bit priority keys (score bits << 32 | ~raster index), unordered.
+// Kept pixels -> 64-bit priority keys (score bits << 32 | ~raster index), unordered.  Each thread
+// reads four state bytes at once; one atomic per wave reserves the wave's slots.
 __global__ __launch_bounds__(256) void k_nms_collect(const float* __restrict__ heat, const uint8_t* __restrict__ state,
                                                      int Hp, int Wp, unsigned long long* __restrict__ keys,
                                                      int* __restrict__ keycnt, int key_cap) {
     const int b = blockIdx.y;
-    const int npx = Hp * Wp;
+    const int npx = Hp * Wp, nq = npx / 4;  // Wp is a multiple of 8
     const int lane = threadIdx.x & 63;
-    for (int i0 = blockIdx.x * 256; i0 < npx; i0 += gridDim.x * 256) {  // (uniform trip count per wave)
-        const int i = i0 + threadIdx.x;
-        const bool kept = i < npx && state[(size_t)b * npx + i] == ST_KEPT;
-        const unsigned long long bal = __ballot(kept);  // one atomic per wave
-        if (!bal) continue;
-        const int leader = __ffsll((long long)bal) - 1;
-        int base = 0;
-        if (lane == leader) base = atomicAdd(&keycnt[b], __popcll(bal));
-        base = __shfl(base, leader);
-        if (kept) {
-            const float s = heat[(size_t)b * npx + i];
-            const unsigned long long key = ((unsigned long long)__float_as_uint(s) << 32) | (unsigned)(0xFFFFFFFFu - (unsigned)i);
-            const int slot = base + __popcll(bal & ((1ull << lane) - 1ull));
-            if (slot < key_cap) keys[(size_t)b * key_cap + slot] = key;
+    const uchar4* st = reinterpret_cast<const uchar4*>(state + (size_t)b * npx);
+    for (int q0 = blockIdx.x * 256; q0 < nq; q0 += gridDim.x * 256) {  // (uniform trip count per wave)
+        const int q = q0 + threadIdx.x;
+        uchar4 v = make_uchar4(0, 0, 0, 0);
+        if (q < nq) v = st[q];
+        const int f[4] = {v.x == ST_KEPT, v.y == ST_KEPT, v.z == ST_KEPT, v.w == ST_KEPT};
+        const int cnt = f[0] + f[1] + f[2] + f[3];
+        int incl = cnt;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int y = __shfl_up(incl, o);
+            if (lane >= o) incl += y;
         }
+        const int tot = __shfl(incl, 63);
+        if (tot == 0) continue;
+        int base = 0;
+        if (lane == 63) base = atomicAdd(&keycnt[b], tot);
+        base = __shfl(base, 63) + incl - cnt;
+#pragma unroll
+        for (int k = 0; k < 4; k++)
+            if (f[k]) {
+                const int i = 4 * q + k;
+                const unsigned long long key = ((unsigned long long)__float_as_uint(heat[(size_t)b * npx + i]) << 32) |
+                                               (unsigned)(0xFFFFFFFFu - (unsigned)i);
+                if (base < key_cap) keys[(size_t)b * key_cap + base] = key;
+                base++;
+            }
     }
 }
 
@@ -481,15 +494,33 @@ __global__ __launch_bounds__(1024) void k_nms_select(const unsigned long long* _
                 if ((k & msk) == pre) atomicAdd(&hist[(k >> shift) & 255], 1);
             }
             __syncthreads();
-            if (threadIdx.x == 0) {
-                int rem = s_krem, acc = 0, d = 255;
-                for (; d > 0; d--) {
-                    if (acc + hist[d] >= rem) break;
-                    acc += hist[d];
+            if (threadIdx.x < 64) {  // the digit holding the rem-th largest: a suffix scan on wave 0
+                const int lane = threadIdx.x, rem = s_krem;
+                int c[4], sum = 0;
+#pragma unroll
+                for (int k = 0; k < 4; k++) {  // lane l owns digits 255 - 4l .. 252 - 4l, top first
+                    c[k] = hist[255 - 4 * lane - k];
+                    sum += c[k];
                 }
-                s_krem = rem - acc;
-                s_prefix = pre | ((unsigned long long)d << shift);
-                s_mask = msk | (255ull << shift);
+                int incl = sum;
+#pragma unroll
+                for (int o = 1; o < 64; o <<= 1) {
+                    const int y = __shfl_up(incl, o);
+                    if (lane >= o) incl += y;
+                }
+                int acc = incl - sum;
+                if (acc < rem && acc + sum >= rem) {
+                    int d = 255 - 4 * lane;
+#pragma unroll
+                    for (int k = 0; k < 4; k++) {
+                        if (acc + c[k] >= rem) break;
+                        acc += c[k];
+                        d--;
+                    }
+                    s_krem = rem - acc;
+                    s_prefix = pre | ((unsigned long long)d << shift);
+                    s_mask = msk | (255ull << shift);
+                }
             }
             __syncthreads();
         }
