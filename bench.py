@@ -167,6 +167,10 @@ def parse():
     ap.add_argument("--frontend-steps", type=int, default=6, help="timed steps of the config[3] batch front end")
     ap.add_argument("--no-frontend", action="store_true")
     ap.add_argument("--ba-reps", type=int, default=5, help="timed calls of the config[2] local-BA window (0: skip)")
+    ap.add_argument("--stage-profile", choices=["network", "all", "none"], default="network",
+                    help="HIP-event stages inside the timed region (network: the extraction stages only)")
+    ap.add_argument("--track-profile-steps", type=int, default=4,
+                    help="extra steps after the timed region with every stage profiled (stage_ms_per_frame)")
     ap.add_argument("--mono-steps", type=int, default=4, help="timed steps of the config[4] monocular HD stream")
     ap.add_argument("--render-workers", type=int, default=0,
                     help="processes rendering the synthetic sequence (0: min(16, cpus / ranks); 1 under rocprofv3 "
@@ -512,7 +516,10 @@ def main():
     run_steps(0, args.warmup)
     torch.cuda.synchronize()
     ctx.tie_stats(reset=True)
-    ctx.profile(True)
+    # headline: per-stage events on the extraction stages only (the roofline kernel); the tracking
+    # stages' per-frame times come from a separate profiled pass (stage_ms_per_frame) so the timed
+    # loop carries no event records on the latency-bound tracking stream
+    ctx.profile(2 if args.stage_profile == "network" else bool(args.stage_profile == "all"))
     ctx.profile_reset()
     if world > 1:
         dist.barrier()
@@ -533,6 +540,19 @@ def main():
         elapsed = float(tt.item())
     frames_timed = B * args.steps
     value = world * frames_timed / elapsed
+
+    # per-stage times of the tracking stages: a few more steps with every stage's events on (kept
+    # out of the timed region; the tracker and the ATE below include these frames)
+    prof_trk, frames_trk = prof, frames_timed
+    if args.stage_profile != "all" and args.track_profile_steps > 0:
+        k0 = args.warmup + args.steps
+        ctx.profile(True)
+        ctx.profile_reset()
+        run_steps(k0, k0 + args.track_profile_steps)
+        torch.cuda.synchronize()
+        prof_trk = ctx.profile_read()
+        ctx.profile(False)
+        frames_trk = B * args.track_profile_steps
 
     # trajectory quality: RTS smoother, then the reference's ATE against the synthetic ground truth
     slam.finish()
@@ -558,12 +578,38 @@ def main():
     achieved = flops_per_launch / avg_s / 1e12
     net_ms = sum(v[0] for k, v in prof.items() if k in LAYER_FLOPS)
     net_flops = sum(LAYER_FLOPS.values()) * frames_timed
-    stage_ms = {k: round(v[0] / frames_timed, 4) for k, v in sorted(prof.items(), key=lambda kv: -kv[1][0])}
+    stage_ms = {k: round(v[0] / frames_timed, 4) for k, v in prof.items() if v[1]}
+    stage_ms.update({k: round(v[0] / frames_trk, 4) for k, v in prof_trk.items() if v[1] and k not in stage_ms})
+    stage_ms = dict(sorted(stage_ms.items(), key=lambda kv: -kv[1]))
     traffic_pf, traffic_tag, traffic_fpl = pmc_traffic(STAGE_KERNEL.get(dom, ""))
     traffic = round(traffic_pf * frames_per_launch) if traffic_pf is not None else None
 
+    # the dominant kernel alone: one extraction chunk (8 frames) and a whole step (B frames) through
+    # the network on the whole chip, nothing else running (HIP events on the launch stream)
+    alone = {}
+    for nb in (8, B):
+        semi_t = torch.zeros((nb, 60, 80, vslam_abi.SEMI_CH), dtype=torch.float32, device=dev)
+        dg_t = torch.zeros((nb, 60, 80, vslam_abi.DESC_DIM), dtype=torch.float32, device=dev)
+        sa = torch.cuda.current_stream().cuda_stream
+        ctx.network_batch_dev(nb, bgr[0].data_ptr(), H, W, semi_t.data_ptr(), dg_t.data_ptr(), sa)
+        torch.cuda.synchronize()
+        ctx.profile(True)
+        ctx.profile_reset()
+        for _ in range(5):
+            ctx.network_batch_dev(nb, bgr[0].data_ptr(), H, W, semi_t.data_ptr(), dg_t.data_ptr(), sa)
+        torch.cuda.synchronize()
+        pa = ctx.profile_read()
+        ctx.profile(False)
+        ms_l, n_l = pa[dom]
+        a_ach = LAYER_FLOPS[dom] * nb / (ms_l / 1e3 / n_l) / 1e12
+        net_l = sum(v[0] for k, v in pa.items() if k in LAYER_FLOPS)
+        alone[f"frames_per_launch_{nb}"] = {"avg_launch_ms": round(ms_l / n_l, 4), "achieved": round(a_ach, 3),
+                                            "frac": round(a_ach / FP32_MFMA_PEAK_TFLOPS, 4),
+                                            "network_tflops": round(sum(LAYER_FLOPS.values()) * nb * 5 / (net_l / 1e3) / 1e12, 3)}
+        del semi_t, dg_t
+
     track_cus = int(os.environ.get("VS_SLAM_TRACK_CUS", "32"))
-    mroof = {"tracker": match_roofline(prof.get("match"), 1, track_cus,
+    mroof = {"tracker": match_roofline(prof_trk.get("match"), 1, track_cus,
                                        "tracking loop: one pair (frame vs reference keyframe) per launch on the "
                                        f"tracker's {track_cus}-CU stream (overlapped with extraction on the rest)")}
     fe = None
@@ -646,10 +692,15 @@ def main():
                 "flops_per_launch": round(flops_per_launch),
                 "note": "network on the extraction stream's CU set (all CUs but VS_SLAM_TRACK_CUS = 32), "
                         "overlapped with tracking; peak is the whole chip's",
+                "alone_whole_chip": alone,
             },
             "match_roofline": mroof,
             "network_tflops": round(net_flops / (net_ms / 1e3) / 1e12, 3),
             "stage_ms_per_frame": stage_ms,
+            "stage_profile": {"timed_region": args.stage_profile,
+                              "tracking_stages_from": (f"{args.track_profile_steps} extra steps after the timed region "
+                                                       "with every stage's HIP events on") if prof_trk is not prof
+                              else "the timed region"},
             "frontend_batch": fe,
             "monocular_hd": mono,
             "local_ba": lba,

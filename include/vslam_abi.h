@@ -500,7 +500,9 @@ int vs_nms_tie_stats(vs_ctx* ctx, long long out[5], int reset);
 /* ---- profiling ----------------------------------------------------------------------- */
 /* When enabled, every stage of the _dev pipelines brackets its launches with hipEvents on the
  * stream it runs on; vs_profile_read returns per-stage accumulated milliseconds and launch
- * counts since the last reset.  Stage names are static strings. */
+ * counts since the last reset.  Stage names are static strings.  on: 0 off, 1 every stage,
+ * 2 the extraction stages only (network, post-processing, MiDaS: a tracker's host loop then runs
+ * without per-stage event records). */
 int vs_profile_enable(vs_ctx* ctx, int on);
 int vs_profile_reset(vs_ctx* ctx);
 int vs_profile_read(vs_ctx* ctx, int max_stages, const char** names, double* ms, int* launches,

@@ -64,8 +64,20 @@ static hipEvent_t take_event(vs_ctx* c) {
     return e;
 }
 
+// Stages of the extraction path (network + post-processing + MiDaS): profile mode 2 times only these,
+// so a tracker's latency-bound host loop runs without per-stage event records.
+static bool extraction_stage(const char* name) {
+    static const char* const kNames[] = {"gray_norm", "conv1_fused", "conv2a", "conv2b_pool", "conv3a", "conv3b_pool",
+                                         "conv4a", "conv4b", "head_a", "head_b", "desc_l2norm", "decode", "nms_rounds",
+                                         "nms_select", "sample", "midas_pre", "midas_net", "midas_post"};
+    for (const char* k : kNames)
+        if (std::strcmp(k, name) == 0) return true;
+    return false;
+}
+
 ProfScope::ProfScope(vs_ctx* c, const char* name, hipStream_t st) : ctx(c), stage(-1), s(st) {
     if (!ctx->prof_on) return;
+    if (ctx->prof_mode == 2 && !extraction_stage(name)) return;
     std::lock_guard<std::mutex> lk(ctx->prof_mu);
     for (size_t i = 0; i < ctx->prof.size(); i++)
         if (std::strcmp(ctx->prof[i].name, name) == 0) stage = (int)i;
@@ -856,7 +868,16 @@ int vs_nms_tie_stats(vs_ctx* ctx, long long out[5], int reset) {
 
 int vs_profile_enable(vs_ctx* ctx, int on) {
     VS_ARG(ctx, "vs_profile_enable: null ctx");
+    VS_ARG(on >= 0 && on <= 2, "vs_profile_enable: mode 0, 1 or 2");
+    std::lock_guard<std::mutex> lk(ctx->prof_mu);
     ctx->prof_on = on != 0;
+    ctx->prof_mode = on;
+    // events up front: a hipEventCreate inside a timed loop costs more than the record itself
+    while (on && ctx->event_pool.size() < 4096) {
+        hipEvent_t e = nullptr;
+        VS_HIP(hipEventCreate(&e));
+        ctx->event_pool.push_back(e);
+    }
     return VS_OK;
 }
 

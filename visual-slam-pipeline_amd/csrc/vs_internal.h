@@ -97,6 +97,7 @@ struct vs_ctx {
     vs::DevBuf tie_totals;  // NMS tie accounting since the last reset: {frames, frames with a tie, window, cut, order}
 
     bool prof_on = false;
+    int prof_mode = 0;  // 1: every stage, 2: extraction stages only (vs_profile_enable)
     std::vector<vs::ProfStage> prof;
     std::vector<hipEvent_t> event_pool;
     std::mutex prof_mu;  // a vs_slam enqueues its next batch's extraction from a helper thread

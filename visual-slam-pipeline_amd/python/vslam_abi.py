@@ -472,7 +472,8 @@ class Context:
         return dict(zip(("frames", "frames_with_tie", "window_ties", "cut_ties", "order_ties"), (int(v) for v in out)))
 
     def profile(self, on=True):
-        _check(self.lib.vs_profile_enable(self.h, 1 if on else 0))
+        """on: False / True (every stage) / 2 (extraction stages only)."""
+        _check(self.lib.vs_profile_enable(self.h, int(on) if on is not True else 1))
 
     def profile_reset(self):
         _check(self.lib.vs_profile_reset(self.h))
