@@ -567,17 +567,19 @@ def main():
 
     # dominant throughput-bound kernel: the network layer with the largest device time (HIP
     # events on the stream the kernels run on, accumulated over the timed region)
-    conv = {k: v for k, v in prof.items() if k in LAYER_FLOPS}
-    dom = max(conv, key=lambda k: conv[k][0])
-    dom_ms, dom_launches = conv[dom]
+    # (--stage-profile none, a diagnostic: the network's events come from the extra profiled steps)
+    net_prof, net_frames = (prof, frames_timed) if any(k in LAYER_FLOPS for k in prof) else (prof_trk, frames_trk)
+    conv = {k: v for k, v in net_prof.items() if k in LAYER_FLOPS}
+    dom = max(conv, key=lambda k: conv[k][0]) if conv else "conv1_fused"
+    dom_ms, dom_launches = conv.get(dom, (float("nan"), 1))
     # the tracker extracts each batch in even chunks (8, 8, 8, 8 frames at B = 32, tracker.hip
     # enqueue_extraction) overlapped with tracking: a launch covers frames_timed / launches frames
     avg_s = dom_ms / 1e3 / dom_launches
-    frames_per_launch = frames_timed / dom_launches
+    frames_per_launch = net_frames / dom_launches
     flops_per_launch = LAYER_FLOPS[dom] * frames_per_launch
     achieved = flops_per_launch / avg_s / 1e12
-    net_ms = sum(v[0] for k, v in prof.items() if k in LAYER_FLOPS)
-    net_flops = sum(LAYER_FLOPS.values()) * frames_timed
+    net_ms = sum(v[0] for v in conv.values()) if conv else float("nan")
+    net_flops = sum(LAYER_FLOPS.values()) * net_frames
     stage_ms = {k: round(v[0] / frames_timed, 4) for k, v in prof.items() if v[1]}
     stage_ms.update({k: round(v[0] / frames_trk, 4) for k, v in prof_trk.items() if v[1] and k not in stage_ms})
     stage_ms = dict(sorted(stage_ms.items(), key=lambda kv: -kv[1]))
@@ -698,6 +700,7 @@ def main():
             "network_tflops": round(net_flops / (net_ms / 1e3) / 1e12, 3),
             "stage_ms_per_frame": stage_ms,
             "stage_profile": {"timed_region": args.stage_profile,
+                              "network_from": "the timed region" if net_prof is prof else "the extra profiled steps",
                               "tracking_stages_from": (f"{args.track_profile_steps} extra steps after the timed region "
                                                        "with every stage's HIP events on") if prof_trk is not prof
                               else "the timed region"},
