@@ -332,8 +332,11 @@ __global__ __launch_bounds__(256, (KS == 3 && CKV == 32) ? 1 : ((CKV == 8 || (KS
 // 8 x 32 block, so no MFMA row is spent on columns past the image edge (8 x 32 tiles waste 22% of
 // the grid at W = 80).  The LDS patch holds the rows those pixels span plus the halo, full width
 // (tiles_y = patch rows, <= 640 patch pixels), and every lane addresses its own pixel in it.
-template <bool POOL, int LAYER, bool FUSE1A, bool LIN = false, int CKT = 8>
-__global__ __launch_bounds__(256, CKT == 4 ? 3 : 2) void k_conv3_db(
+// MB = 32-pixel M blocks per wave: 2 (256-pixel tiles), or 1 for linear tiles of 128 pixels
+// (the 60 x 80 conv4 layers: 152 tiles of 256 pixels x 2 channel tiles per 8 frames fill only
+// 45 % of the workgroup slots of 224 CUs; half-height tiles double the grid).
+template <bool POOL, int LAYER, bool FUSE1A, bool LIN = false, int CKT = 8, int MB = 2>
+__global__ __launch_bounds__(256, CKT == 4 ? (MB == 1 ? 4 : 3) : 2) void k_conv3_db(
     const float* __restrict__ in, int in_cstride, int in_coff, const float* __restrict__ wt,
     const float* __restrict__ bias, int cin, int cout, int cout_pad, float* __restrict__ out,
     int out_cstride, int out_coff, int B, int H, int W, int tiles_x, int tiles_y, int relu,
@@ -341,7 +344,8 @@ __global__ __launch_bounds__(256, CKT == 4 ? 3 : 2) void k_conv3_db(
     // CKT input channels per chunk: 8 (two workgroups per CU), or 4 (about half the LDS, three
     // workgroups per CU, twice the chunk barriers)
     constexpr int CK = CKT, TW = 32, TH = 8, PW = TW + 2, PH = TH + 2, NPIX = PW * PH;
-    constexpr int NPIXC = LIN ? 640 : NPIX;         // patch capacity
+    constexpr int TPIX = 128 * MB;                  // linear tile pixels
+    constexpr int NPIXC = LIN ? (MB == 2 ? 640 : 448) : NPIX;  // patch capacity
     constexpr int Q = CK / 4;                       // float4 per pixel and chunk
     constexpr int NQ = (NPIXC * Q + 255) / 256;     // input float4 per thread
     constexpr int NWV = 9 * CK * 16;                // weight float4 per chunk
@@ -351,6 +355,7 @@ __global__ __launch_bounds__(256, CKT == 4 ? 3 : 2) void k_conv3_db(
     constexpr int SW = S - 6;                       // k-step at which staged loads go to LDS
     static_assert(NPIX > 256 && NPIX <= 512 && 4 * (CK - 1) + 2 < S, "conv3_db geometry");
     static_assert(!LIN || (!POOL && !FUSE1A), "linear tiles: plain 3x3 layers only");
+    static_assert(MB == 2 || (MB == 1 && LIN), "half-height tiles: linear layers only");
     __shared__ float s_in[2][CK * NPIXC];
     __shared__ __attribute__((aligned(16))) float s_w[2][9 * CK * 64];
     __shared__ float s_g[FUSE1A ? GW * GH : 1];
@@ -366,7 +371,7 @@ __global__ __launch_bounds__(256, CKT == 4 ? 3 : 2) void k_conv3_db(
     int b, y0, x0, m0 = 0;
     if constexpr (LIN) {  // tiles_x = tiles per image, tiles_y = patch rows
         b = tile / tiles_x;
-        m0 = (tile - b * tiles_x) * 256;
+        m0 = (tile - b * tiles_x) * TPIX;
         y0 = m0 / W;  // first image row of the tile
         x0 = 0;
     } else {
@@ -381,11 +386,11 @@ __global__ __launch_bounds__(256, CKT == 4 ? 3 : 2) void k_conv3_db(
     const int pw = LIN ? W + 2 : PW;           // patch row pitch
     const int npix = LIN ? pw * tiles_y : NPIX;  // patch pixels (per channel)
     // A-operand base of this lane's pixel in the two M blocks (patch position of tap (0, 0))
-    int abase[2];
+    int abase[2] = {0, 0};
 #pragma unroll
-    for (int r = 0; r < 2; r++) {
+    for (int r = 0; r < MB; r++) {
         if constexpr (LIN) {
-            int m = m0 + (2 * wv + r) * 32 + li;
+            int m = m0 + (MB * wv + r) * 32 + li;
             m = m < HW ? m : HW - 1;  // past the image end: any in-patch pixel, never stored
             const int y = m / W, x = m - y * W;
             abase[r] = (y - y0) * pw + x;
@@ -551,9 +556,11 @@ __global__ __launch_bounds__(256, CKT == 4 ? 3 : 2) void k_conv3_db(
             __builtin_amdgcn_sched_barrier(0);
             acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(A0[c_], B1[c_], acc[0][1], 0, 0, 0);
             if (c1a && s % 4 == 2) conv1a_px(1, s / 4, nxt, wq);
-            __builtin_amdgcn_sched_barrier(0);
-            acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(A1[c_], B0[c_], acc[1][0], 0, 0, 0);
-            acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(A1[c_], B1[c_], acc[1][1], 0, 0, 0);
+            if constexpr (MB == 2) {
+                __builtin_amdgcn_sched_barrier(0);
+                acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(A1[c_], B0[c_], acc[1][0], 0, 0, 0);
+                acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(A1[c_], B1[c_], acc[1][1], 0, 0, 0);
+            }
         }
         __syncthreads();
     }
@@ -579,14 +586,14 @@ __global__ __launch_bounds__(256, CKT == 4 ? 3 : 2) void k_conv3_db(
             }
         } else {
 #pragma unroll
-            for (int r = 0; r < 2; r++) {
+            for (int r = 0; r < MB; r++) {
 #pragma unroll
                 for (int reg = 0; reg < 16; reg++) {
                     const int px = (reg & 3) + 8 * (reg >> 2) + 4 * lh;
                     float v = acc[r][nb][reg] + bv;
                     if (relu) v = fmaxf(v, 0.0f);
                     if constexpr (LIN) {
-                        const int m = m0 + (2 * wv + r) * 32 + px;
+                        const int m = m0 + (MB * wv + r) * 32 + px;
                         if (m < HW) out[((size_t)b * HW + m) * out_cstride + out_coff + n] = v;
                     } else {
                         const int y = y0 + 2 * wv + r, x = x0 + px;
@@ -671,15 +678,34 @@ int conv3(vs_ctx* ctx, const DevLayer& L, const float* in, int in_cstride, int i
         const int lin_rows = (W - 1 + 255) / W + 1 + 2;
         if (!POOL && W % 32 != 0 && lin_rows * (W + 2) <= 640 && conv3_db_enabled() && L.cin % 8 == 0 &&
             L.cout_pad % 64 == 0 && in_cstride % 4 == 0 && in_coff % 4 == 0) {
-            const int tiles = (H * W + 255) / 256;
-            dim3 grid((unsigned)(B * tiles * (L.cout_pad / 64)));
+            const int ntn = L.cout_pad / 64;
             // conv4a / conv4b / the fused head: 4-channel chunks, three workgroups per CU (39 KB LDS, 134
             // VGPRs; same-box A/B over 3 runs each: the three layers 0.1051 -> 0.0993 ms per frame).
-            // VS_CONV_LIN_CK=8 restores 8-channel chunks.
+            // VS_CONV_LIN_CK=8 restores 8-channel chunks.  A grid of fewer than 1024 256-pixel
+            // workgroups (conv4a / conv4b: 304 per 8 frames) runs 128-pixel tiles instead
+            // (VS_CONV_LIN_MB = 1 / 2 forces one size).
             static const int ck = [] {
                 const char* e = std::getenv("VS_CONV_LIN_CK");
                 return e ? std::atoi(e) : 4;
             }();
+            static const int mb_env = [] {
+                const char* e = std::getenv("VS_CONV_LIN_MB");
+                return e ? std::atoi(e) : 0;
+            }();
+            const int tiles256 = (H * W + 255) / 256;
+            const int mb = mb_env == 1 || mb_env == 2 ? mb_env : ((long)B * tiles256 * ntn < 1024 ? 1 : 2);
+            const int lin_rows1 = (W - 1 + 127) / W + 1 + 2;
+            if (ck == 4 && mb == 1 && lin_rows1 * (W + 2) <= 448) {
+                const int tiles = (H * W + 127) / 128;
+                dim3 grid((unsigned)(B * tiles * ntn));
+                hipLaunchKernelGGL((k_conv3_db<false, LAYER, false, true, 4, 1>), grid, dim3(256), 0, s, in,
+                                   in_cstride, in_coff, L.w, L.b, L.cin, L.cout, L.cout_pad, out, out_cstride,
+                                   out_coff, B, H, W, tiles, lin_rows1, 1, nullptr, nullptr);
+                VS_HIP(hipGetLastError());
+                return VS_OK;
+            }
+            const int tiles = tiles256;
+            dim3 grid((unsigned)(B * tiles * ntn));
             if (ck == 4)
                 hipLaunchKernelGGL((k_conv3_db<false, LAYER, false, true, 4>), grid, dim3(256), 0, s, in, in_cstride,
                                    in_coff, L.w, L.b, L.cin, L.cout, L.cout_pad, out, out_cstride, out_coff, B, H, W,

@@ -30,10 +30,15 @@ constexpr int kTlmMaxKp = 1024;
 // workgroup: a keypoint's slot is its cell's prefix count plus the number of earlier keypoints in
 // the same cell (the order the reference's push_back produces).
 constexpr int kTlmMaxCells = 4096;
+// Also: the kp -> map-point table from pinned host memory when given (src), and -1 in the item
+// slots past the grid's last (nit .. nkp), so the call needs no upload or memset of its own.
 __global__ __launch_bounds__(1024) void k_tlm_grid(const vs_keypoint* __restrict__ kps, int nkp, int GW, int GH,
                                                    int* __restrict__ start, int* __restrict__ items,
-                                                   int* __restrict__ work_n) {
+                                                   int* __restrict__ work_n, const int* __restrict__ src,
+                                                   int* __restrict__ kp_to_mp) {
     if (threadIdx.x == 0) *work_n = 0;  // the candidate work list of this call (k_tlm_cand appends)
+    if (src)
+        for (int i = threadIdx.x; i < nkp; i += blockDim.x) kp_to_mp[i] = src[i];
     __shared__ int s_cell[kTlmMaxKp];
     __shared__ int s_start[kTlmMaxCells + 1];
     const int tid = threadIdx.x, nc = GW * GH;
@@ -83,6 +88,7 @@ __global__ __launch_bounds__(1024) void k_tlm_grid(const vs_keypoint* __restrict
         items[s_start[c] + rank] = ki;
     }
     for (int c = tid; c <= nc; c += blockDim.x) start[c] = s_start[c];
+    for (int i = s_start[nc] + tid; i <= nkp; i += blockDim.x) items[i] = -1;
 }
 
 __device__ double desc_l2_dev(const float* __restrict__ a, const float* __restrict__ b) {
@@ -447,7 +453,7 @@ __global__ __launch_bounds__(1024) void k_tlm_resolve(const int* __restrict__ be
 int track_local_map(vs_ctx* ctx, const double* d_mp_pos, const float* d_mp_desc, const uint8_t* d_mp_valid, int n_mp,
                     const vs_keypoint* d_kps, const float* d_desc, int nkp, const double R[9], const double t[3],
                     const double K[4], int img_w, int img_h, int* d_kp_to_mp, int* d_obs_mp, int* d_obs_kp,
-                    int obs_cap, int* d_result, hipStream_t s) {
+                    int obs_cap, int* d_result, hipStream_t s, const int* h_kp_to_mp_src) {
     VS_ARG(nkp >= 0 && nkp <= kTlmMaxKp, "track_local_map: at most 1024 keypoints");
     VS_ARG(img_w > 0 && img_h > 0, "track_local_map: bad image size");
     VS_ARG(((img_w + kTlmCell - 1) / kTlmCell) * ((img_h + kTlmCell - 1) / kTlmCell) <= kTlmMaxCells,
@@ -479,10 +485,11 @@ int track_local_map(vs_ctx* ctx, const double* d_mp_pos, const float* d_mp_desc,
     T.cx = K[2];
     T.cy = K[3];
     ProfScope ps(ctx, "track_local_map", s);
-    VS_HIP(hipMemsetAsync(items, 0xff, (size_t)(nkp + 1) * sizeof(int), s));
     if (nkp > 0) {
-        hipLaunchKernelGGL(k_tlm_grid, dim3(1), dim3(1024), 0, s, d_kps, nkp, GW, GH, start, items, work_n);
+        hipLaunchKernelGGL(k_tlm_grid, dim3(1), dim3(1024), 0, s, d_kps, nkp, GW, GH, start, items, work_n,
+                           h_kp_to_mp_src, d_kp_to_mp);
     } else {
+        VS_HIP(hipMemsetAsync(items, 0xff, sizeof(int), s));
         VS_HIP(hipMemsetAsync(start, 0, (size_t)(GW * GH + 1) * sizeof(int), s));
         VS_HIP(hipMemsetAsync(work_n, 0, sizeof(int), s));
     }

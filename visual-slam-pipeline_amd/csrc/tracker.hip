@@ -228,11 +228,12 @@ __global__ __launch_bounds__(1024) void k_pnp_gather(const int* __restrict__ kpm
 
 // Host-side wall time per back-end operation (VS_SLAM_HOST_PROFILE=1: printed to stderr when the
 // vs_slam is destroyed); the rest of process_frame is the tracker's own host logic.
-enum HostOp { kHChain, kHMatch, kHFmat, kHMotion, kHTlm, kHPnp, kHMatchMap, kHAppend, kHVis, kHFrame, kHWait, kHSpec, kHLoop, kHOps };
+enum HostOp { kHChain, kHMatch, kHFmat, kHMotion, kHTlm, kHPnp, kHMatchMap, kHAppend, kHVis, kHFrame, kHWait, kHSpec, kHLoop,
+              kHTlmSync, kHOps };
 static const char* const kHostOpNames[kHOps] = {"chain", "match", "find_fundamental", "motion_points",
                                                 "track_local_map", "solve_pnp", "match_map", "map_append",
                                                 "visibility", "process_frame (total)", "extract wait",
-                                                "chain: speculation wait", "loop_eval"};
+                                                "chain: speculation wait", "loop_eval", "track_local_map: sync"};
 struct HostProf {
     bool on = false;
     long skip = 64;  // frames before counting starts (first launches load code objects)
@@ -428,6 +429,13 @@ struct GpuOps {
                 (cu < tcu ? tm : cu < tcu + scu ? sm : cu < tcu + scu + pcu ? pm : xm)[cu / 32] |= 1u << (cu % 32);
             if (scu == 0) sm = tm;
             if (pcu == 0) pm = xm;
+            // VS_SLAM_POST_SET = track / all: the post-processing stream on the tracking CUs, or on
+            // every CU (experiments: the tracking CUs idle between latency-bound kernels)
+            if (const char* ps = std::getenv("VS_SLAM_POST_SET")) {
+                if (std::strcmp(ps, "track") == 0) pm = tm;
+                if (std::strcmp(ps, "all") == 0)
+                    for (int k = 0; k < words; k++) pm[k] = tm[k] | xm[k] | sm[k];
+            }
             masked = hipExtStreamCreateWithCUMask(&s, words, tm.data()) == hipSuccess;
             if (masked && hipExtStreamCreateWithCUMask(&xs, words, xm.data()) != hipSuccess) {
                 (void)hipStreamDestroy(s);
@@ -1020,12 +1028,14 @@ struct GpuOps {
             int* d = work.as<int>();
             int* d_kpmp = d + 2;
             int* d_obs = d + 2 + nkp;
-            if (failed(upload(d_kpmp, f.mp_idx.data(), (size_t)nkp * sizeof(int)))) return 0;
-            if (failed(::vs_track_local_map_dev(ctx, map_pos.as<double>(), map_desc.as<float>(),
-                                                map_valid.as<uint8_t>(), m.size(), kps_of(f.slot), desc_of(f.slot), nkp,
-                                                f.R.data(), f.t.data(), K, vs_trk::cfg::IMAGE_WIDTH,
-                                                vs_trk::cfg::IMAGE_HEIGHT, d_kpmp, d_obs, d_obs + obs_cap, obs_cap, d,
-                                                s)))
+            // the kp -> map-point table goes in through pinned memory that k_tlm_grid reads itself
+            int* h_kpmp = reinterpret_cast<int*>(take((size_t)std::max(nkp, 1) * sizeof(int)));
+            if (!h_kpmp) return 0;
+            std::memcpy(h_kpmp, f.mp_idx.data(), (size_t)nkp * sizeof(int));
+            if (failed(vs::track_local_map(ctx, map_pos.as<double>(), map_desc.as<float>(), map_valid.as<uint8_t>(),
+                                           m.size(), kps_of(f.slot), desc_of(f.slot), nkp, f.R.data(), f.t.data(), K,
+                                           vs_trk::cfg::IMAGE_WIDTH, vs_trk::cfg::IMAGE_HEIGHT, d_kpmp, d_obs,
+                                           d_obs + obs_cap, obs_cap, d, s, h_kpmp)))
                 return 0;
             // Speculatively, the refinement's PnP on the tracked points right behind it (the
             // tracker calls solve_pnp on exactly these next, Slam.cpp:1057-1059; solve_pnp checks).
@@ -1047,7 +1057,10 @@ struct GpuOps {
             int* hb = reinterpret_cast<int*>(hall);
             char* hs = spec_run ? hall + wbytes : nullptr;
             flush_spec();  // the next frame's chain, launched while these kernels run
-            if (failed(sync())) return 0;
+            {
+                HostTimer hs(hprof, kHTlmSync);
+                if (failed(sync())) return 0;
+            }
             if (hs) {
                 const int n = reinterpret_cast<const int*>(hs)[1];
                 const float* so = reinterpret_cast<const float*>(hs + 16);
@@ -1491,8 +1504,14 @@ void vs_slam_destroy(vs_slam* sl) {
             if (o.hprof.n[k])
                 std::fprintf(stderr, "vs_slam host %-22s %8ld calls %10.3f ms  %8.1f us/call\n", kHostOpNames[k],
                              o.hprof.n[k], o.hprof.ms[k], 1e3 * o.hprof.ms[k] / o.hprof.n[k]);
-    if (o.hprof.on)
+    if (o.hprof.on) {
         std::fprintf(stderr, "vs_slam speculative chains: %ld launched, %ld used\n", o.cspec_launched, o.cspec_hits);
+        const vs_trk::PhaseProf& ph = sl->trk->phase_prof();
+        for (int k = 0; k < vs_trk::PH_N; k++)
+            if (ph.n[k])
+                std::fprintf(stderr, "vs_slam phase %-27s %8ld calls %10.3f ms  %8.1f us/call\n", vs_trk::phase_name(k),
+                             ph.n[k], ph.ms[k], 1e3 * ph.ms[k] / ph.n[k]);
+    }
     o.destroy_streams();
     DevBuf* bufs[] = {&o.pool_kps, &o.pool_desc, &o.pool_n, &o.pool_depth, &o.pool_norms, &o.semi, &o.dgrid,
                       &o.chain_buf,    &o.work, &o.rows_buf,      &o.map_pos, &o.map_desc,  &o.map_valid, &o.map_tmp,
@@ -1557,7 +1576,7 @@ int vs_slam_process_batch_dev(vs_slam* sl, int B, const uint8_t* d_bgr, const fl
         // the next frame and its chunk's event, for the speculative chain (chain())
         o.next_frame = b + 1 < B ? sl->batch[b + 1].get() : nullptr;
         o.next_ready = b + 1 < B ? X.ev[b + 1 == X.ch[c] ? c : c - 1] : nullptr;
-        if (o.hprof_armed && --o.hprof.skip < 0) o.hprof.on = true, o.hprof_armed = false;
+        if (o.hprof_armed && --o.hprof.skip < 0) o.hprof.on = sl->trk->phase_prof().on = true, o.hprof_armed = false;
         {
             HostTimer ht(o.hprof, kHFrame);
             processed[b] = sl->trk->process_frame(sl->batch[b]) ? 1 : 0;

@@ -152,11 +152,13 @@ int ransac3d_pairs(vs_ctx* ctx, int P, const int* d_pairs, const vs_keypoint* d_
                    const double K[4], const uint32_t* d_seeds, int iters, double thr,
                    double* d_R, double* d_t, int* d_ok, int* d_diag, hipStream_t s,
                    const uint32_t* d_mt_init = nullptr);  // [P][624] init_genrand states (optional)
-// Local-map tracking (d_result = {tracked, observations})
+// Local-map tracking (d_result = {tracked, observations}).  h_kp_to_mp_src (optional): device-
+// readable pinned host memory with the initial kp -> map-point table, copied into d_kp_to_mp by the
+// first kernel (no separate upload); null = d_kp_to_mp already holds it.
 int track_local_map(vs_ctx* ctx, const double* d_mp_pos, const float* d_mp_desc, const uint8_t* d_mp_valid, int n_mp,
                     const vs_keypoint* d_kps, const float* d_desc, int nkp, const double R[9], const double t[3],
                     const double K[4], int img_w, int img_h, int* d_kp_to_mp, int* d_obs_mp, int* d_obs_kp,
-                    int obs_cap, int* d_result, hipStream_t s);
+                    int obs_cap, int* d_result, hipStream_t s, const int* h_kp_to_mp_src = nullptr);
 // Pose LM, nprob problems with point ranges d_off[p]..d_off[p+1]
 int optimize_pose(vs_ctx* ctx, int nprob, const double* d_P, const float* d_p2, const int* d_off, const double K[4],
                   double* d_R, double* d_t, double* d_res, int* d_ok, hipStream_t s);

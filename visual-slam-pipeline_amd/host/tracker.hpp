@@ -27,6 +27,7 @@
 
 #include <algorithm>
 #include <array>
+#include <chrono>
 #include <cmath>
 #include <cstdint>
 #include <cstdio>
@@ -202,6 +203,37 @@ struct Stats {
         triangulated = 0, depth_points = 0, culled = 0, chains_discarded = 0, f_iters = 0;
 };
 
+// Optional host wall time per phase of process_frame (a profiling aid: off unless a back end
+// turns it on; the phases include their back-end calls).
+enum Phase { PH_CHAIN, PH_RECOVERY, PH_MOTION_EKF, PH_TLM, PH_REFINE, PH_KEYFRAME, PH_N };
+inline const char* phase_name(int k) {
+    static const char* const n[PH_N] = {"chain + bridge", "recovery check", "stationary + motion + EKF",
+                                        "local-map tracking", "PnP refinement", "keyframe work"};
+    return n[k];
+}
+struct PhaseProf {
+    bool on = false;
+    double ms[PH_N] = {};
+    long n[PH_N] = {};
+};
+struct PhaseScope {
+    PhaseProf& p;
+    int k;
+    std::chrono::steady_clock::time_point t0;
+    PhaseScope(PhaseProf& pp, int kk) : p(pp), k(kk) {
+        if (p.on) t0 = std::chrono::steady_clock::now();
+    }
+    void end() {
+        if (k < 0) return;
+        if (p.on) {
+            p.ms[k] += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+            p.n[k]++;
+        }
+        k = -1;
+    }
+    ~PhaseScope() { end(); }
+};
+
 // ---- the tracker -----------------------------------------------------------------------------
 template <class Ops>
 class Tracker {
@@ -216,6 +248,7 @@ class Tracker {
     // Debugging aid: one line per stage result (hex floats) so that two back ends' runs can be
     // diffed to the first differing stage (tools/debug_tracker_divergence.py --trace).
     void set_trace(FILE* f) { trace_ = f; }
+    PhaseProf& phase_prof() { return phase_; }
 
     // Slam::compute_gravity_direction (Slam.cpp:1587-1616)
     void compute_gravity_direction() {
@@ -267,6 +300,7 @@ class Tracker {
         // match list is what :841 computes, and the F / 3D-3D / E results are only used when the
         // control flow reaches :880 with these matches
         ref_frame_ = (last_keyframe_ && last_keyframe_->has_desc()) ? last_keyframe_ : last_frame_;
+        PhaseScope ph_chain(phase_, PH_CHAIN);
         ChainResult C = ops_.chain(*ref_frame_, *frame, 42u + (uint32_t)frame_count_);
         stats_.f_iters += C.f_iters;
         last_match_count_ = (int)C.good.size();
@@ -294,8 +328,11 @@ class Tracker {
             }
         }
 
+        ph_chain.end();
         // :875-877 PnP recovery when tracking is lost
+        PhaseScope ph_rec(phase_, PH_RECOVERY);
         const int pnp_result = try_pnp_recovery(frame);
+        ph_rec.end();
         if (pnp_result == 1) return true;
         if (pnp_result == -1) {
             stats_.recovery_failed++;
@@ -309,6 +346,7 @@ class Tracker {
         }
         std::vector<Match> good = C.kept;
 
+        PhaseScope ph_mot(phase_, PH_MOTION_EKF);
         if (process_stationary_frame(frame, good)) return true;  // :913
 
         bool recompute_motion = false;
@@ -422,13 +460,19 @@ class Tracker {
         map_.frames.push_back(frame);
         trace_pose(frame->id, "motion+ekf", R_world_, t_world_);
 
+        ph_mot.end();
         // :1057-1059 local map tracking + PnP refinement
+        PhaseScope ph_tlm(phase_, PH_TLM);
         const int tracked = track_local_map(frame);
+        ph_tlm.end();
         if (trace_)
             std::fprintf(trace_, "%d tlm %d %016llx\n", frame->id, tracked,
                          (unsigned long long)fnv(frame->mp_idx.data(), frame->mp_idx.size() * sizeof(int)));
+        PhaseScope ph_ref(phase_, PH_REFINE);
         refine_pose_via_local_pnp(frame, tracked);
+        ph_ref.end();
         trace_pose(frame->id, "refined", R_world_, t_world_);
+        PhaseScope ph_kf(phase_, PH_KEYFRAME);
 
         // :1061-1070 proactive keyframe.  Deviation: the reference dereferences last_keyframe_
         // unconditionally here, which is null when the first frame was rejected (:820-823 keeps it
@@ -599,6 +643,7 @@ class Tracker {
 
    private:
     FILE* trace_ = nullptr;
+    PhaseProf phase_;
     static uint64_t fnv(const void* p, size_t n) {
         uint64_t h = 1469598103934665603ull;
         for (size_t i = 0; i < n; i++) h = (h ^ static_cast<const uint8_t*>(p)[i]) * 1099511628211ull;
