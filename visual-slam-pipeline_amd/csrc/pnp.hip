@@ -57,7 +57,18 @@ struct PnpHyp {
     int* count;
     double* model;
     int stride;  // hypotheses per problem
+    int tab_n0;  // >= 0: subset is the context's table by point count (row n - tab_n0); -1: per problem
 };
+
+// Subsets depend on (n, iteration budget) only, so the usual budget's are drawn once per context
+// for every n in [kPnpTabMinN, kPnpTabMaxN] (2 MB) and k_pnp_hyp indexes that table by n: no
+// subset launch on the tracker's per-frame path.
+constexpr int kPnpTabIters = 100, kPnpTabMinN = 6, kPnpTabMaxN = 1024;
+
+__device__ __forceinline__ const int* pnp_subset(const PnpHyp& H, int pb, int n, int h) {
+    return H.tab_n0 >= 0 ? H.subset + ((size_t)(n - H.tab_n0) * H.stride + h) * 5
+                         : H.subset + ((size_t)pb * H.stride + h) * 5;
+}
 
 __device__ __attribute__((noinline)) bool epnp_subset(const float* obj, const float* img, const int* idx, int m, const Cam& K, double* rv,
                                    double* tv) {
@@ -102,15 +113,16 @@ constexpr PnpMwcPow make_pnp_mwc_pow() {
 }
 __constant__ PnpMwcPow g_pnp_mwc_pow = make_pnp_mwc_pow();
 
-__global__ __launch_bounds__(256) void k_pnp_subsets(const int* __restrict__ off, int niters0, int min_inliers,
-                                                     PnpHyp H) {
+// n_base >= 0: problem pb has n = n_base + pb points (the table build; off unused, rows pb).
+__global__ __launch_bounds__(256) void k_pnp_subsets(const int* __restrict__ off, int n_base, int niters0,
+                                                     int min_inliers, PnpHyp H) {
     __shared__ int s_draw[kPnpRaw];
     __shared__ uint16_t s_J[kPnpLevels][kPnpRaw + 2];
     __shared__ int s_start[256];
     __shared__ int s_navail;
     __shared__ uint64_t s_rng;
     const int pb = blockIdx.x, tid = threadIdx.x;
-    const int n = off[pb + 1] - off[pb];
+    const int n = n_base >= 0 ? n_base + pb : off[pb + 1] - off[pb];
     const int model_points = n == 4 ? 4 : 5;
     if (!pnp_problem_runs(n, min_inliers, model_points)) return;  // running problems have n > 5
     float per = 0.f;
@@ -214,6 +226,7 @@ __global__ __launch_bounds__(256) void k_pnp_subsets(const int* __restrict__ off
 __global__ __launch_bounds__(64) void k_pnp_hyp(const float* __restrict__ obj_all, const float* __restrict__ img_all,
                                                 const int* __restrict__ off, double fx, double fy, double cx, double cy,
                                                 int niters0, float thr2, int min_inliers, PnpHyp H) {
+    crit_prio();
     __shared__ double sA[144], sV[144];
     __shared__ double sX[15], sUV[10], sAl[5][4], sCw[4][3];
     __shared__ double sTot, sOff, sErr[3], sRt[3][12];
@@ -225,7 +238,7 @@ __global__ __launch_bounds__(64) void k_pnp_hyp(const float* __restrict__ obj_al
     const float* obj = obj_all + 3 * (size_t)o0;
     const float* img = img_all + 2 * (size_t)o0;
     const Cam K{fx, fy, cx, cy};
-    const int* idx = H.subset + ((size_t)pb * H.stride + h) * 5;
+    const int* idx = pnp_subset(H, pb, n, h);
     const int m = model_points;
     PNP_T0();
     if (lane < m) {
@@ -467,6 +480,7 @@ __global__ __launch_bounds__(256) void k_pnp_ransac(const float* __restrict__ ob
                                                     int min_inliers, PnpHyp H, double* __restrict__ Rw,
                                                     double* __restrict__ tw, int* __restrict__ stat,
                                                     uint8_t* __restrict__ mask_all) {
+    crit_prio();
     __shared__ PnpShared S;
     __shared__ double s_lden[kPnpMaxIters];
     const int pb = blockIdx.x, tid = threadIdx.x;
@@ -602,9 +616,33 @@ __global__ __launch_bounds__(256) void k_pnp_ransac(const float* __restrict__ ob
     }
 }
 
+// The context's subset table for kPnpTabIters (built on first use; the build is synchronised
+// once so that any stream may read the table afterwards).
+static int pnp_table(vs_ctx* ctx, hipStream_t s, int** tab) {
+    constexpr int rows = kPnpTabMaxN - kPnpTabMinN + 1;
+    if (!ctx->pnp_tab_ready) {
+        VS_CHECK(ctx->pnp_tab.ensure((size_t)rows * kPnpTabIters * 5 * sizeof(int)));
+        PnpHyp T{};
+        T.subset = ctx->pnp_tab.as<int>();
+        T.stride = kPnpTabIters;
+        T.tab_n0 = -1;
+        hipLaunchKernelGGL(k_pnp_subsets, dim3(rows), dim3(256), 0, s, nullptr, kPnpTabMinN, kPnpTabIters, 0, T);
+        VS_HIP(hipGetLastError());
+        VS_HIP(hipStreamSynchronize(s));
+        ctx->pnp_tab_ready = true;
+    }
+    *tab = ctx->pnp_tab.as<int>();
+    return VS_OK;
+}
+
+int pnp_reserve(vs_ctx* ctx, hipStream_t s) {
+    int* tab;
+    return pnp_table(ctx, s, &tab);
+}
+
 int solve_pnp(vs_ctx* ctx, int nprob, const float* d_obj, const float* d_img, const int* d_off, const double K[4],
               int ransac_iters, int min_inliers, double* d_R, double* d_t, int* d_stat, uint8_t* d_mask,
-              hipStream_t s) {
+              hipStream_t s, int max_n) {
     if (nprob <= 0) return VS_OK;
     VS_ARG(ransac_iters <= kPnpMaxIters, "solve_pnp: ransac_iters above kPnpMaxIters");
     ProfScope ps(ctx, "solve_pnp", s);
@@ -618,7 +656,13 @@ int solve_pnp(vs_ctx* ctx, int nprob, const float* d_obj, const float* d_img, co
     H.subset = reinterpret_cast<int*>(H.model + per * 6);
     H.count = H.subset + per * 5;
     H.stride = niters0;
-    hipLaunchKernelGGL(k_pnp_subsets, dim3(nprob), dim3(256), 0, s, d_off, niters0, min_inliers, H);
+    H.tab_n0 = -1;
+    if (niters0 == kPnpTabIters && max_n >= 0 && max_n <= kPnpTabMaxN) {
+        VS_CHECK(pnp_table(ctx, s, &H.subset));
+        H.tab_n0 = kPnpTabMinN;
+    } else {
+        hipLaunchKernelGGL(k_pnp_subsets, dim3(nprob), dim3(256), 0, s, d_off, -1, niters0, min_inliers, H);
+    }
     hipLaunchKernelGGL(k_pnp_hyp, dim3(nprob, niters0), dim3(64), 0, s, d_obj, d_img, d_off, K[0], K[1], K[2], K[3],
                        niters0, thr2, min_inliers, H);
     hipLaunchKernelGGL(k_pnp_ransac, dim3(nprob), dim3(256), 0, s, d_obj, d_img, d_off, K[0], K[1], K[2], K[3],

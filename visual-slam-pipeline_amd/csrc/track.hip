@@ -36,6 +36,7 @@ __global__ __launch_bounds__(1024) void k_tlm_grid(const vs_keypoint* __restrict
                                                    int* __restrict__ start, int* __restrict__ items,
                                                    int* __restrict__ work_n, const int* __restrict__ src,
                                                    int* __restrict__ kp_to_mp) {
+    crit_prio();
     if (threadIdx.x == 0) *work_n = 0;  // the candidate work list of this call (k_tlm_cand appends)
     if (src)
         for (int i = threadIdx.x; i < nkp; i += blockDim.x) kp_to_mp[i] = src[i];
@@ -121,6 +122,7 @@ __global__ __launch_bounds__(256) void k_tlm_cand(const double* __restrict__ mp_
                                                   int GH, int img_w, int img_h, TlmPose T, int* __restrict__ cnt,
                                                   int* __restrict__ cand, int* __restrict__ work,
                                                   int* __restrict__ work_n) {
+    crit_prio();
     // the keypoint grid and the keypoint coordinates in LDS (one coalesced pass; every lookup of
     // the candidate scan then stays on chip)
     __shared__ int s_start[kTlmMaxCells + 1];
@@ -210,6 +212,7 @@ __global__ __launch_bounds__(256) void k_tlm_cand(const double* __restrict__ mp_
 __global__ __launch_bounds__(256) void k_tlm_dist(const float* __restrict__ mp_desc, const float* __restrict__ desc,
                                                   const int* __restrict__ cand, const int* __restrict__ work,
                                                   const int* __restrict__ work_n, double* __restrict__ dist) {
+    crit_prio();
     const int n = *work_n;
     for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
         const int r = work[i];
@@ -231,6 +234,7 @@ __global__ __launch_bounds__(256) void k_tlm_best(const int* __restrict__ cnt, c
                                                   const double* __restrict__ dist, int n_mp, int* __restrict__ best_ki,
                                                   double* __restrict__ best_d, int* __restrict__ rank,
                                                   int* __restrict__ blkcnt) {
+    crit_prio();
     __shared__ int s_w[4];
     const int mp = blockIdx.x * 256 + threadIdx.x, wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
     int ki0 = -1;
@@ -363,6 +367,7 @@ __global__ __launch_bounds__(1024) void k_tlm_resolve(const int* __restrict__ be
                                                       int n_mp, int nkp, int* __restrict__ kp_to_mp,
                                                       int* __restrict__ obs_mp, int* __restrict__ obs_kp, int obs_cap,
                                                       int* __restrict__ result) {
+    crit_prio();
     __shared__ TlmResolveShared S;
     const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
     const int nblk = (n_mp + 255) / 256;

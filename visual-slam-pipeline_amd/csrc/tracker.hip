@@ -196,6 +196,7 @@ constexpr int kXFirst = 8;
 __global__ __launch_bounds__(1024) void k_pnp_gather(const int* __restrict__ kpmp, int nkp, const double* __restrict__ pos,
                                                      const uint8_t* __restrict__ valid, int n_mp,
                                                      const vs_keypoint* __restrict__ kps, int cap, float* __restrict__ io) {
+    crit_prio();
     __shared__ int s_w[16];
     const int i = threadIdx.x, wv = i >> 6, lane = i & 63;
     const int id = i < nkp ? kpmp[i] : -1;
@@ -265,6 +266,7 @@ struct AsyncEnqueue {
     bool has_task = false, busy = false, quit = false;
     int rc = VS_OK;
     std::string err;
+    const char* what = "next-batch extraction";
     void start(int device) {
         th = std::thread([this, device] {
             (void)hipSetDevice(device);
@@ -305,7 +307,7 @@ struct AsyncEnqueue {
         cv.wait(lk, [&] { return !has_task && !busy; });
         const int r = rc;
         rc = VS_OK;
-        if (r != VS_OK) set_error("vs_slam: next-batch extraction: " + err);
+        if (r != VS_OK) set_error(std::string("vs_slam: ") + what + ": " + err);
         return r;
     }
     void stop() {
@@ -324,6 +326,11 @@ struct GpuOps {
     vs_ctx* ctx = nullptr;
     AsyncEnqueue aq;
     bool async_enqueue = true;  // VS_SLAM_ASYNC_ENQUEUE=0: enqueue the next batch on the caller's thread
+    // A second helper launches the next frame's speculative chain (≈ 40 us of HIP calls) as soon as
+    // chain() has decided it, beside this thread's local-map tracking launches
+    // (VS_SLAM_SPEC_ASYNC=0: launched on this thread once the tracking kernels are enqueued).
+    AsyncEnqueue sq;
+    bool spec_async = true, spec_inflight = false;
     HostProf hprof;
     bool hprof_armed = false;
     // speculative PnP of the tracked points, run right behind local-map tracking (see solve_pnp)
@@ -475,6 +482,7 @@ struct GpuOps {
     }
     void destroy_streams() {
         aq.stop();  // no enqueue may still be running when the streams go
+        sq.stop();
         if (!own_streams) return;
         (void)hipStreamSynchronize(xs);
         (void)hipStreamSynchronize(xp);
@@ -505,6 +513,9 @@ struct GpuOps {
         VS_CHECK(make_streams());
         if (const char* e = std::getenv("VS_SLAM_ASYNC_ENQUEUE")) async_enqueue = e[0] != '0';
         if (async_enqueue) aq.start(ctx->device);
+        if (const char* e = std::getenv("VS_SLAM_SPEC_ASYNC")) spec_async = e[0] != '0';
+        sq.what = "speculative chain launch";
+        if (spec_async) sq.start(ctx->device);
         if (const char* fc = std::getenv("VS_SLAM_CHUNK")) chunk = std::max(1, std::min(kXChunk, std::atoi(fc)));
         const char* hp = std::getenv("VS_SLAM_HOST_PROFILE");
         hprof.on = hp && hp[0] == '1';
@@ -548,6 +559,7 @@ struct GpuOps {
         // map points, PnP hypothesis tables for the largest RANSAC budget (loop closure: 300)
         VS_CHECK(ctx->tlm.ensure((size_t)64 << 20));
         VS_CHECK(ctx->pnp.ensure((size_t)4 * VS_PNP_MAX_ITERS * (6 * sizeof(int) + 6 * sizeof(double))));
+        VS_CHECK(pnp_reserve(ctx, s));  // the PnP subset table (built once here, not in the loop)
         // Loop closure (every 200 keyframes, candidates every 5th keyframe >= 200 ids back,
         // LoopCloser.cpp:44-49): the keyframe archive for kArchInit keyframes (215 MB of HBM), the
         // candidate pool and the matcher key state for kLoopPairs candidates, reserved here because
@@ -883,9 +895,20 @@ struct GpuOps {
         cspec_launched++;
         return VS_OK;
     }
+    // Waits until the helper has enqueued the speculation it was given (cspec and cspec_ev are then
+    // this thread's again); its error, if any, is latched.
+    void spec_sync() {
+        if (!spec_inflight) return;
+        spec_inflight = false;
+        failed(sq.join());
+    }
     vs_trk::ChainResult chain(const vs_trk::Frame& ref, const vs_trk::Frame& cur, uint32_t seed) {
         HostTimer ht(hprof, kHChain);
         vs_trk::ChainResult R;
+        {
+            HostTimer hw(hprof, kHSpec);
+            spec_sync();
+        }
         const bool hit = cspec.valid && cspec.cur == &cur && cspec.ref_slot == ref.slot && cspec.cur_slot == cur.slot &&
                          cspec.seed == seed;
         cspec.valid = false;
@@ -913,6 +936,14 @@ struct GpuOps {
             spec_req.nxt_slot = next_frame->slot;
             spec_req.seed = seed + 1u;
             spec_req.ready = next_ready;
+            if (spec_async) {  // launched now by the helper, beside this frame's tracking launches
+                const SpecReq q = spec_req;
+                spec_req.pending = false;
+                if (q.nxt->slot == q.nxt_slot) {
+                    spec_inflight = true;
+                    sq.submit([this, q] { return launch_spec_chain(q.ref_slot, *q.nxt, q.seed, q.ready); });
+                }
+            }
         }
         return R;
     }
@@ -1049,7 +1080,7 @@ struct GpuOps {
                 spec_run = vs::solve_pnp(ctx, 1, reinterpret_cast<const float*>(io + 16),
                                          reinterpret_cast<const float*>(io + 16 + (size_t)cap * 3 * sizeof(float)),
                                          reinterpret_cast<const int*>(io), K, 100, 10, dRt, dRt + 9, dstat,
-                                         reinterpret_cast<uint8_t*>(dstat + 8), s) == VS_OK;
+                                         reinterpret_cast<uint8_t*>(dstat + 8), s, cap) == VS_OK;
             }
             const size_t rb = wbytes + (spec_run ? spec_bytes : 0);
             char* hall = take(rb);
@@ -1126,7 +1157,7 @@ struct GpuOps {
         if (failed(vs::solve_pnp(ctx, 1, reinterpret_cast<const float*>(d + 16),
                                  reinterpret_cast<const float*>(d + 16 + (size_t)n * 3 * sizeof(float)),
                                  reinterpret_cast<const int*>(d), K, iters, min_inliers, dRt, dRt + 9, dstat,
-                                 reinterpret_cast<uint8_t*>(dstat + 8), s)))
+                                 reinterpret_cast<uint8_t*>(dstat + 8), s, n)))
             return r;
         char* ho = take(out_bytes);
         if (!ho || failed(d2h(ho, dRt, out_bytes)) || failed(sync())) return r;
@@ -1423,6 +1454,12 @@ void dense_record(vs_slam* sl, const vs_trk::Frame& f) {
 int settle(vs_slam* sl) {
     GpuOps& o = sl->ops;
     auto& T = *sl->trk;
+    o.spec_sync();
+    if (o.err != VS_OK) {
+        const int r = o.err;
+        o.err = VS_OK;
+        return r;
+    }
     VS_HIP(hipStreamWaitEvent(o.s, o.cspec_ev, 0));  // a discarded speculation still reads the pool
     for (const auto& f : T.map().frames)  // new keyframes' features into the archive (loop closure)
         if (f->keyframe && f->kf_slot < 0 && f->slot >= 0) VS_CHECK(o.archive(f.get()));
@@ -1590,6 +1627,9 @@ int vs_slam_process_batch_dev(vs_slam* sl, int B, const uint8_t* d_bgr, const fl
     }
     o.next_frame = nullptr;
     o.next_ready = nullptr;
+    o.spec_sync();
+    if (rc == VS_OK && o.err != VS_OK) rc = o.err;
+    o.err = VS_OK;
     o.cspec.valid = false;
     o.spec_req.pending = false;
     // The helper's next-batch enqueue has finished before the call returns, so no thread of this

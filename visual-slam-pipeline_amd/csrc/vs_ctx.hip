@@ -324,7 +324,7 @@ void vs_destroy(vs_ctx* ctx) {
                       &ctx->state, &ctx->flags,  &ctx->keys,   &ctx->keycnt, &ctx->h_img,  &ctx->h_kps,
                       &ctx->h_desc, &ctx->h_n,   &ctx->h_aux0, &ctx->h_aux1, &ctx->h_aux2, &ctx->h_aux3,
                       &ctx->h_aux4, &ctx->h_aux5, &ctx->match_keys, &ctx->match_cnt, &ctx->nms_list, &ctx->norms_sets, &ctx->tlm, &ctx->ba, &ctx->pnp,
-                      &ctx->tie_totals};
+                      &ctx->pnp_tab, &ctx->tie_totals};
     for (DevBuf* b : bufs) b->release();
     for (auto& st : ctx->prof)
         for (auto& pr : st.pending) {
@@ -707,7 +707,7 @@ int vs_solve_pnp(vs_ctx* ctx, const float* obj_pts, const float* img_pts, int n,
     const int off[2] = {0, n};
     VS_HIP(hipMemcpyAsync(dmeta, off, sizeof(off), hipMemcpyHostToDevice, s));
     VS_CHECK(solve_pnp(ctx, 1, ctx->h_aux0.as<float>(), ctx->h_aux1.as<float>(), dmeta, K, ransac_iters, min_inliers,
-                       dRt, dRt + 9, dmeta + 2, dmask, s));
+                       dRt, dRt + 9, dmeta + 2, dmask, s, n));
     double Rt[12];
     int stat[8];
     VS_HIP(hipMemcpyAsync(Rt, dRt, sizeof(Rt), hipMemcpyDeviceToHost, s));

@@ -20,6 +20,17 @@ __device__ __forceinline__ float sqrt_rn(float x) { return (float)sqrt((double)x
 // __fdiv_rn lowers to the v_div_scale / v_div_fmas / v_div_fixup correctly rounded sequence.
 __device__ __forceinline__ float div_rn(float a, float b) { return __fdiv_rn(a, b); }
 
+// ---- issue priority of the tracker's critical path ---------------------------------------
+// The local-map tracking and PnP kernels of frame k share the tracking CUs with frame k + 1's
+// speculative front chain (match, F-RANSAC, 3D-3D RANSAC: 1024-wave grids), which is not on the
+// critical path.  Their waves raise their SIMD issue priority so the latency-bound chains of
+// frame k issue first and the chain's waves fill the gaps.  (-DVS_NO_CRIT_PRIO: A/B builds.)
+__device__ __forceinline__ void crit_prio() {
+#ifndef VS_NO_CRIT_PRIO
+    __builtin_amdgcn_s_setprio(3);
+#endif
+}
+
 // ---- errors ------------------------------------------------------------------------------
 void set_error(const std::string& msg);
 #define VS_HIP(call)                                                                  \
@@ -94,6 +105,8 @@ struct vs_ctx {
     // host-API staging
     vs::DevBuf h_img, h_kps, h_desc, h_n, h_aux0, h_aux1, h_aux2, h_aux3, h_aux4, h_aux5;
     vs::DevBuf match_keys, match_cnt, norms_sets, tlm, ba, pnp;
+    vs::DevBuf pnp_tab;  // PnP RANSAC subsets of the usual budget by point count (pnp.hip)
+    bool pnp_tab_ready = false;
     vs::DevBuf tie_totals;  // NMS tie accounting since the last reset: {frames, frames with a tie, window, cut, order}
 
     bool prof_on = false;
@@ -163,9 +176,13 @@ int track_local_map(vs_ctx* ctx, const double* d_mp_pos, const float* d_mp_desc,
 int optimize_pose(vs_ctx* ctx, int nprob, const double* d_P, const float* d_p2, const int* d_off, const double K[4],
                   double* d_R, double* d_t, double* d_res, int* d_ok, hipStream_t s);
 // PnP RANSAC + LM, nprob problems with point ranges d_off[p]..d_off[p+1]
+// max_n: an upper bound of every problem's point count when the caller knows one (-1: unknown); with
+// the usual budget (100) and max_n <= 1024 the subsets come from the context's table.
 int solve_pnp(vs_ctx* ctx, int nprob, const float* d_obj, const float* d_img, const int* d_off, const double K[4],
               int ransac_iters, int min_inliers, double* d_R, double* d_t, int* d_stat, uint8_t* d_mask,
-              hipStream_t s);
+              hipStream_t s, int max_n = -1);
+// Builds the context's PnP subset table now (synchronises s once); solve_pnp builds it on first use.
+int pnp_reserve(vs_ctx* ctx, hipStream_t s);
 // F-matrix verification: per frame pair (pipeline) or per point set (ABI single problem)
 int fmat_pairs(vs_ctx* ctx, int P, const int* d_pairs, const vs_keypoint* d_kps, int cap, const vs_match* d_good,
                const int* d_ngood, double* d_F, vs_match* d_kept, int* d_nkept, double* d_err, int* d_diag,
