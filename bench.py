@@ -74,8 +74,36 @@ LAYER_FLOPS = {
     "head_b": 2 * 60 * 80 * (65 + 256) * 256,
 }
 
+# Matrix-core FLOPs the Winograd F(2x2, 3x3) kernels execute per frame (round 3, sp_net.hip k_wino3):
+# 16 products per 2 x 2 output tile, input channel and output channel (2.25x fewer than the direct
+# conv's 9 per pixel); conv1a (1 -> 64) stays on the vector ALUs inside conv1.  LAYER_FLOPS above stay
+# the algorithmic (direct-conv) count the roofline contract asks for.
+WINO = os.environ.get("VS_WINO", "1") != "0"
+MFMA_FLOPS = dict(LAYER_FLOPS)
+if WINO:
+    MFMA_FLOPS.update({
+        "conv1_fused": 2 * 16 * 240 * 320 * 64 * 64,
+        "conv2a": 2 * 16 * 120 * 160 * 64 * 64,
+        "conv2b_pool": 2 * 16 * 120 * 160 * 64 * 64,
+        "conv3a": 2 * 16 * 60 * 80 * 128 * 64,
+        "conv3b_pool": 2 * 16 * 60 * 80 * 128 * 128,
+        "conv4a": 2 * 16 * 30 * 40 * 128 * 128,
+        "conv4b": 2 * 16 * 30 * 40 * 128 * 128,
+        "head_a": 2 * 16 * 30 * 40 * 512 * 128,
+    })
+
 # profiling stage -> symbol prefix (as rocprofv3 reports it) of that stage's dominant kernel; the
 # template argument list continues after the prefix (e.g. the chunk width: "<true, 1, true, false, 4>")
+STAGE_KERNEL_WINO = {
+    "conv1_fused": "vs::k_wino3<true, true",
+    "conv2a": "vs::k_wino3<false, false",
+    "conv2b_pool": "vs::k_wino3<true, false",
+    "conv3a": "vs::k_wino3<false, false",
+    "conv3b_pool": "vs::k_wino3<true, false",
+    "conv4a": "vs::k_wino3<false, false",
+    "conv4b": "vs::k_wino3<false, false",
+    "head_a": "vs::k_wino3<false, false",
+}
 STAGE_KERNEL = {
     "conv1_fused": "vs::k_conv3_db<true, 1, true, false",
     "conv2a": "vs::k_conv_mfma<3, false, 2, false",
@@ -87,6 +115,11 @@ STAGE_KERNEL = {
     "head_a": "vs::k_conv3_db<false, 8, false, true",
     "head_b": "vs::k_conv_mfma<1, false, 9, false",
 }
+
+
+STAGE_KERNEL_DIRECT = dict(STAGE_KERNEL)
+if WINO:
+    STAGE_KERNEL.update(STAGE_KERNEL_WINO)
 
 
 def kernel_matches(name, prefix):
@@ -605,8 +638,10 @@ def main():
         ms_l, n_l = pa[dom]
         a_ach = LAYER_FLOPS[dom] * nb / (ms_l / 1e3 / n_l) / 1e12
         net_l = sum(v[0] for k, v in pa.items() if k in LAYER_FLOPS)
+        m_ach = MFMA_FLOPS[dom] * nb / (ms_l / 1e3 / n_l) / 1e12
         alone[f"frames_per_launch_{nb}"] = {"avg_launch_ms": round(ms_l / n_l, 4), "achieved": round(a_ach, 3),
                                             "frac": round(a_ach / FP32_MFMA_PEAK_TFLOPS, 4),
+                                            "mfma_frac": round(m_ach / FP32_MFMA_PEAK_TFLOPS, 4),
                                             "network_tflops": round(sum(LAYER_FLOPS.values()) * nb * 5 / (net_l / 1e3) / 1e12, 3)}
         del semi_t, dg_t
 
@@ -692,8 +727,15 @@ def main():
                 "avg_launch_ms": round(avg_s * 1e3, 4),
                 "frames_per_launch": round(frames_per_launch, 3),
                 "flops_per_launch": round(flops_per_launch),
+                "flops_unit": "algorithmic (direct-convolution) FLOPs, as the roofline contract counts them",
+                "algorithm": "Winograd F(2x2, 3x3), fp32 (sp_net.hip k_wino3)" if WINO else
+                             "direct implicit GEMM, fp32",
+                "mfma_flops_per_launch": round(MFMA_FLOPS[dom] * frames_per_launch),
+                "mfma_achieved": round(MFMA_FLOPS[dom] * frames_per_launch / avg_s / 1e12, 3),
+                "mfma_frac": round(MFMA_FLOPS[dom] * frames_per_launch / avg_s / 1e12 / FP32_MFMA_PEAK_TFLOPS, 4),
                 "note": "network on the extraction stream's CU set (all CUs but VS_SLAM_TRACK_CUS = 32), "
-                        "overlapped with tracking; peak is the whole chip's",
+                        "overlapped with tracking; peak is the whole chip's; achieved / frac count the direct "
+                        "convolution's FLOPs, mfma_* the matrix-core FLOPs the Winograd kernel executes",
                 "alone_whole_chip": alone,
             },
             "match_roofline": mroof,

@@ -65,7 +65,13 @@ def test_bench_exits_nonzero_on_world_mismatch():
                                      ("vs::k_conv3_db<true, 1, true, false4>", False),
                                      ("vs::k_conv3_db<false, 6, false, true, 4>", False)])
 def test_stage_kernel_prefix(name, ok):
-    assert bench.kernel_matches(name, bench.STAGE_KERNEL["conv1_fused"]) == ok
+    assert bench.kernel_matches(name, bench.STAGE_KERNEL_DIRECT["conv1_fused"]) == ok
+
+
+@pytest.mark.parametrize("name,ok", [("vs::k_wino3<true, true>", True), ("vs::k_wino3<true, false>", False),
+                                     ("vs::k_wino3<false, false>", False)])
+def test_stage_kernel_prefix_winograd(name, ok):
+    assert bench.kernel_matches(name, bench.STAGE_KERNEL_WINO["conv1_fused"]) == ok
 
 
 def test_pmc_traffic_per_frame(tmp_path, monkeypatch):
@@ -75,8 +81,8 @@ def test_pmc_traffic_per_frame(tmp_path, monkeypatch):
         "tag": "rX", "frames_per_launch": 8,
         "kernels": {"vs::k_conv3_db<true, 1, true, false, 4>": {"hbm_bytes_per_launch": 8 * 1000.0}}}))
     monkeypatch.setattr(bench, "ROOT", str(tmp_path))
-    assert bench.pmc_traffic(bench.STAGE_KERNEL["conv1_fused"]) == (1000.0, "rX", 8)
-    assert bench.pmc_traffic(bench.STAGE_KERNEL["conv2a"]) == (None, None, None)
+    assert bench.pmc_traffic(bench.STAGE_KERNEL_DIRECT["conv1_fused"]) == (1000.0, "rX", 8)
+    assert bench.pmc_traffic(bench.STAGE_KERNEL_DIRECT["conv2a"]) == (None, None, None)
 
 
 def test_ba_bytes_formula():

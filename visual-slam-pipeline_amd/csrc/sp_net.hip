@@ -17,6 +17,7 @@
 
 #include <cstdlib>
 #include <cstring>
+#include <type_traits>
 
 #include "vs_internal.h"
 
@@ -605,6 +606,263 @@ __global__ __launch_bounds__(256, CKT == 4 ? (MB == 1 ? 4 : 3) : 2) void k_conv3
     }
 }
 
+// Winograd F(2x2, 3x3) conv on v_mfma_f32_16x16x4_f32 (round 3).  Each 2 x 2 output tile is
+//   Y = A^T [ (G g G^T) (.) (B^T d B) ] A      (d: the tile's 4 x 4 input window, g: the 3 x 3 kernel)
+// so the 9 multiply-adds per output pixel, input channel and output channel of the direct conv
+// become 16 per 2 x 2 tile (2.25x fewer matrix-core FLOPs), all in fp32: the transforms are
+// additions (input, output) or precomputed in fp64 and rounded once (weights, DevLayer::wu), and
+// the 16 per-element products are accumulated over the input channels by the matrix cores —
+// 16 independent GEMMs M[xi][tile][cout] = sum_c V[xi][tile][c] U[xi][c][cout].  The parity bar is
+// the fp32 tolerance of the network tests (tests/test_gpu_parity.py), as for the direct conv.
+//
+// Workgroup = 4 x 8 tiles (8 x 16 output pixels, a 10 x 18 input patch) x 64 output channels,
+// 4 waves; wave w owns tiles 16 (w & 1) .. + 15 and output channels 32 (w >> 1) .. + 31 for ALL 16
+// transform elements (32 accumulators of 16 x 16), so the output transform, bias, ReLU and the
+// 2 x 2 max-pool (POOL: a tile IS a pool window) stay in the lane's registers.  MFMA operands:
+// A = V[xi][c0 + lane / 16][tile lane % 16], B = U[xi][c0 + lane / 16][cout lane % 16].
+// LDS images (MI355X_MICROARCH.md, LDS banking): V as [row i][channel][tile][j] so one
+// ds_read_b128 gives a lane the A operands of the 4 elements of a row (conflict-free lane groups);
+// U with the columns of each 32-channel half permuted on the host (position 2i + nb = channel
+// 16 nb + i: both B operands of a lane in one ds_read_b64) and the halves swapped for odd channels
+// (the two 32-lane groups of a read hit different banks).
+// Input channels go in chunks of 4 (one float4 per patch pixel) through a three-stage pipeline
+// with ONE barrier per chunk: during chunk k's 32 MFMAs per wave, the raw patch of chunk k + 2 and
+// the weights of chunk k + 1 go from registers (loaded a chunk earlier) to LDS, and chunk k + 1's
+// patch (in LDS since chunk k - 1) is transformed into the other V buffer (32 tiles x 4 channels:
+// lanes 0-31 of every wave); each row's LDS operands are read one row ahead of its MFMAs.
+// FUSE1A: the patch channels are conv1a (1 -> 64, ReLU) evaluated from a 12 x 20 gray patch.
+template <bool POOL, bool FUSE1A>
+__global__ __launch_bounds__(256, 2) void k_wino3(
+    const float* __restrict__ in, int in_cstride, int in_coff, const float* __restrict__ wu,
+    const float* __restrict__ bias, int cin, int cout, int cout_pad, float* __restrict__ out,
+    int out_cstride, int out_coff, int B, int H, int W, int nbx, int nby,
+    const float* __restrict__ w1a, const float* __restrict__ b1a) {
+    constexpr int CK = 4, TBX = 8, NT = 32, PX = 2 * TBX + 2, PY = 10, NP = PX * PY;  // 18 x 10 patch
+    constexpr int GX = PX + 2, GY = PY + 2;                                            // 20 x 12 gray
+    typedef float f32x2 __attribute__((ext_vector_type(2)));
+    using S0 = std::integral_constant<int, 0>;
+    using S1 = std::integral_constant<int, 1>;
+    __shared__ __attribute__((aligned(16))) float s_x[2][CK][NP];
+    __shared__ __attribute__((aligned(16))) float s_v[2][4][CK][NT][4];
+    __shared__ __attribute__((aligned(16))) float s_u[2][16][CK][64];
+    __shared__ float s_g[FUSE1A ? GX * GY : 1];
+    __shared__ __attribute__((aligned(16))) float s_w1a[FUSE1A ? 64 * 12 : 4];  // [channel][9 taps, bias, 0, 0]
+
+    const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63, li = lane & 15, lk = lane >> 4;
+    const int th = wv & 1, ch = wv >> 1;
+    int blk, nt;
+    xcd_work(cout_pad >> 6, blk, nt);
+    const int n0 = nt * 64;
+    const int b = blk / (nbx * nby), r0 = blk - b * (nbx * nby);
+    const int y0 = (r0 / nbx) * 8, x0 = (r0 % nbx) * 16;
+    const int nchunk = cin / CK;
+
+    // raw patch pixel of this thread (tid < NP): patch (py, px) = input (y0 - 1 + py, x0 - 1 + px)
+    const bool own_px = tid < NP;
+    const int ppy = tid / PX, ppx = tid - (tid / PX) * PX;
+    const int gy = y0 - 1 + ppy, gx = x0 - 1 + ppx;
+    const bool pin = own_px && gy >= 0 && gy < H && gx >= 0 && gx < W;
+    const float* src = in + (((size_t)b * H + (pin ? gy : 0)) * W + (pin ? gx : 0)) * in_cstride + in_coff;
+
+    float gnb[FUSE1A ? 9 : 1];
+    if constexpr (FUSE1A) {
+        const float* g = in + (size_t)b * H * W;
+        for (int i = tid; i < GX * GY; i += 256) {
+            const int yy = i / GX, xx = i - yy * GX;
+            const int sy = y0 - 2 + yy, sx = x0 - 2 + xx;
+            s_g[i] = (sy >= 0 && sy < H && sx >= 0 && sx < W) ? g[(size_t)sy * W + sx] : 0.0f;
+        }
+        for (int i = tid; i < 64 * 12; i += 256) {
+            const int c = i / 12, k = i - c * 12;
+            s_w1a[i] = k < 9 ? w1a[k * 64 + c] : k == 9 ? b1a[c] : 0.0f;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < 9; k++) gnb[k] = own_px ? s_g[(ppy + k / 3) * GX + ppx + k % 3] : 0.0f;
+    }
+
+    // register slots: chunk c's patch in rx[c & 1] (loaded two chunks ahead of its LDS write),
+    // its weights in ru[c & 1] (one chunk ahead)
+    f32x4 rx[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+    f32x4 ru[2][4];
+    auto fetch_x = [&](auto sl_c, int c) {
+        constexpr int sl = decltype(sl_c)::value;
+        if constexpr (!FUSE1A) {
+            if (pin && c < nchunk) rx[sl] = *reinterpret_cast<const f32x4*>(src + c * CK);
+        }
+    };
+    auto fetch_u = [&](auto sl_c, int c) {
+        constexpr int sl = decltype(sl_c)::value;
+        if (c >= nchunk) return;
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const int idx = tid + 256 * j, xi = idx >> 6, cc = (idx >> 4) & 3, q = idx & 15;
+            ru[sl][j] = *reinterpret_cast<const f32x4*>(wu + ((size_t)xi * cin + c * CK + cc) * cout_pad + n0 + 4 * q);
+        }
+    };
+    // chunk c's patch -> s_x[c & 1] (fused: conv1a of its 4 channels at this pixel, 0 outside the image)
+    auto put_x = [&](auto sl_c, int c) {
+        constexpr int sl = decltype(sl_c)::value;
+        if (!own_px || c >= nchunk) return;
+        if constexpr (FUSE1A) {
+#pragma unroll
+            for (int cc = 0; cc < CK; cc++) {
+                const f32x4* wp = reinterpret_cast<const f32x4*>(&s_w1a[(c * CK + cc) * 12]);
+                const f32x4 q0 = wp[0], q1 = wp[1], q2 = wp[2];
+                const float wk[9] = {q0[0], q0[1], q0[2], q0[3], q1[0], q1[1], q1[2], q1[3], q2[0]};
+                float a = q2[1];
+#pragma unroll
+                for (int k = 0; k < 9; k++) a = __builtin_fmaf(gnb[k], wk[k], a);
+                s_x[sl][cc][tid] = pin ? (a > 0.0f ? a : 0.0f) : 0.0f;
+            }
+        } else {
+#pragma unroll
+            for (int cc = 0; cc < CK; cc++) s_x[sl][cc][tid] = pin ? rx[sl][cc] : 0.0f;
+        }
+    };
+    // chunk c's weights -> s_u[c & 1] (channel cc's 32-column halves swapped when cc is odd)
+    auto put_u = [&](auto sl_c, int c) {
+        constexpr int sl = decltype(sl_c)::value;
+        if (c >= nchunk) return;
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const int idx = tid + 256 * j, xi = idx >> 6, cc = (idx >> 4) & 3, q = idx & 15;
+            *reinterpret_cast<f32x4*>(&s_u[sl][xi][cc][4 * (q ^ (8 * (cc & 1)))]) = ru[sl][j];
+        }
+    };
+    // B^T d B of chunk c (s_x[c & 1] -> s_v[c & 1]) for tile t, channel cc (lanes 0-31 of wave cc)
+    auto transform = [&](auto sl_c, int c) {
+        constexpr int sl = decltype(sl_c)::value;
+        if (lane >= 32 || c >= nchunk) return;
+        const int t = lane, cc = wv, tr = t >> 3, tc = t & 7;
+        const float* xp = &s_x[sl][cc][(2 * tr) * PX + 2 * tc];
+        float d[4][4];
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            const f32x2 p0 = *reinterpret_cast<const f32x2*>(xp + i * PX);
+            const f32x2 p1 = *reinterpret_cast<const f32x2*>(xp + i * PX + 2);
+            d[i][0] = p0[0];
+            d[i][1] = p0[1];
+            d[i][2] = p1[0];
+            d[i][3] = p1[1];
+        }
+        float u[4][4];
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            u[0][j] = d[0][j] - d[2][j];
+            u[1][j] = d[1][j] + d[2][j];
+            u[2][j] = d[2][j] - d[1][j];
+            u[3][j] = d[1][j] - d[3][j];
+        }
+#pragma unroll
+        for (int i = 0; i < 4; i++)
+            *reinterpret_cast<f32x4*>(&s_v[sl][i][cc][t][0]) =
+                f32x4{u[i][0] - u[i][2], u[i][1] + u[i][2], u[i][2] - u[i][1], u[i][1] - u[i][3]};
+    };
+
+    f32x4 acc[16][2];
+#pragma unroll
+    for (int x = 0; x < 16; x++) acc[x][0] = acc[x][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    // prologue: V / U of chunk 0 and the patch of chunk 1 in LDS, chunk 1's weights and chunk 2's
+    // patch in registers
+    fetch_x(S0{}, 0);
+    fetch_x(S1{}, 1);
+    fetch_u(S0{}, 0);
+    fetch_u(S1{}, 1);
+    put_x(S0{}, 0);
+    put_x(S1{}, 1);
+    put_u(S0{}, 0);
+    __syncthreads();
+    transform(S0{}, 0);
+    fetch_x(S0{}, 2);
+    __syncthreads();
+    const int ucol = (32 * ch) ^ (32 * (lk & 1));  // this lane's 32-column half in s_u (swizzled)
+    f32x4 opa[2];      // A operands of a row (4 elements)
+    f32x2 opb[2][4];   // B operands of a row (2 x 16 channels per element)
+    auto read_row = [&](int buf, int i, int o) {
+        opa[o] = *reinterpret_cast<const f32x4*>(&s_v[buf][i][lk][16 * th + li][0]);
+#pragma unroll
+        for (int j = 0; j < 4; j++) opb[o][j] = *reinterpret_cast<const f32x2*>(&s_u[buf][4 * i + j][lk][ucol + 2 * li]);
+    };
+    auto mfma_row = [&](int i, int o) {
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const int xi = 4 * i + j;
+            acc[xi][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(opa[o][j], opb[o][j][0], acc[xi][0], 0, 0, 0);
+            acc[xi][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(opa[o][j], opb[o][j][1], acc[xi][1], 0, 0, 0);
+        }
+    };
+    // chunk k (P = k & 1): slots / buffers of chunk k + 1 are P ^ 1, of chunk k + 2 are P
+    auto chunk = [&](auto par, int k) {
+        constexpr int P = decltype(par)::value;
+        using SP = std::integral_constant<int, P>;
+        using SN = std::integral_constant<int, P ^ 1>;
+        fetch_x(SN{}, k + 3);  // slot of chunk k + 1, whose patch went to LDS during chunk k - 1
+        fetch_u(SP{}, k + 2);  // slot of chunk k, whose weights went to LDS during chunk k - 1
+        read_row(P, 0, 0);
+        read_row(P, 1, 1);
+        mfma_row(0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+        read_row(P, 2, 0);
+        put_u(SN{}, k + 1);
+        __builtin_amdgcn_sched_barrier(0);
+        mfma_row(1, 1);
+        __builtin_amdgcn_sched_barrier(0);
+        read_row(P, 3, 1);
+        put_x(SP{}, k + 2);
+        __builtin_amdgcn_sched_barrier(0);
+        mfma_row(2, 0);
+        __builtin_amdgcn_sched_barrier(0);
+        transform(SN{}, k + 1);
+        __builtin_amdgcn_sched_barrier(0);
+        mfma_row(3, 1);
+        __syncthreads();  // chunk k + 1's V / U and chunk k + 2's patch complete; chunk k's buffers free
+    };
+    for (int k = 0; k < nchunk; k += 2) {
+        chunk(S0{}, k);
+        if (k + 1 < nchunk) chunk(S1{}, k + 1);
+    }
+
+    // A^T M A per (tile, output channel); C/D: cout = lane % 16, tile row 4 (lane / 16) + reg
+#pragma unroll
+    for (int nb = 0; nb < 2; nb++) {
+        const int n = n0 + 32 * ch + 16 * nb + li;
+        if (n >= cout) continue;
+        const float bv = bias[n];
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+            const int t = 16 * th + 4 * lk + r, tr = t >> 3, tc = t & 7;
+            const int oy = y0 + 2 * tr, ox = x0 + 2 * tc;
+            float m[4][4];
+#pragma unroll
+            for (int xi = 0; xi < 16; xi++) m[xi >> 2][xi & 3] = acc[xi][nb][r];
+            float s0[4], s1[4];
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                s0[j] = m[0][j] + m[1][j] + m[2][j];
+                s1[j] = m[1][j] - m[2][j] - m[3][j];
+            }
+            const float y00 = s0[0] + s0[1] + s0[2], y01 = s0[1] - s0[2] - s0[3];
+            const float y10 = s1[0] + s1[1] + s1[2], y11 = s1[1] - s1[2] - s1[3];
+            if constexpr (POOL) {
+                if (oy >= H || ox >= W) continue;  // H, W even: a tile inside is a whole window
+                float v = fmaxf(fmaxf(y00, y01), fmaxf(y10, y11)) + bv;
+                v = fmaxf(v, 0.0f);
+                out[(((size_t)b * (H >> 1) + (oy >> 1)) * (W >> 1) + (ox >> 1)) * out_cstride + out_coff + n] = v;
+            } else {
+                const float yv[4] = {y00, y01, y10, y11};
+#pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    const int yy = oy + (q >> 1), xx = ox + (q & 1);
+                    if (yy < H && xx < W)
+                        out[(((size_t)b * H + yy) * W + xx) * out_cstride + out_coff + n] = fmaxf(yv[q] + bv, 0.0f);
+                }
+            }
+        }
+    }
+}
+
 // Descriptor head output: L2-normalise every pixel's 256 channels (MagicLeap export convention,
 // SURVEY.md 8(a) A3).  One wave per pixel, 16-byte loads, shuffle-tree sum of squares.
 __global__ __launch_bounds__(256) void k_desc_l2norm(float* __restrict__ d, long npix) {
@@ -669,10 +927,39 @@ inline bool conv3_db_enabled() {
     return on;
 }
 
+// Winograd F(2x2, 3x3) for every 3x3 layer with a transformed weight copy (round 3; VS_WINO=0
+// selects the direct implicit-GEMM kernels below, for A/B measurements).
+inline bool wino_enabled() {
+    static const bool on = [] {
+        const char* e = std::getenv("VS_WINO");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+
+template <bool POOL, bool FUSE1A>
+int launch_wino(const DevLayer& L, const float* in, int in_cstride, int in_coff, float* out, int out_cstride,
+                int out_coff, int B, int H, int W, hipStream_t s, const DevLayer* L1a) {
+    if (!L.wu || L.cin % 4 != 0 || L.cout_pad % 64 != 0 || (!FUSE1A && (in_cstride % 4 || in_coff % 4)) ||
+        (FUSE1A && (!L1a || L1a->cout != 64 || L.cin != 64)) || (POOL && ((H | W) & 1))) {
+        set_error("conv3 (Winograd): unsupported geometry");
+        return VS_ERR_ARG;
+    }
+    const int nbx = (W + 15) / 16, nby = (H + 7) / 8;
+    dim3 grid((unsigned)((long)B * nbx * nby * (L.cout_pad / 64)));
+    hipLaunchKernelGGL((k_wino3<POOL, FUSE1A>), grid, dim3(256), 0, s, in, in_cstride, in_coff, L.wu, L.b, L.cin,
+                       L.cout, L.cout_pad, out, out_cstride, out_coff, B, H, W, nbx, nby, L1a ? L1a->w : nullptr,
+                       L1a ? L1a->b : nullptr);
+    VS_HIP(hipGetLastError());
+    return VS_OK;
+}
+
 template <bool POOL, int LAYER, bool FUSE1A = false>
 int conv3(vs_ctx* ctx, const DevLayer& L, const float* in, int in_cstride, int in_coff, float* out, int out_cstride,
           int out_coff, int B, int H, int W, hipStream_t s, const DevLayer* L1a = nullptr) {
     (void)ctx;
+    if (wino_enabled() && L.wu)
+        return launch_wino<POOL, FUSE1A>(L, in, in_cstride, in_coff, out, out_cstride, out_coff, B, H, W, s, L1a);
     if constexpr (!FUSE1A) {
         // linear tiles when 8 x 32 tiles would waste columns and the patch fits
         const int lin_rows = (W - 1 + 255) / W + 1 + 2;

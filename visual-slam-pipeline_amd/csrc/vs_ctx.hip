@@ -149,6 +149,29 @@ static int upload_layer(DevLayer& D, int cin, int cout, int cout_pad, int k, con
     VS_HIP(hipMalloc(&D.b, b.size() * sizeof(float)));
     VS_HIP(hipMemcpy(D.w, w.data(), w.size() * sizeof(float), hipMemcpyHostToDevice));
     VS_HIP(hipMemcpy(D.b, b.data(), b.size() * sizeof(float), hipMemcpyHostToDevice));
+    if (k == 3 && cin % 4 == 0) {
+        // Winograd F(2x2, 3x3) weights U[xi = 4i + j][ci][pos(co)] = (G g G^T)[i][j], G = [1 0 0; .5 .5 .5;
+        // .5 -.5 .5; 0 0 1], from the device layout g[a][b] = w[(3a + b)][ci][co] (sp_net.hip k_wino3)
+        static const double G[4][3] = {{1, 0, 0}, {0.5, 0.5, 0.5}, {0.5, -0.5, 0.5}, {0, 0, 1}};
+        std::vector<float> u((size_t)16 * cin * cout_pad);
+        for (int ci = 0; ci < cin; ci++)
+            for (int co = 0; co < cout_pad; co++) {
+                double g[3][3], t[4][3];
+                for (int a = 0; a < 3; a++)
+                    for (int c = 0; c < 3; c++) g[a][c] = w[((size_t)(3 * a + c) * cin + ci) * cout_pad + co];
+                for (int i = 0; i < 4; i++)
+                    for (int c = 0; c < 3; c++) t[i][c] = G[i][0] * g[0][c] + G[i][1] * g[1][c] + G[i][2] * g[2][c];
+                // columns permuted within each 32-column group: position 2i + nb holds output channel
+                // 16 nb + i, so a lane's two B operands (channels li, 16 + li) are one 8-byte LDS read
+                const int pos = (co & ~31) + 2 * (co & 15) + ((co >> 4) & 1);
+                for (int i = 0; i < 4; i++)
+                    for (int j = 0; j < 4; j++)
+                        u[((size_t)(4 * i + j) * cin + ci) * cout_pad + pos] =
+                            (float)(t[i][0] * G[j][0] + t[i][1] * G[j][1] + t[i][2] * G[j][2]);
+            }
+        VS_HIP(hipMalloc(&D.wu, u.size() * sizeof(float)));
+        VS_HIP(hipMemcpy(D.wu, u.data(), u.size() * sizeof(float), hipMemcpyHostToDevice));
+    }
     return VS_OK;
 }
 
@@ -317,9 +340,11 @@ void vs_destroy(vs_ctx* ctx) {
     for (auto& L : ctx->layers) {
         if (L.w) (void)hipFree(L.w);
         if (L.b) (void)hipFree(L.b);
+        if (L.wu) (void)hipFree(L.wu);
     }
     if (ctx->head_a.w) (void)hipFree(ctx->head_a.w);
     if (ctx->head_a.b) (void)hipFree(ctx->head_a.b);
+    if (ctx->head_a.wu) (void)hipFree(ctx->head_a.wu);
     DevBuf* bufs[] = {&ctx->gray,  &ctx->act0,   &ctx->act1,   &ctx->semi,   &ctx->dgrid,  &ctx->heat,
                       &ctx->state, &ctx->flags,  &ctx->keys,   &ctx->keycnt, &ctx->h_img,  &ctx->h_kps,
                       &ctx->h_desc, &ctx->h_n,   &ctx->h_aux0, &ctx->h_aux1, &ctx->h_aux2, &ctx->h_aux3,

@@ -71,6 +71,9 @@ struct DevLayer {
     int cin, cout, cout_pad, k;
     float* w = nullptr;
     float* b = nullptr;
+    // 3x3 layers with cin % 4 == 0: the Winograd F(2x2, 3x3) transformed weights U = G g G^T,
+    // [16][cin][cout_pad] (transform element xi = 4 i + j), computed in fp64 and rounded once
+    float* wu = nullptr;
 };
 
 // ---- growable device scratch -------------------------------------------------------------
