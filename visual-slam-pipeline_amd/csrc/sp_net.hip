@@ -681,23 +681,22 @@ __global__ __launch_bounds__(256, 2) void k_wino3(
         for (int k = 0; k < 9; k++) gnb[k] = own_px ? s_g[(ppy + k / 3) * GX + ppx + k % 3] : 0.0f;
     }
 
-    // register slots: chunk c's patch in rx[c & 1] (loaded two chunks ahead of its LDS write),
-    // its weights in ru[c & 1] (one chunk ahead)
+    // registers: chunk c's patch in rx[c & 1] (loaded two chunks ahead of its LDS write), the next
+    // chunk's weights in ru (loaded one chunk ahead)
     f32x4 rx[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
-    f32x4 ru[2][4];
+    f32x4 ru[4];
     auto fetch_x = [&](auto sl_c, int c) {
         constexpr int sl = decltype(sl_c)::value;
         if constexpr (!FUSE1A) {
             if (pin && c < nchunk) rx[sl] = *reinterpret_cast<const f32x4*>(src + c * CK);
         }
     };
-    auto fetch_u = [&](auto sl_c, int c) {
-        constexpr int sl = decltype(sl_c)::value;
+    auto fetch_u = [&](int c) {
         if (c >= nchunk) return;
 #pragma unroll
         for (int j = 0; j < 4; j++) {
             const int idx = tid + 256 * j, xi = idx >> 6, cc = (idx >> 4) & 3, q = idx & 15;
-            ru[sl][j] = *reinterpret_cast<const f32x4*>(wu + ((size_t)xi * cin + c * CK + cc) * cout_pad + n0 + 4 * q);
+            ru[j] = *reinterpret_cast<const f32x4*>(wu + ((size_t)xi * cin + c * CK + cc) * cout_pad + n0 + 4 * q);
         }
     };
     // chunk c's patch -> s_x[c & 1] (fused: conv1a of its 4 channels at this pixel, 0 outside the image)
@@ -727,7 +726,7 @@ __global__ __launch_bounds__(256, 2) void k_wino3(
 #pragma unroll
         for (int j = 0; j < 4; j++) {
             const int idx = tid + 256 * j, xi = idx >> 6, cc = (idx >> 4) & 3, q = idx & 15;
-            *reinterpret_cast<f32x4*>(&s_u[sl][xi][cc][4 * (q ^ (8 * (cc & 1)))]) = ru[sl][j];
+            *reinterpret_cast<f32x4*>(&s_u[sl][xi][cc][4 * (q ^ (8 * (cc & 1)))]) = ru[j];
         }
     };
     // B^T d B of chunk c (s_x[c & 1] -> s_v[c & 1]) for tile t, channel cc (lanes 0-31 of wave cc)
@@ -768,11 +767,11 @@ __global__ __launch_bounds__(256, 2) void k_wino3(
     // patch in registers
     fetch_x(S0{}, 0);
     fetch_x(S1{}, 1);
-    fetch_u(S0{}, 0);
-    fetch_u(S1{}, 1);
+    fetch_u(0);
     put_x(S0{}, 0);
     put_x(S1{}, 1);
     put_u(S0{}, 0);
+    fetch_u(1);
     __syncthreads();
     transform(S0{}, 0);
     fetch_x(S0{}, 2);
@@ -798,14 +797,15 @@ __global__ __launch_bounds__(256, 2) void k_wino3(
         constexpr int P = decltype(par)::value;
         using SP = std::integral_constant<int, P>;
         using SN = std::integral_constant<int, P ^ 1>;
-        fetch_x(SN{}, k + 3);  // slot of chunk k + 1, whose patch went to LDS during chunk k - 1
-        fetch_u(SP{}, k + 2);  // slot of chunk k, whose weights went to LDS during chunk k - 1
         read_row(P, 0, 0);
         read_row(P, 1, 1);
+        put_u(SN{}, k + 1);    // loaded during chunk k - 1; its buffer's last reader was chunk k - 1
+        fetch_u(k + 2);
+        fetch_x(SN{}, k + 3);  // slot of chunk k + 1, whose patch went to LDS during chunk k - 1
+        __builtin_amdgcn_sched_barrier(0);
         mfma_row(0, 0);
         __builtin_amdgcn_sched_barrier(0);
         read_row(P, 2, 0);
-        put_u(SN{}, k + 1);
         __builtin_amdgcn_sched_barrier(0);
         mfma_row(1, 1);
         __builtin_amdgcn_sched_barrier(0);
@@ -824,16 +824,18 @@ __global__ __launch_bounds__(256, 2) void k_wino3(
         if (k + 1 < nchunk) chunk(S1{}, k + 1);
     }
 
-    // A^T M A per (tile, output channel); C/D: cout = lane % 16, tile row 4 (lane / 16) + reg
+    // A^T M A per (tile, output channel); C/D: cout = lane % 16, tile row 4 (lane / 16) + reg.
+    // Results go through LDS (the staging buffers are free after the last barrier) so that every
+    // global store is a float4 of 4 consecutive channels and a pixel's 32 channels of this wave
+    // form one 128-byte segment (scalar stores of 16 channels per pixel wrote half lines).
+    float* so = &s_u[0][0][0][0] + wv * 2048;  // this wave: [16 tiles x (POOL ? 1 : 4) pixels][32 channels]
 #pragma unroll
     for (int nb = 0; nb < 2; nb++) {
         const int n = n0 + 32 * ch + 16 * nb + li;
-        if (n >= cout) continue;
-        const float bv = bias[n];
+        const float bv = n < cout ? bias[n] : 0.0f;
 #pragma unroll
         for (int r = 0; r < 4; r++) {
-            const int t = 16 * th + 4 * lk + r, tr = t >> 3, tc = t & 7;
-            const int oy = y0 + 2 * tr, ox = x0 + 2 * tc;
+            const int tl = 4 * lk + r;  // tile within the wave's 16
             float m[4][4];
 #pragma unroll
             for (int xi = 0; xi < 16; xi++) m[xi >> 2][xi & 3] = acc[xi][nb][r];
@@ -846,19 +848,33 @@ __global__ __launch_bounds__(256, 2) void k_wino3(
             const float y00 = s0[0] + s0[1] + s0[2], y01 = s0[1] - s0[2] - s0[3];
             const float y10 = s1[0] + s1[1] + s1[2], y11 = s1[1] - s1[2] - s1[3];
             if constexpr (POOL) {
-                if (oy >= H || ox >= W) continue;  // H, W even: a tile inside is a whole window
-                float v = fmaxf(fmaxf(y00, y01), fmaxf(y10, y11)) + bv;
-                v = fmaxf(v, 0.0f);
-                out[(((size_t)b * (H >> 1) + (oy >> 1)) * (W >> 1) + (ox >> 1)) * out_cstride + out_coff + n] = v;
+                so[tl * 32 + 16 * nb + li] = fmaxf(fmaxf(fmaxf(y00, y01), fmaxf(y10, y11)) + bv, 0.0f);
             } else {
-                const float yv[4] = {y00, y01, y10, y11};
-#pragma unroll
-                for (int q = 0; q < 4; q++) {
-                    const int yy = oy + (q >> 1), xx = ox + (q & 1);
-                    if (yy < H && xx < W)
-                        out[(((size_t)b * H + yy) * W + xx) * out_cstride + out_coff + n] = fmaxf(yv[q] + bv, 0.0f);
-                }
+                so[(4 * tl + 0) * 32 + 16 * nb + li] = fmaxf(y00 + bv, 0.0f);
+                so[(4 * tl + 1) * 32 + 16 * nb + li] = fmaxf(y01 + bv, 0.0f);
+                so[(4 * tl + 2) * 32 + 16 * nb + li] = fmaxf(y10 + bv, 0.0f);
+                so[(4 * tl + 3) * 32 + 16 * nb + li] = fmaxf(y11 + bv, 0.0f);
             }
+        }
+    }
+    __syncthreads();
+    constexpr int NV = POOL ? 2 : 8;  // float4 per lane: 16 (POOL) or 64 pixels x 8 float4
+#pragma unroll
+    for (int u = 0; u < NV; u++) {
+        const int e = lane + 64 * u, pix = e >> 3, q = e & 7;
+        const int n = n0 + 32 * ch + 4 * q;
+        if (n >= cout) continue;
+        const f32x4 v = *reinterpret_cast<const f32x4*>(&so[pix * 32 + 4 * q]);
+        const int tl = POOL ? pix : pix >> 2, t = 16 * th + tl, tr = t >> 3, tc = t & 7;
+        if constexpr (POOL) {
+            const int oy = y0 + 2 * tr, ox = x0 + 2 * tc;
+            if (oy >= H || ox >= W) continue;  // H, W even: a tile inside is a whole window
+            *reinterpret_cast<f32x4*>(out + (((size_t)b * (H >> 1) + (oy >> 1)) * (W >> 1) + (ox >> 1)) * out_cstride +
+                                      out_coff + n) = v;
+        } else {
+            const int oy = y0 + 2 * tr + ((pix >> 1) & 1), ox = x0 + 2 * tc + (pix & 1);
+            if (oy >= H || ox >= W) continue;
+            *reinterpret_cast<f32x4*>(out + (((size_t)b * H + oy) * W + ox) * out_cstride + out_coff + n) = v;
         }
     }
 }
@@ -940,7 +956,8 @@ inline bool wino_enabled() {
 template <bool POOL, bool FUSE1A>
 int launch_wino(const DevLayer& L, const float* in, int in_cstride, int in_coff, float* out, int out_cstride,
                 int out_coff, int B, int H, int W, hipStream_t s, const DevLayer* L1a) {
-    if (!L.wu || L.cin % 4 != 0 || L.cout_pad % 64 != 0 || (!FUSE1A && (in_cstride % 4 || in_coff % 4)) ||
+    if (!L.wu || L.cin % 4 != 0 || L.cout_pad % 64 != 0 || L.cout % 4 != 0 || out_cstride % 4 || out_coff % 4 ||
+        (!FUSE1A && (in_cstride % 4 || in_coff % 4)) ||
         (FUSE1A && (!L1a || L1a->cout != 64 || L.cin != 64)) || (POOL && ((H | W) & 1))) {
         set_error("conv3 (Winograd): unsupported geometry");
         return VS_ERR_ARG;
