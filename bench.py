@@ -646,6 +646,7 @@ def main():
         del semi_t, dg_t
 
     track_cus = int(os.environ.get("VS_SLAM_TRACK_CUS", "32"))
+    spec_cus = int(os.environ.get("VS_SLAM_SPEC_CUS", "32"))
     mroof = {"tracker": match_roofline(prof_trk.get("match"), 1, track_cus,
                                        "tracking loop: one pair (frame vs reference keyframe) per launch on the "
                                        f"tracker's {track_cus}-CU stream (overlapped with extraction on the rest)")}
@@ -733,7 +734,8 @@ def main():
                 "mfma_flops_per_launch": round(MFMA_FLOPS[dom] * frames_per_launch),
                 "mfma_achieved": round(MFMA_FLOPS[dom] * frames_per_launch / avg_s / 1e12, 3),
                 "mfma_frac": round(MFMA_FLOPS[dom] * frames_per_launch / avg_s / 1e12 / FP32_MFMA_PEAK_TFLOPS, 4),
-                "note": "network on the extraction stream's CU set (all CUs but VS_SLAM_TRACK_CUS = 32), "
+                "note": f"network on the extraction stream's CU set (all CUs but VS_SLAM_TRACK_CUS = {track_cus} "
+                        f"and VS_SLAM_SPEC_CUS = {spec_cus} for the speculative chain), "
                         "overlapped with tracking; peak is the whole chip's; achieved / frac count the direct "
                         "convolution's FLOPs, mfma_* the matrix-core FLOPs the Winograd kernel executes",
                 "alone_whole_chip": alone,

@@ -421,9 +421,14 @@ struct GpuOps {
         const char* env = std::getenv("VS_SLAM_TRACK_CUS");
         const int tcu = env ? std::atoi(env) : 32;
         // VS_SLAM_SPEC_CUS > 0: the speculative chain gets CUs of its own, carved from the
-        // extraction set (default 0: it shares the tracking CUs)
+        // extraction set.  Default 32 (round 3): with the chain launched at chain() time it overlaps
+        // the local-map / PnP kernels, whose 100 one-wave EPnP hypotheses then share SIMDs with the
+        // chain's 1024-wave RANSAC grids (k_pnp_hyp median 190 -> 139 us with a CU set of its own);
+        // the Winograd network keeps up on the remaining 192 CUs.  Same-box host profile
+        // (profiles/r03t_*): process_frame 496 / 466 / 457 us and 1,943 / 2,029 / 2,061 frames/s at
+        // 0 / 16 / 32 chain CUs.  0: the chain shares the tracking CUs.
         const char* senv = std::getenv("VS_SLAM_SPEC_CUS");
-        const int scu = senv ? std::max(0, std::atoi(senv)) : 0;
+        const int scu = senv ? std::max(0, std::atoi(senv)) : 32;
         // VS_SLAM_POST_CUS > 0: the extraction post-processing (xp) gets CUs of its own, taken from
         // the network's set (default 0: it shares the network's CUs)
         const char* penv = std::getenv("VS_SLAM_POST_CUS");
