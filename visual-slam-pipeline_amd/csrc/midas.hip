@@ -590,6 +590,8 @@ struct DevW {
     float* w = nullptr;
     float* b = nullptr;
     int cop = 0;
+    float* wu = nullptr;  // 3x3 convs: Winograd F(2x2, 3x3) weights (stride-1 steps run k_wino3)
+    float* bz = nullptr;  // their bias, zeros for the bias-free "rn" projections
 };
 
 }  // namespace midas
@@ -644,6 +646,17 @@ static int upload(vs_midas* m) {
             if (L.bias) {
                 VS_HIP(hipMalloc(&D.b, b.size() * sizeof(float)));
                 VS_HIP(hipMemcpy(D.b, b.data(), b.size() * sizeof(float), hipMemcpyHostToDevice));
+            }
+            if (L.k == 3 && L.cin % 4 == 0 && L.cout % 4 == 0) {
+                const std::vector<float> u = winograd_weights(w.data(), L.cin, D.cop);
+                VS_HIP(hipMalloc(&D.wu, u.size() * sizeof(float)));
+                VS_HIP(hipMemcpy(D.wu, u.data(), u.size() * sizeof(float), hipMemcpyHostToDevice));
+                if (L.bias) {
+                    D.bz = D.b;
+                } else {
+                    VS_HIP(hipMalloc(&D.bz, b.size() * sizeof(float)));
+                    VS_HIP(hipMemcpy(D.bz, b.data(), b.size() * sizeof(float), hipMemcpyHostToDevice));
+                }
             }
         }
     }
@@ -704,6 +717,15 @@ static int ensure_batch(vs_midas* m, int B) {
     return VS_OK;
 }
 
+// VS_WINO=0: every conv on k_mid_conv (A/B measurements)
+static bool wino_on() {
+    static const bool on = [] {
+        const char* e = std::getenv("VS_WINO");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+
 // network: m->input [B][256][256][3] -> returns the output tensor pointer [B][256][256]
 static int forward(vs_midas* m, int B, hipStream_t s, float** out) {
     const Net& N = net();
@@ -722,7 +744,28 @@ static int forward(vs_midas* m, int B, hipStream_t s, float** out) {
             a.CoP = m->dev[st.layer].cop, a.k = st.k, a.stride = st.stride, a.pad_t = st.pad_t, a.pad_l = st.pad_l;
             a.act = st.act, a.pre_relu = st.pre_relu;
             const int npix = B * st.Ho * st.Wo;
-            if (st.Co == 1 && st.k == 1 && st.stride == 1)
+            const DevW& D = m->dev[st.layer];
+            if (D.wu && st.k == 3 && st.stride == 1 && st.pad_t == 1 && st.pad_l == 1 && wino_on()) {
+                // stride-1 3x3 (the refinenet residual units, the rn projections, the head): Winograd
+                WinoArgs wa{};
+                wa.in = a.in;
+                wa.in_cstride = st.C;
+                wa.wu = D.wu;
+                wa.bias = D.bz;
+                wa.cin = st.C;
+                wa.cout = st.Co;
+                wa.cout_pad = D.cop;
+                wa.out = a.out;
+                wa.out_cstride = st.Co;
+                wa.B = B;
+                wa.H = st.H;
+                wa.W = st.W;
+                wa.res1 = a.res1;
+                wa.res2 = a.res2;
+                wa.act = st.act;
+                wa.pre_relu = st.pre_relu ? 1 : 0;
+                VS_CHECK(wino3_launch(wa, false, false, s));
+            } else if (st.Co == 1 && st.k == 1 && st.stride == 1)
                 hipLaunchKernelGGL(k_mid_conv_co1, dim3((npix + 255) / 256), dim3(256), 0, s, a);
             else
                 hipLaunchKernelGGL(k_mid_conv, dim3((npix + kCT - 1) / kCT, a.CoP / kCT), dim3(256), 0, s, a);
@@ -851,6 +894,8 @@ void vs_midas_destroy(vs_midas* m) {
     for (auto& D : m->dev) {
         if (D.w) (void)hipFree(D.w);
         if (D.b) (void)hipFree(D.b);
+        if (D.wu) (void)hipFree(D.wu);
+        if (D.bz && D.bz != D.b) (void)hipFree(D.bz);
     }
     for (auto& b : m->slots) b.release();
     m->input.release();

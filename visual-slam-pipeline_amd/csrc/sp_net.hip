@@ -631,12 +631,20 @@ __global__ __launch_bounds__(256, CKT == 4 ? (MB == 1 ? 4 : 3) : 2) void k_conv3
 // patch (in LDS since chunk k - 1) is transformed into the other V buffer (32 tiles x 4 channels:
 // lanes 0-31 of every wave); each row's LDS operands are read one row ahead of its MFMAs.
 // FUSE1A: the patch channels are conv1a (1 -> 64, ReLU) evaluated from a 12 x 20 gray patch.
+// MiDaS (midas.hip) runs its stride-1 3x3 convs through the same kernel (WinoArgs: input-side ReLU,
+// ReLU / ReLU6 / none, residual adds after the activation, as k_mid_conv's epilogue).
 template <bool POOL, bool FUSE1A>
-__global__ __launch_bounds__(256, 2) void k_wino3(
-    const float* __restrict__ in, int in_cstride, int in_coff, const float* __restrict__ wu,
-    const float* __restrict__ bias, int cin, int cout, int cout_pad, float* __restrict__ out,
-    int out_cstride, int out_coff, int B, int H, int W, int nbx, int nby,
-    const float* __restrict__ w1a, const float* __restrict__ b1a) {
+__global__ __launch_bounds__(256, 2) void k_wino3(WinoArgs wa) {
+    const float* __restrict__ in = wa.in;
+    const float* __restrict__ wu = wa.wu;
+    const float* __restrict__ bias = wa.bias;
+    float* __restrict__ out = wa.out;
+    const float* __restrict__ w1a = wa.w1a;
+    const float* __restrict__ b1a = wa.b1a;
+    const int in_cstride = wa.in_cstride, in_coff = wa.in_coff, cin = wa.cin, cout = wa.cout, cout_pad = wa.cout_pad;
+    const int out_cstride = wa.out_cstride, out_coff = wa.out_coff, H = wa.H, W = wa.W, nbx = wa.nbx, nby = wa.nby;
+    const int act = wa.act;
+    const bool pre_relu = wa.pre_relu != 0;
     constexpr int CK = 4, TBX = 8, NT = 32, PX = 2 * TBX + 2, PY = 10, NP = PX * PY;  // 18 x 10 patch
     constexpr int GX = PX + 2, GY = PY + 2;                                            // 20 x 12 gray
     typedef float f32x2 __attribute__((ext_vector_type(2)));
@@ -716,7 +724,10 @@ __global__ __launch_bounds__(256, 2) void k_wino3(
             }
         } else {
 #pragma unroll
-            for (int cc = 0; cc < CK; cc++) s_x[sl][cc][tid] = pin ? rx[sl][cc] : 0.0f;
+            for (int cc = 0; cc < CK; cc++) {
+                const float v = pin ? rx[sl][cc] : 0.0f;
+                s_x[sl][cc][tid] = pre_relu ? fmaxf(v, 0.0f) : v;
+            }
         }
     };
     // chunk c's weights -> s_u[c & 1] (channel cc's 32-column halves swapped when cc is odd)
@@ -847,13 +858,15 @@ __global__ __launch_bounds__(256, 2) void k_wino3(
             }
             const float y00 = s0[0] + s0[1] + s0[2], y01 = s0[1] - s0[2] - s0[3];
             const float y10 = s1[0] + s1[1] + s1[2], y11 = s1[1] - s1[2] - s1[3];
+            // act: 0 none, 1 ReLU, 2 ReLU6 (v > 0 ? min(v, 6) : 0, as midas.hip activate())
+            auto actf = [&](float v) { return act == 0 ? v : v > 0.0f ? (act == 2 && !(v < 6.0f) ? 6.0f : v) : 0.0f; };
             if constexpr (POOL) {
-                so[tl * 32 + 16 * nb + li] = fmaxf(fmaxf(fmaxf(y00, y01), fmaxf(y10, y11)) + bv, 0.0f);
+                so[tl * 32 + 16 * nb + li] = actf(fmaxf(fmaxf(y00, y01), fmaxf(y10, y11)) + bv);
             } else {
-                so[(4 * tl + 0) * 32 + 16 * nb + li] = fmaxf(y00 + bv, 0.0f);
-                so[(4 * tl + 1) * 32 + 16 * nb + li] = fmaxf(y01 + bv, 0.0f);
-                so[(4 * tl + 2) * 32 + 16 * nb + li] = fmaxf(y10 + bv, 0.0f);
-                so[(4 * tl + 3) * 32 + 16 * nb + li] = fmaxf(y11 + bv, 0.0f);
+                so[(4 * tl + 0) * 32 + 16 * nb + li] = actf(y00 + bv);
+                so[(4 * tl + 1) * 32 + 16 * nb + li] = actf(y01 + bv);
+                so[(4 * tl + 2) * 32 + 16 * nb + li] = actf(y10 + bv);
+                so[(4 * tl + 3) * 32 + 16 * nb + li] = actf(y11 + bv);
             }
         }
     }
@@ -874,7 +887,11 @@ __global__ __launch_bounds__(256, 2) void k_wino3(
         } else {
             const int oy = y0 + 2 * tr + ((pix >> 1) & 1), ox = x0 + 2 * tc + (pix & 1);
             if (oy >= H || ox >= W) continue;
-            *reinterpret_cast<f32x4*>(out + (((size_t)b * H + oy) * W + ox) * out_cstride + out_coff + n) = v;
+            const size_t o = (((size_t)b * H + oy) * W + ox) * out_cstride + out_coff + n;
+            f32x4 r = v;
+            if (wa.res1) r = r + *reinterpret_cast<const f32x4*>(wa.res1 + o);
+            if (wa.res2) r = *reinterpret_cast<const f32x4*>(wa.res2 + o) + r;
+            *reinterpret_cast<f32x4*>(out + o) = r;
         }
     }
 }
@@ -953,6 +970,26 @@ inline bool wino_enabled() {
     return on;
 }
 
+}  // namespace
+
+int wino3_launch(WinoArgs a, bool pool, bool fuse1a, hipStream_t s) {
+    a.nbx = (a.W + 15) / 16;
+    a.nby = (a.H + 7) / 8;
+    dim3 grid((unsigned)((long)a.B * a.nbx * a.nby * (a.cout_pad / 64)));
+    if (pool && fuse1a)
+        hipLaunchKernelGGL((k_wino3<true, true>), grid, dim3(256), 0, s, a);
+    else if (pool)
+        hipLaunchKernelGGL((k_wino3<true, false>), grid, dim3(256), 0, s, a);
+    else if (fuse1a)
+        return VS_ERR_ARG;
+    else
+        hipLaunchKernelGGL((k_wino3<false, false>), grid, dim3(256), 0, s, a);
+    VS_HIP(hipGetLastError());
+    return VS_OK;
+}
+
+namespace {
+
 template <bool POOL, bool FUSE1A>
 int launch_wino(const DevLayer& L, const float* in, int in_cstride, int in_coff, float* out, int out_cstride,
                 int out_coff, int B, int H, int W, hipStream_t s, const DevLayer* L1a) {
@@ -962,13 +999,25 @@ int launch_wino(const DevLayer& L, const float* in, int in_cstride, int in_coff,
         set_error("conv3 (Winograd): unsupported geometry");
         return VS_ERR_ARG;
     }
-    const int nbx = (W + 15) / 16, nby = (H + 7) / 8;
-    dim3 grid((unsigned)((long)B * nbx * nby * (L.cout_pad / 64)));
-    hipLaunchKernelGGL((k_wino3<POOL, FUSE1A>), grid, dim3(256), 0, s, in, in_cstride, in_coff, L.wu, L.b, L.cin,
-                       L.cout, L.cout_pad, out, out_cstride, out_coff, B, H, W, nbx, nby, L1a ? L1a->w : nullptr,
-                       L1a ? L1a->b : nullptr);
-    VS_HIP(hipGetLastError());
-    return VS_OK;
+    WinoArgs a{};
+    a.in = in;
+    a.in_cstride = in_cstride;
+    a.in_coff = in_coff;
+    a.wu = L.wu;
+    a.bias = L.b;
+    a.cin = L.cin;
+    a.cout = L.cout;
+    a.cout_pad = L.cout_pad;
+    a.out = out;
+    a.out_cstride = out_cstride;
+    a.out_coff = out_coff;
+    a.B = B;
+    a.H = H;
+    a.W = W;
+    a.w1a = L1a ? L1a->w : nullptr;
+    a.b1a = L1a ? L1a->b : nullptr;
+    a.act = 1;  // every SuperPoint 3x3 conv is followed by ReLU
+    return wino3_launch(a, POOL, FUSE1A, s);
 }
 
 template <bool POOL, int LAYER, bool FUSE1A = false>

@@ -139,6 +139,29 @@ static void to_dev_layout(const float* wsrc, const float* bsrc, const LayerDef& 
     }
 }
 
+// Winograd F(2x2, 3x3) weights U[xi = 4i + j][ci][pos(co)] = (G g G^T)[i][j], G = [1 0 0; .5 .5 .5;
+// .5 -.5 .5; 0 0 1], from the device layout g[a][b] = w[(3a + b)][ci][co] (sp_net.hip k_wino3).
+// Columns permuted within each 32-column group: position 2i + nb holds output channel 16 nb + i, so
+// a lane's two B operands (channels li, 16 + li) are one 8-byte LDS read.
+std::vector<float> winograd_weights(const float* w, int cin, int cout_pad) {
+    static const double G[4][3] = {{1, 0, 0}, {0.5, 0.5, 0.5}, {0.5, -0.5, 0.5}, {0, 0, 1}};
+    std::vector<float> u((size_t)16 * cin * cout_pad);
+    for (int ci = 0; ci < cin; ci++)
+        for (int co = 0; co < cout_pad; co++) {
+            double g[3][3], t[4][3];
+            for (int a = 0; a < 3; a++)
+                for (int c = 0; c < 3; c++) g[a][c] = w[((size_t)(3 * a + c) * cin + ci) * cout_pad + co];
+            for (int i = 0; i < 4; i++)
+                for (int c = 0; c < 3; c++) t[i][c] = G[i][0] * g[0][c] + G[i][1] * g[1][c] + G[i][2] * g[2][c];
+            const int pos = (co & ~31) + 2 * (co & 15) + ((co >> 4) & 1);
+            for (int i = 0; i < 4; i++)
+                for (int j = 0; j < 4; j++)
+                    u[((size_t)(4 * i + j) * cin + ci) * cout_pad + pos] =
+                        (float)(t[i][0] * G[j][0] + t[i][1] * G[j][1] + t[i][2] * G[j][2]);
+        }
+    return u;
+}
+
 static int upload_layer(DevLayer& D, int cin, int cout, int cout_pad, int k, const std::vector<float>& w,
                         const std::vector<float>& b) {
     D.cin = cin;
@@ -150,25 +173,7 @@ static int upload_layer(DevLayer& D, int cin, int cout, int cout_pad, int k, con
     VS_HIP(hipMemcpy(D.w, w.data(), w.size() * sizeof(float), hipMemcpyHostToDevice));
     VS_HIP(hipMemcpy(D.b, b.data(), b.size() * sizeof(float), hipMemcpyHostToDevice));
     if (k == 3 && cin % 4 == 0) {
-        // Winograd F(2x2, 3x3) weights U[xi = 4i + j][ci][pos(co)] = (G g G^T)[i][j], G = [1 0 0; .5 .5 .5;
-        // .5 -.5 .5; 0 0 1], from the device layout g[a][b] = w[(3a + b)][ci][co] (sp_net.hip k_wino3)
-        static const double G[4][3] = {{1, 0, 0}, {0.5, 0.5, 0.5}, {0.5, -0.5, 0.5}, {0, 0, 1}};
-        std::vector<float> u((size_t)16 * cin * cout_pad);
-        for (int ci = 0; ci < cin; ci++)
-            for (int co = 0; co < cout_pad; co++) {
-                double g[3][3], t[4][3];
-                for (int a = 0; a < 3; a++)
-                    for (int c = 0; c < 3; c++) g[a][c] = w[((size_t)(3 * a + c) * cin + ci) * cout_pad + co];
-                for (int i = 0; i < 4; i++)
-                    for (int c = 0; c < 3; c++) t[i][c] = G[i][0] * g[0][c] + G[i][1] * g[1][c] + G[i][2] * g[2][c];
-                // columns permuted within each 32-column group: position 2i + nb holds output channel
-                // 16 nb + i, so a lane's two B operands (channels li, 16 + li) are one 8-byte LDS read
-                const int pos = (co & ~31) + 2 * (co & 15) + ((co >> 4) & 1);
-                for (int i = 0; i < 4; i++)
-                    for (int j = 0; j < 4; j++)
-                        u[((size_t)(4 * i + j) * cin + ci) * cout_pad + pos] =
-                            (float)(t[i][0] * G[j][0] + t[i][1] * G[j][1] + t[i][2] * G[j][2]);
-            }
+        const std::vector<float> u = winograd_weights(w.data(), cin, cout_pad);
         VS_HIP(hipMalloc(&D.wu, u.size() * sizeof(float)));
         VS_HIP(hipMemcpy(D.wu, u.data(), u.size() * sizeof(float), hipMemcpyHostToDevice));
     }

@@ -151,6 +151,28 @@ int sp_forward(vs_ctx* ctx, int B, const uint8_t* d_img, int channels, int h, in
 int sp_postprocess(vs_ctx* ctx, int B, int hc, int wc, int h, int w, vs_keypoint* d_kps,
                    float* d_desc, int* d_n, int cap, hipStream_t s, const float* semi = nullptr,
                    const float* dgrid = nullptr);
+// Winograd F(2x2, 3x3) stride-1 pad-1 convolution (sp_net.hip k_wino3), NHWC fp32: U = the
+// transformed weights (winograd_weights), bias [cout_pad] (required), act 0 / 1 / 2 = none / ReLU /
+// ReLU6 after the bias, then out = act(.) + res1, out = res2 + out (optional, [pixel][out_cstride]).
+struct WinoArgs {
+    const float* in;
+    int in_cstride, in_coff;
+    const float* wu;
+    const float* bias;
+    int cin, cout, cout_pad;
+    float* out;
+    int out_cstride, out_coff;
+    int B, H, W, nbx, nby;
+    const float* w1a;
+    const float* b1a;
+    const float* res1;
+    const float* res2;
+    int act, pre_relu;
+};
+int wino3_launch(WinoArgs a, bool pool, bool fuse1a, hipStream_t s);
+// U[xi][ci][pos(co)] from direct-layout 3x3 weights w[(3a + b)][ci][co] (cout_pad columns; pos
+// permutes each 32-column group for k_wino3's paired operand reads).  fp64, rounded once.
+std::vector<float> winograd_weights(const float* w, int cin, int cout_pad);
 // Matching
 int match_pairs(vs_ctx* ctx, int P, const int* d_pairs, int F, const float* d_desc,
                 const int* d_n, int cap, float ratio, vs_match* d_raw, int* d_nraw,
