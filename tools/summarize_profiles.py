@@ -32,21 +32,28 @@ def short(name):
 
 
 def per_kernel(path, counter, grids=None):
-    """Mean counter value x 1024 per dispatch of each kernel (FETCH_SIZE / WRITE_SIZE are KB); the
-    distinct grid sizes of each kernel's dispatches go to `grids` (one size = one launch shape)."""
+    """Mean counter value x 1024 per dispatch of each kernel (FETCH_SIZE / WRITE_SIZE are KB) over
+    the dispatches of its most frequent grid size (the tracker's extraction chunk: bench.py's
+    network-alone block adds B-frame launches of the same kernels, which must not be averaged in);
+    the distinct grid sizes of each kernel's dispatches go to `grids`."""
     per_disp = collections.defaultdict(float)
-    names = {}
+    names, grid_of = {}, {}
     for r in csv.DictReader(open(path)):
         if r["Counter_Name"] == counter:
             d = r.get("Dispatch_Id") or str(len(names))
             per_disp[d] += float(r["Counter_Value"]) * 1024.0
             names[d] = short(r["Kernel_Name"])
+            grid_of[d] = r.get("Grid_Size", "")
             if grids is not None and r.get("Grid_Size"):
                 grids.setdefault(names[d], set()).add(r["Grid_Size"])
-    agg = collections.defaultdict(list)
+    agg = collections.defaultdict(lambda: collections.defaultdict(list))
     for d, v in per_disp.items():
-        agg[names[d]].append(v)
-    return {k: sum(v) / len(v) for k, v in agg.items()}
+        agg[names[d]][grid_of[d]].append(v)
+    out = {}
+    for k, by_grid in agg.items():
+        v = max(by_grid.values(), key=len)
+        out[k] = sum(v) / len(v)
+    return out
 
 
 def per_dispatch(path):
