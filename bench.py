@@ -737,7 +737,9 @@ def main():
                 "note": f"network on the extraction stream's CU set (all CUs but VS_SLAM_TRACK_CUS = {track_cus} "
                         f"and VS_SLAM_SPEC_CUS = {spec_cus} for the speculative chain), "
                         "overlapped with tracking; peak is the whole chip's; achieved / frac count the direct "
-                        "convolution's FLOPs, mfma_* the matrix-core FLOPs the Winograd kernel executes",
+                        "convolution's FLOPs (the algorithmic work), so with Winograd's 2.25x fewer multiplies frac "
+                        "can exceed 1 (alone_whole_chip at 32 frames); mfma_* count the matrix-core FLOPs the "
+                        "Winograd kernel executes (its utilisation of the fp32 MFMA peak)",
                 "alone_whole_chip": alone,
             },
             "match_roofline": mroof,
