@@ -628,8 +628,8 @@ __global__ __launch_bounds__(256, CKT == 4 ? (MB == 1 ? 4 : 3) : 2) void k_conv3
 // Input channels go in chunks of 4 (one float4 per patch pixel) through a three-stage pipeline
 // with ONE barrier per chunk: during chunk k's 32 MFMAs per wave, the raw patch of chunk k + 2 and
 // the weights of chunk k + 1 go from registers (loaded a chunk earlier) to LDS, and chunk k + 1's
-// patch (in LDS since chunk k - 1) is transformed into the other V buffer (32 tiles x 4 channels:
-// lanes 0-31 of every wave); each row's LDS operands are read one row ahead of its MFMAs.
+// patch (in LDS since chunk k - 1) is transformed into the other V buffer (32 tiles x 4 channels x
+// 2 row halves on the 256 lanes); each row's LDS operands are read one row ahead of its MFMAs.
 // FUSE1A: the patch channels are conv1a (1 -> 64, ReLU) evaluated from a 12 x 20 gray patch.
 // MiDaS (midas.hip) runs its stride-1 3x3 convs through the same kernel (WinoArgs: input-side ReLU,
 // ReLU / ReLU6 / none, residual adds after the activation, as k_mid_conv's epilogue).
@@ -740,34 +740,42 @@ __global__ __launch_bounds__(256, 2) void k_wino3(WinoArgs wa) {
             *reinterpret_cast<f32x4*>(&s_u[sl][xi][cc][4 * (q ^ (8 * (cc & 1)))]) = ru[j];
         }
     };
-    // B^T d B of chunk c (s_x[c & 1] -> s_v[c & 1]) for tile t, channel cc (lanes 0-31 of wave cc)
+    // B^T d B of chunk c (s_x[c & 1] -> s_v[c & 1]) on all 64 lanes: lane = (tile t, channel cc)
+    // of a channel pair, and the wave's half (wave-uniform: no divergence) takes V rows 2 half and
+    // 2 half + 1, which need input rows half .. half + 2 only
     auto transform = [&](auto sl_c, int c) {
         constexpr int sl = decltype(sl_c)::value;
-        if (lane >= 32 || c >= nchunk) return;
-        const int t = lane, cc = wv, tr = t >> 3, tc = t & 7;
-        const float* xp = &s_x[sl][cc][(2 * tr) * PX + 2 * tc];
-        float d[4][4];
+        if (c >= nchunk) return;
+        const int t = lane & 31, cc = 2 * (wv & 1) + (lane >> 5), half = wv >> 1, tr = t >> 3, tc = t & 7;
+        const float* xp = &s_x[sl][cc][(2 * tr + half) * PX + 2 * tc];
+        float e[3][4];
 #pragma unroll
-        for (int i = 0; i < 4; i++) {
+        for (int i = 0; i < 3; i++) {
             const f32x2 p0 = *reinterpret_cast<const f32x2*>(xp + i * PX);
             const f32x2 p1 = *reinterpret_cast<const f32x2*>(xp + i * PX + 2);
-            d[i][0] = p0[0];
-            d[i][1] = p0[1];
-            d[i][2] = p1[0];
-            d[i][3] = p1[1];
+            e[i][0] = p0[0];
+            e[i][1] = p0[1];
+            e[i][2] = p1[0];
+            e[i][3] = p1[1];
         }
-        float u[4][4];
+        float ua[4], ub[4];  // rows 2 half, 2 half + 1 of B^T d
+        if (half == 0) {
 #pragma unroll
-        for (int j = 0; j < 4; j++) {
-            u[0][j] = d[0][j] - d[2][j];
-            u[1][j] = d[1][j] + d[2][j];
-            u[2][j] = d[2][j] - d[1][j];
-            u[3][j] = d[1][j] - d[3][j];
+            for (int j = 0; j < 4; j++) {
+                ua[j] = e[0][j] - e[2][j];  // d0 - d2
+                ub[j] = e[1][j] + e[2][j];  // d1 + d2
+            }
+        } else {
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                ua[j] = e[1][j] - e[0][j];  // d2 - d1
+                ub[j] = e[0][j] - e[2][j];  // d1 - d3
+            }
         }
-#pragma unroll
-        for (int i = 0; i < 4; i++)
-            *reinterpret_cast<f32x4*>(&s_v[sl][i][cc][t][0]) =
-                f32x4{u[i][0] - u[i][2], u[i][1] + u[i][2], u[i][2] - u[i][1], u[i][1] - u[i][3]};
+        *reinterpret_cast<f32x4*>(&s_v[sl][2 * half][cc][t][0]) =
+            f32x4{ua[0] - ua[2], ua[1] + ua[2], ua[2] - ua[1], ua[1] - ua[3]};
+        *reinterpret_cast<f32x4*>(&s_v[sl][2 * half + 1][cc][t][0]) =
+            f32x4{ub[0] - ub[2], ub[1] + ub[2], ub[2] - ub[1], ub[1] - ub[3]};
     };
 
     f32x4 acc[16][2];
