@@ -400,10 +400,22 @@ __global__ __launch_bounds__(256) void k_mid_conv_co1(ConvArgs a) {
     if (p >= npix) return;
     const float* src = a.in + (size_t)p * a.C;
     float s = 0.f;
-    for (int c = 0; c < a.C; c++) {
-        float t = src[c];
+    auto term = [&](float t, int c) {
         if (a.pre_relu) t = t > 0.f ? t : 0.f;
         s = fmaf(t, a.w[(size_t)c * a.CoP], s);
+    };
+    if ((a.C & 3) == 0) {
+        // round 3: the pixel's channels as float4 loads (32 scalar loads per thread at a 128-byte
+        // lane stride had made this 4.2 MFLOP layer 15 % of MiDaS); the same sequential fmaf chain
+        for (int c = 0; c < a.C; c += 4) {
+            const float4 t = *reinterpret_cast<const float4*>(src + c);
+            term(t.x, c);
+            term(t.y, c + 1);
+            term(t.z, c + 2);
+            term(t.w, c + 3);
+        }
+    } else {
+        for (int c = 0; c < a.C; c++) term(src[c], c);
     }
     float v = activate(s + (a.bias ? a.bias[0] : 0.f), a.act);
     if (a.res1) v = v + a.res1[p];
@@ -412,6 +424,8 @@ __global__ __launch_bounds__(256) void k_mid_conv_co1(ConvArgs a) {
 }
 
 // Depthwise k x k, stride s, TF-same padding, bias + ReLU6; one thread per (pixel, 4 channels).
+// (Round 3: four outputs per thread sharing each kernel row's loads measured the same, 1.02 ms per
+// 32-frame batch; not kept.)
 __global__ __launch_bounds__(256) void k_mid_dw(const float* __restrict__ in, const float* __restrict__ w,
                                                 const float* __restrict__ bias, float* __restrict__ out, int B, int H,
                                                 int W, int C, int Ho, int Wo, int k, int stride, int pad_t, int pad_l) {
