@@ -275,16 +275,23 @@ struct ConvArgs {
     const float* res1;
     const float* res2;
     float* out;
+    float* part;  // split-K: raw partial sums [split][pixel][Co] instead of out (k_mid_splitk finishes)
     int B, H, W, C, Ho, Wo, Co, CoP, k, stride, pad_t, pad_l, act, pre_relu;
+    int splits;   // K splits (blockIdx.z), 1 = none
 };
 
 constexpr int kCT = 64;  // output pixels x channels per workgroup
 constexpr int kCK = 16;  // input channels per K chunk
 constexpr int kAS = kCK + 4;  // LDS row stride of the pixel operand (floats)
+constexpr int kOS = kCT + 4;  // LDS row stride of the staged output tile (floats)
+static_assert(kCT * kOS <= 4 * kCT * kAS, "output tile must fit the operand buffers");
 
 __global__ __launch_bounds__(256) void k_mid_conv(ConvArgs a) {
-    __shared__ float sA[2][kCT * kAS];  // [pixel][16 k] (k permuted for float4 fragments), double-buffered
-    __shared__ float sB[2][kCT * kAS];  // [cout][16 k]
+    // sA [2][pixel][16 k] (k permuted for float4 fragments), double-buffered; sB [2][cout][16 k]; after
+    // the K loop the same LDS holds the output tile [pixel][64 channels] (row stride kOS)
+    __shared__ __attribute__((aligned(16))) float smem[4 * kCT * kAS];
+    float(*sA)[kCT * kAS] = reinterpret_cast<float(*)[kCT * kAS]>(smem);
+    float(*sB)[kCT * kAS] = reinterpret_cast<float(*)[kCT * kAS]>(smem + 2 * kCT * kAS);
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, li = lane & 15, lg = lane >> 4;
     const int npix = a.B * a.Ho * a.Wo;
     const int p0 = blockIdx.x * kCT, n0 = blockIdx.y * kCT;
@@ -312,6 +319,8 @@ __global__ __launch_bounds__(256) void k_mid_conv(ConvArgs a) {
         for (int j = 0; j < 2; j++) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
     const int nchunk = (a.C + kCK - 1) / kCK;
     const int T = a.k * a.k * nchunk;  // (tap, channel chunk) steps
+    // split-K: this workgroup's contiguous range of steps
+    const int t0 = (int)((long)T * blockIdx.z / a.splits), t1 = (int)((long)T * (blockIdx.z + 1) / a.splits);
     float v[4], u[4];
     // operands of step t into registers (global loads; issued one step ahead of their MFMAs)
     auto fetch = [&](int t) {
@@ -346,12 +355,12 @@ __global__ __launch_bounds__(256) void k_mid_conv(ConvArgs a) {
             sB[buf][co * kAS + 4 * j + kq] = u[j];
         }
     };
-    fetch(0);
-    stage(0);
+    fetch(t0);
+    stage(t0 & 1);
     __syncthreads();
-    for (int t = 0; t < T; t++) {
+    for (int t = t0; t < t1; t++) {
         const int cur = t & 1;
-        if (t + 1 < T) fetch(t + 1);
+        if (t + 1 < t1) fetch(t + 1);
         float4 fa[2], fb[2];
 #pragma unroll
         for (int i = 0; i < 2; i++) {
@@ -367,8 +376,60 @@ __global__ __launch_bounds__(256) void k_mid_conv(ConvArgs a) {
                     acc[i][m] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[i][j], fb[m][j], acc[i][m], 0, 0, 0);
         // the other buffer was last read in step t - 1, which every wave finished before the
         // barrier that ended it
-        if (t + 1 < T) stage(cur ^ 1);
+        if (t + 1 < t1) stage(cur ^ 1);
         __syncthreads();
+    }
+    if ((a.Co & 3) == 0) {
+        // through LDS so that every global access is a float4 of 4 channels and a pixel's 64 channels
+        // form whole 256-byte rows (the direct stores below write 64-byte pieces per pixel: partial
+        // lines on the HBM-bound expand / project layers).  The K loop's last barrier freed the LDS.
+#pragma unroll
+        for (int i = 0; i < 2; i++)
+#pragma unroll
+            for (int m = 0; m < 2; m++)
+#pragma unroll
+                for (int e = 0; e < 4; e++) smem[(wq * 32 + 16 * i + 4 * lg + e) * kOS + wt * 32 + 16 * m + li] = acc[i][m][e];
+        __syncthreads();
+        float* dst = a.part ? a.part + (size_t)blockIdx.z * npix * a.Co : a.out;
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const int idx = tid + 256 * j, px = idx >> 4, c4 = 4 * (idx & 15);
+            const int gpix = p0 + px, c = n0 + c4;
+            if (gpix >= npix || c >= a.Co) continue;
+            f32x4 ov = *reinterpret_cast<const f32x4*>(&smem[px * kOS + c4]);
+            const size_t o = (size_t)gpix * a.Co + c;
+            if (!a.part) {
+                const f32x4 bv = a.bias ? *reinterpret_cast<const f32x4*>(a.bias + c) : f32x4{0.f, 0.f, 0.f, 0.f};
+                f32x4 r1 = {0.f, 0.f, 0.f, 0.f}, r2 = {0.f, 0.f, 0.f, 0.f};
+                if (a.res1) r1 = *reinterpret_cast<const f32x4*>(a.res1 + o);
+                if (a.res2) r2 = *reinterpret_cast<const f32x4*>(a.res2 + o);
+#pragma unroll
+                for (int e = 0; e < 4; e++) {
+                    float t = activate(ov[e] + bv[e], a.act);
+                    if (a.res1) t = t + r1[e];
+                    if (a.res2) t = r2[e] + t;
+                    ov[e] = t;
+                }
+            }
+            *reinterpret_cast<f32x4*>(dst + o) = ov;
+        }
+        return;
+    }
+    if (a.part) {  // split-K partials, finished by k_mid_splitk
+        float* dst = a.part + (size_t)blockIdx.z * npix * a.Co;
+#pragma unroll
+        for (int i = 0; i < 2; i++)
+#pragma unroll
+            for (int m = 0; m < 2; m++) {
+                const int co = n0 + wt * 32 + 16 * m + li;
+                if (co >= a.Co) continue;
+#pragma unroll
+                for (int e = 0; e < 4; e++) {
+                    const int gpix = p0 + wq * 32 + 16 * i + 4 * lg + e;
+                    if (gpix < npix) dst[(size_t)gpix * a.Co + co] = acc[i][m][e];
+                }
+            }
+        return;
     }
     // D[pixel 4 lg + e][cout li] of fragment (i, m)
 #pragma unroll
@@ -393,34 +454,116 @@ __global__ __launch_bounds__(256) void k_mid_conv(ConvArgs a) {
 
 // 1 x 1 convolution to a single output channel (the head's last layer, 32 -> 1 at the full
 // 256 x 256): one thread per pixel, a plain dot product over the channels.  On the implicit GEMM it
-// would occupy a 64-wide output tile for one channel (63/64 of the MFMA work padding).
+// would occupy a 64-wide output tile for one channel (63/64 of the MFMA work padding).  The
+// workgroup's 256 pixel rows (C floats each, contiguous in HBM) are staged through LDS with
+// coalesced float4 loads, rows padded to C + 4 floats so that the per-pixel float4 reads are
+// conflict-free (round 3: direct per-thread row loads at a 4C-byte lane stride reached 0.9 TB/s).
+constexpr int kCo1MaxC = 32;
 __global__ __launch_bounds__(256) void k_mid_conv_co1(ConvArgs a) {
-    const int p = blockIdx.x * 256 + threadIdx.x;
+    __shared__ float sx[256 * (kCo1MaxC + 4)];
+    const int tid = threadIdx.x;
     const int npix = a.B * a.Ho * a.Wo;
+    const int p0 = blockIdx.x * 256, p = p0 + tid;
+    const int C = a.C, C4 = C >> 2, RS = C + 4;
+    const int nv = (min(256, npix - p0)) * C4;  // float4s of this workgroup's rows
+    const float4* src = reinterpret_cast<const float4*>(a.in + (size_t)p0 * C);
+    for (int i = tid; i < nv; i += 256) {
+        const int r = i / C4, q = i - r * C4;
+        *reinterpret_cast<float4*>(&sx[r * RS + 4 * q]) = src[i];
+    }
+    __syncthreads();
     if (p >= npix) return;
-    const float* src = a.in + (size_t)p * a.C;
     float s = 0.f;
     auto term = [&](float t, int c) {
         if (a.pre_relu) t = t > 0.f ? t : 0.f;
         s = fmaf(t, a.w[(size_t)c * a.CoP], s);
     };
-    if ((a.C & 3) == 0) {
-        // round 3: the pixel's channels as float4 loads (32 scalar loads per thread at a 128-byte
-        // lane stride had made this 4.2 MFLOP layer 15 % of MiDaS); the same sequential fmaf chain
-        for (int c = 0; c < a.C; c += 4) {
-            const float4 t = *reinterpret_cast<const float4*>(src + c);
-            term(t.x, c);
-            term(t.y, c + 1);
-            term(t.z, c + 2);
-            term(t.w, c + 3);
-        }
-    } else {
-        for (int c = 0; c < a.C; c++) term(src[c], c);
+    for (int c = 0; c < C; c += 4) {
+        const float4 t = *reinterpret_cast<const float4*>(&sx[tid * RS + c]);
+        term(t.x, c);
+        term(t.y, c + 1);
+        term(t.z, c + 2);
+        term(t.w, c + 3);
     }
     float v = activate(s + (a.bias ? a.bias[0] : 0.f), a.act);
     if (a.res1) v = v + a.res1[p];
     if (a.res2) v = a.res2[p] + v;
     a.out[p] = v;
+}
+
+// The stem (3 -> 32, 3 x 3, stride 2 at 256^2): K = 27 would fill 27 of the implicit GEMM's 16 x 9
+// K slots per tap and 8192 workgroups of 9 barriers each; here a thread computes one output pixel's
+// 32 channels on the vector ALUs (weights broadcast from LDS, the 3 x 3 x C window from L1) and the
+// workgroup's 256 x 32 outputs leave through LDS as coalesced float4 rows.  C <= 4, Co == 32.
+constexpr int kStemCo = 32, kStemMaxC = 4;
+__global__ __launch_bounds__(256) void k_mid_stem(ConvArgs a) {
+    __shared__ float sw[9 * kStemMaxC * kStemCo];
+    __shared__ __attribute__((aligned(16))) float so[256 * (kStemCo + 4)];
+    const int tid = threadIdx.x, C = a.C, kk = a.k * a.k;
+    for (int i = tid; i < kk * C * kStemCo; i += 256) {
+        const int co = i % kStemCo, tc = i / kStemCo;  // tc = tap * C + channel
+        sw[i] = a.w[(size_t)tc * a.CoP + co];
+    }
+    __syncthreads();
+    const int npix = a.B * a.Ho * a.Wo, p0 = blockIdx.x * 256, p = p0 + tid;
+    float acc[kStemCo];
+#pragma unroll
+    for (int co = 0; co < kStemCo; co++) acc[co] = 0.f;
+    if (p < npix) {
+        const int b = p / (a.Ho * a.Wo), rem = p - b * a.Ho * a.Wo, oy = rem / a.Wo, ox = rem - oy * a.Wo;
+        for (int ky = 0; ky < a.k; ky++) {
+            const int iy = oy * a.stride - a.pad_t + ky;
+            if (iy < 0 || iy >= a.H) continue;
+            for (int kx = 0; kx < a.k; kx++) {
+                const int ix = ox * a.stride - a.pad_l + kx;
+                if (ix < 0 || ix >= a.W) continue;
+                const float* src = a.in + (((size_t)b * a.H + iy) * a.W + ix) * C;
+                const float* wt = sw + (ky * a.k + kx) * C * kStemCo;
+                for (int c = 0; c < C; c++) {
+                    const float x = src[c];
+#pragma unroll
+                    for (int co = 0; co < kStemCo; co++) acc[co] = fmaf(x, wt[c * kStemCo + co], acc[co]);
+                }
+            }
+        }
+    }
+#pragma unroll
+    for (int co = 0; co < kStemCo; co++) so[tid * (kStemCo + 4) + co] = activate(acc[co] + (a.bias ? a.bias[co] : 0.f), a.act);
+    __syncthreads();
+    const int nv = min(256, npix - p0) * (kStemCo / 4);
+    f32x4* dst = reinterpret_cast<f32x4*>(a.out + (size_t)p0 * kStemCo);
+    for (int i = tid; i < nv; i += 256) {
+        const int r = i / (kStemCo / 4), q = i - r * (kStemCo / 4);
+        dst[i] = *reinterpret_cast<const f32x4*>(&so[r * (kStemCo + 4) + 4 * q]);
+    }
+}
+
+// Split-K finish: out = epilogue(sum of the S partials in split order), the epilogue of
+// k_mid_conv (bias, activation, then the residual adds); Co % 4 == 0, 4 channels per thread.
+__global__ __launch_bounds__(256) void k_mid_splitk(ConvArgs a) {
+    const int npix = a.B * a.Ho * a.Wo, C4 = a.Co >> 2;
+    const long idx = (long)blockIdx.x * 256 + threadIdx.x;
+    if (idx >= (long)npix * C4) return;
+    const int c = 4 * (int)(idx % C4);
+    const float4* P = reinterpret_cast<const float4*>(a.part);
+    const size_t plane = (size_t)npix * C4;
+    float4 acc = P[idx];
+    for (int z = 1; z < a.splits; z++) {
+        const float4 t = P[z * plane + idx];
+        acc.x += t.x;
+        acc.y += t.y;
+        acc.z += t.z;
+        acc.w += t.w;
+    }
+    float o[4] = {acc.x, acc.y, acc.z, acc.w};
+#pragma unroll
+    for (int e = 0; e < 4; e++) {
+        float v = activate(o[e] + (a.bias ? a.bias[c + e] : 0.f), a.act);
+        if (a.res1) v = v + a.res1[4 * idx + e];
+        if (a.res2) v = a.res2[4 * idx + e] + v;
+        o[e] = v;
+    }
+    reinterpret_cast<float4*>(a.out)[idx] = make_float4(o[0], o[1], o[2], o[3]);
 }
 
 // Depthwise k x k, stride s, TF-same padding, bias + ReLU6; one thread per (pixel, 4 channels).
@@ -455,6 +598,65 @@ __global__ __launch_bounds__(256) void k_mid_dw(const float* __restrict__ in, co
     s.z = activate(s.z, A_RELU6);
     s.w = activate(s.w, A_RELU6);
     reinterpret_cast<float4*>(out)[idx] = s;
+}
+
+// Stride-1 depthwise K x K for PX consecutive output pixels of a row per thread (4 channels): each
+// kernel row's K weights and PX + K - 1 input pixels are loaded once for the PX outputs (the
+// per-output kernel above re-reads 2 K^2 float4 per output: L2-bandwidth-bound on the 16^2 / 8^2
+// layers).  Every output's taps are summed in the same (ky, kx) order as k_mid_dw.
+template <int K, int PX>
+__global__ __launch_bounds__(256) void k_mid_dw_row(const float* __restrict__ in, const float* __restrict__ w,
+                                                    const float* __restrict__ bias, float* __restrict__ out, int B,
+                                                    int H, int W, int C, int pad_t, int pad_l) {
+    const int C4 = C / 4, nxg = (W + PX - 1) / PX;
+    const long idx = (long)blockIdx.x * 256 + threadIdx.x;
+    if (idx >= (long)B * H * nxg * C4) return;
+    const int c4 = (int)(idx % C4);
+    const long g = idx / C4;
+    const int xg = (int)(g % nxg), oy = (int)((g / nxg) % H), b = (int)(g / ((long)nxg * H));
+    const int x0 = xg * PX;
+    const float4* in4 = reinterpret_cast<const float4*>(in);
+    const float4* w4 = reinterpret_cast<const float4*>(w);
+    const float4 bv = reinterpret_cast<const float4*>(bias)[c4];
+    float4 acc[PX];
+#pragma unroll
+    for (int p = 0; p < PX; p++) acc[p] = bv;
+    for (int ky = 0; ky < K; ky++) {
+        const int iy = oy - pad_t + ky;
+        if (iy < 0 || iy >= H) continue;
+        float4 wr[K], row[PX + K - 1];
+#pragma unroll
+        for (int kx = 0; kx < K; kx++) wr[kx] = w4[(size_t)(ky * K + kx) * C4 + c4];
+        const size_t rbase = ((size_t)b * H + iy) * W;
+#pragma unroll
+        for (int j = 0; j < PX + K - 1; j++) {
+            const int ix = x0 - pad_l + j;
+            row[j] = (ix >= 0 && ix < W) ? in4[(rbase + ix) * C4 + c4] : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+#pragma unroll
+        for (int p = 0; p < PX; p++)
+#pragma unroll
+            for (int kx = 0; kx < K; kx++) {
+                // taps outside the image are skipped (not added as zero), as in k_mid_dw
+                const int ix = x0 + p - pad_l + kx;
+                if (ix < 0 || ix >= W) continue;
+                acc[p].x = fmaf(row[p + kx].x, wr[kx].x, acc[p].x);
+                acc[p].y = fmaf(row[p + kx].y, wr[kx].y, acc[p].y);
+                acc[p].z = fmaf(row[p + kx].z, wr[kx].z, acc[p].z);
+                acc[p].w = fmaf(row[p + kx].w, wr[kx].w, acc[p].w);
+            }
+    }
+    float4* o4 = reinterpret_cast<float4*>(out) + (((size_t)b * H + oy) * W) * C4 + c4;
+#pragma unroll
+    for (int p = 0; p < PX; p++) {
+        if (x0 + p >= W) continue;
+        float4 v = acc[p];
+        v.x = activate(v.x, A_RELU6);
+        v.y = activate(v.y, A_RELU6);
+        v.z = activate(v.z, A_RELU6);
+        v.w = activate(v.w, A_RELU6);
+        o4[(size_t)(x0 + p) * C4] = v;
+    }
 }
 
 // x2 bilinear upsampling (torch interpolate, mode "bilinear"), NHWC, 4 channels per thread.
@@ -619,6 +821,7 @@ struct vs_midas {
     std::vector<int> slot_of;       // tensor -> slot
     std::vector<size_t> slot_elems; // floats per frame per slot
     vs::DevBuf input, post_part;
+    vs::DevBuf splitk;  // k_mid_conv split-K partials (largest step's S x pixels x Co)
     int batch_cap = 0;
 };
 
@@ -723,10 +926,39 @@ static float* tensor_ptr(vs_midas* m, int t) {
     return s == -2 ? m->input.as<float>() : m->slots[s].as<float>();
 }
 
+// K splits of an implicit-GEMM step: the encoder's 1x1 projections at 8^2-16^2 (K up to 1392, 64 x 64
+// tiles over 2k-8k pixels: 128-384 workgroups, each walking up to 87 K steps) fill the chip only when
+// K is split.  S raises the workgroup count toward VS_MIDAS_SPLITK_WGS (default 1024; 0 = never
+// split) with at least 3 K steps per split; the partials are summed in split order by k_mid_splitk.
+// S is sized for a nominal 32-frame batch whatever B is, so that a frame's depth does not depend on
+// the batch it was computed in (the summation order follows S).
+static int splitk_of(const Step& st, int /*B*/) {
+    constexpr int B = 32;
+    static const int target = [] {
+        const char* e = std::getenv("VS_MIDAS_SPLITK_WGS");
+        return e ? std::atoi(e) : 1024;
+    }();
+    if (target <= 0 || st.Co % 4 != 0 || st.Co == 1) return 1;
+    const long npix = (long)B * st.Ho * st.Wo;
+    const long nwg = (npix + kCT - 1) / kCT * ((st.Co + kCT - 1) / kCT);
+    const int T = st.k * st.k * ((st.C + kCK - 1) / kCK);
+    long S = (target + nwg - 1) / nwg;
+    S = std::min<long>(S, T / 3);
+    S = std::min<long>(S, 16);
+    return S > 1 ? (int)S : 1;
+}
+
 static int ensure_batch(vs_midas* m, int B) {
     if (B <= m->batch_cap) return VS_OK;
     for (size_t i = 0; i < m->slots.size(); i++) VS_CHECK(m->slots[i].ensure((size_t)B * m->slot_elems[i] * sizeof(float)));
     VS_CHECK(m->input.ensure((size_t)B * kIn * kIn * 3 * sizeof(float)));
+    size_t part = 0;
+    for (const Step& st : net().steps)
+        if (st.kind == K_CONV) {
+            const int S = splitk_of(st, B);
+            if (S > 1) part = std::max(part, (size_t)S * B * st.Ho * st.Wo * st.Co);
+        }
+    if (part) VS_CHECK(m->splitk.ensure(part * sizeof(float)));
     m->batch_cap = B;
     return VS_OK;
 }
@@ -735,6 +967,15 @@ static int ensure_batch(vs_midas* m, int B) {
 static bool wino_on() {
     static const bool on = [] {
         const char* e = std::getenv("VS_WINO");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+
+// VS_MIDAS_DW_ROW=0: stride-1 depthwise layers on the per-output k_mid_dw (A/B measurements)
+static bool dw_row_on() {
+    static const bool on = [] {
+        const char* e = std::getenv("VS_MIDAS_DW_ROW");
         return !(e && e[0] == '0');
     }();
     return on;
@@ -757,6 +998,7 @@ static int forward(vs_midas* m, int B, hipStream_t s, float** out) {
             a.B = B, a.H = st.H, a.W = st.W, a.C = st.C, a.Ho = st.Ho, a.Wo = st.Wo, a.Co = st.Co;
             a.CoP = m->dev[st.layer].cop, a.k = st.k, a.stride = st.stride, a.pad_t = st.pad_t, a.pad_l = st.pad_l;
             a.act = st.act, a.pre_relu = st.pre_relu;
+            a.splits = 1;
             const int npix = B * st.Ho * st.Wo;
             const DevW& D = m->dev[st.layer];
             if (D.wu && st.k == 3 && st.stride == 1 && st.pad_t == 1 && st.pad_l == 1 && wino_on()) {
@@ -779,10 +1021,33 @@ static int forward(vs_midas* m, int B, hipStream_t s, float** out) {
                 wa.act = st.act;
                 wa.pre_relu = st.pre_relu ? 1 : 0;
                 VS_CHECK(wino3_launch(wa, false, false, s));
-            } else if (st.Co == 1 && st.k == 1 && st.stride == 1)
+            } else if (st.Co == 1 && st.k == 1 && st.stride == 1) {
+                VS_ARG(st.C % 4 == 0 && st.C <= kCo1MaxC, "midas: 1x1 single-channel conv needs C % 4 == 0, C <= 32");
                 hipLaunchKernelGGL(k_mid_conv_co1, dim3((npix + 255) / 256), dim3(256), 0, s, a);
+            } else if (st.Co == kStemCo && st.C <= kStemMaxC && st.k <= 3 && !st.pre_relu && st.res1 < 0 && st.res2 < 0) {
+                hipLaunchKernelGGL(k_mid_stem, dim3((npix + 255) / 256), dim3(256), 0, s, a);
+            } else {
+                const int S = splitk_of(st, B);
+                if (S > 1) {
+                    a.part = m->splitk.as<float>();
+                    a.splits = S;
+                }
+                hipLaunchKernelGGL(k_mid_conv, dim3((npix + kCT - 1) / kCT, a.CoP / kCT, S), dim3(256), 0, s, a);
+                if (S > 1) {
+                    const long n = (long)npix * (st.Co / 4);
+                    hipLaunchKernelGGL(k_mid_splitk, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, a);
+                }
+            }
+        } else if (st.kind == K_DW && st.stride == 1 && (st.k == 3 || st.k == 5) && dw_row_on()) {
+            constexpr int PX = 8;
+            const long n = (long)B * st.H * ((st.W + PX - 1) / PX) * (st.C / 4);
+            const dim3 grid((unsigned)((n + 255) / 256));
+            if (st.k == 3)
+                hipLaunchKernelGGL((k_mid_dw_row<3, PX>), grid, dim3(256), 0, s, tensor_ptr(m, st.in), m->dev[st.layer].w,
+                                   m->dev[st.layer].b, tensor_ptr(m, st.out), B, st.H, st.W, st.C, st.pad_t, st.pad_l);
             else
-                hipLaunchKernelGGL(k_mid_conv, dim3((npix + kCT - 1) / kCT, a.CoP / kCT), dim3(256), 0, s, a);
+                hipLaunchKernelGGL((k_mid_dw_row<5, PX>), grid, dim3(256), 0, s, tensor_ptr(m, st.in), m->dev[st.layer].w,
+                                   m->dev[st.layer].b, tensor_ptr(m, st.out), B, st.H, st.W, st.C, st.pad_t, st.pad_l);
         } else if (st.kind == K_DW) {
             const long n = (long)B * st.Ho * st.Wo * (st.C / 4);
             hipLaunchKernelGGL(k_mid_dw, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, tensor_ptr(m, st.in),
@@ -914,6 +1179,7 @@ void vs_midas_destroy(vs_midas* m) {
     for (auto& b : m->slots) b.release();
     m->input.release();
     m->post_part.release();
+    m->splitk.release();
     delete m;
 }
 

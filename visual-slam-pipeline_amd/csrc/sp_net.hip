@@ -633,8 +633,13 @@ __global__ __launch_bounds__(256, CKT == 4 ? (MB == 1 ? 4 : 3) : 2) void k_conv3
 // FUSE1A: the patch channels are conv1a (1 -> 64, ReLU) evaluated from a 12 x 20 gray patch.
 // MiDaS (midas.hip) runs its stride-1 3x3 convs through the same kernel (WinoArgs: input-side ReLU,
 // ReLU / ReLU6 / none, residual adds after the activation, as k_mid_conv's epilogue).
-template <bool POOL, bool FUSE1A>
+// C32 (cout <= 32, MiDaS's head at 128^2 / 256^2): the wave pair of a tile half splits the 16
+// transform elements instead of the 64 output channels (wave ch takes rows 2 ch, 2 ch + 1 of the 4 x 4
+// domain for channels 0..31), so no MFMA multiplies a zero weight column; the two partial output
+// transforms are added through LDS (Y = A^T (M_rows01 + M_rows23) A) before bias and activation.
+template <bool POOL, bool FUSE1A, bool C32 = false>
 __global__ __launch_bounds__(256, 2) void k_wino3(WinoArgs wa) {
+    static_assert(!(C32 && (POOL || FUSE1A)), "C32 is the plain (MiDaS) variant");
     const float* __restrict__ in = wa.in;
     const float* __restrict__ wu = wa.wu;
     const float* __restrict__ bias = wa.bias;
@@ -795,7 +800,7 @@ __global__ __launch_bounds__(256, 2) void k_wino3(WinoArgs wa) {
     transform(S0{}, 0);
     fetch_x(S0{}, 2);
     __syncthreads();
-    const int ucol = (32 * ch) ^ (32 * (lk & 1));  // this lane's 32-column half in s_u (swizzled)
+    const int ucol = (C32 ? 0 : 32 * ch) ^ (32 * (lk & 1));  // this lane's 32-column half in s_u (swizzled)
     f32x4 opa[2];      // A operands of a row (4 elements)
     f32x2 opb[2][4];   // B operands of a row (2 x 16 channels per element)
     auto read_row = [&](int buf, int i, int o) {
@@ -811,11 +816,36 @@ __global__ __launch_bounds__(256, 2) void k_wino3(WinoArgs wa) {
             acc[xi][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(opa[o][j], opb[o][j][1], acc[xi][1], 0, 0, 0);
         }
     };
+    // C32: this wave's row r (domain row 2 ch + r) into accumulators 4 r .. 4 r + 3
+    auto mfma_row_c32 = [&](int r, int o) {
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            acc[4 * r + j][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(opa[o][j], opb[o][j][0], acc[4 * r + j][0], 0, 0, 0);
+            acc[4 * r + j][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(opa[o][j], opb[o][j][1], acc[4 * r + j][1], 0, 0, 0);
+        }
+    };
     // chunk k (P = k & 1): slots / buffers of chunk k + 1 are P ^ 1, of chunk k + 2 are P
     auto chunk = [&](auto par, int k) {
         constexpr int P = decltype(par)::value;
         using SP = std::integral_constant<int, P>;
         using SN = std::integral_constant<int, P ^ 1>;
+        if constexpr (C32) {
+            read_row(P, 2 * ch, 0);
+            read_row(P, 2 * ch + 1, 1);
+            put_u(SN{}, k + 1);
+            fetch_u(k + 2);
+            fetch_x(SN{}, k + 3);
+            __builtin_amdgcn_sched_barrier(0);
+            mfma_row_c32(0, 0);
+            __builtin_amdgcn_sched_barrier(0);
+            put_x(SP{}, k + 2);
+            __builtin_amdgcn_sched_barrier(0);
+            mfma_row_c32(1, 1);
+            __builtin_amdgcn_sched_barrier(0);
+            transform(SN{}, k + 1);
+            __syncthreads();
+            return;
+        }
         read_row(P, 0, 0);
         read_row(P, 1, 1);
         put_u(SN{}, k + 1);    // loaded during chunk k - 1; its buffer's last reader was chunk k - 1
@@ -848,16 +878,55 @@ __global__ __launch_bounds__(256, 2) void k_wino3(WinoArgs wa) {
     // global store is a float4 of 4 consecutive channels and a pixel's 32 channels of this wave
     // form one 128-byte segment (scalar stores of 16 channels per pixel wrote half lines).
     float* so = &s_u[0][0][0][0] + wv * 2048;  // this wave: [16 tiles x (POOL ? 1 : 4) pixels][32 channels]
+    if constexpr (C32) {
+        // waves ch = 1 (domain rows 2, 3) leave their partial transforms in their LDS region; the
+        // ch = 0 partner (rows 0, 1) adds them below
+        if (ch == 1) {
+#pragma unroll
+            for (int nb = 0; nb < 2; nb++)
+#pragma unroll
+                for (int r = 0; r < 4; r++) {
+                    const int tl = 4 * lk + r;
+                    float m2[4], m3[4];
+#pragma unroll
+                    for (int j = 0; j < 4; j++) {
+                        m2[j] = acc[j][nb][r];
+                        m3[j] = acc[4 + j][nb][r];
+                    }
+                    float s0[4], s1[4];
+#pragma unroll
+                    for (int j = 0; j < 4; j++) {
+                        s0[j] = m2[j];
+                        s1[j] = -m2[j] - m3[j];
+                    }
+                    so[(4 * tl + 0) * 32 + 16 * nb + li] = s0[0] + s0[1] + s0[2];
+                    so[(4 * tl + 1) * 32 + 16 * nb + li] = s0[1] - s0[2] - s0[3];
+                    so[(4 * tl + 2) * 32 + 16 * nb + li] = s1[0] + s1[1] + s1[2];
+                    so[(4 * tl + 3) * 32 + 16 * nb + li] = s1[1] - s1[2] - s1[3];
+                }
+        }
+        __syncthreads();
+    }
+    const float* sp = so + 2 * 2048;  // C32: the ch = 1 partner's partials (read by ch = 0 waves only)
 #pragma unroll
     for (int nb = 0; nb < 2; nb++) {
-        const int n = n0 + 32 * ch + 16 * nb + li;
+        const int n = n0 + (C32 ? 0 : 32 * ch) + 16 * nb + li;
         const float bv = n < cout ? bias[n] : 0.0f;
 #pragma unroll
         for (int r = 0; r < 4; r++) {
             const int tl = 4 * lk + r;  // tile within the wave's 16
             float m[4][4];
+            if constexpr (C32) {
 #pragma unroll
-            for (int xi = 0; xi < 16; xi++) m[xi >> 2][xi & 3] = acc[xi][nb][r];
+                for (int j = 0; j < 4; j++) {
+                    m[0][j] = acc[j][nb][r];
+                    m[1][j] = acc[4 + j][nb][r];
+                    m[2][j] = m[3][j] = 0.0f;
+                }
+            } else {
+#pragma unroll
+                for (int xi = 0; xi < 16; xi++) m[xi >> 2][xi & 3] = acc[xi][nb][r];
+            }
             float s0[4], s1[4];
 #pragma unroll
             for (int j = 0; j < 4; j++) {
@@ -870,6 +939,14 @@ __global__ __launch_bounds__(256, 2) void k_wino3(WinoArgs wa) {
             auto actf = [&](float v) { return act == 0 ? v : v > 0.0f ? (act == 2 && !(v < 6.0f) ? 6.0f : v) : 0.0f; };
             if constexpr (POOL) {
                 so[tl * 32 + 16 * nb + li] = actf(fmaxf(fmaxf(y00, y01), fmaxf(y10, y11)) + bv);
+            } else if constexpr (C32) {
+                if (ch == 0) {
+                    const int o0 = (4 * tl) * 32 + 16 * nb + li;
+                    so[o0] = actf(y00 + sp[o0] + bv);
+                    so[o0 + 32] = actf(y01 + sp[o0 + 32] + bv);
+                    so[o0 + 64] = actf(y10 + sp[o0 + 64] + bv);
+                    so[o0 + 96] = actf(y11 + sp[o0 + 96] + bv);
+                }
             } else {
                 so[(4 * tl + 0) * 32 + 16 * nb + li] = actf(y00 + bv);
                 so[(4 * tl + 1) * 32 + 16 * nb + li] = actf(y01 + bv);
@@ -883,7 +960,7 @@ __global__ __launch_bounds__(256, 2) void k_wino3(WinoArgs wa) {
 #pragma unroll
     for (int u = 0; u < NV; u++) {
         const int e = lane + 64 * u, pix = e >> 3, q = e & 7;
-        const int n = n0 + 32 * ch + 4 * q;
+        const int n = n0 + 32 * ch + 4 * q;  // C32: the ch = 1 waves' n >= 32 >= cout (nothing to store)
         if (n >= cout) continue;
         const f32x4 v = *reinterpret_cast<const f32x4*>(&so[pix * 32 + 4 * q]);
         const int tl = POOL ? pix : pix >> 2, t = 16 * th + tl, tr = t >> 3, tc = t & 7;
@@ -978,6 +1055,15 @@ inline bool wino_enabled() {
     return on;
 }
 
+// VS_WINO_C32=0: cout <= 32 layers on the 64-channel variant (A/B measurements)
+bool wino_c32_on() {
+    static const bool on = [] {
+        const char* e = std::getenv("VS_WINO_C32");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+
 }  // namespace
 
 int wino3_launch(WinoArgs a, bool pool, bool fuse1a, hipStream_t s) {
@@ -990,6 +1076,8 @@ int wino3_launch(WinoArgs a, bool pool, bool fuse1a, hipStream_t s) {
         hipLaunchKernelGGL((k_wino3<true, false>), grid, dim3(256), 0, s, a);
     else if (fuse1a)
         return VS_ERR_ARG;
+    else if (a.cout <= 32 && wino_c32_on())
+        hipLaunchKernelGGL((k_wino3<false, false, true>), grid, dim3(256), 0, s, a);
     else
         hipLaunchKernelGGL((k_wino3<false, false>), grid, dim3(256), 0, s, a);
     VS_HIP(hipGetLastError());
