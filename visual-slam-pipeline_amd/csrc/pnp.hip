@@ -483,6 +483,7 @@ __global__ __launch_bounds__(256) void k_pnp_ransac(const float* __restrict__ ob
     crit_prio();
     __shared__ PnpShared S;
     __shared__ double s_lden[kPnpMaxIters];
+    __shared__ int s_cnt[kPnpMaxIters];  // the counts, staged for the serial replay (LDS, not L2, latency)
     const int pb = blockIdx.x, tid = threadIdx.x;
     const int o0 = off[pb], n = off[pb + 1] - o0;
     const float* obj = obj_all + 3 * (size_t)o0;
@@ -523,6 +524,7 @@ __global__ __launch_bounds__(256) void k_pnp_ransac(const float* __restrict__ ob
         // sequential accept / budget replay reads them
         for (int it = tid; it < niters0; it += blockDim.x) {
             const int c = count[it];
+            s_cnt[it] = c;
             s_lden[it] = c >= 0 ? ransac_log_denom((double)(n - c) / n, model_points) : 0.0;
         }
         __syncthreads();
@@ -530,7 +532,7 @@ __global__ __launch_bounds__(256) void k_pnp_ransac(const float* __restrict__ ob
             int niters = niters0, best = 0, best_iter = -1, it = 0;
             const double log_num = ransac_log_num(conf);
             for (; it < niters; it++) {
-                const int c = count[it];
+                const int c = s_cnt[it];
                 if (c < 0) continue;
                 if (c > (best > model_points - 1 ? best : model_points - 1)) {
                     best = c;
