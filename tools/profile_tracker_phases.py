@@ -42,7 +42,7 @@ def main():
     step(0)
     torch.cuda.synchronize()
     cyc = np.zeros(8, np.uint64)
-    pcyc = np.zeros(8, np.uint64)
+    pcyc = np.zeros(16, np.uint64)  # vs_debug_pnp_cycles copies 16 counters
     rcyc = np.zeros(8, np.uint64)
     lib.vs_debug_fm_cycles(cyc.ctypes.data, 1)
     lib.vs_debug_pnp_cycles(pcyc.ctypes.data, 1)
@@ -65,7 +65,9 @@ def main():
                           for k, n in enumerate(["load+control", "mtm", "jacobi", "sort", "variants", "count"])},
                       "pnp_ransac_kcycles_per_call": {
                           n: round(float(pcyc[k]) / max(1, prof.get("solve_pnp", (0, 1))[1]) / 1e3, 1)
-                          for k, n in ((6, "replay"), (7, "inliers+lm"))},
+                          for k, n in ((6, "replay"), (7, "lm tail"), (8, "inlier mask + lm rotations"), (9, "lm point terms"),
+                                       (10, "lm reduction"), (11, "lm control+solve"))},
+                      "pnp_lm_evaluations_per_call": round(float(pcyc[12]) / max(1, prof.get("solve_pnp", (0, 1))[1]), 2),
                       "ransac3d_kcycles_per_launch": {
                           n: round(float(rcyc[k]) / max(1, prof.get("ransac3d", (0, 1))[1]) / 1e3, 1)
                           for k, n in enumerate(["backproject", "mt_init", "twists", "sampling", "hypotheses",

@@ -30,7 +30,7 @@ constexpr int kPnpMaxIters = VS_PNP_MAX_ITERS;
 
 #ifdef VS_PNP_PROFILE
 // k_pnp_hyp phase cycle counters (profiling build only: make -C visual-slam-pipeline_amd prof)
-__device__ unsigned long long g_pnp_cycles[8];
+__device__ unsigned long long g_pnp_cycles[16];  // 0-5 k_pnp_hyp, 6-7 k_pnp_ransac, 8-12 its LM split
 #define PNP_T0() long long _pn_t = clock64()
 #define PNP_T(k)                                                             \
     do {                                                                     \
@@ -577,13 +577,16 @@ __global__ __launch_bounds__(256) void k_pnp_ransac(const float* __restrict__ ob
                 rod_v2m(r, S.rots.R[tid]);
             }
             __syncthreads();
+            PNP_T(8);  // rotations
             const LmRots& L = S.rots;
             double acc[kLmTerms], tot[kLmTerms];
             for (int k = 0; k < kLmTerms; k++) acc[k] = 0;
             for (int i = tid; i < n; i += blockDim.x)
                 if (mask[i])
                     lm_point(L, p + 3, K, obj[3 * i], obj[3 * i + 1], obj[3 * i + 2], img[2 * i], img[2 * i + 1], acc);
+            PNP_T(9);  // point terms (thread 0's share)
             block_sum_to0<kLmTerms>(acc, S.red, tot);  // tot valid on thread 0 (its only reader)
+            PNP_T(10);  // reduction
             if (tid == 0) {
                 if (first)
                     S.lm.init(p, tot);
@@ -592,10 +595,14 @@ __global__ __launch_bounds__(256) void k_pnp_ransac(const float* __restrict__ ob
                 S.go = S.lm.step();
             }
             __syncthreads();
+            PNP_T(11);  // LM control + solve
+#ifdef VS_PNP_PROFILE
+            if (tid == 0) atomicAdd(&g_pnp_cycles[12], 1ull);  // LM evaluations
+#endif
             if (!S.go) break;
             for (int k = 0; k < 6; k++) p[k] = S.lm.cand[k];
         }
-        PNP_T(7);
+        PNP_T(7);  // (after the LM loop: its last iteration's exit)
     }
     // outputs: Slam.cpp:519-526
     if (tid == 0) {
@@ -677,10 +684,10 @@ int solve_pnp(vs_ctx* ctx, int nprob, const float* d_obj, const float* d_img, co
 
 #ifdef VS_PNP_PROFILE
 extern "C" int vs_debug_pnp_cycles(unsigned long long* out, int reset) {
-    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(vs::g_pnp_cycles), sizeof(unsigned long long) * 8) != hipSuccess)
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(vs::g_pnp_cycles), sizeof(unsigned long long) * 16) != hipSuccess)
         return -1;
     if (reset) {
-        unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        unsigned long long z[16] = {};
         if (hipMemcpyToSymbol(HIP_SYMBOL(vs::g_pnp_cycles), z, sizeof(z)) != hipSuccess) return -1;
     }
     return 0;
