@@ -6,7 +6,7 @@ mkdir -p gpurun_out/$TAG
 export TMPDIR=/tmp
 O=gpurun_out/$TAG
 VARIANTS=${VARIANTS:-"nosplit|VS_MIDAS_SPLITK_WGS=0 default|VS_NONE=1"}
-timeout -k 10 600 python -u -m pytest tests/test_gpu_midas.py tests/test_gpu_monocular.py -m gpu -x -q \
+timeout -k 10 600 python -u -m pytest tests/test_gpu_midas.py tests/test_gpu_monocular.py tests/test_gpu_parity.py -m gpu -x -q \
     --timeout 300 --timeout-method thread -p no:cacheprovider > $O/pytest.log 2>&1
 rc=$?; echo "pytest rc=$rc"; tail -3 $O/pytest.log
 if [ $rc -ne 0 ]; then exit $rc; fi

@@ -948,6 +948,25 @@ static int splitk_of(const Step& st, int /*B*/) {
     return S > 1 ? (int)S : 1;
 }
 
+// Input-channel splits of a Winograd step (k_wino3 split-K): the 8^2 / 16^2 decoder convs (256-512
+// channels) are one workgroup per 8 x 16 tile block and 64 output channels — 256 workgroups walking
+// 64-128 channel chunks each, one wave per SIMD — so S raises the count toward 1024 with at least
+// 8 chunks per split, for steps of at most 256 workgroups (VS_MIDAS_WINO_SPLITK=0: never).  Sized
+// for a nominal 32-frame batch, as splitk_of.
+static int wino_splits_of(const Step& st) {
+    static const bool on = [] {
+        const char* e = std::getenv("VS_MIDAS_WINO_SPLITK");
+        return !(e && e[0] == '0');
+    }();
+    if (!on || st.Co % 4 != 0 || st.C % 4 != 0) return 1;
+    constexpr long B = 32;
+    const long nwg = B * ((st.W + 15) / 16) * ((st.H + 7) / 8) * ((st.Co + kCT - 1) / kCT);
+    if (nwg > 256) return 1;  // 512 workgroups (the 32^2 convs) measured slower split in two (r03am)
+    long S = (1024 + nwg - 1) / nwg;
+    S = std::min<long>(S, (st.C / 4) / 8);
+    return S > 1 ? (int)S : 1;
+}
+
 static int ensure_batch(vs_midas* m, int B) {
     if (B <= m->batch_cap) return VS_OK;
     for (size_t i = 0; i < m->slots.size(); i++) VS_CHECK(m->slots[i].ensure((size_t)B * m->slot_elems[i] * sizeof(float)));
@@ -955,7 +974,7 @@ static int ensure_batch(vs_midas* m, int B) {
     size_t part = 0;
     for (const Step& st : net().steps)
         if (st.kind == K_CONV) {
-            const int S = splitk_of(st, B);
+            const int S = std::max(splitk_of(st, B), st.k == 3 && st.stride == 1 ? wino_splits_of(st) : 1);
             if (S > 1) part = std::max(part, (size_t)S * B * st.Ho * st.Wo * st.Co);
         }
     if (part) VS_CHECK(m->splitk.ensure(part * sizeof(float)));
@@ -1020,7 +1039,18 @@ static int forward(vs_midas* m, int B, hipStream_t s, float** out) {
                 wa.res2 = a.res2;
                 wa.act = st.act;
                 wa.pre_relu = st.pre_relu ? 1 : 0;
+                const int S = wino_splits_of(st);
+                if (S > 1) {
+                    wa.part = m->splitk.as<float>();
+                    wa.splits = S;
+                }
                 VS_CHECK(wino3_launch(wa, false, false, s));
+                if (S > 1) {  // bias, activation and the residual adds on the summed partials
+                    a.part = m->splitk.as<float>();
+                    a.splits = S;
+                    const long n = (long)npix * (st.Co / 4);
+                    hipLaunchKernelGGL(k_mid_splitk, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, a);
+                }
             } else if (st.Co == 1 && st.k == 1 && st.stride == 1) {
                 VS_ARG(st.C % 4 == 0 && st.C <= kCo1MaxC, "midas: 1x1 single-channel conv needs C % 4 == 0, C <= 32");
                 hipLaunchKernelGGL(k_mid_conv_co1, dim3((npix + 255) / 256), dim3(256), 0, s, a);

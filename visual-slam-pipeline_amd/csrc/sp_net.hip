@@ -637,9 +637,13 @@ __global__ __launch_bounds__(256, CKT == 4 ? (MB == 1 ? 4 : 3) : 2) void k_conv3
 // transform elements instead of the 64 output channels (wave ch takes rows 2 ch, 2 ch + 1 of the 4 x 4
 // domain for channels 0..31), so no MFMA multiplies a zero weight column; the two partial output
 // transforms are added through LDS (Y = A^T (M_rows01 + M_rows23) A) before bias and activation.
-template <bool POOL, bool FUSE1A, bool C32 = false>
+// SPLIT: input-channel split-K (WinoArgs::part / splits, MiDaS's 8^2-16^2 decoder convs); a template
+// parameter so that the unsplit instantiations keep their code (runtime split support had cost them
+// 5-13 %, r03an).
+template <bool POOL, bool FUSE1A, bool C32 = false, bool SPLIT = false>
 __global__ __launch_bounds__(256, 2) void k_wino3(WinoArgs wa) {
     static_assert(!(C32 && (POOL || FUSE1A)), "C32 is the plain (MiDaS) variant");
+    static_assert(!(SPLIT && (POOL || FUSE1A)), "SPLIT is the plain (MiDaS) variant");
     const float* __restrict__ in = wa.in;
     const float* __restrict__ wu = wa.wu;
     const float* __restrict__ bias = wa.bias;
@@ -668,7 +672,11 @@ __global__ __launch_bounds__(256, 2) void k_wino3(WinoArgs wa) {
     const int n0 = nt * 64;
     const int b = blk / (nbx * nby), r0 = blk - b * (nbx * nby);
     const int y0 = (r0 / nbx) * 8, x0 = (r0 % nbx) * 16;
-    const int nchunk = cin / CK;
+    // split-K: this workgroup's input-channel chunks [cb, cb + nchunk)
+    const int split = SPLIT ? (int)blockIdx.y : 0, nsplit = SPLIT ? wa.splits : 1;
+    const int cb = SPLIT ? (int)((long)(cin / CK) * split / nsplit) : 0;
+    const int nchunk = SPLIT ? (int)((long)(cin / CK) * (split + 1) / nsplit) - cb : cin / CK;
+    constexpr bool raw = SPLIT;
 
     // raw patch pixel of this thread (tid < NP): patch (py, px) = input (y0 - 1 + py, x0 - 1 + px)
     const bool own_px = tid < NP;
@@ -701,7 +709,7 @@ __global__ __launch_bounds__(256, 2) void k_wino3(WinoArgs wa) {
     auto fetch_x = [&](auto sl_c, int c) {
         constexpr int sl = decltype(sl_c)::value;
         if constexpr (!FUSE1A) {
-            if (pin && c < nchunk) rx[sl] = *reinterpret_cast<const f32x4*>(src + c * CK);
+            if (pin && c < nchunk) rx[sl] = *reinterpret_cast<const f32x4*>(src + (cb + c) * CK);
         }
     };
     auto fetch_u = [&](int c) {
@@ -709,7 +717,7 @@ __global__ __launch_bounds__(256, 2) void k_wino3(WinoArgs wa) {
 #pragma unroll
         for (int j = 0; j < 4; j++) {
             const int idx = tid + 256 * j, xi = idx >> 6, cc = (idx >> 4) & 3, q = idx & 15;
-            ru[j] = *reinterpret_cast<const f32x4*>(wu + ((size_t)xi * cin + c * CK + cc) * cout_pad + n0 + 4 * q);
+            ru[j] = *reinterpret_cast<const f32x4*>(wu + ((size_t)xi * cin + (cb + c) * CK + cc) * cout_pad + n0 + 4 * q);
         }
     };
     // chunk c's patch -> s_x[c & 1] (fused: conv1a of its 4 channels at this pixel, 0 outside the image)
@@ -911,7 +919,7 @@ __global__ __launch_bounds__(256, 2) void k_wino3(WinoArgs wa) {
 #pragma unroll
     for (int nb = 0; nb < 2; nb++) {
         const int n = n0 + (C32 ? 0 : 32 * ch) + 16 * nb + li;
-        const float bv = n < cout ? bias[n] : 0.0f;
+        const float bv = (n < cout && !raw) ? bias[n] : 0.0f;
 #pragma unroll
         for (int r = 0; r < 4; r++) {
             const int tl = 4 * lk + r;  // tile within the wave's 16
@@ -935,8 +943,11 @@ __global__ __launch_bounds__(256, 2) void k_wino3(WinoArgs wa) {
             }
             const float y00 = s0[0] + s0[1] + s0[2], y01 = s0[1] - s0[2] - s0[3];
             const float y10 = s1[0] + s1[1] + s1[2], y11 = s1[1] - s1[2] - s1[3];
-            // act: 0 none, 1 ReLU, 2 ReLU6 (v > 0 ? min(v, 6) : 0, as midas.hip activate())
-            auto actf = [&](float v) { return act == 0 ? v : v > 0.0f ? (act == 2 && !(v < 6.0f) ? 6.0f : v) : 0.0f; };
+            // act: 0 none, 1 ReLU, 2 ReLU6 (v > 0 ? min(v, 6) : 0, as midas.hip activate()); raw
+            // split-K partials take neither bias nor activation
+            auto actf = [&](float v) {
+                return (act == 0 || raw) ? v : v > 0.0f ? (act == 2 && !(v < 6.0f) ? 6.0f : v) : 0.0f;
+            };
             if constexpr (POOL) {
                 so[tl * 32 + 16 * nb + li] = actf(fmaxf(fmaxf(y00, y01), fmaxf(y10, y11)) + bv);
             } else if constexpr (C32) {
@@ -972,6 +983,11 @@ __global__ __launch_bounds__(256, 2) void k_wino3(WinoArgs wa) {
         } else {
             const int oy = y0 + 2 * tr + ((pix >> 1) & 1), ox = x0 + 2 * tc + (pix & 1);
             if (oy >= H || ox >= W) continue;
+            if constexpr (raw) {
+                const size_t pp = (size_t)split * wa.B * H * W + ((size_t)b * H + oy) * W + ox;
+                *reinterpret_cast<f32x4*>(wa.part + pp * cout + n) = v;
+                continue;
+            }
             const size_t o = (((size_t)b * H + oy) * W + ox) * out_cstride + out_coff + n;
             f32x4 r = v;
             if (wa.res1) r = r + *reinterpret_cast<const f32x4*>(wa.res1 + o);
@@ -1069,15 +1085,21 @@ bool wino_c32_on() {
 int wino3_launch(WinoArgs a, bool pool, bool fuse1a, hipStream_t s) {
     a.nbx = (a.W + 15) / 16;
     a.nby = (a.H + 7) / 8;
-    dim3 grid((unsigned)((long)a.B * a.nbx * a.nby * (a.cout_pad / 64)));
+    if (a.splits < 1) a.splits = 1;
+    if (a.splits > 1 && (pool || fuse1a || !a.part || a.cout % 4 != 0 || a.splits > a.cin / 4)) return VS_ERR_ARG;
+    dim3 grid((unsigned)((long)a.B * a.nbx * a.nby * (a.cout_pad / 64)), (unsigned)a.splits);
     if (pool && fuse1a)
         hipLaunchKernelGGL((k_wino3<true, true>), grid, dim3(256), 0, s, a);
     else if (pool)
         hipLaunchKernelGGL((k_wino3<true, false>), grid, dim3(256), 0, s, a);
     else if (fuse1a)
         return VS_ERR_ARG;
+    else if (a.cout <= 32 && wino_c32_on() && a.splits > 1)
+        hipLaunchKernelGGL((k_wino3<false, false, true, true>), grid, dim3(256), 0, s, a);
     else if (a.cout <= 32 && wino_c32_on())
         hipLaunchKernelGGL((k_wino3<false, false, true>), grid, dim3(256), 0, s, a);
+    else if (a.splits > 1)
+        hipLaunchKernelGGL((k_wino3<false, false, false, true>), grid, dim3(256), 0, s, a);
     else
         hipLaunchKernelGGL((k_wino3<false, false>), grid, dim3(256), 0, s, a);
     VS_HIP(hipGetLastError());

@@ -168,6 +168,11 @@ struct WinoArgs {
     const float* res1;
     const float* res2;
     int act, pre_relu;
+    // split-K over the input channels (blockIdx.y = split, splits <= 1: none): the output-transformed
+    // partial sums (no bias, activation or residual) go to part [split][B*H*W][cout]; the caller
+    // finishes them (midas.hip k_mid_splitk).  Non-pool, non-fused only.
+    float* part;
+    int splits;
 };
 int wino3_launch(WinoArgs a, bool pool, bool fuse1a, hipStream_t s);
 // U[xi][ci][pos(co)] from direct-layout 3x3 weights w[(3a + b)][ci][co] (cout_pad columns; pos
