@@ -604,16 +604,18 @@ __global__ __launch_bounds__(256) void k_mid_dw(const float* __restrict__ in, co
 // kernel row's K weights and PX + K - 1 input pixels are loaded once for the PX outputs (the
 // per-output kernel above re-reads 2 K^2 float4 per output: L2-bandwidth-bound on the 16^2 / 8^2
 // layers).  Every output's taps are summed in the same (ky, kx) order as k_mid_dw.
-template <int K, int PX>
+// ST = 2: the stride-2 layers, PX outputs from 2 PX + K - 2 input pixels per kernel row.
+template <int K, int PX, int ST = 1>
 __global__ __launch_bounds__(256) void k_mid_dw_row(const float* __restrict__ in, const float* __restrict__ w,
                                                     const float* __restrict__ bias, float* __restrict__ out, int B,
-                                                    int H, int W, int C, int pad_t, int pad_l) {
-    const int C4 = C / 4, nxg = (W + PX - 1) / PX;
+                                                    int H, int W, int C, int Ho, int Wo, int pad_t, int pad_l) {
+    constexpr int NR = ST * (PX - 1) + K;  // input pixels per kernel row
+    const int C4 = C / 4, nxg = (Wo + PX - 1) / PX;
     const long idx = (long)blockIdx.x * 256 + threadIdx.x;
-    if (idx >= (long)B * H * nxg * C4) return;
+    if (idx >= (long)B * Ho * nxg * C4) return;
     const int c4 = (int)(idx % C4);
     const long g = idx / C4;
-    const int xg = (int)(g % nxg), oy = (int)((g / nxg) % H), b = (int)(g / ((long)nxg * H));
+    const int xg = (int)(g % nxg), oy = (int)((g / nxg) % Ho), b = (int)(g / ((long)nxg * Ho));
     const int x0 = xg * PX;
     const float4* in4 = reinterpret_cast<const float4*>(in);
     const float4* w4 = reinterpret_cast<const float4*>(w);
@@ -622,15 +624,15 @@ __global__ __launch_bounds__(256) void k_mid_dw_row(const float* __restrict__ in
 #pragma unroll
     for (int p = 0; p < PX; p++) acc[p] = bv;
     for (int ky = 0; ky < K; ky++) {
-        const int iy = oy - pad_t + ky;
+        const int iy = oy * ST - pad_t + ky;
         if (iy < 0 || iy >= H) continue;
-        float4 wr[K], row[PX + K - 1];
+        float4 wr[K], row[NR];
 #pragma unroll
         for (int kx = 0; kx < K; kx++) wr[kx] = w4[(size_t)(ky * K + kx) * C4 + c4];
         const size_t rbase = ((size_t)b * H + iy) * W;
 #pragma unroll
-        for (int j = 0; j < PX + K - 1; j++) {
-            const int ix = x0 - pad_l + j;
+        for (int j = 0; j < NR; j++) {
+            const int ix = x0 * ST - pad_l + j;
             row[j] = (ix >= 0 && ix < W) ? in4[(rbase + ix) * C4 + c4] : make_float4(0.f, 0.f, 0.f, 0.f);
         }
 #pragma unroll
@@ -638,18 +640,18 @@ __global__ __launch_bounds__(256) void k_mid_dw_row(const float* __restrict__ in
 #pragma unroll
             for (int kx = 0; kx < K; kx++) {
                 // taps outside the image are skipped (not added as zero), as in k_mid_dw
-                const int ix = x0 + p - pad_l + kx;
+                const int ix = (x0 + p) * ST - pad_l + kx;
                 if (ix < 0 || ix >= W) continue;
-                acc[p].x = fmaf(row[p + kx].x, wr[kx].x, acc[p].x);
-                acc[p].y = fmaf(row[p + kx].y, wr[kx].y, acc[p].y);
-                acc[p].z = fmaf(row[p + kx].z, wr[kx].z, acc[p].z);
-                acc[p].w = fmaf(row[p + kx].w, wr[kx].w, acc[p].w);
+                acc[p].x = fmaf(row[ST * p + kx].x, wr[kx].x, acc[p].x);
+                acc[p].y = fmaf(row[ST * p + kx].y, wr[kx].y, acc[p].y);
+                acc[p].z = fmaf(row[ST * p + kx].z, wr[kx].z, acc[p].z);
+                acc[p].w = fmaf(row[ST * p + kx].w, wr[kx].w, acc[p].w);
             }
     }
-    float4* o4 = reinterpret_cast<float4*>(out) + (((size_t)b * H + oy) * W) * C4 + c4;
+    float4* o4 = reinterpret_cast<float4*>(out) + (((size_t)b * Ho + oy) * Wo) * C4 + c4;
 #pragma unroll
     for (int p = 0; p < PX; p++) {
-        if (x0 + p >= W) continue;
+        if (x0 + p >= Wo) continue;
         float4 v = acc[p];
         v.x = activate(v.x, A_RELU6);
         v.y = activate(v.y, A_RELU6);
@@ -991,7 +993,7 @@ static bool wino_on() {
     return on;
 }
 
-// VS_MIDAS_DW_ROW=0: stride-1 depthwise layers on the per-output k_mid_dw (A/B measurements)
+// VS_MIDAS_DW_ROW=0: the depthwise layers on the per-output k_mid_dw (A/B measurements)
 static bool dw_row_on() {
     static const bool on = [] {
         const char* e = std::getenv("VS_MIDAS_DW_ROW");
@@ -1068,16 +1070,26 @@ static int forward(vs_midas* m, int B, hipStream_t s, float** out) {
                     hipLaunchKernelGGL(k_mid_splitk, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, a);
                 }
             }
-        } else if (st.kind == K_DW && st.stride == 1 && (st.k == 3 || st.k == 5) && dw_row_on()) {
+        } else if (st.kind == K_DW && (st.stride == 1 || st.stride == 2) && (st.k == 3 || st.k == 5) && dw_row_on()) {
             constexpr int PX = 8;
-            const long n = (long)B * st.H * ((st.W + PX - 1) / PX) * (st.C / 4);
+            const long n = (long)B * st.Ho * ((st.Wo + PX - 1) / PX) * (st.C / 4);
             const dim3 grid((unsigned)((n + 255) / 256));
-            if (st.k == 3)
-                hipLaunchKernelGGL((k_mid_dw_row<3, PX>), grid, dim3(256), 0, s, tensor_ptr(m, st.in), m->dev[st.layer].w,
-                                   m->dev[st.layer].b, tensor_ptr(m, st.out), B, st.H, st.W, st.C, st.pad_t, st.pad_l);
+            const float* din = tensor_ptr(m, st.in);
+            float* dout = tensor_ptr(m, st.out);
+            const float* dw = m->dev[st.layer].w;
+            const float* db = m->dev[st.layer].b;
+#define VS_DW_ROW(K_, S_)                                                                                          \
+    hipLaunchKernelGGL((k_mid_dw_row<K_, PX, S_>), grid, dim3(256), 0, s, din, dw, db, dout, B, st.H, st.W, st.C, st.Ho, \
+                       st.Wo, st.pad_t, st.pad_l)
+            if (st.k == 3 && st.stride == 1)
+                VS_DW_ROW(3, 1);
+            else if (st.k == 5 && st.stride == 1)
+                VS_DW_ROW(5, 1);
+            else if (st.k == 3)
+                VS_DW_ROW(3, 2);
             else
-                hipLaunchKernelGGL((k_mid_dw_row<5, PX>), grid, dim3(256), 0, s, tensor_ptr(m, st.in), m->dev[st.layer].w,
-                                   m->dev[st.layer].b, tensor_ptr(m, st.out), B, st.H, st.W, st.C, st.pad_t, st.pad_l);
+                VS_DW_ROW(5, 2);
+#undef VS_DW_ROW
         } else if (st.kind == K_DW) {
             const long n = (long)B * st.Ho * st.Wo * (st.C / 4);
             hipLaunchKernelGGL(k_mid_dw, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, tensor_ptr(m, st.in),
