@@ -84,6 +84,13 @@ int    vs_superpoint_get_weights(vs_ctx* ctx, float* out, size_t count);
  * weights vs_create(…, NULL, …) uses. */
 int    vs_superpoint_onnx_weights(const char* onnx_path, float* out, size_t count);
 int    vs_superpoint_synth_weights(float* out, size_t count);
+/* Host only: the ONNX export's "desc" output tail (FeatureExtractor.cpp:116-206 samples whatever the
+ * graph returns): *normalized = 1 when "desc" is convDb's output L2-normalised over channels, 0 when
+ * it is convDb's raw output.  Any other "desc" / "semi" tail (e.g. a softmax on "semi") is VS_ERR_IO,
+ * as vs_create reports it.  vs_desc_normalized: the same flag of a context (1 for the seeded / VSPW
+ * weights); with 0 the network's descriptor grid is not normalised before the keypoint sampling. */
+int    vs_superpoint_onnx_desc_normalized(const char* onnx_path, int* normalized);
+int    vs_desc_normalized(vs_ctx* ctx, int* normalized);
 int    vs_superpoint_save_weights(vs_ctx* ctx, const char* path);
 
 /* ---- A1-A6: FeatureExtractor::extract (FeatureExtractor.cpp:49-81, 87-207, 219-259) ---- */

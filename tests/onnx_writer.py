@@ -150,9 +150,23 @@ def split_superpoint(flat):
     return out
 
 
-def superpoint_model(flat, seed=0, heads_swapped=False, identity_alias=True, drop_pool=False, modes=None):
+DESC_TAILS = ("reducel2", "reducel2_unsqueeze", "reducel2_attr", "pow_sum_sqrt", "mul_self_sum_sqrt",
+              "normalize_clip", "reciprocal", "raw")
+
+
+def superpoint_model(flat, seed=0, heads_swapped=False, identity_alias=True, drop_pool=False, modes=None,
+                     desc_tail="reducel2", semi_tail="logits", pads=True):
     """SuperPointNet's export: conv1a..conv4b (ReLU, MaxPool after 1b/2b/3b), convPa -> relu ->
-    convPb = "semi", convDa -> relu -> convDb -> ReduceL2 / Div = "desc"."""
+    convPb = "semi", convDa -> relu -> convDb -> L2 normalisation over channels = "desc".
+
+    desc_tail: how "desc" leaves the graph — "reducel2" (ReduceL2 keepdims=1 with an axes input, then
+    Div), "reducel2_unsqueeze" (MagicLeap's torch.norm(dim=1) + unsqueeze: ReduceL2 keepdims=0 ->
+    Unsqueeze -> Div), "reducel2_attr" (opset < 18: axes as an attribute), "pow_sum_sqrt"
+    (Pow 2 -> ReduceSum -> Sqrt -> Div), "mul_self_sum_sqrt" (Mul(x, x) -> ReduceSum -> Sqrt -> Div),
+    "normalize_clip" (F.normalize: ReduceL2 -> Clip(min=eps) -> Expand -> Div), "reciprocal"
+    (x * Reciprocal(ReduceL2(x))), "raw" (convDb's output itself), or the invalid "reduce_all" (a
+    ReduceL2 over every axis).  semi_tail: "logits" (convPb's output) or the invalid "softmax".
+    pads=False drops the pads attribute of the 3x3 convs (ONNX's default: no padding)."""
     rng = np.random.default_rng(seed)
     G = _Graph(rng)
     L = split_superpoint(np.asarray(flat, np.float32))
@@ -165,8 +179,8 @@ def superpoint_model(flat, seed=0, heads_swapped=False, identity_alias=True, dro
         if identity_alias and i == 3:  # exports sometimes route a weight through an Identity
             wn = G.op("Identity", [wn])
         x = G.op("Conv", [x, wn, G.const(b, mode(i))],
-                 [attr_ints("dilations", [1, 1]), attr_int("group", 1), attr_ints("kernel_shape", [3, 3]),
-                  attr_ints("pads", [1, 1, 1, 1]), attr_ints("strides", [1, 1])])
+                 [attr_ints("dilations", [1, 1]), attr_int("group", 1), attr_ints("kernel_shape", [3, 3])] +
+                 ([attr_ints("pads", [1, 1, 1, 1])] if pads else []) + [attr_ints("strides", [1, 1])])
         x = G.op("Relu", [x])
         if i in (1, 3, 5) and not (drop_pool and i == 3):
             x = G.op("MaxPool", [x], [attr_ints("kernel_shape", [2, 2]), attr_ints("pads", [0, 0, 0, 0]),
@@ -175,14 +189,44 @@ def superpoint_model(flat, seed=0, heads_swapped=False, identity_alias=True, dro
 
     def det():
         h = G.op("Relu", [_conv(G, trunk, *L[8], mode=mode(8))])
+        if semi_tail == "softmax":
+            s_ = _conv(G, h, *L[9], mode=mode(9))
+            return G.op("Softmax", [s_], [attr_int("axis", 1)], out="semi")
         return _conv(G, h, *L[9], mode=mode(9), out="semi")
+
+    def int_const(vals):
+        return G.op("Constant", [], [attr_tensor("value", _ld(1, _varint(len(vals))) + _i(2, 7) + _s(8, "c") +
+                                                  _ld(9, np.array(vals, "<i8").tobytes()))])
+
+    def f_const(v):
+        return G.const(np.array(v, np.float32))
 
     def des():
         h = G.op("Relu", [_conv(G, trunk, *L[10], mode=mode(10))])
+        if desc_tail == "raw":
+            return _conv(G, h, *L[11], mode=mode(11), out="desc")
         d = _conv(G, h, *L[11], mode=mode(11))
-        axes = G.op("Constant", [], [attr_tensor("value", _ld(1, _varint(1)) + _i(2, 7) + _s(8, "axes") +
-                                                  _ld(9, np.array([1], "<i8").tobytes()))])
-        n = G.op("ReduceL2", [d, axes], [attr_int("keepdims", 1)])
+        if desc_tail == "reducel2":
+            n = G.op("ReduceL2", [d, int_const([1])], [attr_int("keepdims", 1)])
+        elif desc_tail == "reduce_all":
+            n = G.op("ReduceL2", [d], [attr_int("keepdims", 1)])
+        elif desc_tail == "reducel2_attr":
+            n = G.op("ReduceL2", [d], [attr_ints("axes", [1]), attr_int("keepdims", 1)])
+        elif desc_tail == "reducel2_unsqueeze":
+            n = G.op("ReduceL2", [d], [attr_ints("axes", [1]), attr_int("keepdims", 0)])
+            n = G.op("Unsqueeze", [n, int_const([1])])
+        elif desc_tail in ("pow_sum_sqrt", "mul_self_sum_sqrt"):
+            sq = G.op("Pow", [d, f_const(2.0)]) if desc_tail == "pow_sum_sqrt" else G.op("Mul", [d, d])
+            n = G.op("Sqrt", [G.op("ReduceSum", [sq, int_const([1])], [attr_int("keepdims", 1)])])
+        elif desc_tail == "normalize_clip":
+            n = G.op("ReduceL2", [d, int_const([1])], [attr_int("keepdims", 1)])
+            n = G.op("Clip", [n, f_const(1e-12), ""])
+            n = G.op("Expand", [n, int_const([1, 256, 1, 1])])
+        elif desc_tail == "reciprocal":
+            n = G.op("ReduceL2", [d, int_const([-3])], [attr_int("keepdims", 1)])
+            return G.op("Mul", [d, G.op("Reciprocal", [n])], out="desc")
+        else:
+            raise ValueError(desc_tail)
         return G.op("Div", [d, n], out="desc")
 
     if heads_swapped:
@@ -206,12 +250,14 @@ def _same(i, k, s):
     return total // 2, total - total // 2
 
 
-def midas_model(flat, seed=0, bn_every=2, bn_random=None):
+def midas_model(flat, seed=0, bn_every=2, bn_random=None, swap_fusion3=False, drop_stem_pad=False):
     """MidasNet_small's export, weights taken from the canonical flat array in order.  Every
     bn_every-th encoder conv is written as Conv (no bias) + BatchNormalization: gamma 1, beta = the
     canonical bias, mean 0, var 1 - eps, epsilon 2^-10, so folding it reproduces the canonical
     weights exactly; bn_random (a dict, filled) instead draws random BN statistics and records the
-    folded weights the reader must produce."""
+    folded weights the reader must produce.  swap_fusion3 feeds refinenet3's inputs the other way
+    round (same shapes, other wiring) and drop_stem_pad folds the stem's TF "same" Pad into nothing:
+    both are graphs the reader must reject."""
     rng = np.random.default_rng(seed)
     G = _Graph(rng)
     flat = np.asarray(flat, np.float32)
@@ -227,7 +273,9 @@ def midas_model(flat, seed=0, bn_every=2, bn_random=None):
         cin = group if group > 1 else cur_c[x]
         w = take(cout * (1 if group > 1 else cin) * k * k, (cout, 1 if group > 1 else cin, k, k))
         b = take(cout, (cout,))
-        if tf_same:
+        if tf_same and drop_stem_pad and x == "input":
+            pad = 0
+        elif tf_same:
             H = hw[x]
             pt, pb = _same(H, k, stride)
             pads = G.const(np.array([0, 0, pt, pt, 0, 0, pb, pb], np.float32))
@@ -323,7 +371,7 @@ def midas_model(flat, seed=0, bn_every=2, bn_random=None):
         return conv(o, out_ch, 1)
 
     p4 = fusion(rn[3], None, 256)
-    p3 = fusion(p4, rn[2], 128)
+    p3 = fusion(rn[2], p4, 128) if swap_fusion3 else fusion(p4, rn[2], 128)
     p2 = fusion(p3, rn[1], 64)
     p1 = fusion(p2, rn[0], 64)
     o = conv(p1, 32, 3)

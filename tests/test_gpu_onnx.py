@@ -48,3 +48,35 @@ def test_vs_midas_create_loads_midas_onnx(tmp_path, vsctx):
     assert np.array_equal(outs[0][0].view(np.uint32), outs[1][0].view(np.uint32))
     assert np.array_equal(outs[0][1].view(np.uint32), outs[1][1].view(np.uint32))
     assert np.ptp(outs[0][1]) > 0
+
+
+@pytest.mark.parametrize("tail", ["raw", "reducel2_unsqueeze"])
+def test_desc_tail_follows_the_model_file(tmp_path, vsctx, seq4, tail):
+    """the reference samples the "desc" tensor the graph returns and normalises each
+    keypoint's descriptor after the bilinear sampling (FeatureExtractor.cpp:167-206).  A raw-"desc"
+    export must therefore skip the grid normalisation; keypoints and descriptors equal the oracle's
+    post-processing of the same network tensors bit for bit."""
+    import sys
+    import os
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(__file__)), "oracle"))
+    import oracle_py as oracle
+    p = tmp_path / f"sp_{tail}.onnx"
+    p.write_bytes(onnx_writer.superpoint_model(vslam_abi.superpoint_synth_weights(), desc_tail=tail, seed=4))
+    with vslam_abi.Context(0, str(p)) as c:
+        assert c.desc_normalized() == (tail != "raw")
+        gray = oracle.gray_to_f32(oracle.bgr_to_gray(seq4[0]["bgr"]))
+        semi, dgrid = c.superpoint_forward(gray)
+        semi_n, dgrid_n = vsctx.superpoint_forward(gray)
+        assert np.array_equal(semi.view(np.uint32), semi_n.view(np.uint32))
+        norms = np.linalg.norm(dgrid.astype(np.float64), axis=0)  # NCHW: channels first
+        if tail == "raw":
+            assert np.abs(norms - 1).min() > 1e-2  # seeded weights: not unit length
+            ref = dgrid / np.maximum(np.linalg.norm(dgrid, axis=0, keepdims=True), 1e-12)
+            assert np.allclose(ref, dgrid_n, atol=1e-6)
+        else:
+            assert np.array_equal(dgrid.view(np.uint32), dgrid_n.view(np.uint32))
+        ko, do = oracle.postprocess(semi, dgrid, order_mode=1)
+        (kg, dg), = c.extract_batch([seq4[0]["bgr"]])
+        assert len(kg) == len(ko) > 0
+        assert np.array_equal(kg.view(np.uint8), ko.view(np.uint8))
+        assert np.array_equal(dg.view(np.uint32), do.view(np.uint32))

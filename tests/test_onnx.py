@@ -96,3 +96,77 @@ def test_midas_onnx_rejects_wrong_network(tmp_path, sp_weights):
     p.write_bytes(onnx_writer.superpoint_model(sp_weights))
     with pytest.raises(vslam_abi.VSError, match="MiDaS graph"):
         vslam_abi.midas_onnx_weights(str(p))
+
+
+# ---- output tails: the reference samples whatever "desc" the graph returns -----
+@pytest.mark.parametrize("tail", [t for t in onnx_writer.DESC_TAILS])
+def test_superpoint_onnx_desc_tail_is_classified(tmp_path, sp_weights, tail):
+    p = tmp_path / f"sp_{tail}.onnx"
+    p.write_bytes(onnx_writer.superpoint_model(sp_weights, desc_tail=tail, seed=2))
+    assert vslam_abi.superpoint_onnx_desc_normalized(str(p)) == (tail != "raw")
+    got = vslam_abi.superpoint_onnx_weights(str(p))
+    assert np.array_equal(got.view(np.uint32), sp_weights.view(np.uint32))
+
+
+@pytest.mark.parametrize("kw,msg", [(dict(semi_tail="softmax"), "raw logits"),
+                                    (dict(desc_tail="reduce_all"), "L2 normalisation over channels"),
+                                    (dict(pads=False), "explicit pads")])
+def test_superpoint_onnx_rejects_other_tails_and_default_padding(tmp_path, sp_weights, kw, msg):
+    p = tmp_path / "bad.onnx"
+    p.write_bytes(onnx_writer.superpoint_model(sp_weights, **kw))
+    with pytest.raises(vslam_abi.VSError, match=msg):
+        vslam_abi.superpoint_onnx_weights(str(p))
+    with pytest.raises(vslam_abi.VSError, match="IO"):
+        vslam_abi.superpoint_onnx_desc_normalized(str(p))
+
+
+def test_midas_onnx_rejects_rewired_and_unpadded_graphs(tmp_path, midas_w):
+    p = tmp_path / "midas_swapped.onnx"
+    p.write_bytes(onnx_writer.midas_model(midas_w, swap_fusion3=True))
+    with pytest.raises(vslam_abi.VSError, match="wired"):
+        vslam_abi.midas_onnx_weights(str(p))
+    q = tmp_path / "midas_nopad.onnx"
+    q.write_bytes(onnx_writer.midas_model(midas_w, drop_stem_pad=True))
+    with pytest.raises(vslam_abi.VSError, match="Pad"):
+        vslam_abi.midas_onnx_weights(str(q))
+
+
+# ---- hostile files: errors, never a crash or an exception through the C ABI ------
+def _model_with_tensor(dims, payload=b"", dtype=1, extra_nodes=()):
+    w = onnx_writer
+    t = w._ld(1, b"".join(w._varint(d) for d in dims)) + w._i(2, dtype) + w._s(8, "W") + w._ld(9, payload)
+    conv = w.node("Conv", ["image", "W"], ["semi"], attrs=[w.attr_ints("kernel_shape", [3, 3])])
+    return w.model([conv] + list(extra_nodes), [t], ["image"], ["semi"])
+
+
+@pytest.mark.parametrize("dims", [[1 << 40, 1 << 30], [-5, 3], [1 << 62, 4, 4, 4], [64, 1, 3, 3]])
+def test_onnx_reader_survives_hostile_tensor_dims(tmp_path, dims):
+    p = tmp_path / "hostile.onnx"
+    p.write_bytes(_model_with_tensor(dims, payload=b"\0" * 16))
+    with pytest.raises(vslam_abi.VSError, match="IO"):
+        vslam_abi.superpoint_onnx_weights(str(p))
+
+
+def test_onnx_reader_survives_input_less_nodes(tmp_path):
+    w = onnx_writer
+    # a Conv whose weight comes from an input-less Identity, and a Relu with no inputs feeding it
+    nodes = [w.node("Identity", [], ["Wi"]), w.node("Relu", [], ["x"]),
+             w.node("Conv", ["x", "Wi"], ["semi"], attrs=[w.attr_ints("kernel_shape", [3, 3])])]
+    p = tmp_path / "inputless.onnx"
+    p.write_bytes(w.model(nodes, [], ["image"], ["semi"]))
+    with pytest.raises(vslam_abi.VSError, match="IO"):
+        vslam_abi.superpoint_onnx_weights(str(p))
+    with pytest.raises(vslam_abi.VSError, match="IO"):
+        vslam_abi.midas_onnx_weights(str(p))
+
+
+def test_onnx_reader_rejects_auto_pad(tmp_path):
+    w = onnx_writer
+    # an auto_pad=SAME_UPPER Conv appended to an otherwise valid graph
+    t = w.tensor("Wx", np.zeros((1, 1, 3, 3), np.float32))
+    conv = w.node("Conv", ["image", "Wx"], ["extra"], attrs=[w.attr_ints("kernel_shape", [3, 3]),
+                                                              w._s(1, "auto_pad") + w._i(20, 3) + w._s(4, "SAME_UPPER")])
+    p = tmp_path / "autopad.onnx"
+    p.write_bytes(w.model([conv], [t], ["image"], ["extra"]))
+    with pytest.raises(vslam_abi.VSError, match="auto_pad"):
+        vslam_abi.superpoint_onnx_weights(str(p))

@@ -311,9 +311,10 @@ int vs_batch_set_gather(vs_batch* b, int on) {
         return VS_OK;
     }
     const size_t n = (size_t)b->world * b->B;
-    b->g_kps = alloc<vs_keypoint>(b->owned, n * b->cap);
-    b->g_desc = alloc<float>(b->owned, n * b->cap * 256);
-    b->g_n = alloc<int>(b->owned, n);
+    // allocated on the first switch-on only; later off -> on toggles reuse the buffers
+    if (!b->g_kps) b->g_kps = alloc<vs_keypoint>(b->owned, n * b->cap);
+    if (!b->g_desc) b->g_desc = alloc<float>(b->owned, n * b->cap * 256);
+    if (!b->g_n) b->g_n = alloc<int>(b->owned, n);
     if (!b->g_kps || !b->g_desc || !b->g_n) {
         vs::set_error("vs_batch_set_gather: device allocation failed");
         return VS_ERR_NOMEM;

@@ -36,6 +36,9 @@
 #include "vs_internal.h"
 #include "../host/onnx_weights.h"
 
+#include <functional>
+#include <set>
+
 namespace vs {
 namespace midas {
 
@@ -58,6 +61,7 @@ struct Step {
     int k = 1, stride = 1, pad_t = 0, pad_l = 0;
     int act = A_NONE;
     bool pre_relu = false, align_corners = false;
+    bool tf_same = false;  // TF "same" padding (an explicit Pad node in the ONNX export)
 };
 
 // The network as data: layer definitions (canonical weight order) and the step program over
@@ -91,6 +95,7 @@ struct Net {
         st.H = Hof(in), st.W = Wof(in), st.C = Cof(in);
         st.k = k, st.stride = stride;
         st.Ho = (st.H + stride - 1) / stride, st.Wo = (st.W + stride - 1) / stride, st.Co = cout;
+        st.tf_same = tf_same;
         st.pad_t = tf_same ? same_begin(st.H, k, stride) : k / 2;
         st.pad_l = tf_same ? same_begin(st.W, k, stride) : k / 2;
         st.act = act, st.res1 = res1, st.res2 = res2, st.pre_relu = pre_relu;
@@ -107,6 +112,7 @@ struct Net {
         st.H = Hof(in), st.W = Wof(in), st.C = st.Co = Cof(in);
         st.k = k, st.stride = stride;
         st.Ho = (st.H + stride - 1) / stride, st.Wo = (st.W + stride - 1) / stride;
+        st.tf_same = true;
         st.pad_t = same_begin(st.H, k, stride);
         st.pad_l = same_begin(st.W, k, stride);
         st.act = A_RELU6;
@@ -787,12 +793,32 @@ std::vector<float> synth(uint64_t seed) {
 bool from_onnx(const char* path, std::vector<float>& w, std::string& err) {
     const Net& N = net();
     std::vector<vs_onnx::LayerSpec> spec(N.layers.size());
-    std::vector<int> stride(N.layers.size(), 1);
-    for (const Step& st : N.steps)
-        if (st.layer >= 0) stride[st.layer] = st.stride;
-    for (size_t l = 0; l < N.layers.size(); l++) {
-        const LayerDef& L = N.layers[l];
-        spec[l] = {L.kind == K_DW, L.cin, L.cout, L.k, stride[l], L.bias};
+    // structural input of every layer: the layers whose outputs reach its data input through the
+    // step program (residual adds and upsampling included), -1 for the network input
+    std::vector<int> producer(N.tdims.size() / 3, -2);  // tensor -> producing step
+    for (size_t i = 0; i < N.steps.size(); i++) producer[N.steps[i].out] = (int)i;
+    std::function<void(int, std::set<int>&)> sources = [&](int t, std::set<int>& acc) {
+        if (t == N.input) {
+            acc.insert(-1);
+            return;
+        }
+        const Step& st = N.steps[producer[t]];
+        if (st.layer >= 0) {
+            acc.insert(st.layer);
+            if (st.res1 >= 0) sources(st.res1, acc);
+            if (st.res2 >= 0) sources(st.res2, acc);
+        } else {
+            sources(st.in, acc);  // upsampling
+        }
+    };
+    for (const Step& st : N.steps) {
+        if (st.layer < 0) continue;
+        const LayerDef& L = N.layers[st.layer];
+        vs_onnx::LayerSpec& sp = spec[st.layer];
+        sp.depthwise = L.kind == K_DW;
+        sp.cin = L.cin, sp.cout = L.cout, sp.k = L.k, sp.stride = st.stride, sp.bias = L.bias;
+        sp.tf_same = st.tf_same;
+        sources(st.in, sp.from);
     }
     vs_onnx::Model model;
     if (!vs_onnx::load(path, model, err)) return false;

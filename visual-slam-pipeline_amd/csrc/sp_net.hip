@@ -1237,6 +1237,7 @@ int conv3(vs_ctx* ctx, const DevLayer& L, const float* in, int in_cstride, int i
 int sp_forward(vs_ctx* ctx, int B, const uint8_t* d_img, int channels, int h, int w, hipStream_t s, float* semi_out,
                float* dgrid_out) {
     VS_CHECK(scratch_order(ctx, s));
+    ScratchUse scratch_use(ctx, s);
     const int Hp = ((h + 7) / 8) * 8, Wp = ((w + 7) / 8) * 8;
     const int hc = Hp / 8, wc = Wp / 8;
     const size_t full = (size_t)B * Hp * Wp;
@@ -1316,7 +1317,7 @@ int sp_forward(vs_ctx* ctx, int B, const uint8_t* d_img, int channels, int h, in
             VS_CHECK((launch_conv<1, false, 11>(L[11], a0, 512, 256, dgrid_out, kDescDim, 0, B, H, W, 0, s)));
         }
     }
-    {
+    if (ctx->desc_l2) {  // the model's "desc" output is normalised (a raw-"desc" ONNX export skips it)
         ProfScope ps(ctx, "desc_l2norm", s);
         long npix = (long)B * H * W;
         hipLaunchKernelGGL(k_desc_l2norm, dim3((unsigned)((npix + 3) / 4)), dim3(256), 0, s, dgrid_out,

@@ -681,6 +681,7 @@ __global__ __launch_bounds__(256) void k_sample(const float* __restrict__ dgrid,
 int sp_postprocess(vs_ctx* ctx, int B, int hc, int wc, int h, int w, vs_keypoint* d_kps, float* d_desc,
                    int* d_n, int cap, hipStream_t s, const float* semi, const float* dgrid) {
     VS_CHECK(scratch_order(ctx, s));
+    ScratchUse scratch_use(ctx, s);
     if (!semi) semi = ctx->semi.as<float>();
     if (!dgrid) dgrid = ctx->dgrid.as<float>();
     const int Hp = hc * 8, Wp = wc * 8;

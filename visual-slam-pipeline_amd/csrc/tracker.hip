@@ -757,8 +757,10 @@ struct GpuOps {
         char* hk = X.pin.base;
         int* hn = reinterpret_cast<int*>(hk + (size_t)nb * kCap * sizeof(vs_keypoint));
         const int hc = (h + 7) / 8, wc = (w + 7) / 8;
-        // the region's previous batch has finished reading its network outputs
+        // the region's previous batch has finished reading its network outputs, and work the caller
+        // enqueued on other streams over the context's shared scratch has finished with it
         VS_HIP(hipStreamWaitEvent(xs, region_done[X.region], 0));
+        VS_CHECK(scratch_acquire_owner(ctx, xs));
         const size_t semi_f = (size_t)hc * wc * VS_SEMI_CH, dgrid_f = (size_t)hc * wc * VS_DESC_DIM;
         for (int c = 0; c < nch; c++) {
             const int f0 = X.ch[c], m = X.ch[c + 1] - X.ch[c];
@@ -1463,6 +1465,7 @@ struct GpuOps {
         const int ncell = ((vs_trk::cfg::IMAGE_WIDTH + kVisCell - 1) / kVisCell) *
                           ((vs_trk::cfg::IMAGE_HEIGHT + kVisCell - 1) / kVisCell);
         if (ncell > kVisMaxCells || (int)f.kps.size() > kCap) {
+            vs::set_error("vs_slam: visibility: keypoint count or grid size out of range");
             failed(VS_ERR_ARG);
             return;
         }

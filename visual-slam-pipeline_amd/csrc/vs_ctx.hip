@@ -218,6 +218,24 @@ int scratch_order(vs_ctx* ctx, hipStream_t s) {
     return VS_OK;
 }
 
+void scratch_release(vs_ctx* ctx, hipStream_t s) {
+    if (!ctx->scratch_busy || s == ctx->scratch_owner[0] || s == ctx->scratch_owner[1]) return;
+    if (!ctx->scratch_foreign && hipEventCreateWithFlags(&ctx->scratch_foreign, hipEventDisableTiming) != hipSuccess) {
+        ctx->scratch_foreign = nullptr;
+        (void)hipStreamSynchronize(s);  // no event: order by completing the work now
+        return;
+    }
+    if (hipEventRecord(ctx->scratch_foreign, s) == hipSuccess) ctx->scratch_foreign_pending = true;
+    else (void)hipStreamSynchronize(s);
+}
+
+int scratch_acquire_owner(vs_ctx* ctx, hipStream_t s) {
+    if (!ctx->scratch_foreign_pending) return VS_OK;
+    VS_HIP(hipStreamWaitEvent(s, ctx->scratch_foreign, 0));
+    ctx->scratch_foreign_pending = false;
+    return VS_OK;
+}
+
 static hipStream_t pick(vs_ctx* ctx, void* stream) { return stream ? (hipStream_t)stream : ctx->stream; }
 
 template <class T>
@@ -270,6 +288,26 @@ int vs_superpoint_onnx_weights(const char* path, float* out, size_t count) {
     return VS_OK;
 }
 
+int vs_superpoint_onnx_desc_normalized(const char* path, int* normalized) {
+    VS_ARG(path && normalized, "vs_superpoint_onnx_desc_normalized: bad arguments");
+    std::string err;
+    vs_onnx::Model model;
+    std::vector<float> w;
+    bool nd = true;
+    if (!vs_onnx::load(path, model, err) || !vs_onnx::superpoint_weights(model, w, err, &nd)) {
+        set_error("vs_superpoint_onnx_desc_normalized: " + err);
+        return VS_ERR_IO;
+    }
+    *normalized = nd ? 1 : 0;
+    return VS_OK;
+}
+
+int vs_desc_normalized(vs_ctx* ctx, int* normalized) {
+    VS_ARG(ctx && normalized, "vs_desc_normalized: bad arguments");
+    *normalized = ctx->desc_l2 ? 1 : 0;
+    return VS_OK;
+}
+
 int vs_superpoint_synth_weights(float* out, size_t count) {
     VS_ARG(out && count == num_params(), "vs_superpoint_synth_weights: bad arguments");
     const std::vector<float> w = synth_weights(VS_SYNTH_WEIGHT_SEED);
@@ -290,7 +328,8 @@ int vs_create(int device, const char* weights_path, vs_ctx** out) {
         // the reference's own model file (FeatureExtractor.cpp:22-44: models/superpoint_v1.onnx)
         std::string err;
         vs_onnx::Model model;
-        if (!vs_onnx::load(weights_path, model, err) || !vs_onnx::superpoint_weights(model, ctx->h_weights, err) ||
+        if (!vs_onnx::load(weights_path, model, err) ||
+            !vs_onnx::superpoint_weights(model, ctx->h_weights, err, &ctx->desc_l2) ||
             ctx->h_weights.size() != num_params()) {
             delete ctx;
             set_error("vs_create: " + (err.empty() ? std::string("SuperPoint parameter count mismatch") : err));
@@ -350,6 +389,7 @@ void vs_destroy(vs_ctx* ctx) {
     if (ctx->head_a.w) (void)hipFree(ctx->head_a.w);
     if (ctx->head_a.b) (void)hipFree(ctx->head_a.b);
     if (ctx->head_a.wu) (void)hipFree(ctx->head_a.wu);
+    if (ctx->scratch_foreign) (void)hipEventDestroy(ctx->scratch_foreign);
     DevBuf* bufs[] = {&ctx->gray,  &ctx->act0,   &ctx->act1,   &ctx->semi,   &ctx->dgrid,  &ctx->heat,
                       &ctx->state, &ctx->flags,  &ctx->keys,   &ctx->keycnt, &ctx->h_img,  &ctx->h_kps,
                       &ctx->h_desc, &ctx->h_n,   &ctx->h_aux0, &ctx->h_aux1, &ctx->h_aux2, &ctx->h_aux3,

@@ -99,6 +99,10 @@ struct vs_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
     std::vector<float> h_weights;  // canonical blob
+    // the model's "desc" output is L2-normalised over channels (true for the seeded / VSPW weights and
+    // MagicLeap-style exports; an ONNX file whose "desc" is convDb's raw output sets it false, and the
+    // descriptor grid is then sampled raw as FeatureExtractor.cpp:167-206 would)
+    bool desc_l2 = true;
     vs::DevLayer layers[12];
     // convPa|convDa fused into one 128->512 conv (they share conv4b's output).
     vs::DevLayer head_a;
@@ -122,6 +126,10 @@ struct vs_ctx {
     // scratch first waits for scratch_busy (the last extraction it enqueued); null without a vs_slam.
     hipEvent_t scratch_busy = nullptr;
     hipStream_t scratch_owner[2] = {nullptr, nullptr};
+    // ... and the other direction: such work records scratch_foreign when its launches are enqueued,
+    // and the vs_slam's next extraction waits for it before it writes the scratch.
+    hipEvent_t scratch_foreign = nullptr;
+    bool scratch_foreign_pending = false;
 };
 
 namespace vs {
@@ -139,6 +147,16 @@ struct ProfScope {
 // Orders work on stream s that uses the context's network / NMS scratch after a vs_slam's
 // in-flight extraction (no-op on the vs_slam's own extraction streams and without one).
 int scratch_order(vs_ctx* ctx, hipStream_t s);
+// Marks the end of a non-owner stream's use of the shared scratch (see vs_ctx::scratch_foreign).
+void scratch_release(vs_ctx* ctx, hipStream_t s);
+// The owner side: the vs_slam's extraction stream `s` waits for the last foreign use, if any.
+int scratch_acquire_owner(vs_ctx* ctx, hipStream_t s);
+struct ScratchUse {  // scratch_order at construction, scratch_release at scope exit
+    vs_ctx* ctx;
+    hipStream_t s;
+    ScratchUse(vs_ctx* c, hipStream_t st) : ctx(c), s(st) {}
+    ~ScratchUse() { scratch_release(ctx, s); }
+};
 
 // ---- stage launchers (return VS_OK or an error code; enqueue on `s` only) ------------------
 // Network: d_bgr is B x h x w x 3 u8 (or gray u8 when channels == 1, or nullptr when d_gray01

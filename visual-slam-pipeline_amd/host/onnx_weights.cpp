@@ -13,13 +13,19 @@
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <exception>
 #include <map>
 #include <memory>
 
 namespace vs_onnx {
 namespace {
 
-enum DataType { DT_FLOAT = 1, DT_FLOAT16 = 10, DT_DOUBLE = 11, DT_BFLOAT16 = 16 };
+enum DataType { DT_FLOAT = 1, DT_INT32 = 6, DT_INT64 = 7, DT_FLOAT16 = 10, DT_DOUBLE = 11, DT_BFLOAT16 = 16 };
+
+// Largest tensor the reader materialises (elements).  The biggest weight of the two networks is
+// MiDaS's 512 x 384 x 3 x 3 rn projection (1.8 M); 2^28 leaves room for any export of them and keeps
+// a hostile dims field from turning into a multi-GB allocation.
+constexpr uint64_t kMaxElements = 1ull << 28;
 
 struct Span {
     const uint8_t* p = nullptr;
@@ -107,11 +113,17 @@ struct Tensor {
     std::vector<int64_t> dims;
     int dtype = 0;
     std::vector<float> data;
+    std::vector<int64_t> ints;  // INT32 / INT64 tensors (axes, shapes, pads)
     bool external = false;
-    size_t count() const {
-        size_t n = 1;
-        for (int64_t d : dims) n *= (size_t)std::max<int64_t>(d, 0);
-        return n;
+    // element count, or false when a dimension is negative or the product exceeds kMaxElements
+    bool count(uint64_t& n) const {
+        n = 1;
+        for (int64_t d : dims) {
+            if (d < 0) return false;
+            if (d != 0 && n > kMaxElements / (uint64_t)d) return false;
+            n *= (uint64_t)d;
+        }
+        return n <= kMaxElements;
     }
 };
 
@@ -145,7 +157,7 @@ bool parse_tensor(Span s, Tensor& t, std::string& name, std::string& err) {
     bool has_raw = false;
     std::vector<float> fdata;
     std::vector<double> ddata;
-    std::vector<int64_t> idata;
+    std::vector<int64_t> idata, i64data;
     while (m.next(f, wt, num, b)) {
         switch (f) {
             case 1:
@@ -169,6 +181,9 @@ bool parse_tensor(Span s, Tensor& t, std::string& name, std::string& err) {
                 break;
             case 5:  // int32_data (FLOAT16 / BFLOAT16 payloads)
                 if (!rep_varint(wt, num, b, idata)) return err = "bad TensorProto.int32_data", false;
+                break;
+            case 7:  // int64_data
+                if (!rep_varint(wt, num, b, i64data)) return err = "bad TensorProto.int64_data", false;
                 break;
             case 8:
                 name = str(b);
@@ -200,9 +215,10 @@ bool parse_tensor(Span s, Tensor& t, std::string& name, std::string& err) {
     }
     if (m.bad) return err = "malformed TensorProto", false;
     if (t.external) return true;  // only an error if a convolution needs it
-    const size_t n = t.count();
-    t.data.resize(n);
-    auto need = [&](size_t have) {
+    uint64_t n64 = 0;
+    if (!t.count(n64)) return err = "tensor " + name + ": dimensions out of range", false;
+    const size_t n = (size_t)n64;
+    auto need = [&](size_t have) {  // checked before anything of size n is allocated
         if (have != n) {
             err = "tensor " + name + ": " + std::to_string(have) + " values for " + std::to_string(n) + " elements";
             return false;
@@ -213,6 +229,7 @@ bool parse_tensor(Span s, Tensor& t, std::string& name, std::string& err) {
         case DT_FLOAT:
             if (has_raw) {
                 if (!need(raw.size() / 4) || raw.size() % 4) return false;
+                t.data.resize(n);
                 std::memcpy(t.data.data(), raw.p, n * 4);  // little-endian, as the host
             } else {
                 if (!need(fdata.size())) return false;
@@ -221,7 +238,8 @@ bool parse_tensor(Span s, Tensor& t, std::string& name, std::string& err) {
             return true;
         case DT_DOUBLE:
             if (has_raw) {
-                if (!need(raw.size() / 8)) return false;
+                if (!need(raw.size() / 8) || raw.size() % 8) return false;
+                t.data.resize(n);
                 for (size_t i = 0; i < n; i++) {
                     double v;
                     std::memcpy(&v, raw.p + 8 * i, 8);
@@ -229,19 +247,19 @@ bool parse_tensor(Span s, Tensor& t, std::string& name, std::string& err) {
                 }
             } else {
                 if (!need(ddata.size())) return false;
+                t.data.resize(n);
                 for (size_t i = 0; i < n; i++) t.data[i] = (float)ddata[i];
             }
             return true;
         case DT_FLOAT16:
         case DT_BFLOAT16: {
+            if (has_raw ? (!need(raw.size() / 2) || raw.size() % 2) : !need(idata.size())) return false;
             std::vector<uint16_t> h(n);
-            if (has_raw) {
-                if (!need(raw.size() / 2)) return false;
+            if (has_raw)
                 std::memcpy(h.data(), raw.p, n * 2);
-            } else {
-                if (!need(idata.size())) return false;
+            else
                 for (size_t i = 0; i < n; i++) h[i] = (uint16_t)idata[i];
-            }
+            t.data.resize(n);
             for (size_t i = 0; i < n; i++) {
                 if (t.dtype == DT_FLOAT16) {
                     t.data[i] = half_to_float(h[i]);
@@ -252,9 +270,34 @@ bool parse_tensor(Span s, Tensor& t, std::string& name, std::string& err) {
             }
             return true;
         }
-        default:
-            t.data.clear();  // integer tensors (shapes, axes): not weights
+        case DT_INT32:
+        case DT_INT64: {  // axes, shapes, pads: kept when small, never weights
+            if (n > 64) return true;
+            const size_t es = t.dtype == DT_INT64 ? 8 : 4;
+            if (has_raw) {
+                if (!need(raw.size() / es) || raw.size() % es) return false;
+                for (size_t i = 0; i < n; i++) {
+                    if (es == 8) {
+                        int64_t v;
+                        std::memcpy(&v, raw.p + 8 * i, 8);
+                        t.ints.push_back(v);
+                    } else {
+                        int32_t v;
+                        std::memcpy(&v, raw.p + 4 * i, 4);
+                        t.ints.push_back(v);
+                    }
+                }
+            } else if (t.dtype == DT_INT32) {
+                if (!need(idata.size())) return false;
+                for (int64_t v : idata) t.ints.push_back((int32_t)(uint32_t)v);
+            } else {
+                t.ints = i64data;
+                if (!need(t.ints.size())) return false;
+            }
             return true;
+        }
+        default:
+            return true;  // other integer / string tensors: not weights
     }
 }
 
@@ -275,8 +318,10 @@ bool parse_attribute(Span s, Node& n, std::map<std::string, Tensor>& tensors, st
     float fv = 0;
     bool has_t = false;
     Span tspan;
+    std::string sv;
     while (m.next(f, wt, num, b)) {
         if (f == 1) name = str(b);
+        else if (f == 4 && wt == 2) sv = str(b);
         else if (f == 2 && wt == 5) {
             uint32_t u = (uint32_t)num;
             std::memcpy(&fv, &u, 4);
@@ -292,6 +337,9 @@ bool parse_attribute(Span s, Node& n, std::map<std::string, Tensor>& tensors, st
     else if (name == "pads") n.ints_pads = ints;
     else if (name == "group") n.group = i;
     else if (name == "epsilon") n.epsilon = fv;
+    else if (name == "auto_pad") n.auto_pad = sv;
+    else if (name == "keepdims") n.keepdims = i;
+    else if (name == "axes") n.ints_axes = ints, n.has_axes = true;
     else if (name == "dilations") {
         for (int64_t d : ints)
             if (d != 1) return err = "dilated convolutions are not part of these networks", false;
@@ -379,7 +427,8 @@ const Tensor* find_tensor(const Raw& r, const std::map<std::string, int>& produc
         auto it = r.tensors.find(name);
         if (it != r.tensors.end()) return &it->second;
         auto p = producer.find(name);
-        if (p == producer.end() || r.nodes[p->second].op != "Identity") return nullptr;
+        if (p == producer.end() || r.nodes[p->second].op != "Identity" || r.nodes[p->second].in.empty())
+            return nullptr;
         name = r.nodes[p->second].in[0];
     }
     return nullptr;
@@ -403,7 +452,7 @@ bool looks_like_onnx(const char* path) {
            (field == 14 && wt == 2);
 }
 
-bool load(const char* path, Model& model, std::string& err) {
+static bool load_impl(const char* path, Model& model, std::string& err) {
     std::vector<uint8_t> buf;
     if (!read_file(path, buf, err)) return false;
     Raw r;
@@ -430,10 +479,16 @@ bool load(const char* path, Model& model, std::string& err) {
     model.nodes = r.nodes;
     model.inputs = r.inputs;
     model.outputs = r.outputs;
+    for (const auto& kv : r.tensors) {
+        model.consts.insert(kv.first);
+        if (kv.second.dtype == DT_INT32 || kv.second.dtype == DT_INT64) model.int_consts[kv.first] = kv.second.ints;
+    }
     for (int i = 0; i < (int)r.nodes.size(); i++) {
         const Node& n = r.nodes[i];
         if (n.op != "Conv") continue;
-        if (n.in.size() < 2) return err = "Conv node without a weight input", false;
+        if (n.in.size() < 2 || n.in[0].empty()) return err = "Conv node without a data or weight input", false;
+        if (!n.auto_pad.empty() && n.auto_pad != "NOTSET")
+            return err = "Conv with auto_pad " + n.auto_pad + " (only explicit pads are supported)", false;
         const Tensor* W = find_tensor(r, producer, n.in[1]);
         if (!W) return err = "Conv weight " + n.in[1] + " is not a constant of the graph", false;
         if (W->external) return err = "Conv weight " + n.in[1] + " is stored externally (unsupported)", false;
@@ -507,6 +562,7 @@ int trace_back(const Model& m, const std::map<std::string, int>& producer, const
             return -2;
         }
         const Node& n = m.nodes[p->second];
+        if (n.in.empty()) return -2;
         if (n.op == "Identity" || n.op == "Cast" || n.op == "Dropout") {
         } else if (n.op == "Relu" || n.op == "MaxPool") {
             if (n.op == "MaxPool") {
@@ -524,9 +580,79 @@ int trace_back(const Model& m, const std::map<std::string, int>& producer, const
     return -2;
 }
 
+// Follow `name` back through ops that do not change the tensor's meaning (Identity / Cast).
+std::string strip_alias(const Model& m, const std::map<std::string, int>& producer, std::string name) {
+    for (int hop = 0; hop < 16; hop++) {
+        auto p = producer.find(name);
+        if (p == producer.end()) return name;
+        const Node& n = m.nodes[p->second];
+        if ((n.op != "Identity" && n.op != "Cast") || n.in.empty()) return name;
+        name = n.in[0];
+    }
+    return name;
+}
+
+// The reduction axes of a ReduceL2 / ReduceSum node: the "axes" attribute (opset < 18) or the
+// constant second input (opset 18).  True when they are exactly the channel axis (1, or -3 of NCHW).
+bool reduces_channels(const Model& m, const Node& n) {
+    std::vector<int64_t> axes;
+    if (n.has_axes) {
+        axes = n.ints_axes;
+    } else if (n.in.size() > 1 && !n.in[1].empty()) {
+        auto it = m.int_consts.find(n.in[1]);
+        if (it == m.int_consts.end()) return false;
+        axes = it->second;
+    } else {
+        return false;  // no axes: a reduction over every axis
+    }
+    return axes.size() == 1 && (axes[0] == 1 || axes[0] == -3);
+}
+
+// Is `name` the per-pixel L2 norm over channels of tensor `x` (up to Unsqueeze / Expand / a constant
+// clamp from below: Clip(min) / Max(eps))?  ReduceL2(x) or Sqrt(ReduceSum(Pow(x, 2) | Mul(x, x))).
+bool is_channel_norm_of(const Model& m, const std::map<std::string, int>& producer, std::string name,
+                        const std::string& x) {
+    for (int hop = 0; hop < 16; hop++) {
+        name = strip_alias(m, producer, name);
+        auto p = producer.find(name);
+        if (p == producer.end()) return false;
+        const Node& n = m.nodes[p->second];
+        if (n.in.empty()) return false;
+        if (n.op == "Unsqueeze" || n.op == "Expand" || n.op == "Clip") {
+            name = n.in[0];
+        } else if (n.op == "Max") {  // max(norm, eps): one operand a constant
+            if (n.in.size() != 2) return false;
+            const bool c0 = m.consts.count(n.in[0]) > 0, c1 = m.consts.count(n.in[1]) > 0;
+            if (c0 == c1) return false;
+            name = c0 ? n.in[1] : n.in[0];
+        } else if (n.op == "ReduceL2") {
+            return reduces_channels(m, n) && strip_alias(m, producer, n.in[0]) == x;
+        } else if (n.op == "Sqrt") {
+            auto q = producer.find(strip_alias(m, producer, n.in[0]));
+            if (q == producer.end()) return false;
+            const Node& rs = m.nodes[q->second];
+            if (rs.op != "ReduceSum" || rs.in.empty() || !reduces_channels(m, rs)) return false;
+            auto r = producer.find(strip_alias(m, producer, rs.in[0]));
+            if (r == producer.end()) return false;
+            const Node& sq = m.nodes[r->second];
+            if (sq.op == "Mul" && sq.in.size() == 2)
+                return strip_alias(m, producer, sq.in[0]) == x && strip_alias(m, producer, sq.in[1]) == x;
+            if (sq.op == "Pow" && sq.in.size() == 2 && strip_alias(m, producer, sq.in[0]) == x) {
+                // exponent 2: a float constant (initializer / Constant); its value is not kept by the
+                // reader, so any constant exponent on a Pow feeding ReduceSum -> Sqrt is taken as 2
+                return m.consts.count(sq.in[1]) > 0;
+            }
+            return false;
+        } else {
+            return false;
+        }
+    }
+    return false;
+}
+
 }  // namespace
 
-bool superpoint_weights(const Model& m, std::vector<float>& out, std::string& err) {
+static bool superpoint_weights_impl(const Model& m, std::vector<float>& out, std::string& err, bool* desc_normalized) {
     // canonical layers (vs_ctx.hip kLayers): cin, cout, k
     static const int L[12][3] = {{1, 64, 3},    {64, 64, 3},   {64, 64, 3},   {64, 64, 3},
                                  {64, 128, 3},  {128, 128, 3}, {128, 128, 3}, {128, 128, 3},
@@ -577,18 +703,112 @@ bool superpoint_weights(const Model& m, std::vector<float>& out, std::string& er
         if (c.cin_g != L[l][0] || c.cout != L[l][1] || c.kh != L[l][2] || c.kw != L[l][2] || c.group != 1 ||
             c.stride != 1)
             return err = "SuperPoint graph: layer " + std::to_string(l) + " has the wrong shape", false;
+        // explicit pads k/2 on all four sides (ONNX's default is no padding; auto_pad is rejected by load)
+        if (L[l][2] > 1 && c.pads.size() != 4)
+            return err = "SuperPoint graph: layer " + std::to_string(l) + " has no explicit pads", false;
         for (int64_t p : c.pads)
             if (p != L[l][2] / 2) return err = "SuperPoint graph: unexpected Conv padding", false;
         out.insert(out.end(), c.w.begin(), c.w.end());
         out.insert(out.end(), c.b.begin(), c.b.end());
     }
+    // output tails (FeatureExtractor.cpp:114-124 requests "semi" and "desc" by name)
+    auto is_output = [&](const char* nm) { return std::find(m.outputs.begin(), m.outputs.end(), nm) != m.outputs.end(); };
+    if (!is_output("semi") || !is_output("desc"))
+        return err = "SuperPoint graph: outputs \"semi\" and \"desc\" required (FeatureExtractor.cpp:114)", false;
+    const std::string pb = m.convs[slot[9]].output, db = m.convs[slot[11]].output;
+    {
+        const std::string sn = strip_alias(m, producer, "semi");
+        if (sn != pb) {
+            auto p = producer.find(sn);
+            const std::string op = p == producer.end() ? std::string("graph input") : m.nodes[p->second].op;
+            return err = "SuperPoint graph: \"semi\" must be convPb's raw logits (the reference applies its own "
+                         "softmax, FeatureExtractor.cpp:128-151); found " + op, false;
+        }
+    }
+    bool normed = false;
+    {
+        const std::string dn = strip_alias(m, producer, "desc");
+        if (dn != db) {
+            auto p = producer.find(dn);
+            bool ok = false;
+            if (p != producer.end()) {
+                const Node& n = m.nodes[p->second];
+                if (n.op == "Div" && n.in.size() == 2) {
+                    ok = strip_alias(m, producer, n.in[0]) == db && is_channel_norm_of(m, producer, n.in[1], db);
+                } else if (n.op == "Mul" && n.in.size() == 2) {  // x * Reciprocal(norm)
+                    for (int a = 0; a < 2 && !ok; a++) {
+                        if (strip_alias(m, producer, n.in[a]) != db) continue;
+                        auto q = producer.find(strip_alias(m, producer, n.in[1 - a]));
+                        if (q != producer.end() && m.nodes[q->second].op == "Reciprocal" && !m.nodes[q->second].in.empty())
+                            ok = is_channel_norm_of(m, producer, m.nodes[q->second].in[0], db);
+                    }
+                }
+            }
+            if (!ok)
+                return err = "SuperPoint graph: \"desc\" must be convDb's output or its L2 normalisation over "
+                             "channels (FeatureExtractor.cpp:167-206 samples it as given)", false;
+            normed = true;
+        }
+    }
+    if (desc_normalized) *desc_normalized = normed;
     return true;
 }
 
-bool midas_weights(const Model& m, const std::vector<LayerSpec>& spec, std::vector<float>& out, std::string& err) {
+namespace {
+
+// The canonical layers (= conv indices, graph order) whose outputs reach tensor `name` through
+// element-wise / padding / resize ops and Adds, stopping at each conv; -1 for the graph input.
+// False when another op is in the way.
+bool conv_sources(const Model& m, const std::map<std::string, int>& producer, const std::map<std::string, int>& conv_of,
+                  const std::string& name, std::map<std::string, std::set<int>>& memo, std::set<int>& out, int depth = 0) {
+    if (depth > 256) return false;
+    auto mm = memo.find(name);
+    if (mm != memo.end()) {
+        out.insert(mm->second.begin(), mm->second.end());
+        return true;
+    }
+    std::set<int> acc;
+    auto c = conv_of.find(name);
+    if (c != conv_of.end()) {
+        acc.insert(c->second);
+    } else {
+        auto p = producer.find(name);
+        if (p == producer.end()) {
+            if (std::find(m.inputs.begin(), m.inputs.end(), name) == m.inputs.end()) return false;
+            acc.insert(-1);
+        } else {
+            const Node& n = m.nodes[p->second];
+            static const char* pass[] = {"Identity", "Cast", "Relu", "Clip", "Pad", "Resize", "Upsample",
+                                         "Dropout", "Squeeze", "Unsqueeze"};
+            bool through = false;
+            for (const char* op : pass) through |= n.op == op;
+            if (through) {
+                if (n.in.empty() || !conv_sources(m, producer, conv_of, n.in[0], memo, acc, depth + 1)) return false;
+            } else if (n.op == "Add" || n.op == "Sum") {
+                for (const std::string& in : n.in)
+                    if (!conv_sources(m, producer, conv_of, in, memo, acc, depth + 1)) return false;
+            } else {
+                return false;
+            }
+        }
+    }
+    memo[name] = acc;
+    out.insert(acc.begin(), acc.end());
+    return true;
+}
+
+}  // namespace
+
+static bool midas_weights_impl(const Model& m, const std::vector<LayerSpec>& spec, std::vector<float>& out,
+                               std::string& err) {
     if (m.convs.size() != spec.size())
         return err = "MiDaS graph: expected " + std::to_string(spec.size()) + " convolutions, found " +
                      std::to_string(m.convs.size()), false;
+    std::map<std::string, int> producer, conv_of;
+    for (int i = 0; i < (int)m.nodes.size(); i++)
+        for (auto& o : m.nodes[i].out) producer[o] = i;
+    for (int i = 0; i < (int)m.convs.size(); i++) conv_of[m.convs[i].output] = i;
+    std::map<std::string, std::set<int>> memo;
     out.clear();
     for (size_t l = 0; l < spec.size(); l++) {
         const Conv& c = m.convs[l];
@@ -598,6 +818,23 @@ bool midas_weights(const Model& m, const std::vector<LayerSpec>& spec, std::vect
         if (!ok || c.kh != s.k || c.kw != s.k || c.stride != s.stride)
             return err = "MiDaS graph: convolution " + std::to_string(l) + " does not match the v2.1-small layer (" +
                          std::to_string(c.cout) + "x" + std::to_string(c.cin_g) + "x" + std::to_string(c.kh) + ")", false;
+        // padding: TF "same" layers take an explicit Pad node and pads 0; the others pads k/2
+        const int want_pad = s.tf_same ? 0 : s.k / 2;
+        if (want_pad > 0 && c.pads.size() != 4)
+            return err = "MiDaS graph: convolution " + std::to_string(l) + " has no explicit pads", false;
+        for (int64_t p : c.pads)
+            if (p != want_pad) return err = "MiDaS graph: convolution " + std::to_string(l) + " has unexpected pads", false;
+        if (s.tf_same) {
+            auto p = producer.find(strip_alias(m, producer, c.input));
+            if (p == producer.end() || m.nodes[p->second].op != "Pad")
+                return err = "MiDaS graph: convolution " + std::to_string(l) + " lacks its TF-same Pad", false;
+        }
+        if (!s.from.empty()) {
+            std::set<int> got;
+            if (!conv_sources(m, producer, conv_of, c.input, memo, got) || got != s.from)
+                return err = "MiDaS graph: convolution " + std::to_string(l) +
+                             " is not wired as the v2.1-small layer (its input comes from other layers)", false;
+        }
         out.insert(out.end(), c.w.begin(), c.w.end());
         if (s.bias) {
             out.insert(out.end(), c.b.begin(), c.b.end());
@@ -607,6 +844,32 @@ bool midas_weights(const Model& m, const std::vector<LayerSpec>& spec, std::vect
         }
     }
     return true;
+}
+
+// The public entry points never let an exception (std::bad_alloc on a hostile file, ...) escape:
+// they sit under the C ABI (vs_create, vs_midas_create, vs_*_onnx_weights).
+template <class F>
+static bool guarded(std::string& err, F&& f) {
+    try {
+        return f();
+    } catch (const std::exception& e) {
+        err = std::string("ONNX reader: ") + e.what();
+    } catch (...) {
+        err = "ONNX reader: unknown exception";
+    }
+    return false;
+}
+
+bool load(const char* path, Model& model, std::string& err) {
+    return guarded(err, [&] { return load_impl(path, model, err); });
+}
+
+bool superpoint_weights(const Model& m, std::vector<float>& out, std::string& err, bool* desc_normalized) {
+    return guarded(err, [&] { return superpoint_weights_impl(m, out, err, desc_normalized); });
+}
+
+bool midas_weights(const Model& m, const std::vector<LayerSpec>& spec, std::vector<float>& out, std::string& err) {
+    return guarded(err, [&] { return midas_weights_impl(m, spec, out, err); });
 }
 
 }  // namespace vs_onnx

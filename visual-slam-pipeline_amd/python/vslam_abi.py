@@ -112,6 +112,8 @@ _SIG = {
     "vs_profile_enable": (_I, [_P, _I]),
     "vs_nms_tie_stats": (_I, [_P, _P, _I]),
     "vs_superpoint_onnx_weights": (_I, [ctypes.c_char_p, _P, ctypes.c_size_t]),
+    "vs_superpoint_onnx_desc_normalized": (_I, [ctypes.c_char_p, _P]),
+    "vs_desc_normalized": (_I, [_P, _P]),
     "vs_superpoint_synth_weights": (_I, [_P, ctypes.c_size_t]),
     "vs_midas_onnx_weights": (_I, [ctypes.c_char_p, _P, ctypes.c_size_t]),
     "vs_midas_synth_weights": (_I, [_P, ctypes.c_size_t]),
@@ -165,6 +167,15 @@ def superpoint_onnx_weights(path):
     out = np.zeros(lib.vs_superpoint_num_params(), np.float32)
     _check(lib.vs_superpoint_onnx_weights(os.fsencode(path), _ptr(out), out.size))
     return out
+
+
+def superpoint_onnx_desc_normalized(path):
+    """The ONNX export's "desc" tail (host only): True when convDb's output is L2-normalised over
+    channels in the graph, False when "desc" is the raw conv output (vs_superpoint_onnx_desc_normalized)."""
+    lib = load_library()
+    v = ctypes.c_int(-1)
+    _check(lib.vs_superpoint_onnx_desc_normalized(os.fsencode(path), ctypes.byref(v)))
+    return bool(v.value)
 
 
 def superpoint_synth_weights():
@@ -241,6 +252,12 @@ class Context:
         out = np.empty(n, np.float32)
         _check(self.lib.vs_superpoint_get_weights(self.h, _ptr(out), n))
         return out
+
+    def desc_normalized(self):
+        """Whether the network's "desc" grid is L2-normalised before sampling (vs_desc_normalized)."""
+        v = ctypes.c_int(-1)
+        _check(self.lib.vs_desc_normalized(self.h, ctypes.byref(v)))
+        return bool(v.value)
 
     def save_weights(self, path):
         _check(self.lib.vs_superpoint_save_weights(self.h, path.encode()))
