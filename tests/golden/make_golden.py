@@ -259,9 +259,76 @@ def gen_ba_config2():
                 err=np.array([eb, ea]), stats=np.array(stats, np.int32))
 
 
+def gen_geometry_large():
+    """the shared-solver stages pinned independently at the sizes the tracker runs
+    them (values from tests/indep.py, the oracle must agree):
+      fmat400  findFundamentalMat(FM_RANSAC, 3 px, 0.999) on n = 400 matches, 35 % outliers (the
+               tracker's per-frame F verification runs on up to SP_MAX_KEYPOINTS matches,
+               Slam.cpp:884-910);
+      emat400  findEssentialMat(RANSAC, 0.999, 1 px) + recoverPose + depth scale, n = 400, 35 %
+               outliers (Slam.cpp:1193-1213, 73-157);
+      pnp400   the local refinement PnP, solvePnPRansac(100 iterations, 8 px, 0.99), min 10 inliers
+               (Slam.cpp:1424 -> 505-529), n = 400, 30 % outliers;
+      pnp2000  the recovery-size PnP (Slam.cpp:577: 300 iterations, 15 inliers) against a map-sized
+               correspondence set, n = 2,000, 40 % outliers."""
+    from test_oracle_emat import _depth_maps
+    from test_oracle_emat import two_view as two_view_e
+    from test_oracle_fmat import two_view as two_view_f
+    from test_oracle_pnp import pnp_problem
+    out = {}
+    p1, p2, F, outl = two_view_f(400, 201, 0.5, 0.35)
+    ok, Fi, mask, diag = indep.find_fundamental(p1, p2)
+    oko, Fo, masko, diago = oracle.find_fundamental(p1, p2)
+    assert ok and oko and np.array_equal(masko.astype(bool), mask) and list(diago) == list(diag), (diag, diago)
+    assert np.max(np.abs(Fo - Fi)) <= 1e-9 * np.abs(Fi).max()
+    assert not np.any(mask & outl) and mask.sum() >= 0.9 * (~outl).sum()  # known answer: the labels
+    out.update(fmat400_p1=p1, fmat400_p2=p2, fmat400_F=Fi, fmat400_mask=mask.astype(np.uint8),
+               fmat400_diag=np.array(diag, np.int32))
+
+    p1, p2, R, t, X, outl = two_view_e(400, 202, noise=0.4, outlier_frac=0.35)
+    d1, d2 = _depth_maps(X, R, t, p1, p2)
+    ok_e, E, emask, fdiag = indep.find_essential(p1, p2)
+    ok, Ri, ti, mask, inl, good = indep.estimate_motion(p1, p2)
+    assert ok and _rot_angle(Ri, R) < 5e-3
+    sc = indep.estimate_scale(p1, p2, Ri, ti, d1, d2)
+    assert abs(sc * np.linalg.norm(ti) - np.linalg.norm(t)) < 0.05 * np.linalg.norm(t)
+    oko, Ro, to, masko, inlo, goodo = oracle.estimate_motion(p1, p2)
+    fo = oracle.find_essential(p1, p2)[3]
+    assert oko and inlo == inl and goodo == good and list(fo[:3]) == list(fdiag), (fo, fdiag, inl, inlo)
+    assert np.max(np.abs(Ro - Ri)) <= 1e-7 and np.max(np.abs(to - ti)) <= 1e-6
+    sco = oracle.estimate_scale(p1, p2, Ro, to, d1, d2)
+    assert abs(sco - sc) <= 1e-6 * abs(sc)
+    i1, v1 = _sparse(d1)
+    i2, v2 = _sparse(d2)
+    out.update(emat400_p1=p1, emat400_p2=p2, emat400_d1i=i1, emat400_d1v=v1, emat400_d2i=i2, emat400_d2v=v2,
+               emat400_R=Ri, emat400_t=ti, emat400_scale=np.float64(sc), emat400_fdiag=np.array(fdiag, np.int32),
+               emat400_inl=np.int32(inl), emat400_good=np.int32(good))
+
+    for tag, (n, seed, noise, of, iters, min_inl) in {"pnp400": (400, 203, 0.7, 0.3, 100, 10),
+                                                        "pnp2000": (2000, 204, 0.7, 0.4, 300, 15)}.items():
+        obj, img, R, t, outl = pnp_problem(n, seed, noise=noise, outlier_frac=of)
+        ok_r, rv, tv, inl_r, mask, diag = indep.pnp_ransac(obj, img, iters)
+        succ, Rw, tw, cnt = indep.solve_pnp(obj, img, iters, min_inl)
+        assert succ and _rot_angle(Rw, R.T) < 5e-3
+        assert not np.any(mask & outl)
+        so, Ro, to, co = oracle.solve_pnp(obj, img, iters, min_inl)
+        oo = oracle.pnp_ransac(obj, img, iters)
+        # mask, count and pose; not the winning iteration: with 5-point subsets M^T M (10 x 12) has a
+        # two-dimensional null space, its basis is solver-dependent (LAPACK here, round-robin Jacobi in
+        # the product), EPnP's 5 Gauss-Newton steps start from different betas, and two hypotheses of
+        # equal inlier count swap places (here: iteration 1 vs 5, both with the 280 true inliers)
+        assert so and co == cnt and np.array_equal(oo[4].astype(bool), mask), (co, cnt, list(oo[5][:2]), list(diag))
+        assert np.max(np.abs(Ro - Rw)) <= 1e-8 and np.max(np.abs(to - tw)) <= 1e-8, (
+            np.max(np.abs(Ro - Rw)), np.max(np.abs(to - tw)))
+        out.update({f"{tag}_obj": obj, f"{tag}_img": img, f"{tag}_R": Rw, f"{tag}_t": tw, f"{tag}_cnt": np.int32(cnt),
+                    f"{tag}_mask": mask.astype(np.uint8), f"{tag}_diag": np.array(diag, np.int32),
+                    f"{tag}_iters": np.int32(iters), f"{tag}_min_inliers": np.int32(min_inl)})
+    return out
+
+
 GENERATORS = dict(postprocess=gen_postprocess, match=gen_match, ransac3d=gen_ransac3d, fmat=gen_fmat, emat=gen_emat,
                   pnp=gen_pnp, tlm=gen_tlm, pose=gen_pose, ba=gen_ba, ba_window=gen_ba_window,
-                  ba_config2=gen_ba_config2)
+                  ba_config2=gen_ba_config2, geometry_large=gen_geometry_large)
 
 
 def main():
