@@ -92,3 +92,50 @@ def recovery_sequence(L, n_frames, k_jump, seed=13, n_land=20000):
         feats.append((k, d))
         ids.append(i)
     return feats, P
+
+
+class NoisySequence:
+    """Realistic-noise features along the closed loop (a known-answer run that
+    is neither ideal nor random-weight): every landmark has a fixed saliency and a frame keeps its
+    400 most salient visible landmarks (saliency jittered per frame), so detections repeat across
+    frames as a trained detector's do; then
+
+    * keypoints carry `px` pixels of Gaussian position noise;
+    * descriptors carry `desc_noise` per dimension of Gaussian noise (unit 256-d vectors: 0.03 puts
+      a true pair at ~0.68 against ~1.41 for unrelated landmarks, before the ratio test);
+    * a fraction `shuffle` of each frame's keypoints carry the descriptor of another of its own
+      keypoints (a random derangement among them), independently per frame, so ratio matching
+      between two frames yields confidently wrong pairs (outliers for F / 3D-3D / PnP);
+    * the depth image loses a fraction `dropout` of its pixels (0 = invalid, Frame.cpp:51-52).
+
+    frame(g) returns (keypoints, descriptors, depth, landmark ids, wrong) for processed frame g
+    (rendered frame g mod U); wrong marks the keypoints whose descriptor is not their landmark's."""
+
+    def __init__(self, L, n_land=20000, seed=17, shuffle=0.2, px=0.7, desc_noise=0.03, dropout=0.03, cap=400):
+        self.L, self.fr = L, loop_frames(L)
+        self.P, self.D = landmarks(self.fr, n_land=n_land, seed=seed)
+        rng = np.random.default_rng(seed + 1)
+        self.sal = rng.uniform(0.0, 1.0, len(self.P))
+        self.seed, self.shuffle, self.px, self.dn, self.dropout, self.cap = seed, shuffle, px, desc_noise, dropout, cap
+
+    def frame(self, g):
+        U = len(self.fr)
+        f = self.fr[g % U]
+        rng = np.random.default_rng((self.seed, g))
+        idx, u, v = visible(f, self.P)
+        score = self.sal[idx] * (1.0 + rng.normal(0, 0.1, len(idx)))
+        idx = idx[np.argsort(-score, kind="stable")[:self.cap]]
+        n = len(idx)
+        k = np.zeros(n, KP_DTYPE)
+        k["x"] = u[idx] + rng.normal(0, self.px, n)
+        k["y"] = v[idx] + rng.normal(0, self.px, n)
+        k["size"], k["angle"], k["response"], k["class_id"] = 8.0, -1.0, 0.5, -1
+        src = idx.copy()
+        sel = np.nonzero(rng.random(n) < self.shuffle)[0]
+        if len(sel) > 1:
+            src[sel] = idx[np.roll(sel, 1 + int(rng.integers(0, len(sel) - 1)))]
+        d = self.D[src] + rng.normal(0, self.dn, (n, 256)).astype(np.float32)
+        d /= np.linalg.norm(d, axis=1, keepdims=True)
+        depth = self.L["depth"][g % U].copy()
+        depth[rng.random(depth.shape) < self.dropout] = 0.0
+        return k, d.astype(np.float32), depth, idx, src != idx

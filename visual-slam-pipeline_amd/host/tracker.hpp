@@ -658,10 +658,10 @@ class Tracker {
     }
     void trace_chain(int id, const ChainResult& C) const {
         if (!trace_) return;
-        std::fprintf(trace_, "%d chain raw=%d good=%d/%016llx fok=%d fit=%d kept=%d epi=%a/%a ok3d=%d okE=%d sc=%a\n", id,
-                     C.n_raw, (int)C.good.size(), (unsigned long long)fnv(C.good.data(), C.good.size() * sizeof(Match)),
-                     (int)C.f_ok, C.f_iters, (int)C.kept.size(), C.epi_before, C.epi_after, (int)C.ok3d, (int)C.okE,
-                     C.scale);
+        std::fprintf(trace_, "%d chain ref=%d raw=%d good=%d/%016llx fok=%d fit=%d kept=%d epi=%a/%a ok3d=%d okE=%d sc=%a\n",
+                     id, ref_frame_ ? ref_frame_->id : -1, C.n_raw, (int)C.good.size(),
+                     (unsigned long long)fnv(C.good.data(), C.good.size() * sizeof(Match)), (int)C.f_ok, C.f_iters,
+                     (int)C.kept.size(), C.epi_before, C.epi_after, (int)C.ok3d, (int)C.okE, C.scale);
         if (C.ok3d) trace_pose(id, "r3d", C.R3, C.t3);
         if (C.okE) trace_pose(id, "rE", C.RE, C.tE);
     }

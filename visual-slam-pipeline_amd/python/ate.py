@@ -18,8 +18,10 @@ def closest(ts, gt_ts):
     return np.where(np.abs(ts - left) <= np.abs(right - ts), i - 1, i)
 
 
-def compute_ate(est_ts, est_xyz, gt_ts, gt_xyz, max_dt=0.05):
-    """Returns dict(ate_rmse, scale, R, t, n) or ate_rmse = -1 with fewer than 3 pairs."""
+def compute_ate(est_ts, est_xyz, gt_ts, gt_xyz, max_dt=0.05, with_scale=True):
+    """Returns dict(ate_rmse, scale, R, t, n) or ate_rmse = -1 with fewer than 3 pairs.
+    with_scale=False: the SE(3) alignment (scale fixed at 1) — not the reference's figure, reported
+    beside it because a sim(3) fit can shrink a diverged trajectory onto the truth."""
     est_ts = np.asarray(est_ts, np.float64)
     est_xyz = np.asarray(est_xyz, np.float64).reshape(-1, 3)
     gt_ts = np.asarray(gt_ts, np.float64)
@@ -42,7 +44,7 @@ def compute_ate(est_ts, est_xyz, gt_ts, gt_xyz, max_dt=0.05):
     if np.linalg.det(U @ Vt) < 0:
         D[2, 2] = -1
     R = U @ D @ Vt
-    scale = float(np.trace(np.diag(S) @ D) / sigma_est) if sigma_est > 0 else 1.0
+    scale = float(np.trace(np.diag(S) @ D) / sigma_est) if sigma_est > 0 and with_scale else 1.0
     t = gm - scale * R @ em
     aligned = (scale * (R @ e.T)).T + t
     rmse = float(np.sqrt(((aligned - g) ** 2).sum(1).mean()))
