@@ -182,7 +182,10 @@ def match_roofline(ms_launches, pairs_per_launch, cus, where):
     flops = 2.0 * 400 * 400 * 256 * pairs_per_launch
     peak = FP32_MFMA_PEAK_TFLOPS * cus / 256
     ach = flops / avg_s / 1e12
-    return {"where": where, "kernel": "vs::k_match<2, 2, 32, 32, 32, 1, 1, NORMS> (64 x 64 tiles)", "bound": "mfma",
+    # csrc/match.hip launch(): one or two pairs per launch take 32 x 32 tiles, more take 64 x 64
+    kernel = ("vs::k_match<2, 2, 16, 16, 32, 1, 1, ...> (32 x 32 tiles)" if pairs_per_launch <= 2 else
+              "vs::k_match<2, 2, 32, 32, 32, 1, 1, ...> (64 x 64 tiles)")
+    return {"where": where, "kernel": kernel, "bound": "mfma",
             "achieved": round(ach, 3), "peak": round(peak, 2), "unit": "TFLOP/s", "frac": round(ach / peak, 4),
             "cus": cus, "pairs_per_launch": pairs_per_launch, "avg_launch_us": round(avg_s * 1e6, 2),
             "us_per_pair": round(avg_s * 1e6 / pairs_per_launch, 2), "launches": launches,
@@ -248,7 +251,18 @@ def cpu_baseline(L, nframes, ba=None):
         model = next(ln.split(":", 1)[1].strip() for ln in open("/proc/cpuinfo") if ln.startswith("model name"))
     except (OSError, StopIteration):
         pass
+    table = None
+    try:  # config[0] as SURVEY 8(d) defines it: 200 frames at 1, 4 and the box's CPU share (tools/cpu_baseline.py)
+        doc = json.load(open(os.path.join(ROOT, "profiles", "cpu_baseline.json")))
+        table = {"source": "profiles/cpu_baseline.json (tools/cpu_baseline.py on the GPU box, " + doc.get("tag", "?") + ")",
+                 "cpu_model": doc.get("cpu_model"), "frames": doc["runs"][0]["frames"],
+                 "runs": [{"threads": r["threads"], "value": r["value"], "unit": r["unit"],
+                           "ms_per_frame_extract": r["ms_per_frame"]["extract"],
+                           "ms_per_frame_track": r["ms_per_frame"]["track"]} for r in doc["runs"]]}
+    except (OSError, ValueError, KeyError, IndexError):
+        pass
     return {"value": nframes / dt, "unit": "frames/s", "cores": threads, "kind": "port", "cpu_model": model,
+            "config0_table": table,
             "local_ba": ba_cpu,
             "caveats": "a restatement, not the reference binary (OpenCV / ONNX Runtime / g2o are absent): the network "
                        "is the oracle's OpenMP fp32 direct convolution, not ONNX Runtime's MLAS (SURVEY.md 8(d)); "
@@ -256,7 +270,6 @@ def cpu_baseline(L, nframes, ba=None):
                        "(the reference's randomized kd-tree: ~2-5 ms per 400 x 400 pair, SURVEY.md A7)",
             "ms_per_frame": {"extract": round(t_ext / nframes * 1e3, 3), "track": round(t_trk / nframes * 1e3, 3),
                              **stages},
-            "full_table": "profiles/r02_cpu_baseline.json (200 frames at 1, 4, 16 threads; tools/cpu_baseline.py)",
             "sample": f"first {nframes} frames of the same synthetic 640x480 RGB-D sequence through the oracle/ "
                       f"CPU restatement (OpenMP fp32 SuperPoint + decode/NMS/sample, then Slam::process_frame with "
                       f"exact 2-NN matching, F-RANSAC, 3D-3D RANSAC / E fallback, EKF, local-map tracking, PnP, "
@@ -610,8 +623,12 @@ def main():
     # enqueue_extraction) overlapped with tracking: a launch covers frames_timed / launches frames
     avg_s = dom_ms / 1e3 / dom_launches
     frames_per_launch = net_frames / dom_launches
-    flops_per_launch = LAYER_FLOPS[dom] * frames_per_launch
+    # roofline FLOPs = what the matrix cores execute (Winograd: 2.25x fewer than the direct
+    # convolution); the direct-convolution count is reported as the effective rate
+    flops_per_launch = MFMA_FLOPS[dom] * frames_per_launch
     achieved = flops_per_launch / avg_s / 1e12
+    eff_flops_per_launch = LAYER_FLOPS[dom] * frames_per_launch
+    eff_achieved = eff_flops_per_launch / avg_s / 1e12
     net_ms = sum(v[0] for v in conv.values()) if conv else float("nan")
     net_flops = sum(LAYER_FLOPS.values()) * net_frames
     stage_ms = {k: round(v[0] / frames_timed, 4) for k, v in prof.items() if v[1]}
@@ -640,9 +657,10 @@ def main():
         a_ach = LAYER_FLOPS[dom] * nb / (ms_l / 1e3 / n_l) / 1e12
         net_l = sum(v[0] for k, v in pa.items() if k in LAYER_FLOPS)
         m_ach = MFMA_FLOPS[dom] * nb / (ms_l / 1e3 / n_l) / 1e12
-        alone[f"frames_per_launch_{nb}"] = {"avg_launch_ms": round(ms_l / n_l, 4), "achieved": round(a_ach, 3),
-                                            "frac": round(a_ach / FP32_MFMA_PEAK_TFLOPS, 4),
-                                            "mfma_frac": round(m_ach / FP32_MFMA_PEAK_TFLOPS, 4),
+        alone[f"frames_per_launch_{nb}"] = {"avg_launch_ms": round(ms_l / n_l, 4), "achieved": round(m_ach, 3),
+                                            "frac": round(m_ach / FP32_MFMA_PEAK_TFLOPS, 4),
+                                            "effective_achieved": round(a_ach, 3),
+                                            "effective_frac": round(a_ach / FP32_MFMA_PEAK_TFLOPS, 4),
                                             "network_tflops": round(sum(LAYER_FLOPS.values()) * nb * 5 / (net_l / 1e3) / 1e12, 3)}
         del semi_t, dg_t
 
@@ -737,22 +755,26 @@ def main():
                 "avg_launch_ms": round(avg_s * 1e3, 4),
                 "frames_per_launch": round(frames_per_launch, 3),
                 "flops_per_launch": round(flops_per_launch),
-                "flops_unit": "algorithmic (direct-convolution) FLOPs, as the roofline contract counts them",
+                "flops_unit": "FLOPs the matrix cores execute (Winograd F(2x2, 3x3): 16 products per 2x2 output "
+                              "tile, input and output channel); conv1a (1 -> 64, vector ALUs) not counted",
                 "algorithm": "Winograd F(2x2, 3x3), fp32 (sp_net.hip k_wino3)" if WINO else
                              "direct implicit GEMM, fp32",
-                "mfma_flops_per_launch": round(MFMA_FLOPS[dom] * frames_per_launch),
-                "mfma_achieved": round(MFMA_FLOPS[dom] * frames_per_launch / avg_s / 1e12, 3),
-                "mfma_frac": round(MFMA_FLOPS[dom] * frames_per_launch / avg_s / 1e12 / FP32_MFMA_PEAK_TFLOPS, 4),
+                "effective_flops_per_launch": round(eff_flops_per_launch),
+                "effective_achieved": round(eff_achieved, 3),
+                "effective_frac": round(eff_achieved / FP32_MFMA_PEAK_TFLOPS, 4),
+                "effective_note": "direct-convolution FLOPs (the algorithmic work of conv1a + conv1b) / time: the "
+                                  "throughput a direct kernel would need to match; with Winograd it can exceed the peak",
                 "note": f"network on the extraction stream's CU set (all CUs but VS_SLAM_TRACK_CUS = {track_cus} "
                         f"and VS_SLAM_SPEC_CUS = {spec_cus} for the speculative chain), "
-                        "overlapped with tracking; peak is the whole chip's; achieved / frac count the direct "
-                        "convolution's FLOPs (the algorithmic work), so with Winograd's 2.25x fewer multiplies frac "
-                        "can exceed 1 (alone_whole_chip at 32 frames); mfma_* count the matrix-core FLOPs the "
-                        "Winograd kernel executes (its utilisation of the fp32 MFMA peak)",
+                        "overlapped with tracking; peak is the whole chip's (so frac is a lower bound of the "
+                        "utilisation of the CUs the network holds)",
                 "alone_whole_chip": alone,
             },
             "match_roofline": mroof,
             "network_tflops": round(net_flops / (net_ms / 1e3) / 1e12, 3),
+            "network_tflops_note": "direct-convolution (algorithmic) FLOPs of the whole network / its time; "
+                                   "network_mfma_tflops: the FLOPs the matrix cores execute",
+            "network_mfma_tflops": round(sum(MFMA_FLOPS.values()) * net_frames / (net_ms / 1e3) / 1e12, 3),
             "stage_ms_per_frame": stage_ms,
             "stage_profile": {"timed_region": args.stage_profile,
                               "network_from": "the timed region" if net_prof is prof else "the extra profiled steps",

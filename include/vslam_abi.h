@@ -405,6 +405,15 @@ int vs_batch_set_gather(vs_batch* b, int on);
 /* The last step's feature records on the device (gather mode: all ranks' frames in global order;
  * otherwise this rank's), e.g. for vs_spcf_write_dev. */
 int vs_batch_features_dev(vs_batch* b, const vs_keypoint** d_kps, const float** d_desc, const int** d_n, int* frames);
+/* Test support, host only (no device): vs_batch_step_dev's per-step record exchange
+ * (csrc/batch_exchange.h — the ring halo, or the all-gather with gather != 0) run for `world` ranks in
+ * one process over an in-memory transport, one thread per rank.  Inputs are [steps][world][B]
+ * records (kps_in [..][cap], desc_in [..][cap][256], n_in); outputs slot 0 of every rank after
+ * every step (slot0_kps [steps][world][cap], slot0_desc, slot0_n [steps][world]) and, with gather,
+ * every rank's gathered tables (g_* [steps][world][world B] records).  world <= 64. */
+int vs_batch_exchange_loopback(int world, int B, int cap, int steps, int gather, const vs_keypoint* kps_in,
+                               const float* desc_in, const int* n_in, vs_keypoint* slot0_kps, float* slot0_desc,
+                               int* slot0_n, vs_keypoint* g_kps, float* g_desc, int* g_n);
 
 /* ---- F2: the SPCF feature cache as the batch interchange (FeatureExtractor.cpp:261-381) ---
  * Byte layout of the reference's save_cache / load_cache: u32 magic 0x53504346 ("SPCF"),

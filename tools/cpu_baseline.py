@@ -63,16 +63,17 @@ def main():
     ap.add_argument("--frames", type=int, default=200)
     ap.add_argument("--threads", default=None, help="comma list (default 1,4,<OMP_NUM_THREADS or nproc>)")
     ap.add_argument("--out", default=None)
+    ap.add_argument("--tag", default=None, help="round tag recorded in the output (e.g. r04)")
     args = ap.parse_args()
     import synth
     from oracle_long_run import _weights
-    nmax = int(os.environ.get("OMP_NUM_THREADS", "0")) or (os.cpu_count() or 1)
+    nmax = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
     threads = [int(x) for x in args.threads.split(",")] if args.threads else sorted({1, 4, nmax})
     L = synth.loop_sequence(LOOP, workers=min(8, os.cpu_count() or 1))
     w = _weights()
     res = {"what": "config[0] CPU baseline: oracle/ CPU restatement (OpenMP fp32 SuperPoint extract, then "
                    "Slam::process_frame over the CPU stages), bench.py's synthetic 640x480 RGB-D closed loop",
-           "cpu_model": cpu_model(), "nproc": os.cpu_count(),
+           "cpu_model": cpu_model(), "nproc": os.cpu_count(), "tag": args.tag,
            "affinity": len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else None,
            "runs": []}
     for nt in threads:

@@ -19,6 +19,7 @@
 #include <cstring>
 #include <vector>
 
+#include "batch_exchange.h"
 #include "vs_internal.h"
 
 namespace {
@@ -78,6 +79,38 @@ Rccl g_rccl;
             return VS_ERR_HIP;                                                                         \
         }                                                                                              \
     } while (0)
+
+// The exchange's transport on the GPU: device-to-device copies and RCCL point-to-point / all-gather,
+// all enqueued on the step's stream.
+struct RcclTransport final : vs_bx::Transport {
+    RcclComm comm;
+    hipStream_t s;
+    RcclTransport(RcclComm c, hipStream_t st) : comm(c), s(st) {}
+    int copy(void* dst, const void* src, size_t bytes) override {
+        VS_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, s));
+        return VS_OK;
+    }
+    int group_start() override {
+        VS_RCCL(g_rccl.group_start());
+        return VS_OK;
+    }
+    int group_end() override {
+        VS_RCCL(g_rccl.group_end());
+        return VS_OK;
+    }
+    int send(const void* buf, size_t bytes, int peer) override {
+        VS_RCCL(g_rccl.send(buf, bytes, kRcclChar, peer, comm, s));
+        return VS_OK;
+    }
+    int recv(void* buf, size_t bytes, int peer) override {
+        VS_RCCL(g_rccl.recv(buf, bytes, kRcclChar, peer, comm, s));
+        return VS_OK;
+    }
+    int all_gather(const void* src, void* dst, size_t bytes_per_rank) override {
+        VS_RCCL(g_rccl.all_gather(src, dst, bytes_per_rank, kRcclChar, comm, s));
+        return VS_OK;
+    }
+};
 
 template <class T>
 T* alloc(std::vector<void*>& owned, size_t count) {  // zeroed; a failure leaves a null in `owned`
@@ -224,46 +257,15 @@ int vs_batch_step_dev(vs_batch* b, const uint8_t* d_bgr, const float* d_depth, c
     }
     VS_CHECK(vs_network_batch_dev(ctx, B, d_bgr, h, w, b->semi, b->dgrid, s));
     VS_CHECK(vs_postprocess_batch_dev(ctx, B, b->semi, b->dgrid, h, w, b->kps + rec_k, b->desc + rec_d, b->n + 1, cap, s));
-    if (xchg) {
-        const size_t kb = rec_k * sizeof(vs_keypoint), db = rec_d * sizeof(float);
-        if (b->gather) {
-            // all-gather the step's records; the neighbour record is frame rank * B - 1 of the
-            // gathered step (rank 0: the global last frame, next step's neighbour)
-            VS_RCCL(g_rccl.all_gather(b->n + 1, b->g_n, (size_t)B * sizeof(int), kRcclChar, b->comm, s));
-            VS_RCCL(g_rccl.all_gather(b->kps + rec_k, b->g_kps, (size_t)B * kb, kRcclChar, b->comm, s));
-            VS_RCCL(g_rccl.all_gather(b->desc + rec_d, b->g_desc, (size_t)B * db, kRcclChar, b->comm, s));
-            const size_t j = ((size_t)b->rank * B + (size_t)b->world * B - 1) % ((size_t)b->world * B);
-            VS_HIP(hipMemcpyAsync(b->rx_kps, b->g_kps + j * rec_k, kb, hipMemcpyDeviceToDevice, s));
-            VS_HIP(hipMemcpyAsync(b->rx_desc, b->g_desc + j * rec_d, db, hipMemcpyDeviceToDevice, s));
-            VS_HIP(hipMemcpyAsync(b->rx_n, b->g_n + j, sizeof(int), hipMemcpyDeviceToDevice, s));
-        } else if (b->world == 1) {  // a one-rank ring: the record goes to itself
-            VS_HIP(hipMemcpyAsync(b->rx_kps, b->kps + (size_t)B * rec_k, kb, hipMemcpyDeviceToDevice, s));
-            VS_HIP(hipMemcpyAsync(b->rx_desc, b->desc + (size_t)B * rec_d, db, hipMemcpyDeviceToDevice, s));
-            VS_HIP(hipMemcpyAsync(b->rx_n, b->n + B, sizeof(int), hipMemcpyDeviceToDevice, s));
-        } else {
-            // ring: last record to rank + 1, the neighbour's from rank - 1 (three sends, three receives)
-            const int nxt = (b->rank + 1) % b->world, prv = (b->rank + b->world - 1) % b->world;
-            VS_RCCL(g_rccl.group_start());
-            VS_RCCL(g_rccl.send(b->kps + (size_t)B * rec_k, kb, kRcclChar, nxt, b->comm, s));
-            VS_RCCL(g_rccl.send(b->desc + (size_t)B * rec_d, db, kRcclChar, nxt, b->comm, s));
-            VS_RCCL(g_rccl.send(b->n + B, sizeof(int), kRcclChar, nxt, b->comm, s));
-            VS_RCCL(g_rccl.recv(b->rx_kps, kb, kRcclChar, prv, b->comm, s));
-            VS_RCCL(g_rccl.recv(b->rx_desc, db, kRcclChar, prv, b->comm, s));
-            VS_RCCL(g_rccl.recv(b->rx_n, sizeof(int), kRcclChar, prv, b->comm, s));
-            VS_RCCL(g_rccl.group_end());
-        }
-        if (b->rank > 0) {  // slot 0 <- rank - 1's last frame of this step
-            VS_HIP(hipMemcpyAsync(b->kps, b->rx_kps, kb, hipMemcpyDeviceToDevice, s));
-            VS_HIP(hipMemcpyAsync(b->desc, b->rx_desc, db, hipMemcpyDeviceToDevice, s));
-            VS_HIP(hipMemcpyAsync(b->n, b->rx_n, sizeof(int), hipMemcpyDeviceToDevice, s));
-        } else {  // slot 0 <- the previous step's global last frame (none before the first step)
-            VS_HIP(hipMemcpyAsync(b->kps, b->carry_kps, kb, hipMemcpyDeviceToDevice, s));
-            VS_HIP(hipMemcpyAsync(b->desc, b->carry_desc, db, hipMemcpyDeviceToDevice, s));
-            VS_HIP(hipMemcpyAsync(b->n, b->carry_n, sizeof(int), hipMemcpyDeviceToDevice, s));
-            VS_HIP(hipMemcpyAsync(b->carry_kps, b->rx_kps, kb, hipMemcpyDeviceToDevice, s));
-            VS_HIP(hipMemcpyAsync(b->carry_desc, b->rx_desc, db, hipMemcpyDeviceToDevice, s));
-            VS_HIP(hipMemcpyAsync(b->carry_n, b->rx_n, sizeof(int), hipMemcpyDeviceToDevice, s));
-        }
+    if (xchg) {  // slot 0 <- frame rank * B - 1 (batch_exchange.h, shared with the CPU loopback test)
+        vs_bx::Tables tb;
+        tb.B = B, tb.cap = cap, tb.rank = b->rank, tb.world = b->world, tb.gather = b->gather;
+        tb.kps = reinterpret_cast<uint8_t*>(b->kps), tb.desc = b->desc, tb.n = b->n;
+        tb.g_kps = reinterpret_cast<uint8_t*>(b->g_kps), tb.g_desc = b->g_desc, tb.g_n = b->g_n;
+        tb.rx_kps = reinterpret_cast<uint8_t*>(b->rx_kps), tb.rx_desc = b->rx_desc, tb.rx_n = b->rx_n;
+        tb.carry_kps = reinterpret_cast<uint8_t*>(b->carry_kps), tb.carry_desc = b->carry_desc, tb.carry_n = b->carry_n;
+        RcclTransport x(b->comm, s);
+        VS_CHECK(vs_bx::exchange(tb, x));
     }
     // the RANSAC seed of pair p is 42 + its processed-frame index (Slam.cpp:276)
     for (int p = 0; p < B; p++) b->h_seeds[p] = (uint32_t)(42 + frame_count0 + p);

@@ -92,6 +92,7 @@ _SIG = {
     "vs_batch_step_dev": (_I, [_P, _P, _P, _P, _I, _P, _P]),
     "vs_batch_features_dev": (_I, [_P, _P, _P, _P, _P]),
     "vs_batch_set_gather": (_I, [_P, _I]),
+    "vs_batch_exchange_loopback": (_I, [_I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
     "vs_spcf_write": (ctypes.c_int, [ctypes.c_char_p, _I, _P, _P, _P, _P, _I, _I]),
     "vs_spcf_write_dev": (_I, [_P, ctypes.c_char_p, _I, _P, _P, _P, _P, _I, _I, _P]),
     "vs_spcf_read": (_I, [ctypes.c_char_p, _I, _I, _P, _P, _P, _P, _P]),
@@ -176,6 +177,29 @@ def superpoint_onnx_desc_normalized(path):
     v = ctypes.c_int(-1)
     _check(lib.vs_superpoint_onnx_desc_normalized(os.fsencode(path), ctypes.byref(v)))
     return bool(v.value)
+
+
+def batch_exchange_loopback(world, kps, desc, n, gather=False):
+    """vs_batch_exchange_loopback (host only): kps [steps][world][B][cap] KEYPOINT_DTYPE, desc
+    [steps][world][B][cap][256] f32, n [steps][world][B] i32 -> (slot0_kps [steps][world][cap],
+    slot0_desc, slot0_n [steps][world], gathered (g_kps, g_desc, g_n) per [steps][world] or None)."""
+    lib = load_library()
+    kps = np.ascontiguousarray(kps, KEYPOINT_DTYPE)
+    desc = np.ascontiguousarray(desc, np.float32)
+    n = np.ascontiguousarray(n, np.int32)
+    steps, w, B, cap = kps.shape
+    assert w == world and desc.shape == (steps, world, B, cap, 256) and n.shape == (steps, world, B)
+    s0k = np.zeros((steps, world, cap), KEYPOINT_DTYPE)
+    s0d = np.zeros((steps, world, cap, 256), np.float32)
+    s0n = np.zeros((steps, world), np.int32)
+    g = None
+    if gather:
+        g = (np.zeros((steps, world, world * B, cap), KEYPOINT_DTYPE),
+             np.zeros((steps, world, world * B, cap, 256), np.float32), np.zeros((steps, world, world * B), np.int32))
+    _check(lib.vs_batch_exchange_loopback(world, B, cap, steps, int(bool(gather)), _ptr(kps), _ptr(desc), _ptr(n),
+                                          _ptr(s0k), _ptr(s0d), _ptr(s0n), *(tuple(_ptr(a) for a in g) if g else
+                                                                             (None, None, None))))
+    return s0k, s0d, s0n, g
 
 
 def superpoint_synth_weights():
