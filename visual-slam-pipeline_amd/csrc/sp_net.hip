@@ -648,8 +648,7 @@ __global__ __launch_bounds__(256, 2) void k_wino3(WinoArgs wa) {
     const float* __restrict__ wu = wa.wu;
     const float* __restrict__ bias = wa.bias;
     float* __restrict__ out = wa.out;
-    const float* __restrict__ w1a = wa.w1a;
-    const float* __restrict__ b1a = wa.b1a;
+    const float* __restrict__ w1a = wa.w1a;  // FUSE1A: [64][9 taps, bias, 0, 0], read as scalar loads
     const int in_cstride = wa.in_cstride, in_coff = wa.in_coff, cin = wa.cin, cout = wa.cout, cout_pad = wa.cout_pad;
     const int out_cstride = wa.out_cstride, out_coff = wa.out_coff, H = wa.H, W = wa.W, nbx = wa.nbx, nby = wa.nby;
     const int act = wa.act;
@@ -663,7 +662,6 @@ __global__ __launch_bounds__(256, 2) void k_wino3(WinoArgs wa) {
     __shared__ __attribute__((aligned(16))) float s_v[2][4][CK][NT][4];
     __shared__ __attribute__((aligned(16))) float s_u[2][16][CK][64];
     __shared__ float s_g[FUSE1A ? GX * GY : 1];
-    __shared__ __attribute__((aligned(16))) float s_w1a[FUSE1A ? 64 * 12 : 4];  // [channel][9 taps, bias, 0, 0]
 
     const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63, li = lane & 15, lk = lane >> 4;
     const int th = wv & 1, ch = wv >> 1;
@@ -693,10 +691,6 @@ __global__ __launch_bounds__(256, 2) void k_wino3(WinoArgs wa) {
             const int sy = y0 - 2 + yy, sx = x0 - 2 + xx;
             s_g[i] = (sy >= 0 && sy < H && sx >= 0 && sx < W) ? g[(size_t)sy * W + sx] : 0.0f;
         }
-        for (int i = tid; i < 64 * 12; i += 256) {
-            const int c = i / 12, k = i - c * 12;
-            s_w1a[i] = k < 9 ? w1a[k * 64 + c] : k == 9 ? b1a[c] : 0.0f;
-        }
         __syncthreads();
 #pragma unroll
         for (int k = 0; k < 9; k++) gnb[k] = own_px ? s_g[(ppy + k / 3) * GX + ppx + k % 3] : 0.0f;
@@ -706,14 +700,16 @@ __global__ __launch_bounds__(256, 2) void k_wino3(WinoArgs wa) {
     // chunk's weights in ru (loaded one chunk ahead)
     f32x4 rx[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
     f32x4 ru[4];
-    auto fetch_x = [&](auto sl_c, int c) {
+    // G (guarded): the chunk index may run past the last chunk (the pipeline's tail); the steady
+    // state below runs unguarded instantiations (no per-chunk branches around the staging code)
+    auto fetch_x = [&](auto sl_c, auto g_c, int c) {
         constexpr int sl = decltype(sl_c)::value;
         if constexpr (!FUSE1A) {
-            if (pin && c < nchunk) rx[sl] = *reinterpret_cast<const f32x4*>(src + (cb + c) * CK);
+            if (pin && (!decltype(g_c)::value || c < nchunk)) rx[sl] = *reinterpret_cast<const f32x4*>(src + (cb + c) * CK);
         }
     };
-    auto fetch_u = [&](int c) {
-        if (c >= nchunk) return;
+    auto fetch_u = [&](auto g_c, int c) {
+        if (decltype(g_c)::value && c >= nchunk) return;
 #pragma unroll
         for (int j = 0; j < 4; j++) {
             const int idx = tid + 256 * j, xi = idx >> 6, cc = (idx >> 4) & 3, q = idx & 15;
@@ -721,14 +717,20 @@ __global__ __launch_bounds__(256, 2) void k_wino3(WinoArgs wa) {
         }
     };
     // chunk c's patch -> s_x[c & 1] (fused: conv1a of its 4 channels at this pixel, 0 outside the image)
-    auto put_x = [&](auto sl_c, int c) {
+    auto put_x = [&](auto sl_c, auto g_c, int c) {
         constexpr int sl = decltype(sl_c)::value;
-        if (!own_px || c >= nchunk) return;
+        if (decltype(g_c)::value && c >= nchunk) return;
         if constexpr (FUSE1A) {
+            // the chunk's 4 x (9 taps + bias) are wave-uniform: scalar loads into SGPRs, v_fma_f32 with an
+            // SGPR operand (no LDS staging, no operand moves); same fmaf chain as before
+            const f32x4* wp = reinterpret_cast<const f32x4*>(w1a + (size_t)(c * CK) * 12);
+            f32x4 q[3 * CK];
+#pragma unroll
+            for (int i = 0; i < 3 * CK; i++) q[i] = wp[i];
+            if (!own_px) return;
 #pragma unroll
             for (int cc = 0; cc < CK; cc++) {
-                const f32x4* wp = reinterpret_cast<const f32x4*>(&s_w1a[(c * CK + cc) * 12]);
-                const f32x4 q0 = wp[0], q1 = wp[1], q2 = wp[2];
+                const f32x4 q0 = q[3 * cc], q1 = q[3 * cc + 1], q2 = q[3 * cc + 2];
                 const float wk[9] = {q0[0], q0[1], q0[2], q0[3], q1[0], q1[1], q1[2], q1[3], q2[0]};
                 float a = q2[1];
 #pragma unroll
@@ -736,6 +738,7 @@ __global__ __launch_bounds__(256, 2) void k_wino3(WinoArgs wa) {
                 s_x[sl][cc][tid] = pin ? (a > 0.0f ? a : 0.0f) : 0.0f;
             }
         } else {
+            if (!own_px) return;
 #pragma unroll
             for (int cc = 0; cc < CK; cc++) {
                 const float v = pin ? rx[sl][cc] : 0.0f;
@@ -744,9 +747,9 @@ __global__ __launch_bounds__(256, 2) void k_wino3(WinoArgs wa) {
         }
     };
     // chunk c's weights -> s_u[c & 1] (channel cc's 32-column halves swapped when cc is odd)
-    auto put_u = [&](auto sl_c, int c) {
+    auto put_u = [&](auto sl_c, auto g_c, int c) {
         constexpr int sl = decltype(sl_c)::value;
-        if (c >= nchunk) return;
+        if (decltype(g_c)::value && c >= nchunk) return;
 #pragma unroll
         for (int j = 0; j < 4; j++) {
             const int idx = tid + 256 * j, xi = idx >> 6, cc = (idx >> 4) & 3, q = idx & 15;
@@ -756,10 +759,12 @@ __global__ __launch_bounds__(256, 2) void k_wino3(WinoArgs wa) {
     // B^T d B of chunk c (s_x[c & 1] -> s_v[c & 1]) on all 64 lanes: lane = (tile t, channel cc)
     // of a channel pair, and the wave's half (wave-uniform: no divergence) takes V rows 2 half and
     // 2 half + 1, which need input rows half .. half + 2 only
-    auto transform = [&](auto sl_c, int c) {
+    auto transform = [&](auto sl_c, auto g_c, int c) {
         constexpr int sl = decltype(sl_c)::value;
-        if (c >= nchunk) return;
-        const int t = lane & 31, cc = 2 * (wv & 1) + (lane >> 5), half = wv >> 1, tr = t >> 3, tc = t & 7;
+        if (decltype(g_c)::value && c >= nchunk) return;
+        // half is wave-uniform: readfirstlane makes the branch below a scalar branch (no exec masks)
+        const int t = lane & 31, cc = 2 * (wv & 1) + (lane >> 5), tr = t >> 3, tc = t & 7;
+        const int half = __builtin_amdgcn_readfirstlane(wv >> 1);
         const float* xp = &s_x[sl][cc][(2 * tr + half) * PX + 2 * tc];
         float e[3][4];
 #pragma unroll
@@ -797,16 +802,18 @@ __global__ __launch_bounds__(256, 2) void k_wino3(WinoArgs wa) {
 
     // prologue: V / U of chunk 0 and the patch of chunk 1 in LDS, chunk 1's weights and chunk 2's
     // patch in registers
-    fetch_x(S0{}, 0);
-    fetch_x(S1{}, 1);
-    fetch_u(0);
-    put_x(S0{}, 0);
-    put_x(S1{}, 1);
-    put_u(S0{}, 0);
-    fetch_u(1);
+    using GY_ = std::true_type;
+    using GN_ = std::false_type;
+    fetch_x(S0{}, GY_{}, 0);
+    fetch_x(S1{}, GY_{}, 1);
+    fetch_u(GY_{}, 0);
+    put_x(S0{}, GY_{}, 0);
+    put_x(S1{}, GY_{}, 1);
+    put_u(S0{}, GY_{}, 0);
+    fetch_u(GY_{}, 1);
     __syncthreads();
-    transform(S0{}, 0);
-    fetch_x(S0{}, 2);
+    transform(S0{}, GY_{}, 0);
+    fetch_x(S0{}, GY_{}, 2);
     __syncthreads();
     const int ucol = (C32 ? 0 : 32 * ch) ^ (32 * (lk & 1));  // this lane's 32-column half in s_u (swizzled)
     f32x4 opa[2];      // A operands of a row (4 elements)
@@ -833,32 +840,32 @@ __global__ __launch_bounds__(256, 2) void k_wino3(WinoArgs wa) {
         }
     };
     // chunk k (P = k & 1): slots / buffers of chunk k + 1 are P ^ 1, of chunk k + 2 are P
-    auto chunk = [&](auto par, int k) {
+    auto chunk = [&](auto par, auto g_c, int k) {
         constexpr int P = decltype(par)::value;
         using SP = std::integral_constant<int, P>;
         using SN = std::integral_constant<int, P ^ 1>;
         if constexpr (C32) {
             read_row(P, 2 * ch, 0);
             read_row(P, 2 * ch + 1, 1);
-            put_u(SN{}, k + 1);
-            fetch_u(k + 2);
-            fetch_x(SN{}, k + 3);
+            put_u(SN{}, g_c, k + 1);
+            fetch_u(g_c, k + 2);
+            fetch_x(SN{}, g_c, k + 3);
             __builtin_amdgcn_sched_barrier(0);
             mfma_row_c32(0, 0);
             __builtin_amdgcn_sched_barrier(0);
-            put_x(SP{}, k + 2);
+            put_x(SP{}, g_c, k + 2);
             __builtin_amdgcn_sched_barrier(0);
             mfma_row_c32(1, 1);
             __builtin_amdgcn_sched_barrier(0);
-            transform(SN{}, k + 1);
+            transform(SN{}, g_c, k + 1);
             __syncthreads();
             return;
         }
         read_row(P, 0, 0);
         read_row(P, 1, 1);
-        put_u(SN{}, k + 1);    // loaded during chunk k - 1; its buffer's last reader was chunk k - 1
-        fetch_u(k + 2);
-        fetch_x(SN{}, k + 3);  // slot of chunk k + 1, whose patch went to LDS during chunk k - 1
+        put_u(SN{}, g_c, k + 1);    // loaded during chunk k - 1; its buffer's last reader was chunk k - 1
+        fetch_u(g_c, k + 2);
+        fetch_x(SN{}, g_c, k + 3);  // slot of chunk k + 1, whose patch went to LDS during chunk k - 1
         __builtin_amdgcn_sched_barrier(0);
         mfma_row(0, 0);
         __builtin_amdgcn_sched_barrier(0);
@@ -867,18 +874,25 @@ __global__ __launch_bounds__(256, 2) void k_wino3(WinoArgs wa) {
         mfma_row(1, 1);
         __builtin_amdgcn_sched_barrier(0);
         read_row(P, 3, 1);
-        put_x(SP{}, k + 2);
+        put_x(SP{}, g_c, k + 2);
         __builtin_amdgcn_sched_barrier(0);
         mfma_row(2, 0);
         __builtin_amdgcn_sched_barrier(0);
-        transform(SN{}, k + 1);
+        transform(SN{}, g_c, k + 1);
         __builtin_amdgcn_sched_barrier(0);
         mfma_row(3, 1);
         __syncthreads();  // chunk k + 1's V / U and chunk k + 2's patch complete; chunk k's buffers free
     };
-    for (int k = 0; k < nchunk; k += 2) {
-        chunk(S0{}, k);
-        if (k + 1 < nchunk) chunk(S1{}, k + 1);
+    // steady state: a chunk pair (k, k + 1) touches chunks up to k + 4, so it runs unguarded while
+    // k + 4 < nchunk; the tail pairs keep the guards
+    int k = 0;
+    for (; k + 4 < nchunk; k += 2) {
+        chunk(S0{}, GN_{}, k);
+        chunk(S1{}, GN_{}, k + 1);
+    }
+    for (; k < nchunk; k += 2) {
+        chunk(S0{}, GY_{}, k);
+        if (k + 1 < nchunk) chunk(S1{}, GY_{}, k + 1);
     }
 
     // A^T M A per (tile, output channel); C/D: cout = lane % 16, tile row 4 (lane / 16) + reg.
@@ -1113,7 +1127,7 @@ int launch_wino(const DevLayer& L, const float* in, int in_cstride, int in_coff,
                 int out_coff, int B, int H, int W, hipStream_t s, const DevLayer* L1a) {
     if (!L.wu || L.cin % 4 != 0 || L.cout_pad % 64 != 0 || L.cout % 4 != 0 || out_cstride % 4 || out_coff % 4 ||
         (!FUSE1A && (in_cstride % 4 || in_coff % 4)) ||
-        (FUSE1A && (!L1a || L1a->cout != 64 || L.cin != 64)) || (POOL && ((H | W) & 1))) {
+        (FUSE1A && (!L1a || L1a->cout != 64 || L.cin != 64 || !L1a->w1a_rows)) || (POOL && ((H | W) & 1))) {
         set_error("conv3 (Winograd): unsupported geometry");
         return VS_ERR_ARG;
     }
@@ -1132,8 +1146,8 @@ int launch_wino(const DevLayer& L, const float* in, int in_cstride, int in_coff,
     a.B = B;
     a.H = H;
     a.W = W;
-    a.w1a = L1a ? L1a->w : nullptr;
-    a.b1a = L1a ? L1a->b : nullptr;
+    a.w1a = L1a ? L1a->w1a_rows : nullptr;  // [64][9 taps, bias, 0, 0]
+    a.b1a = nullptr;
     a.act = 1;  // every SuperPoint 3x3 conv is followed by ReLU
     return wino3_launch(a, POOL, FUSE1A, s);
 }

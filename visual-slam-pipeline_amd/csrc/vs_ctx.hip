@@ -172,6 +172,15 @@ static int upload_layer(DevLayer& D, int cin, int cout, int cout_pad, int k, con
     VS_HIP(hipMalloc(&D.b, b.size() * sizeof(float)));
     VS_HIP(hipMemcpy(D.w, w.data(), w.size() * sizeof(float), hipMemcpyHostToDevice));
     VS_HIP(hipMemcpy(D.b, b.data(), b.size() * sizeof(float), hipMemcpyHostToDevice));
+    if (k == 3 && cin == 1) {  // conv1a: [cout][9 taps, bias, 0, 0]
+        std::vector<float> rows((size_t)cout * 12, 0.0f);
+        for (int c = 0; c < cout; c++) {
+            for (int t = 0; t < 9; t++) rows[(size_t)c * 12 + t] = w[(size_t)t * cout_pad + c];
+            rows[(size_t)c * 12 + 9] = b[c];
+        }
+        VS_HIP(hipMalloc(&D.w1a_rows, rows.size() * sizeof(float)));
+        VS_HIP(hipMemcpy(D.w1a_rows, rows.data(), rows.size() * sizeof(float), hipMemcpyHostToDevice));
+    }
     if (k == 3 && cin % 4 == 0) {
         const std::vector<float> u = winograd_weights(w.data(), cin, cout_pad);
         VS_HIP(hipMalloc(&D.wu, u.size() * sizeof(float)));
@@ -385,6 +394,7 @@ void vs_destroy(vs_ctx* ctx) {
         if (L.w) (void)hipFree(L.w);
         if (L.b) (void)hipFree(L.b);
         if (L.wu) (void)hipFree(L.wu);
+        if (L.w1a_rows) (void)hipFree(L.w1a_rows);
     }
     if (ctx->head_a.w) (void)hipFree(ctx->head_a.w);
     if (ctx->head_a.b) (void)hipFree(ctx->head_a.b);

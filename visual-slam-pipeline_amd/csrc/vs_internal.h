@@ -74,6 +74,9 @@ struct DevLayer {
     // 3x3 layers with cin % 4 == 0: the Winograd F(2x2, 3x3) transformed weights U = G g G^T,
     // [16][cin][cout_pad] (transform element xi = 4 i + j), computed in fp64 and rounded once
     float* wu = nullptr;
+    // conv1a (cin 1, 3x3): per output channel its 9 taps, bias, 0, 0 ([cout][12]) — read by the fused
+    // conv1 kernel as wave-uniform (scalar) loads
+    float* w1a_rows = nullptr;
 };
 
 // ---- growable device scratch -------------------------------------------------------------
