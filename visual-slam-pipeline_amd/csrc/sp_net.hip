@@ -640,6 +640,12 @@ __global__ __launch_bounds__(256, CKT == 4 ? (MB == 1 ? 4 : 3) : 2) void k_conv3
 // SPLIT: input-channel split-K (WinoArgs::part / splits, MiDaS's 8^2-16^2 decoder convs); a template
 // parameter so that the unsplit instantiations keep their code (runtime split support had cost them
 // 5-13 %, r03an).
+#ifndef VS_WINO_SCHED
+#define VS_WINO_SCHED 1  // main-loop schedule (A/B builds): 0 fenced segments, 1 interleaved, 2 free
+#endif
+#ifndef VS_WINO_PRIO
+#define VS_WINO_PRIO 0   // 1: s_setprio(1) over each MFMA row region (A/B)
+#endif
 template <bool POOL, bool FUSE1A, bool C32 = false, bool SPLIT = false>
 __global__ __launch_bounds__(256, 2) void k_wino3(WinoArgs wa) {
     static_assert(!(C32 && (POOL || FUSE1A)), "C32 is the plain (MiDaS) variant");
@@ -658,7 +664,10 @@ __global__ __launch_bounds__(256, 2) void k_wino3(WinoArgs wa) {
     typedef float f32x2 __attribute__((ext_vector_type(2)));
     using S0 = std::integral_constant<int, 0>;
     using S1 = std::integral_constant<int, 1>;
-    __shared__ __attribute__((aligned(16))) float s_x[2][CK][NP];
+    // one slot per thread (NP = 180 patch pixels used): every thread stores its chunk value without a
+    // branch (threads past the patch write slots nobody reads), so the staging code has no basic-block
+    // boundaries and interleaves with the MFMAs
+    __shared__ __attribute__((aligned(16))) float s_x[2][CK][256];
     __shared__ __attribute__((aligned(16))) float s_v[2][4][CK][NT][4];
     __shared__ __attribute__((aligned(16))) float s_u[2][16][CK][64];
     __shared__ float s_g[FUSE1A ? GX * GY : 1];
@@ -705,7 +714,9 @@ __global__ __launch_bounds__(256, 2) void k_wino3(WinoArgs wa) {
     auto fetch_x = [&](auto sl_c, auto g_c, int c) {
         constexpr int sl = decltype(sl_c)::value;
         if constexpr (!FUSE1A) {
-            if (pin && (!decltype(g_c)::value || c < nchunk)) rx[sl] = *reinterpret_cast<const f32x4*>(src + (cb + c) * CK);
+            // src is clamped in the image (pin == false: pixel 0 of the frame), so the load needs no
+            // branch; put_x zeroes what lies outside
+            if (!decltype(g_c)::value || c < nchunk) rx[sl] = *reinterpret_cast<const f32x4*>(src + (cb + c) * CK);
         }
     };
     auto fetch_u = [&](auto g_c, int c) {
@@ -727,7 +738,6 @@ __global__ __launch_bounds__(256, 2) void k_wino3(WinoArgs wa) {
             f32x4 q[3 * CK];
 #pragma unroll
             for (int i = 0; i < 3 * CK; i++) q[i] = wp[i];
-            if (!own_px) return;
 #pragma unroll
             for (int cc = 0; cc < CK; cc++) {
                 const f32x4 q0 = q[3 * cc], q1 = q[3 * cc + 1], q2 = q[3 * cc + 2];
@@ -738,7 +748,6 @@ __global__ __launch_bounds__(256, 2) void k_wino3(WinoArgs wa) {
                 s_x[sl][cc][tid] = pin ? (a > 0.0f ? a : 0.0f) : 0.0f;
             }
         } else {
-            if (!own_px) return;
 #pragma unroll
             for (int cc = 0; cc < CK; cc++) {
                 const float v = pin ? rx[sl][cc] : 0.0f;
@@ -762,9 +771,8 @@ __global__ __launch_bounds__(256, 2) void k_wino3(WinoArgs wa) {
     auto transform = [&](auto sl_c, auto g_c, int c) {
         constexpr int sl = decltype(sl_c)::value;
         if (decltype(g_c)::value && c >= nchunk) return;
-        // half is wave-uniform: readfirstlane makes the branch below a scalar branch (no exec masks)
         const int t = lane & 31, cc = 2 * (wv & 1) + (lane >> 5), tr = t >> 3, tc = t & 7;
-        const int half = __builtin_amdgcn_readfirstlane(wv >> 1);
+        const int half = wv >> 1;
         const float* xp = &s_x[sl][cc][(2 * tr + half) * PX + 2 * tc];
         float e[3][4];
 #pragma unroll
@@ -776,19 +784,18 @@ __global__ __launch_bounds__(256, 2) void k_wino3(WinoArgs wa) {
             e[i][2] = p1[0];
             e[i][3] = p1[1];
         }
-        float ua[4], ub[4];  // rows 2 half, 2 half + 1 of B^T d
-        if (half == 0) {
+        // rows 2 half, 2 half + 1 of B^T d without a branch (the selects are wave-uniform):
+        //   half 0: ua = d0 - d2 = e0 - e2, ub = d1 + d2 = e1 + e2
+        //   half 1: ua = d2 - d1 = e1 - e0, ub = d1 - d3 = e0 - e2
+        // i.e. ua = y - x, ub = r + sg e2 (fmaf(+-1, e2, r) == r +- e2 exactly)
+        const bool h1 = half != 0;
+        const float sg = h1 ? -1.0f : 1.0f;
+        float ua[4], ub[4];
 #pragma unroll
-            for (int j = 0; j < 4; j++) {
-                ua[j] = e[0][j] - e[2][j];  // d0 - d2
-                ub[j] = e[1][j] + e[2][j];  // d1 + d2
-            }
-        } else {
-#pragma unroll
-            for (int j = 0; j < 4; j++) {
-                ua[j] = e[1][j] - e[0][j];  // d2 - d1
-                ub[j] = e[0][j] - e[2][j];  // d1 - d3
-            }
+        for (int j = 0; j < 4; j++) {
+            const float y = h1 ? e[1][j] : e[0][j], x = h1 ? e[0][j] : e[2][j], r = h1 ? e[0][j] : e[1][j];
+            ua[j] = y - x;
+            ub[j] = __builtin_fmaf(sg, e[2][j], r);
         }
         *reinterpret_cast<f32x4*>(&s_v[sl][2 * half][cc][t][0]) =
             f32x4{ua[0] - ua[2], ua[1] + ua[2], ua[2] - ua[1], ua[1] - ua[3]};
@@ -861,6 +868,7 @@ __global__ __launch_bounds__(256, 2) void k_wino3(WinoArgs wa) {
             __syncthreads();
             return;
         }
+#if VS_WINO_SCHED == 0
         read_row(P, 0, 0);
         read_row(P, 1, 1);
         put_u(SN{}, g_c, k + 1);    // loaded during chunk k - 1; its buffer's last reader was chunk k - 1
@@ -881,6 +889,65 @@ __global__ __launch_bounds__(256, 2) void k_wino3(WinoArgs wa) {
         transform(SN{}, g_c, k + 1);
         __builtin_amdgcn_sched_barrier(0);
         mfma_row(3, 1);
+#elif VS_WINO_SCHED == 1
+        // interleaved: each row's 8 MFMAs carry the staging / conv1a / transform work between them
+        // (sched_group_barrier: MFMA=0x8 VALU=0x2 VMEM=0x10 DS_READ=0x100 DS_WRITE=0x200)
+        read_row(P, 0, 0);
+        read_row(P, 1, 1);
+        __builtin_amdgcn_sched_barrier(0);
+        if (VS_WINO_PRIO) __builtin_amdgcn_s_setprio(1);
+        mfma_row(0, 0);
+        put_u(SN{}, g_c, k + 1);
+        fetch_u(g_c, k + 2);
+        fetch_x(SN{}, g_c, k + 3);
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+            __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);
+            __builtin_amdgcn_sched_group_barrier(0x010, 1, 0);
+            __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        read_row(P, 2, 0);
+        mfma_row(1, 1);
+        put_x(SP{}, g_c, k + 2);
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 1);
+            __builtin_amdgcn_sched_group_barrier(0x100, 1, 1);
+            __builtin_amdgcn_sched_group_barrier(0x002, 6, 1);
+            __builtin_amdgcn_sched_group_barrier(0x200, 1, 1);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        read_row(P, 3, 1);
+        mfma_row(2, 0);
+        transform(SN{}, g_c, k + 1);
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 2);
+            __builtin_amdgcn_sched_group_barrier(0x100, 2, 2);
+            __builtin_amdgcn_sched_group_barrier(0x002, 3, 2);
+            __builtin_amdgcn_sched_group_barrier(0x200, 1, 2);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        mfma_row(3, 1);
+        if (VS_WINO_PRIO) __builtin_amdgcn_s_setprio(0);
+#else
+        // no scheduling fences: the compiler's own interleave
+        read_row(P, 0, 0);
+        read_row(P, 1, 1);
+        put_u(SN{}, g_c, k + 1);
+        fetch_u(g_c, k + 2);
+        fetch_x(SN{}, g_c, k + 3);
+        mfma_row(0, 0);
+        read_row(P, 2, 0);
+        mfma_row(1, 1);
+        read_row(P, 3, 1);
+        put_x(SP{}, g_c, k + 2);
+        mfma_row(2, 0);
+        transform(SN{}, g_c, k + 1);
+        mfma_row(3, 1);
+#endif
         __syncthreads();  // chunk k + 1's V / U and chunk k + 2's patch complete; chunk k's buffers free
     };
     // steady state: a chunk pair (k, k + 1) touches chunks up to k + 4, so it runs unguarded while
