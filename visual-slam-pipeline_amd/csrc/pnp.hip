@@ -28,6 +28,10 @@ using namespace vs_pnp;
 
 constexpr int kPnpMaxIters = VS_PNP_MAX_ITERS;
 
+#ifndef VS_PNP_JACOBI
+#define VS_PNP_JACOBI 1  // 0: the round-2 single-copy Jacobi (shuffled angles, two barriers per round)
+#endif
+
 #ifdef VS_PNP_PROFILE
 // k_pnp_hyp phase cycle counters (profiling build only: make -C visual-slam-pipeline_amd prof)
 __device__ unsigned long long g_pnp_cycles[16];  // 0-5 k_pnp_hyp, 6-7 k_pnp_ransac, 8-12 its LM split
@@ -227,7 +231,13 @@ __global__ __launch_bounds__(64) void k_pnp_hyp(const float* __restrict__ obj_al
                                                 const int* __restrict__ off, double fx, double fy, double cx, double cy,
                                                 int niters0, float thr2, int min_inliers, PnpHyp H) {
     crit_prio();
+#if VS_PNP_JACOBI == 1
+    __shared__ double sAb[2][144], sVb[2][144];  // ping-pong matrices: one barrier per Jacobi round
+    double* sA = sAb[0];
+    double* sV = sVb[0];
+#else
     __shared__ double sA[144], sV[144];
+#endif
     __shared__ double sX[15], sUV[10], sAl[5][4], sCw[4][3];
     __shared__ double sTot, sOff, sErr[3], sRt[3][12];
     __shared__ int sOk, sPerm[12];
@@ -276,6 +286,83 @@ __global__ __launch_bounds__(64) void k_pnp_hyp(const float* __restrict__ obj_al
         __syncthreads();
         PNP_T(1);
         const double total = sTot;
+#if VS_PNP_JACOBI == 1
+        // Round-robin Jacobi with the matrices ping-ponged between two LDS copies: every lane of
+        // 0..35 reads its 2 x 2 block (pair a rows i0 < i1, pair b columns j0 < j1), its V entries
+        // (rows 2a, 2a + 1 at the block's columns) and the two diagonal blocks of its pairs from the
+        // round's copy, computes both angles itself (no shuffles; the same inputs as the diagonal
+        // lane's, so the same angles), rotates (column b, then row a, as the sequential statement)
+        // and writes every value to the other copy; one barrier per round.  Bit-identical to
+        // sym_eig_rr<12>.
+        {
+            const int ba = lane / 6, bb = lane % 6;
+            const bool blk = lane < 36;
+            int pk[11];  // the lane's round pairs, packed 4 bits each (rounds unrolled: static indices)
+#pragma unroll
+            for (int r = 0; r < 11; r++) {
+                int a0, a1, b0, b1;
+                rr_pair(12, r, ba, a0, a1);
+                rr_pair(12, r, bb, b0, b1);
+                pk[r] = a0 | a1 << 4 | b0 << 8 | b1 << 12;
+            }
+            int cur = 0;
+            for (int sweep = 0; sweep < 30; sweep++) {
+                if (lane == 0) {
+                    const double* A = sAb[cur];
+                    double o = 0;
+                    for (int p = 0; p < 12; p++)
+                        for (int q = p + 1; q < 12; q++) o += A[p * 12 + q] * A[p * 12 + q];
+                    sOff = o;
+                }
+                __syncthreads();
+                if (!(sOff > 1e-32 * total)) break;
+#pragma unroll
+                for (int r = 0; r < 11; r++) {
+                    const double* A = sAb[cur];
+                    const double* V = sVb[cur];
+                    double* An = sAb[cur ^ 1];
+                    double* Vn = sVb[cur ^ 1];
+                    if (blk) {
+                        const int i0 = pk[r] & 15, i1 = (pk[r] >> 4) & 15, j0 = (pk[r] >> 8) & 15, j1 = pk[r] >> 12;
+                        double x00 = A[i0 * 12 + j0], x01 = A[i0 * 12 + j1], x10 = A[i1 * 12 + j0], x11 = A[i1 * 12 + j1];
+                        const double p0 = V[(2 * ba) * 12 + j0], q0 = V[(2 * ba) * 12 + j1];
+                        const double p1 = V[(2 * ba + 1) * 12 + j0], q1 = V[(2 * ba + 1) * 12 + j1];
+                        double ca = 1.0, sa = 0.0, cb = 1.0, sb = 0.0;
+                        const bool acta = jacobi_angle(A[i0 * 12 + i0], A[i1 * 12 + i1], A[i0 * 12 + i1], ca, sa);
+                        const bool actb = jacobi_angle(A[j0 * 12 + j0], A[j1 * 12 + j1], A[j0 * 12 + j1], cb, sb);
+                        if (actb) {
+                            const double y00 = cb * x00 - sb * x01, y01 = sb * x00 + cb * x01;
+                            const double y10 = cb * x10 - sb * x11, y11 = sb * x10 + cb * x11;
+                            x00 = y00;
+                            x01 = y01;
+                            x10 = y10;
+                            x11 = y11;
+                        }
+                        if (acta) {
+                            const double y00 = ca * x00 - sa * x10, y10 = sa * x00 + ca * x10;
+                            const double y01 = ca * x01 - sa * x11, y11 = sa * x01 + ca * x11;
+                            x00 = y00;
+                            x01 = y01;
+                            x10 = y10;
+                            x11 = y11;
+                        }
+                        An[i0 * 12 + j0] = x00;
+                        An[i0 * 12 + j1] = x01;
+                        An[i1 * 12 + j0] = x10;
+                        An[i1 * 12 + j1] = x11;
+                        Vn[(2 * ba) * 12 + j0] = actb ? cb * p0 - sb * q0 : p0;
+                        Vn[(2 * ba) * 12 + j1] = actb ? sb * p0 + cb * q0 : q0;
+                        Vn[(2 * ba + 1) * 12 + j0] = actb ? cb * p1 - sb * q1 : p1;
+                        Vn[(2 * ba + 1) * 12 + j1] = actb ? sb * p1 + cb * q1 : q1;
+                    }
+                    cur ^= 1;
+                    __syncthreads();
+                }
+            }
+            sA = sAb[cur];
+            sV = sVb[cur];
+        }
+#else
         for (int sweep = 0; sweep < 30; sweep++) {
             if (lane == 0) {
                 double o = 0;
@@ -363,6 +450,7 @@ __global__ __launch_bounds__(64) void k_pnp_hyp(const float* __restrict__ obj_al
                 __syncthreads();
             }
         }
+#endif
         PNP_T(2);
         // eigenvalues in descending order, columns of V swapped along (sym_eig_rr's selection
         // sort): lane 0 runs the sort on the eigenvalues and a column index, the wave moves the
@@ -433,7 +521,11 @@ __global__ __launch_bounds__(64) void k_pnp_hyp(const float* __restrict__ obj_al
             for (int i = 0; i < 10; i++) uv[i] = i < 2 * m ? sUV[i] : 0.0;
             epnp_L_rho(sV, cw, v, L, rho);
             double R[9], t[3];
-            sErr[lane] = epnp_variant<5>(lane, L, rho, v, al, X, uv, m, K, R, t);
+            // the three approximations as one code path on lanes 0..2 (pnp_solvers.h
+            // epnp_betas_init_uniform: bit-identical to epnp_variant's divergent solves)
+            double be[4];
+            epnp_betas_init_uniform(lane, L, rho, be);
+            sErr[lane] = epnp_refine<5>(be, L, rho, v, al, X, uv, m, K, R, t);
             for (int k = 0; k < 9; k++) sRt[lane][k] = R[k];
             for (int k = 0; k < 3; k++) sRt[lane][9 + k] = t[k];
         }

@@ -531,11 +531,8 @@ VS_HD inline void epnp_L_rho(const double* um, const double cw[4][3], double v[4
 // MAXN bounds n at compile time: the point loops run to MAXN with an i < n guard (the same
 // operations in the same order), so on the device (MAXN = 5) they unroll and the arrays stay in
 // registers instead of scratch.
-template <int MAXN>
-VS_HD inline double epnp_variant(int s, const double L[6][10], const double rho[6], const double v[4][12],
-                                 const double (*alphas)[4], const double* X, const double* uv, int n, const Cam& K,
-                                 double* R, double* t) {
-    double be[4];
+// The initial betas of approximation s (least squares on the selected L columns).
+VS_HD inline void epnp_betas_init(int s, const double L[6][10], const double rho[6], double be[4]) {
     if (s == 0) {  // N = 4: B11 B12 B13 B14
         double A[24], b[6], x[4];
         for (int j = 0; j < 6; j++) {
@@ -602,6 +599,55 @@ VS_HD inline double epnp_variant(int s, const double L[6][10], const double rho[
         be[2] = b0 ? x[3] / b0 : 0.0;
         be[3] = 0.0;
     }
+}
+
+// The same initial betas with one lstsq<6, 5> for every s (the selected columns first, zero columns
+// after them): Householder QR skips a zero column (nrm == 0), leaves it zero (d = 0 in every
+// update), and back substitution gives it x = 0 and subtracts exact zeros for it, so the result is
+// bit-identical to epnp_betas_init's lstsq<6, N>; on the device the three approximations then run
+// the same code on three lanes instead of three divergent solves.
+VS_HD inline void epnp_betas_init_uniform(int s, const double L[6][10], const double rho[6], double be[4]) {
+    double A[30], b[6], x[5];
+    const int c3 = s == 0 ? 3 : 2, c4 = s == 0 ? 6 : 3;  // s = 0: L0 L1 L3 L6; s = 1: L0 L1 L2; s = 2: L0..L4
+    const int ncol = s == 0 ? 4 : s == 1 ? 3 : 5;
+    for (int j = 0; j < 6; j++) {
+        A[j * 5 + 0] = L[j][0];
+        A[j * 5 + 1] = L[j][1];
+        A[j * 5 + 2] = L[j][c3 == 3 ? 3 : 2];
+        A[j * 5 + 3] = ncol > 3 ? L[j][c4] : 0.0;
+        A[j * 5 + 4] = ncol > 4 ? L[j][4] : 0.0;
+        b[j] = rho[j];
+    }
+    lstsq<6, 5>(A, b, x);
+    if (s == 0) {
+        const double sg = x[0] < 0 ? -1.0 : 1.0;
+        const double b0 = sqrt(sg * x[0]);
+        be[0] = b0;
+        be[1] = b0 ? (sg * x[1]) / b0 : 0.0;
+        be[2] = b0 ? (sg * x[2]) / b0 : 0.0;
+        be[3] = b0 ? (sg * x[3]) / b0 : 0.0;
+    } else {
+        double b0, b1;
+        if (x[0] < 0) {
+            b0 = sqrt(-x[0]);
+            b1 = (x[2] < 0) ? sqrt(-x[2]) : 0.0;
+        } else {
+            b0 = sqrt(x[0]);
+            b1 = (x[2] > 0) ? sqrt(x[2]) : 0.0;
+        }
+        if (x[1] < 0) b0 = -b0;
+        be[0] = b0;
+        be[1] = b1;
+        be[2] = (s == 2 && b0) ? x[3] / b0 : 0.0;
+        be[3] = 0.0;
+    }
+}
+
+// Gauss-Newton on the betas, then the pose by Kabsch; returns the mean reprojection error.
+template <int MAXN>
+VS_HD inline double epnp_refine(double be[4], const double L[6][10], const double rho[6], const double v[4][12],
+                                const double (*alphas)[4], const double* X, const double* uv, int n, const Cam& K,
+                                double* R, double* t) {
     for (int it = 0; it < 5; it++) {  // Gauss-Newton on the 6 distance constraints
         double A[24], b[6], x[4];
         for (int j = 0; j < 6; j++) {
@@ -664,6 +710,15 @@ VS_HD inline double epnp_variant(int s, const double L[6][10], const double rho[
         err += sqrt(du * du + dvv * dvv);
     }
     return err / n;
+}
+
+template <int MAXN>
+VS_HD inline double epnp_variant(int s, const double L[6][10], const double rho[6], const double v[4][12],
+                                 const double (*alphas)[4], const double* X, const double* uv, int n, const Cam& K,
+                                 double* R, double* t) {
+    double be[4];
+    epnp_betas_init(s, L, rho, be);
+    return epnp_refine<MAXN>(be, L, rho, v, alphas, X, uv, n, K, R, t);
 }
 
 // n >= 4 correspondences (object points X[3i..], image points u[2i..]).  Returns R (world ->

@@ -728,8 +728,10 @@ __global__ __launch_bounds__(256, 2) void k_wino3(WinoArgs wa) {
         }
     };
     // chunk c's patch -> s_x[c & 1] (fused: conv1a of its 4 channels at this pixel, 0 outside the image)
-    auto put_x = [&](auto sl_c, auto g_c, int c) {
+    // channels [LO, HI) of the chunk (the schedule may split a chunk's conv1a over two MFMA rows)
+    auto put_x_part = [&](auto sl_c, auto g_c, auto lo_c, auto hi_c, int c) {
         constexpr int sl = decltype(sl_c)::value;
+        constexpr int LO = decltype(lo_c)::value, HI = decltype(hi_c)::value;
         if (decltype(g_c)::value && c >= nchunk) return;
         if constexpr (FUSE1A) {
             // the chunk's 4 x (9 taps + bias) are wave-uniform: scalar loads into SGPRs, v_fma_f32 with an
@@ -737,9 +739,9 @@ __global__ __launch_bounds__(256, 2) void k_wino3(WinoArgs wa) {
             const f32x4* wp = reinterpret_cast<const f32x4*>(w1a + (size_t)(c * CK) * 12);
             f32x4 q[3 * CK];
 #pragma unroll
-            for (int i = 0; i < 3 * CK; i++) q[i] = wp[i];
+            for (int i = 3 * LO; i < 3 * HI; i++) q[i] = wp[i];
 #pragma unroll
-            for (int cc = 0; cc < CK; cc++) {
+            for (int cc = LO; cc < HI; cc++) {
                 const f32x4 q0 = q[3 * cc], q1 = q[3 * cc + 1], q2 = q[3 * cc + 2];
                 const float wk[9] = {q0[0], q0[1], q0[2], q0[3], q1[0], q1[1], q1[2], q1[3], q2[0]};
                 float a = q2[1];
@@ -749,12 +751,16 @@ __global__ __launch_bounds__(256, 2) void k_wino3(WinoArgs wa) {
             }
         } else {
 #pragma unroll
-            for (int cc = 0; cc < CK; cc++) {
+            for (int cc = LO; cc < HI; cc++) {
                 const float v = pin ? rx[sl][cc] : 0.0f;
                 s_x[sl][cc][tid] = pre_relu ? fmaxf(v, 0.0f) : v;
             }
         }
     };
+    using I0 = std::integral_constant<int, 0>;
+    using I2 [[maybe_unused]] = std::integral_constant<int, 2>;
+    using I4 = std::integral_constant<int, CK>;
+    auto put_x = [&](auto sl_c, auto g_c, int c) { put_x_part(sl_c, g_c, I0{}, I4{}, c); };
     // chunk c's weights -> s_u[c & 1] (channel cc's 32-column halves swapped when cc is odd)
     auto put_u = [&](auto sl_c, auto g_c, int c) {
         constexpr int sl = decltype(sl_c)::value;
@@ -932,6 +938,46 @@ __global__ __launch_bounds__(256, 2) void k_wino3(WinoArgs wa) {
         __builtin_amdgcn_sched_barrier(0);
         mfma_row(3, 1);
         if (VS_WINO_PRIO) __builtin_amdgcn_s_setprio(0);
+#elif VS_WINO_SCHED == 3
+        // as 1, with conv1a split over rows 0 and 1 and the transform over rows 2 and 3
+        read_row(P, 0, 0);
+        read_row(P, 1, 1);
+        __builtin_amdgcn_sched_barrier(0);
+        mfma_row(0, 0);
+        put_u(SN{}, g_c, k + 1);
+        fetch_u(g_c, k + 2);
+        fetch_x(SN{}, g_c, k + 3);
+        put_x_part(SP{}, g_c, I0{}, I2{}, k + 2);
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+            __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);
+            __builtin_amdgcn_sched_group_barrier(0x010, 1, 0);
+            __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        read_row(P, 2, 0);
+        mfma_row(1, 1);
+        put_x_part(SP{}, g_c, I2{}, I4{}, k + 2);
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 1);
+            __builtin_amdgcn_sched_group_barrier(0x100, 1, 1);
+            __builtin_amdgcn_sched_group_barrier(0x002, 4, 1);
+            __builtin_amdgcn_sched_group_barrier(0x200, 1, 1);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        read_row(P, 3, 1);
+        transform(SN{}, g_c, k + 1);
+        mfma_row(2, 0);
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+            __builtin_amdgcn_sched_group_barrier(0x100, 2, 2);
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 2);
+            __builtin_amdgcn_sched_group_barrier(0x002, 3, 2);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        mfma_row(3, 1);
 #else
         // no scheduling fences: the compiler's own interleave
         read_row(P, 0, 0);
