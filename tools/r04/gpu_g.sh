@@ -2,11 +2,11 @@
 # PnP hypothesis kernel: ping-pong Jacobi + uniform beta init (bit-identical): parity, kernel time, headline A/B
 export TMPDIR=/tmp
 O=gpurun_out/r04g; mkdir -p $O
-timeout -k 10 900 python -u -m pytest tests/test_gpu_pnp.py tests/test_golden.py tests/test_gpu_tracking.py tests/test_gpu_tracker.py tests/test_gpu_tracker_bench.py -m gpu -x -q --timeout 600 --timeout-method thread -p no:cacheprovider > $O/pytest.log 2>&1
+timeout -k 10 900 python -u -m pytest tests/test_gpu_pnp.py tests/test_golden.py tests/test_gpu_tracking.py tests/test_gpu_tracker.py tests/test_gpu_tracker_bench.py tests/test_gpu_tracker_ideal.py -m gpu -x -q --timeout 600 --timeout-method thread -p no:cacheprovider > $O/pytest.log 2>&1
 rc=$?; tail -3 $O/pytest.log; [ $rc -eq 0 ] || exit $rc
 ARGS="--steps 20 --warmup 5 --no-cpu-baseline --no-frontend --mono-steps 0 --ba-reps 0"
 for r in 1 2; do
-  for nl in ws1:ab/ws1.so head:visual-slam-pipeline_amd/libvslam_hip.so; do
+  for nl in ws1:ab/ws1.so pnp:ab/pnponly.so head:visual-slam-pipeline_amd/libvslam_hip.so; do
     n=${nl%%:*}; lib=${nl#*:}
     VS_LIB_PATH=$lib VS_SLAM_HOST_PROFILE=1 timeout -k 10 300 python -u bench.py $ARGS > $O/bench_${n}_$r.json 2> $O/bench_${n}_$r.err || exit 1
     python3 -c "import json; d=json.loads(open('$O/bench_${n}_$r.json').read().strip().splitlines()[-1]); print('bench $n $r', d['value'], d['stage_ms_per_frame'].get('solve_pnp'), d['stage_ms_per_frame'].get('track_local_map'))"

@@ -207,16 +207,38 @@ __global__ __launch_bounds__(256) void k_tlm_cand(const double* __restrict__ mp_
     for (int j = 0; j < c; j++) work[base + incl - c + j] = mp * kTlmMaxCand + j;
 }
 
-// Phase 2: the cv::norm distance (:451) of every (map point, candidate) pair on the work list,
-// grid-stride (the list holds only real candidates, a few per visible map point).
+// Phase 2: the cv::norm distance (:451) of every (map point, candidate) pair on the work list
+// (a few per visible map point), one wave per pair, grid-stride: lane q loads float4 q of both
+// descriptors (one coalesced 1 KB row each) and forms the group term ((v0^2 + v1^2) + v2^2) + v3^2
+// in double; the 64 terms are then added in order q = 0..63 by lane 0 from LDS — the same terms and
+// the same sequential sum as desc_l2_dev (cv::norm's groups of four), so bit-identical, with the
+// loads in parallel instead of a 64-step strided walk per lane.
 __global__ __launch_bounds__(256) void k_tlm_dist(const float* __restrict__ mp_desc, const float* __restrict__ desc,
                                                   const int* __restrict__ cand, const int* __restrict__ work,
                                                   const int* __restrict__ work_n, double* __restrict__ dist) {
     crit_prio();
+    __shared__ double s_t[4][64];
     const int n = *work_n;
-    for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    for (int i = blockIdx.x * 4 + wv; i < n; i += gridDim.x * 4) {  // wave-uniform
         const int r = work[i];
-        dist[r] = desc_l2_dev(mp_desc + (size_t)(r / kTlmMaxCand) * 256, desc + (size_t)cand[r] * 256);
+        const float4 x = reinterpret_cast<const float4*>(mp_desc + (size_t)(r / kTlmMaxCand) * 256)[lane];
+        const float4 y = reinterpret_cast<const float4*>(desc + (size_t)cand[r] * 256)[lane];
+        const double v0 = (double)(x.x - y.x), v1 = (double)(x.y - y.y);
+        const double v2 = (double)(x.z - y.z), v3 = (double)(x.w - y.w);
+        s_t[wv][lane] = v0 * v0 + v1 * v1 + v2 * v2 + v3 * v3;
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        if (lane == 0) {
+            double s = 0;
+#pragma unroll
+            for (int q = 0; q < 64; q++) s += s_t[wv][q];
+            dist[r] = sqrt(s);
+        }
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
 }
 
@@ -382,35 +404,58 @@ __global__ __launch_bounds__(1024) void k_tlm_resolve(const int* __restrict__ be
         S.total = INT_MAX;
     }
     if (nblk <= kTlmMaxBlk) {
-        for (int b = tid; b < nblk; b += 1024) S.pre[b] = blkcnt[b];
-        __syncthreads();
-        if (tid == 0) {
-            int acc = 0;
-            for (int b = 0; b < nblk; b++) {
-                const int c = S.pre[b];
-                S.pre[b] = acc;
-                acc += c;
-            }
-            S.total = acc;
+        // exclusive prefix over the block counts: 4 consecutive blocks per thread, a wave scan of the
+        // thread totals, the waves' totals across the workgroup (integer sums: exact in any order)
+        int v[4], run = 0;
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const int b = 4 * tid + k;
+            v[k] = b < nblk ? blkcnt[b] : 0;
+            run += v[k];
         }
+        int incl = run;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int y = __shfl_up(incl, o);
+            if (lane >= o) incl += y;
+        }
+        if (lane == 63) S.wcnt[wv] = incl;
+        __syncthreads();
+        int before = incl - run, all = 0;
+        for (int w = 0; w < 16; w++) {
+            if (w < wv) before += S.wcnt[w];
+            all += S.wcnt[w];
+        }
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const int b = 4 * tid + k;
+            if (b < nblk) S.pre[b] = before;
+            before += v[k];
+        }
+        if (tid == 0) S.total = all;
     }
     __syncthreads();
     if (S.total <= kTlmCandBuf) {
         for (int m0 = 0; m0 < n_mp; m0 += 16 * 1024) {
-            int kis[16];  // all loads of the round issued before any is used (latency, not bandwidth)
+            // all loads of the round issued before any is used (latency, not bandwidth): the rank and
+            // distance are read unconditionally (in bounds), so they do not wait for best_ki
+            int kis[16], rks[16];
+            double bds[16];
 #pragma unroll
             for (int u = 0; u < 16; u++) {
-                const int mp = m0 + u * 1024 + tid;
-                kis[u] = mp < n_mp ? best_ki[mp] : -1;
+                const int mp = min(m0 + u * 1024 + tid, n_mp - 1);
+                kis[u] = best_ki[mp];
+                rks[u] = rank[mp];
+                bds[u] = best_d[mp];
             }
 #pragma unroll
             for (int u = 0; u < 16; u++) {
                 const int mp = m0 + u * 1024 + tid;
-                if (kis[u] < 0) continue;
-                const int j = S.pre[mp >> 8] + rank[mp];
+                if (mp >= n_mp || kis[u] < 0) continue;
+                const int j = S.pre[mp >> 8] + rks[u];
                 S.cmp[j] = mp;
                 S.cki[j] = kis[u];
-                S.cd[j] = (unsigned long long)__double_as_longlong(best_d[mp]);
+                S.cd[j] = (unsigned long long)__double_as_longlong(bds[u]);
                 atomicMin(&S.first[kis[u]], j);
             }
         }
@@ -501,7 +546,7 @@ int track_local_map(vs_ctx* ctx, const double* d_mp_pos, const float* d_mp_desc,
     if (n_mp > 0) {
         hipLaunchKernelGGL(k_tlm_cand, dim3((n_mp + 255) / 256), dim3(256), 0, s, d_mp_pos, d_mp_desc, d_mp_valid, n_mp,
                            d_kps, d_desc, start, items, GW, GH, img_w, img_h, T, cnt, cand, work, work_n);
-        hipLaunchKernelGGL(k_tlm_dist, dim3(128), dim3(256), 0, s, d_mp_desc, d_desc, cand, work, work_n, dist);
+        hipLaunchKernelGGL(k_tlm_dist, dim3(512), dim3(256), 0, s, d_mp_desc, d_desc, cand, work, work_n, dist);
     }
     if (n_mp > 0)
         hipLaunchKernelGGL(k_tlm_best, dim3(nblk), dim3(256), 0, s, cnt, cand, dist, n_mp, best_ki, best_d, rank,
