@@ -327,33 +327,37 @@ __global__ __launch_bounds__(64) void k_pnp_hyp(const float* __restrict__ obj_al
                         double x00 = A[i0 * 12 + j0], x01 = A[i0 * 12 + j1], x10 = A[i1 * 12 + j0], x11 = A[i1 * 12 + j1];
                         const double p0 = V[(2 * ba) * 12 + j0], q0 = V[(2 * ba) * 12 + j1];
                         const double p1 = V[(2 * ba + 1) * 12 + j0], q1 = V[(2 * ba + 1) * 12 + j1];
-                        double ca = 1.0, sa = 0.0, cb = 1.0, sb = 0.0;
-                        const bool acta = jacobi_angle(A[i0 * 12 + i0], A[i1 * 12 + i1], A[i0 * 12 + i1], ca, sa);
-                        const bool actb = jacobi_angle(A[j0 * 12 + j0], A[j1 * 12 + j1], A[j0 * 12 + j1], cb, sb);
-                        if (actb) {
+                        // both angles branch-free (jacobi_angle_nb) and the skipped rotations as
+                        // selects: one straight-line block per round, the two angle chains interleaved
+                        double ca, sa, cb, sb;
+                        const bool acta = jacobi_angle_nb(A[i0 * 12 + i0], A[i1 * 12 + i1], A[i0 * 12 + i1], ca, sa);
+                        const bool actb = jacobi_angle_nb(A[j0 * 12 + j0], A[j1 * 12 + j1], A[j0 * 12 + j1], cb, sb);
+                        {
                             const double y00 = cb * x00 - sb * x01, y01 = sb * x00 + cb * x01;
                             const double y10 = cb * x10 - sb * x11, y11 = sb * x10 + cb * x11;
-                            x00 = y00;
-                            x01 = y01;
-                            x10 = y10;
-                            x11 = y11;
+                            x00 = actb ? y00 : x00;
+                            x01 = actb ? y01 : x01;
+                            x10 = actb ? y10 : x10;
+                            x11 = actb ? y11 : x11;
                         }
-                        if (acta) {
+                        {
                             const double y00 = ca * x00 - sa * x10, y10 = sa * x00 + ca * x10;
                             const double y01 = ca * x01 - sa * x11, y11 = sa * x01 + ca * x11;
-                            x00 = y00;
-                            x01 = y01;
-                            x10 = y10;
-                            x11 = y11;
+                            x00 = acta ? y00 : x00;
+                            x01 = acta ? y01 : x01;
+                            x10 = acta ? y10 : x10;
+                            x11 = acta ? y11 : x11;
                         }
                         An[i0 * 12 + j0] = x00;
                         An[i0 * 12 + j1] = x01;
                         An[i1 * 12 + j0] = x10;
                         An[i1 * 12 + j1] = x11;
-                        Vn[(2 * ba) * 12 + j0] = actb ? cb * p0 - sb * q0 : p0;
-                        Vn[(2 * ba) * 12 + j1] = actb ? sb * p0 + cb * q0 : q0;
-                        Vn[(2 * ba + 1) * 12 + j0] = actb ? cb * p1 - sb * q1 : p1;
-                        Vn[(2 * ba + 1) * 12 + j1] = actb ? sb * p1 + cb * q1 : q1;
+                        const double v0 = cb * p0 - sb * q0, w0 = sb * p0 + cb * q0;
+                        const double v1 = cb * p1 - sb * q1, w1 = sb * p1 + cb * q1;
+                        Vn[(2 * ba) * 12 + j0] = actb ? v0 : p0;
+                        Vn[(2 * ba) * 12 + j1] = actb ? w0 : q0;
+                        Vn[(2 * ba + 1) * 12 + j0] = actb ? v1 : p1;
+                        Vn[(2 * ba + 1) * 12 + j1] = actb ? w1 : q1;
                     }
                     cur ^= 1;
                     __syncthreads();

@@ -136,6 +136,19 @@ VS_HD inline bool jacobi_angle(double app, double aqq, double apq, double& c, do
     s = (d >= 0 ? h : -h) / w;
     return true;
 }
+// The same arithmetic without the early exit, for the device's parallel rounds: (c, s) are
+// computed unconditionally (meaningless when the rotation is skipped — the caller selects on the
+// flag), so a lane's two angles compile to one straight-line pair of interleaved chains instead of
+// two serialised branches.  Where the rotation runs, (c, s) are bit-identical to jacobi_angle's.
+VS_HD inline bool jacobi_angle_nb(double app, double aqq, double apq, double& c, double& s) {
+    const double d = aqq - app, h = 2.0 * apq;
+    const double r = sqrt(d * d + h * h);
+    const double u = fabs(d) + r;
+    const double w = sqrt(2.0 * r * u);
+    c = u / w;
+    s = (d >= 0 ? h : -h) / w;
+    return !(fabs(apq) < 1e-150);
+}
 
 // Cyclic Jacobi eigen-decomposition of the symmetric n x n matrix A (row-major, destroyed):
 // w[k] eigenvalues in descending order, V[i*n + k] the k-th eigenvector (columns).
