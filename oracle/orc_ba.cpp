@@ -14,6 +14,7 @@
 // errors) are taken in fixed chunks of 256 observations (chunk sums added in order), the order
 // the GPU reduces in; the dense solve is a right-looking Cholesky without OpenCV's SVD fallback
 // (S is SPD by construction: the pose blocks carry the 1e10 damping).
+#include <cfloat>
 #include <cmath>
 #include <cstring>
 #include <vector>
@@ -37,24 +38,38 @@ double chunked_sum(int n, F term) {
     return total;
 }
 
-// right-looking dense Cholesky solve of S x = b (n x n, row-major, destroyed); false if not SPD
+// S x = b in the arithmetic of cv::solve(S, b, x, DECOMP_CHOLESKY) (Optimizer.cpp:516; OpenCV's
+// hal Cholesky, restated): row by row, L_ij = (S_ij - sum_{k<j} L_ik L_jk) * R_j for j < i and
+// R_i = 1 / sqrt(S_ii - sum_{k<i} L_ik^2), every sum in ascending k, R kept on the diagonal; false
+// (not solved) when a pivot is below DBL_EPSILON.  Then y_i = (b_i - sum_{k<i} L_ik y_k) * R_i and
+// x_i = (y_i - sum_{k>i, descending} L_ki x_k) * R_i.  (S row-major n x n, only its lower
+// triangle is read; overwritten by L.)
 bool chol_solve(std::vector<double>& S, int n, std::vector<double>& b) {
-    for (int k = 0; k < n; k++) {
-        const double d = S[(size_t)k * n + k];
-        if (!(d > 0)) return false;
-        const double l = std::sqrt(d);
-        S[(size_t)k * n + k] = l;
-        for (int i = k + 1; i < n; i++) S[(size_t)i * n + k] /= l;
-        for (int i = k + 1; i < n; i++)
-            for (int j = k + 1; j <= i; j++) S[(size_t)i * n + j] -= S[(size_t)i * n + k] * S[(size_t)j * n + k];
+    for (int i = 0; i < n; i++) {
+        double* Li = &S[(size_t)i * n];
+        for (int j = 0; j < i; j++) {
+            const double* Lj = &S[(size_t)j * n];
+            double s = Li[j];
+            for (int k = 0; k < j; k++) s -= Li[k] * Lj[k];
+            Li[j] = s * Lj[j];
+        }
+        double s = Li[i];
+        for (int k = 0; k < i; k++) {
+            const double t = Li[k];
+            s -= t * t;
+        }
+        if (s < DBL_EPSILON) return false;
+        Li[i] = 1.0 / std::sqrt(s);
     }
-    for (int k = 0; k < n; k++) {  // L y = b
-        b[k] /= S[(size_t)k * n + k];
-        for (int i = k + 1; i < n; i++) b[i] -= S[(size_t)i * n + k] * b[k];
+    for (int i = 0; i < n; i++) {  // L y = b
+        double s = b[i];
+        for (int k = 0; k < i; k++) s -= S[(size_t)i * n + k] * b[k];
+        b[i] = s * S[(size_t)i * n + i];
     }
-    for (int k = n - 1; k >= 0; k--) {  // L^T x = y
-        b[k] /= S[(size_t)k * n + k];
-        for (int i = 0; i < k; i++) b[i] -= S[(size_t)k * n + i] * b[k];
+    for (int i = n - 1; i >= 0; i--) {  // L^T x = y
+        double s = b[i];
+        for (int k = n - 1; k > i; k--) s -= S[(size_t)k * n + i] * b[k];
+        b[i] = s * S[(size_t)i * n + i];
     }
     return true;
 }

@@ -20,6 +20,10 @@
 // global cost sums use fixed chunks of 256 observations.  Arithmetic shared via ba_solvers.h.
 #include <hip/hip_runtime.h>
 
+#include <cfloat>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <vector>
 
 #include "ba_solvers.h"
@@ -35,7 +39,7 @@ struct BaCtl {
 };
 
 struct BaDev {
-    int N, M, n_obs, n_pairs, n_chunks;
+    int N, M, n_obs, n_pairs, n_chunks, np;  // np: the Schur dimension 6N padded to 32
     Cam K;
     const int *okf, *opt, *oslot, *kf_off, *kf_obs, *pt_off, *pt_obs, *pv_off, *pv_kf, *ab_off, *ab_u, *ab_h, *ab_j,
         *kb_off, *kb_u, *kb_j;
@@ -103,11 +107,13 @@ __global__ __launch_bounds__(kCostChunk) void k_ba_chunk_sums(BaDev d, int mode,
 
 // Hpp, bp per keyframe in gather order (:407-451), one 64-lane workgroup per keyframe: lane
 // l < 21 owns upper-triangular element l of Hpp (mirrored), lanes 21..26 own bp — each element is
-// the same sequential sum over the keyframe's observations as in the oracle.  The observation
-// indices are staged 64 at a time so the term loads do not wait on index loads.
+// the same sequential sum over the keyframe's valid observations as in the oracle.  The observation
+// terms are staged 64 at a time through two LDS buffers, the next stage's loads in flight while the
+// current one is summed (one barrier per stage); an invalid observation adds +0.0, which leaves
+// the sum unchanged (it starts at +0.0 and so is never -0.0).
 __global__ __launch_bounds__(64) void k_ba_kf_acc(BaDev d) {
     BA_LIVE(d);
-    __shared__ double s_t[64][15];  // per staged observation: Jp (12), ru_w, rv_w, valid
+    __shared__ double s_t[2][64][16];  // per staged observation: Jp (12), ru_w, rv_w, valid (0 / 1)
     const int i = blockIdx.x, l = threadIdx.x;
     if (i >= d.N) return;
     int r = 0, c = 0;
@@ -121,30 +127,43 @@ __global__ __launch_bounds__(64) void k_ba_kf_acc(BaDev d) {
     } else {
         r = l - 21;
     }
-    double acc = 0;
+    // the two products of the lane's element: s[r] s[cb] + s[6 + r] s[cb2]
+    const int cb = l < 21 ? c : 12, cb2 = l < 21 ? 6 + c : 13;
     const int q0 = d.kf_off[i], q1 = d.kf_off[i + 1];
-    for (int qb = q0; qb < q1; qb += 64) {
+    double v[15];
+    auto fetch = [&](int qb) {
         if (qb + l < q1) {
             const ObsTerms& ot = d.terms[d.kf_obs[qb + l]];
+#pragma unroll
             for (int k = 0; k < 6; k++) {
-                s_t[l][k] = ot.Jp[0][k];
-                s_t[l][6 + k] = ot.Jp[1][k];
+                v[k] = ot.Jp[0][k];
+                v[6 + k] = ot.Jp[1][k];
             }
-            s_t[l][12] = ot.ru_w;
-            s_t[l][13] = ot.rv_w;
-            s_t[l][14] = ot.valid ? 1.0 : 0.0;
+            v[12] = ot.ru_w;
+            v[13] = ot.rv_w;
+            v[14] = ot.valid ? 1.0 : 0.0;
         }
+    };
+    fetch(q0);
+    double acc = 0;
+    int buf = 0;
+    for (int qb = q0; qb < q1; qb += 64) {
+        if (qb + l < q1)
+#pragma unroll
+            for (int k = 0; k < 15; k++) s_t[buf][l][k] = v[k];
         __syncthreads();
+        if (qb + 64 < q1) fetch(qb + 64);
         const int m = min(64, q1 - qb);
-        if (l < 27)
+        if (l < 27) {
+            const double* T = &s_t[buf][0][0];
+#pragma unroll 4
             for (int k = 0; k < m; k++) {
-                if (s_t[k][14] == 0.0) continue;
-                if (l < 21)
-                    acc += s_t[k][r] * s_t[k][c] + s_t[k][6 + r] * s_t[k][6 + c];
-                else
-                    acc += s_t[k][r] * s_t[k][12] + s_t[k][6 + r] * s_t[k][13];
+                const double* t = T + 16 * k;
+                const double term = t[r] * t[cb] + t[6 + r] * t[cb2];
+                acc += t[14] != 0.0 ? term : 0.0;
             }
-        __syncthreads();
+        }
+        buf ^= 1;
     }
     if (l < 21) {
         if (r == c) acc += kPoseDamp;
@@ -155,6 +174,10 @@ __global__ __launch_bounds__(64) void k_ba_kf_acc(BaDev d) {
     }
 }
 
+// Hmm, bm and the Hpm blocks per point (one thread per point), in observation order.  Each Hpm
+// slot (one per observing keyframe) is summed in registers over the observations of that slot and
+// stored once (the oracle's += from zero, in the same order), instead of a read-modify-write of
+// global memory per observation.
 __global__ void k_ba_pt_acc(BaDev d) {
     BA_LIVE(d);
     const int j = blockIdx.x * blockDim.x + threadIdx.x;
@@ -163,14 +186,24 @@ __global__ void k_ba_pt_acc(BaDev d) {
     for (int k = 0; k < 9; k++) H[k] = 0;
     for (int k = 0; k < 3; k++) b[k] = 0;
     const int p0 = d.pv_off[j], np = d.pv_off[j + 1] - p0;
-    for (int s = 0; s < np; s++)
-        for (int k = 0; k < 18; k++) d.Hpm[18 * (size_t)(p0 + s) + k] = 0;
-    for (int q = d.pt_off[j]; q < d.pt_off[j + 1]; q++) {
-        const int o = d.pt_obs[q];
-        const ObsTerms& ot = d.terms[o];
-        if (!ot.valid) continue;
-        ba_add_point(ot, H, b);
-        ba_add_cross(ot, d.Hpm + 18 * (size_t)(p0 + d.oslot[o]));
+    const int qa = d.pt_off[j], qe = d.pt_off[j + 1];
+    for (int q = qa; q < qe; q++) {
+        const ObsTerms& ot = d.terms[d.pt_obs[q]];
+        if (ot.valid) ba_add_point(ot, H, b);
+    }
+    for (int sl = 0; sl < np; sl++) {
+        double X[18];
+#pragma unroll
+        for (int k = 0; k < 18; k++) X[k] = 0;
+        for (int q = qa; q < qe; q++) {
+            const int o = d.pt_obs[q];
+            if (d.oslot[o] != sl) continue;
+            const ObsTerms& ot = d.terms[o];
+            if (ot.valid) ba_add_cross(ot, X);
+        }
+        double* dst = d.Hpm + 18 * (size_t)(p0 + sl);
+#pragma unroll
+        for (int k = 0; k < 18; k++) dst[k] = X[k];
     }
     for (int k = 0; k < 9; k++) d.Hmm[9 * (size_t)j + k] = H[k];
     for (int k = 0; k < 3; k++) d.bm[3 * (size_t)j + k] = b[k];
@@ -179,18 +212,20 @@ __global__ void k_ba_pt_acc(BaDev d) {
     d.pvalid[j] = ok;
     for (int k = 0; k < 9; k++) d.Hinv[9 * (size_t)j + k] = Hi[k];
     if (ok)
-        for (int s = 0; s < np; s++) ba_schur_u(d.Hpm + 18 * (size_t)(p0 + s), Hi, d.U + 18 * (size_t)(p0 + s));
+        for (int sl = 0; sl < np; sl++) ba_schur_u(d.Hpm + 18 * (size_t)(p0 + sl), Hi, d.U + 18 * (size_t)(p0 + sl));
 }
 
 // grid: N*N workgroups of 64 threads; threads 0..35 own S_ab(r, c), threads 0..5 then own b_a(r)
-// on the diagonal workgroups.  The (U, Hpm, point) index lists are staged 64 at a time in LDS so
-// the products' loads do not wait on index loads; sums run over the lists in order (the oracle's).
+// on the diagonal workgroups.  The (U, Hpm) pairs of the common points are staged 64 at a time
+// through two LDS buffers, the next stage's loads in flight while the current one is summed (one
+// barrier per stage); sums run over the lists in order (the oracle's), a skipped point (no
+// inverse) subtracting +0.0, which leaves every value unchanged.
 __global__ __launch_bounds__(64) void k_ba_schur(BaDev d) {
     BA_LIVE(d);
-    __shared__ double s_U[64][18], s_H[64][18];
-    __shared__ int s_ok[64];
+    __shared__ double s_U[2][64][18], s_H[2][64][18];
+    __shared__ int s_ok[2][64];
     const int a = blockIdx.x / d.N, b = blockIdx.x % d.N, t = threadIdx.x;
-    const int n = 6 * d.N;
+    const int np = d.np;
     const double lam = d.ctl->lambda;
     const int r = t / 6, c = t % 6;
     double s = 0.0;
@@ -198,63 +233,111 @@ __global__ __launch_bounds__(64) void k_ba_schur(BaDev d) {
         s = a == b ? d.Hpp[36 * a + r * 6 + c] : 0.0;
         if (a == b && r == c) s *= (1.0 + lam);
     }
+    double u[18], h[18];
+    int ok = 0;
     const int pair = a * d.N + b;
     const int q0 = d.ab_off[pair], q1 = d.ab_off[pair + 1];
-    for (int qb = q0; qb < q1; qb += 64) {
+    auto fetch = [&](int qb) {
         const int q = qb + t;
         if (q < q1) {
             const double* U = d.U + 18 * (size_t)d.ab_u[q];
             const double* Hh = d.Hpm + 18 * (size_t)d.ab_h[q];
+#pragma unroll
             for (int k = 0; k < 18; k++) {
-                s_U[t][k] = U[k];
-                s_H[t][k] = Hh[k];
+                u[k] = U[k];
+                h[k] = Hh[k];
             }
-            s_ok[t] = d.pvalid[d.ab_j[q]];
+            ok = d.pvalid[d.ab_j[q]];
+        }
+    };
+    fetch(q0);
+    int buf = 0;
+    for (int qb = q0; qb < q1; qb += 64) {
+        if (qb + t < q1) {
+#pragma unroll
+            for (int k = 0; k < 18; k++) {
+                s_U[buf][t][k] = u[k];
+                s_H[buf][t][k] = h[k];
+            }
+            s_ok[buf][t] = ok;
         }
         __syncthreads();
+        if (qb + 64 < q1) fetch(qb + 64);
         const int m = min(64, q1 - qb);
         if (t < 36)
-            for (int k = 0; k < m; k++)
-                if (s_ok[k]) s -= ba_schur_s(s_U[k], s_H[k], r, c);
-        __syncthreads();
+#pragma unroll 4
+            for (int k = 0; k < m; k++) {
+                const double v = ba_schur_s(s_U[buf][k], s_H[buf][k], r, c);
+                s -= s_ok[buf][k] ? v : 0.0;
+            }
+        buf ^= 1;
     }
-    if (t < 36) d.S[(size_t)(6 * a + r) * n + 6 * b + c] = s;
+    if (t < 36) d.S[(size_t)(6 * a + r) * np + 6 * b + c] = s;
     if (a != b) return;
+    __syncthreads();  // both buffers free again
     double sb = t < 6 ? d.bp[6 * a + t] : 0.0;
+    double bmv[3];
     const int k0 = d.kb_off[a], k1 = d.kb_off[a + 1];
-    for (int qb = k0; qb < k1; qb += 64) {
+    auto fetch_b = [&](int qb) {
         const int q = qb + t;
         if (q < k1) {
             const int j = d.kb_j[q];
             const double* U = d.U + 18 * (size_t)d.kb_u[q];
-            for (int k = 0; k < 18; k++) s_U[t][k] = U[k];
-            for (int k = 0; k < 3; k++) s_H[t][k] = d.bm[3 * (size_t)j + k];
-            s_ok[t] = d.pvalid[j];
+#pragma unroll
+            for (int k = 0; k < 18; k++) u[k] = U[k];
+#pragma unroll
+            for (int k = 0; k < 3; k++) bmv[k] = d.bm[3 * (size_t)j + k];
+            ok = d.pvalid[j];
+        }
+    };
+    fetch_b(k0);
+    buf = 0;
+    for (int qb = k0; qb < k1; qb += 64) {
+        if (qb + t < k1) {
+#pragma unroll
+            for (int k = 0; k < 18; k++) s_U[buf][t][k] = u[k];
+#pragma unroll
+            for (int k = 0; k < 3; k++) s_H[buf][t][k] = bmv[k];
+            s_ok[buf][t] = ok;
         }
         __syncthreads();
+        if (qb + 64 < k1) fetch_b(qb + 64);
         const int m = min(64, k1 - qb);
         if (t < 6)
-            for (int k = 0; k < m; k++)
-                if (s_ok[k]) sb -= ba_schur_b(s_U[k], s_H[k], t);
-        __syncthreads();
+#pragma unroll 4
+            for (int k = 0; k < m; k++) {
+                const double v = ba_schur_b(s_U[buf][k], s_H[buf][k], t);
+                sb -= s_ok[buf][k] ? v : 0.0;
+            }
+        buf ^= 1;
     }
     if (t < 6) d.bs[6 * a + t] = sb;
 }
 
-// Right-looking Cholesky of S (lower triangle) and S dp = -bs, blocked, one workgroup:
-//   * 32-column panels staged in LDS; one thread per panel row; per column every thread takes
-//     the pivot sqrt itself and divides the column entries it needs on the fly, so one barrier
-//     per column suffices (the divided column is stored one step later, when nothing reads it);
-//   * the trailing lower triangle is updated by all waves in 4 x 4 register tiles;
-//   * both triangular solves are blocked the same way: the rows below (above) a finished block
-//     take that block's contributions in parallel, the 32 x 32 diagonal block is solved by one
-//     wave out of LDS.
-// Every element still receives its updates in the order of the oracle's sequential chol_solve
-// (orc_ba.cpp: ascending k for the factor and the forward solve, descending k for the backward
-// solve), so the factor and the solution are bit-identical.
+// S dp = -bs by Cholesky in the arithmetic of cv::solve(S, -bs, dp, DECOMP_CHOLESKY)
+// (Optimizer.cpp:516; OpenCV's hal Cholesky): each L entry is (S_ij - sum_{k<j} L_ik L_jk) * R_j
+// with the sum in ascending k and R_j = 1 / sqrt(S_jj - sum_{k<j} L_jk^2) kept as the diagonal;
+// a pivot below DBL_EPSILON fails the solve; the substitutions multiply by R as well.
+// S is held padded to np = 6N rounded up to 32 with an identity block (rows / columns n..np-1;
+// k_ba_pad sets it once per call): every padded L entry and solution value is exactly 0 and the
+// padded pivots are 1, and no real element ever takes a padded term, so the real part is
+// bit-identical to the unpadded statement while every panel is a full 32 columns (straight-line
+// code, no edge guards).  One workgroup, right-looking over 32-column panels — every element still
+// takes its terms in ascending k, so the factor and the solution are bit-identical to the oracle's
+// row-oriented statement (oracle/orc_ba.cpp chol_solve):
+//   1. wave 0 factors the panel's 32 x 32 diagonal block in registers (lane = row): the pivot and
+//      the column entries it needs come by readlane, so the 32-step sqrt -> reciprocal -> update
+//      chain runs without a barrier, while waves 1.. load the panel rows below;
+//   2. every row below takes the diagonal block (a 32-step substitution per row, one thread per
+//      row, the block's L and R broadcast out of LDS);
+//   3. the trailing lower triangle takes the panel's 32 columns in 4 x 4 register tiles, the
+//      panel held k-major in LDS (one 32-byte read per 4 rows);
+//   4. both substitutions are blocked the same way: wave 0 solves the 32 x 32 diagonal block by
+//      readlane broadcasts, the rows below (above) take the finished block in parallel.
 constexpr int kCholNB = 32;
-constexpr int kCholLd = kCholNB + 1;  // LDS row stride: rows one thread apart fall in different banks
-constexpr int kCholMaxN = 6 * VS_BA_MAX_KEYFRAMES;
+constexpr int kCholMaxN = 6 * VS_BA_MAX_KEYFRAMES;  // a multiple of kCholNB
+static_assert(kCholMaxN % kCholNB == 0, "padded Schur dimension");
+constexpr int kCholLd = kCholMaxN;  // PnT row length
 
 #ifdef VS_BA_PROFILE
 // phase cycle counters of k_ba_chol (profiling build only: make -C visual-slam-pipeline_amd prof)
@@ -270,119 +353,130 @@ __device__ unsigned long long g_ba_cycles[8];
 #define BA_T(k)
 #endif
 
-__device__ __forceinline__ void wave_sync() {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+// lane l's value of v, wave-uniform (two v_readlane_b32)
+__device__ __forceinline__ double readlane_f64(double v, int l) {
+    const unsigned long long b = (unsigned long long)__double_as_longlong(v);
+    const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)b, l);
+    const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(b >> 32), l);
+    return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
 }
 
-__global__ __launch_bounds__(1024) void k_ba_chol(BaDev d) {
+// the padded rows n..np-1 of S: identity (their columns >= n above the diagonal are never read)
+__global__ void k_ba_pad(BaDev d) {
+    const int n = 6 * d.N, np = d.np;
+    const int g = blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= (np - n) * np) return;
+    const int i = n + g / np, j = g % np;
+    d.S[(size_t)i * np + j] = i == j ? 1.0 : 0.0;
+}
+
+__global__ __launch_bounds__(512) void k_ba_chol(BaDev d) {
     BA_LIVE(d);
-    const int n = 6 * d.N, tid = threadIdx.x, nt = blockDim.x, lane = tid & 63;
+    const int n = 6 * d.N, np = d.np, tid = threadIdx.x, nt = blockDim.x, lane = tid & 63;
     double* S = d.S;
-    __shared__ double Pn[kCholMaxN * kCholLd];  // panel rows K0..n-1 x columns K0..K0+nb-1
-    __shared__ double xs[kCholMaxN];
-    __shared__ double Db[kCholNB * kCholLd];  // diagonal block for the solves
-    __shared__ double Lc[kCholMaxN];           // the divided panel column of the current step
-    __shared__ double s_piv;
+    __shared__ __attribute__((aligned(16))) double PnT[kCholNB * kCholLd];  // the panel, k-major: PnT[k * kCholLd + row]
+    __shared__ double Rd[kCholMaxN];                                         // reciprocal diagonal R
+    __shared__ double xs[kCholMaxN];                                         // right-hand side / solution
     __shared__ int bad;
     if (tid == 0) bad = 0;
+    for (int i = tid; i < np; i += nt) xs[i] = i < n ? -d.bs[i] : 0.0;
     __syncthreads();
     BA_T0();
-    for (int K0 = 0; K0 < n; K0 += kCholNB) {
-        const int nb = min(kCholNB, n - K0), rows = n - K0;
-        for (int e = tid; e < rows * nb; e += nt) {
-            const int r = e / nb, c = e % nb;
-            Pn[r * kCholLd + c] = S[(size_t)(K0 + r) * n + K0 + c];
+    for (int K0 = 0; K0 < np; K0 += kCholNB) {
+        const int below = np - K0 - kCholNB, rb = tid - 64;
+        double a[kCholNB];
+        if (tid < 64) {
+            // 1. the diagonal block: lane i < 32 holds row K0 + i (lanes 32.. duplicate row 31; the
+            // entries right of the diagonal are computed as garbage and never read)
+            const int lr = min(lane, kCholNB - 1);
+#pragma unroll
+            for (int c = 0; c < kCholNB; c++) a[c] = S[(size_t)(K0 + lr) * np + K0 + c];
+            bool fail = false;
+#pragma unroll
+            for (int c = 0; c < kCholNB; c++) {
+                const double s = readlane_f64(a[c], c);
+                fail |= s < DBL_EPSILON;
+                const double r = 1.0 / sqrt(s);
+                if (lane == 0) Rd[K0 + c] = r;
+                const double l = a[c] * r;
+                a[c] = l;
+                // the column's entries by readlane, 8 at a time (the scheduler would otherwise hoist
+                // all of them into SGPRs at once)
+#pragma unroll
+                for (int j = c + 1; j < kCholNB; j++) {
+                    a[j] -= l * readlane_f64(l, j);
+                    if ((j - c) % 8 == 0) __builtin_amdgcn_sched_barrier(0);
+                }
+            }
+            // the whole row (neither PnT's nor S's upper triangle is read, and S is rebuilt by
+            // every iteration's k_ba_schur)
+            if (lane < kCholNB) {
+#pragma unroll
+                for (int c = 0; c < kCholNB; c++) {
+                    PnT[c * kCholLd + K0 + lane] = a[c];
+                    S[(size_t)(K0 + lane) * np + K0 + c] = a[c];
+                }
+            }
+            if (lane == 0 && fail) bad = 1;
+        } else if (rb < below) {
+#pragma unroll
+            for (int c = 0; c < kCholNB; c++) a[c] = S[(size_t)(K0 + kCholNB + rb) * np + K0 + c];
         }
         __syncthreads();
         BA_T(0);
-        // panel: thread r owns row r, held in registers (columns unrolled).  Step kk: the owner of
-        // row kk publishes the pivot sqrt; every row below divides its column-kk entry once and
-        // publishes it in Lc; then each row applies column kk to its columns kk+1.. .
-        double prow[kCholNB];
-        const bool own = tid < rows;
+        if (bad) break;
+        // 2. rows below: L_ic = (S_ic - sum_{k<c} L_ik L_ck) * R_c, column by column
+        if (tid >= 64 && rb < below) {
+            const int i = K0 + kCholNB + rb;
 #pragma unroll
-        for (int c = 0; c < kCholNB; c++) prow[c] = (own && c < nb) ? Pn[tid * kCholLd + c] : 0.0;
-        bool stop = false;
+            for (int c = 0; c < kCholNB; c++) {
+                const double l = a[c] * Rd[K0 + c];
+                a[c] = l;
 #pragma unroll
-        for (int kk = 0; kk < kCholNB; kk++) {
-            if (kk < nb && !stop) {
-                if (tid == kk) {
-                    const double v = prow[kk];
-                    if (!(v > 0)) bad = 1;
-                    s_piv = sqrt(v);
-                    prow[kk] = s_piv;
-                }
-                __syncthreads();
-                stop = bad != 0;
-                if (!stop) {
-                    const double piv = s_piv;
-                    double lrk = 0.0;
-                    if (own && tid > kk) {
-                        lrk = prow[kk] / piv;
-                        prow[kk] = lrk;
-                        Lc[tid] = lrk;
-                    }
-                    __syncthreads();
-                    if (own && tid > kk) {
+                for (int j = c + 1; j < kCholNB; j++) a[j] -= l * PnT[c * kCholLd + K0 + j];
+                __builtin_amdgcn_sched_barrier(0);  // one column's LDS reads in flight at a time
+            }
 #pragma unroll
-                        for (int c = kk + 1; c < kCholNB; c++)
-                            if (c < nb && c <= tid) prow[c] -= lrk * Lc[c];
-                    }
-                }
+            for (int c = 0; c < kCholNB; c++) {
+                PnT[c * kCholLd + i] = a[c];
+                S[(size_t)i * np + K0 + c] = a[c];
             }
         }
-        __syncthreads();
-        if (own && !bad)
-#pragma unroll
-            for (int c = 0; c < kCholNB; c++)
-                if (c < nb && c <= tid) Pn[tid * kCholLd + c] = prow[c];
         __syncthreads();
         BA_T(1);
-        if (bad) break;
-        for (int e = tid; e < rows * nb; e += nt) {  // the factored L columns
-            const int r = e / nb, c = e % nb;
-            if (c <= r) S[(size_t)(K0 + r) * n + K0 + c] = Pn[r * kCholLd + c];
-        }
-        // trailing lower triangle (rows / columns K0 + nb ..), 4 x 4 tiles on or below the diagonal
-        const int base = nb, m = rows - nb;
-        const int mt = (m + 3) / 4;
-        const long tiles = (long)mt * (mt + 1) / 2;
-        for (long t = tid; t < tiles; t += nt) {
+        // 3. trailing lower triangle (rows / columns K0 + 32 ..), 4 x 4 tiles on or below the
+        // diagonal, tile t = ti (ti + 1) / 2 + tj so that neighbouring lanes share their rows
+        const int base = K0 + kCholNB, mt = below / 4;
+        const int tiles = mt * (mt + 1) / 2;
+        for (int t = tid; t < tiles; t += nt) {
             int ti = (int)((sqrt(8.0 * (double)t + 1.0) - 1.0) * 0.5);
-            while ((long)ti * (ti + 1) / 2 > t) ti--;
-            while ((long)(ti + 1) * (ti + 2) / 2 <= t) ti++;
-            const int tj = (int)(t - (long)ti * (ti + 1) / 2);
+            while (ti * (ti + 1) / 2 > t) ti--;
+            while ((ti + 1) * (ti + 2) / 2 <= t) ti++;
+            const int tj = t - ti * (ti + 1) / 2;
+            const int r0 = base + 4 * ti, c0 = base + 4 * tj;
+            const bool diag = ti == tj;
             double acc[4][4];
-            int ri[4], cj[4];
-#pragma unroll
-            for (int x = 0; x < 4; x++) {
-                ri[x] = base + 4 * ti + x;
-                cj[x] = base + 4 * tj + x;
-            }
 #pragma unroll
             for (int x = 0; x < 4; x++)
 #pragma unroll
-                for (int y = 0; y < 4; y++)
-                    acc[x][y] = (ri[x] < rows && cj[y] <= ri[x]) ? S[(size_t)(K0 + ri[x]) * n + K0 + cj[y]] : 0.0;
-            for (int kk = 0; kk < nb; kk++) {
-                double a[4], b[4];
-#pragma unroll
-                for (int x = 0; x < 4; x++) {
-                    a[x] = ri[x] < rows ? Pn[ri[x] * kCholLd + kk] : 0.0;
-                    b[x] = cj[x] < rows ? Pn[cj[x] * kCholLd + kk] : 0.0;
-                }
+                for (int y = 0; y < 4; y++) acc[x][y] = S[(size_t)(r0 + x) * np + c0 + y];
+#pragma unroll 8
+            for (int k = 0; k < kCholNB; k++) {
+                const double2* pr = reinterpret_cast<const double2*>(&PnT[k * kCholLd + r0]);
+                const double2* pc = reinterpret_cast<const double2*>(&PnT[k * kCholLd + c0]);
+                const double2 a01 = pr[0], a23 = pr[1], b01 = pc[0], b23 = pc[1];
+                const double av[4] = {a01.x, a01.y, a23.x, a23.y}, bv[4] = {b01.x, b01.y, b23.x, b23.y};
 #pragma unroll
                 for (int x = 0; x < 4; x++)
 #pragma unroll
-                    for (int y = 0; y < 4; y++) acc[x][y] -= a[x] * b[y];
+                    for (int y = 0; y < 4; y++) acc[x][y] -= av[x] * bv[y];
             }
+            // (a diagonal tile's entries above the diagonal belong to S's upper triangle: not stored)
 #pragma unroll
             for (int x = 0; x < 4; x++)
 #pragma unroll
                 for (int y = 0; y < 4; y++)
-                    if (ri[x] < rows && cj[y] <= ri[x]) S[(size_t)(K0 + ri[x]) * n + K0 + cj[y]] = acc[x][y];
+                    if (!diag || y <= x) S[(size_t)(r0 + x) * np + c0 + y] = acc[x][y];
         }
         __syncthreads();
         BA_T(2);
@@ -391,66 +485,78 @@ __global__ __launch_bounds__(1024) void k_ba_chol(BaDev d) {
         if (tid == 0) d.ctl->solved = 0;
         return;
     }
-    // L y = -bs: block by block; y[i] = (b[i] - sum_{k < i} L[i][k] y[k]) / L[i][i], the sum in
-    // ascending k (the oracle's column sweep applies the same subtractions in the same order)
-    for (int i = tid; i < n; i += nt) xs[i] = -d.bs[i];
-    __syncthreads();
-    for (int K0 = 0; K0 < n; K0 += kCholNB) {
-        const int nb = min(kCholNB, n - K0);
-        for (int e = tid; e < nb * nb; e += nt) Db[(e / nb) * kCholLd + e % nb] = S[(size_t)(K0 + e / nb) * n + K0 + e % nb];
-        __syncthreads();
-        if (tid < 64) {  // lane i holds x[K0 + i] and row i of the diagonal block
-            double x = lane < nb ? xs[K0 + lane] : 0.0;
-            double drow[kCholNB];
+    // 4a. L y = -bs: y_i = (x_i - sum_{k<i} L_ik y_k) * R_i, ascending k.  In the diagonal block lane
+    // i keeps x_i and takes -0 * y_k for k >= i (its row's upper part is zeroed), so the loop has no
+    // lane conditions; y_i = x_i R_i at the end is the y_k the other lanes used.
+    for (int K0 = 0; K0 < np; K0 += kCholNB) {
+        int ln = lane;
+        asm volatile("" : "+v"(ln));  // per-block lane compares: not hoisted into live SGPR masks
+        double Lr[kCholNB];
+        if (tid < 64) {
+            const int lr = min(ln, kCholNB - 1);
 #pragma unroll
-            for (int j = 0; j < kCholNB; j++) drow[j] = (lane < nb && j <= lane && j < nb) ? Db[lane * kCholLd + j] : 1.0;
+            for (int c = 0; c < kCholNB; c++) {
+                const double v = S[(size_t)(K0 + lr) * np + K0 + c];
+                Lr[c] = c < ln ? v : 0.0;
+            }
+            double x = xs[K0 + lr];
 #pragma unroll
             for (int k = 0; k < kCholNB; k++) {
-                if (k < nb) {
-                    const double q = x / drow[k];  // lane k: x[k] /= L[k][k]
-                    if (lane == k) x = q;
-                    const double xk = __shfl(q, k);
-                    if (lane > k && lane < nb) x -= drow[k] * xk;
-                }
+                const double y = readlane_f64(x, k) * Rd[K0 + k];
+                x -= Lr[k] * y;
             }
-            if (lane < nb) xs[K0 + lane] = x;
+            if (ln < kCholNB) xs[K0 + ln] = x * Rd[K0 + ln];
+        } else {
+            // the rows below: their block entries loaded while wave 0 solves the block
+            const int i = min(K0 + kCholNB + (tid - 64), np - 1);
+#pragma unroll
+            for (int c = 0; c < kCholNB; c++) Lr[c] = S[(size_t)i * np + K0 + c];
         }
         __syncthreads();
-        for (int i = K0 + nb + tid; i < n; i += nt) {  // rows below take this block, ascending k
-            double s = xs[i];
-            const double* Li = S + (size_t)i * n + K0;
-            for (int k = 0; k < nb; k++) s -= Li[k] * xs[K0 + k];
-            xs[i] = s;
+        if (tid >= 64) {
+            const int i = K0 + kCholNB + (tid - 64);
+            if (i < np) {
+                double s = xs[i];
+#pragma unroll
+                for (int k = 0; k < kCholNB; k++) s -= Lr[k] * xs[K0 + k];
+                xs[i] = s;
+            }
         }
         __syncthreads();
     }
     BA_T(3);
-    // L^T x = y: blocks from the last; rows above take a finished block in descending k
-    const int nblk = (n + kCholNB - 1) / kCholNB;
-    for (int bI = nblk - 1; bI >= 0; bI--) {
-        const int K0 = bI * kCholNB, nb = min(kCholNB, n - K0);
-        for (int e = tid; e < nb * nb; e += nt) Db[(e / nb) * kCholLd + e % nb] = S[(size_t)(K0 + e / nb) * n + K0 + e % nb];
-        __syncthreads();
-        if (tid < 64) {  // lane i holds x[K0 + i] and column i of the diagonal block
-            double x = lane < nb ? xs[K0 + lane] : 0.0;
-            double dcol[kCholNB];
+    // 4b. L^T x = y: x_i = (y_i - sum_{k>i, descending} L_ki x_k) * R_i (the block's column entries
+    // above the diagonal zeroed the same way)
+    for (int K0 = np - kCholNB; K0 >= 0; K0 -= kCholNB) {
+        int ln = lane;
+        asm volatile("" : "+v"(ln));
+        double Lc[kCholNB];
+        if (tid < 64) {
+            const int lc = min(ln, kCholNB - 1);
 #pragma unroll
-            for (int j = 0; j < kCholNB; j++) dcol[j] = (lane < nb && j >= lane && j < nb) ? Db[j * kCholLd + lane] : 1.0;
-#pragma unroll
-            for (int kq = kCholNB - 1; kq >= 0; kq--) {
-                if (kq < nb) {
-                    const double q = x / dcol[kq];  // lane kq: x[kq] /= L[kq][kq]
-                    if (lane == kq) x = q;
-                    const double xk = __shfl(q, kq);
-                    if (lane < kq) x -= dcol[kq] * xk;
-                }
+            for (int k = 0; k < kCholNB; k++) {
+                const double v = S[(size_t)(K0 + k) * np + K0 + lc];
+                Lc[k] = k > ln ? v : 0.0;
             }
-            if (lane < nb) xs[K0 + lane] = x;
+            double x = xs[K0 + lc];
+#pragma unroll
+            for (int k = kCholNB - 1; k >= 0; k--) {
+                const double v = readlane_f64(x, k) * Rd[K0 + k];
+                x -= Lc[k] * v;
+            }
+            if (ln < kCholNB) xs[K0 + ln] = x * Rd[K0 + ln];
+        } else {
+            // the rows above: column i of the block's rows, loaded while wave 0 solves the block
+            const int i = min(tid - 64, np - 1);
+#pragma unroll
+            for (int k = 0; k < kCholNB; k++) Lc[k] = S[(size_t)(K0 + k) * np + i];
         }
         __syncthreads();
-        for (int i = tid; i < K0; i += nt) {
+        if (tid >= 64 && tid - 64 < K0) {
+            const int i = tid - 64;
             double s = xs[i];
-            for (int k = nb - 1; k >= 0; k--) s -= S[(size_t)(K0 + k) * n + i] * xs[K0 + k];
+#pragma unroll
+            for (int k = kCholNB - 1; k >= 0; k--) s -= Lc[k] * xs[K0 + k];
             xs[i] = s;
         }
         __syncthreads();
@@ -553,6 +659,11 @@ int local_ba(vs_ctx* ctx, int N, double* R, double* t, int M, double* P, int n_o
     VS_ARG(N <= VS_BA_MAX_KEYFRAMES, "vs_local_ba: more keyframes than VS_BA_MAX_KEYFRAMES");
     for (int o = 0; o < n_obs; o++)
         VS_ARG(okf[o] >= 0 && okf[o] < N && opt[o] >= 0 && opt[o] < M, "vs_local_ba: observation index out of range");
+    // host phase wall times (VS_BA_HOST_PROFILE=1: one stderr line per call)
+    static const bool hprof = std::getenv("VS_BA_HOST_PROFILE") != nullptr;
+    using hclock = std::chrono::steady_clock;
+    const hclock::time_point h0 = hclock::now();
+    hclock::time_point h1 = h0, h2 = h0, h3 = h0;
     // ---- structure (host, once) ----
     std::vector<std::vector<int>> observers(M);
     std::vector<int> oslot(n_obs);
@@ -614,7 +725,7 @@ int local_ba(vs_ctx* ctx, int N, double* R, double* t, int M, double* P, int n_o
     }
     // ---- device buffers (one allocation) ----
     const int n_chunks = cdiv(n_obs, kCostChunk);
-    const int n = 6 * N;
+    const int n = 6 * N, np = (n + 31) / 32 * 32;
     size_t bytes = 0;
     auto take = [&](size_t b) {
         const size_t at = bytes;
@@ -632,9 +743,10 @@ int local_ba(vs_ctx* ctx, int N, double* R, double* t, int M, double* P, int n_o
                  o_pc = take(sizeof(PoseC) * N), o_pcn = take(sizeof(PoseC) * N),
                  o_terms = take(sizeof(ObsTerms) * (size_t)n_obs), o_Hpp = take(288ull * N), o_bp = take(48ull * N),
                  o_Hmm = take(72ull * M), o_bm = take(24ull * M), o_Hpm = take(144ull * n_pairs),
-                 o_Hinv = take(72ull * M), o_U = take(144ull * n_pairs), o_S = take(8ull * n * n),
+                 o_Hinv = take(72ull * M), o_U = take(144ull * n_pairs), o_S = take(8ull * np * np),
                  o_bs = take(8ull * n), o_dp = take(8ull * n), o_chunk = take(8ull * n_chunks),
                  o_pvalid = take(4ull * M), o_ctl = take(sizeof(BaCtl));
+    h1 = hclock::now();
     VS_CHECK(ctx->ba.ensure(bytes));
     char* base = ctx->ba.as<char>();
     hipStream_t s = ctx->stream;
@@ -672,12 +784,14 @@ int local_ba(vs_ctx* ctx, int N, double* R, double* t, int M, double* P, int n_o
     ctl0.done = max_iter <= 0;
     VS_HIP(up(o_ctl, &ctl0, sizeof(ctl0)));
 
+    h2 = hclock::now();
     BaDev d;
     d.N = N;
     d.M = M;
     d.n_obs = n_obs;
     d.n_pairs = n_pairs;
     d.n_chunks = n_chunks;
+    d.np = np;
     d.K = Cam{K4[0], K4[1], K4[2], K4[3]};
 #define BA_PTR(T, o) reinterpret_cast<T*>(base + (o))
     d.okf = BA_PTR(int, o_okf);
@@ -724,6 +838,7 @@ int local_ba(vs_ctx* ctx, int N, double* R, double* t, int M, double* P, int n_o
         ProfScope ps(ctx, "local_ba", s);
         const int T = 256;
         hipLaunchKernelGGL(k_ba_init, dim3(cdiv(N, T)), dim3(T), 0, s, d, (const double*)(base + o_R));
+        if (np > n) hipLaunchKernelGGL(k_ba_pad, dim3(cdiv((long)(np - n) * np, T)), dim3(T), 0, s, d);
         hipLaunchKernelGGL(k_ba_pose_cache, dim3(cdiv(N, T)), dim3(T), 0, s, d, 0, 0);
         hipLaunchKernelGGL(k_ba_chunk_sums, dim3(n_chunks), dim3(kCostChunk), 0, s, d, 2, 0);
         hipLaunchKernelGGL(k_ba_control, dim3(1), dim3(1), 0, s, d, 2);
@@ -735,7 +850,7 @@ int local_ba(vs_ctx* ctx, int N, double* R, double* t, int M, double* P, int n_o
             hipLaunchKernelGGL(k_ba_kf_acc, dim3(N), dim3(64), 0, s, d);
             hipLaunchKernelGGL(k_ba_pt_acc, dim3(cdiv(M, T)), dim3(T), 0, s, d);
             hipLaunchKernelGGL(k_ba_schur, dim3(N * N), dim3(64), 0, s, d);
-            hipLaunchKernelGGL(k_ba_chol, dim3(1), dim3(1024), 0, s, d);
+            hipLaunchKernelGGL(k_ba_chol, dim3(1), dim3(512), 0, s, d);
             hipLaunchKernelGGL(k_ba_update, dim3(cdiv(M + N, T)), dim3(T), 0, s, d);
             hipLaunchKernelGGL(k_ba_pose_cache, dim3(cdiv(N, T)), dim3(T), 0, s, d, 1, 1);
             hipLaunchKernelGGL(k_ba_chunk_sums, dim3(n_chunks), dim3(kCostChunk), 0, s, d, 1, 1);
@@ -749,12 +864,20 @@ int local_ba(vs_ctx* ctx, int N, double* R, double* t, int M, double* P, int n_o
                            (double*)(base + o_t), (double*)(base + o_Pn));
         VS_HIP(hipGetLastError());
     }
+    h3 = hclock::now();
     BaCtl out;
     VS_HIP(hipMemcpyAsync(&out, base + o_ctl, sizeof(out), hipMemcpyDeviceToHost, s));
     VS_HIP(hipMemcpyAsync(R, base + o_R, 72ull * N, hipMemcpyDeviceToHost, s));
     VS_HIP(hipMemcpyAsync(t, base + o_t, 24ull * N, hipMemcpyDeviceToHost, s));
     VS_HIP(hipMemcpyAsync(P, base + o_Pn, 24ull * M, hipMemcpyDeviceToHost, s));
     VS_HIP(hipStreamSynchronize(s));
+    if (hprof) {
+        auto ms = [](hclock::time_point a, hclock::time_point b) {
+            return std::chrono::duration<double, std::milli>(b - a).count();
+        };
+        std::fprintf(stderr, "vs_local_ba host: structure %.3f ms, upload %.3f ms, enqueue %.3f ms, wait %.3f ms\n",
+                     ms(h0, h1), ms(h1, h2), ms(h2, h3), ms(h3, hclock::now()));
+    }
     *err_before = out.err_before;
     *err_after = out.err_after;
     if (stats) {

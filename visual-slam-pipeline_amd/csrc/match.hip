@@ -30,8 +30,9 @@
 //     best0 — the exact top-2 of the union, independent of arrival order;
 //   * the last workgroup of a pair to arrive (a device-scope counter; every atomic of the earlier
 //     workgroups has returned before their arrival) reads and resets the keys with atomicExch,
-//     applies the ratio test and compacts the good rows in query order.  Keys and counters are
-//     left reset for the next launch.
+//     applies the ratio test and compacts the good rows in query order: up to 4 x NTH queries per
+//     pass with all their exchanges in flight, per-wave ballots and one barrier.  Keys and
+//     counters are left reset for the next launch.
 #include <hip/hip_runtime.h>
 
 #include <climits>
@@ -55,6 +56,7 @@ __device__ __forceinline__ void static_for(F&& f) {
 }
 
 constexpr unsigned long long kNoKey = ~0ull;
+constexpr int kTailChunks = 4;  // last arrival: query chunks of NTH per pass
 
 // Sequential fmaf-chain squared norm of every descriptor row of F frames.
 __global__ __launch_bounds__(256) void k_desc_norms(const float* __restrict__ desc, const int* __restrict__ n,
@@ -129,8 +131,8 @@ __global__ __launch_bounds__(64 * NWQ * NWT) void k_match(MatchArgs a) {
     __shared__ float4 sbuf[NB][R * RS4];
     __shared__ float s_norm[R];
     __shared__ unsigned long long s_top[NWT > 1 ? NWT : 1][TQ][2];
-    __shared__ int s_wave[NW];
-    __shared__ int s_last, s_base;
+    __shared__ int s_cnt[kTailChunks][NW];
+    __shared__ int s_last;
 
     // linear work index: XCD x (= blockIdx % 8 under round-robin placement) takes a contiguous range
     const int L = (blockIdx.x & 7) * a.per_xcd + (blockIdx.x >> 3);
@@ -389,46 +391,63 @@ __global__ __launch_bounds__(64 * NWQ * NWT) void k_match(MatchArgs a) {
     if (!s_last) return;
 
     // ---- last arrival: ratio test + order-preserving compaction (Slam.cpp:1151-1157) ----
-    if (tid == 0) {
-        s_base = 0;
-        atomicExch(a.cnt + p, 0u);
-    }
-    __syncthreads();
+    // up to kTailChunks x NTH queries per pass: every key exchange of the pass in flight together,
+    // per-wave ballots, one barrier, then each thread's slot from the per-(chunk, wave) counts
+    if (tid == 0) atomicExch(a.cnt + p, 0u);
     vs_match* raw = a.raw + (size_t)p * a.ostride;
     vs_match* good = a.good + (size_t)p * a.ostride;
-    for (int c0 = 0; c0 < n1; c0 += NTH) {
-        const int i = c0 + tid;
-        bool f = false;
-        vs_match m;
-        if (i < n1) {
-            const unsigned long long k0 = atomicExch(B0 + i, kNoKey), k1 = atomicExch(B1 + i, kNoKey);
-            const float dist0 = sqrt_rn(__uint_as_float((unsigned)(k0 >> 32)));
-            const float dist1 = sqrt_rn(__uint_as_float((unsigned)(k1 >> 32)));
-            m.query_idx = i;
-            m.train_idx = (int)(unsigned)k0;
-            m.img_idx = 0;
-            m.distance = dist0;
-            raw[i] = m;
-            f = dist0 < a.ratio * dist1;
+    int base = 0;
+    for (int c0 = 0; c0 < n1; c0 += kTailChunks * NTH) {
+        unsigned long long k0[kTailChunks], k1[kTailChunks];
+#pragma unroll
+        for (int u = 0; u < kTailChunks; u++) {
+            const int i = c0 + u * NTH + tid;
+            k0[u] = k1[u] = kNoKey;
+            if (i < n1) {
+                k0[u] = atomicExch(B0 + i, kNoKey);
+                k1[u] = atomicExch(B1 + i, kNoKey);
+            }
         }
-        const unsigned long long bal = __ballot(f);
-        const int before = __popcll(bal & ((1ull << lane) - 1ull));
-        if (lane == 0) s_wave[wv] = __popcll(bal);
-        __syncthreads();
-        int off = s_base;
-        for (int k = 0; k < wv; k++) off += s_wave[k];
-        if (f) good[off + before] = m;
-        __syncthreads();
-        if (tid == 0) {
-            int tot = 0;
-            for (int k = 0; k < NW; k++) tot += s_wave[k];
-            s_base += tot;
+        bool f[kTailChunks];
+        vs_match m[kTailChunks];
+        int before[kTailChunks];
+#pragma unroll
+        for (int u = 0; u < kTailChunks; u++) {
+            const int i = c0 + u * NTH + tid;
+            f[u] = false;
+            if (i < n1) {
+                const float dist0 = sqrt_rn(__uint_as_float((unsigned)(k0[u] >> 32)));
+                const float dist1 = sqrt_rn(__uint_as_float((unsigned)(k1[u] >> 32)));
+                m[u].query_idx = i;
+                m[u].train_idx = (int)(unsigned)k0[u];
+                m[u].img_idx = 0;
+                m[u].distance = dist0;
+                raw[i] = m[u];
+                f[u] = dist0 < a.ratio * dist1;
+            }
+            const unsigned long long bal = __ballot(f[u]);
+            before[u] = __popcll(bal & ((1ull << lane) - 1ull));
+            if (lane == 0) s_cnt[u][wv] = __popcll(bal);
         }
         __syncthreads();
+        int run = base;
+#pragma unroll
+        for (int u = 0; u < kTailChunks; u++) {
+            int off = run;
+#pragma unroll
+            for (int w = 0; w < NW; w++) {
+                const int cw = s_cnt[u][w];
+                off += w < wv ? cw : 0;
+                run += cw;
+            }
+            if (f[u]) good[off + before[u]] = m[u];
+        }
+        base = run;
+        if (c0 + kTailChunks * NTH < n1) __syncthreads();  // s_cnt is rewritten by the next pass
     }
     if (tid == 0) {
         a.nraw[p] = n1;
-        a.ngood[p] = s_base;
+        a.ngood[p] = base;
     }
 }
 
