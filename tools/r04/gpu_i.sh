@@ -1,5 +1,5 @@
 #!/bin/bash
-# local-BA: Cholesky rewrite + double-buffered kf_acc / schur staging + register Hpm slots (cv::solve DECOMP_CHOLESKY arithmetic, wave-0 diagonal block): parity, phases, config[2] timing
+# local-BA: look-ahead Cholesky, flat host structure, LM enqueue stops after convergence
 export TMPDIR=/tmp
 O=gpurun_out/r04i; mkdir -p $O
 timeout -k 10 600 python -u -m pytest tests/test_gpu_ba.py tests/test_golden.py -m gpu -x -q --timeout 300 --timeout-method thread -p no:cacheprovider > $O/pytest.log 2>&1

@@ -15,7 +15,7 @@
 //                     diagonal - sum over common points (ascending) of U_a Hpm_b^T; b_a likewise
 //   k_ba_chol         dense right-looking Cholesky + the two triangular solves (one workgroup)
 //   k_ba_update       back-substitution dm = Hinv (-bm - sum Hpm^T dp), new poses
-//   k_ba_chunk_sums / k_ba_control   new cost, accept / reject, lambda, convergence
+//   k_ba_cost         new cost (fixed chunks) + accept / reject, lambda, convergence (last chunk)
 // Every element is accumulated in the same order as the CPU restatement (oracle/orc_ba.cpp); the
 // global cost sums use fixed chunks of 256 observations.  Arithmetic shared via ba_solvers.h.
 #include <hip/hip_runtime.h>
@@ -36,6 +36,7 @@ using namespace vs_ba;
 struct BaCtl {
     double lambda, total_cost, new_cost, err_before, err_after;
     int iter, accepted, done, solved, take, max_iter;
+    unsigned arrive;  // k_ba_cost's arrival counter (left at 0)
 };
 
 struct BaDev {
@@ -50,6 +51,7 @@ struct BaDev {
     double *Hpp, *bp, *Hmm, *bm, *Hpm, *Hinv, *U, *S, *bs, *dp, *chunk;
     int* pvalid;
     BaCtl* ctl;
+    int* done_host;  // mapped pinned host memory: ctl->done after every accept / reject
 };
 
 #define BA_LIVE(d) \
@@ -77,10 +79,51 @@ __global__ void k_ba_obs(BaDev d) {
     ba_obs_terms(d.pc[d.okf[o]], d.P + 3 * (size_t)d.opt[o], d.ouv[2 * o], d.ouv[2 * o + 1], d.K, d.terms[o]);
 }
 
-// mode 0: total_cost from the terms; 1: new_cost (new params); 2: squared error (current params).
-// One 256-lane workgroup per fixed chunk of kCostChunk observations: the per-observation terms in
-// parallel into LDS, then lane 0 sums them in observation order (the oracle's chunked order).
-__global__ __launch_bounds__(kCostChunk) void k_ba_chunk_sums(BaDev d, int mode, int check) {
+// mode 0: total_cost; 1: new cost + accept/reject; 2: err_before; 3: err_after
+// s: the cost summed over the chunks in order (k_ba_cost's last workgroup)
+__device__ void ba_control(const BaDev& d, int mode, double s) {
+    BaCtl& c = *d.ctl;
+    if (mode <= 1 && c.done) return;
+    if (mode == 0) {
+        c.total_cost = s;
+        return;
+    }
+    if (mode == 2) {
+        c.err_before = sqrt(s / d.n_obs);
+        return;
+    }
+    if (mode == 3) {
+        c.err_after = sqrt(s / d.n_obs);
+        return;
+    }
+    c.take = 0;
+    if (!c.solved) {  // the oracle: lambda * 10 and the next iteration
+        c.lambda *= 10;
+    } else {
+        c.new_cost = s;
+        if (s < c.total_cost) {
+            c.take = 1;
+            c.lambda = c.lambda * 0.5 > 1e-7 ? c.lambda * 0.5 : 1e-7;
+            c.accepted++;
+            const double rel = (c.total_cost - s) / (c.total_cost + 1e-10);
+            if (rel < 1e-4) c.done = 1;
+        } else {
+            c.lambda *= 5.0;
+            if (c.lambda > 1e6) c.done = 1;
+        }
+    }
+    c.iter++;
+    if (c.iter >= c.max_iter) c.done = 1;
+    __hip_atomic_store(d.done_host, c.done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// The global cost and the LM control in one launch.  mode 0: total_cost from the terms; 1: new_cost
+// (new params); 2: squared error (current params).  One 256-lane workgroup per fixed chunk of
+// kCostChunk observations: the per-observation terms in parallel into LDS, then lane 0 sums them in
+// observation order (the oracle's chunked order) and publishes the chunk with a device-scope atomic
+// store; the last chunk to arrive (a device-scope counter, every earlier chunk's store performed
+// before its arrival) sums the chunks in order and runs the control step cmode (ba_control).
+__global__ __launch_bounds__(kCostChunk) void k_ba_cost(BaDev d, int mode, int check, int cmode) {
     if (check) BA_LIVE(d);
     __shared__ double s_v[kCostChunk];
     const int c = blockIdx.x, t = threadIdx.x;
@@ -101,7 +144,15 @@ __global__ __launch_bounds__(kCostChunk) void k_ba_chunk_sums(BaDev d, int mode,
     if (t == 0) {
         double sum = 0;
         for (int k = 0; k < o1 - o0; k++) sum += s_v[k];
-        d.chunk[c] = sum;
+        __hip_atomic_store(d.chunk + c, sum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const unsigned prev = __hip_atomic_fetch_add(&d.ctl->arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (prev == (unsigned)d.n_chunks - 1) {
+            __hip_atomic_store(&d.ctl->arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            double tot = 0;
+            for (int k = 0; k < d.n_chunks; k++) tot += __hip_atomic_load(d.chunk + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            ba_control(d, cmode, tot);
+        }
     }
 }
 
@@ -215,8 +266,54 @@ __global__ void k_ba_pt_acc(BaDev d) {
         for (int sl = 0; sl < np; sl++) ba_schur_u(d.Hpm + 18 * (size_t)(p0 + sl), Hi, d.U + 18 * (size_t)(p0 + sl));
 }
 
-// grid: N*N workgroups of 64 threads; threads 0..35 own S_ab(r, c), threads 0..5 then own b_a(r)
-// on the diagonal workgroups.  The (U, Hpm) pairs of the common points are staged 64 at a time
+// b_a = bp_a - sum over the points of keyframe a (ascending) of U_a bm, one 64-lane workgroup per
+// keyframe (threads 0..5 own b_a(r)), staged like the S blocks
+__device__ __forceinline__ void schur_b(const BaDev& d, int a, double (*s_U)[64][18], double (*s_H)[64][18],
+                                        int (*s_ok)[64]) {
+    const int t = threadIdx.x;
+    double u[18];
+    int ok = 0;
+    double sb = t < 6 ? d.bp[6 * a + t] : 0.0;
+    double bmv[3];
+    const int k0 = d.kb_off[a], k1 = d.kb_off[a + 1];
+    auto fetch_b = [&](int qb) {
+        const int q = qb + t;
+        if (q < k1) {
+            const int j = d.kb_j[q];
+            const double* U = d.U + 18 * (size_t)d.kb_u[q];
+#pragma unroll
+            for (int k = 0; k < 18; k++) u[k] = U[k];
+#pragma unroll
+            for (int k = 0; k < 3; k++) bmv[k] = d.bm[3 * (size_t)j + k];
+            ok = d.pvalid[j];
+        }
+    };
+    fetch_b(k0);
+    int buf = 0;
+    for (int qb = k0; qb < k1; qb += 64) {
+        if (qb + t < k1) {
+#pragma unroll
+            for (int k = 0; k < 18; k++) s_U[buf][t][k] = u[k];
+#pragma unroll
+            for (int k = 0; k < 3; k++) s_H[buf][t][k] = bmv[k];
+            s_ok[buf][t] = ok;
+        }
+        __syncthreads();
+        if (qb + 64 < k1) fetch_b(qb + 64);
+        const int m = min(64, k1 - qb);
+        if (t < 6)
+#pragma unroll 4
+            for (int k = 0; k < m; k++) {
+                const double v = ba_schur_b(s_U[buf][k], s_H[buf][k], t);
+                sb -= s_ok[buf][k] ? v : 0.0;
+            }
+        buf ^= 1;
+    }
+    if (t < 6) d.bs[6 * a + t] = sb;
+}
+
+// grid: N*N workgroups of 64 threads, threads 0..35 owning S_ab(r, c), then N workgroups for b_a
+// (schur_b).  The (U, Hpm) pairs of the common points are staged 64 at a time
 // through two LDS buffers, the next stage's loads in flight while the current one is summed (one
 // barrier per stage); sums run over the lists in order (the oracle's), a skipped point (no
 // inverse) subtracting +0.0, which leaves every value unchanged.
@@ -224,7 +321,12 @@ __global__ __launch_bounds__(64) void k_ba_schur(BaDev d) {
     BA_LIVE(d);
     __shared__ double s_U[2][64][18], s_H[2][64][18];
     __shared__ int s_ok[2][64];
-    const int a = blockIdx.x / d.N, b = blockIdx.x % d.N, t = threadIdx.x;
+    const int t = threadIdx.x;
+    if ((int)blockIdx.x >= d.N * d.N) {  // workgroups N*N ..: b_a, beside the S blocks
+        schur_b(d, (int)blockIdx.x - d.N * d.N, s_U, s_H, s_ok);
+        return;
+    }
+    const int a = blockIdx.x / d.N, b = blockIdx.x % d.N;
     const int np = d.np;
     const double lam = d.ctl->lambda;
     const int r = t / 6, c = t % 6;
@@ -273,46 +375,8 @@ __global__ __launch_bounds__(64) void k_ba_schur(BaDev d) {
         buf ^= 1;
     }
     if (t < 36) d.S[(size_t)(6 * a + r) * np + 6 * b + c] = s;
-    if (a != b) return;
-    __syncthreads();  // both buffers free again
-    double sb = t < 6 ? d.bp[6 * a + t] : 0.0;
-    double bmv[3];
-    const int k0 = d.kb_off[a], k1 = d.kb_off[a + 1];
-    auto fetch_b = [&](int qb) {
-        const int q = qb + t;
-        if (q < k1) {
-            const int j = d.kb_j[q];
-            const double* U = d.U + 18 * (size_t)d.kb_u[q];
-#pragma unroll
-            for (int k = 0; k < 18; k++) u[k] = U[k];
-#pragma unroll
-            for (int k = 0; k < 3; k++) bmv[k] = d.bm[3 * (size_t)j + k];
-            ok = d.pvalid[j];
-        }
-    };
-    fetch_b(k0);
-    buf = 0;
-    for (int qb = k0; qb < k1; qb += 64) {
-        if (qb + t < k1) {
-#pragma unroll
-            for (int k = 0; k < 18; k++) s_U[buf][t][k] = u[k];
-#pragma unroll
-            for (int k = 0; k < 3; k++) s_H[buf][t][k] = bmv[k];
-            s_ok[buf][t] = ok;
-        }
-        __syncthreads();
-        if (qb + 64 < k1) fetch_b(qb + 64);
-        const int m = min(64, k1 - qb);
-        if (t < 6)
-#pragma unroll 4
-            for (int k = 0; k < m; k++) {
-                const double v = ba_schur_b(s_U[buf][k], s_H[buf][k], t);
-                sb -= s_ok[buf][k] ? v : 0.0;
-            }
-        buf ^= 1;
-    }
-    if (t < 6) d.bs[6 * a + t] = sb;
 }
+
 
 // S dp = -bs by Cholesky in the arithmetic of cv::solve(S, -bs, dp, DECOMP_CHOLESKY)
 // (Optimizer.cpp:516; OpenCV's hal Cholesky): each L entry is (S_ij - sum_{k<j} L_ik L_jk) * R_j
@@ -325,9 +389,9 @@ __global__ __launch_bounds__(64) void k_ba_schur(BaDev d) {
 // code, no edge guards).  One workgroup, right-looking over 32-column panels — every element still
 // takes its terms in ascending k, so the factor and the solution are bit-identical to the oracle's
 // row-oriented statement (oracle/orc_ba.cpp chol_solve):
-//   1. wave 0 factors the panel's 32 x 32 diagonal block in registers (lane = row): the pivot and
-//      the column entries it needs come by readlane, so the 32-step sqrt -> reciprocal -> update
-//      chain runs without a barrier, while waves 1.. load the panel rows below;
+//   1. wave 0 factors the panel's 32 x 32 diagonal block in registers (lane = row, readlane
+//      broadcasts): the 32-step sqrt -> reciprocal -> update chain runs without a workgroup
+//      barrier, and one panel ahead, beside the other waves' trailing update (look-ahead);
 //   2. every row below takes the diagonal block (a 32-step substitution per row, one thread per
 //      row, the block's L and R broadcast out of LDS);
 //   3. the trailing lower triangle takes the panel's 32 columns in 4 x 4 register tiles, the
@@ -361,6 +425,13 @@ __device__ __forceinline__ double readlane_f64(double v, int l) {
     return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
 }
 
+// orders a wave's LDS accesses for the compiler (LDS itself is in order within a wave)
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 // the padded rows n..np-1 of S: identity (their columns >= n above the diagonal are never read)
 __global__ void k_ba_pad(BaDev d) {
     const int n = 6 * d.N, np = d.np;
@@ -377,64 +448,158 @@ __global__ __launch_bounds__(512) void k_ba_chol(BaDev d) {
     __shared__ __attribute__((aligned(16))) double PnT[kCholNB * kCholLd];  // the panel, k-major: PnT[k * kCholLd + row]
     __shared__ double Rd[kCholMaxN];                                         // reciprocal diagonal R
     __shared__ double xs[kCholMaxN];                                         // right-hand side / solution
+    __shared__ double Dg[kCholNB * 33];                                      // wave 0's diagonal block
     __shared__ int bad;
     if (tid == 0) bad = 0;
     for (int i = tid; i < np; i += nt) xs[i] = i < n ? -d.bs[i] : 0.0;
     __syncthreads();
     BA_T0();
-    for (int K0 = 0; K0 < np; K0 += kCholNB) {
-        const int below = np - K0 - kCholNB, rb = tid - 64;
-        double a[kCholNB];
+    // wave 0: the diagonal block at K0 factored in registers, lane i < 32 holding row K0 + i (lanes
+    // 32.. duplicate row 31): the pivot and the column entries come by readlane (8 at a time: the
+    // scheduler would otherwise hoist a whole column's into SGPRs), then the rows go to Dg (the
+    // entries right of the diagonal are garbage, never read).  R into Rd; returns false if a pivot
+    // is below DBL_EPSILON.
+    auto diag_block = [&](int K0) {
+        double g[kCholNB];
+        const int lr = min(lane, kCholNB - 1);
+#pragma unroll
+        for (int c = 0; c < kCholNB; c++) g[c] = S[(size_t)(K0 + lr) * np + K0 + c];
+        bool fail = false;
+#pragma unroll
+        for (int c = 0; c < kCholNB; c++) {
+            const double s = readlane_f64(g[c], c);
+            fail |= s < DBL_EPSILON;
+            const double r = 1.0 / sqrt(s);
+            if (lane == 0) Rd[K0 + c] = r;
+            const double l = g[c] * r;
+            g[c] = l;
+#pragma unroll
+            for (int j = c + 1; j < kCholNB; j++) {
+                g[j] -= l * readlane_f64(l, j);
+                if ((j - c) % 8 == 0) __builtin_amdgcn_sched_barrier(0);
+            }
+        }
+        if (lane < kCholNB)
+#pragma unroll
+            for (int c = 0; c < kCholNB; c++) Dg[lane * 33 + c] = g[c];
+        return !fail;
+    };
+    // 4 x 4 tiles of the lower triangle: rows r0.., columns c0.. take the panel's 32 columns (PnT)
+    auto tile_update = [&](int r0, int c0, bool diag) {
+        double acc[4][4];
+#pragma unroll
+        for (int x = 0; x < 4; x++)
+#pragma unroll
+            for (int y = 0; y < 4; y++) acc[x][y] = S[(size_t)(r0 + x) * np + c0 + y];
+#pragma unroll 8
+        for (int k = 0; k < kCholNB; k++) {
+            const double2* pr = reinterpret_cast<const double2*>(&PnT[k * kCholLd + r0]);
+            const double2* pc = reinterpret_cast<const double2*>(&PnT[k * kCholLd + c0]);
+            const double2 a01 = pr[0], a23 = pr[1], b01 = pc[0], b23 = pc[1];
+            const double av[4] = {a01.x, a01.y, a23.x, a23.y}, bv[4] = {b01.x, b01.y, b23.x, b23.y};
+#pragma unroll
+            for (int x = 0; x < 4; x++)
+#pragma unroll
+                for (int y = 0; y < 4; y++) acc[x][y] -= av[x] * bv[y];
+        }
+        // (a diagonal tile's entries above the diagonal belong to S's upper triangle: not stored)
+#pragma unroll
+        for (int x = 0; x < 4; x++)
+#pragma unroll
+            for (int y = 0; y < 4; y++)
+                if (!diag || y <= x) S[(size_t)(r0 + x) * np + c0 + y] = acc[x][y];
+    };
+    // forward substitution of the diagonal block at K0 (wave 0): y_i = (x_i - sum_{k<i} L_ik y_k) * R_i,
+    // ascending k, the block's L from PnT (published in [A]).  Lane i keeps x_i and takes -0 * y_k for
+    // k >= i (its row's upper part is zeroed), so the loop has no lane conditions; y_i = x_i R_i at
+    // the end is the y_k the other lanes used.
+    auto fwd_block = [&](int K0) {
+        int ln = lane;
+        asm volatile("" : "+v"(ln));  // per-block lane compares: not hoisted into live SGPR masks
+        const int lr = min(ln, kCholNB - 1);
+        double Lr[kCholNB];
+#pragma unroll
+        for (int c = 0; c < kCholNB; c++) {
+            const double v = PnT[c * kCholLd + K0 + lr];
+            Lr[c] = c < ln ? v : 0.0;
+        }
+        double x = xs[K0 + lr];
+#pragma unroll
+        for (int k = 0; k < kCholNB; k++) {
+            const double y = readlane_f64(x, k) * Rd[K0 + k];
+            x -= Lr[k] * y;
+        }
+        if (ln < kCholNB) xs[K0 + ln] = x * Rd[K0 + ln];
+    };
+    double a[kCholNB];
+    // round K1: [D] wave 0 factors the diagonal block at K1 while waves 1.. finish the previous
+    // panel's trailing update (rows / columns K1 + 32 ..); then panel K1: [A] publish the block,
+    // [B] the rows below, [C] the next panel's columns
+    for (int K1 = 0;; K1 += kCholNB) {
         if (tid < 64) {
-            // 1. the diagonal block: lane i < 32 holds row K0 + i (lanes 32.. duplicate row 31; the
-            // entries right of the diagonal are computed as garbage and never read)
-            const int lr = min(lane, kCholNB - 1);
+            if (!diag_block(K1) && lane == 0) bad = 1;
+        } else if (K1 > 0) {
+            // forward substitution, rows below the previous block: x_i -= sum_c L_i,c y_c (ascending c;
+            // the block's y from [C], the panel still in PnT)
+            const int Kp = K1 - kCholNB, i = K1 + (tid - 64);
+            if (i < np) {
+                double sx = xs[i];
 #pragma unroll
-            for (int c = 0; c < kCholNB; c++) a[c] = S[(size_t)(K0 + lr) * np + K0 + c];
-            bool fail = false;
-#pragma unroll
-            for (int c = 0; c < kCholNB; c++) {
-                const double s = readlane_f64(a[c], c);
-                fail |= s < DBL_EPSILON;
-                const double r = 1.0 / sqrt(s);
-                if (lane == 0) Rd[K0 + c] = r;
-                const double l = a[c] * r;
-                a[c] = l;
-                // the column's entries by readlane, 8 at a time (the scheduler would otherwise hoist
-                // all of them into SGPRs at once)
-#pragma unroll
-                for (int j = c + 1; j < kCholNB; j++) {
-                    a[j] -= l * readlane_f64(l, j);
-                    if ((j - c) % 8 == 0) __builtin_amdgcn_sched_barrier(0);
-                }
+                for (int c = 0; c < kCholNB; c++) sx -= PnT[c * kCholLd + i] * xs[Kp + c];
+                xs[i] = sx;
             }
-            // the whole row (neither PnT's nor S's upper triangle is read, and S is rebuilt by
-            // every iteration's k_ba_schur)
-            if (lane < kCholNB) {
-#pragma unroll
-                for (int c = 0; c < kCholNB; c++) {
-                    PnT[c * kCholLd + K0 + lane] = a[c];
-                    S[(size_t)(K0 + lane) * np + K0 + c] = a[c];
-                }
+            const int base = K1 + kCholNB, m2 = (np - base) / 4;
+            const int tiles = m2 * (m2 + 1) / 2;
+            for (int t = tid - 64; t < tiles; t += nt - 64) {
+                int ti = (int)((sqrt(8.0 * (double)t + 1.0) - 1.0) * 0.5);
+                while (ti * (ti + 1) / 2 > t) ti--;
+                while ((ti + 1) * (ti + 2) / 2 <= t) ti++;
+                const int tj = t - ti * (ti + 1) / 2;
+                tile_update(base + 4 * ti, base + 4 * tj, ti == tj);
             }
-            if (lane == 0 && fail) bad = 1;
+        }
+        __syncthreads();
+        BA_T(0);
+        if (bad) break;
+        const int K0 = K1, below = np - K0 - kCholNB, rb = tid - 64;
+        // [A] wave 0 publishes the factored diagonal block (PnT for the rows below, S for the
+        // substitutions); waves 1.. load the panel rows below it
+        if (tid < 64) {
+            // lane (i, h): row i, columns 16 h .. 16 h + 15 (the entries right of the diagonal are
+            // garbage: neither PnT's nor S's upper part is read, and S is rebuilt by every
+            // iteration's k_ba_schur)
+            const int i = lane & 31, h = lane >> 5;
+#pragma unroll
+            for (int q = 0; q < 16; q++) {
+                const int c = 16 * h + q;
+                const double v = Dg[i * 33 + c];
+                PnT[c * kCholLd + K0 + i] = v;
+                S[(size_t)(K0 + i) * np + K0 + c] = v;
+            }
         } else if (rb < below) {
 #pragma unroll
             for (int c = 0; c < kCholNB; c++) a[c] = S[(size_t)(K0 + kCholNB + rb) * np + K0 + c];
         }
         __syncthreads();
-        BA_T(0);
-        if (bad) break;
-        // 2. rows below: L_ic = (S_ic - sum_{k<c} L_ik L_ck) * R_c, column by column
+        if (below == 0) break;
+        // [B] rows below: L_ic = (S_ic - sum_{k<c} L_ik L_ck) * R_c, column by column
         if (tid >= 64 && rb < below) {
             const int i = K0 + kCholNB + rb;
+            // column c + 1 of the block is read from LDS while column c is applied (two columns of
+            // reads in flight, not the whole block's: the scheduler would hoist them all and spill)
+            double col[2][kCholNB];
+#pragma unroll
+            for (int j = 1; j < kCholNB; j++) col[0][j] = PnT[K0 + j];
 #pragma unroll
             for (int c = 0; c < kCholNB; c++) {
+                if (c + 1 < kCholNB)
+#pragma unroll
+                    for (int j = c + 2; j < kCholNB; j++) col[(c + 1) & 1][j] = PnT[(c + 1) * kCholLd + K0 + j];
                 const double l = a[c] * Rd[K0 + c];
                 a[c] = l;
 #pragma unroll
-                for (int j = c + 1; j < kCholNB; j++) a[j] -= l * PnT[c * kCholLd + K0 + j];
-                __builtin_amdgcn_sched_barrier(0);  // one column's LDS reads in flight at a time
+                for (int j = c + 1; j < kCholNB; j++) a[j] -= l * col[c & 1][j];
+                __builtin_amdgcn_sched_barrier(0);
             }
 #pragma unroll
             for (int c = 0; c < kCholNB; c++) {
@@ -444,39 +609,24 @@ __global__ __launch_bounds__(512) void k_ba_chol(BaDev d) {
         }
         __syncthreads();
         BA_T(1);
-        // 3. trailing lower triangle (rows / columns K0 + 32 ..), 4 x 4 tiles on or below the
-        // diagonal, tile t = ti (ti + 1) / 2 + tj so that neighbouring lanes share their rows
-        const int base = K0 + kCholNB, mt = below / 4;
-        const int tiles = mt * (mt + 1) / 2;
-        for (int t = tid; t < tiles; t += nt) {
-            int ti = (int)((sqrt(8.0 * (double)t + 1.0) - 1.0) * 0.5);
-            while (ti * (ti + 1) / 2 > t) ti--;
-            while ((ti + 1) * (ti + 2) / 2 <= t) ti++;
-            const int tj = t - ti * (ti + 1) / 2;
-            const int r0 = base + 4 * ti, c0 = base + 4 * tj;
-            const bool diag = ti == tj;
-            double acc[4][4];
-#pragma unroll
-            for (int x = 0; x < 4; x++)
-#pragma unroll
-                for (int y = 0; y < 4; y++) acc[x][y] = S[(size_t)(r0 + x) * np + c0 + y];
-#pragma unroll 8
-            for (int k = 0; k < kCholNB; k++) {
-                const double2* pr = reinterpret_cast<const double2*>(&PnT[k * kCholLd + r0]);
-                const double2* pc = reinterpret_cast<const double2*>(&PnT[k * kCholLd + c0]);
-                const double2 a01 = pr[0], a23 = pr[1], b01 = pc[0], b23 = pc[1];
-                const double av[4] = {a01.x, a01.y, a23.x, a23.y}, bv[4] = {b01.x, b01.y, b23.x, b23.y};
-#pragma unroll
-                for (int x = 0; x < 4; x++)
-#pragma unroll
-                    for (int y = 0; y < 4; y++) acc[x][y] -= av[x] * bv[y];
+        // [C] the next panel's columns (K0 + 32 .. K0 + 63, every row from K0 + 32) take this panel,
+        // so that the next diagonal block and rows below are complete
+        // (wave 0 meanwhile: the forward substitution of this block, fwd_block)
+        const int Kn = K0 + kCholNB, mt = below / 4;
+        const int tiles = 8 * mt - 28;  // the 8 x 8 lower-triangular head (36 tiles) + 8 per row block below
+        if (tid < 64) fwd_block(K0);
+        for (int t = tid - 64; tid >= 64 && t < tiles; t += nt - 64) {
+            int ti, tj;
+            if (t < 36) {
+                ti = (int)((sqrt(8.0 * (double)t + 1.0) - 1.0) * 0.5);
+                while (ti * (ti + 1) / 2 > t) ti--;
+                while ((ti + 1) * (ti + 2) / 2 <= t) ti++;
+                tj = t - ti * (ti + 1) / 2;
+            } else {
+                ti = 8 + (t - 36) / 8;
+                tj = (t - 36) % 8;
             }
-            // (a diagonal tile's entries above the diagonal belong to S's upper triangle: not stored)
-#pragma unroll
-            for (int x = 0; x < 4; x++)
-#pragma unroll
-                for (int y = 0; y < 4; y++)
-                    if (!diag || y <= x) S[(size_t)(r0 + x) * np + c0 + y] = acc[x][y];
+            tile_update(Kn + 4 * ti, Kn + 4 * tj, ti == tj);
         }
         __syncthreads();
         BA_T(2);
@@ -485,45 +635,9 @@ __global__ __launch_bounds__(512) void k_ba_chol(BaDev d) {
         if (tid == 0) d.ctl->solved = 0;
         return;
     }
-    // 4a. L y = -bs: y_i = (x_i - sum_{k<i} L_ik y_k) * R_i, ascending k.  In the diagonal block lane
-    // i keeps x_i and takes -0 * y_k for k >= i (its row's upper part is zeroed), so the loop has no
-    // lane conditions; y_i = x_i R_i at the end is the y_k the other lanes used.
-    for (int K0 = 0; K0 < np; K0 += kCholNB) {
-        int ln = lane;
-        asm volatile("" : "+v"(ln));  // per-block lane compares: not hoisted into live SGPR masks
-        double Lr[kCholNB];
-        if (tid < 64) {
-            const int lr = min(ln, kCholNB - 1);
-#pragma unroll
-            for (int c = 0; c < kCholNB; c++) {
-                const double v = S[(size_t)(K0 + lr) * np + K0 + c];
-                Lr[c] = c < ln ? v : 0.0;
-            }
-            double x = xs[K0 + lr];
-#pragma unroll
-            for (int k = 0; k < kCholNB; k++) {
-                const double y = readlane_f64(x, k) * Rd[K0 + k];
-                x -= Lr[k] * y;
-            }
-            if (ln < kCholNB) xs[K0 + ln] = x * Rd[K0 + ln];
-        } else {
-            // the rows below: their block entries loaded while wave 0 solves the block
-            const int i = min(K0 + kCholNB + (tid - 64), np - 1);
-#pragma unroll
-            for (int c = 0; c < kCholNB; c++) Lr[c] = S[(size_t)i * np + K0 + c];
-        }
-        __syncthreads();
-        if (tid >= 64) {
-            const int i = K0 + kCholNB + (tid - 64);
-            if (i < np) {
-                double s = xs[i];
-#pragma unroll
-                for (int k = 0; k < kCholNB; k++) s -= Lr[k] * xs[K0 + k];
-                xs[i] = s;
-            }
-        }
-        __syncthreads();
-    }
+    // the last block's forward substitution (the other blocks' ran inside the factorization)
+    if (tid < 64) fwd_block(np - kCholNB);
+    __syncthreads();
     BA_T(3);
     // 4b. L^T x = y: x_i = (y_i - sum_{k>i, descending} L_ki x_k) * R_i (the block's column entries
     // above the diagonal zeroed the same way)
@@ -585,56 +699,24 @@ __global__ void k_ba_update(BaDev d) {
             d.rv_new[3 * i + k] = d.rv[3 * i + k] + d.dp[6 * i + k];
             d.tv_new[3 * i + k] = d.tv[3 * i + k] + d.dp[6 * i + 3 + k];
         }
+        pose_cache(d.rv_new + 3 * i, d.tv_new + 3 * i, d.pc_new[i]);  // for the new cost
     }
 }
 
-// mode 0: total_cost; 1: new cost + accept/reject; 2: err_before; 3: err_after
-__global__ void k_ba_control(BaDev d, int mode) {
-    BaCtl& c = *d.ctl;
-    if (mode <= 1 && c.done) return;
-    double s = 0;
-    for (int k = 0; k < d.n_chunks; k++) s += d.chunk[k];
-    if (mode == 0) {
-        c.total_cost = s;
-        return;
-    }
-    if (mode == 2) {
-        c.err_before = sqrt(s / d.n_obs);
-        return;
-    }
-    if (mode == 3) {
-        c.err_after = sqrt(s / d.n_obs);
-        return;
-    }
-    c.take = 0;
-    if (!c.solved) {  // the oracle: lambda * 10 and the next iteration
-        c.lambda *= 10;
-    } else {
-        c.new_cost = s;
-        if (s < c.total_cost) {
-            c.take = 1;
-            c.lambda = c.lambda * 0.5 > 1e-7 ? c.lambda * 0.5 : 1e-7;
-            c.accepted++;
-            const double rel = (c.total_cost - s) / (c.total_cost + 1e-10);
-            if (rel < 1e-4) c.done = 1;
-        } else {
-            c.lambda *= 5.0;
-            if (c.lambda > 1e6) c.done = 1;
-        }
-    }
-    c.iter++;
-    if (c.iter >= c.max_iter) c.done = 1;
-}
-
+// an accepted step: the new parameters become current, and so does the pose cache (pc always
+// belongs to rv / tv, so no pose-cache launch starts an iteration)
 __global__ void k_ba_commit(BaDev d) {
     if (!d.ctl->take) return;
     const int g = blockIdx.x * blockDim.x + threadIdx.x;
-    if (g < 3 * d.M)
+    if (g < 3 * d.M) {
         d.P[g] = d.P_new[g];
-    else if (g < 3 * d.M + 3 * d.N) {
-        const int k = g - 3 * d.M;
-        d.rv[k] = d.rv_new[k];
-        d.tv[k] = d.tv_new[k];
+    } else if (g < 3 * d.M + d.N) {
+        const int i = g - 3 * d.M;
+        for (int k = 0; k < 3; k++) {
+            d.rv[3 * i + k] = d.rv_new[3 * i + k];
+            d.tv[3 * i + k] = d.tv_new[3 * i + k];
+        }
+        pose_cache(d.rv + 3 * i, d.tv + 3 * i, d.pc[i]);
     }
 }
 
@@ -664,22 +746,7 @@ int local_ba(vs_ctx* ctx, int N, double* R, double* t, int M, double* P, int n_o
     using hclock = std::chrono::steady_clock;
     const hclock::time_point h0 = hclock::now();
     hclock::time_point h1 = h0, h2 = h0, h3 = h0;
-    // ---- structure (host, once) ----
-    std::vector<std::vector<int>> observers(M);
-    std::vector<int> oslot(n_obs);
-    for (int o = 0; o < n_obs; o++) {
-        auto& ob = observers[opt[o]];
-        int s = 0;
-        while (s < (int)ob.size() && ob[s] != okf[o]) s++;
-        if (s == (int)ob.size()) ob.push_back(okf[o]);
-        oslot[o] = s;
-    }
-    std::vector<int> pv_off(M + 1, 0), pv_kf;
-    for (int j = 0; j < M; j++) {
-        pv_off[j + 1] = pv_off[j] + (int)observers[j].size();
-        pv_kf.insert(pv_kf.end(), observers[j].begin(), observers[j].end());
-    }
-    const int n_pairs = pv_off[M];
+    // ---- structure (host, once; flat arrays) ----
     auto csr = [&](const int* key, int nk, std::vector<int>& off, std::vector<int>& lst) {
         off.assign(nk + 1, 0);
         for (int o = 0; o < n_obs; o++) off[key[o] + 1]++;
@@ -691,14 +758,31 @@ int local_ba(vs_ctx* ctx, int N, double* R, double* t, int M, double* P, int n_o
     std::vector<int> kf_off, kf_obs, pt_off, pt_obs;
     csr(okf, N, kf_off, kf_obs);
     csr(opt, M, pt_off, pt_obs);
+    // the observers of every point: its distinct keyframes in order of first appearance among its
+    // observations (point_observers, :257-263), and every observation's slot among them
+    std::vector<int> oslot(n_obs), pv_off(M + 1), pv_kf(n_obs);
+    int n_pairs = 0;
+    for (int j = 0; j < M; j++) {
+        const int b0 = n_pairs;
+        pv_off[j] = b0;
+        for (int q = pt_off[j]; q < pt_off[j + 1]; q++) {
+            const int o = pt_obs[q], k = okf[o];
+            int sl = 0;
+            while (b0 + sl < n_pairs && pv_kf[b0 + sl] != k) sl++;
+            if (b0 + sl == n_pairs) pv_kf[n_pairs++] = k;
+            oslot[o] = sl;
+        }
+    }
+    pv_off[M] = n_pairs;
     // common points per (a, b), ascending j, with the U (j, a) and Hpm (j, b) pair indices; and the
     // points of every keyframe, ascending, with U (j, a)
     std::vector<int> ab_cnt(N * N, 0), kb_cnt(N, 0);
     for (int j = 0; j < M; j++) {
-        const int no = (int)observers[j].size();
+        const int* ob = pv_kf.data() + pv_off[j];
+        const int no = pv_off[j + 1] - pv_off[j];
         for (int x = 0; x < no; x++) {
-            kb_cnt[observers[j][x]]++;
-            for (int y = 0; y < no; y++) ab_cnt[observers[j][x] * N + observers[j][y]]++;
+            kb_cnt[ob[x]]++;
+            for (int y = 0; y < no; y++) ab_cnt[ob[x] * N + ob[y]]++;
         }
     }
     std::vector<int> ab_off(N * N + 1, 0), kb_off(N + 1, 0);
@@ -709,13 +793,14 @@ int local_ba(vs_ctx* ctx, int N, double* R, double* t, int M, double* P, int n_o
     {
         std::vector<int> fa(ab_off.begin(), ab_off.end() - 1), fk(kb_off.begin(), kb_off.end() - 1);
         for (int j = 0; j < M; j++) {
-            const int no = (int)observers[j].size();
+            const int* ob = pv_kf.data() + pv_off[j];
+            const int no = pv_off[j + 1] - pv_off[j];
             for (int x = 0; x < no; x++) {
-                const int a = observers[j][x];
+                const int a = ob[x];
                 kb_u[fk[a]] = pv_off[j] + x;
                 kb_j[fk[a]++] = j;
                 for (int y = 0; y < no; y++) {
-                    const int p = a * N + observers[j][y];
+                    const int p = a * N + ob[y];
                     ab_u[fa[p]] = pv_off[j] + x;
                     ab_h[fa[p]] = pv_off[j] + y;
                     ab_j[fa[p]++] = j;
@@ -749,6 +834,13 @@ int local_ba(vs_ctx* ctx, int N, double* R, double* t, int M, double* P, int n_o
     h1 = hclock::now();
     VS_CHECK(ctx->ba.ensure(bytes));
     char* base = ctx->ba.as<char>();
+    if (!ctx->ba_done_h) {
+        VS_HIP(hipHostMalloc((void**)&ctx->ba_done_h, 64, hipHostMallocMapped));
+        VS_HIP(hipHostGetDevicePointer((void**)&ctx->ba_done_d, ctx->ba_done_h, 0));
+        for (hipEvent_t& e : ctx->ba_ev) VS_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    }
+    volatile int* done_h = ctx->ba_done_h;
+    *done_h = 0;
     hipStream_t s = ctx->stream;
     auto up = [&](size_t off, const void* src, size_t n_bytes) {
         return hipMemcpyAsync(base + off, src, n_bytes, hipMemcpyHostToDevice, s);
@@ -833,6 +925,7 @@ int local_ba(vs_ctx* ctx, int N, double* R, double* t, int M, double* P, int n_o
     d.chunk = BA_PTR(double, o_chunk);
     d.pvalid = BA_PTR(int, o_pvalid);
     d.ctl = BA_PTR(BaCtl, o_ctl);
+    d.done_host = ctx->ba_done_d;
 #undef BA_PTR
     {
         ProfScope ps(ctx, "local_ba", s);
@@ -840,26 +933,27 @@ int local_ba(vs_ctx* ctx, int N, double* R, double* t, int M, double* P, int n_o
         hipLaunchKernelGGL(k_ba_init, dim3(cdiv(N, T)), dim3(T), 0, s, d, (const double*)(base + o_R));
         if (np > n) hipLaunchKernelGGL(k_ba_pad, dim3(cdiv((long)(np - n) * np, T)), dim3(T), 0, s, d);
         hipLaunchKernelGGL(k_ba_pose_cache, dim3(cdiv(N, T)), dim3(T), 0, s, d, 0, 0);
-        hipLaunchKernelGGL(k_ba_chunk_sums, dim3(n_chunks), dim3(kCostChunk), 0, s, d, 2, 0);
-        hipLaunchKernelGGL(k_ba_control, dim3(1), dim3(1), 0, s, d, 2);
+        hipLaunchKernelGGL(k_ba_cost, dim3(n_chunks), dim3(kCostChunk), 0, s, d, 2, 0, 2);
+        // Iteration it is enqueued once iteration it - 2 has finished and had not converged (the
+        // flag ba_control mirrors to the host): the device always has the next iteration queued,
+        // and at most one iteration past convergence is enqueued, where every launch returns at once.
         for (int it = 0; it < max_iter; it++) {
-            hipLaunchKernelGGL(k_ba_pose_cache, dim3(cdiv(N, T)), dim3(T), 0, s, d, 0, 1);
+            if (it >= 2) {
+                VS_HIP(hipEventSynchronize(ctx->ba_ev[it & 1]));
+                if (*done_h) break;
+            }
             hipLaunchKernelGGL(k_ba_obs, dim3(cdiv(n_obs, T)), dim3(T), 0, s, d);
-            hipLaunchKernelGGL(k_ba_chunk_sums, dim3(n_chunks), dim3(kCostChunk), 0, s, d, 0, 1);
-            hipLaunchKernelGGL(k_ba_control, dim3(1), dim3(1), 0, s, d, 0);
+            hipLaunchKernelGGL(k_ba_cost, dim3(n_chunks), dim3(kCostChunk), 0, s, d, 0, 1, 0);
             hipLaunchKernelGGL(k_ba_kf_acc, dim3(N), dim3(64), 0, s, d);
             hipLaunchKernelGGL(k_ba_pt_acc, dim3(cdiv(M, T)), dim3(T), 0, s, d);
-            hipLaunchKernelGGL(k_ba_schur, dim3(N * N), dim3(64), 0, s, d);
+            hipLaunchKernelGGL(k_ba_schur, dim3(N * N + N), dim3(64), 0, s, d);
             hipLaunchKernelGGL(k_ba_chol, dim3(1), dim3(512), 0, s, d);
             hipLaunchKernelGGL(k_ba_update, dim3(cdiv(M + N, T)), dim3(T), 0, s, d);
-            hipLaunchKernelGGL(k_ba_pose_cache, dim3(cdiv(N, T)), dim3(T), 0, s, d, 1, 1);
-            hipLaunchKernelGGL(k_ba_chunk_sums, dim3(n_chunks), dim3(kCostChunk), 0, s, d, 1, 1);
-            hipLaunchKernelGGL(k_ba_control, dim3(1), dim3(1), 0, s, d, 1);
-            hipLaunchKernelGGL(k_ba_commit, dim3(cdiv(3 * M + 3 * N, T)), dim3(T), 0, s, d);
+            hipLaunchKernelGGL(k_ba_cost, dim3(n_chunks), dim3(kCostChunk), 0, s, d, 1, 1, 1);
+            hipLaunchKernelGGL(k_ba_commit, dim3(cdiv(3 * M + N, T)), dim3(T), 0, s, d);
+            VS_HIP(hipEventRecord(ctx->ba_ev[it & 1], s));
         }
-        hipLaunchKernelGGL(k_ba_pose_cache, dim3(cdiv(N, T)), dim3(T), 0, s, d, 0, 0);
-        hipLaunchKernelGGL(k_ba_chunk_sums, dim3(n_chunks), dim3(kCostChunk), 0, s, d, 2, 0);
-        hipLaunchKernelGGL(k_ba_control, dim3(1), dim3(1), 0, s, d, 3);
+        hipLaunchKernelGGL(k_ba_cost, dim3(n_chunks), dim3(kCostChunk), 0, s, d, 2, 0, 3);
         hipLaunchKernelGGL(k_ba_finish, dim3(cdiv(3 * M + N, T)), dim3(T), 0, s, d, (double*)(base + o_R),
                            (double*)(base + o_t), (double*)(base + o_Pn));
         VS_HIP(hipGetLastError());

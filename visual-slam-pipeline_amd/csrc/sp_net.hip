@@ -646,6 +646,10 @@ __global__ __launch_bounds__(256, CKT == 4 ? (MB == 1 ? 4 : 3) : 2) void k_conv3
 #ifndef VS_WINO_PRIO
 #define VS_WINO_PRIO 0   // 1: s_setprio(1) over each MFMA row region (A/B)
 #endif
+#ifndef VS_WINO_ABL
+#define VS_WINO_ABL 0    // latency ablation (results are wrong): 1 no weight staging after the prologue,
+                         // 2 no input transform, 3 no patch staging / conv1a, 4 no chunk barrier
+#endif
 template <bool POOL, bool FUSE1A, bool C32 = false, bool SPLIT = false>
 __global__ __launch_bounds__(256, 2) void k_wino3(WinoArgs wa) {
     static_assert(!(C32 && (POOL || FUSE1A)), "C32 is the plain (MiDaS) variant");
@@ -903,9 +907,11 @@ __global__ __launch_bounds__(256, 2) void k_wino3(WinoArgs wa) {
         __builtin_amdgcn_sched_barrier(0);
         if (VS_WINO_PRIO) __builtin_amdgcn_s_setprio(1);
         mfma_row(0, 0);
-        put_u(SN{}, g_c, k + 1);
-        fetch_u(g_c, k + 2);
-        fetch_x(SN{}, g_c, k + 3);
+        if (VS_WINO_ABL != 1) {
+            put_u(SN{}, g_c, k + 1);
+            fetch_u(g_c, k + 2);
+        }
+        if (VS_WINO_ABL != 3) fetch_x(SN{}, g_c, k + 3);
 #pragma unroll
         for (int i = 0; i < 8; i++) {
             __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
@@ -916,7 +922,7 @@ __global__ __launch_bounds__(256, 2) void k_wino3(WinoArgs wa) {
         __builtin_amdgcn_sched_barrier(0);
         read_row(P, 2, 0);
         mfma_row(1, 1);
-        put_x(SP{}, g_c, k + 2);
+        if (VS_WINO_ABL != 3) put_x(SP{}, g_c, k + 2);
 #pragma unroll
         for (int i = 0; i < 8; i++) {
             __builtin_amdgcn_sched_group_barrier(0x008, 1, 1);
@@ -927,7 +933,7 @@ __global__ __launch_bounds__(256, 2) void k_wino3(WinoArgs wa) {
         __builtin_amdgcn_sched_barrier(0);
         read_row(P, 3, 1);
         mfma_row(2, 0);
-        transform(SN{}, g_c, k + 1);
+        if (VS_WINO_ABL != 2) transform(SN{}, g_c, k + 1);
 #pragma unroll
         for (int i = 0; i < 8; i++) {
             __builtin_amdgcn_sched_group_barrier(0x008, 1, 2);
@@ -994,7 +1000,7 @@ __global__ __launch_bounds__(256, 2) void k_wino3(WinoArgs wa) {
         transform(SN{}, g_c, k + 1);
         mfma_row(3, 1);
 #endif
-        __syncthreads();  // chunk k + 1's V / U and chunk k + 2's patch complete; chunk k's buffers free
+        if (VS_WINO_ABL != 4) __syncthreads();  // chunk k + 1's V / U and chunk k + 2's patch complete; chunk k's buffers free
     };
     // steady state: a chunk pair (k, k + 1) touches chunks up to k + 4, so it runs unguarded while
     // k + 4 < nchunk; the tail pairs keep the guards

@@ -400,6 +400,9 @@ void vs_destroy(vs_ctx* ctx) {
     if (ctx->head_a.b) (void)hipFree(ctx->head_a.b);
     if (ctx->head_a.wu) (void)hipFree(ctx->head_a.wu);
     if (ctx->scratch_foreign) (void)hipEventDestroy(ctx->scratch_foreign);
+    for (hipEvent_t e : ctx->ba_ev)
+        if (e) (void)hipEventDestroy(e);
+    if (ctx->ba_done_h) (void)hipHostFree(ctx->ba_done_h);
     DevBuf* bufs[] = {&ctx->gray,  &ctx->act0,   &ctx->act1,   &ctx->semi,   &ctx->dgrid,  &ctx->heat,
                       &ctx->state, &ctx->flags,  &ctx->keys,   &ctx->keycnt, &ctx->h_img,  &ctx->h_kps,
                       &ctx->h_desc, &ctx->h_n,   &ctx->h_aux0, &ctx->h_aux1, &ctx->h_aux2, &ctx->h_aux3,

@@ -133,6 +133,11 @@ struct vs_ctx {
     // and the vs_slam's next extraction waits for it before it writes the scratch.
     hipEvent_t scratch_foreign = nullptr;
     bool scratch_foreign_pending = false;
+    // local BA: the LM "done" flag mirrored into mapped pinned host memory by k_ba_control, and two
+    // events, so that the host stops enqueueing iterations once the device has converged (ba.hip)
+    int* ba_done_h = nullptr;
+    int* ba_done_d = nullptr;
+    hipEvent_t ba_ev[2] = {nullptr, nullptr};
 };
 
 namespace vs {
