@@ -18,6 +18,8 @@
 // with -ffp-contract=off like the oracle).
 #include <hip/hip_runtime.h>
 
+#include <climits>
+
 #include "block_reduce.h"
 #include "pnp_solvers.h"
 #include "vs_internal.h"
@@ -624,21 +626,52 @@ __global__ __launch_bounds__(256) void k_pnp_ransac(const float* __restrict__ ob
             s_lden[it] = c >= 0 ? ransac_log_denom((double)(n - c) / n, model_points) : 0.0;
         }
         __syncthreads();
-        if (tid == 0) {
-            int niters = niters0, best = 0, best_iter = -1, it = 0;
+        // The sequential loop `for (it = 0; it < niters; it++) if (count > max(best, mp - 1)) { best,
+        // niters = update(niters) }` on wave 0: a hypothesis is accepted iff its count exceeds every
+        // earlier count and the floor mp - 1 (the running best is the prefix maximum), so the accepted
+        // positions of 64 hypotheses at a time come from one wave scan; only they are walked in order,
+        // each applying the same budget update to the running niters and stopping at the first
+        // position >= niters.  The loop's exit value is max(final niters, last accepted + 1).
+        if (tid < 64) {
             const double log_num = ransac_log_num(conf);
-            for (; it < niters; it++) {
-                const int c = s_cnt[it];
-                if (c < 0) continue;
-                if (c > (best > model_points - 1 ? best : model_points - 1)) {
-                    best = c;
-                    best_iter = it;
-                    niters = ransac_update_from_denom(log_num, s_lden[it], niters);
+            int niters = niters0, best = 0, best_iter = -1, floor_max = model_points - 1;
+            bool stop = false;
+            for (int base = 0; base < niters && !stop; base += 64) {
+                const int i = base + tid;
+                const int c = i < niters0 ? s_cnt[i] : -1;
+                int m = c;  // inclusive prefix maximum over the chunk
+#pragma unroll
+                for (int o = 1; o < 64; o <<= 1) {
+                    const int t = __shfl_up(m, o);
+                    if (tid >= o) m = m > t ? m : t;
                 }
+                int ex = __shfl_up(m, 1);
+                if (tid == 0) ex = INT_MIN;
+                const int prev = ex > floor_max ? ex : floor_max;
+                unsigned long long acc = __ballot(c > prev);
+                while (acc) {
+                    const int l = __ffsll((long long)acc) - 1;
+                    acc &= acc - 1;
+                    const int j = base + l;
+                    if (j >= niters) {
+                        stop = true;
+                        break;
+                    }
+                    best = __shfl(c, l);
+                    best_iter = j;
+                    niters = ransac_update_from_denom(log_num, s_lden[j], niters);
+                }
+                const int cm = __shfl(m, 63);
+                floor_max = cm > floor_max ? cm : floor_max;
             }
-            S.best = best;
-            S.best_iter = best_iter;
-            S.niters_run = it;
+            if (tid == 0) {
+                S.best = best;
+                S.best_iter = best_iter;
+                S.niters_run = niters > best_iter + 1 ? niters : best_iter + 1;
+            }
+        }
+        if (tid == 0) {
+            const int best = S.best, best_iter = S.best_iter;
             if (best > 0) {
                 const double* mo = H.model + ((size_t)pb * H.stride + best_iter) * 6;
                 for (int k = 0; k < 3; k++) {
