@@ -30,9 +30,10 @@
 //     best0 — the exact top-2 of the union, independent of arrival order;
 //   * the last workgroup of a pair to arrive (a device-scope counter; every atomic of the earlier
 //     workgroups has returned before their arrival) reads and resets the keys with atomicExch,
-//     applies the ratio test and compacts the good rows in query order: up to 4 x NTH queries per
-//     pass with all their exchanges in flight, per-wave ballots and one barrier.  Keys and
-//     counters are left reset for the next launch.
+//     applies the ratio test and compacts the good rows in query order: NTH queries per pass,
+//     per-wave ballots and one barrier per pass (several chunks per pass raised the whole kernel's
+//     VGPR count and cost the 64 x 64 main loop an occupancy step).  Keys and counters are left
+//     reset for the next launch.
 #include <hip/hip_runtime.h>
 
 #include <climits>
@@ -56,7 +57,7 @@ __device__ __forceinline__ void static_for(F&& f) {
 }
 
 constexpr unsigned long long kNoKey = ~0ull;
-constexpr int kTailChunks = 4;  // last arrival: query chunks of NTH per pass
+constexpr int kTailChunks = 1;  // last arrival: query chunks of NTH per pass (more raise the kernel's VGPR count)
 
 // Sequential fmaf-chain squared norm of every descriptor row of F frames.
 __global__ __launch_bounds__(256) void k_desc_norms(const float* __restrict__ desc, const int* __restrict__ n,
@@ -391,8 +392,8 @@ __global__ __launch_bounds__(64 * NWQ * NWT) void k_match(MatchArgs a) {
     if (!s_last) return;
 
     // ---- last arrival: ratio test + order-preserving compaction (Slam.cpp:1151-1157) ----
-    // up to kTailChunks x NTH queries per pass: every key exchange of the pass in flight together,
-    // per-wave ballots, one barrier, then each thread's slot from the per-(chunk, wave) counts
+    // kTailChunks x NTH queries per pass: the pass's key exchanges in flight together, per-wave
+    // ballots, one barrier, then each thread's slot from the per-(chunk, wave) counts
     if (tid == 0) atomicExch(a.cnt + p, 0u);
     vs_match* raw = a.raw + (size_t)p * a.ostride;
     vs_match* good = a.good + (size_t)p * a.ostride;
