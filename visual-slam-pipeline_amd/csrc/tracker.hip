@@ -93,6 +93,43 @@ __global__ __launch_bounds__(256) void k_gather_rows(const float* __restrict__ s
         reinterpret_cast<const float4*>(src + (size_t)rows[r] * 256)[lane];
 }
 
+// Slam's map-point insertion mirrored in HBM (map_append): for the k new points, the position (3
+// doubles from the staging upload), the descriptor row of the source frame and the valid flag, one
+// 64-lane wave per point
+__global__ __launch_bounds__(256) void k_map_append(const double* __restrict__ pos_in, const int* __restrict__ rows,
+                                                    int k, const float* __restrict__ desc_src, double* __restrict__ pos,
+                                                    float* __restrict__ desc, uint8_t* __restrict__ valid) {
+    const int r = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (r >= k) return;
+    reinterpret_cast<float4*>(desc + (size_t)r * 256)[lane] =
+        reinterpret_cast<const float4*>(desc_src + (size_t)rows[r] * 256)[lane];
+    if (lane < 3) pos[3 * (size_t)r + lane] = pos_in[3 * (size_t)r + lane];
+    if (lane == 3) valid[r] = 1;
+}
+
+// A list of device-to-device copies in one launch (the settle step's keyframe archiving and slot
+// moves: tens of small hipMemcpyAsync per batch, each a blit kernel and a host round of its own).
+// blockIdx.y = job; 16-byte words when source, destination and size allow, else 4-byte words (every
+// size here is a multiple of 4).
+struct CopyJob {
+    const void* src;
+    void* dst;
+    unsigned long long bytes;
+};
+__global__ __launch_bounds__(256) void k_copy_jobs(const CopyJob* __restrict__ jobs) {
+    const CopyJob J = jobs[blockIdx.y];
+    const size_t t0 = (size_t)blockIdx.x * 256 + threadIdx.x, stride = (size_t)gridDim.x * 256;
+    if ((((uintptr_t)J.src | (uintptr_t)J.dst | (uintptr_t)J.bytes) & 15) == 0) {
+        const uint4* a = reinterpret_cast<const uint4*>(J.src);
+        uint4* b = reinterpret_cast<uint4*>(J.dst);
+        for (size_t i = t0; i < J.bytes / 16; i += stride) b[i] = a[i];
+    } else {
+        const unsigned* a = reinterpret_cast<const unsigned*>(J.src);
+        unsigned* b = reinterpret_cast<unsigned*>(J.dst);
+        for (size_t i = t0; i < J.bytes / 4; i += stride) b[i] = a[i];
+    }
+}
+
 // Visibility sweep (Slam.cpp:1089-1108): for every valid map point, Optimizer::project_point
 // (Optimizer.cpp:26-48) with the camera->world pose; bit 0 = inside the image (increase_visible),
 // bit 1 = some keypoint within TRACK_VISIBILITY_RADIUS (increase_found).  Every workgroup first
@@ -458,6 +495,8 @@ struct GpuOps {
     // [arch_cap][kCap] keypoints, [arch_cap][kCap][256] descriptors, [arch_cap] counts.
     DevBuf arch_kps, arch_desc, arch_n;
     int arch_cap = 0, arch_used = 0;
+    std::vector<CopyJob> cjobs;  // pending copies, one k_copy_jobs launch per flush_copies()
+    DevBuf cjob_buf;
     DevBuf lc_buf;  // loop-closure candidate pool and outputs
     DevBuf dlt_buf;  // [kCap] DLT solutions of a keyframe match (match_dlt)
     int err = VS_OK;                     // first error inside an Ops call (the tracker has no error channel)
@@ -707,12 +746,26 @@ struct GpuOps {
         if (f->slot >= 2 * B) owner[f->slot - 2 * B] = nullptr;
         f->slot = -1;
     }
+    // queued: the caller flushes (flush_copies) before anything reads slot `to`
     int copy_slot(int from, int to) {
-        VS_HIP(hipMemcpyAsync(kps_of(to), kps_of(from), kCap * sizeof(vs_keypoint), hipMemcpyDeviceToDevice, s));
-        VS_HIP(hipMemcpyAsync(desc_of(to), desc_of(from), (size_t)kCap * 256 * sizeof(float), hipMemcpyDeviceToDevice, s));
-        VS_HIP(hipMemcpyAsync(pool_n.as<int>() + to, pool_n.as<int>() + from, sizeof(int), hipMemcpyDeviceToDevice, s));
-        VS_HIP(hipMemcpyAsync(depth_of(to), depth_of(from), (size_t)h * w * sizeof(float), hipMemcpyDeviceToDevice, s));
-        VS_HIP(hipMemcpyAsync(norms_of(to), norms_of(from), kCap * sizeof(float), hipMemcpyDeviceToDevice, s));
+        cjobs.push_back({kps_of(from), kps_of(to), kCap * sizeof(vs_keypoint)});
+        cjobs.push_back({desc_of(from), desc_of(to), (size_t)kCap * 256 * sizeof(float)});
+        cjobs.push_back({pool_n.as<int>() + from, pool_n.as<int>() + to, sizeof(int)});
+        cjobs.push_back({depth_of(from), depth_of(to), (size_t)h * w * sizeof(float)});
+        cjobs.push_back({norms_of(from), norms_of(to), kCap * sizeof(float)});
+        return VS_OK;
+    }
+    int flush_copies() {
+        if (cjobs.empty()) return VS_OK;
+        const int nj = (int)cjobs.size();
+        size_t mx = 0;
+        for (const CopyJob& j : cjobs) mx = std::max(mx, (size_t)j.bytes);
+        VS_CHECK(cjob_buf.ensure((size_t)nj * sizeof(CopyJob)));
+        VS_CHECK(upload(cjob_buf.p, cjobs.data(), (size_t)nj * sizeof(CopyJob)));
+        const unsigned bx = (unsigned)std::min<size_t>(64, std::max<size_t>(1, (mx / 16 + 255) / 256));
+        hipLaunchKernelGGL(k_copy_jobs, dim3(bx, nj), dim3(256), 0, s, cjob_buf.as<CopyJob>());
+        cjobs.clear();
+        VS_HIP(hipGetLastError());
         return VS_OK;
     }
     // Host features (SPCF cache / caller-extracted) into a persistent slot.
@@ -1236,6 +1289,7 @@ struct GpuOps {
 
     int grow_archive(int need) {
         if (need <= arch_cap) return VS_OK;
+        VS_CHECK(flush_copies());  // pending archive copies target the old buffers
         const int cap = std::max(need, std::max(16, 2 * arch_cap));
         DevBuf nk, nd, nn;
         VS_CHECK(nk.ensure((size_t)cap * kCap * sizeof(vs_keypoint)));
@@ -1276,16 +1330,15 @@ struct GpuOps {
             total = kb + db + nb + pb + 2 * mb + 3 * cb + rb + gb + sb;
         }
     };
-    // A keyframe's features into the archive (at settle, while its pool slot is still intact)
+    // A keyframe's features into the archive (at settle, while its pool slot is still intact; queued,
+    // flushed by the caller)
     int archive(vs_trk::Frame* f) {
         if (f->kf_slot >= 0 || f->slot < 0) return VS_OK;
         VS_CHECK(grow_archive(arch_used + 1));
         const int a = arch_used++;
-        VS_HIP(hipMemcpyAsync(arch_kps.as<vs_keypoint>() + (size_t)a * kCap, kps_of(f->slot), kCap * sizeof(vs_keypoint),
-                              hipMemcpyDeviceToDevice, s));
-        VS_HIP(hipMemcpyAsync(arch_desc.as<float>() + (size_t)a * kCap * 256, desc_of(f->slot),
-                              (size_t)kCap * 256 * sizeof(float), hipMemcpyDeviceToDevice, s));
-        VS_HIP(hipMemcpyAsync(arch_n.as<int>() + a, pool_n.as<int>() + f->slot, sizeof(int), hipMemcpyDeviceToDevice, s));
+        cjobs.push_back({kps_of(f->slot), arch_kps.as<vs_keypoint>() + (size_t)a * kCap, kCap * sizeof(vs_keypoint)});
+        cjobs.push_back({desc_of(f->slot), arch_desc.as<float>() + (size_t)a * kCap * 256, (size_t)kCap * 256 * sizeof(float)});
+        cjobs.push_back({pool_n.as<int>() + f->slot, arch_n.as<int>() + a, sizeof(int)});
         f->kf_slot = a;
         return VS_OK;
     }
@@ -1438,16 +1491,26 @@ struct GpuOps {
         HostTimer ht(hprof, kHAppend);
         const int k = (int)rows.size();
         if (failed(grow_map(first + k))) return;
-        if (failed(upload(map_pos.as<double>() + (size_t)3 * first, m.pos.data() + (size_t)3 * first,
-                          (size_t)3 * k * sizeof(double))))
+        if (k == 0) {
+            map_n = first;
             return;
-        if (failed(rows_buf.ensure((size_t)k * sizeof(int)))) return;
-        int* d_rows = rows_buf.as<int>();
-        if (failed(upload(d_rows, rows.data(), (size_t)k * sizeof(int)))) return;
-        hipLaunchKernelGGL(k_gather_rows, dim3((k + 3) / 4), dim3(256), 0, s, desc_of(src.slot), d_rows, k,
-                           map_desc.as<float>() + (size_t)first * 256);
-        if (failed(hipMemsetAsync(map_valid.as<uint8_t>() + first, 1, (size_t)k, s) == hipSuccess ? VS_OK : VS_ERR_HIP))
+        }
+        // one staging upload (positions, then the source rows) and one kernel (positions, descriptor
+        // rows, valid flags)
+        const size_t pbytes = (size_t)3 * k * sizeof(double), rbytes = (size_t)k * sizeof(int);
+        if (failed(rows_buf.ensure(pbytes + rbytes))) return;
+        char* hb = take(pbytes + rbytes);
+        if (!hb) return;
+        std::memcpy(hb, m.pos.data() + (size_t)3 * first, pbytes);
+        std::memcpy(hb + pbytes, rows.data(), rbytes);
+        if (failed(hipMemcpyAsync(rows_buf.p, hb, pbytes + rbytes, hipMemcpyHostToDevice, s) == hipSuccess ? VS_OK
+                                                                                                : VS_ERR_HIP))
             return;
+        const double* d_pos = rows_buf.as<double>();
+        const int* d_rows = reinterpret_cast<const int*>(rows_buf.as<char>() + pbytes);
+        hipLaunchKernelGGL(k_map_append, dim3((k + 3) / 4), dim3(256), 0, s, d_pos, d_rows, k, desc_of(src.slot),
+                           map_pos.as<double>() + (size_t)3 * first, map_desc.as<float>() + (size_t)first * 256,
+                           map_valid.as<uint8_t>() + first);
         map_n = first + k;
         // no synchronisation: the next append's upload into rows_buf is ordered behind this gather on
         // the same stream, and the pinned staging it came from is recycled only at a sync()
@@ -1533,6 +1596,7 @@ int settle(vs_slam* sl) {
     VS_HIP(hipStreamWaitEvent(o.s, o.cspec_ev, 0));  // a discarded speculation still reads the pool
     for (const auto& f : T.map().frames)  // new keyframes' features into the archive (loop closure)
         if (f->keyframe && f->kf_slot < 0 && f->slot >= 0) VS_CHECK(o.archive(f.get()));
+    VS_CHECK(o.flush_copies());  // before any slot below is released and reused
     if (sl->dense && !sl->dense_depth.empty()) {
         VS_CHECK(vs_dense_integrate_dev(sl->dense, (int)sl->dense_depth.size(), sl->dense_depth.data(), o.h, o.w,
                                         sl->dense_R.data(), sl->dense_t.data(), o.s));
@@ -1573,6 +1637,7 @@ int settle(vs_slam* sl) {
             f->depth = nullptr;
         }
     }
+    VS_CHECK(o.flush_copies());  // the slot moves
     T.retain_live_frames();  // live frames keep a host copy of their depth beyond the caller's buffer
     sl->batch.clear();
     return o.sync();
@@ -1623,7 +1688,7 @@ void vs_slam_destroy(vs_slam* sl) {
     DevBuf* bufs[] = {&o.pool_kps, &o.pool_desc, &o.pool_n, &o.pool_depth, &o.pool_norms, &o.semi, &o.dgrid,
                       &o.chain_buf,    &o.work, &o.rows_buf,      &o.map_pos, &o.map_desc,  &o.map_valid, &o.map_tmp,
                       &o.pnp_io,       &o.hdr_buf, &o.chain_buf2, &o.hdr_buf2, &o.mstate2,
-                      &o.arch_kps,     &o.arch_desc, &o.arch_n,   &o.lc_buf,    &o.dlt_buf};
+                      &o.arch_kps,     &o.arch_desc, &o.arch_n,   &o.lc_buf,    &o.dlt_buf, &o.cjob_buf};
     for (DevBuf* b : bufs) b->release();
     if (sl->trace) std::fclose(sl->trace);
     delete sl;
