@@ -19,7 +19,7 @@ def main():
 
     import synth
     import vslam_abi as va
-    lib = va.load_library(os.path.join(ROOT, "visual-slam-pipeline_amd", "libvslam_hip_prof.so"))
+    lib = va.load_library(os.environ.get("VS_PROF_LIB") or os.path.join(ROOT, "visual-slam-pipeline_amd", "libvslam_hip_prof.so"))
     lib.vs_debug_fm_cycles.argtypes = [ctypes.c_void_p, ctypes.c_int]
     lib.vs_debug_pnp_cycles.argtypes = [ctypes.c_void_p, ctypes.c_int]
     lib.vs_debug_r3_cycles.argtypes = [ctypes.c_void_p, ctypes.c_int]

@@ -31,7 +31,8 @@ using namespace vs_pnp;
 constexpr int kPnpMaxIters = VS_PNP_MAX_ITERS;
 
 #ifndef VS_PNP_JACOBI
-#define VS_PNP_JACOBI 1  // 0: the round-2 single-copy Jacobi (shuffled angles, two barriers per round)
+#define VS_PNP_JACOBI 2  // 0: the round-2 single-copy Jacobi (shuffled angles, two barriers per round); 1: every lane its two angles;
+                         // 2: ping-pong, each angle computed once (lanes 36..41) and read from LDS (1 -> 2: Jacobi -7 %)
 #endif
 
 #ifdef VS_PNP_PROFILE
@@ -233,8 +234,10 @@ __global__ __launch_bounds__(64) void k_pnp_hyp(const float* __restrict__ obj_al
                                                 const int* __restrict__ off, double fx, double fy, double cx, double cy,
                                                 int niters0, float thr2, int min_inliers, PnpHyp H) {
     crit_prio();
-#if VS_PNP_JACOBI == 1
+#if VS_PNP_JACOBI >= 1
     __shared__ double sAb[2][144], sVb[2][144];  // ping-pong matrices: one barrier per Jacobi round
+    [[maybe_unused]] __shared__ double sC[6], sS[6];  // VS_PNP_JACOBI 2: the round's angles
+    [[maybe_unused]] __shared__ int sAct[6];
     double* sA = sAb[0];
     double* sV = sVb[0];
 #else
@@ -288,14 +291,15 @@ __global__ __launch_bounds__(64) void k_pnp_hyp(const float* __restrict__ obj_al
         __syncthreads();
         PNP_T(1);
         const double total = sTot;
-#if VS_PNP_JACOBI == 1
+#if VS_PNP_JACOBI >= 1
         // Round-robin Jacobi with the matrices ping-ponged between two LDS copies: every lane of
         // 0..35 reads its 2 x 2 block (pair a rows i0 < i1, pair b columns j0 < j1), its V entries
         // (rows 2a, 2a + 1 at the block's columns) and the two diagonal blocks of its pairs from the
         // round's copy, computes both angles itself (no shuffles; the same inputs as the diagonal
         // lane's, so the same angles), rotates (column b, then row a, as the sequential statement)
-        // and writes every value to the other copy; one barrier per round.  Bit-identical to
-        // sym_eig_rr<12>.
+        // and writes every value to the other copy; one barrier per round.  VS_PNP_JACOBI 2 (the
+        // default): lanes 36..41 compute the round's six angles once (same inputs, same angles) and the
+        // block lanes read theirs from LDS.  Bit-identical to sym_eig_rr<12>.
         {
             const int ba = lane / 6, bb = lane % 6;
             const bool blk = lane < 36;
@@ -324,16 +328,33 @@ __global__ __launch_bounds__(64) void k_pnp_hyp(const float* __restrict__ obj_al
                     const double* V = sVb[cur];
                     double* An = sAb[cur ^ 1];
                     double* Vn = sVb[cur ^ 1];
+#if VS_PNP_JACOBI == 2
+                    if (lane >= 36 && lane < 42) {  // pair k's angle once (the same inputs as every user's)
+                        int p0, q0;
+                        rr_pair(12, r, lane - 36, p0, q0);
+                        double c, sn;
+                        const bool act = jacobi_angle_nb(A[p0 * 12 + p0], A[q0 * 12 + q0], A[p0 * 12 + q0], c, sn);
+                        sC[lane - 36] = c;
+                        sS[lane - 36] = sn;
+                        sAct[lane - 36] = act;
+                    }
+                    __syncthreads();
+#endif
                     if (blk) {
                         const int i0 = pk[r] & 15, i1 = (pk[r] >> 4) & 15, j0 = (pk[r] >> 8) & 15, j1 = pk[r] >> 12;
                         double x00 = A[i0 * 12 + j0], x01 = A[i0 * 12 + j1], x10 = A[i1 * 12 + j0], x11 = A[i1 * 12 + j1];
                         const double p0 = V[(2 * ba) * 12 + j0], q0 = V[(2 * ba) * 12 + j1];
                         const double p1 = V[(2 * ba + 1) * 12 + j0], q1 = V[(2 * ba + 1) * 12 + j1];
+#if VS_PNP_JACOBI == 2
+                        const double ca = sC[ba], sa = sS[ba], cb = sC[bb], sb = sS[bb];
+                        const bool acta = sAct[ba] != 0, actb = sAct[bb] != 0;
+#else
                         // both angles branch-free (jacobi_angle_nb) and the skipped rotations as
                         // selects: one straight-line block per round, the two angle chains interleaved
                         double ca, sa, cb, sb;
                         const bool acta = jacobi_angle_nb(A[i0 * 12 + i0], A[i1 * 12 + i1], A[i0 * 12 + i1], ca, sa);
                         const bool actb = jacobi_angle_nb(A[j0 * 12 + j0], A[j1 * 12 + j1], A[j0 * 12 + j1], cb, sb);
+#endif
                         {
                             const double y00 = cb * x00 - sb * x01, y01 = sb * x00 + cb * x01;
                             const double y10 = cb * x10 - sb * x11, y11 = sb * x10 + cb * x11;
