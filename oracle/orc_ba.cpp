@@ -12,8 +12,9 @@
 // lambda * 5 and stop above 1e6; write-back of poses 1..N-1 and all points.
 // Deviations (documented in DESIGN.md): the three global sums (total_cost, new_cost, the RMS
 // errors) are taken in fixed chunks of 256 observations (chunk sums added in order), the order
-// the GPU reduces in; the dense solve is a right-looking Cholesky without OpenCV's SVD fallback
-// (S is SPD by construction: the pose blocks carry the 1e10 damping).
+// the GPU reduces in.  The dense solve restates OpenCV's row-oriented hal Cholesky (chol_solve
+// below) without the DECOMP_SVD retry of :518 (never reached: S is SPD by construction, the pose
+// blocks carry the 1e10 damping, so every pivot is far above DBL_EPSILON).
 #include <cfloat>
 #include <cmath>
 #include <cstring>
