@@ -130,6 +130,26 @@ __global__ __launch_bounds__(256) void k_copy_jobs(const CopyJob* __restrict__ j
     }
 }
 
+// The tracking stream's small host <-> device transfers through coherent (fine-grained) mapped pinned
+// memory, as a kernel: results go straight into host memory (the kernel's stores cross the fabric
+// themselves, so the host's stream synchronisation sees them) and inputs are read from it, without a
+// copy command in the stream (a hipMemcpyAsync D2H started ~11 us after the kernel before it in the
+// kernel trace, profiles/r04n_tracker_chain_trace.txt).  16-, 4- or 1-byte words as the alignment
+// allows.
+__global__ __launch_bounds__(256) void k_copy_bytes(const char* __restrict__ src, char* __restrict__ dst, size_t bytes) {
+    const size_t t0 = (size_t)blockIdx.x * 256 + threadIdx.x, stride = (size_t)gridDim.x * 256;
+    const uintptr_t al = (uintptr_t)src | (uintptr_t)dst | (uintptr_t)bytes;
+    if ((al & 15) == 0) {
+        for (size_t i = t0; i < bytes / 16; i += stride)
+            reinterpret_cast<uint4*>(dst)[i] = reinterpret_cast<const uint4*>(src)[i];
+    } else if ((al & 3) == 0) {
+        for (size_t i = t0; i < bytes / 4; i += stride)
+            reinterpret_cast<unsigned*>(dst)[i] = reinterpret_cast<const unsigned*>(src)[i];
+    } else {
+        for (size_t i = t0; i < bytes; i += stride) dst[i] = src[i];
+    }
+}
+
 // Visibility sweep (Slam.cpp:1089-1108): for every valid map point, Optimizer::project_point
 // (Optimizer.cpp:26-48) with the camera->world pose; bit 0 = inside the image (increase_visible),
 // bit 1 = some keypoint within TRACK_VISIBILITY_RADIUS (increase_found).  Every workgroup first
@@ -234,6 +254,8 @@ __global__ __launch_bounds__(256) void k_visibility(const double* __restrict__ p
 struct Pinned {
     char* base = nullptr;
     size_t cap = 0, used = 0;
+    unsigned flags = hipHostMallocDefault;
+    explicit Pinned(unsigned f = hipHostMallocDefault) : flags(f) {}
     ~Pinned() {
         if (base) (void)hipHostFree(base);
     }
@@ -244,11 +266,45 @@ struct Pinned {
         cap = 0;
         used = 0;
         size_t c = std::max(n, (size_t)1 << 20);
-        if (hipHostMalloc(&base, c, hipHostMallocDefault) != hipSuccess) {
+        if (hipHostMalloc(&base, c, flags) != hipSuccess) {
             set_error("hipHostMalloc failed");
             return VS_ERR_NOMEM;
         }
         cap = c;
+        dev = base;
+        if ((flags & hipHostMallocMapped) && hipHostGetDevicePointer(&dev, base, 0) != hipSuccess) {
+            set_error("hipHostGetDevicePointer failed");
+            return VS_ERR_HIP;
+        }
+        return VS_OK;
+    }
+    void* dev = nullptr;  // the device's address of base (mapped allocations)
+    // the device's address of [p, p + bytes) when it lies in this coherent mapped block, else nullptr
+    char* dev_of(const void* p, size_t bytes) const {
+        const char* c = static_cast<const char*>(p);
+        if (!(flags & hipHostMallocCoherent) || !(flags & hipHostMallocMapped) || c < base || c + bytes > base + cap)
+            return nullptr;
+        return static_cast<char*>(dev) + (c - base);
+    }
+    static int copy_kernel(const void* src, void* dst, size_t bytes, hipStream_t st) {
+        const int blocks = (int)std::min<size_t>((bytes / 16 + 256) / 256, 64);
+        hipLaunchKernelGGL(k_copy_bytes, dim3(blocks), dim3(256), 0, st, static_cast<const char*>(src),
+                           static_cast<char*>(dst), bytes);
+        VS_HIP(hipGetLastError());
+        return VS_OK;
+    }
+    // dst (in this block) <- src (device memory), enqueued on st
+    int to_host(void* dst, const void* src, size_t bytes, hipStream_t st) const {
+        if (bytes == 0) return VS_OK;
+        if (char* d = dev_of(dst, bytes)) return copy_kernel(src, d, bytes, st);
+        VS_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, st));
+        return VS_OK;
+    }
+    // dst (device memory) <- src (in this block), enqueued on st
+    int to_device(void* dst, const void* src, size_t bytes, hipStream_t st) const {
+        if (bytes == 0) return VS_OK;
+        if (char* d = dev_of(src, bytes)) return copy_kernel(d, dst, bytes, st);
+        VS_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, st));
         return VS_OK;
     }
     char* take(size_t n) {
@@ -442,7 +498,7 @@ struct GpuOps {
     hipStream_t s2 = nullptr;
     hipEvent_t cspec_ev = nullptr;
     DevBuf chain_buf2, hdr_buf2, mstate2;
-    Pinned cpin;
+    Pinned cpin{hipHostMallocCoherent | hipHostMallocMapped};
     struct ChainSpec {
         bool valid = false;
         const vs_trk::Frame* cur = nullptr;
@@ -489,7 +545,7 @@ struct GpuOps {
     DevBuf chain_buf, work, rows_buf, map_pos, map_desc, map_valid, map_tmp, pnp_io, hdr_buf;
     int map_cap = 0, map_n = 0;
     bool valid_dirty = false;
-    Pinned pin;
+    Pinned pin{hipHostMallocCoherent | hipHostMallocMapped};  // results come back by k_copy_bytes (d2h)
     std::vector<vs_trk::Frame*> owner;  // persistent slot owners (slots 2B .. 2B + kPersist)
     // Keyframe feature archive (loop closure reads keyframes long after their slots are gone):
     // [arch_cap][kCap] keypoints, [arch_cap][kCap][256] descriptors, [arch_cap] counts.
@@ -683,10 +739,7 @@ struct GpuOps {
         if (failed(sync()) || failed(pin.reserve(n + 64))) return nullptr;
         return pin.take(n);
     }
-    int d2h(void* dst, const void* src, size_t bytes) {
-        VS_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, s));
-        return VS_OK;
-    }
+    int d2h(void* dst, const void* src, size_t bytes) { return pin.to_host(dst, src, bytes, s); }
     // H2D of a host array through the pinned staging area
     int upload(void* dst, const void* src, size_t bytes) {
         if (bytes == 0) return VS_OK;
@@ -697,8 +750,7 @@ struct GpuOps {
             p = pin.take(bytes);
         }
         std::memcpy(p, src, bytes);
-        VS_HIP(hipMemcpyAsync(dst, p, bytes, hipMemcpyHostToDevice, s));
-        return VS_OK;
+        return pin.to_device(dst, p, bytes, s);
     }
 
     int grow_map(int need) {
@@ -944,7 +996,8 @@ struct GpuOps {
         double* dd = reinterpret_cast<double*>(cbuf + kChainDbl);
         vs_match* good = reinterpret_cast<vs_match*>(cbuf + kChainGood);
         vs_match* kept = reinterpret_cast<vs_match*>(cbuf + kChainKept);
-        VS_HIP(hipMemcpyAsync(dh, hhdr, kHdrBytes, hipMemcpyHostToDevice, st));
+        const Pinned& P = (hout >= cpin.base && hout < cpin.base + cpin.cap) ? cpin : pin;  // the speculative or the direct chain
+        VS_CHECK(P.to_device(dh, hhdr, kHdrBytes, st));
         VS_CHECK(match_pairs(ctx, 1, dh, S, pool_desc.as<float>(), pool_n.as<int>(), kCap, vs_trk::cfg::L2_RATIO_THRESHOLD,
                              reinterpret_cast<vs_match*>(cbuf + kChainRaw), di + 3, good, di + 4, st,
                              pool_norms.as<float>(), keys, cnt));
@@ -955,8 +1008,7 @@ struct GpuOps {
                                 st, reinterpret_cast<const uint32_t*>(dh + 4)));
         VS_CHECK(emat_pairs(ctx, 1, dh, pool_kps.as<vs_keypoint>(), kCap, kept, di + 5, di + 6, pool_depth.as<float>(), h,
                             w, K, dd + 23, dd + 32, dd + 35, di + 7, di + 20, st));
-        VS_HIP(hipMemcpyAsync(hout, cbuf, kChainRaw, hipMemcpyDeviceToHost, st));
-        return VS_OK;
+        return P.to_host(hout, cbuf, kChainRaw, st);
     }
     static vs_trk::ChainResult parse_chain(const char* hc) {
         vs_trk::ChainResult R;
@@ -1266,7 +1318,7 @@ struct GpuOps {
         std::memcpy(hb, off, 16);
         std::memcpy(hb + 16, obj.data(), (size_t)n * 3 * sizeof(float));
         std::memcpy(hb + 16 + (size_t)n * 3 * sizeof(float), img.data(), (size_t)n * 2 * sizeof(float));
-        if (failed(hipMemcpyAsync(d, hb, in_bytes, hipMemcpyHostToDevice, s) == hipSuccess ? VS_OK : VS_ERR_HIP))
+        if (failed(pin.to_device(d, hb, in_bytes, s)))
             return r;
         double* dRt = reinterpret_cast<double*>(d + in_pad);
         int* dstat = reinterpret_cast<int*>(dRt + 12);
@@ -1503,9 +1555,7 @@ struct GpuOps {
         if (!hb) return;
         std::memcpy(hb, m.pos.data() + (size_t)3 * first, pbytes);
         std::memcpy(hb + pbytes, rows.data(), rbytes);
-        if (failed(hipMemcpyAsync(rows_buf.p, hb, pbytes + rbytes, hipMemcpyHostToDevice, s) == hipSuccess ? VS_OK
-                                                                                                : VS_ERR_HIP))
-            return;
+        if (failed(pin.to_device(rows_buf.p, hb, pbytes + rbytes, s))) return;
         const double* d_pos = rows_buf.as<double>();
         const int* d_rows = reinterpret_cast<const int*>(rows_buf.as<char>() + pbytes);
         hipLaunchKernelGGL(k_map_append, dim3((k + 3) / 4), dim3(256), 0, s, d_pos, d_rows, k, desc_of(src.slot),
