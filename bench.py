@@ -665,7 +665,7 @@ def main():
         del semi_t, dg_t
 
     track_cus = int(os.environ.get("VS_SLAM_TRACK_CUS", "32"))
-    spec_cus = int(os.environ.get("VS_SLAM_SPEC_CUS", "32"))
+    spec_cus = int(os.environ.get("VS_SLAM_SPEC_CUS", "8"))
     mroof = {"tracker": match_roofline(prof_trk.get("match"), 1, track_cus,
                                        "tracking loop: one pair (frame vs reference keyframe) per launch on the "
                                        f"tracker's {track_cus}-CU stream (overlapped with extraction on the rest)")}

@@ -577,9 +577,12 @@ struct GpuOps {
         // chain's 1024-wave RANSAC grids (k_pnp_hyp median 190 -> 139 us with a CU set of its own);
         // the Winograd network keeps up on the remaining 192 CUs.  Same-box host profile
         // (profiles/r03t_*): process_frame 496 / 466 / 457 us and 1,943 / 2,029 / 2,061 frames/s at
-        // 0 / 16 / 32 chain CUs.  0: the chain shares the tracking CUs.
+        // 0 / 16 / 32 chain CUs.  0: the chain shares the tracking CUs.  Round 4 default 8: with the
+        // tracker at ~0.40 ms per frame the chain (one F-RANSAC workgroup, a 3D-3D grid) still ends
+        // before its frame is tracked on 8 CUs, and the network gains 24: same box, three rounds,
+        // 2,305 -> 2,339 frames/s (profiles/r04z_cu_partition.txt; 4 CUs: 2,252).
         const char* senv = std::getenv("VS_SLAM_SPEC_CUS");
-        const int scu = senv ? std::max(0, std::atoi(senv)) : 32;
+        const int scu = senv ? std::max(0, std::atoi(senv)) : 8;
         // VS_SLAM_POST_CUS > 0: the extraction post-processing (xp) gets CUs of its own, taken from
         // the network's set (default 0: it shares the network's CUs)
         const char* penv = std::getenv("VS_SLAM_POST_CUS");
@@ -588,8 +591,15 @@ struct GpuOps {
         if (tcu > 0 && ncu >= 2 * (tcu + scu + pcu)) {
             const int words = (ncu + 31) / 32;
             std::vector<uint32_t> tm(words, 0u), xm(words, 0u), sm(words, 0u), pm(words, 0u);
-            for (int cu = 0; cu < ncu; cu++)
-                (cu < tcu ? tm : cu < tcu + scu ? sm : cu < tcu + scu + pcu ? pm : xm)[cu / 32] |= 1u << (cu % 32);
+            // VS_SLAM_CU_SPREAD=1 (experiments): each set takes the same share of every 1/8 of the CU
+            // ids (one XCD each when the ids run XCD by XCD) instead of one contiguous range
+            const char* spr = std::getenv("VS_SLAM_CU_SPREAD");
+            const bool spread = spr && spr[0] == '1' && ncu % 8 == 0;
+            for (int cu = 0; cu < ncu; cu++) {
+                const int j = spread ? cu % (ncu / 8) : cu;
+                const int t = spread ? tcu / 8 : tcu, sp = spread ? scu / 8 : scu, pp = spread ? pcu / 8 : pcu;
+                (j < t ? tm : j < t + sp ? sm : j < t + sp + pp ? pm : xm)[cu / 32] |= 1u << (cu % 32);
+            }
             if (scu == 0) sm = tm;
             if (pcu == 0) pm = xm;
             // VS_SLAM_POST_SET = track / all: the post-processing stream on the tracking CUs, or on
@@ -598,6 +608,13 @@ struct GpuOps {
                 if (std::strcmp(ps, "track") == 0) pm = tm;
                 if (std::strcmp(ps, "all") == 0)
                     for (int k = 0; k < words; k++) pm[k] = tm[k] | xm[k] | sm[k];
+            }
+            // VS_SLAM_NET_SET = spec / track / all: the network stream also on the speculative chain's
+            // CUs, the tracking CUs or both (experiments: those CUs idle between latency-bound kernels)
+            if (const char* ns = std::getenv("VS_SLAM_NET_SET")) {
+                const bool wspec = std::strcmp(ns, "spec") == 0 || std::strcmp(ns, "all") == 0;
+                const bool wtrack = std::strcmp(ns, "track") == 0 || std::strcmp(ns, "all") == 0;
+                for (int k = 0; k < words; k++) xm[k] |= (wspec ? sm[k] : 0u) | (wtrack ? tm[k] : 0u);
             }
             masked = hipExtStreamCreateWithCUMask(&s, words, tm.data()) == hipSuccess;
             if (masked && hipExtStreamCreateWithCUMask(&xs, words, xm.data()) != hipSuccess) {
