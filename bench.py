@@ -667,8 +667,12 @@ def main():
     track_cus = int(os.environ.get("VS_SLAM_TRACK_CUS", "32"))
     spec_cus = int(os.environ.get("VS_SLAM_SPEC_CUS", "8"))
     mroof = {"tracker": match_roofline(prof_trk.get("match"), 1, track_cus,
-                                       "tracking loop: one pair (frame vs reference keyframe) per launch on the "
-                                       f"tracker's {track_cus}-CU stream (overlapped with extraction on the rest)")}
+                                       "tracking loop: one pair per launch on the tracker's "
+                                       f"{track_cus}-CU stream (keyframe matches, chains the speculation missed; "
+                                       "overlapped with extraction on the rest)"),
+             "speculative": match_roofline(prof_trk.get("match_spec"), 1, spec_cus,
+                                           "the next frame's speculative chain (frame vs reference keyframe), one pair "
+                                           f"per launch on the chain's {spec_cus} CUs, off the critical path")}
     fe = None
     progress("config[3] batch front end")
     if not args.no_frontend and args.frontend_steps > 0:

@@ -566,7 +566,8 @@ int match_pairs(vs_ctx* ctx, int P, const int* d_pairs, int F, const float* d_de
     } else {
         VS_CHECK(match_state(ctx, P, cap, &a.keys, &a.cnt, s));
     }
-    ProfScope ps(ctx, "match", s);
+    // the tracker's speculative chain (its own key state) is timed apart from the tracking stream's matches
+    ProfScope ps(ctx, (d_keys && d_cnt) ? "match_spec" : "match", s);
     static const bool pre_norms = std::getenv("VS_MATCH_NORMS") != nullptr;  // experiment: norms first
     if (!d_norms && pre_norms) {
         VS_CHECK(ctx->norms_sets.ensure(((size_t)F * cap * sizeof(float) + 255) & ~(size_t)255));
