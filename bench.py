@@ -175,7 +175,7 @@ def match_roofline(ms_launches, pairs_per_launch, cus, where):
     """The descriptor matcher (k_match, one launch per call) against the fp32 MFMA peak: 2 n^2 256
     FLOP per pair at n = 400 keypoints (every synthetic frame reaches SP_MAX_KEYPOINTS), HIP-event
     time on the stream the kernel runs on.  The peak is scaled to the CUs the launch may use."""
-    if not ms_launches or not ms_launches[1]:
+    if not ms_launches or not ms_launches[1] or cus <= 0:
         return None
     ms, launches = ms_launches
     avg_s = ms / 1e3 / launches
@@ -666,6 +666,8 @@ def main():
 
     track_cus = int(os.environ.get("VS_SLAM_TRACK_CUS", "32"))
     spec_cus = int(os.environ.get("VS_SLAM_SPEC_CUS", "8"))
+    if spec_cus <= 0:  # the chain shares the tracking CUs (or, VS_SLAM_SPEC_SET=net, the network's)
+        spec_cus = 256 - track_cus if os.environ.get("VS_SLAM_SPEC_SET") == "net" else track_cus
     mroof = {"tracker": match_roofline(prof_trk.get("match"), 1, track_cus,
                                        "tracking loop: one pair per launch on the tracker's "
                                        f"{track_cus}-CU stream (keyframe matches, chains the speculation missed; "

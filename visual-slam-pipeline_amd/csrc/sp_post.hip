@@ -70,6 +70,7 @@ enum : uint8_t { ST_UNDECIDED = 0, ST_KEPT = 1, ST_OUT = 2 };
 // tests of tests/test_gpu_parity.py).
 __global__ __launch_bounds__(256) void k_decode(const float* __restrict__ semi, int hc, int wc, int B,
                                                 float* __restrict__ heat) {
+    post_prio();
     int idx = blockIdx.x * blockDim.x + threadIdx.x;
     int ncell = hc * wc;
     if (idx >= B * ncell) return;
@@ -119,6 +120,7 @@ __device__ __forceinline__ int floor_bin(unsigned key) {
 
 __global__ __launch_bounds__(kNmsThreads) void k_nms_lmax(const float* __restrict__ heat, int B, int Hp, int Wp,
                                                           int tiles_x, int* __restrict__ hist) {
+    post_prio();
     const int b = blockIdx.y;
     __shared__ unsigned s_key[kNmsReg * kNmsReg];
     __shared__ unsigned s_rmax[kNmsReg * kNmsTile];
@@ -181,6 +183,7 @@ __global__ __launch_bounds__(kNmsThreads) void k_nms_lmax(const float* __restric
 // or 0 (no floor) with fewer.  One workgroup per frame: a suffix scan over the bins from the top.
 __global__ __launch_bounds__(kNmsThreads) void k_nms_floor(const int* __restrict__ hist, int max_kp,
                                                            unsigned* __restrict__ floor_bits) {
+    post_prio();
     constexpr int PER = kFloorBins / kNmsThreads;  // bins per thread (thread 0 owns the top bins)
     const int b = blockIdx.x, t = threadIdx.x, lane = t & 63, wv = t >> 6;
     const int* h = hist + (size_t)b * kFloorBins;
@@ -235,6 +238,7 @@ __global__ __launch_bounds__(kNmsThreads) void k_nms_round(const float* __restri
                                                            int* __restrict__ flags, uint8_t* __restrict__ tflags,
                                                            const unsigned* __restrict__ floor_bits, int r, int B,
                                                            int Hp, int Wp, int tiles_x, int ntiles) {
+    post_prio();
     const int b = blockIdx.y;
     if (flags[r * B + b] == 0) return;
     if (r > 0 && tflags[((size_t)r * B + b) * ntiles + blockIdx.x] == 0) return;
@@ -360,6 +364,7 @@ __global__ __launch_bounds__(kNmsThreads) void k_nms_round(const float* __restri
 __global__ __launch_bounds__(1024) void k_nms_finish(const float* __restrict__ heat, uint8_t* __restrict__ state,
                                                      const int* __restrict__ flags, int R, int B, int Hp, int Wp,
                                                      int* __restrict__ lists, int max_rounds, int* __restrict__ ferr) {
+    post_prio();
     const int b = blockIdx.x;
     if (flags[R * B + b] == 0) return;
     __shared__ int s_n[2];
@@ -412,6 +417,7 @@ __global__ __launch_bounds__(1024) void k_nms_finish(const float* __restrict__ h
 __global__ __launch_bounds__(256) void k_nms_collect(const float* __restrict__ heat, const uint8_t* __restrict__ state,
                                                      int Hp, int Wp, unsigned long long* __restrict__ keys,
                                                      int* __restrict__ keycnt, int key_cap) {
+    post_prio();
     const int b = blockIdx.y;
     const int npx = Hp * Wp, nq = npx / 4;  // Wp is a multiple of 8
     const int lane = threadIdx.x & 63;
@@ -459,6 +465,7 @@ __global__ __launch_bounds__(1024) void k_nms_select(const unsigned long long* _
                                                      int cap, int* __restrict__ nout, int* __restrict__ err,
                                                      const int* __restrict__ ferr, const float* __restrict__ heat,
                                                      int* __restrict__ ties, unsigned long long* __restrict__ totals) {
+    post_prio();
     const int b = blockIdx.x;
     if (ferr[b]) {  // NMS not finished: no keypoints, a negative count that every consumer rejects
         if (threadIdx.x == 0) nout[b] = VS_ERR_NOTCONV;
@@ -627,6 +634,7 @@ __global__ __launch_bounds__(1024) void k_nms_select(const unsigned long long* _
 __global__ __launch_bounds__(256) void k_sample(const float* __restrict__ dgrid, int hc, int wc,
                                                 const vs_keypoint* __restrict__ kps, const int* __restrict__ nkp,
                                                 int cap, float* __restrict__ desc) {
+    post_prio();
     __shared__ float s_v[4][256];
     __shared__ float s_norm[4];
     const int b = blockIdx.y;

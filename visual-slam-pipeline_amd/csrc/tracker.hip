@@ -602,6 +602,10 @@ struct GpuOps {
             }
             if (scu == 0) sm = tm;
             if (pcu == 0) pm = xm;
+            // VS_SLAM_SPEC_SET=net with VS_SLAM_SPEC_CUS=0 (experiments): the speculative chain on the
+            // network's CUs instead of the tracking CUs
+            if (const char* ss = std::getenv("VS_SLAM_SPEC_SET"))
+                if (scu == 0 && std::strcmp(ss, "net") == 0) sm = xm;
             // VS_SLAM_POST_SET = track / all: the post-processing stream on the tracking CUs, or on
             // every CU (experiments: the tracking CUs idle between latency-bound kernels)
             if (const char* ps = std::getenv("VS_SLAM_POST_SET")) {

@@ -31,6 +31,15 @@ __device__ __forceinline__ void crit_prio() {
 #endif
 }
 
+// The extraction post-processing (decode, NMS, sampling) shares the network's CUs with the next
+// chunk's convolution waves, and the tracker waits for a chunk's features: its waves issue ahead of
+// the convolutions'.  (-DVS_NO_POST_PRIO: A/B builds.)
+__device__ __forceinline__ void post_prio() {
+#ifndef VS_NO_POST_PRIO
+    __builtin_amdgcn_s_setprio(2);
+#endif
+}
+
 // ---- errors ------------------------------------------------------------------------------
 void set_error(const std::string& msg);
 #define VS_HIP(call)                                                                  \
