@@ -606,10 +606,11 @@ struct GpuOps {
             // network's CUs instead of the tracking CUs
             if (const char* ss = std::getenv("VS_SLAM_SPEC_SET"))
                 if (scu == 0 && std::strcmp(ss, "net") == 0) sm = xm;
-            // VS_SLAM_POST_SET = track / all: the post-processing stream on the tracking CUs, or on
+            // VS_SLAM_POST_SET = track / spec / all: the post-processing stream on the tracking CUs, the chain's, or on
             // every CU (experiments: the tracking CUs idle between latency-bound kernels)
             if (const char* ps = std::getenv("VS_SLAM_POST_SET")) {
                 if (std::strcmp(ps, "track") == 0) pm = tm;
+                if (std::strcmp(ps, "spec") == 0 && scu > 0) pm = sm;
                 if (std::strcmp(ps, "all") == 0)
                     for (int k = 0; k < words; k++) pm[k] = tm[k] | xm[k] | sm[k];
             }
