@@ -55,3 +55,40 @@ def test_local_ba_bailouts_and_single_step(vsctx, oracle):
     _compare(vsctx.local_ba(R, t, P0, kf, pt, uv, max_iter=1), oracle.local_ba(R, t, P0, kf, pt, uv, max_iter=1))
     with pytest.raises(RuntimeError):
         vsctx.local_ba(R, t, P0, kf, pt + 1000, uv)  # point index out of range
+
+
+_BAND_SCRIPT = r"""
+import sys
+import numpy as np
+sys.path[:0] = sys.argv[2].split("|")
+import synth, vslam_abi
+ctx = vslam_abi.Context(0)
+out = {}
+for tag, (N, M, seed, kw) in {"c2": (50, 10000, 7, dict(span=3, noise=1.0, pert=0.05)),
+                              "s5": (30, 6000, 4, {})}.items():
+    R, t, P, P0, kf, pt, uv = synth.ba_window(N, M, seed, **kw)
+    g = ctx.local_ba(R, t, P0, kf, pt, uv)
+    for i, a in enumerate(g):
+        out[f"{tag}_{i}"] = np.asarray(a)
+ctx.close()
+np.savez(sys.argv[1], **out)
+"""
+
+
+def test_local_ba_band_equals_dense(tmp_path):
+    """k_ba_chol_band (the banded Cholesky, chosen for these windows: band 17 and 29) against the dense
+    look-ahead kernel (VS_BA_BAND=0): every output bit for bit.  The band kernel skips only products
+    with exact zeros outside S's band, in the dense kernel's per-element order."""
+    import os
+    import subprocess
+    import sys
+    paths = "|".join(p for p in sys.path if p)
+    res = {}
+    for band in ("1", "0"):
+        f = tmp_path / f"band{band}.npz"
+        subprocess.run([sys.executable, "-c", _BAND_SCRIPT, str(f), paths], check=True, timeout=240,
+                       env={**os.environ, "VS_BA_BAND": band})
+        res[band] = np.load(f)
+    assert res["1"].files == res["0"].files
+    for k in res["1"].files:
+        assert np.array_equal(res["1"][k], res["0"][k]), k

@@ -13,7 +13,8 @@
 //   k_ba_pt_acc       per point: Hmm, bm, Hpm in gather order, Cholesky inverse, U = Hpm Hinv
 //   k_ba_schur        one workgroup per (a, b) block: S_ab = [a == b] Hpp_a (1 + lambda) on the
 //                     diagonal - sum over common points (ascending) of U_a Hpm_b^T; b_a likewise
-//   k_ba_chol         dense right-looking Cholesky + the two triangular solves (one workgroup)
+//   k_ba_chol         dense right-looking Cholesky + the two triangular solves (one workgroup), or
+//   k_ba_chol_band    the same for a banded S (one wave, the band in LDS; bit-identical results)
 //   k_ba_update       back-substitution dm = Hinv (-bm - sum Hpm^T dp), new poses
 //   k_ba_cost         new cost (fixed chunks) + accept / reject, lambda, convergence (last chunk)
 // Every element is accumulated in the same order as the CPU restatement (oracle/orc_ba.cpp); the
@@ -41,6 +42,7 @@ struct BaCtl {
 
 struct BaDev {
     int N, M, n_obs, n_pairs, n_chunks, np;  // np: the Schur dimension 6N padded to 32
+    int band;                                 // S_ij = 0 for i - j > band (k_ba_chol_band), from the observer pairs
     Cam K;
     const int *okf, *opt, *oslot, *kf_off, *kf_obs, *pt_off, *pt_obs, *pv_off, *pv_kf, *ab_off, *ab_u, *ab_h, *ab_j,
         *kb_off, *kb_u, *kb_j;
@@ -432,6 +434,126 @@ __device__ __forceinline__ void wave_lds_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// S dp = -bs for a banded S (k_ba_chol's arithmetic, fewer terms).  When no point is seen by two
+// keyframes more than Bb apart, S_ij = 0 for i - j > band = 6 Bb + 5, and a Cholesky factor keeps
+// that band (no fill outside it).  Every term the dense statement adds outside the band is a
+// product with an exact zero, so skipping them leaves every element's value unchanged (at most the
+// sign of an exact-zero element can differ, which no later result sees) — the factor and the
+// solution are the oracle's (oracle/orc_ba.cpp chol_solve), element for element in the same order.
+// One wave, right-looking with the matrix as its band in LDS (row i, offset d = i - j): at column j
+// every lane updates its elements of the trailing band triangle (i, k) with j < k <= i <= j + band,
+// L = acc * R taken on the fly (the stored value stays the accumulated one), and the next pivot
+// R_{j+1} = 1 / sqrt(acc_{j+1,j+1} - L_{j+1,j}^2) is evaluated by every lane from the same LDS values
+// (lane-uniform, so the sqrt / division chain interleaves with the element updates instead of
+// running on a masked lane after them).  The forward substitution rides along; the backward one runs
+// from the last row with x_k broadcast from the lane that finished it.  Chosen by the host when the
+// band fits kBandMaxW columns; a pivot below DBL_EPSILON fails the solve as in k_ba_chol.
+constexpr int kBandMaxW = 36;  // band + 1 <= kBandMaxW (band <= 35: Bb <= 5)
+// trailing-triangle elements per lane for a band: ceil(band (band + 1) / 2 / 64)
+constexpr int band_slots(int band) { return (band * (band + 1) / 2 + 63) / 64; }
+template <int NS>
+__global__ __launch_bounds__(64) void k_ba_chol_band(BaDev d) {
+    BA_LIVE(d);
+    const int n = 6 * d.N, np = d.np, B = d.band, W = B + 1, lane = threadIdx.x;
+    // A[i * W + dd] = acc (i, i - dd); the 64 cells past the band are each lane's dummy store target
+    __shared__ double A[kCholMaxN * kBandMaxW + 64];
+    __shared__ double Rd[kCholMaxN], xs[kCholMaxN + 64];
+    for (int e = lane; e < n * W; e += 64) {
+        const int i = e / W, dd = e % W;
+        A[e] = dd <= i ? d.S[(size_t)i * np + (i - dd)] : 0.0;
+    }
+    for (int i = lane; i < n; i += 64) xs[i] = -d.bs[i];
+    const int dummyA = kCholMaxN * kBandMaxW + lane, dummyX = kCholMaxN + lane;
+    // this lane's trailing-triangle elements e = lane + 64 q -> (a, b), 0 <= b <= a < B, i = j + 1 + a,
+    // k = j + 1 + b, as offsets from row j + 1: the element, L_ij's and L_kj's slots.  e = 0 (0, 0) is
+    // the next pivot, which every lane evaluates; e = 1 (1, 0) and e = 2 (1, 1) are lane 1's and lane
+    // 2's first elements, whose new values are the pivot after next's inputs (read back by readlane).
+    const int nel = B * (B + 1) / 2;
+    int ea[NS], oe[NS], oi[NS], ok[NS];
+#pragma unroll
+    for (int q = 0; q < NS; q++) {
+        const int e = lane + 64 * q;
+        int a = 0;
+        while ((a + 1) * (a + 2) / 2 <= e) a++;
+        const int b = e - a * (a + 1) / 2;
+        ea[q] = e < nel && e > 0 ? a : n;  // n: never a live row offset
+        oe[q] = a * W + (a - b);
+        oi[q] = a * W + a + 1;
+        ok[q] = b * W + b + 1;
+    }
+    __syncthreads();
+    bool bad = A[0] < DBL_EPSILON;
+    double Rj = 1.0 / sqrt(A[0]);
+    double p1 = A[W + 1], p0 = A[W];  // acc (1, 0), acc (1, 1): the next pivot's inputs
+    double xj = xs[0];                 // x_j with its forward terms so far
+    if (lane == 0) Rd[0] = Rj;
+    for (int j = 0; j < n && !bad; j++) {
+        const int j1 = j + 1, base = j1 * W;
+        const double yj = xj * Rj;
+        // the next pivot, lane-uniform and branch-free (meaningless past the last row)
+        const double l = p1 * Rj;
+        const double accn = p0 - l * l;
+        const bool badn = j1 < n && accn < DBL_EPSILON;
+        const double Rn = 1.0 / sqrt(accn);
+        // the lane's elements: all loads first, then the updates, then the stores (a dead slot
+        // reads its own cells harmlessly and stores to its dummy cell)
+        double xi[NS], xl[NS], xk[NS];
+        int st[NS];
+#pragma unroll
+        for (int q = 0; q < NS; q++) {
+            const bool live = j1 + ea[q] < n;
+            st[q] = live ? base + oe[q] : dummyA;
+            const int bq = live ? base : 0;
+            xi[q] = A[bq + oe[q]];
+            xl[q] = A[bq + oi[q]];
+            xk[q] = A[bq + ok[q]];
+        }
+        const bool fl = lane < B && j1 + lane < n;
+        const int fi = fl ? j1 + lane : dummyX;
+        const double xf = xs[fl ? j1 + lane : 0], lf = A[fl ? base + lane * W + lane + 1 : 0];
+        double v0 = 0.0;
+#pragma unroll
+        for (int q = 0; q < NS; q++) {
+            const double v = xi[q] - (xl[q] * Rj) * (xk[q] * Rj);
+            A[st[q]] = v;
+            if (q == 0) v0 = v;
+        }
+        const double xn = xf - (lf * Rj) * yj;  // forward substitution: x_i -= L_ij y_j
+        xs[fi] = xn;
+        if (lane == 0) {
+            xs[j] = yj;
+            if (j1 < n) {
+                A[base] = accn;
+                Rd[j1] = Rn;
+            }
+        }
+        p1 = readlane_f64(v0, 1);
+        p0 = readlane_f64(v0, 2);
+        xj = readlane_f64(xn, 0);
+        bad = badn;
+        Rj = Rn;
+        wave_lds_sync();
+    }
+    if (bad) {
+        if (lane == 0) d.ctl->solved = 0;
+        return;
+    }
+    // backward: x_k = y'_k R_k with y'_k = y_k - sum_{k' > k, descending} L_k'k x_k'
+    double yk = xs[n - 1];
+    for (int k = n - 1; k >= 0; k--) {
+        const double xkk = yk * Rd[k];  // lane-uniform
+        const bool live = lane < B && k - 1 - lane >= 0;
+        const int i = live ? k - 1 - lane : 0;
+        const double yn = xs[i] - (A[live ? k * W + lane + 1 : 0] * Rd[i]) * xkk;
+        xs[live ? i : dummyX] = yn;
+        if (lane == 0) xs[k] = xkk;
+        yk = readlane_f64(yn, 0);
+        wave_lds_sync();
+    }
+    for (int i = lane; i < n; i += 64) d.dp[i] = xs[i];
+    if (lane == 0) d.ctl->solved = 1;
+}
+
 // the padded rows n..np-1 of S: identity (their columns >= n above the diagonal are never read)
 __global__ void k_ba_pad(BaDev d) {
     const int n = 6 * d.N, np = d.np;
@@ -785,6 +907,11 @@ int local_ba(vs_ctx* ctx, int N, double* R, double* t, int M, double* P, int n_o
             for (int y = 0; y < no; y++) ab_cnt[ob[x] * N + ob[y]]++;
         }
     }
+    // S's band: block (a, b) is nonzero only when a point is seen by both keyframes
+    int band_blocks = 0;
+    for (int a = 0; a < N; a++)
+        for (int b = 0; b < a; b++)
+            if (ab_cnt[a * N + b]) band_blocks = std::max(band_blocks, a - b);
     std::vector<int> ab_off(N * N + 1, 0), kb_off(N + 1, 0);
     for (int p = 0; p < N * N; p++) ab_off[p + 1] = ab_off[p] + ab_cnt[p];
     for (int a = 0; a < N; a++) kb_off[a + 1] = kb_off[a] + kb_cnt[a];
@@ -884,7 +1011,24 @@ int local_ba(vs_ctx* ctx, int N, double* R, double* t, int M, double* P, int n_o
     d.n_pairs = n_pairs;
     d.n_chunks = n_chunks;
     d.np = np;
+    d.band = 6 * band_blocks + 5;
     d.K = Cam{K4[0], K4[1], K4[2], K4[3]};
+    // the banded Cholesky when the band fits it (VS_BA_BAND=0: always the dense kernel, A/B)
+    static const bool band_off = [] {
+        const char* e = std::getenv("VS_BA_BAND");
+        return e && e[0] == '0';
+    }();
+    bool use_band = !band_off && d.band + 1 <= kBandMaxW;
+    void (*chol_band)(BaDev) = nullptr;  // the instantiation for the band's elements per lane
+    switch (band_slots(d.band)) {
+        case 1: chol_band = k_ba_chol_band<1>; break;
+        case 2: chol_band = k_ba_chol_band<2>; break;
+        case 3: chol_band = k_ba_chol_band<3>; break;
+        case 5: chol_band = k_ba_chol_band<5>; break;
+        case 7: chol_band = k_ba_chol_band<7>; break;
+        case 10: chol_band = k_ba_chol_band<10>; break;
+        default: use_band = false;  // (band = 6 Bb + 5 gives 1, 2, 3, 5, 7 or 10)
+    }
 #define BA_PTR(T, o) reinterpret_cast<T*>(base + (o))
     d.okf = BA_PTR(int, o_okf);
     d.opt = BA_PTR(int, o_opt);
@@ -947,7 +1091,10 @@ int local_ba(vs_ctx* ctx, int N, double* R, double* t, int M, double* P, int n_o
             hipLaunchKernelGGL(k_ba_kf_acc, dim3(N), dim3(64), 0, s, d);
             hipLaunchKernelGGL(k_ba_pt_acc, dim3(cdiv(M, T)), dim3(T), 0, s, d);
             hipLaunchKernelGGL(k_ba_schur, dim3(N * N + N), dim3(64), 0, s, d);
-            hipLaunchKernelGGL(k_ba_chol, dim3(1), dim3(512), 0, s, d);
+            if (use_band)
+                hipLaunchKernelGGL(chol_band, dim3(1), dim3(64), 0, s, d);
+            else
+                hipLaunchKernelGGL(k_ba_chol, dim3(1), dim3(512), 0, s, d);
             hipLaunchKernelGGL(k_ba_update, dim3(cdiv(M + N, T)), dim3(T), 0, s, d);
             hipLaunchKernelGGL(k_ba_cost, dim3(n_chunks), dim3(kCostChunk), 0, s, d, 1, 1, 1);
             hipLaunchKernelGGL(k_ba_commit, dim3(cdiv(3 * M + N, T)), dim3(T), 0, s, d);
