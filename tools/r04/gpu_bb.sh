@@ -2,7 +2,7 @@
 # BA: banded Cholesky (k_ba_chol_band, one wave, S's band in LDS) vs the dense look-ahead kernel (VS_BA_BAND=0):
 # BA parity and goldens, config[2] timing A/B, kernel trace
 export TMPDIR=/tmp
-O=gpurun_out/r04bb3; mkdir -p $O
+O=gpurun_out/r04bb6; mkdir -p $O
 timeout -k 10 600 python -u -m pytest tests/test_gpu_ba.py tests/test_golden.py -m gpu -x -q --timeout 300 --timeout-method thread -p no:cacheprovider > $O/pytest.log 2>&1
 rc=$?; tail -3 $O/pytest.log; [ $rc -eq 0 ] || exit $rc
 for r in 1 2; do

@@ -458,9 +458,18 @@ __global__ __launch_bounds__(64) void k_ba_chol_band(BaDev d) {
     // A[i * W + dd] = acc (i, i - dd); the 64 cells past the band are each lane's dummy store target
     __shared__ double A[kCholMaxN * kBandMaxW + 64];
     __shared__ double Rd[kCholMaxN], xs[kCholMaxN + 64];
-    for (int e = lane; e < n * W; e += 64) {
-        const int i = e / W, dd = e % W;
-        A[e] = dd <= i ? d.S[(size_t)i * np + (i - dd)] : 0.0;
+    // the band out of S (just written by k_ba_schur, in L2): eight loads in flight per lane, then
+    // their LDS stores (one load at a time cost a global round trip per element)
+    for (int e0 = lane; e0 < n * W; e0 += 64 * 8) {
+        double v[8];
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+            const int e = e0 + 64 * u, i = e / W, dd = e - i * W;
+            v[u] = (e < n * W && dd <= i) ? d.S[(size_t)i * np + (i - dd)] : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < 8; u++)
+            if (e0 + 64 * u < n * W) A[e0 + 64 * u] = v[u];
     }
     for (int i = lane; i < n; i += 64) xs[i] = -d.bs[i];
     const int dummyA = kCholMaxN * kBandMaxW + lane, dummyX = kCholMaxN + lane;
