@@ -165,7 +165,8 @@ def superpoint_model(flat, seed=0, heads_swapped=False, identity_alias=True, dro
     (Pow 2 -> ReduceSum -> Sqrt -> Div), "mul_self_sum_sqrt" (Mul(x, x) -> ReduceSum -> Sqrt -> Div),
     "normalize_clip" (F.normalize: ReduceL2 -> Clip(min=eps) -> Expand -> Div), "reciprocal"
     (x * Reciprocal(ReduceL2(x))), "raw" (convDb's output itself), or the invalid "reduce_all" (a
-    ReduceL2 over every axis).  semi_tail: "logits" (convPb's output) or the invalid "softmax".
+    ReduceL2 over every axis), "pow3_sum_sqrt" (exponent 3: not a norm) and "clip_max" (a clamp with an
+    upper bound on the norm).  semi_tail: "logits" (convPb's output) or the invalid "softmax".
     pads=False drops the pads attribute of the 3x3 convs (ONNX's default: no padding)."""
     rng = np.random.default_rng(seed)
     G = _Graph(rng)
@@ -215,13 +216,19 @@ def superpoint_model(flat, seed=0, heads_swapped=False, identity_alias=True, dro
         elif desc_tail == "reducel2_unsqueeze":
             n = G.op("ReduceL2", [d], [attr_ints("axes", [1]), attr_int("keepdims", 0)])
             n = G.op("Unsqueeze", [n, int_const([1])])
-        elif desc_tail in ("pow_sum_sqrt", "mul_self_sum_sqrt"):
-            sq = G.op("Pow", [d, f_const(2.0)]) if desc_tail == "pow_sum_sqrt" else G.op("Mul", [d, d])
+        elif desc_tail in ("pow_sum_sqrt", "mul_self_sum_sqrt", "pow3_sum_sqrt"):
+            if desc_tail == "mul_self_sum_sqrt":
+                sq = G.op("Mul", [d, d])
+            else:
+                sq = G.op("Pow", [d, f_const(2.0 if desc_tail == "pow_sum_sqrt" else 3.0)])
             n = G.op("Sqrt", [G.op("ReduceSum", [sq, int_const([1])], [attr_int("keepdims", 1)])])
         elif desc_tail == "normalize_clip":
             n = G.op("ReduceL2", [d, int_const([1])], [attr_int("keepdims", 1)])
             n = G.op("Clip", [n, f_const(1e-12), ""])
             n = G.op("Expand", [n, int_const([1, 256, 1, 1])])
+        elif desc_tail == "clip_max":
+            n = G.op("ReduceL2", [d, int_const([1])], [attr_int("keepdims", 1)])
+            n = G.op("Clip", [n, f_const(1e-12), f_const(0.5)])
         elif desc_tail == "reciprocal":
             n = G.op("ReduceL2", [d, int_const([-3])], [attr_int("keepdims", 1)])
             return G.op("Mul", [d, G.op("Reciprocal", [n])], out="desc")

@@ -147,8 +147,10 @@ __global__ __launch_bounds__(kCostChunk) void k_ba_cost(BaDev d, int mode, int c
         double sum = 0;
         for (int k = 0; k < o1 - o0; k++) sum += s_v[k];
         __hip_atomic_store(d.chunk + c, sum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        const unsigned prev = __hip_atomic_fetch_add(&d.ctl->arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        // the chunk sum is ordered before the arrival by the HIP memory model (release RMW), and the
+        // last arriver's loads after every other chunk's arrival (acquire RMW) — ADVICE r04: no
+        // reliance on an inline s_waitcnt and the current ISA's ordering
+        const unsigned prev = __hip_atomic_fetch_add(&d.ctl->arrive, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
         if (prev == (unsigned)d.n_chunks - 1) {
             __hip_atomic_store(&d.ctl->arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             double tot = 0;
@@ -403,6 +405,9 @@ __global__ __launch_bounds__(64) void k_ba_schur(BaDev d) {
 constexpr int kCholNB = 32;
 constexpr int kCholMaxN = 6 * VS_BA_MAX_KEYFRAMES;  // a multiple of kCholNB
 static_assert(kCholMaxN % kCholNB == 0, "padded Schur dimension");
+// k_ba_chol (512 lanes) maps one thread to one row below the panel (rb = tid - 64) and in both
+// substitutions: every row beyond the first panel needs a thread of waves 1..7
+static_assert(kCholMaxN - kCholNB <= 512 - 64, "k_ba_chol: one thread per row needs <= 448 rows below the panel");
 constexpr int kCholLd = kCholMaxN;  // PnT row length
 
 #ifdef VS_BA_PROFILE
@@ -449,6 +454,9 @@ __device__ __forceinline__ void wave_lds_sync() {
 // from the last row with x_k broadcast from the lane that finished it.  Chosen by the host when the
 // band fits kBandMaxW columns; a pivot below DBL_EPSILON fails the solve as in k_ba_chol.
 constexpr int kBandMaxW = 36;  // band + 1 <= kBandMaxW (band <= 35: Bb <= 5)
+static_assert((kCholMaxN * kBandMaxW + 64 + kCholMaxN + kCholMaxN + 64) * sizeof(double) <= 160 * 1024,
+              "k_ba_chol_band: the band, R and x must fit one CU's LDS (raise VS_BA_MAX_KEYFRAMES only with a "
+              "narrower kBandMaxW)");
 // trailing-triangle elements per lane for a band: ceil(band (band + 1) / 2 / 64)
 constexpr int band_slots(int band) { return (band * (band + 1) / 2 + 63) / 64; }
 template <int NS>

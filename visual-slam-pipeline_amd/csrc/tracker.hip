@@ -1694,7 +1694,13 @@ int settle(vs_slam* sl) {
         if (T.is_live(f.get())) {
             if (f->slot >= 0 && f->slot < 2 * o.B) {
                 const int to = o.persistent_slot(f.get());
-                if (to < 0) return VS_ERR_CAPACITY;
+                if (to < 0) {
+                    // the moves queued so far are complete (their frames already point at the new slots):
+                    // run them before reporting, so that no later flush copies a reused batch slot
+                    // 
+                    const int rc = o.flush_copies();
+                    return rc != VS_OK ? rc : VS_ERR_CAPACITY;
+                }
                 VS_CHECK(o.copy_slot(f->slot, to));
                 f->slot = to;
             }

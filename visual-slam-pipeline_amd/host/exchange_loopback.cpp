@@ -8,6 +8,8 @@
 // world size, which one GPU box cannot give RCCL.
 #include <condition_variable>
 #include <cstring>
+#include <exception>
+#include <new>
 #include <deque>
 #include <mutex>
 #include <thread>
@@ -27,18 +29,31 @@ struct Hub {
     std::vector<std::vector<uint8_t>> stage;
     int arrived = 0;
     long generation = 0;
+    // set by a rank that fails: every wait below also wakes on it and returns VS_ERR_IO, so no rank
+    // stays blocked on a message or barrier arrival that will never come
+    bool aborted = false;
     explicit Hub(int w) : world(w), box((size_t)w * w), stage(w) {}
 
-    void barrier() {
+    void abort() {
+        {
+            std::lock_guard<std::mutex> lk(mu);
+            aborted = true;
+        }
+        cv.notify_all();
+    }
+    int barrier() {
         std::unique_lock<std::mutex> lk(mu);
+        if (aborted) return VS_ERR_IO;
         const long gen = generation;
         if (++arrived == world) {
             arrived = 0;
             generation++;
             cv.notify_all();
         } else {
-            cv.wait(lk, [&] { return generation != gen; });
+            cv.wait(lk, [&] { return generation != gen || aborted; });
+            if (generation == gen) return VS_ERR_IO;
         }
+        return 0;
     }
 };
 
@@ -66,7 +81,8 @@ struct Loopback final : vs_bx::Transport {
         if (peer < 0 || peer >= hub.world) return VS_ERR_ARG;
         std::unique_lock<std::mutex> lk(hub.mu);
         auto& q = hub.box[(size_t)peer * hub.world + rank];
-        hub.cv.wait(lk, [&] { return !q.empty(); });
+        hub.cv.wait(lk, [&] { return !q.empty() || hub.aborted; });
+        if (q.empty()) return VS_ERR_IO;
         std::vector<uint8_t> m = std::move(q.front());
         q.pop_front();
         if (m.size() != bytes) return VS_ERR_ARG;  // a message of another size: mismatched pairing
@@ -79,13 +95,12 @@ struct Loopback final : vs_bx::Transport {
             const auto* p = static_cast<const uint8_t*>(src);
             hub.stage[rank].assign(p, p + bytes_per_rank);
         }
-        hub.barrier();
+        if (int rc = hub.barrier()) return rc;
         for (int r = 0; r < hub.world; r++) {
             if (hub.stage[r].size() != bytes_per_rank) return VS_ERR_ARG;
             std::memcpy(static_cast<uint8_t*>(dst) + (size_t)r * bytes_per_rank, hub.stage[r].data(), bytes_per_rank);
         }
-        hub.barrier();  // every rank has read the stage before it is reused
-        return 0;
+        return hub.barrier();  // every rank has read the stage before it is reused
     }
 };
 
@@ -101,7 +116,7 @@ extern "C" int vs_batch_exchange_loopback(int world, int B, int cap, int steps, 
     const size_t kb = (size_t)cap * vs_bx::kKpBytes, dfl = (size_t)cap * 256;
     Hub hub(world);
     std::vector<int> rcs(world, 0);
-    auto rank_main = [&](int r) {
+    auto rank_body = [&](int r) {
         // this rank's tables (zeroed: slot 0 / carry hold count 0 before the first step)
         std::vector<uint8_t> kps((size_t)(B + 1) * kb, 0), rx_k(kb, 0), carry_k(kb, 0), gk;
         std::vector<float> desc((size_t)(B + 1) * dfl, 0.f), rx_d(dfl, 0.f), carry_d(dfl, 0.f), gd;
@@ -128,7 +143,8 @@ extern "C" int vs_batch_exchange_loopback(int world, int B, int cap, int steps, 
             const int rc = vs_bx::exchange(t, x);
             if (rc != 0) {
                 rcs[r] = rc;
-                return;  // the other ranks block in recv / barrier: the caller sees the error after join
+                hub.abort();  // wakes the ranks blocked in recv / barrier: they return VS_ERR_IO
+                return;
             }
             const size_t o = (size_t)st * world + r;
             std::memcpy(reinterpret_cast<uint8_t*>(slot0_kps) + o * kb, t.kps_slot(0), kb);
@@ -141,9 +157,32 @@ extern "C" int vs_batch_exchange_loopback(int world, int B, int cap, int steps, 
             }
         }
     };
+    // no exception crosses the C ABI: a rank that throws (allocation of its tables) records the error
+    // and aborts the hub like a failing exchange
+    auto rank_main = [&](int r) {
+        try {
+            rank_body(r);
+        } catch (const std::bad_alloc&) {
+            rcs[r] = VS_ERR_NOMEM;
+            hub.abort();
+        } catch (...) {
+            rcs[r] = VS_ERR_IO;
+            hub.abort();
+        }
+    };
     std::vector<std::thread> th;
-    for (int r = 0; r < world; r++) th.emplace_back(rank_main, r);
+    try {
+        th.reserve(world);
+        for (int r = 0; r < world; r++) th.emplace_back(rank_main, r);
+    } catch (...) {  // thread creation failed: release the ranks already started, then report
+        hub.abort();
+        for (auto& t : th) t.join();
+        return VS_ERR_NOMEM;
+    }
     for (auto& t : th) t.join();
+    // the first failure is the cause; VS_ERR_IO from the ranks it woke is the consequence
+    for (int rc : rcs)
+        if (rc != 0 && rc != VS_ERR_IO) return rc;
     for (int rc : rcs)
         if (rc != 0) return rc;
     return VS_OK;

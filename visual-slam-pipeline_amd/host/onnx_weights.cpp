@@ -340,6 +340,7 @@ bool parse_attribute(Span s, Node& n, std::map<std::string, Tensor>& tensors, st
     else if (name == "auto_pad") n.auto_pad = sv;
     else if (name == "keepdims") n.keepdims = i;
     else if (name == "axes") n.ints_axes = ints, n.has_axes = true;
+    else if (name == "max") n.has_max = true;
     else if (name == "dilations") {
         for (int64_t d : ints)
             if (d != 1) return err = "dilated convolutions are not part of these networks", false;
@@ -482,6 +483,7 @@ static bool load_impl(const char* path, Model& model, std::string& err) {
     for (const auto& kv : r.tensors) {
         model.consts.insert(kv.first);
         if (kv.second.dtype == DT_INT32 || kv.second.dtype == DT_INT64) model.int_consts[kv.first] = kv.second.ints;
+        if (kv.second.data.size() == 1 && !kv.second.external) model.float_scalars[kv.first] = kv.second.data[0];
     }
     for (int i = 0; i < (int)r.nodes.size(); i++) {
         const Node& n = r.nodes[i];
@@ -618,7 +620,10 @@ bool is_channel_norm_of(const Model& m, const std::map<std::string, int>& produc
         if (p == producer.end()) return false;
         const Node& n = m.nodes[p->second];
         if (n.in.empty()) return false;
-        if (n.op == "Unsqueeze" || n.op == "Expand" || n.op == "Clip") {
+        if (n.op == "Unsqueeze" || n.op == "Expand") {
+            name = n.in[0];
+        } else if (n.op == "Clip") {  // a clamp from below only: no max (input 3 or, opset < 11, attribute)
+            if (n.has_max || (n.in.size() > 2 && !n.in[2].empty())) return false;
             name = n.in[0];
         } else if (n.op == "Max") {  // max(norm, eps): one operand a constant
             if (n.in.size() != 2) return false;
@@ -638,9 +643,10 @@ bool is_channel_norm_of(const Model& m, const std::map<std::string, int>& produc
             if (sq.op == "Mul" && sq.in.size() == 2)
                 return strip_alias(m, producer, sq.in[0]) == x && strip_alias(m, producer, sq.in[1]) == x;
             if (sq.op == "Pow" && sq.in.size() == 2 && strip_alias(m, producer, sq.in[0]) == x) {
-                // exponent 2: a float constant (initializer / Constant); its value is not kept by the
-                // reader, so any constant exponent on a Pow feeding ReduceSum -> Sqrt is taken as 2
-                return m.consts.count(sq.in[1]) > 0;
+                // the exponent must be the scalar float constant 2 (any other exponent is
+                // not an L2 norm, and the graph is then refused)
+                auto e = m.float_scalars.find(strip_alias(m, producer, sq.in[1]));
+                return e != m.float_scalars.end() && e->second == 2.0f;
             }
             return false;
         } else {

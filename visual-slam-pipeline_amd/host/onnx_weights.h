@@ -34,6 +34,7 @@ struct Node {
     std::vector<std::string> in, out;
     std::vector<int64_t> ints_kernel, ints_strides, ints_pads, ints_axes;
     bool has_axes = false;      // an "axes" attribute (opset < 18 reductions)
+    bool has_max = false;       // a "max" attribute (Clip, opset < 11)
     int64_t group = 1;
     int64_t keepdims = 1;
     float epsilon = 1e-5f;
@@ -46,6 +47,7 @@ struct Model {
     std::vector<Conv> convs;                   // in graph order
     std::map<std::string, std::vector<int64_t>> int_consts;  // small INT32 / INT64 constants (axes, shapes)
     std::set<std::string> consts;              // every initializer / Constant output name
+    std::map<std::string, float> float_scalars;  // one-element FLOAT constants (Pow exponents, Clip bounds)
 };
 
 // Parse `path` and collect its convolutions.  Returns false with a message in err.
