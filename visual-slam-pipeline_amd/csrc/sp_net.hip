@@ -1204,6 +1204,22 @@ inline bool wino_enabled() {
     return on;
 }
 
+inline bool wino4_enabled() {
+    static const bool on = [] {
+        const char* e = std::getenv("VS_WINO4");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+
+inline long wino4_min_wg() {
+    static const long n = [] {
+        const char* e = std::getenv("VS_WINO4_MIN_WG");
+        return e ? std::atol(e) : 64L;
+    }();
+    return n;
+}
+
 // VS_WINO_C32=0: cout <= 32 layers on the 64-channel variant (A/B measurements)
 bool wino_c32_on() {
     static const bool on = [] {
@@ -1268,6 +1284,14 @@ int launch_wino(const DevLayer& L, const float* in, int in_cstride, int in_coff,
     a.w1a = L1a ? L1a->w1a_rows : nullptr;  // [64][9 taps, bias, 0, 0]
     a.b1a = nullptr;
     a.act = 1;  // every SuperPoint 3x3 conv is followed by ReLU
+    // F(4x4, 3x3) (round 5, wino4.hip) on the layers whose 16 x 16-pixel workgroups are many per frame:
+    // at least VS_WINO4_MIN_WG (default 64) per frame — a property of the layer's geometry alone, so a
+    // frame's result never depends on the batch it is extracted in; VS_WINO4=0 keeps every layer on
+    // F(2x2, 3x3) (A/B)
+    if (L.wu4 && wino4_enabled() && (long)((H + 15) / 16) * ((W + 15) / 16) * (L.cout_pad / 64) >= wino4_min_wg()) {
+        a.wu = L.wu4;
+        return wino4_launch(a, POOL, FUSE1A, s);
+    }
     return wino3_launch(a, POOL, FUSE1A, s);
 }
 

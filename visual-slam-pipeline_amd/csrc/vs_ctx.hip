@@ -162,6 +162,38 @@ std::vector<float> winograd_weights(const float* w, int cin, int cout_pad) {
     return u;
 }
 
+// Winograd F(4x4, 3x3) weights (wino4.hip): U[xi = 6i + j][ci][co] = (G g G^T)[i][j] with
+// G = [1/4 0 0; -1/6 -1/6 -1/6; -1/6 1/6 -1/6; 1/24 1/12 1/6; 1/24 -1/12 1/6; 0 0 1], in fp64 and rounded
+// once, stored in the order the kernel's lanes load their MFMA B operands: per (64-column tile nt,
+// 4-channel k-step kk, 16-column group cg, domain half xh) 64 lanes x 20 floats, lane (lk, li) holding
+// U[18 xh + x][4 kk + lk][64 nt + 16 cg + li] at x = 0..17 (two floats of padding: 16-byte loads).
+std::vector<float> winograd4_weights(const float* w, int cin, int cout_pad) {
+    static const double G[6][3] = {{0.25, 0, 0},
+                                   {-1.0 / 6, -1.0 / 6, -1.0 / 6},
+                                   {-1.0 / 6, 1.0 / 6, -1.0 / 6},
+                                   {1.0 / 24, 1.0 / 12, 1.0 / 6},
+                                   {1.0 / 24, -1.0 / 12, 1.0 / 6},
+                                   {0, 0, 1}};
+    const int nk = cin / 4;
+    std::vector<float> u((size_t)40 * cin * cout_pad, 0.0f);  // 36 used of 40 per (ci, co)
+    for (int ci = 0; ci < cin; ci++)
+        for (int co = 0; co < cout_pad; co++) {
+            double g[3][3], t[6][3];
+            for (int a = 0; a < 3; a++)
+                for (int c = 0; c < 3; c++) g[a][c] = w[((size_t)(3 * a + c) * cin + ci) * cout_pad + co];
+            for (int i = 0; i < 6; i++)
+                for (int c = 0; c < 3; c++) t[i][c] = G[i][0] * g[0][c] + G[i][1] * g[1][c] + G[i][2] * g[2][c];
+            const int kk = ci / 4, lk = ci % 4, nt = co / 64, cg = (co % 64) / 16, li = co % 16;
+            for (int i = 0; i < 6; i++)
+                for (int j = 0; j < 6; j++) {
+                    const int xh = i / 3, x = 6 * (i % 3) + j;
+                    const size_t o = (((((size_t)nt * nk + kk) * 4 + cg) * 2 + xh) * 64 + lk * 16 + li) * 20 + x;
+                    u[o] = (float)(t[i][0] * G[j][0] + t[i][1] * G[j][1] + t[i][2] * G[j][2]);
+                }
+        }
+    return u;
+}
+
 static int upload_layer(DevLayer& D, int cin, int cout, int cout_pad, int k, const std::vector<float>& w,
                         const std::vector<float>& b) {
     D.cin = cin;
@@ -185,6 +217,9 @@ static int upload_layer(DevLayer& D, int cin, int cout, int cout_pad, int k, con
         const std::vector<float> u = winograd_weights(w.data(), cin, cout_pad);
         VS_HIP(hipMalloc(&D.wu, u.size() * sizeof(float)));
         VS_HIP(hipMemcpy(D.wu, u.data(), u.size() * sizeof(float), hipMemcpyHostToDevice));
+        const std::vector<float> u4 = winograd4_weights(w.data(), cin, cout_pad);
+        VS_HIP(hipMalloc(&D.wu4, u4.size() * sizeof(float)));
+        VS_HIP(hipMemcpy(D.wu4, u4.data(), u4.size() * sizeof(float), hipMemcpyHostToDevice));
     }
     return VS_OK;
 }
@@ -394,11 +429,13 @@ void vs_destroy(vs_ctx* ctx) {
         if (L.w) (void)hipFree(L.w);
         if (L.b) (void)hipFree(L.b);
         if (L.wu) (void)hipFree(L.wu);
+        if (L.wu4) (void)hipFree(L.wu4);
         if (L.w1a_rows) (void)hipFree(L.w1a_rows);
     }
     if (ctx->head_a.w) (void)hipFree(ctx->head_a.w);
     if (ctx->head_a.b) (void)hipFree(ctx->head_a.b);
     if (ctx->head_a.wu) (void)hipFree(ctx->head_a.wu);
+    if (ctx->head_a.wu4) (void)hipFree(ctx->head_a.wu4);
     if (ctx->scratch_foreign) (void)hipEventDestroy(ctx->scratch_foreign);
     for (hipEvent_t e : ctx->ba_ev)
         if (e) (void)hipEventDestroy(e);

@@ -83,6 +83,9 @@ struct DevLayer {
     // 3x3 layers with cin % 4 == 0: the Winograd F(2x2, 3x3) transformed weights U = G g G^T,
     // [16][cin][cout_pad] (transform element xi = 4 i + j), computed in fp64 and rounded once
     float* wu = nullptr;
+    // the same layers' Winograd F(4x4, 3x3) weights U = G g G^T (round 5, wino4.hip; fp64, rounded once) in
+    // the order the kernel's lanes load their B operands (winograd4_weights)
+    float* wu4 = nullptr;
     // conv1a (cin 1, 3x3): per output channel its 9 taps, bias, 0, 0 ([cout][12]) — read by the fused
     // conv1 kernel as wave-uniform (scalar) loads
     float* w1a_rows = nullptr;
@@ -210,6 +213,10 @@ struct WinoArgs {
     int splits;
 };
 int wino3_launch(WinoArgs a, bool pool, bool fuse1a, hipStream_t s);
+// Winograd F(4x4, 3x3) (wino4.hip k_wino4): 16 x 16-pixel x 64-channel workgroups; bias + ReLU (+ 2 x 2 pool,
+// + fused conv1a); wa.wu = winograd4_weights images.  VS_ERR_ARG for geometry it does not cover.
+int wino4_launch(WinoArgs a, bool pool, bool fuse1a, hipStream_t s);
+std::vector<float> winograd4_weights(const float* w, int cin, int cout_pad);
 // U[xi][ci][pos(co)] from direct-layout 3x3 weights w[(3a + b)][ci][co] (cout_pad columns; pos
 // permutes each 32-column group for k_wino3's paired operand reads).  fp64, rounded once.
 std::vector<float> winograd_weights(const float* w, int cin, int cout_pad);

@@ -1,0 +1,394 @@
+// wino4.hip — Winograd F(4x4, 3x3) convolution on v_mfma_f32_16x16x4_f32 for SuperPoint's large
+// stride-1 3x3 layers (round 5; replaces ONNX Runtime's Conv inside Session::Run, reference
+// src/FeatureExtractor.cpp:116-124, topology SURVEY.md 8(a) A3).
+//
+// Each 4 x 4 output tile is  Y = A^T [ (G g G^T) (.) (B^T d B) ] A  over its 6 x 6 input window d
+// (points 0, +-1, +-2 and infinity; Lavin & Gray's matrices):
+//   B^T = [4 0 -5 0 1 0; 0 -4 -4 1 1 0; 0 4 -4 -1 1 0; 0 -2 -1 2 1 0; 0 2 -1 -2 1 0; 0 4 0 -5 0 1]
+//   A^T = [1 1 1 1 1 0; 0 1 -1 2 -2 0; 0 1 1 4 4 0; 0 1 -1 8 -8 1]
+// 36 products per tile, input channel and output channel instead of the direct form's 144 (the
+// F(2x2) kernel k_wino3 does 64 per four 2 x 2 tiles): 2.25 per output pixel against 4 (F(2x2)) and
+// 9 (direct).  Everything is fp32: G g G^T is computed in fp64 at weight upload and rounded once
+// (winograd4_weights, vs_ctx.hip), the input and output transforms are fp32 adds / fmas, and the 36
+// element-wise products are accumulated over the input channels by the matrix cores as 36
+// independent GEMMs  M[xi][tile][cout] = sum_c V[xi][tile][c] U[xi][c][cout].  Parity bar: the
+// network's fp32 tolerance against torch fp64 (tests/test_gpu_parity.py, stated there).
+//
+// Workgroup = 16 x 16 output pixels (4 x 4 tiles, an 18 x 18 input patch) x 64 output channels,
+// 8 waves.  Wave w owns output channels 16 (w & 3) .. + 15 of all 16 tiles for the transform
+// elements of domain rows 3 (w >> 2) .. + 2 (18 of the 36: eighteen 16 x 16 accumulators), so each
+// wave's partial output transform A^T M_rows A stays in registers and the two halves are added
+// once, through LDS, in the epilogue.  Per 4-channel k-step a wave issues 18 MFMAs; its operands
+// are one 6-float row of V and of U per domain row (3 ds_read_b64 each, conflict-free images).
+//
+// Per k-step k (one barrier), while the MFMAs of k run on buffers k & 1:
+//   * U of k + 1 (36 KB, prearranged on the host in the LDS image's order) goes global -> LDS by
+//     global_load_lds_dwordx4 (no VGPRs, no ds_write);
+//   * the patch of k + 1 (in LDS since step k - 1) is transformed into V of k + 1: thread
+//     (domain row i = its wave, channel, tile) forms row i of B^T d from four patch rows and
+//     applies the row transform (the row index is wave-uniform, so its coefficients are scalars);
+//   * the patch of k + 2 is written to LDS — from registers loaded one step earlier, or (FUSE1A,
+//     conv1) evaluated as conv1a (1 -> 64, 3 x 3, ReLU) from a 20 x 20 gray patch.
+// POOL: a 4 x 4 tile holds four whole 2 x 2 pool windows; bias, ReLU and the pool are applied to
+// the summed halves before the results go through LDS to float4 stores.
+#include <hip/hip_runtime.h>
+
+#include <cstdlib>
+#include <cstring>
+#include <type_traits>
+
+#include "vs_internal.h"
+
+namespace vs {
+
+namespace {
+
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int kW4Patch = 18;                 // 18 x 18 input patch
+constexpr int kW4NP = kW4Patch * kW4Patch;   // 324
+constexpr int kW4V = 8 * 4 * 16 * 6;         // V image per k-step: [row 8][ch 4][tile 16][col 6] (rows 6, 7: dummy)
+constexpr int kW4X = 4 * 512;                // patch per k-step: [ch 4][512 slots] (slots >= 324: dummy)
+constexpr int kW4G = 20 * 20;                // FUSE1A gray patch
+constexpr int kW4OffV = 0;
+constexpr int kW4OffX = kW4OffV + 2 * kW4V;
+constexpr int kW4OffG = kW4OffX + 2 * kW4X;
+constexpr int kW4Main = kW4OffG + kW4G;
+constexpr int kW4Epi = 16384;                // epilogue: the partial halves, then the output staging
+constexpr int kW4Lds = kW4Main > kW4Epi ? kW4Main : kW4Epi;
+static_assert(kW4Lds * 4 <= 64 * 1024, "LDS");
+constexpr int kW4B = 4 * 2 * 64 * 20;        // B operands per k-step: [cg 4][xh 2][lane 64][20 (18 used)]
+
+__device__ inline void w4_xcd_work(int ntiles, int& tile, int& nt) {
+    const int nblk = gridDim.x;
+    int w = blockIdx.x;
+    if ((nblk & 7) == 0) w = (w & 7) * (nblk >> 3) + (w >> 3);
+    tile = w / ntiles;
+    nt = w - tile * ntiles;
+}
+
+// row transform of a 6-vector by B (V[i][:] = T_i B): the factored F(4, 3) input transform
+__device__ inline void w4_rowB(const float t[6], float o[6]) {
+    const float a = t[1] + t[2], b = t[3] + t[4];
+    const float c = t[1] - t[2], e = t[4] - t[3];
+    const float f = t[3] - t[1], g = t[4] - t[2];
+    o[0] = __builtin_fmaf(4.0f, t[0], __builtin_fmaf(-5.0f, t[2], t[4]));
+    o[1] = __builtin_fmaf(-4.0f, a, b);
+    o[2] = __builtin_fmaf(4.0f, c, e);
+    o[3] = __builtin_fmaf(2.0f, f, g);
+    o[4] = __builtin_fmaf(-2.0f, f, g);
+    o[5] = __builtin_fmaf(4.0f, t[1], __builtin_fmaf(-5.0f, t[3], t[5]));
+}
+
+// R = m A (4 outputs from a 6-vector): the factored F(4, 3) output transform
+__device__ inline void w4_rowA(const float m[6], float r[4]) {
+    const float a = m[1] + m[2], b = m[1] - m[2], c = m[3] + m[4], e = m[3] - m[4];
+    r[0] = m[0] + a + c;
+    r[1] = __builtin_fmaf(2.0f, e, b);
+    r[2] = __builtin_fmaf(4.0f, c, a);
+    r[3] = __builtin_fmaf(8.0f, e, b) + m[5];
+}
+
+// one lane's B operands of a k-step: U[18 xh + x][ch][cout] for x = 0..17 (4 x 16 B + 8 B)
+struct W4B {
+    f32x4 q[4];
+    f32x2 r;
+    __device__ float operator[](int x) const { return x < 16 ? q[x >> 2][x & 3] : r[x - 16]; }
+};
+
+template <bool POOL, bool FUSE1A>
+__global__ __launch_bounds__(512, 1) void k_wino4(WinoArgs wa) {
+    const float* __restrict__ in = wa.in;
+    const float* __restrict__ bias = wa.bias;
+    float* __restrict__ out = wa.out;
+    const float* __restrict__ w1a = wa.w1a;  // FUSE1A: [64][9 taps, bias, 0, 0]
+    const int in_cstride = wa.in_cstride, in_coff = wa.in_coff, cin = wa.cin, cout = wa.cout;
+    const int out_cstride = wa.out_cstride, out_coff = wa.out_coff, H = wa.H, W = wa.W, nbx = wa.nbx, nby = wa.nby;
+    const int ntn = wa.cout_pad >> 6;
+    __shared__ __attribute__((aligned(16))) float lds[kW4Lds];
+
+    const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63, li = lane & 15, lk = lane >> 4;
+    const int cg = wv & 3, xh = wv >> 2;
+    int blk, nt;
+    w4_xcd_work(ntn, blk, nt);
+    const int b = blk / (nbx * nby), r0 = blk - b * (nbx * nby);
+    const int y0 = (r0 / nbx) * 16, x0 = (r0 % nbx) * 16;
+    const int nk = cin >> 2;
+    // this lane's B operands: [nt][k-step][cg][xh][lane][20]
+    const float* __restrict__ wb = wa.wu + ((size_t)nt * nk * 8 + cg * 2 + xh) * (64 * 20) + lane * 20;
+
+    // ---- patch role: slot p of the 18 x 18 patch, every thread (slots >= 324 are written, never read).
+    // Waves 6, 7, 0, 1, 2, 3 hold the 324 real pixels, so the patch work lands beside the transform work
+    // on the other waves of the SIMD pairs.
+    const int p = ((wv + 2) & 7) * 64 + lane;
+    const bool own_px = p < kW4NP;
+    const int ppy = p / kW4Patch, ppx = p - (p / kW4Patch) * kW4Patch;
+    const int gy = y0 - 1 + ppy, gx = x0 - 1 + ppx;
+    const bool pin = own_px && gy >= 0 && gy < H && gx >= 0 && gx < W;
+    const float* src = in + (((size_t)b * H + (pin ? gy : 0)) * W + (pin ? gx : 0)) * in_cstride + in_coff;
+    // +0 outside the image (conv padding) by a bit mask: a select between two stores became a branch
+    const uint32_t pmask = pin ? ~0u : 0u;
+    auto masked = [&](float v) { return __builtin_bit_cast(float, __builtin_bit_cast(uint32_t, v) & pmask); };
+    float gnb[FUSE1A ? 9 : 1];
+    if constexpr (FUSE1A) {
+        const float* g = in + (size_t)b * H * W;
+        for (int i = tid; i < kW4G; i += 512) {
+            const int yy = i / 20, xx = i - (i / 20) * 20;
+            const int sy = y0 - 2 + yy, sx = x0 - 2 + xx;
+            lds[kW4OffG + i] = (sy >= 0 && sy < H && sx >= 0 && sx < W) ? g[(size_t)sy * W + sx] : 0.0f;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < 9; k++) gnb[k] = own_px ? lds[kW4OffG + (ppy + k / 3) * 20 + ppx + k % 3] : 0.0f;
+    }
+    using GY_ = std::true_type;   // guarded: the k-step index may run past the last one (pipeline tail)
+    using GN_ = std::false_type;  // steady state: no guards, so no basic-block boundaries around the work
+    f32x4 rx = {0.f, 0.f, 0.f, 0.f};
+    auto fetch_x = [&](auto g_c, int c) {
+        if constexpr (!FUSE1A) {
+            // src is clamped into the image (pin == false: pixel 0 of the frame); put_x zeroes what lies outside
+            if (!decltype(g_c)::value || c < nk) rx = *reinterpret_cast<const f32x4*>(src + 4 * c);
+        }
+    };
+    // patch of k-step c -> lds[X slot]: [ch][slot]
+    auto put_x = [&](int slot, auto g_c, int c) {
+        if (decltype(g_c)::value && c >= nk) return;
+        float* xs = lds + kW4OffX + slot * kW4X + p;
+        if constexpr (FUSE1A) {
+            // the k-step's 4 x (9 taps + bias) are wave-uniform: scalar loads, v_fma_f32 with SGPR operands
+            const f32x4* wp = reinterpret_cast<const f32x4*>(w1a + (size_t)(4 * c) * 12);
+#pragma unroll
+            for (int cc = 0; cc < 4; cc++) {
+                const f32x4 q0 = wp[3 * cc], q1 = wp[3 * cc + 1], q2 = wp[3 * cc + 2];
+                const float wk[9] = {q0[0], q0[1], q0[2], q0[3], q1[0], q1[1], q1[2], q1[3], q2[0]};
+                float a = q2[1];
+#pragma unroll
+                for (int k = 0; k < 9; k++) a = __builtin_fmaf(gnb[k], wk[k], a);
+                xs[cc * 512] = masked(a > 0.0f ? a : 0.0f);
+            }
+        } else {
+#pragma unroll
+            for (int cc = 0; cc < 4; cc++) xs[cc * 512] = masked(rx[cc]);
+        }
+    };
+
+    // ---- transform role: thread (domain row i = its wave, channel tc, tile tt); waves 6 and 7 repeat
+    // rows 0 and 1 into dummy rows of the image, so that the code has no branch
+    const int ti = wv, tc = lane >> 4, tt = lane & 15, tty = tt >> 2, ttx = tt & 3;
+    // row i of B^T: four patch rows and their coefficients (wave-uniform)
+    int rr0 = 1, rr1 = 2, rr2 = 3, rr3 = 4;
+    float k0 = 0.f, k1 = 0.f, k2 = 0.f, k3 = 0.f;
+    switch (ti) {
+        case 0: case 6: rr0 = 0; rr1 = 2; rr2 = 4; rr3 = 4; k0 = 4.f; k1 = -5.f; k2 = 1.f; k3 = 0.f; break;
+        case 1: case 7: k0 = -4.f; k1 = -4.f; k2 = 1.f; k3 = 1.f; break;
+        case 2: k0 = 4.f; k1 = -4.f; k2 = -1.f; k3 = 1.f; break;
+        case 3: k0 = -2.f; k1 = -1.f; k2 = 2.f; k3 = 1.f; break;
+        case 4: k0 = 2.f; k1 = -1.f; k2 = -2.f; k3 = 1.f; break;
+        default: rr0 = 1; rr1 = 3; rr2 = 5; rr3 = 5; k0 = 4.f; k1 = -5.f; k2 = 1.f; k3 = 0.f; break;
+    }
+    const int xbase = tc * 512 + (4 * tty) * kW4Patch + 4 * ttx;
+    const int vbase = ((ti * 4 + tc) * 16 + tt) * 6;
+    auto transform = [&](int slot, auto g_c, int c) {
+        if (decltype(g_c)::value && c >= nk) return;
+        const float* xs = lds + kW4OffX + slot * kW4X + xbase;
+        float e[4][6];
+        const int rows[4] = {rr0, rr1, rr2, rr3};
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+#pragma unroll
+            for (int h = 0; h < 3; h++) {
+                const f32x2 v = *reinterpret_cast<const f32x2*>(xs + rows[r] * kW4Patch + 2 * h);
+                e[r][2 * h] = v[0];
+                e[r][2 * h + 1] = v[1];
+            }
+        }
+        float t[6], o[6];
+#pragma unroll
+        for (int j = 0; j < 6; j++)
+            t[j] = __builtin_fmaf(k3, e[3][j], __builtin_fmaf(k2, e[2][j], __builtin_fmaf(k1, e[1][j], k0 * e[0][j])));
+        w4_rowB(t, o);
+        float* vs = lds + kW4OffV + slot * kW4V + vbase;
+#pragma unroll
+        for (int h = 0; h < 3; h++) *reinterpret_cast<f32x2*>(vs + 2 * h) = f32x2{o[2 * h], o[2 * h + 1]};
+    };
+    // ---- B operands straight from L2 into registers, one k-step ahead (no LDS image, no barrier)
+    auto fetch_b = [&](W4B& bq, auto g_c, int c) {
+        if (decltype(g_c)::value && c >= nk) return;
+        const float* q = wb + (size_t)c * kW4B;
+#pragma unroll
+        for (int j = 0; j < 4; j++) bq.q[j] = *reinterpret_cast<const f32x4*>(q + 4 * j);
+        bq.r = *reinterpret_cast<const f32x2*>(q + 16);
+    };
+
+    f32x4 acc[18];
+#pragma unroll
+    for (int x = 0; x < 18; x++) acc[x] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    // prologue: patches 0, 1 in LDS, patch 2 and the B operands of step 0 in registers, V 0 transformed
+    W4B bA, bB;
+    fetch_b(bA, GY_{}, 0);
+    fetch_x(GY_{}, 0);
+    put_x(0, GY_{}, 0);
+    fetch_x(GY_{}, 1);
+    put_x(1, GY_{}, 1);
+    fetch_x(GY_{}, 2);
+    __syncthreads();
+    transform(0, GY_{}, 0);
+    __syncthreads();
+
+    // A operands: V[3 xh + rr][lk][li][0..5]
+    const int aoff = kW4OffV + (lk * 16 + li) * 6 + 3 * xh * (4 * 16 * 6);
+    // k-step k on buffers P = k & 1 with B operands bc, loading the next step's into bn
+    auto step = [&](auto par, auto g_c, int k, const W4B& bc, W4B& bn) {
+        constexpr int P = decltype(par)::value;
+        fetch_b(bn, g_c, k + 1);
+        const float* av = lds + aoff + P * kW4V;
+        f32x2 a2[3][3];
+#pragma unroll
+        for (int rr = 0; rr < 3; rr++)
+#pragma unroll
+            for (int h = 0; h < 3; h++) a2[rr][h] = *reinterpret_cast<const f32x2*>(av + rr * (4 * 16 * 6) + 2 * h);
+#pragma unroll
+        for (int rr = 0; rr < 3; rr++) {
+#pragma unroll
+            for (int j = 0; j < 6; j++)
+                acc[6 * rr + j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a2[rr][j >> 1][j & 1], bc[6 * rr + j],
+                                                                       acc[6 * rr + j], 0, 0, 0);
+            if (rr == 0) transform(P ^ 1, g_c, k + 1);
+            if (rr == 1) {
+                put_x(P, g_c, k + 2);
+                fetch_x(g_c, k + 3);
+            }
+        }
+        __syncthreads();  // V of k + 1 and the patch of k + 2 complete; the buffers of k free
+    };
+    using S0 = std::integral_constant<int, 0>;
+    using S1 = std::integral_constant<int, 1>;
+    int k = 0;
+    for (; k + 4 < nk; k += 2) {  // a pair touches k-steps up to k + 4
+        step(S0{}, GN_{}, k, bA, bB);
+        step(S1{}, GN_{}, k + 1, bB, bA);
+    }
+    for (; k < nk; k += 2) {
+        step(S0{}, GY_{}, k, bA, bB);
+        if (k + 1 < nk) step(S1{}, GY_{}, k + 1, bB, bA);
+    }
+
+    // ---- epilogue: partial output transforms, halves added through LDS
+    // acc[6 rr + j][r]: tile 4 lk + r, channel 16 cg + li, domain (3 xh + rr, j)
+    float y[4][16];  // [r][4 p + q]
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+        float R[3][4];
+#pragma unroll
+        for (int rr = 0; rr < 3; rr++) {
+            float m[6];
+#pragma unroll
+            for (int j = 0; j < 6; j++) m[j] = acc[6 * rr + j][r];
+            w4_rowA(m, R[rr]);
+        }
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            if (xh == 0) {  // rows 0, 1, 2: A^T columns (1,0,0,0), (1,1,1,1), (1,-1,1,-1)
+                const float s = R[1][q] + R[2][q], d = R[1][q] - R[2][q];
+                y[r][q] = R[0][q] + s;
+                y[r][4 + q] = d;
+                y[r][8 + q] = s;
+                y[r][12 + q] = d;
+            } else {        // rows 3, 4, 5: (1,2,4,8), (1,-2,4,-8), (0,0,0,1)
+                const float s = R[0][q] + R[1][q], d = R[0][q] - R[1][q];
+                y[r][q] = s;
+                y[r][4 + q] = 2.0f * d;
+                y[r][8 + q] = 4.0f * s;
+                y[r][12 + q] = __builtin_fmaf(8.0f, d, R[2][q]);
+            }
+        }
+    }
+    float* yp = lds;  // [cg][tile][16 px][16 ch]: the xh = 1 halves
+    float* so = lds;  // then [pixel][64 ch]: the outputs (after every half has been read)
+    if (xh == 1) {
+#pragma unroll
+        for (int r = 0; r < 4; r++)
+#pragma unroll
+            for (int e = 0; e < 16; e++) yp[((cg * 16 + 4 * lk + r) * 16 + e) * 16 + li] = y[r][e];
+    }
+    __syncthreads();
+    if (xh == 0) {
+#pragma unroll
+        for (int r = 0; r < 4; r++)
+#pragma unroll
+            for (int e = 0; e < 16; e++) y[r][e] += yp[((cg * 16 + 4 * lk + r) * 16 + e) * 16 + li];
+    }
+    __syncthreads();
+    if (xh == 0) {
+        const int n = 16 * cg + li;
+        const float bv = (nt * 64 + n < cout) ? bias[nt * 64 + n] : 0.0f;
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+            const int t = 4 * lk + r, ty = t >> 2, tx = t & 3;
+            if constexpr (POOL) {
+#pragma unroll
+                for (int pp = 0; pp < 2; pp++)
+#pragma unroll
+                    for (int qq = 0; qq < 2; qq++) {
+                        const int e0 = 8 * pp + 2 * qq;
+                        float m = fmaxf(fmaxf(y[r][e0], y[r][e0 + 1]), fmaxf(y[r][e0 + 4], y[r][e0 + 5])) + bv;
+                        m = m > 0.0f ? m : 0.0f;
+                        so[((2 * ty + pp) * 8 + 2 * tx + qq) * 64 + n] = m;
+                    }
+            } else {
+#pragma unroll
+                for (int e = 0; e < 16; e++) {
+                    float m = y[r][e] + bv;
+                    m = m > 0.0f ? m : 0.0f;
+                    so[((4 * ty + (e >> 2)) * 16 + 4 * tx + (e & 3)) * 64 + n] = m;
+                }
+            }
+        }
+    }
+    __syncthreads();
+    constexpr int NV = POOL ? 2 : 8;  // float4 per thread: 64 (POOL) or 256 pixels x 16
+#pragma unroll
+    for (int u = 0; u < NV; u++) {
+        const int e = tid + 512 * u, pix = e >> 4, q = e & 15;
+        const int n = nt * 64 + 4 * q;
+        if (n >= cout) continue;
+        const f32x4 v = *reinterpret_cast<const f32x4*>(&so[pix * 64 + 4 * q]);
+        if constexpr (POOL) {
+            const int oy = (y0 >> 1) + (pix >> 3), ox = (x0 >> 1) + (pix & 7);
+            if (oy >= (H >> 1) || ox >= (W >> 1)) continue;
+            *reinterpret_cast<f32x4*>(out + (((size_t)b * (H >> 1) + oy) * (W >> 1) + ox) * out_cstride + out_coff + n) = v;
+        } else {
+            const int oy = y0 + (pix >> 4), ox = x0 + (pix & 15);
+            if (oy >= H || ox >= W) continue;
+            *reinterpret_cast<f32x4*>(out + (((size_t)b * H + oy) * W + ox) * out_cstride + out_coff + n) = v;
+        }
+    }
+}
+
+}  // namespace
+
+// F(4x4, 3x3) launch: SuperPoint layers (bias + ReLU; POOL: 2 x 2 max-pool; FUSE1A: conv1a fused).
+// wa.wu = winograd4_weights(...) images; cin % 4 == 0, cout_pad % 64 == 0, cout % 4 == 0.
+int wino4_launch(WinoArgs a, bool pool, bool fuse1a, hipStream_t s) {
+    if (a.cin % 4 || a.cout_pad % 64 || a.cout % 4 || a.out_cstride % 4 || a.out_coff % 4 ||
+        (!fuse1a && (a.in_cstride % 4 || a.in_coff % 4)) || (pool && ((a.H | a.W) & 1)) ||
+        (fuse1a && (!a.w1a || a.cin != 64)) || a.res1 || a.res2 || a.splits > 1 || a.pre_relu || a.act != 1)
+        return VS_ERR_ARG;
+    a.nbx = (a.W + 15) / 16;
+    a.nby = (a.H + 15) / 16;
+    dim3 grid((unsigned)((long)a.B * a.nbx * a.nby * (a.cout_pad / 64)));
+    if (pool && fuse1a)
+        hipLaunchKernelGGL((k_wino4<true, true>), grid, dim3(512), 0, s, a);
+    else if (pool)
+        hipLaunchKernelGGL((k_wino4<true, false>), grid, dim3(512), 0, s, a);
+    else if (fuse1a)
+        hipLaunchKernelGGL((k_wino4<false, true>), grid, dim3(512), 0, s, a);
+    else
+        hipLaunchKernelGGL((k_wino4<false, false>), grid, dim3(512), 0, s, a);
+    VS_HIP(hipGetLastError());
+    return VS_OK;
+}
+
+}  // namespace vs
