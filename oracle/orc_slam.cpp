@@ -32,8 +32,52 @@ struct StageTimer {
     ~StageTimer() { *acc += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count(); }
 };
 
+// Op log (VS_OPLOG=path; test infrastructure): one JSON line per back-end call of the tracker with the
+// inputs the glue chose and the kernel outputs it got, doubles as C99 hex floats (exact), tagged with the
+// frame being processed.  tests/slam_glue_ref.py replays Slam::process_frame (Slam.cpp:809-1135) on these
+// kernel outputs, restated from the reference alone, and checks the glue's decisions and poses.
+struct OpLog {
+    FILE* fp = nullptr;
+    int cur = -1;  // id of the frame being processed
+    explicit operator bool() const { return fp != nullptr; }
+    void begin(const char* op) { std::fprintf(fp, "{\"f\":%d,\"op\":\"%s\"", cur, op); }
+    void end() { std::fputs("}\n", fp); }
+    void i(const char* k, long v) { std::fprintf(fp, ",\"%s\":%ld", k, v); }
+    void d(const char* k, double v) { std::fprintf(fp, ",\"%s\":\"%a\"", k, v); }
+    template <class T> void dv(const char* k, const T* v, size_t n) {
+        std::fprintf(fp, ",\"%s\":[", k);
+        for (size_t j = 0; j < n; j++) std::fprintf(fp, "%s\"%a\"", j ? "," : "", (double)v[j]);
+        std::fputc(']', fp);
+    }
+    void iv(const char* k, const int* v, size_t n) {
+        std::fprintf(fp, ",\"%s\":[", k);
+        for (size_t j = 0; j < n; j++) std::fprintf(fp, "%s%d", j ? "," : "", v[j]);
+        std::fputc(']', fp);
+    }
+    void matches(const char* k, const std::vector<Match>& m) {
+        std::fprintf(fp, ",\"%s\":[", k);
+        for (size_t j = 0; j < m.size(); j++) std::fprintf(fp, "%s[%d,%d]", j ? "," : "", m[j].query_idx, m[j].train_idx);
+        std::fputc(']', fp);
+    }
+    void pairs(const char* k, const std::vector<std::pair<int, int>>& m) {
+        std::fprintf(fp, ",\"%s\":[", k);
+        for (size_t j = 0; j < m.size(); j++) std::fprintf(fp, "%s[%d,%d]", j ? "," : "", m[j].first, m[j].second);
+        std::fputc(']', fp);
+    }
+    void motion(const vs_trk::ChainResult& R) {
+        i("ok3d", R.ok3d);
+        dv("R3", R.R3.data(), 9);
+        dv("t3", R.t3.data(), 3);
+        i("okE", R.okE);
+        dv("RE", R.RE.data(), 9);
+        dv("tE", R.tE.data(), 3);
+        d("scale", R.scale);
+    }
+};
+
 struct OracleOps {
     double sec[kNStage] = {};
+    OpLog log;
     double K[4] = {vs_trk::cfg::FX, vs_trk::cfg::FY, vs_trk::cfg::CX, vs_trk::cfg::CY};
     int h = vs_trk::cfg::IMAGE_HEIGHT, w = vs_trk::cfg::IMAGE_WIDTH;
     std::vector<float> map_desc;  // M x 256
@@ -53,18 +97,32 @@ struct OracleOps {
         orc_match_ratio(a.desc.data(), n1, b.desc.data(), n2, ratio, reinterpret_cast<orc_match*>(raw.data()), &nr,
                         reinterpret_cast<orc_match*>(good.data()), &ng);
         good.resize(ng);
+        if (log && !in_dlt) {
+            log.begin("match");
+            log.i("a", a.id), log.i("b", b.id), log.d("ratio", ratio), log.matches("good", good), log.end();
+        }
         return good;
     }
+    bool in_dlt = false;
 
     // match() and the DLT of every good match (the tracker triangulates from them)
     std::vector<Match> match_dlt(const Frame& a, const Frame& b, float ratio, const double P1[12], const double P2[12],
                                  std::vector<std::array<float, 4>>& X4) {
+        in_dlt = true;
         std::vector<Match> m = match(a, b, ratio);
+        in_dlt = false;
         X4.resize(m.size());
         for (size_t i = 0; i < m.size(); i++) {
             const auto& ka = a.kps[m[i].query_idx];
             const auto& kb = b.kps[m[i].train_idx];
             vs_pnp::dlt_point(P1, P2, ka.x, ka.y, kb.x, kb.y, X4[i].data());
+        }
+        if (log) {
+            log.begin("match_dlt");
+            log.i("a", a.id), log.i("b", b.id), log.d("ratio", ratio), log.matches("good", m);
+            log.dv("P1", P1, 12), log.dv("P2", P2, 12);
+            log.dv("X4", X4.empty() ? (const float*)nullptr : X4[0].data(), 4 * X4.size());
+            log.end();
         }
         return m;
     }
@@ -99,7 +157,9 @@ struct OracleOps {
 
     vs_trk::ChainResult chain(const Frame& ref, const Frame& cur, uint32_t seed) {
         vs_trk::ChainResult R;
+        in_dlt = true;  // the chain's own match is logged with the chain
         R.good = match(ref, cur, vs_trk::cfg::L2_RATIO_THRESHOLD);
+        in_dlt = false;
         const int n = (int)R.good.size();
         double F[9], err[2];
         int diag[4], f_ok = 0;
@@ -119,6 +179,11 @@ struct OracleOps {
         std::vector<float> p1, p2;
         points(ref, cur, R.kept, p1, p2);
         motion(ref, cur, p1, p2, seed, R);
+        if (log) {
+            log.begin("chain");
+            log.i("a", ref.id), log.i("b", cur.id), log.i("seed", seed), log.matches("good", R.good);
+            log.i("f_ok", R.f_ok), log.matches("kept", R.kept), log.motion(R), log.end();
+        }
         return R;
     }
 
@@ -128,13 +193,25 @@ struct OracleOps {
         mask.assign(std::max(n, 1), 0);
         double F[9];
         int diag[4];
-        return orc_find_fundamental(p1.data(), p2.data(), n, 3.0, 0.999, 1000, F, mask.data(), diag) != 0;
+        const bool ok = orc_find_fundamental(p1.data(), p2.data(), n, 3.0, 0.999, 1000, F, mask.data(), diag) != 0;
+        if (log) {
+            std::vector<int> mk(mask.begin(), mask.begin() + n);
+            log.begin("ffund");
+            log.i("n", n), log.dv("p1", p1.data(), p1.size()), log.dv("p2", p2.data(), p2.size()), log.i("ok", ok);
+            log.iv("mask", mk.data(), mk.size()), log.end();
+        }
+        return ok;
     }
 
     vs_trk::ChainResult motion_points(const Frame& ref, const Frame& cur, const std::vector<float>& p1,
                                       const std::vector<float>& p2, uint32_t seed) {
         vs_trk::ChainResult R;
         motion(ref, cur, p1, p2, seed, R);
+        if (log) {
+            log.begin("motion");
+            log.i("a", ref.id), log.i("b", cur.id), log.i("seed", seed), log.dv("p1", p1.data(), p1.size());
+            log.dv("p2", p2.data(), p2.size()), log.motion(R), log.end();
+        }
         return R;
     }
 
@@ -151,6 +228,14 @@ struct OracleOps {
                                                 &n_obs);
         obs.clear();
         for (int i = 0; i < std::min(n_obs, cap); i++) obs.emplace_back(om[i], ok[i]);
+        if (log) {
+            int nvalid = 0;
+            for (uint8_t v : m.valid) nvalid += v;
+            log.begin("tlm");
+            log.i("fid", f.id), log.dv("R", f.R.data(), 9), log.dv("t", f.t.data(), 3), log.i("nmp", nmp);
+            log.i("nvalid", nvalid), log.i("tracked", tracked), log.iv("mp_idx", f.mp_idx.data(), f.mp_idx.size());
+            log.pairs("obs", obs), log.end();
+        }
         return tracked;
     }
 
@@ -161,6 +246,13 @@ struct OracleOps {
         r.success = orc_solve_pnp(obj.data(), img.data(), (int)(obj.size() / 3), K, iters, min_inliers,
                                   r.R_world.data(), r.t_world.data(), &inl) != 0;
         r.inlier_count = r.success ? inl : 0;
+        if (log) {
+            log.begin("pnp");
+            log.i("n", (long)(obj.size() / 3)), log.i("iters", iters), log.i("min_inl", min_inliers);
+            log.dv("obj", obj.data(), obj.size()), log.dv("img", img.data(), img.size());
+            log.i("ok", r.success), log.dv("R", r.R_world.data(), 9), log.dv("t", r.t_world.data(), 3);
+            log.i("inl", r.inlier_count), log.end();
+        }
         return r;
     }
 
@@ -181,6 +273,13 @@ struct OracleOps {
             int inl = 0, g = 0;
             orc_estimate_motion(p1.data(), p2.data(), n, K, R, t, mask.data(), &inl, &g);
             out[i].inliers = inl;
+        }
+        if (log) {
+            std::vector<int> ids, ng, ni;
+            for (size_t i = 0; i < kfs.size(); i++) ids.push_back(kfs[i]->id), ng.push_back(out[i].n_good), ni.push_back(out[i].inliers);
+            log.begin("loop_eval");
+            log.i("cur", cur.id), log.iv("kfs", ids.data(), ids.size()), log.iv("n_good", ng.data(), ng.size());
+            log.iv("inliers", ni.data(), ni.size()), log.end();
         }
         return out;
     }
@@ -233,6 +332,11 @@ struct OracleOps {
         orc_match_ratio(f.desc.data(), n1, t.data(), n2, ratio, reinterpret_cast<orc_match*>(raw.data()), &nr,
                         reinterpret_cast<orc_match*>(good.data()), &ng);
         for (int i = 0; i < ng; i++) out.emplace_back(good[i].query_idx, good[i].train_idx);
+        if (log) {
+            log.begin("match_map");
+            log.i("fid", f.id), log.iv("ids", ids.data(), ids.size()), log.d("ratio", ratio), log.pairs("pairs", out);
+            log.end();
+        }
         return out;
     }
 
@@ -240,6 +344,10 @@ struct OracleOps {
         map_desc.resize((size_t)(first + rows.size()) * 256);
         for (size_t i = 0; i < rows.size(); i++)
             std::memcpy(&map_desc[(size_t)(first + i) * 256], &src.desc[(size_t)rows[i] * 256], 256 * sizeof(float));
+        if (log) {
+            log.begin("map_append");
+            log.i("first", first), log.i("src", src.id), log.iv("rows", rows.data(), rows.size()), log.end();
+        }
     }
 
     void map_valid_changed() {}
@@ -264,6 +372,12 @@ struct OracleOps {
                 }
             }
         }
+        if (log) {
+            std::vector<int> fl(flags.begin(), flags.end());
+            log.begin("vis");
+            log.i("fid", f.id), log.dv("R", R.data(), 9), log.dv("t", t.data(), 3), log.iv("flags", fl.data(), fl.size());
+            log.end();
+        }
     }
 };
 
@@ -275,9 +389,11 @@ struct OrcSlam {
     OrcSlam() {
         if (const char* p = std::getenv("VS_TRACE_ORACLE")) trace = std::fopen(p, "w");
         trk.set_trace(trace);
+        if (const char* p = std::getenv("VS_OPLOG")) ops.log.fp = std::fopen(p, "w");
     }
     ~OrcSlam() {
         if (trace) std::fclose(trace);
+        if (ops.log.fp) std::fclose(ops.log.fp);
     }
 };
 
@@ -318,7 +434,18 @@ int orc_slam_process(void* h, int n_kp, const orc_keypoint* kps, const float* de
     f->desc.assign(desc, desc + (size_t)n_kp * 256);
     f->mp_idx.assign(n_kp, -1);
     f->depth = depth;
+    s->ops.log.cur = id;
     const int r = s->trk.process_frame(f) ? 1 : 0;
+    if (OpLog& L = s->ops.log) {  // the glue's outcome for this frame (compared by tests/slam_glue_ref.py)
+        const auto& m = s->trk.map();
+        int nvalid = 0;
+        for (uint8_t v : m.valid) nvalid += v;
+        L.begin("frame_end");
+        L.i("ret", r), L.i("kf", f->keyframe), L.dv("R", f->R.data(), 9), L.dv("t", f->t.data(), 3);
+        L.i("nmp", m.size()), L.i("nvalid", nvalid), L.i("frame_count", s->trk.frame_count());
+        L.i("kf_count", s->trk.keyframe_count()), L.i("match_count", s->trk.last_match_count()), L.end();
+        std::fflush(L.fp);
+    }
     s->holding.push_back(f);
     std::vector<vs_trk::FramePtr> keep;
     for (auto& g : s->holding) {

@@ -1,0 +1,674 @@
+"""Independent restatement of the tracking loop's glue (test infrastructure only).
+
+`GlueRef` is `Slam::process_frame` (reference src/Slam.cpp:809-1135) and the helpers it calls
+(try_pnp_recovery :535-613, setup_new_keyframe :699-725, cull_map_points :473-500, triangulate_points
+:1246-1356, is_keyframe :1359-1368, refine_pose_via_local_pnp :1373-1473, run_pnp :1477-1522,
+create_points_from_depth :1526-1577, the EKF :1654-1744, Optimizer::project_point Optimizer.cpp:26-48)
+with the constants of include/Config.h, written in numpy from the reference alone: it shares no source
+with the product's glue (visual-slam-pipeline_amd/host/tracker.hpp) nor with the oracle.
+
+It does not run kernels.  It replays the op log of the oracle tracker (VS_OPLOG, oracle/orc_slam.cpp:
+one record per back-end call with the inputs the C++ glue chose and the kernel outputs it got) and, for
+every frame, takes the kernel outputs it needs by key — the front chain of (reference, current), the
+bridge matches, the DLT points of a keyframe pair, local-map tracking, every PnP — after checking the
+inputs the C++ glue passed against its own state: the reference frame, the 3D-3D seed (42 + frame
+count, Slam.cpp:276), the pose handed to local-map tracking, the projection matrices of a
+triangulation, the 3D-2D correspondences of every PnP (the map positions, float32 as the reference
+casts them), the map rows appended.  After each frame it compares the glue's outcome (return value,
+keyframe flag, pose, map size and valid points, frame / keyframe counts, match count) with its own.
+
+Deviation kept by both: after a rejected first frame `last_keyframe_` is null and the
+reference would dereference it at Slam.cpp:1063; the proactive-keyframe check is skipped then.
+Not restated (raise if reached): the accelerometer paths (stationary frames, height prior) and loop
+closure (every 200th keyframe) — the replayed sequences have neither.
+"""
+import json
+
+import numpy as np
+
+# ---- include/Config.h -------------------------------------------------------------------------
+IMAGE_WIDTH, IMAGE_HEIGHT = 640, 480
+FX, FY, CX, CY = 525.0, 525.0, 319.5, 239.5
+DEPTH_MIN = float(np.float32(0.1))  # constexpr float 0.1f, promoted where compared with doubles
+MIN_MATCHES = 30
+TRIANG_MAX_REPROJ_ERROR, TRIANG_MIN_DEPTH, TRIANG_MAX_DEPTH, TRIANG_MAX_CAM_DIST = 3.0, 0.05, 50.0, 5.0
+PNP_INTERVAL, PNP_MIN_POINTS = 5, 10
+PNP_RECOVERY_MAX_JUMP, PNP_RECOVERY_BLEND_CLOSE, PNP_RECOVERY_BLEND_FAR = 1.5, 0.8, 0.3
+PNP_REFINE_MAX_JUMP, PNP_PERIODIC_MAX_JUMP, PNP_PERIODIC_BLEND = 1.0, 1.5, 0.5
+KF_MIN_FRAME_GAP, KF_MIN_MATCHES = 10, 50
+LC_CHECK_INTERVAL = 200
+L2_RATIO_THRESHOLD, FLANN_RATIO_THRESHOLD = 0.75, 0.7
+TRACK_VISIBILITY_RADIUS = 8.0
+CULL_FOUND_RATIO_YOUNG, CULL_FOUND_RATIO_OLD = np.float32(0.15), np.float32(0.30)
+MOTION_SCALE = 0.05
+EKF_SIGMA_VIS_3D3D, EKF_SIGMA_VIS_EMAT = 0.04, 0.10
+EKF_PROCESS_ACCEL, EKF_VEL_DECAY, EKF_INNOV_GATE, EKF_MAX_STEP = 1.0, 0.95, 0.3, 0.10
+K = np.array([[FX, 0, CX], [0, FY, CY], [0, 0, 1.0]])
+
+
+class GlueMismatch(AssertionError):
+    pass
+
+
+def _hex(v):
+    return np.array([float.fromhex(x) for x in v], dtype=np.float64)
+
+
+def cv_round(x):
+    """std::round (half away from zero) of a float coordinate."""
+    x = float(x)
+    return int(np.floor(x + 0.5)) if x >= 0 else -int(np.floor(-x + 0.5))
+
+
+def project_point(pw, R, t):
+    """Optimizer::project_point (Optimizer.cpp:26-48): camera-to-world pose (R, t); (-1, -1) behind."""
+    Rc = R.T
+    tc = -Rc @ t
+    pc = Rc @ pw + tc
+    z = pc[2]
+    if z < 1e-6:
+        return -1.0, -1.0
+    return FX * pc[0] / z + CX, FY * pc[1] / z + CY
+
+
+def rodrigues_vec(R):
+    """cv::Rodrigues, matrix -> rotation vector (orthonormalised first, as OpenCV does by SVD)."""
+    U, _, Vt = np.linalg.svd(R)
+    R = U @ Vt
+    rx, ry, rz = R[2, 1] - R[1, 2], R[0, 2] - R[2, 0], R[1, 0] - R[0, 1]
+    s = np.sqrt((rx * rx + ry * ry + rz * rz) * 0.25)
+    c = min(max((R[0, 0] + R[1, 1] + R[2, 2] - 1) * 0.5, -1.0), 1.0)
+    theta = np.arccos(c)
+    if s < 1e-5:
+        if c > 0:
+            return np.zeros(3)
+        t = (np.diag(R) + 1) * 0.5
+        r = np.sqrt(np.maximum(t, 0)) * theta
+        if R[0, 1] < 0:
+            r[1] = -r[1]
+        if R[0, 2] < 0:
+            r[2] = -r[2]
+        if abs(r[0]) < abs(r[1]) and abs(r[0]) < abs(r[2]) and (R[1, 2] > 0) != (r[1] * r[2] > 0):
+            r[2] = -r[2]
+        return r
+    return np.array([rx, ry, rz]) * (theta / (2 * s))
+
+
+def rodrigues_mat(r):
+    """cv::Rodrigues, rotation vector -> matrix."""
+    theta = float(np.linalg.norm(r))
+    if theta < np.finfo(np.float64).eps:
+        return np.eye(3)
+    c, s = np.cos(theta), np.sin(theta)
+    u = r / theta
+    rx = np.array([[0, -u[2], u[1]], [u[2], 0, -u[0]], [-u[1], u[0], 0]])
+    return c * np.eye(3) + (1 - c) * np.outer(u, u) + s * rx
+
+
+class Frame:
+    def __init__(self, fid, ts, kps, depth):
+        self.id = fid
+        self.ts = ts
+        self.kx = np.asarray(kps["x"], np.float32)
+        self.ky = np.asarray(kps["y"], np.float32)
+        self.n = len(self.kx)
+        self.depth = depth  # float32 [480, 640] metres or None
+        self.R = np.eye(3)
+        self.t = np.zeros(3)
+        self.kf = False
+        self.mp_idx = np.full(self.n, -1, np.int64)
+
+    def has_depth(self):
+        return self.depth is not None
+
+
+class OpLog:
+    """The oracle tracker's op log, grouped by the frame being processed."""
+
+    def __init__(self, path):
+        self.by_frame = {}
+        for ln in open(path):
+            r = json.loads(ln)
+            self.by_frame.setdefault(r["f"], []).append(r)
+
+    def frame(self, fid):
+        return FrameOps(self.by_frame.get(fid, []), fid)
+
+
+class FrameOps:
+    def __init__(self, recs, fid):
+        self.recs = recs
+        self.used = [False] * len(recs)
+        self.fid = fid
+
+    def take(self, ops, optional=False, **key):
+        ops = (ops,) if isinstance(ops, str) else ops
+        for i, r in enumerate(self.recs):
+            if self.used[i] or r["op"] not in ops:
+                continue
+            if all(r.get(k) == v for k, v in key.items()):
+                self.used[i] = True
+                return r
+        if optional:
+            return None
+        raise GlueMismatch(f"frame {self.fid}: the C++ glue made no {ops} call with {key}; "
+                           f"calls: {[(r['op'], {k: r.get(k) for k in ('a', 'b', 'n', 'iters')}) for r in self.recs]}")
+
+    def unused(self):
+        return [r["op"] for r, u in zip(self.recs, self.used) if not u]
+
+
+class GlueRef:
+    def __init__(self, oplog):
+        self.log = OpLog(oplog) if isinstance(oplog, str) else oplog
+        self.R_world = np.eye(3)
+        self.t_world = np.zeros(3)
+        self.frames = []           # Map::add_frame order
+        self.last_frame = None
+        self.last_keyframe = None
+        self.frame_count = 0
+        self.keyframe_count = 0
+        self.last_match_count = 0
+        self.last_good_scale = -1.0
+        self.pnp_recovery_cooldown = 0
+        self.ekf_init = False
+        self.ekf_x = np.zeros(6)
+        self.ekf_P = np.zeros((6, 6))
+        self.last_frame_time = 0.0
+        self.last_translation = np.zeros(3)
+        # map points
+        self.mp_pos, self.mp_valid, self.mp_first_kf, self.mp_obs = [], [], [], []
+        self.mp_visible, self.mp_found = [], []
+        self.appended = []         # (source frame id, keypoint row) of every new map point, in order
+        self.branch = {}           # frame id -> "3d3d" / "emat" / "emat_failed" / "recovery" / ...
+        self.counts = dict(bridges=0, via_3d3d=0, via_emat=0, emat_failed=0, recoveries=0, recovery_failed=0,
+                           pnp_refined=0, periodic_pnp=0, triangulated=0, depth_points=0, ekf_gated=0,
+                           ekf_clamped=0, proactive_kf=0, regular_kf=0, culled=0, cull_rounds=0)
+        self.ops = None
+
+    # ---- map ---------------------------------------------------------------------------------
+    def _add_point(self, pt, src, row, obs):
+        i = len(self.mp_pos)
+        self.mp_pos.append(np.asarray(pt, np.float64))
+        self.mp_valid.append(True)
+        self.mp_first_kf.append(self.keyframe_count)
+        self.mp_obs.append(list(obs))
+        self.mp_visible.append(0)
+        self.mp_found.append(0)
+        self.appended.append((src.id, row))
+        return i
+
+    def _n_valid(self):
+        return int(sum(self.mp_valid))
+
+    # ---- Slam.cpp:1526-1577 --------------------------------------------------------------------
+    def create_points_from_depth(self, f):
+        if not f.has_depth():
+            return
+        R, t = f.R, f.t
+        for i in range(f.n):
+            if f.mp_idx[i] >= 0:
+                continue
+            u, v = f.kx[i], f.ky[i]
+            px, py = cv_round(u), cv_round(v)
+            if px < 0 or px >= IMAGE_WIDTH or py < 0 or py >= IMAGE_HEIGHT:
+                continue
+            z = f.depth[py, px]
+            if z <= np.float32(0.1) or float(z) > TRIANG_MAX_CAM_DIST:
+                continue
+            zd = float(z)
+            p_cam = np.array([(float(u) - CX) * zd / FX, (float(v) - CY) * zd / FY, zd])
+            p_world = R @ p_cam + t
+            f.mp_idx[i] = self._add_point(p_world, f, i, [(f.id, i)])
+            self.counts["depth_points"] += 1
+
+    # ---- Slam.cpp:1246-1356 (cv::triangulatePoints' 4-vectors from the op log: float32) ---------
+    def triangulate_points(self, f1, f2, matches, rec):
+        R1c, R2c = f1.R.T, f2.R.T
+        t1c, t2c = -R1c @ f1.t, -R2c @ f2.t
+        P1 = K @ np.hstack([R1c, t1c[:, None]])
+        P2 = K @ np.hstack([R2c, t2c[:, None]])
+        for mine, theirs in ((P1, rec["P1"]), (P2, rec["P2"])):
+            if not np.allclose(mine.ravel(), _hex(theirs), rtol=0, atol=1e-9 * max(1.0, np.abs(mine).max())):
+                raise GlueMismatch(f"frame {self.ops.fid}: triangulation projection matrices differ")
+        if len(matches) < 5:
+            return
+        X4 = np.array([float.fromhex(x) for x in rec["X4"]], np.float64).astype(np.float32).reshape(-1, 4)
+        use_real_depth = f2.has_depth()
+        for i, (q, tr) in enumerate(matches):
+            w = X4[i, 3]
+            if abs(w) < 1e-6:
+                continue
+            pt = np.array([X4[i, 0] / w, X4[i, 1] / w, X4[i, 2] / w], np.float32).astype(np.float64)
+            x2, y2 = f2.kx[tr], f2.ky[tr]
+            if use_real_depth:
+                px, py = cv_round(x2), cv_round(y2)
+                if 0 <= px < IMAGE_WIDTH and 0 <= py < IMAGE_HEIGHT:
+                    zr = f2.depth[py, px]
+                    if zr > np.float32(0.1) and float(zr) < 10.0:
+                        zd = float(zr)
+                        p_cam = np.array([(float(x2) - CX) * zd / FX, (float(y2) - CY) * zd / FY, zd])
+                        pt = f2.R @ p_cam + f2.t
+            z1 = (R1c @ pt + t1c)[2]
+            z2 = (R2c @ pt + t2c)[2]
+            if z1 < TRIANG_MIN_DEPTH or z1 > TRIANG_MAX_DEPTH or z2 < TRIANG_MIN_DEPTH or z2 > TRIANG_MAX_DEPTH:
+                continue
+            u2, v2 = project_point(pt, f2.R, f2.t)
+            if np.sqrt((u2 - float(x2)) ** 2 + (v2 - float(y2)) ** 2) > TRIANG_MAX_REPROJ_ERROR:
+                continue
+            u1, v1 = project_point(pt, f1.R, f1.t)
+            if np.sqrt((u1 - float(f1.kx[q])) ** 2 + (v1 - float(f1.ky[q])) ** 2) > TRIANG_MAX_REPROJ_ERROR:
+                continue
+            if np.linalg.norm(pt - f2.t) > TRIANG_MAX_CAM_DIST:
+                continue
+            nid = self._add_point(pt, f2, tr, [(f1.id, q), (f2.id, tr)])
+            f1.mp_idx[q] = nid
+            f2.mp_idx[tr] = nid
+            self.counts["triangulated"] += 1
+
+    # ---- Slam.cpp:473-500 --------------------------------------------------------------------
+    def cull_map_points(self, f):
+        before = self._n_valid()
+        self._cull_map_points(f)
+        self.counts["culled"] += before - self._n_valid()
+
+    def _cull_map_points(self, f):
+        Rc = f.R.T
+        tc = -Rc @ f.t
+        for i in range(f.n):
+            mp = f.mp_idx[i]
+            if 0 <= mp < len(self.mp_pos) and self.mp_valid[mp]:
+                pc = Rc @ self.mp_pos[mp] + tc
+                z = pc[2]
+                if z < DEPTH_MIN:
+                    self.mp_valid[mp] = False
+                    continue
+                u = FX * pc[0] / z + CX
+                v = FY * pc[1] / z + CY
+                dx, dy = u - float(f.kx[i]), v - float(f.ky[i])
+                if dx * dx + dy * dy > 400.0:
+                    self.mp_valid[mp] = False
+
+    # ---- Slam.cpp:699-725 (ENABLE_LOCAL_BA is false) ---------------------------------------------
+    def setup_new_keyframe(self, f):
+        if self.last_keyframe is not None:
+            rec = self.ops.take(("match_dlt",), a=self.last_keyframe.id, b=f.id)
+            m = rec["good"]
+            if len(m) >= MIN_MATCHES:
+                self.triangulate_points(self.last_keyframe, f, m, rec)
+        self.create_points_from_depth(f)
+        self.cull_map_points(f)
+
+    # ---- Slam.cpp:505-529 --------------------------------------------------------------------
+    def _correspondences(self, f):
+        obj, img = [], []
+        for i in range(f.n):
+            mp = f.mp_idx[i]
+            if 0 <= mp < len(self.mp_pos) and self.mp_valid[mp]:
+                obj.append(self.mp_pos[mp].astype(np.float32))
+                img.append((f.kx[i], f.ky[i]))
+        return (np.array(obj, np.float32).reshape(-1, 3), np.array(img, np.float32).reshape(-1, 2))
+
+    def solve_pnp(self, obj, img, iters, min_inliers):
+        if len(obj) < min_inliers:  # returns before cv::solvePnPRansac
+            rec = self.ops.take("pnp", optional=True, n=len(obj), iters=iters, min_inl=min_inliers)
+            return None
+        rec = self.ops.take("pnp", n=len(obj), iters=iters, min_inl=min_inliers)
+        # the map positions as float32 (the reference's cv::Point3f): equal up to a one-ulp flip of the
+        # float rounding, which a last-bit difference of the fp64 map position may cause
+        if not (len(rec["obj"]) == obj.size and np.allclose(_hex(rec["obj"]), obj.ravel(), rtol=1e-6, atol=1e-6)
+                and np.array_equal(_hex(rec["img"]).astype(np.float32), img.ravel())):
+            raise GlueMismatch(f"frame {self.ops.fid}: PnP correspondences differ (map positions / keypoints)")
+        if not rec["ok"]:
+            return None
+        return _hex(rec["R"]).reshape(3, 3), _hex(rec["t"]), rec["inl"]
+
+    # ---- Slam.cpp:535-613 --------------------------------------------------------------------
+    def try_pnp_recovery(self, f):
+        if self.pnp_recovery_cooldown > 0:
+            self.pnp_recovery_cooldown -= 1
+        if self.last_match_count >= MIN_MATCHES:
+            return 0
+        if self.pnp_recovery_cooldown > 0:
+            self.last_frame = f
+            return -1
+        ids = [i for i in range(len(self.mp_pos)) if self.mp_valid[i]]
+        if len(ids) >= 50 and f.n > 0:
+            rec = self.ops.take("match_map", fid=f.id)
+            if rec["ids"] != ids or float.fromhex(rec["ratio"]) != np.float32(FLANN_RATIO_THRESHOLD):
+                raise GlueMismatch(f"frame {f.id}: recovery matched against other map points")
+            obj = np.array([self.mp_pos[ids[t]] for _, t in rec["pairs"]], np.float64).astype(np.float32).reshape(-1, 3)
+            img = np.array([(f.kx[q], f.ky[q]) for q, _ in rec["pairs"]], np.float32).reshape(-1, 2)
+            if len(obj) >= 20:
+                r = self.solve_pnp(obj, img, 300, 15)
+                if r is not None:
+                    R_p, t_p, _ = r
+                    jump = np.linalg.norm(t_p - self.t_world)
+                    if jump < PNP_RECOVERY_MAX_JUMP:
+                        blend = PNP_RECOVERY_BLEND_CLOSE if jump < 0.1 else PNP_RECOVERY_BLEND_FAR
+                        self.R_world = R_p.copy()
+                        self.t_world = (1.0 - blend) * self.t_world + blend * t_p
+                        f.R, f.t = self.R_world.copy(), self.t_world.copy()
+                        self.frames.append(f)
+                        f.kf = True
+                        self.keyframe_count += 1
+                        self.create_points_from_depth(f)
+                        self.last_keyframe = f
+                        self.last_frame = f
+                        self.frame_count += 1
+                        if self.ekf_init:
+                            self.ekf_x[:3] = self.t_world
+                            self.ekf_x[3:] = 0
+                        self.last_frame_time = f.ts
+                        self.pnp_recovery_cooldown = 10
+                        self.counts["recoveries"] += 1
+                        return 1
+        self.last_frame = f
+        self.counts["recovery_failed"] += 1
+        return -1
+
+    # ---- Slam.cpp:1654-1744 ------------------------------------------------------------------
+    def ekf_initialize(self, pos, ts):
+        self.ekf_x = np.zeros(6)
+        self.ekf_x[:3] = pos
+        self.ekf_P = np.diag([0.001] * 3 + [0.01] * 3)
+        self.last_frame_time = ts
+        self.ekf_init = True
+
+    def ekf_predict(self, dt):
+        if not self.ekf_init or dt <= 0:
+            return
+        d = EKF_VEL_DECAY
+        for i in range(3):
+            self.ekf_x[i] += self.ekf_x[i + 3] * dt
+            self.ekf_x[i + 3] *= d
+        F = np.eye(6)
+        Q = np.zeros((6, 6))
+        sa = EKF_PROCESS_ACCEL
+        for i in range(3):
+            F[i, i + 3] = dt
+            F[i + 3, i + 3] = d
+            Q[i, i] = 0.25 * dt * dt * dt * dt * sa * sa
+            Q[i + 3, i + 3] = dt * dt * sa * sa
+            Q[i, i + 3] = Q[i + 3, i] = 0.5 * dt * dt * dt * sa * sa
+        self.ekf_P = F @ self.ekf_P @ F.T + Q
+
+    def ekf_update_visual(self, z, sigma):
+        if not self.ekf_init:
+            return
+        H = np.zeros((3, 6))
+        H[:, :3] = np.eye(3)
+        Rm = np.eye(3) * (sigma * sigma)
+        y = z - H @ self.ekf_x
+        S = H @ self.ekf_P @ H.T + Rm
+        Kg = self.ekf_P @ H.T @ np.linalg.inv(S)
+        self.ekf_x = self.ekf_x + Kg @ y
+        IKH = np.eye(6) - Kg @ H
+        self.ekf_P = IKH @ self.ekf_P @ IKH.T + Kg @ Rm @ Kg.T
+
+    # ---- Slam.cpp:1373-1473 ------------------------------------------------------------------
+    def refine_pose_via_local_pnp(self, f, tracked):
+        if tracked < 10:
+            return
+        obj, img = self._correspondences(f)
+        r = self.solve_pnp(obj, img, 100, 10)
+        if r is None:
+            return
+        R_p, t_p, inl = r
+        jump = np.linalg.norm(t_p - self.t_world)
+        if jump < PNP_REFINE_MAX_JUMP:
+            ratio = inl / len(obj)
+            blend = min(0.5, 0.3 + 0.2 * max(0.0, min(1.0, (ratio - 0.5) / 0.5)))
+            t_b = (1.0 - blend) * self.t_world + blend * t_p
+            rv = (1.0 - blend) * rodrigues_vec(self.R_world) + blend * rodrigues_vec(R_p)
+            self.R_world = rodrigues_mat(rv)
+            self.t_world = t_b
+            f.R, f.t = self.R_world.copy(), self.t_world.copy()
+            self.counts["pnp_refined"] += 1
+
+    # ---- Slam.cpp:1477-1522 ------------------------------------------------------------------
+    def run_pnp(self, f):
+        obj, img = self._correspondences(f)
+        r = self.solve_pnp(obj, img, 100, PNP_MIN_POINTS)
+        if r is None:
+            return
+        R_p, t_p, _ = r
+        if np.linalg.norm(t_p - f.t) > PNP_PERIODIC_MAX_JUMP:
+            return
+        b = PNP_PERIODIC_BLEND
+        t_b = (1.0 - b) * f.t + b * t_p
+        rv = (1.0 - b) * rodrigues_vec(f.R) + b * rodrigues_vec(R_p)
+        self.R_world = rodrigues_mat(rv)
+        self.t_world = t_b
+        f.R, f.t = self.R_world.copy(), self.t_world.copy()
+        self.counts["periodic_pnp"] += 1
+
+    # ---- Slam.cpp:1359-1368 ------------------------------------------------------------------
+    def is_keyframe(self, f, match_count):
+        if self.last_keyframe is None:
+            return True
+        if f.id - self.last_keyframe.id < KF_MIN_FRAME_GAP:
+            return False
+        return match_count >= KF_MIN_MATCHES
+
+    # ---- Slam.cpp:1089-1108 ------------------------------------------------------------------
+    def visibility(self, f):
+        rec = self.ops.take("vis", fid=f.id)
+        flags = rec["flags"]
+        if len(flags) != len(self.mp_pos):
+            raise GlueMismatch(f"frame {f.id}: visibility over {len(flags)} map points, mine {len(self.mp_pos)}")
+        rr = TRACK_VISIBILITY_RADIUS * TRACK_VISIBILITY_RADIUS
+        kx, ky = f.kx.astype(np.float64), f.ky.astype(np.float64)
+        for i in range(len(self.mp_pos)):
+            if not self.mp_valid[i]:
+                mine = 0
+            else:
+                u, v = project_point(self.mp_pos[i], self.R_world, self.t_world)
+                mine = 0
+                if 0 <= u < IMAGE_WIDTH and 0 <= v < IMAGE_HEIGHT:
+                    mine = 1
+                    self.mp_visible[i] += 1
+                    d2 = (u - kx) ** 2 + (v - ky) ** 2
+                    if np.any(d2 < rr):
+                        mine = 3
+                        self.mp_found[i] += 1
+            if mine != flags[i]:
+                raise GlueMismatch(f"frame {f.id}: map point {i} visibility {flags[i]} vs mine {mine}")
+
+    def cull(self):
+        self.counts["cull_rounds"] += 1
+        before = self._n_valid()
+        self._cull()
+        self.counts["culled"] += before - self._n_valid()
+
+    def _cull(self):
+        for i in range(len(self.mp_pos)):
+            if not self.mp_valid[i]:
+                continue
+            age = self.keyframe_count - self.mp_first_kf[i]
+            ratio = (np.float32(self.mp_found[i]) / np.float32(self.mp_visible[i])
+                     if self.mp_visible[i] > 0 else np.float32(0))
+            if age >= 3 and self.mp_visible[i] > 0 and ratio < CULL_FOUND_RATIO_YOUNG:
+                self.mp_valid[i] = False
+            if age >= 5 and len(self.mp_obs[i]) <= 2 and ratio < CULL_FOUND_RATIO_OLD:
+                self.mp_valid[i] = False
+
+    # ---- Slam.cpp:809-1135 -------------------------------------------------------------------
+    def process_frame(self, f):
+        self.ops = self.log.frame(f.id)
+        self._first_new = len(self.mp_pos)
+        ret = self._process(f)
+        self._check(f, ret)
+        return ret
+
+    def _chain(self, ref, f):
+        rec = self.ops.take("chain", a=ref.id, b=f.id)
+        if rec["seed"] != 42 + self.frame_count:
+            raise GlueMismatch(f"frame {f.id}: 3D-3D RANSAC seeded {rec['seed']}, Slam.cpp:276 gives "
+                               f"{42 + self.frame_count}")
+        return rec
+
+    def _process(self, f):
+        if f.n < MIN_MATCHES:
+            self.last_frame = f
+            self.branch[f.id] = "rejected"
+            return False
+        if self.last_frame is None:
+            f.R, f.t = self.R_world.copy(), self.t_world.copy()
+            f.kf = True
+            self.frames.append(f)
+            self.last_frame = self.last_keyframe = f
+            self.keyframe_count += 1
+            self.frame_count += 1
+            self.branch[f.id] = "first"
+            return True
+
+        ref = self.last_keyframe if (self.last_keyframe is not None and self.last_keyframe.n > 0) else self.last_frame
+        ch = self._chain(ref, f)
+        self.last_match_count = len(ch["good"])
+        # bridge keyframe (:846-872)
+        if self.last_match_count < MIN_MATCHES and self.last_frame is not None and self.last_frame is not ref:
+            temp = self.ops.take("match", a=self.last_frame.id, b=f.id)["good"]
+            if len(temp) >= MIN_MATCHES:
+                lf = self.last_frame
+                if not lf.kf:
+                    lf.kf = True
+                    self.keyframe_count += 1
+                    self.counts["bridges"] += 1
+                    if self.last_keyframe is not None:
+                        rec = self.ops.take(("match_dlt",), a=self.last_keyframe.id, b=lf.id)
+                        if len(rec["good"]) >= MIN_MATCHES:
+                            self.triangulate_points(self.last_keyframe, lf, rec["good"], rec)
+                    self.create_points_from_depth(lf)
+                    self.last_keyframe = lf
+                ref = self.last_keyframe
+                ch = self._chain(ref, f)
+                self.last_match_count = len(ch["good"])
+        # PnP recovery (:875-877)
+        r = self.try_pnp_recovery(f)
+        if r == 1:
+            self.branch[f.id] = "recovery"
+            return True
+        if r == -1:
+            self.branch[f.id] = "recovery_failed"
+            return False
+        # F verification (:880-910): the chain's kept list; stationary handling needs an accelerometer
+        # motion (:953-984)
+        R_ref, t_ref = ref.R, ref.t
+        use_3d3d = bool(ch["ok3d"])
+        if use_3d3d:
+            R_new = R_ref @ _hex(ch["R3"]).reshape(3, 3).T
+            t_new = t_ref - R_new @ _hex(ch["t3"])
+            self.counts["via_3d3d"] += 1
+            self.branch[f.id] = "3d3d"
+        else:
+            if not ch["okE"]:
+                self.last_frame = f
+                self.counts["emat_failed"] += 1
+                self.branch[f.id] = "emat_failed"
+                return False
+            scale = float.fromhex(ch["scale"])
+            if scale <= 0:
+                scale = self.last_good_scale if self.last_good_scale > 0 else MOTION_SCALE
+            else:
+                self.last_good_scale = scale
+            R_new = R_ref @ _hex(ch["RE"]).reshape(3, 3).T
+            t_new = t_ref - R_new @ (scale * _hex(ch["tE"]))
+            self.counts["via_emat"] += 1
+            self.branch[f.id] = "emat"
+        # EKF (:986-1047)
+        if not self.ekf_init:
+            self.ekf_initialize(self.t_world, f.ts)
+        dt = f.ts - self.last_frame_time
+        if 0 < dt < 1.0:
+            self.ekf_predict(dt)
+        sigma = EKF_SIGMA_VIS_3D3D if use_3d3d else EKF_SIGMA_VIS_EMAT
+        innovation = np.linalg.norm(t_new - self.ekf_x[:3])
+        self.counts["ekf_gated"] += innovation >= EKF_INNOV_GATE
+        self.ekf_update_visual(t_new, sigma if innovation < EKF_INNOV_GATE else innovation * 0.5)
+        ekf_pos = self.ekf_x[:3].copy()
+        delta = ekf_pos - self.t_world
+        step = np.linalg.norm(delta)
+        if step > EKF_MAX_STEP and step > 1e-6:
+            self.counts["ekf_clamped"] += 1
+            delta = delta * (EKF_MAX_STEP / step)
+            ekf_pos = self.t_world + delta
+            self.ekf_x[:3] = ekf_pos
+            self.ekf_x[3:] = delta / max(0.01, f.ts - self.last_frame_time)
+        self.last_translation = delta.copy()
+        t_new = ekf_pos
+        self.last_frame_time = f.ts
+        self.R_world, self.t_world = R_new, t_new
+        f.R, f.t = self.R_world.copy(), self.t_world.copy()
+        self.frames.append(f)
+        # local-map tracking + PnP refinement (:1057-1059)
+        rec = self.ops.take("tlm", fid=f.id)
+        if not (np.allclose(_hex(rec["R"]), f.R.ravel(), rtol=0, atol=1e-9)
+                and np.allclose(_hex(rec["t"]), f.t, rtol=0, atol=1e-9)):
+            raise GlueMismatch(f"frame {f.id}: local-map tracking ran at another pose: "
+                               f"{_hex(rec['t'])} vs mine {f.t}")
+        if rec["nmp"] != len(self.mp_pos) or rec["nvalid"] != self._n_valid():
+            raise GlueMismatch(f"frame {f.id}: local map {rec['nmp']}/{rec['nvalid']} points, mine "
+                               f"{len(self.mp_pos)}/{self._n_valid()}")
+        f.mp_idx = np.array(rec["mp_idx"], np.int64)
+        for mp, kp in rec["obs"]:
+            self.mp_obs[mp].append((f.id, kp))
+        tracked = rec["tracked"]
+        self.refine_pose_via_local_pnp(f, tracked)
+        # proactive keyframe (:1061-1070)
+        if not f.kf and self.last_match_count < MIN_MATCHES * 2 and self.last_keyframe is not None:
+            if f.id - self.last_keyframe.id >= 5:
+                self.counts["proactive_kf"] += 1
+                f.kf = True
+                self.keyframe_count += 1
+                self.setup_new_keyframe(f)
+                self.last_keyframe = f
+        # regular keyframe (:1073-1129)
+        if self.is_keyframe(f, self.last_match_count):
+            self.counts["regular_kf"] += 1
+            f.kf = True
+            self.keyframe_count += 1
+            self.setup_new_keyframe(f)
+            if self.keyframe_count % PNP_INTERVAL == 0:
+                self.run_pnp(f)
+            if self.keyframe_count % LC_CHECK_INTERVAL == 0:
+                raise NotImplementedError("loop closure is not restated here")
+            self.visibility(f)
+            if self.keyframe_count % 3 == 0:
+                self.cull()
+            self.last_keyframe = f
+        self.last_frame = f
+        self.frame_count += 1
+        return True
+
+    def _check(self, f, ret):
+        end = self.ops.take("frame_end")
+        # the map rows the C++ glue appended (descriptor row of the creating keypoint) == the points
+        # created here, in order
+        theirs = []
+        while True:
+            rec = self.ops.take("map_append", optional=True)
+            if rec is None:
+                break
+            if rec["first"] != self._first_new + len(theirs):
+                raise GlueMismatch(f"frame {f.id}: map rows appended at {rec['first']}, expected "
+                                   f"{self._first_new + len(theirs)}")
+            theirs += [(rec["src"], r) for r in rec["rows"]]
+        mine = self.appended[self._first_new:]
+        if theirs != mine:
+            raise GlueMismatch(f"frame {f.id}: new map points (frame, keypoint) differ: {len(theirs)} vs {len(mine)}; "
+                               f"first difference at {next((i for i, (a, b) in enumerate(zip(theirs, mine)) if a != b), None)}")
+        left = self.ops.unused()
+        if left:
+            raise GlueMismatch(f"frame {f.id}: C++ glue calls the restatement does not make: {left}")
+        got = dict(ret=bool(end["ret"]), kf=bool(end["kf"]), nmp=end["nmp"], nvalid=end["nvalid"],
+                   frame_count=end["frame_count"], kf_count=end["kf_count"], match_count=end["match_count"])
+        mine = dict(ret=ret, kf=f.kf, nmp=len(self.mp_pos), nvalid=self._n_valid(), frame_count=self.frame_count,
+                    kf_count=self.keyframe_count, match_count=self.last_match_count)
+        if got != mine:
+            raise GlueMismatch(f"frame {f.id}: C++ glue {got} vs restatement {mine}")
+        if ret:
+            dR = np.abs(_hex(end["R"]) - f.R.ravel()).max()
+            dt = np.abs(_hex(end["t"]) - f.t).max()
+            if dR > 1e-9 or dt > 1e-9:
+                raise GlueMismatch(f"frame {f.id}: pose differs by {dR:.3g} (R) / {dt:.3g} m (t)")

@@ -48,17 +48,19 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int kW4Patch = 18;                 // 18 x 18 input patch
 constexpr int kW4NP = kW4Patch * kW4Patch;   // 324
-constexpr int kW4V = 8 * 4 * 16 * 6;         // V image per k-step: [row 8][ch 4][tile 16][col 6] (rows 6, 7: dummy)
-constexpr int kW4X = 4 * 512;                // patch per k-step: [ch 4][512 slots] (slots >= 324: dummy)
-constexpr int kW4G = 20 * 20;                // FUSE1A gray patch
-constexpr int kW4OffV = 0;
-constexpr int kW4OffX = kW4OffV + 2 * kW4V;
-constexpr int kW4OffG = kW4OffX + 2 * kW4X;
-constexpr int kW4Main = kW4OffG + kW4G;
-constexpr int kW4Epi = 16384;                // epilogue: the partial halves, then the output staging
-constexpr int kW4Lds = kW4Main > kW4Epi ? kW4Main : kW4Epi;
-static_assert(kW4Lds * 4 <= 64 * 1024, "LDS");
-constexpr int kW4B = 4 * 2 * 64 * 20;        // B operands per k-step: [cg 4][xh 2][lane 64][20 (18 used)]
+// per k-step of 4 SUB channels (SUB 4-channel MFMA sub-steps between two barriers)
+template <int SUB> struct W4Geo {
+    static constexpr int CH = 4 * SUB;
+    static constexpr int V = 8 * CH * 16 * 6;   // V image: [row 8][ch][tile 16][col 6] (rows 6, 7: dummy)
+    static constexpr int X = CH * 512;          // patch: [ch][512 slots] (slots >= 324: dummy)
+    static constexpr int OffV = 0;
+    static constexpr int OffX = 2 * V;
+    static constexpr int OffG = OffX + 2 * X;
+    static constexpr int Main = OffG + 400;     // + the FUSE1A gray patch (20 x 20)
+    static constexpr int Lds = Main > 16384 ? Main : 16384;  // epilogue: partial halves, then the outputs
+    static_assert(Lds * 4 <= 160 * 1024, "LDS");
+};
+constexpr int kW4B = 4 * 2 * 64 * 20;        // B operands per 4 channels: [cg 4][xh 2][lane 64][20 (18 used)]
 
 __device__ inline void w4_xcd_work(int ntiles, int& tile, int& nt) {
     const int nblk = gridDim.x;
@@ -90,15 +92,21 @@ __device__ inline void w4_rowA(const float m[6], float r[4]) {
     r[3] = __builtin_fmaf(8.0f, e, b) + m[5];
 }
 
-// one lane's B operands of a k-step: U[18 xh + x][ch][cout] for x = 0..17 (4 x 16 B + 8 B)
+#ifndef VS_W4_ABL
+#define VS_W4_ABL 0  // latency ablation (results are wrong): 1 no transform, 2 no patch staging, 3 no MFMA,
+                     // 4 no barrier in the k-loop, 5 no B loads
+#endif
+// one lane's B operands of a 4-channel sub-step: U[18 xh + x][ch][cout] for x = 0..17 (4 x 16 B + 8 B)
 struct W4B {
     f32x4 q[4];
     f32x2 r;
     __device__ float operator[](int x) const { return x < 16 ? q[x >> 2][x & 3] : r[x - 16]; }
 };
 
-template <bool POOL, bool FUSE1A>
+template <bool POOL, bool FUSE1A, int SUB>
 __global__ __launch_bounds__(512, 1) void k_wino4(WinoArgs wa) {
+    using Geo = W4Geo<SUB>;
+    constexpr int CH = Geo::CH;
     const float* __restrict__ in = wa.in;
     const float* __restrict__ bias = wa.bias;
     float* __restrict__ out = wa.out;
@@ -106,7 +114,7 @@ __global__ __launch_bounds__(512, 1) void k_wino4(WinoArgs wa) {
     const int in_cstride = wa.in_cstride, in_coff = wa.in_coff, cin = wa.cin, cout = wa.cout;
     const int out_cstride = wa.out_cstride, out_coff = wa.out_coff, H = wa.H, W = wa.W, nbx = wa.nbx, nby = wa.nby;
     const int ntn = wa.cout_pad >> 6;
-    __shared__ __attribute__((aligned(16))) float lds[kW4Lds];
+    __shared__ __attribute__((aligned(16))) float lds[Geo::Lds];
 
     const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63, li = lane & 15, lk = lane >> 4;
     const int cg = wv & 3, xh = wv >> 2;
@@ -114,9 +122,9 @@ __global__ __launch_bounds__(512, 1) void k_wino4(WinoArgs wa) {
     w4_xcd_work(ntn, blk, nt);
     const int b = blk / (nbx * nby), r0 = blk - b * (nbx * nby);
     const int y0 = (r0 / nbx) * 16, x0 = (r0 % nbx) * 16;
-    const int nk = cin >> 2;
-    // this lane's B operands: [nt][k-step][cg][xh][lane][20]
-    const float* __restrict__ wb = wa.wu + ((size_t)nt * nk * 8 + cg * 2 + xh) * (64 * 20) + lane * 20;
+    const int nk = cin / CH;  // k-steps
+    // this lane's B operands: [nt][4-channel chunk][cg][xh][lane][20]
+    const float* __restrict__ wb = wa.wu + ((size_t)nt * (cin >> 2) * 8 + cg * 2 + xh) * (64 * 20) + lane * 20;
 
     // ---- patch role: slot p of the 18 x 18 patch, every thread (slots >= 324 are written, never read).
     // Waves 6, 7, 0, 1, 2, 3 hold the 324 real pixels, so the patch work lands beside the transform work
@@ -133,33 +141,38 @@ __global__ __launch_bounds__(512, 1) void k_wino4(WinoArgs wa) {
     float gnb[FUSE1A ? 9 : 1];
     if constexpr (FUSE1A) {
         const float* g = in + (size_t)b * H * W;
-        for (int i = tid; i < kW4G; i += 512) {
+        for (int i = tid; i < 400; i += 512) {
             const int yy = i / 20, xx = i - (i / 20) * 20;
             const int sy = y0 - 2 + yy, sx = x0 - 2 + xx;
-            lds[kW4OffG + i] = (sy >= 0 && sy < H && sx >= 0 && sx < W) ? g[(size_t)sy * W + sx] : 0.0f;
+            lds[Geo::OffG + i] = (sy >= 0 && sy < H && sx >= 0 && sx < W) ? g[(size_t)sy * W + sx] : 0.0f;
         }
         __syncthreads();
 #pragma unroll
-        for (int k = 0; k < 9; k++) gnb[k] = own_px ? lds[kW4OffG + (ppy + k / 3) * 20 + ppx + k % 3] : 0.0f;
+        for (int k = 0; k < 9; k++) gnb[k] = own_px ? lds[Geo::OffG + (ppy + k / 3) * 20 + ppx + k % 3] : 0.0f;
     }
     using GY_ = std::true_type;   // guarded: the k-step index may run past the last one (pipeline tail)
     using GN_ = std::false_type;  // steady state: no guards, so no basic-block boundaries around the work
-    f32x4 rx = {0.f, 0.f, 0.f, 0.f};
+    f32x4 rx[SUB];
+#pragma unroll
+    for (int u = 0; u < SUB; u++) rx[u] = f32x4{0.f, 0.f, 0.f, 0.f};
     auto fetch_x = [&](auto g_c, int c) {
         if constexpr (!FUSE1A) {
             // src is clamped into the image (pin == false: pixel 0 of the frame); put_x zeroes what lies outside
-            if (!decltype(g_c)::value || c < nk) rx = *reinterpret_cast<const f32x4*>(src + 4 * c);
+            if (!decltype(g_c)::value || c < nk)
+#pragma unroll
+                for (int u = 0; u < SUB; u++) rx[u] = *reinterpret_cast<const f32x4*>(src + CH * c + 4 * u);
         }
     };
     // patch of k-step c -> lds[X slot]: [ch][slot]
     auto put_x = [&](int slot, auto g_c, int c) {
         if (decltype(g_c)::value && c >= nk) return;
-        float* xs = lds + kW4OffX + slot * kW4X + p;
+        if (VS_W4_ABL == 2) return;
+        float* xs = lds + Geo::OffX + slot * Geo::X + p;
         if constexpr (FUSE1A) {
-            // the k-step's 4 x (9 taps + bias) are wave-uniform: scalar loads, v_fma_f32 with SGPR operands
-            const f32x4* wp = reinterpret_cast<const f32x4*>(w1a + (size_t)(4 * c) * 12);
+            // the k-step's channels' 9 taps + bias are wave-uniform: scalar loads, v_fma_f32 with SGPR operands
+            const f32x4* wp = reinterpret_cast<const f32x4*>(w1a + (size_t)(CH * c) * 12);
 #pragma unroll
-            for (int cc = 0; cc < 4; cc++) {
+            for (int cc = 0; cc < CH; cc++) {
                 const f32x4 q0 = wp[3 * cc], q1 = wp[3 * cc + 1], q2 = wp[3 * cc + 2];
                 const float wk[9] = {q0[0], q0[1], q0[2], q0[3], q1[0], q1[1], q1[2], q1[3], q2[0]};
                 float a = q2[1];
@@ -169,36 +182,49 @@ __global__ __launch_bounds__(512, 1) void k_wino4(WinoArgs wa) {
             }
         } else {
 #pragma unroll
-            for (int cc = 0; cc < 4; cc++) xs[cc * 512] = masked(rx[cc]);
+            for (int cc = 0; cc < CH; cc++) xs[cc * 512] = masked(rx[cc >> 2][cc & 3]);
         }
     };
 
-    // ---- transform role: thread (domain row i = its wave, channel tc, tile tt); waves 6 and 7 repeat
-    // rows 0 and 1 into dummy rows of the image, so that the code has no branch
-    const int ti = wv, tc = lane >> 4, tt = lane & 15, tty = tt >> 2, ttx = tt & 3;
-    // row i of B^T: four patch rows and their coefficients (wave-uniform)
-    int rr0 = 1, rr1 = 2, rr2 = 3, rr3 = 4;
-    float k0 = 0.f, k1 = 0.f, k2 = 0.f, k3 = 0.f;
-    switch (ti) {
-        case 0: case 6: rr0 = 0; rr1 = 2; rr2 = 4; rr3 = 4; k0 = 4.f; k1 = -5.f; k2 = 1.f; k3 = 0.f; break;
-        case 1: case 7: k0 = -4.f; k1 = -4.f; k2 = 1.f; k3 = 1.f; break;
-        case 2: k0 = 4.f; k1 = -4.f; k2 = -1.f; k3 = 1.f; break;
-        case 3: k0 = -2.f; k1 = -1.f; k2 = 2.f; k3 = 1.f; break;
-        case 4: k0 = 2.f; k1 = -1.f; k2 = -2.f; k3 = 1.f; break;
-        default: rr0 = 1; rr1 = 3; rr2 = 5; rr3 = 5; k0 = 4.f; k1 = -5.f; k2 = 1.f; k3 = 0.f; break;
+    // ---- transform role: SUB items per thread, item u = (domain row i, channel, tile) of index
+    // tid + 512 u over [row][ch][tile]; rows 6 and 7 are dummy rows of the image (waves past the six
+    // real rows repeat rows 0 and 1 there), so that the code has no branch
+    struct TrItem {
+        int rr[4];
+        float kc[4];
+        int xbase, vbase;
+    };
+    TrItem tri[SUB];
+#pragma unroll
+    for (int u = 0; u < SUB; u++) {
+        const int idx = tid + 512 * u, ti = idx / (16 * CH), tc = (idx >> 4) % CH, tt = idx & 15;
+        TrItem& T = tri[u];
+        // row i of B^T: four patch rows and their coefficients (wave-uniform)
+        T.rr[0] = 1, T.rr[1] = 2, T.rr[2] = 3, T.rr[3] = 4;
+        switch (ti) {
+            case 0: case 6: T.rr[0] = 0, T.rr[1] = 2, T.rr[2] = 4, T.rr[3] = 4;
+                T.kc[0] = 4.f, T.kc[1] = -5.f, T.kc[2] = 1.f, T.kc[3] = 0.f; break;
+            case 1: case 7: T.kc[0] = -4.f, T.kc[1] = -4.f, T.kc[2] = 1.f, T.kc[3] = 1.f; break;
+            case 2: T.kc[0] = 4.f, T.kc[1] = -4.f, T.kc[2] = -1.f, T.kc[3] = 1.f; break;
+            case 3: T.kc[0] = -2.f, T.kc[1] = -1.f, T.kc[2] = 2.f, T.kc[3] = 1.f; break;
+            case 4: T.kc[0] = 2.f, T.kc[1] = -1.f, T.kc[2] = -2.f, T.kc[3] = 1.f; break;
+            default: T.rr[0] = 1, T.rr[1] = 3, T.rr[2] = 5, T.rr[3] = 5;
+                T.kc[0] = 4.f, T.kc[1] = -5.f, T.kc[2] = 1.f, T.kc[3] = 0.f; break;
+        }
+        T.xbase = tc * 512 + (4 * (tt >> 2)) * kW4Patch + 4 * (tt & 3);
+        T.vbase = ((ti * CH + tc) * 16 + tt) * 6;
     }
-    const int xbase = tc * 512 + (4 * tty) * kW4Patch + 4 * ttx;
-    const int vbase = ((ti * 4 + tc) * 16 + tt) * 6;
-    auto transform = [&](int slot, auto g_c, int c) {
+    auto transform = [&](int u, int slot, auto g_c, int c) {
         if (decltype(g_c)::value && c >= nk) return;
-        const float* xs = lds + kW4OffX + slot * kW4X + xbase;
+        if (VS_W4_ABL == 1) return;
+        const TrItem& T = tri[u];
+        const float* xs = lds + Geo::OffX + slot * Geo::X + T.xbase;
         float e[4][6];
-        const int rows[4] = {rr0, rr1, rr2, rr3};
 #pragma unroll
         for (int r = 0; r < 4; r++) {
 #pragma unroll
             for (int h = 0; h < 3; h++) {
-                const f32x2 v = *reinterpret_cast<const f32x2*>(xs + rows[r] * kW4Patch + 2 * h);
+                const f32x2 v = *reinterpret_cast<const f32x2*>(xs + T.rr[r] * kW4Patch + 2 * h);
                 e[r][2 * h] = v[0];
                 e[r][2 * h + 1] = v[1];
             }
@@ -206,19 +232,28 @@ __global__ __launch_bounds__(512, 1) void k_wino4(WinoArgs wa) {
         float t[6], o[6];
 #pragma unroll
         for (int j = 0; j < 6; j++)
-            t[j] = __builtin_fmaf(k3, e[3][j], __builtin_fmaf(k2, e[2][j], __builtin_fmaf(k1, e[1][j], k0 * e[0][j])));
+            t[j] = __builtin_fmaf(T.kc[3], e[3][j],
+                                  __builtin_fmaf(T.kc[2], e[2][j], __builtin_fmaf(T.kc[1], e[1][j], T.kc[0] * e[0][j])));
         w4_rowB(t, o);
-        float* vs = lds + kW4OffV + slot * kW4V + vbase;
+        float* vs = lds + Geo::OffV + slot * Geo::V + T.vbase;
 #pragma unroll
         for (int h = 0; h < 3; h++) *reinterpret_cast<f32x2*>(vs + 2 * h) = f32x2{o[2 * h], o[2 * h + 1]};
     };
     // ---- B operands straight from L2 into registers, one k-step ahead (no LDS image, no barrier)
-    auto fetch_b = [&](W4B& bq, auto g_c, int c) {
+    // one W4B per 4-channel sub-step
+    struct W4BS {
+        W4B s[SUB];
+    };
+    auto fetch_b = [&](W4BS& bq, auto g_c, int c) {
         if (decltype(g_c)::value && c >= nk) return;
-        const float* q = wb + (size_t)c * kW4B;
+        if (VS_W4_ABL == 5) return;
 #pragma unroll
-        for (int j = 0; j < 4; j++) bq.q[j] = *reinterpret_cast<const f32x4*>(q + 4 * j);
-        bq.r = *reinterpret_cast<const f32x2*>(q + 16);
+        for (int u = 0; u < SUB; u++) {
+            const float* q = wb + (size_t)(SUB * c + u) * kW4B;
+#pragma unroll
+            for (int j = 0; j < 4; j++) bq.s[u].q[j] = *reinterpret_cast<const f32x4*>(q + 4 * j);
+            bq.s[u].r = *reinterpret_cast<const f32x2*>(q + 16);
+        }
     };
 
     f32x4 acc[18];
@@ -226,7 +261,7 @@ __global__ __launch_bounds__(512, 1) void k_wino4(WinoArgs wa) {
     for (int x = 0; x < 18; x++) acc[x] = f32x4{0.f, 0.f, 0.f, 0.f};
 
     // prologue: patches 0, 1 in LDS, patch 2 and the B operands of step 0 in registers, V 0 transformed
-    W4B bA, bB;
+    W4BS bA, bB;
     fetch_b(bA, GY_{}, 0);
     fetch_x(GY_{}, 0);
     put_x(0, GY_{}, 0);
@@ -234,34 +269,44 @@ __global__ __launch_bounds__(512, 1) void k_wino4(WinoArgs wa) {
     put_x(1, GY_{}, 1);
     fetch_x(GY_{}, 2);
     __syncthreads();
-    transform(0, GY_{}, 0);
+#pragma unroll
+    for (int u = 0; u < SUB; u++) transform(u, 0, GY_{}, 0);
     __syncthreads();
 
-    // A operands: V[3 xh + rr][lk][li][0..5]
-    const int aoff = kW4OffV + (lk * 16 + li) * 6 + 3 * xh * (4 * 16 * 6);
+    // A operands of sub-step s: V[3 xh + rr][4 s + lk][li][0..5]
+    const int aoff = Geo::OffV + (lk * 16 + li) * 6 + 3 * xh * (CH * 16 * 6);
     // k-step k on buffers P = k & 1 with B operands bc, loading the next step's into bn
-    auto step = [&](auto par, auto g_c, int k, const W4B& bc, W4B& bn) {
+    auto step = [&](auto par, auto g_c, int k, const W4BS& bc, W4BS& bn) {
         constexpr int P = decltype(par)::value;
         fetch_b(bn, g_c, k + 1);
-        const float* av = lds + aoff + P * kW4V;
-        f32x2 a2[3][3];
 #pragma unroll
-        for (int rr = 0; rr < 3; rr++)
+        for (int sb = 0; sb < SUB; sb++) {
+            const float* av = lds + aoff + P * Geo::V + sb * (4 * 16 * 6);
+            f32x2 a2[3][3];
 #pragma unroll
-            for (int h = 0; h < 3; h++) a2[rr][h] = *reinterpret_cast<const f32x2*>(av + rr * (4 * 16 * 6) + 2 * h);
+            for (int rr = 0; rr < 3; rr++)
 #pragma unroll
-        for (int rr = 0; rr < 3; rr++) {
+                for (int h = 0; h < 3; h++)
+                    a2[rr][h] = *reinterpret_cast<const f32x2*>(av + rr * (CH * 16 * 6) + 2 * h);
 #pragma unroll
-            for (int j = 0; j < 6; j++)
-                acc[6 * rr + j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a2[rr][j >> 1][j & 1], bc[6 * rr + j],
-                                                                       acc[6 * rr + j], 0, 0, 0);
-            if (rr == 0) transform(P ^ 1, g_c, k + 1);
-            if (rr == 1) {
-                put_x(P, g_c, k + 2);
-                fetch_x(g_c, k + 3);
+            for (int rr = 0; rr < 3; rr++) {
+#pragma unroll
+                for (int j = 0; j < 6; j++) {
+                    if (VS_W4_ABL == 3) {
+                        acc[6 * rr + j][0] += a2[rr][j >> 1][j & 1] * bc.s[sb][6 * rr + j];
+                        continue;
+                    }
+                    acc[6 * rr + j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a2[rr][j >> 1][j & 1], bc.s[sb][6 * rr + j],
+                                                                           acc[6 * rr + j], 0, 0, 0);
+                }
+                if (rr == 0) transform(sb, P ^ 1, g_c, k + 1);
+                if (rr == 1 && sb == 0) {
+                    put_x(P, g_c, k + 2);
+                    fetch_x(g_c, k + 3);
+                }
             }
         }
-        __syncthreads();  // V of k + 1 and the patch of k + 2 complete; the buffers of k free
+        if (VS_W4_ABL != 4) __syncthreads();  // V of k + 1 and the patch of k + 2 complete; the buffers of k free
     };
     using S0 = std::integral_constant<int, 0>;
     using S1 = std::integral_constant<int, 1>;
@@ -379,14 +424,31 @@ int wino4_launch(WinoArgs a, bool pool, bool fuse1a, hipStream_t s) {
     a.nbx = (a.W + 15) / 16;
     a.nby = (a.H + 15) / 16;
     dim3 grid((unsigned)((long)a.B * a.nbx * a.nby * (a.cout_pad / 64)));
-    if (pool && fuse1a)
-        hipLaunchKernelGGL((k_wino4<true, true>), grid, dim3(512), 0, s, a);
-    else if (pool)
-        hipLaunchKernelGGL((k_wino4<true, false>), grid, dim3(512), 0, s, a);
-    else if (fuse1a)
-        hipLaunchKernelGGL((k_wino4<false, true>), grid, dim3(512), 0, s, a);
-    else
-        hipLaunchKernelGGL((k_wino4<false, false>), grid, dim3(512), 0, s, a);
+    // 4-channel k-steps; VS_WINO4_SUB=2 runs 8-channel steps (two MFMA sub-steps per barrier: 256 VGPRs,
+    // measured 5 % slower over the network, profiles/r05e_wino4_sub_ab.txt)
+    static const int sub = [] {
+        const char* e = std::getenv("VS_WINO4_SUB");
+        return e && e[0] == '2' ? 2 : 1;
+    }();
+    if (sub == 2 && a.cin % 8 == 0) {
+        if (pool && fuse1a)
+            hipLaunchKernelGGL((k_wino4<true, true, 2>), grid, dim3(512), 0, s, a);
+        else if (pool)
+            hipLaunchKernelGGL((k_wino4<true, false, 2>), grid, dim3(512), 0, s, a);
+        else if (fuse1a)
+            hipLaunchKernelGGL((k_wino4<false, true, 2>), grid, dim3(512), 0, s, a);
+        else
+            hipLaunchKernelGGL((k_wino4<false, false, 2>), grid, dim3(512), 0, s, a);
+    } else {
+        if (pool && fuse1a)
+            hipLaunchKernelGGL((k_wino4<true, true, 1>), grid, dim3(512), 0, s, a);
+        else if (pool)
+            hipLaunchKernelGGL((k_wino4<true, false, 1>), grid, dim3(512), 0, s, a);
+        else if (fuse1a)
+            hipLaunchKernelGGL((k_wino4<false, true, 1>), grid, dim3(512), 0, s, a);
+        else
+            hipLaunchKernelGGL((k_wino4<false, false, 1>), grid, dim3(512), 0, s, a);
+    }
     VS_HIP(hipGetLastError());
     return VS_OK;
 }
