@@ -59,6 +59,7 @@ CONV1_MIN_BYTES_PER_FRAME = 480 * 640 * 4 + 240 * 320 * 64 * 4
 # 1 KB descriptor gathers 1,638,400 + heatmap write and read 1,228,800 + 420,800 of records out
 POST_BYTES_PER_FRAME = 1248000 + 1638400 + 1228800 + 420800
 LOOP_FRAMES = 126               # one lap of synth.loop_trajectory (0.3 m/s, 10 processed frames/s)
+PIONEER_FRAMES = 848            # freiburg2_pioneer_slam3: 2,544 images, every 3rd processed (README.md:5)
 T0 = 1311868164.0               # TUM-like timestamps, 0.1 s per processed frame (FRAME_STEP = 3)
 
 # Algorithmic FLOPs of each SuperPoint layer per 640x480 frame (2 * MACs).
@@ -92,6 +93,22 @@ if WINO:
         "head_a": 2 * 16 * 30 * 40 * 512 * 128,
     })
 
+# Round 5: the layers with at least 64 workgroups of 16 x 16 pixels per frame run Winograd F(4x4, 3x3)
+# (wino4.hip k_wino4: 36 products per 4 x 4 output tile, input and output channel, 2.25 per pixel
+# against F(2x2)'s 4); the tiles the kernel computes include the padding of its 16 x 16-pixel workgroups
+# (120 x 160: 8 x 10 workgroups; 60 x 80: 4 x 5).  conv4a / conv4b (40 workgroups per frame) stay on F(2x2).
+WINO4 = WINO and os.environ.get("VS_WINO4", "1") != "0"
+WINO4_LAYERS = ("conv1_fused", "conv2a", "conv2b_pool", "conv3a", "conv3b_pool", "head_a")
+if WINO4:
+    MFMA_FLOPS.update({
+        "conv1_fused": 2 * 36 * 120 * 160 * 64 * 64,
+        "conv2a": 2 * 36 * 60 * 80 * 64 * 64,
+        "conv2b_pool": 2 * 36 * 60 * 80 * 64 * 64,
+        "conv3a": 2 * 36 * 32 * 40 * 128 * 64,
+        "conv3b_pool": 2 * 36 * 32 * 40 * 128 * 128,
+        "head_a": 2 * 36 * 16 * 20 * 512 * 128,
+    })
+
 # profiling stage -> symbol prefix (as rocprofv3 reports it) of that stage's dominant kernel; the
 # template argument list continues after the prefix (e.g. the chunk width: "<true, 1, true, false, 4>")
 STAGE_KERNEL_WINO = {
@@ -117,9 +134,20 @@ STAGE_KERNEL = {
 }
 
 
+STAGE_KERNEL_WINO4 = {
+    "conv1_fused": "vs::k_wino4<true, true",
+    "conv2a": "vs::k_wino4<false, false",
+    "conv2b_pool": "vs::k_wino4<true, false",
+    "conv3a": "vs::k_wino4<false, false",
+    "conv3b_pool": "vs::k_wino4<true, false",
+    "head_a": "vs::k_wino4<false, false",
+}
+
 STAGE_KERNEL_DIRECT = dict(STAGE_KERNEL)
 if WINO:
     STAGE_KERNEL.update(STAGE_KERNEL_WINO)
+if WINO4:
+    STAGE_KERNEL.update(STAGE_KERNEL_WINO4)
 
 
 def kernel_matches(name, prefix):
@@ -195,12 +223,14 @@ def match_roofline(ms_launches, pairs_per_launch, cus, where):
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--batch", type=int, default=32, help="frames per GPU per step")
     ap.add_argument("--cpu-frames", type=int, default=24, help="cpu_baseline sample size (processed frames)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--frontend-steps", type=int, default=6, help="timed steps of the config[3] batch front end")
+    ap.add_argument("--frontend-steps", type=int, default=4, help="timed steps of the config[3] batch front end")
+    ap.add_argument("--frontend-frames", type=int, default=318,
+                    help="config[3] frames per GPU per step (318: the 2,544-image sequence's shard at 8 GPUs)")
     ap.add_argument("--no-frontend", action="store_true")
     ap.add_argument("--ba-reps", type=int, default=5, help="timed calls of the config[2] local-BA window (0: skip)")
     ap.add_argument("--stage-profile", choices=["network", "all", "none"], default="network",
@@ -319,28 +349,49 @@ def local_ba(ctx, reps):
 
 
 def frontend_batch(ctx, L, B, rank, world, steps, warmup):
-    """BASELINE config[3]: frame-sharded extract + pair geometry (+ RCCL all-gather when world > 1)."""
+    """BASELINE config[3]: the offline frame-sharded front end through the C ABI (vs_batch_submit_dev /
+    vs_batch_collect, csrc/batch.hip — the path INTEGRATION.md gives a C++ driver): per step each rank
+    extracts its B frames, receives its halo frame's record over RCCL (point-to-point ring) and runs
+    match + F verification + 3D-3D RANSAC + E fallback on the B pairs ending in its frames, the next
+    step's network overlapping this step's geometry.  B = the per-GPU shard of the 2,544-image sequence
+    (FRAME_STEP 1: 2544 / 8 = 318), so at 8 GPUs one step is the whole sequence."""
     import torch
     import torch.distributed as dist
-    from vslam_pipeline import DevicePipeline
+
+    import vslam_abi
     U = len(L["bgr"])
     n_total = world * B
-    idx = [(rank * B + j) % U for j in range(B)]
     dev = torch.device("cuda", torch.cuda.current_device())
+    # the rank's frames of every step (the synthetic loop repeats every U frames; consecutive frames
+    # stay consecutive across the lap seam)
+    idx = [(rank * B + j) % U for j in range(B)]
     frames = torch.from_numpy(L["bgr"][idx]).to(dev)
     depth = torch.from_numpy(L["depth"][idx]).to(dev)
     depth_prev = torch.from_numpy(L["depth"][(rank * B - 1) % U]).to(dev)
-    pipe = DevicePipeline(ctx, B, H, W, rank=rank, world=world)
+    uid = None
+    if world > 1:  # rank 0's RCCL communicator id, distributed over the torch process group
+        t = torch.zeros(vslam_abi.VS_BATCH_ID_BYTES if hasattr(vslam_abi, "VS_BATCH_ID_BYTES") else 128,
+                        dtype=torch.uint8, device=dev)
+        if rank == 0:
+            t.copy_(torch.frombuffer(bytearray(vslam_abi.batch_unique_id()), dtype=torch.uint8).to(dev))
+        dist.broadcast(t, 0)
+        uid = bytes(t.cpu().numpy().tobytes())
+    bt = vslam_abi.Batch(ctx, B, H, W, rank=rank, world=world, uid=uid)
+    s = torch.cuda.current_stream().cuda_stream
+    motions = []
 
     def run(first, count):
-        pending = None
+        inflight = 0
         for i in range(first, first + count):
-            S = pipe.submit(frames, depth, frame_count0=i * n_total + rank * B, depth_prev=depth_prev)
-            if pending is not None:
-                pipe.collect(pending)
-            pending = S
-        if pending is not None:
-            pipe.collect(pending)
+            halo = depth_prev.data_ptr() if (world > 1 and (i > 0 or rank > 0)) else None
+            bt.submit_dev(frames.data_ptr(), depth.data_ptr(), halo, i * n_total + rank * B, s)
+            inflight += 1
+            if inflight == 2:
+                motions.append(bt.collect())
+                inflight -= 1
+        while inflight:
+            motions.append(bt.collect())
+            inflight -= 1
 
     run(0, warmup)
     torch.cuda.synchronize()
@@ -361,49 +412,74 @@ def frontend_batch(ctx, L, B, rank, world, steps, warmup):
         tt = torch.tensor([el], dtype=torch.float64, device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         el = float(tt.item())
-    # the matcher alone on the last step's resident descriptors (B consecutive pairs per launch, whole chip):
-    # inside the pipeline it shares the CUs with the next step's network
-    S = pipe.sets[(pipe.k - 1) % 2]
-    cap = S.desc.shape[1]
-    sm = torch.cuda.current_stream().cuda_stream
+    last = motions[-1]
+    # the matcher alone on the last step's resident records (B - 1 consecutive pairs of the block per
+    # launch, whole chip): inside the pipeline it shares the CUs with the next step's network
+    kps_p, desc_p, n_p, nf = bt.features_dev()
+    cap = vslam_abi.SP_MAX_KEYPOINTS
+    P = nf - 1
+    pairs = torch.tensor([[p, p + 1] for p in range(P)], dtype=torch.int32, device=dev)
+    raw = torch.zeros(P * cap * vslam_abi.MATCH_DTYPE.itemsize, dtype=torch.uint8, device=dev)
+    good = torch.zeros_like(raw)
+    nraw = torch.zeros(P, dtype=torch.int32, device=dev)
+    ngood = torch.zeros_like(nraw)
+    ctx.match_pairs_dev(P, pairs.data_ptr(), nf, desc_p, n_p, cap, 0.75, raw.data_ptr(), nraw.data_ptr(),
+                        good.data_ptr(), ngood.data_ptr(), s)
+    torch.cuda.synchronize()
     ctx.profile(True)
     ctx.profile_reset()
     for _ in range(20):
-        ctx.match_pairs_dev(B, pipe.pairs.data_ptr(), B + 1, S.desc.data_ptr(), S.n.data_ptr(), cap, 0.75,
-                            S.raw.data_ptr(), S.nraw.data_ptr(), S.good.data_ptr(), S.ngood.data_ptr(), sm)
+        ctx.match_pairs_dev(P, pairs.data_ptr(), nf, desc_p, n_p, cap, 0.75, raw.data_ptr(), nraw.data_ptr(),
+                            good.data_ptr(), ngood.data_ptr(), s)
     torch.cuda.synchronize()
     alone = ctx.profile_read().get("match")
     ctx.profile(False)
-    # post-processing alone (decode + NMS + top-K + sampling) on the same step's network outputs,
-    # whole chip: in the pipelines it queues behind the network's workgroups on the same CUs
-    h, w = H, W
-    ctx.postprocess_batch_dev(B, S.semi.data_ptr(), S.dgrid.data_ptr(), h, w, S.kps[1:].data_ptr(),
-                              S.desc[1:].data_ptr(), S.n[1:].data_ptr(), cap, sm)
+    # the pipeline's own launches matched B pairs each: the same pair lists (bit-exact kernel)
+    assert np.array_equal(ngood.cpu().numpy(), last["n_good"][1:]), "matcher alone differs from the pipeline"
+    bt.close()
+    # post-processing alone (decode + NMS + top-K + sampling) on 32 frames' network outputs, whole chip:
+    # in the pipelines it queues behind the network's workgroups on the same CUs
+    nb = min(B, 32)
+    hc, wc = H // 8, W // 8
+    semi = torch.zeros((nb, hc, wc, vslam_abi.SEMI_CH), dtype=torch.float32, device=dev)
+    dgrid = torch.zeros((nb, hc, wc, vslam_abi.DESC_DIM), dtype=torch.float32, device=dev)
+    kps = torch.zeros((nb, cap * vslam_abi.KEYPOINT_DTYPE.itemsize), dtype=torch.uint8, device=dev)
+    desc = torch.zeros((nb, cap, 256), dtype=torch.float32, device=dev)
+    n = torch.zeros(nb, dtype=torch.int32, device=dev)
+    ctx.network_batch_dev(nb, frames.data_ptr(), H, W, semi.data_ptr(), dgrid.data_ptr(), s)
+    ctx.postprocess_batch_dev(nb, semi.data_ptr(), dgrid.data_ptr(), H, W, kps.data_ptr(), desc.data_ptr(),
+                              n.data_ptr(), cap, s)
     torch.cuda.synchronize()
     ctx.profile(True)
     ctx.profile_reset()
     reps = 10
     for _ in range(reps):
-        ctx.postprocess_batch_dev(B, S.semi.data_ptr(), S.dgrid.data_ptr(), h, w, S.kps[1:].data_ptr(),
-                                  S.desc[1:].data_ptr(), S.n[1:].data_ptr(), cap, sm)
+        ctx.postprocess_batch_dev(nb, semi.data_ptr(), dgrid.data_ptr(), H, W, kps.data_ptr(), desc.data_ptr(),
+                                  n.data_ptr(), cap, s)
     torch.cuda.synchronize()
     pp = ctx.profile_read()
     ctx.profile(False)
-    post_ms = sum(pp[k][0] for k in ("decode", "nms_rounds", "nms_select", "sample") if k in pp) / (reps * B)
+    post_ms = sum(pp[k][0] for k in ("decode", "nms_rounds", "nms_select", "sample") if k in pp) / (reps * nb)
     post = {"what": "FeatureExtractor.cpp:126-259 after the network (decode, greedy NMS, top-400, border erase, "
-                    "descriptor sampling) on one step's resident semi / descriptor grids, alone on the whole chip",
-            "frames_per_launch": B, "ms_per_frame": round(post_ms, 5),
-            "stage_ms_per_frame": {k: round(pp[k][0] / (reps * B), 5) for k in ("decode", "nms_rounds", "nms_select",
-                                                                                "sample") if k in pp},
+                    "descriptor sampling) on 32 frames' resident semi / descriptor grids, alone on the whole chip",
+            "frames_per_launch": nb, "ms_per_frame": round(post_ms, 5),
+            "stage_ms_per_frame": {k: round(pp[k][0] / (reps * nb), 5) for k in ("decode", "nms_rounds", "nms_select",
+                                                                                 "sample") if k in pp},
             "roofline": {"bound": "hbm", "algorithmic_bytes_per_frame": POST_BYTES_PER_FRAME,
                          "achieved": round(POST_BYTES_PER_FRAME / (post_ms / 1e3) / 1e9, 2), "peak": 8000.0,
                          "unit": "GB/s", "frac": round(POST_BYTES_PER_FRAME / (post_ms / 1e3) / 8e12, 5)}}
+    del frames, depth
     return {"value": round(world * B * steps / el, 3), "unit": "frames/s", "ms_per_step": round(el / steps * 1e3, 3),
-            "_match": alone, "_match_in_pipeline": prof.get("match"), "steps": steps, "frames_per_gpu_per_step": B,
-            "postprocess_alone": post,
+            "_match": alone, "_match_pairs": P, "_match_in_pipeline": prof.get("match"), "steps": steps,
+            "frames_per_gpu_per_step": B, "postprocess_alone": post,
+            "pairs_3d3d_ok": int(last["ok"].sum()), "pairs_emat_ok": int(last["eok"].sum()),
             "workload": "config[3] offline batch: per-GPU SuperPoint extract + ratio matching + F-RANSAC + 3D-3D "
-                        "RANSAC (E fallback) over consecutive frame pairs, no tracking state",
-            "parallelism": f"frame-sharded x{world}" + (" + RCCL all-gather of feature records" if world > 1 else "")}
+                        "RANSAC (E fallback) over consecutive frame pairs, no tracking state; the per-GPU shard of "
+                        "the 2,544-image sequence (318 frames) per step",
+            "path": "C ABI vs_batch_submit_dev / vs_batch_collect (csrc/batch.hip): two steps in flight, the next "
+                    "step's network beside this step's geometry",
+            "parallelism": f"frame-sharded x{world}" + (" + RCCL point-to-point halo ring over xGMI" if world > 1 else ""),
+            "scaling": "weak"}
 
 
 def monocular_hd(ctx, B, rank, world, steps, warmup, workers):
@@ -526,16 +602,40 @@ def main():
     B = args.batch
     dev = torch.device("cuda", torch.cuda.current_device())
 
-    # one lap of the closed-loop path; rank r starts its sequence 16 r frames further along
+    # headline input: the non-repeating Pioneer-like drive of synth.pioneer_trajectory,
+    # at least the reference sequence's 848 processed frames (2,544 images at FRAME_STEP 3,
+    # main.cpp:1096-1107) and every frame the run tracks distinct; each rank renders every world-th frame
+    # and the ranks all-gather them (replicas: every GPU tracks the same drive).  The closed loop
+    # (synth.loop_sequence) stays the input of the config[3] batch front end.
     workers = args.render_workers or max(1, min(16, (os.cpu_count() or 1) // max(world, 1)))
-    L0 = synth.loop_sequence(LOOP_FRAMES, workers=workers)
-    U = LOOP_FRAMES
-    roll = (16 * rank) % U
-    L = {k: (np.roll(v, -roll, axis=0) if isinstance(v, np.ndarray) and v.ndim >= 1 else v) for k, v in L0.items()}
-    wrap = np.concatenate([np.arange(U), np.arange(B)])  # a batch starting anywhere is contiguous
-    bgr = torch.from_numpy(L["bgr"][wrap]).to(dev)
-    dep = torch.from_numpy(L["depth"][wrap]).to(dev)
-    hdep = [L["depth"][i] for i in wrap]
+    n_path = max(PIONEER_FRAMES, B * (args.warmup + args.steps + args.track_profile_steps))
+    poses = synth.pioneer_trajectory(n_path)
+    mine = list(range(rank, n_path, world))
+    pb, pd = synth.render_frames(poses, mine, workers=workers)
+    if world > 1:
+        per = (n_path + world - 1) // world
+        gb = torch.zeros((world, per) + pb.shape[1:], dtype=torch.uint8, device=dev)
+        gd = torch.zeros((world, per) + pd.shape[1:], dtype=torch.float32, device=dev)
+        lb = torch.zeros((per,) + pb.shape[1:], dtype=torch.uint8, device=dev)
+        ld = torch.zeros((per,) + pd.shape[1:], dtype=torch.float32, device=dev)
+        lb[:len(mine)].copy_(torch.from_numpy(pb))
+        ld[:len(mine)].copy_(torch.from_numpy(pd))
+        dist.all_gather_into_tensor(gb, lb)
+        dist.all_gather_into_tensor(gd, ld)
+        order = [(i % world, i // world) for i in range(n_path)]
+        bgr = torch.stack([gb[r, j] for r, j in order])
+        dep = torch.stack([gd[r, j] for r, j in order])
+        del gb, gd, lb, ld
+    else:
+        bgr = torch.from_numpy(pb).to(dev)
+        dep = torch.from_numpy(pd).to(dev)
+    del pb, pd
+    Lp = dict(t_wc=np.stack([p[1] for p in poses]), R_wc=np.stack([p[0] for p in poses]))
+    hdep_all = dep.cpu().numpy()  # the tracker keeps host copies of live frames' depth
+    hdep = [hdep_all[i] for i in range(n_path)]
+    Lp["depth"] = hdep_all
+    progress(f"{n_path}-frame drive rendered ({len(mine)} frames on this rank)")
+    L = synth.loop_sequence(LOOP_FRAMES, workers=workers)  # config[3]: the closed loop
 
     ctx = vslam_abi.Context(local if world > 1 else 0)
     slam = vslam_abi.Slam(ctx, max_batch=B)
@@ -544,8 +644,7 @@ def main():
 
     def step(k):
         g0 = k * B
-        i0 = g0 % U
-        return slam.process_batch_dev(B, bgr[i0].data_ptr(), dep[i0].data_ptr(), hdep[i0:i0 + B],
+        return slam.process_batch_dev(B, bgr[g0].data_ptr(), dep[g0].data_ptr(), hdep[g0:g0 + B],
                                       [T0 + 0.1 * (g0 + j) for j in range(B)], [3 * (g0 + j) for j in range(B)])
 
     progress(f"sequence rendered, tracker ready; {args.warmup} warmup steps")
@@ -554,7 +653,7 @@ def main():
         # never across the warmup / timed boundary: every timed batch is extracted inside the timed region
         for k in range(k0, k1):
             if k + 1 < k1:
-                i1 = ((k + 1) * B) % U
+                i1 = (k + 1) * B
                 slam.prefetch_batch_dev(B, bgr[i1].data_ptr(), dep[i1].data_ptr())
             step(k)
 
@@ -603,9 +702,9 @@ def main():
     # trajectory quality: RTS smoother, then the reference's ATE against the synthetic ground truth
     slam.finish()
     ids, ts, R, t = slam.trajectory()
-    g = np.round((ts - T0) / 0.1).astype(int) % U
-    a = ate.compute_ate(ts, t, ts, L["t_wc"][g])
-    a_se3 = ate.compute_ate(ts, t, ts, L["t_wc"][g], with_scale=False)
+    g = np.round((ts - T0) / 0.1).astype(int)
+    a = ate.compute_ate(ts, t, ts, Lp["t_wc"][g])
+    a_se3 = ate.compute_ate(ts, t, ts, Lp["t_wc"][g], with_scale=False)
     stats = slam.stats_dict()
     dense_points = dense.size()
     ate_t = torch.tensor([a["ate_rmse"]], dtype=torch.float64, device=dev)
@@ -678,10 +777,12 @@ def main():
     fe = None
     progress("config[3] batch front end")
     if not args.no_frontend and args.frontend_steps > 0:
-        fe = frontend_batch(ctx, L, B, rank, world, args.frontend_steps, 2)
-        mroof["frontend_batch"] = match_roofline(fe.pop("_match"), B, 256,
-                                                 f"config[3] batch front end's last step: {B} consecutive pairs per "
-                                                 "launch on the resident descriptors, alone on the whole chip")
+        fe = frontend_batch(ctx, L, args.frontend_frames, rank, world, args.frontend_steps, 1)
+        P = fe.pop("_match_pairs")
+        mroof["frontend_batch"] = match_roofline(fe.pop("_match"), P, 256,
+                                                 f"config[3] batch front end's last step: {P} consecutive pairs of the "
+                                                 "block per launch on the resident descriptors, alone on the whole "
+                                                 f"chip (the pipeline's launches: {args.frontend_frames} pairs)")
         inp = fe.pop("_match_in_pipeline")
         if mroof["frontend_batch"] and inp and inp[1]:
             mroof["frontend_batch"]["in_pipeline_avg_launch_us"] = round(inp[0] * 1e3 / inp[1], 2)
@@ -700,7 +801,8 @@ def main():
         cpu = None
         if not args.no_cpu_baseline and world == 1:
             progress("cpu baseline")
-            cpu = cpu_baseline(L, args.cpu_frames, lba_problem)
+            cpu = cpu_baseline(dict(bgr=bgr[:args.cpu_frames].cpu().numpy(), depth=hdep_all[:args.cpu_frames]),
+                               args.cpu_frames, lba_problem)
             if lba is not None and cpu.get("local_ba"):
                 lba["cpu_ms_per_call_1thread"] = cpu["local_ba"]["ms_per_call"]
         result = {
@@ -721,7 +823,11 @@ def main():
                 "workload": "config[1]: 640x480 RGB-D stream, end-to-end Slam::process_frame per processed frame "
                             "(HIP SuperPoint extract + match + F-RANSAC + 3D-3D/E motion + EKF + local-map tracking "
                             "+ PnP + keyframes + loop closure every 200 keyframes, RTS at the end) and the main "
-                            "loop's dense voxel fusion of every processed frame (main.cpp:1116-1139)",
+                            "loop's dense voxel fusion of every processed frame (main.cpp:1116-1139), on a "
+                            f"non-repeating {n_path}-frame Pioneer-like drive (synth.pioneer_trajectory: the "
+                            "reference sequence's 848 processed frames or more; every tracked frame distinct)",
+                "path_frames": n_path,
+                "timed_frames_distinct": frames_timed,
                 "frames_per_gpu_per_step": B,
                 "resolution": "640x480",
                 "max_keypoints": 400,
@@ -739,6 +845,7 @@ def main():
                             "without a common motion, 0.7 px, 3 % depth dropouts) the same tracker holds 5-7 mm "
                             "(tests/test_tracker_noisy.py: 58 % wrong over 300 frames, 36 % over 848)"},
             "tracker_stats": stats,
+            "map_points": stats.get("map_points"), "keyframes": stats.get("keyframes"),
             "nms_ties": dict(ties, note="per timed frame (vs_nms_tie_stats): window / cut ties can change the keypoint "
                                         "set vs the reference's unstable std::sort (FeatureExtractor.cpp:238), order "
                                         "ties only the order of equal-score keypoints in the list; zero = identical "
@@ -761,9 +868,13 @@ def main():
                 "avg_launch_ms": round(avg_s * 1e3, 4),
                 "frames_per_launch": round(frames_per_launch, 3),
                 "flops_per_launch": round(flops_per_launch),
-                "flops_unit": "FLOPs the matrix cores execute (Winograd F(2x2, 3x3): 16 products per 2x2 output "
-                              "tile, input and output channel); conv1a (1 -> 64, vector ALUs) not counted",
-                "algorithm": "Winograd F(2x2, 3x3), fp32 (sp_net.hip k_wino3)" if WINO else
+                "flops_unit": ("FLOPs the matrix cores execute (Winograd F(4x4, 3x3): 36 products per 4x4 output "
+                               "tile, input and output channel); conv1a (1 -> 64, vector ALUs) not counted")
+                if WINO4 and dom in WINO4_LAYERS else
+                ("FLOPs the matrix cores execute (Winograd F(2x2, 3x3): 16 products per 2x2 output tile, input "
+                 "and output channel); conv1a (1 -> 64, vector ALUs) not counted"),
+                "algorithm": ("Winograd F(4x4, 3x3), fp32 (wino4.hip k_wino4)" if WINO4 and dom in WINO4_LAYERS else
+                              "Winograd F(2x2, 3x3), fp32 (sp_net.hip k_wino3)") if WINO else
                              "direct implicit GEMM, fp32",
                 "effective_flops_per_launch": round(eff_flops_per_launch),
                 "effective_achieved": round(eff_achieved, 3),

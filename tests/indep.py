@@ -118,6 +118,11 @@ def epnp(X, uv, K):
     n = len(X)
     c0 = X.mean(0)
     evals, evecs = np.linalg.eigh((X - c0).T @ (X - c0))
+    # principal axes with their largest-magnitude component positive (the library's convention;
+    # the signs are arbitrary in cv::SVD, but they decide the control points and so M)
+    for c in range(3):
+        if evecs[np.argmax(np.abs(evecs[:, c])), c] < 0:
+            evecs[:, c] = -evecs[:, c]
     order = np.argsort(evals)[::-1]
     cw = [c0] + [c0 + math.sqrt(max(evals[o], 0.0) / n) * evecs[:, o] for o in order]
     cw = np.array(cw)
@@ -133,6 +138,15 @@ def epnp(X, uv, K):
             M[2 * i + 1, 3 * j:3 * j + 3] = [0.0, alphas[i, j] * K[1], alphas[i, j] * (K[3] - uv[i, 1])]
     w, V = np.linalg.eigh(M.T @ M)
     v = [V[:, np.argsort(w)[k]] for k in range(4)]  # k-th smallest eigenvalue
+    if n <= 5:
+        # A 4- or 5-point M has a null space of dimension 12 - 2n >= 2, in which any solver's basis
+        # is arbitrary (cv::SVD's follows rounding) and the N = 2 / 3 approximations depend on it.
+        # The library takes the Householder QR basis of M^T (LAPACK's dgeqrf sign convention):
+        # null vectors Q e_{2n}, Q e_{2n+1}, ..., then the eigenvectors of the smallest nonzero
+        # eigenvalues; numpy's QR of the same M^T gives the same basis to rounding.
+        Q, _ = np.linalg.qr(M.T, mode="complete")
+        nz = 12 - 2 * n
+        v = [Q[:, 2 * n + k] for k in range(nz)] + [V[:, np.argsort(w)[k]] for k in range(nz, 4)]
     pairs = [(0, 1), (0, 2), (0, 3), (1, 2), (1, 3), (2, 3)]
     L = np.zeros((6, 10))
     rho = np.zeros(6)

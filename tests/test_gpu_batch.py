@@ -75,3 +75,37 @@ def test_batch_c_abi_equals_device_pipeline(vsctx, frames, pipeline_results, mod
             assert np.array_equal(r["eR"].reshape(B, 9)[e], p["eR"].reshape(B, 9)[e])
             assert np.array_equal(r["escale"][e], p["escale"][e])
             assert r["ok"][1:].sum() >= B - 3  # the pairs inside the block track on this sequence
+
+
+@pytest.mark.parametrize("mode", ["none", "ring"])
+def test_batch_submit_collect_pipelined_equals_steps(vsctx, frames, pipeline_results, mode):
+    """vs_batch_submit_dev / vs_batch_collect with two steps in flight (step k + 1's network beside step
+    k's geometry, round 5) give the same pair motions as the synchronous steps; a third submit while
+    two are in flight, and a collect with none, are refused."""
+    dev = torch.device("cuda", 0)
+    bgr, dep = frames
+    with_comm = mode != "none"
+    fr = [torch.from_numpy(bgr[k * B:(k + 1) * B]).to(dev) for k in range(STEPS)]
+    de = [torch.from_numpy(dep[k * B:(k + 1) * B]).to(dev) for k in range(STEPS)]
+    s = torch.cuda.current_stream().cuda_stream
+    torch.cuda.synchronize()
+    with vslam_abi.Batch(vsctx, B, uid=vslam_abi.batch_unique_id() if with_comm else None) as bt:
+        with pytest.raises(vslam_abi.VSError, match="no step in flight"):
+            bt.collect()
+        halo = lambda k: de[k - 1][-1].data_ptr() if (with_comm and k > 0) else None
+        bt.submit_dev(fr[0].data_ptr(), de[0].data_ptr(), halo(0), 0, s)
+        bt.submit_dev(fr[1].data_ptr(), de[1].data_ptr(), halo(1), B, s)
+        with pytest.raises(vslam_abi.VSError, match="in flight"):
+            bt.submit_dev(fr[2].data_ptr(), de[2].data_ptr(), halo(2), 2 * B, s)
+        out = [bt.collect()]
+        bt.submit_dev(fr[2].data_ptr(), de[2].data_ptr(), halo(2), 2 * B, s)
+        out += [bt.collect(), bt.collect()]
+    for k in range(STEPS):
+        r, p = out[k], pipeline_results[k]
+        assert np.array_equal(r["ok"], p["ok"]) and np.array_equal(r["eok"], p["eok"])
+        assert np.array_equal(r["n_good"], p["n_good"])
+        assert np.array_equal(r["R"].reshape(B, 9)[r["ok"] == 1], p["R"].reshape(B, 9)[p["ok"] == 1])
+        assert np.array_equal(r["t"][r["ok"] == 1], p["t"][p["ok"] == 1])
+        e = r["eok"] == 1
+        assert np.array_equal(r["eR"].reshape(B, 9)[e], p["eR"].reshape(B, 9)[e])
+        assert np.array_equal(r["escale"][e], p["escale"][e])

@@ -30,6 +30,32 @@ def test_pnp_independent_equals_oracle(oracle, n, seed, noise, out):
         assert _rot_angle(Rw, R.T) < 1e-6
 
 
+@pytest.mark.parametrize("seed", [202, 5, 7])
+def test_epnp_hypotheses_independent_equal_oracle(oracle, seed):
+    """Every RANSAC hypothesis, not only the winner: EPnP on the cv::RNG 5-point subsets (and
+    4-point problems) equals numpy's restatement to 1e-9.  This holds because both take the same
+    basis of the subset's 2-dimensional null space (the QR basis of M^T from sign-canonical control
+    points, pnp_solvers.h epnp_small_eig) -- the N = 2 / 3 approximations depend on that basis."""
+    from test_oracle_pnp import pnp_problem, cv_rng
+    obj, img, R, t, outl = pnp_problem(150, seed, noise=0.6, outlier_frac=0.3)
+    g, n, worst, count = cv_rng(), len(obj), 0.0, 0
+    for it in range(300):
+        idx = []
+        m = 4 if it % 10 == 9 else 5
+        while len(idx) < m:
+            v = next(g) % n
+            if v not in idx:
+                idx.append(v)
+        ok, Ro, to = oracle.epnp(obj[idx].astype(np.float64), img[idx].astype(np.float64))
+        r = indep.epnp(obj[idx], img[idx], (525.0, 525.0, 319.5, 239.5))
+        assert bool(ok) == (r is not None)
+        if r is None:
+            continue
+        count += 1
+        worst = max(worst, np.abs(Ro - r[0]).max(), np.abs(to - r[1]).max() / max(1.0, np.abs(r[1]).max()))
+    assert count > 250 and worst < 1e-9
+
+
 @pytest.mark.parametrize("n,seed,noise,out", [(80, 203, 0.0, 0.0), (200, 204, 0.5, 0.35), (14, 205, 0.4, 0.0)])
 def test_fundamental_independent_equals_oracle(oracle, n, seed, noise, out):
     from test_oracle_fmat import two_view

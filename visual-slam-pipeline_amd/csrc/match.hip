@@ -99,6 +99,8 @@ struct MatchArgs {
     const int* n;          // rows per frame
     int qstride, tstride;
     int qblocks, tblocks;  // grid extents per pair (capacity)
+    int qfull, tfull;      // blocks whole at capacity (largest-first order; 0: pair-major order)
+    int npairs;
     int work, per_xcd;     // P * qblocks * tblocks; blocks per XCD range
     float ratio;
     unsigned long long* keys;  // [P][2][kcap]
@@ -138,9 +140,32 @@ __global__ __launch_bounds__(64 * NWQ * NWT) void k_match(MatchArgs a) {
     // linear work index: XCD x (= blockIdx % 8 under round-robin placement) takes a contiguous range
     const int L = (blockIdx.x & 7) * a.per_xcd + (blockIdx.x >> 3);
     if (L >= a.work) return;
+    // largest first (round 5): the workgroups whose tiles are whole at capacity come first, pair by
+    // pair, and the edge tiles (the last query / train block of a 400-row frame holds 16 rows) after
+    // them, so that the grid's last dispatch wave is made of short workgroups and the launch's tail is
+    // shorter; a.qfull / a.tfull = 0 keeps the plain pair-major order
     const int per_pair = a.qblocks * a.tblocks;
-    const int p = L / per_pair, r0 = L - p * per_pair;
-    const int qb = r0 / a.tblocks, tb = r0 - qb * a.tblocks;
+    int p, qb, tb;
+    const int nfull = a.qfull * a.tfull;
+    if (nfull == 0) {
+        p = L / per_pair;
+        const int r0 = L - p * per_pair;
+        qb = r0 / a.tblocks, tb = r0 - qb * a.tblocks;
+    } else if (L < a.npairs * nfull) {
+        p = L / nfull;
+        const int r0 = L - p * nfull;
+        qb = r0 / a.tfull, tb = r0 - qb * a.tfull;
+    } else {
+        const int edges = per_pair - nfull, L2 = L - a.npairs * nfull;
+        p = L2 / edges;
+        const int e = L2 - p * edges, rows = (a.qblocks - a.qfull) * a.tblocks;
+        if (e < rows) {
+            qb = a.qfull + e / a.tblocks, tb = e - (e / a.tblocks) * a.tblocks;
+        } else {
+            const int e2 = e - rows, tw = a.tblocks - a.tfull;
+            qb = e2 / tw, tb = a.tfull + e2 - (e2 / tw) * tw;
+        }
+    }
     const int qf = a.pairs[2 * p], tf = a.pairs[2 * p + 1];
     const int n1 = a.n[qf], n2 = a.n[tf];
     const int tid = threadIdx.x;
@@ -495,6 +520,19 @@ static void launch_tile(MatchArgs& a, int P, int cap_q, int cap_t, bool norms, h
     a.qblocks = (cap_q + TQ - 1) / TQ;
     a.tblocks = (cap_t + TT - 1) / TT;
     a.work = P * a.qblocks * a.tblocks;
+    a.npairs = P;
+    // largest-first order for multi-pair launches whose capacity leaves edge tiles: opt-in
+    // (VS_MATCH_ORDER=1), measured slower -- 318 pairs 0.463 vs 0.495 of peak pair-major, 512 pairs
+    // 0.485 vs 0.524 (profiles/r05h_match_order_ab.txt): the edge tiles' short blocks interleaved with
+    // whole ones fill the CUs better than a tail of edge tiles alone
+    static const bool lf = [] {
+        const char* e = std::getenv("VS_MATCH_ORDER");
+        return e && e[0] == '1';
+    }();
+    const int qf = cap_q / TQ, tf = cap_t / TT;
+    const bool edges = qf * tf < a.qblocks * a.tblocks;
+    a.qfull = (lf && P > 2 && edges && qf > 0 && tf > 0) ? qf : 0;
+    a.tfull = a.qfull ? tf : 0;
     a.per_xcd = (a.work + 7) / 8;
     const unsigned blocks = (unsigned)(8 * a.per_xcd);
     static const char* abl = std::getenv("VS_MATCH_ABLATE");  // latency study only

@@ -30,11 +30,6 @@ using namespace vs_pnp;
 
 constexpr int kPnpMaxIters = VS_PNP_MAX_ITERS;
 
-#ifndef VS_PNP_JACOBI
-#define VS_PNP_JACOBI 2  // 0: the round-2 single-copy Jacobi (shuffled angles, two barriers per round); 1: every lane its two angles;
-                         // 2: ping-pong, each angle computed once (lanes 36..41) and read from LDS (1 -> 2: Jacobi -7 %)
-#endif
-
 #ifdef VS_PNP_PROFILE
 // k_pnp_hyp phase cycle counters (profiling build only: make -C visual-slam-pipeline_amd prof)
 __device__ unsigned long long g_pnp_cycles[16];  // 0-5 k_pnp_hyp, 6-7 k_pnp_ransac, 8-12 its LM split
@@ -97,6 +92,239 @@ __device__ __attribute__((noinline)) bool epnp_subset(const float* obj, const fl
 
 __device__ inline bool pnp_problem_runs(int n, int min_inliers, int model_points) {
     return !(n < min_inliers || n < 4) && n != model_points;
+}
+
+// a lane's double, read by the whole wave (static lane index: two v_readlane into SGPRs)
+__device__ __forceinline__ double lane_bcast(double x, int src) {
+    const unsigned long long b = (unsigned long long)__double_as_longlong(x);
+    const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)b, src);
+    const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(b >> 32), src);
+    return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+
+struct EpShared {
+    double R[10][10];  // R of M^T = Q R (upper triangle)
+    double B[10][10];  // R R^T
+    double U[8][10];   // tridiagonal reflectors (indices k+1..9), tt their taus
+    double tt[8];
+    double v[4][12];   // the four eigenvectors (pnp_solvers.h epnp_small_eig's v)
+};
+
+// pnp_solvers.h epnp_small_eig spread over one wave, bit-identical to it: lane j < 2m keeps column j
+// of M^T in registers through the QR (each reflector read by the wave with v_readlane), lanes a <= b
+// form B = R R^T from LDS, lane i < 10 keeps row i of B through the tridiagonalisation (B stays
+// exactly symmetric, so a lane's own reflector entry is its column k), lanes 0-31 / 32-63 run the
+// multisection for the smallest / second smallest eigenvalue (one Sturm count per lane, a ballot
+// picks the subinterval), lanes 0 / 1 the inverse iterations, lanes 0-3 the back-transformations.
+__device__ __forceinline__ void epnp_small_eig_wave(const double (*al)[4], const double* uv, int m, const Cam& K,
+                                                    int lane, EpShared& S) {
+    const int nc = 2 * m;
+    double c[12];
+#pragma unroll
+    for (int r = 0; r < 12; r++) c[r] = lane < nc ? ep_mt(al, uv, K, lane, r) : 0.0;
+    double my_alpha = 0, my_tau = 0;
+    // 1. QR of M^T
+#pragma unroll
+    for (int k = 0; k < 10; k++) {
+        if (k >= nc) continue;  // (m = 4: 8 columns; not break: the loop must unroll for static k)
+        double s = 0;
+#pragma unroll
+        for (int r = k; r < 12; r++) s += c[r] * c[r];
+        double alpha, u0, tau;
+        ep_householder(s, c[k], alpha, u0, tau);
+        if (lane == k) {
+            c[k] = u0;
+            my_alpha = alpha;
+            my_tau = tau;
+        }
+        double u[12];
+#pragma unroll
+        for (int r = k; r < 12; r++) u[r] = lane_bcast(c[r], k);
+        const double tk = lane_bcast(tau, k);
+        if (lane > k && lane < nc) {
+            double w = 0;
+#pragma unroll
+            for (int r = k; r < 12; r++) w += u[r] * c[r];
+            const double f = tk * w;
+#pragma unroll
+            for (int r = k; r < 12; r++) c[r] = c[r] - f * u[r];
+        }
+    }
+    double x[12];  // lanes 0..3: the vectors mapped back through Q
+    const int nz = nc == 10 ? 2 : 4;
+#pragma unroll
+    for (int r = 0; r < 12; r++) x[r] = (lane < nz && r == nc + lane) ? 1.0 : 0.0;
+    if (nc == 10) {
+        // 2. B = R R^T
+        if (lane < 10) {
+#pragma unroll
+            for (int a = 0; a < 10; a++) S.R[a][lane] = a < lane ? c[a] : a == lane ? my_alpha : 0.0;
+        }
+        __syncthreads();
+        if (lane < 55) {  // upper-triangle element (a, b), a <= b
+            int a = 0, rem = lane;
+            while (rem >= 10 - a) {
+                rem -= 10 - a;
+                a++;
+            }
+            const int b = a + rem;
+            double s = 0;
+#pragma unroll
+            for (int k = 0; k < 10; k++)
+                if (k >= b) s += S.R[a][k] * S.R[b][k];
+            S.B[a][b] = s;
+            S.B[b][a] = s;
+        }
+        __syncthreads();
+        // tridiagonalisation
+        double br[10];
+#pragma unroll
+        for (int j = 0; j < 10; j++) br[j] = lane < 10 ? S.B[lane][j] : 0.0;
+        double d[10], e[9];
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+            double s = 0;
+#pragma unroll
+            for (int j = k + 1; j < 10; j++) s += br[j] * br[j];
+            double alpha, u0, t;
+            ep_householder(s, br[k + 1], alpha, u0, t);
+            e[k] = lane_bcast(alpha, k);
+            d[k] = lane_bcast(br[k], k);
+            const double tk = lane_bcast(t, k);
+            double U[10];
+            U[k + 1] = lane_bcast(u0, k);
+#pragma unroll
+            for (int j = k + 2; j < 10; j++) U[j] = lane_bcast(br[j], k);
+            if (lane == k) {
+#pragma unroll
+                for (int j = k + 1; j < 10; j++) S.U[k][j] = U[j];
+                S.tt[k] = tk;
+            }
+            const bool act = lane > k && lane < 10;
+            const double uo = lane == k + 1 ? U[k + 1] : br[k];  // this row's reflector entry (B symmetric)
+            double p = 0;
+            if (act) {
+                double q = 0;
+#pragma unroll
+                for (int j = k + 1; j < 10; j++) q += br[j] * U[j];
+                p = tk * q;
+            }
+            double pv = 0;
+#pragma unroll
+            for (int i = k + 1; i < 10; i++) pv += lane_bcast(p, i) * U[i];
+            const double Kc = (0.5 * tk) * pv;
+            const double w = p - Kc * uo;
+            double wj[10];
+#pragma unroll
+            for (int j = k + 1; j < 10; j++) wj[j] = lane_bcast(w, j);
+            if (act) {
+#pragma unroll
+                for (int j = k + 1; j < 10; j++) br[j] = br[j] - (uo * wj[j] + w * U[j]);
+            }
+        }
+        d[8] = lane_bcast(br[8], 8);
+        d[9] = lane_bcast(br[9], 9);
+        e[8] = lane_bcast(br[9], 8);
+        // 3. multisection: lanes 0-31 the smallest eigenvalue, 32-63 the second smallest
+        double e2[9], lo = 0, hi = 0;
+#pragma unroll
+        for (int i = 0; i < 9; i++) e2[i] = e[i] * e[i];
+#pragma unroll
+        for (int i = 0; i < 10; i++) {
+            const double rad = (i > 0 ? fabs(e[i - 1]) : 0.0) + (i < 9 ? fabs(e[i]) : 0.0);
+            const double l = d[i] - rad, h = d[i] + rad;
+            lo = (i == 0 || l < lo) ? l : lo;
+            hi = (i == 0 || h > hi) ? h : hi;
+        }
+        const int tsel = lane >> 5;
+        const double fj = ep_frac(lane & 31);
+        double a0 = lo, b0 = hi, a1 = lo, b1 = hi;
+        for (int st = 0; st < kEpMsSteps; st++) {
+            const double a = tsel ? a1 : a0, wd = tsel ? b1 - a1 : b0 - a0;
+            const bool above = ep_sturm(d, e2, a + wd * fj) > tsel;
+            const unsigned long long bal = __ballot(above);
+            const unsigned m0 = (unsigned)bal, m1 = (unsigned)(bal >> 32);
+            const int j0 = m0 ? __builtin_ctz(m0) : kEpMsPts, j1 = m1 ? __builtin_ctz(m1) : kEpMsPts;
+            const double w0 = b0 - a0, w1 = b1 - a1;
+            const double na0 = j0 > 0 ? a0 + w0 * ep_frac(j0 - 1) : a0;
+            const double nb0 = j0 < kEpMsPts ? a0 + w0 * ep_frac(j0) : b0;
+            const double na1 = j1 > 0 ? a1 + w1 * ep_frac(j1 - 1) : a1;
+            const double nb1 = j1 < kEpMsPts ? a1 + w1 * ep_frac(j1) : b1;
+            a0 = na0;
+            b0 = nb0;
+            a1 = na1;
+            b1 = nb1;
+        }
+        // 4. inverse iteration, lane t for eigenvalue t
+        const double fa = fabs(lo), fb = fabs(hi);
+        const double tnorm = fa > fb ? fa : fb;
+        const double tiny = tnorm > 0 ? DBL_EPSILON * tnorm : DBL_MIN;
+        const double lam0 = 0.5 * (a0 + b0), lam1 = 0.5 * (a1 + b1);
+        const bool cluster = lam1 - lam0 <= 1e-3 * tnorm;
+        double y[10];
+        if (lane < 2) {
+            EpLu f;
+            ep_lu(d, e, lane ? lam1 : lam0, tiny, f);
+#pragma unroll
+            for (int i = 0; i < 10; i++) y[i] = ep_start(i);
+            for (int it = 0; it < kEpInvIters; it++) {
+                ep_lu_solve(f, y);
+                ep_normalize10(y);
+                if (cluster) {
+                    double y0[10];
+#pragma unroll
+                    for (int i = 0; i < 10; i++) y0[i] = lane_bcast(y[i], 0);
+                    if (lane == 1) {
+                        double dt = 0;
+#pragma unroll
+                        for (int i = 0; i < 10; i++) dt += y0[i] * y[i];
+#pragma unroll
+                        for (int i = 0; i < 10; i++) y[i] = y[i] - dt * y0[i];
+                        ep_normalize10(y);
+                    }
+                }
+            }
+            // back through the tridiagonal reflectors
+#pragma unroll
+            for (int k = 7; k >= 0; k--) {
+                double w = 0;
+#pragma unroll
+                for (int i = k + 1; i < 10; i++) w += S.U[k][i] * y[i];
+                const double fk = S.tt[k] * w;
+#pragma unroll
+                for (int i = k + 1; i < 10; i++) y[i] = y[i] - fk * S.U[k][i];
+            }
+        }
+        double yt[10];
+#pragma unroll
+        for (int i = 0; i < 10; i++) {
+            const double y0 = lane_bcast(y[i], 0), y1 = lane_bcast(y[i], 1);
+            yt[i] = lane == 2 ? y0 : y1;
+        }
+        if (lane == 2 || lane == 3) {
+#pragma unroll
+            for (int r = 0; r < 10; r++) x[r] = yt[r];
+        }
+    }
+    // 5. v = Q x, lanes 0..3
+#pragma unroll
+    for (int k = 9; k >= 0; k--) {
+        if (k >= nc) continue;
+        double u[12];
+#pragma unroll
+        for (int r = k; r < 12; r++) u[r] = lane_bcast(c[r], k);
+        const double tk = lane_bcast(my_tau, k);
+        double w = 0;
+#pragma unroll
+        for (int r = k; r < 12; r++) w += u[r] * x[r];
+        const double fk = tk * w;
+#pragma unroll
+        for (int r = k; r < 12; r++) x[r] = x[r] - fk * u[r];
+    }
+    if (lane < 4) {
+#pragma unroll
+        for (int r = 0; r < 12; r++) S.v[lane][r] = x[r];
+    }
 }
 
 // 1. subsets of the initial budget from the cv::RNG stream (getSubset: repeats rejected); the
@@ -225,27 +453,19 @@ __global__ __launch_bounds__(256) void k_pnp_subsets(const int* __restrict__ off
     }
 }
 
-// 2. one hypothesis per wave64 workgroup: EPnP on its subset with the 12 x 12 eigen-decomposition
-//    spread over the wave (LDS-resident round-robin Jacobi: a round's 6 disjoint rotations run in
-//    parallel with the per-element arithmetic of the sequential sym_eig_rr<12>, so the model is
-//    bit-identical to the host's), the three beta
-//    approximations on lanes 0-2, then the inlier count over all points by the whole wave.
+// 2. one hypothesis per wave64 workgroup: EPnP on its subset with the four smallest eigenvectors
+//    of M^T M spread over the wave (epnp_small_eig_wave: QR null space + tridiagonal multisection and
+//    inverse iteration, bit-identical to the host's epnp_small_eig; round 5, replacing the 12 x 12
+//    round-robin Jacobi), the three beta approximations on lanes 0-2, then the inlier count over all
+//    points by the whole wave.
 __global__ __launch_bounds__(64) void k_pnp_hyp(const float* __restrict__ obj_all, const float* __restrict__ img_all,
                                                 const int* __restrict__ off, double fx, double fy, double cx, double cy,
                                                 int niters0, float thr2, int min_inliers, PnpHyp H) {
     crit_prio();
-#if VS_PNP_JACOBI >= 1
-    __shared__ double sAb[2][144], sVb[2][144];  // ping-pong matrices: one barrier per Jacobi round
-    [[maybe_unused]] __shared__ double sC[6], sS[6];  // VS_PNP_JACOBI 2: the round's angles
-    [[maybe_unused]] __shared__ int sAct[6];
-    double* sA = sAb[0];
-    double* sV = sVb[0];
-#else
-    __shared__ double sA[144], sV[144];
-#endif
+    __shared__ EpShared sE;
     __shared__ double sX[15], sUV[10], sAl[5][4], sCw[4][3];
-    __shared__ double sTot, sOff, sErr[3], sRt[3][12];
-    __shared__ int sOk, sPerm[12];
+    __shared__ double sErr[3], sRt[3][12];
+    __shared__ int sOk;
     const int pb = blockIdx.x, h = blockIdx.y, lane = threadIdx.x;
     const int o0 = off[pb], n = off[pb + 1] - o0;
     const int model_points = n == 4 ? 4 : 5;
@@ -277,261 +497,11 @@ __global__ __launch_bounds__(64) void k_pnp_hyp(const float* __restrict__ obj_al
     PNP_T(0);
     bool ok = sOk != 0;
     if (ok) {
-        for (int e = lane; e < 144; e += 64) {
-            sA[e] = epnp_mtm<5>(sAl, sUV, m, K, e / 12, e % 12);
-            sV[e] = (e / 12 == e % 12) ? 1.0 : 0.0;
-        }
-        __syncthreads();
-        // sym_eig_rr<12> (pnp_solvers.h): the 6 disjoint rotations of each round in parallel
-        if (lane == 0) {
-            double total = 0;
-            for (int i = 0; i < 144; i++) total += sA[i] * sA[i];
-            sTot = total;
-        }
+        // the four smallest eigenvectors of M^T M (pnp_solvers.h epnp_small_eig, spread over the wave)
+        epnp_small_eig_wave(sAl, sUV, m, K, lane, sE);
         __syncthreads();
         PNP_T(1);
-        const double total = sTot;
-#if VS_PNP_JACOBI >= 1
-        // Round-robin Jacobi with the matrices ping-ponged between two LDS copies: every lane of
-        // 0..35 reads its 2 x 2 block (pair a rows i0 < i1, pair b columns j0 < j1), its V entries
-        // (rows 2a, 2a + 1 at the block's columns) and the two diagonal blocks of its pairs from the
-        // round's copy, computes both angles itself (no shuffles; the same inputs as the diagonal
-        // lane's, so the same angles), rotates (column b, then row a, as the sequential statement)
-        // and writes every value to the other copy; one barrier per round.  VS_PNP_JACOBI 2 (the
-        // default): lanes 36..41 compute the round's six angles once (same inputs, same angles) and the
-        // block lanes read theirs from LDS.  Bit-identical to sym_eig_rr<12>.
-        {
-            const int ba = lane / 6, bb = lane % 6;
-            const bool blk = lane < 36;
-            int pk[11];  // the lane's round pairs, packed 4 bits each (rounds unrolled: static indices)
-#pragma unroll
-            for (int r = 0; r < 11; r++) {
-                int a0, a1, b0, b1;
-                rr_pair(12, r, ba, a0, a1);
-                rr_pair(12, r, bb, b0, b1);
-                pk[r] = a0 | a1 << 4 | b0 << 8 | b1 << 12;
-            }
-            int cur = 0;
-            for (int sweep = 0; sweep < 30; sweep++) {
-                if (lane == 0) {
-                    const double* A = sAb[cur];
-                    double o = 0;
-                    for (int p = 0; p < 12; p++)
-                        for (int q = p + 1; q < 12; q++) o += A[p * 12 + q] * A[p * 12 + q];
-                    sOff = o;
-                }
-                __syncthreads();
-                if (!(sOff > 1e-32 * total)) break;
-#pragma unroll
-                for (int r = 0; r < 11; r++) {
-                    const double* A = sAb[cur];
-                    const double* V = sVb[cur];
-                    double* An = sAb[cur ^ 1];
-                    double* Vn = sVb[cur ^ 1];
-#if VS_PNP_JACOBI == 2
-                    if (lane >= 36 && lane < 42) {  // pair k's angle once (the same inputs as every user's)
-                        int p0, q0;
-                        rr_pair(12, r, lane - 36, p0, q0);
-                        double c, sn;
-                        const bool act = jacobi_angle_nb(A[p0 * 12 + p0], A[q0 * 12 + q0], A[p0 * 12 + q0], c, sn);
-                        sC[lane - 36] = c;
-                        sS[lane - 36] = sn;
-                        sAct[lane - 36] = act;
-                    }
-                    __syncthreads();
-#endif
-                    if (blk) {
-                        const int i0 = pk[r] & 15, i1 = (pk[r] >> 4) & 15, j0 = (pk[r] >> 8) & 15, j1 = pk[r] >> 12;
-                        double x00 = A[i0 * 12 + j0], x01 = A[i0 * 12 + j1], x10 = A[i1 * 12 + j0], x11 = A[i1 * 12 + j1];
-                        const double p0 = V[(2 * ba) * 12 + j0], q0 = V[(2 * ba) * 12 + j1];
-                        const double p1 = V[(2 * ba + 1) * 12 + j0], q1 = V[(2 * ba + 1) * 12 + j1];
-#if VS_PNP_JACOBI == 2
-                        const double ca = sC[ba], sa = sS[ba], cb = sC[bb], sb = sS[bb];
-                        const bool acta = sAct[ba] != 0, actb = sAct[bb] != 0;
-#else
-                        // both angles branch-free (jacobi_angle_nb) and the skipped rotations as
-                        // selects: one straight-line block per round, the two angle chains interleaved
-                        double ca, sa, cb, sb;
-                        const bool acta = jacobi_angle_nb(A[i0 * 12 + i0], A[i1 * 12 + i1], A[i0 * 12 + i1], ca, sa);
-                        const bool actb = jacobi_angle_nb(A[j0 * 12 + j0], A[j1 * 12 + j1], A[j0 * 12 + j1], cb, sb);
-#endif
-                        {
-                            const double y00 = cb * x00 - sb * x01, y01 = sb * x00 + cb * x01;
-                            const double y10 = cb * x10 - sb * x11, y11 = sb * x10 + cb * x11;
-                            x00 = actb ? y00 : x00;
-                            x01 = actb ? y01 : x01;
-                            x10 = actb ? y10 : x10;
-                            x11 = actb ? y11 : x11;
-                        }
-                        {
-                            const double y00 = ca * x00 - sa * x10, y10 = sa * x00 + ca * x10;
-                            const double y01 = ca * x01 - sa * x11, y11 = sa * x01 + ca * x11;
-                            x00 = acta ? y00 : x00;
-                            x01 = acta ? y01 : x01;
-                            x10 = acta ? y10 : x10;
-                            x11 = acta ? y11 : x11;
-                        }
-                        An[i0 * 12 + j0] = x00;
-                        An[i0 * 12 + j1] = x01;
-                        An[i1 * 12 + j0] = x10;
-                        An[i1 * 12 + j1] = x11;
-                        const double v0 = cb * p0 - sb * q0, w0 = sb * p0 + cb * q0;
-                        const double v1 = cb * p1 - sb * q1, w1 = sb * p1 + cb * q1;
-                        Vn[(2 * ba) * 12 + j0] = actb ? v0 : p0;
-                        Vn[(2 * ba) * 12 + j1] = actb ? w0 : q0;
-                        Vn[(2 * ba + 1) * 12 + j0] = actb ? v1 : p1;
-                        Vn[(2 * ba + 1) * 12 + j1] = actb ? w1 : q1;
-                    }
-                    cur ^= 1;
-                    __syncthreads();
-                }
-            }
-            sA = sAb[cur];
-            sV = sVb[cur];
-        }
-#else
-        for (int sweep = 0; sweep < 30; sweep++) {
-            if (lane == 0) {
-                double o = 0;
-                for (int p = 0; p < 12; p++)
-                    for (int q = p + 1; q < 12; q++) o += sA[p * 12 + q] * sA[p * 12 + q];
-                sOff = o;
-            }
-            __syncthreads();
-            if (!(sOff > 1e-32 * total)) break;
-            // Each lane of 0..35 keeps one 2 x 2 block of A in registers for the round: (pair a rows
-            // i0 < i1, pair b columns j0 < j1), a = lane / 6, b = lane % 6.  The diagonal-block lanes
-            // (a == b) compute the round's angles from their registers and shuffle them out; every
-            // block takes its column rotation (b) and then its row rotation (a) -- per element exactly
-            // the sequential statement's column-then-row order; V's rows 2a, 2a + 1 take the column
-            // rotation of pair b in the same lane; the blocks go back to the LDS matrix and the next
-            // round's blocks are read.
-            const int ba = lane / 6, bb = lane % 6;
-            const bool blk = lane < 36;
-            int i0, i1, j0, j1;
-            double x00 = 0, x01 = 0, x10 = 0, x11 = 0, p0 = 0, q0 = 0, p1 = 0, q1 = 0;
-            // the round's A block and the V entries (rows 2a, 2a + 1 at the block's columns)
-            int pk[11];  // the lane's round pairs, packed 4 bits each (rounds unrolled: static indices)
-#pragma unroll
-            for (int r = 0; r < 11; r++) {
-                int a0, a1, b0, b1;
-                rr_pair(12, r, ba, a0, a1);
-                rr_pair(12, r, bb, b0, b1);
-                pk[r] = a0 | a1 << 4 | b0 << 8 | b1 << 12;
-            }
-            auto load_blk = [&](int r) {
-                i0 = pk[r] & 15;
-                i1 = (pk[r] >> 4) & 15;
-                j0 = (pk[r] >> 8) & 15;
-                j1 = pk[r] >> 12;
-                x00 = sA[i0 * 12 + j0];
-                x01 = sA[i0 * 12 + j1];
-                x10 = sA[i1 * 12 + j0];
-                x11 = sA[i1 * 12 + j1];
-                p0 = sV[(2 * ba) * 12 + j0];
-                q0 = sV[(2 * ba) * 12 + j1];
-                p1 = sV[(2 * ba + 1) * 12 + j0];
-                q1 = sV[(2 * ba + 1) * 12 + j1];
-            };
-            if (blk) load_blk(0);
-#pragma unroll
-            for (int r = 0; r < 11; r++) {
-                double c = 1.0, sn = 0.0;
-                int act = 0;
-                if (blk && ba == bb) act = jacobi_angle(x00, x11, x01, c, sn);  // (A[p][p], A[q][q], A[p][q])
-                const double ca = __shfl(c, 7 * ba), sa = __shfl(sn, 7 * ba);
-                const double cb = __shfl(c, 7 * bb), sb = __shfl(sn, 7 * bb);
-                const int acta = __shfl(act, 7 * ba), actb = __shfl(act, 7 * bb);
-                if (blk) {
-                    if (actb) {
-                        const double y00 = cb * x00 - sb * x01, y01 = sb * x00 + cb * x01;
-                        const double y10 = cb * x10 - sb * x11, y11 = sb * x10 + cb * x11;
-                        x00 = y00;
-                        x01 = y01;
-                        x10 = y10;
-                        x11 = y11;
-                    }
-                    if (acta) {
-                        const double y00 = ca * x00 - sa * x10, y10 = sa * x00 + ca * x10;
-                        const double y01 = ca * x01 - sa * x11, y11 = sa * x01 + ca * x11;
-                        x00 = y00;
-                        x01 = y01;
-                        x10 = y10;
-                        x11 = y11;
-                    }
-                    sA[i0 * 12 + j0] = x00;
-                    sA[i0 * 12 + j1] = x01;
-                    sA[i1 * 12 + j0] = x10;
-                    sA[i1 * 12 + j1] = x11;
-                }
-                // V's rows 2a, 2a + 1 at this block's column pair b take the column rotation the
-                // lane already holds for A (each V entry once per round, no shuffles)
-                if (blk && actb) {
-                    sV[(2 * ba) * 12 + j0] = cb * p0 - sb * q0;
-                    sV[(2 * ba) * 12 + j1] = sb * p0 + cb * q0;
-                    sV[(2 * ba + 1) * 12 + j0] = cb * p1 - sb * q1;
-                    sV[(2 * ba + 1) * 12 + j1] = sb * p1 + cb * q1;
-                }
-                __syncthreads();
-                if (blk && r + 1 < 11) load_blk(r + 1);  // the next round's block
-                __syncthreads();
-            }
-        }
-#endif
         PNP_T(2);
-        // eigenvalues in descending order, columns of V swapped along (sym_eig_rr's selection
-        // sort): lane 0 runs the sort on the eigenvalues and a column index, the wave moves the
-        // columns once (the same moves as swapping them step by step)
-        if (lane == 0) {
-            double w[12];
-            int pm[12];
-#pragma unroll
-            for (int i = 0; i < 12; i++) {
-                w[i] = sA[i * 12 + i];
-                pm[i] = i;
-            }
-#pragma unroll
-            for (int i = 0; i < 11; i++) {
-                int mx = i;
-                double wm = w[i];
-#pragma unroll
-                for (int j = i + 1; j < 12; j++)
-                    if (w[j] > wm) {
-                        mx = j;
-                        wm = w[j];
-                    }
-                // swap entries i and mx with compile-time indices only (the arrays stay in registers)
-                int pmx = pm[i];
-#pragma unroll
-                for (int j = i + 1; j < 12; j++) pmx = j == mx ? pm[j] : pmx;
-#pragma unroll
-                for (int j = i + 1; j < 12; j++)
-                    if (j == mx) {
-                        w[j] = w[i];
-                        pm[j] = pm[i];
-                    }
-                w[i] = wm;
-                pm[i] = pmx;
-            }
-#pragma unroll
-            for (int i = 0; i < 12; i++) sPerm[i] = pm[i];
-        }
-        __syncthreads();
-        {
-            double tv[3];
-#pragma unroll
-            for (int u = 0; u < 3; u++) {
-                const int e = lane + 64 * u;
-                if (e < 144) tv[u] = sV[(e / 12) * 12 + sPerm[e % 12]];
-            }
-            __syncthreads();
-#pragma unroll
-            for (int u = 0; u < 3; u++) {
-                const int e = lane + 64 * u;
-                if (e < 144) sV[e] = tv[u];
-            }
-        }
-        __syncthreads();
         PNP_T(3);
         if (lane < 3) {  // one beta approximation per lane
             double cw[4][3], v[4][12], L[6][10], rho[6], al[5][4], X[15], uv[10];
@@ -546,7 +516,11 @@ __global__ __launch_bounds__(64) void k_pnp_hyp(const float* __restrict__ obj_al
             for (int i = 0; i < 15; i++) X[i] = i < 3 * m ? sX[i] : 0.0;
 #pragma unroll
             for (int i = 0; i < 10; i++) uv[i] = i < 2 * m ? sUV[i] : 0.0;
-            epnp_L_rho(sV, cw, v, L, rho);
+#pragma unroll
+            for (int k = 0; k < 4; k++)
+#pragma unroll
+                for (int i = 0; i < 12; i++) v[k][i] = sE.v[k][i];
+            epnp_L_rho_v(v, cw, L, rho);
             double R[9], t[3];
             // the three approximations as one code path on lanes 0..2 (pnp_solvers.h
             // epnp_betas_init_uniform: bit-identical to epnp_variant's divergent solves)

@@ -458,6 +458,16 @@ VS_HD inline bool epnp_control(const double* X, int n, double cw[4][3], double (
         }
     double dc[3], uc[9];
     sym_eig<3>(C, dc, uc);
+    // Each principal axis with its largest-magnitude component positive (the first on ties): the
+    // control points, hence M and the QR basis of its null space (epnp_small_eig), stop depending
+    // on the eigen-solver's arbitrary signs.
+    for (int i = 0; i < 3; i++) {
+        int r = 0;
+        for (int q = 1; q < 3; q++)
+            if (fabs(uc[q * 3 + i]) > fabs(uc[r * 3 + i])) r = q;
+        if (uc[r * 3 + i] < 0)
+            for (int q = 0; q < 3; q++) uc[q * 3 + i] = -uc[q * 3 + i];
+    }
     for (int i = 1; i < 4; i++) {
         const double k = sqrt((dc[i - 1] > 0 ? dc[i - 1] : 0.0) / n);
         for (int j = 0; j < 3; j++) cw[i][j] = cw[0][j] + k * uc[j * 3 + (i - 1)];
@@ -513,11 +523,268 @@ VS_HD inline double epnp_mtm(const double (*alphas)[4], const double* uv, int n,
     return s;
 }
 
+// ------------------------------------------- the four smallest eigenvectors for m = 4 / 5 points
+// A RANSAC subset has m <= 5 points, so M (2m x 12) has rank <= 2m and M^T M a null space of
+// dimension >= 12 - 2m.  Instead of diagonalising the 12 x 12 M^T M:
+//   1. Householder QR of M^T (12 x 2m) = Q [R; 0]: M^T M = Q diag(R R^T, 0) Q^T, so the last
+//      12 - 2m columns of Q span the null space exactly (m = 4: all four vectors, nothing else);
+//   2. m = 5: the two smallest eigenpairs of B = R R^T (10 x 10): Householder tridiagonalisation
+//      T = H_7..H_0 B H_0..H_7, the two smallest eigenvalues of T by 33-way multisection of the
+//      Sturm count, their vectors by inverse iteration (LU with partial pivoting of T - lambda I,
+//      kEpInvIters steps from a fixed start, Gram-Schmidt against the first when the two are closer
+//      than 1e-3 ||T||), mapped back through the tridiagonal and QR reflectors.
+// v[0], v[1] = null vectors (Q e_10, Q e_11), v[2], v[3] = eigenvectors of the smallest and the
+// second smallest nonzero eigenvalue (m = 4: v[k] = Q e_{8+k}).  The null space is as accurate as M
+// (not M^T M) allows; the eigenvectors within it are an arbitrary orthonormal basis, as any
+// solver's are.  Every step is a fixed sequence of IEEE operations; pnp.hip spreads each over a
+// wave (one lane per column / row / multisection point) without changing any value.
+constexpr int kEpMsSteps = 12;  // multisection steps: 33^12 > 2^60, below the rounding of any interval
+constexpr int kEpMsPts = 32;    // interior points per step and eigenvalue
+constexpr int kEpInvIters = 3;  // inverse iterations
+constexpr double kEpBig = 0x1p256, kEpSmall = 0x1p-256, kEpTiny = 0x1p-200;
+
+// Householder reflector H = I - tau u u^T taking x (sum of squares s, leading entry x0) to alpha e_0;
+// u = (x0 - alpha, x_1, ...), tau = 1 / (|x| (|x| + |x0|)) = 2 / u^T u (0 when x = 0).
+VS_HD inline void ep_householder(double s, double x0, double& alpha, double& u0, double& tau) {
+    const double nrm = sqrt(s);
+    alpha = x0 >= 0 ? -nrm : nrm;
+    u0 = x0 - alpha;
+    tau = s > 0 ? 1.0 / (nrm * (nrm + fabs(x0))) : 0.0;
+}
+
+// entry r of column j of M^T (= row j of M)
+VS_HD inline double ep_mt(const double (*al)[4], const double* uv, const Cam& K, int j, int r) {
+    const int i = j >> 1;
+    return (j & 1) ? epnp_m1(al[i], uv[2 * i + 1], K, r) : epnp_m0(al[i], uv[2 * i], K, r);
+}
+
+// Sturm count of the 10 x 10 tridiagonal (d, e2 = e^2): the number of eigenvalues < x, from the
+// sign changes of the leading principal minors p_i = (d_i - x) p_{i-1} - e2_{i-1} p_{i-2}.  A zero
+// minor becomes -2^-200 p_{i-1} (a tiny pivot of the other sign, as a Sturm / LDL^T count treats
+// it); consecutive minors are rescaled together by 2^-+256 outside [2^-256, 2^256].
+VS_HD inline int ep_sturm(const double* d, const double* e2, double x) {
+    double pp = 1.0, pc = d[0] - x;
+    if (pc == 0) pc = -kEpTiny;
+    int cnt = pc < 0;
+    VS_UNROLL
+    for (int i = 1; i < 10; i++) {
+        double pn = (d[i] - x) * pc - e2[i - 1] * pp;
+        if (pn == 0) pn = -kEpTiny * pc;
+        cnt += (pn < 0) != (pc < 0);
+        pp = pc;
+        pc = pn;
+        const double a = fabs(pc), b = fabs(pp);
+        const double mx = a > b ? a : b;
+        const double sc = mx > kEpBig ? kEpSmall : mx < kEpSmall ? kEpBig : 1.0;
+        pc *= sc;
+        pp *= sc;
+    }
+    return cnt;
+}
+
+VS_HD inline double ep_frac(int j) { return (double)(j + 1) / (double)(kEpMsPts + 1); }
+
+// LU with partial pivoting of the tridiagonal T - lam I (dgttrf's elimination, one division per
+// step); pivots below tiny in magnitude are set to +-tiny, inv[i] = 1 / U_ii.
+struct EpLu {
+    double dd[10], du[9], du2[8], dl[9], inv[10];
+    bool sw[9];
+};
+VS_HD inline void ep_lu(const double* d, const double* e, double lam, double tiny, EpLu& f) {
+    VS_UNROLL
+    for (int i = 0; i < 10; i++) f.dd[i] = d[i] - lam;
+    VS_UNROLL
+    for (int i = 0; i < 9; i++) f.du[i] = f.dl[i] = e[i];
+    VS_UNROLL
+    for (int i = 0; i < 8; i++) f.du2[i] = 0.0;
+    VS_UNROLL
+    for (int i = 0; i < 9; i++) {
+        const double a = f.dd[i], l = f.dl[i], u = f.du[i], a1 = f.dd[i + 1];
+        const bool sw = !(fabs(a) >= fabs(l));  // row interchange
+        double fact = (sw ? a : l) / (sw ? l : a);
+        if (!sw && a == 0) fact = 0.0;
+        f.sw[i] = sw;
+        f.dd[i] = sw ? l : a;
+        f.dl[i] = fact;
+        f.du[i] = sw ? a1 : u;
+        f.dd[i + 1] = (sw ? u : a1) - fact * (sw ? a1 : u);
+        if (i < 8) {
+            const double u1 = f.du[i + 1];
+            f.du2[i] = sw ? u1 : 0.0;
+            f.du[i + 1] = sw ? -fact * u1 : u1;
+        }
+    }
+    VS_UNROLL
+    for (int i = 0; i < 10; i++) {
+        const double a = f.dd[i];
+        f.dd[i] = fabs(a) < tiny ? (a < 0 ? -tiny : tiny) : a;
+        f.inv[i] = 1.0 / f.dd[i];
+    }
+}
+VS_HD inline void ep_lu_solve(const EpLu& f, double* b) {
+    VS_UNROLL
+    for (int i = 0; i < 9; i++) {
+        const double b0 = b[i], b1 = b[i + 1];
+        b[i] = f.sw[i] ? b1 : b0;
+        b[i + 1] = (f.sw[i] ? b0 : b1) - f.dl[i] * (f.sw[i] ? b1 : b0);
+    }
+    b[9] = b[9] * f.inv[9];
+    b[8] = (b[8] - f.du[8] * b[9]) * f.inv[8];
+    VS_UNROLL
+    for (int i = 7; i >= 0; i--) b[i] = (b[i] - f.du[i] * b[i + 1] - f.du2[i] * b[i + 2]) * f.inv[i];
+}
+VS_HD inline void ep_normalize10(double* y) {
+    double s = 0;
+    VS_UNROLL
+    for (int i = 0; i < 10; i++) s += y[i] * y[i];
+    const double inv = 1.0 / sqrt(s);
+    VS_UNROLL
+    for (int i = 0; i < 10; i++) y[i] *= inv;
+}
+// fixed start vector of the inverse iteration (no structure a tridiagonal eigenvector shares)
+VS_HD inline double ep_start(int i) {
+    constexpr double s[10] = {0.53, -0.41, 0.37, 0.61, -0.29, 0.47, -0.33, 0.59, 0.43, -0.51};
+    return s[i];
+}
+
+// Sequential statement (host oracle; the device's parallel version in pnp.hip is bit-identical).
+VS_HD inline void epnp_small_eig(const double (*al)[4], const double* uv, int m, const Cam& K, double v[4][12]) {
+    const int nc = 2 * m;  // 8 or 10
+    double C[10][12], alpha[10], tau[10];
+    for (int j = 0; j < nc; j++)
+        for (int r = 0; r < 12; r++) C[j][r] = ep_mt(al, uv, K, j, r);
+    // 1. QR of M^T: column k keeps its reflector u (rows k..11), alpha[k] = R_kk
+    for (int k = 0; k < nc; k++) {
+        double s = 0;
+        for (int r = k; r < 12; r++) s += C[k][r] * C[k][r];
+        double u0;
+        ep_householder(s, C[k][k], alpha[k], u0, tau[k]);
+        C[k][k] = u0;
+        for (int j = k + 1; j < nc; j++) {
+            double w = 0;
+            for (int r = k; r < 12; r++) w += C[k][r] * C[j][r];
+            const double f = tau[k] * w;
+            for (int r = k; r < 12; r++) C[j][r] = C[j][r] - f * C[k][r];
+        }
+    }
+    double x[4][12];
+    const int nz = nc == 10 ? 2 : 4;  // null vectors
+    for (int q = 0; q < 4; q++)
+        for (int r = 0; r < 12; r++) x[q][r] = (q < nz && r == nc + q) ? 1.0 : 0.0;
+    if (nc == 10) {
+        // 2. B = R R^T (R_ak = C[k][a] above the diagonal, alpha[a] on it), upper triangle then mirrored
+        double B[10][10];
+        for (int a = 0; a < 10; a++)
+            for (int b = a; b < 10; b++) {
+                double s = 0;
+                for (int k = b; k < 10; k++) s += (k == a ? alpha[a] : C[k][a]) * (k == b ? alpha[b] : C[k][b]);
+                B[a][b] = B[b][a] = s;
+            }
+        // tridiagonalisation: reflector k (indices k+1..9) in U[k], tau in tt[k]
+        double d[10], e[9], U[8][10], tt[8];
+        for (int k = 0; k < 8; k++) {
+            double s = 0;
+            for (int j = k + 1; j < 10; j++) s += B[k][j] * B[k][j];
+            double u0, t;
+            ep_householder(s, B[k][k + 1], e[k], u0, t);
+            d[k] = B[k][k];
+            tt[k] = t;
+            for (int j = k + 1; j < 10; j++) U[k][j] = j == k + 1 ? u0 : B[k][j];
+            double p[10], w[10];
+            for (int i = k + 1; i < 10; i++) {
+                double q = 0;
+                for (int j = k + 1; j < 10; j++) q += B[i][j] * U[k][j];
+                p[i] = t * q;
+            }
+            double pv = 0;
+            for (int i = k + 1; i < 10; i++) pv += p[i] * U[k][i];
+            const double Kc = (0.5 * t) * pv;
+            for (int i = k + 1; i < 10; i++) w[i] = p[i] - Kc * U[k][i];
+            for (int i = k + 1; i < 10; i++)
+                for (int j = k + 1; j < 10; j++) B[i][j] = B[i][j] - (U[k][i] * w[j] + w[i] * U[k][j]);
+        }
+        d[8] = B[8][8];
+        d[9] = B[9][9];
+        e[8] = B[8][9];
+        // 3. the two smallest eigenvalues: Gershgorin interval, multisection
+        double e2[9], lo = 0, hi = 0;
+        for (int i = 0; i < 9; i++) e2[i] = e[i] * e[i];
+        for (int i = 0; i < 10; i++) {
+            const double rad = (i > 0 ? fabs(e[i - 1]) : 0.0) + (i < 9 ? fabs(e[i]) : 0.0);
+            const double l = d[i] - rad, h = d[i] + rad;
+            lo = (i == 0 || l < lo) ? l : lo;
+            hi = (i == 0 || h > hi) ? h : hi;
+        }
+        double a_t[2] = {lo, lo}, b_t[2] = {hi, hi};
+        for (int st = 0; st < kEpMsSteps; st++)
+            for (int t = 0; t < 2; t++) {
+                const double a = a_t[t], wd = b_t[t] - a_t[t];
+                int js = kEpMsPts;
+                for (int j = 0; j < kEpMsPts; j++)
+                    if (ep_sturm(d, e2, a + wd * ep_frac(j)) > t) {
+                        js = j;
+                        break;
+                    }
+                a_t[t] = js > 0 ? a + wd * ep_frac(js - 1) : a;
+                b_t[t] = js < kEpMsPts ? a + wd * ep_frac(js) : b_t[t];
+            }
+        // 4. inverse iteration
+        const double fa = fabs(lo), fb = fabs(hi);
+        const double tnorm = fa > fb ? fa : fb;
+        const double tiny = tnorm > 0 ? DBL_EPSILON * tnorm : DBL_MIN;
+        double lam[2], y[2][10];
+        EpLu f[2];
+        for (int t = 0; t < 2; t++) {
+            lam[t] = 0.5 * (a_t[t] + b_t[t]);
+            ep_lu(d, e, lam[t], tiny, f[t]);
+            for (int i = 0; i < 10; i++) y[t][i] = ep_start(i);
+        }
+        const bool cluster = lam[1] - lam[0] <= 1e-3 * tnorm;
+        for (int it = 0; it < kEpInvIters; it++) {
+            for (int t = 0; t < 2; t++) {
+                ep_lu_solve(f[t], y[t]);
+                ep_normalize10(y[t]);
+            }
+            if (cluster) {
+                double dt = 0;
+                for (int i = 0; i < 10; i++) dt += y[0][i] * y[1][i];
+                for (int i = 0; i < 10; i++) y[1][i] = y[1][i] - dt * y[0][i];
+                ep_normalize10(y[1]);
+            }
+        }
+        // 5. back through the tridiagonal reflectors (H_7 first), into the QR basis
+        for (int t = 0; t < 2; t++) {
+            for (int k = 7; k >= 0; k--) {
+                double w = 0;
+                for (int i = k + 1; i < 10; i++) w += U[k][i] * y[t][i];
+                const double fk = tt[k] * w;
+                for (int i = k + 1; i < 10; i++) y[t][i] = y[t][i] - fk * U[k][i];
+            }
+            for (int r = 0; r < 10; r++) x[2 + t][r] = y[t][r];
+        }
+    }
+    // 6. v = Q x (Q = H_0 .. H_{nc-1}: H_{nc-1} first)
+    for (int q = 0; q < 4; q++) {
+        for (int k = nc - 1; k >= 0; k--) {
+            double w = 0;
+            for (int r = k; r < 12; r++) w += C[k][r] * x[q][r];
+            const double fk = tau[k] * w;
+            for (int r = k; r < 12; r++) x[q][r] = x[q][r] - fk * C[k][r];
+        }
+        for (int r = 0; r < 12; r++) v[q][r] = x[q][r];
+    }
+}
+
 // From the eigenvectors um (columns, descending eigenvalues): v[k] = eigenvector of the k-th
 // smallest eigenvalue, the L_6x10 matrix and the squared control point distances rho.
+VS_HD inline void epnp_L_rho_v(const double v[4][12], const double cw[4][3], double L[6][10], double rho[6]);
 VS_HD inline void epnp_L_rho(const double* um, const double cw[4][3], double v[4][12], double L[6][10], double rho[6]) {
     for (int k = 0; k < 4; k++)
         for (int i = 0; i < 12; i++) v[k][i] = um[i * 12 + (11 - k)];
+    epnp_L_rho_v(v, cw, L, rho);
+}
+// L and rho from the four eigenvectors v[k] (k-th smallest eigenvalue)
+VS_HD inline void epnp_L_rho_v(const double v[4][12], const double cw[4][3], double L[6][10], double rho[6]) {
     const int pa[6] = {0, 0, 0, 1, 1, 2}, pb[6] = {1, 2, 3, 2, 3, 3};
     for (int j = 0; j < 6; j++) {
         double dv[4][3];
@@ -741,13 +1008,18 @@ VS_HD bool epnp(const double* X, const double* uv, int n, const Cam& K, double* 
     if (n < 4 || n > MAXN) return false;
     double cw[4][3], alphas[MAXN][4];
     if (!epnp_control(X, n, cw, alphas)) return false;
-    double MtM[144];
-    for (int a = 0; a < 12; a++)
-        for (int b = 0; b < 12; b++) MtM[a * 12 + b] = epnp_mtm<MAXN>(alphas, uv, n, K, a, b);
-    double dm[12], um[144];
-    sym_eig_rr<12>(MtM, dm, um);
     double v[4][12], L[6][10], rho[6];
-    epnp_L_rho(um, cw, v, L, rho);
+    if (n <= 5) {  // RANSAC subsets: the null space by QR, two eigenpairs of R R^T
+        epnp_small_eig(alphas, uv, n, K, v);
+        epnp_L_rho_v(v, cw, L, rho);
+    } else {
+        double MtM[144];
+        for (int a = 0; a < 12; a++)
+            for (int b = 0; b < 12; b++) MtM[a * 12 + b] = epnp_mtm<MAXN>(alphas, uv, n, K, a, b);
+        double dm[12], um[144];
+        sym_eig_rr<12>(MtM, dm, um);
+        epnp_L_rho(um, cw, v, L, rho);
+    }
     double best_err = 0;
     bool have = false;
     for (int s = 0; s < 3; s++) {

@@ -92,6 +92,8 @@ __device__ inline void w4_rowA(const float m[6], float r[4]) {
     r[3] = __builtin_fmaf(8.0f, e, b) + m[5];
 }
 
+}  // namespace
+
 #ifndef VS_W4_ABL
 #define VS_W4_ABL 0  // latency ablation (results are wrong): 1 no transform, 2 no patch staging, 3 no MFMA,
                      // 4 no barrier in the k-loop, 5 no B loads
@@ -411,8 +413,6 @@ __global__ __launch_bounds__(512, 1) void k_wino4(WinoArgs wa) {
         }
     }
 }
-
-}  // namespace
 
 // F(4x4, 3x3) launch: SuperPoint layers (bias + ReLU; POOL: 2 x 2 max-pool; FUSE1A: conv1a fused).
 // wa.wu = winograd4_weights(...) images; cin % 4 == 0, cout_pad % 64 == 0, cout % 4 == 0.

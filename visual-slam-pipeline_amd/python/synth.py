@@ -198,6 +198,48 @@ def loop_trajectory(n=126, radius=0.6, seed=SEED):
     return poses
 
 
+def pioneer_trajectory(n=848, step=0.03, seed=SEED):
+    """n camera->world poses along a smooth, open (non-repeating) Pioneer-like drive through the room: a
+    0.6 m-radius turn whose centre wanders on two slow incommensurate oscillations, resampled to `step`
+    metres between processed frames (0.3 m/s at 10 processed frames/s, the reference's FRAME_STEP 3 of
+    a 30 Hz stream), heading along the path (yaw rate about 0.5 rad/s), 0.4 m above the floor and at
+    least about 1 m from every wall.  The 848 processed frames of freiburg2_pioneer_slam3's 2,544 images
+    (main.cpp:1096-1107) by default; any n extends the same drive."""
+    rng = np.random.default_rng(seed + 41)
+    ph = rng.uniform(0, 2 * np.pi, 3)
+    # dense parametric curve, then arc-length resampling
+    u = np.linspace(0.0, (n * step / 0.6) * 1.6 + 10.0, 200000)
+    x = 0.6 * np.cos(u + ph[0]) + 0.9 * np.cos(0.137 * u + ph[1])
+    z = 0.6 * np.sin(u + ph[0]) + 0.7 * np.sin(0.113 * u + ph[2])
+    seg = np.hypot(np.diff(x), np.diff(z))
+    s_cum = np.concatenate([[0.0], np.cumsum(seg)])
+    assert s_cum[-1] >= (n + 1) * step, "curve too short"
+    sk = np.arange(n + 1) * step
+    xs, zs = np.interp(sk, s_cum, x), np.interp(sk, s_cum, z)
+    poses = []
+    for i in range(n):
+        fwd = np.array([xs[i + 1] - xs[i], 0.0, zs[i + 1] - zs[i]])
+        yaw = np.arctan2(fwd[0], fwd[2])
+        poses.append((yaw_rotation(yaw), np.array([xs[i], 0.0, zs[i]])))
+    return poses
+
+
+def render_frames(poses, indices, seed=SEED, workers=None, K=K_TUM, w=W, h=H):
+    """Render frames `indices` of a pose list (each frame's depth dropouts seeded by its index):
+    (bgr [len, h, w, 3] u8, depth [len, h, w] f32)."""
+    jobs = [(i, poses[i][0], poses[i][1], seed, K, w, h) for i in indices]
+    if workers is None:
+        import os
+        workers = min(16, os.cpu_count() or 1, max(len(jobs), 1))
+    if workers > 1 and len(jobs) > 1:
+        import multiprocessing as mp
+        with mp.get_context("fork").Pool(workers) as pool:
+            out = pool.map(_render_one, jobs, chunksize=max(1, len(jobs) // (4 * workers)))
+    else:
+        out = [_render_one(j) for j in jobs]
+    return np.stack([o[0] for o in out]), np.stack([o[1] for o in out])
+
+
 def _render_one(args):
     i, R, t, seed, K, w, h = args
     scene = Scene(seed)

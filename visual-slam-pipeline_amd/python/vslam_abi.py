@@ -90,6 +90,8 @@ _SIG = {
     "vs_batch_create": (_I, [_P, _I, _I, _I, _I, _I, _P, ctypes.POINTER(_P)]),
     "vs_batch_destroy": (None, [_P]),
     "vs_batch_step_dev": (_I, [_P, _P, _P, _P, _I, _P, _P]),
+    "vs_batch_submit_dev": (_I, [_P, _P, _P, _P, _I, _P]),
+    "vs_batch_collect": (_I, [_P, _P]),
     "vs_batch_features_dev": (_I, [_P, _P, _P, _P, _P]),
     "vs_batch_set_gather": (_I, [_P, _I]),
     "vs_batch_exchange_loopback": (_I, [_I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
@@ -869,6 +871,27 @@ class Batch:
     def step_dev(self, d_bgr, d_depth, d_depth_prev, frame_count0, stream=None):
         out = (PairMotion * self.B)()
         _check(self.lib.vs_batch_step_dev(self.h, d_bgr, d_depth, d_depth_prev, frame_count0, out, stream))
+        return self._motions(out)
+
+    def submit_dev(self, d_bgr, d_depth, d_depth_prev, frame_count0, stream=None):
+        """Enqueue a step (vs_batch_submit_dev); at most two in flight."""
+        _check(self.lib.vs_batch_submit_dev(self.h, d_bgr, d_depth, d_depth_prev, frame_count0, stream))
+
+    def collect(self):
+        """The oldest submitted step's pair motions (vs_batch_collect)."""
+        out = (PairMotion * self.B)()
+        _check(self.lib.vs_batch_collect(self.h, out))
+        return self._motions(out)
+
+    def features_dev(self):
+        """(kps, desc, n device pointers, frames) of the last collected step (vs_batch_features_dev)."""
+        k, d, n, f = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_int()
+        _check(self.lib.vs_batch_features_dev(self.h, ctypes.byref(k), ctypes.byref(d), ctypes.byref(n),
+                                              ctypes.byref(f)))
+        return k.value, d.value, n.value, f.value
+
+    @staticmethod
+    def _motions(out):
         return dict(ok=np.array([m.ok3d for m in out], np.int32), R=np.array([list(m.R3) for m in out]),
                     t=np.array([list(m.t3) for m in out]), eok=np.array([m.okE for m in out], np.int32),
                     eR=np.array([list(m.RE) for m in out]), et=np.array([list(m.tE) for m in out]),
