@@ -84,6 +84,30 @@ extern "C" int orc_epnp(const double* X, const double* uv, int n, const double K
     return epnp<4096>(X, uv, n, cam, R, t) ? 1 : 0;
 }
 
+// test hook mirroring the device's vs_debug_epnp (pnp.hip): per problem (v[4][12] of
+// epnp_small_eig, R[9], t[3], ok, rod_m2v(R)[3], rod_v2m of it[9]) for m = 4 / 5 points
+extern "C" int orc_epnp_debug(const double* X, const double* uv, const int* m, int count, const double K[4],
+                              double* out) {
+    const Cam cam{K[0], K[1], K[2], K[3]};
+    for (int p = 0; p < count; p++) {
+        double* o = out + (size_t)p * 73;
+        double cw[4][3], al[5][4], v[4][12], R[9] = {}, t[3] = {};
+        bool ok = m[p] >= 4 && m[p] <= 5 && epnp_control(X + 15 * p, m[p], cw, al);
+        if (ok) epnp_small_eig(al, uv + 10 * p, m[p], cam, v);
+        for (int k = 0; k < 48; k++) o[k] = ok ? v[k / 12][k % 12] : 0.0;
+        ok = ok && epnp<5>(X + 15 * p, uv + 10 * p, m[p], cam, R, t);
+        for (int k = 0; k < 9; k++) o[48 + k] = R[k];
+        for (int k = 0; k < 3; k++) o[57 + k] = t[k];
+        o[60] = ok ? 1.0 : 0.0;
+        double rv[3], R2[9];
+        rod_m2v(R, rv);
+        rod_v2m(rv, R2);
+        for (int k = 0; k < 3; k++) o[61 + k] = rv[k];
+        for (int k = 0; k < 9; k++) o[64 + k] = R2[k];
+    }
+    return 0;
+}
+
 extern "C" int orc_pnp_ransac(const float* obj, const float* img, int n, const double K[4], int max_iters,
                               double thr, double conf, double rvec[3], double tvec[3], uint8_t* mask,
                               int* n_inliers, int diag[4]) {

@@ -77,3 +77,33 @@ def test_solve_pnp_batch_dev(vsctx, oracle):
              mask[off[p]:off[p + 1]], st[p, 2:6])
         assert st[p, 6] == len(pr[0])
         _check_against_oracle(oracle, g, pr[0], pr[1], 300, 10)
+
+
+def test_epnp_sequential_device_equals_host(vsctx, oracle):
+    """pnp_solvers.h's sequential EPnP compiled for the device (one lane per problem; the product
+    path runs the wave-parallel k_pnp_hyp, also for n == model points): the eigenvectors of
+    epnp_small_eig, the pose and its Rodrigues round trip equal the host's bit for bit on 4- and
+    5-point problems, noisy and exact."""
+    import ctypes
+
+    import vslam_abi
+    lib = vslam_abi.load_library()
+    lib.vs_debug_epnp.restype = ctypes.c_int
+    lib.vs_debug_epnp.argtypes = [ctypes.c_void_p] * 3 + [ctypes.c_int] + [ctypes.c_void_p] * 2
+    rng = np.random.default_rng(9)
+    count = 2000
+    m = np.where(np.arange(count) % 5 == 0, 4, 5).astype(np.int32)
+    X = np.zeros((count, 15))
+    uv = np.zeros((count, 10))
+    for p in range(count):
+        obj, img, _, _, _ = pnp_problem(int(m[p]), 1000 + p, noise=0.5 if p % 2 else 0.0)
+        X[p, :3 * m[p]] = obj.astype(np.float64).ravel()
+        uv[p, :2 * m[p]] = img.astype(np.float64).ravel()
+    K = np.array([525.0, 525.0, 319.5, 239.5])
+    dev = np.zeros((count, 73))
+    assert lib.vs_debug_epnp(X.ctypes.data, uv.ctypes.data, m.ctypes.data, count, K.ctypes.data, dev.ctypes.data) == 0
+    host = oracle.epnp_debug(X, uv, m, tuple(K))
+    bad_v = np.nonzero(np.any(dev[:, :48].view(np.uint64) != host[:, :48].view(np.uint64), axis=1))[0]
+    bad_p = np.nonzero(np.any(dev[:, 48:].view(np.uint64) != host[:, 48:].view(np.uint64), axis=1))[0]
+    assert len(bad_v) == 0 and len(bad_p) == 0, (bad_v[:5], bad_p[:5], np.abs(dev - host).max())
+    assert host[:, 60].sum() > 0.9 * count

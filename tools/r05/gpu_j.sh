@@ -1,0 +1,8 @@
+#!/bin/bash
+# Round-5: k_pnp_hyp eigen-stage split (profiling build) + PnP / tracker parity
+export TMPDIR=/tmp
+O=gpurun_out/r05j; mkdir -p $O
+timeout -k 10 600 python -u -m pytest tests/test_gpu_pnp.py::test_epnp_sequential_device_equals_host tests/test_gpu_pnp.py tests/test_golden.py tests/test_gpu_tracker_ideal.py tests/test_gpu_tracker_bench.py -q --timeout 300 --timeout-method thread -p no:cacheprovider > $O/pytest.log 2>&1; rc=$?; grep -E "passed|failed|Error" $O/pytest.log | tail -8; echo "pytest rc=$rc"
+timeout -k 10 300 python -u tools/profile_tracker_phases.py > $O/phases.json 2> $O/phases.err || { tail -5 $O/phases.err; exit 1; }
+python3 -c "
+import json; d=json.loads(open('$O/phases.json').read().strip().splitlines()[-1]); print('pnp phases', d.get('pnp_hyp_kcycles_per_hypothesis_x100'))"

@@ -32,7 +32,7 @@ constexpr int kPnpMaxIters = VS_PNP_MAX_ITERS;
 
 #ifdef VS_PNP_PROFILE
 // k_pnp_hyp phase cycle counters (profiling build only: make -C visual-slam-pipeline_amd prof)
-__device__ unsigned long long g_pnp_cycles[16];  // 0-5 k_pnp_hyp, 6-7 k_pnp_ransac, 8-12 its LM split
+__device__ unsigned long long g_pnp_cycles[24];  // k_pnp_hyp 0-5, 13-19 (1-3, 13-14 eigen stages, 15-19 the variants' stages), 6-7 k_pnp_ransac, 8-12 its LM split
 #define PNP_T0() long long _pn_t = clock64()
 #define PNP_T(k)                                                             \
     do {                                                                     \
@@ -72,24 +72,6 @@ __device__ __forceinline__ const int* pnp_subset(const PnpHyp& H, int pb, int n,
                          : H.subset + ((size_t)pb * H.stride + h) * 5;
 }
 
-__device__ __attribute__((noinline)) bool epnp_subset(const float* obj, const float* img, const int* idx, int m, const Cam& K, double* rv,
-                                   double* tv) {
-    double X[15], uv[10];
-    for (int j = 0; j < m; j++) {
-        const int i = idx[j];
-        X[3 * j] = obj[3 * i];
-        X[3 * j + 1] = obj[3 * i + 1];
-        X[3 * j + 2] = obj[3 * i + 2];
-        uv[2 * j] = img[2 * i];
-        uv[2 * j + 1] = img[2 * i + 1];
-    }
-    double R[9], t[3];
-    if (!epnp<5>(X, uv, m, K, R, t)) return false;
-    rod_m2v(R, rv);
-    for (int k = 0; k < 3; k++) tv[k] = t[k];
-    return true;
-}
-
 __device__ inline bool pnp_problem_runs(int n, int min_inliers, int model_points) {
     return !(n < min_inliers || n < 4) && n != model_points;
 }
@@ -116,10 +98,19 @@ struct EpShared {
 // exactly symmetric, so a lane's own reflector entry is its column k), lanes 0-31 / 32-63 run the
 // multisection for the smallest / second smallest eigenvalue (one Sturm count per lane, a ballot
 // picks the subinterval), lanes 0 / 1 the inverse iterations, lanes 0-3 the back-transformations.
+#ifdef VS_PNP_PROFILE
+#define EP_T(k)                                                                   \
+    do {                                                                          \
+        if (lane == 0) atomicAdd(&g_pnp_cycles[k], (unsigned long long)(clock64() - tprof)); \
+        tprof = clock64();                                                        \
+    } while (0)
+#else
+#define EP_T(k)
+#endif
 __device__ __forceinline__ void epnp_small_eig_wave(const double (*al)[4], const double* uv, int m, const Cam& K,
-                                                    int lane, EpShared& S) {
+                                                    int lane, EpShared& S, [[maybe_unused]] long long& tprof) {
     const int nc = 2 * m;
-    double c[12];
+    double c[12], t[12];
 #pragma unroll
     for (int r = 0; r < 12; r++) c[r] = lane < nc ? ep_mt(al, uv, K, lane, r) : 0.0;
     double my_alpha = 0, my_tau = 0;
@@ -127,11 +118,10 @@ __device__ __forceinline__ void epnp_small_eig_wave(const double (*al)[4], const
 #pragma unroll
     for (int k = 0; k < 10; k++) {
         if (k >= nc) continue;  // (m = 4: 8 columns; not break: the loop must unroll for static k)
-        double s = 0;
 #pragma unroll
-        for (int r = k; r < 12; r++) s += c[r] * c[r];
+        for (int r = 0; r < 12; r++) t[r] = r >= k ? c[r] * c[r] : -0.0;
         double alpha, u0, tau;
-        ep_householder(s, c[k], alpha, u0, tau);
+        ep_householder(tsum<12>(t), c[k], alpha, u0, tau);
         if (lane == k) {
             c[k] = u0;
             my_alpha = alpha;
@@ -142,10 +132,9 @@ __device__ __forceinline__ void epnp_small_eig_wave(const double (*al)[4], const
         for (int r = k; r < 12; r++) u[r] = lane_bcast(c[r], k);
         const double tk = lane_bcast(tau, k);
         if (lane > k && lane < nc) {
-            double w = 0;
 #pragma unroll
-            for (int r = k; r < 12; r++) w += u[r] * c[r];
-            const double f = tk * w;
+            for (int r = 0; r < 12; r++) t[r] = r >= k ? u[r] * c[r] : -0.0;
+            const double f = tk * tsum<12>(t);
 #pragma unroll
             for (int r = k; r < 12; r++) c[r] = c[r] - f * u[r];
         }
@@ -168,14 +157,14 @@ __device__ __forceinline__ void epnp_small_eig_wave(const double (*al)[4], const
                 a++;
             }
             const int b = a + rem;
-            double s = 0;
 #pragma unroll
-            for (int k = 0; k < 10; k++)
-                if (k >= b) s += S.R[a][k] * S.R[b][k];
+            for (int k = 0; k < 10; k++) t[k] = k >= b ? S.R[a][k] * S.R[b][k] : -0.0;
+            const double s = tsum<10>(t);
             S.B[a][b] = s;
             S.B[b][a] = s;
         }
         __syncthreads();
+        EP_T(1);
         // tridiagonalisation
         double br[10];
 #pragma unroll
@@ -183,14 +172,13 @@ __device__ __forceinline__ void epnp_small_eig_wave(const double (*al)[4], const
         double d[10], e[9];
 #pragma unroll
         for (int k = 0; k < 8; k++) {
-            double s = 0;
 #pragma unroll
-            for (int j = k + 1; j < 10; j++) s += br[j] * br[j];
-            double alpha, u0, t;
-            ep_householder(s, br[k + 1], alpha, u0, t);
+            for (int j = 0; j < 10; j++) t[j] = j > k ? br[j] * br[j] : -0.0;
+            double alpha, u0, tk0;
+            ep_householder(tsum<10>(t), br[k + 1], alpha, u0, tk0);
             e[k] = lane_bcast(alpha, k);
             d[k] = lane_bcast(br[k], k);
-            const double tk = lane_bcast(t, k);
+            const double tk = lane_bcast(tk0, k);
             double U[10];
             U[k + 1] = lane_bcast(u0, k);
 #pragma unroll
@@ -202,17 +190,12 @@ __device__ __forceinline__ void epnp_small_eig_wave(const double (*al)[4], const
             }
             const bool act = lane > k && lane < 10;
             const double uo = lane == k + 1 ? U[k + 1] : br[k];  // this row's reflector entry (B symmetric)
-            double p = 0;
-            if (act) {
-                double q = 0;
 #pragma unroll
-                for (int j = k + 1; j < 10; j++) q += br[j] * U[j];
-                p = tk * q;
-            }
-            double pv = 0;
+            for (int j = 0; j < 10; j++) t[j] = j > k ? br[j] * U[j] : -0.0;
+            const double p = act ? tk * tsum<10>(t) : 0.0;
 #pragma unroll
-            for (int i = k + 1; i < 10; i++) pv += lane_bcast(p, i) * U[i];
-            const double Kc = (0.5 * tk) * pv;
+            for (int i = 0; i < 10; i++) t[i] = i > k ? lane_bcast(p, i) * U[i] : -0.0;
+            const double Kc = (0.5 * tk) * tsum<10>(t);
             const double w = p - Kc * uo;
             double wj[10];
 #pragma unroll
@@ -225,10 +208,10 @@ __device__ __forceinline__ void epnp_small_eig_wave(const double (*al)[4], const
         d[8] = lane_bcast(br[8], 8);
         d[9] = lane_bcast(br[9], 9);
         e[8] = lane_bcast(br[9], 8);
-        // 3. multisection: lanes 0-31 the smallest eigenvalue, 32-63 the second smallest
-        double e2[9], lo = 0, hi = 0;
-#pragma unroll
-        for (int i = 0; i < 9; i++) e2[i] = e[i] * e[i];
+        EP_T(2);
+        // 3. scaled to ||T|| in [1, 2); multisection: lanes 0-31 the smallest eigenvalue, 32-63 the
+        //    second smallest
+        double lo = 0, hi = 0;
 #pragma unroll
         for (int i = 0; i < 10; i++) {
             const double rad = (i > 0 ? fabs(e[i - 1]) : 0.0) + (i < 9 ? fabs(e[i]) : 0.0);
@@ -236,6 +219,17 @@ __device__ __forceinline__ void epnp_small_eig_wave(const double (*al)[4], const
             lo = (i == 0 || l < lo) ? l : lo;
             hi = (i == 0 || h > hi) ? h : hi;
         }
+        const double sc = ep_scale(fabs(lo) > fabs(hi) ? fabs(lo) : fabs(hi));
+        double e2[9];
+#pragma unroll
+        for (int i = 0; i < 10; i++) d[i] *= sc;
+#pragma unroll
+        for (int i = 0; i < 9; i++) {
+            e[i] *= sc;
+            e2[i] = e[i] * e[i];
+        }
+        lo *= sc;
+        hi *= sc;
         const int tsel = lane >> 5;
         const double fj = ep_frac(lane & 31);
         double a0 = lo, b0 = hi, a1 = lo, b1 = hi;
@@ -255,9 +249,9 @@ __device__ __forceinline__ void epnp_small_eig_wave(const double (*al)[4], const
             a1 = na1;
             b1 = nb1;
         }
-        // 4. inverse iteration, lane t for eigenvalue t
-        const double fa = fabs(lo), fb = fabs(hi);
-        const double tnorm = fa > fb ? fa : fb;
+        EP_T(3);
+        // 4. inverse iteration, lane q for eigenvalue q
+        const double tnorm = fabs(lo) > fabs(hi) ? fabs(lo) : fabs(hi);
         const double tiny = tnorm > 0 ? DBL_EPSILON * tnorm : DBL_MIN;
         const double lam0 = 0.5 * (a0 + b0), lam1 = 0.5 * (a1 + b1);
         const bool cluster = lam1 - lam0 <= 1e-3 * tnorm;
@@ -269,28 +263,20 @@ __device__ __forceinline__ void epnp_small_eig_wave(const double (*al)[4], const
             for (int i = 0; i < 10; i++) y[i] = ep_start(i);
             for (int it = 0; it < kEpInvIters; it++) {
                 ep_lu_solve(f, y);
-                ep_normalize10(y);
                 if (cluster) {
                     double y0[10];
 #pragma unroll
                     for (int i = 0; i < 10; i++) y0[i] = lane_bcast(y[i], 0);
-                    if (lane == 1) {
-                        double dt = 0;
-#pragma unroll
-                        for (int i = 0; i < 10; i++) dt += y0[i] * y[i];
-#pragma unroll
-                        for (int i = 0; i < 10; i++) y[i] = y[i] - dt * y0[i];
-                        ep_normalize10(y);
-                    }
+                    if (lane == 1) ep_orth10(y0, y);
                 }
             }
+            ep_normalize10(y);
             // back through the tridiagonal reflectors
 #pragma unroll
             for (int k = 7; k >= 0; k--) {
-                double w = 0;
 #pragma unroll
-                for (int i = k + 1; i < 10; i++) w += S.U[k][i] * y[i];
-                const double fk = S.tt[k] * w;
+                for (int i = 0; i < 10; i++) t[i] = i > k ? S.U[k][i] * y[i] : -0.0;
+                const double fk = S.tt[k] * tsum<10>(t);
 #pragma unroll
                 for (int i = k + 1; i < 10; i++) y[i] = y[i] - fk * S.U[k][i];
             }
@@ -306,6 +292,7 @@ __device__ __forceinline__ void epnp_small_eig_wave(const double (*al)[4], const
             for (int r = 0; r < 10; r++) x[r] = yt[r];
         }
     }
+    EP_T(13);
     // 5. v = Q x, lanes 0..3
 #pragma unroll
     for (int k = 9; k >= 0; k--) {
@@ -314,10 +301,9 @@ __device__ __forceinline__ void epnp_small_eig_wave(const double (*al)[4], const
 #pragma unroll
         for (int r = k; r < 12; r++) u[r] = lane_bcast(c[r], k);
         const double tk = lane_bcast(my_tau, k);
-        double w = 0;
 #pragma unroll
-        for (int r = k; r < 12; r++) w += u[r] * x[r];
-        const double fk = tk * w;
+        for (int r = 0; r < 12; r++) t[r] = r >= k ? u[r] * x[r] : -0.0;
+        const double fk = tk * tsum<12>(t);
 #pragma unroll
         for (int r = k; r < 12; r++) x[r] = x[r] - fk * u[r];
     }
@@ -325,6 +311,7 @@ __device__ __forceinline__ void epnp_small_eig_wave(const double (*al)[4], const
 #pragma unroll
         for (int r = 0; r < 12; r++) S.v[lane][r] = x[r];
     }
+    EP_T(14);
 }
 
 // 1. subsets of the initial budget from the cv::RNG stream (getSubset: repeats rejected); the
@@ -469,15 +456,17 @@ __global__ __launch_bounds__(64) void k_pnp_hyp(const float* __restrict__ obj_al
     const int pb = blockIdx.x, h = blockIdx.y, lane = threadIdx.x;
     const int o0 = off[pb], n = off[pb + 1] - o0;
     const int model_points = n == 4 ? 4 : 5;
-    if (h >= niters0 || !pnp_problem_runs(n, min_inliers, model_points)) return;
+    // n == model points: OpenCV's single EPnP on all points, hypothesis 0 here (k_pnp_ransac reads it)
+    const bool single = n == model_points && !(n < min_inliers || n < 4);
+    if (h >= niters0 || (single ? h > 0 : !pnp_problem_runs(n, min_inliers, model_points))) return;
     const float* obj = obj_all + 3 * (size_t)o0;
     const float* img = img_all + 2 * (size_t)o0;
     const Cam K{fx, fy, cx, cy};
-    const int* idx = pnp_subset(H, pb, n, h);
+    const int* idx = single ? nullptr : pnp_subset(H, pb, n, h);
     const int m = model_points;
     PNP_T0();
     if (lane < m) {
-        const int i = idx[lane];
+        const int i = single ? lane : idx[lane];
         sX[3 * lane] = obj[3 * i];
         sX[3 * lane + 1] = obj[3 * i + 1];
         sX[3 * lane + 2] = obj[3 * i + 2];
@@ -498,11 +487,13 @@ __global__ __launch_bounds__(64) void k_pnp_hyp(const float* __restrict__ obj_al
     bool ok = sOk != 0;
     if (ok) {
         // the four smallest eigenvectors of M^T M (pnp_solvers.h epnp_small_eig, spread over the wave)
-        epnp_small_eig_wave(sAl, sUV, m, K, lane, sE);
+#ifdef VS_PNP_PROFILE
+        epnp_small_eig_wave(sAl, sUV, m, K, lane, sE, _pn_t);
+#else
+        long long tp = 0;
+        epnp_small_eig_wave(sAl, sUV, m, K, lane, sE, tp);
+#endif
         __syncthreads();
-        PNP_T(1);
-        PNP_T(2);
-        PNP_T(3);
         if (lane < 3) {  // one beta approximation per lane
             double cw[4][3], v[4][12], L[6][10], rho[6], al[5][4], X[15], uv[10];
             for (int i = 0; i < 4; i++)
@@ -526,7 +517,17 @@ __global__ __launch_bounds__(64) void k_pnp_hyp(const float* __restrict__ obj_al
             // epnp_betas_init_uniform: bit-identical to epnp_variant's divergent solves)
             double be[4];
             epnp_betas_init_uniform(lane, L, rho, be);
+#ifdef VS_PNP_PROFILE
+            PNP_T(15);  // L, rho, initial betas
+            const int slot[4] = {16, 17, 18, 19};
+            auto mark = [&](int k) {
+                if (lane == 0) atomicAdd(&g_pnp_cycles[slot[k]], (unsigned long long)(clock64() - _pn_t));
+                _pn_t = clock64();
+            };
+            sErr[lane] = epnp_refine<5>(be, L, rho, v, al, X, uv, m, K, R, t, mark);
+#else
             sErr[lane] = epnp_refine<5>(be, L, rho, v, al, X, uv, m, K, R, t);
+#endif
             for (int k = 0; k < 9; k++) sRt[lane][k] = R[k];
             for (int k = 0; k < 3; k++) sRt[lane][9 + k] = t[k];
         }
@@ -592,10 +593,14 @@ __global__ __launch_bounds__(256) void k_pnp_ransac(const float* __restrict__ ob
     const int model_points = n == 4 ? 4 : 5;
     const int niters0 = max_iters > 1 ? max_iters : 1;
 
-    if (n == model_points) {  // OpenCV: a single EPnP on all points, every point an inlier
+    if (n == model_points) {  // OpenCV: a single EPnP on all points (k_pnp_hyp's hypothesis 0), every point an inlier
         if (tid == 0) {
-            int idx[5] = {0, 1, 2, 3, 4};
-            const bool ok = epnp_subset(obj, img, idx, n, K, S.rv, S.tv);
+            const size_t h0 = (size_t)pb * H.stride;
+            const bool ok = H.count[h0] >= 0;
+            for (int k = 0; k < 3; k++) {
+                S.rv[k] = H.model[h0 * 6 + k];
+                S.tv[k] = H.model[h0 * 6 + 3 + k];
+            }
             S.best = ok ? n : 0;
             S.best_iter = -1;
             S.niters_run = 0;
@@ -804,14 +809,59 @@ int solve_pnp(vs_ctx* ctx, int nprob, const float* d_obj, const float* d_img, co
     return VS_OK;
 }
 
+// test hook: the sequential EPnP (the n == model-points path of k_pnp_ransac) on count problems of
+// m = 4 / 5 points, one thread each: out[p] = (v[4][12] of epnp_small_eig, R[9], t[3], ok, rod_m2v(R), rod_v2m of it)
+__global__ void k_debug_epnp(const double* X, const double* uv, const int* m, int count, double fx, double fy,
+                             double cx, double cy, double* out) {
+    const int p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= count) return;
+    const Cam K{fx, fy, cx, cy};
+    double* o = out + (size_t)p * 73;
+    double cw[4][3], al[5][4], v[4][12], R[9] = {}, t[3] = {};
+    bool ok = epnp_control(X + 15 * p, m[p], cw, al);
+    if (ok) epnp_small_eig(al, uv + 10 * p, m[p], K, v);
+    for (int k = 0; k < 48; k++) o[k] = ok ? v[k / 12][k % 12] : 0.0;
+    ok = ok && epnp<5>(X + 15 * p, uv + 10 * p, m[p], K, R, t);
+    for (int k = 0; k < 9; k++) o[48 + k] = R[k];
+    for (int k = 0; k < 3; k++) o[57 + k] = t[k];
+    o[60] = ok ? 1.0 : 0.0;
+    double rv[3], R2[9];  // the model's Rodrigues round trip (k_pnp_ransac: rod_m2v, then rod_v2m)
+    rod_m2v(R, rv);
+    rod_v2m(rv, R2);
+    for (int k = 0; k < 3; k++) o[61 + k] = rv[k];
+    for (int k = 0; k < 9; k++) o[64 + k] = R2[k];
+}
+
 }  // namespace vs
+
+extern "C" int vs_debug_epnp(const double* X, const double* uv, const int* m, int count, const double* K,
+                             double* out) {
+    if (count <= 0) return 0;
+    double *dX, *duv, *dout;
+    int* dm;
+    if (hipMalloc(&dX, sizeof(double) * 15 * count) != hipSuccess) return -1;
+    (void)hipMalloc(&duv, sizeof(double) * 10 * count);
+    (void)hipMalloc(&dout, sizeof(double) * 73 * count);
+    (void)hipMalloc(&dm, sizeof(int) * count);
+    (void)hipMemcpy(dX, X, sizeof(double) * 15 * count, hipMemcpyHostToDevice);
+    (void)hipMemcpy(duv, uv, sizeof(double) * 10 * count, hipMemcpyHostToDevice);
+    (void)hipMemcpy(dm, m, sizeof(int) * count, hipMemcpyHostToDevice);
+    hipLaunchKernelGGL(vs::k_debug_epnp, dim3((count + 63) / 64), dim3(64), 0, 0, dX, duv, dm, count, K[0], K[1], K[2],
+                       K[3], dout);
+    const hipError_t e = hipMemcpy(out, dout, sizeof(double) * 73 * count, hipMemcpyDeviceToHost);
+    (void)hipFree(dX);
+    (void)hipFree(duv);
+    (void)hipFree(dout);
+    (void)hipFree(dm);
+    return e == hipSuccess ? 0 : -1;
+}
 
 #ifdef VS_PNP_PROFILE
 extern "C" int vs_debug_pnp_cycles(unsigned long long* out, int reset) {
-    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(vs::g_pnp_cycles), sizeof(unsigned long long) * 16) != hipSuccess)
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(vs::g_pnp_cycles), sizeof(unsigned long long) * 24) != hipSuccess)
         return -1;
     if (reset) {
-        unsigned long long z[16] = {};
+        unsigned long long z[24] = {};
         if (hipMemcpyToSymbol(HIP_SYMBOL(vs::g_pnp_cycles), z, sizeof(z)) != hipSuccess) return -1;
     }
     return 0;

@@ -291,36 +291,63 @@ VS_HD void sym_eig_rr(double* A, double* w, double* V) {
 VS_HD inline void dlt_point(const double P1[12], const double P2[12], float x1, float y1, float x2, float y2,
                             float X[4]);
 
+// Pairwise sum of t[0..N) in a fixed tree (halves, the first one rounded up): the same order on
+// host and device, log2(N) dependent additions instead of N - 1.  Callers pad skipped terms with
+// -0.0 (x + -0.0 == x for every x, so padding never changes a sum and the device folds it away).
+template <int N>
+VS_HD inline double tsum(const double* t) {
+    if constexpr (N == 1) {
+        return t[0];
+    } else {
+        constexpr int H = (N + 1) / 2;
+        return tsum<H>(t) + tsum<N - H>(t + H);
+    }
+}
+
 // Least squares min ||A x - b|| for an M x N (M >= N) matrix by Householder QR (A, b destroyed).
+// Column k's reflector u = (a_kk - alpha, a_k+1,k, ...) has u^T u = 2 |a| (|a| + |a_kk|), so one
+// division per column (tau = 2 / u^T u) replaces one per updated column; R_kk = alpha exactly and
+// back substitution multiplies by 1 / alpha.  A zero column is skipped (x = 0 for it): trailing zero
+// columns leave the other unknowns bit-identical (epnp_betas_init_uniform relies on this).
 template <int M, int N>
 VS_HD void lstsq(double* A, double* b, double* x) {
+    double inv[N];
+    VS_UNROLL
     for (int k = 0; k < N; k++) {
-        double nrm = 0;
-        for (int i = k; i < M; i++) nrm += A[i * N + k] * A[i * N + k];
-        nrm = sqrt(nrm);
-        if (nrm == 0) continue;
-        const double alpha = A[k * N + k] > 0 ? -nrm : nrm;
-        double v[M];
-        for (int i = 0; i < M; i++) v[i] = (i < k) ? 0.0 : A[i * N + k];
-        v[k] -= alpha;
-        double vv = 0;
-        for (int i = k; i < M; i++) vv += v[i] * v[i];
-        if (vv == 0) continue;
-        for (int j = k; j < N; j++) {
-            double d = 0;
-            for (int i = k; i < M; i++) d += v[i] * A[i * N + j];
-            const double f = 2.0 * d / vv;
-            for (int i = k; i < M; i++) A[i * N + j] -= f * v[i];
+        double t[M];
+        VS_UNROLL
+        for (int i = 0; i < M; i++) t[i] = i >= k ? A[i * N + k] * A[i * N + k] : -0.0;
+        const double s = tsum<M>(t);
+        inv[k] = 0.0;
+        if (!(s > 0)) continue;
+        const double nrm = sqrt(s), akk = A[k * N + k];
+        const double alpha = akk > 0 ? -nrm : nrm;
+        const double tau = 1.0 / (nrm * (nrm + fabs(akk)));
+        double u[M];
+        VS_UNROLL
+        for (int i = 0; i < M; i++) u[i] = i > k ? A[i * N + k] : i == k ? akk - alpha : 0.0;
+        VS_UNROLL
+        for (int j = k + 1; j < N; j++) {
+            VS_UNROLL
+            for (int i = 0; i < M; i++) t[i] = i >= k ? u[i] * A[i * N + j] : -0.0;
+            const double f = tau * tsum<M>(t);
+            VS_UNROLL
+            for (int i = k; i < M; i++) A[i * N + j] = A[i * N + j] - f * u[i];
         }
-        double d = 0;
-        for (int i = k; i < M; i++) d += v[i] * b[i];
-        const double f = 2.0 * d / vv;
-        for (int i = k; i < M; i++) b[i] -= f * v[i];
+        VS_UNROLL
+        for (int i = 0; i < M; i++) t[i] = i >= k ? u[i] * b[i] : -0.0;
+        const double f = tau * tsum<M>(t);
+        VS_UNROLL
+        for (int i = k; i < M; i++) b[i] = b[i] - f * u[i];
+        A[k * N + k] = alpha;
+        inv[k] = 1.0 / alpha;
     }
+    VS_UNROLL
     for (int k = N - 1; k >= 0; k--) {
         double s = b[k];
-        for (int j = k + 1; j < N; j++) s -= A[k * N + j] * x[j];
-        x[k] = (A[k * N + k] != 0) ? s / A[k * N + k] : 0.0;
+        VS_UNROLL
+        for (int j = k + 1; j < N; j++) s = s - A[k * N + j] * x[j];
+        x[k] = s * inv[k];
     }
 }
 
@@ -529,19 +556,22 @@ VS_HD inline double epnp_mtm(const double (*alphas)[4], const double* uv, int n,
 //   1. Householder QR of M^T (12 x 2m) = Q [R; 0]: M^T M = Q diag(R R^T, 0) Q^T, so the last
 //      12 - 2m columns of Q span the null space exactly (m = 4: all four vectors, nothing else);
 //   2. m = 5: the two smallest eigenpairs of B = R R^T (10 x 10): Householder tridiagonalisation
-//      T = H_7..H_0 B H_0..H_7, the two smallest eigenvalues of T by 33-way multisection of the
-//      Sturm count, their vectors by inverse iteration (LU with partial pivoting of T - lambda I,
-//      kEpInvIters steps from a fixed start, Gram-Schmidt against the first when the two are closer
-//      than 1e-3 ||T||), mapped back through the tridiagonal and QR reflectors.
+//      T = H_7..H_0 B H_0..H_7 (scaled by a power of two to ||T|| in [1, 2)), the two smallest
+//      eigenvalues of T by 33-way multisection of the Sturm count, their vectors by inverse
+//      iteration (LU with partial pivoting of T - lambda I, kEpInvIters solves from a fixed start,
+//      the second made orthogonal to the first after every solve when the two are closer than
+//      1e-3 ||T||, as LAPACK's dstein does), mapped back through the tridiagonal and QR reflectors.
 // v[0], v[1] = null vectors (Q e_10, Q e_11), v[2], v[3] = eigenvectors of the smallest and the
 // second smallest nonzero eigenvalue (m = 4: v[k] = Q e_{8+k}).  The null space is as accurate as M
-// (not M^T M) allows; the eigenvectors within it are an arbitrary orthonormal basis, as any
-// solver's are.  Every step is a fixed sequence of IEEE operations; pnp.hip spreads each over a
-// wave (one lane per column / row / multisection point) without changing any value.
-constexpr int kEpMsSteps = 12;  // multisection steps: 33^12 > 2^60, below the rounding of any interval
+// (not M^T M) allows; within it the basis is the QR's, which numpy's QR of the same M^T reproduces
+// (tests/indep.py) -- any solver's basis there is arbitrary, and EPnP's N = 2 / 3 approximations
+// depend on it.  Every step is a fixed sequence of IEEE operations (sums in tsum's tree order);
+// pnp.hip spreads each over a wave (one lane per column / row / multisection point) without
+// changing any value.
+constexpr int kEpMsSteps = 10;  // multisection steps: 33^10 > 1.5e15, the interval at the rounding of ||T||
 constexpr int kEpMsPts = 32;    // interior points per step and eigenvalue
-constexpr int kEpInvIters = 3;  // inverse iterations
-constexpr double kEpBig = 0x1p256, kEpSmall = 0x1p-256, kEpTiny = 0x1p-200;
+constexpr int kEpInvIters = 3;  // inverse iteration solves
+constexpr double kEpTiny = 0x1p-200;
 
 // Householder reflector H = I - tau u u^T taking x (sum of squares s, leading entry x0) to alpha e_0;
 // u = (x0 - alpha, x_1, ...), tau = 1 / (|x| (|x| + |x0|)) = 2 / u^T u (0 when x = 0).
@@ -558,10 +588,10 @@ VS_HD inline double ep_mt(const double (*al)[4], const double* uv, const Cam& K,
     return (j & 1) ? epnp_m1(al[i], uv[2 * i + 1], K, r) : epnp_m0(al[i], uv[2 * i], K, r);
 }
 
-// Sturm count of the 10 x 10 tridiagonal (d, e2 = e^2): the number of eigenvalues < x, from the
-// sign changes of the leading principal minors p_i = (d_i - x) p_{i-1} - e2_{i-1} p_{i-2}.  A zero
-// minor becomes -2^-200 p_{i-1} (a tiny pivot of the other sign, as a Sturm / LDL^T count treats
-// it); consecutive minors are rescaled together by 2^-+256 outside [2^-256, 2^256].
+// Sturm count of the 10 x 10 tridiagonal (d, e2 = e^2, ||T|| < 2): the number of eigenvalues < x,
+// from the sign changes of the leading principal minors p_i = (d_i - x) p_{i-1} - e2_{i-1} p_{i-2}.
+// A zero minor becomes -2^-200 p_{i-1} (a tiny pivot of the other sign, as an LDL^T count treats
+// it).  With ||T|| < 2 and x inside the Gershgorin interval |p_i| < 6^10, so no rescaling.
 VS_HD inline int ep_sturm(const double* d, const double* e2, double x) {
     double pp = 1.0, pc = d[0] - x;
     if (pc == 0) pc = -kEpTiny;
@@ -573,11 +603,6 @@ VS_HD inline int ep_sturm(const double* d, const double* e2, double x) {
         cnt += (pn < 0) != (pc < 0);
         pp = pc;
         pc = pn;
-        const double a = fabs(pc), b = fabs(pp);
-        const double mx = a > b ? a : b;
-        const double sc = mx > kEpBig ? kEpSmall : mx < kEpSmall ? kEpBig : 1.0;
-        pc *= sc;
-        pp *= sc;
     }
     return cnt;
 }
@@ -633,11 +658,14 @@ VS_HD inline void ep_lu_solve(const EpLu& f, double* b) {
     VS_UNROLL
     for (int i = 7; i >= 0; i--) b[i] = (b[i] - f.du[i] * b[i + 1] - f.du2[i] * b[i + 2]) * f.inv[i];
 }
-VS_HD inline void ep_normalize10(double* y) {
-    double s = 0;
+VS_HD inline double ep_dot10(const double* a, const double* b) {
+    double t[10];
     VS_UNROLL
-    for (int i = 0; i < 10; i++) s += y[i] * y[i];
-    const double inv = 1.0 / sqrt(s);
+    for (int i = 0; i < 10; i++) t[i] = a[i] * b[i];
+    return tsum<10>(t);
+}
+VS_HD inline void ep_normalize10(double* y) {
+    const double inv = 1.0 / sqrt(ep_dot10(y, y));
     VS_UNROLL
     for (int i = 0; i < 10; i++) y[i] *= inv;
 }
@@ -646,24 +674,36 @@ VS_HD inline double ep_start(int i) {
     constexpr double s[10] = {0.53, -0.41, 0.37, 0.61, -0.29, 0.47, -0.33, 0.59, 0.43, -0.51};
     return s[i];
 }
+// y1 -= (y0 . y1 / y0 . y0) y0 (the solves' growth, at most ~2^52 each, is never normalised away
+// in between: kEpInvIters solves stay far inside the double range)
+VS_HD inline void ep_orth10(const double* y0, double* y1) {
+    const double c = ep_dot10(y0, y1) / ep_dot10(y0, y0);
+    VS_UNROLL
+    for (int i = 0; i < 10; i++) y1[i] = y1[i] - c * y0[i];
+}
+// 2^-e with ||T|| * 2^-e in [1, 2) (exact; 1 for ||T|| = 0 or not finite)
+VS_HD inline double ep_scale(double tnorm) {
+    if (!(tnorm > 0) || !(tnorm <= DBL_MAX)) return 1.0;
+    int e;
+    frexp(tnorm, &e);  // tnorm = f 2^e, f in [0.5, 1)
+    return ldexp(1.0, 1 - e);
+}
 
 // Sequential statement (host oracle; the device's parallel version in pnp.hip is bit-identical).
 VS_HD inline void epnp_small_eig(const double (*al)[4], const double* uv, int m, const Cam& K, double v[4][12]) {
     const int nc = 2 * m;  // 8 or 10
-    double C[10][12], alpha[10], tau[10];
+    double C[10][12], alpha[10], tau[10], t[12];
     for (int j = 0; j < nc; j++)
         for (int r = 0; r < 12; r++) C[j][r] = ep_mt(al, uv, K, j, r);
     // 1. QR of M^T: column k keeps its reflector u (rows k..11), alpha[k] = R_kk
     for (int k = 0; k < nc; k++) {
-        double s = 0;
-        for (int r = k; r < 12; r++) s += C[k][r] * C[k][r];
+        for (int r = 0; r < 12; r++) t[r] = r >= k ? C[k][r] * C[k][r] : -0.0;
         double u0;
-        ep_householder(s, C[k][k], alpha[k], u0, tau[k]);
+        ep_householder(tsum<12>(t), C[k][k], alpha[k], u0, tau[k]);
         C[k][k] = u0;
         for (int j = k + 1; j < nc; j++) {
-            double w = 0;
-            for (int r = k; r < 12; r++) w += C[k][r] * C[j][r];
-            const double f = tau[k] * w;
+            for (int r = 0; r < 12; r++) t[r] = r >= k ? C[k][r] * C[j][r] : -0.0;
+            const double f = tau[k] * tsum<12>(t);
             for (int r = k; r < 12; r++) C[j][r] = C[j][r] - f * C[k][r];
         }
     }
@@ -676,29 +716,26 @@ VS_HD inline void epnp_small_eig(const double (*al)[4], const double* uv, int m,
         double B[10][10];
         for (int a = 0; a < 10; a++)
             for (int b = a; b < 10; b++) {
-                double s = 0;
-                for (int k = b; k < 10; k++) s += (k == a ? alpha[a] : C[k][a]) * (k == b ? alpha[b] : C[k][b]);
-                B[a][b] = B[b][a] = s;
+                for (int k = 0; k < 10; k++)
+                    t[k] = k >= b ? (k == a ? alpha[a] : C[k][a]) * (k == b ? alpha[b] : C[k][b]) : -0.0;
+                B[a][b] = B[b][a] = tsum<10>(t);
             }
         // tridiagonalisation: reflector k (indices k+1..9) in U[k], tau in tt[k]
         double d[10], e[9], U[8][10], tt[8];
         for (int k = 0; k < 8; k++) {
-            double s = 0;
-            for (int j = k + 1; j < 10; j++) s += B[k][j] * B[k][j];
-            double u0, t;
-            ep_householder(s, B[k][k + 1], e[k], u0, t);
+            for (int j = 0; j < 10; j++) t[j] = j > k ? B[k][j] * B[k][j] : -0.0;
+            double u0, tk;
+            ep_householder(tsum<10>(t), B[k][k + 1], e[k], u0, tk);
             d[k] = B[k][k];
-            tt[k] = t;
-            for (int j = k + 1; j < 10; j++) U[k][j] = j == k + 1 ? u0 : B[k][j];
+            tt[k] = tk;
+            for (int j = 0; j < 10; j++) U[k][j] = j > k + 1 ? B[k][j] : j == k + 1 ? u0 : 0.0;
             double p[10], w[10];
             for (int i = k + 1; i < 10; i++) {
-                double q = 0;
-                for (int j = k + 1; j < 10; j++) q += B[i][j] * U[k][j];
-                p[i] = t * q;
+                for (int j = 0; j < 10; j++) t[j] = j > k ? B[i][j] * U[k][j] : -0.0;
+                p[i] = tk * tsum<10>(t);
             }
-            double pv = 0;
-            for (int i = k + 1; i < 10; i++) pv += p[i] * U[k][i];
-            const double Kc = (0.5 * t) * pv;
+            for (int i = 0; i < 10; i++) t[i] = i > k ? p[i] * U[k][i] : -0.0;
+            const double Kc = (0.5 * tk) * tsum<10>(t);
             for (int i = k + 1; i < 10; i++) w[i] = p[i] - Kc * U[k][i];
             for (int i = k + 1; i < 10; i++)
                 for (int j = k + 1; j < 10; j++) B[i][j] = B[i][j] - (U[k][i] * w[j] + w[i] * U[k][j]);
@@ -706,69 +743,67 @@ VS_HD inline void epnp_small_eig(const double (*al)[4], const double* uv, int m,
         d[8] = B[8][8];
         d[9] = B[9][9];
         e[8] = B[8][9];
-        // 3. the two smallest eigenvalues: Gershgorin interval, multisection
-        double e2[9], lo = 0, hi = 0;
-        for (int i = 0; i < 9; i++) e2[i] = e[i] * e[i];
+        // 3. scaled to ||T|| in [1, 2) (Gershgorin bound); the two smallest eigenvalues by multisection
+        double lo = 0, hi = 0;
         for (int i = 0; i < 10; i++) {
             const double rad = (i > 0 ? fabs(e[i - 1]) : 0.0) + (i < 9 ? fabs(e[i]) : 0.0);
             const double l = d[i] - rad, h = d[i] + rad;
             lo = (i == 0 || l < lo) ? l : lo;
             hi = (i == 0 || h > hi) ? h : hi;
         }
+        const double sc = ep_scale(fabs(lo) > fabs(hi) ? fabs(lo) : fabs(hi));
+        double e2[9];
+        for (int i = 0; i < 10; i++) d[i] *= sc;
+        for (int i = 0; i < 9; i++) {
+            e[i] *= sc;
+            e2[i] = e[i] * e[i];
+        }
+        lo *= sc;
+        hi *= sc;
         double a_t[2] = {lo, lo}, b_t[2] = {hi, hi};
         for (int st = 0; st < kEpMsSteps; st++)
-            for (int t = 0; t < 2; t++) {
-                const double a = a_t[t], wd = b_t[t] - a_t[t];
+            for (int q = 0; q < 2; q++) {
+                const double a = a_t[q], wd = b_t[q] - a_t[q];
                 int js = kEpMsPts;
                 for (int j = 0; j < kEpMsPts; j++)
-                    if (ep_sturm(d, e2, a + wd * ep_frac(j)) > t) {
+                    if (ep_sturm(d, e2, a + wd * ep_frac(j)) > q) {
                         js = j;
                         break;
                     }
-                a_t[t] = js > 0 ? a + wd * ep_frac(js - 1) : a;
-                b_t[t] = js < kEpMsPts ? a + wd * ep_frac(js) : b_t[t];
+                a_t[q] = js > 0 ? a + wd * ep_frac(js - 1) : a;
+                b_t[q] = js < kEpMsPts ? a + wd * ep_frac(js) : b_t[q];
             }
         // 4. inverse iteration
-        const double fa = fabs(lo), fb = fabs(hi);
-        const double tnorm = fa > fb ? fa : fb;
+        const double tnorm = fabs(lo) > fabs(hi) ? fabs(lo) : fabs(hi);
         const double tiny = tnorm > 0 ? DBL_EPSILON * tnorm : DBL_MIN;
         double lam[2], y[2][10];
         EpLu f[2];
-        for (int t = 0; t < 2; t++) {
-            lam[t] = 0.5 * (a_t[t] + b_t[t]);
-            ep_lu(d, e, lam[t], tiny, f[t]);
-            for (int i = 0; i < 10; i++) y[t][i] = ep_start(i);
+        for (int q = 0; q < 2; q++) {
+            lam[q] = 0.5 * (a_t[q] + b_t[q]);
+            ep_lu(d, e, lam[q], tiny, f[q]);
+            for (int i = 0; i < 10; i++) y[q][i] = ep_start(i);
         }
         const bool cluster = lam[1] - lam[0] <= 1e-3 * tnorm;
         for (int it = 0; it < kEpInvIters; it++) {
-            for (int t = 0; t < 2; t++) {
-                ep_lu_solve(f[t], y[t]);
-                ep_normalize10(y[t]);
-            }
-            if (cluster) {
-                double dt = 0;
-                for (int i = 0; i < 10; i++) dt += y[0][i] * y[1][i];
-                for (int i = 0; i < 10; i++) y[1][i] = y[1][i] - dt * y[0][i];
-                ep_normalize10(y[1]);
-            }
+            for (int q = 0; q < 2; q++) ep_lu_solve(f[q], y[q]);
+            if (cluster) ep_orth10(y[0], y[1]);
         }
-        // 5. back through the tridiagonal reflectors (H_7 first), into the QR basis
-        for (int t = 0; t < 2; t++) {
+        // 5. normalised, back through the tridiagonal reflectors (H_7 first), into the QR basis
+        for (int q = 0; q < 2; q++) {
+            ep_normalize10(y[q]);
             for (int k = 7; k >= 0; k--) {
-                double w = 0;
-                for (int i = k + 1; i < 10; i++) w += U[k][i] * y[t][i];
-                const double fk = tt[k] * w;
-                for (int i = k + 1; i < 10; i++) y[t][i] = y[t][i] - fk * U[k][i];
+                for (int i = 0; i < 10; i++) t[i] = i > k ? U[k][i] * y[q][i] : -0.0;
+                const double fk = tt[k] * tsum<10>(t);
+                for (int i = k + 1; i < 10; i++) y[q][i] = y[q][i] - fk * U[k][i];
             }
-            for (int r = 0; r < 10; r++) x[2 + t][r] = y[t][r];
+            for (int r = 0; r < 10; r++) x[2 + q][r] = y[q][r];
         }
     }
     // 6. v = Q x (Q = H_0 .. H_{nc-1}: H_{nc-1} first)
     for (int q = 0; q < 4; q++) {
         for (int k = nc - 1; k >= 0; k--) {
-            double w = 0;
-            for (int r = k; r < 12; r++) w += C[k][r] * x[q][r];
-            const double fk = tau[k] * w;
+            for (int r = 0; r < 12; r++) t[r] = r >= k ? C[k][r] * x[q][r] : -0.0;
+            const double fk = tau[k] * tsum<12>(t);
             for (int r = k; r < 12; r++) x[q][r] = x[q][r] - fk * C[k][r];
         }
         for (int r = 0; r < 12; r++) v[q][r] = x[q][r];
@@ -924,10 +959,16 @@ VS_HD inline void epnp_betas_init_uniform(int s, const double L[6][10], const do
 }
 
 // Gauss-Newton on the betas, then the pose by Kabsch; returns the mean reprojection error.
-template <int MAXN>
+struct NoMark {
+    VS_HD void operator()(int) const {}
+};
+// mark(k) at the stage ends (0: Gauss-Newton, 1: control points + cross-covariance, 2: Kabsch,
+// 3: reprojection error): the device's profiling build counts cycles there, everything else
+// passes NoMark
+template <int MAXN, class Mark = NoMark>
 VS_HD inline double epnp_refine(double be[4], const double L[6][10], const double rho[6], const double v[4][12],
                                 const double (*alphas)[4], const double* X, const double* uv, int n, const Cam& K,
-                                double* R, double* t) {
+                                double* R, double* t, Mark mark = Mark()) {
     for (int it = 0; it < 5; it++) {  // Gauss-Newton on the 6 distance constraints
         double A[24], b[6], x[4];
         for (int j = 0; j < 6; j++) {
@@ -944,6 +985,7 @@ VS_HD inline double epnp_refine(double be[4], const double L[6][10], const doubl
         lstsq<6, 4>(A, b, x);
         for (int k = 0; k < 4; k++) be[k] += x[k];
     }
+    mark(0);
     // camera coordinates of control and object points
     double ccs[4][3];
     for (int i = 0; i < 4; i++)
@@ -978,8 +1020,10 @@ VS_HD inline double epnp_refine(double be[4], const double L[6][10], const doubl
         for (int a = 0; a < 3; a++)
             for (int b = 0; b < 3; b++) ABt[a * 3 + b] += pc[a] * pw[b];
     }
+    mark(1);
     rotation_from_cross(ABt, R);
     for (int c = 0; c < 3; c++) t[c] = pc0[c] - (R[c * 3] * pw0[0] + R[c * 3 + 1] * pw0[1] + R[c * 3 + 2] * pw0[2]);
+    mark(2);
     double err = 0;
     VS_UNROLL
     for (int i = 0; i < MAXN; i++) {
@@ -989,6 +1033,7 @@ VS_HD inline double epnp_refine(double be[4], const double L[6][10], const doubl
         const double du = uv[2 * i] - u, dvv = uv[2 * i + 1] - vv;
         err += sqrt(du * du + dvv * dvv);
     }
+    mark(3);
     return err / n;
 }
 
