@@ -92,7 +92,7 @@ extern "C" int orc_epnp_debug(const double* X, const double* uv, const int* m, i
     for (int p = 0; p < count; p++) {
         double* o = out + (size_t)p * 73;
         double cw[4][3], al[5][4], v[4][12], R[9] = {}, t[3] = {};
-        bool ok = m[p] >= 4 && m[p] <= 5 && epnp_control(X + 15 * p, m[p], cw, al);
+        bool ok = m[p] >= 4 && m[p] <= 5 && epnp_control<5>(X + 15 * p, m[p], cw, al);
         if (ok) epnp_small_eig(al, uv + 10 * p, m[p], cam, v);
         for (int k = 0; k < 48; k++) o[k] = ok ? v[k / 12][k % 12] : 0.0;
         ok = ok && epnp<5>(X + 15 * p, uv + 10 * p, m[p], cam, R, t);

@@ -42,7 +42,7 @@ def main():
     step(0)
     torch.cuda.synchronize()
     cyc = np.zeros(8, np.uint64)
-    pcyc = np.zeros(24, np.uint64)  # vs_debug_pnp_cycles copies 24 counters
+    pcyc = np.zeros(32, np.uint64)  # vs_debug_pnp_cycles copies 32 counters
     rcyc = np.zeros(8, np.uint64)
     lib.vs_debug_fm_cycles(cyc.ctypes.data, 1)
     lib.vs_debug_pnp_cycles(pcyc.ctypes.data, 1)
@@ -62,12 +62,14 @@ def main():
                       "kcycles_per_launch": {names[k]: round(float(cyc[k]) / calls / 1e3, 1) for k in range(1, 8)},
                       "pnp_hyp_kcycles_per_hypothesis_x100": {
                           n: round(float(pcyc[k]) / max(1, prof.get("solve_pnp", (0, 1))[1]) / 1e3, 1)
-                          for k, n in ((0, "load+control"), (1, "eig: M^T QR + R R^T"), (2, "eig: tridiagonal"),
+                          for k, n in ((21, "points to LDS + subset"), (22, "control: centroid + covariance"), (23, "control: sym_eig<3>"),
+                                       (24, "control: axes, CC"), (25, "control: inverse + alphas"), (0, "control: rest"), (1, "eig: M^T QR + R R^T"), (2, "eig: tridiagonal"),
                                        (3, "eig: multisection"), (13, "eig: inverse iteration"),
                                        (14, "eig: Q back-transform"), (15, "variants: L, rho, initial betas"),
                                        (16, "variants: Gauss-Newton"), (17, "variants: control points, ABt"),
                                        (18, "variants: Kabsch"), (19, "variants: reprojection error"),
-                                       (4, "variants: rest"), (5, "count"))},
+                                       (4, "variants: rest"), (20, "best + Rodrigues round trip"),
+                                       (5, "count"))},
                       "pnp_ransac_kcycles_per_call": {
                           n: round(float(pcyc[k]) / max(1, prof.get("solve_pnp", (0, 1))[1]) / 1e3, 1)
                           for k, n in ((6, "replay"), (7, "lm tail"), (8, "inlier mask + lm rotations"), (9, "lm point terms"),

@@ -32,7 +32,7 @@ constexpr int kPnpMaxIters = VS_PNP_MAX_ITERS;
 
 #ifdef VS_PNP_PROFILE
 // k_pnp_hyp phase cycle counters (profiling build only: make -C visual-slam-pipeline_amd prof)
-__device__ unsigned long long g_pnp_cycles[24];  // k_pnp_hyp 0-5, 13-19 (1-3, 13-14 eigen stages, 15-19 the variants' stages), 6-7 k_pnp_ransac, 8-12 its LM split
+__device__ unsigned long long g_pnp_cycles[32];  // k_pnp_hyp 0-5, 13-21 (1-3, 13-14 eigen stages, 15-19 the variants' stages, 20-21 loads / Rodrigues, 22-25 control points), 6-7 k_pnp_ransac, 8-12 its LM split
 #define PNP_T0() long long _pn_t = clock64()
 #define PNP_T(k)                                                             \
     do {                                                                     \
@@ -66,6 +66,7 @@ struct PnpHyp {
 // for every n in [kPnpTabMinN, kPnpTabMaxN] (2 MB) and k_pnp_hyp indexes that table by n: no
 // subset launch on the tracker's per-frame path.
 constexpr int kPnpTabIters = 100, kPnpTabMinN = 6, kPnpTabMaxN = 1024;
+constexpr int kPnpLdsPts = 512;  // points k_pnp_hyp stages in LDS (the tracker's problems have <= 400)
 
 __device__ __forceinline__ const int* pnp_subset(const PnpHyp& H, int pb, int n, int h) {
     return H.tab_n0 >= 0 ? H.subset + ((size_t)(n - H.tab_n0) * H.stride + h) * 5
@@ -450,8 +451,9 @@ __global__ __launch_bounds__(64) void k_pnp_hyp(const float* __restrict__ obj_al
                                                 int niters0, float thr2, int min_inliers, PnpHyp H) {
     crit_prio();
     __shared__ EpShared sE;
+    __shared__ float sObj[3 * kPnpLdsPts], sImg[2 * kPnpLdsPts];  // the problem's first points, for the count
     __shared__ double sX[15], sUV[10], sAl[5][4], sCw[4][3];
-    __shared__ double sErr[3], sRt[3][12];
+    __shared__ double sErr[3], sRt[3][12], sL[6][10], sRho[6];
     __shared__ int sOk;
     const int pb = blockIdx.x, h = blockIdx.y, lane = threadIdx.x;
     const int o0 = off[pb], n = off[pb + 1] - o0;
@@ -465,18 +467,47 @@ __global__ __launch_bounds__(64) void k_pnp_hyp(const float* __restrict__ obj_al
     const int* idx = single ? nullptr : pnp_subset(H, pb, n, h);
     const int m = model_points;
     PNP_T0();
-    if (lane < m) {
-        const int i = single ? lane : idx[lane];
-        sX[3 * lane] = obj[3 * i];
-        sX[3 * lane + 1] = obj[3 * i + 1];
-        sX[3 * lane + 2] = obj[3 * i + 2];
-        sUV[2 * lane] = img[2 * i];
-        sUV[2 * lane + 1] = img[2 * i + 1];
+    // the problem's points (up to kPnpLdsPts) into LDS, loaded beside the subset indices: the
+    // subset gather and the inlier count then read LDS instead of two dependent global loads
+    const int nl = n < kPnpLdsPts ? n : kPnpLdsPts;
+    const int si = lane < m ? (single ? lane : idx[lane]) : 0;
+    {
+        float ob[3 * kPnpLdsPts / 64], im[2 * kPnpLdsPts / 64];
+#pragma unroll
+        for (int j = 0; j < 3 * kPnpLdsPts / 64; j++) ob[j] = lane + 64 * j < 3 * nl ? obj[lane + 64 * j] : 0.f;
+#pragma unroll
+        for (int j = 0; j < 2 * kPnpLdsPts / 64; j++) im[j] = lane + 64 * j < 2 * nl ? img[lane + 64 * j] : 0.f;
+#pragma unroll
+        for (int j = 0; j < 3 * kPnpLdsPts / 64; j++) sObj[lane + 64 * j] = ob[j];
+#pragma unroll
+        for (int j = 0; j < 2 * kPnpLdsPts / 64; j++) sImg[lane + 64 * j] = im[j];
     }
     __syncthreads();
+    if (lane < m) {
+        const float* o = si < nl ? sObj + 3 * si : obj + 3 * si;
+        const float* q = si < nl ? sImg + 2 * si : img + 2 * si;
+        sX[3 * lane] = o[0];
+        sX[3 * lane + 1] = o[1];
+        sX[3 * lane + 2] = o[2];
+        sUV[2 * lane] = q[0];
+        sUV[2 * lane + 1] = q[1];
+    }
+    __syncthreads();
+    PNP_T(21);
     if (lane == 0) {
-        double cw[4][3], al[5][4];
-        sOk = epnp_control(sX, m, cw, al);
+        double cw[4][3], al[5][4], Xr[15];
+#pragma unroll
+        for (int i = 0; i < 15; i++) Xr[i] = i < 3 * m ? sX[i] : 0.0;  // registers, not LDS, in the sums
+#ifdef VS_PNP_PROFILE
+        const int cslot[4] = {22, 23, 24, 25};
+        auto cmark = [&](int k) {
+            atomicAdd(&g_pnp_cycles[cslot[k]], (unsigned long long)(clock64() - _pn_t));
+            _pn_t = clock64();
+        };
+        sOk = epnp_control<5>(Xr, m, cw, al, cmark);
+#else
+        sOk = epnp_control<5>(Xr, m, cw, al);
+#endif
         for (int i = 0; i < 4; i++)
             for (int c = 0; c < 3; c++) sCw[i][c] = cw[i][c];
         for (int i = 0; i < m; i++)
@@ -494,29 +525,18 @@ __global__ __launch_bounds__(64) void k_pnp_hyp(const float* __restrict__ obj_al
         epnp_small_eig_wave(sAl, sUV, m, K, lane, sE, tp);
 #endif
         __syncthreads();
+        // L_6x10 and rho once for the three approximations, one entry per lane, kept in LDS with
+        // the eigenvectors, alphas and points: the variants read them there instead of holding
+        // ~190 VGPRs of copies through the Gauss-Newton loop
+        if (lane < 60) sL[lane / 10][lane % 10] = epnp_L_entry(sE.v, lane / 10, lane % 10);
+        if (lane < 6) sRho[lane] = epnp_rho_entry(sCw, lane);
+        __syncthreads();
         if (lane < 3) {  // one beta approximation per lane
-            double cw[4][3], v[4][12], L[6][10], rho[6], al[5][4], X[15], uv[10];
-            for (int i = 0; i < 4; i++)
-                for (int c = 0; c < 3; c++) cw[i][c] = sCw[i][c];
-            // constant bounds (m <= 5): the copies unroll and the arrays stay in registers
-#pragma unroll
-            for (int i = 0; i < 5; i++)
-#pragma unroll
-                for (int j = 0; j < 4; j++) al[i][j] = i < m ? sAl[i][j] : 0.0;
-#pragma unroll
-            for (int i = 0; i < 15; i++) X[i] = i < 3 * m ? sX[i] : 0.0;
-#pragma unroll
-            for (int i = 0; i < 10; i++) uv[i] = i < 2 * m ? sUV[i] : 0.0;
-#pragma unroll
-            for (int k = 0; k < 4; k++)
-#pragma unroll
-                for (int i = 0; i < 12; i++) v[k][i] = sE.v[k][i];
-            epnp_L_rho_v(v, cw, L, rho);
             double R[9], t[3];
             // the three approximations as one code path on lanes 0..2 (pnp_solvers.h
             // epnp_betas_init_uniform: bit-identical to epnp_variant's divergent solves)
             double be[4];
-            epnp_betas_init_uniform(lane, L, rho, be);
+            epnp_betas_init_uniform(lane, sL, sRho, be);
 #ifdef VS_PNP_PROFILE
             PNP_T(15);  // L, rho, initial betas
             const int slot[4] = {16, 17, 18, 19};
@@ -524,9 +544,9 @@ __global__ __launch_bounds__(64) void k_pnp_hyp(const float* __restrict__ obj_al
                 if (lane == 0) atomicAdd(&g_pnp_cycles[slot[k]], (unsigned long long)(clock64() - _pn_t));
                 _pn_t = clock64();
             };
-            sErr[lane] = epnp_refine<5>(be, L, rho, v, al, X, uv, m, K, R, t, mark);
+            sErr[lane] = epnp_refine<5>(be, sL, sRho, sE.v, sAl, sX, sUV, m, K, R, t, mark);
 #else
-            sErr[lane] = epnp_refine<5>(be, L, rho, v, al, X, uv, m, K, R, t);
+            sErr[lane] = epnp_refine<5>(be, sL, sRho, sE.v, sAl, sX, sUV, m, K, R, t);
 #endif
             for (int k = 0; k < 9; k++) sRt[lane][k] = R[k];
             for (int k = 0; k < 3; k++) sRt[lane][9 + k] = t[k];
@@ -547,8 +567,11 @@ __global__ __launch_bounds__(64) void k_pnp_hyp(const float* __restrict__ obj_al
     if (ok) {
         double R[9];
         rod_v2m(rv, R);
+        PNP_T(20);
         int c = 0;
-        for (int i = lane; i < n; i += 64)
+        for (int i = lane; i < nl; i += 64)
+            c += reproj_err2(R, tv, K, sObj[3 * i], sObj[3 * i + 1], sObj[3 * i + 2], sImg[2 * i], sImg[2 * i + 1]) <= thr2;
+        for (int i = nl + lane; i < n; i += 64)
             c += reproj_err2(R, tv, K, obj[3 * i], obj[3 * i + 1], obj[3 * i + 2], img[2 * i], img[2 * i + 1]) <= thr2;
         for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o);
         cnt = c;
@@ -818,7 +841,7 @@ __global__ void k_debug_epnp(const double* X, const double* uv, const int* m, in
     const Cam K{fx, fy, cx, cy};
     double* o = out + (size_t)p * 73;
     double cw[4][3], al[5][4], v[4][12], R[9] = {}, t[3] = {};
-    bool ok = epnp_control(X + 15 * p, m[p], cw, al);
+    bool ok = epnp_control<5>(X + 15 * p, m[p], cw, al);
     if (ok) epnp_small_eig(al, uv + 10 * p, m[p], K, v);
     for (int k = 0; k < 48; k++) o[k] = ok ? v[k / 12][k % 12] : 0.0;
     ok = ok && epnp<5>(X + 15 * p, uv + 10 * p, m[p], K, R, t);
@@ -858,10 +881,10 @@ extern "C" int vs_debug_epnp(const double* X, const double* uv, const int* m, in
 
 #ifdef VS_PNP_PROFILE
 extern "C" int vs_debug_pnp_cycles(unsigned long long* out, int reset) {
-    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(vs::g_pnp_cycles), sizeof(unsigned long long) * 24) != hipSuccess)
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(vs::g_pnp_cycles), sizeof(unsigned long long) * 32) != hipSuccess)
         return -1;
     if (reset) {
-        unsigned long long z[24] = {};
+        unsigned long long z[32] = {};
         if (hipMemcpyToSymbol(HIP_SYMBOL(vs::g_pnp_cycles), z, sizeof(z)) != hipSuccess) return -1;
     }
     return 0;

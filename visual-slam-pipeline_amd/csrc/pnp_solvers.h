@@ -26,9 +26,11 @@
 #if defined(__HIPCC__)
 #define VS_HD __host__ __device__
 #define VS_UNROLL _Pragma("unroll")
+#define VS_NOUNROLL _Pragma("unroll 1")
 #else
 #define VS_HD
 #define VS_UNROLL
+#define VS_NOUNROLL
 #endif
 
 namespace vs_pnp {
@@ -463,6 +465,10 @@ VS_HD inline float reproj_err2(const double* R, const double* t, const Cam& K, f
 }
 
 // ----------------------------------------------------------------------------------- EPnP
+// stage marks for the device's profiling build (cycle counters); everything else passes NoMark
+struct NoMark {
+    VS_HD void operator()(int) const {}
+};
 // Written as stages so the device can spread one hypothesis over a wave (pnp.hip): control
 // points and barycentric coordinates, one M^T M entry at a time (each entry's sum runs over the
 // points in order, as the host's row-pair accumulation does), the 12 x 12 eigen-decomposition,
@@ -470,21 +476,30 @@ VS_HD inline float reproj_err2(const double* R, const double* t, const Cam& K, f
 // pose per call.  epnp() composes them sequentially; the device composes the same functions.
 
 // Control points cw (centroid + principal axes) and barycentric coordinates; false if degenerate.
-VS_HD inline bool epnp_control(const double* X, int n, double cw[4][3], double (*alphas)[4]) {
+// MAXN bounds n at compile time (the point loops run to MAXN with an i < n guard, the same
+// operations in the same order), so on the device they unroll over a register copy of the points.
+template <int MAXN, class Mark = NoMark>
+VS_HD inline bool epnp_control(const double* X, int n, double cw[4][3], double (*alphas)[4], Mark mark = Mark()) {
     for (int j = 0; j < 3; j++) {
         double s = 0;
-        for (int i = 0; i < n; i++) s += X[3 * i + j];
+        VS_UNROLL
+        for (int i = 0; i < MAXN; i++)
+            if (i < n) s += X[3 * i + j];
         cw[0][j] = s / n;
     }
     double C[9];
     for (int a = 0; a < 3; a++)
         for (int b = 0; b < 3; b++) {
             double s = 0;
-            for (int i = 0; i < n; i++) s += (X[3 * i + a] - cw[0][a]) * (X[3 * i + b] - cw[0][b]);
+            VS_UNROLL
+            for (int i = 0; i < MAXN; i++)
+                if (i < n) s += (X[3 * i + a] - cw[0][a]) * (X[3 * i + b] - cw[0][b]);
             C[a * 3 + b] = s;
         }
+    mark(0);
     double dc[3], uc[9];
     sym_eig<3>(C, dc, uc);
+    mark(1);
     // Each principal axis with its largest-magnitude component positive (the first on ties): the
     // control points, hence M and the QR basis of its null space (epnp_small_eig), stop depending
     // on the eigen-solver's arbitrary signs.
@@ -503,6 +518,7 @@ VS_HD inline bool epnp_control(const double* X, int n, double cw[4][3], double (
     double CC[9];
     for (int r = 0; r < 3; r++)
         for (int c = 0; c < 3; c++) CC[r * 3 + c] = cw[c + 1][r] - cw[0][r];
+    mark(2);
     const double det = det3(CC);
     if (fabs(det) < 1e-300) return false;
     double CI[9];
@@ -515,7 +531,9 @@ VS_HD inline bool epnp_control(const double* X, int n, double cw[4][3], double (
     CI[6] = (CC[3] * CC[7] - CC[4] * CC[6]) / det;
     CI[7] = (CC[1] * CC[6] - CC[0] * CC[7]) / det;
     CI[8] = (CC[0] * CC[4] - CC[1] * CC[3]) / det;
-    for (int i = 0; i < n; i++) {
+    VS_UNROLL
+    for (int i = 0; i < MAXN; i++) {
+        if (i >= n) continue;
         const double p[3] = {X[3 * i] - cw[0][0], X[3 * i + 1] - cw[0][1], X[3 * i + 2] - cw[0][2]};
         double a1 = CI[0] * p[0] + CI[1] * p[1] + CI[2] * p[2];
         double a2 = CI[3] * p[0] + CI[4] * p[1] + CI[5] * p[2];
@@ -525,6 +543,7 @@ VS_HD inline bool epnp_control(const double* X, int n, double cw[4][3], double (
         alphas[i][3] = a3;
         alphas[i][0] = 1.0 - a1 - a2 - a3;
     }
+    mark(3);
     return true;
 }
 
@@ -819,25 +838,27 @@ VS_HD inline void epnp_L_rho(const double* um, const double cw[4][3], double v[4
     epnp_L_rho_v(v, cw, L, rho);
 }
 // L and rho from the four eigenvectors v[k] (k-th smallest eigenvalue)
+// Entry (j, c) of L_6x10 (pair j of control points, product c of the betas) and rho[j]: one
+// expression per entry, so the device computes each on its own lane with the same arithmetic.
+VS_HD inline double epnp_L_entry(const double v[4][12], int j, int c) {
+    constexpr int pa[6] = {0, 0, 0, 1, 1, 2}, pb[6] = {1, 2, 3, 2, 3, 3};
+    constexpr int ka[10] = {0, 0, 1, 0, 1, 2, 0, 1, 2, 3}, kb[10] = {0, 1, 1, 2, 2, 2, 3, 3, 3, 3};
+    const int a = ka[c], b = kb[c], p = 3 * pa[j], q = 3 * pb[j];
+    const double d0 = (v[a][p] - v[a][q]) * (v[b][p] - v[b][q]);
+    const double d1 = (v[a][p + 1] - v[a][q + 1]) * (v[b][p + 1] - v[b][q + 1]);
+    const double d2 = (v[a][p + 2] - v[a][q + 2]) * (v[b][p + 2] - v[b][q + 2]);
+    const double dt = d0 + d1 + d2;
+    return a == b ? dt : 2.0 * dt;
+}
+VS_HD inline double epnp_rho_entry(const double cw[4][3], int j) {
+    constexpr int pa[6] = {0, 0, 0, 1, 1, 2}, pb[6] = {1, 2, 3, 2, 3, 3};
+    const double dx = cw[pa[j]][0] - cw[pb[j]][0], dy = cw[pa[j]][1] - cw[pb[j]][1], dz = cw[pa[j]][2] - cw[pb[j]][2];
+    return dx * dx + dy * dy + dz * dz;
+}
 VS_HD inline void epnp_L_rho_v(const double v[4][12], const double cw[4][3], double L[6][10], double rho[6]) {
-    const int pa[6] = {0, 0, 0, 1, 1, 2}, pb[6] = {1, 2, 3, 2, 3, 3};
     for (int j = 0; j < 6; j++) {
-        double dv[4][3];
-        for (int k = 0; k < 4; k++)
-            for (int c = 0; c < 3; c++) dv[k][c] = v[k][3 * pa[j] + c] - v[k][3 * pb[j] + c];
-        auto dot = [&](int a, int b) { return dv[a][0] * dv[b][0] + dv[a][1] * dv[b][1] + dv[a][2] * dv[b][2]; };
-        L[j][0] = dot(0, 0);
-        L[j][1] = 2.0 * dot(0, 1);
-        L[j][2] = dot(1, 1);
-        L[j][3] = 2.0 * dot(0, 2);
-        L[j][4] = 2.0 * dot(1, 2);
-        L[j][5] = dot(2, 2);
-        L[j][6] = 2.0 * dot(0, 3);
-        L[j][7] = 2.0 * dot(1, 3);
-        L[j][8] = 2.0 * dot(2, 3);
-        L[j][9] = dot(3, 3);
-        const double dx = cw[pa[j]][0] - cw[pb[j]][0], dy = cw[pa[j]][1] - cw[pb[j]][1], dz = cw[pa[j]][2] - cw[pb[j]][2];
-        rho[j] = dx * dx + dy * dy + dz * dz;
+        for (int c = 0; c < 10; c++) L[j][c] = epnp_L_entry(v, j, c);
+        rho[j] = epnp_rho_entry(cw, j);
     }
 }
 
@@ -959,9 +980,6 @@ VS_HD inline void epnp_betas_init_uniform(int s, const double L[6][10], const do
 }
 
 // Gauss-Newton on the betas, then the pose by Kabsch; returns the mean reprojection error.
-struct NoMark {
-    VS_HD void operator()(int) const {}
-};
 // mark(k) at the stage ends (0: Gauss-Newton, 1: control points + cross-covariance, 2: Kabsch,
 // 3: reprojection error): the device's profiling build counts cycles there, everything else
 // passes NoMark
@@ -969,18 +987,34 @@ template <int MAXN, class Mark = NoMark>
 VS_HD inline double epnp_refine(double be[4], const double L[6][10], const double rho[6], const double v[4][12],
                                 const double (*alphas)[4], const double* X, const double* uv, int n, const Cam& K,
                                 double* R, double* t, Mark mark = Mark()) {
+    double Lr[6][10], rr[6];  // register copies (the device passes LDS arrays)
+    VS_UNROLL
+    for (int j = 0; j < 6; j++) {
+        rr[j] = rho[j];
+        VS_UNROLL
+        for (int c = 0; c < 10; c++) Lr[j][c] = L[j][c];
+    }
+    VS_NOUNROLL  // one copy of the body: the device's instruction cache, not its ALUs, bounds this code
     for (int it = 0; it < 5; it++) {  // Gauss-Newton on the 6 distance constraints
         double A[24], b[6], x[4];
+        // the beta products once; every sum in tsum's tree order
+        const double q[10] = {be[0] * be[0], be[0] * be[1], be[1] * be[1], be[0] * be[2], be[1] * be[2],
+                              be[2] * be[2], be[0] * be[3], be[1] * be[3], be[2] * be[3], be[3] * be[3]};
+        VS_UNROLL
         for (int j = 0; j < 6; j++) {
-            const double* l = L[j];
-            A[j * 4 + 0] = 2 * l[0] * be[0] + l[1] * be[1] + l[3] * be[2] + l[6] * be[3];
-            A[j * 4 + 1] = l[1] * be[0] + 2 * l[2] * be[1] + l[4] * be[2] + l[7] * be[3];
-            A[j * 4 + 2] = l[3] * be[0] + l[4] * be[1] + 2 * l[5] * be[2] + l[8] * be[3];
-            A[j * 4 + 3] = l[6] * be[0] + l[7] * be[1] + l[8] * be[2] + 2 * l[9] * be[3];
-            b[j] = rho[j] - (l[0] * be[0] * be[0] + l[1] * be[0] * be[1] + l[2] * be[1] * be[1] +
-                             l[3] * be[0] * be[2] + l[4] * be[1] * be[2] + l[5] * be[2] * be[2] +
-                             l[6] * be[0] * be[3] + l[7] * be[1] * be[3] + l[8] * be[2] * be[3] +
-                             l[9] * be[3] * be[3]);
+            const double* l = Lr[j];
+            const double a0[4] = {(2 * l[0]) * be[0], l[1] * be[1], l[3] * be[2], l[6] * be[3]};
+            const double a1[4] = {l[1] * be[0], (2 * l[2]) * be[1], l[4] * be[2], l[7] * be[3]};
+            const double a2[4] = {l[3] * be[0], l[4] * be[1], (2 * l[5]) * be[2], l[8] * be[3]};
+            const double a3[4] = {l[6] * be[0], l[7] * be[1], l[8] * be[2], (2 * l[9]) * be[3]};
+            A[j * 4 + 0] = tsum<4>(a0);
+            A[j * 4 + 1] = tsum<4>(a1);
+            A[j * 4 + 2] = tsum<4>(a2);
+            A[j * 4 + 3] = tsum<4>(a3);
+            double lq[10];
+            VS_UNROLL
+            for (int k = 0; k < 10; k++) lq[k] = l[k] * q[k];
+            b[j] = rr[j] - tsum<10>(lq);
         }
         lstsq<6, 4>(A, b, x);
         for (int k = 0; k < 4; k++) be[k] += x[k];
@@ -1052,7 +1086,7 @@ template <int MAXN>
 VS_HD bool epnp(const double* X, const double* uv, int n, const Cam& K, double* Rout, double* tout) {
     if (n < 4 || n > MAXN) return false;
     double cw[4][3], alphas[MAXN][4];
-    if (!epnp_control(X, n, cw, alphas)) return false;
+    if (!epnp_control<MAXN>(X, n, cw, alphas)) return false;
     double v[4][12], L[6][10], rho[6];
     if (n <= 5) {  // RANSAC subsets: the null space by QR, two eigenpairs of R R^T
         epnp_small_eig(alphas, uv, n, K, v);
