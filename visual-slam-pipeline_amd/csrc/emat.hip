@@ -5,7 +5,7 @@
 // One workgroup (4 wave64s) per problem.  The reference runs this path when the 3D-3D estimate
 // fails (Slam.cpp:965-984), so in the pipeline a problem whose 3D-3D result is ok exits at once.
 // RANSAC: chunks of 32 subsets drawn by lane 0 with the cv::RNG stream (5 distinct indices, no
-// subset check), one 5-point solve per lane (up to 10 models, LDS), rounds of 4 hypotheses scored
+// subset check), one 5-point solve per lane, 8 lanes of each wave (up to 10 models, LDS), rounds of 4 hypotheses scored
 // by the waves (Sampson error, ballot counts, early exit below the current best) and replayed in
 // order by lane 0.  recoverPose: the cheirality test of every point under the four decompositions
 // in parallel.  Scale: per-point candidates sorted in LDS (bitonic), IQR filter, median.  Numerical
@@ -20,7 +20,7 @@ namespace vs {
 using namespace vs_em;
 
 constexpr int kEmMaxPts = VS_EM_MAX_POINTS;
-constexpr int kEmChunk = 32;  // one 5-point solve per lane of wave 0; workspace in LDS
+constexpr int kEmChunk = 32;  // 5-point solves per round, 8 per wave; workspace in LDS
 constexpr int kEmThreads = 256;
 constexpr int kEmWaves = kEmThreads / 64;
 
@@ -168,16 +168,19 @@ __global__ __launch_bounds__(kEmThreads) void k_emat(const int* __restrict__ pai
         }
         __syncthreads();
         const int chunk = S.chunk;
-        if (tid < chunk) {
+        // the chunk's solves spread over the four waves (lanes 0..7 of each): one SIMD per wave, and
+        // each wave waits only for the slowest of its 8 root searches, not of 32
+        const int js = wv * (kEmChunk / kEmWaves) + lane;
+        if (lane < kEmChunk / kEmWaves && js < chunk) {
             double s1[10], s2[10];
             for (int i = 0; i < 5; i++) {
-                const int k = S.subset[5 * tid + i];
+                const int k = S.subset[5 * js + i];
                 s1[2 * i] = S.q1[2 * k];
                 s1[2 * i + 1] = S.q1[2 * k + 1];
                 s2[2 * i] = S.q2[2 * k];
                 s2[2 * i + 1] = S.q2[2 * k + 1];
             }
-            S.nmod[tid] = five_point(s1, s2, &S.Em[tid * kMaxModels * 9], &S.ws[tid], kEmChunk);
+            S.nmod[js] = five_point(s1, s2, &S.Em[js * kMaxModels * 9], &S.ws[js], kEmChunk);
         }
         __syncthreads();
         for (int r0 = 0; r0 < chunk; r0 += kEmWaves) {

@@ -14,8 +14,9 @@
 //     linear triangulation (smallest right singular vector of the 4 x 4 DLT system), cheirality
 //     with distance threshold 50, ties resolved R1 t, R2 t, R1 -t, R2 -t in that order.
 // Numerical choices that differ from OpenCV's implementation (orthonormal basis from Gaussian
-// elimination + Gram-Schmidt instead of an SVD; real roots by derivative-interval bisection
-// instead of cv::solvePoly) yield the same E up to rounding; host and device share this code.
+// elimination + Gram-Schmidt instead of an SVD; real roots by derivative intervals refined with the
+// Illinois method instead of cv::solvePoly) yield the same E up to rounding; host and device share
+// this code.
 #pragma once
 
 #include "pnp_solvers.h"
@@ -85,31 +86,82 @@ constexpr int kWsC = 233;     // interval cuts
 constexpr int kWsN = 245;     // roots of the current level
 constexpr int kWsSize = 256;
 
-// real roots of sum_k P[k] x^k (degree <= 10, P in the workspace) in ascending order, written to
-// the workspace at kWsR; returns the count.  Each derivative level's roots split the line into
-// monotone intervals of the level above, which are bisected.
-VS_HD inline int poly_real_roots(double* W, int wst) {
+// Real roots of sum_k c[k] x^k (degree <= 10, c in registers) in ascending order, written to the
+// workspace at kWsR; returns the count.  Each derivative level's roots split the line into monotone
+// intervals of the level above; a sign change is refined by safeguarded Newton from the interval's
+// midpoint (bisection whenever the Newton point leaves the bracket or the step does not halve;
+// geometric when the bracket spans orders of magnitude) until the step is 2^-50 of the iterate
+// (2^-26 for the derivatives' roots, which only cut intervals) or the bracket is at adjacent doubles.  The derivatives are evaluated by Horner over a fixed degree 10 - m (exact zero
+// coefficients above the true degree change no bit), with the coefficients in registers.
+constexpr double kRootTol = 0x1p-50;  // the polynomial's own roots (they become E)
+constexpr double kCutTol = 0x1p-26;   // a derivative's roots: they only cut the line into monotone pieces
+VS_HD inline int poly_real_roots(const double* c, double* W, int wst) {
 #define WS(i) W[(size_t)(i) * wst]
-    int n = 10;
+    // (static indices only: the coefficients stay in registers)
     double amax = 0;
-    for (int k = 0; k <= 10; k++) amax = fabs(WS(kWsP + k)) > amax ? fabs(WS(kWsP + k)) : amax;
-    while (n > 0 && fabs(WS(kWsP + n)) <= 1e-300 * amax) n--;  // exactly vanishing leading terms
+    VS_UNROLL
+    for (int k = 0; k <= 10; k++) amax = fabs(c[k]) > amax ? fabs(c[k]) : amax;
+    int n = 0;  // the degree: vanishing leading terms dropped
+    VS_UNROLL
+    for (int k = 1; k <= 10; k++)
+        if (fabs(c[k]) > 1e-300 * amax) n = k;
     if (n <= 0) return 0;
-    const double lead = WS(kWsP + n);
+    double lead = 0;
+    VS_UNROLL
+    for (int k = 0; k <= 10; k++) lead = k == n ? c[k] : lead;
+    // root bound: the positive root of the Cauchy polynomial |c_n| x^n - sum_k<n |c_k| x^k, by Newton
+    // from Cauchy's bound 1 + max |c_k / c_n| (above it, where the polynomial is increasing and
+    // convex, the iterates decrease monotonically), kept only where it evaluates positive (a
+    // certified bound) and widened by 2^-20; else Cauchy's bound
     double bound = 0;
-    for (int k = 0; k < n; k++) {
-        const double r = fabs(WS(kWsP + k) / lead);
+    VS_UNROLL
+    for (int k = 0; k < 10; k++) {
+        if (k >= n) continue;
+        const double r = fabs(c[k] / lead);
         bound = r > bound ? r : bound;
     }
     bound += 1.0;
+    {
+        double ac[11];
+        VS_UNROLL
+        for (int k = 0; k <= 10; k++) ac[k] = k < n ? -fabs(c[k]) : k == n ? fabs(c[k]) : 0.0;
+        double x = bound;
+        for (int it = 0; it < 12; it++) {
+            double f = ac[10], df = 0.0;
+            VS_UNROLL
+            for (int k = 9; k >= 0; k--) {
+                df = df * x + f;
+                f = f * x + ac[k];
+            }
+            if (!(df > 0) || !(f > 0)) break;
+            const double xn = x - f / df;
+            if (!(xn < x)) break;
+            x = xn;
+        }
+        const double xb = x * (1.0 + 0x1p-20);
+        double f = ac[10];
+        VS_UNROLL
+        for (int k = 9; k >= 0; k--) f = f * xb + ac[k];
+        if (f > 0 && xb < bound) bound = xb;
+    }
     int nr = 0;
-    for (int m = n - 1; m >= 0; m--) {
-        const int deg = n - m;
-        for (int k = 0; k <= deg; k++) {  // m-th derivative: P[k + m] (k + m)! / k!
+    VS_UNROLL
+    for (int m = 9; m >= 0; m--) {
+        if (m > n - 1) continue;
+        // m-th derivative: c[k + m] (k + m)! / k!, zero above the degree n - m
+        double D[11];
+        VS_UNROLL
+        for (int k = 0; k <= 10 - m; k++) {
             double f = 1.0;
             for (int q = 0; q < m; q++) f *= (double)(k + m - q);
-            WS(kWsD + k) = WS(kWsP + k + m) * f;
+            D[k] = k + m <= n ? c[k + m] * f : 0.0;
         }
+#define VS_EM_EV(x, v)                                \
+    do {                                              \
+        v = D[10 - m];                                \
+        VS_UNROLL                                     \
+        for (int k = 9 - m; k >= 0; k--) v = v * (x) + D[k]; \
+    } while (0)
         int nc = 0;
         WS(kWsC + nc++) = -bound;
         for (int i = 0; i < nr; i++) {
@@ -120,37 +172,56 @@ VS_HD inline int poly_real_roots(double* W, int wst) {
         int cnt = 0;
         for (int i = 0; i + 1 < nc; i++) {
             double a = WS(kWsC + i), b = WS(kWsC + i + 1);
-            auto ev = [&](double x) {
-                double v = WS(kWsD + deg);
-                for (int k = deg - 1; k >= 0; k--) v = v * x + WS(kWsD + k);
-                return v;
-            };
-            double fa = ev(a);
-            const double fb = ev(b);
+            double fa, fb0;
+            VS_EM_EV(a, fa);
+            VS_EM_EV(b, fb0);
             if (fa == 0) {
                 if (cnt == 0 || WS(kWsN + cnt - 1) != a) WS(kWsN + cnt++) = a;
                 continue;
             }
-            if ((fa < 0) == (fb < 0)) continue;
-            for (int it = 0; it < 200; it++) {
-                const double mid = 0.5 * (a + b);
-                if (mid <= a || mid >= b) break;
-                const double fm = ev(mid);
-                if (fm == 0) {
-                    a = b = mid;
+            if ((fa < 0) == (fb0 < 0)) continue;
+            // safeguarded Newton (rtsafe): a Newton step when it stays inside the bracket and at
+            // least halves the step before last, else bisection; the bracket keeps the sign change
+            double x = (a > 0 && b > 16.0 * a) || (b < 0 && a < 16.0 * b) ? (a > 0 ? 1.0 : -1.0) * sqrt(a * b)
+                                                                           : 0.5 * (a + b);
+            double dxold = b - a, dx = dxold, root = x;
+            for (int it = 0; it < 100; it++) {
+                double f = D[10 - m], df = 0.0;  // value and derivative (Horner pair)
+                VS_UNROLL
+                for (int k = 9 - m; k >= 0; k--) {
+                    df = df * x + f;
+                    f = f * x + D[k];
+                }
+                root = x;
+                if (f == 0) break;
+                if ((f < 0) == (fa < 0))
+                    a = x;
+                else
+                    b = x;
+                double mid = 0.5 * (a + b);
+                if (mid <= a || mid >= b) break;  // the bracket is at adjacent doubles
+                // a bracket spanning orders of magnitude on one side of 0 is split geometrically
+                if ((a > 0 && b > 16.0 * a) || (b < 0 && a < 16.0 * b)) mid = (a > 0 ? 1.0 : -1.0) * sqrt(a * b);
+                const double xn = df != 0 ? x - f / df : mid;
+                if (!(xn > a && xn < b) || fabs(2.0 * f) > fabs(dxold * df)) {
+                    dxold = dx;
+                    dx = mid - a;
+                    x = mid;
+                } else {
+                    dxold = dx;
+                    dx = x - xn;
+                    x = xn;
+                }
+                if (fabs(dx) <= (m == 0 ? kRootTol : kCutTol) * fabs(x)) {
+                    root = x;
                     break;
                 }
-                if ((fm < 0) == (fa < 0)) {
-                    a = mid;
-                    fa = fm;
-                } else {
-                    b = mid;
-                }
             }
-            WS(kWsN + cnt++) = 0.5 * (a + b);
+            WS(kWsN + cnt++) = root;
         }
         for (int i = 0; i < cnt; i++) WS(kWsR + i) = WS(kWsN + i);
         nr = cnt;
+#undef VS_EM_EV
     }
     return nr;
 #undef WS
@@ -159,7 +230,8 @@ VS_HD inline int poly_real_roots(double* W, int wst) {
 // 5-point solver: q1, q2 = 5 normalised correspondences (x, y interleaved, double).  Writes up to
 // kMaxModels essential matrices to Eout[k * 9 + q] (row-major, unit Frobenius norm) and returns the
 // count.  W / wst: the workspace (kWsSize doubles).
-VS_HD inline int five_point(const double* q1, const double* q2, double* Eout, double* W, int wst) {
+template <class Mark = vs_pnp::NoMark>
+VS_HD inline int five_point(const double* q1, const double* q2, double* Eout, double* W, int wst, Mark mark = Mark()) {
 #define WS(i) W[(size_t)(i) * wst]
 #define AA(r, c) WS(kWsA + (r) * 20 + (c))
     // epipolar rows: q2^T E q1 = 0 with e = (e11 e12 e13 e21 e22 e23 e31 e32 e33)
@@ -254,6 +326,7 @@ VS_HD inline int five_point(const double* q1, const double* q2, double* Eout, do
             VS_UNROLL
             for (int j = 0; j < 9; j++) B[f][j] = H[f][j];
     }
+    mark(0);
     // 10 x 20 coefficient matrix: row 0 = det(E), rows 1..9 = entries of 2 E E^T E - tr(E E^T) E;
     // monomial lambda_i lambda_j lambda_k (i <= j <= k, lambda = (x, y, z, 1)) collects the
     // symmetrised trilinear terms
@@ -291,27 +364,47 @@ VS_HD inline int five_point(const double* q1, const double* q2, double* Eout, do
                 VS_UNROLL
                 for (int r = 0; r < 10; r++) AA(r, col) = acc[r];
             }
-    // Gauss-Jordan on the first 10 columns (partial pivoting), in the workspace
+    mark(1);
+    // Gauss-Jordan on the first 10 columns (partial pivoting), in the workspace; each step stages
+    // the pivot row and then every other row through registers (static column ranges: the loads of
+    // a row issue together instead of one dependent LDS round trip per element)
+    VS_UNROLL
     for (int k = 0; k < 10; k++) {
         int p = k;
-        for (int r = k + 1; r < 10; r++)
-            if (fabs(AA(r, k)) > fabs(AA(p, k))) p = r;
-        if (!(fabs(AA(p, k)) > 1e-300)) return 0;
-        if (p != k)
-            for (int c = k; c < 20; c++) {
-                const double tmp = AA(k, c);
-                AA(k, c) = AA(p, c);
-                AA(p, c) = tmp;
+        double big = fabs(AA(k, k));
+        for (int r = k + 1; r < 10; r++) {
+            const double v = fabs(AA(r, k));
+            if (v > big) {
+                big = v;
+                p = r;
             }
-        const double inv = 1.0 / AA(k, k);
-        for (int c = k; c < 20; c++) AA(k, c) *= inv;
+        }
+        if (!(big > 1e-300)) return 0;
+        double pk[20];
+        VS_UNROLL
+        for (int c = k; c < 20; c++) pk[c] = AA(p, c);
+        if (p != k) {
+            VS_UNROLL
+            for (int c = k; c < 20; c++) AA(p, c) = AA(k, c);
+        }
+        const double inv = 1.0 / pk[k];
+        VS_UNROLL
+        for (int c = k; c < 20; c++) {
+            pk[c] *= inv;
+            AA(k, c) = pk[c];
+        }
         for (int r = 0; r < 10; r++) {
             if (r == k) continue;
             const double f = AA(r, k);
             if (f == 0) continue;
-            for (int c = k; c < 20; c++) AA(r, c) -= f * AA(k, c);
+            double rw[20];
+            VS_UNROLL
+            for (int c = k; c < 20; c++) rw[c] = AA(r, c);
+            VS_UNROLL
+            for (int c = k; c < 20; c++) AA(r, c) = rw[c] - f * pk[c];
         }
     }
+    mark(2);
     // B(z) rows <e> - z <f> over (x, y, 1): x-poly deg 3, y-poly deg 3, 1-poly deg 4 (coefficient
     // arrays indexed by the power of z); rest monomials: xz^2 xz x yz^2 yz y z^3 z^2 z 1
     double bx[3][4], by[3][4], b1[3][5];
@@ -361,9 +454,9 @@ VS_HD inline int five_point(const double* q1, const double* q2, double* Eout, do
         pmul(b1[0], 4, m2, 6, full);
         for (int k = 0; k <= 10; k++) c[k] += full[k];
     }
-    VS_UNROLL
-    for (int k = 0; k < 11; k++) WS(kWsP + k) = c[k];
-    const int nz = poly_real_roots(W, wst);
+    mark(3);
+    const int nz = poly_real_roots(c, W, wst);
+    mark(4);
     int count = 0;
     for (int ri = 0; ri < nz && count < kMaxModels; ri++) {
         const double z = WS(kWsR + ri);
