@@ -22,8 +22,10 @@
 // are one 6-float row of V and of U per domain row (3 ds_read_b64 each, conflict-free images).
 //
 // Per k-step k (one barrier), while the MFMAs of k run on buffers k & 1:
-//   * U of k + 1 (36 KB, prearranged on the host in the LDS image's order) goes global -> LDS by
-//     global_load_lds_dwordx4 (no VGPRs, no ds_write);
+//   * each lane's B operands of k + 1 (U, prearranged on the host in MFMA operand order, 20 floats
+//     per lane and domain-row half) are read from L2 straight into registers one step ahead (no LDS
+//     image and no barrier for U; the first version staged U through LDS with global_load_lds and
+//     was slower);
 //   * the patch of k + 1 (in LDS since step k - 1) is transformed into V of k + 1: thread
 //     (domain row i = its wave, channel, tile) forms row i of B^T d from four patch rows and
 //     applies the row transform (the row index is wave-uniform, so its coefficients are scalars);
