@@ -15,9 +15,11 @@ tracks its own sequence (its own start on the closed-loop synthetic path) and va
 summed over ranks (weak scaling).  The run ends with the RTS smoother and the reference's ATE
 (main.cpp:258-332) against the synthetic ground truth.
 
-frontend_batch — BASELINE config[3], offline batch: each rank extracts its block of the step's
-frames, matches consecutive pairs and runs F verification + 3D-3D (+E) per pair (DevicePipeline);
-with N > 1 the per-frame feature records are all-gathered over RCCL every step.
+frontend_batch — BASELINE config[3], offline batch through the C ABI (vs_batch_submit_dev /
+vs_batch_collect, csrc/batch.hip, two steps in flight): each rank extracts its block of B = 318 frames
+(the per-GPU shard of the 2,544-image sequence), receives its halo frame's record over the RCCL
+point-to-point ring (N > 1), matches the B consecutive pairs ending in its frames and runs F
+verification + 3D-3D (+E) per pair.
 
 monocular_hd — BASELINE config[4]: a synthetic 1280x720 stream (the build's HD camera synth.K_HD)
 through DepthEstimator::estimate (MiDaS v2.1-small at 256x256, seeded weights: the reference ships
@@ -348,6 +350,43 @@ def local_ba(ctx, reps):
     return res, (R, t, P0, kf, pt, uv, iters)
 
 
+def batch_schedule(submit, collect, first, count, depth=2):
+    """Steps first..first+count-1 through vs_batch_submit_dev / vs_batch_collect with at most `depth`
+    steps in flight (the next step's network beside this step's geometry); returns
+    the collected motions in step order."""
+    out, inflight = [], 0
+    for i in range(first, first + count):
+        submit(i)
+        inflight += 1
+        if inflight == depth:
+            out.append(collect())
+            inflight -= 1
+    while inflight:
+        out.append(collect())
+        inflight -= 1
+    return out
+
+
+def batch_halo_needed(step, rank, world):
+    """vs_batch_submit_dev needs the depth of frame rank * B - 1 with a communicator, except on rank 0's
+    first step (batch.hip; without one, slot 0 carries over from the previous step)."""
+    return world > 1 and (step > 0 or rank > 0)
+
+
+def share_batch_id(rank, world, make_id, device="cpu", nbytes=128):
+    """Rank 0's vs_batch communicator id (make_id() -> bytes) on every rank, broadcast over the torch
+    process group (RCCL on the GPU box, gloo in the CPU tests); None for one rank (no communicator)."""
+    if world <= 1:
+        return None
+    import torch
+    import torch.distributed as dist
+    t = torch.zeros(nbytes, dtype=torch.uint8, device=device)
+    if rank == 0:
+        t.copy_(torch.frombuffer(bytearray(make_id()), dtype=torch.uint8).to(device))
+    dist.broadcast(t, 0)
+    return bytes(t.cpu().numpy().tobytes())
+
+
 def frontend_batch(ctx, L, B, rank, world, steps, warmup):
     """BASELINE config[3]: the offline frame-sharded front end through the C ABI (vs_batch_submit_dev /
     vs_batch_collect, csrc/batch.hip — the path INTEGRATION.md gives a C++ driver): per step each rank
@@ -368,30 +407,19 @@ def frontend_batch(ctx, L, B, rank, world, steps, warmup):
     frames = torch.from_numpy(L["bgr"][idx]).to(dev)
     depth = torch.from_numpy(L["depth"][idx]).to(dev)
     depth_prev = torch.from_numpy(L["depth"][(rank * B - 1) % U]).to(dev)
-    uid = None
-    if world > 1:  # rank 0's RCCL communicator id, distributed over the torch process group
-        t = torch.zeros(vslam_abi.VS_BATCH_ID_BYTES if hasattr(vslam_abi, "VS_BATCH_ID_BYTES") else 128,
-                        dtype=torch.uint8, device=dev)
-        if rank == 0:
-            t.copy_(torch.frombuffer(bytearray(vslam_abi.batch_unique_id()), dtype=torch.uint8).to(dev))
-        dist.broadcast(t, 0)
-        uid = bytes(t.cpu().numpy().tobytes())
+    # rank 0's RCCL communicator id, distributed over the torch process group
+    uid = share_batch_id(rank, world, vslam_abi.batch_unique_id, dev,
+                         getattr(vslam_abi, "VS_BATCH_ID_BYTES", 128))
     bt = vslam_abi.Batch(ctx, B, H, W, rank=rank, world=world, uid=uid)
     s = torch.cuda.current_stream().cuda_stream
     motions = []
 
+    def submit(i):
+        halo = depth_prev.data_ptr() if batch_halo_needed(i, rank, world) else None
+        bt.submit_dev(frames.data_ptr(), depth.data_ptr(), halo, i * n_total + rank * B, s)
+
     def run(first, count):
-        inflight = 0
-        for i in range(first, first + count):
-            halo = depth_prev.data_ptr() if (world > 1 and (i > 0 or rank > 0)) else None
-            bt.submit_dev(frames.data_ptr(), depth.data_ptr(), halo, i * n_total + rank * B, s)
-            inflight += 1
-            if inflight == 2:
-                motions.append(bt.collect())
-                inflight -= 1
-        while inflight:
-            motions.append(bt.collect())
-            inflight -= 1
+        motions.extend(batch_schedule(submit, bt.collect, first, count))
 
     run(0, warmup)
     torch.cuda.synchronize()

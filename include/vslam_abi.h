@@ -401,9 +401,11 @@ int vs_batch_step_dev(vs_batch* b, const uint8_t* d_bgr, const float* d_depth, c
                       int frame_count0, vs_pair_motion* out, void* stream);
 /* The same step split in two (round 5), so that consecutive steps overlap: submit enqueues the step
  * (network on the batch's network stream; post-processing, exchange and pair geometry on its geometry
- * stream; both first wait for the work enqueued on `stream`, which in turn waits for the step's end)
- * and returns without synchronising; at most two steps are in flight.  collect waits for the oldest
- * submitted step and writes its pair motions.  vs_batch_step_dev == submit + collect. */
+ * stream; both first wait for the work already enqueued on `stream`) and returns without
+ * synchronising; at most two steps are in flight, and the next step's network runs beside this
+ * step's geometry.  The step's inputs (d_bgr, d_depth, d_depth_prev) must stay unchanged until its
+ * collect returns.  collect waits for the oldest submitted step and writes its pair motions.
+ * vs_batch_step_dev == submit + collect. */
 int vs_batch_submit_dev(vs_batch* b, const uint8_t* d_bgr, const float* d_depth, const float* d_depth_prev,
                         int frame_count0, void* stream);
 int vs_batch_collect(vs_batch* b, vs_pair_motion* out);

@@ -89,3 +89,62 @@ def test_ba_bytes_formula():
     # 30k observations, 10k points, 50 keyframes: ~7 MB per LM iteration (SURVEY.md 8(d) quotes ~5 MB)
     b = bench.ba_bytes_per_iteration(50, 10000, 30000)
     assert 5e6 < b < 8e6
+
+
+# ---- config[3] through the C ABI (bench.frontend_batch: vs_batch_submit_dev / vs_batch_collect) ----
+def test_batch_schedule_keeps_two_steps_in_flight():
+    events, live, peak = [], [0], [0]
+
+    def submit(i):
+        events.append(("s", i))
+        live[0] += 1
+        peak[0] = max(peak[0], live[0])
+
+    def collect():
+        live[0] -= 1
+        done = [e[1] for e in events if e[0] == "s"][len([e for e in events if e[0] == "c"])]
+        events.append(("c", done))
+        return done
+
+    out = bench.batch_schedule(submit, collect, 3, 5)
+    assert out == [3, 4, 5, 6, 7] and peak[0] == 2 and live[0] == 0
+    # the next step is submitted before the previous one is collected (the overlap), in order
+    assert events[:4] == [("s", 3), ("s", 4), ("c", 3), ("s", 5)]
+    assert bench.batch_schedule(submit, collect, 0, 1) == [0]
+
+
+def test_batch_halo_rule():
+    assert not bench.batch_halo_needed(0, 0, 1) and not bench.batch_halo_needed(5, 0, 1)  # no communicator
+    assert not bench.batch_halo_needed(0, 0, 4)                                          # rank 0, first step
+    assert bench.batch_halo_needed(0, 1, 4) and bench.batch_halo_needed(1, 0, 4)
+
+
+def _share_id_worker(rank, world, port, q):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    uid = bench.share_batch_id(rank, world, lambda: bytes(range(7, 135)), "cpu", 128)
+    q.put((rank, uid))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_share_batch_id_reaches_every_rank(world):
+    """rank 0's vs_batch communicator id arrives byte for byte on every rank over the process group
+    (gloo here; the GPU box's RCCL group carries the same broadcast)."""
+    import socket
+
+    import torch.multiprocessing as mp
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_share_id_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    got = dict(q.get(timeout=120) for _ in range(world))
+    for p in ps:
+        p.join(60)
+    assert all(got[r] == bytes(range(7, 135)) for r in range(world))
+    assert bench.share_batch_id(0, 1, lambda: b"x") is None

@@ -363,8 +363,8 @@ int vs_batch_submit_dev(vs_batch* b, const uint8_t* d_bgr, const float* d_depth,
     VS_HIP(hipGetLastError());
     VS_HIP(hipMemcpyAsync(S.host, S.packed, (size_t)kPacked * B * sizeof(double), hipMemcpyDeviceToHost, sg));
     VS_HIP(hipEventRecord(S.geo_done, sg));
-    // the caller's stream sees the step complete (its later work may reuse the inputs)
-    VS_HIP(hipStreamWaitEvent(cs, S.geo_done, 0));
+    // (the caller's stream is not made to wait here: the next submit's network must start beside this
+    // step's geometry; the inputs stay the caller's to keep until vs_batch_collect returns)
     S.pending = true;
     b->submitted++;
     return VS_OK;
