@@ -1,13 +1,16 @@
 // latency probe of emat_solvers.h five_point on one lane (round 5)
 #include <hip/hip_runtime.h>
 #include <cstdio>
+#ifndef NL
+#define NL 32
+#endif
 #include "../../visual-slam-pipeline_amd/csrc/emat_solvers.h"
 using namespace vs_em;
 __global__ void k(const double* q, double* out, long long* cyc) {
     __shared__ double ws[kWsSize * 32];
     __shared__ double E[32 * kMaxModels * 9];
     const int l = threadIdx.x;
-    if (l >= 32) return;
+    if (l >= NL) return;
     double q1[10], q2[10];
     for (int i = 0; i < 10; i++) { q1[i] = q[20 * l + i]; q2[i] = q[20 * l + 10 + i]; }
     long long st[6];
