@@ -308,6 +308,7 @@ int vs_batch_submit_dev(vs_batch* b, const uint8_t* d_bgr, const float* d_depth,
            "vs_batch_submit_dev: d_depth_prev (frame rank * B - 1) is required with a communicator");
     BatchSet& S = b->set[b->submitted & 1];
     const BatchSet& P = b->set[(b->submitted + 1) & 1];  // the previous step's set
+    VS_HIP(hipSetDevice(ctx->device));
     hipEvent_t in_ready;
     VS_HIP(hipEventCreateWithFlags(&in_ready, hipEventDisableTiming));
     VS_HIP(hipEventRecord(in_ready, cs));
@@ -325,7 +326,8 @@ int vs_batch_submit_dev(vs_batch* b, const uint8_t* d_bgr, const float* d_depth,
     else
         VS_HIP(hipMemcpyAsync(S.depth, P.depth + (size_t)B * plane, plane * sizeof(float), hipMemcpyDeviceToDevice, sn));
     VS_HIP(hipMemcpyAsync(S.depth + plane, d_depth, (size_t)B * plane * sizeof(float), hipMemcpyDeviceToDevice, sn));
-    VS_CHECK(vs_network_batch_dev(ctx, B, d_bgr, h, w, S.semi, S.dgrid, sn));
+    // the grid stays raw: the post-processing below normalises the corners it samples
+    VS_CHECK(vs::sp_forward(ctx, B, d_bgr, 3, h, w, sn, S.semi, S.dgrid, true));
     VS_HIP(hipEventRecord(S.net_done, sn));
     // ---- geometry stream (in order: step k - 1's tables, which slot 0 copies from, are complete)
     hipStream_t sg = b->s_geo;
@@ -335,7 +337,8 @@ int vs_batch_submit_dev(vs_batch* b, const uint8_t* d_bgr, const float* d_depth,
         VS_HIP(hipMemcpyAsync(S.desc, P.desc + (size_t)B * rec_d, rec_d * sizeof(float), hipMemcpyDeviceToDevice, sg));
         VS_HIP(hipMemcpyAsync(S.n, P.n + B, sizeof(int), hipMemcpyDeviceToDevice, sg));
     }
-    VS_CHECK(vs_postprocess_batch_dev(ctx, B, S.semi, S.dgrid, h, w, S.kps + rec_k, S.desc + rec_d, S.n + 1, cap, sg));
+    VS_CHECK(vs::sp_postprocess(ctx, B, (h + 7) / 8, (w + 7) / 8, h, w, S.kps + rec_k, S.desc + rec_d, S.n + 1, cap, sg,
+                                S.semi, S.dgrid, true));
     if (xchg) {  // slot 0 <- frame rank * B - 1 (batch_exchange.h, shared with the CPU loopback test)
         vs_bx::Tables tb;
         tb.B = B, tb.cap = cap, tb.rank = b->rank, tb.world = b->world, tb.gather = b->gather;

@@ -1130,23 +1130,6 @@ __global__ __launch_bounds__(256, 2) void k_wino3(WinoArgs wa) {
     }
 }
 
-// Descriptor head output: L2-normalise every pixel's 256 channels (MagicLeap export convention,
-// SURVEY.md 8(a) A3).  One wave per pixel, 16-byte loads, shuffle-tree sum of squares.
-__global__ __launch_bounds__(256) void k_desc_l2norm(float* __restrict__ d, long npix) {
-    long p = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
-    int lane = threadIdx.x & 63;
-    if (p >= npix) return;
-    f32x4* row = reinterpret_cast<f32x4*>(d + (size_t)p * 256);
-    f32x4 v = row[lane];
-    float ss = v[0] * v[0] + v[1] * v[1] + v[2] * v[2] + v[3] * v[3];
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) ss += __shfl_xor(ss, o);
-    float nrm = sqrtf(ss);
-    nrm = fmaxf(nrm, 1e-12f);
-    v[0] /= nrm; v[1] /= nrm; v[2] /= nrm; v[3] /= nrm;
-    row[lane] = v;
-}
-
 namespace {
 
 template <int KS, bool POOL, int LAYER, bool FUSE1A = false, int CKV = (KS == 3 ? 16 : 32)>
@@ -1392,7 +1375,7 @@ int conv3(vs_ctx* ctx, const DevLayer& L, const float* in, int in_cstride, int i
 }  // namespace
 
 int sp_forward(vs_ctx* ctx, int B, const uint8_t* d_img, int channels, int h, int w, hipStream_t s, float* semi_out,
-               float* dgrid_out) {
+               float* dgrid_out, bool grid_raw) {
     VS_CHECK(scratch_order(ctx, s));
     ScratchUse scratch_use(ctx, s);
     const int Hp = ((h + 7) / 8) * 8, Wp = ((w + 7) / 8) * 8;
@@ -1474,13 +1457,9 @@ int sp_forward(vs_ctx* ctx, int B, const uint8_t* d_img, int channels, int h, in
             VS_CHECK((launch_conv<1, false, 11>(L[11], a0, 512, 256, dgrid_out, kDescDim, 0, B, H, W, 0, s)));
         }
     }
-    if (ctx->desc_l2) {  // the model's "desc" output is normalised (a raw-"desc" ONNX export skips it)
-        ProfScope ps(ctx, "desc_l2norm", s);
-        long npix = (long)B * H * W;
-        hipLaunchKernelGGL(k_desc_l2norm, dim3((unsigned)((npix + 3) / 4)), dim3(256), 0, s, dgrid_out,
-                           npix);
-        VS_HIP(hipGetLastError());
-    }
+    // the model's "desc" output is normalised (a raw-"desc" ONNX export skips it); grid_raw: the
+    // caller's post-processing normalises the sampled corners instead (sp_postprocess)
+    if (ctx->desc_l2 && !grid_raw) VS_CHECK(desc_grid_l2norm(ctx, (long)B * H * W, dgrid_out, s));
     return VS_OK;
 }
 

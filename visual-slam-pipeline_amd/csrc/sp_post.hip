@@ -64,42 +64,23 @@ constexpr int kFinishMaxRounds = 1 << 14; // k_nms_finish's round cap (VS_NMS_FI
 enum : uint8_t { ST_UNDECIDED = 0, ST_KEPT = 1, ST_OUT = 2 };
 
 // ---------------------------------------------------------------------------------------------
-// A4 decode: one thread per 8x8 cell.  std::exp(float) is glibc's expf, which is not correctly
-// rounded; glibc_expf.h restates its algorithm instruction for instruction (checked exhaustively
-// against libm on the host by tests/test_oracle.py, and on the device through the decode parity
-// tests of tests/test_gpu_parity.py).
-__global__ __launch_bounds__(256) void k_decode(const float* __restrict__ semi, int hc, int wc, int B,
-                                                float* __restrict__ heat) {
-    post_prio();
-    int idx = blockIdx.x * blockDim.x + threadIdx.x;
-    int ncell = hc * wc;
-    if (idx >= B * ncell) return;
-    int b = idx / ncell, cidx = idx - b * ncell;
-    int cy = cidx / wc, cx = cidx - cy * wc;
-    const float* p = semi + (size_t)idx * kSemiCh;
-    float cell[kSemiCh];
-#pragma unroll
-    for (int c = 0; c < kSemiCh; c++) cell[c] = p[c];
-    float mx = cell[0];
-#pragma unroll
-    for (int c = 1; c < kSemiCh; c++) mx = (cell[c] > mx) ? cell[c] : mx;
-    float sum = 0.0f;
-#pragma unroll
-    for (int c = 0; c < kSemiCh; c++) {
-        cell[c] = vs_expf::glibc_expf(cell[c] - mx);
-        sum += cell[c];
-    }
-    const int Wp = wc * 8;
-    float* hb = heat + (size_t)b * ncell * 64;
-#pragma unroll
-    for (int c = 0; c < 64; c += 4) {
-        float4 v;
-        v.x = div_rn(cell[c], sum);
-        v.y = div_rn(cell[c + 1], sum);
-        v.z = div_rn(cell[c + 2], sum);
-        v.w = div_rn(cell[c + 3], sum);
-        *reinterpret_cast<float4*>(hb + (size_t)(cy * 8 + c / 8) * Wp + cx * 8 + (c % 8)) = v;
-    }
+// A4 decode (inside k_nms_lmax): softmax of each 8x8 cell over its 65 channels, dustbin dropped.
+// std::exp(float) is glibc's expf, which is not correctly rounded; glibc_expf.h restates its
+// algorithm instruction for instruction (checked exhaustively against libm on the host by
+// tests/test_oracle.py, and on the device through the decode parity tests of
+// tests/test_gpu_parity.py).  The maximum and the sum run over the channels in order, as the
+// reference's loops do.
+
+// Workgroup -> (frame, tile), XCD-aware: the hardware deals consecutive workgroups to the eight
+// XCDs in turn, so workgroup L runs on XCD L % 8; the mapping hands each XCD a contiguous run of
+// tiles (a frame per XCD at 8 frames of 300 tiles), so the 4-px halo rows a tile shares with its
+// neighbours are fetched into one L2 instead of one per XCD.
+__device__ __forceinline__ void tile_of_block(int ntiles, int B, int& b, int& tile) {
+    const int N = ntiles * B, L = blockIdx.y * gridDim.x + blockIdx.x;
+    const int per = N / 8, rem = N % 8, xcd = L % 8, k = L / 8;
+    const int logical = (xcd < rem ? xcd * (per + 1) : rem * (per + 1) + (xcd - rem) * per) + k;
+    b = logical / ntiles;
+    tile = logical - b * ntiles;
 }
 
 // 9-wide windows over a (32 + 8)^2 LDS region of 32-bit score keys: row pass (40 region rows x 32
@@ -118,29 +99,109 @@ __device__ __forceinline__ int floor_bin(unsigned key) {
     return bin < 0 ? 0 : bin >= kFloorBins ? kFloorBins - 1 : bin;
 }
 
-__global__ __launch_bounds__(kNmsThreads) void k_nms_lmax(const float* __restrict__ heat, int B, int Hp, int Wp,
-                                                          int tiles_x, int* __restrict__ hist) {
+// The decode is fused in: the workgroup decodes the 6 x 6 cells under its 40 x 40 region straight
+// from semi into LDS (the heatmap is never re-read from HBM here) and writes its 32 x 32 interior
+// to the heatmap once, for the NMS rounds and the selection.
+constexpr int kNmsCells = kNmsTile / 8 + 2;  // cells per side under a tile's region (4-px halo < a cell)
+__global__ __launch_bounds__(kNmsThreads) void k_nms_lmax(const float* __restrict__ semi, int hc, int wc,
+                                                          float* __restrict__ heat, int B, int Hp, int Wp,
+                                                          int tiles_x, int ntiles, int* __restrict__ hist) {
     post_prio();
-    const int b = blockIdx.y;
-    __shared__ unsigned s_key[kNmsReg * kNmsReg];
-    __shared__ unsigned s_rmax[kNmsReg * kNmsTile];
+    int b, tile;
+    tile_of_block(ntiles, B, b, tile);
+    constexpr int kPw = kNmsCells * 8, kNc = kNmsCells * kNmsCells;
+    constexpr int kWaves = kNmsThreads / 64, kCpw = kNc / kWaves;  // cells per wave
+    static_assert(kNc % kWaves == 0 && kCpw <= 64, "k_nms_lmax: the region's cells split evenly over the waves");
+    __shared__ float s_prob[kPw * kPw];  // the cells' probabilities, 48 x 48 px
+    // the decode's exps, then (dead after the decode) the window passes' keys and row maxima
+    constexpr int kExpWords = kWaves * kCpw * kSemiCh, kKeyWords = kNmsReg * kNmsReg + kNmsReg * kNmsTile;
+    __shared__ unsigned s_u[kExpWords > kKeyWords ? kExpWords : kKeyWords];
+    __shared__ float s_csum[kNc];
     __shared__ int s_hist[kFloorBins];
     __shared__ int s_any;
-    const int tx = blockIdx.x % tiles_x, ty = blockIdx.x / tiles_x;
+    unsigned* s_key = s_u;                        // [kNmsReg * kNmsReg]
+    unsigned* s_rmax = s_u + kNmsReg * kNmsReg;   // [kNmsReg * kNmsTile]
+    const int tx = tile % tiles_x, ty = tile / tiles_x;
     const int gx0 = tx * kNmsTile - kRadius, gy0 = ty * kNmsTile - kRadius;
-    const float* hb = heat + (size_t)b * Hp * Wp;
+    const int cx0 = tx * (kNmsTile / 8) - 1, cy0 = ty * (kNmsTile / 8) - 1;  // the region's first cell
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     if (threadIdx.x == 0) s_any = 0;
+    for (int i = threadIdx.x; i < kFloorBins; i += kNmsThreads) s_hist[i] = 0;
+    {
+        // decode, kCpw cells per wave: lane c holds channel c of each cell (the dustbin channel 64 read
+        // by every lane), the maxima by butterfly (the maximum's value does not depend on the order;
+        // only the sign of a zero maximum could, and x - 0 and x - (-0) are equal for every x that
+        // reaches expf), the exps to LDS, lanes 0 .. kCpw - 1 sum one cell's 65 exps each in channel
+        // order, every lane divides its channel
+        float v[kCpw], dust[kCpw], mx[kCpw];
+        bool ok[kCpw];
+#pragma unroll
+        for (int j = 0; j < kCpw; j++) {
+            const int q = wv * kCpw + j, ci = q / kNmsCells, cj = q - ci * kNmsCells;
+            const int cy = cy0 + ci, cx = cx0 + cj;
+            ok[j] = cy >= 0 && cy < hc && cx >= 0 && cx < wc;
+            const float* p = semi + (((size_t)b * hc + (ok[j] ? cy : 0)) * wc + (ok[j] ? cx : 0)) * kSemiCh;
+            v[j] = p[lane];
+            dust[j] = p[64];
+        }
+#pragma unroll
+        for (int j = 0; j < kCpw; j++) {
+            float m = v[j] > dust[j] ? v[j] : dust[j];
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) {
+                const float t = __shfl_xor(m, o);
+                m = t > m ? t : m;
+            }
+            mx[j] = m;
+        }
+        float* ex = reinterpret_cast<float*>(s_u) + wv * kCpw * kSemiCh;
+        float xd = 0.0f;  // lane j < kCpw: cell j's dustbin term
+#pragma unroll
+        for (int j = 0; j < kCpw; j++) {
+            v[j] = vs_expf::glibc_expf(v[j] - mx[j]);
+            ex[j * kSemiCh + lane] = v[j];
+            if (lane == j) xd = dust[j] - mx[j];
+        }
+        if (lane < kCpw) ex[lane * kSemiCh + 64] = vs_expf::glibc_expf(xd);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        if (lane < kCpw) {
+            const float* e = ex + lane * kSemiCh;
+            float sum = 0.0f;
+            for (int c = 0; c < kSemiCh; c++) sum += e[c];
+            s_csum[wv * kCpw + lane] = sum;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+        for (int j = 0; j < kCpw; j++) {
+            const int q = wv * kCpw + j, ci = q / kNmsCells, cj = q - ci * kNmsCells;
+            if (ok[j]) s_prob[(ci * 8 + lane / 8) * kPw + cj * 8 + (lane % 8)] = div_rn(v[j], s_csum[q]);
+        }
+    }
+    __syncthreads();  // s_prob complete; the exps are dead (s_u becomes the keys)
+    float* hb = heat + (size_t)b * Hp * Wp;
     for (int i = threadIdx.x; i < kNmsReg * kNmsReg; i += kNmsThreads) {
         const int ry = i / kNmsReg, rx = i - ry * kNmsReg;
         const int gy = gy0 + ry, gx = gx0 + rx;
         unsigned key = 0;
         if (gy >= 0 && gy < Hp && gx >= 0 && gx < Wp) {
-            const float v = hb[(size_t)gy * Wp + gx];
+            const float v = s_prob[(ry + 8 - kRadius) * kPw + rx + 8 - kRadius];
             key = v > kConfThresh ? __float_as_uint(v) : 0u;
         }
         s_key[i] = key;
     }
-    for (int i = threadIdx.x; i < kFloorBins; i += kNmsThreads) s_hist[i] = 0;
+    // the interior to the heatmap (rows of 32 floats, 16-byte stores)
+    for (int i = threadIdx.x; i < kNmsTile * kNmsTile / 4; i += kNmsThreads) {
+        const int iy = i / (kNmsTile / 4), ix = 4 * (i - iy * (kNmsTile / 4));
+        const int gy = gy0 + kRadius + iy, gx = gx0 + kRadius + ix;  // Wp is a multiple of 8
+        if (gy < Hp && gx < Wp) {
+            const float* q = &s_prob[(iy + 8) * kPw + ix + 8];
+            *reinterpret_cast<float4*>(hb + (size_t)gy * Wp + gx) = make_float4(q[0], q[1], q[2], q[3]);
+        }
+    }
     __syncthreads();
     for (int i = threadIdx.x; i < kNmsReg * kNmsTile; i += kNmsThreads) {
         const int ry = i / kNmsTile, ix = i - ry * kNmsTile;
@@ -239,14 +300,15 @@ __global__ __launch_bounds__(kNmsThreads) void k_nms_round(const float* __restri
                                                            const unsigned* __restrict__ floor_bits, int r, int B,
                                                            int Hp, int Wp, int tiles_x, int ntiles) {
     post_prio();
-    const int b = blockIdx.y;
+    int b, tile;
+    tile_of_block(ntiles, B, b, tile);
     if (flags[r * B + b] == 0) return;
-    if (r > 0 && tflags[((size_t)r * B + b) * ntiles + blockIdx.x] == 0) return;
+    if (r > 0 && tflags[((size_t)r * B + b) * ntiles + tile] == 0) return;
     __shared__ unsigned s_key[kNmsReg * kNmsReg];
     __shared__ unsigned s_rmax[kNmsReg * kNmsTile];
     __shared__ uint8_t s_kept[kNmsReg * kNmsReg];
     __shared__ uint8_t s_rkept[kNmsReg * kNmsTile];
-    const int tx = blockIdx.x % tiles_x, ty = blockIdx.x / tiles_x;
+    const int tx = tile % tiles_x, ty = tile / tiles_x;
     const int gx0 = tx * kNmsTile - kRadius, gy0 = ty * kNmsTile - kRadius;
     const float* hb = heat + (size_t)b * Hp * Wp;
     uint8_t* sb = state + (size_t)b * Hp * Wp;
@@ -348,7 +410,7 @@ __global__ __launch_bounds__(kNmsThreads) void k_nms_round(const float* __restri
     // only a tile with undecided interior pixels has anything to do next round (its neighbours'
     // decisions reach it through the halo it reloads)
     if (__syncthreads_or(und) && threadIdx.x == 0) {
-        tflags[((size_t)(r + 1) * B + b) * ntiles + blockIdx.x] = 1;
+        tflags[((size_t)(r + 1) * B + b) * ntiles + tile] = 1;
         flags[(r + 1) * B + b] = 1;
     }
 }
@@ -628,12 +690,44 @@ __global__ __launch_bounds__(1024) void k_nms_select(const unsigned long long* _
     }
 }
 
+// The descriptor head's L2 normalisation of one grid cell (MagicLeap export convention, SURVEY.md
+// 8(a) A3): the cell's 256 channels 4 per lane across a wave, sum of squares per lane then a
+// butterfly (every lane ends with the same bits: each step adds the same two values), norm clamped
+// at 1e-12, correctly rounded sqrt and division.  Shared by the grid pass and the sampler's
+// per-corner form, so both give the same bits.
+__device__ __forceinline__ float4 desc_cell_l2(float4 v) {
+    float ss = v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) ss += __shfl_xor(ss, o);
+    const float nrm = fmaxf(sqrt_rn(ss), 1e-12f);
+    return make_float4(div_rn(v.x, nrm), div_rn(v.y, nrm), div_rn(v.z, nrm), div_rn(v.w, nrm));
+}
+
+// The whole grid normalised in place (the network's "desc" output for callers that take the grid:
+// vs_network_batch_dev, vs_superpoint_forward).  One wave per cell, 16-byte accesses.
+__global__ __launch_bounds__(256) void k_desc_l2norm(float* __restrict__ d, long npix) {
+    const long p = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (p >= npix) return;
+    float4* row = reinterpret_cast<float4*>(d + (size_t)p * kDescDim);
+    row[lane] = desc_cell_l2(row[lane]);
+}
+
+int desc_grid_l2norm(vs_ctx* ctx, long npix, float* grid, hipStream_t s) {
+    ProfScope ps(ctx, "desc_l2norm", s);
+    hipLaunchKernelGGL(k_desc_l2norm, dim3((unsigned)((npix + 3) / 4)), dim3(256), 0, s, grid, npix);
+    VS_HIP(hipGetLastError());
+    return VS_OK;
+}
+
 // A6: bilinear sampling of the normalised coarse grid + per-keypoint L2 normalisation.  One wave
 // per keypoint; each lane owns 4 channels; the sum of squares runs sequentially over c = 0..255
-// on lane 0 (the reference's order) from LDS.
+// on lane 0 (the reference's order) from LDS.  norm_corners: the grid is the head's raw output and
+// each of the four corner cells is normalised here (desc_cell_l2, the same bits as the grid pass)
+// — the pipeline's form: the network never writes and re-reads the normalised grid.
 __global__ __launch_bounds__(256) void k_sample(const float* __restrict__ dgrid, int hc, int wc,
                                                 const vs_keypoint* __restrict__ kps, const int* __restrict__ nkp,
-                                                int cap, float* __restrict__ desc) {
+                                                int cap, float* __restrict__ desc, int norm_corners) {
     post_prio();
     __shared__ float s_v[4][256];
     __shared__ float s_norm[4];
@@ -653,10 +747,16 @@ __global__ __launch_bounds__(256) void k_sample(const float* __restrict__ dgrid,
         float wx = sx - x0;
         float wy = sy - y0;
         const float* g = dgrid + (size_t)b * hc * wc * 256;
-        const float4 v00 = reinterpret_cast<const float4*>(g + ((size_t)y0 * wc + x0) * 256)[lane];
-        const float4 v01 = reinterpret_cast<const float4*>(g + ((size_t)y0 * wc + x1) * 256)[lane];
-        const float4 v10 = reinterpret_cast<const float4*>(g + ((size_t)y1 * wc + x0) * 256)[lane];
-        const float4 v11 = reinterpret_cast<const float4*>(g + ((size_t)y1 * wc + x1) * 256)[lane];
+        float4 v00 = reinterpret_cast<const float4*>(g + ((size_t)y0 * wc + x0) * 256)[lane];
+        float4 v01 = reinterpret_cast<const float4*>(g + ((size_t)y0 * wc + x1) * 256)[lane];
+        float4 v10 = reinterpret_cast<const float4*>(g + ((size_t)y1 * wc + x0) * 256)[lane];
+        float4 v11 = reinterpret_cast<const float4*>(g + ((size_t)y1 * wc + x1) * 256)[lane];
+        if (norm_corners) {  // (wave-uniform)
+            v00 = desc_cell_l2(v00);
+            v01 = desc_cell_l2(v01);
+            v10 = desc_cell_l2(v10);
+            v11 = desc_cell_l2(v11);
+        }
         const float a00[4] = {v00.x, v00.y, v00.z, v00.w}, a01[4] = {v01.x, v01.y, v01.z, v01.w};
         const float a10[4] = {v10.x, v10.y, v10.z, v10.w}, a11[4] = {v11.x, v11.y, v11.z, v11.w};
 #pragma unroll
@@ -687,7 +787,7 @@ __global__ __launch_bounds__(256) void k_sample(const float* __restrict__ dgrid,
 }
 
 int sp_postprocess(vs_ctx* ctx, int B, int hc, int wc, int h, int w, vs_keypoint* d_kps, float* d_desc,
-                   int* d_n, int cap, hipStream_t s, const float* semi, const float* dgrid) {
+                   int* d_n, int cap, hipStream_t s, const float* semi, const float* dgrid, bool grid_raw) {
     VS_CHECK(scratch_order(ctx, s));
     ScratchUse scratch_use(ctx, s);
     if (!semi) semi = ctx->semi.as<float>();
@@ -723,18 +823,16 @@ int sp_postprocess(vs_ctx* ctx, int B, int hc, int wc, int h, int w, vs_keypoint
     int* ties = keycnt + 2 * B;
     int* fhist = ties + 3 * B;
     uint8_t* tflags = reinterpret_cast<uint8_t*>(flags + nflag);
+    VS_HIP(hipMemsetAsync(flags, 0, nflag * sizeof(int) + (size_t)(kNmsMaxRounds + 1) * B * ntiles, s));
+    VS_HIP(hipMemsetAsync(flags, 0x01, (size_t)B * sizeof(int), s));  // round 0 runs for every frame
     {
-        ProfScope ps(ctx, "decode", s);
-        int ncell = B * hc * wc;
-        hipLaunchKernelGGL(k_decode, dim3((ncell + 255) / 256), dim3(256), 0, s, semi, hc, wc, B, ctx->heat.as<float>());
+        ProfScope ps(ctx, "decode", s);  // decode + strict local maxima, one pass over semi
+        hipLaunchKernelGGL(k_nms_lmax, dim3(ntiles, B), dim3(kNmsThreads), 0, s, semi, hc, wc, ctx->heat.as<float>(), B,
+                           Hp, Wp, tiles_x, ntiles, fhist);
         VS_HIP(hipGetLastError());
     }
     {
         ProfScope ps(ctx, "nms_rounds", s);
-        VS_HIP(hipMemsetAsync(flags, 0, nflag * sizeof(int) + (size_t)(kNmsMaxRounds + 1) * B * ntiles, s));
-        VS_HIP(hipMemsetAsync(flags, 0x01, (size_t)B * sizeof(int), s));  // round 0 runs for every frame
-        hipLaunchKernelGGL(k_nms_lmax, dim3(ntiles, B), dim3(kNmsThreads), 0, s, ctx->heat.as<float>(), B, Hp, Wp,
-                           tiles_x, fhist);
         hipLaunchKernelGGL(k_nms_floor, dim3(B), dim3(kNmsThreads), 0, s, fhist, max_kp, floor_bits);
         for (int r = 0; r < kNmsMaxRounds; r++) {
             hipLaunchKernelGGL(k_nms_round, dim3(ntiles, B), dim3(kNmsThreads), 0, s, ctx->heat.as<float>(),
@@ -756,7 +854,7 @@ int sp_postprocess(vs_ctx* ctx, int B, int hc, int wc, int h, int w, vs_keypoint
     {
         ProfScope ps(ctx, "sample", s);
         hipLaunchKernelGGL(k_sample, dim3((max_kp + 3) / 4, B), dim3(256), 0, s, dgrid, hc, wc,
-                           d_kps, d_n, cap, d_desc);
+                           d_kps, d_n, cap, d_desc, (grid_raw && ctx->desc_l2) ? 1 : 0);
         VS_HIP(hipGetLastError());
     }
     return VS_OK;

@@ -893,11 +893,11 @@ struct GpuOps {
             const int f0 = X.ch[c], m = X.ch[c + 1] - X.ch[c];
             float* sm = semi.as<float>() + (size_t)(s0 + f0) * semi_f;
             float* dg = dgrid.as<float>() + (size_t)(s0 + f0) * dgrid_f;
-            VS_CHECK(sp_forward(ctx, m, d_bgr + (size_t)f0 * h * w * 3, 3, h, w, xs, sm, dg));
+            VS_CHECK(sp_forward(ctx, m, d_bgr + (size_t)f0 * h * w * 3, 3, h, w, xs, sm, dg, true));
             VS_HIP(hipEventRecord(X.net[c], xs));
             VS_HIP(hipStreamWaitEvent(xp, X.net[c], 0));
             VS_CHECK(sp_postprocess(ctx, m, hc, wc, h, w, kps_of(s0 + f0), desc_of(s0 + f0), pool_n.as<int>() + s0 + f0,
-                                    kCap, xp, sm, dg));
+                                    kCap, xp, sm, dg, true));
             // descriptor row norms once per frame (matching reuses them for every pair)
             VS_CHECK(desc_norms(ctx, m, desc_of(s0 + f0), pool_n.as<int>() + s0 + f0, kCap, norms_of(s0 + f0), xp));
             if (d_depth)

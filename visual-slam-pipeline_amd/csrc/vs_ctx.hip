@@ -491,9 +491,9 @@ int vs_extract_batch_dev(vs_ctx* ctx, int B, const uint8_t* d_imgs, int h, int w
     VS_ARG(B > 0 && h >= 8 && w >= 8 && cap >= 1, "vs_extract_batch_dev: bad sizes");
     hipStream_t s = pick(ctx, stream);
     VS_HIP(hipSetDevice(ctx->device));
-    VS_CHECK(sp_forward(ctx, B, d_imgs, 3, h, w, s));
+    VS_CHECK(sp_forward(ctx, B, d_imgs, 3, h, w, s, nullptr, nullptr, true));  // raw grid: the sampler normalises
     const int hc = (h + 7) / 8, wc = (w + 7) / 8;
-    VS_CHECK(sp_postprocess(ctx, B, hc, wc, h, w, d_kps, d_desc, d_n, cap, s));
+    VS_CHECK(sp_postprocess(ctx, B, hc, wc, h, w, d_kps, d_desc, d_n, cap, s, nullptr, nullptr, true));
     return VS_OK;
 }
 
@@ -533,10 +533,10 @@ int vs_extract_batch(vs_ctx* ctx, int B, const uint8_t* const* imgs, int h, int 
     VS_CHECK(ctx->h_kps.ensure((size_t)B * cap * sizeof(vs_keypoint)));
     VS_CHECK(ctx->h_desc.ensure((size_t)B * cap * 256 * sizeof(float)));
     VS_CHECK(ctx->h_n.ensure((size_t)B * sizeof(int)));
-    VS_CHECK(sp_forward(ctx, B, ctx->h_img.as<uint8_t>(), channels, h, w, s));
+    VS_CHECK(sp_forward(ctx, B, ctx->h_img.as<uint8_t>(), channels, h, w, s, nullptr, nullptr, true));
     const int hc = (h + 7) / 8, wc = (w + 7) / 8;
     VS_CHECK(sp_postprocess(ctx, B, hc, wc, h, w, ctx->h_kps.as<vs_keypoint>(), ctx->h_desc.as<float>(),
-                            ctx->h_n.as<int>(), cap, s));
+                            ctx->h_n.as<int>(), cap, s, nullptr, nullptr, true));
     VS_CHECK(sp_postprocess_check(ctx, B, s));
     VS_HIP(hipMemcpyAsync(n, ctx->h_n.p, (size_t)B * sizeof(int), hipMemcpyDeviceToHost, s));
     VS_HIP(hipMemcpyAsync(kps, ctx->h_kps.p, (size_t)B * cap * sizeof(vs_keypoint), hipMemcpyDeviceToHost, s));

@@ -181,14 +181,17 @@ struct ScratchUse {  // scratch_order at construction, scratch_release at scope 
 // ---- stage launchers (return VS_OK or an error code; enqueue on `s` only) ------------------
 // Network: d_bgr is B x h x w x 3 u8 (or gray u8 when channels == 1, or nullptr when d_gray01
 // already holds B x h x w fp32 in [0,1]).  Produces ctx->semi [B][hc][wc][65] and ctx->dgrid
-// [B][hc][wc][256] (L2-normalised over channels).
+// [B][hc][wc][256] (L2-normalised over channels; grid_raw: left as the head's raw output, for a
+// post-processing call with grid_raw that normalises the four corners it samples instead).
 // semi_out / dgrid_out (optional) replace ctx->semi / ctx->dgrid as the output tensors.
 int sp_forward(vs_ctx* ctx, int B, const uint8_t* d_img, int channels, int h, int w,
-               hipStream_t s, float* semi_out = nullptr, float* dgrid_out = nullptr);
+               hipStream_t s, float* semi_out = nullptr, float* dgrid_out = nullptr, bool grid_raw = false);
 // Post-processing: semi / dgrid (default ctx->semi / ctx->dgrid) -> keypoints, descriptors, counts.
 int sp_postprocess(vs_ctx* ctx, int B, int hc, int wc, int h, int w, vs_keypoint* d_kps,
                    float* d_desc, int* d_n, int cap, hipStream_t s, const float* semi = nullptr,
-                   const float* dgrid = nullptr);
+                   const float* dgrid = nullptr, bool grid_raw = false);
+// The grid's L2 normalisation in place (npix cells of 256 channels; sp_post.hip).
+int desc_grid_l2norm(vs_ctx* ctx, long npix, float* grid, hipStream_t s);
 // Winograd F(2x2, 3x3) stride-1 pad-1 convolution (sp_net.hip k_wino3), NHWC fp32: U = the
 // transformed weights (winograd_weights), bias [cout_pad] (required), act 0 / 1 / 2 = none / ReLU /
 // ReLU6 after the bias, then out = act(.) + res1, out = res2 + out (optional, [pixel][out_cstride]).
