@@ -2,7 +2,8 @@
 `make -C visual-slam-pipeline_amd prof`): lane-0 clock64 deltas summed over the launches of one
 stress-window solve.  Phases: 0 the next diagonal block (wave 0) beside the trailing update (waves 1..),
 plus the first block; 1 publishing the block + the rows below; 2 the next panel's columns; 3 forward
-solve; 4 backward solve."""
+solve; 4 backward solve; for the banded kernel (k_ba_chol_band): 5 the band into LDS, 6 the
+factorisation with the forward solve, 7 the backward solve.  --span selects the window (3: banded)."""
 import ctypes
 import json
 import os
@@ -20,17 +21,19 @@ def main():
     lib = va.load_library(os.path.join(ROOT, "visual-slam-pipeline_amd", "libvslam_hip_prof.so"))
     lib.vs_debug_ba_cycles.argtypes = [ctypes.c_void_p, ctypes.c_int]
     from test_gpu_ba import windowed_problem
-    R, t, P, P0, kf, pt, uv = windowed_problem(50, 10000, 7, span=3, noise=1.0, pert=0.05)
+    span = int(sys.argv[sys.argv.index("--span") + 1]) if "--span" in sys.argv else 3
+    R, t, P, P0, kf, pt, uv = windowed_problem(50, 10000, 7, span=span, noise=1.0, pert=0.05)
     ctx = va.Context(0)
     ctx.local_ba(R, t, P0, kf, pt, uv)
     cyc = np.zeros(8, np.uint64)
     lib.vs_debug_ba_cycles(cyc.ctypes.data, 1)
     g = ctx.local_ba(R, t, P0, kf, pt, uv)
     lib.vs_debug_ba_cycles(cyc.ctypes.data, 1)
-    names = ["diag_ahead+trailing", "publish+rows_below", "next_panel_cols", "fwd_solve", "bwd_solve"]
+    names = ["diag_ahead+trailing", "publish+rows_below", "next_panel_cols", "fwd_solve", "bwd_solve",
+             "band: load", "band: factor+forward", "band: backward"]
     iters = int(g[5][0])
     print(json.dumps({"lm_iterations": iters,
-                      "kcycles_per_solve": {names[k]: round(float(cyc[k]) / max(iters, 1) / 1e3, 1) for k in range(5)}}))
+                      "kcycles_per_solve": {names[k]: round(float(cyc[k]) / max(iters, 1) / 1e3, 1) for k in range(8)}}))
     ctx.close()
 
 

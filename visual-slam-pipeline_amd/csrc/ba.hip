@@ -14,7 +14,8 @@
 //   k_ba_schur        one workgroup per (a, b) block: S_ab = [a == b] Hpp_a (1 + lambda) on the
 //                     diagonal - sum over common points (ascending) of U_a Hpm_b^T; b_a likewise
 //   k_ba_chol         dense right-looking Cholesky + the two triangular solves (one workgroup), or
-//   k_ba_chol_band    the same for a banded S (one wave, the band in LDS; bit-identical results)
+//   k_ba_chol_band    the same for a banded S (two waves: the pivot chain beside the column updates, the
+//                     band in LDS; bit-identical results)
 //   k_ba_update       back-substitution dm = Hinv (-bm - sum Hpm^T dp), new poses
 //   k_ba_cost         new cost (fixed chunks) + accept / reject, lambda, convergence (last chunk)
 // Every element is accumulated in the same order as the CPU restatement (oracle/orc_ba.cpp); the
@@ -445,130 +446,167 @@ __device__ __forceinline__ void wave_lds_sync() {
 // product with an exact zero, so skipping them leaves every element's value unchanged (at most the
 // sign of an exact-zero element can differ, which no later result sees) — the factor and the
 // solution are the oracle's (oracle/orc_ba.cpp chol_solve), element for element in the same order.
-// One wave, right-looking with the matrix as its band in LDS (row i, offset d = i - j): at column j
-// every lane updates its elements of the trailing band triangle (i, k) with j < k <= i <= j + band,
-// L = acc * R taken on the fly (the stored value stays the accumulated one), and the next pivot
-// R_{j+1} = 1 / sqrt(acc_{j+1,j+1} - L_{j+1,j}^2) is evaluated by every lane from the same LDS values
-// (lane-uniform, so the sqrt / division chain interleaves with the element updates instead of
-// running on a masked lane after them).  The forward substitution rides along; the backward one runs
-// from the last row with x_k broadcast from the lane that finished it.  Chosen by the host when the
-// band fits kBandMaxW columns; a pivot below DBL_EPSILON fails the solve as in k_ba_chol.
+// Right-looking with the matrix as its band in LDS (row i, offset d = i - j), two waves per column:
+// wave 0 runs the pivot chain — R_{j+1} = 1 / sqrt(acc_{j+1,j+1} - (acc_{j+1,j} R_j)^2), then the
+// next pivot's two inputs (the column-j updates of acc_{j+2,j+2} and acc_{j+2,j+1}, the same
+// operations wave 1 would apply, stored by wave 0) — while wave 1 applies column j to the rest of the
+// trailing band triangle (i, k), j < k <= i <= j + band, with L = acc * R taken on the fly (the stored
+// value stays the accumulated one) and carries the forward substitution; one barrier per column.
+// The waves touch disjoint cells within a column: wave 0 reads rows j + 1, j + 2 and writes two cells
+// of row j + 2 that wave 1 does not read in that column; wave 1 writes rows >= j + 3.  The backward
+// substitution keeps each open row's running value in a register of lane (row mod 64).  Chosen by
+// the host when the band fits kBandMaxW columns; a pivot below DBL_EPSILON fails the solve as in
+// k_ba_chol.
 constexpr int kBandMaxW = 36;  // band + 1 <= kBandMaxW (band <= 35: Bb <= 5)
-static_assert((kCholMaxN * kBandMaxW + 64 + kCholMaxN + kCholMaxN + 64) * sizeof(double) <= 160 * 1024,
+static_assert(((kCholMaxN + kBandMaxW) * kBandMaxW + 64 + kCholMaxN + 64 + kCholMaxN + 64) * sizeof(double) <= 160 * 1024,
               "k_ba_chol_band: the band, R and x must fit one CU's LDS (raise VS_BA_MAX_KEYFRAMES only with a "
               "narrower kBandMaxW)");
 // trailing-triangle elements per lane for a band: ceil(band (band + 1) / 2 / 64)
 constexpr int band_slots(int band) { return (band * (band + 1) / 2 + 63) / 64; }
 template <int NS>
-__global__ __launch_bounds__(64) void k_ba_chol_band(BaDev d) {
+__global__ __launch_bounds__(128) void k_ba_chol_band(BaDev d) {
     BA_LIVE(d);
-    const int n = 6 * d.N, np = d.np, B = d.band, W = B + 1, lane = threadIdx.x;
-    // A[i * W + dd] = acc (i, i - dd); the 64 cells past the band are each lane's dummy store target
-    __shared__ double A[kCholMaxN * kBandMaxW + 64];
-    __shared__ double Rd[kCholMaxN], xs[kCholMaxN + 64];
-    // the band out of S (just written by k_ba_schur, in L2): eight loads in flight per lane, then
-    // their LDS stores (one load at a time cost a global round trip per element)
-    for (int e0 = lane; e0 < n * W; e0 += 64 * 8) {
+    BA_T0();
+    const int n = 6 * d.N, np = d.np, B = d.band, W = B + 1;
+    const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
+    // A[i * W + dd] = acc (i, i - dd), rows n .. n + B - 1 zero padding (elements past the last row
+    // compute there, unread, instead of testing their row); the 64 cells past the padding rows are
+    // each lane's dummy store target
+    __shared__ double A[(kCholMaxN + kBandMaxW) * kBandMaxW + 64];
+    __shared__ double Rd[kCholMaxN + 64], xs[kCholMaxN + 64];
+    __shared__ int s_bad;
+    // the band out of S (just written by k_ba_schur, in L2): eight loads in flight per thread, then
+    // their LDS stores
+    for (int e0 = tid; e0 < n * W; e0 += 128 * 8) {
         double v[8];
 #pragma unroll
         for (int u = 0; u < 8; u++) {
-            const int e = e0 + 64 * u, i = e / W, dd = e - i * W;
+            const int e = e0 + 128 * u, i = e / W, dd = e - i * W;
             v[u] = (e < n * W && dd <= i) ? d.S[(size_t)i * np + (i - dd)] : 0.0;
         }
 #pragma unroll
         for (int u = 0; u < 8; u++)
-            if (e0 + 64 * u < n * W) A[e0 + 64 * u] = v[u];
+            if (e0 + 128 * u < n * W) A[e0 + 128 * u] = v[u];
     }
-    for (int i = lane; i < n; i += 64) xs[i] = -d.bs[i];
-    const int dummyA = kCholMaxN * kBandMaxW + lane, dummyX = kCholMaxN + lane;
-    // this lane's trailing-triangle elements e = lane + 64 q -> (a, b), 0 <= b <= a < B, i = j + 1 + a,
-    // k = j + 1 + b, as offsets from row j + 1: the element, L_ij's and L_kj's slots.  e = 0 (0, 0) is
-    // the next pivot, which every lane evaluates; e = 1 (1, 0) and e = 2 (1, 1) are lane 1's and lane
-    // 2's first elements, whose new values are the pivot after next's inputs (read back by readlane).
+    for (int i = tid; i < n; i += 128) xs[i] = -d.bs[i];
+    for (int i = tid; i < B * W; i += 128) A[n * W + i] = 0.0;
+    for (int i = n + tid; i < kCholMaxN + 64; i += 128) xs[i] = 0.0;
+    if (tid == 0) s_bad = 0;
+    const int dummyA = (kCholMaxN + kBandMaxW) * kBandMaxW + lane, dummyX = kCholMaxN + lane;
+    // wave 1's trailing-triangle elements e = lane + 64 q -> (a, b), 0 <= b <= a < B, i = j + 1 + a,
+    // k = j + 1 + b, as offsets from row j + 1: the element, L_ij's and L_kj's cells.  (0, 0) is the
+    // pivot (wave 0 evaluates it), (1, 0) and (1, 1) are wave 0's; slots past the triangle read the
+    // base cell and store to the dummy cell.
     const int nel = B * (B + 1) / 2;
-    int ea[NS], oe[NS], oi[NS], ok[NS];
+    int oe[NS], oi[NS], ok[NS];
+    bool dead[NS];
 #pragma unroll
     for (int q = 0; q < NS; q++) {
         const int e = lane + 64 * q;
         int a = 0;
         while ((a + 1) * (a + 2) / 2 <= e) a++;
         const int b = e - a * (a + 1) / 2;
-        ea[q] = e < nel && e > 0 ? a : n;  // n: never a live row offset
-        oe[q] = a * W + (a - b);
-        oi[q] = a * W + a + 1;
-        ok[q] = b * W + b + 1;
+        dead[q] = e >= nel || e < 3;
+        oe[q] = dead[q] ? 0 : a * W + (a - b);
+        oi[q] = dead[q] ? 0 : a * W + a + 1;
+        ok[q] = dead[q] ? 0 : b * W + b + 1;
     }
     __syncthreads();
-    bool bad = A[0] < DBL_EPSILON;
-    double Rj = 1.0 / sqrt(A[0]);
-    double p1 = A[W + 1], p0 = A[W];  // acc (1, 0), acc (1, 1): the next pivot's inputs
-    double xj = xs[0];                 // x_j with its forward terms so far
-    if (lane == 0) Rd[0] = Rj;
-    for (int j = 0; j < n && !bad; j++) {
-        const int j1 = j + 1, base = j1 * W;
-        const double yj = xj * Rj;
-        // the next pivot, lane-uniform and branch-free (meaningless past the last row)
-        const double l = p1 * Rj;
-        const double accn = p0 - l * l;
-        const bool badn = j1 < n && accn < DBL_EPSILON;
-        const double Rn = 1.0 / sqrt(accn);
-        // the lane's elements: all loads first, then the updates, then the stores (a dead slot
-        // reads its own cells harmlessly and stores to its dummy cell)
-        double xi[NS], xl[NS], xk[NS];
-        int st[NS];
-#pragma unroll
-        for (int q = 0; q < NS; q++) {
-            const bool live = j1 + ea[q] < n;
-            st[q] = live ? base + oe[q] : dummyA;
-            const int bq = live ? base : 0;
-            xi[q] = A[bq + oe[q]];
-            xl[q] = A[bq + oi[q]];
-            xk[q] = A[bq + ok[q]];
-        }
-        const bool fl = lane < B && j1 + lane < n;
-        const int fi = fl ? j1 + lane : dummyX;
-        const double xf = xs[fl ? j1 + lane : 0], lf = A[fl ? base + lane * W + lane + 1 : 0];
-        double v0 = 0.0;
-#pragma unroll
-        for (int q = 0; q < NS; q++) {
-            const double v = xi[q] - (xl[q] * Rj) * (xk[q] * Rj);
-            A[st[q]] = v;
-            if (q == 0) v0 = v;
-        }
-        const double xn = xf - (lf * Rj) * yj;  // forward substitution: x_i -= L_ij y_j
-        xs[fi] = xn;
-        if (lane == 0) {
-            xs[j] = yj;
-            if (j1 < n) {
-                A[base] = accn;
-                Rd[j1] = Rn;
-            }
-        }
-        p1 = readlane_f64(v0, 1);
-        p0 = readlane_f64(v0, 2);
-        xj = readlane_f64(xn, 0);
-        bad = badn;
-        Rj = Rn;
-        wave_lds_sync();
-    }
-    if (bad) {
-        if (lane == 0) d.ctl->solved = 0;
+    BA_T(5);  // the band, R and x into LDS
+    if (A[0] < DBL_EPSILON) {
+        if (tid == 0) d.ctl->solved = 0;
         return;
     }
-    // backward: x_k = y'_k R_k with y'_k = y_k - sum_{k' > k, descending} L_k'k x_k'
-    double yk = xs[n - 1];
-    for (int k = n - 1; k >= 0; k--) {
-        const double xkk = yk * Rd[k];  // lane-uniform
-        const bool live = lane < B && k - 1 - lane >= 0;
-        const int i = live ? k - 1 - lane : 0;
-        const double yn = xs[i] - (A[live ? k * W + lane + 1 : 0] * Rd[i]) * xkk;
-        xs[live ? i : dummyX] = yn;
-        if (lane == 0) xs[k] = xkk;
-        yk = readlane_f64(yn, 0);
-        wave_lds_sync();
+    double Rj = 1.0 / sqrt(A[0]);      // wave 0: R_j of the column being applied (both waves: R_0)
+    double p1 = A[W + 1], p0 = A[W];    // wave 0: acc (j+1, j), acc (j+1, j+1) before column j
+    double xj = xs[0];                  // wave 1: x_j with its forward terms so far
+    if (tid == 0) Rd[0] = Rj;
+    bool bad = false;
+    for (int j = 0; j < n; j++) {
+        const int j1 = j + 1, base = j1 * W;
+        if (wv == 0) {
+            // the next pivot's inputs, read before the chain so that their latency hides under it
+            const double q22 = A[base + W], q21 = A[base + W + 1], q20 = A[base + W + 2], q10 = A[base + 1];
+            const double l = p1 * Rj;
+            const double accn = p0 - l * l;
+            const bool badn = j1 < n && accn < DBL_EPSILON;
+            const double Rn = 1.0 / sqrt(accn);
+            // column j's updates of (j+2, j+2) and (j+2, j+1): wave 1's operations on those cells
+            p0 = q22 - (q20 * Rj) * (q20 * Rj);
+            p1 = q21 - (q20 * Rj) * (q10 * Rj);
+            A[base + W] = p0;
+            A[base + W + 1] = p1;
+            Rd[j1 < n ? j1 : kCholMaxN + lane] = Rn;
+            if (badn) s_bad = 1;
+            Rj = Rn;
+        } else {
+            const double Rc = j == 0 ? Rj : Rd[j];
+            double xi[NS], xl[NS], xk[NS];
+#pragma unroll
+            for (int q = 0; q < NS; q++) {
+                xi[q] = A[base + oe[q]];
+                xl[q] = A[base + oi[q]];
+                xk[q] = A[base + ok[q]];
+            }
+            const bool fl = lane < B;  // the forward substitution's rows j + 1 .. j + B
+            const double xf = xs[j1 + (fl ? lane : 0)], lf = A[base + (fl ? lane * W + lane + 1 : 0)];
+            const double yj = xj * Rc;
+#pragma unroll
+            for (int q = 0; q < NS; q++) {
+                const double v = xi[q] - (xl[q] * Rc) * (xk[q] * Rc);
+                A[dead[q] ? dummyA : base + oe[q]] = v;
+            }
+            const double xn = xf - (lf * Rc) * yj;  // forward substitution: x_i -= L_ij y_j
+            xs[fl ? j1 + lane : dummyX] = xn;
+            xs[j] = yj;  // (every lane, the same value)
+            xj = readlane_f64(xn, 0);
+        }
+        __syncthreads();
+        if (s_bad) {
+            bad = true;
+            break;
+        }
     }
+    BA_T(6);  // factorisation + forward substitution
+    if (bad) {
+        if (tid == 0) d.ctl->solved = 0;
+        return;
+    }
+    if (wv != 0) return;
+    // backward: x_k = y'_k R_k with y'_k = y_k - sum_{k' > k, descending} L_k'k x_k'.  Row i's running
+    // value stays in lane (i mod 64)'s register — at most B < 64 rows are open at once — so the chain
+    // from one step to the next is a readlane, two products and a difference: step k reads row k's
+    // final value, every open row i in [k - B, k - 1] subtracts (L_ki R_i) x_k, and the lane that
+    // finished row k takes up row k - 64 (the forward value, untouched until step k - 64 + B) with
+    // its R.  A lane's row ib satisfies 0 <= k - ib <= 63, so its cell k W + k - ib is always inside
+    // the band array (read unconditionally, used only while the row is open), one step ahead.
+    int ib = (n - 1) - ((n - 1 - lane) & 63);  // this lane's open row (< 0: none)
+    double acc = ib >= 0 ? xs[ib] : 0.0, ri = ib >= 0 ? Rd[ib] : 0.0;
+    int aix = (n - 1) * (W + 1) - ib;
+    double al = A[aix];
+    for (int k0 = n - 1; k0 >= 0; k0 -= 64) {
+        const double nxt = ib >= 64 ? xs[ib - 64] : 0.0, rnx = ib >= 64 ? Rd[ib - 64] : 0.0;
+        const double rblk = Rd[k0 - lane >= 0 ? k0 - lane : 0];  // lane t: R_{k0 - t}
+        const int kend = k0 - 63 > 0 ? k0 - 63 : 0;
+        for (int k = k0; k >= kend; k--) {
+            const int aixn = aix - (W + 1);
+            const double aln = A[aixn > 0 ? aixn : 0];
+            const double yk = readlane_f64(acc, k & 63);
+            const double xkk = yk * readlane_f64(rblk, k0 - k);  // lane-uniform
+            const double an = acc - (al * ri) * xkk;
+            const bool open = (unsigned)(k - 1 - ib) < (unsigned)B, fin = k == ib;
+            xs[fin ? k : dummyX] = xkk;
+            acc = fin ? nxt : (open ? an : acc);
+            ri = fin ? rnx : ri;
+            ib = fin ? ib - 64 : ib;
+            aix = fin ? aixn + 64 : aixn;
+            al = aln;
+        }
+    }
+    wave_lds_sync();
     for (int i = lane; i < n; i += 64) d.dp[i] = xs[i];
     if (lane == 0) d.ctl->solved = 1;
+    BA_T(7);  // backward substitution + the solution out
 }
 
 // the padded rows n..np-1 of S: identity (their columns >= n above the diagonal are never read)
@@ -1109,7 +1147,7 @@ int local_ba(vs_ctx* ctx, int N, double* R, double* t, int M, double* P, int n_o
             hipLaunchKernelGGL(k_ba_pt_acc, dim3(cdiv(M, T)), dim3(T), 0, s, d);
             hipLaunchKernelGGL(k_ba_schur, dim3(N * N + N), dim3(64), 0, s, d);
             if (use_band)
-                hipLaunchKernelGGL(chol_band, dim3(1), dim3(64), 0, s, d);
+                hipLaunchKernelGGL(chol_band, dim3(1), dim3(128), 0, s, d);
             else
                 hipLaunchKernelGGL(k_ba_chol, dim3(1), dim3(512), 0, s, d);
             hipLaunchKernelGGL(k_ba_update, dim3(cdiv(M + N, T)), dim3(T), 0, s, d);
