@@ -25,15 +25,17 @@ def main():
     R, t, P, P0, kf, pt, uv = windowed_problem(50, 10000, 7, span=span, noise=1.0, pert=0.05)
     ctx = va.Context(0)
     ctx.local_ba(R, t, P0, kf, pt, uv)
-    cyc = np.zeros(8, np.uint64)
+    cyc = np.zeros(16, np.uint64)
     lib.vs_debug_ba_cycles(cyc.ctypes.data, 1)
     g = ctx.local_ba(R, t, P0, kf, pt, uv)
     lib.vs_debug_ba_cycles(cyc.ctypes.data, 1)
     names = ["diag_ahead+trailing", "publish+rows_below", "next_panel_cols", "fwd_solve", "bwd_solve",
-             "band: load", "band: factor+forward", "band: backward"]
+             "band: load", "band: factor+forward", "band: backward", "band: wave 0 column work",
+             "band: wave 0 barrier wait", "band: wave 1 column work", "band: wave 1 barrier wait",
+             "band: wave 2 column work", "band: wave 2 barrier wait"]
     iters = int(g[5][0])
     print(json.dumps({"lm_iterations": iters,
-                      "kcycles_per_solve": {names[k]: round(float(cyc[k]) / max(iters, 1) / 1e3, 1) for k in range(8)}}))
+                      "kcycles_per_solve": {names[k]: round(float(cyc[k]) / max(iters, 1) / 1e3, 1) for k in range(14)}}))
     ctx.close()
 
 

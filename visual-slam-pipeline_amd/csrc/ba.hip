@@ -413,7 +413,7 @@ constexpr int kCholLd = kCholMaxN;  // PnT row length
 
 #ifdef VS_BA_PROFILE
 // phase cycle counters of k_ba_chol (profiling build only: make -C visual-slam-pipeline_amd prof)
-__device__ unsigned long long g_ba_cycles[8];
+__device__ unsigned long long g_ba_cycles[16];
 #define BA_T0() long long _ba_t = clock64()
 #define BA_T(k)                                                               \
     do {                                                                      \
@@ -461,14 +461,41 @@ constexpr int kBandMaxW = 36;  // band + 1 <= kBandMaxW (band <= 35: Bb <= 5)
 static_assert(((kCholMaxN + kBandMaxW) * kBandMaxW + 64 + kCholMaxN + 64 + kCholMaxN + 64) * sizeof(double) <= 160 * 1024,
               "k_ba_chol_band: the band, R and x must fit one CU's LDS (raise VS_BA_MAX_KEYFRAMES only with a "
               "narrower kBandMaxW)");
+// 1.0 / sqrt(x), bit for bit, for 2^-700 <= x <= 2^700: the compiler's correctly rounded sqrt and
+// division expansions without their range scaling (scale factor 1 in that range: v_rsq + the
+// Goldschmidt steps, then v_rcp + two Newton steps + the final remainder step), 17 dependent
+// operations instead of 31.  tools/r05/rsq_exact.hip compared it with 1.0 / sqrt(x) on 537 M inputs
+// over the range: no difference.  Outside the range: the plain expression.
+__device__ __forceinline__ double recip_sqrt_rn(double x) {
+    if (!(x >= 0x1p-700 && x <= 0x1p700)) return 1.0 / sqrt(x);
+    const double y = __builtin_amdgcn_rsq(x);
+    double g = x * y, h = 0.5 * y;
+    const double r = fma(-h, g, 0.5);
+    g = fma(g, r, g);
+    h = fma(h, r, h);
+    double d = fma(-g, g, x);
+    g = fma(d, h, g);
+    d = fma(-g, g, x);
+    const double s = fma(d, h, g);  // sqrt (x)
+    double z = __builtin_amdgcn_rcp(s);
+    double e = fma(-s, z, 1.0);
+    z = fma(z, e, z);
+    e = fma(-s, z, 1.0);
+    z = fma(z, e, z);
+    const double rr = fma(-s, z, 1.0);
+    return fma(rr, z, z);
+}
 // trailing-triangle elements per lane for a band: ceil(band (band + 1) / 2 / 64)
 constexpr int band_slots(int band) { return (band * (band + 1) / 2 + 63) / 64; }
+constexpr int kBandThreads = 128;  // wave 0: the pivot chain, wave 1: the column updates (a third wave
+                                   // sharing the updates measured no faster: both are latency-bound)
 template <int NS>
-__global__ __launch_bounds__(128) void k_ba_chol_band(BaDev d) {
+__global__ __launch_bounds__(kBandThreads) void k_ba_chol_band(BaDev d) {
     BA_LIVE(d);
     BA_T0();
     const int n = 6 * d.N, np = d.np, B = d.band, W = B + 1;
-    const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);  // (wave-uniform: scalar branches)
     // A[i * W + dd] = acc (i, i - dd), rows n .. n + B - 1 zero padding (elements past the last row
     // compute there, unread, instead of testing their row); the 64 cells past the padding rows are
     // each lane's dummy store target
@@ -477,20 +504,20 @@ __global__ __launch_bounds__(128) void k_ba_chol_band(BaDev d) {
     __shared__ int s_bad;
     // the band out of S (just written by k_ba_schur, in L2): eight loads in flight per thread, then
     // their LDS stores
-    for (int e0 = tid; e0 < n * W; e0 += 128 * 8) {
+    for (int e0 = tid; e0 < n * W; e0 += kBandThreads * 8) {
         double v[8];
 #pragma unroll
         for (int u = 0; u < 8; u++) {
-            const int e = e0 + 128 * u, i = e / W, dd = e - i * W;
+            const int e = e0 + kBandThreads * u, i = e / W, dd = e - i * W;
             v[u] = (e < n * W && dd <= i) ? d.S[(size_t)i * np + (i - dd)] : 0.0;
         }
 #pragma unroll
         for (int u = 0; u < 8; u++)
-            if (e0 + 128 * u < n * W) A[e0 + 128 * u] = v[u];
+            if (e0 + kBandThreads * u < n * W) A[e0 + kBandThreads * u] = v[u];
     }
-    for (int i = tid; i < n; i += 128) xs[i] = -d.bs[i];
-    for (int i = tid; i < B * W; i += 128) A[n * W + i] = 0.0;
-    for (int i = n + tid; i < kCholMaxN + 64; i += 128) xs[i] = 0.0;
+    for (int i = tid; i < n; i += kBandThreads) xs[i] = -d.bs[i];
+    for (int i = tid; i < B * W; i += kBandThreads) A[n * W + i] = 0.0;
+    for (int i = n + tid; i < kCholMaxN + 64; i += kBandThreads) xs[i] = 0.0;
     if (tid == 0) s_bad = 0;
     const int dummyA = (kCholMaxN + kBandMaxW) * kBandMaxW + lane, dummyX = kCholMaxN + lane;
     // wave 1's trailing-triangle elements e = lane + 64 q -> (a, b), 0 <= b <= a < B, i = j + 1 + a,
@@ -517,29 +544,48 @@ __global__ __launch_bounds__(128) void k_ba_chol_band(BaDev d) {
         if (tid == 0) d.ctl->solved = 0;
         return;
     }
-    double Rj = 1.0 / sqrt(A[0]);      // wave 0: R_j of the column being applied (both waves: R_0)
-    double p1 = A[W + 1], p0 = A[W];    // wave 0: acc (j+1, j), acc (j+1, j+1) before column j
-    double xj = xs[0];                  // wave 1: x_j with its forward terms so far
+    double Rj = recip_sqrt_rn(A[0]);  // R_0 (both waves)
     if (tid == 0) Rd[0] = Rj;
+    // Each wave runs its own loop over the columns (wv is wave-uniform: scalar branches), one barrier
+    // per column in each.  A bad pivot does not stop the loops (the rest computes on garbage and is
+    // discarded): the verdict is shared once, after them.
     bool bad = false;
-    for (int j = 0; j < n; j++) {
-        const int j1 = j + 1, base = j1 * W;
-        if (wv == 0) {
+#ifdef VS_BA_PROFILE
+    long long t_work = 0, t_wait = 0, t_a = clock64();
+#define VS_BAND_T_BARRIER()          \
+    do {                             \
+        const long long t_b = clock64(); \
+        t_work += t_b - t_a;         \
+        __syncthreads();             \
+        t_a = clock64();             \
+        t_wait += t_a - t_b;         \
+    } while (0)
+#else
+#define VS_BAND_T_BARRIER() __syncthreads()
+#endif
+    if (wv == 0) {
+        double p1 = A[W + 1], p0 = A[W];  // acc (j+1, j), acc (j+1, j+1) before column j
+        for (int j = 0; j < n; j++) {
+            const int j1 = j + 1, base = j1 * W;
             // the next pivot's inputs, read before the chain so that their latency hides under it
             const double q22 = A[base + W], q21 = A[base + W + 1], q20 = A[base + W + 2], q10 = A[base + 1];
             const double l = p1 * Rj;
             const double accn = p0 - l * l;
-            const bool badn = j1 < n && accn < DBL_EPSILON;
-            const double Rn = 1.0 / sqrt(accn);
+            bad |= j1 < n && accn < DBL_EPSILON;
+            const double Rn = recip_sqrt_rn(accn);
             // column j's updates of (j+2, j+2) and (j+2, j+1): wave 1's operations on those cells
             p0 = q22 - (q20 * Rj) * (q20 * Rj);
             p1 = q21 - (q20 * Rj) * (q10 * Rj);
             A[base + W] = p0;
             A[base + W + 1] = p1;
             Rd[j1 < n ? j1 : kCholMaxN + lane] = Rn;
-            if (badn) s_bad = 1;
             Rj = Rn;
-        } else {
+            VS_BAND_T_BARRIER();
+        }
+    } else {
+        double xj = xs[0];  // x_j with its forward terms so far
+        for (int j = 0; j < n; j++) {
+            const int j1 = j + 1, base = j1 * W;
             const double Rc = j == 0 ? Rj : Rd[j];
             double xi[NS], xl[NS], xk[NS];
 #pragma unroll
@@ -560,15 +606,20 @@ __global__ __launch_bounds__(128) void k_ba_chol_band(BaDev d) {
             xs[fl ? j1 + lane : dummyX] = xn;
             xs[j] = yj;  // (every lane, the same value)
             xj = readlane_f64(xn, 0);
-        }
-        __syncthreads();
-        if (s_bad) {
-            bad = true;
-            break;
+            VS_BAND_T_BARRIER();
         }
     }
+#undef VS_BAND_T_BARRIER
+#ifdef VS_BA_PROFILE
+    if (lane == 0) {  // 8 + 2w / 9 + 2w: wave w's column work / barrier wait
+        atomicAdd(&g_ba_cycles[8 + 2 * wv], (unsigned long long)t_work);
+        atomicAdd(&g_ba_cycles[9 + 2 * wv], (unsigned long long)t_wait);
+    }
+#endif
+    if (wv == 0 && bad) s_bad = 1;
+    __syncthreads();
     BA_T(6);  // factorisation + forward substitution
-    if (bad) {
+    if (s_bad) {
         if (tid == 0) d.ctl->solved = 0;
         return;
     }
@@ -1147,7 +1198,7 @@ int local_ba(vs_ctx* ctx, int N, double* R, double* t, int M, double* P, int n_o
             hipLaunchKernelGGL(k_ba_pt_acc, dim3(cdiv(M, T)), dim3(T), 0, s, d);
             hipLaunchKernelGGL(k_ba_schur, dim3(N * N + N), dim3(64), 0, s, d);
             if (use_band)
-                hipLaunchKernelGGL(chol_band, dim3(1), dim3(128), 0, s, d);
+                hipLaunchKernelGGL(chol_band, dim3(1), dim3(kBandThreads), 0, s, d);
             else
                 hipLaunchKernelGGL(k_ba_chol, dim3(1), dim3(512), 0, s, d);
             hipLaunchKernelGGL(k_ba_update, dim3(cdiv(M + N, T)), dim3(T), 0, s, d);
@@ -1188,9 +1239,9 @@ int local_ba(vs_ctx* ctx, int N, double* R, double* t, int M, double* P, int n_o
 
 #ifdef VS_BA_PROFILE
 extern "C" int vs_debug_ba_cycles(unsigned long long* out, int reset) {
-    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(vs::g_ba_cycles), sizeof(unsigned long long) * 8) != hipSuccess) return -1;
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(vs::g_ba_cycles), sizeof(unsigned long long) * 16) != hipSuccess) return -1;
     if (reset) {
-        unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        unsigned long long z[16] = {};
         if (hipMemcpyToSymbol(HIP_SYMBOL(vs::g_ba_cycles), z, sizeof(z)) != hipSuccess) return -1;
     }
     return 0;
