@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round-5: the full GPU suite and the default bench line after the post-processing fusion
 export TMPDIR=/tmp
-O=gpurun_out/r05v; mkdir -p $O
+O=gpurun_out/${GPU_V_OUT:-r05v}; mkdir -p $O
 ( while sleep 45; do echo "[hb] $(date +%T)"; done ) & HB=$!
 trap "kill $HB" EXIT
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -p no:cacheprovider > $O/pytest.log 2>&1 || { tail -30 $O/pytest.log; exit 1; }
