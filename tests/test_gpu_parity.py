@@ -100,6 +100,37 @@ def test_postprocess_edges(vsctx, oracle):
         assert _kp_equal(kg, ko) and _bits_equal(dgpu, do)
 
 
+@pytest.mark.parametrize("hc,wc", [(19, 25), (13, 7), (5, 41)])
+def test_postprocess_partial_tiles(vsctx, oracle, hc, wc):
+    """Cell grids whose pixel sizes are not multiples of the 32-pixel NMS tile: the decode fused into
+    k_nms_lmax (halo cells past the grid, partial tiles, the interior heatmap stores) and the
+    XCD-aware tile order, bit-exact against the CPU restatement."""
+    rng = np.random.default_rng(hc * 100 + wc)
+    semi = (rng.standard_normal((65, hc, wc)) * 3).astype(np.float32)
+    dg = rng.standard_normal((256, hc, wc)).astype(np.float32)
+    dg /= np.linalg.norm(dg, axis=0, keepdims=True)
+    for h, w in [(hc * 8, wc * 8), (hc * 8 - 3, wc * 8 - 5)]:
+        kg, dgpu = vsctx.postprocess(semi, dg, h=h, w=w)
+        ko, do = oracle.postprocess(semi, dg, h=h, w=w, order_mode=1)
+        assert _kp_equal(kg, ko) and _bits_equal(dgpu, do)
+
+
+def test_extract_odd_geometry_raw_grid_equals_network_plus_oracle_post(vsctx, oracle):
+    """Extraction at 152 x 200 (partial NMS tiles) through the raw-grid path — the network leaves the
+    descriptor grid unnormalised and the sampler normalises the corners it reads — equals the
+    normalised network output post-processed by the CPU restatement, bit for bit."""
+    rng = np.random.default_rng(5)
+    h, w = 152, 200
+    img = (rng.random((h, w, 3)) * 255).astype(np.uint8)
+    img[40:90, 60:150] = 255 - img[40:90, 60:150]  # some structure
+    kps, desc = vsctx.extract(img)
+    gray = oracle.gray_to_f32(oracle.bgr_to_gray(img))
+    semi, dg = vsctx.superpoint_forward(gray)
+    ko, do = oracle.postprocess(semi, dg, h=h, w=w, order_mode=1)
+    assert len(kps) > 0
+    assert _kp_equal(kps, ko) and _bits_equal(desc, do)
+
+
 def test_extract_end_to_end_equals_network_plus_oracle_post(vsctx, oracle, seq4):
     f = seq4[2]
     kps, desc = vsctx.extract(f["bgr"])
