@@ -1,7 +1,7 @@
 #!/bin/bash
-# Round-5: the exact unscaled division / square root in the PnP solvers: exactness probe, parity, kernel A/B
+# Round-5: PnP solver changes (the unscaled division / sqrt experiment; the LM pivot reciprocals): probe, parity, kernel A/B
 export TMPDIR=/tmp
-O=gpurun_out/r05z; mkdir -p $O
+O=gpurun_out/${GPU_Z_OUT:-r05z}; mkdir -p $O
 ( while sleep 45; do echo "[hb] $(date +%T)"; done ) & HB=$!
 trap "kill $HB" EXIT
 timeout -k 10 120 tools/r05/rsq_exact > $O/probe.txt 2>&1 || { cat $O/probe.txt; exit 1; }

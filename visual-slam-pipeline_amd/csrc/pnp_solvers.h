@@ -1169,6 +1169,8 @@ VS_HD inline void lm_point(const LmRots& L, const double* t, const Cam& K, doubl
 }
 
 // Solves (J^T J with its diagonal scaled by 1 + lambda) d = -J^T r by Cholesky; false if not SPD.
+// Each pivot's reciprocal is taken once: the factor's column and both substitutions multiply by it,
+// so the substitutions' chains are products, not divisions (the device's latency).
 VS_HD inline bool lm_solve(const double* acc, double lambda, double* d) {
     double A[36];
     int k = 0;
@@ -1182,27 +1184,29 @@ VS_HD inline bool lm_solve(const double* acc, double lambda, double* d) {
         A[a * 6 + a] *= 1.0 + lambda;
         d[a] = -acc[21 + a];
     }
+    double inv[6];
     for (int j = 0; j < 6; j++) {
         double s = A[j * 6 + j];
         for (int q = 0; q < j; q++) s -= A[j * 6 + q] * A[j * 6 + q];
         if (!(s > 0)) return false;
         const double r = sqrt(s);
         A[j * 6 + j] = r;
+        inv[j] = 1.0 / r;
         for (int i = j + 1; i < 6; i++) {
             double w = A[i * 6 + j];
             for (int q = 0; q < j; q++) w -= A[i * 6 + q] * A[j * 6 + q];
-            A[i * 6 + j] = w / r;
+            A[i * 6 + j] = w * inv[j];
         }
     }
     for (int i = 0; i < 6; i++) {
         double w = d[i];
         for (int q = 0; q < i; q++) w -= A[i * 6 + q] * d[q];
-        d[i] = w / A[i * 6 + i];
+        d[i] = w * inv[i];
     }
     for (int i = 5; i >= 0; i--) {
         double w = d[i];
         for (int q = i + 1; q < 6; q++) w -= A[q * 6 + i] * d[q];
-        d[i] = w / A[i * 6 + i];
+        d[i] = w * inv[i];
     }
     return true;
 }
