@@ -1198,7 +1198,7 @@ inline bool wino4_enabled() {
 inline long wino4_min_wg() {
     static const long n = [] {
         const char* e = std::getenv("VS_WINO4_MIN_WG");
-        return e ? std::atol(e) : 64L;
+        return e ? std::atol(e) : 32L;
     }();
     return n;
 }
@@ -1268,7 +1268,8 @@ int launch_wino(const DevLayer& L, const float* in, int in_cstride, int in_coff,
     a.b1a = nullptr;
     a.act = 1;  // every SuperPoint 3x3 conv is followed by ReLU
     // F(4x4, 3x3) (round 5, wino4.hip) on the layers whose 16 x 16-pixel workgroups are many per frame:
-    // at least VS_WINO4_MIN_WG (default 64) per frame — a property of the layer's geometry alone, so a
+    // at least VS_WINO4_MIN_WG (default 32: conv4a/b's 40 included — alone on the chip they run 5 %
+    // slower than F(2x2), beside the tracker 14 % faster, +2.5 % frames/s) per frame — a property of the layer's geometry alone, so a
     // frame's result never depends on the batch it is extracted in; VS_WINO4=0 keeps every layer on
     // F(2x2, 3x3) (A/B)
     if (L.wu4 && wino4_enabled() && (long)((H + 15) / 16) * ((W + 15) / 16) * (L.cout_pad / 64) >= wino4_min_wg()) {
