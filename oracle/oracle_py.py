@@ -50,6 +50,7 @@ _SIG = {
     "orc_fmat_verify": (_I, [_P, _P, _P, _I, _P, _P, _P, _P, _P]),
     "orc_local_ba": (_I, [_I, _P, _P, _I, _P, _I, _P, _P, _P, _P, _I, _P, _P, _P]),
     "orc_five_point": (_I, [_P, _P, _P]),
+    "orc_poly_real_roots": (_I, [_P, _P]),
     "orc_find_essential": (_I, [_P, _P, _I, _P, ctypes.c_double, ctypes.c_double, _I, _P, _P, _P]),
     "orc_recover_pose": (_I, [_P, _P, _P, _I, _P, _P, _P, _P]),
     "orc_estimate_motion": (_I, [_P, _P, _I, _P, _P, _P, _P, _P, _P]),
@@ -351,6 +352,16 @@ def local_ba(R, t, P, obs_kf, obs_pt, obs_uv, K=(525.0, 525.0, 319.5, 239.5), ma
 
 
 _K = (525.0, 525.0, 319.5, 239.5)
+
+
+def poly_real_roots(c):
+    """Real roots of sum c[k] x^k (k = 0..10), as five_point's root search finds them, ascending."""
+    c0 = np.asarray(c, np.float64).ravel()
+    c = np.zeros(11)
+    c[:len(c0)] = c0
+    r = np.zeros(10)
+    n = lib().orc_poly_real_roots(_p(c), _p(r))
+    return r[:n].copy()
 
 
 def five_point(q1, q2):

@@ -42,6 +42,15 @@ int count_inl(const double* E, const std::vector<double>& q1, const std::vector<
 
 }  // namespace
 
+// the degree-10 real-root search five_point runs (emat_solvers.h poly_real_roots): c[0..10]
+// ascending; roots ascending into roots[0..9]; returns the count
+extern "C" int orc_poly_real_roots(const double* c, double* roots) {
+    double W[kWsSize];
+    const int n = poly_real_roots(c, W, 1);
+    for (int i = 0; i < n; i++) roots[i] = W[kWsR + i];
+    return n;
+}
+
 extern "C" int orc_five_point(const double* q1, const double* q2, double* E_out) {
     double E[kMaxModels][9];
     const int n = five_point(q1, q2, E);

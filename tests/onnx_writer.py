@@ -150,8 +150,8 @@ def split_superpoint(flat):
     return out
 
 
-DESC_TAILS = ("reducel2", "reducel2_unsqueeze", "reducel2_attr", "pow_sum_sqrt", "mul_self_sum_sqrt",
-              "normalize_clip", "reciprocal", "raw")
+DESC_TAILS = ("reducel2", "reducel2_unsqueeze", "reducel2_attr", "pow_sum_sqrt", "pow_int_sum_sqrt",
+              "pow_value_float_sum_sqrt", "mul_self_sum_sqrt", "normalize_clip", "reciprocal", "raw")
 
 
 def superpoint_model(flat, seed=0, heads_swapped=False, identity_alias=True, drop_pool=False, modes=None,
@@ -162,7 +162,8 @@ def superpoint_model(flat, seed=0, heads_swapped=False, identity_alias=True, dro
     desc_tail: how "desc" leaves the graph — "reducel2" (ReduceL2 keepdims=1 with an axes input, then
     Div), "reducel2_unsqueeze" (MagicLeap's torch.norm(dim=1) + unsqueeze: ReduceL2 keepdims=0 ->
     Unsqueeze -> Div), "reducel2_attr" (opset < 18: axes as an attribute), "pow_sum_sqrt"
-    (Pow 2 -> ReduceSum -> Sqrt -> Div), "mul_self_sum_sqrt" (Mul(x, x) -> ReduceSum -> Sqrt -> Div),
+    (Pow 2 -> ReduceSum -> Sqrt -> Div; "pow_int_sum_sqrt": the exponent an INT64 Constant 2,
+    "pow_value_float_sum_sqrt": a Constant with value_float 2), "mul_self_sum_sqrt" (Mul(x, x) -> ReduceSum -> Sqrt -> Div),
     "normalize_clip" (F.normalize: ReduceL2 -> Clip(min=eps) -> Expand -> Div), "reciprocal"
     (x * Reciprocal(ReduceL2(x))), "raw" (convDb's output itself), or the invalid "reduce_all" (a
     ReduceL2 over every axis), "pow3_sum_sqrt" (exponent 3: not a norm) and "clip_max" (a clamp with an
@@ -216,9 +217,16 @@ def superpoint_model(flat, seed=0, heads_swapped=False, identity_alias=True, dro
         elif desc_tail == "reducel2_unsqueeze":
             n = G.op("ReduceL2", [d], [attr_ints("axes", [1]), attr_int("keepdims", 0)])
             n = G.op("Unsqueeze", [n, int_const([1])])
-        elif desc_tail in ("pow_sum_sqrt", "mul_self_sum_sqrt", "pow3_sum_sqrt"):
+        elif desc_tail in ("pow_sum_sqrt", "mul_self_sum_sqrt", "pow3_sum_sqrt", "pow_int_sum_sqrt",
+                           "pow_value_float_sum_sqrt", "pow_int3_sum_sqrt"):
             if desc_tail == "mul_self_sum_sqrt":
                 sq = G.op("Mul", [d, d])
+            elif desc_tail in ("pow_int_sum_sqrt", "pow_int3_sum_sqrt"):
+                e = G.op("Constant", [], [attr_tensor("value", _i(2, 7) + _s(8, "e") + _ld(
+                    9, np.array([2 if desc_tail == "pow_int_sum_sqrt" else 3], "<i8").tobytes()))])
+                sq = G.op("Pow", [d, e])
+            elif desc_tail == "pow_value_float_sum_sqrt":
+                sq = G.op("Pow", [d, G.op("Constant", [], [attr_float("value_float", 2.0)])])
             else:
                 sq = G.op("Pow", [d, f_const(2.0 if desc_tail == "pow_sum_sqrt" else 3.0)])
             n = G.op("Sqrt", [G.op("ReduceSum", [sq, int_const([1])], [attr_int("keepdims", 1)])])

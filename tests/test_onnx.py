@@ -111,6 +111,7 @@ def test_superpoint_onnx_desc_tail_is_classified(tmp_path, sp_weights, tail):
 @pytest.mark.parametrize("kw,msg", [(dict(semi_tail="softmax"), "raw logits"),
                                     (dict(desc_tail="reduce_all"), "L2 normalisation over channels"),
                                     (dict(desc_tail="pow3_sum_sqrt"), "L2 normalisation over channels"),
+                                    (dict(desc_tail="pow_int3_sum_sqrt"), "L2 normalisation over channels"),
                                     (dict(desc_tail="clip_max"), "L2 normalisation over channels"),
                                     (dict(pads=False), "explicit pads")])
 def test_superpoint_onnx_rejects_other_tails_and_default_padding(tmp_path, sp_weights, kw, msg):

@@ -232,3 +232,64 @@ def test_estimate_scale_known_answer_and_restatement(oracle):
     assert abs(s2 - s_true) < 0.02 * s_true and abs(s1 - s_true) < 0.02 * s_true
     # too few depth samples -> -1 (Slam.cpp:190)
     assert oracle.estimate_scale(p1[:5], p2[:5], R, t_unit, d1, None) == -1.0
+
+
+def _found(roots, r, tol):
+    return np.any(np.abs(roots - r) <= tol * max(1.0, abs(r)))
+
+
+@pytest.mark.parametrize("seed", range(20))
+def test_poly_real_roots_simple_roots(oracle, seed):
+    """five_point's degree-10 real-root search (emat_solvers.h poly_real_roots) on polynomials with
+    well separated real roots and complex pairs: every real root to 1e-12, none invented."""
+    rng = np.random.default_rng(seed)
+    nr = int(rng.integers(0, 6))
+    real = np.sort(rng.uniform(-3, 3, nr))
+    while nr > 1 and np.min(np.diff(real)) < 0.05:
+        real = np.sort(rng.uniform(-3, 3, nr))
+    poly = np.poly1d([1.0])
+    for r in real:
+        poly *= np.poly1d([1.0, -r])
+    for _ in range((10 - nr) // 2):
+        a, b = rng.uniform(-2, 2), rng.uniform(0.3, 2)
+        poly *= np.poly1d([1.0, -2 * a, a * a + b * b])
+    got = oracle.poly_real_roots(poly.coeffs[::-1] * rng.uniform(0.5, 2))
+    assert len(got) == nr, (got, real)
+    assert np.all(np.abs(got - real) <= 1e-12 * np.maximum(1, np.abs(real)))
+
+
+@pytest.mark.parametrize("gap", [0.0, 1e-13, 1e-10, 1e-9, 1e-8])
+def test_poly_real_roots_near_double_root(oracle, gap):
+    """the derivative's roots (the cuts between monotone pieces) are refined to 2^-26 only,
+    so a cut can land outside a pair of roots closer than that; the pair then shows no sign change on
+    either side.  A cut at which the polynomial is within rounding noise of zero is taken as a root: a
+    (near-)double root is never lost, and the separated roots stay exact."""
+    poly = np.poly1d([1.0, -1.0]) * np.poly1d([1.0, -(1.0 + gap)])
+    for r in (-2.5, 0.3, 2.0):
+        poly *= np.poly1d([1.0, -r])
+    poly *= np.poly1d([1.0, 0.4, 1.3]) * np.poly1d([1.0, -1.0, 2.0]) * np.poly1d([1.0, 3.0])
+    got = oracle.poly_real_roots(poly.coeffs[::-1])
+    assert 1 <= np.sum(np.abs(got - 1.0) < 1e-6) <= 2, got
+    for r in (-3.0, -2.5, 0.3, 2.0):
+        assert _found(got, r, 1e-12), (r, got)
+    assert len(got) <= 7
+
+
+def test_poly_real_roots_huge_root_bound(oracle):
+    """A tiny leading coefficient puts the Cauchy bound near 1e280.  The search is capped where every
+    derivative level's Horner sums stay finite (2^97 here: the root near -1e40 is not searched), the
+    geometric bracket split takes sqrt|a| sqrt|b| (sqrt(a b) would overflow) and a bracket straddling 0
+    that wide is split at 0 first, so the small roots come out exact instead of being lost to the
+    iteration limit."""
+    small = np.poly1d([1.0, -1.0]) * np.poly1d([1.0, -2.0]) * np.poly1d([1.0, -3.0])
+    for lead in (1e-280, 1e-200, 1e-120):
+        c = np.zeros(11)
+        c[:4] = small.coeffs[::-1]
+        c[10] = lead
+        got = oracle.poly_real_roots(c)
+        assert np.all(np.isfinite(got)) and np.all(np.abs(got) <= 2.0 ** 97), got
+        for r in (1.0, 2.0, 3.0):
+            assert _found(got, r, 1e-12), (lead, got)
+        big = -(1.0 / lead) ** (1.0 / 7.0)  # x^7 ~ -c3 / c10 far out
+        if abs(big) < 2.0 ** 90:
+            assert _found(got, big, 1e-9), (big, got)

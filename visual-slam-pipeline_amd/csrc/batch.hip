@@ -141,6 +141,7 @@ struct BatchSet {
     uint32_t* h_seeds = nullptr;  // pinned
     hipEvent_t net_done = nullptr, geo_done = nullptr;
     bool pending = false;
+    bool gathered = false;  // the step in this set all-gathered its records (g_kps / g_desc / g_n)
 };
 
 }  // namespace
@@ -339,6 +340,7 @@ int vs_batch_submit_dev(vs_batch* b, const uint8_t* d_bgr, const float* d_depth,
     }
     VS_CHECK(vs::sp_postprocess(ctx, B, (h + 7) / 8, (w + 7) / 8, h, w, S.kps + rec_k, S.desc + rec_d, S.n + 1, cap, sg,
                                 S.semi, S.dgrid, true));
+    S.gathered = xchg && b->gather;
     if (xchg) {  // slot 0 <- frame rank * B - 1 (batch_exchange.h, shared with the CPU loopback test)
         vs_bx::Tables tb;
         tb.B = B, tb.cap = cap, tb.rank = b->rank, tb.world = b->world, tb.gather = b->gather;
@@ -410,6 +412,7 @@ int vs_batch_step_dev(vs_batch* b, const uint8_t* d_bgr, const float* d_depth, c
 
 int vs_batch_set_gather(vs_batch* b, int on) {
     VS_ARG(b, "vs_batch_set_gather: null argument");
+    VS_ARG(b->collected == b->submitted, "vs_batch_set_gather: steps in flight (collect them first)");
     if (!on || b->gather || !b->comm) {
         b->gather = on && b->comm;
         return VS_OK;
@@ -430,7 +433,9 @@ int vs_batch_set_gather(vs_batch* b, int on) {
 int vs_batch_features_dev(vs_batch* b, const vs_keypoint** d_kps, const float** d_desc, const int** d_n, int* frames) {
     VS_ARG(b && d_kps && d_desc && d_n && frames, "vs_batch_features_dev: null argument");
     VS_ARG(b->collected == b->submitted, "vs_batch_features_dev: steps in flight (collect them first)");
-    if (b->comm && b->gather) {
+    // the records of the last collected step as that step produced them: the gathered table only when
+    // that step all-gathered (gather switched on after it leaves its own set's records)
+    if (b->comm && b->collected > 0 && b->set[b->last_set].gathered) {
         *d_kps = b->g_kps, *d_desc = b->g_desc, *d_n = b->g_n, *frames = b->world * b->B;
     } else {
         const BatchSet& S = b->set[b->last_set];

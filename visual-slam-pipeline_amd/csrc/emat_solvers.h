@@ -95,6 +95,25 @@ constexpr int kWsSize = 256;
 // coefficients above the true degree change no bit), with the coefficients in registers.
 constexpr double kRootTol = 0x1p-50;  // the polynomial's own roots (they become E)
 constexpr double kCutTol = 0x1p-26;   // a derivative's roots: they only cut the line into monotone pieces
+// split point of a bracket (a, b) that plain bisection would shrink too slowly: a bracket on one side
+// of 0 spanning orders of magnitude is split geometrically — sqrt|a| sqrt|b| (a product first would
+// overflow near the root bound or underflow for tiny ends; an end at 0 counts as 2^-32 of the other) —
+// and a bracket straddling 0 wider than 2^20 at 0 itself; anything else, or a split point that is not
+// strictly inside (a, b), gives the midpoint
+VS_HD inline bool wide_bracket(double a, double b) {
+    return (a >= 0 && b > 16.0 * a) || (b <= 0 && a < 16.0 * b) || (a < 0 && b > 0 && b - a > 0x1p20);
+}
+VS_HD inline double split_point(double a, double b) {
+    double g;
+    if (a < 0 && b > 0)
+        g = 0.0;
+    else if (a >= 0)
+        g = a == 0 ? b * 0x1p-32 : sqrt(a) * sqrt(b);
+    else
+        g = b == 0 ? a * 0x1p-32 : -(sqrt(-a) * sqrt(-b));
+    return g > a && g < b ? g : 0.5 * (a + b);
+}
+
 VS_HD inline int poly_real_roots(const double* c, double* W, int wst) {
 #define WS(i) W[(size_t)(i) * wst]
     // (static indices only: the coefficients stay in registers)
@@ -144,6 +163,17 @@ VS_HD inline int poly_real_roots(const double* c, double* W, int wst) {
         for (int k = 9; k >= 0; k--) f = f * xb + ac[k];
         if (f > 0 && xb < bound) bound = xb;
     }
+    // the search stays where every level's Horner sums are finite: |x| <= 2^e with
+    // 2^(e n) * 2^26 * amax < 2^1000 (the derivatives' factorial factors are below 2^22, 11 terms below
+    // 2^4), a power of two so host and device agree; roots beyond it (E ~ the third basis matrix
+    // alone, far outside any image) are not searched
+    {
+        int ea;
+        frexp(amax, &ea);
+        const int e = (1000 - 26 - ea) / n;
+        const double cap = ldexp(1.0, e < 1000 ? e : 1000);
+        bound = bound < cap ? bound : cap;
+    }
     int nr = 0;
     VS_UNROLL
     for (int m = 9; m >= 0; m--) {
@@ -175,15 +205,26 @@ VS_HD inline int poly_real_roots(const double* c, double* W, int wst) {
             double fa, fb0;
             VS_EM_EV(a, fa);
             VS_EM_EV(b, fb0);
-            if (fa == 0) {
+            // a cut (a root of the derivative, refined to kCutTol only) at which this level's value is
+            // within rounding noise of zero is a (near-)double root: the two roots lie within the
+            // noise of the cut, so a sign test on either side can miss both; the cut is taken as the
+            // root instead (an exact double root has no sign change at all)
+            bool at_root = fa == 0;
+            if (!at_root && i > 0) {
+                double s = fabs(D[10 - m]);
+                const double ax = fabs(a);
+                VS_UNROLL
+                for (int k = 9 - m; k >= 0; k--) s = s * ax + fabs(D[k]);
+                at_root = fabs(fa) <= 0x1p-48 * s;
+            }
+            if (at_root) {
                 if (cnt == 0 || WS(kWsN + cnt - 1) != a) WS(kWsN + cnt++) = a;
                 continue;
             }
             if ((fa < 0) == (fb0 < 0)) continue;
             // safeguarded Newton (rtsafe): a Newton step when it stays inside the bracket and at
             // least halves the step before last, else bisection; the bracket keeps the sign change
-            double x = (a > 0 && b > 16.0 * a) || (b < 0 && a < 16.0 * b) ? (a > 0 ? 1.0 : -1.0) * sqrt(a * b)
-                                                                           : 0.5 * (a + b);
+            double x = wide_bracket(a, b) ? split_point(a, b) : 0.5 * (a + b);
             double dxold = b - a, dx = dxold, root = x;
             for (int it = 0; it < 100; it++) {
                 double f = D[10 - m], df = 0.0;  // value and derivative (Horner pair)
@@ -200,8 +241,8 @@ VS_HD inline int poly_real_roots(const double* c, double* W, int wst) {
                     b = x;
                 double mid = 0.5 * (a + b);
                 if (mid <= a || mid >= b) break;  // the bracket is at adjacent doubles
-                // a bracket spanning orders of magnitude on one side of 0 is split geometrically
-                if ((a > 0 && b > 16.0 * a) || (b < 0 && a < 16.0 * b)) mid = (a > 0 ? 1.0 : -1.0) * sqrt(a * b);
+                // a bracket spanning orders of magnitude is split geometrically (or at 0)
+                if (wide_bracket(a, b)) mid = split_point(a, b);
                 const double xn = df != 0 ? x - f / df : mid;
                 if (!(xn > a && xn < b) || fabs(2.0 * f) > fabs(dxold * df)) {
                     dxold = dx;

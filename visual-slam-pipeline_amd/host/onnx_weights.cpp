@@ -344,6 +344,14 @@ bool parse_attribute(Span s, Node& n, std::map<std::string, Tensor>& tensors, st
     else if (name == "dilations") {
         for (int64_t d : ints)
             if (d != 1) return err = "dilated convolutions are not part of these networks", false;
+    } else if (name == "value_float" && n.op == "Constant") {  // a scalar Constant (opset >= 12)
+        Tensor t;
+        t.dtype = DT_FLOAT, t.data = {fv};
+        if (!n.out.empty()) tensors[n.out[0]] = std::move(t);
+    } else if (name == "value_int" && n.op == "Constant") {
+        Tensor t;
+        t.dtype = DT_INT64, t.ints = {i};
+        if (!n.out.empty()) tensors[n.out[0]] = std::move(t);
     } else if (name == "value" && has_t && n.op == "Constant") {
         Tensor t;
         std::string tn;
@@ -645,8 +653,13 @@ bool is_channel_norm_of(const Model& m, const std::map<std::string, int>& produc
             if (sq.op == "Pow" && sq.in.size() == 2 && strip_alias(m, producer, sq.in[0]) == x) {
                 // the exponent must be the scalar float constant 2 (any other exponent is
                 // not an L2 norm, and the graph is then refused)
-                auto e = m.float_scalars.find(strip_alias(m, producer, sq.in[1]));
-                return e != m.float_scalars.end() && e->second == 2.0f;
+                // (a float scalar, or — ADVICE r05 — a one-element INT32 / INT64 constant, from an
+                // initializer or a Constant node's value / value_float / value_int)
+                const std::string en = strip_alias(m, producer, sq.in[1]);
+                auto e = m.float_scalars.find(en);
+                if (e != m.float_scalars.end()) return e->second == 2.0f;
+                auto ei = m.int_consts.find(en);
+                return ei != m.int_consts.end() && ei->second.size() == 1 && ei->second[0] == 2;
             }
             return false;
         } else {
