@@ -9,11 +9,15 @@ RGB-D frame goes through
                                  scale fallback, EKF, local-map tracking, PnP refinement, keyframes
                                  with triangulation / depth points / culling, the visibility sweep,
                                  periodic PnP)
-through vs_slam_process_batch_dev (host/tracker.hpp over the HIP kernels), frames resident in HBM.
-Tracking is sequential within a sequence ("replicas only"): with --gpus N each rank
-tracks its own sequence (its own start on the closed-loop synthetic path) and value is the frames/s
-summed over ranks (weak scaling).  The run ends with the RTS smoother and the reference's ATE
-(main.cpp:258-332) against the synthetic ground truth.
+through vs_slam_process_batch_dev (host/tracker.hpp over the HIP kernels), frames resident in HBM
+(the PCIe upload a host-buffer caller adds is measured separately: input_upload).  The input is the
+non-repeating Pioneer-like drive of synth.pioneer_trajectory (headline_plan: 928 processed frames at
+the driver's --steps 20 --warmup 5, timed frames 160-799), the drive tests/test_gpu_headline_drive.py
+pins bit for bit against the oracle tracker.  Tracking is sequential within a sequence ("replicas
+only"): with --gpus N every rank tracks the SAME drive independently and value is the
+frames/s summed over ranks (weak scaling) — a 1 -> N curve of it is linear by construction;
+frontend_batch is the frame-batched (sharded, RCCL) scaling figure.  The run ends with the RTS
+smoother and the reference's ATE (main.cpp:258-332) against the synthetic ground truth.
 
 frontend_batch — BASELINE config[3], offline batch through the C ABI (vs_batch_submit_dev /
 vs_batch_collect, csrc/batch.hip, two steps in flight): each rank extracts its block of B = 318 frames
@@ -95,12 +99,16 @@ if WINO:
         "head_a": 2 * 16 * 30 * 40 * 512 * 128,
     })
 
-# Round 5: the layers with at least 64 workgroups of 16 x 16 pixels per frame run Winograd F(4x4, 3x3)
-# (wino4.hip k_wino4: 36 products per 4 x 4 output tile, input and output channel, 2.25 per pixel
-# against F(2x2)'s 4); the tiles the kernel computes include the padding of its 16 x 16-pixel workgroups
-# (120 x 160: 8 x 10 workgroups; 60 x 80: 4 x 5).  conv4a / conv4b (40 workgroups per frame) stay on F(2x2).
+# Round 5: the layers with at least VS_WINO4_MIN_WG (default 32) workgroups of 16 x 16 pixels x 64
+# output channels per frame run Winograd F(4x4, 3x3) (wino4.hip k_wino4: 36 products per 4 x 4 output
+# tile, input and output channel, 2.25 per pixel against F(2x2)'s 4) — every 3x3 layer at 640 x 480,
+# conv4a / conv4b (4 x 5 workgroups x 2 channel blocks = 40) included (sp_net.hip:1271-1275); the tiles
+# the kernel computes include the padding of its 16 x 16-pixel workgroups (120 x 160: 8 x 10
+# workgroups; 60 x 80: 4 x 5).
 WINO4 = WINO and os.environ.get("VS_WINO4", "1") != "0"
-WINO4_LAYERS = ("conv1_fused", "conv2a", "conv2b_pool", "conv3a", "conv3b_pool", "head_a")
+WINO4_MIN_WG = int(os.environ.get("VS_WINO4_MIN_WG", "32"))
+WINO4_LAYERS = ("conv1_fused", "conv2a", "conv2b_pool", "conv3a", "conv3b_pool", "head_a") + (
+    ("conv4a", "conv4b") if WINO4_MIN_WG <= 40 else ())
 if WINO4:
     MFMA_FLOPS.update({
         "conv1_fused": 2 * 36 * 120 * 160 * 64 * 64,
@@ -110,6 +118,8 @@ if WINO4:
         "conv3b_pool": 2 * 36 * 32 * 40 * 128 * 128,
         "head_a": 2 * 36 * 16 * 20 * 512 * 128,
     })
+    if "conv4a" in WINO4_LAYERS:
+        MFMA_FLOPS.update({"conv4a": 2 * 36 * 16 * 20 * 128 * 128, "conv4b": 2 * 36 * 16 * 20 * 128 * 128})
 
 # profiling stage -> symbol prefix (as rocprofv3 reports it) of that stage's dominant kernel; the
 # template argument list continues after the prefix (e.g. the chunk width: "<true, 1, true, false, 4>")
@@ -144,6 +154,8 @@ STAGE_KERNEL_WINO4 = {
     "conv3b_pool": "vs::k_wino4<true, false",
     "head_a": "vs::k_wino4<false, false",
 }
+if "conv4a" in WINO4_LAYERS:
+    STAGE_KERNEL_WINO4.update({"conv4a": "vs::k_wino4<false, false", "conv4b": "vs::k_wino4<false, false"})
 
 STAGE_KERNEL_DIRECT = dict(STAGE_KERNEL)
 if WINO:
@@ -171,6 +183,34 @@ def pmc_traffic(prefix):
         if kernel_matches(name, prefix) and fpl:
             return k["hbm_bytes_per_launch"] / fpl, doc.get("tag"), fpl
     return None, None, None
+
+
+def headline_plan(B, warmup, steps, profile_steps):
+    """The headline drive and its step schedule: (n_path, [(k0, k1), ...]) — the processed frames of
+    synth.pioneer_trajectory(n_path) and the step ranges run_tracker_steps takes in order: warm-up,
+    the timed steps, the extra stage-profiled steps (each range prefetches only inside itself).
+    n_path >= the reference sequence's 848 processed frames and >= every frame the schedule tracks."""
+    n_path = max(PIONEER_FRAMES, B * (warmup + steps + profile_steps))
+    ranges = [(0, warmup), (warmup, warmup + steps)]
+    if profile_steps > 0:
+        ranges.append((warmup + steps, warmup + steps + profile_steps))
+    return n_path, ranges
+
+
+def run_tracker_steps(slam, bgr, dep, hdep, B, k0, k1):
+    """Steps k0..k1-1 of the headline through vs_slam_process_batch_dev: step k = processed frames
+    kB..kB+B-1 (device frames bgr[kB], depth dep[kB]; host depth hdep; TUM-like timestamps, FRAME_STEP
+    3 ids).  Each batch's extraction is prefetched behind the previous one's (vs_slam_prefetch_batch_dev),
+    never across the range's end.  Returns the per-frame process_frame results."""
+    out = []
+    for k in range(k0, k1):
+        if k + 1 < k1:
+            i1 = (k + 1) * B
+            slam.prefetch_batch_dev(B, bgr[i1].data_ptr(), dep[i1].data_ptr())
+        g0 = k * B
+        out += list(slam.process_batch_dev(B, bgr[g0].data_ptr(), dep[g0].data_ptr(), hdep[g0:g0 + B],
+                                           [T0 + 0.1 * (g0 + j) for j in range(B)], [3 * (g0 + j) for j in range(B)]))
+    return out
 
 
 def launch_plan(gpus, environ, argv):
@@ -226,7 +266,7 @@ def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--warmup", type=int, default=5, help="untimed steps (5: the driver's own command)")
     ap.add_argument("--batch", type=int, default=32, help="frames per GPU per step")
     ap.add_argument("--cpu-frames", type=int, default=24, help="cpu_baseline sample size (processed frames)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -636,7 +676,8 @@ def main():
     # and the ranks all-gather them (replicas: every GPU tracks the same drive).  The closed loop
     # (synth.loop_sequence) stays the input of the config[3] batch front end.
     workers = args.render_workers or max(1, min(16, (os.cpu_count() or 1) // max(world, 1)))
-    n_path = max(PIONEER_FRAMES, B * (args.warmup + args.steps + args.track_profile_steps))
+    n_path, ranges = headline_plan(B, args.warmup, args.steps,
+                                   args.track_profile_steps if args.stage_profile != "all" else 0)
     poses = synth.pioneer_trajectory(n_path)
     mine = list(range(rank, n_path, world))
     pb, pd = synth.render_frames(poses, mine, workers=workers)
@@ -670,23 +711,15 @@ def main():
     dense = vslam_abi.Dense(ctx)  # main.cpp:1116-1139: every processed frame fused into the dense cloud
     slam.attach_dense(dense)
 
-    def step(k):
-        g0 = k * B
-        return slam.process_batch_dev(B, bgr[g0].data_ptr(), dep[g0].data_ptr(), hdep[g0:g0 + B],
-                                      [T0 + 0.1 * (g0 + j) for j in range(B)], [3 * (g0 + j) for j in range(B)])
-
     progress(f"sequence rendered, tracker ready; {args.warmup} warmup steps")
+
     def run_steps(k0, k1):
-        # each batch's extraction is prefetched behind the previous batch's (vs_slam_prefetch_batch_dev),
-        # never across the warmup / timed boundary: every timed batch is extracted inside the timed region
-        for k in range(k0, k1):
-            if k + 1 < k1:
-                i1 = (k + 1) * B
-                slam.prefetch_batch_dev(B, bgr[i1].data_ptr(), dep[i1].data_ptr())
-            step(k)
+        # never prefetched across the warmup / timed boundary: every timed batch is extracted inside
+        # the timed region
+        run_tracker_steps(slam, bgr, dep, hdep, B, k0, k1)
 
     torch.cuda.synchronize()
-    run_steps(0, args.warmup)
+    run_steps(*ranges[0])
     torch.cuda.synchronize()
     ctx.tie_stats(reset=True)
     # headline: per-stage events on the extraction stages only (the roofline kernel); the tracking
@@ -698,7 +731,7 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    run_steps(args.warmup, args.warmup + args.steps)
+    run_steps(*ranges[1])
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -717,15 +750,43 @@ def main():
     # per-stage times of the tracking stages: a few more steps with every stage's events on (kept
     # out of the timed region; the tracker and the ATE below include these frames)
     prof_trk, frames_trk = prof, frames_timed
-    if args.stage_profile != "all" and args.track_profile_steps > 0:
-        k0 = args.warmup + args.steps
+    if len(ranges) > 2:
         ctx.profile(True)
         ctx.profile_reset()
-        run_steps(k0, k0 + args.track_profile_steps)
+        run_steps(*ranges[2])
         torch.cuda.synchronize()
         prof_trk = ctx.profile_read()
         ctx.profile(False)
         frames_trk = B * args.track_profile_steps
+
+    # the PCIe leg a host-buffer caller adds (the reference hands process_frame a host cv::Mat,
+    # Frame.cpp:25-29): one batch of BGR + depth from pinned host memory into HBM, timed alone — the
+    # headline keeps the frames resident (the boundary takes device pointers)
+    upload = None
+    if B > 0:
+        hb = torch.empty(tuple(bgr[:B].shape), dtype=torch.uint8, pin_memory=True)
+        hd = torch.empty(tuple(dep[:B].shape), dtype=torch.float32, pin_memory=True)
+        hb.copy_(bgr[:B].cpu())
+        hd.copy_(dep[:B].cpu())
+        db, dd = torch.empty_like(bgr[:B]), torch.empty_like(dep[:B])
+        db.copy_(hb, non_blocking=True)
+        dd.copy_(hd, non_blocking=True)
+        torch.cuda.synchronize()
+        reps = 5
+        tu = time.perf_counter()
+        for _ in range(reps):
+            db.copy_(hb, non_blocking=True)
+            dd.copy_(hd, non_blocking=True)
+        torch.cuda.synchronize()
+        up_s = (time.perf_counter() - tu) / (reps * B)
+        nbytes = (hb.numel() + hd.numel() * 4) // B
+        upload = {"what": "H2D copy of one batch's BGR + depth (pinned host -> HBM), alone; excluded from value",
+                  "bytes_per_frame": int(nbytes), "ms_per_frame": round(up_s * 1e3, 4),
+                  "GB_per_s": round(nbytes / up_s / 1e9, 2),
+                  "serialised_frames_per_s": round(world / (elapsed / frames_timed + up_s), 3),
+                  "note": "serialised = the upload added to every frame's time on its rank with no overlap (an "
+                          "upper bound of the cost: a caller can copy the next batch while this one tracks)"}
+        del hb, hd, db, dd
 
     # trajectory quality: RTS smoother, then the reference's ATE against the synthetic ground truth
     slam.finish()
@@ -856,10 +917,18 @@ def main():
                             "reference sequence's 848 processed frames or more; every tracked frame distinct)",
                 "path_frames": n_path,
                 "timed_frames_distinct": frames_timed,
+                "timed_frames": [ranges[1][0] * B, ranges[1][1] * B - 1],
+                "parity": "tests/test_gpu_headline_drive.py: this drive and schedule (headline_plan, "
+                          "run_tracker_steps) == the oracle tracker bit for bit, and its op log replayed "
+                          "through the independent glue restatement (tests/slam_glue_ref.py)",
                 "frames_per_gpu_per_step": B,
                 "resolution": "640x480",
                 "max_keypoints": 400,
-                "parallelism": f"replicas x{world} (one sequence per GPU; tracking is sequential within one)",
+                "parallelism": f"replicas x{world} (the same drive on every GPU; tracking is sequential within one: "
+                               "a 1 -> N curve of value is linear by construction, frontend_batch is the "
+                               "frame-batched scaling figure)",
+                "input": "frames resident in HBM before the timed region (device-pointer boundary); the PCIe "
+                         "leg of a host-buffer caller: input_upload",
             },
             "ate_rmse_m": round(float(ate_t.item()), 4),
             "ate": {"rank0_rmse_m": round(a["ate_rmse"], 4), "scale": round(a["scale"], 4), "frames": a["n"],
@@ -872,6 +941,7 @@ def main():
                             "tools/analyze_bench_trajectory.py); with realistic noise (up to 75 % wrong matches "
                             "without a common motion, 0.7 px, 3 % depth dropouts) the same tracker holds 5-7 mm "
                             "(tests/test_tracker_noisy.py: 58 % wrong over 300 frames, 36 % over 848)"},
+            "input_upload": upload,
             "tracker_stats": stats,
             "map_points": stats.get("map_points"), "keyframes": stats.get("keyframes"),
             "nms_ties": dict(ties, note="per timed frame (vs_nms_tie_stats): window / cut ties can change the keypoint "

@@ -118,10 +118,11 @@ class NoisySequence:
         self.sal = rng.uniform(0.0, 1.0, len(self.P))
         self.seed, self.shuffle, self.px, self.dn, self.dropout, self.cap = seed, shuffle, px, desc_noise, dropout, cap
 
-    def frame(self, g):
+    def frame(self, g, key=None):
+        """key: the noise draw (default g): a held camera re-observes rendered frame g with fresh noise."""
         U = len(self.fr)
         f = self.fr[g % U]
-        rng = np.random.default_rng((self.seed, g))
+        rng = np.random.default_rng((self.seed, g if key is None else key))
         idx, u, v = visible(f, self.P)
         score = self.sal[idx] * (1.0 + rng.normal(0, 0.1, len(idx)))
         idx = idx[np.argsort(-score, kind="stable")[:self.cap]]

@@ -17,10 +17,16 @@ triangulation, the 3D-2D correspondences of every PnP (the map positions, float3
 casts them), the map rows appended.  After each frame it compares the glue's outcome (return value,
 keyframe flag, pose, map size and valid points, frame / keyframe counts, match count) with its own.
 
+Round 6 adds the two branches the first version raised on: the accelerometer paths
+(Slam::set_accelerometer_data / compute_gravity_direction :1580-1616, is_frame_stationary :1621-1651,
+process_stationary_frame :618-694, the post-stationary transition :916-951, the EKF height update
+:1720-1744) and loop closure (LoopCloser::detect LoopCloser.cpp:16-100 on the logged per-candidate
+match / E-RANSAC counts, Slam::handle_loop_closure :730-798 with its PnP verification and PGO
+constraint).  The restatement picks the candidates, the stationary frames, the gravity axis and the
+loop itself; the log only supplies kernel outputs.
+
 Deviation kept by both: after a rejected first frame `last_keyframe_` is null and the
 reference would dereference it at Slam.cpp:1063; the proactive-keyframe check is skipped then.
-Not restated (raise if reached): the accelerometer paths (stationary frames, height prior) and loop
-closure (every 200th keyframe) — the replayed sequences have neither.
 """
 import json
 
@@ -37,6 +43,8 @@ PNP_RECOVERY_MAX_JUMP, PNP_RECOVERY_BLEND_CLOSE, PNP_RECOVERY_BLEND_FAR = 1.5, 0
 PNP_REFINE_MAX_JUMP, PNP_PERIODIC_MAX_JUMP, PNP_PERIODIC_BLEND = 1.0, 1.5, 0.5
 KF_MIN_FRAME_GAP, KF_MIN_MATCHES = 10, 50
 LC_CHECK_INTERVAL = 200
+LC_MIN_FRAME_GAP, LC_MIN_INLIERS, LC_MAX_JUMP, LC_MIN_JUMP, LC_NEARBY_FRAME_RANGE = 200, 30, 0.5, 0.01, 30
+PGO_LC_TRANS_SIGMA, PGO_LC_ROT_SIGMA, EKF_SIGMA_HEIGHT = 0.03, 0.01, 0.01
 L2_RATIO_THRESHOLD, FLANN_RATIO_THRESHOLD = 0.75, 0.7
 TRACK_VISIBILITY_RADIUS = 8.0
 CULL_FOUND_RATIO_YOUNG, CULL_FOUND_RATIO_OLD = np.float32(0.15), np.float32(0.30)
@@ -185,6 +193,178 @@ class GlueRef:
                            pnp_refined=0, periodic_pnp=0, triangulated=0, depth_points=0, ekf_gated=0,
                            ekf_clamped=0, proactive_kf=0, regular_kf=0, culled=0, cull_rounds=0)
         self.ops = None
+        # accelerometer (Slam.cpp:1580-1651) and loop closure (:730-798) state
+        self.accel = None          # [n, 4] timestamp, ax, ay, az
+        self.gravity = None
+        self.initial_height = 0.0
+        self.has_initial_height = False
+        self.was_stationary = False
+        self.loop_edges, self.loop_constraints, self.loop_count = [], [], 0
+        self.counts.update(stationary=0, chains_recomputed=0, loops_detected=0, loop_constraints=0)
+
+    # ---- Slam.cpp:35-38, 1580-1616 ---------------------------------------------------------------
+    def set_initial_pose(self, R, t):
+        self.R_world = np.array(R, np.float64).reshape(3, 3).copy()
+        self.t_world = np.array(t, np.float64).reshape(3).copy()
+
+    def set_accelerometer(self, samples):
+        """Slam::set_accelerometer_data, then compute_gravity_direction (main.cpp:1066 calls it once)."""
+        self.accel = np.array(samples, np.float64).reshape(-1, 4)
+        if len(self.accel) == 0:
+            return
+        n = len(self.accel)
+        ax, ay, az = (float(sum(self.accel[:, k].tolist())) for k in (1, 2, 3))  # sequential sums
+        g = self.R_world @ np.array([ax / n, ay / n, az / n])
+        nrm = float(np.sqrt(g[0] * g[0] + g[1] * g[1] + g[2] * g[2]))
+        if nrm > 1e-6:
+            g = g / nrm
+        axis = int(np.argmax(np.abs(g)))  # first maximum, as the strict > of :1603-1606
+        self.gravity = np.zeros(3)
+        self.gravity[axis] = 1.0 if g[axis] > 0 else -1.0
+        t = self.t_world
+        self.initial_height = t[0] * self.gravity[0] + t[1] * self.gravity[1] + t[2] * self.gravity[2]
+        self.has_initial_height = True
+
+    # ---- Slam.cpp:1621-1651 ------------------------------------------------------------------
+    def is_frame_stationary(self, ts):
+        if self.accel is None or len(self.accel) == 0:
+            return False
+        window, thr = 0.1, 0.15
+        tt = self.accel[:, 0]
+        lo, hi = 0, len(tt) - 1
+        while lo < hi:  # the reference's search: lo stops at the last sample when all are earlier
+            mid = (lo + hi) // 2
+            if tt[mid] < ts - window:
+                lo = mid + 1
+            else:
+                hi = mid
+        mags = []
+        i = lo
+        while i < len(tt) and tt[i] <= ts + window:
+            a = self.accel[i]
+            mags.append(float(np.sqrt(a[1] * a[1] + a[2] * a[2] + a[3] * a[3])))
+            i += 1
+        if len(mags) < 5:
+            return False
+        mean = 0.0
+        for m in mags:
+            mean += m
+        mean /= len(mags)
+        var = 0.0
+        for m in mags:
+            var += (m - mean) * (m - mean)
+        var /= len(mags)
+        return float(np.sqrt(var)) < thr
+
+    # ---- Slam.cpp:618-694 --------------------------------------------------------------------
+    def process_stationary_frame(self, f, kept):
+        if not self.is_frame_stationary(f.ts) or self.frame_count <= 5:
+            return False
+        f.R, f.t = self.R_world.copy(), self.t_world.copy()
+        self.frames.append(f)
+        tracked = self._track_local_map(f)
+        if tracked >= 10:
+            obj, img = self._correspondences(f)
+            r = self.solve_pnp(obj, img, 100, 10)
+            if r is not None:
+                self.R_world = r[0].copy()
+                f.R, f.t = self.R_world.copy(), self.t_world.copy()
+        if self.last_keyframe is not None:
+            R_diff = self.R_world.T @ self.last_keyframe.R
+            if float(np.linalg.norm(rodrigues_vec(R_diff))) > 0.25:
+                f.kf = True
+                self.keyframe_count += 1
+                self.create_points_from_depth(f)
+                self.last_keyframe = f
+        self.last_frame = f
+        self.last_match_count = len(kept)
+        self.frame_count += 1
+        self.was_stationary = True
+        self.last_translation = np.zeros(3)
+        if self.ekf_init:
+            self.ekf_x[3:] = 0
+            self.ekf_x[:3] = self.t_world
+            for i in range(3, 6):
+                self.ekf_P[i, :] = 0
+                self.ekf_P[:, i] = 0
+                self.ekf_P[i, i] = 1e-4
+        self.last_frame_time = f.ts
+        self.counts["stationary"] += 1
+        return True
+
+    # ---- Slam.cpp:1720-1744 ------------------------------------------------------------------
+    def ekf_update_height(self, h_target, sigma_h):
+        if not self.ekf_init or self.gravity is None:
+            return
+        H = np.zeros((1, 6))
+        H[0, :3] = self.gravity
+        Rh = np.array([[sigma_h * sigma_h]])
+        h_pred = 0.0
+        for i in range(3):
+            h_pred += self.gravity[i] * self.ekf_x[i]
+        y = np.array([h_target - h_pred])
+        S = H @ self.ekf_P @ H.T + Rh
+        Kg = self.ekf_P @ H.T @ np.linalg.inv(S)
+        self.ekf_x = self.ekf_x + Kg @ y
+        IKH = np.eye(6) - Kg @ H
+        self.ekf_P = IKH @ self.ekf_P @ IKH.T + Kg @ Rh @ Kg.T
+
+    # ---- LoopCloser.cpp:16-100 + Slam.cpp:730-798 ----------------------------------------------
+    def handle_loop_closure(self, f):
+        if f.n == 0:
+            return
+        kfs = [g for g in self.frames if g.kf]  # Map::get_keyframes: add order
+        if len(kfs) < 2:
+            return
+        cand, checked = [], 0
+        for kf in kfs:
+            if f.id - kf.id < LC_MIN_FRAME_GAP or kf.n == 0:
+                continue
+            checked += 1
+            if checked % 5 != 0:
+                continue
+            cand.append(kf)
+        if not cand:
+            return
+        rec = self.ops.take("loop_eval", cur=f.id)
+        if rec["kfs"] != [kf.id for kf in cand]:
+            raise GlueMismatch(f"frame {f.id}: loop candidates {rec['kfs']}, mine {[kf.id for kf in cand]}")
+        for kf, ng in zip(cand, rec["n_good"]):  # knnMatch(current, keyframe) + ratio 0.75 (:51-64)
+            m = self.ops.take("match", a=f.id, b=kf.id)
+            if len(m["good"]) != ng or float.fromhex(m["ratio"]) != np.float32(L2_RATIO_THRESHOLD):
+                raise GlueMismatch(f"frame {f.id}: loop candidate {kf.id} matched {len(m['good'])}, evaluated {ng}")
+        best, best_inl = None, 0
+        for kf, ng, inl in zip(cand, rec["n_good"], rec["inliers"]):
+            if ng < MIN_MATCHES or inl < LC_MIN_INLIERS:
+                continue
+            if inl > best_inl:
+                best, best_inl = kf, inl
+        if best is None or best_inl < LC_MIN_INLIERS:
+            return
+        self.loop_count += 1
+        self.counts["loops_detected"] += 1
+        self.loop_edges.append((best.id, f.id))
+        ids = [i for i in range(len(self.mp_pos))
+               if self.mp_valid[i] and any(abs(fid - best.id) < LC_NEARBY_FRAME_RANGE for fid, _ in self.mp_obs[i])]
+        obj = np.zeros((0, 3), np.float32)
+        img = np.zeros((0, 2), np.float32)
+        if len(ids) >= 20 and f.n > 0:
+            mm = self.ops.take("match_map", fid=f.id)
+            if mm["ids"] != ids or float.fromhex(mm["ratio"]) != np.float32(FLANN_RATIO_THRESHOLD):
+                raise GlueMismatch(f"frame {f.id}: loop verification matched against other map points")
+            obj = np.array([self.mp_pos[ids[t]] for _, t in mm["pairs"]], np.float64).astype(np.float32).reshape(-1, 3)
+            img = np.array([(f.kx[q], f.ky[q]) for q, _ in mm["pairs"]], np.float32).reshape(-1, 2)
+        r = self.solve_pnp(obj, img, 300, 15)
+        if r is None:
+            return
+        R_p, t_p, _ = r
+        jump = float(np.linalg.norm(t_p - self.t_world))
+        if jump >= LC_MAX_JUMP or jump <= LC_MIN_JUMP:
+            return
+        Rft = best.R.T
+        self.loop_constraints.append((best.id, f.id, Rft @ R_p, Rft @ (t_p - best.t), PGO_LC_TRANS_SIGMA,
+                                      PGO_LC_ROT_SIGMA))
+        self.counts["loop_constraints"] += 1
 
     # ---- map ---------------------------------------------------------------------------------
     def _add_point(self, pt, src, row, obs):
@@ -451,29 +631,44 @@ class GlueRef:
             return False
         return match_count >= KF_MIN_MATCHES
 
-    # ---- Slam.cpp:1089-1108 ------------------------------------------------------------------
+    # ---- Slam.cpp:1089-1108 (vectorised over the map; the same per-point expressions) ----------
+    def _project_all(self, R, t):
+        P = np.array(self.mp_pos, np.float64).reshape(-1, 3)
+        Rc = R.T
+        tc = -Rc @ t
+        x, y, z = P[:, 0], P[:, 1], P[:, 2]
+        pc = [Rc[i, 0] * x + Rc[i, 1] * y + Rc[i, 2] * z + tc[i] for i in range(3)]
+        with np.errstate(divide="ignore", invalid="ignore"):
+            u = FX * pc[0] / pc[2] + CX
+            v = FY * pc[1] / pc[2] + CY
+        behind = pc[2] < 1e-6
+        u[behind] = -1.0
+        v[behind] = -1.0
+        return u, v
+
     def visibility(self, f):
         rec = self.ops.take("vis", fid=f.id)
-        flags = rec["flags"]
+        flags = np.array(rec["flags"], np.int64)
         if len(flags) != len(self.mp_pos):
             raise GlueMismatch(f"frame {f.id}: visibility over {len(flags)} map points, mine {len(self.mp_pos)}")
         rr = TRACK_VISIBILITY_RADIUS * TRACK_VISIBILITY_RADIUS
         kx, ky = f.kx.astype(np.float64), f.ky.astype(np.float64)
-        for i in range(len(self.mp_pos)):
-            if not self.mp_valid[i]:
-                mine = 0
-            else:
-                u, v = project_point(self.mp_pos[i], self.R_world, self.t_world)
-                mine = 0
-                if 0 <= u < IMAGE_WIDTH and 0 <= v < IMAGE_HEIGHT:
-                    mine = 1
-                    self.mp_visible[i] += 1
-                    d2 = (u - kx) ** 2 + (v - ky) ** 2
-                    if np.any(d2 < rr):
-                        mine = 3
-                        self.mp_found[i] += 1
-            if mine != flags[i]:
-                raise GlueMismatch(f"frame {f.id}: map point {i} visibility {flags[i]} vs mine {mine}")
+        u, v = self._project_all(self.R_world, self.t_world)
+        valid = np.array(self.mp_valid, bool)
+        inimg = valid & (u >= 0) & (u < IMAGE_WIDTH) & (v >= 0) & (v < IMAGE_HEIGHT)
+        found = np.zeros(len(u), bool)
+        idx = np.nonzero(inimg)[0]
+        for c0 in range(0, len(idx), 4096):
+            j = idx[c0:c0 + 4096]
+            d2 = (u[j, None] - kx[None, :]) ** 2 + (v[j, None] - ky[None, :]) ** 2
+            found[j] = np.any(d2 < rr, axis=1)
+        mine = np.where(found, 3, np.where(inimg, 1, 0))
+        self.mp_visible = (np.array(self.mp_visible, np.int64) + inimg).tolist()
+        self.mp_found = (np.array(self.mp_found, np.int64) + found).tolist()
+        bad = np.nonzero(mine != flags)[0]
+        if len(bad):
+            i = int(bad[0])
+            raise GlueMismatch(f"frame {f.id}: map point {i} visibility {flags[i]} vs mine {mine[i]}")
 
     def cull(self):
         self.counts["cull_rounds"] += 1
@@ -482,16 +677,32 @@ class GlueRef:
         self.counts["culled"] += before - self._n_valid()
 
     def _cull(self):
-        for i in range(len(self.mp_pos)):
-            if not self.mp_valid[i]:
-                continue
-            age = self.keyframe_count - self.mp_first_kf[i]
-            ratio = (np.float32(self.mp_found[i]) / np.float32(self.mp_visible[i])
-                     if self.mp_visible[i] > 0 else np.float32(0))
-            if age >= 3 and self.mp_visible[i] > 0 and ratio < CULL_FOUND_RATIO_YOUNG:
-                self.mp_valid[i] = False
-            if age >= 5 and len(self.mp_obs[i]) <= 2 and ratio < CULL_FOUND_RATIO_OLD:
-                self.mp_valid[i] = False
+        valid = np.array(self.mp_valid, bool)
+        vis = np.array(self.mp_visible, np.int64)
+        fnd = np.array(self.mp_found, np.int64)
+        age = self.keyframe_count - np.array(self.mp_first_kf, np.int64)
+        nobs = np.array([len(o) for o in self.mp_obs], np.int64)
+        with np.errstate(divide="ignore", invalid="ignore"):
+            ratio = np.where(vis > 0, fnd.astype(np.float32) / vis.astype(np.float32), np.float32(0))
+        drop = valid & (((age >= 3) & (vis > 0) & (ratio < CULL_FOUND_RATIO_YOUNG)) |
+                        ((age >= 5) & (nobs <= 2) & (ratio < CULL_FOUND_RATIO_OLD)))
+        for i in np.nonzero(drop)[0]:
+            self.mp_valid[int(i)] = False
+
+    # ---- Slam.cpp:380-469 (the kernel's result from the log, at the pose the glue holds) ---------
+    def _track_local_map(self, f):
+        rec = self.ops.take("tlm", fid=f.id)
+        if not (np.allclose(_hex(rec["R"]), f.R.ravel(), rtol=0, atol=1e-9)
+                and np.allclose(_hex(rec["t"]), f.t, rtol=0, atol=1e-9)):
+            raise GlueMismatch(f"frame {f.id}: local-map tracking ran at another pose: "
+                               f"{_hex(rec['t'])} vs mine {f.t}")
+        if rec["nmp"] != len(self.mp_pos) or rec["nvalid"] != self._n_valid():
+            raise GlueMismatch(f"frame {f.id}: local map {rec['nmp']}/{rec['nvalid']} points, mine "
+                               f"{len(self.mp_pos)}/{self._n_valid()}")
+        f.mp_idx = np.array(rec["mp_idx"], np.int64)
+        for mp, kp in rec["obs"]:
+            self.mp_obs[mp].append((f.id, kp))
+        return rec["tracked"]
 
     # ---- Slam.cpp:809-1135 -------------------------------------------------------------------
     def process_frame(self, f):
@@ -552,16 +763,55 @@ class GlueRef:
         if r == -1:
             self.branch[f.id] = "recovery_failed"
             return False
-        # F verification (:880-910): the chain's kept list; stationary handling needs an accelerometer
+        # F verification (:880-910): the chain's kept list (the F inliers when F is non-empty)
+        kept = ch["kept"] if ch["f_ok"] else ch["good"]
+        if not ch["f_ok"] and ch["kept"] != ch["good"]:
+            raise GlueMismatch(f"frame {f.id}: F failed but the chain kept {len(ch['kept'])} of {len(ch['good'])}")
+        # stationary frame (:912-913)
+        if self.process_stationary_frame(f, kept):
+            self.branch[f.id] = "stationary"
+            return True
+        mot = ch
+        # post-stationary transition (:916-951): a new reference, matching and F verification again,
+        # then the motion of those points
+        if self.was_stationary and self.last_frame is not None:
+            self.was_stationary = False
+            lf = self.last_frame
+            if not lf.kf:
+                lf.kf = True
+                self.keyframe_count += 1
+                self.create_points_from_depth(lf)
+                self.last_keyframe = lf
+            ref = self.last_keyframe
+            good = self.ops.take("match", a=ref.id, b=f.id)["good"]
+            self.last_match_count = len(good)
+            p1 = np.array([(ref.kx[q], ref.ky[q]) for q, _ in good], np.float32).reshape(-1, 2)
+            p2 = np.array([(f.kx[t], f.ky[t]) for _, t in good], np.float32).reshape(-1, 2)
+            if len(good) >= 8:
+                fr = self.ops.take("ffund", n=len(good))
+                if not (np.array_equal(_hex(fr["p1"]).astype(np.float32), p1.ravel())
+                        and np.array_equal(_hex(fr["p2"]).astype(np.float32), p2.ravel())):
+                    raise GlueMismatch(f"frame {f.id}: post-stationary F ran on other points")
+                if fr["ok"]:
+                    keep = np.array(fr["mask"], bool)
+                    p1, p2 = p1[keep], p2[keep]
+            mot = self.ops.take("motion", a=ref.id, b=f.id)
+            if mot["seed"] != 42 + self.frame_count:
+                raise GlueMismatch(f"frame {f.id}: post-stationary motion seeded {mot['seed']}")
+            if not (np.array_equal(_hex(mot["p1"]).astype(np.float32), p1.ravel())
+                    and np.array_equal(_hex(mot["p2"]).astype(np.float32), p2.ravel())):
+                raise GlueMismatch(f"frame {f.id}: post-stationary motion on other points")
+            self.counts["chains_recomputed"] += 1
         # motion (:953-984)
         R_ref, t_ref = ref.R, ref.t
-        use_3d3d = bool(ch["ok3d"])
+        use_3d3d = bool(mot["ok3d"])
         if use_3d3d:
-            R_new = R_ref @ _hex(ch["R3"]).reshape(3, 3).T
-            t_new = t_ref - R_new @ _hex(ch["t3"])
+            R_new = R_ref @ _hex(mot["R3"]).reshape(3, 3).T
+            t_new = t_ref - R_new @ _hex(mot["t3"])
             self.counts["via_3d3d"] += 1
             self.branch[f.id] = "3d3d"
         else:
+            ch = mot
             if not ch["okE"]:
                 self.last_frame = f
                 self.counts["emat_failed"] += 1
@@ -586,6 +836,8 @@ class GlueRef:
         innovation = np.linalg.norm(t_new - self.ekf_x[:3])
         self.counts["ekf_gated"] += innovation >= EKF_INNOV_GATE
         self.ekf_update_visual(t_new, sigma if innovation < EKF_INNOV_GATE else innovation * 0.5)
+        if self.gravity is not None and self.has_initial_height:  # :1013-1016
+            self.ekf_update_height(self.initial_height, EKF_SIGMA_HEIGHT)
         ekf_pos = self.ekf_x[:3].copy()
         delta = ekf_pos - self.t_world
         step = np.linalg.norm(delta)
@@ -602,18 +854,7 @@ class GlueRef:
         f.R, f.t = self.R_world.copy(), self.t_world.copy()
         self.frames.append(f)
         # local-map tracking + PnP refinement (:1057-1059)
-        rec = self.ops.take("tlm", fid=f.id)
-        if not (np.allclose(_hex(rec["R"]), f.R.ravel(), rtol=0, atol=1e-9)
-                and np.allclose(_hex(rec["t"]), f.t, rtol=0, atol=1e-9)):
-            raise GlueMismatch(f"frame {f.id}: local-map tracking ran at another pose: "
-                               f"{_hex(rec['t'])} vs mine {f.t}")
-        if rec["nmp"] != len(self.mp_pos) or rec["nvalid"] != self._n_valid():
-            raise GlueMismatch(f"frame {f.id}: local map {rec['nmp']}/{rec['nvalid']} points, mine "
-                               f"{len(self.mp_pos)}/{self._n_valid()}")
-        f.mp_idx = np.array(rec["mp_idx"], np.int64)
-        for mp, kp in rec["obs"]:
-            self.mp_obs[mp].append((f.id, kp))
-        tracked = rec["tracked"]
+        tracked = self._track_local_map(f)
         self.refine_pose_via_local_pnp(f, tracked)
         # proactive keyframe (:1061-1070)
         if not f.kf and self.last_match_count < MIN_MATCHES * 2 and self.last_keyframe is not None:
@@ -632,7 +873,7 @@ class GlueRef:
             if self.keyframe_count % PNP_INTERVAL == 0:
                 self.run_pnp(f)
             if self.keyframe_count % LC_CHECK_INTERVAL == 0:
-                raise NotImplementedError("loop closure is not restated here")
+                self.handle_loop_closure(f)
             self.visibility(f)
             if self.keyframe_count % 3 == 0:
                 self.cull()

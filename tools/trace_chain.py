@@ -3,7 +3,8 @@
 
     python3 tools/trace_chain.py gpurun_out/prof_trace/trace_kernel_trace.csv
 
-The tracking queue is the one that runs ``k_tlm_grid``; a frame's chain starts at ``k_tlm_grid`` and ends at the
+The tracking queue is the one that runs ``k_tlm_resolve``; a frame's chain starts at ``k_tlm_grid`` (``k_tlm_cand``
+since round 6, the grid being built at extraction) and ends at the
 first copy after ``k_pnp_ransac`` (the packed result read back: a copy command, or ``k_copy_bytes`` into
 coherent host memory).  For the steady-state frames (the median over
 all chains) it prints every step's duration and the gap before it, the chain's span, the sum of its kernels, and the
@@ -86,9 +87,11 @@ def main(path):
         byq[r["Queue_Id"]].append(r)
     for q, rs in byq.items():
         names = {short(r["Kernel_Name"]) for r in rs}
-        if "k_tlm_grid" in names:
+        # round 6: the keypoint grid is built at extraction, so a chain starts at k_tlm_cand
+        first = "k_tlm_grid" if "k_tlm_grid" in names and "k_tlm_resolve" in names else "k_tlm_cand"
+        if "k_tlm_resolve" in names and first in names:
             summarize(f"tracking queue {q} (local-map tracking + speculative PnP)",
-                      [c for c in chains(rs, "k_tlm_grid", "k_pnp_ransac") if len(c) <= 12], None)
+                      [c for c in chains(rs, first, "k_pnp_ransac") if len(c) <= 12], None)
         if "k_fmat<true>" in names:
             summarize(f"speculative queue {q} (match -> F -> 3D-3D -> E)",
                       [c for c in chains(rs, "k_match<2, 2, 16, 16, 32, 1, 1, true, 0>", "k_emat<true>")
