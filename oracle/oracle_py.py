@@ -43,6 +43,7 @@ _SIG = {
     "orc_optimize_pose": (_I, [_P, _P, _I, _P, _P, _P, _P, _P, _P]),
     "orc_epnp": (_I, [_P, _P, _I, _P, _P, _P]),
     "orc_epnp_debug": (_I, [_P, _P, _P, _I, _P, _P]),
+    "orc_epnp_eig_stages": (_I, [_P, _P, _P, _I, _P, _P]),
     "orc_pnp_ransac": (_I, [_P, _P, _I, _P, _I, ctypes.c_double, ctypes.c_double, _P, _P, _P, _P, _P]),
     "orc_solve_pnp": (_I, [_P, _P, _I, _P, _I, _I, _P, _P, _P]),
     "orc_find_fundamental": (_I, [_P, _P, _I, ctypes.c_double, ctypes.c_double, _I, _P, _P, _P]),
@@ -585,6 +586,16 @@ class Slam:
         c = np.zeros((cap, 16))
         lib().orc_slam_loops(self.h, cap, _p(e), _p(c), ctypes.byref(ne))
         return e[:ne.value], c[:nc]
+
+
+def epnp_eig_stages(X, uv, m, K=(525.0, 525.0, 319.5, 239.5)):
+    """epnp_small_eig's stage results per problem (216 doubles, pnp_solvers.h dbg layout)."""
+    X = np.ascontiguousarray(X, np.float64)
+    uv = np.ascontiguousarray(uv, np.float64)
+    m = np.ascontiguousarray(m, np.int32)
+    out = np.zeros((len(m), 216))
+    lib().orc_epnp_eig_stages(_p(X), _p(uv), _p(m), len(m), _p(np.asarray(K, np.float64)), _p(out))
+    return out
 
 
 def epnp_debug(X, uv, m, K=(525.0, 525.0, 319.5, 239.5)):

@@ -84,6 +84,20 @@ extern "C" int orc_epnp(const double* X, const double* uv, int n, const double K
     return epnp<4096>(X, uv, n, cam, R, t) ? 1 : 0;
 }
 
+// the stage results of epnp_small_eig (216 doubles per problem, pnp_solvers.h dbg layout), as the
+// device's vs_debug_epnp_mode(3) dumps them
+extern "C" int orc_epnp_eig_stages(const double* X, const double* uv, const int* m, int count, const double K[4],
+                                   double* out) {
+    const Cam cam{K[0], K[1], K[2], K[3]};
+    for (int p = 0; p < count; p++) {
+        double* o = out + (size_t)p * 216;
+        for (int k = 0; k < 216; k++) o[k] = 0.0;
+        double cw[4][3], al[5][4], v[4][12];
+        if (m[p] >= 4 && m[p] <= 5 && epnp_control<5>(X + 15 * p, m[p], cw, al)) epnp_small_eig(al, uv + 10 * p, m[p], cam, v, o);
+    }
+    return 0;
+}
+
 // test hook mirroring the device's vs_debug_epnp (pnp.hip): per problem (v[4][12] of
 // epnp_small_eig, R[9], t[3], ok, rod_m2v(R)[3], rod_v2m of it[9]) for m = 4 / 5 points
 extern "C" int orc_epnp_debug(const double* X, const double* uv, const int* m, int count, const double K[4],

@@ -109,3 +109,67 @@ def test_batch_submit_collect_pipelined_equals_steps(vsctx, frames, pipeline_res
         e = r["eok"] == 1
         assert np.array_equal(r["eR"].reshape(B, 9)[e], p["eR"].reshape(B, 9)[e])
         assert np.array_equal(r["escale"][e], p["escale"][e])
+
+
+@pytest.fixture(scope="module")
+def drive_frames():
+    """Distinct frames of the headline's Pioneer-like drive (every pair a new view)."""
+    poses = synth.pioneer_trajectory(848)
+    return synth.render_frames(poses, list(range(2 * B)), workers=8)
+
+
+@pytest.mark.parametrize("mode", ["none", "ring", "gather"])
+def test_batch_step_equals_oracle(vsctx, oracle, drive_frames, mode):
+    """config[3]'s C ABI step against the CPU oracle directly (not through
+    DevicePipeline): for every pair (frame p - 1, frame p) of a step, the oracle's ratio matching
+    (Slam.cpp:1140-1172), F verification (:880-910), 3D-3D RANSAC with seed 42 + frame index (:214-375)
+    and, where it fails, the E-matrix motion + depth scale (:1193-1213, :73-207) on the same GPU
+    features: n_good, ok, eok exact; 3D-3D R, t <= 1e-12; E R, t, scale <= 1e-9.  Step 1's
+    pair 0 joins the previous step's last frame: the carry without a communicator, the one-rank RCCL
+    ring / all-gather with one."""
+    dev = torch.device("cuda", 0)
+    bgr, dep = drive_frames
+    feats = vsctx.extract_batch(list(bgr))
+    with_comm = mode != "none"
+    s = torch.cuda.current_stream().cuda_stream
+    out = []
+    with vslam_abi.Batch(vsctx, B, uid=vslam_abi.batch_unique_id() if with_comm else None) as bt:
+        if mode == "gather":
+            bt.set_gather(True)
+        for k in range(2):
+            fr = torch.from_numpy(bgr[k * B:(k + 1) * B]).to(dev)
+            de = torch.from_numpy(dep[k * B:(k + 1) * B]).to(dev)
+            halo = torch.from_numpy(dep[k * B - 1]).to(dev) if (with_comm and k > 0) else None
+            torch.cuda.synchronize()
+            out.append(bt.step_dev(fr.data_ptr(), de.data_ptr(), None if halo is None else halo.data_ptr(), k * B, s))
+    checked = n3 = nE = 0
+    for k in range(2):
+        r = out[k]
+        for p in range(B):
+            g = k * B + p
+            if g == 0:
+                continue  # no previous frame
+            (k0, d0), (k1, d1) = feats[g - 1], feats[g]
+            _, good = oracle.match_ratio(d0, d1)
+            assert r["n_good"][p] == len(good), (k, p)
+            _, keep, _, _ = oracle.fmat_verify(k0, k1, good)
+            kept = good[keep]
+            p1 = np.stack([k0["x"][kept["query_idx"]], k0["y"][kept["query_idx"]]], 1)
+            p2 = np.stack([k1["x"][kept["train_idx"]], k1["y"][kept["train_idx"]]], 1)
+            ok, R, t, _ = oracle.ransac_3d3d(p1, p2, dep[g - 1], dep[g], seed=42 + g)
+            assert bool(r["ok"][p]) == ok, (k, p)
+            if ok:
+                n3 += 1
+                assert np.abs(r["R"].reshape(B, 3, 3)[p] - R).max() <= 1e-12
+                assert np.abs(r["t"][p] - t).max() <= 1e-12
+            else:
+                eok, eR, et, _, _, _ = oracle.estimate_motion(p1, p2)
+                assert bool(r["eok"][p]) == eok, (k, p)
+                if eok:
+                    nE += 1
+                    sc = oracle.estimate_scale(p1, p2, eR, et, dep[g - 1], dep[g])
+                    assert np.abs(r["eR"].reshape(B, 3, 3)[p] - eR).max() <= 1e-9
+                    assert np.abs(r["et"][p] - et).max() <= 1e-9 and abs(r["escale"][p] - sc) <= 1e-9
+            checked += 1
+    print(mode, checked, "pairs:", n3, "3D-3D,", nE, "E")
+    assert checked == 2 * B - 1 and n3 >= B

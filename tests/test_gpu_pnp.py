@@ -107,3 +107,66 @@ def test_epnp_sequential_device_equals_host(vsctx, oracle):
     bad_p = np.nonzero(np.any(dev[:, 48:].view(np.uint64) != host[:, 48:].view(np.uint64), axis=1))[0]
     assert len(bad_v) == 0 and len(bad_p) == 0, (bad_v[:5], bad_p[:5], np.abs(dev - host).max())
     assert host[:, 60].sum() > 0.9 * count
+
+
+@pytest.mark.parametrize("mode", [1, 2])
+def test_epnp_out_of_line_device_equals_host(vsctx, oracle, mode):
+    """the sequential EPnP behind a noinline call (mode 1: one problem per lane; mode 2:
+    called by lane 0 of a wave alone, as k_pnp_ransac once did) gives the host's pose and Rodrigues round
+    trip bit for bit on the same 2,000 problems (the cause of the round-5 divergence)."""
+    import ctypes
+
+    import vslam_abi
+    lib = vslam_abi.load_library()
+    lib.vs_debug_epnp_mode.restype = ctypes.c_int
+    lib.vs_debug_epnp_mode.argtypes = [ctypes.c_void_p] * 3 + [ctypes.c_int] + [ctypes.c_void_p] * 2 + [ctypes.c_int]
+    rng = np.random.default_rng(9)
+    count = 2000
+    m = np.where(np.arange(count) % 5 == 0, 4, 5).astype(np.int32)
+    X = np.zeros((count, 15))
+    uv = np.zeros((count, 10))
+    for p in range(count):
+        obj, img, _, _, _ = pnp_problem(int(m[p]), 1000 + p, noise=0.5 if p % 2 else 0.0)
+        X[p, :3 * m[p]] = obj.astype(np.float64).ravel()
+        uv[p, :2 * m[p]] = img.astype(np.float64).ravel()
+    K = np.array([525.0, 525.0, 319.5, 239.5])
+    dev = np.zeros((count, 73))
+    assert lib.vs_debug_epnp_mode(X.ctypes.data, uv.ctypes.data, m.ctypes.data, count, K.ctypes.data,
+                                  dev.ctypes.data, mode) == 0
+    host = oracle.epnp_debug(X, uv, m, tuple(K))
+    bad = np.nonzero(np.any(dev[:, 48:].view(np.uint64) != host[:, 48:].view(np.uint64), axis=1))[0]
+    print("mode", mode, "differing problems:", len(bad), "max |d|", np.abs(dev[:, 48:] - host[:, 48:]).max())
+    assert len(bad) == 0, (bad[:5], np.abs(dev[:, 48:] - host[:, 48:]).max())
+
+
+def test_epnp_eig_stages_out_of_line(vsctx, oracle):
+    """Where the out-of-line divergence starts: epnp_small_eig called out of line on the device dumps its
+    stage results (QR, B = R R^T, the tridiagonal, the multisection brackets, the inverse iteration, v);
+    the test reports the first stage whose bits differ from the host's (diagnostic; asserts nothing about
+    the out-of-line build's correctness, only that the dump ran)."""
+    import ctypes
+
+    import vslam_abi
+    lib = vslam_abi.load_library()
+    lib.vs_debug_epnp_mode.restype = ctypes.c_int
+    lib.vs_debug_epnp_mode.argtypes = [ctypes.c_void_p] * 3 + [ctypes.c_int] + [ctypes.c_void_p] * 2 + [ctypes.c_int]
+    count = 200
+    m = np.where(np.arange(count) % 5 == 0, 4, 5).astype(np.int32)
+    X = np.zeros((count, 15))
+    uv = np.zeros((count, 10))
+    for p in range(count):
+        obj, img, _, _, _ = pnp_problem(int(m[p]), 1000 + p, noise=0.5 if p % 2 else 0.0)
+        X[p, :3 * m[p]] = obj.astype(np.float64).ravel()
+        uv[p, :2 * m[p]] = img.astype(np.float64).ravel()
+    K = np.array([525.0, 525.0, 319.5, 239.5])
+    dev = np.zeros((count, 216))
+    assert lib.vs_debug_epnp_mode(X.ctypes.data, uv.ctypes.data, m.ctypes.data, count, K.ctypes.data,
+                                  dev.ctypes.data, 3) == 0
+    host = oracle.epnp_eig_stages(X, uv, m, tuple(K))
+    stages = [("alpha", 0, 10), ("tau", 10, 20), ("B", 20, 120), ("d", 120, 130), ("e", 130, 139), ("scale", 139, 140),
+              ("lo", 140, 141), ("hi", 141, 142), ("a", 142, 144), ("b", 144, 146), ("lambda", 146, 148),
+              ("y", 148, 168), ("v", 168, 216)]
+    for name, a, b in stages:
+        bad = np.nonzero(np.any(dev[:, a:b].view(np.uint64) != host[:, a:b].view(np.uint64), axis=1))[0]
+        print(f"stage {name:7s}: {len(bad):4d} problems differ; first {bad[:3].tolist()}",
+              "" if not len(bad) else f"dev {dev[bad[0], a:min(b, a + 4)].tolist()} host {host[bad[0], a:min(b, a + 4)].tolist()}")

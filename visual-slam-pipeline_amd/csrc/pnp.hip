@@ -855,7 +855,87 @@ __global__ void k_debug_epnp(const double* X, const double* uv, const int* m, in
     for (int k = 0; k < 9; k++) o[64 + k] = R2[k];
 }
 
+// The same sequential EPnP behind a call boundary the compiler may not remove (the
+// product once called it out of line from k_pnp_ransac and got eigenvectors different from the host's).
+// mode 1: one problem per lane; mode 2: one problem per wave, called by lane 0 alone (the divergent call
+// k_pnp_ransac made).
+__device__ __attribute__((noinline)) bool epnp_out_of_line(const double* X, const double* uv, int m, const Cam& K,
+                                                          double* R, double* t) {
+    return epnp<5>(X, uv, m, K, R, t);
+}
+
+__device__ __attribute__((noinline)) void eig_out_of_line(const double (*al)[4], const double* uv, int m, const Cam& K,
+                                                          double v[4][12], double* dbg) {
+    epnp_small_eig(al, uv, m, K, v, dbg);
+}
+
+// mode 3: the control points inline, epnp_small_eig out of line, its stage results (216 doubles) in out
+__global__ void k_debug_eig_ool(const double* X, const double* uv, const int* m, int count, double fx, double fy,
+                                double cx, double cy, double* out) {
+    const int p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= count) return;
+    const Cam K{fx, fy, cx, cy};
+    double cw[4][3], al[5][4], v[4][12];
+    double* o = out + (size_t)p * 216;
+    for (int k = 0; k < 216; k++) o[k] = 0.0;
+    if (epnp_control<5>(X + 15 * p, m[p], cw, al)) eig_out_of_line(al, uv + 10 * p, m[p], K, v, o);
+}
+
+__global__ void k_debug_epnp_ool(const double* X, const double* uv, const int* m, int count, double fx, double fy,
+                                 double cx, double cy, double* out, int mode) {
+    const int p = mode == 2 ? blockIdx.x : blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= count || (mode == 2 && threadIdx.x != 0)) return;
+    const Cam K{fx, fy, cx, cy};
+    double* o = out + (size_t)p * 73;
+    double R[9] = {}, t[3] = {};
+    const bool ok = epnp_out_of_line(X + 15 * p, uv + 10 * p, m[p], K, R, t);
+    for (int k = 0; k < 48; k++) o[k] = 0.0;
+    for (int k = 0; k < 9; k++) o[48 + k] = R[k];
+    for (int k = 0; k < 3; k++) o[57 + k] = t[k];
+    o[60] = ok ? 1.0 : 0.0;
+    double rv[3], R2[9];
+    rod_m2v(R, rv);
+    rod_v2m(rv, R2);
+    for (int k = 0; k < 3; k++) o[61 + k] = rv[k];
+    for (int k = 0; k < 9; k++) o[64 + k] = R2[k];
+}
+
 }  // namespace vs
+
+extern "C" int vs_debug_epnp(const double* X, const double* uv, const int* m, int count, const double* K, double* out);
+
+// mode 0: vs_debug_epnp; 1, 2: the out-of-line call (k_debug_epnp_ool)
+extern "C" int vs_debug_epnp_mode(const double* X, const double* uv, const int* m, int count, const double* K,
+                                  double* out, int mode) {
+    if (count <= 0) return 0;
+    if (mode == 0) return vs_debug_epnp(X, uv, m, count, K, out);
+    double *dX, *duv, *dout;
+    int* dm;
+    if (hipMalloc(&dX, sizeof(double) * 15 * count) != hipSuccess) return -1;
+    (void)hipMalloc(&duv, sizeof(double) * 10 * count);
+    (void)hipMalloc(&dout, sizeof(double) * 73 * count);
+    (void)hipMalloc(&dm, sizeof(int) * count);
+    (void)hipMemcpy(dX, X, sizeof(double) * 15 * count, hipMemcpyHostToDevice);
+    (void)hipMemcpy(duv, uv, sizeof(double) * 10 * count, hipMemcpyHostToDevice);
+    (void)hipMemcpy(dm, m, sizeof(int) * count, hipMemcpyHostToDevice);
+    const dim3 grid(mode == 2 ? count : (count + 63) / 64);
+    size_t per = 73;
+    if (mode == 3) {  // out: [count][216] stage results
+        per = 216;
+        (void)hipFree(dout);
+        (void)hipMalloc(&dout, sizeof(double) * per * count);
+        hipLaunchKernelGGL(vs::k_debug_eig_ool, grid, dim3(64), 0, 0, dX, duv, dm, count, K[0], K[1], K[2], K[3], dout);
+    } else {
+        hipLaunchKernelGGL(vs::k_debug_epnp_ool, grid, dim3(64), 0, 0, dX, duv, dm, count, K[0], K[1], K[2], K[3], dout,
+                           mode);
+    }
+    const hipError_t e = hipMemcpy(out, dout, sizeof(double) * per * count, hipMemcpyDeviceToHost);
+    (void)hipFree(dX);
+    (void)hipFree(duv);
+    (void)hipFree(dout);
+    (void)hipFree(dm);
+    return e == hipSuccess ? 0 : -1;
+}
 
 extern "C" int vs_debug_epnp(const double* X, const double* uv, const int* m, int count, const double* K,
                              double* out) {

@@ -709,7 +709,11 @@ VS_HD inline double ep_scale(double tnorm) {
 }
 
 // Sequential statement (host oracle; the device's parallel version in pnp.hip is bit-identical).
-VS_HD inline void epnp_small_eig(const double (*al)[4], const double* uv, int m, const Cam& K, double v[4][12]) {
+// dbg (test hook): when non-null, the stage results land in dbg[0..215]: alpha[10],
+// tau[10], B[100] (before tridiagonalisation), d[10] and e[9] after it, the scale, lo, hi, the
+// multisection brackets a[2] / b[2], lambda[2], y[2][10] after inverse iteration, v[48].
+VS_HD inline void epnp_small_eig(const double (*al)[4], const double* uv, int m, const Cam& K, double v[4][12],
+                                 double* dbg = nullptr) {
     const int nc = 2 * m;  // 8 or 10
     double C[10][12], alpha[10], tau[10], t[12];
     for (int j = 0; j < nc; j++)
@@ -739,6 +743,12 @@ VS_HD inline void epnp_small_eig(const double (*al)[4], const double* uv, int m,
                     t[k] = k >= b ? (k == a ? alpha[a] : C[k][a]) * (k == b ? alpha[b] : C[k][b]) : -0.0;
                 B[a][b] = B[b][a] = tsum<10>(t);
             }
+        if (dbg)
+            for (int i = 0; i < 10; i++) {
+                dbg[i] = alpha[i];
+                dbg[10 + i] = tau[i];
+                for (int j = 0; j < 10; j++) dbg[20 + 10 * i + j] = B[i][j];
+            }
         // tridiagonalisation: reflector k (indices k+1..9) in U[k], tau in tt[k]
         double d[10], e[9], U[8][10], tt[8];
         for (int k = 0; k < 8; k++) {
@@ -762,6 +772,10 @@ VS_HD inline void epnp_small_eig(const double (*al)[4], const double* uv, int m,
         d[8] = B[8][8];
         d[9] = B[9][9];
         e[8] = B[8][9];
+        if (dbg) {
+            for (int i = 0; i < 10; i++) dbg[120 + i] = d[i];
+            for (int i = 0; i < 9; i++) dbg[130 + i] = e[i];
+        }
         // 3. scaled to ||T|| in [1, 2) (Gershgorin bound); the two smallest eigenvalues by multisection
         double lo = 0, hi = 0;
         for (int i = 0; i < 10; i++) {
@@ -792,6 +806,12 @@ VS_HD inline void epnp_small_eig(const double (*al)[4], const double* uv, int m,
                 a_t[q] = js > 0 ? a + wd * ep_frac(js - 1) : a;
                 b_t[q] = js < kEpMsPts ? a + wd * ep_frac(js) : b_t[q];
             }
+        if (dbg) {
+            dbg[139] = sc;
+            dbg[140] = lo;
+            dbg[141] = hi;
+            for (int q = 0; q < 2; q++) dbg[142 + q] = a_t[q], dbg[144 + q] = b_t[q];
+        }
         // 4. inverse iteration
         const double tnorm = fabs(lo) > fabs(hi) ? fabs(lo) : fabs(hi);
         const double tiny = tnorm > 0 ? DBL_EPSILON * tnorm : DBL_MIN;
@@ -807,6 +827,11 @@ VS_HD inline void epnp_small_eig(const double (*al)[4], const double* uv, int m,
             for (int q = 0; q < 2; q++) ep_lu_solve(f[q], y[q]);
             if (cluster) ep_orth10(y[0], y[1]);
         }
+        if (dbg)
+            for (int q = 0; q < 2; q++) {
+                dbg[146 + q] = lam[q];
+                for (int i = 0; i < 10; i++) dbg[148 + 10 * q + i] = y[q][i];
+            }
         // 5. normalised, back through the tridiagonal reflectors (H_7 first), into the QR basis
         for (int q = 0; q < 2; q++) {
             ep_normalize10(y[q]);
@@ -827,6 +852,9 @@ VS_HD inline void epnp_small_eig(const double (*al)[4], const double* uv, int m,
         }
         for (int r = 0; r < 12; r++) v[q][r] = x[q][r];
     }
+    if (dbg)
+        for (int q = 0; q < 4; q++)
+            for (int r = 0; r < 12; r++) dbg[168 + 12 * q + r] = v[q][r];
 }
 
 // From the eigenvectors um (columns, descending eigenvalues): v[k] = eigenvector of the k-th

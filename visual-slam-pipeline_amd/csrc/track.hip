@@ -30,16 +30,10 @@ constexpr int kTlmMaxKp = 1024;
 // workgroup: a keypoint's slot is its cell's prefix count plus the number of earlier keypoints in
 // the same cell (the order the reference's push_back produces).
 constexpr int kTlmMaxCells = 4096;
-// Also: the kp -> map-point table from pinned host memory when given (src), and -1 in the item
-// slots past the grid's last (nit .. nkp), so the call needs no upload or memset of its own.
-__global__ __launch_bounds__(1024) void k_tlm_grid(const vs_keypoint* __restrict__ kps, int nkp, int GW, int GH,
-                                                   int* __restrict__ start, int* __restrict__ items,
-                                                   int* __restrict__ work_n, const int* __restrict__ src,
-                                                   int* __restrict__ kp_to_mp) {
-    crit_prio();
-    if (threadIdx.x == 0) *work_n = 0;  // the candidate work list of this call (k_tlm_cand appends)
-    if (src)
-        for (int i = threadIdx.x; i < nkp; i += blockDim.x) kp_to_mp[i] = src[i];
+// The grid of one frame's keypoints into start[GW * GH + 1] / items[nkp + 1] (-1 in the item slots past
+// the grid's last, nit .. nkp); one 1024-thread workgroup.
+__device__ void tlm_build_grid(const vs_keypoint* __restrict__ kps, int nkp, int GW, int GH, int* __restrict__ start,
+                               int* __restrict__ items) {
     __shared__ int s_cell[kTlmMaxKp];
     __shared__ int s_start[kTlmMaxCells + 1];
     const int tid = threadIdx.x, nc = GW * GH;
@@ -90,6 +84,30 @@ __global__ __launch_bounds__(1024) void k_tlm_grid(const vs_keypoint* __restrict
     }
     for (int c = tid; c <= nc; c += blockDim.x) start[c] = s_start[c];
     for (int i = s_start[nc] + tid; i <= nkp; i += blockDim.x) items[i] = -1;
+}
+
+// Also: the kp -> map-point table from pinned host memory when given (src), so the call needs no
+// upload or memset of its own.
+__global__ __launch_bounds__(1024) void k_tlm_grid(const vs_keypoint* __restrict__ kps, int nkp, int GW, int GH,
+                                                   int* __restrict__ start, int* __restrict__ items,
+                                                   int* __restrict__ work_n, const int* __restrict__ src,
+                                                   int* __restrict__ kp_to_mp) {
+    crit_prio();
+    if (threadIdx.x == 0) *work_n = 0;  // the candidate work list of this call (k_tlm_cand appends)
+    if (src)
+        for (int i = threadIdx.x; i < nkp; i += blockDim.x) kp_to_mp[i] = src[i];
+    tlm_build_grid(kps, nkp, GW, GH, start, items);
+}
+
+// Round 6: the grids of a batch of frame slots, built when their keypoints exist (the tracker's
+// extraction chunk, off the tracking chain); one workgroup per frame: grid[f] = start | items of frame
+// slot0 + f (kTlmGridInts ints per slot), counts from n[f].
+__global__ __launch_bounds__(1024) void k_tlm_grid_slots(const vs_keypoint* __restrict__ kps, const int* __restrict__ n,
+                                                         int kp_stride, int GW, int GH, int* __restrict__ grid) {
+    const int f = blockIdx.x;
+    const int nkp = min(max(n[f], 0), kTlmMaxKp);
+    int* start = grid + (size_t)f * kTlmGridInts;
+    tlm_build_grid(kps + (size_t)f * kp_stride, nkp, GW, GH, start, start + GW * GH + 1);
 }
 
 __device__ double desc_l2_dev(const float* __restrict__ a, const float* __restrict__ b) {
@@ -255,8 +273,11 @@ __global__ __launch_bounds__(256) void k_tlm_dist(const float* __restrict__ mp_d
 __global__ __launch_bounds__(256) void k_tlm_best(const int* __restrict__ cnt, const int* __restrict__ cand,
                                                   const double* __restrict__ dist, int n_mp, int* __restrict__ best_ki,
                                                   double* __restrict__ best_d, int* __restrict__ rank,
-                                                  int* __restrict__ blkcnt) {
+                                                  int* __restrict__ blkcnt, int* __restrict__ work_n) {
     crit_prio();
+    // k_tlm_dist (the last reader of the work list's length) has finished: zero it for the next call,
+    // whose k_tlm_cand appends without a grid kernel to reset it (round 6)
+    if (blockIdx.x == 0 && threadIdx.x == 0) *work_n = 0;
     __shared__ int s_w[4];
     const int mp = blockIdx.x * 256 + threadIdx.x, wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
     int ki0 = -1;
@@ -384,18 +405,30 @@ __device__ void tlm_resolve_pass(TlmResolveShared& S, int nc, int* __restrict__ 
 // Phase 3b: the assignment in map-point order (Slam.cpp:460-465).  The candidates (k_tlm_best)
 // go to an LDS buffer in map-point order -- directly at block prefix + rank when they all fit,
 // else 1024 map points at a time with a pass whenever the buffer could overflow.
+// The PnP input the tracker's refinement takes next (Slam::refine_pose_via_local_pnp's tracked_points,
+// Slam.cpp:1408-1420): keypoints in order whose (final) map point is valid, as float object points and
+// image points; io = [off {0, n, 0, 0} | obj cap x 3 | img cap x 2].
+struct TlmGatherArgs {
+    const double* pos = nullptr;
+    const uint8_t* valid = nullptr;
+    const vs_keypoint* kps = nullptr;
+    float* io = nullptr;
+    int cap = 0;
+};
+
 __global__ __launch_bounds__(1024) void k_tlm_resolve(const int* __restrict__ best_ki, const double* __restrict__ best_d,
                                                       const int* __restrict__ rank, const int* __restrict__ blkcnt,
                                                       int n_mp, int nkp, int* __restrict__ kp_to_mp,
                                                       int* __restrict__ obs_mp, int* __restrict__ obs_kp, int obs_cap,
-                                                      int* __restrict__ result) {
+                                                      int* __restrict__ result, const int* __restrict__ src,
+                                                      TlmGatherArgs G) {
     crit_prio();
     __shared__ TlmResolveShared S;
     const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
     const int nblk = (n_mp + 255) / 256;
     for (int k = tid; k < nkp; k += 1024) {
         S.best[k] = (unsigned long long)__double_as_longlong(1e9);
-        S.kpmp[k] = kp_to_mp[k];
+        S.kpmp[k] = src ? src[k] : kp_to_mp[k];  // src: the host's table in pinned memory (no upload)
         S.first[k] = INT_MAX;
         S.bcnt[k] = 0;
     }
@@ -497,32 +530,79 @@ __global__ __launch_bounds__(1024) void k_tlm_resolve(const int* __restrict__ be
         result[0] = S.nobs;  // each record is one tracked++ and one add_observation
         result[1] = S.nobs;
     }
+    if (G.io) {  // nkp <= 1024: one keypoint per thread, in order (a block prefix of the ballots)
+        const int id = tid < nkp ? S.kpmp[tid] : -1;
+        const bool use = id >= 0 && id < n_mp && G.valid[id];
+        const unsigned long long bal = __ballot(use);
+        __syncthreads();  // every reader of S.wcnt above is done
+        if (lane == 0) S.wcnt[wv] = __popcll(bal);
+        __syncthreads();
+        int o = 0, n = 0;
+        for (int k = 0; k < 16; k++) {
+            if (k < wv) o += S.wcnt[k];
+            n += S.wcnt[k];
+        }
+        float* obj = G.io + 4;
+        float* img = obj + 3 * G.cap;
+        if (use) {
+            o += __popcll(bal & ((1ull << lane) - 1ull));
+            obj[3 * o] = (float)G.pos[3 * id];
+            obj[3 * o + 1] = (float)G.pos[3 * id + 1];
+            obj[3 * o + 2] = (float)G.pos[3 * id + 2];
+            img[2 * o] = G.kps[tid].x;
+            img[2 * o + 1] = G.kps[tid].y;
+        }
+        if (tid == 0) {
+            int* off = reinterpret_cast<int*>(G.io);
+            off[0] = 0;
+            off[1] = n;
+            off[2] = off[3] = 0;
+        }
+    }
 }
 
+
+int tlm_grid_slots(const vs_keypoint* d_kps, const int* d_n, int nframes, int kp_stride, int img_w, int img_h,
+                   int* d_grid, hipStream_t s) {
+    if (nframes <= 0) return VS_OK;
+    VS_ARG(img_w > 0 && img_h > 0 && ((img_w + kTlmCell - 1) / kTlmCell) * ((img_h + kTlmCell - 1) / kTlmCell) <= kTlmMaxCells,
+           "tlm_grid_slots: image too large for the keypoint grid");
+    static_assert(kTlmGridInts >= kTlmMaxCells + 1 + kTlmMaxKp + 1, "grid slot too small");
+    const int GW = (img_w + kTlmCell - 1) / kTlmCell, GH = (img_h + kTlmCell - 1) / kTlmCell;
+    hipLaunchKernelGGL(k_tlm_grid_slots, dim3(nframes), dim3(1024), 0, s, d_kps, d_n, kp_stride, GW, GH, d_grid);
+    VS_HIP(hipGetLastError());
+    return VS_OK;
+}
 
 int track_local_map(vs_ctx* ctx, const double* d_mp_pos, const float* d_mp_desc, const uint8_t* d_mp_valid, int n_mp,
                     const vs_keypoint* d_kps, const float* d_desc, int nkp, const double R[9], const double t[3],
                     const double K[4], int img_w, int img_h, int* d_kp_to_mp, int* d_obs_mp, int* d_obs_kp,
-                    int obs_cap, int* d_result, hipStream_t s, const int* h_kp_to_mp_src) {
+                    int obs_cap, int* d_result, hipStream_t s, const int* h_kp_to_mp_src, const TlmExtra* ex) {
     VS_ARG(nkp >= 0 && nkp <= kTlmMaxKp, "track_local_map: at most 1024 keypoints");
     VS_ARG(img_w > 0 && img_h > 0, "track_local_map: bad image size");
     VS_ARG(((img_w + kTlmCell - 1) / kTlmCell) * ((img_h + kTlmCell - 1) / kTlmCell) <= kTlmMaxCells,
            "track_local_map: image too large for the keypoint grid");
+    VS_ARG(!ex || !ex->gather_io || ex->gather_cap >= nkp, "track_local_map: gather capacity below the keypoints");
     const int GW = (img_w + kTlmCell - 1) / kTlmCell, GH = (img_h + kTlmCell - 1) / kTlmCell;
-    const size_t grid_bytes = (size_t)(GW * GH + 1) * sizeof(int) + (size_t)(nkp + 1) * sizeof(int);
+    // layout: the work list's length first (a fixed place: k_tlm_best leaves it zero for the next
+    // call), then the grid, the per-map-point arrays
+    const size_t grid_bytes = 16 + (size_t)(GW * GH + 1) * sizeof(int) + (size_t)(nkp + 1) * sizeof(int);
     const size_t per_mp = 3 * sizeof(int) + sizeof(double) + (size_t)kTlmMaxCand * (2 * sizeof(int) + sizeof(double));
     const int nblk = (n_mp + 255) / 256;
+    void* before = ctx->tlm.p;
     VS_CHECK(ctx->tlm.ensure(grid_bytes + 64 + (size_t)(n_mp + 1) * per_mp + (size_t)(nblk + 2) * sizeof(int)));
     char* base = static_cast<char*>(ctx->tlm.p);
-    int* start = reinterpret_cast<int*>(base);
+    int* work_n = reinterpret_cast<int*>(base);
+    const bool pre_grid = ex && ex->grid && nkp > 0;
+    if (pre_grid && ctx->tlm.p != before) VS_HIP(hipMemsetAsync(work_n, 0, sizeof(int), s));  // a new buffer
+    int* start = pre_grid ? const_cast<int*>(ex->grid) : reinterpret_cast<int*>(base + 16);
     int* items = start + GW * GH + 1;
     double* dist = reinterpret_cast<double*>(base + ((grid_bytes + 15) / 16) * 16);
     int* cand = reinterpret_cast<int*>(dist + (size_t)(n_mp + 1) * kTlmMaxCand);
     int* cnt = cand + (size_t)(n_mp + 1) * kTlmMaxCand;
     int* best_ki = cnt + (n_mp + 1);
     int* rank = best_ki + (n_mp + 1);
-    int* work_n = rank + (n_mp + 1);
-    int* blkcnt = work_n + 1;
+    int* blkcnt = rank + (n_mp + 1) + 1;
     int* work = blkcnt + nblk + 1;
     double* best_d =
         reinterpret_cast<double*>(base + (((size_t)(reinterpret_cast<char*>(work + (size_t)(n_mp + 1) * kTlmMaxCand) - base) + 15) / 16) * 16);
@@ -535,7 +615,9 @@ int track_local_map(vs_ctx* ctx, const double* d_mp_pos, const float* d_mp_desc,
     T.cx = K[2];
     T.cy = K[3];
     ProfScope ps(ctx, "track_local_map", s);
-    if (nkp > 0) {
+    if (pre_grid) {
+        // the grid was built with the frame's keypoints; k_tlm_resolve reads the host's table itself
+    } else if (nkp > 0) {
         hipLaunchKernelGGL(k_tlm_grid, dim3(1), dim3(1024), 0, s, d_kps, nkp, GW, GH, start, items, work_n,
                            h_kp_to_mp_src, d_kp_to_mp);
     } else {
@@ -550,9 +632,17 @@ int track_local_map(vs_ctx* ctx, const double* d_mp_pos, const float* d_mp_desc,
     }
     if (n_mp > 0)
         hipLaunchKernelGGL(k_tlm_best, dim3(nblk), dim3(256), 0, s, cnt, cand, dist, n_mp, best_ki, best_d, rank,
-                           blkcnt);
+                           blkcnt, work_n);
+    TlmGatherArgs G;
+    if (ex && ex->gather_io) {
+        G.pos = d_mp_pos;
+        G.valid = d_mp_valid;
+        G.kps = d_kps;
+        G.io = ex->gather_io;
+        G.cap = ex->gather_cap;
+    }
     hipLaunchKernelGGL(k_tlm_resolve, dim3(1), dim3(1024), 0, s, best_ki, best_d, rank, blkcnt, n_mp, nkp, d_kp_to_mp,
-                       d_obs_mp, d_obs_kp, obs_cap, d_result);
+                       d_obs_mp, d_obs_kp, obs_cap, d_result, pre_grid ? h_kp_to_mp_src : nullptr, G);
     VS_HIP(hipGetLastError());
     return VS_OK;
 }

@@ -339,43 +339,6 @@ constexpr size_t kHdrBytes = kHdrWords * sizeof(uint32_t);
 constexpr int kXChunk = 16;
 constexpr int kXFirst = 8;
 
-// The PnP input of Slam::refine_pose_via_local_pnp (tracked_points, :1408-1420) straight from the
-// local-map tracking result: keypoints (in order) whose map point is valid, as float object
-// points and image points; io = [off {0, n, 0, 0} | obj cap x 3 | img cap x 2].  One workgroup.
-__global__ __launch_bounds__(1024) void k_pnp_gather(const int* __restrict__ kpmp, int nkp, const double* __restrict__ pos,
-                                                     const uint8_t* __restrict__ valid, int n_mp,
-                                                     const vs_keypoint* __restrict__ kps, int cap, float* __restrict__ io) {
-    crit_prio();
-    __shared__ int s_w[16];
-    const int i = threadIdx.x, wv = i >> 6, lane = i & 63;
-    const int id = i < nkp ? kpmp[i] : -1;
-    const bool use = id >= 0 && id < n_mp && valid[id];
-    const unsigned long long bal = __ballot(use);
-    if (lane == 0) s_w[wv] = __popcll(bal);
-    __syncthreads();
-    int o = 0, n = 0;
-    for (int k = 0; k < 16; k++) {
-        if (k < wv) o += s_w[k];
-        n += s_w[k];
-    }
-    float* obj = io + 4;
-    float* img = obj + 3 * cap;
-    if (use) {
-        o += __popcll(bal & ((1ull << lane) - 1ull));
-        obj[3 * o] = (float)pos[3 * id];
-        obj[3 * o + 1] = (float)pos[3 * id + 1];
-        obj[3 * o + 2] = (float)pos[3 * id + 2];
-        img[2 * o] = kps[i].x;
-        img[2 * o + 1] = kps[i].y;
-    }
-    if (i == 0) {
-        int* off = reinterpret_cast<int*>(io);
-        off[0] = 0;
-        off[1] = n;
-        off[2] = off[3] = 0;
-    }
-}
-
 // Host-side wall time per back-end operation (VS_SLAM_HOST_PROFILE=1: printed to stderr when the
 // vs_slam is destroyed); the rest of process_frame is the tracker's own host logic.
 enum HostOp { kHChain, kHMatch, kHFmat, kHMotion, kHTlm, kHPnp, kHMatchMap, kHAppend, kHVis, kHFrame, kHWait, kHSpec, kHLoop,
@@ -542,6 +505,8 @@ struct GpuOps {
     int B = 0, h = 0, w = 0, S = 0, batch_region = 0;
     double K[4] = {vs_trk::cfg::FX, vs_trk::cfg::FY, vs_trk::cfg::CX, vs_trk::cfg::CY};
     DevBuf pool_kps, pool_desc, pool_n, pool_depth, pool_norms, semi, dgrid;
+    DevBuf pool_grid;  // per slot: the keypoint grid of local-map tracking (vs::kTlmGridInts ints, round 6)
+    bool pre_grid = true;  // VS_SLAM_PRE_GRID=0: the grid kernel in the tracking chain instead (A/B)
     DevBuf chain_buf, work, rows_buf, map_pos, map_desc, map_valid, map_tmp, pnp_io, hdr_buf;
     int map_cap = 0, map_n = 0;
     bool valid_dirty = false;
@@ -561,6 +526,7 @@ struct GpuOps {
     float* desc_of(int slot) const { return pool_desc.as<float>() + (size_t)slot * kCap * 256; }
     float* depth_of(int slot) const { return pool_depth.as<float>() + (size_t)slot * h * w; }
     float* norms_of(int slot) const { return pool_norms.as<float>() + (size_t)slot * kCap; }
+    int* grid_of(int slot) const { return pool_grid.as<int>() + (size_t)slot * kTlmGridInts; }
 
     // Two streams on disjoint CU sets: the latency-bound tracking kernels keep VS_SLAM_TRACK_CUS
     // (default 32) CUs to themselves, so they never queue behind the network's long-running
@@ -707,6 +673,8 @@ struct GpuOps {
         VS_CHECK(pool_n.ensure((size_t)S * sizeof(int)));
         VS_CHECK(pool_depth.ensure((size_t)S * h * w * sizeof(float)));
         VS_CHECK(pool_norms.ensure((size_t)S * kCap * sizeof(float)));
+        VS_CHECK(pool_grid.ensure((size_t)S * kTlmGridInts * sizeof(int)));
+        if (const char* e = std::getenv("VS_SLAM_PRE_GRID")) pre_grid = e[0] != '0';
         VS_HIP(hipMemsetAsync(pool_n.p, 0, (size_t)S * sizeof(int), s));
         const int hc = (h + 7) / 8, wc = (w + 7) / 8;
         // network outputs per batch region (2 B frames): a chunk's post-processing reads its own
@@ -736,6 +704,7 @@ struct GpuOps {
         // the context's per-stage scratch at its largest in-loop size: local-map tracking for 200k
         // map points, PnP hypothesis tables for the largest RANSAC budget (loop closure: 300)
         VS_CHECK(ctx->tlm.ensure((size_t)64 << 20));
+        VS_HIP(hipMemsetAsync(ctx->tlm.p, 0, 16, s));  // the work list's length (k_tlm_best re-zeroes it)
         VS_CHECK(ctx->pnp.ensure((size_t)4 * VS_PNP_MAX_ITERS * (6 * sizeof(int) + 6 * sizeof(double))));
         VS_CHECK(pnp_reserve(ctx, s));  // the PnP subset table (built once here, not in the loop)
         // Loop closure (every 200 keyframes, candidates every 5th keyframe >= 200 ids back,
@@ -827,6 +796,7 @@ struct GpuOps {
         cjobs.push_back({pool_n.as<int>() + from, pool_n.as<int>() + to, sizeof(int)});
         cjobs.push_back({depth_of(from), depth_of(to), (size_t)h * w * sizeof(float)});
         cjobs.push_back({norms_of(from), norms_of(to), kCap * sizeof(float)});
+        cjobs.push_back({grid_of(from), grid_of(to), (size_t)kTlmGridInts * sizeof(int)});
         return VS_OK;
     }
     int flush_copies() {
@@ -852,6 +822,8 @@ struct GpuOps {
         VS_CHECK(upload(desc_of(slot), desc, (size_t)n * 256 * sizeof(float)));
         VS_CHECK(upload(pool_n.as<int>() + slot, &n, sizeof(int)));
         VS_CHECK(desc_norms(ctx, 1, desc_of(slot), pool_n.as<int>() + slot, kCap, norms_of(slot), s));
+        VS_CHECK(tlm_grid_slots(kps_of(slot), pool_n.as<int>() + slot, 1, kCap, vs_trk::cfg::IMAGE_WIDTH,
+                                vs_trk::cfg::IMAGE_HEIGHT, grid_of(slot), s));
         if (f.depth)
             VS_CHECK(upload(depth_of(slot), f.depth, (size_t)h * w * sizeof(float)));
         else
@@ -900,6 +872,10 @@ struct GpuOps {
                                     kCap, xp, sm, dg, true));
             // descriptor row norms once per frame (matching reuses them for every pair)
             VS_CHECK(desc_norms(ctx, m, desc_of(s0 + f0), pool_n.as<int>() + s0 + f0, kCap, norms_of(s0 + f0), xp));
+            // the keypoint grid of local-map tracking, per frame, while the keypoints are fresh (round 6:
+            // one kernel off the tracking chain)
+            VS_CHECK(tlm_grid_slots(kps_of(s0 + f0), pool_n.as<int>() + s0 + f0, m, kCap, vs_trk::cfg::IMAGE_WIDTH,
+                                    vs_trk::cfg::IMAGE_HEIGHT, grid_of(s0 + f0), xp));
             if (d_depth)
                 VS_HIP(hipMemcpyAsync(depth_of(s0 + f0), d_depth + (size_t)f0 * h * w, (size_t)m * h * w * sizeof(float),
                                       hipMemcpyDeviceToDevice, xp));
@@ -1253,18 +1229,23 @@ struct GpuOps {
             int* h_kpmp = reinterpret_cast<int*>(take((size_t)std::max(nkp, 1) * sizeof(int)));
             if (!h_kpmp) return 0;
             std::memcpy(h_kpmp, f.mp_idx.data(), (size_t)nkp * sizeof(int));
+            // Speculatively, the refinement's PnP on the tracked points right behind it (the tracker calls
+            // solve_pnp on exactly these next, Slam.cpp:1057-1059; solve_pnp checks); its input gathered
+            // by the resolve kernel itself (round 6: no gather kernel), the grid built at extraction.
+            char* io = work.as<char>() + wbytes;
+            vs::TlmExtra ex;
+            ex.grid = pre_grid && (int)f.kps.size() <= 1024 ? grid_of(f.slot) : nullptr;
+            if (spec_on) {
+                ex.gather_io = reinterpret_cast<float*>(io);
+                ex.gather_cap = cap;
+            }
             if (failed(vs::track_local_map(ctx, map_pos.as<double>(), map_desc.as<float>(), map_valid.as<uint8_t>(),
                                            m.size(), kps_of(f.slot), desc_of(f.slot), nkp, f.R.data(), f.t.data(), K,
                                            vs_trk::cfg::IMAGE_WIDTH, vs_trk::cfg::IMAGE_HEIGHT, d_kpmp, d_obs,
-                                           d_obs + obs_cap, obs_cap, d, s, h_kpmp)))
+                                           d_obs + obs_cap, obs_cap, d, s, h_kpmp, &ex)))
                 return 0;
-            // Speculatively, the refinement's PnP on the tracked points right behind it (the
-            // tracker calls solve_pnp on exactly these next, Slam.cpp:1057-1059; solve_pnp checks).
             bool spec_run = false;
             if (spec_on) {
-                char* io = work.as<char>() + wbytes;
-                hipLaunchKernelGGL(k_pnp_gather, dim3(1), dim3(1024), 0, s, d_kpmp, nkp, map_pos.as<double>(),
-                                   map_valid.as<uint8_t>(), m.size(), kps_of(f.slot), cap, reinterpret_cast<float*>(io));
                 double* dRt = reinterpret_cast<double*>(io + io_pad);
                 int* dstat = reinterpret_cast<int*>(dRt + 12);
                 spec_run = vs::solve_pnp(ctx, 1, reinterpret_cast<const float*>(io + 16),
@@ -1763,7 +1744,7 @@ void vs_slam_destroy(vs_slam* sl) {
                              ph.n[k], ph.ms[k], 1e3 * ph.ms[k] / ph.n[k]);
     }
     o.destroy_streams();
-    DevBuf* bufs[] = {&o.pool_kps, &o.pool_desc, &o.pool_n, &o.pool_depth, &o.pool_norms, &o.semi, &o.dgrid,
+    DevBuf* bufs[] = {&o.pool_kps, &o.pool_desc, &o.pool_n, &o.pool_depth, &o.pool_norms, &o.pool_grid, &o.semi, &o.dgrid,
                       &o.chain_buf,    &o.work, &o.rows_buf,      &o.map_pos, &o.map_desc,  &o.map_valid, &o.map_tmp,
                       &o.pnp_io,       &o.hdr_buf, &o.chain_buf2, &o.hdr_buf2, &o.mstate2,
                       &o.arch_kps,     &o.arch_desc, &o.arch_n,   &o.lc_buf,    &o.dlt_buf, &o.cjob_buf};

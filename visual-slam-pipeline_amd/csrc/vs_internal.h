@@ -243,10 +243,22 @@ int ransac3d_pairs(vs_ctx* ctx, int P, const int* d_pairs, const vs_keypoint* d_
 // Local-map tracking (d_result = {tracked, observations}).  h_kp_to_mp_src (optional): device-
 // readable pinned host memory with the initial kp -> map-point table, copied into d_kp_to_mp by the
 // first kernel (no separate upload); null = d_kp_to_mp already holds it.
+// Round 6, the tracker's chain: a keypoint grid built ahead of time per frame slot (tlm_grid_slots:
+// kTlmGridInts ints per slot, start | items), so the call skips its grid kernel, and the PnP input of
+// the refinement gathered by the resolve kernel itself (io = [off {0, n, 0, 0} | obj cap x 3 | img cap x 2]).
+constexpr int kTlmGridInts = 4096 + 1 + 1024 + 1;
+struct TlmExtra {
+    const int* grid = nullptr;  // this frame's slot in the grid pool, or null
+    float* gather_io = nullptr;  // tracked_points (Slam.cpp:1408-1420) into this block, or null
+    int gather_cap = 0;
+};
+int tlm_grid_slots(const vs_keypoint* d_kps, const int* d_n, int nframes, int kp_stride, int img_w, int img_h,
+                   int* d_grid, hipStream_t s);
 int track_local_map(vs_ctx* ctx, const double* d_mp_pos, const float* d_mp_desc, const uint8_t* d_mp_valid, int n_mp,
                     const vs_keypoint* d_kps, const float* d_desc, int nkp, const double R[9], const double t[3],
                     const double K[4], int img_w, int img_h, int* d_kp_to_mp, int* d_obs_mp, int* d_obs_kp,
-                    int obs_cap, int* d_result, hipStream_t s, const int* h_kp_to_mp_src = nullptr);
+                    int obs_cap, int* d_result, hipStream_t s, const int* h_kp_to_mp_src = nullptr,
+                    const TlmExtra* ex = nullptr);
 // Pose LM, nprob problems with point ranges d_off[p]..d_off[p+1]
 int optimize_pose(vs_ctx* ctx, int nprob, const double* d_P, const float* d_p2, const int* d_off, const double K[4],
                   double* d_R, double* d_t, double* d_res, int* d_ok, hipStream_t s);

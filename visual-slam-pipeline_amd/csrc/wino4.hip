@@ -98,7 +98,8 @@ __device__ inline void w4_rowA(const float m[6], float r[4]) {
 
 #ifndef VS_W4_ABL
 #define VS_W4_ABL 0  // latency ablation (results are wrong): 1 no transform, 2 no patch staging, 3 no MFMA,
-                     // 4 no barrier in the k-loop, 5 no B loads
+                     // 4 no barrier in the k-loop, 5 no B loads, 6 half the k-steps, 7 two k-steps only
+                     // (6 and 7 separate the per-workgroup fixed cost from the per-k-step cost)
 #endif
 // one lane's B operands of a 4-channel sub-step: U[18 xh + x][ch][cout] for x = 0..17 (4 x 16 B + 8 B)
 struct W4B {
@@ -126,7 +127,7 @@ __global__ __launch_bounds__(512, 1) void k_wino4(WinoArgs wa) {
     w4_xcd_work(ntn, blk, nt);
     const int b = blk / (nbx * nby), r0 = blk - b * (nbx * nby);
     const int y0 = (r0 / nbx) * 16, x0 = (r0 % nbx) * 16;
-    const int nk = cin / CH;  // k-steps
+    const int nk = VS_W4_ABL == 6 ? cin / CH / 2 : VS_W4_ABL == 7 ? 2 : cin / CH;  // k-steps
     // this lane's B operands: [nt][4-channel chunk][cg][xh][lane][20]
     const float* __restrict__ wb = wa.wu + ((size_t)nt * (cin >> 2) * 8 + cg * 2 + xh) * (64 * 20) + lane * 20;
 
