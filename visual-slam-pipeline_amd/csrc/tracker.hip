@@ -342,11 +342,12 @@ constexpr int kXFirst = 8;
 // Host-side wall time per back-end operation (VS_SLAM_HOST_PROFILE=1: printed to stderr when the
 // vs_slam is destroyed); the rest of process_frame is the tracker's own host logic.
 enum HostOp { kHChain, kHMatch, kHFmat, kHMotion, kHTlm, kHPnp, kHMatchMap, kHAppend, kHVis, kHFrame, kHWait, kHSpec, kHLoop,
-              kHTlmSync, kHOps };
+              kHTlmSync, kHSpecNext, kHOps };
 static const char* const kHostOpNames[kHOps] = {"chain", "match", "find_fundamental", "motion_points",
                                                 "track_local_map", "solve_pnp", "match_map", "map_append",
                                                 "visibility", "process_frame (total)", "extract wait",
-                                                "chain: speculation wait", "loop_eval", "track_local_map: sync"};
+                                                "chain: speculation wait", "loop_eval", "track_local_map: sync",
+                                                "next chain read-ahead wait"};
 struct HostProf {
     bool on = false;
     long skip = 64;  // frames before counting starts (first launches load code objects)
@@ -615,6 +616,8 @@ struct GpuOps {
         }
         for (auto& e : region_done) VS_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
         VS_HIP(hipEventCreateWithFlags(&cspec_ev, hipEventDisableTiming));
+        VS_HIP(hipEventCreateWithFlags(&tlm_ev, hipEventDisableTiming));
+        VS_HIP(hipEventCreateWithFlags(&tspec.ev, hipEventDisableTiming));
         VS_HIP(hipEventCreateWithFlags(&xdone, hipEventDisableTiming));
         // the extraction streams share the context's network / NMS scratch: any other stream that
         // uses it waits for the last extraction enqueued here (vs::scratch_order)
@@ -645,6 +648,8 @@ struct GpuOps {
             X.net.clear();
         }
         (void)hipEventDestroy(cspec_ev);
+        (void)hipEventDestroy(tlm_ev);
+        (void)hipEventDestroy(tspec.ev);
         (void)hipStreamDestroy(xs);
         (void)hipStreamDestroy(xp);
         (void)hipStreamDestroy(s);
@@ -691,6 +696,8 @@ struct GpuOps {
         VS_CHECK(cpin.reserve(kHdrBytes + kChainRaw + 64));
         if (const char* e = std::getenv("VS_SLAM_SPEC_CHAIN")) cspec_on = e[0] != '0';
         VS_CHECK(pin.reserve((size_t)4 << 20));
+        VS_CHECK(spin.reserve((size_t)1 << 20));  // one speculation: <= 8 KB table + ~60 KB results at 1024 keypoints
+        if (const char* e = std::getenv("VS_SLAM_SPEC_TLM")) tlm_spec_on = e[0] != '0';
         owner.assign(kPersist, nullptr);
         VS_CHECK(grow_map(1 << 16));
         // map-sized scratch up front (a later growth would wait for the extraction stream too):
@@ -746,6 +753,7 @@ struct GpuOps {
 
     int grow_map(int need) {
         if (need <= map_cap) return VS_OK;
+        map_ver++;
         int cap = std::max(need, map_cap * 2);
         DevBuf np, nd, nv;
         VS_CHECK(np.ensure((size_t)cap * 3 * sizeof(double)));
@@ -1075,10 +1083,18 @@ struct GpuOps {
             HostTimer hw(hprof, kHSpec);
             spec_sync();
         }
-        const bool hit = cspec.valid && cspec.cur == &cur && cspec.ref_slot == ref.slot && cspec.cur_slot == cur.slot &&
-                         cspec.seed == seed;
-        cspec.valid = false;
-        if (hit) {
+        // the next frame's chain read back ahead of this call (speculate_next), the frame after it then
+        // already launched
+        const bool nhit = cnext.valid && cnext.cur == &cur && cnext.ref_slot == ref.slot && cnext.cur_slot == cur.slot &&
+                          cnext.seed == seed;
+        const bool launched = nhit && cnext.launched_next;
+        if (nhit) R = cnext.R;
+        cnext.valid = false;
+        const bool hit = !nhit && cspec.valid && cspec.cur == &cur && cspec.ref_slot == ref.slot &&
+                         cspec.cur_slot == cur.slot && cspec.seed == seed;
+        if (!launched) cspec.valid = false;  // (a launched speculation belongs to the next frame)
+        if (nhit) {
+        } else if (hit) {
             HostTimer hw(hprof, kHSpec);
             if (failed(hipEventSynchronize(cspec_ev) == hipSuccess ? VS_OK : VS_ERR_HIP)) return R;
             R = parse_chain(cpin.base + kHdrBytes);
@@ -1092,7 +1108,8 @@ struct GpuOps {
         // The launch itself (~40 us of HIP calls) is deferred until this frame's local-map tracking
         // and PnP are enqueued (flush_spec), so it overlaps them instead of delaying them.
         spec_req.pending = false;
-        if (cspec_on && err == VS_OK && next_frame && next_frame != &cur && next_frame->slot >= 0 && ref.slot >= 0) {
+        if (!launched && cspec_on && err == VS_OK && next_frame && next_frame != &cur && next_frame->slot >= 0 &&
+            ref.slot >= 0) {
             const int ng = (int)R.good.size(), gap = cur.id - ref.id;
             const bool kf = (gap >= vs_trk::cfg::KF_MIN_FRAME_GAP && ng >= vs_trk::cfg::KF_MIN_MATCHES) ||
                             (ng < 2 * vs_trk::cfg::MIN_MATCHES && gap >= 5);
@@ -1202,91 +1219,254 @@ struct GpuOps {
         return R;
     }
 
-    // Observations can outnumber keypoints (a later map point may take a keypoint over with a
-    // smaller distance, Slam.cpp:460-465, and each takeover adds an observation): start with room
-    // for 4 per keypoint and rerun with the exact count when that is exceeded.
+    // One local-map tracking launch into a work area (device) and a pinned block: one device block
+    // read back with ONE copy, [tracking words | speculative PnP io + result], the refinement's PnP on
+    // the tracked points right behind the tracking kernels (the tracker calls solve_pnp on exactly these
+    // next, Slam.cpp:1057-1059; solve_pnp checks), its input gathered by k_tlm_resolve, the keypoint
+    // grid built at extraction.  Observations can outnumber keypoints (a later map point may take a
+    // keypoint over with a smaller distance, Slam.cpp:460-465, each takeover adding an observation):
+    // obs_cap = 4 per keypoint first, the exact count on a rerun.
+    struct TlmLaunch {
+        int nkp = 0, obs_cap = 0, cap = 0;
+        size_t wbytes = 0, io_pad = 0;
+        bool spec_run = false;
+        char* hall = nullptr;  // the pinned result block
+    };
+    int enqueue_tlm(const vs_trk::Map& m, const vs_trk::Frame& f, const double* R, const double* t, int obs_cap,
+                    DevBuf& wk, char* h_kpmp, char* hall_area, size_t hall_cap, TlmLaunch& L) {
+        const int nkp = (int)f.kps.size();
+        L.nkp = nkp;
+        L.obs_cap = obs_cap;
+        const int words = 2 + nkp + 2 * obs_cap;
+        L.wbytes = ((size_t)words * sizeof(int) + 255) & ~(size_t)255;
+        L.cap = std::max(nkp, 1);
+        const size_t io_bytes = 16 + (size_t)L.cap * 5 * sizeof(float);
+        L.io_pad = (io_bytes + 15) & ~(size_t)15;
+        const size_t spec_bytes = L.io_pad + 12 * sizeof(double) + 8 * sizeof(int);
+        const bool spec_on = nkp > 0 && nkp <= 1024;
+        VS_CHECK(wk.ensure(L.wbytes + (spec_on ? spec_bytes + (size_t)L.cap : 0)));
+        int* d = wk.as<int>();
+        int* d_kpmp = d + 2;
+        int* d_obs = d + 2 + nkp;
+        std::memcpy(h_kpmp, f.mp_idx.data(), (size_t)nkp * sizeof(int));  // read by k_tlm_resolve itself
+        char* io = wk.as<char>() + L.wbytes;
+        vs::TlmExtra ex;
+        ex.grid = pre_grid && nkp <= 1024 ? grid_of(f.slot) : nullptr;
+        if (spec_on) {
+            ex.gather_io = reinterpret_cast<float*>(io);
+            ex.gather_cap = L.cap;
+        }
+        VS_CHECK(vs::track_local_map(ctx, map_pos.as<double>(), map_desc.as<float>(), map_valid.as<uint8_t>(), m.size(),
+                                     kps_of(f.slot), desc_of(f.slot), nkp, R, t, K, vs_trk::cfg::IMAGE_WIDTH,
+                                     vs_trk::cfg::IMAGE_HEIGHT, d_kpmp, d_obs, d_obs + obs_cap, obs_cap, d, s,
+                                     reinterpret_cast<const int*>(h_kpmp), &ex));
+        L.spec_run = false;
+        if (spec_on) {
+            double* dRt = reinterpret_cast<double*>(io + L.io_pad);
+            int* dstat = reinterpret_cast<int*>(dRt + 12);
+            L.spec_run = vs::solve_pnp(ctx, 1, reinterpret_cast<const float*>(io + 16),
+                                       reinterpret_cast<const float*>(io + 16 + (size_t)L.cap * 3 * sizeof(float)),
+                                       reinterpret_cast<const int*>(io), K, 100, 10, dRt, dRt + 9, dstat,
+                                       reinterpret_cast<uint8_t*>(dstat + 8), s, L.cap) == VS_OK;
+        }
+        const size_t rb = L.wbytes + (L.spec_run ? spec_bytes : 0);
+        if (rb > hall_cap) return VS_ERR_CAPACITY;
+        L.hall = hall_area;
+        const Pinned& P = (hall_area >= spin.base && hall_area < spin.base + spin.cap) ? spin : pin;
+        return P.to_host(L.hall, wk.p, rb, s);
+    }
+    // The launch's results (its copy has landed): kp -> map-point table, observations, the speculative
+    // PnP; returns tracked, or -1 when the observations overflowed obs_cap (rerun with L.obs_cap set to
+    // their count).
+    int read_tlm(vs_trk::Frame& f, TlmLaunch& L, std::vector<std::pair<int, int>>& obs) {
+        const int* hb = reinterpret_cast<const int*>(L.hall);
+        const int nkp = L.nkp, cap = L.cap;
+        spec_valid = false;
+        if (L.spec_run) {
+            const char* hs = L.hall + L.wbytes;
+            const int n = reinterpret_cast<const int*>(hs)[1];
+            const float* so = reinterpret_cast<const float*>(hs + 16);
+            spec_obj.assign(so, so + (size_t)3 * n);
+            spec_img.assign(so + (size_t)3 * cap, so + (size_t)3 * cap + (size_t)2 * n);
+            const double* Rt = reinterpret_cast<const double*>(hs + L.io_pad);
+            const int* st = reinterpret_cast<const int*>(Rt + 12);
+            spec = vs_trk::PnPResult();
+            spec.success = n > 0 && st[0] != 0;
+            spec.inlier_count = spec.success ? st[1] : 0;
+            if (spec.success) {
+                std::memcpy(spec.R_world.data(), Rt, 9 * sizeof(double));
+                std::memcpy(spec.t_world.data(), Rt + 9, 3 * sizeof(double));
+            }
+            spec_valid = true;
+        }
+        const int n_obs = hb[1];
+        if (n_obs > L.obs_cap) {
+            spec_valid = false;
+            L.obs_cap = n_obs;
+            return -1;
+        }
+        std::memcpy(f.mp_idx.data(), hb + 2, (size_t)nkp * sizeof(int));
+        obs.clear();
+        for (int i = 0; i < n_obs; i++) obs.emplace_back(hb[2 + nkp + i], hb[2 + nkp + L.obs_cap + i]);
+        return hb[0];
+    }
+
+    // ---- round 6: speculative local-map tracking of the batch's next frame ----------------------
+    // While frame i's tracking kernels run, the next frame's front chain (the speculative chain on s2)
+    // is read back as soon as it lands, the next-but-one frame's chain is launched, and — when the
+    // tracker's rules make frame i a non-keyframe and the next frame's path plain
+    // (Tracker::predict_next_pose) — the next frame's local-map tracking + PnP is enqueued behind frame
+    // i's at the predicted pose, into its own work area and pinned block.  Frame i + 1's
+    // track_local_map uses it only when its frame, slot, keypoints, pose (bit for bit), map size and
+    // map version equal the speculation's: the results are then the ones the call would compute.
+    std::function<bool(const vs_trk::Frame&, const vs_trk::Frame&, const vs_trk::ChainResult&, const vs_trk::Frame**,
+                       vs_trk::M3&, vs_trk::V3&)>
+        predict;                  // Tracker::predict_next_pose (set by vs_slam_create)
+    bool tlm_spec_on = true;      // VS_SLAM_SPEC_TLM=0 disables
+    bool next_kps_ready = false;  // the next frame's keypoints are on the host (its chunk was waited)
+    const vs_trk::Frame* next2_frame = nullptr;  // the frame after it, and its chunk's event
+    hipEvent_t next2_ready = nullptr;
+    struct NextChain {  // the next frame's chain, read back ahead of its chain() call
+        bool valid = false, launched_next = false;
+        const vs_trk::Frame* cur = nullptr;
+        int ref_slot = -1, cur_slot = -1;
+        uint32_t seed = 0;
+        vs_trk::ChainResult R;
+    } cnext;
+    struct TlmSpec {
+        bool valid = false;
+        const vs_trk::Frame* f = nullptr;
+        int slot = -1, map_n = 0;
+        long map_ver = 0;
+        vs_trk::M3 R;
+        vs_trk::V3 t;
+        TlmLaunch L;
+        hipEvent_t ev = nullptr;
+    } tspec;
+    DevBuf work2;
+    Pinned spin{hipHostMallocCoherent | hipHostMallocMapped};  // the speculation's pinned block (never reset)
+    hipEvent_t tlm_ev = nullptr;  // the direct launch's copy has landed
+    long map_ver = 0;             // bumped by every map append and valid-flag change
+    long tspec_launched = 0, tspec_hits = 0;
+
+    // Reads the next frame's speculative chain back (waiting for it) into cnext.
+    bool take_next_chain(const vs_trk::Frame* nxt) {
+        spec_sync();
+        if (!(cspec.valid && cspec.cur == nxt)) return false;
+        HostTimer hw(hprof, kHSpecNext);
+        if (failed(hipEventSynchronize(cspec_ev) == hipSuccess ? VS_OK : VS_ERR_HIP)) return false;
+        cnext.R = parse_chain(cpin.base + kHdrBytes);
+        cnext.valid = true;
+        cnext.launched_next = false;
+        cnext.cur = cspec.cur;
+        cnext.ref_slot = cspec.ref_slot;
+        cnext.cur_slot = cspec.cur_slot;
+        cnext.seed = cspec.seed;
+        cspec.valid = false;
+        cspec_hits++;
+        return true;
+    }
+    void speculate_next(const vs_trk::Map& m, const vs_trk::Frame& f) {
+        const vs_trk::Frame* nxt = next_frame;
+        if (!tlm_spec_on || !predict || err != VS_OK || !nxt || !next_kps_ready || nxt->slot < 0 || valid_dirty ||
+            nxt->kps.empty() || nxt->kps.size() > 1024)
+            return;
+        if (!std::all_of(nxt->mp_idx.begin(), nxt->mp_idx.end(), [](int v) { return v < 0; })) return;
+        if (!cnext.valid && !take_next_chain(nxt)) return;
+        if (!(cnext.valid && cnext.cur == nxt)) return;
+        const vs_trk::Frame* ref = nullptr;
+        vs_trk::M3 R;
+        vs_trk::V3 t;
+        if (!predict(f, *nxt, cnext.R, &ref, R, t) || !ref || ref->slot != cnext.ref_slot || nxt->slot != cnext.cur_slot)
+            return;
+        // the frame after it: its chain against the reference chain() would predict (the rule of
+        // chain(): the next frame becomes a keyframe by the id gap and its match count)
+        if (!cnext.launched_next && cspec_on && next2_frame && next2_frame->slot >= 0) {
+            const int ng = (int)cnext.R.good.size(), gap = nxt->id - ref->id;
+            const bool kf = (gap >= vs_trk::cfg::KF_MIN_FRAME_GAP && ng >= vs_trk::cfg::KF_MIN_MATCHES) ||
+                            (ng < 2 * vs_trk::cfg::MIN_MATCHES && gap >= 5);
+            if (failed(launch_spec_chain(kf ? nxt->slot : ref->slot, *next2_frame, cnext.seed + 1u, next2_ready))) return;
+            cnext.launched_next = true;
+        }
+        const int nkp = (int)nxt->kps.size();
+        TlmSpec& T = tspec;
+        T.valid = false;
+        char* hk = spin.base;
+        char* ha = spin.base + 8192;
+        if (failed(enqueue_tlm(m, *nxt, R.data(), t.data(), std::max(4 * nkp, 64), work2, hk, ha, spin.cap - 8192, T.L)))
+            return;
+        if (failed(hipEventRecord(T.ev, s) == hipSuccess ? VS_OK : VS_ERR_HIP)) return;
+        T.valid = true;
+        T.f = nxt;
+        T.slot = nxt->slot;
+        T.map_n = m.size();
+        T.map_ver = map_ver;
+        T.R = R;
+        T.t = t;
+        tspec_launched++;
+    }
+
     int track_local_map(vs_trk::Map& m, vs_trk::Frame& f, std::vector<std::pair<int, int>>& obs) {
         HostTimer ht(hprof, kHTlm);
         obs.clear();
         const int nkp = (int)f.kps.size();
         if (failed(sync_valid(m))) return 0;
-        int obs_cap = std::max(4 * nkp, 64);
-        for (int attempt = 0; attempt < 2; attempt++) {
-            // one device block, read back with ONE copy: [tracking words | speculative PnP io + result]
-            const int words = 2 + nkp + 2 * obs_cap;
-            const size_t wbytes = ((size_t)words * sizeof(int) + 255) & ~(size_t)255;
-            spec_valid = false;
-            const int cap = std::max(nkp, 1);
-            const size_t io_bytes = 16 + (size_t)cap * 5 * sizeof(float), io_pad = (io_bytes + 15) & ~(size_t)15;
-            const size_t spec_bytes = io_pad + 12 * sizeof(double) + 8 * sizeof(int);
-            const bool spec_on = nkp > 0 && nkp <= 1024;
-            const size_t total = wbytes + (spec_on ? spec_bytes + (size_t)cap : 0);
-            if (failed(work.ensure(total))) return 0;
-            int* d = work.as<int>();
-            int* d_kpmp = d + 2;
-            int* d_obs = d + 2 + nkp;
-            // the kp -> map-point table goes in through pinned memory that k_tlm_grid reads itself
-            int* h_kpmp = reinterpret_cast<int*>(take((size_t)std::max(nkp, 1) * sizeof(int)));
-            if (!h_kpmp) return 0;
-            std::memcpy(h_kpmp, f.mp_idx.data(), (size_t)nkp * sizeof(int));
-            // Speculatively, the refinement's PnP on the tracked points right behind it (the tracker calls
-            // solve_pnp on exactly these next, Slam.cpp:1057-1059; solve_pnp checks); its input gathered
-            // by the resolve kernel itself (round 6: no gather kernel), the grid built at extraction.
-            char* io = work.as<char>() + wbytes;
-            vs::TlmExtra ex;
-            ex.grid = pre_grid && (int)f.kps.size() <= 1024 ? grid_of(f.slot) : nullptr;
-            if (spec_on) {
-                ex.gather_io = reinterpret_cast<float*>(io);
-                ex.gather_cap = cap;
-            }
-            if (failed(vs::track_local_map(ctx, map_pos.as<double>(), map_desc.as<float>(), map_valid.as<uint8_t>(),
-                                           m.size(), kps_of(f.slot), desc_of(f.slot), nkp, f.R.data(), f.t.data(), K,
-                                           vs_trk::cfg::IMAGE_WIDTH, vs_trk::cfg::IMAGE_HEIGHT, d_kpmp, d_obs,
-                                           d_obs + obs_cap, obs_cap, d, s, h_kpmp, &ex)))
-                return 0;
-            bool spec_run = false;
-            if (spec_on) {
-                double* dRt = reinterpret_cast<double*>(io + io_pad);
-                int* dstat = reinterpret_cast<int*>(dRt + 12);
-                spec_run = vs::solve_pnp(ctx, 1, reinterpret_cast<const float*>(io + 16),
-                                         reinterpret_cast<const float*>(io + 16 + (size_t)cap * 3 * sizeof(float)),
-                                         reinterpret_cast<const int*>(io), K, 100, 10, dRt, dRt + 9, dstat,
-                                         reinterpret_cast<uint8_t*>(dstat + 8), s, cap) == VS_OK;
-            }
-            const size_t rb = wbytes + (spec_run ? spec_bytes : 0);
-            char* hall = take(rb);
-            if (!hall || failed(d2h(hall, work.p, rb))) return 0;
-            int* hb = reinterpret_cast<int*>(hall);
-            char* hs = spec_run ? hall + wbytes : nullptr;
-            flush_spec();  // the next frame's chain, launched while these kernels run
+        TlmSpec& T = tspec;
+        const bool hit = T.valid && T.f == &f && T.slot == f.slot && T.L.nkp == nkp && T.map_n == m.size() &&
+                         T.map_ver == map_ver && std::memcmp(T.R.data(), f.R.data(), sizeof(T.R)) == 0 &&
+                         std::memcmp(T.t.data(), f.t.data(), sizeof(T.t)) == 0 &&
+                         std::all_of(f.mp_idx.begin(), f.mp_idx.end(), [](int v) { return v < 0; });
+        T.valid = false;
+        if (hit) {
+            tspec_hits++;
+            TlmLaunch L = T.L;
+            hipEvent_t ev = T.ev;
+            // the speculation's copy block stays untouched until the next speculation is enqueued,
+            // which waits for nothing of ours: read it first
             {
                 HostTimer hs(hprof, kHTlmSync);
-                if (failed(sync())) return 0;
+                if (failed(hipEventSynchronize(ev) == hipSuccess ? VS_OK : VS_ERR_HIP)) return 0;
             }
-            if (hs) {
-                const int n = reinterpret_cast<const int*>(hs)[1];
-                const float* so = reinterpret_cast<const float*>(hs + 16);
-                spec_obj.assign(so, so + (size_t)3 * n);
-                spec_img.assign(so + (size_t)3 * cap, so + (size_t)3 * cap + (size_t)2 * n);
-                const double* Rt = reinterpret_cast<const double*>(hs + io_pad);
-                const int* st = reinterpret_cast<const int*>(Rt + 12);
-                spec = vs_trk::PnPResult();
-                spec.success = n > 0 && st[0] != 0;
-                spec.inlier_count = spec.success ? st[1] : 0;
-                if (spec.success) {
-                    std::memcpy(spec.R_world.data(), Rt, 9 * sizeof(double));
-                    std::memcpy(spec.t_world.data(), Rt + 9, 3 * sizeof(double));
-                }
-                spec_valid = true;
+            std::vector<std::pair<int, int>> o2;
+            std::vector<int> kpmp_save = f.mp_idx;
+            const int tracked = read_tlm(f, L, o2);
+            const bool spec_ok = spec_valid;
+            const vs_trk::PnPResult sp = spec;
+            const std::vector<float> so = spec_obj, si = spec_img;
+            if (tracked >= 0) {
+                obs.swap(o2);
+                flush_spec();
+                speculate_next(m, f);  // the frame after this one, behind nothing of ours
+                spec_valid = spec_ok;  // (speculate_next does not touch the PnP speculation, but be explicit)
+                spec = sp;
+                spec_obj = so;
+                spec_img = si;
+                return tracked;
             }
-            const int n_obs = hb[1];
-            if (n_obs > obs_cap) {  // rerun from the same inputs with room for every observation
-                obs_cap = n_obs;
-                continue;
+            f.mp_idx = kpmp_save;  // overflowed: the direct path below with the exact capacity
+        }
+        int obs_cap = std::max(4 * nkp, 64);
+        for (int attempt = 0; attempt < 2; attempt++) {
+            char* hk = take((size_t)std::max(nkp, 1) * sizeof(int));
+            const int words = 2 + nkp + 2 * obs_cap;
+            const int cap = std::max(nkp, 1);
+            const size_t rb = (((size_t)words * sizeof(int) + 255) & ~(size_t)255) + ((16 + (size_t)cap * 20 + 15) & ~(size_t)15) +
+                              12 * sizeof(double) + 8 * sizeof(int);
+            char* ha = hk ? take(rb) : nullptr;
+            if (!hk || !ha) return 0;
+            TlmLaunch L;
+            if (failed(enqueue_tlm(m, f, f.R.data(), f.t.data(), obs_cap, work, hk, ha, rb, L))) return 0;
+            if (failed(hipEventRecord(tlm_ev, s) == hipSuccess ? VS_OK : VS_ERR_HIP)) return 0;
+            flush_spec();  // the next frame's chain, launched while these kernels run
+            if (attempt == 0) speculate_next(m, f);
+            {
+                HostTimer hs(hprof, kHTlmSync);
+                if (failed(hipEventSynchronize(tlm_ev) == hipSuccess ? VS_OK : VS_ERR_HIP)) return 0;
             }
-            std::memcpy(f.mp_idx.data(), hb + 2, (size_t)nkp * sizeof(int));
-            for (int i = 0; i < n_obs; i++) obs.emplace_back(hb[2 + nkp + i], hb[2 + nkp + obs_cap + i]);
-            return hb[0];
+            pin.used = 0;  // every pinned transfer of ours is before tlm_ev (the speculation uses spin)
+            const int tracked = read_tlm(f, L, obs);
+            if (tracked >= 0) return tracked;
+            obs_cap = L.obs_cap;  // rerun from the same inputs with room for every observation
         }
         failed(VS_ERR_CAPACITY);
         return 0;
@@ -1545,6 +1725,7 @@ struct GpuOps {
     void map_append(const vs_trk::Map& m, int first, const vs_trk::Frame& src, const std::vector<int>& rows) {
         HostTimer ht(hprof, kHAppend);
         const int k = (int)rows.size();
+        map_ver++;
         if (failed(grow_map(first + k))) return;
         if (k == 0) {
             map_n = first;
@@ -1569,7 +1750,10 @@ struct GpuOps {
         // the same stream, and the pinned staging it came from is recycled only at a sync()
     }
 
-    void map_valid_changed() { valid_dirty = true; }
+    void map_valid_changed() {
+        valid_dirty = true;
+        map_ver++;
+    }
 
     void visibility(const vs_trk::Map& m, const vs_trk::Frame& f, const vs_trk::M3& R, const vs_trk::V3& t,
                     std::vector<uint8_t>& flags) {
@@ -1721,6 +1905,11 @@ int vs_slam_create(vs_ctx* ctx, int max_batch, int h, int w, vs_slam** out) {
         return rc;
     }
     sl->trk = std::make_unique<vs_trk::Tracker<GpuOps>>(sl->ops);
+    vs_trk::Tracker<GpuOps>* trk = sl->trk.get();
+    sl->ops.predict = [trk](const vs_trk::Frame& cur, const vs_trk::Frame& nxt, const vs_trk::ChainResult& C,
+                            const vs_trk::Frame** ref, vs_trk::M3& R, vs_trk::V3& t) {
+        return trk->predict_next_pose(cur, nxt, C, ref, R, t);
+    };
     if (const char* p = std::getenv("VS_TRACE_GPU")) sl->trace = std::fopen(p, "w");
     sl->trk->set_trace(sl->trace);
     *out = sl;
@@ -1737,6 +1926,8 @@ void vs_slam_destroy(vs_slam* sl) {
                              o.hprof.n[k], o.hprof.ms[k], 1e3 * o.hprof.ms[k] / o.hprof.n[k]);
     if (o.hprof.on) {
         std::fprintf(stderr, "vs_slam speculative chains: %ld launched, %ld used\n", o.cspec_launched, o.cspec_hits);
+        std::fprintf(stderr, "vs_slam speculative next-frame local-map tracking: %ld launched, %ld used\n",
+                     o.tspec_launched, o.tspec_hits);
         const vs_trk::PhaseProf& ph = sl->trk->phase_prof();
         for (int k = 0; k < vs_trk::PH_N; k++)
             if (ph.n[k])
@@ -1804,9 +1995,19 @@ int vs_slam_process_batch_dev(vs_slam* sl, int B, const uint8_t* d_bgr, const fl
         const auto& X = o.xb[o.xcur];
         if (b == X.ch[c]) rc = o.wait_chunk(sl->batch, c++);
         if (rc != VS_OK) break;
-        // the next frame and its chunk's event, for the speculative chain (chain())
+        // the next frame and its chunk's event, for the speculative chain (chain()); the frame after
+        // it, for the read-ahead of speculate_next
         o.next_frame = b + 1 < B ? sl->batch[b + 1].get() : nullptr;
         o.next_ready = b + 1 < B ? X.ev[b + 1 == X.ch[c] ? c : c - 1] : nullptr;
+        o.next_kps_ready = b + 1 < X.ch[c];  // the next frame's chunk was waited (host keypoints)
+        o.next2_frame = b + 2 < B ? sl->batch[b + 2].get() : nullptr;
+        if (b + 2 < B) {
+            int c2 = c;
+            while (b + 2 >= X.ch[c2]) c2++;
+            o.next2_ready = X.ev[c2 - 1];
+        } else {
+            o.next2_ready = nullptr;
+        }
         if (o.hprof_armed && --o.hprof.skip < 0) o.hprof.on = sl->trk->phase_prof().on = true, o.hprof_armed = false;
         {
             HostTimer ht(o.hprof, kHFrame);
@@ -1821,7 +2022,12 @@ int vs_slam_process_batch_dev(vs_slam* sl, int B, const uint8_t* d_bgr, const fl
     }
     o.next_frame = nullptr;
     o.next_ready = nullptr;
+    o.next2_frame = nullptr;
+    o.next2_ready = nullptr;
+    o.next_kps_ready = false;
     o.spec_sync();
+    o.cnext.valid = false;  // (no speculation outlives the call: its frames may go)
+    o.tspec.valid = false;
     if (rc == VS_OK && o.err != VS_OK) rc = o.err;
     o.err = VS_OK;
     o.cspec.valid = false;

@@ -420,22 +420,8 @@ class Tracker {
 
         // :986-1047 EKF predict + update
         {
-            if (!ekf_init_) ekf_initialize(t_world_, frame->timestamp);
-            const double dt = frame->timestamp - last_frame_time_;
-            const double ekf_dt = dt;
-            if (dt > 0 && dt < 1.0) ekf_predict(dt);
             Snapshot snap;
-            std::memcpy(snap.x_pred, x_, sizeof(x_));
-            std::memcpy(snap.P_pred, P_, sizeof(P_));
-            const double sigma_vis = use_3d3d ? cfg::EKF_SIGMA_VIS_3D3D : cfg::EKF_SIGMA_VIS_EMAT;
-            const V3 dinn{t_new[0] - x_[0], t_new[1] - x_[1], t_new[2] - x_[2]};
-            const double innovation = norm3(dinn);
-            if (innovation < cfg::EKF_INNOV_GATE)
-                ekf_update_visual(t_new, sigma_vis);
-            else
-                ekf_update_visual(t_new, innovation * 0.5);
-            if (has_gravity_ && has_initial_height_) ekf_update_height(initial_height_, cfg::EKF_SIGMA_HEIGHT);
-            std::memcpy(snap.P_filt, P_, sizeof(P_));
+            const double ekf_dt = ekf_fuse(t_new, use_3d3d, frame->timestamp, &snap);
             V3 ekf_pos{x_[0], x_[1], x_[2]};
             V3 delta{ekf_pos[0] - t_world_[0], ekf_pos[1] - t_world_[1], ekf_pos[2] - t_world_[2]};
             const double step = norm3(delta);
@@ -503,6 +489,53 @@ class Tracker {
         last_frame_ = frame;
         frame_count_++;
         stats_.processed++;
+        return true;
+    }
+
+    // Round 6 (back-end speculation, no state change): the pose the NEXT frame `nxt` will get at
+    // Slam.cpp:953-1047 from its front-chain result C (match -> F -> 3D-3D / E against `ref`), computed
+    // now, while `cur`'s local-map tracking runs.  Only where the plain path is certain: `cur` (the
+    // frame being processed, past its motion and EKF step) does not become a keyframe (:1061-1072 decide
+    // that from its match count and id gap, already known), `nxt` has enough keypoints and matches that
+    // no bridge (:847), recovery (:875) or stationary branch (:913-951) can run, and the EKF runs.  The
+    // pose is the EKF position before the step clamp (:1026-1033), which depends on `cur`'s refined
+    // pose: the back end checks the prediction bit for bit against the pose process_frame then sets,
+    // so a clamped (or otherwise different) step only costs the speculation.  ref_out: the frame the
+    // next chain must have matched against.
+    bool predict_next_pose(const Frame& cur, const Frame& nxt, const ChainResult& C, const Frame** ref_out, M3& R,
+                           V3& t) {
+        if (cur.keyframe || !last_keyframe_ || !ekf_init_) return false;
+        if (!accel_.empty() || was_stationary_) return false;
+        if (last_match_count_ < cfg::MIN_MATCHES * 2 && cur.id - last_keyframe_->id >= 5) return false;  // proactive kf
+        if (cur.id - last_keyframe_->id >= cfg::KF_MIN_FRAME_GAP && last_match_count_ >= cfg::KF_MIN_MATCHES)
+            return false;  // regular keyframe (is_keyframe with a last keyframe)
+        if ((int)nxt.kps.size() < cfg::MIN_MATCHES || (int)C.good.size() < cfg::MIN_MATCHES) return false;
+        if (!C.ok3d && !C.okE) return false;
+        const Frame* ref = last_keyframe_->has_desc() ? last_keyframe_.get() : &cur;
+        M3 R_new;
+        V3 t_new;
+        if (C.ok3d) {
+            R_new = mul_bt(ref->R, C.R3);
+            const V3 m = mulv(R_new, C.t3);
+            t_new = {ref->t[0] - m[0], ref->t[1] - m[1], ref->t[2] - m[2]};
+        } else {
+            const double scale = C.scale > 0 ? C.scale : (last_good_scale_ > 0 ? last_good_scale_ : cfg::MOTION_SCALE);
+            R_new = mul_bt(ref->R, C.RE);
+            const V3 st{scale * C.tE[0], scale * C.tE[1], scale * C.tE[2]};
+            const V3 m = mulv(R_new, st);
+            t_new = {ref->t[0] - m[0], ref->t[1] - m[1], ref->t[2] - m[2]};
+        }
+        double x0[6], P0[36];
+        std::memcpy(x0, x_, sizeof(x_));
+        std::memcpy(P0, P_, sizeof(P_));
+        const double lft = last_frame_time_;
+        ekf_fuse(t_new, C.ok3d, nxt.timestamp, nullptr);
+        t = V3{x_[0], x_[1], x_[2]};
+        std::memcpy(x_, x0, sizeof(x_));
+        std::memcpy(P_, P0, sizeof(P_));
+        last_frame_time_ = lft;
+        R = R_new;
+        *ref_out = ref;
         return true;
     }
 
@@ -1234,6 +1267,28 @@ class Tracker {
                     if (std::abs(w[k]) > tol) s += V[i * 6 + k] * V[j * 6 + k] / w[k];
                 out[i * 6 + j] = s;
             }
+    }
+    // :986-1016: EKF initialisation / prediction / visual update (innovation gate) / height update for
+    // the motion estimate t_new of a frame at time ts; the snapshot's predicted and filtered parts when
+    // given; returns the prediction interval.  x_ then holds the fused state (before the step clamp).
+    double ekf_fuse(const V3& t_new, bool use_3d3d, double ts, Snapshot* snap) {
+        if (!ekf_init_) ekf_initialize(t_world_, ts);
+        const double dt = ts - last_frame_time_;
+        if (dt > 0 && dt < 1.0) ekf_predict(dt);
+        if (snap) {
+            std::memcpy(snap->x_pred, x_, sizeof(x_));
+            std::memcpy(snap->P_pred, P_, sizeof(P_));
+        }
+        const double sigma_vis = use_3d3d ? cfg::EKF_SIGMA_VIS_3D3D : cfg::EKF_SIGMA_VIS_EMAT;
+        const V3 dinn{t_new[0] - x_[0], t_new[1] - x_[1], t_new[2] - x_[2]};
+        const double innovation = norm3(dinn);
+        if (innovation < cfg::EKF_INNOV_GATE)
+            ekf_update_visual(t_new, sigma_vis);
+        else
+            ekf_update_visual(t_new, innovation * 0.5);
+        if (has_gravity_ && has_initial_height_) ekf_update_height(initial_height_, cfg::EKF_SIGMA_HEIGHT);
+        if (snap) std::memcpy(snap->P_filt, P_, sizeof(P_));
+        return dt;
     }
     void ekf_initialize(const V3& pos, double ts) {
         for (int i = 0; i < 6; i++) x_[i] = i < 3 ? pos[i] : 0.0;
