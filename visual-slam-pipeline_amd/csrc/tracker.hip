@@ -1320,10 +1320,15 @@ struct GpuOps {
     // track_local_map uses it only when its frame, slot, keypoints, pose (bit for bit), map size and
     // map version equal the speculation's: the results are then the ones the call would compute.
     std::function<bool(const vs_trk::Frame&, const vs_trk::Frame&, const vs_trk::ChainResult&, const vs_trk::Frame**,
-                       vs_trk::M3&, vs_trk::V3&)>
+                       vs_trk::M3&, vs_trk::V3&, bool)>
         predict;                  // Tracker::predict_next_pose (set by vs_slam_create)
     bool tlm_spec_on = true;      // VS_SLAM_SPEC_TLM=0 disables
     bool next_kps_ready = false;  // the next frame's keypoints are on the host (its chunk was waited)
+    // the batch being tracked and its next chunk to wait (process_batch_dev's loop): speculate_next waits
+    // for the chunk of a next frame that starts one, instead of skipping the speculation
+    std::vector<vs_trk::FramePtr>* bframes = nullptr;
+    int* bchunk = nullptr;
+    int next_index = -1;
     const vs_trk::Frame* next2_frame = nullptr;  // the frame after it, and its chunk's event
     hipEvent_t next2_ready = nullptr;
     struct NextChain {  // the next frame's chain, read back ahead of its chain() call
@@ -1368,16 +1373,25 @@ struct GpuOps {
     }
     void speculate_next(const vs_trk::Map& m, const vs_trk::Frame& f) {
         const vs_trk::Frame* nxt = next_frame;
-        if (!tlm_spec_on || !predict || err != VS_OK || !nxt || !next_kps_ready || nxt->slot < 0 || valid_dirty ||
-            nxt->kps.empty() || nxt->kps.size() > 1024)
-            return;
-        if (!std::all_of(nxt->mp_idx.begin(), nxt->mp_idx.end(), [](int v) { return v < 0; })) return;
+        if (!tlm_spec_on || !predict || err != VS_OK || !nxt || nxt->slot < 0 || valid_dirty) return;
         if (!cnext.valid && !take_next_chain(nxt)) return;
         if (!(cnext.valid && cnext.cur == nxt)) return;
         const vs_trk::Frame* ref = nullptr;
         vs_trk::M3 R;
         vs_trk::V3 t;
-        if (!predict(f, *nxt, cnext.R, &ref, R, t) || !ref || ref->slot != cnext.ref_slot || nxt->slot != cnext.cur_slot)
+        if (!next_kps_ready && bframes && bchunk) {  // the next frame opens a chunk: wait for it now (once
+            const XBatch& X = xb[xcur];             // this frame is known to stay a non-keyframe, whose
+            const int c = *bchunk;                   // remaining work then needs nothing on this stream)
+            if (c + 1 < (int)X.ch.size() && next_index == X.ch[c] && predict(f, *nxt, cnext.R, &ref, R, t, true)) {
+                if (failed(wait_chunk(*bframes, c))) return;
+                ++*bchunk;
+                next_kps_ready = true;
+            }
+        }
+        if (!next_kps_ready || nxt->kps.empty() || nxt->kps.size() > 1024) return;
+        if (!std::all_of(nxt->mp_idx.begin(), nxt->mp_idx.end(), [](int v) { return v < 0; })) return;
+        if (!predict(f, *nxt, cnext.R, &ref, R, t, false) || !ref || ref->slot != cnext.ref_slot ||
+            nxt->slot != cnext.cur_slot)
             return;
         // the frame after it: its chain against the reference chain() would predict (the rule of
         // chain(): the next frame becomes a keyframe by the id gap and its match count)
@@ -1385,7 +1399,16 @@ struct GpuOps {
             const int ng = (int)cnext.R.good.size(), gap = nxt->id - ref->id;
             const bool kf = (gap >= vs_trk::cfg::KF_MIN_FRAME_GAP && ng >= vs_trk::cfg::KF_MIN_MATCHES) ||
                             (ng < 2 * vs_trk::cfg::MIN_MATCHES && gap >= 5);
-            if (failed(launch_spec_chain(kf ? nxt->slot : ref->slot, *next2_frame, cnext.seed + 1u, next2_ready))) return;
+            const int rs = kf ? nxt->slot : ref->slot;
+            const vs_trk::Frame* n2 = next2_frame;
+            const uint32_t sd = cnext.seed + 1u;
+            hipEvent_t rdy = next2_ready;
+            if (spec_async) {  // ~40 us of HIP calls, on the helper beside this thread's tracking launch
+                spec_inflight = true;
+                sq.submit([this, rs, n2, sd, rdy] { return launch_spec_chain(rs, *n2, sd, rdy); });
+            } else if (failed(launch_spec_chain(rs, *n2, sd, rdy))) {
+                return;
+            }
             cnext.launched_next = true;
         }
         const int nkp = (int)nxt->kps.size();
@@ -1907,8 +1930,8 @@ int vs_slam_create(vs_ctx* ctx, int max_batch, int h, int w, vs_slam** out) {
     sl->trk = std::make_unique<vs_trk::Tracker<GpuOps>>(sl->ops);
     vs_trk::Tracker<GpuOps>* trk = sl->trk.get();
     sl->ops.predict = [trk](const vs_trk::Frame& cur, const vs_trk::Frame& nxt, const vs_trk::ChainResult& C,
-                            const vs_trk::Frame** ref, vs_trk::M3& R, vs_trk::V3& t) {
-        return trk->predict_next_pose(cur, nxt, C, ref, R, t);
+                            const vs_trk::Frame** ref, vs_trk::M3& R, vs_trk::V3& t, bool cur_only) {
+        return trk->predict_next_pose(cur, nxt, C, ref, R, t, cur_only);
     };
     if (const char* p = std::getenv("VS_TRACE_GPU")) sl->trace = std::fopen(p, "w");
     sl->trk->set_trace(sl->trace);
@@ -2000,6 +2023,9 @@ int vs_slam_process_batch_dev(vs_slam* sl, int B, const uint8_t* d_bgr, const fl
         o.next_frame = b + 1 < B ? sl->batch[b + 1].get() : nullptr;
         o.next_ready = b + 1 < B ? X.ev[b + 1 == X.ch[c] ? c : c - 1] : nullptr;
         o.next_kps_ready = b + 1 < X.ch[c];  // the next frame's chunk was waited (host keypoints)
+        o.bframes = &sl->batch;
+        o.bchunk = &c;
+        o.next_index = b + 1;
         o.next2_frame = b + 2 < B ? sl->batch[b + 2].get() : nullptr;
         if (b + 2 < B) {
             int c2 = c;
@@ -2025,6 +2051,9 @@ int vs_slam_process_batch_dev(vs_slam* sl, int B, const uint8_t* d_bgr, const fl
     o.next2_frame = nullptr;
     o.next2_ready = nullptr;
     o.next_kps_ready = false;
+    o.bframes = nullptr;
+    o.bchunk = nullptr;
+    o.next_index = -1;
     o.spec_sync();
     o.cnext.valid = false;  // (no speculation outlives the call: its frames may go)
     o.tspec.valid = false;

@@ -502,13 +502,15 @@ class Tracker {
     // pose: the back end checks the prediction bit for bit against the pose process_frame then sets,
     // so a clamped (or otherwise different) step only costs the speculation.  ref_out: the frame the
     // next chain must have matched against.
+    // cur_only: only the conditions on `cur` (nxt and C unused).
     bool predict_next_pose(const Frame& cur, const Frame& nxt, const ChainResult& C, const Frame** ref_out, M3& R,
-                           V3& t) {
+                           V3& t, bool cur_only = false) {
         if (cur.keyframe || !last_keyframe_ || !ekf_init_) return false;
         if (!accel_.empty() || was_stationary_) return false;
         if (last_match_count_ < cfg::MIN_MATCHES * 2 && cur.id - last_keyframe_->id >= 5) return false;  // proactive kf
         if (cur.id - last_keyframe_->id >= cfg::KF_MIN_FRAME_GAP && last_match_count_ >= cfg::KF_MIN_MATCHES)
             return false;  // regular keyframe (is_keyframe with a last keyframe)
+        if (cur_only) return true;
         if ((int)nxt.kps.size() < cfg::MIN_MATCHES || (int)C.good.size() < cfg::MIN_MATCHES) return false;
         if (!C.ok3d && !C.okE) return false;
         const Frame* ref = last_keyframe_->has_desc() ? last_keyframe_.get() : &cur;
