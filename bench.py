@@ -65,6 +65,7 @@ CONV1_MIN_BYTES_PER_FRAME = 480 * 640 * 4 + 240 * 320 * 64 * 4
 # 1 KB descriptor gathers 1,638,400 + heatmap write and read 1,228,800 + 420,800 of records out
 POST_BYTES_PER_FRAME = 1248000 + 1638400 + 1228800 + 420800
 LOOP_FRAMES = 126               # one lap of synth.loop_trajectory (0.3 m/s, 10 processed frames/s)
+FRONTEND_STEP_M = 0.01          # config[3]: every image of the 30 Hz stream (FRAME_STEP 1), 0.3 m/s
 PIONEER_FRAMES = 848            # freiburg2_pioneer_slam3: 2,544 images, every 3rd processed (README.md:5)
 T0 = 1311868164.0               # TUM-like timestamps, 0.1 s per processed frame (FRAME_STEP = 3)
 
@@ -427,26 +428,37 @@ def share_batch_id(rank, world, make_id, device="cpu", nbytes=128):
     return bytes(t.cpu().numpy().tobytes())
 
 
-def frontend_batch(ctx, L, B, rank, world, steps, warmup):
+def frontend_frame_indices(B, rank, world):
+    """config[3]'s frames on a rank: its B consecutive frames of the world * B-frame sequence and its halo
+    frame (the one before its first; rank 0's is the sequence's last, the previous pass's)."""
+    return list(range(rank * B, rank * B + B)), (rank * B - 1) % (world * B)
+
+
+def frontend_batch(ctx, B, rank, world, steps, warmup, workers=8):
     """BASELINE config[3]: the offline frame-sharded front end through the C ABI (vs_batch_submit_dev /
     vs_batch_collect, csrc/batch.hip — the path INTEGRATION.md gives a C++ driver): per step each rank
     extracts its B frames, receives its halo frame's record over RCCL (point-to-point ring) and runs
     match + F verification + 3D-3D RANSAC + E fallback on the B pairs ending in its frames, the next
     step's network overlapping this step's geometry.  B = the per-GPU shard of the 2,544-image sequence
-    (FRAME_STEP 1: 2544 / 8 = 318), so at 8 GPUs one step is the whole sequence."""
+    (FRAME_STEP 1: 2544 / 8 = 318), so at 8 GPUs one step is the whole sequence.
+
+    Input: world * B distinct frames of the Pioneer-like drive at FRAME_STEP 1 spacing
+    (synth.pioneer_trajectory with 0.01 m per frame, a third of the tracked drive's); each rank renders its
+    own B frames plus its halo frame (rank * B - 1).  Every step is the same offline pass over the
+    sequence, so rank 0's halo after the first step is the sequence's last frame (one seam pair per step)."""
     import torch
     import torch.distributed as dist
 
     import vslam_abi
-    U = len(L["bgr"])
     n_total = world * B
     dev = torch.device("cuda", torch.cuda.current_device())
-    # the rank's frames of every step (the synthetic loop repeats every U frames; consecutive frames
-    # stay consecutive across the lap seam)
-    idx = [(rank * B + j) % U for j in range(B)]
-    frames = torch.from_numpy(L["bgr"][idx]).to(dev)
-    depth = torch.from_numpy(L["depth"][idx]).to(dev)
-    depth_prev = torch.from_numpy(L["depth"][(rank * B - 1) % U]).to(dev)
+    poses = synth.pioneer_trajectory(n_total, step=FRONTEND_STEP_M)
+    own, halo_idx = frontend_frame_indices(B, rank, world)
+    fb, fd = synth.render_frames(poses, own + [halo_idx], workers=workers)
+    frames = torch.from_numpy(fb[:B]).to(dev)
+    depth = torch.from_numpy(fd[:B]).to(dev)
+    depth_prev = torch.from_numpy(fd[B]).to(dev)
+    del fb, fd
     # rank 0's RCCL communicator id, distributed over the torch process group
     uid = share_batch_id(rank, world, vslam_abi.batch_unique_id, dev,
                          getattr(vslam_abi, "VS_BATCH_ID_BYTES", 128))
@@ -674,7 +686,7 @@ def main():
     # at least the reference sequence's 848 processed frames (2,544 images at FRAME_STEP 3,
     # main.cpp:1096-1107) and every frame the run tracks distinct; each rank renders every world-th frame
     # and the ranks all-gather them (replicas: every GPU tracks the same drive).  The closed loop
-    # (synth.loop_sequence) stays the input of the config[3] batch front end.
+    # (synth.loop_sequence) is the monocular stream's (config[4]); config[3] renders its own drive frames.
     workers = args.render_workers or max(1, min(16, (os.cpu_count() or 1) // max(world, 1)))
     n_path, ranges = headline_plan(B, args.warmup, args.steps,
                                    args.track_profile_steps if args.stage_profile != "all" else 0)
@@ -704,7 +716,6 @@ def main():
     hdep = [hdep_all[i] for i in range(n_path)]
     Lp["depth"] = hdep_all
     progress(f"{n_path}-frame drive rendered ({len(mine)} frames on this rank)")
-    L = synth.loop_sequence(LOOP_FRAMES, workers=workers)  # config[3]: the closed loop
 
     ctx = vslam_abi.Context(local if world > 1 else 0)
     slam = vslam_abi.Slam(ctx, max_batch=B)
@@ -866,7 +877,7 @@ def main():
     fe = None
     progress("config[3] batch front end")
     if not args.no_frontend and args.frontend_steps > 0:
-        fe = frontend_batch(ctx, L, args.frontend_frames, rank, world, args.frontend_steps, 1)
+        fe = frontend_batch(ctx, args.frontend_frames, rank, world, args.frontend_steps, 1, workers)
         P = fe.pop("_match_pairs")
         mroof["frontend_batch"] = match_roofline(fe.pop("_match"), P, 256,
                                                  f"config[3] batch front end's last step: {P} consecutive pairs of the "

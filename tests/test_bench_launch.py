@@ -113,6 +113,20 @@ def test_batch_schedule_keeps_two_steps_in_flight():
     assert bench.batch_schedule(submit, collect, 0, 1) == [0]
 
 
+@pytest.mark.parametrize("world", [1, 2, 8])
+def test_frontend_frames_are_distinct(world):
+    """config[3]'s ranks take disjoint, consecutive blocks of one world * B-frame drive
+    (no frame repeats), and each halo frame is the frame before the rank's block."""
+    B = 318
+    seen = []
+    for r in range(world):
+        own, halo = bench.frontend_frame_indices(B, r, world)
+        assert own == list(range(r * B, (r + 1) * B))
+        assert halo == (own[0] - 1) % (world * B)
+        seen += own
+    assert sorted(seen) == list(range(world * B))
+
+
 def test_batch_halo_rule():
     assert not bench.batch_halo_needed(0, 0, 1) and not bench.batch_halo_needed(5, 0, 1)  # no communicator
     assert not bench.batch_halo_needed(0, 0, 4)                                          # rank 0, first step

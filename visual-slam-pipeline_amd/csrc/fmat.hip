@@ -35,7 +35,7 @@ using namespace vs_fm;
 
 constexpr int kFmMaxPts = VS_FM_MAX_POINTS;
 constexpr int kMaxChunk = 256;
-constexpr int kThreads = 256;  // 4 wave64s, one per SIMD: the 7-point solver needs > 128 VGPRs (spills to AGPRs, not scratch)
+constexpr int kThreads = 512;  // 8 wave64s, two per SIMD: the 7-point solver needs > 128 VGPRs (<= 256 at two waves per SIMD)
 constexpr int kWaves = kThreads / 64;
 constexpr int kRawCap = 7 * kMaxChunk + 128;
 constexpr int kLevels = 8;  // pointer-doubling levels: 2^8 >= kMaxChunk attempts
@@ -81,7 +81,7 @@ struct FmShared {
     };
     int nmod[kMaxChunk];
     float score[kMaxChunk * 3];  // RANSAC: inlier count; LMedS: median error
-    int scan[kThreads];
+    int scan[kWaves];
     double F[9];
     uint64_t rng;
     int niters, best, best_iter, iter, fail_at, done, aborted, ok, chunk, inliers, serial_next, nchunk, navail,
@@ -422,23 +422,28 @@ __global__ __launch_bounds__(kThreads) void k_fmat(const int* __restrict__ pairs
         bits |= (uint32_t)in << (i - lo);
         local += in;
     }
-    S.scan[tid] = local;
-    __syncthreads();
-    if (tid == 0) {
-        int acc = 0;
-        for (int q = 0; q < kThreads; q++) {
-            const int c = S.scan[q];
-            S.scan[q] = acc;
-            acc += c;
-        }
-        S.inliers = acc;
+    // exclusive scan of the per-thread counts: wave shuffles, then the kWaves wave totals
+    int incl = local;
+    for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(incl, o);
+        if (lane >= o) incl += y;
     }
+    if (lane == 63) S.scan[wv] = incl;
+    __syncthreads();
+    int wbase = 0, total = 0;
+    for (int w = 0; w < kWaves; w++) {
+        const int c = S.scan[w];
+        wbase += w < wv ? c : 0;
+        total += c;
+    }
+    const int excl = wbase + incl - local;
+    if (tid == 0) S.inliers = total;
     __syncthreads();
     bool ok = have_f;
     if (method == 3 && have_f && S.inliers < 7) ok = false;  // LMeDS: result = count >= modelPoints
     // keep everything when F is empty (Slam.cpp:887, 892)
     {
-        int w = ok ? S.scan[tid] : lo;
+        int w = ok ? excl : lo;
         for (int i = lo; i < hi; i++) {
             const bool in = ok ? ((bits >> (i - lo)) & 1u) : true;
             if (mask_out) mask_out[(FROM_MATCHES ? (size_t)pb * cap : (size_t)off[pb]) + i] = ok ? in : 0;

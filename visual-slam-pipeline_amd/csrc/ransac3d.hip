@@ -193,7 +193,8 @@ __global__ __launch_bounds__(256) void k_ransac3d(const int* __restrict__ pairs,
                                                   const uint32_t* __restrict__ seeds,
                                                   const uint32_t* __restrict__ mt_init, int iters, double thr,
                                                   double* __restrict__ R_out, double* __restrict__ t_out,
-                                                  int* __restrict__ ok_out, int* __restrict__ diag_out) {
+                                                  int* __restrict__ ok_out, int* __restrict__ diag_out, int G,
+                                                  int* __restrict__ sync) {
     __shared__ D3 sP1[kMaxPts3d], sP2[kMaxPts3d];
     __shared__ uint32_t s_mt[kMtN], s_nw[kMtN], s_out[2 * kMtN];
     __shared__ int s_samp[kMaxIters3d * 3];
@@ -204,7 +205,7 @@ __global__ __launch_bounds__(256) void k_ransac3d(const int* __restrict__ pairs,
     __shared__ int s_start[kMaxIters3d];
     __shared__ int s_navail;
     __shared__ double s_in[6][kMaxPts3d];  // inlier coordinates for the refit
-    const int p = blockIdx.x;
+    const int p = blockIdx.x / G, g = blockIdx.x % G;  // G workgroups per pair share its hypotheses
     const int rf = pairs[2 * p], cf = pairs[2 * p + 1];
     const int n = min(ngood[p], kMaxPts3d);
     const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
@@ -249,8 +250,8 @@ __global__ __launch_bounds__(256) void k_ransac3d(const int* __restrict__ pairs,
         __syncthreads();
     }
     const int N = s_N;
-    if (N < 10) {
-        if (tid == 0) {
+    if (N < 10) {  // every workgroup of the pair sees the same N
+        if (tid == 0 && g == 0) {
             ok_out[p] = 0;
             diag_out[4 * p + 0] = N;
             diag_out[4 * p + 1] = 0;
@@ -354,21 +355,29 @@ __global__ __launch_bounds__(256) void k_ransac3d(const int* __restrict__ pairs,
     __syncthreads();
     R3_T(3);
 
-    // ---- hypotheses, one lane each; keep the first best per lane, then the first best overall ----
+    // ---- hypotheses: workgroup g takes iterations g, g + G, ...; Lh lanes per hypothesis split the
+    // points (Lh = the largest power of two that keeps all of them on the 256 lanes at once) and sum
+    // their counts; keep the first best per lane, then the first best overall ----
+    const int hn = (iters - g + G - 1) / G;
+    int Lh = 1;
+    while (Lh < 64 && 2 * Lh * hn <= 256) Lh <<= 1;
+    const int part = tid & (Lh - 1);
     int my_best = 0, my_it = INT_MAX;
-    for (int it = tid; it < iters; it += blockDim.x) {
+    for (int k = tid / Lh; k < hn; k += 256 / Lh) {
+        const int it = g + G * k;
         double R[9], t[3];
         hypothesis_dev(sP1, sP2, s_samp[3 * it], s_samp[3 * it + 1], s_samp[3 * it + 2], R, t);
         int inl = 0;
 #pragma unroll 4
-        for (int j = 0; j < N; j++) inl += inlier_dev(R, t, sP1[j], sP2[j], thr);  // unrolled: loads run ahead
+        for (int j = part; j < N; j += Lh) inl += inlier_dev(R, t, sP1[j], sP2[j], thr);  // unrolled: loads run ahead
+        for (int o = 1; o < Lh; o <<= 1) inl += __shfl_xor(inl, o);  // the Lh lanes of this hypothesis (all active)
         if (inl > my_best) {
             my_best = inl;
             my_it = it;
         }
     }
     // first strictly-best iteration overall = max count, then min iteration (a total order, so the
-    // butterfly / wave-order reduction is exact)
+    // butterfly / wave-order / workgroup-order reduction is exact)
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
         const int oc = __shfl_xor(my_best, o), oi = __shfl_xor(my_it, o);
@@ -389,6 +398,31 @@ __global__ __launch_bounds__(256) void k_ransac3d(const int* __restrict__ pairs,
             bc = s_bc[k];
             bi = s_bi[k];
         }
+    if (G > 1) {
+        // the pair's last workgroup to finish takes the G results (agent-scope release/acquire on the
+        // arrival counter) and continues with the winner; it re-arms the counter for the next launch
+        int* sy = sync + (size_t)p * (1 + 2 * G);
+        __shared__ int s_last;
+        if (tid == 0) {
+            __hip_atomic_store(&sy[1 + 2 * g], bc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(&sy[2 + 2 * g], bi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const int old = __hip_atomic_fetch_add(&sy[0], 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+            s_last = old == G - 1;
+            if (s_last) __hip_atomic_store(&sy[0], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        __syncthreads();
+        if (!s_last) return;
+        bc = 0;
+        bi = INT_MAX;
+        for (int q = 0; q < G; q++) {
+            const int c = __hip_atomic_load(&sy[1 + 2 * q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const int i = __hip_atomic_load(&sy[2 + 2 * q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (c > bc || (c == bc && i < bi)) {
+                bc = c;
+                bi = i;
+            }
+        }
+    }
     if (bc == 0) bi = -1;
     const int best_inliers = bc, best_it = bi;
     // inlier flags of the winning hypothesis, in parallel (every lane re-derives the model), then
@@ -477,12 +511,14 @@ __global__ __launch_bounds__(256) void k_ransac3d(const int* __restrict__ pairs,
 int ransac3d_pairs(vs_ctx* ctx, int P, const int* d_pairs, const vs_keypoint* d_kps, int cap, const vs_match* d_good,
                    const int* d_ngood, const float* d_depth, int h, int w, const double K[4],
                    const uint32_t* d_seeds, int iters, double thr, double* d_R, double* d_t, int* d_ok, int* d_diag,
-                   hipStream_t s, const uint32_t* d_mt_init) {
+                   hipStream_t s, const uint32_t* d_mt_init, int split, int* d_sync) {
     if (P <= 0) return VS_OK;
     VS_ARG(iters > 0 && iters <= kMaxIters3d, "ransac_3d3d: iters must be in [1, 1024]");
+    VS_ARG(split >= 1 && split <= kMaxSplit3d && (split == 1 || d_sync), "ransac_3d3d: bad workgroup split");
     ProfScope ps(ctx, "ransac3d", s);
-    hipLaunchKernelGGL(k_ransac3d, dim3(P), dim3(256), 0, s, d_pairs, d_kps, cap, d_good, d_ngood, d_depth, h, w, K[0],
-                       K[1], K[2], K[3], d_seeds, d_mt_init, iters, thr, d_R, d_t, d_ok, d_diag);
+    hipLaunchKernelGGL(k_ransac3d, dim3(P * split), dim3(256), 0, s, d_pairs, d_kps, cap, d_good, d_ngood, d_depth, h,
+                       w, K[0], K[1], K[2], K[3], d_seeds, d_mt_init, iters, thr, d_R, d_t, d_ok, d_diag, split,
+                       d_sync);
     VS_HIP(hipGetLastError());
     return VS_OK;
 }

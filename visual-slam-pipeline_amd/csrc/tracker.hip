@@ -323,7 +323,9 @@ struct Pinned {
 constexpr size_t kChainInts = 0, kChainDbl = 128, kChainGood = 128 + 36 * 8;
 constexpr size_t kChainKept = kChainGood + (size_t)kCap * sizeof(vs_match);
 constexpr size_t kChainRaw = kChainKept + (size_t)kCap * sizeof(vs_match);
-constexpr size_t kChainBytes = kChainRaw + (size_t)kCap * sizeof(vs_match);
+constexpr size_t kChainSync = kChainRaw + (size_t)kCap * sizeof(vs_match);  // k_ransac3d's arrival counter + results
+constexpr int kChainSplit3d = 4;  // k_ransac3d workgroups per chain (its 200 hypotheses on 4 CUs)
+constexpr size_t kChainBytes = kChainSync + 256;
 // chain header: pair slots, the 3D-3D seed, 0, then its MT19937 init_genrand state
 constexpr int kHdrWords = 4 + 624;
 constexpr size_t kHdrBytes = kHdrWords * sizeof(uint32_t);
@@ -688,6 +690,9 @@ struct GpuOps {
         VS_CHECK(dgrid.ensure((size_t)2 * B * hc * wc * VS_DESC_DIM * sizeof(float)));
         VS_CHECK(chain_buf.ensure(kChainBytes));
         VS_CHECK(chain_buf2.ensure(kChainBytes));
+        VS_HIP(hipMemsetAsync(chain_buf.as<char>() + kChainSync, 0, kChainBytes - kChainSync, s));
+        VS_HIP(hipMemsetAsync(chain_buf2.as<char>() + kChainSync, 0, kChainBytes - kChainSync, s));
+        if (const char* e = std::getenv("VS_SLAM_R3_SPLIT")) r3_split = std::max(1, std::min(kMaxSplit3d, std::atoi(e)));
         VS_CHECK(hdr_buf.ensure(kHdrBytes));
         VS_CHECK(hdr_buf2.ensure(kHdrBytes));
         VS_CHECK(mstate2.ensure(2 * kCap * sizeof(unsigned long long) + 256));
@@ -1011,7 +1016,8 @@ struct GpuOps {
                             st));
         VS_CHECK(ransac3d_pairs(ctx, 1, dh, pool_kps.as<vs_keypoint>(), kCap, kept, di + 5, pool_depth.as<float>(), h, w,
                                 K, reinterpret_cast<const uint32_t*>(dh + 2), 200, 0.05, dd + 11, dd + 20, di + 6, di + 16,
-                                st, reinterpret_cast<const uint32_t*>(dh + 4)));
+                                st, reinterpret_cast<const uint32_t*>(dh + 4), r3_split,
+                                reinterpret_cast<int*>(cbuf + kChainSync)));
         VS_CHECK(emat_pairs(ctx, 1, dh, pool_kps.as<vs_keypoint>(), kCap, kept, di + 5, di + 6, pool_depth.as<float>(), h,
                             w, K, dd + 23, dd + 32, dd + 35, di + 7, di + 20, st));
         return P.to_host(hout, cbuf, kChainRaw, st);
@@ -1323,6 +1329,7 @@ struct GpuOps {
                        vs_trk::M3&, vs_trk::V3&, bool)>
         predict;                  // Tracker::predict_next_pose (set by vs_slam_create)
     bool tlm_spec_on = true;      // VS_SLAM_SPEC_TLM=0 disables
+    int r3_split = kChainSplit3d;  // VS_SLAM_R3_SPLIT: k_ransac3d workgroups per chain (1 = one CU)
     bool next_kps_ready = false;  // the next frame's keypoints are on the host (its chunk was waited)
     // the batch being tracked and its next chunk to wait (process_batch_dev's loop): speculate_next waits
     // for the chunk of a next frame that starts one, instead of skipping the speculation

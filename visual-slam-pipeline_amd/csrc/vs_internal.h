@@ -239,7 +239,10 @@ int ransac3d_pairs(vs_ctx* ctx, int P, const int* d_pairs, const vs_keypoint* d_
                    const vs_match* d_good, const int* d_ngood, const float* d_depth, int h, int w,
                    const double K[4], const uint32_t* d_seeds, int iters, double thr,
                    double* d_R, double* d_t, int* d_ok, int* d_diag, hipStream_t s,
-                   const uint32_t* d_mt_init = nullptr);  // [P][624] init_genrand states (optional)
+                   const uint32_t* d_mt_init = nullptr,  // [P][624] init_genrand states (optional)
+                   int split = 1,            // workgroups per pair (1 .. kMaxSplit3d)
+                   int* d_sync = nullptr);   // split > 1: [P][1 + 2 split] ints, zero before the first launch
+constexpr int kMaxSplit3d = 8;
 // Local-map tracking (d_result = {tracked, observations}).  h_kp_to_mp_src (optional): device-
 // readable pinned host memory with the initial kp -> map-point table, copied into d_kp_to_mp by the
 // first kernel (no separate upload); null = d_kp_to_mp already holds it.
