@@ -449,6 +449,7 @@ def frontend_batch(ctx, B, rank, world, steps, warmup, workers=8):
     import torch
     import torch.distributed as dist
 
+    import synth
     import vslam_abi
     n_total = world * B
     dev = torch.device("cuda", torch.cuda.current_device())

@@ -111,9 +111,11 @@ def test_epnp_sequential_device_equals_host(vsctx, oracle):
 
 @pytest.mark.parametrize("mode", [1, 2])
 def test_epnp_out_of_line_device_equals_host(vsctx, oracle, mode):
-    """the sequential EPnP behind a noinline call (mode 1: one problem per lane; mode 2:
-    called by lane 0 of a wave alone, as k_pnp_ransac once did) gives the host's pose and Rodrigues round
-    trip bit for bit on the same 2,000 problems (the cause of the round-5 divergence)."""
+    """VERDICT r05 #7 regression: the sequential EPnP behind a noinline call (mode 1: one problem per lane;
+    mode 2: called by lane 0 of a wave alone, as k_pnp_ransac once did) gives the host's pose and Rodrigues
+    round trip bit for bit on the same 2,000 problems.  The round-5 divergence was the out-of-line code for
+    B = R R^T's diagonal select (`k == a ? alpha[a] : C[k][a]`, two private arrays) reading C[k][a]
+    (tools/r06/epnp_b_repro.hip); the statement now substitutes by assignment."""
     import ctypes
 
     import vslam_abi
@@ -140,10 +142,9 @@ def test_epnp_out_of_line_device_equals_host(vsctx, oracle, mode):
 
 
 def test_epnp_eig_stages_out_of_line(vsctx, oracle):
-    """Where the out-of-line divergence starts: epnp_small_eig called out of line on the device dumps its
-    stage results (QR, B = R R^T, the tridiagonal, the multisection brackets, the inverse iteration, v);
-    the test reports the first stage whose bits differ from the host's (diagnostic; asserts nothing about
-    the out-of-line build's correctness, only that the dump ran)."""
+    """epnp_small_eig called out of line on the device dumps its stage results (QR, B = R R^T, the
+    tridiagonal, the multisection brackets, the inverse iteration, v); every stage equals the host's bit
+    for bit (the stage the round-5 divergence started at was B)."""
     import ctypes
 
     import vslam_abi
@@ -166,7 +167,10 @@ def test_epnp_eig_stages_out_of_line(vsctx, oracle):
     stages = [("alpha", 0, 10), ("tau", 10, 20), ("B", 20, 120), ("d", 120, 130), ("e", 130, 139), ("scale", 139, 140),
               ("lo", 140, 141), ("hi", 141, 142), ("a", 142, 144), ("b", 144, 146), ("lambda", 146, 148),
               ("y", 148, 168), ("v", 168, 216)]
+    total = 0
     for name, a, b in stages:
         bad = np.nonzero(np.any(dev[:, a:b].view(np.uint64) != host[:, a:b].view(np.uint64), axis=1))[0]
         print(f"stage {name:7s}: {len(bad):4d} problems differ; first {bad[:3].tolist()}",
               "" if not len(bad) else f"dev {dev[bad[0], a:min(b, a + 4)].tolist()} host {host[bad[0], a:min(b, a + 4)].tolist()}")
+        total += len(bad)
+    assert total == 0

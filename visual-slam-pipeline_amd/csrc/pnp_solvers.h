@@ -735,12 +735,19 @@ VS_HD inline void epnp_small_eig(const double (*al)[4], const double* uv, int m,
     for (int q = 0; q < 4; q++)
         for (int r = 0; r < 12; r++) x[q][r] = (q < nz && r == nc + q) ? 1.0 : 0.0;
     if (nc == 10) {
-        // 2. B = R R^T (R_ak = C[k][a] above the diagonal, alpha[a] on it), upper triangle then mirrored
+        // 2. B = R R^T (R_ak = C[k][a] above the diagonal, alpha[a] on it), upper triangle then mirrored.
+        // The diagonal factor is substituted by assignment, not by `k == a ? alpha[a] : C[k][a]`: in a
+        // non-inlined gfx950 copy of this function that select between the two private arrays came out
+        // as C[k][a] (tools/r06/epnp_b_repro.hip modes 10-17).
         double B[10][10];
         for (int a = 0; a < 10; a++)
             for (int b = a; b < 10; b++) {
-                for (int k = 0; k < 10; k++)
-                    t[k] = k >= b ? (k == a ? alpha[a] : C[k][a]) * (k == b ? alpha[b] : C[k][b]) : -0.0;
+                for (int k = 0; k < 10; k++) {
+                    double fa = C[k][a], fb = C[k][b];
+                    if (k == a) fa = alpha[a];
+                    if (k == b) fb = alpha[b];
+                    t[k] = k >= b ? fa * fb : -0.0;
+                }
                 B[a][b] = B[b][a] = tsum<10>(t);
             }
         if (dbg)
