@@ -8,7 +8,8 @@ from test_oracle_tracking import _kps, pose_problem
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("seed,n_kp,n_mp", [(0, 120, 400), (1, 400, 900), (2, 400, 20000), (3, 5, 3000)])
+@pytest.mark.parametrize("seed,n_kp,n_mp", [(0, 120, 400), (1, 400, 900), (2, 400, 20000), (3, 5, 3000), (4, 1024, 60000),
+                                          (5, 1000, 12000)])
 def test_track_local_map_bit_exact(vsctx, oracle, seed, n_kp, n_mp):
     kxy, desc, pos, mdesc, valid, R, t = restate.synthetic_tracking_problem(n_kp, n_mp, seed)
     kps = _kps(oracle, kxy)

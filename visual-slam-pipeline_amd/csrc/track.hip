@@ -307,39 +307,57 @@ __global__ __launch_bounds__(256) void k_tlm_best(const int* __restrict__ cnt, c
 
 constexpr int kTlmCandBuf = 4096;  // candidates buffered in LDS between resolve passes
 constexpr int kTlmMaxBlk = 4096;  // map points / 256 handled by the direct placement
-constexpr int kTlmBucket = 8;     // per-keypoint candidate bucket of a resolve pass
 
 struct TlmResolveShared {
     unsigned long long best[kTlmMaxKp];  // bits of the running minimum (d >= 0: order-preserving)
     int kpmp[kTlmMaxKp];
-    int first[kTlmMaxKp];  // first buffered candidate of a keypoint in the current pass
-    int bcnt[kTlmMaxKp];   // candidates of a keypoint in the current pass
-    int bkt[kTlmMaxKp][kTlmBucket];  // their buffer indices (any order) while they fit
+    int bcnt[kTlmMaxKp];  // candidates of a keypoint in the current pass
+    int seg[kTlmMaxKp];   // their segment in order[]
+    int order[kTlmCandBuf];  // the pass's candidates grouped by keypoint (any order within a group)
     int cmp[kTlmCandBuf], cki[kTlmCandBuf];
     unsigned long long cd[kTlmCandBuf];
     int pre[kTlmMaxBlk];
     int wcnt[16];
     int nobs, nc, total;
 };
-// ~132 KB: one workgroup per CU within gfx950's 160 KB of LDS (this kernel is written for gfx950 only)
+// ~120 KB: one workgroup per CU within gfx950's 160 KB of LDS (this kernel is written for gfx950 only)
 static_assert(sizeof(TlmResolveShared) <= 160 * 1024, "k_tlm_resolve's shared state exceeds gfx950's 160 KB LDS");
 
 // One pass over the nc buffered candidates (map-point order): winners are strictly below the
-// carried minimum and below every earlier buffered candidate of the keypoint (a keypoint's
-// candidates start at its first one); the last winner of a keypoint has its smallest distance
-// (winners strictly decrease); observations are compacted in candidate order.
-__device__ void tlm_resolve_pass(TlmResolveShared& S, int nc, int* __restrict__ obs_mp, int* __restrict__ obs_kp,
-                                 int obs_cap) {
+// carried minimum and below every earlier buffered candidate of the keypoint; the last winner of a
+// keypoint has its smallest distance (winners strictly decrease); observations are compacted in
+// candidate order.  The earlier candidates of a keypoint are found through a counting sort by
+// keypoint (counts, a scan over the nkp keypoints, the scatter), so a candidate compares with its own
+// keypoint's group only, however many candidates a keypoint draws.
+__device__ void tlm_resolve_pass(TlmResolveShared& S, int nc, int nkp, int* __restrict__ obs_mp,
+                                 int* __restrict__ obs_kp, int obs_cap) {
     const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
-    // each keypoint's candidates into its bucket (unordered: the test below compares positions)
+    int slot[kTlmCandBuf / 1024];
 #pragma unroll
     for (int r = 0; r < kTlmCandBuf / 1024; r++) {
         const int t = r * 1024 + tid;
-        if (t < nc) {
-            const int ki = S.cki[t];
-            const int slot = atomicAdd(&S.bcnt[ki], 1);
-            if (slot < kTlmBucket) S.bkt[ki][slot] = t;
+        slot[r] = t < nc ? atomicAdd(&S.bcnt[S.cki[t]], 1) : 0;
+    }
+    __syncthreads();
+    {  // exclusive scan of the counts, one keypoint per thread (nkp <= 1024)
+        const int c = tid < nkp ? S.bcnt[tid] : 0;
+        int incl = c;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int y = __shfl_up(incl, o);
+            if (lane >= o) incl += y;
         }
+        if (lane == 63) S.wcnt[wv] = incl;
+        __syncthreads();
+        int base = incl - c;
+        for (int w = 0; w < wv; w++) base += S.wcnt[w];
+        if (tid < nkp) S.seg[tid] = base;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < kTlmCandBuf / 1024; r++) {
+        const int t = r * 1024 + tid;
+        if (t < nc) S.order[S.seg[S.cki[t]] + slot[r]] = t;
     }
     __syncthreads();
     bool win[kTlmCandBuf / 1024];
@@ -351,15 +369,10 @@ __device__ void tlm_resolve_pass(TlmResolveShared& S, int nc, int* __restrict__ 
             const int ki = S.cki[t];
             const unsigned long long d = S.cd[t];
             bool w = d < S.best[ki];
-            const int nb = S.bcnt[ki];
-            if (nb <= kTlmBucket) {  // the keypoint's other candidates: earlier and not larger -> loses
-                for (int k = 0; k < nb && w; k++) {
-                    const int j = S.bkt[ki][k];
-                    if (j < t && S.cd[j] <= d) w = false;
-                }
-            } else {
-                for (int j = S.first[ki]; j < t && w; j++)
-                    if (S.cki[j] == ki && S.cd[j] <= d) w = false;
+            const int s0 = S.seg[ki], nb = S.bcnt[ki];
+            for (int k = 0; k < nb && w; k++) {  // the keypoint's other candidates: earlier and not larger -> loses
+                const int j = S.order[s0 + k];
+                if (j < t && S.cd[j] <= d) w = false;
             }
             win[r] = w;
         }
@@ -369,8 +382,7 @@ __device__ void tlm_resolve_pass(TlmResolveShared& S, int nc, int* __restrict__ 
     for (int r = 0; r < kTlmCandBuf / 1024; r++) {
         const int t = r * 1024 + tid;
         if (t < nc) {
-            S.first[S.cki[t]] = INT_MAX;  // every reader is past the barrier above
-            S.bcnt[S.cki[t]] = 0;
+            S.bcnt[S.cki[t]] = 0;  // every reader is past the barrier above
             if (win[r]) atomicMin(&S.best[S.cki[t]], S.cd[t]);
         }
     }
@@ -403,8 +415,7 @@ __device__ void tlm_resolve_pass(TlmResolveShared& S, int nc, int* __restrict__ 
 }
 
 // Phase 3b: the assignment in map-point order (Slam.cpp:460-465).  The candidates (k_tlm_best)
-// go to an LDS buffer in map-point order -- directly at block prefix + rank when they all fit,
-// else 1024 map points at a time with a pass whenever the buffer could overflow.
+// go to an LDS buffer in map-point order at block prefix + rank, kTlmCandBuf of them per pass.
 // The PnP input the tracker's refinement takes next (Slam::refine_pose_via_local_pnp's tracked_points,
 // Slam.cpp:1408-1420): keypoints in order whose (final) map point is valid, as float object points and
 // image points; io = [off {0, n, 0, 0} | obj cap x 3 | img cap x 2].
@@ -429,7 +440,6 @@ __global__ __launch_bounds__(1024) void k_tlm_resolve(const int* __restrict__ be
     for (int k = tid; k < nkp; k += 1024) {
         S.best[k] = (unsigned long long)__double_as_longlong(1e9);
         S.kpmp[k] = src ? src[k] : kp_to_mp[k];  // src: the host's table in pinned memory (no upload)
-        S.first[k] = INT_MAX;
         S.bcnt[k] = 0;
     }
     if (tid == 0) {
@@ -468,33 +478,42 @@ __global__ __launch_bounds__(1024) void k_tlm_resolve(const int* __restrict__ be
         if (tid == 0) S.total = all;
     }
     __syncthreads();
-    if (S.total <= kTlmCandBuf) {
-        for (int m0 = 0; m0 < n_mp; m0 += 16 * 1024) {
-            // all loads of the round issued before any is used (latency, not bandwidth): the rank and
-            // distance are read unconditionally (in bounds), so they do not wait for best_ki
-            int kis[16], rks[16];
-            double bds[16];
+    if (nblk <= kTlmMaxBlk) {
+        // Passes over windows of kTlmCandBuf candidates in map-point order: candidate j (block prefix +
+        // rank) goes to slot j - p0 of the pass whose window holds it.  Each pass reads every map point's
+        // (ki, rank, d) with all loads of a round in flight (L2 latency, not a chain of 1024-point
+        // chunks); a pass's outcome does not depend on where a window ends (a candidate wins iff it is
+        // below every earlier candidate of its keypoint, carried across passes in S.best).
+        const int total = S.total;
+        for (int p0 = 0; p0 < total; p0 += kTlmCandBuf) {
+            const int pend = min(total, p0 + kTlmCandBuf);
+            for (int m0 = 0; m0 < n_mp; m0 += 16 * 1024) {
+                // all loads of the round issued before any is used: the rank and distance are read
+                // unconditionally (in bounds), so they do not wait for best_ki
+                int kis[16], rks[16];
+                double bds[16];
 #pragma unroll
-            for (int u = 0; u < 16; u++) {
-                const int mp = min(m0 + u * 1024 + tid, n_mp - 1);
-                kis[u] = best_ki[mp];
-                rks[u] = rank[mp];
-                bds[u] = best_d[mp];
-            }
+                for (int u = 0; u < 16; u++) {
+                    const int mp = min(m0 + u * 1024 + tid, n_mp - 1);
+                    kis[u] = best_ki[mp];
+                    rks[u] = rank[mp];
+                    bds[u] = best_d[mp];
+                }
 #pragma unroll
-            for (int u = 0; u < 16; u++) {
-                const int mp = m0 + u * 1024 + tid;
-                if (mp >= n_mp || kis[u] < 0) continue;
-                const int j = S.pre[mp >> 8] + rks[u];
-                S.cmp[j] = mp;
-                S.cki[j] = kis[u];
-                S.cd[j] = (unsigned long long)__double_as_longlong(bds[u]);
-                atomicMin(&S.first[kis[u]], j);
+                for (int u = 0; u < 16; u++) {
+                    const int mp = m0 + u * 1024 + tid;
+                    if (mp >= n_mp || kis[u] < 0) continue;
+                    const int j = S.pre[mp >> 8] + rks[u];
+                    if (j < p0 || j >= pend) continue;
+                    S.cmp[j - p0] = mp;
+                    S.cki[j - p0] = kis[u];
+                    S.cd[j - p0] = (unsigned long long)__double_as_longlong(bds[u]);
+                }
             }
+            __syncthreads();
+            tlm_resolve_pass(S, pend - p0, nkp, obs_mp, obs_kp, obs_cap);
         }
-        __syncthreads();
-        tlm_resolve_pass(S, S.total, obs_mp, obs_kp, obs_cap);
-    } else {
+    } else {  // more than kTlmMaxBlk * 256 map points: 1024 at a time, a pass whenever the buffer could overflow
         for (int c0 = 0; c0 < n_mp; c0 += 1024) {
             const int mp = c0 + tid;
             const int ki0 = mp < n_mp ? best_ki[mp] : -1;
@@ -512,14 +531,13 @@ __global__ __launch_bounds__(1024) void k_tlm_resolve(const int* __restrict__ be
                 S.cmp[j] = mp;
                 S.cki[j] = ki0;
                 S.cd[j] = (unsigned long long)__double_as_longlong(best_d[mp]);
-                atomicMin(&S.first[ki0], j);
             }
             __syncthreads();
             const int nc = S.nc + add;
             if (tid == 0) S.nc = nc;
             __syncthreads();
             if (nc + 1024 <= kTlmCandBuf && c0 + 1024 < n_mp) continue;  // uniform
-            tlm_resolve_pass(S, nc, obs_mp, obs_kp, obs_cap);
+            tlm_resolve_pass(S, nc, nkp, obs_mp, obs_kp, obs_cap);
             if (tid == 0) S.nc = 0;
             __syncthreads();
         }

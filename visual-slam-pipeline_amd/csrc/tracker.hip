@@ -150,6 +150,22 @@ __global__ __launch_bounds__(256) void k_copy_bytes(const char* __restrict__ src
     }
 }
 
+// The reference frame of a speculative chain two frames ahead: the keyframe rule chain() predicts with
+// (Slam.cpp:1061-1072, is_keyframe :1360) on the ratio-test count of the chain before it (prev[4], the
+// same stream, so already final): kf_slot when that frame becomes a keyframe, else base_slot.  Written
+// into the chain's header (the pair every kernel of the chain reads) and into its result block (int 28)
+// for the host's check.
+__global__ void k_pick_ref(const int* __restrict__ prev, int kf_slot, int base_slot, int gap, int* __restrict__ hdr,
+                           int* __restrict__ res) {
+    if (threadIdx.x != 0) return;
+    const int ng = prev[4];
+    const bool kf = (gap >= vs_trk::cfg::KF_MIN_FRAME_GAP && ng >= vs_trk::cfg::KF_MIN_MATCHES) ||
+                    (ng < 2 * vs_trk::cfg::MIN_MATCHES && gap >= 5);
+    const int slot = kf ? kf_slot : base_slot;
+    hdr[0] = slot;
+    res[28] = slot;
+}
+
 // Visibility sweep (Slam.cpp:1089-1108): for every valid map point, Optimizer::project_point
 // (Optimizer.cpp:26-48) with the camera->world pose; bit 0 = inside the image (increase_visible),
 // bit 1 = some keypoint within TRACK_VISIBILITY_RADIUS (increase_found).  Every workgroup first
@@ -329,6 +345,7 @@ constexpr size_t kChainBytes = kChainSync + 256;
 // chain header: pair slots, the 3D-3D seed, 0, then its MT19937 init_genrand state
 constexpr int kHdrWords = 4 + 624;
 constexpr size_t kHdrBytes = kHdrWords * sizeof(uint32_t);
+constexpr size_t kSpecBlock = (kHdrBytes + kChainRaw + 64 + 255) & ~(size_t)255;  // a speculation's pinned [header | result]
 
 // Extraction chunks: the batch's network + post-processing runs chunk by chunk on the extraction
 // streams while the tracker consumes the chunks already done (process_batch_dev).  The batch is
@@ -462,15 +479,44 @@ struct GpuOps {
     // Speculative front chain of the batch's next frame (see chain()): its own stream on the tracking
     // CU set, result block, header, matcher key state and pinned host block [header | result].
     hipStream_t s2 = nullptr;
-    hipEvent_t cspec_ev = nullptr;
-    DevBuf chain_buf2, hdr_buf2, mstate2;
+    DevBuf mstate2;
     Pinned cpin{hipHostMallocCoherent | hipHostMallocMapped};
+    // Up to two speculative chains in flight on s2 (VS_SLAM_SPEC_DEPTH=2, the default): the next frame's
+    // and the one after it, whose reference frame is picked on the device (k_pick_ref) from the ratio-test
+    // count of the chain before it, by the keyframe rule chain() predicts with.  Each has its own result
+    // block, header, event and pinned [header | result] block.
     struct ChainSpec {
         bool valid = false;
         const vs_trk::Frame* cur = nullptr;
-        int ref_slot = -1, cur_slot = -1;
+        int ref_slot = -1, cur_slot = -1;  // ref_slot < 0: picked on the device, read back with the result
         uint32_t seed = 0;
-    } cspec;
+        int kf_slot = -1, base_slot = -1, gap = 0;  // the device pick's inputs
+        long seq = 0, prev_seq = 0;                 // launch order; the chain whose count the pick read
+        hipEvent_t ev = nullptr;
+        DevBuf buf, hdr;
+        char* hbase = nullptr;
+    } cspec[2];
+    long cspec_seq = 0;
+    int spec_depth = 2;  // VS_SLAM_SPEC_DEPTH=1: one chain ahead only
+    int find_spec(const vs_trk::Frame* f) const {
+        for (int k = 0; k < 2; k++)
+            if (cspec[k].valid && cspec[k].cur == f) return k;
+        return -1;
+    }
+    // the reference slot a speculation ran with (a device pick: from its result block, once its event passed)
+    int spec_ref_slot(const ChainSpec& E) const {
+        return E.ref_slot >= 0 ? E.ref_slot : reinterpret_cast<const int*>(E.hbase + kHdrBytes + kChainInts)[28];
+    }
+    // E is the chain of the frame in slot cur_slot with seed, against reference rs as the rule decides it
+    // for the frame before it (kf_slot / base_slot / gap) on the count of the chain prev_seq: host-chosen
+    // with rs, or device-picked from that same chain and candidates
+    static bool spec_matches(const ChainSpec& E, int rs, int kf_slot, int base_slot, int gap, uint32_t seed,
+                             long prev_seq, int cur_slot) {
+        if (!E.valid || E.cur_slot != cur_slot || E.seed != seed) return false;
+        if (E.ref_slot >= 0) return E.ref_slot == rs;
+        return prev_seq != 0 && E.prev_seq == prev_seq && E.kf_slot == kf_slot && E.base_slot == base_slot &&
+               E.gap == gap;
+    }
     bool cspec_on = true;                       // VS_SLAM_SPEC_CHAIN=0 disables
     const vs_trk::Frame* next_frame = nullptr;  // the batch's next frame (process_batch_dev)
     hipEvent_t next_ready = nullptr;            // its extraction chunk's event
@@ -617,7 +663,7 @@ struct GpuOps {
             VS_HIP(hipStreamCreateWithFlags(&xp, hipStreamNonBlocking));
         }
         for (auto& e : region_done) VS_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-        VS_HIP(hipEventCreateWithFlags(&cspec_ev, hipEventDisableTiming));
+        for (auto& E : cspec) VS_HIP(hipEventCreateWithFlags(&E.ev, hipEventDisableTiming));
         VS_HIP(hipEventCreateWithFlags(&tlm_ev, hipEventDisableTiming));
         VS_HIP(hipEventCreateWithFlags(&tspec.ev, hipEventDisableTiming));
         VS_HIP(hipEventCreateWithFlags(&xdone, hipEventDisableTiming));
@@ -649,7 +695,7 @@ struct GpuOps {
             X.ev.clear();
             X.net.clear();
         }
-        (void)hipEventDestroy(cspec_ev);
+        for (auto& E : cspec) (void)hipEventDestroy(E.ev);
         (void)hipEventDestroy(tlm_ev);
         (void)hipEventDestroy(tspec.ev);
         (void)hipStreamDestroy(xs);
@@ -689,16 +735,20 @@ struct GpuOps {
         VS_CHECK(semi.ensure((size_t)2 * B * hc * wc * VS_SEMI_CH * sizeof(float)));
         VS_CHECK(dgrid.ensure((size_t)2 * B * hc * wc * VS_DESC_DIM * sizeof(float)));
         VS_CHECK(chain_buf.ensure(kChainBytes));
-        VS_CHECK(chain_buf2.ensure(kChainBytes));
         VS_HIP(hipMemsetAsync(chain_buf.as<char>() + kChainSync, 0, kChainBytes - kChainSync, s));
-        VS_HIP(hipMemsetAsync(chain_buf2.as<char>() + kChainSync, 0, kChainBytes - kChainSync, s));
         if (const char* e = std::getenv("VS_SLAM_R3_SPLIT")) r3_split = std::max(1, std::min(kMaxSplit3d, std::atoi(e)));
         VS_CHECK(hdr_buf.ensure(kHdrBytes));
-        VS_CHECK(hdr_buf2.ensure(kHdrBytes));
         VS_CHECK(mstate2.ensure(2 * kCap * sizeof(unsigned long long) + 256));
         VS_HIP(hipMemsetAsync(mstate2.p, 0xFF, 2 * kCap * sizeof(unsigned long long), s));
         VS_HIP(hipMemsetAsync(mstate2.as<char>() + 2 * kCap * sizeof(unsigned long long), 0, 256, s));
-        VS_CHECK(cpin.reserve(kHdrBytes + kChainRaw + 64));
+        for (auto& E : cspec) {
+            VS_CHECK(E.buf.ensure(kChainBytes));
+            VS_HIP(hipMemsetAsync(E.buf.as<char>() + kChainSync, 0, kChainBytes - kChainSync, s));
+            VS_CHECK(E.hdr.ensure(kHdrBytes));
+        }
+        VS_CHECK(cpin.reserve(2 * kSpecBlock));
+        for (int k = 0; k < 2; k++) cspec[k].hbase = cpin.base + k * kSpecBlock;
+        if (const char* e = std::getenv("VS_SLAM_SPEC_DEPTH")) spec_depth = std::max(1, std::min(2, std::atoi(e)));
         if (const char* e = std::getenv("VS_SLAM_SPEC_CHAIN")) cspec_on = e[0] != '0';
         VS_CHECK(pin.reserve((size_t)4 << 20));
         VS_CHECK(spin.reserve((size_t)1 << 20));  // one speculation: <= 8 KB table + ~60 KB results at 1024 keypoints
@@ -1001,14 +1051,23 @@ struct GpuOps {
     // match -> F verification -> 3D-3D -> E fallback for the pair in the header, on stream st, into
     // the result block cbuf, copied back to hout (pinned); keys / cnt: the matcher's key state
     // (nullptr: the context's)
+    struct PickArgs {  // a device-picked reference (k_pick_ref)
+        const int* prev;
+        int kf_slot, base_slot, gap;
+    };
     int enqueue_chain(hipStream_t st, char* cbuf, int* dh, const uint32_t* hhdr, char* hout, unsigned long long* keys,
-                      unsigned* cnt) {
+                      unsigned* cnt, const PickArgs* pick = nullptr) {
         int* di = reinterpret_cast<int*>(cbuf + kChainInts);
         double* dd = reinterpret_cast<double*>(cbuf + kChainDbl);
         vs_match* good = reinterpret_cast<vs_match*>(cbuf + kChainGood);
         vs_match* kept = reinterpret_cast<vs_match*>(cbuf + kChainKept);
         const Pinned& P = (hout >= cpin.base && hout < cpin.base + cpin.cap) ? cpin : pin;  // the speculative or the direct chain
         VS_CHECK(P.to_device(dh, hhdr, kHdrBytes, st));
+        if (pick) {
+            hipLaunchKernelGGL(k_pick_ref, dim3(1), dim3(64), 0, st, pick->prev, pick->kf_slot, pick->base_slot,
+                               pick->gap, dh, di);
+            VS_HIP(hipGetLastError());
+        }
         VS_CHECK(match_pairs(ctx, 1, dh, S, pool_desc.as<float>(), pool_n.as<int>(), kCap, vs_trk::cfg::L2_RATIO_THRESHOLD,
                              reinterpret_cast<vs_match*>(cbuf + kChainRaw), di + 3, good, di + 4, st,
                              pool_norms.as<float>(), keys, cnt));
@@ -1058,24 +1117,40 @@ struct GpuOps {
     // on s2 beside this frame's local-map tracking and PnP: it is the next frame's chain whenever
     // this frame neither becomes a keyframe nor is rejected (the reference frame and the processed
     // count then carry over, Slam.cpp:838, 276).  chain() uses it only when slots and seed match.
-    int launch_spec_chain(int ref_slot, const vs_trk::Frame& nxt, uint32_t seed, hipEvent_t ready) {
-        VS_HIP(hipEventSynchronize(cspec_ev));  // the previous speculation released cpin / chain_buf2
-        uint32_t* hh = reinterpret_cast<uint32_t*>(cpin.base);
-        fill_hdr(hh, ref_slot, nxt.slot, seed);
+    // pick_prev >= 0: the reference is picked on the device from that entry's chain (launched before this
+    // one on s2): kf_slot if its frame becomes a keyframe by the rule, else base_slot (gap: that frame's
+    // id gap to base_slot's frame).
+    int launch_spec_chain(int ref_slot, const vs_trk::Frame& nxt, uint32_t seed, hipEvent_t ready, int pick_prev = -1,
+                          int kf_slot = -1, int base_slot = -1, int gap = 0) {
+        // the entry: a free one, else the older (never the one the pick reads)
+        int k = !cspec[0].valid ? 0 : !cspec[1].valid ? 1 : (cspec[0].seq < cspec[1].seq ? 0 : 1);
+        if (k == pick_prev) k ^= 1;
+        ChainSpec& E = cspec[k];
+        VS_HIP(hipEventSynchronize(E.ev));  // its previous chain released the buffers
+        uint32_t* hh = reinterpret_cast<uint32_t*>(E.hbase);
+        fill_hdr(hh, pick_prev >= 0 ? base_slot : ref_slot, nxt.slot, seed);
         if (ready) VS_HIP(hipStreamWaitEvent(s2, ready, 0));  // its extraction chunk
         unsigned long long* keys = mstate2.as<unsigned long long>();
         unsigned* cnt = reinterpret_cast<unsigned*>(mstate2.as<char>() + 2 * kCap * sizeof(unsigned long long));
-        VS_CHECK(enqueue_chain(s2, chain_buf2.as<char>(), hdr_buf2.as<int>(), hh, cpin.base + kHdrBytes, keys, cnt));
-        VS_HIP(hipEventRecord(cspec_ev, s2));
-        cspec.valid = true;
-        cspec.cur = &nxt;
-        cspec.ref_slot = ref_slot;
-        cspec.cur_slot = nxt.slot;
-        cspec.seed = seed;
+        PickArgs pk{};
+        if (pick_prev >= 0) pk = PickArgs{cspec[pick_prev].buf.as<int>(), kf_slot, base_slot, gap};
+        VS_CHECK(enqueue_chain(s2, E.buf.as<char>(), E.hdr.as<int>(), hh, E.hbase + kHdrBytes, keys, cnt,
+                               pick_prev >= 0 ? &pk : nullptr));
+        VS_HIP(hipEventRecord(E.ev, s2));
+        E.valid = true;
+        E.cur = &nxt;
+        E.ref_slot = pick_prev >= 0 ? -1 : ref_slot;
+        E.cur_slot = nxt.slot;
+        E.seed = seed;
+        E.kf_slot = kf_slot;
+        E.base_slot = base_slot;
+        E.gap = gap;
+        E.prev_seq = pick_prev >= 0 ? cspec[pick_prev].seq : 0;
+        E.seq = ++cspec_seq;
         cspec_launched++;
         return VS_OK;
     }
-    // Waits until the helper has enqueued the speculation it was given (cspec and cspec_ev are then
+    // Waits until the helper has enqueued the speculations it was given (cspec[] and their events are then
     // this thread's again); its error, if any, is latched.
     void spec_sync() {
         if (!spec_inflight) return;
@@ -1096,14 +1171,27 @@ struct GpuOps {
         const bool launched = nhit && cnext.launched_next;
         if (nhit) R = cnext.R;
         cnext.valid = false;
-        const bool hit = !nhit && cspec.valid && cspec.cur == &cur && cspec.ref_slot == ref.slot &&
-                         cspec.cur_slot == cur.slot && cspec.seed == seed;
-        if (!launched) cspec.valid = false;  // (a launched speculation belongs to the next frame)
+        bool hit = false;
+        long r_seq = nhit ? cnext.seq : 0;  // the speculation R came from
+        const int e = nhit ? -1 : find_spec(&cur);
+        if (e >= 0) {
+            ChainSpec& E = cspec[e];
+            if (E.cur_slot == cur.slot && E.seed == seed && (E.ref_slot < 0 || E.ref_slot == ref.slot)) {
+                HostTimer hw(hprof, kHSpec);
+                if (failed(hipEventSynchronize(E.ev) == hipSuccess ? VS_OK : VS_ERR_HIP)) return R;
+                hit = spec_ref_slot(E) == ref.slot;
+                if (hit) {
+                    R = parse_chain(E.hbase + kHdrBytes);
+                    r_seq = E.seq;
+                }
+            }
+            E.valid = false;  // this frame's: used or not, it is done
+        }
+        if (!launched)  // speculations for later frames stay unless this frame's own chain was not launched ahead
+            for (auto& E : cspec)
+                if (E.valid && E.cur != next_frame && E.cur != next2_frame) E.valid = false;
         if (nhit) {
         } else if (hit) {
-            HostTimer hw(hprof, kHSpec);
-            if (failed(hipEventSynchronize(cspec_ev) == hipSuccess ? VS_OK : VS_ERR_HIP)) return R;
-            R = parse_chain(cpin.base + kHdrBytes);
             cspec_hits++;
         } else {
             R = chain_impl(ref, cur, seed);
@@ -1119,8 +1207,13 @@ struct GpuOps {
             const int ng = (int)R.good.size(), gap = cur.id - ref.id;
             const bool kf = (gap >= vs_trk::cfg::KF_MIN_FRAME_GAP && ng >= vs_trk::cfg::KF_MIN_MATCHES) ||
                             (ng < 2 * vs_trk::cfg::MIN_MATCHES && gap >= 5);
+            const int rs = kf && cur.slot >= 0 ? cur.slot : ref.slot;
+            const int e1 = find_spec(next_frame);
+            if (e1 >= 0 && spec_matches(cspec[e1], rs, cur.slot, ref.slot, gap, seed + 1u, r_seq, next_frame->slot))
+                return R;  // already in flight (a device pick on this very chain's count)
+            if (e1 >= 0) cspec[e1].valid = false;
             spec_req.pending = true;
-            spec_req.ref_slot = kf && cur.slot >= 0 ? cur.slot : ref.slot;
+            spec_req.ref_slot = rs;
             spec_req.nxt = next_frame;
             spec_req.nxt_slot = next_frame->slot;
             spec_req.seed = seed + 1u;
@@ -1338,11 +1431,14 @@ struct GpuOps {
     int next_index = -1;
     const vs_trk::Frame* next2_frame = nullptr;  // the frame after it, and its chunk's event
     hipEvent_t next2_ready = nullptr;
+    const vs_trk::Frame* next3_frame = nullptr;  // and the one after that (VS_SLAM_SPEC_DEPTH=2)
+    hipEvent_t next3_ready = nullptr;
     struct NextChain {  // the next frame's chain, read back ahead of its chain() call
         bool valid = false, launched_next = false;
         const vs_trk::Frame* cur = nullptr;
         int ref_slot = -1, cur_slot = -1;
         uint32_t seed = 0;
+        long seq = 0;  // the speculation it came from
         vs_trk::ChainResult R;
     } cnext;
     struct TlmSpec {
@@ -1364,17 +1460,20 @@ struct GpuOps {
     // Reads the next frame's speculative chain back (waiting for it) into cnext.
     bool take_next_chain(const vs_trk::Frame* nxt) {
         spec_sync();
-        if (!(cspec.valid && cspec.cur == nxt)) return false;
+        const int e = find_spec(nxt);
+        if (e < 0) return false;
+        ChainSpec& E = cspec[e];
         HostTimer hw(hprof, kHSpecNext);
-        if (failed(hipEventSynchronize(cspec_ev) == hipSuccess ? VS_OK : VS_ERR_HIP)) return false;
-        cnext.R = parse_chain(cpin.base + kHdrBytes);
+        if (failed(hipEventSynchronize(E.ev) == hipSuccess ? VS_OK : VS_ERR_HIP)) return false;
+        cnext.R = parse_chain(E.hbase + kHdrBytes);
         cnext.valid = true;
         cnext.launched_next = false;
-        cnext.cur = cspec.cur;
-        cnext.ref_slot = cspec.ref_slot;
-        cnext.cur_slot = cspec.cur_slot;
-        cnext.seed = cspec.seed;
-        cspec.valid = false;
+        cnext.cur = E.cur;
+        cnext.ref_slot = spec_ref_slot(E);
+        cnext.cur_slot = E.cur_slot;
+        cnext.seed = E.seed;
+        cnext.seq = E.seq;
+        E.valid = false;
         cspec_hits++;
         return true;
     }
@@ -1410,10 +1509,25 @@ struct GpuOps {
             const vs_trk::Frame* n2 = next2_frame;
             const uint32_t sd = cnext.seed + 1u;
             hipEvent_t rdy = next2_ready;
-            if (spec_async) {  // ~40 us of HIP calls, on the helper beside this thread's tracking launch
+            // launched one frame earlier with its reference picked on the device from the next frame's count?
+            const int e2 = find_spec(n2);
+            const bool have = e2 >= 0 && spec_matches(cspec[e2], rs, nxt->slot, ref->slot, gap, sd, cnext.seq, n2->slot);
+            if (e2 >= 0 && !have) cspec[e2].valid = false;
+            // depth 2: the chain after it too, its reference picked on the device from n2's count
+            const vs_trk::Frame* n3 = spec_depth >= 2 ? next3_frame : nullptr;
+            const bool go3 = n3 && n3->slot >= 0 && find_spec(n3) < 0;
+            const int kf3 = n2->slot, base3 = rs, gap3 = n2->id - (kf ? nxt->id : ref->id);
+            hipEvent_t rdy3 = next3_ready;
+            auto job = [this, have, rs, n2, sd, rdy, go3, n3, kf3, base3, gap3, rdy3]() -> int {
+                if (!have) VS_CHECK(launch_spec_chain(rs, *n2, sd, rdy));
+                const int p = go3 ? find_spec(n2) : -1;
+                if (p >= 0) VS_CHECK(launch_spec_chain(-1, *n3, sd + 1u, rdy3, p, kf3, base3, gap3));
+                return VS_OK;
+            };
+            if (spec_async) {  // ~40 us of HIP calls per chain, on the helper beside this thread's tracking launch
                 spec_inflight = true;
-                sq.submit([this, rs, n2, sd, rdy] { return launch_spec_chain(rs, *n2, sd, rdy); });
-            } else if (failed(launch_spec_chain(rs, *n2, sd, rdy))) {
+                sq.submit(job);
+            } else if (failed(job())) {
                 return;
             }
             cnext.launched_next = true;
@@ -1860,7 +1974,7 @@ int settle(vs_slam* sl) {
         o.err = VS_OK;
         return r;
     }
-    VS_HIP(hipStreamWaitEvent(o.s, o.cspec_ev, 0));  // a discarded speculation still reads the pool
+    for (auto& E : o.cspec) VS_HIP(hipStreamWaitEvent(o.s, E.ev, 0));  // a discarded speculation still reads the pool
     for (const auto& f : T.map().frames)  // new keyframes' features into the archive (loop closure)
         if (f->keyframe && f->kf_slot < 0 && f->slot >= 0) VS_CHECK(o.archive(f.get()));
     VS_CHECK(o.flush_copies());  // before any slot below is released and reused
@@ -1967,7 +2081,7 @@ void vs_slam_destroy(vs_slam* sl) {
     o.destroy_streams();
     DevBuf* bufs[] = {&o.pool_kps, &o.pool_desc, &o.pool_n, &o.pool_depth, &o.pool_norms, &o.pool_grid, &o.semi, &o.dgrid,
                       &o.chain_buf,    &o.work, &o.rows_buf,      &o.map_pos, &o.map_desc,  &o.map_valid, &o.map_tmp,
-                      &o.pnp_io,       &o.hdr_buf, &o.chain_buf2, &o.hdr_buf2, &o.mstate2,
+                      &o.pnp_io,       &o.hdr_buf, &o.cspec[0].buf, &o.cspec[0].hdr, &o.cspec[1].buf, &o.cspec[1].hdr, &o.mstate2,
                       &o.arch_kps,     &o.arch_desc, &o.arch_n,   &o.lc_buf,    &o.dlt_buf, &o.cjob_buf};
     for (DevBuf* b : bufs) b->release();
     if (sl->trace) std::fclose(sl->trace);
@@ -2034,13 +2148,14 @@ int vs_slam_process_batch_dev(vs_slam* sl, int B, const uint8_t* d_bgr, const fl
         o.bchunk = &c;
         o.next_index = b + 1;
         o.next2_frame = b + 2 < B ? sl->batch[b + 2].get() : nullptr;
-        if (b + 2 < B) {
-            int c2 = c;
-            while (b + 2 >= X.ch[c2]) c2++;
-            o.next2_ready = X.ev[c2 - 1];
-        } else {
-            o.next2_ready = nullptr;
-        }
+        o.next3_frame = b + 3 < B ? sl->batch[b + 3].get() : nullptr;
+        o.next2_ready = o.next3_ready = nullptr;
+        for (int d = 2; d <= 3; d++)
+            if (b + d < B) {
+                int c2 = c;
+                while (b + d >= X.ch[c2]) c2++;
+                (d == 2 ? o.next2_ready : o.next3_ready) = X.ev[c2 - 1];
+            }
         if (o.hprof_armed && --o.hprof.skip < 0) o.hprof.on = sl->trk->phase_prof().on = true, o.hprof_armed = false;
         {
             HostTimer ht(o.hprof, kHFrame);
@@ -2057,6 +2172,8 @@ int vs_slam_process_batch_dev(vs_slam* sl, int B, const uint8_t* d_bgr, const fl
     o.next_ready = nullptr;
     o.next2_frame = nullptr;
     o.next2_ready = nullptr;
+    o.next3_frame = nullptr;
+    o.next3_ready = nullptr;
     o.next_kps_ready = false;
     o.bframes = nullptr;
     o.bchunk = nullptr;
@@ -2066,7 +2183,7 @@ int vs_slam_process_batch_dev(vs_slam* sl, int B, const uint8_t* d_bgr, const fl
     o.tspec.valid = false;
     if (rc == VS_OK && o.err != VS_OK) rc = o.err;
     o.err = VS_OK;
-    o.cspec.valid = false;
+    for (auto& E : o.cspec) E.valid = false;
     o.spec_req.pending = false;
     // The helper's next-batch enqueue has finished before the call returns, so no thread of this
     // vs_slam touches the context's scratch once the caller has it back; the prefetched batch's
