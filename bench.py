@@ -991,9 +991,11 @@ def main():
                 "effective_frac": round(eff_achieved / FP32_MFMA_PEAK_TFLOPS, 4),
                 "effective_note": "direct-convolution FLOPs (the algorithmic work of conv1a + conv1b) / time: the "
                                   "throughput a direct kernel would need to match; with Winograd it can exceed the peak",
-                "note": f"network on the extraction stream's CU set (all CUs but VS_SLAM_TRACK_CUS = {track_cus} "
-                        f"and VS_SLAM_SPEC_CUS = {spec_cus} for the speculative chain), "
-                        "overlapped with tracking; peak is the whole chip's (so frac is a lower bound of the "
+                "note": f"network on the extraction stream's CU set (all CUs but the VS_SLAM_TRACK_CUS = {track_cus} "
+                        "tracking CUs; " + (f"shared with the VS_SLAM_SPEC_CUS = {spec_cus} CUs of the speculative chains"
+                                           if os.environ.get("VS_SLAM_NET_SET", "spec") in ("spec", "all") else
+                                           f"without the VS_SLAM_SPEC_CUS = {spec_cus} CUs of the speculative chains") +
+                        "), overlapped with tracking; peak is the whole chip's (so frac is a lower bound of the "
                         "utilisation of the CUs the network holds)",
                 "alone_whole_chip": alone,
             },

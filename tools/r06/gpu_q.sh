@@ -1,0 +1,24 @@
+#!/bin/bash
+# Round-6: the headline is now bound by the extraction stream; CU-set and chunk-size A/B (same box)
+export TMPDIR=/tmp
+O=gpurun_out/${GPU_OUT:-r06q}; mkdir -p $O
+( while sleep 45; do echo "[hb] $(date +%T)"; done ) & HB=$!
+trap "kill $HB" EXIT
+H="--no-cpu-baseline --no-frontend --mono-steps 0 --ba-reps 0"
+run() {  # name, env...
+  local n=$1; shift
+  env "$@" timeout -k 10 300 python -u bench.py $H > $O/b_$n.json 2> $O/b_$n.err || { tail -20 $O/b_$n.err; return 1; }
+  python3 -c "
+import json; d=json.loads(open('$O/b_$n.json').read().strip().splitlines()[-1]); s=d['stage_ms_per_frame']
+net=sum(v for k,v in s.items() if k.startswith('conv') or k.startswith('head') or k=='gray_norm')
+print('$n', d['value'], d['ms_per_step'], 'net/frame %.4f' % net, 'conv1', d['roofline']['avg_launch_ms'])"
+}
+run base VS_X=0 &&
+run t24 VS_SLAM_TRACK_CUS=24 &&
+run t16 VS_SLAM_TRACK_CUS=16 &&
+run s4 VS_SLAM_SPEC_CUS=4 &&
+run ch16 VS_SLAM_CHUNK=16 &&
+run ch12 VS_SLAM_CHUNK=12 &&
+run nettrack VS_SLAM_NET_SET=track &&
+run netspec VS_SLAM_NET_SET=spec &&
+run base2 VS_X=0

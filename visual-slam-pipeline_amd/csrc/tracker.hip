@@ -629,9 +629,13 @@ struct GpuOps {
                 if (std::strcmp(ps, "all") == 0)
                     for (int k = 0; k < words; k++) pm[k] = tm[k] | xm[k] | sm[k];
             }
-            // VS_SLAM_NET_SET = spec / track / all: the network stream also on the speculative chain's
-            // CUs, the tracking CUs or both (experiments: those CUs idle between latency-bound kernels)
-            if (const char* ns = std::getenv("VS_SLAM_NET_SET")) {
+            // VS_SLAM_NET_SET = spec (default) / none / track / all: the network stream also on the
+            // speculative chains' CUs (with two chains in flight they wait for the network's frames
+            // anyway; the headline is extraction-bound: +3.5 %, profiles/r06s_net_on_spec_cus_ab.txt), on
+            // the tracking CUs (-9 %: the tracking chain is latency-bound) or both
+            {
+                const char* ns = std::getenv("VS_SLAM_NET_SET");
+                if (!ns) ns = "spec";
                 const bool wspec = std::strcmp(ns, "spec") == 0 || std::strcmp(ns, "all") == 0;
                 const bool wtrack = std::strcmp(ns, "track") == 0 || std::strcmp(ns, "all") == 0;
                 for (int k = 0; k < words; k++) xm[k] |= (wspec ? sm[k] : 0u) | (wtrack ? tm[k] : 0u);

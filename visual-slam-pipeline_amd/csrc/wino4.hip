@@ -50,16 +50,25 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int kW4Patch = 18;                 // 18 x 18 input patch
 constexpr int kW4NP = kW4Patch * kW4Patch;   // 324
+// The patch in LDS: rows kW4RS floats apart, channels W4Geo::CS apart.  A transform lane (channel tc,
+// tile row a, tile column b) reads at tc CS + 4 a kW4RS + 4 b (+ the same row / column offset in every
+// lane): with 4 kW4RS = 16 mod 64 and CS = 2 mod 64 the 32 lanes of a ds_read_b64 group fall on 32
+// distinct bank pairs (row stride 18 and channel stride 512 gave up to 4-way conflicts).
+constexpr int kW4RS = 20;
+constexpr int kW4PadSlot = kW4Patch * kW4RS;  // 360: 16 dummy slots after the patch (a partly real wave's rest)
 // per k-step of 4 SUB channels (SUB 4-channel MFMA sub-steps between two barriers)
 template <int SUB> struct W4Geo {
     static constexpr int CH = 4 * SUB;
     static constexpr int V = 8 * CH * 16 * 6;   // V image: [row 8][ch][tile 16][col 6] (rows 6, 7: dummy)
-    static constexpr int X = CH * 512;          // patch: [ch][512 slots] (slots >= 324: dummy)
+    static constexpr int CS = 386;              // patch channel stride: 18 rows x kW4RS + 16 dummy slots + 10, = 2 mod 64
+    static constexpr int X = CH * CS;           // patch: [ch][CS]
     static constexpr int OffV = 0;
     static constexpr int OffX = 2 * V;
     static constexpr int OffG = OffX + 2 * X;
     static constexpr int Main = OffG + 400;     // + the FUSE1A gray patch (20 x 20)
-    static constexpr int Lds = Main > 16384 ? Main : 16384;  // epilogue: partial halves, then the outputs
+    static constexpr int YS = 16 * 16 + 4;       // epilogue: a tile's 16 px x 16 ch of a half, 4 floats of skew
+    static constexpr int Epi = 64 * YS > 16384 ? 64 * YS : 16384;
+    static constexpr int Lds = Main > Epi ? Main : Epi;  // epilogue: partial halves, then the outputs
     static_assert(Lds * 4 <= 160 * 1024, "LDS");
 };
 constexpr int kW4B = 4 * 2 * 64 * 20;        // B operands per 4 channels: [cg 4][xh 2][lane 64][20 (18 used)]
@@ -136,7 +145,9 @@ __global__ __launch_bounds__(512, 1) void k_wino4(WinoArgs wa) {
     // on the other waves of the SIMD pairs.
     const int p = ((wv + 2) & 7) * 64 + lane;
     const bool own_px = p < kW4NP;
+    const bool dummy_wave = ((wv + 2) & 7) * 64 >= kW4NP;  // wave-uniform: no patch pixel at all
     const int ppy = p / kW4Patch, ppx = p - (p / kW4Patch) * kW4Patch;
+    const int pq = own_px ? ppy * kW4RS + ppx : kW4PadSlot + (lane & 15);  // the slot's place in the LDS patch
     const int gy = y0 - 1 + ppy, gx = x0 - 1 + ppx;
     const bool pin = own_px && gy >= 0 && gy < H && gx >= 0 && gx < W;
     const float* src = in + (((size_t)b * H + (pin ? gy : 0)) * W + (pin ? gx : 0)) * in_cstride + in_coff;
@@ -161,6 +172,7 @@ __global__ __launch_bounds__(512, 1) void k_wino4(WinoArgs wa) {
 #pragma unroll
     for (int u = 0; u < SUB; u++) rx[u] = f32x4{0.f, 0.f, 0.f, 0.f};
     auto fetch_x = [&](auto g_c, int c) {
+        if (dummy_wave) return;
         if constexpr (!FUSE1A) {
             // src is clamped into the image (pin == false: pixel 0 of the frame); put_x zeroes what lies outside
             if (!decltype(g_c)::value || c < nk)
@@ -171,8 +183,8 @@ __global__ __launch_bounds__(512, 1) void k_wino4(WinoArgs wa) {
     // patch of k-step c -> lds[X slot]: [ch][slot]
     auto put_x = [&](int slot, auto g_c, int c) {
         if (decltype(g_c)::value && c >= nk) return;
-        if (VS_W4_ABL == 2) return;
-        float* xs = lds + Geo::OffX + slot * Geo::X + p;
+        if (VS_W4_ABL == 2 || dummy_wave) return;
+        float* xs = lds + Geo::OffX + slot * Geo::X + pq;
         if constexpr (FUSE1A) {
             // the k-step's channels' 9 taps + bias are wave-uniform: scalar loads, v_fma_f32 with SGPR operands
             const f32x4* wp = reinterpret_cast<const f32x4*>(w1a + (size_t)(CH * c) * 12);
@@ -183,11 +195,11 @@ __global__ __launch_bounds__(512, 1) void k_wino4(WinoArgs wa) {
                 float a = q2[1];
 #pragma unroll
                 for (int k = 0; k < 9; k++) a = __builtin_fmaf(gnb[k], wk[k], a);
-                xs[cc * 512] = masked(a > 0.0f ? a : 0.0f);
+                xs[cc * Geo::CS] = masked(a > 0.0f ? a : 0.0f);
             }
         } else {
 #pragma unroll
-            for (int cc = 0; cc < CH; cc++) xs[cc * 512] = masked(rx[cc >> 2][cc & 3]);
+            for (int cc = 0; cc < CH; cc++) xs[cc * Geo::CS] = masked(rx[cc >> 2][cc & 3]);
         }
     };
 
@@ -216,7 +228,7 @@ __global__ __launch_bounds__(512, 1) void k_wino4(WinoArgs wa) {
             default: T.rr[0] = 1, T.rr[1] = 3, T.rr[2] = 5, T.rr[3] = 5;
                 T.kc[0] = 4.f, T.kc[1] = -5.f, T.kc[2] = 1.f, T.kc[3] = 0.f; break;
         }
-        T.xbase = tc * 512 + (4 * (tt >> 2)) * kW4Patch + 4 * (tt & 3);
+        T.xbase = tc * Geo::CS + (4 * (tt >> 2)) * kW4RS + 4 * (tt & 3);
         T.vbase = ((ti * CH + tc) * 16 + tt) * 6;
     }
     auto transform = [&](int u, int slot, auto g_c, int c) {
@@ -229,7 +241,7 @@ __global__ __launch_bounds__(512, 1) void k_wino4(WinoArgs wa) {
         for (int r = 0; r < 4; r++) {
 #pragma unroll
             for (int h = 0; h < 3; h++) {
-                const f32x2 v = *reinterpret_cast<const f32x2*>(xs + T.rr[r] * kW4Patch + 2 * h);
+                const f32x2 v = *reinterpret_cast<const f32x2*>(xs + T.rr[r] * kW4RS + 2 * h);
                 e[r][2 * h] = v[0];
                 e[r][2 * h + 1] = v[1];
             }
@@ -355,20 +367,22 @@ __global__ __launch_bounds__(512, 1) void k_wino4(WinoArgs wa) {
             }
         }
     }
-    float* yp = lds;  // [cg][tile][16 px][16 ch]: the xh = 1 halves
+    // [cg][tile][16 px][16 ch] with tiles YS floats apart: the xh = 1 halves (4 YS = 16 mod 32, so lanes
+    // lk = 0 and 1 of a ds_read_b32 group land on different banks)
+    float* yp = lds;
     float* so = lds;  // then [pixel][64 ch]: the outputs (after every half has been read)
     if (xh == 1) {
 #pragma unroll
         for (int r = 0; r < 4; r++)
 #pragma unroll
-            for (int e = 0; e < 16; e++) yp[((cg * 16 + 4 * lk + r) * 16 + e) * 16 + li] = y[r][e];
+            for (int e = 0; e < 16; e++) yp[(cg * 16 + 4 * lk + r) * Geo::YS + e * 16 + li] = y[r][e];
     }
     __syncthreads();
     if (xh == 0) {
 #pragma unroll
         for (int r = 0; r < 4; r++)
 #pragma unroll
-            for (int e = 0; e < 16; e++) y[r][e] += yp[((cg * 16 + 4 * lk + r) * 16 + e) * 16 + li];
+            for (int e = 0; e < 16; e++) y[r][e] += yp[(cg * 16 + 4 * lk + r) * Geo::YS + e * 16 + li];
     }
     __syncthreads();
     if (xh == 0) {
