@@ -114,8 +114,11 @@ VS_HD inline double split_point(double a, double b) {
     return g > a && g < b ? g : 0.5 * (a + b);
 }
 
-VS_HD inline int poly_real_roots(const double* c, double* W, int wst) {
-#define WS(i) W[(size_t)(i) * wst]
+// ---- the root search in three shared pieces: the host loop below (poly_real_roots) and the
+// device's wave-parallel search (emat.hip, one interval per lane) call the same arithmetic ----
+
+// the degree (vanishing leading terms dropped; 0 = nothing to search) and the search bound
+VS_HD inline int roots_degree_bound(const double* c, double& bound_out) {
     // (static indices only: the coefficients stay in registers)
     double amax = 0;
     VS_UNROLL
@@ -174,24 +177,101 @@ VS_HD inline int poly_real_roots(const double* c, double* W, int wst) {
         const double cap = ldexp(1.0, e < 1000 ? e : 1000);
         bound = bound < cap ? bound : cap;
     }
+    bound_out = bound;
+    return n;
+}
+
+// m-th derivative: c[k + m] (k + m)! / k!, zero above the degree n - m
+VS_HD inline void roots_deriv(const double* c, int n, int m, double D[11]) {
+    VS_UNROLL
+    for (int k = 0; k <= 10 - m; k++) {
+        double f = 1.0;
+        for (int q = 0; q < m; q++) f *= (double)(k + m - q);
+        D[k] = k + m <= n ? c[k + m] * f : 0.0;
+    }
+}
+
+// One monotone interval [a, b] (the i-th, between two cuts) of derivative level m: 0 = no root,
+// 1 = the left cut a itself is taken as the root (a near-double root), 2 = a root refined in (a, b).
+VS_HD inline int roots_interval(const double D[11], int m, int i, double a, double b, double& root_out) {
+#define VS_EM_EV(x, v)                                       \
+    do {                                                     \
+        v = D[10 - m];                                       \
+        VS_UNROLL                                            \
+        for (int k = 9 - m; k >= 0; k--) v = v * (x) + D[k]; \
+    } while (0)
+    double fa, fb0;
+    VS_EM_EV(a, fa);
+    VS_EM_EV(b, fb0);
+    // a cut (a root of the derivative, refined to kCutTol only) at which this level's value is
+    // within rounding noise of zero is a (near-)double root: the two roots lie within the
+    // noise of the cut, so a sign test on either side can miss both; the cut is taken as the
+    // root instead (an exact double root has no sign change at all)
+    bool at_root = fa == 0;
+    if (!at_root && i > 0) {
+        double s = fabs(D[10 - m]);
+        const double ax = fabs(a);
+        VS_UNROLL
+        for (int k = 9 - m; k >= 0; k--) s = s * ax + fabs(D[k]);
+        at_root = fabs(fa) <= 0x1p-48 * s;
+    }
+    if (at_root) {
+        root_out = a;
+        return 1;
+    }
+    if ((fa < 0) == (fb0 < 0)) return 0;
+    // safeguarded Newton (rtsafe): a Newton step when it stays inside the bracket and at
+    // least halves the step before last, else bisection; the bracket keeps the sign change
+    double x = wide_bracket(a, b) ? split_point(a, b) : 0.5 * (a + b);
+    double dxold = b - a, dx = dxold, root = x;
+    for (int it = 0; it < 100; it++) {
+        double f = D[10 - m], df = 0.0;  // value and derivative (Horner pair)
+        VS_UNROLL
+        for (int k = 9 - m; k >= 0; k--) {
+            df = df * x + f;
+            f = f * x + D[k];
+        }
+        root = x;
+        if (f == 0) break;
+        if ((f < 0) == (fa < 0))
+            a = x;
+        else
+            b = x;
+        double mid = 0.5 * (a + b);
+        if (mid <= a || mid >= b) break;  // the bracket is at adjacent doubles
+        // a bracket spanning orders of magnitude is split geometrically (or at 0)
+        if (wide_bracket(a, b)) mid = split_point(a, b);
+        const double xn = df != 0 ? x - f / df : mid;
+        if (!(xn > a && xn < b) || fabs(2.0 * f) > fabs(dxold * df)) {
+            dxold = dx;
+            dx = mid - a;
+            x = mid;
+        } else {
+            dxold = dx;
+            dx = x - xn;
+            x = xn;
+        }
+        if (fabs(dx) <= (m == 0 ? kRootTol : kCutTol) * fabs(x)) {
+            root = x;
+            break;
+        }
+    }
+    root_out = root;
+    return 2;
+#undef VS_EM_EV
+}
+
+VS_HD inline int poly_real_roots(const double* c, double* W, int wst) {
+#define WS(i) W[(size_t)(i) * wst]
+    double bound;
+    const int n = roots_degree_bound(c, bound);
+    if (n <= 0) return 0;
     int nr = 0;
     VS_UNROLL
     for (int m = 9; m >= 0; m--) {
         if (m > n - 1) continue;
-        // m-th derivative: c[k + m] (k + m)! / k!, zero above the degree n - m
         double D[11];
-        VS_UNROLL
-        for (int k = 0; k <= 10 - m; k++) {
-            double f = 1.0;
-            for (int q = 0; q < m; q++) f *= (double)(k + m - q);
-            D[k] = k + m <= n ? c[k + m] * f : 0.0;
-        }
-#define VS_EM_EV(x, v)                                \
-    do {                                              \
-        v = D[10 - m];                                \
-        VS_UNROLL                                     \
-        for (int k = 9 - m; k >= 0; k--) v = v * (x) + D[k]; \
-    } while (0)
+        roots_deriv(c, n, m, D);
         int nc = 0;
         WS(kWsC + nc++) = -bound;
         for (int i = 0; i < nr; i++) {
@@ -201,80 +281,25 @@ VS_HD inline int poly_real_roots(const double* c, double* W, int wst) {
         WS(kWsC + nc++) = bound;
         int cnt = 0;
         for (int i = 0; i + 1 < nc; i++) {
-            double a = WS(kWsC + i), b = WS(kWsC + i + 1);
-            double fa, fb0;
-            VS_EM_EV(a, fa);
-            VS_EM_EV(b, fb0);
-            // a cut (a root of the derivative, refined to kCutTol only) at which this level's value is
-            // within rounding noise of zero is a (near-)double root: the two roots lie within the
-            // noise of the cut, so a sign test on either side can miss both; the cut is taken as the
-            // root instead (an exact double root has no sign change at all)
-            bool at_root = fa == 0;
-            if (!at_root && i > 0) {
-                double s = fabs(D[10 - m]);
-                const double ax = fabs(a);
-                VS_UNROLL
-                for (int k = 9 - m; k >= 0; k--) s = s * ax + fabs(D[k]);
-                at_root = fabs(fa) <= 0x1p-48 * s;
-            }
-            if (at_root) {
-                if (cnt == 0 || WS(kWsN + cnt - 1) != a) WS(kWsN + cnt++) = a;
-                continue;
-            }
-            if ((fa < 0) == (fb0 < 0)) continue;
-            // safeguarded Newton (rtsafe): a Newton step when it stays inside the bracket and at
-            // least halves the step before last, else bisection; the bracket keeps the sign change
-            double x = wide_bracket(a, b) ? split_point(a, b) : 0.5 * (a + b);
-            double dxold = b - a, dx = dxold, root = x;
-            for (int it = 0; it < 100; it++) {
-                double f = D[10 - m], df = 0.0;  // value and derivative (Horner pair)
-                VS_UNROLL
-                for (int k = 9 - m; k >= 0; k--) {
-                    df = df * x + f;
-                    f = f * x + D[k];
-                }
-                root = x;
-                if (f == 0) break;
-                if ((f < 0) == (fa < 0))
-                    a = x;
-                else
-                    b = x;
-                double mid = 0.5 * (a + b);
-                if (mid <= a || mid >= b) break;  // the bracket is at adjacent doubles
-                // a bracket spanning orders of magnitude is split geometrically (or at 0)
-                if (wide_bracket(a, b)) mid = split_point(a, b);
-                const double xn = df != 0 ? x - f / df : mid;
-                if (!(xn > a && xn < b) || fabs(2.0 * f) > fabs(dxold * df)) {
-                    dxold = dx;
-                    dx = mid - a;
-                    x = mid;
-                } else {
-                    dxold = dx;
-                    dx = x - xn;
-                    x = xn;
-                }
-                if (fabs(dx) <= (m == 0 ? kRootTol : kCutTol) * fabs(x)) {
-                    root = x;
-                    break;
-                }
-            }
-            WS(kWsN + cnt++) = root;
+            double r;
+            const int kind = roots_interval(D, m, i, WS(kWsC + i), WS(kWsC + i + 1), r);
+            // an at-root cut repeating the last root found is the same root
+            if (kind == 1 && !(cnt == 0 || WS(kWsN + cnt - 1) != r)) continue;
+            if (kind != 0) WS(kWsN + cnt++) = r;
         }
         for (int i = 0; i < cnt; i++) WS(kWsR + i) = WS(kWsN + i);
         nr = cnt;
-#undef VS_EM_EV
     }
     return nr;
 #undef WS
 }
 
-// 5-point solver: q1, q2 = 5 normalised correspondences (x, y interleaved, double).  Writes up to
-// kMaxModels essential matrices to Eout[k * 9 + q] (row-major, unit Frobenius norm) and returns the
-// count.  W / wst: the workspace (kWsSize doubles).
-template <class Mark = vs_pnp::NoMark>
-VS_HD inline int five_point(const double* q1, const double* q2, double* Eout, double* W, int wst, Mark mark = Mark()) {
-#define WS(i) W[(size_t)(i) * wst]
-#define AA(r, c) WS(kWsA + (r) * 20 + (c))
+// ---- five_point in stages (the host's sequential solver below; the device's wave-parallel one in
+// emat.hip runs the same stage arithmetic) ----
+
+// stage 1: the rotated orthonormal basis B of the null space of the 5 x 9 epipolar system (q1, q2 =
+// 5 normalised correspondences, x, y interleaved); false when the system is degenerate
+VS_HD inline bool fp_basis(const double* q1, const double* q2, double B[4][9]) {
     // epipolar rows: q2^T E q1 = 0 with e = (e11 e12 e13 e21 e22 e23 e31 e32 e33)
     double Q[5][9];
     VS_UNROLL
@@ -302,7 +327,7 @@ VS_HD inline int five_point(const double* q1, const double* q2, double* Eout, do
                 big = fabs(Q[r][k]);
                 p = r;
             }
-        if (!(big > 1e-300)) return 0;
+        if (!(big > 1e-300)) return false;
         VS_UNROLL
         for (int r = k + 1; r < 5; r++) {
             const bool sw = r == p;
@@ -320,7 +345,6 @@ VS_HD inline int five_point(const double* q1, const double* q2, double* Eout, do
             for (int j = k; j < 9; j++) Q[r][j] -= f * Q[k][j];
         }
     }
-    double B[4][9];
     VS_UNROLL
     for (int f = 0; f < 4; f++) {
         VS_UNROLL
@@ -348,7 +372,7 @@ VS_HD inline int five_point(const double* q1, const double* q2, double* Eout, do
         VS_UNROLL
         for (int j = 0; j < 9; j++) nn += B[f][j] * B[f][j];
         nn = sqrt(nn);
-        if (!(nn > 0)) return 0;
+        if (!(nn > 0)) return false;
         VS_UNROLL
         for (int j = 0; j < 9; j++) B[f][j] /= nn;
     }
@@ -367,44 +391,161 @@ VS_HD inline int five_point(const double* q1, const double* q2, double* Eout, do
             VS_UNROLL
             for (int j = 0; j < 9; j++) B[f][j] = H[f][j];
     }
+    return true;
+}
+
+// stage 2: the coefficient column of the monomial lambda_i lambda_j lambda_k (i <= j <= k, lambda =
+// (x, y, z, 1)) of the 10 x 20 matrix — row 0 = det(E), rows 1..9 = the entries of 2 E E^T E -
+// tr(E E^T) E, each the sum of its distinct symmetrised trilinear terms; B row-major [4][9].
+// Returns the column (Nister's monomial order).
+VS_HD inline int fp_column(const double* B, int i, int j, int k, double acc[10]) {
+    int ex[4] = {0, 0, 0, 0};
+    ex[i]++;
+    ex[j]++;
+    ex[k]++;
+    const int col = nister_index(ex[0], ex[1], ex[2]);
+    const int perm[6][3] = {{i, j, k}, {i, k, j}, {j, i, k}, {j, k, i}, {k, i, j}, {k, j, i}};
+    VS_UNROLL
+    for (int r = 0; r < 10; r++) acc[r] = 0;
+    VS_UNROLL
+    for (int pi = 0; pi < 6; pi++) {
+        bool dup = false;
+        VS_UNROLL
+        for (int pj = 0; pj < pi; pj++)
+            dup |= perm[pj][0] == perm[pi][0] && perm[pj][1] == perm[pi][1] && perm[pj][2] == perm[pi][2];
+        if (dup) continue;
+        const double* Ea = B + 9 * perm[pi][0];
+        const double* Eb = B + 9 * perm[pi][1];
+        const double* Ec = B + 9 * perm[pi][2];
+        acc[0] += det3m(Ea, Eb, Ec);
+        double T[9];
+        trilin(Ea, Eb, Ec, T);
+        VS_UNROLL
+        for (int e = 0; e < 9; e++) acc[1 + e] += T[e];
+    }
+    return col;
+}
+
+// the triples (i <= j <= k) of stage 2 in their loop order, packed i | j << 2 | k << 4
+constexpr unsigned char kFpTriples[20] = {0x00, 0x10, 0x20, 0x30, 0x14, 0x24, 0x34, 0x28, 0x38, 0x3c,
+                                          0x15, 0x25, 0x35, 0x29, 0x39, 0x3d, 0x2a, 0x3a, 0x3e, 0x3f};
+
+// stage 4: B(z) = rows <e> - z <f> of the reduced matrix (AA(r, c) = W[(r * 20 + c) * wst]) over
+// (x, y, 1) — x-poly degree 3, y-poly degree 3, 1-poly degree 4, coefficient arrays indexed by the
+// power of z (rest monomials xz^2 xz x yz^2 yz y z^3 z^2 z 1) — and det B(z) (degree 10) by cofactor
+// expansion with polynomial products
+VS_HD inline void fp_bpoly(const double* W, int wst, double bx[3][4], double by[3][4], double b1[3][5], double c[11]) {
+#define AA(r, cc) W[(size_t)((r) * 20 + (cc)) * wst]
+    VS_UNROLL
+    for (int i = 0; i < 3; i++) {
+        const int re = 4 + 2 * i, rf = 5 + 2 * i;
+        bx[i][3] = -AA(rf, 10);
+        bx[i][2] = AA(re, 10) - AA(rf, 11);
+        bx[i][1] = AA(re, 11) - AA(rf, 12);
+        bx[i][0] = AA(re, 12);
+        by[i][3] = -AA(rf, 13);
+        by[i][2] = AA(re, 13) - AA(rf, 14);
+        by[i][1] = AA(re, 14) - AA(rf, 15);
+        by[i][0] = AA(re, 15);
+        b1[i][4] = -AA(rf, 16);
+        b1[i][3] = AA(re, 16) - AA(rf, 17);
+        b1[i][2] = AA(re, 17) - AA(rf, 18);
+        b1[i][1] = AA(re, 18) - AA(rf, 19);
+        b1[i][0] = AA(re, 19);
+    }
+#undef AA
+    auto pmul = [](const double* a, int na, const double* b, int nb, double* out) {
+        for (int k = 0; k <= na + nb; k++) out[k] = 0;
+        for (int i = 0; i <= na; i++)
+            for (int j = 0; j <= nb; j++) out[i + j] += a[i] * b[j];
+    };
+    VS_UNROLL
+    for (int k = 0; k < 11; k++) c[k] = 0;
+    // det = bx0 (by1 b12 - b11 by2) - by0 (bx1 b12 - b11 bx2) + b10 (bx1 by2 - by1 bx2)
+    double t1[8], t2[8], m1[8], full[11];
+    pmul(by[1], 3, b1[2], 4, t1);
+    pmul(b1[1], 4, by[2], 3, t2);
+    for (int k = 0; k <= 7; k++) m1[k] = t1[k] - t2[k];
+    pmul(bx[0], 3, m1, 7, full);
+    for (int k = 0; k <= 10; k++) c[k] += full[k];
+    pmul(bx[1], 3, b1[2], 4, t1);
+    pmul(b1[1], 4, bx[2], 3, t2);
+    for (int k = 0; k <= 7; k++) m1[k] = t1[k] - t2[k];
+    pmul(by[0], 3, m1, 7, full);
+    for (int k = 0; k <= 10; k++) c[k] -= full[k];
+    double u1[7], u2[7], m2[7];
+    pmul(bx[1], 3, by[2], 3, u1);
+    pmul(by[1], 3, bx[2], 3, u2);
+    for (int k = 0; k <= 6; k++) m2[k] = u1[k] - u2[k];
+    pmul(b1[0], 4, m2, 6, full);
+    for (int k = 0; k <= 10; k++) c[k] += full[k];
+}
+
+// stage 6: the model of root z — (x, y) from the null vector of B(z) (the largest cross product of
+// two rows), E = x E0 + y E1 + z E2 + E3 normalised to unit Frobenius norm; false when degenerate
+VS_HD inline bool fp_model(double z, const double (*bx)[4], const double (*by)[4], const double (*b1)[5],
+                           const double* B, double* Eout) {
+    double Bz[3][3];
+    VS_UNROLL
+    for (int i = 0; i < 3; i++) {
+        Bz[i][0] = ((bx[i][3] * z + bx[i][2]) * z + bx[i][1]) * z + bx[i][0];
+        Bz[i][1] = ((by[i][3] * z + by[i][2]) * z + by[i][1]) * z + by[i][0];
+        Bz[i][2] = (((b1[i][4] * z + b1[i][3]) * z + b1[i][2]) * z + b1[i][1]) * z + b1[i][0];
+    }
+    double best0 = 0, best1 = 0, best2 = 0, bn = -1;
+    VS_UNROLL
+    for (int a = 0; a < 3; a++)
+        VS_UNROLL
+        for (int b = a + 1; b < 3; b++) {
+            const double cx = Bz[a][1] * Bz[b][2] - Bz[a][2] * Bz[b][1];
+            const double cy = Bz[a][2] * Bz[b][0] - Bz[a][0] * Bz[b][2];
+            const double cz = Bz[a][0] * Bz[b][1] - Bz[a][1] * Bz[b][0];
+            const double nn = cx * cx + cy * cy + cz * cz;
+            if (nn > bn) {
+                bn = nn;
+                best0 = cx;
+                best1 = cy;
+                best2 = cz;
+            }
+        }
+    const double nrm = sqrt(bn > 0 ? bn : 0.0);
+    if (!(nrm > 0)) return false;
+    const double v0 = best0 / nrm, v1 = best1 / nrm, v2 = best2 / nrm;
+    if (fabs(v2) < 1e-10) return false;
+    const double x = v0 / v2, y = v1 / v2;
+    double e[9], en = 0;
+    VS_UNROLL
+    for (int q = 0; q < 9; q++) {
+        e[q] = B[q] * x + B[9 + q] * y + B[18 + q] * z + B[27 + q];
+        en += e[q] * e[q];
+    }
+    en = sqrt(en);
+    if (!(en > 0)) return false;
+    VS_UNROLL
+    for (int q = 0; q < 9; q++) Eout[q] = e[q] / en;
+    return true;
+}
+
+// 5-point solver: q1, q2 = 5 normalised correspondences (x, y interleaved, double).  Writes up to
+// kMaxModels essential matrices to Eout[k * 9 + q] (row-major, unit Frobenius norm) and returns the
+// count.  W / wst: the workspace (kWsSize doubles).
+template <class Mark = vs_pnp::NoMark>
+VS_HD inline int five_point(const double* q1, const double* q2, double* Eout, double* W, int wst, Mark mark = Mark()) {
+#define WS(i) W[(size_t)(i) * wst]
+#define AA(r, c) WS(kWsA + (r) * 20 + (c))
+    double B[4][9];
+    if (!fp_basis(q1, q2, B)) return 0;
     mark(0);
-    // 10 x 20 coefficient matrix: row 0 = det(E), rows 1..9 = entries of 2 E E^T E - tr(E E^T) E;
-    // monomial lambda_i lambda_j lambda_k (i <= j <= k, lambda = (x, y, z, 1)) collects the
-    // symmetrised trilinear terms
+    // 10 x 20 coefficient matrix, one column per monomial
     for (int r = 0; r < 10; r++)
         for (int c = 0; c < 20; c++) AA(r, c) = 0;
     VS_UNROLL
-    for (int i = 0; i < 4; i++)
+    for (int t = 0; t < 20; t++) {
+        double acc[10];
+        const int col = fp_column(&B[0][0], kFpTriples[t] & 3, (kFpTriples[t] >> 2) & 3, kFpTriples[t] >> 4, acc);
         VS_UNROLL
-        for (int j = i; j < 4; j++)
-            VS_UNROLL
-            for (int k = j; k < 4; k++) {
-                int ex[4] = {0, 0, 0, 0};
-                ex[i]++;
-                ex[j]++;
-                ex[k]++;
-                const int col = nister_index(ex[0], ex[1], ex[2]);
-                const int perm[6][3] = {{i, j, k}, {i, k, j}, {j, i, k}, {j, k, i}, {k, i, j}, {k, j, i}};
-                double acc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-                VS_UNROLL
-                for (int pi = 0; pi < 6; pi++) {
-                    bool dup = false;
-                    VS_UNROLL
-                    for (int pj = 0; pj < pi; pj++)
-                        dup |= perm[pj][0] == perm[pi][0] && perm[pj][1] == perm[pi][1] && perm[pj][2] == perm[pi][2];
-                    if (dup) continue;
-                    const double* Ea = B[perm[pi][0]];
-                    const double* Eb = B[perm[pi][1]];
-                    const double* Ec = B[perm[pi][2]];
-                    acc[0] += det3m(Ea, Eb, Ec);
-                    double T[9];
-                    trilin(Ea, Eb, Ec, T);
-                    VS_UNROLL
-                    for (int e = 0; e < 9; e++) acc[1 + e] += T[e];
-                }
-                VS_UNROLL
-                for (int r = 0; r < 10; r++) AA(r, col) = acc[r];
-            }
+        for (int r = 0; r < 10; r++) AA(r, col) = acc[r];
+    }
     mark(1);
     // Gauss-Jordan on the first 10 columns (partial pivoting), in the workspace; each step stages
     // the pivot row and then every other row through registers (static column ranges: the loads of
@@ -446,102 +587,14 @@ VS_HD inline int five_point(const double* q1, const double* q2, double* Eout, do
         }
     }
     mark(2);
-    // B(z) rows <e> - z <f> over (x, y, 1): x-poly deg 3, y-poly deg 3, 1-poly deg 4 (coefficient
-    // arrays indexed by the power of z); rest monomials: xz^2 xz x yz^2 yz y z^3 z^2 z 1
-    double bx[3][4], by[3][4], b1[3][5];
-    VS_UNROLL
-    for (int i = 0; i < 3; i++) {
-        const int re = 4 + 2 * i, rf = 5 + 2 * i;
-        bx[i][3] = -AA(rf, 10);
-        bx[i][2] = AA(re, 10) - AA(rf, 11);
-        bx[i][1] = AA(re, 11) - AA(rf, 12);
-        bx[i][0] = AA(re, 12);
-        by[i][3] = -AA(rf, 13);
-        by[i][2] = AA(re, 13) - AA(rf, 14);
-        by[i][1] = AA(re, 14) - AA(rf, 15);
-        by[i][0] = AA(re, 15);
-        b1[i][4] = -AA(rf, 16);
-        b1[i][3] = AA(re, 16) - AA(rf, 17);
-        b1[i][2] = AA(re, 17) - AA(rf, 18);
-        b1[i][1] = AA(re, 18) - AA(rf, 19);
-        b1[i][0] = AA(re, 19);
-    }
-    // det B(z) (degree 10) by cofactor expansion with polynomial products
-    auto pmul = [](const double* a, int na, const double* b, int nb, double* out) {
-        for (int k = 0; k <= na + nb; k++) out[k] = 0;
-        for (int i = 0; i <= na; i++)
-            for (int j = 0; j <= nb; j++) out[i + j] += a[i] * b[j];
-    };
-    double c[11];
-    VS_UNROLL
-    for (int k = 0; k < 11; k++) c[k] = 0;
-    {
-        // det = bx0 (by1 b12 - b11 by2) - by0 (bx1 b12 - b11 bx2) + b10 (bx1 by2 - by1 bx2)
-        double t1[8], t2[8], m1[8], full[11];
-        pmul(by[1], 3, b1[2], 4, t1);
-        pmul(b1[1], 4, by[2], 3, t2);
-        for (int k = 0; k <= 7; k++) m1[k] = t1[k] - t2[k];
-        pmul(bx[0], 3, m1, 7, full);
-        for (int k = 0; k <= 10; k++) c[k] += full[k];
-        pmul(bx[1], 3, b1[2], 4, t1);
-        pmul(b1[1], 4, bx[2], 3, t2);
-        for (int k = 0; k <= 7; k++) m1[k] = t1[k] - t2[k];
-        pmul(by[0], 3, m1, 7, full);
-        for (int k = 0; k <= 10; k++) c[k] -= full[k];
-        double u1[7], u2[7], m2[7];
-        pmul(bx[1], 3, by[2], 3, u1);
-        pmul(by[1], 3, bx[2], 3, u2);
-        for (int k = 0; k <= 6; k++) m2[k] = u1[k] - u2[k];
-        pmul(b1[0], 4, m2, 6, full);
-        for (int k = 0; k <= 10; k++) c[k] += full[k];
-    }
+    double bx[3][4], by[3][4], b1[3][5], c[11];
+    fp_bpoly(W, wst, bx, by, b1, c);
     mark(3);
     const int nz = poly_real_roots(c, W, wst);
     mark(4);
     int count = 0;
-    for (int ri = 0; ri < nz && count < kMaxModels; ri++) {
-        const double z = WS(kWsR + ri);
-        double Bz[3][3];
-        VS_UNROLL
-        for (int i = 0; i < 3; i++) {
-            Bz[i][0] = ((bx[i][3] * z + bx[i][2]) * z + bx[i][1]) * z + bx[i][0];
-            Bz[i][1] = ((by[i][3] * z + by[i][2]) * z + by[i][1]) * z + by[i][0];
-            Bz[i][2] = (((b1[i][4] * z + b1[i][3]) * z + b1[i][2]) * z + b1[i][1]) * z + b1[i][0];
-        }
-        // null vector of Bz: the largest cross product of two rows
-        double best0 = 0, best1 = 0, best2 = 0, bn = -1;
-        VS_UNROLL
-        for (int a = 0; a < 3; a++)
-            VS_UNROLL
-            for (int b = a + 1; b < 3; b++) {
-                const double cx = Bz[a][1] * Bz[b][2] - Bz[a][2] * Bz[b][1];
-                const double cy = Bz[a][2] * Bz[b][0] - Bz[a][0] * Bz[b][2];
-                const double cz = Bz[a][0] * Bz[b][1] - Bz[a][1] * Bz[b][0];
-                const double nn = cx * cx + cy * cy + cz * cz;
-                if (nn > bn) {
-                    bn = nn;
-                    best0 = cx;
-                    best1 = cy;
-                    best2 = cz;
-                }
-            }
-        const double nrm = sqrt(bn > 0 ? bn : 0.0);
-        if (!(nrm > 0)) continue;
-        const double v0 = best0 / nrm, v1 = best1 / nrm, v2 = best2 / nrm;
-        if (fabs(v2) < 1e-10) continue;
-        const double x = v0 / v2, y = v1 / v2;
-        double e[9], en = 0;
-        VS_UNROLL
-        for (int q = 0; q < 9; q++) {
-            e[q] = B[0][q] * x + B[1][q] * y + B[2][q] * z + B[3][q];
-            en += e[q] * e[q];
-        }
-        en = sqrt(en);
-        if (!(en > 0)) continue;
-        VS_UNROLL
-        for (int q = 0; q < 9; q++) Eout[count * 9 + q] = e[q] / en;
-        count++;
-    }
+    for (int ri = 0; ri < nz && count < kMaxModels; ri++)
+        if (fp_model(WS(kWsR + ri), bx, by, b1, &B[0][0], Eout + count * 9)) count++;
     return count;
 #undef AA
 #undef WS
@@ -623,7 +676,7 @@ VS_HD inline bool cheiral_ok(const double* R, const double* t, double x1, double
     double AtA[16], w[4], V[16];
     for (int i = 0; i < 4; i++)
         for (int j = 0; j < 4; j++) AtA[i * 4 + j] = A[0][i] * A[0][j] + A[1][i] * A[1][j] + A[2][i] * A[2][j] + A[3][i] * A[3][j];
-    vs_pnp::sym_eig<4>(AtA, w, V);
+    vs_pnp::sym_eig_static<4>(AtA, w, V);
     const double Q0 = V[0 * 4 + 3], Q1 = V[1 * 4 + 3], Q2 = V[2 * 4 + 3], Q3 = V[3 * 4 + 3];
     if (!(Q2 * Q3 > 0)) return false;
     const double X = Q0 / Q3, Y = Q1 / Q3, Z = Q2 / Q3;

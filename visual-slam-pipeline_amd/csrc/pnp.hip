@@ -796,6 +796,17 @@ static int pnp_table(vs_ctx* ctx, hipStream_t s, int** tab) {
     return VS_OK;
 }
 
+int subset_table(int rows, int n_base, int iters, int* out, hipStream_t s) {
+    VS_ARG(rows > 0 && n_base > 5 && iters > 0 && out, "subset_table: bad arguments");
+    PnpHyp T{};
+    T.subset = out;
+    T.stride = iters;
+    T.tab_n0 = -1;
+    hipLaunchKernelGGL(k_pnp_subsets, dim3(rows), dim3(256), 0, s, nullptr, n_base, iters, 0, T);
+    VS_HIP(hipGetLastError());
+    return VS_OK;
+}
+
 int pnp_reserve(vs_ctx* ctx, hipStream_t s) {
     int* tab;
     return pnp_table(ctx, s, &tab);

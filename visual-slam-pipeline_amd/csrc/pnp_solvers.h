@@ -204,6 +204,85 @@ VS_HD void sym_eig(double* A, double* w, double* V) {
     }
 }
 
+// sym_eig with every index static once unrolled (the device keeps A, V and w in registers instead of
+// a private array indexed at run time): the same rotations in the same order, the same selection sort
+// (the running maximum's value tracked beside its position; the swaps as selects), the same results.
+template <int N>
+VS_HD void sym_eig_static(double* A, double* w, double* V) {
+    VS_UNROLL
+    for (int i = 0; i < N; i++)
+        VS_UNROLL
+        for (int j = 0; j < N; j++) V[i * N + j] = (i == j) ? 1.0 : 0.0;
+    double total = 0;
+    VS_UNROLL
+    for (int i = 0; i < N * N; i++) total += A[i] * A[i];
+    VS_NOUNROLL
+    for (int sweep = 0; sweep < 30; sweep++) {
+        double off = 0;
+        VS_UNROLL
+        for (int p = 0; p < N; p++)
+            VS_UNROLL
+            for (int q = p + 1; q < N; q++) off += A[p * N + q] * A[p * N + q];
+        if (!(off > 1e-32 * total)) break;
+        VS_UNROLL
+        for (int p = 0; p < N - 1; p++)
+            VS_UNROLL
+            for (int q = p + 1; q < N; q++) {
+                double c, s;
+                if (!jacobi_angle(A[p * N + p], A[q * N + q], A[p * N + q], c, s)) continue;
+                VS_UNROLL
+                for (int k = 0; k < N; k++) {
+                    const double akp = A[k * N + p], akq = A[k * N + q];
+                    A[k * N + p] = c * akp - s * akq;
+                    A[k * N + q] = s * akp + c * akq;
+                }
+                VS_UNROLL
+                for (int k = 0; k < N; k++) {
+                    const double apk = A[p * N + k], aqk = A[q * N + k];
+                    A[p * N + k] = c * apk - s * aqk;
+                    A[q * N + k] = s * apk + c * aqk;
+                }
+                VS_UNROLL
+                for (int k = 0; k < N; k++) {
+                    const double vkp = V[k * N + p], vkq = V[k * N + q];
+                    V[k * N + p] = c * vkp - s * vkq;
+                    V[k * N + q] = s * vkp + c * vkq;
+                }
+            }
+    }
+    VS_UNROLL
+    for (int i = 0; i < N; i++) w[i] = A[i * N + i];
+    VS_UNROLL
+    for (int i = 0; i < N - 1; i++) {  // selection sort, descending
+        int m = i;
+        double wm = w[i];
+        VS_UNROLL
+        for (int j = i + 1; j < N; j++)
+            if (w[j] > wm) {
+                wm = w[j];
+                m = j;
+            }
+        if (m != i) {
+            const double tw = w[i];
+            w[i] = wm;
+            VS_UNROLL
+            for (int j = i + 1; j < N; j++)
+                if (j == m) w[j] = tw;
+            VS_UNROLL
+            for (int k = 0; k < N; k++) {
+                const double tv = V[k * N + i];
+                double vm = tv;
+                VS_UNROLL
+                for (int j = i + 1; j < N; j++) vm = j == m ? V[k * N + j] : vm;
+                V[k * N + i] = vm;
+                VS_UNROLL
+                for (int j = i + 1; j < N; j++)
+                    if (j == m) V[k * N + j] = tv;
+            }
+        }
+    }
+}
+
 // Parallel-order Jacobi (even N): each sweep is N - 1 rounds of N / 2 disjoint rotations in the
 // round-robin (circle) order; a round takes every angle from the matrix as the round starts, then
 // applies all column rotations of A, all row rotations of A, and all column rotations of V.

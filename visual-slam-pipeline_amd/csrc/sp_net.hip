@@ -1274,6 +1274,7 @@ int launch_wino(const DevLayer& L, const float* in, int in_cstride, int in_coff,
     // F(2x2, 3x3) (A/B)
     if (L.wu4 && wino4_enabled() && (long)((H + 15) / 16) * ((W + 15) / 16) * (L.cout_pad / 64) >= wino4_min_wg()) {
         a.wu = L.wu4;
+        a.wu3 = L.wu4x3;
         return wino4_launch(a, POOL, FUSE1A, s);
     }
     return wino3_launch(a, POOL, FUSE1A, s);

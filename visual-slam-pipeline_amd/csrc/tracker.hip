@@ -341,7 +341,9 @@ constexpr size_t kChainKept = kChainGood + (size_t)kCap * sizeof(vs_match);
 constexpr size_t kChainRaw = kChainKept + (size_t)kCap * sizeof(vs_match);
 constexpr size_t kChainSync = kChainRaw + (size_t)kCap * sizeof(vs_match);  // k_ransac3d's arrival counter + results
 constexpr int kChainSplit3d = 4;  // k_ransac3d workgroups per chain (its 200 hypotheses on 4 CUs)
-constexpr size_t kChainBytes = kChainSync + 256;
+constexpr size_t kChainEmSync = kChainSync + 256;  // k_emat's split-workgroup meeting area (one problem)
+constexpr int kChainSplitEm = 8;  // k_emat workgroups per chain (its first 64 iterations on the chain's 8 CUs)
+constexpr size_t kChainBytes = kChainEmSync + kEmSyncBytes;
 // chain header: pair slots, the 3D-3D seed, 0, then its MT19937 init_genrand state
 constexpr int kHdrWords = 4 + 624;
 constexpr size_t kHdrBytes = kHdrWords * sizeof(uint32_t);
@@ -773,6 +775,7 @@ struct GpuOps {
         VS_HIP(hipMemsetAsync(ctx->tlm.p, 0, 16, s));  // the work list's length (k_tlm_best re-zeroes it)
         VS_CHECK(ctx->pnp.ensure((size_t)4 * VS_PNP_MAX_ITERS * (6 * sizeof(int) + 6 * sizeof(double))));
         VS_CHECK(pnp_reserve(ctx, s));  // the PnP subset table (built once here, not in the loop)
+        VS_CHECK(emat_reserve(ctx, s));  // and findEssentialMat's
         // Loop closure (every 200 keyframes, candidates every 5th keyframe >= 200 ids back,
         // LoopCloser.cpp:44-49): the keyframe archive for kArchInit keyframes (215 MB of HBM), the
         // candidate pool and the matcher key state for kLoopPairs candidates, reserved here because
@@ -1082,7 +1085,7 @@ struct GpuOps {
                                 st, reinterpret_cast<const uint32_t*>(dh + 4), r3_split,
                                 reinterpret_cast<int*>(cbuf + kChainSync)));
         VS_CHECK(emat_pairs(ctx, 1, dh, pool_kps.as<vs_keypoint>(), kCap, kept, di + 5, di + 6, pool_depth.as<float>(), h,
-                            w, K, dd + 23, dd + 32, dd + 35, di + 7, di + 20, st));
+                            w, K, dd + 23, dd + 32, dd + 35, di + 7, di + 20, st, kChainSplitEm, cbuf + kChainEmSync));
         return P.to_host(hout, cbuf, kChainRaw, st);
     }
     static vs_trk::ChainResult parse_chain(const char* hc) {

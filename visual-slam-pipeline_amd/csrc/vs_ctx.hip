@@ -167,7 +167,8 @@ std::vector<float> winograd_weights(const float* w, int cin, int cout_pad) {
 // once, stored in the order the kernel's lanes load their MFMA B operands: per (64-column tile nt,
 // 4-channel k-step kk, 16-column group cg, domain half xh) 64 lanes x 20 floats, lane (lk, li) holding
 // U[18 xh + x][4 kk + lk][64 nt + 16 cg + li] at x = 0..17 (two floats of padding: 16-byte loads).
-std::vector<float> winograd4_weights(const float* w, int cin, int cout_pad) {
+// xg = 2: [nt][chunk][cg][half 2][lane][20] (rows 3 h .. 3 h + 2); xg = 3: [nt][chunk][cg][pair 3][lane][12]
+std::vector<float> winograd4_weights(const float* w, int cin, int cout_pad, int xg) {
     static const double G[6][3] = {{0.25, 0, 0},
                                    {-1.0 / 6, -1.0 / 6, -1.0 / 6},
                                    {-1.0 / 6, 1.0 / 6, -1.0 / 6},
@@ -175,7 +176,8 @@ std::vector<float> winograd4_weights(const float* w, int cin, int cout_pad) {
                                    {1.0 / 24, -1.0 / 12, 1.0 / 6},
                                    {0, 0, 1}};
     const int nk = cin / 4;
-    std::vector<float> u((size_t)40 * cin * cout_pad, 0.0f);  // 36 used of 40 per (ci, co)
+    const int rg = 6 / xg, bs = xg == 2 ? 20 : 12;
+    std::vector<float> u((size_t)xg * bs * cin * cout_pad, 0.0f);  // 36 used of 40 (xg 2) / 36 (xg 3) per (ci, co)
     for (int ci = 0; ci < cin; ci++)
         for (int co = 0; co < cout_pad; co++) {
             double g[3][3], t[6][3];
@@ -186,8 +188,8 @@ std::vector<float> winograd4_weights(const float* w, int cin, int cout_pad) {
             const int kk = ci / 4, lk = ci % 4, nt = co / 64, cg = (co % 64) / 16, li = co % 16;
             for (int i = 0; i < 6; i++)
                 for (int j = 0; j < 6; j++) {
-                    const int xh = i / 3, x = 6 * (i % 3) + j;
-                    const size_t o = (((((size_t)nt * nk + kk) * 4 + cg) * 2 + xh) * 64 + lk * 16 + li) * 20 + x;
+                    const int xh = i / rg, x = 6 * (i % rg) + j;
+                    const size_t o = (((((size_t)nt * nk + kk) * 4 + cg) * xg + xh) * 64 + lk * 16 + li) * bs + x;
                     u[o] = (float)(t[i][0] * G[j][0] + t[i][1] * G[j][1] + t[i][2] * G[j][2]);
                 }
         }
@@ -220,6 +222,9 @@ static int upload_layer(DevLayer& D, int cin, int cout, int cout_pad, int k, con
         const std::vector<float> u4 = winograd4_weights(w.data(), cin, cout_pad);
         VS_HIP(hipMalloc(&D.wu4, u4.size() * sizeof(float)));
         VS_HIP(hipMemcpy(D.wu4, u4.data(), u4.size() * sizeof(float), hipMemcpyHostToDevice));
+        const std::vector<float> u43 = winograd4_weights(w.data(), cin, cout_pad, 3);
+        VS_HIP(hipMalloc(&D.wu4x3, u43.size() * sizeof(float)));
+        VS_HIP(hipMemcpy(D.wu4x3, u43.data(), u43.size() * sizeof(float), hipMemcpyHostToDevice));
     }
     return VS_OK;
 }
@@ -430,12 +435,14 @@ void vs_destroy(vs_ctx* ctx) {
         if (L.b) (void)hipFree(L.b);
         if (L.wu) (void)hipFree(L.wu);
         if (L.wu4) (void)hipFree(L.wu4);
+        if (L.wu4x3) (void)hipFree(L.wu4x3);
         if (L.w1a_rows) (void)hipFree(L.w1a_rows);
     }
     if (ctx->head_a.w) (void)hipFree(ctx->head_a.w);
     if (ctx->head_a.b) (void)hipFree(ctx->head_a.b);
     if (ctx->head_a.wu) (void)hipFree(ctx->head_a.wu);
     if (ctx->head_a.wu4) (void)hipFree(ctx->head_a.wu4);
+    if (ctx->head_a.wu4x3) (void)hipFree(ctx->head_a.wu4x3);
     if (ctx->scratch_foreign) (void)hipEventDestroy(ctx->scratch_foreign);
     for (hipEvent_t e : ctx->ba_ev)
         if (e) (void)hipEventDestroy(e);
@@ -444,7 +451,7 @@ void vs_destroy(vs_ctx* ctx) {
                       &ctx->state, &ctx->flags,  &ctx->keys,   &ctx->keycnt, &ctx->h_img,  &ctx->h_kps,
                       &ctx->h_desc, &ctx->h_n,   &ctx->h_aux0, &ctx->h_aux1, &ctx->h_aux2, &ctx->h_aux3,
                       &ctx->h_aux4, &ctx->h_aux5, &ctx->match_keys, &ctx->match_cnt, &ctx->nms_list, &ctx->norms_sets, &ctx->tlm, &ctx->ba, &ctx->pnp,
-                      &ctx->pnp_tab, &ctx->tie_totals};
+                      &ctx->pnp_tab, &ctx->em_tab, &ctx->em_sync, &ctx->tie_totals};
     for (DevBuf* b : bufs) b->release();
     for (auto& st : ctx->prof)
         for (auto& pr : st.pending) {

@@ -86,6 +86,8 @@ struct DevLayer {
     // the same layers' Winograd F(4x4, 3x3) weights U = G g G^T (round 5, wino4.hip; fp64, rounded once) in
     // the order the kernel's lanes load their B operands (winograd4_weights)
     float* wu4 = nullptr;
+    // the same for k_wino4's 3-row-group variant (XG = 3, round 6: [nt][chunk][cg 4][row pair 3][lane][12])
+    float* wu4x3 = nullptr;
     // conv1a (cin 1, 3x3): per output channel its 9 taps, bias, 0, 0 ([cout][12]) — read by the fused
     // conv1 kernel as wave-uniform (scalar) loads
     float* w1a_rows = nullptr;
@@ -129,6 +131,9 @@ struct vs_ctx {
     vs::DevBuf match_keys, match_cnt, norms_sets, tlm, ba, pnp;
     vs::DevBuf pnp_tab;  // PnP RANSAC subsets of the usual budget by point count (pnp.hip)
     bool pnp_tab_ready = false;
+    vs::DevBuf em_tab;  // findEssentialMat subsets (1,000 iterations) by point count (emat.hip)
+    bool em_tab_ready = false;
+    vs::DevBuf em_sync;  // k_emat's split-workgroup meeting area for the context's own calls (zeroed)
     vs::DevBuf tie_totals;  // NMS tie accounting since the last reset: {frames, frames with a tie, window, cut, order}
 
     bool prof_on = false;
@@ -199,6 +204,7 @@ struct WinoArgs {
     const float* in;
     int in_cstride, in_coff;
     const float* wu;
+    const float* wu3;  // wino4 only: the XG = 3 weight image (nullptr: XG = 2 only)
     const float* bias;
     int cin, cout, cout_pad;
     float* out;
@@ -219,7 +225,7 @@ int wino3_launch(WinoArgs a, bool pool, bool fuse1a, hipStream_t s);
 // Winograd F(4x4, 3x3) (wino4.hip k_wino4): 16 x 16-pixel x 64-channel workgroups; bias + ReLU (+ 2 x 2 pool,
 // + fused conv1a); wa.wu = winograd4_weights images.  VS_ERR_ARG for geometry it does not cover.
 int wino4_launch(WinoArgs a, bool pool, bool fuse1a, hipStream_t s);
-std::vector<float> winograd4_weights(const float* w, int cin, int cout_pad);
+std::vector<float> winograd4_weights(const float* w, int cin, int cout_pad, int xg = 2);
 // U[xi][ci][pos(co)] from direct-layout 3x3 weights w[(3a + b)][ci][co] (cout_pad columns; pos
 // permutes each 32-column group for k_wino3's paired operand reads).  fp64, rounded once.
 std::vector<float> winograd_weights(const float* w, int cin, int cout_pad);
@@ -279,10 +285,23 @@ int fmat_pairs(vs_ctx* ctx, int P, const int* d_pairs, const vs_keypoint* d_kps,
                hipStream_t s);
 int fmat_points(vs_ctx* ctx, int P, const float* d_p1, const float* d_p2, const int* d_off, double thr, double conf,
                 int max_iters, double* d_F, uint8_t* d_mask, double* d_err, int* d_diag, hipStream_t s);
-// Essential-matrix motion + depth scale (A12): per frame pair (pipeline) or per point set
+// Essential-matrix motion + depth scale (A12): per frame pair (pipeline) or per point set.
+// The first 8 split RANSAC iterations of a problem run on split workgroups (emat.hip), which meet in
+// d_sync (kEmSyncBytes per problem, zeroed once; re-armed by the kernel): a caller whose launches may
+// overlap another's passes its own, nullptr takes the context's (split <= 0: the default — one problem
+// the whole 1,000-iteration budget, kEmSplitMax; a batch 8; the tracker's chains pass 8).
+constexpr int kEmSplitMax = 125;
+constexpr size_t kEmSyncBytes = 786432;
+constexpr int kEmTabMinN = 6;  // the subset table's first row: n = 6 (every n > 5 runs RANSAC)
 int emat_pairs(vs_ctx* ctx, int P, const int* d_pairs, const vs_keypoint* d_kps, int cap, const vs_match* d_kept,
                const int* d_nkept, const int* d_skip, const float* d_depth, int h, int w, const double K[4],
-               double* d_R, double* d_t, double* d_scale, int* d_ok, int* d_diag, hipStream_t s);
+               double* d_R, double* d_t, double* d_scale, int* d_ok, int* d_diag, hipStream_t s, int split = 0,
+               char* d_sync = nullptr);
+// Builds the context's findEssentialMat subset table now (synchronises s once); emat_* build it on first use.
+int emat_reserve(vs_ctx* ctx, hipStream_t s);
+// cv::RNG subsets (5 distinct indices, repeats redrawn) of rows problems with n = n_base + row points,
+// iters per row, into out[row][iters][5] (pnp.hip: the PnP sampler, the same RANSACPointSetRegistrator)
+int subset_table(int rows, int n_base, int iters, int* out, hipStream_t s);
 int emat_points(vs_ctx* ctx, int P, const float* d_p1, const float* d_p2, const int* d_off, const float* d_depth1,
                 const float* d_depth2, int h, int w, const double K[4], double* d_R, double* d_t, double* d_scale,
                 int* d_ok, int* d_diag, hipStream_t s);

@@ -15,11 +15,14 @@
 // network's fp32 tolerance against torch fp64 (tests/test_gpu_parity.py, stated there).
 //
 // Workgroup = 16 x 16 output pixels (4 x 4 tiles, an 18 x 18 input patch) x 64 output channels,
-// 8 waves.  Wave w owns output channels 16 (w & 3) .. + 15 of all 16 tiles for the transform
-// elements of domain rows 3 (w >> 2) .. + 2 (18 of the 36: eighteen 16 x 16 accumulators), so each
-// wave's partial output transform A^T M_rows A stays in registers and the two halves are added
-// once, through LDS, in the epilogue.  Per 4-channel k-step a wave issues 18 MFMAs; its operands
-// are one 6-float row of V and of U per domain row (3 ds_read_b64 each, conflict-free images).
+// 4 XG waves.  Wave w owns output channels 16 (w & 3) .. + 15 of all 16 tiles for the transform
+// elements of domain rows RG (w >> 2) .. + RG - 1 (RG = 6 / XG: 6 RG sixteen-by-sixteen accumulators), so
+// each wave's partial output transform A^T M_rows A stays in registers and the XG parts are added once,
+// through LDS, in the epilogue.  XG = 3 (round 6, the default): 12 waves of 12 accumulators, ~144 VGPRs,
+// 3 waves per SIMD — the kernel is bound by the latency of its staging chain (profiles/r05c ablation), so
+// the third wave per SIMD is what pays (+3.6 % headline, profiles/r06xg_headline_ab.txt); XG = 2 (round 5):
+// 8 waves of 18.  Per 4-channel k-step a wave issues 6 RG MFMAs; its operands are one 6-float row of V and
+// of U per domain row (3 ds_read_b64 each, conflict-free images).
 //
 // Per k-step k (one barrier), while the MFMAs of k run on buffers k & 1:
 //   * each lane's B operands of k + 1 (U, prearranged on the host in MFMA operand order, 20 floats
@@ -71,7 +74,6 @@ template <int SUB> struct W4Geo {
     static constexpr int Lds = Main > Epi ? Main : Epi;  // epilogue: partial halves, then the outputs
     static_assert(Lds * 4 <= 160 * 1024, "LDS");
 };
-constexpr int kW4B = 4 * 2 * 64 * 20;        // B operands per 4 channels: [cg 4][xh 2][lane 64][20 (18 used)]
 
 __device__ inline void w4_xcd_work(int ntiles, int& tile, int& nt) {
     const int nblk = gridDim.x;
@@ -110,17 +112,32 @@ __device__ inline void w4_rowA(const float m[6], float r[4]) {
                      // 4 no barrier in the k-loop, 5 no B loads, 6 half the k-steps, 7 two k-steps only
                      // (6 and 7 separate the per-workgroup fixed cost from the per-k-step cost)
 #endif
-// one lane's B operands of a 4-channel sub-step: U[18 xh + x][ch][cout] for x = 0..17 (4 x 16 B + 8 B)
-struct W4B {
+// one lane's B operands of a 4-channel sub-step: U[6 RG xh + x][ch][cout] for x < 6 RG (XG = 2: 18 = 4 x 16 B
+// + 8 B; XG = 3: 12 = 3 x 16 B)
+template <int XG> struct W4B;
+template <> struct W4B<2> {
     f32x4 q[4];
     f32x2 r;
     __device__ float operator[](int x) const { return x < 16 ? q[x >> 2][x & 3] : r[x - 16]; }
 };
+template <> struct W4B<3> {
+    f32x4 q[3];
+    __device__ float operator[](int x) const { return q[x >> 2][x & 3]; }
+};
 
-template <bool POOL, bool FUSE1A, int SUB>
-__global__ __launch_bounds__(512, 1) void k_wino4(WinoArgs wa) {
+// XG: domain-row groups per workgroup — 2: rows 0-2 | 3-5 on 8 waves (18 accumulators each, 2 waves per
+// SIMD); 3 (round 6): rows 0-1 | 2-3 | 4-5 on 12 waves (12 accumulators each, 3 waves per SIMD to hide the
+// staging chain's latency; the same A operand traffic in total)
+template <bool POOL, bool FUSE1A, int SUB, int XG>
+__global__ __launch_bounds__(256 * XG, 1) void k_wino4(WinoArgs wa) {
+    static_assert(XG == 2 || (XG == 3 && SUB == 1), "XG");
     using Geo = W4Geo<SUB>;
     constexpr int CH = Geo::CH;
+    constexpr int RG = 6 / XG;         // domain rows per wave
+    constexpr int NT = 256 * XG;       // threads
+    constexpr int NW = NT / 64;        // waves
+    constexpr int BS = XG == 2 ? 20 : 12;  // B operand floats per lane in the weight image
+    constexpr int BK = 4 * XG * 64 * BS;   // B operands per 4 channels
     const float* __restrict__ in = wa.in;
     const float* __restrict__ bias = wa.bias;
     float* __restrict__ out = wa.out;
@@ -138,14 +155,16 @@ __global__ __launch_bounds__(512, 1) void k_wino4(WinoArgs wa) {
     const int y0 = (r0 / nbx) * 16, x0 = (r0 % nbx) * 16;
     const int nk = VS_W4_ABL == 6 ? cin / CH / 2 : VS_W4_ABL == 7 ? 2 : cin / CH;  // k-steps
     // this lane's B operands: [nt][4-channel chunk][cg][xh][lane][20]
-    const float* __restrict__ wb = wa.wu + ((size_t)nt * (cin >> 2) * 8 + cg * 2 + xh) * (64 * 20) + lane * 20;
+    const float* __restrict__ wb = wa.wu + ((size_t)nt * (cin >> 2) * (4 * XG) + cg * XG + xh) * (64 * BS) + lane * BS;
 
     // ---- patch role: slot p of the 18 x 18 patch, every thread (slots >= 324 are written, never read).
-    // Waves 6, 7, 0, 1, 2, 3 hold the 324 real pixels, so the patch work lands beside the transform work
-    // on the other waves of the SIMD pairs.
-    const int p = ((wv + 2) & 7) * 64 + lane;
+    // XG = 2: waves 6, 7, 0, 1, 2, 3 hold the 324 real pixels, so the patch work lands beside the transform
+    // work on the other waves of the SIMD pairs; XG = 3: waves 6-11 (the transform is on waves 0-5).
+    constexpr int PW = XG == 2 ? 2 : 6;
+    const int pslot = (wv + PW) % NW;
+    const int p = pslot * 64 + lane;
     const bool own_px = p < kW4NP;
-    const bool dummy_wave = ((wv + 2) & 7) * 64 >= kW4NP;  // wave-uniform: no patch pixel at all
+    const bool dummy_wave = pslot * 64 >= kW4NP;  // wave-uniform: no patch pixel at all
     const int ppy = p / kW4Patch, ppx = p - (p / kW4Patch) * kW4Patch;
     const int pq = own_px ? ppy * kW4RS + ppx : kW4PadSlot + (lane & 15);  // the slot's place in the LDS patch
     const int gy = y0 - 1 + ppy, gx = x0 - 1 + ppx;
@@ -157,7 +176,7 @@ __global__ __launch_bounds__(512, 1) void k_wino4(WinoArgs wa) {
     float gnb[FUSE1A ? 9 : 1];
     if constexpr (FUSE1A) {
         const float* g = in + (size_t)b * H * W;
-        for (int i = tid; i < 400; i += 512) {
+        for (int i = tid; i < 400; i += NT) {
             const int yy = i / 20, xx = i - (i / 20) * 20;
             const int sy = y0 - 2 + yy, sx = x0 - 2 + xx;
             lds[Geo::OffG + i] = (sy >= 0 && sy < H && sx >= 0 && sx < W) ? g[(size_t)sy * W + sx] : 0.0f;
@@ -234,6 +253,7 @@ __global__ __launch_bounds__(512, 1) void k_wino4(WinoArgs wa) {
     auto transform = [&](int u, int slot, auto g_c, int c) {
         if (decltype(g_c)::value && c >= nk) return;
         if (VS_W4_ABL == 1) return;
+        if (XG == 3 && wv >= 6) return;  // the six real rows on waves 0-5
         const TrItem& T = tri[u];
         const float* xs = lds + Geo::OffX + slot * Geo::X + T.xbase;
         float e[4][6];
@@ -259,23 +279,23 @@ __global__ __launch_bounds__(512, 1) void k_wino4(WinoArgs wa) {
     // ---- B operands straight from L2 into registers, one k-step ahead (no LDS image, no barrier)
     // one W4B per 4-channel sub-step
     struct W4BS {
-        W4B s[SUB];
+        W4B<XG> s[SUB];
     };
     auto fetch_b = [&](W4BS& bq, auto g_c, int c) {
         if (decltype(g_c)::value && c >= nk) return;
         if (VS_W4_ABL == 5) return;
 #pragma unroll
         for (int u = 0; u < SUB; u++) {
-            const float* q = wb + (size_t)(SUB * c + u) * kW4B;
+            const float* q = wb + (size_t)(SUB * c + u) * BK;
 #pragma unroll
-            for (int j = 0; j < 4; j++) bq.s[u].q[j] = *reinterpret_cast<const f32x4*>(q + 4 * j);
-            bq.s[u].r = *reinterpret_cast<const f32x2*>(q + 16);
+            for (int j = 0; j < (XG == 2 ? 4 : 3); j++) bq.s[u].q[j] = *reinterpret_cast<const f32x4*>(q + 4 * j);
+            if constexpr (XG == 2) bq.s[u].r = *reinterpret_cast<const f32x2*>(q + 16);
         }
     };
 
-    f32x4 acc[18];
+    f32x4 acc[6 * RG];
 #pragma unroll
-    for (int x = 0; x < 18; x++) acc[x] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int x = 0; x < 6 * RG; x++) acc[x] = f32x4{0.f, 0.f, 0.f, 0.f};
 
     // prologue: patches 0, 1 in LDS, patch 2 and the B operands of step 0 in registers, V 0 transformed
     W4BS bA, bB;
@@ -290,8 +310,8 @@ __global__ __launch_bounds__(512, 1) void k_wino4(WinoArgs wa) {
     for (int u = 0; u < SUB; u++) transform(u, 0, GY_{}, 0);
     __syncthreads();
 
-    // A operands of sub-step s: V[3 xh + rr][4 s + lk][li][0..5]
-    const int aoff = Geo::OffV + (lk * 16 + li) * 6 + 3 * xh * (CH * 16 * 6);
+    // A operands of sub-step s: V[RG xh + rr][4 s + lk][li][0..5]
+    const int aoff = Geo::OffV + (lk * 16 + li) * 6 + RG * xh * (CH * 16 * 6);
     // k-step k on buffers P = k & 1 with B operands bc, loading the next step's into bn
     auto step = [&](auto par, auto g_c, int k, const W4BS& bc, W4BS& bn) {
         constexpr int P = decltype(par)::value;
@@ -299,14 +319,14 @@ __global__ __launch_bounds__(512, 1) void k_wino4(WinoArgs wa) {
 #pragma unroll
         for (int sb = 0; sb < SUB; sb++) {
             const float* av = lds + aoff + P * Geo::V + sb * (4 * 16 * 6);
-            f32x2 a2[3][3];
+            f32x2 a2[RG][3];
 #pragma unroll
-            for (int rr = 0; rr < 3; rr++)
+            for (int rr = 0; rr < RG; rr++)
 #pragma unroll
                 for (int h = 0; h < 3; h++)
                     a2[rr][h] = *reinterpret_cast<const f32x2*>(av + rr * (CH * 16 * 6) + 2 * h);
 #pragma unroll
-            for (int rr = 0; rr < 3; rr++) {
+            for (int rr = 0; rr < RG; rr++) {
 #pragma unroll
                 for (int j = 0; j < 6; j++) {
                     if (VS_W4_ABL == 3) {
@@ -337,14 +357,14 @@ __global__ __launch_bounds__(512, 1) void k_wino4(WinoArgs wa) {
         if (k + 1 < nk) step(S1{}, GY_{}, k + 1, bB, bA);
     }
 
-    // ---- epilogue: partial output transforms, halves added through LDS
-    // acc[6 rr + j][r]: tile 4 lk + r, channel 16 cg + li, domain (3 xh + rr, j)
+    // ---- epilogue: partial output transforms, the groups' parts added through LDS
+    // acc[6 rr + j][r]: tile 4 lk + r, channel 16 cg + li, domain (RG xh + rr, j)
     float y[4][16];  // [r][4 p + q]
 #pragma unroll
     for (int r = 0; r < 4; r++) {
-        float R[3][4];
+        float R[RG][4];
 #pragma unroll
-        for (int rr = 0; rr < 3; rr++) {
+        for (int rr = 0; rr < RG; rr++) {
             float m[6];
 #pragma unroll
             for (int j = 0; j < 6; j++) m[j] = acc[6 * rr + j][r];
@@ -352,37 +372,60 @@ __global__ __launch_bounds__(512, 1) void k_wino4(WinoArgs wa) {
         }
 #pragma unroll
         for (int q = 0; q < 4; q++) {
-            if (xh == 0) {  // rows 0, 1, 2: A^T columns (1,0,0,0), (1,1,1,1), (1,-1,1,-1)
-                const float s = R[1][q] + R[2][q], d = R[1][q] - R[2][q];
-                y[r][q] = R[0][q] + s;
-                y[r][4 + q] = d;
-                y[r][8 + q] = s;
-                y[r][12 + q] = d;
-            } else {        // rows 3, 4, 5: (1,2,4,8), (1,-2,4,-8), (0,0,0,1)
-                const float s = R[0][q] + R[1][q], d = R[0][q] - R[1][q];
-                y[r][q] = s;
-                y[r][4 + q] = 2.0f * d;
-                y[r][8 + q] = 4.0f * s;
-                y[r][12 + q] = __builtin_fmaf(8.0f, d, R[2][q]);
+            if constexpr (XG == 2) {
+                if (xh == 0) {  // rows 0, 1, 2: A^T columns (1,0,0,0), (1,1,1,1), (1,-1,1,-1)
+                    const float s = R[1][q] + R[2][q], d = R[1][q] - R[2][q];
+                    y[r][q] = R[0][q] + s;
+                    y[r][4 + q] = d;
+                    y[r][8 + q] = s;
+                    y[r][12 + q] = d;
+                } else {        // rows 3, 4, 5: (1,2,4,8), (1,-2,4,-8), (0,0,0,1)
+                    const float s = R[0][q] + R[1][q], d = R[0][q] - R[1][q];
+                    y[r][q] = s;
+                    y[r][4 + q] = 2.0f * d;
+                    y[r][8 + q] = 4.0f * s;
+                    y[r][12 + q] = __builtin_fmaf(8.0f, d, R[2][q]);
+                }
+            } else {
+                if (xh == 0) {         // rows 0, 1: (1,0,0,0), (1,1,1,1)
+                    y[r][q] = R[0][q] + R[1][q];
+                    y[r][4 + q] = R[1][q];
+                    y[r][8 + q] = R[1][q];
+                    y[r][12 + q] = R[1][q];
+                } else if (xh == 1) {  // rows 2, 3: (1,-1,1,-1), (1,2,4,8)
+                    y[r][q] = R[0][q] + R[1][q];
+                    y[r][4 + q] = __builtin_fmaf(2.0f, R[1][q], -R[0][q]);
+                    y[r][8 + q] = __builtin_fmaf(4.0f, R[1][q], R[0][q]);
+                    y[r][12 + q] = __builtin_fmaf(8.0f, R[1][q], -R[0][q]);
+                } else {               // rows 4, 5: (1,-2,4,-8), (0,0,0,1)
+                    y[r][q] = R[0][q];
+                    y[r][4 + q] = -2.0f * R[0][q];
+                    y[r][8 + q] = 4.0f * R[0][q];
+                    y[r][12 + q] = __builtin_fmaf(-8.0f, R[0][q], R[1][q]);
+                }
             }
         }
     }
-    // [cg][tile][16 px][16 ch] with tiles YS floats apart: the xh = 1 halves (4 YS = 16 mod 32, so lanes
-    // lk = 0 and 1 of a ds_read_b32 group land on different banks)
+    // [cg][tile][16 px][16 ch] with tiles YS floats apart: a group's parts (4 YS = 16 mod 32, so lanes
+    // lk = 0 and 1 of a ds_read_b32 group land on different banks), added by group 0, one group at a time
     float* yp = lds;
-    float* so = lds;  // then [pixel][64 ch]: the outputs (after every half has been read)
-    if (xh == 1) {
+    float* so = lds;  // then [pixel][64 ch]: the outputs (after every part has been read)
 #pragma unroll
-        for (int r = 0; r < 4; r++)
+    for (int gx = 1; gx < XG; gx++) {
+        if (xh == gx) {
 #pragma unroll
-            for (int e = 0; e < 16; e++) yp[(cg * 16 + 4 * lk + r) * Geo::YS + e * 16 + li] = y[r][e];
-    }
-    __syncthreads();
-    if (xh == 0) {
+            for (int r = 0; r < 4; r++)
 #pragma unroll
-        for (int r = 0; r < 4; r++)
+                for (int e = 0; e < 16; e++) yp[(cg * 16 + 4 * lk + r) * Geo::YS + e * 16 + li] = y[r][e];
+        }
+        __syncthreads();
+        if (xh == 0) {
 #pragma unroll
-            for (int e = 0; e < 16; e++) y[r][e] += yp[(cg * 16 + 4 * lk + r) * Geo::YS + e * 16 + li];
+            for (int r = 0; r < 4; r++)
+#pragma unroll
+                for (int e = 0; e < 16; e++) y[r][e] += yp[(cg * 16 + 4 * lk + r) * Geo::YS + e * 16 + li];
+        }
+        if (gx + 1 < XG) __syncthreads();
     }
     __syncthreads();
     if (xh == 0) {
@@ -412,10 +455,10 @@ __global__ __launch_bounds__(512, 1) void k_wino4(WinoArgs wa) {
         }
     }
     __syncthreads();
-    constexpr int NV = POOL ? 2 : 8;  // float4 per thread: 64 (POOL) or 256 pixels x 16
+    constexpr int NE = POOL ? 64 * 16 : 256 * 16;  // float4s: 64 (POOL) or 256 pixels x 16
 #pragma unroll
-    for (int u = 0; u < NV; u++) {
-        const int e = tid + 512 * u, pix = e >> 4, q = e & 15;
+    for (int e = tid; e < NE; e += NT) {
+        const int pix = e >> 4, q = e & 15;
         const int n = nt * 64 + 4 * q;
         if (n >= cout) continue;
         const f32x4 v = *reinterpret_cast<const f32x4*>(&so[pix * 64 + 4 * q]);
@@ -447,25 +490,32 @@ int wino4_launch(WinoArgs a, bool pool, bool fuse1a, hipStream_t s) {
         const char* e = std::getenv("VS_WINO4_SUB");
         return e && e[0] == '2' ? 2 : 1;
     }();
+    // VS_WINO4_XG=2: the 8-wave variant (domain halves) instead of the 12-wave one (row pairs)
+    static const int xg_env = [] {
+        const char* e = std::getenv("VS_WINO4_XG");
+        return e && e[0] == '2' ? 2 : 3;
+    }();
+    const int xg = (sub == 1 && a.wu3) ? xg_env : 2;
+#define VS_W4_LAUNCH(S_, X_)                                                                              \
+    do {                                                                                                \
+        if (pool && fuse1a)                                                                             \
+            hipLaunchKernelGGL((k_wino4<true, true, S_, X_>), grid, dim3(256 * X_), 0, s, a);           \
+        else if (pool)                                                                                  \
+            hipLaunchKernelGGL((k_wino4<true, false, S_, X_>), grid, dim3(256 * X_), 0, s, a);          \
+        else if (fuse1a)                                                                                \
+            hipLaunchKernelGGL((k_wino4<false, true, S_, X_>), grid, dim3(256 * X_), 0, s, a);          \
+        else                                                                                            \
+            hipLaunchKernelGGL((k_wino4<false, false, S_, X_>), grid, dim3(256 * X_), 0, s, a);         \
+    } while (0)
     if (sub == 2 && a.cin % 8 == 0) {
-        if (pool && fuse1a)
-            hipLaunchKernelGGL((k_wino4<true, true, 2>), grid, dim3(512), 0, s, a);
-        else if (pool)
-            hipLaunchKernelGGL((k_wino4<true, false, 2>), grid, dim3(512), 0, s, a);
-        else if (fuse1a)
-            hipLaunchKernelGGL((k_wino4<false, true, 2>), grid, dim3(512), 0, s, a);
-        else
-            hipLaunchKernelGGL((k_wino4<false, false, 2>), grid, dim3(512), 0, s, a);
+        VS_W4_LAUNCH(2, 2);
+    } else if (xg == 3) {
+        a.wu = a.wu3;
+        VS_W4_LAUNCH(1, 3);
     } else {
-        if (pool && fuse1a)
-            hipLaunchKernelGGL((k_wino4<true, true, 1>), grid, dim3(512), 0, s, a);
-        else if (pool)
-            hipLaunchKernelGGL((k_wino4<true, false, 1>), grid, dim3(512), 0, s, a);
-        else if (fuse1a)
-            hipLaunchKernelGGL((k_wino4<false, true, 1>), grid, dim3(512), 0, s, a);
-        else
-            hipLaunchKernelGGL((k_wino4<false, false, 1>), grid, dim3(512), 0, s, a);
+        VS_W4_LAUNCH(1, 2);
     }
+#undef VS_W4_LAUNCH
     VS_HIP(hipGetLastError());
     return VS_OK;
 }
