@@ -94,3 +94,29 @@ def test_estimate_motion_small_and_split_edges(vsctx, oracle, n, seed):
     assert dg[1] == fdiag[0] and dg[2] == fdiag[1]
     if oko:
         assert np.array_equal(Rg, Ro) and np.array_equal(tg, to)
+
+
+@pytest.mark.parametrize("split", [1, 2, 8])
+def test_estimate_motion_small_split_continuation(vsctx, oracle, split):
+    """The workgroup split forced small (1, 2, 8 workgroups = the first 8 / 16 / 64 iterations in parallel), so
+    problems whose budget runs past the split finish in the last workgroup's continuation rounds (n = 400 at 50 %
+    outliers runs 392 iterations): the same outcome as the oracle, iterations and winning iteration included."""
+    import ctypes
+
+    import vslam_abi
+    lib = vslam_abi.load_library()
+    lib.vs_debug_emat_split.restype = ctypes.c_int
+    lib.vs_debug_emat_split.argtypes = [ctypes.c_int]
+    assert lib.vs_debug_emat_split(split) == 0
+    try:
+        for n, seed, noise, out in [(400, 4, 0.7, 0.5), (200, 1, 0.5, 0.4), (80, 0, 0.3, 0.2), (6, 21, 0.4, 0.0)]:
+            p1, p2, R, t, X, outl = two_view(n, seed, noise=noise, outlier_frac=out)
+            d1, d2 = _depth_maps(X, R, t, p1, p2)
+            okg, Rg, tg, scg, dg = vsctx.estimate_motion(p1, p2, d1, d2)
+            oko, Ro, to, sco, fdiag, inl, good = _oracle_motion(oracle, p1, p2, d1, d2)
+            assert okg == oko, (split, n)
+            assert dg[1] == fdiag[0] and dg[2] == fdiag[1], (split, n, dg[:3], fdiag)
+            if oko:
+                assert np.array_equal(Rg, Ro) and np.array_equal(tg, to) and scg == sco, (split, n)
+    finally:
+        lib.vs_debug_emat_split(0)

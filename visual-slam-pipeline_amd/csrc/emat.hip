@@ -717,7 +717,9 @@ int emat_reserve(vs_ctx* ctx, hipStream_t s) {
 // the whole budget, kEmSplitMax workgroups; a batch of problems beside other streams (config[4]: the 32 pairs
 // of a step beside the network) 8 — the solves' CU time, not their latency, is what such a step pays
 // (profiles/r06em3_mono_split_ab.txt).  VS_EMAT_SPLIT=1..125 overrides both.
+static int g_em_split_test = 0;  // vs_debug_emat_split (tests): forces every launch's split
 static int em_launch_setup(vs_ctx* ctx, int P, int split, char** sync, hipStream_t s) {
+    if (g_em_split_test > 0) split = g_em_split_test;
     static const int env_split = [] {
         const char* e = std::getenv("VS_EMAT_SPLIT");
         const int v = e ? std::atoi(e) : 0;
@@ -726,7 +728,7 @@ static int em_launch_setup(vs_ctx* ctx, int P, int split, char** sync, hipStream
     if (split <= 0) split = env_split ? env_split : P == 1 ? kEmSplitMax : 8;
     VS_ARG(split <= kEmSplitMax, "emat: split above kEmSplitMax");
     VS_CHECK(emat_reserve(ctx, s));
-    if (split > 1 && !*sync) {
+    if (!*sync) {  // round 0 writes its models and counts there at every split, 1 included
         const size_t need = (size_t)P * kEmSyncBytes;
         if (ctx->em_sync.bytes < need) {
             VS_CHECK(ctx->em_sync.ensure(need));
@@ -742,6 +744,7 @@ int emat_pairs(vs_ctx* ctx, int P, const int* d_pairs, const vs_keypoint* d_kps,
                double* d_R, double* d_t, double* d_scale, int* d_ok, int* d_diag, hipStream_t s, int split,
                char* d_sync) {
     if (P <= 0) return VS_OK;
+    VS_ARG(!d_sync || P == 1, "emat_pairs: a caller's meeting area holds one problem");
     VS_ARG(cap <= kEmMaxPts, "emat_pairs: cap above VS_EM_MAX_POINTS");
     const int G = em_launch_setup(ctx, P, split, &d_sync, s);
     if (G < 0) return G;
@@ -792,6 +795,14 @@ __global__ __launch_bounds__(64) void k_debug_five_point(const double* __restric
 // clocks (optional, [count][8]): wall_clock64 stamps after each stage of five_point_wave
 extern "C" int vs_debug_five_point_ck(const double* q1, const double* q2, int count, double* E_out, int* nmod,
                                       long long* clocks);
+// test hook: every later k_emat launch of the process uses `split` workgroups per problem (1..125; 0 restores
+// the defaults), so the continuation rounds behind a small split are checked against the oracle
+extern "C" int vs_debug_emat_split(int split) {
+    if (split < 0 || split > vs::kEmSplitMax) return -1;
+    vs::g_em_split_test = split;
+    return 0;
+}
+
 extern "C" int vs_debug_five_point(const double* q1, const double* q2, int count, double* E_out, int* nmod) {
     return vs_debug_five_point_ck(q1, q2, count, E_out, nmod, nullptr);
 }
