@@ -145,7 +145,12 @@ __global__ __launch_bounds__(256 * XG, 1) void k_wino4(WinoArgs wa) {
     const int in_cstride = wa.in_cstride, in_coff = wa.in_coff, cin = wa.cin, cout = wa.cout;
     const int out_cstride = wa.out_cstride, out_coff = wa.out_coff, H = wa.H, W = wa.W, nbx = wa.nbx, nby = wa.nby;
     const int ntn = wa.cout_pad >> 6;
-    __shared__ __attribute__((aligned(16))) float lds[Geo::Lds];
+    // XG = 3: the epilogue holds both other groups' partial transforms at once (one pass; 133 KB, within
+    // the CU's 160 KB: a workgroup fills its CU's VGPRs anyway)
+    constexpr int kEpiParts = XG == 3 ? 2 : 1;
+    constexpr int kLds = Geo::Lds > kEpiParts * 64 * Geo::YS ? Geo::Lds : kEpiParts * 64 * Geo::YS;
+    static_assert(kLds * 4 <= 160 * 1024, "LDS");
+    __shared__ __attribute__((aligned(16))) float lds[kLds];
 
     const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63, li = lane & 15, lk = lane >> 4;
     const int cg = wv & 3, xh = wv >> 2;
@@ -407,25 +412,26 @@ __global__ __launch_bounds__(256 * XG, 1) void k_wino4(WinoArgs wa) {
         }
     }
     // [cg][tile][16 px][16 ch] with tiles YS floats apart: a group's parts (4 YS = 16 mod 32, so lanes
-    // lk = 0 and 1 of a ds_read_b32 group land on different banks), added by group 0, one group at a time
+    // lk = 0 and 1 of a ds_read_b32 group land on different banks), all written at once, added by group 0
     float* yp = lds;
     float* so = lds;  // then [pixel][64 ch]: the outputs (after every part has been read)
+    if (xh > 0) {  // group xh's part into region xh - 1
+        float* yq = yp + (xh - 1) * (64 * Geo::YS);
 #pragma unroll
-    for (int gx = 1; gx < XG; gx++) {
-        if (xh == gx) {
+        for (int r = 0; r < 4; r++)
+#pragma unroll
+            for (int e = 0; e < 16; e++) yq[(cg * 16 + 4 * lk + r) * Geo::YS + e * 16 + li] = y[r][e];
+    }
+    __syncthreads();
+    if (xh == 0) {  // group 0 adds the parts in group order
+#pragma unroll
+        for (int gx = 1; gx < XG; gx++) {
+            const float* yq = yp + (gx - 1) * (64 * Geo::YS);
 #pragma unroll
             for (int r = 0; r < 4; r++)
 #pragma unroll
-                for (int e = 0; e < 16; e++) yp[(cg * 16 + 4 * lk + r) * Geo::YS + e * 16 + li] = y[r][e];
+                for (int e = 0; e < 16; e++) y[r][e] += yq[(cg * 16 + 4 * lk + r) * Geo::YS + e * 16 + li];
         }
-        __syncthreads();
-        if (xh == 0) {
-#pragma unroll
-            for (int r = 0; r < 4; r++)
-#pragma unroll
-                for (int e = 0; e < 16; e++) y[r][e] += yp[(cg * 16 + 4 * lk + r) * Geo::YS + e * 16 + li];
-        }
-        if (gx + 1 < XG) __syncthreads();
     }
     __syncthreads();
     if (xh == 0) {
