@@ -107,3 +107,24 @@ def test_fmat_verify_pairs_dev_matches_oracle(vsctx, oracle):
             assert np.allclose(err[p], err_o, rtol=1e-12, atol=0)
         else:
             assert (err[p] == 0).all()
+
+
+@pytest.mark.parametrize("split", [1, 3, 8])
+def test_find_fundamental_split_matches_oracle(vsctx, oracle, split):
+    """Round 6: the first 64-hypothesis chunk scored by `split` workgroups at once (full counts, the last
+    workgroup to arrive replays the chunk and continues alone; 1 = the sequential rounds): the registrator's
+    outcome equals the oracle's at every split, one-chunk and multi-chunk budgets included."""
+    import ctypes
+
+    import vslam_abi
+    lib = vslam_abi.load_library()
+    lib.vs_debug_fmat_split.restype = ctypes.c_int
+    lib.vs_debug_fmat_split.argtypes = [ctypes.c_int]
+    assert lib.vs_debug_fmat_split(split) == 0
+    try:
+        for n, seed, noise, out in [(60, 0, 0.0, 0.0), (150, 1, 0.5, 0.3), (400, 2, 1.0, 0.5), (120, 5, 0.5, 0.6),
+                                    (15, 4, 0.3, 0.0), (300, 9, 0.7, 0.1)]:
+            p1, p2, F, outl = two_view(n, seed, noise, out)
+            _cmp_find(vsctx.find_fundamental(p1, p2), oracle.find_fundamental(p1, p2), n, p1, p2, oracle)
+    finally:
+        lib.vs_debug_fmat_split(0)

@@ -26,7 +26,7 @@ def main():
     P, n = 32, 300
     dev = lambda a: torch.from_numpy(np.ascontiguousarray(a).view(np.uint8)).cuda()  # noqa: E731
     names = ["-", "solve7", "score", "replay", "final", "rng+mod", "reject", "collinear"]
-    for out in (0.1, 0.3):
+    for out in [float(x) for x in os.environ.get("FM_OUT", "0.1,0.3").split(",")]:
         probs = [two_view(n, 1000 + i, 0.7, out)[:2] for i in range(P)]
         cap, pairs, kp_tab, goods, ngood = _pairs_inputs(va, probs)
         bufs = [dev(pairs), dev(kp_tab), dev(goods), dev(ngood)]

@@ -25,6 +25,8 @@
 // -ffp-contract=off).
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include "block_reduce.h"
 #include "fmat_solvers.h"
 #include "vs_internal.h"
@@ -39,6 +41,18 @@ constexpr int kThreads = 512;  // 8 wave64s, two per SIMD: the 7-point solver ne
 constexpr int kWaves = kThreads / 64;
 constexpr int kRawCap = 7 * kMaxChunk + 128;
 constexpr int kLevels = 8;  // pointer-doubling levels: 2^8 >= kMaxChunk attempts
+
+// Round 6: the first chunk (64 hypotheses) is scored by G = kFmSplit workgroups at once — workgroup g
+// scores hypotheses 8 g + w, 8 g + w + 8 G, ... on wave w (every model's full count) after drawing and solving
+// the whole chunk like the others (the same subsets and models: the computation is deterministic) —
+// and the pair's last workgroup to arrive replays the chunk in iteration order and continues alone.
+// The counts meet in FmSync (kFmSyncBytes per pair, zeroed once, the counter re-armed by the kernel).
+struct FmSync {
+    int arrived;
+    int pad[15];
+    int count[kFmFirstChunk * 3];
+};
+static_assert(sizeof(FmSync) <= kFmSyncBytes, "FmSync");
 
 // Mont(A^k), k < kRawCap: the generator stepped k times from the Montgomery one (pnp_solvers.h)
 struct MwcPow {
@@ -230,6 +244,7 @@ __device__ void draw_subsets(FmShared& S, int n, int base, int want, int attempt
 // Problem source: FROM_MATCHES = pairs of frames + keypoints + good matches (pipeline), else
 // point arrays with offsets (ABI single-problem path).
 // diag[p][8] = {method, iterations run, winning iteration, inliers, F ok, n, kept, chunks}
+// Grid: G x P workgroups (G = split; blockIdx = g P + p).  sync: FmSync per pair (G > 1).
 template <bool FROM_MATCHES>
 __global__ __launch_bounds__(kThreads) void k_fmat(const int* __restrict__ pairs, const vs_keypoint* __restrict__ kps,
                                               int cap, const vs_match* __restrict__ good,
@@ -238,10 +253,12 @@ __global__ __launch_bounds__(kThreads) void k_fmat(const int* __restrict__ pairs
                                               double thr, double conf, int max_iters, double* __restrict__ Fout,
                                               uint8_t* __restrict__ mask_out, vs_match* __restrict__ kept,
                                               int* __restrict__ nkept, double* __restrict__ err,
-                                              int* __restrict__ diag) {
+                                              int* __restrict__ diag, int G, char* __restrict__ sync) {
     __shared__ FmShared S;
     __shared__ double red4[kWaves * 4];
-    const int pb = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    __shared__ int s_last;
+    const int P = gridDim.x / G, gw = blockIdx.x / P, pb = blockIdx.x - gw * P;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     int n;
     const vs_match* gm = nullptr;
     if (FROM_MATCHES) {
@@ -266,6 +283,8 @@ __global__ __launch_bounds__(kThreads) void k_fmat(const int* __restrict__ pairs
     }
     int* dg = diag + 8 * pb;
     const int method = n < 7 ? 0 : n == 7 ? 1 : n >= 15 ? 2 : 3;
+    const bool split = G > 1 && method == 2;
+    if (gw > 0 && !split) return;  // one workgroup per pair unless its RANSAC is split
     const float thr2 = (float)(thr * thr);
     if (tid == 0) {
         S.rng = (uint64_t)-1;
@@ -325,7 +344,54 @@ __global__ __launch_bounds__(kThreads) void k_fmat(const int* __restrict__ pairs
         }
         __syncthreads();
         FM_T(1);
-        if (method == 2) {
+        if (method == 2 && split && S.nchunk == 0) {
+            // the first chunk split over the pair's workgroups: every model's full count (a count is
+            // only ever compared with the running best, so the early exit changes no decision)
+            FmSync* sy = reinterpret_cast<FmSync*>(sync + (size_t)pb * kFmSyncBytes);
+            for (int h = kWaves * gw + wv; h < chunk; h += kWaves * G) {  // the whole chunk at any G
+                for (int k = 0; k < S.nmod[h]; k++) {
+                    const int m = 3 * h + k;
+                    double F[9];
+                    for (int q = 0; q < 9; q++) F[q] = S.Fm[m * 9 + q];
+                    int cnt = 0;
+                    for (int i0 = 0; i0 < n; i0 += 64) {
+                        const int i = i0 + lane;
+                        const bool in = i < n && fm_inlier(F, S.p1[2 * i], S.p1[2 * i + 1], S.p2[2 * i],
+                                                           S.p2[2 * i + 1], thr2);
+                        cnt += __popcll(__ballot(in));
+                    }
+                    if (lane == 0) sy->count[m] = cnt;
+                }
+            }
+            __threadfence();
+            __syncthreads();
+            if (tid == 0) {
+                const int old = __hip_atomic_fetch_add(&sy->arrived, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+                s_last = old == G - 1;
+                if (s_last) __hip_atomic_store(&sy->arrived, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            __syncthreads();
+            if (!s_last) return;
+            __threadfence();
+            for (int m = tid; m < 3 * chunk; m += kThreads) S.score[m] = (float)sy->count[m];
+            __syncthreads();
+            if (tid == 0) {  // the chunk in iteration order, stopping at the budget
+                int it = S.iter;
+                for (int hh = 0; hh < chunk && it < S.niters; hh++, it++)
+                    for (int k = 0; k < S.nmod[hh]; k++) {
+                        const int m = 3 * hh + k;
+                        const int cnt = (int)S.score[m];
+                        if (cnt > (S.best > 6 ? S.best : 6)) {
+                            S.best = cnt;
+                            S.niters = vs_pnp::ransac_update_num_iters(conf, (double)(n - cnt) / n, 7, S.niters);
+                            S.best_iter = it;
+                            for (int q = 0; q < 9; q++) S.F[q] = S.Fm[m * 9 + q];
+                        }
+                    }
+                S.iter = it;
+            }
+            __syncthreads();
+        } else if (method == 2) {
             // Rounds of kWaves hypotheses: wave w scores hypothesis r0 + w (its lanes sweep the
             // points), then lane 0 replays the round in iteration order.  A model whose count can
             // no longer exceed max(best, 6) at the round's start stops early (it cannot be taken:
@@ -484,14 +550,52 @@ __global__ __launch_bounds__(kThreads) void k_fmat(const int* __restrict__ pairs
     }
 }
 
+static int g_fm_split_test = -1;  // vs_debug_fmat_split (tests): forces every launch's split
+// the pipeline's default: 1 unless VS_FMAT_SPLIT says otherwise
+static int env_or_one() {
+    static const int v = [] {
+        const char* e = std::getenv("VS_FMAT_SPLIT");
+        const int x = e ? std::atoi(e) : 0;
+        return x >= 1 && x <= kFmSplit ? x : 1;
+    }();
+    return v;
+}
+// the split and its meeting area (the context's, zeroed, for callers without one).  Default: the ABI's point-set
+// calls (latency-bound, alone on their CUs) kFmSplit; the pipeline's frame pairs 1 — beside the network on a
+// shared CU set, eight workgroups waiting for free CUs cost more than the scoring rounds they save
+// (profiles/r06fm_fmat_split_ab.txt).  VS_FMAT_SPLIT=1..8 overrides both.
+static int fm_launch_setup(vs_ctx* ctx, int P, int split, char** sync, hipStream_t s) {
+    static const int env_split = [] {
+        const char* e = std::getenv("VS_FMAT_SPLIT");
+        const int v = e ? std::atoi(e) : 0;
+        return v >= 1 && v <= kFmSplit ? v : 0;
+    }();
+    if (split <= 0) split = env_split ? env_split : kFmSplit;
+    if (g_fm_split_test > 0) split = g_fm_split_test;
+    split = split < 1 ? 1 : split;
+    VS_ARG(split <= kFmSplit, "fmat: split above kFmSplit");
+    if (split > 1 && !*sync) {
+        const size_t need = (size_t)P * kFmSyncBytes;
+        if (ctx->fm_sync.bytes < need) {
+            VS_CHECK(ctx->fm_sync.ensure(need));
+            VS_HIP(hipMemsetAsync(ctx->fm_sync.p, 0, ctx->fm_sync.bytes, s));
+        }
+        *sync = ctx->fm_sync.as<char>();
+    }
+    return split;
+}
+
 int fmat_pairs(vs_ctx* ctx, int P, const int* d_pairs, const vs_keypoint* d_kps, int cap, const vs_match* d_good,
                const int* d_ngood, double* d_F, vs_match* d_kept, int* d_nkept, double* d_err, int* d_diag,
-               hipStream_t s) {
+               hipStream_t s, int split, char* d_sync) {
     if (P <= 0) return VS_OK;
     VS_ARG(cap <= kFmMaxPts, "fmat_pairs: cap above VS_FM_MAX_POINTS");
+    VS_ARG(!d_sync || P == 1, "fmat_pairs: a caller's meeting area holds one pair");
+    const int G = fm_launch_setup(ctx, P, split > 0 ? split : env_or_one(), &d_sync, s);
+    if (G < 0) return G;
     ProfScope ps(ctx, "fmat_ransac", s);
-    hipLaunchKernelGGL(k_fmat<true>, dim3(P), dim3(kThreads), 0, s, d_pairs, d_kps, cap, d_good, d_ngood, nullptr, nullptr,
-                       nullptr, 3.0, 0.999, 1000, d_F, nullptr, d_kept, d_nkept, d_err, d_diag);
+    hipLaunchKernelGGL(k_fmat<true>, dim3(P * G), dim3(kThreads), 0, s, d_pairs, d_kps, cap, d_good, d_ngood, nullptr,
+                       nullptr, nullptr, 3.0, 0.999, 1000, d_F, nullptr, d_kept, d_nkept, d_err, d_diag, G, d_sync);
     VS_HIP(hipGetLastError());
     return VS_OK;
 }
@@ -499,14 +603,24 @@ int fmat_pairs(vs_ctx* ctx, int P, const int* d_pairs, const vs_keypoint* d_kps,
 int fmat_points(vs_ctx* ctx, int P, const float* d_p1, const float* d_p2, const int* d_off, double thr, double conf,
                 int max_iters, double* d_F, uint8_t* d_mask, double* d_err, int* d_diag, hipStream_t s) {
     if (P <= 0) return VS_OK;
+    char* d_sync = nullptr;
+    const int G = fm_launch_setup(ctx, P, 0, &d_sync, s);
+    if (G < 0) return G;
     ProfScope ps(ctx, "fmat_ransac", s);
-    hipLaunchKernelGGL(k_fmat<false>, dim3(P), dim3(kThreads), 0, s, nullptr, nullptr, 0, nullptr, nullptr, d_p1, d_p2,
-                       d_off, thr, conf, max_iters, d_F, d_mask, nullptr, nullptr, d_err, d_diag);
+    hipLaunchKernelGGL(k_fmat<false>, dim3(P * G), dim3(kThreads), 0, s, nullptr, nullptr, 0, nullptr, nullptr, d_p1,
+                       d_p2, d_off, thr, conf, max_iters, d_F, d_mask, nullptr, nullptr, d_err, d_diag, G, d_sync);
     VS_HIP(hipGetLastError());
     return VS_OK;
 }
 
 }  // namespace vs
+
+// test hook: every later k_fmat launch of the process uses `split` workgroups per pair (1..8; 0 restores the defaults)
+extern "C" int vs_debug_fmat_split(int split) {
+    if (split < 0 || split > vs::kFmSplit) return -1;
+    vs::g_fm_split_test = split > 0 ? split : -1;
+    return 0;
+}
 
 #ifdef VS_FM_PROFILE
 extern "C" int vs_debug_fm_cycles(unsigned long long* out, int reset) {

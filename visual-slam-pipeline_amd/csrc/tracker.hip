@@ -343,7 +343,8 @@ constexpr size_t kChainSync = kChainRaw + (size_t)kCap * sizeof(vs_match);  // k
 constexpr int kChainSplit3d = 4;  // k_ransac3d workgroups per chain (its 200 hypotheses on 4 CUs)
 constexpr size_t kChainEmSync = kChainSync + 256;  // k_emat's split-workgroup meeting area (one problem)
 constexpr int kChainSplitEm = 8;  // k_emat workgroups per chain (its first 64 iterations on the chain's 8 CUs)
-constexpr size_t kChainBytes = kChainEmSync + kEmSyncBytes;
+constexpr size_t kChainFmSync = kChainEmSync + kEmSyncBytes;  // k_fmat's (one pair)
+constexpr size_t kChainBytes = kChainFmSync + kFmSyncBytes;
 // chain header: pair slots, the 3D-3D seed, 0, then its MT19937 init_genrand state
 constexpr int kHdrWords = 4 + 624;
 constexpr size_t kHdrBytes = kHdrWords * sizeof(uint32_t);
@@ -1079,7 +1080,7 @@ struct GpuOps {
                              reinterpret_cast<vs_match*>(cbuf + kChainRaw), di + 3, good, di + 4, st,
                              pool_norms.as<float>(), keys, cnt));
         VS_CHECK(fmat_pairs(ctx, 1, dh, pool_kps.as<vs_keypoint>(), kCap, good, di + 4, dd, kept, di + 5, dd + 9, di + 8,
-                            st));
+                            st, 0, cbuf + kChainFmSync));
         VS_CHECK(ransac3d_pairs(ctx, 1, dh, pool_kps.as<vs_keypoint>(), kCap, kept, di + 5, pool_depth.as<float>(), h, w,
                                 K, reinterpret_cast<const uint32_t*>(dh + 2), 200, 0.05, dd + 11, dd + 20, di + 6, di + 16,
                                 st, reinterpret_cast<const uint32_t*>(dh + 4), r3_split,

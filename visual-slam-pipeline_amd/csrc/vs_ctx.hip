@@ -451,7 +451,7 @@ void vs_destroy(vs_ctx* ctx) {
                       &ctx->state, &ctx->flags,  &ctx->keys,   &ctx->keycnt, &ctx->h_img,  &ctx->h_kps,
                       &ctx->h_desc, &ctx->h_n,   &ctx->h_aux0, &ctx->h_aux1, &ctx->h_aux2, &ctx->h_aux3,
                       &ctx->h_aux4, &ctx->h_aux5, &ctx->match_keys, &ctx->match_cnt, &ctx->nms_list, &ctx->norms_sets, &ctx->tlm, &ctx->ba, &ctx->pnp,
-                      &ctx->pnp_tab, &ctx->em_tab, &ctx->em_sync, &ctx->tie_totals};
+                      &ctx->pnp_tab, &ctx->em_tab, &ctx->em_sync, &ctx->fm_sync, &ctx->tie_totals};
     for (DevBuf* b : bufs) b->release();
     for (auto& st : ctx->prof)
         for (auto& pr : st.pending) {

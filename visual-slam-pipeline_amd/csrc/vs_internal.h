@@ -134,6 +134,7 @@ struct vs_ctx {
     vs::DevBuf em_tab;  // findEssentialMat subsets (1,000 iterations) by point count (emat.hip)
     bool em_tab_ready = false;
     vs::DevBuf em_sync;  // k_emat's split-workgroup meeting area for the context's own calls (zeroed)
+    vs::DevBuf fm_sync;  // k_fmat's (zeroed)
     vs::DevBuf tie_totals;  // NMS tie accounting since the last reset: {frames, frames with a tie, window, cut, order}
 
     bool prof_on = false;
@@ -280,9 +281,14 @@ int solve_pnp(vs_ctx* ctx, int nprob, const float* d_obj, const float* d_img, co
 // Builds the context's PnP subset table now (synchronises s once); solve_pnp builds it on first use.
 int pnp_reserve(vs_ctx* ctx, hipStream_t s);
 // F-matrix verification: per frame pair (pipeline) or per point set (ABI single problem)
+// F-RANSAC's first chunk (64 hypotheses) can be scored by split workgroups at once (fmat.hip; default 1 for
+// frame pairs, kFmSplit for the ABI's point sets), meeting in d_sync (kFmSyncBytes per pair, zeroed once): a
+// caller whose launches may overlap another's passes its own (P == 1), nullptr takes the context's.
+constexpr int kFmSplit = 8, kFmFirstChunk = 64;
+constexpr size_t kFmSyncBytes = 1024;
 int fmat_pairs(vs_ctx* ctx, int P, const int* d_pairs, const vs_keypoint* d_kps, int cap, const vs_match* d_good,
                const int* d_ngood, double* d_F, vs_match* d_kept, int* d_nkept, double* d_err, int* d_diag,
-               hipStream_t s);
+               hipStream_t s, int split = 0, char* d_sync = nullptr);
 int fmat_points(vs_ctx* ctx, int P, const float* d_p1, const float* d_p2, const int* d_off, double thr, double conf,
                 int max_iters, double* d_F, uint8_t* d_mask, double* d_err, int* d_diag, hipStream_t s);
 // Essential-matrix motion + depth scale (A12): per frame pair (pipeline) or per point set.
