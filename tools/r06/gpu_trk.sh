@@ -1,0 +1,19 @@
+#!/bin/bash
+# Round-6: tracking CUs 32 (default) vs 28 vs 24 (more CUs for the network, the binding stream), 3 rounds
+export TMPDIR=/tmp
+O=gpurun_out/${GPU_OUT:-r06trk}; mkdir -p $O
+( while sleep 45; do echo "[hb] $(date +%T)"; done ) & HB=$!
+trap "kill $HB" EXIT
+H="--no-cpu-baseline --no-frontend --mono-steps 0 --ba-reps 0"
+run() {
+  tag=$1; shift
+  env "$@" timeout -k 10 300 python -u bench.py $H > $O/b_$tag.json 2> $O/b_$tag.err || { tail -20 $O/b_$tag.err; exit 1; }
+  python3 -c "
+import json; d=json.loads(open('$O/b_$tag.json').read().strip().splitlines()[-1]); s=d['stage_ms_per_frame']
+print('$tag', d['value'], d['ms_per_step'], 'fmat', s.get('fmat_ransac'), 'match_spec', s.get('match_spec'), 'net', round(sum(v for k,v in s.items() if k.startswith('conv') or k.startswith('head')), 4))"
+}
+for r in 1 2 3; do
+  run def$r VS_X=0
+  run t28$r VS_SLAM_TRACK_CUS=28
+  run t24$r VS_SLAM_TRACK_CUS=24
+done
