@@ -268,7 +268,8 @@ int vs_estimate_motion(vs_ctx* ctx, const float* p1, const float* p2, int n, con
  * matches d_kept [p][cap] / d_nkept, depth slots d_depth [slot][h][w], or NULL for a monocular
  * stream: no scale, *d_scale = -1, BASELINE config[4]); pairs with d_skip[p] != 0
  * (e.g. the 3D-3D result was ok) are skipped.  d_R [p][9], d_t [p][3], d_scale [p], d_ok [p],
- * d_diag [p][8].  cap <= VS_EM_MAX_POINTS. */
+ * d_diag [p][8].  cap <= VS_EM_MAX_POINTS.  The RANSAC's workgroups meet in a per-context area
+ * (round 6), so calls on one context must not overlap in time across different streams. */
 int vs_emat_motion_pairs_dev(vs_ctx* ctx, int P, const int* d_pairs, const vs_keypoint* d_kps,
                              int cap, const vs_match* d_kept, const int* d_nkept, const int* d_skip,
                              const float* d_depth, int h, int w, const double K[4], double* d_R,
