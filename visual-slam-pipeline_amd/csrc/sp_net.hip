@@ -55,13 +55,12 @@ __global__ void k_gray_norm(const uint8_t* __restrict__ img, int channels, int h
 // contiguous range of work items w = tile * ntiles + output-channel tile: the ntiles workgroups of
 // one spatial tile run back to back on one XCD and read its input patch through one L2 instead of
 // ntiles times from the fabric.  Falls back to the plain order when the grid is not a multiple of 8.
-__device__ inline void xcd_work(int ntiles, int& tile, int& nt) {
-    const int nblk = gridDim.x;
-    int w = blockIdx.x;
+__device__ inline void xcd_work_at(int w, int nblk, int ntiles, int& tile, int& nt) {
     if ((nblk & 7) == 0) w = (w & 7) * (nblk >> 3) + (w >> 3);
     tile = w / ntiles;
     nt = w - tile * ntiles;
 }
+__device__ inline void xcd_work(int ntiles, int& tile, int& nt) { xcd_work_at(blockIdx.x, gridDim.x, ntiles, tile, nt); }
 
 // Generic conv (KS = 3: 3x3 pad 1 over 8x32 spatial tiles; KS = 1: 1x1 over linear 256-pixel
 // tiles) on v_mfma_f32_32x32x2_f32.  256 threads = 4 waves; wave wv owns tile rows 2wv, 2wv+1
@@ -81,12 +80,14 @@ struct ConvGeom {
 // (1 -> 64, 3x3, ReLU) for each 16-channel chunk of its 10x34 input patch from a 12x36 gray patch
 // in LDS, so the 64-channel full-resolution conv1a activation never goes through HBM.  Patch
 // positions outside the image are conv1b's zero padding (0, not conv1a evaluated there).
-template <int KS, bool POOL, int LAYER, bool FUSE1A = false, int CKV = (KS == 3 ? 16 : 32)>
-__global__ __launch_bounds__(256, (KS == 3 && CKV == 32) ? 1 : ((CKV == 8 || (KS == 1 && CKV == 16)) ? 3 : 2)) void k_conv_mfma(
+// The body, for workgroup w_blk of an n_blk-workgroup grid (k_conv_mfma: blockIdx.x of gridDim.x;
+// k_conv1x1_pair: its sub-grid's own index and size).
+template <int KS, bool POOL, bool FUSE1A, int CKV>
+__device__ __forceinline__ void conv_mfma_body(
     const float* __restrict__ in, int in_cstride, int in_coff, const float* __restrict__ wt,
     const float* __restrict__ bias, int cin, int cout, int cout_pad, float* __restrict__ out,
     int out_cstride, int out_coff, int B, int H, int W, int tiles_x, int tiles_y, int relu,
-    const float* __restrict__ w1a, const float* __restrict__ b1a) {
+    const float* __restrict__ w1a, const float* __restrict__ b1a, int w_blk, int n_blk) {
     using G = ConvGeom<KS, CKV>;
     constexpr int CK = G::CK;
     constexpr int Q = CK / 4;                                  // float4 per pixel and chunk
@@ -102,7 +103,7 @@ __global__ __launch_bounds__(256, (KS == 3 && CKV == 32) ? 1 : ((CKV == 8 || (KS
     const int tid = threadIdx.x;
     const int wv = tid >> 6, lane = tid & 63, li = lane & 31, lh = lane >> 5;
     int tile, nt;
-    xcd_work(cout_pad >> 6, tile, nt);
+    xcd_work_at(w_blk, n_blk, cout_pad >> 6, tile, nt);
     const int n0 = nt * 64;
     int b = 0, y0 = 0, x0 = 0;
     long m0 = 0;  // KS == 1: first linear pixel of the tile
@@ -318,6 +319,39 @@ __global__ __launch_bounds__(256, (KS == 3 && CKV == 32) ? 1 : ((CKV == 8 || (KS
             }
         }
     }
+}
+
+template <int KS, bool POOL, int LAYER, bool FUSE1A = false, int CKV = (KS == 3 ? 16 : 32)>
+__global__ __launch_bounds__(256, (KS == 3 && CKV == 32) ? 1 : ((CKV == 8 || (KS == 1 && CKV == 16)) ? 3 : 2)) void k_conv_mfma(
+    const float* __restrict__ in, int in_cstride, int in_coff, const float* __restrict__ wt,
+    const float* __restrict__ bias, int cin, int cout, int cout_pad, float* __restrict__ out,
+    int out_cstride, int out_coff, int B, int H, int W, int tiles_x, int tiles_y, int relu,
+    const float* __restrict__ w1a, const float* __restrict__ b1a) {
+    conv_mfma_body<KS, POOL, FUSE1A, CKV>(in, in_cstride, in_coff, wt, bias, cin, cout, cout_pad, out, out_cstride,
+                                          out_coff, B, H, W, tiles_x, tiles_y, relu, w1a, b1a, blockIdx.x, gridDim.x);
+}
+
+// Two 1x1 convolutions in one grid (round 6: SuperPoint's convDb and convPb, which read different channel
+// ranges of head_a's output): the first n_first workgroups run the first, the rest the second, each
+// with its own XCD-aware order — one launch, the second layer's workgroups filling the first's tail.
+struct Conv1x1Args {
+    const float* in;
+    int in_cstride, in_coff;
+    const float* wt;
+    const float* bias;
+    int cin, cout, cout_pad;
+    float* out;
+    int out_cstride, out_coff;
+};
+template <int CKV>
+__global__ __launch_bounds__(256, CKV == 16 ? 3 : 2) void k_conv1x1_pair(Conv1x1Args a, Conv1x1Args b, int n_first,
+                                                                          int B, int H, int W) {
+    const bool first = (int)blockIdx.x < n_first;
+    const Conv1x1Args& c = first ? a : b;
+    const int w = first ? (int)blockIdx.x : (int)blockIdx.x - n_first;
+    const int n = first ? n_first : (int)gridDim.x - n_first;
+    conv_mfma_body<1, false, false, CKV>(c.in, c.in_cstride, c.in_coff, c.wt, c.bias, c.cin, c.cout, c.cout_pad, c.out,
+                                         c.out_cstride, c.out_coff, B, H, W, 1, 1, 0, nullptr, nullptr, w, n);  // no ReLU after the heads
 }
 
 // Double-buffered 3x3 conv: 8-channel chunks, s_in / s_w in two LDS buffers (63 KB with the fused
@@ -1451,7 +1485,24 @@ int sp_forward(vs_ctx* ctx, int B, const uint8_t* d_img, int channels, int h, in
             const char* e = std::getenv("VS_CONV1X1_CK");
             return e ? std::atoi(e) : 16;
         }();
-        if (ck1 == 16) {
+        // round 6: both in one grid (convDb's workgroups first: both sub-grids keep an 8-aligned XCD order);
+        // VS_HEADB_PAIR=0: two launches
+        static const bool pair = [] {
+            const char* e = std::getenv("VS_HEADB_PAIR");
+            return !(e && e[0] == '0');
+        }();
+        if (ck1 == 16 && pair) {
+            const DevLayer& P = L[9];
+            const DevLayer& D = L[11];
+            if (P.cin % 16 || D.cin % 16 || P.cout_pad % 64 || D.cout_pad % 64) return VS_ERR_ARG;
+            const long nb = ((long)B * H * W + 255) / 256;
+            const Conv1x1Args d{a0, 512, 256, D.w, D.b, D.cin, D.cout, D.cout_pad, dgrid_out, kDescDim, 0};
+            const Conv1x1Args p{a0, 512, 0, P.w, P.b, P.cin, P.cout, P.cout_pad, semi_out, kSemiCh, 0};
+            const int n_first = (int)(nb * (D.cout_pad / 64));
+            hipLaunchKernelGGL(k_conv1x1_pair<16>, dim3((unsigned)(n_first + nb * (P.cout_pad / 64))), dim3(256), 0, s,
+                               d, p, n_first, B, H, W);
+            VS_HIP(hipGetLastError());
+        } else if (ck1 == 16) {
             VS_CHECK((launch_conv<1, false, 9, false, 16>(L[9], a0, 512, 0, semi_out, kSemiCh, 0, B, H, W, 0, s)));
             VS_CHECK((launch_conv<1, false, 11, false, 16>(L[11], a0, 512, 256, dgrid_out, kDescDim, 0, B, H, W, 0, s)));
         } else {
